@@ -1,0 +1,22 @@
+// Host construction of the bin atlas and the scale-mode lookup structures.
+//
+// Nearest-bin pools: for a cube-map cell with centre c, corner radius r_c and nearest-bin
+// distance rho_c, any direction q in the cell has its nearest bin n(q) within
+// d(q, n(q)) <= d(q, n(c)) <= r_c + rho_c of q, hence within 2 r_c + rho_c of c.  The pool of
+// c holds every bin inside that radius (plus margin), so a scan of the pool with the exact
+// canonical dot returns the same bin as a brute-force scan of all B bins.
+#pragma once
+#include <vector>
+
+namespace gcs {
+namespace atlas {
+
+void fibonacci(int B, double* dirs /*B*3*/);
+void knn(const double* dirs, int B, int K, int* out /*B*K*/);
+void nearest(const double* dirs, int B, int nq, const double* q, int* out);
+void reverse(const int* knn, int B, int K, std::vector<int>& off, std::vector<int>& idx);
+int grid_for_bins(int B);
+void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& width);
+
+}  // namespace atlas
+}  // namespace gcs

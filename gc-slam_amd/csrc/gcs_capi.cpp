@@ -1,0 +1,965 @@
+// C-ABI of libgcslam_hip.so (include/gcslam_hip.h): per-hypothesis context, the 14-step
+// bin-path scan (FS/backend/pipeline.py:316-1591 calling convention), per-operator entry
+// points for parity tests, host numerics and the hypothesis all-reduce payload.
+#include "gcslam_hip.h"
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "gcs_atlas.h"
+#include "gcs_host.h"
+#include "gcs_kernels.h"
+#include "gcs_layout.h"
+#include "gcs_math.h"
+
+using namespace gcs;
+using host::Belief;
+using host::DZ;
+
+// device stages timed with hipEvents when timing is enabled
+enum { ST_POINTS = 0, ST_SORT = 1, ST_BINS = 2, ST_MF = 3, ST_PT = 4, ST_PUSH = 5, kStages = 6 };
+
+struct gcs_ctx {
+  gcs_config cfg{};
+  int B = 0, cap = 0, K = 0, G = 0, pool_width = 0, ncell = 0, max_raw = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  // atlas (device)
+  double* d_bin_dirs = nullptr;
+  int* d_knn = nullptr;
+  int* d_rknn_off = nullptr;
+  int* d_rknn = nullptr;
+  int* d_pools = nullptr;
+  std::vector<double> dirs_host;
+  std::vector<int> knn_host;
+  // per-point
+  PointRec* d_recs = nullptr;
+  uint32_t *d_keys = nullptr, *d_vals = nullptr, *d_keys_s = nullptr, *d_vals_s = nullptr;
+  void* d_sort_tmp = nullptr;
+  size_t sort_bytes = 0;
+  int* d_nearest = nullptr;
+  // per-bin
+  int2* d_ranges = nullptr;
+  uint8_t* d_flags = nullptr;
+  double* d_scan = nullptr;
+  double* d_map = nullptr;
+  double* d_derived = nullptr;
+  double* d_bin_partials = nullptr;
+  // reductions
+  double* d_partials = nullptr;
+  size_t partials_len = 0;
+  double* d_scalars = nullptr;
+  double* h_scalars = nullptr;  // pinned
+  // host state
+  Belief belief{};
+  double iw_nu[7], iw_Psi[7 * 36], Q[DZ * DZ];
+  double last_dPsi[7 * 36], last_dnu[7];
+  bool have_last = false;
+  int last_n_sel = 0, last_stride = 1;
+  // device stage timing (hipEvents on the context stream; harvested lazily)
+  bool timing = false, pending = false;
+  hipEvent_t ev[kStages][2] = {};
+  bool ev_rec[kStages] = {};
+  double stage_ms_sum[kStages] = {};
+  long stage_count[kStages] = {};
+};
+
+namespace {
+
+int fail(gcs_ctx* c, int code, const std::string& m) {
+  if (c) c->err = m;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                         \
+  do {                                                                                            \
+    hipError_t _e = (expr);                                                                       \
+    if (_e != hipSuccess) return fail((ctx), GCS_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+constexpr int kRedBlocks = 512;
+int red_blocks(long n) { return (int)std::max(1L, std::min((long)kRedBlocks, (n + 255) / 256)); }
+
+void harvest(gcs_ctx* c) {
+  if (!c->pending) return;
+  for (int st = 0; st < kStages; ++st) {
+    if (!c->ev_rec[st]) continue;
+    (void)hipEventSynchronize(c->ev[st][1]);
+    float ms = 0.0f;
+    if (hipEventElapsedTime(&ms, c->ev[st][0], c->ev[st][1]) == hipSuccess) {
+      c->stage_ms_sum[st] += ms;
+      c->stage_count[st] += 1;
+    }
+    c->ev_rec[st] = false;
+  }
+  c->pending = false;
+}
+
+struct StageTimer {
+  gcs_ctx* c;
+  int st;
+  StageTimer(gcs_ctx* cc, int s) : c(cc), st(s) {
+    if (c->timing) (void)hipEventRecord(c->ev[st][0], c->stream);
+  }
+  ~StageTimer() {
+    if (c->timing) {
+      (void)hipEventRecord(c->ev[st][1], c->stream);
+      c->ev_rec[st] = true;
+      c->pending = true;
+    }
+  }
+};
+
+void to_host_belief(const gcs_belief& in, Belief& b) {
+  memcpy(b.X_anchor, in.X_anchor, sizeof(b.X_anchor));
+  b.stamp = in.stamp_sec;
+  memcpy(b.z_lin, in.z_lin, sizeof(b.z_lin));
+  memcpy(b.L, in.L, sizeof(b.L));
+  memcpy(b.h, in.h, sizeof(b.h));
+}
+
+void from_host_belief(const Belief& b, gcs_belief& out) {
+  memcpy(out.X_anchor, b.X_anchor, sizeof(b.X_anchor));
+  out.stamp_sec = b.stamp;
+  memcpy(out.z_lin, b.z_lin, sizeof(b.z_lin));
+  memcpy(out.L, b.L, sizeof(b.L));
+  memcpy(out.h, b.h, sizeof(b.h));
+}
+
+int upload_atlas(gcs_ctx* c) {
+  const int B = c->B, K = c->K;
+  std::vector<double> d4((size_t)B * 4, 0.0);
+  for (int b = 0; b < B; ++b)
+    for (int k = 0; k < 3; ++k) d4[(size_t)b * 4 + k] = c->dirs_host[(size_t)b * 3 + k];
+  HIPCHK(c, hipMemcpy(c->d_bin_dirs, d4.data(), d4.size() * sizeof(double), hipMemcpyHostToDevice));
+  if (c->cfg.mode == GCS_MODE_SCALE) {
+    c->knn_host.assign((size_t)B * K, 0);
+    atlas::knn(c->dirs_host.data(), B, K, c->knn_host.data());
+    std::vector<int> off, idx, pools;
+    atlas::reverse(c->knn_host.data(), B, K, off, idx);
+    c->G = atlas::grid_for_bins(B);
+    c->ncell = 6 * c->G * c->G;
+    atlas::cell_pools(c->dirs_host.data(), B, c->G, pools, c->pool_width);
+    if (c->d_pools) (void)hipFree(c->d_pools);
+    HIPCHK(c, hipMalloc(&c->d_pools, pools.size() * sizeof(int)));
+    HIPCHK(c, hipMemcpy(c->d_pools, pools.data(), pools.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_knn, c->knn_host.data(), c->knn_host.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_rknn_off, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->d_rknn, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  return GCS_OK;
+}
+
+// ---------------------------------------------------------------- device stages
+int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, const double* w, int n_raw, double t0,
+                 double t1, const double* xi, double* p0_out, double* w_out, double* wb_out) {
+  if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
+  if (point_step < 12) return fail(c, GCS_ERR_ARG, "point_step must be >= 12 bytes");
+  int stride = std::max(1, (int)((n_raw + (long)c->cap - 1) / c->cap));  // ceil(N/cap), point_budget.py:160
+  int n_sel = (n_raw + stride - 1) / stride;
+  c->last_n_sel = n_sel;
+  c->last_stride = stride;
+  hipStream_t s = c->stream;
+  harvest(c);
+  StageTimer timer(c, ST_POINTS);
+  if (n_raw > 0) {
+    HIPCHK(c, launch_budget(w, n_raw, stride, c->d_partials, red_blocks(n_raw), c->d_scalars, s));
+  } else {
+    HIPCHK(c, hipMemsetAsync(c->d_scalars, 0, 3 * sizeof(double), s));
+  }
+  PointKernelArgs a{};
+  a.xyz = (const uint8_t*)xyz;
+  a.point_step = point_step;
+  a.timestamps = t;
+  a.weights = w;
+  a.n_raw = n_raw;
+  a.n_sel = n_sel;
+  a.stride = stride;
+  a.cap = c->cap;
+  a.t0 = t0;
+  a.t1 = t1;
+  memcpy(a.xi, xi, 6 * sizeof(double));
+  memcpy(a.origin, c->cfg.lidar_origin, 3 * sizeof(double));
+  a.tau = c->cfg.tau;
+  a.bin_dirs = c->d_bin_dirs;
+  a.n_bins = c->B;
+  a.knn = c->d_knn;
+  a.k = c->K;
+  a.pools = c->d_pools;
+  a.pool_width = c->pool_width;
+  a.grid = c->G;
+  a.recs = c->d_recs;
+  a.keys = c->d_keys;
+  a.vals = c->d_vals;
+  a.scalars = c->d_scalars;
+  a.p0_out = p0_out;
+  a.w_out = w_out;
+  a.w_budget_out = wb_out;
+  a.nearest_out = c->d_nearest;
+  HIPCHK(c, launch_points(a, c->cfg.mode == GCS_MODE_SCALE, c->d_partials, red_blocks(c->cap), s));
+  return GCS_OK;
+}
+
+BinKernelArgs bin_args(gcs_ctx* c) {
+  BinKernelArgs b{};
+  b.recs = c->d_recs;
+  b.sorted_vals = c->d_vals_s;
+  b.ranges = c->d_ranges;
+  b.flags = c->d_flags;
+  b.rknn_off = c->d_rknn_off;
+  b.rknn = c->d_rknn;
+  b.bin_dirs = c->d_bin_dirs;
+  b.n_bins = c->B;
+  b.cap = c->cap;
+  memcpy(b.origin, c->cfg.lidar_origin, 3 * sizeof(double));
+  b.tau = c->cfg.tau;
+  b.scan = c->d_scan;
+  return b;
+}
+
+int stage_bins(gcs_ctx* c) {
+  hipStream_t s = c->stream;
+  BinKernelArgs b = bin_args(c);
+  int nblk = (c->B + 255) / 256;
+  if (c->cfg.mode == GCS_MODE_SCALE) {
+    int end_bit = 1;
+    while ((1u << end_bit) <= (unsigned)c->B) ++end_bit;
+    {
+      StageTimer timer(c, ST_SORT);
+      HIPCHK(c, launch_sort(c->d_sort_tmp, c->sort_bytes, c->d_keys, c->d_keys_s, c->d_vals, c->d_vals_s, c->cap, end_bit, s));
+      HIPCHK(c, hipMemsetAsync(c->d_ranges, 0, (size_t)c->B * sizeof(int2), s));
+      HIPCHK(c, hipMemsetAsync(c->d_flags, 0, (size_t)c->B, s));
+      HIPCHK(c, launch_bucket_mark(c->d_keys_s, c->cap, c->B, c->d_knn, c->K, c->d_ranges, c->d_flags, s));
+    }
+    StageTimer timer(c, ST_BINS);
+    HIPCHK(c, launch_bins_scale(b, c->d_partials, s));
+  } else {
+    StageTimer timer(c, ST_BINS);
+    HIPCHK(c, launch_dense(b, c->d_bin_partials, c->d_partials, s));
+  }
+  HIPCHK(c, launch_bin_cert_final(c->d_partials, nblk, c->d_scalars, s));
+  return GCS_OK;
+}
+
+int stage_mf(gcs_ctx* c) {
+  StageTimer timer(c, ST_MF);
+  HIPCHK(c, launch_mf(c->d_scan, c->d_map, c->B, c->d_partials, red_blocks(c->B), c->d_scalars, c->stream));
+  return GCS_OK;
+}
+
+int stage_pt(gcs_ctx* c) {
+  StageTimer timer(c, ST_PT);
+  HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars, c->stream));
+  return GCS_OK;
+}
+
+int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) {
+  PushArgs pa{};
+  so3_exp(z_t + 3, pa.R);
+  pa.t[0] = z_t[0];
+  pa.t[1] = z_t[1];
+  pa.t[2] = 0.0;  // t_z := 0 before the map update (CHANGELOG.md:575-578)
+  memcpy(pa.Sigma_pose, Sig6, 36 * sizeof(double));
+  pa.gamma = gamma;
+  StageTimer timer(c, ST_PUSH);
+  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->stream));
+  return GCS_OK;
+}
+
+int pull_scalars(gcs_ctx* c) {
+  HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, SC_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
+double trig(double lift, double psd, double nu, double mer, double rho, double dts, double exs, double alpha, double beta) {
+  return lift + psd + nu + mer + rho + fabs(1.0 - dts) + fabs(1.0 - exs) + fabs(1.0 - alpha) + fabs(1.0 - beta);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gcs_version(void) { return "gcslam-mi355x 0.1.0 (gfx950)"; }
+int gcs_abi_version(void) { return GCS_ABI_VERSION; }
+const char* gcs_last_error(const gcs_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
+  if (!cfg || !out) return GCS_ERR_ARG;
+  *out = nullptr;
+  if (cfg->n_bins < 1 || cfg->n_points_cap < 1 || cfg->max_raw_points < 0) return GCS_ERR_ARG;
+  if (cfg->mode == GCS_MODE_SCALE && (cfg->k_cand < 1 || cfg->k_cand > 32 || cfg->k_cand > cfg->n_bins)) return GCS_ERR_ARG;
+  if (!(cfg->tau > 0.0)) return GCS_ERR_ARG;
+  gcs_ctx* c = new gcs_ctx();
+  c->cfg = *cfg;
+  c->B = cfg->n_bins;
+  c->cap = cfg->n_points_cap;
+  c->K = cfg->mode == GCS_MODE_SCALE ? cfg->k_cand : 0;
+  c->max_raw = cfg->max_raw_points;
+  auto bad = [&](hipError_t e) {
+    if (e != hipSuccess) {
+      gcs_ctx_destroy(c);
+      return true;
+    }
+    return false;
+  };
+  if (bad(hipSetDevice(cfg->device))) return GCS_ERR_HIP;
+  if (bad(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
+  c->own_stream = true;
+  const size_t B = c->B, cap = c->cap;
+  if (bad(hipMalloc(&c->d_bin_dirs, B * 4 * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_recs, cap * sizeof(PointRec)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_nearest, cap * sizeof(int)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_scan, B * SF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_map, B * MF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_derived, B * MD_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMemset(c->d_map, 0, B * MF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMemset(c->d_scan, 0, B * SF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  c->partials_len = std::max<size_t>((size_t)kRedBlocks * 24, ((B + 255) / 256) * 5 + 64);
+  if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocDefault))) return GCS_ERR_HIP;
+  if (cfg->mode == GCS_MODE_SCALE) {
+    if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_rknn_off, (B + 1) * sizeof(int)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_rknn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_keys, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_vals, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_keys_s, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_vals_s, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_ranges, B * sizeof(int2)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_flags, B))) return GCS_ERR_HIP;
+    c->sort_bytes = sort_temp_bytes(c->cap);
+    if (bad(hipMalloc(&c->d_sort_tmp, std::max<size_t>(c->sort_bytes, 16)))) return GCS_ERR_HIP;
+  } else {
+    size_t nchunks = (cap + 255) / 256;
+    if (bad(hipMalloc(&c->d_bin_partials, nchunks * 19 * B * sizeof(double)))) return GCS_ERR_HIP;
+  }
+  c->dirs_host.assign(B * 3, 0.0);
+  atlas::fibonacci(c->B, c->dirs_host.data());
+  if (upload_atlas(c) != GCS_OK) {
+    gcs_ctx_destroy(c);
+    return GCS_ERR_HIP;
+  }
+  if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->stream))) return GCS_ERR_HIP;
+  if (bad(hipStreamSynchronize(c->stream))) return GCS_ERR_HIP;
+  // identity prior (belief.py:320-358) and datasheet IW state
+  memset(&c->belief, 0, sizeof(Belief));
+  for (int i = 0; i < DZ; ++i) c->belief.L[i * DZ + i] = 1e-6;
+  host::datasheet_iw_state(c->iw_nu, c->iw_Psi);
+  host::process_noise_Q(c->iw_nu, c->iw_Psi, c->Q);
+  *out = c;
+  return GCS_OK;
+}
+
+int gcs_ctx_destroy(gcs_ctx* c) {
+  if (!c) return GCS_OK;
+  void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_vals,
+                  c->d_keys_s, c->d_vals_s, c->d_sort_tmp, c->d_nearest, c->d_ranges, c->d_flags, c->d_scan,
+                  c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->h_scalars) (void)hipHostFree(c->h_scalars);
+  for (int st = 0; st < kStages; ++st)
+    for (int k = 0; k < 2; ++k)
+      if (c->ev[st][k]) (void)hipEventDestroy(c->ev[st][k]);
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return GCS_OK;
+}
+
+int gcs_ctx_set_stream(gcs_ctx* c, void* s) {
+  if (!c) return GCS_ERR_ARG;
+  if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  c->stream = (hipStream_t)s;
+  c->own_stream = false;
+  return GCS_OK;
+}
+
+int gcs_ctx_synchronize(gcs_ctx* c) {
+  if (!c) return GCS_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
+int gcs_ctx_enable_timing(gcs_ctx* c, int32_t on) {
+  if (!c) return GCS_ERR_ARG;
+  if (on && !c->ev[0][0])
+    for (int st = 0; st < kStages; ++st)
+      for (int k = 0; k < 2; ++k) HIPCHK(c, hipEventCreate(&c->ev[st][k]));
+  c->timing = on != 0;
+  return GCS_OK;
+}
+
+int gcs_ctx_stage_times(gcs_ctx* c, double* ms_sum, int64_t* counts, int32_t reset) {
+  if (!c) return GCS_ERR_ARG;
+  harvest(c);
+  for (int st = 0; st < kStages; ++st) {
+    if (ms_sum) ms_sum[st] = c->stage_ms_sum[st];
+    if (counts) counts[st] = c->stage_count[st];
+    if (reset) { c->stage_ms_sum[st] = 0.0; c->stage_count[st] = 0; }
+  }
+  return GCS_OK;
+}
+
+int gcs_ctx_set_atlas(gcs_ctx* c, const double* dirs) {
+  if (!c || !dirs) return GCS_ERR_ARG;
+  c->dirs_host.assign(dirs, dirs + (size_t)c->B * 3);
+  return upload_atlas(c);
+}
+
+int gcs_ctx_get_atlas(gcs_ctx* c, double* dirs, int32_t* knn) {
+  if (!c) return GCS_ERR_ARG;
+  if (dirs) memcpy(dirs, c->dirs_host.data(), c->dirs_host.size() * sizeof(double));
+  if (knn && !c->knn_host.empty()) memcpy(knn, c->knn_host.data(), c->knn_host.size() * sizeof(int));
+  return GCS_OK;
+}
+
+int gcs_ctx_set_belief(gcs_ctx* c, const gcs_belief* b) {
+  if (!c || !b) return GCS_ERR_ARG;
+  to_host_belief(*b, c->belief);
+  return GCS_OK;
+}
+
+int gcs_ctx_get_belief(gcs_ctx* c, gcs_belief* b) {
+  if (!c || !b) return GCS_ERR_ARG;
+  from_host_belief(c->belief, *b);
+  return GCS_OK;
+}
+
+int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
+  if (!c || !map) return GCS_ERR_ARG;
+  HIPCHK(c, hipMemcpyAsync(c->d_map, map, (size_t)c->B * MF_COUNT * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, launch_map_derive(c->d_map, c->d_derived, c->B, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
+int gcs_ctx_get_map(gcs_ctx* c, double* map, double* derived) {
+  if (!c) return GCS_ERR_ARG;
+  if (map) HIPCHK(c, hipMemcpyAsync(map, c->d_map, (size_t)c->B * MF_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (derived)
+    HIPCHK(c, hipMemcpyAsync(derived, c->d_derived, (size_t)c->B * MD_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
+int gcs_ctx_get_scan_stats(gcs_ctx* c, double* scan) {
+  if (!c || !scan) return GCS_ERR_ARG;
+  HIPCHK(c, hipMemcpyAsync(scan, c->d_scan, (size_t)c->B * SF_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
+int gcs_ctx_device_arrays(gcs_ctx* c, double** scan, double** map, double** derived) {
+  if (!c) return GCS_ERR_ARG;
+  if (scan) *scan = c->d_scan;
+  if (map) *map = c->d_map;
+  if (derived) *derived = c->d_derived;
+  return GCS_OK;
+}
+
+int gcs_ctx_set_iw_state(gcs_ctx* c, const double* nu, const double* Psi) {
+  if (!c || !nu || !Psi) return GCS_ERR_ARG;
+  memcpy(c->iw_nu, nu, sizeof(c->iw_nu));
+  memcpy(c->iw_Psi, Psi, sizeof(c->iw_Psi));
+  host::process_noise_Q(c->iw_nu, c->iw_Psi, c->Q);
+  return GCS_OK;
+}
+
+int gcs_ctx_get_iw_state(gcs_ctx* c, double* nu, double* Psi, double* Q) {
+  if (!c) return GCS_ERR_ARG;
+  if (nu) memcpy(nu, c->iw_nu, sizeof(c->iw_nu));
+  if (Psi) memcpy(Psi, c->iw_Psi, sizeof(c->iw_Psi));
+  if (Q) memcpy(Q, c->Q, sizeof(c->Q));
+  return GCS_OK;
+}
+
+// ---------------------------------------------------------------- per-operator entry points
+int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const double* t, const double* w, int32_t n,
+                    double t0, double t1, const double* xi, double* p0_dev, double* w_out_dev, double* w_budget_dev,
+                    int32_t* nearest_dev, double* cert) {
+  if (!c || !xi) return GCS_ERR_ARG;
+  int rc = stage_points(c, xyz, point_step, t, w, n, t0, t1, xi, p0_dev, w_out_dev, w_budget_dev);
+  if (rc) return rc;
+  if (nearest_dev)
+    HIPCHK(c, hipMemcpyAsync(nearest_dev, c->d_nearest, (size_t)c->cap * sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+  if ((rc = pull_scalars(c))) return rc;
+  if (cert)
+    for (int k = 0; k < 8; ++k) cert[k] = c->h_scalars[k];
+  return GCS_OK;
+}
+
+namespace {
+__global__ void k_materialize(const PointRec* recs, const int* nearest, const int* knn, const double* bin_dirs, int cap,
+                              int B, int K, bool scale, double ox, double oy, double oz, double tau, int* ids, double* r) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= cap) return;
+  PointRec pr = recs[i];
+  double rx = pr.x - ox, ry = pr.y - oy, rz = pr.z - oz;
+  double nrm = sqrt(dot3_exact(rx, ry, rz, rx, ry, rz)) + kEpsMass;
+  double d0 = rx / nrm, d1 = ry / nrm, d2 = rz / nrm;
+  double it = 1.0 / tau;
+  if (scale) {
+    const int* row = knn + (size_t)nearest[i] * K;
+    for (int k = 0; k < K; ++k) {
+      const double* bd = bin_dirs + 4 * (size_t)row[k];
+      double s = dot3_exact(d0, d1, d2, bd[0], bd[1], bd[2]);
+      if (ids) ids[(size_t)i * K + k] = row[k];
+      if (r) r[(size_t)i * K + k] = exp((s - pr.m) * it) * pr.iz;
+    }
+  } else {
+    for (int b = 0; b < B; ++b) {
+      const double* bd = bin_dirs + 4 * (size_t)b;
+      double s = dot3_exact(d0, d1, d2, bd[0], bd[1], bd[2]);
+      if (r) r[(size_t)i * B + b] = exp((s - pr.m) * it) * pr.iz;
+    }
+  }
+}
+}  // namespace
+
+int gcs_bin_soft_assign(gcs_ctx* c, int32_t* ids, double* r) {
+  if (!c) return GCS_ERR_ARG;
+  bool scale = c->cfg.mode == GCS_MODE_SCALE;
+  hipLaunchKernelGGL(k_materialize, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, (const PointRec*)c->d_recs,
+                     (const int*)c->d_nearest, (const int*)c->d_knn, (const double*)c->d_bin_dirs, c->cap, c->B, c->K,
+                     scale, c->cfg.lidar_origin[0], c->cfg.lidar_origin[1], c->cfg.lidar_origin[2], c->cfg.tau, ids, r);
+  HIPCHK(c, hipGetLastError());
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
+int gcs_scan_bin_moment_match(gcs_ctx* c, double* cert) {
+  if (!c) return GCS_ERR_ARG;
+  int rc = stage_bins(c);
+  if (rc) return rc;
+  if ((rc = pull_scalars(c))) return rc;
+  if (cert)
+    for (int k = 0; k < 5; ++k) cert[k] = c->h_scalars[SC_BIN_NSUM + k];
+  return GCS_OK;
+}
+
+int gcs_matrix_fisher_rotation(gcs_ctx* c, double* mf) {
+  if (!c) return GCS_ERR_ARG;
+  int rc = stage_mf(c);
+  if (rc) return rc;
+  if ((rc = pull_scalars(c))) return rc;
+  if (mf) {
+    int k = 0;
+    for (int i = 0; i < 9; ++i) mf[k++] = c->h_scalars[SC_MF_H + i];
+    mf[k++] = c->h_scalars[SC_MF_NEFF];
+    for (int i = 0; i < 9; ++i) mf[k++] = c->h_scalars[SC_MF_MAPSCAT + i];
+    mf[k++] = c->h_scalars[SC_MF_MAPND];
+    mf[k++] = c->h_scalars[SC_MF_SCANN];
+    for (int i = 0; i < 9; ++i) mf[k++] = c->h_scalars[SC_MF_R + i];
+    for (int i = 0; i < 3; ++i) mf[k++] = c->h_scalars[SC_MF_S + i];
+    for (int i = 0; i < 9; ++i) mf[k++] = c->h_scalars[SC_MF_V + i];
+  }
+  return GCS_OK;
+}
+
+int gcs_planar_translation(gcs_ctx* c, const double* R_hat, double* pt) {
+  if (!c || !R_hat) return GCS_ERR_ARG;
+  HIPCHK(c, hipMemcpyAsync(c->d_scalars + SC_MF_R, R_hat, 9 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  int rc = stage_pt(c);
+  if (rc) return rc;
+  if ((rc = pull_scalars(c))) return rc;
+  if (pt) {
+    for (int i = 0; i < 9; ++i) pt[i] = c->h_scalars[SC_PT_L + i];
+    for (int i = 0; i < 3; ++i) pt[9 + i] = c->h_scalars[SC_PT_H + i];
+    pt[12] = c->h_scalars[SC_PT_NEFF];
+  }
+  return GCS_OK;
+}
+
+int gcs_pushforward(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) {
+  if (!c || !z_t || !Sig6) return GCS_ERR_ARG;
+  int rc = stage_push(c, z_t, Sig6, gamma);
+  if (rc) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
+// ---------------------------------------------------------------- the per-scan pipeline
+int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
+  using clk = std::chrono::steady_clock;
+  if (!c || !in || !out) return fail(c, GCS_ERR_ARG, "null argument");
+  if (in->imu_len < 1 || !in->imu_stamps || !in->imu_gyro || !in->imu_accel) return fail(c, GCS_ERR_ARG, "IMU window required");
+  auto T0 = clk::now();
+  const double* Q = in->Q ? in->Q : c->Q;
+  double* cert = out->cert;
+  memset(cert, 0, sizeof(out->cert));
+  double Tsum = 0.0;
+  // 2 PredictDiffusion
+  Belief prev = c->belief, pred;
+  double pinfl[3];
+  host::predict_diffusion(prev, Q, in->dt_sec, pred, pinfl);
+  cert[6] = pinfl[0]; cert[7] = pinfl[1]; cert[8] = pinfl[2];
+  Tsum += trig(pinfl[0], pinfl[1], 0, 0, 0, pinfl[2], 1, 1, 1);
+  // 3 IMU membership window + preintegration -> deskew twist (pipeline.py:432-483)
+  std::vector<double> covp(DZ * DZ);
+  host::spd_inverse_lifted(DZ, pred.L, kEpsLift, covp.data());
+  double sigma_warp = std::max(sqrt(covp[15 * DZ + 15]), 0.01);
+  cert[38] = sigma_warp;
+  std::vector<double> wimu(in->imu_len);
+  for (int i = 0; i < in->imu_len; ++i)
+    wimu[i] = smooth_window(in->imu_stamps[i], in->scan_start_time, in->scan_end_time, sigma_warp);
+  double mu_inc[DZ], pose0[6];
+  host::mean_increment(pred, mu_inc);
+  host::mean_world_pose(prev, pose0);
+  host::PreintOut pre;
+  host::preintegrate_imu(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wimu.data(), pose0 + 3, mu_inc + 9,
+                         mu_inc + 12, c->cfg.gravity_W, pre);
+  double xi[6];
+  host::se3_log(pre.delta_pose, xi);
+  if (c->cfg.deskew_rotation_only) xi[0] = xi[1] = xi[2] = 0.0;
+  cert[10] = pre.ess;
+  auto T1 = clk::now();
+  // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
+  int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
+                        in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr);
+  if (rc) return rc;
+  if ((rc = stage_bins(c))) return rc;
+  if ((rc = stage_mf(c))) return rc;
+  if ((rc = stage_pt(c))) return rc;
+  if ((rc = pull_scalars(c))) return rc;
+  auto T2 = clk::now();
+  const double* S = c->h_scalars;
+  // budget cert (point_budget.py:182-212)
+  double mass_in = S[SC_MASS_IN];
+  double budget_ess = 1.0 / (S[SC_BUDGET_W2] + (double)c->cap * kEpsMass);
+  double budget_mer = kEpsMass / (mass_in + kEpsMass);
+  cert[0] = budget_ess;
+  cert[1] = std::min(1.0, c->cap / (in->n_points + kEpsMass));
+  cert[2] = budget_mer;
+  cert[3] = mass_in;
+  cert[4] = c->last_n_sel;
+  cert[5] = c->last_stride;
+  Tsum += budget_mer;
+  if (!std::isfinite(mass_in)) return fail(c, GCS_ERR_NONFINITE, "non-finite point weights");
+  // deskew cert
+  cert[9] = S[SC_DESKEW_WOUT] / (S[SC_DESKEW_WIN] + kEpsMass);
+  // soft assign cert (binning.py:71-75,118-125)
+  double avg_ent = S[SC_ENTROPY] / ((double)c->cap + kEpsMass);
+  cert[11] = avg_ent;
+  cert[12] = exp(avg_ent);
+  cert[13] = S[SC_MAXRESP];
+  // moment match cert (binning.py:193-196)
+  double mm_ess = S[SC_BIN_NSUM] * S[SC_BIN_NSUM] / (S[SC_BIN_N2SUM] + kEpsMass);
+  cert[14] = mm_ess;
+  cert[15] = S[SC_BIN_SUPP] / (double)c->B;
+  cert[16] = S[SC_BIN_PSD];
+  cert[17] = S[SC_BIN_EPSR];
+  Tsum += S[SC_BIN_PSD] + S[SC_BIN_EPSR];
+  // 7 MatrixFisherRotation tail (matrix_fisher_evidence.py:240-256,310-394)
+  double pose_pred[6], R_pred[9];
+  host::mean_world_pose(pred, pose_pred);
+  so3_exp(pose_pred + 3, R_pred);
+  const double* sv = S + SC_MF_S;
+  const double* V = S + SC_MF_V;
+  const double* Rmf = S + SC_MF_R;
+  double Lrot_raw[9], Lrot[9];
+  double dg[3] = {sv[1] + sv[2], sv[0] + sv[2], sv[0] + sv[1]};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Lrot_raw[3 * i + j] = V[3 * i] * dg[0] * V[3 * j] + V[3 * i + 1] * dg[1] * V[3 * j + 1] + V[3 * i + 2] * dg[2] * V[3 * j + 2];
+  double mf_delta = host::psd_project(3, Lrot_raw, kEpsPsd, Lrot);
+  double Rerr[9], drot[3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Rerr[3 * i + j] = R_pred[i] * Rmf[j] + R_pred[3 + i] * Rmf[3 + j] + R_pred[6 + i] * Rmf[6 + j];
+  so3_log(Rerr, drot);
+  double hrot[3];
+  for (int i = 0; i < 3; ++i) hrot[i] = Lrot[3 * i] * drot[0] + Lrot[3 * i + 1] * drot[1] + Lrot[3 * i + 2] * drot[2];
+  double mf_neff = S[SC_MF_NEFF];
+  double mf_mer = kEpsMass / (mf_neff + kEpsMass);
+  cert[18] = mf_delta; cert[19] = mf_mer; cert[20] = mf_neff;
+  cert[21] = sv[0]; cert[22] = sv[1]; cert[23] = sv[2];
+  cert[24] = 0.5 * (drot[0] * hrot[0] + drot[1] * hrot[1] + drot[2] * hrot[2]);
+  Tsum += mf_delta + mf_mer;
+  // 8 PlanarTranslationEvidence tail (matrix_fisher_evidence.py:565-671)
+  double Tmap[9], ev[3], Vt[9];
+  double nd = S[SC_MF_MAPND] + kEpsMass;
+  for (int k = 0; k < 9; ++k) Tmap[k] = S[SC_MF_MAPSCAT + k] / nd;
+  double Tsym[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Tsym[3 * i + j] = 0.5 * (Tmap[3 * i + j] + Tmap[3 * j + i]);
+  host::jacobi_eigh(3, Tsym, ev, Vt);
+  std::sort(ev, ev + 3);
+  double lam1 = std::max(ev[2], kEpsMass), lam3 = std::max(ev[0], 0.0);
+  double zs = lam3 / lam1;
+  double Lf[9], hf[3], Lreg[9], twls[3];
+  for (int k = 0; k < 9; ++k) Lf[k] = S[SC_PT_L + k];
+  for (int k = 0; k < 3; ++k) hf[k] = S[SC_PT_H + k];
+  memcpy(Lreg, Lf, sizeof(Lreg));
+  Lreg[0] += kEpsMass; Lreg[4] += kEpsMass; Lreg[8] += kEpsMass;
+  host::solve3(Lreg, hf, twls);
+  double mask[3] = {1.0, 1.0, zs};
+  double Ltr_raw[9], Ltr[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Ltr_raw[3 * i + j] = Lf[3 * i + j] * mask[i] * mask[j];
+  double pt_delta = host::psd_project(3, Ltr_raw, kEpsPsd, Ltr);
+  double dtr[3] = {twls[0] - pose_pred[0], twls[1] - pose_pred[1], twls[2] - pose_pred[2]};
+  double htr[3];
+  for (int i = 0; i < 3; ++i) htr[i] = Ltr[3 * i] * dtr[0] + Ltr[3 * i + 1] * dtr[1] + Ltr[3 * i + 2] * dtr[2];
+  double pt_neff = S[SC_PT_NEFF];
+  double pt_mer = kEpsMass / (pt_neff + kEpsMass);
+  cert[25] = pt_delta; cert[26] = pt_mer; cert[27] = pt_neff; cert[28] = zs;
+  cert[29] = 0.5 * (dtr[0] * htr[0] + dtr[1] * htr[1] + dtr[2] * htr[2]);
+  Tsum += pt_delta + pt_mer;
+  memcpy(out->R_mf, Rmf, sizeof(out->R_mf));
+  memcpy(out->t_wls, twls, sizeof(out->t_wls));
+  // 9 evidence (build_combined_lidar_evidence_22d) + external + power tempering (pipeline.py:1038-1117)
+  double Lraw[DZ * DZ], hraw[DZ];
+  for (int i = 0; i < DZ * DZ; ++i) Lraw[i] = in->L_ext ? in->L_ext[i] : 0.0;
+  for (int i = 0; i < DZ; ++i) hraw[i] = in->h_ext ? in->h_ext[i] : 0.0;
+  for (int i = 0; i < 3; ++i) {
+    hraw[i] += htr[i];
+    hraw[3 + i] += hrot[i];
+    for (int j = 0; j < 3; ++j) {
+      Lraw[i * DZ + j] += Ltr[3 * i + j];
+      Lraw[(3 + i) * DZ + 3 + j] += Lrot[3 * i + j];
+    }
+  }
+  auto nrm = [](const double* v, int n, int stride) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += v[i * stride] * v[i * stride];
+    return sqrt(s);
+  };
+  double dt_pose = nrm(Lraw + 15 * DZ, 6, 1) + nrm(Lraw + 15, 6, DZ);
+  double dt_vel = nrm(Lraw + 15 * DZ + 6, 3, 1) + nrm(Lraw + 6 * DZ + 15, 3, DZ);
+  double dt_asym = fabs(dt_vel - dt_pose) / (dt_vel + dt_pose + kEpsMass);
+  dt_asym = std::min(std::max(dt_asym, 0.0), 1.0);
+  double z_to_xy = fabs(Lraw[2 * DZ + 2]) / (0.5 * (fabs(Lraw[0]) + fabs(Lraw[DZ + 1])) + kEpsMass);
+  // combined evidence cert: aggregate of the LiDAR certs [deskew, soft assign, moment match, MF, planar]
+  double ess_total = (pre.ess + cert[12] + mm_ess + 0.0 + 0.0) / 5.0;
+  double ess_to_exc = ess_total / (0.0 + kEpsMass);
+  double s_z = z_to_xy / (z_to_xy + 1.0);
+  double s_exc = 1.0 / (1.0 + ess_to_exc / 50.0);
+  double sc = std::min(std::max(dt_asym * s_z * s_exc, 0.0), 1.0);
+  double beta = 0.25 + 0.75 * sc;
+  beta = std::min(std::max(beta, 0.25), 1.0);
+  cert[30] = beta; cert[39] = dt_asym; cert[40] = z_to_xy;
+  Tsum += fabs(1.0 - beta);
+  double Lev[DZ * DZ], hev[DZ];
+  for (int i = 0; i < DZ * DZ; ++i) Lev[i] = beta * Lraw[i];
+  for (int i = 0; i < DZ; ++i) hev[i] = beta * hraw[i];
+  // excitation prior scaling (excitation.py:15-64)
+  double e_dt = Lev[15 * DZ + 15], e_ex = 0.0, p_dt = pred.L[15 * DZ + 15], p_ex = 0.0;
+  for (int i = 16; i < 22; ++i) { e_ex += Lev[i * DZ + i]; p_ex += pred.L[i * DZ + i]; }
+  double s_dt = e_dt / (e_dt + p_dt + 1e-12), s_ex = e_ex / (e_ex + p_ex + 1e-12);
+  double a_dt = 1.0 - s_dt, a_ex = 1.0 - s_ex;
+  for (int j = 0; j < DZ; ++j) { pred.L[15 * DZ + j] *= a_dt; }
+  for (int i = 0; i < DZ; ++i) { pred.L[i * DZ + 15] *= a_dt; }
+  pred.h[15] *= a_dt;
+  for (int r = 16; r < 22; ++r) for (int j = 0; j < DZ; ++j) pred.L[r * DZ + j] *= a_ex;
+  for (int i = 0; i < DZ; ++i) for (int r = 16; r < 22; ++r) pred.L[i * DZ + r] *= a_ex;
+  for (int r = 16; r < 22; ++r) pred.h[r] *= a_ex;
+  cert[31] = s_dt; cert[32] = s_ex;
+  Tsum += fabs(s_dt) + fabs(s_ex);
+  // 10 FusionScaleFromCertificates: alpha_min = alpha_max = 1 (constants.py:89-90)
+  const double alpha = 1.0;
+  cert[33] = alpha;
+  // 11 InfoFusionAdditive (fusion.py:186-191)
+  Belief post = pred;
+  double Lsum[DZ * DZ];
+  for (int i = 0; i < DZ * DZ; ++i) Lsum[i] = pred.L[i] + alpha * Lev[i];
+  double fdelta = host::psd_project(DZ, Lsum, kEpsPsd, post.L);
+  for (int i = 0; i < DZ; ++i) post.h[i] = pred.h[i] + alpha * hev[i];
+  cert[34] = fdelta;
+  Tsum += fdelta;
+  // 12 PoseUpdateFrobeniusRecompose (recompose.py:94-205)
+  cert[35] = Tsum;
+  double fs = Tsum / (Tsum + 1.0);
+  cert[36] = fs;
+  double dz[DZ], corr[6], dpc[6], e6[6];
+  host::mean_increment(post, dz);
+  host::bch3(post.z_lin, dz, corr);
+  for (int i = 0; i < 6; ++i) dpc[i] = dz[i] + fs * corr[i];
+  Belief rec = post;
+  se3_exp(dpc, e6);
+  host::se3_compose(post.X_anchor, e6, rec.X_anchor);
+  for (int i = 0; i < 6; ++i) rec.z_lin[i] = post.z_lin[i] - dpc[i];
+  for (int i = 0; i < DZ; ++i) {
+    double s = 0.0;
+    for (int j = 0; j < 6; ++j) s += post.L[i * DZ + j] * dpc[j];
+    rec.h[i] = post.h[i] - s;
+  }
+  host::process_iw_suffstats(pred.L, pred.h, rec.L, rec.h, out->iw_process_dPsi, out->iw_process_dnu);
+  memcpy(c->last_dPsi, out->iw_process_dPsi, sizeof(c->last_dPsi));
+  memcpy(c->last_dnu, out->iw_process_dnu, sizeof(c->last_dnu));
+  // 13 PoseCovInflationPushforward with z_t (pipeline.py:1244-1246)
+  double z_t[6], covr[DZ * DZ], Sig6[36];
+  host::mean_world_pose(rec, z_t);
+  host::spd_inverse_lifted(DZ, rec.L, kEpsLift, covr);
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) Sig6[6 * i + j] = covr[i * DZ + j];
+  if ((rc = stage_push(c, z_t, Sig6, c->cfg.forgetting_factor))) return rc;
+  memcpy(out->z_t, z_t, sizeof(out->z_t));
+  // 14 AnchorDriftUpdate (anchor_drift.py:93-191)
+  double dz2[DZ];
+  host::mean_increment(rec, dz2);
+  double dm = sqrt(dz2[0] * dz2[0] + dz2[1] * dz2[1] + dz2[2] * dz2[2]);
+  double dr = sqrt(dz2[3] * dz2[3] + dz2[4] * dz2[4] + dz2[5] * dz2[5]);
+  double rho = std::min(std::max(std::max(dm / 0.5, dr / 0.2), 0.0), 1.0);
+  Belief fin = rec;
+  double sd[6];
+  for (int i = 0; i < 6; ++i) sd[i] = rho * dz2[i];
+  se3_exp(sd, e6);
+  host::se3_compose(rec.X_anchor, e6, fin.X_anchor);
+  for (int i = 0; i < DZ; ++i) fin.z_lin[i] = (1.0 - rho) * dz2[i];
+  for (int i = 0; i < DZ; ++i) {
+    double s = 0.0;
+    for (int j = 0; j < DZ; ++j) s += rec.L[i * DZ + j] * fin.z_lin[j];
+    fin.h[i] = s;
+  }
+  cert[37] = rho;
+  for (int i = 0; i < DZ * DZ; ++i) out->L_evidence[i] = Lev[i];
+  for (int i = 0; i < DZ; ++i) out->h_evidence[i] = hev[i];
+  for (int i = 0; i < DZ; ++i)
+    if (!std::isfinite(fin.h[i])) return fail(c, GCS_ERR_NONFINITE, "non-finite belief after scan");
+  c->belief = fin;
+  from_host_belief(fin, out->belief);
+  c->have_last = true;
+  auto T3 = clk::now();
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  out->stage_ms[0] = ms(T0, T1);
+  out->stage_ms[1] = ms(T1, T2);
+  out->stage_ms[2] = ms(T2, T3);
+  out->stage_ms[3] = ms(T0, T3);
+  return GCS_OK;
+}
+
+// ---------------------------------------------------------------- hypothesis payload / combine
+int gcs_hypothesis_payload(gcs_ctx* c, double w_iw, double w_bary, double* p) {
+  if (!c || !p) return GCS_ERR_ARG;
+  memset(p, 0, GCS_PAYLOAD_LEN * sizeof(double));
+  int k = 0;
+  for (int i = 0; i < 252; ++i) p[k++] = w_iw * (c->have_last ? c->last_dPsi[i] : 0.0);
+  for (int i = 0; i < 7; ++i) p[k++] = w_iw * (c->have_last ? c->last_dnu[i] : 0.0);
+  k += 27 + 3;  // measurement-noise IW stats: out of scope this round (zeros)
+  const Belief& b = c->belief;
+  for (int i = 0; i < DZ * DZ; ++i) p[k++] = w_bary * b.L[i];
+  for (int i = 0; i < DZ; ++i) p[k++] = w_bary * b.h[i];
+  for (int i = 0; i < DZ; ++i) p[k++] = w_bary * b.z_lin[i];
+  double mu[DZ], n2 = 0.0;
+  host::mean_increment(b, mu);
+  for (int i = 0; i < DZ; ++i) { p[k++] = w_bary * mu[i]; n2 += mu[i] * mu[i]; }
+  p[k++] = w_bary * n2;
+  return k == GCS_PAYLOAD_LEN ? GCS_OK : fail(c, GCS_ERR_STATE, "payload size mismatch");
+}
+
+int gcs_hypothesis_combine(gcs_ctx* c, const double* p, int32_t scan_count, gcs_belief* comb, double* cert) {
+  if (!c || !p) return GCS_ERR_ARG;
+  const double* dPsi = p;
+  const double* dnu = p + 252;
+  const double* L = p + 289;
+  const double* h = L + 484;
+  const double* z = h + 22;
+  const double* mu = z + 22;
+  double n2 = mu[22];
+  Belief out{};
+  double delta = host::psd_project(DZ, L, kEpsPsd, out.L);
+  memcpy(out.h, h, sizeof(out.h));
+  memcpy(out.z_lin, z, sizeof(out.z_lin));
+  memcpy(out.X_anchor, c->belief.X_anchor, sizeof(out.X_anchor));
+  out.stamp = c->belief.stamp;
+  double m2 = 0.0;
+  for (int i = 0; i < DZ; ++i) m2 += mu[i] * mu[i];
+  double wp = std::min(1, scan_count);
+  double dP[252], dn[7], nu2[7], Psi2[252], c2[2];
+  for (int i = 0; i < 252; ++i) dP[i] = wp * dPsi[i];
+  for (int i = 0; i < 7; ++i) dn[i] = wp * dnu[i];
+  host::process_iw_apply(c->iw_nu, c->iw_Psi, dP, dn, nu2, Psi2, c2);
+  memcpy(c->iw_nu, nu2, sizeof(nu2));
+  memcpy(c->iw_Psi, Psi2, sizeof(Psi2));
+  host::process_noise_Q(c->iw_nu, c->iw_Psi, c->Q);
+  if (comb) from_host_belief(out, *comb);
+  if (cert) { cert[0] = delta; cert[1] = n2 - m2; cert[2] = c2[0]; cert[3] = c2[1]; }
+  return GCS_OK;
+}
+
+// ---------------------------------------------------------------- host numerics
+int gcs_psd_project(int32_t n, const double* M, double eps, double* out, double* cert6) {
+  if (n < 1 || n > 64 || !M || !out) return GCS_ERR_ARG;
+  host::psd_project(n, M, eps, out, cert6);
+  return GCS_OK;
+}
+int gcs_spd_solve_lifted(int32_t n, const double* L, const double* b, double eps, double* x) {
+  if (n < 1 || n > 64 || !L || !b || !x) return GCS_ERR_ARG;
+  host::spd_solve_lifted(n, L, b, eps, x);
+  return GCS_OK;
+}
+int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps, double* Li) {
+  if (n < 1 || n > 64 || !L || !Li) return GCS_ERR_ARG;
+  host::spd_inverse_lifted(n, L, eps, Li);
+  return GCS_OK;
+}
+int gcs_svd3(const double* H, double* U, double* s, double* V) {
+  if (!H || !U || !s || !V) return GCS_ERR_ARG;
+  svd3(H, U, s, V);
+  return GCS_OK;
+}
+int gcs_predict_diffusion(const gcs_belief* prev, const double* Q, double dt, gcs_belief* pred, double* cert) {
+  if (!prev || !Q || !pred) return GCS_ERR_ARG;
+  Belief a, b;
+  to_host_belief(*prev, a);
+  double infl[3];
+  host::predict_diffusion(a, Q, dt, b, infl);
+  from_host_belief(b, *pred);
+  if (cert) { cert[0] = infl[0]; cert[1] = infl[1]; cert[2] = infl[2]; cert[3] = 0.0; }
+  return GCS_OK;
+}
+int gcs_info_fusion_additive(const gcs_belief* pred, const double* L_ev, const double* h_ev, double alpha,
+                             gcs_belief* post, double* delta) {
+  if (!pred || !L_ev || !h_ev || !post) return GCS_ERR_ARG;
+  Belief a, b;
+  to_host_belief(*pred, a);
+  b = a;
+  double Ls[DZ * DZ];
+  for (int i = 0; i < DZ * DZ; ++i) Ls[i] = a.L[i] + alpha * L_ev[i];
+  double d = host::psd_project(DZ, Ls, kEpsPsd, b.L);
+  for (int i = 0; i < DZ; ++i) b.h[i] = a.h[i] + alpha * h_ev[i];
+  from_host_belief(b, *post);
+  if (delta) *delta = d;
+  return GCS_OK;
+}
+int gcs_preintegrate_imu(int32_t m, const double* st, const double* gy, const double* ac, const double* w,
+                         const double* rv, const double* gb, const double* ab, const double* g, double* dp, double* ess) {
+  if (m < 1 || !st || !gy || !ac || !w || !rv || !gb || !ab || !g || !dp) return GCS_ERR_ARG;
+  host::PreintOut o;
+  host::preintegrate_imu(m, st, gy, ac, w, rv, gb, ab, g, o);
+  memcpy(dp, o.delta_pose, 6 * sizeof(double));
+  if (ess) *ess = o.ess;
+  return GCS_OK;
+}
+int gcs_belief_world_pose(const gcs_belief* b, double* pose6) {
+  if (!b || !pose6) return GCS_ERR_ARG;
+  Belief a;
+  to_host_belief(*b, a);
+  host::mean_world_pose(a, pose6);
+  return GCS_OK;
+}
+int gcs_fibonacci_atlas(int32_t B, double* dirs) {
+  if (B < 1 || !dirs) return GCS_ERR_ARG;
+  atlas::fibonacci(B, dirs);
+  return GCS_OK;
+}
+int gcs_knn_table(int32_t B, const double* dirs, int32_t k, int32_t* knn) {
+  if (B < 1 || k < 1 || k > B || !dirs || !knn) return GCS_ERR_ARG;
+  atlas::knn(dirs, B, k, knn);
+  return GCS_OK;
+}
+int gcs_nearest_bins(int32_t B, const double* dirs, int32_t nq, const double* q, int32_t* out) {
+  if (B < 1 || nq < 0 || !dirs || (nq && (!q || !out))) return GCS_ERR_ARG;
+  atlas::nearest(dirs, B, nq, q, out);
+  return GCS_OK;
+}
+
+}  // extern "C"

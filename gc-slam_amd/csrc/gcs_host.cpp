@@ -1,0 +1,367 @@
+// Host 22-D numerics (see gcs_host.h).  Each function cites the reference it restates.
+#include "gcs_host.h"
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+
+#include "gcs_math.h"
+
+namespace gcs {
+namespace host {
+
+void jacobi_eigh(int n, const double* A, double* w, double* V) {
+  std::vector<double> a(A, A + n * n);
+  for (int i = 0; i < n * n; ++i) V[i] = 0.0;
+  for (int i = 0; i < n; ++i) V[i * n + i] = 1.0;
+  double fro = 0.0;
+  for (int i = 0; i < n * n; ++i) fro += a[i] * a[i];
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0.0;
+    for (int p = 0; p < n; ++p)
+      for (int q = p + 1; q < n; ++q) off += a[p * n + q] * a[p * n + q];
+    if (off == 0.0 || off <= 1e-36 * fro) break;
+    for (int p = 0; p < n - 1; ++p) {
+      for (int q = p + 1; q < n; ++q) {
+        double apq = a[p * n + q];
+        if (apq == 0.0) continue;
+        double app = a[p * n + p], aqq = a[q * n + q];
+        if (fabs(apq) < 1e-18 * sqrt(fabs(app * aqq)) && sweep > 3) {
+          a[p * n + q] = a[q * n + p] = 0.0;
+          continue;
+        }
+        double theta = (aqq - app) / (2.0 * apq);
+        double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+        double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        for (int k = 0; k < n; ++k) {
+          double akp = a[k * n + p], akq = a[k * n + q];
+          a[k * n + p] = c * akp - s * akq;
+          a[k * n + q] = s * akp + c * akq;
+        }
+        for (int k = 0; k < n; ++k) {
+          double apk = a[p * n + k], aqk = a[q * n + k];
+          a[p * n + k] = c * apk - s * aqk;
+          a[q * n + k] = s * apk + c * aqk;
+        }
+        a[p * n + q] = a[q * n + p] = 0.0;
+        for (int k = 0; k < n; ++k) {
+          double vkp = V[k * n + p], vkq = V[k * n + q];
+          V[k * n + p] = c * vkp - s * vkq;
+          V[k * n + q] = s * vkp + c * vkq;
+        }
+      }
+    }
+  }
+  for (int i = 0; i < n; ++i) w[i] = a[i * n + i];
+}
+
+// domain_projection_psd_core, FS/common/primitives.py:80-123
+double psd_project(int n, const double* M, double eps_psd, double* out, double* cert6) {
+  std::vector<double> s(n * n), w(n), V(n * n);
+  double sym2 = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      s[i * n + j] = 0.5 * (M[i * n + j] + M[j * n + i]);
+      double d = s[i * n + j] - M[i * n + j];
+      sym2 += d * d;
+    }
+  bool zero = true;
+  for (int i = 0; i < n * n; ++i) zero = zero && s[i] == 0.0;
+  if (zero) {
+    for (int i = 0; i < n * n; ++i) V[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
+    for (int i = 0; i < n; ++i) w[i] = 0.0;
+  } else {
+    jacobi_eigh(n, s.data(), w.data(), V.data());
+  }
+  double emin = INFINITY, emax = -INFINITY, nn = 0.0;
+  for (int k = 0; k < n; ++k) {
+    w[k] = w[k] > eps_psd ? w[k] : eps_psd;
+    emin = std::min(emin, w[k]);
+    emax = std::max(emax, w[k]);
+    nn += (w[k] < 10.0 * eps_psd) ? 1.0 : 0.0;
+  }
+  double d2 = 0.0;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double v = 0.0;
+      for (int k = 0; k < n; ++k) v += V[i * n + k] * w[k] * V[j * n + k];
+      out[i * n + j] = v;
+      double dd = v - s[i * n + j];
+      d2 += dd * dd;
+    }
+  double delta = sqrt(d2);
+  if (cert6) {
+    cert6[0] = delta; cert6[1] = sqrt(sym2); cert6[2] = emin; cert6[3] = emax; cert6[4] = emax / emin; cert6[5] = nn;
+  }
+  return delta;
+}
+
+bool cholesky(int n, const double* A, double* Lc) {
+  for (int i = 0; i < n * n; ++i) Lc[i] = 0.0;
+  for (int j = 0; j < n; ++j) {
+    double s = A[j * n + j];
+    for (int k = 0; k < j; ++k) s -= Lc[j * n + k] * Lc[j * n + k];
+    if (!(s > 0.0)) return false;
+    double d = sqrt(s);
+    Lc[j * n + j] = d;
+    for (int i = j + 1; i < n; ++i) {
+      double t = A[i * n + j];
+      for (int k = 0; k < j; ++k) t -= Lc[i * n + k] * Lc[j * n + k];
+      Lc[i * n + j] = t / d;
+    }
+  }
+  return true;
+}
+
+// spd_cholesky_solve_lifted_core, primitives.py:141-166
+void spd_solve_lifted(int n, const double* L, const double* b, double eps_lift, double* x) {
+  std::vector<double> A(L, L + n * n), Lc(n * n), y(n);
+  for (int i = 0; i < n; ++i) A[i * n + i] += eps_lift;
+  cholesky(n, A.data(), Lc.data());
+  for (int i = 0; i < n; ++i) {
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= Lc[i * n + k] * y[k];
+    y[i] = s / Lc[i * n + i];
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    double s = y[i];
+    for (int k = i + 1; k < n; ++k) s -= Lc[k * n + i] * x[k];
+    x[i] = s / Lc[i * n + i];
+  }
+}
+
+// spd_cholesky_inverse_lifted_core, primitives.py:169-192
+void spd_inverse_lifted(int n, const double* L, double eps_lift, double* Linv) {
+  std::vector<double> A(L, L + n * n), Lc(n * n), Ci(n * n, 0.0);
+  for (int i = 0; i < n; ++i) A[i * n + i] += eps_lift;
+  cholesky(n, A.data(), Lc.data());
+  for (int c = 0; c < n; ++c)
+    for (int i = 0; i < n; ++i) {
+      double s = (i == c) ? 1.0 : 0.0;
+      for (int k = 0; k < i; ++k) s -= Lc[i * n + k] * Ci[k * n + c];
+      Ci[i * n + c] = s / Lc[i * n + i];
+    }
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      double s = 0.0;
+      for (int k = 0; k < n; ++k) s += Ci[k * n + i] * Ci[k * n + j];
+      Linv[i * n + j] = s;
+    }
+}
+
+void solve3(const double* A, const double* b, double* x) {
+  double M[3][4];
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) M[i][j] = A[3 * i + j];
+    M[i][3] = b[i];
+  }
+  for (int c = 0; c < 3; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < 3; ++r)
+      if (fabs(M[r][c]) > fabs(M[piv][c])) piv = r;
+    if (piv != c)
+      for (int j = 0; j < 4; ++j) std::swap(M[c][j], M[piv][j]);
+    for (int r = c + 1; r < 3; ++r) {
+      double f = M[r][c] / M[c][c];
+      for (int j = c; j < 4; ++j) M[r][j] -= f * M[c][j];
+    }
+  }
+  for (int i = 2; i >= 0; --i) {
+    double s = M[i][3];
+    for (int j = i + 1; j < 3; ++j) s -= M[i][j] * x[j];
+    x[i] = s / M[i][i];
+  }
+}
+
+// se3_compose, se3_jax.py:405-424
+void se3_compose(const double* a, const double* b, double* out) {
+  double Ra[9], Rb[9], R[9];
+  so3_exp(a + 3, Ra);
+  so3_exp(b + 3, Rb);
+  mat3_mul(Ra, Rb, R);
+  for (int i = 0; i < 3; ++i) out[i] = a[i] + Ra[3 * i] * b[0] + Ra[3 * i + 1] * b[1] + Ra[3 * i + 2] * b[2];
+  so3_log(R, out + 3);
+}
+
+// se3_log, se3_jax.py:210-245 (with _se3_V_inv, :169-207)
+void se3_log(const double* T, double* out) {
+  double R[9], phi[3];
+  so3_exp(T + 3, R);
+  so3_log(R, phi);
+  double theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  double theta = sqrt(theta_sq);
+  bool small = theta < kSmallAngle;
+  double st = small ? 1.0 : theta;
+  double st2 = theta_sq < kSmallAngle * kSmallAngle ? 1.0 : theta_sq;
+  double denom = 2.0 * st * sin(st) + 1e-12;
+  double D = small ? 1.0 / 12.0 + theta_sq / 720.0 : (1.0 / st2) - (1.0 + cos(st)) / denom;
+  double K[9], K2[9];
+  skew3(phi, K);
+  mat3_mul(K, K, K2);
+  for (int i = 0; i < 3; ++i) {
+    double acc = T[i];
+    for (int j = 0; j < 3; ++j) acc += (-0.5 * K[3 * i + j] + D * K2[3 * i + j]) * T[j];
+    out[i] = acc;
+  }
+  out[3] = phi[0]; out[4] = phi[1]; out[5] = phi[2];
+}
+
+// BeliefGaussianInfo.mean_increment / mean_world_pose, belief.py:373-434
+void mean_increment(const Belief& b, double* dz) { spd_solve_lifted(DZ, b.L, b.h, kEpsLift, dz); }
+
+void mean_world_pose(const Belief& b, double* pose6) {
+  double dz[DZ], e[6];
+  mean_increment(b, dz);
+  se3_exp(dz, e);
+  se3_compose(b.X_anchor, e, pose6);
+}
+
+// _predict_diffusion_core, predict.py:43-103
+void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& pred, double* infl3) {
+  const int n = DZ;
+  double mean_prev[DZ], cov_prev[DZ * DZ], cov_raw[DZ * DZ], cov_psd[DZ * DZ], Lp[DZ * DZ], Lpsd[DZ * DZ];
+  spd_solve_lifted(n, prev.L, prev.h, kEpsLift, mean_prev);
+  spd_inverse_lifted(n, prev.L, kEpsLift, cov_prev);
+  const double lam = 0.1;  // GC_OU_DAMPING_LAMBDA, constants.py:248
+  double ef = exp(-2.0 * lam * dt);
+  double dc = (1.0 - ef) / (2.0 * lam + kF64Eps);
+  for (int i = 0; i < n * n; ++i) cov_raw[i] = ef * cov_prev[i] + dc * Q[i];
+  double d1 = psd_project(n, cov_raw, kEpsPsd, cov_psd);
+  spd_inverse_lifted(n, cov_psd, kEpsLift, Lp);
+  double d2 = psd_project(n, Lp, kEpsPsd, Lpsd);
+  memcpy(pred.X_anchor, prev.X_anchor, sizeof(pred.X_anchor));
+  pred.stamp = prev.stamp + dt;
+  memcpy(pred.z_lin, prev.z_lin, sizeof(pred.z_lin));
+  memcpy(pred.L, Lpsd, sizeof(pred.L));
+  for (int i = 0; i < n; ++i) {
+    double s = 0.0;
+    for (int j = 0; j < n; ++j) s += Lpsd[i * n + j] * mean_prev[j];
+    pred.h[i] = s;
+  }
+  infl3[0] = 2.0 * kEpsLift * n;
+  infl3[1] = d1 + d2;
+  infl3[2] = dt;
+}
+
+// preintegrate_imu_relative_pose_jax, imu_preintegration.py:47-147
+void preintegrate_imu(int m, const double* stamps, const double* gyro, const double* accel, const double* w,
+                      const double* rotvec_start, const double* gb, const double* ab, const double* g, PreintOut& out) {
+  double R[9], v[3] = {0, 0, 0}, p[3] = {0, 0, 0};
+  so3_exp(rotvec_start, R);
+  double ess = 0.0;
+  for (int i = 0; i < m; ++i) ess += w[i];
+  for (int i = 0; i < m; ++i) {
+    double dt = (i + 1 < m) ? stamps[i + 1] - stamps[i] : 0.0;
+    dt = dt > 0.0 ? dt : 0.0;
+    double dte = w[i] * dt;
+    double om[3] = {(gyro[3 * i] - gb[0]) * dte, (gyro[3 * i + 1] - gb[1]) * dte, (gyro[3 * i + 2] - gb[2]) * dte};
+    double dR[9], Rn[9];
+    so3_exp(om, dR);
+    mat3_mul(R, dR, Rn);
+    double a_body[3] = {accel[3 * i] - ab[0], accel[3 * i + 1] - ab[1], accel[3 * i + 2] - ab[2]};
+    double aw[3];
+    for (int k = 0; k < 3; ++k) aw[k] = R[3 * k] * a_body[0] + R[3 * k + 1] * a_body[1] + R[3 * k + 2] * a_body[2] + g[k];
+    for (int k = 0; k < 3; ++k) {
+      double vn = v[k] + aw[k] * dte;
+      p[k] = p[k] + v[k] * dte + 0.5 * aw[k] * (dte * dte);
+      v[k] = vn;
+    }
+    memcpy(R, Rn, sizeof(R));
+  }
+  double R0[9], dR[9];
+  so3_exp(rotvec_start, R0);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) dR[3 * i + j] = R0[i] * R[j] + R0[3 + i] * R[3 + j] + R0[6 + i] * R[6 + j];
+  for (int i = 0; i < 3; ++i) out.delta_pose[i] = R0[i] * p[0] + R0[3 + i] * p[1] + R0[6 + i] * p[2];
+  so3_log(dR, out.delta_pose + 3);
+  out.ess = ess;
+}
+
+static const int kBlkDim[7] = {3, 3, 3, 3, 3, 1, 6};
+static const int kBlkStart[7] = {0, 3, 6, 9, 12, 15, 16};
+
+// process_noise_iw_suffstats_from_info_jax, inverse_wishart_jax.py:71-123
+void process_iw_suffstats(const double* L_pred, const double* h_pred, const double* L_post, const double* h_post,
+                          double* dPsi, double* dnu) {
+  double mu0[DZ], mu1[DZ], Sig[DZ * DZ];
+  spd_solve_lifted(DZ, L_pred, h_pred, kEpsLift, mu0);
+  spd_solve_lifted(DZ, L_post, h_post, kEpsLift, mu1);
+  spd_inverse_lifted(DZ, L_post, kEpsLift, Sig);
+  for (int i = 0; i < 7 * 36; ++i) dPsi[i] = 0.0;
+  for (int b = 0; b < 7; ++b) {
+    int s0 = kBlkStart[b], d = kBlkDim[b];
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < d; ++j)
+        dPsi[b * 36 + i * 6 + j] = (mu1[s0 + i] - mu0[s0 + i]) * (mu1[s0 + j] - mu0[s0 + j]) + Sig[(s0 + i) * DZ + s0 + j];
+    dnu[b] = 1.0;
+  }
+}
+
+// create_datasheet_process_noise_state, structures/inverse_wishart_jax.py:42-80
+void datasheet_iw_state(double* nu, double* Psi) {
+  const double sig[7] = {1e-4, 8.7e-7, 9.5e-5, 1e-8, 1e-6, 1e-6, 1e-8};
+  for (int i = 0; i < 7 * 36; ++i) Psi[i] = 0.0;
+  for (int b = 0; b < 7; ++b) {
+    nu[b] = kBlkDim[b] + 1.0 + 0.5;
+    for (int i = 0; i < kBlkDim[b]; ++i) Psi[b * 36 + i * 6 + i] = sig[b] * 0.5;
+  }
+}
+
+static double softplus(double x) { return x > 0.0 ? x + log1p(exp(-x)) : log1p(exp(x)); }
+
+// process_noise_state_to_Q_jax, inverse_wishart_jax.py:35-68
+void process_noise_Q(const double* nu, const double* Psi, double* Q) {
+  double Qr[DZ * DZ];
+  for (int i = 0; i < DZ * DZ; ++i) Qr[i] = 0.0;
+  for (int b = 0; b < 7; ++b) {
+    double denom = softplus(50.0 * (nu[b] - kBlkDim[b] - 1.0)) / 50.0 + 1e-12;
+    int s0 = kBlkStart[b];
+    int e = std::min(s0 + 6, DZ) - s0;
+    for (int i = 0; i < e; ++i)
+      for (int j = 0; j < e; ++j) {
+        double mask = (i < kBlkDim[b] && j < kBlkDim[b]) ? 1.0 : 0.0;
+        Qr[(s0 + i) * DZ + s0 + j] = Psi[b * 36 + i * 6 + j] / denom * mask;
+      }
+  }
+  psd_project(DZ, Qr, kEpsPsd, Q);
+}
+
+// process_noise_iw_apply_suffstats_jax, inverse_wishart_jax.py:126-185
+void process_iw_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double* nu_out,
+                      double* Psi_out, double* cert2) {
+  const double rho[7] = {0.99, 0.995, 0.95, 0.999, 0.999, 0.9999, 0.9999};
+  double dsum = 0.0, nsum = 0.0;
+  for (int b = 0; b < 7; ++b) {
+    double raw[36];
+    for (int i = 0; i < 6; ++i)
+      for (int j = 0; j < 6; ++j) {
+        double mask = (i < kBlkDim[b] && j < kBlkDim[b]) ? 1.0 : 0.0;
+        raw[i * 6 + j] = (rho[b] * Psi[b * 36 + i * 6 + j] + dPsi[b * 36 + i * 6 + j]) * mask;
+      }
+    dsum += psd_project(6, raw, kEpsPsd, Psi_out + b * 36);
+    double nu_raw = rho[b] * nu[b] + dnu[b];
+    double nu_min = kBlkDim[b] + 1.0 + 0.5;
+    double nu_floor = nu_min + softplus(nu_raw - nu_min);
+    double nn = 1000.0 - softplus(1000.0 - nu_floor);
+    nsum += fabs(nn - nu_raw);
+    nu_out[b] = nn;
+  }
+  cert2[0] = dsum;
+  cert2[1] = nsum;
+}
+
+// _bch3_correction, recompose.py:50-91
+void bch3(const double* xi1, const double* xi2, double* out) {
+  double c1[3], c2[3], c3[3];
+  cross3(xi1 + 3, xi2, c1);
+  cross3(xi1, xi2 + 3, c2);
+  cross3(xi1 + 3, xi2 + 3, c3);
+  for (int i = 0; i < 3; ++i) {
+    out[i] = 0.5 * (c1[i] + c2[i]);
+    out[3 + i] = 0.5 * c3[i];
+  }
+}
+
+}  // namespace host
+}  // namespace gcs

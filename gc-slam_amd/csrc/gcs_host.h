@@ -1,0 +1,58 @@
+// Host-side 22-D numerics: the tail of the per-scan pipeline (predict, tempering, fusion,
+// recompose, IW, hypothesis combine).  Restates FS/common/primitives.py, FS/common/belief.py
+// and the small operators in FS/backend/operators/ in C++ (the 22x22 algebra is latency bound;
+// SURVEY.md section 7 step 5 places it on host C++ or one workgroup).
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+namespace gcs {
+namespace host {
+
+constexpr int DZ = 22;
+
+// Symmetric eigen-decomposition by cyclic Jacobi (row-major n x n); w unsorted, V columns.
+void jacobi_eigh(int n, const double* A, double* w, double* V);
+// domain_projection_psd_core; cert6 = [delta, sym_delta, eig_min, eig_max, cond, near_null]
+double psd_project(int n, const double* M, double eps_psd, double* out, double* cert6 = nullptr);
+bool cholesky(int n, const double* A, double* Lc);
+void spd_solve_lifted(int n, const double* L, const double* b, double eps_lift, double* x);
+void spd_inverse_lifted(int n, const double* L, double eps_lift, double* Linv);
+void solve3(const double* A, const double* b, double* x);  // LU with partial pivoting
+
+struct Belief {
+  double X_anchor[6];
+  double stamp;
+  double z_lin[DZ];
+  double L[DZ * DZ];
+  double h[DZ];
+};
+
+void se3_compose(const double* a, const double* b, double* out);
+void se3_log(const double* T, double* out);
+void mean_increment(const Belief& b, double* dz);
+void mean_world_pose(const Belief& b, double* pose6);
+
+// predict_diffusion (predict.py:43-103); infl = [lift_strength, psd_delta, dt_scale]
+void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& pred, double* infl3);
+
+struct PreintOut {
+  double delta_pose[6];
+  double ess;
+};
+void preintegrate_imu(int m, const double* stamps, const double* gyro, const double* accel, const double* w,
+                      const double* rotvec_start, const double* gb, const double* ab, const double* g, PreintOut& out);
+
+// IW process noise (inverse_wishart_jax.py)
+void process_iw_suffstats(const double* L_pred, const double* h_pred, const double* L_post, const double* h_post,
+                          double* dPsi /*7x36*/, double* dnu /*7*/);
+void datasheet_iw_state(double* nu, double* Psi);
+void process_noise_Q(const double* nu, const double* Psi, double* Q);
+void process_iw_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double* nu_out,
+                      double* Psi_out, double* cert2);
+
+void bch3(const double* xi1, const double* xi2, double* out);
+
+}  // namespace host
+}  // namespace gcs

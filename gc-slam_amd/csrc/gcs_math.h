@@ -1,0 +1,356 @@
+// Host/device f64 math shared by the HIP kernels and the host 22-D tail.
+// Lie maps restate fl_ws/src/fl_slam_poc/fl_slam_poc/common/geometry/se3_jax.py;
+// the PSD projection restates domain_projection_psd_core (common/primitives.py:80-123)
+// with a 3x3 cyclic Jacobi eigensolver instead of LAPACK syevd.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#define GCS_HD __host__ __device__ __forceinline__
+
+namespace gcs {
+
+constexpr double kEpsPsd = 1e-12;     // constants.py:70
+constexpr double kEpsLift = 1e-9;     // constants.py:71
+constexpr double kEpsMass = 1e-12;    // constants.py:72
+constexpr double kEpsR = 1e-6;        // constants.py:73
+constexpr double kKappaR0 = 0.8;      // constants.py:95
+constexpr double kKappaTau = 0.03;    // constants.py:96
+constexpr double kF64Eps = 2.220446049250313e-16;
+constexpr double kSmallAngle = 1e-7;  // se3_jax.py:29
+constexpr double kWeightFloor = 1e-12;  // constants.py:256
+constexpr double kTimeWarpSigmaFrac = 0.1;  // constants.py:143
+
+// Canonical dot (x*x' + y*y') + z*z' with no fused multiply-add: the op order the
+// oracle uses, so nearest-bin / kNN decisions are bit-identical (DESIGN.md "indices").
+GCS_HD double dot3_exact(double ax, double ay, double az, double bx, double by, double bz) {
+#pragma clang fp contract(off)
+  double xx = ax * bx;
+  double yy = ay * by;
+  double zz = az * bz;
+  double s = xx + yy;
+  return s + zz;
+}
+
+GCS_HD double sigmoid(double x) {
+  // numerically symmetric logistic
+  if (x >= 0.0) {
+    double e = exp(-x);
+    return 1.0 / (1.0 + e);
+  }
+  double e = exp(x);
+  return e / (1.0 + e);
+}
+
+// smooth_window_weights, imu_preintegration.py:20-43
+GCS_HD double smooth_window(double t, double start, double end, double sigma) {
+  double sig = sigma > 1e-6 ? sigma : 1e-6;
+  double w = sigmoid((t - start) / sig) * sigmoid((end - t) / sig);
+  return w * (1.0 - kWeightFloor) + kWeightFloor;
+}
+
+// kappa_from_resultant_batch, kappa.py:130-169
+GCS_HD double kappa_from_rbar(double rbar) {
+  double R = rbar < 0.0 ? 0.0 : rbar;
+  R = R > 1.0 - kEpsR ? 1.0 - kEpsR : R;
+  double R2 = R * R;
+  double k_low = (R * (3.0 - R2)) / (1.0 - R2 + kEpsR);
+  double om = 1.0 - R2;
+  double k_high = -log(om > kEpsR ? om : kEpsR);
+  double s = sigmoid((R - kKappaR0) / kKappaTau);
+  return (1.0 - s) * k_low + s * k_high;
+}
+
+// --------------------------------------------------------------------------- 3x3 helpers
+// Symmetric 3x3 stored as a[9] row-major.
+GCS_HD void mat3_mul(const double* A, const double* B, double* C) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+
+GCS_HD void skew3(const double* v, double* K) {
+  K[0] = 0.0; K[1] = -v[2]; K[2] = v[1];
+  K[3] = v[2]; K[4] = 0.0; K[5] = -v[0];
+  K[6] = -v[1]; K[7] = v[0]; K[8] = 0.0;
+}
+
+// so3_exp, se3_jax.py:260-300
+GCS_HD void so3_exp(const double* w, double* R) {
+  double theta_sq = w[0] * w[0] + w[1] * w[1] + w[2] * w[2];
+  double theta = sqrt(theta_sq);
+  double K[9], K2[9];
+  skew3(w, K);
+  mat3_mul(K, K, K2);
+  bool small = theta < kSmallAngle;
+  double st = small ? 1.0 : theta;
+  double st2 = theta_sq < kSmallAngle * kSmallAngle ? 1.0 : theta_sq;
+  double a = small ? 1.0 : sin(st) / st;
+  double b = small ? 0.5 : (1.0 - cos(st)) / st2;
+  for (int i = 0; i < 9; ++i) R[i] = a * K[i] + b * K2[i];
+  R[0] += 1.0; R[4] += 1.0; R[8] += 1.0;
+}
+
+// so3_log, se3_jax.py:303-365 (softmax near-pi axis mixture)
+GCS_HD void so3_log(const double* R, double* w) {
+  double ct = 0.5 * (R[0] + R[4] + R[8] - 1.0);
+  ct = ct < -1.0 ? -1.0 : (ct > 1.0 ? 1.0 : ct);
+  double theta = acos(ct);
+  double vx = 0.5 * (R[7] - R[5]), vy = 0.5 * (R[2] - R[6]), vz = 0.5 * (R[3] - R[1]);
+  if (theta < kSmallAngle) { w[0] = vx; w[1] = vy; w[2] = vz; return; }
+  const double pi = 3.141592653589793;
+  if (fabs(theta - pi) < 1e-7) {
+    double d0 = 50.0 * (R[0] + 1.0), d1 = 50.0 * (R[4] + 1.0), d2 = 50.0 * (R[8] + 1.0);
+    double m = d0 > d1 ? d0 : d1; m = m > d2 ? m : d2;
+    double e0 = exp(d0 - m), e1 = exp(d1 - m), e2 = exp(d2 - m), es = e0 + e1 + e2;
+    e0 /= es; e1 /= es; e2 /= es;
+    double ax = e0 * (R[0] + 1.0) + e1 * R[1] + e2 * R[2];
+    double ay = e0 * R[3] + e1 * (R[4] + 1.0) + e2 * R[5];
+    double az = e0 * R[6] + e1 * R[7] + e2 * (R[8] + 1.0);
+    double n = sqrt(ax * ax + ay * ay + az * az);
+    n = n < kSmallAngle ? 1.0 : n;
+    w[0] = ax / n * theta; w[1] = ay / n * theta; w[2] = az / n * theta;
+    return;
+  }
+  double s = sin(theta);
+  s = fabs(s) < kSmallAngle ? 1.0 : s;
+  double f = theta / (2.0 * s);
+  w[0] = f * (2.0 * vx); w[1] = f * (2.0 * vy); w[2] = f * (2.0 * vz);
+}
+
+// B(theta), C(theta) of se3_exp / se3_V, se3_jax.py:488-500
+GCS_HD void se3_BC(double theta_sq, double* B, double* C, double* sin_c, double* cos_c) {
+  double theta = sqrt(theta_sq);
+  bool small = theta < kSmallAngle;
+  double st = small ? 1.0 : theta;
+  double st2 = theta_sq < kSmallAngle * kSmallAngle ? 1.0 : theta_sq;
+  double sn = sin(st), cs = cos(st);
+  *B = small ? 0.5 - theta_sq / 24.0 : (1.0 - cs) / st2;
+  *C = small ? 1.0 / 6.0 - theta_sq / 120.0 : (st - sn) / (st2 * st);
+  *sin_c = small ? 1.0 : sn / st;
+  *cos_c = small ? 0.5 : (1.0 - cs) / st2;
+}
+
+// se3_exp (se3_jax.py:474-504): out = [V rho, phi]
+GCS_HD void se3_exp(const double* xi, double* out) {
+  const double* phi = xi + 3;
+  double theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  double B, C, a, b;
+  se3_BC(theta_sq, &B, &C, &a, &b);
+  double K[9], K2[9];
+  skew3(phi, K);
+  mat3_mul(K, K, K2);
+  for (int i = 0; i < 3; ++i) {
+    double acc = xi[i];
+    for (int j = 0; j < 3; ++j) acc += (B * K[3 * i + j] + C * K2[3 * i + j]) * xi[j];
+    out[i] = acc;
+  }
+  out[3] = phi[0]; out[4] = phi[1]; out[5] = phi[2];
+}
+
+// Per-point deskew: T = se3_exp(alpha xi); p0 = R^T (p - t)  (deskew_constant_twist.py:51-58)
+GCS_HD void deskew_point(double alpha, const double* xi, const double* p, double* p0) {
+  double rho[3] = {alpha * xi[0], alpha * xi[1], alpha * xi[2]};
+  double phi[3] = {alpha * xi[3], alpha * xi[4], alpha * xi[5]};
+  double theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  double B, C, a, b;
+  se3_BC(theta_sq, &B, &C, &a, &b);
+  double K[9], K2[9];
+  skew3(phi, K);
+  mat3_mul(K, K, K2);
+  double t[3];
+  for (int i = 0; i < 3; ++i) {
+    t[i] = rho[i] + (B * K[3 * i] + C * K2[3 * i]) * rho[0] + (B * K[3 * i + 1] + C * K2[3 * i + 1]) * rho[1] +
+           (B * K[3 * i + 2] + C * K2[3 * i + 2]) * rho[2];
+  }
+  double q[3] = {p[0] - t[0], p[1] - t[1], p[2] - t[2]};
+  for (int i = 0; i < 3; ++i) {
+    // column i of R: R[j][i] = delta_ji + a K[j][i] + b K2[j][i]
+    double acc = q[i];
+    for (int j = 0; j < 3; ++j) acc += (a * K[3 * j + i] + b * K2[3 * j + i]) * q[j];
+    p0[i] = acc;
+  }
+}
+
+// Cyclic Jacobi eigensolver for a symmetric 3x3 (row-major a[9]); returns eigenvalues w[3]
+// (unsorted) and eigenvectors as columns of V[9].  Deterministic sweep order (0,1),(0,2),(1,2).
+GCS_HD void eigh3_jacobi(const double* A, double* w, double* V) {
+  double a[9];
+  for (int i = 0; i < 9; ++i) { a[i] = A[i]; V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    double off = a[1] * a[1] + a[2] * a[2] + a[5] * a[5];
+    double diag = a[0] * a[0] + a[4] * a[4] + a[8] * a[8];
+    if (off <= 1e-40 * diag || off == 0.0) break;
+    for (int pq = 0; pq < 3; ++pq) {
+      int p = pq == 2 ? 1 : 0;
+      int q = pq == 0 ? 1 : 2;
+      double apq = a[3 * p + q];
+      if (apq == 0.0) continue;
+      double app = a[4 * p], aqq = a[4 * q];
+      double theta = (aqq - app) / (2.0 * apq);
+      double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+      double c = 1.0 / sqrt(t * t + 1.0);
+      double s = t * c;
+      // A' = J^T A J with J = rotation in (p,q)
+      for (int k = 0; k < 3; ++k) {
+        double akp = a[3 * k + p], akq = a[3 * k + q];
+        a[3 * k + p] = c * akp - s * akq;
+        a[3 * k + q] = s * akp + c * akq;
+      }
+      for (int k = 0; k < 3; ++k) {
+        double apk = a[3 * p + k], aqk = a[3 * q + k];
+        a[3 * p + k] = c * apk - s * aqk;
+        a[3 * q + k] = s * apk + c * aqk;
+      }
+      a[3 * p + q] = 0.0;
+      a[3 * q + p] = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        double vkp = V[3 * k + p], vkq = V[3 * k + q];
+        V[3 * k + p] = c * vkp - s * vkq;
+        V[3 * k + q] = s * vkp + c * vkq;
+      }
+    }
+  }
+  w[0] = a[0]; w[1] = a[4]; w[2] = a[8];
+}
+
+// DomainProjectionPSD for a 3x3 (primitives.py:80-123).  M_psd = V diag(max(w,eps)) V^T
+// and the projection delta ||M_psd - M_sym||_F.  Exact fast path for the all-zero matrix
+// (LAPACK returns V = I there, so the reference gives eps*I and delta = sqrt(3) eps exactly).
+GCS_HD double psd_project3(const double* M, double* out) {
+  double s[9];
+  s[0] = M[0]; s[4] = M[4]; s[8] = M[8];
+  s[1] = s[3] = 0.5 * (M[1] + M[3]);
+  s[2] = s[6] = 0.5 * (M[2] + M[6]);
+  s[5] = s[7] = 0.5 * (M[5] + M[7]);
+  bool zero = true;
+  for (int i = 0; i < 9; ++i) zero = zero && (s[i] == 0.0);
+  if (zero) {
+    for (int i = 0; i < 9; ++i) out[i] = (i % 4 == 0) ? kEpsPsd : 0.0;
+    return 1.7320508075688772e-12;
+  }
+  double w[3], V[9];
+  eigh3_jacobi(s, w, V);
+  for (int k = 0; k < 3; ++k) w[k] = w[k] > kEpsPsd ? w[k] : kEpsPsd;
+  double d2 = 0.0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double v = V[3 * i] * w[0] * V[3 * j] + V[3 * i + 1] * w[1] * V[3 * j + 1] + V[3 * i + 2] * w[2] * V[3 * j + 2];
+      out[3 * i + j] = v;
+      double dd = v - s[3 * i + j];
+      d2 += dd * dd;
+    }
+  return sqrt(d2);
+}
+
+// Inverse of a general 3x3 via adjugate / determinant (jnp.linalg.inv restated).
+GCS_HD void inv3(const double* m, double* o) {
+  double c00 = m[4] * m[8] - m[5] * m[7];
+  double c01 = m[5] * m[6] - m[3] * m[8];
+  double c02 = m[3] * m[7] - m[4] * m[6];
+  double det = m[0] * c00 + m[1] * c01 + m[2] * c02;
+  double id = 1.0 / det;
+  o[0] = c00 * id;
+  o[1] = (m[2] * m[7] - m[1] * m[8]) * id;
+  o[2] = (m[1] * m[5] - m[2] * m[4]) * id;
+  o[3] = c01 * id;
+  o[4] = (m[0] * m[8] - m[2] * m[6]) * id;
+  o[5] = (m[2] * m[3] - m[0] * m[5]) * id;
+  o[6] = c02 * id;
+  o[7] = (m[1] * m[6] - m[0] * m[7]) * id;
+  o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
+}
+
+GCS_HD void cross3(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// 3x3 SVD H = U diag(s) V^T by one-sided (Hestenes) Jacobi, s sorted descending.
+// Columns of U for (numerically) zero singular values are completed orthonormally; the
+// Matrix-Fisher consumer fixes det(U V^T) afterwards, so the completion sign is immaterial.
+GCS_HD void svd3(const double* H, double* U, double* s, double* V) {
+  double A[9];
+  for (int i = 0; i < 9; ++i) { A[i] = H[i]; V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
+  for (int sweep = 0; sweep < 30; ++sweep) {
+    bool rotated = false;
+    for (int pq = 0; pq < 3; ++pq) {
+      int p = pq == 2 ? 1 : 0;
+      int q = pq == 0 ? 1 : 2;
+      double al = 0.0, be = 0.0, ga = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        al += A[3 * k + p] * A[3 * k + p];
+        be += A[3 * k + q] * A[3 * k + q];
+        ga += A[3 * k + p] * A[3 * k + q];
+      }
+      if (ga == 0.0 || fabs(ga) <= 1e-17 * sqrt(al * be)) continue;
+      rotated = true;
+      double zeta = (be - al) / (2.0 * ga);
+      double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+      double c = 1.0 / sqrt(1.0 + t * t);
+      double sn = c * t;
+      for (int k = 0; k < 3; ++k) {
+        double ap = A[3 * k + p], aq = A[3 * k + q];
+        A[3 * k + p] = c * ap - sn * aq;
+        A[3 * k + q] = sn * ap + c * aq;
+        double vp = V[3 * k + p], vq = V[3 * k + q];
+        V[3 * k + p] = c * vp - sn * vq;
+        V[3 * k + q] = sn * vp + c * vq;
+      }
+    }
+    if (!rotated) break;
+  }
+  double sv[3];
+  int ord[3] = {0, 1, 2};
+  for (int j = 0; j < 3; ++j) sv[j] = sqrt(A[j] * A[j] + A[3 + j] * A[3 + j] + A[6 + j] * A[6 + j]);
+  // sort descending (stable on ties)
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 2 - i; ++j)
+      if (sv[ord[j]] < sv[ord[j + 1]]) { int tmp = ord[j]; ord[j] = ord[j + 1]; ord[j + 1] = tmp; }
+  double Vs[9], As[9];
+  for (int j = 0; j < 3; ++j) {
+    s[j] = sv[ord[j]];
+    for (int k = 0; k < 3; ++k) { Vs[3 * k + j] = V[3 * k + ord[j]]; As[3 * k + j] = A[3 * k + ord[j]]; }
+  }
+  for (int i = 0; i < 9; ++i) V[i] = Vs[i];
+  double tiny = s[0] * 1e-13;
+  int rank = 0;
+  for (int j = 0; j < 3; ++j) {
+    if (s[j] > tiny && s[j] > 0.0) {
+      for (int k = 0; k < 3; ++k) U[3 * k + j] = As[3 * k + j] / s[j];
+      rank = j + 1;
+    }
+  }
+  if (rank == 0) {
+    for (int i = 0; i < 9; ++i) U[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    return;
+  }
+  double u0[3] = {U[0], U[3], U[6]};
+  double u1[3];
+  if (rank >= 2) {
+    u1[0] = U[1]; u1[1] = U[4]; u1[2] = U[7];
+  } else {
+    // any unit vector orthogonal to u0: cross with the axis least aligned with it
+    double ax[3] = {0.0, 0.0, 0.0};
+    double a0 = fabs(u0[0]), a1 = fabs(u0[1]), a2 = fabs(u0[2]);
+    ax[(a0 <= a1 && a0 <= a2) ? 0 : (a1 <= a2 ? 1 : 2)] = 1.0;
+    cross3(u0, ax, u1);
+    double n = sqrt(u1[0] * u1[0] + u1[1] * u1[1] + u1[2] * u1[2]);
+    for (int k = 0; k < 3; ++k) u1[k] /= n;
+    U[1] = u1[0]; U[4] = u1[1]; U[7] = u1[2];
+  }
+  if (rank <= 2) {
+    double u2[3];
+    cross3(u0, u1, u2);
+    U[2] = u2[0]; U[5] = u2[1]; U[8] = u2[2];
+  }
+}
+
+GCS_HD double det3(const double* m) {
+  return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
+}
+
+}  // namespace gcs

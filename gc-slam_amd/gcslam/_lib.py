@@ -1,0 +1,162 @@
+"""ctypes binding of libgcslam_hip.so (include/gcslam_hip.h).
+
+The library is loaded from this package directory.  There is no CPU fallback: a missing or
+unloadable library raises at import time of the operators (docs/GC_SLAM.md:130 forbids
+"GPU if available else CPU"; so does the north star).
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+LIB_NAME = "libgcslam_hip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+D_Z = 22
+CERT_LEN = 64
+PAYLOAD_LEN = 840
+SCAN_FIELDS = 26
+MAP_FIELDS = 26
+DERIVED_FIELDS = 16
+MODE_DENSE, MODE_SCALE = 0, 1
+
+c_double_p = C.POINTER(C.c_double)
+c_int32_p = C.POINTER(C.c_int32)
+c_int64_p = C.POINTER(C.c_int64)
+
+
+class GcsConfig(C.Structure):
+    _fields_ = [("device", C.c_int32), ("n_bins", C.c_int32), ("n_points_cap", C.c_int32),
+                ("max_raw_points", C.c_int32), ("mode", C.c_int32), ("k_cand", C.c_int32),
+                ("tau", C.c_double), ("lidar_origin", C.c_double * 3), ("deskew_rotation_only", C.c_int32),
+                ("forgetting_factor", C.c_double), ("gravity_W", C.c_double * 3)]
+
+
+class GcsScanInputs(C.Structure):
+    _fields_ = [("xyz_dev", C.c_void_p), ("point_step", C.c_int32), ("timestamps_dev", C.c_void_p),
+                ("weights_dev", C.c_void_p), ("n_points", C.c_int32), ("imu_stamps", c_double_p),
+                ("imu_gyro", c_double_p), ("imu_accel", c_double_p), ("imu_len", C.c_int32),
+                ("scan_start_time", C.c_double), ("scan_end_time", C.c_double), ("dt_sec", C.c_double),
+                ("Q", c_double_p), ("L_ext", c_double_p), ("h_ext", c_double_p)]
+
+
+class GcsBelief(C.Structure):
+    _fields_ = [("X_anchor", C.c_double * 6), ("stamp_sec", C.c_double), ("z_lin", C.c_double * D_Z),
+                ("L", C.c_double * (D_Z * D_Z)), ("h", C.c_double * D_Z)]
+
+
+class GcsScanOutputs(C.Structure):
+    _fields_ = [("belief", GcsBelief), ("iw_process_dPsi", C.c_double * 252), ("iw_process_dnu", C.c_double * 7),
+                ("z_t", C.c_double * 6), ("L_evidence", C.c_double * (D_Z * D_Z)), ("h_evidence", C.c_double * D_Z),
+                ("R_mf", C.c_double * 9), ("t_wls", C.c_double * 3), ("cert", C.c_double * CERT_LEN),
+                ("stage_ms", C.c_double * 8)]
+
+
+# (name, restype, argtypes) for every symbol declared in include/gcslam_hip.h
+_SIGS = [
+    ("gcs_version", C.c_char_p, []),
+    ("gcs_abi_version", C.c_int, []),
+    ("gcs_ctx_create", C.c_int, [C.POINTER(GcsConfig), C.POINTER(C.c_void_p)]),
+    ("gcs_ctx_destroy", C.c_int, [C.c_void_p]),
+    ("gcs_last_error", C.c_char_p, [C.c_void_p]),
+    ("gcs_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("gcs_ctx_synchronize", C.c_int, [C.c_void_p]),
+    ("gcs_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int32]),
+    ("gcs_ctx_stage_times", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int32]),
+    ("gcs_ctx_set_atlas", C.c_int, [C.c_void_p, c_double_p]),
+    ("gcs_ctx_get_atlas", C.c_int, [C.c_void_p, c_double_p, c_int32_p]),
+    ("gcs_ctx_set_belief", C.c_int, [C.c_void_p, C.POINTER(GcsBelief)]),
+    ("gcs_ctx_get_belief", C.c_int, [C.c_void_p, C.POINTER(GcsBelief)]),
+    ("gcs_ctx_set_map", C.c_int, [C.c_void_p, c_double_p]),
+    ("gcs_ctx_get_map", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
+    ("gcs_ctx_get_scan_stats", C.c_int, [C.c_void_p, c_double_p]),
+    ("gcs_ctx_device_arrays", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
+                                        C.POINTER(C.c_void_p)]),
+    ("gcs_ctx_set_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
+    ("gcs_ctx_get_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p]),
+    ("gcs_scan", C.c_int, [C.c_void_p, C.POINTER(GcsScanInputs), C.POINTER(GcsScanOutputs)]),
+    ("gcs_point_stage", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_double,
+                                  C.c_double, c_double_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, c_double_p]),
+    ("gcs_bin_soft_assign", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("gcs_scan_bin_moment_match", C.c_int, [C.c_void_p, c_double_p]),
+    ("gcs_matrix_fisher_rotation", C.c_int, [C.c_void_p, c_double_p]),
+    ("gcs_planar_translation", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
+    ("gcs_pushforward", C.c_int, [C.c_void_p, c_double_p, c_double_p, C.c_double]),
+    ("gcs_psd_project", C.c_int, [C.c_int32, c_double_p, C.c_double, c_double_p, c_double_p]),
+    ("gcs_spd_solve_lifted", C.c_int, [C.c_int32, c_double_p, c_double_p, C.c_double, c_double_p]),
+    ("gcs_spd_inverse_lifted", C.c_int, [C.c_int32, c_double_p, C.c_double, c_double_p]),
+    ("gcs_svd3", C.c_int, [c_double_p, c_double_p, c_double_p, c_double_p]),
+    ("gcs_predict_diffusion", C.c_int, [C.POINTER(GcsBelief), c_double_p, C.c_double, C.POINTER(GcsBelief),
+                                        c_double_p]),
+    ("gcs_info_fusion_additive", C.c_int, [C.POINTER(GcsBelief), c_double_p, c_double_p, C.c_double,
+                                           C.POINTER(GcsBelief), c_double_p]),
+    ("gcs_preintegrate_imu", C.c_int, [C.c_int32, c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                       c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
+    ("gcs_belief_world_pose", C.c_int, [C.POINTER(GcsBelief), c_double_p]),
+    ("gcs_fibonacci_atlas", C.c_int, [C.c_int32, c_double_p]),
+    ("gcs_knn_table", C.c_int, [C.c_int32, c_double_p, C.c_int32, c_int32_p]),
+    ("gcs_nearest_bins", C.c_int, [C.c_int32, c_double_p, C.c_int32, c_double_p, c_int32_p]),
+    ("gcs_hypothesis_payload", C.c_int, [C.c_void_p, C.c_double, C.c_double, c_double_p]),
+    ("gcs_hypothesis_combine", C.c_int, [C.c_void_p, c_double_p, C.c_int32, C.POINTER(GcsBelief), c_double_p]),
+]
+
+SYMBOLS = [s[0] for s in _SIGS]
+
+_lib = None
+
+
+def load():
+    """Load the HIP library (raises RuntimeError if it was not built: no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not found: build it with __graft_entry__.build() "
+                           "(make -C gc-slam_amd); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in _SIGS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(c_double_p)
+
+
+def iptr(a: np.ndarray):
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(c_int32_p)
+
+
+def check(rc: int, ctx=None, what: str = "gcs call"):
+    """Map gcs_status to the reference's exception types (fail fast, pipeline.py:546-548)."""
+    if rc == 0:
+        return
+    msg = ""
+    if ctx is not None:
+        msg = load().gcs_last_error(ctx).decode(errors="replace")
+    if rc in (-1, -3):
+        raise ValueError(f"{what} failed ({rc}): {msg}")
+    raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def belief_to_struct(X_anchor, stamp, z_lin, L, h) -> GcsBelief:
+    b = GcsBelief()
+    b.X_anchor[:] = np.asarray(X_anchor, np.float64).ravel().tolist()
+    b.stamp_sec = float(stamp)
+    b.z_lin[:] = np.asarray(z_lin, np.float64).ravel().tolist()
+    b.L[:] = np.asarray(L, np.float64).ravel().tolist()
+    b.h[:] = np.asarray(h, np.float64).ravel().tolist()
+    return b
+
+
+def struct_to_arrays(b: GcsBelief):
+    return (np.array(b.X_anchor[:]), float(b.stamp_sec), np.array(b.z_lin[:]),
+            np.array(b.L[:]).reshape(D_Z, D_Z), np.array(b.h[:]))

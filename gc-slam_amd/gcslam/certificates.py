@@ -1,0 +1,112 @@
+"""Certificate structures mirroring FS/common/certificates.py (the fields that are numerically live
+on the bin path: influence magnitudes feed the Frobenius strength, support feeds tempering)."""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field, replace
+from typing import List, Optional
+
+
+@dataclass
+class ConditioningCert:          # certificates.py:22-35
+    eig_min: float = 1.0
+    eig_max: float = 1.0
+    cond: float = 1.0
+    near_null_count: int = 0
+
+
+@dataclass
+class SupportCert:               # certificates.py:39-49
+    ess_total: float = 0.0
+    support_frac: float = 1.0
+
+
+@dataclass
+class MismatchCert:              # certificates.py:52-62
+    nll_per_ess: float = 0.0
+    directional_score: float = 1.0
+
+
+@dataclass
+class InfluenceCert:             # certificates.py:78-109
+    lift_strength: float = 0.0
+    psd_projection_delta: float = 0.0
+    nu_projection_delta: float = 0.0
+    mass_epsilon_ratio: float = 0.0
+    anchor_drift_rho: float = 0.0
+    dt_scale: float = 1.0
+    extrinsic_scale: float = 1.0
+    trust_alpha: float = 1.0
+    power_beta: float = 1.0
+
+    @classmethod
+    def identity(cls):
+        return cls()
+
+    def with_overrides(self, **kw):
+        return replace(self, **kw)
+
+
+@dataclass
+class CertBundle:                # certificates.py:349-486
+    chart_id: str
+    anchor_id: str
+    exact: bool
+    approximation_triggers: List[str] = field(default_factory=list)
+    frobenius_applied: bool = False
+    conditioning: ConditioningCert = field(default_factory=ConditioningCert)
+    support: SupportCert = field(default_factory=SupportCert)
+    mismatch: MismatchCert = field(default_factory=MismatchCert)
+    influence: InfluenceCert = field(default_factory=InfluenceCert)
+
+    @classmethod
+    def create_exact(cls, chart_id, anchor_id, **kw):
+        return cls(chart_id=chart_id, anchor_id=anchor_id, exact=True, **kw)
+
+    @classmethod
+    def create_approx(cls, chart_id, anchor_id, triggers, **kw):
+        return cls(chart_id=chart_id, anchor_id=anchor_id, exact=False, approximation_triggers=list(triggers), **kw)
+
+    def total_trigger_magnitude(self) -> float:
+        i = self.influence
+        return (i.lift_strength + i.psd_projection_delta + i.nu_projection_delta + i.mass_epsilon_ratio
+                + i.anchor_drift_rho + abs(1.0 - i.dt_scale) + abs(1.0 - i.extrinsic_scale)
+                + abs(1.0 - i.trust_alpha) + abs(1.0 - i.power_beta))
+
+
+@dataclass
+class ExpectedEffect:            # certificates.py:488-505
+    objective_name: str
+    predicted: float
+    realized: Optional[float] = None
+
+
+def aggregate_certificates(certs: List[CertBundle]) -> CertBundle:
+    """certificates.py:511-700 restricted to the fields carried here."""
+    if not certs:
+        return CertBundle.create_exact("GC-RIGHT-01", "unknown")
+    t = certs[0]
+    n = len(certs)
+    return CertBundle(
+        chart_id=t.chart_id, anchor_id=t.anchor_id, exact=all(c.exact for c in certs),
+        approximation_triggers=[x for c in certs for x in c.approximation_triggers],
+        frobenius_applied=any(c.frobenius_applied for c in certs),
+        conditioning=ConditioningCert(min(c.conditioning.eig_min for c in certs),
+                                      max(c.conditioning.eig_max for c in certs),
+                                      max(c.conditioning.cond for c in certs),
+                                      sum(c.conditioning.near_null_count for c in certs)),
+        support=SupportCert(sum(c.support.ess_total for c in certs) / n,
+                            sum(c.support.support_frac for c in certs) / n),
+        mismatch=MismatchCert(sum(c.mismatch.nll_per_ess for c in certs),
+                              sum(c.mismatch.directional_score for c in certs) / n),
+        influence=InfluenceCert(
+            lift_strength=sum(c.influence.lift_strength for c in certs),
+            psd_projection_delta=sum(c.influence.psd_projection_delta for c in certs),
+            nu_projection_delta=sum(c.influence.nu_projection_delta for c in certs),
+            mass_epsilon_ratio=max(c.influence.mass_epsilon_ratio for c in certs),
+            anchor_drift_rho=max(c.influence.anchor_drift_rho for c in certs),
+            dt_scale=min(c.influence.dt_scale for c in certs),
+            extrinsic_scale=min(c.influence.extrinsic_scale for c in certs),
+            trust_alpha=min(c.influence.trust_alpha for c in certs),
+            power_beta=min(c.influence.power_beta for c in certs)),
+    )

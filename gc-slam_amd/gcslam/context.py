@@ -1,0 +1,234 @@
+"""One hypothesis on one GPU: owns the device map-bin statistics, the atlas lookup structures and
+the host belief / IW state (wraps gcs_ctx, include/gcslam_hip.h).
+
+Device memory for scans is plain torch CUDA tensors (HIP on ROCm); the context runs on torch's
+current stream so ordering with torch producers is implicit.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def tau_for_bins(n_bins: int, tau_48: float = 0.1) -> float:
+    """DECLARED soft-assign temperature: tau_B = tau_48 * 48 / B (DESIGN.md "temperature")."""
+    return tau_48 * 48.0 / float(n_bins)
+
+
+class HypothesisContext:
+    def __init__(self, n_bins=48, n_points_cap=8192, max_raw_points=None, mode="dense", k_cand=16, tau=None,
+                 lidar_origin=(0.0, 0.0, 0.0), deskew_rotation_only=False, forgetting_factor=0.99,
+                 gravity_W=(0.0, 0.0, -9.81), device=0, use_torch_stream=True):
+        self.lib = L.load()
+        cfg = L.GcsConfig()
+        cfg.device = int(device)
+        cfg.n_bins = int(n_bins)
+        cfg.n_points_cap = int(n_points_cap)
+        cfg.max_raw_points = int(max_raw_points if max_raw_points is not None else max(n_points_cap, 1) * 8)
+        cfg.mode = L.MODE_SCALE if mode == "scale" else L.MODE_DENSE
+        cfg.k_cand = int(k_cand)
+        cfg.tau = float(tau if tau is not None else tau_for_bins(n_bins))
+        cfg.lidar_origin[:] = [float(x) for x in lidar_origin]
+        cfg.deskew_rotation_only = int(bool(deskew_rotation_only))
+        cfg.forgetting_factor = float(forgetting_factor)
+        cfg.gravity_W[:] = [float(x) for x in gravity_W]
+        self.cfg = cfg
+        self.mode = mode
+        self.device = int(device)
+        h = C.c_void_p()
+        rc = self.lib.gcs_ctx_create(C.byref(cfg), C.byref(h))
+        L.check(rc, None, "gcs_ctx_create")
+        self.h = h
+        if use_torch_stream:
+            torch = _torch()
+            with torch.cuda.device(self.device):
+                s = torch.cuda.current_stream().cuda_stream
+            L.check(self.lib.gcs_ctx_set_stream(self.h, C.c_void_p(s)), self.h, "set_stream")
+
+    # ------------------------------------------------------------------ lifetime
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gcs_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def n_bins(self):
+        return self.cfg.n_bins
+
+    @property
+    def cap(self):
+        return self.cfg.n_points_cap
+
+    def _chk(self, rc, what):
+        L.check(rc, self.h, what)
+
+    # ------------------------------------------------------------------ state
+    def atlas(self):
+        B = self.n_bins
+        dirs = np.zeros((B, 3))
+        knn = np.zeros((B, max(1, self.cfg.k_cand)), np.int32)
+        self._chk(self.lib.gcs_ctx_get_atlas(self.h, L.dptr(dirs), L.iptr(knn)), "get_atlas")
+        return dirs, (knn if self.mode == "scale" else None)
+
+    def set_atlas(self, dirs):
+        d = np.ascontiguousarray(dirs, np.float64)
+        self._chk(self.lib.gcs_ctx_set_atlas(self.h, L.dptr(d)), "set_atlas")
+
+    def set_belief(self, X_anchor, stamp, z_lin, Lm, h):
+        b = L.belief_to_struct(X_anchor, stamp, z_lin, Lm, h)
+        self._chk(self.lib.gcs_ctx_set_belief(self.h, C.byref(b)), "set_belief")
+
+    def get_belief(self):
+        b = L.GcsBelief()
+        self._chk(self.lib.gcs_ctx_get_belief(self.h, C.byref(b)), "get_belief")
+        return L.struct_to_arrays(b)
+
+    def get_map(self):
+        B = self.n_bins
+        m = np.zeros(L.MAP_FIELDS * B)
+        d = np.zeros(L.DERIVED_FIELDS * B)
+        self._chk(self.lib.gcs_ctx_get_map(self.h, L.dptr(m), L.dptr(d)), "get_map")
+        return m.reshape(L.MAP_FIELDS, B), d.reshape(L.DERIVED_FIELDS, B)
+
+    def set_map(self, map_fields):
+        m = np.ascontiguousarray(map_fields, np.float64).reshape(-1)
+        self._chk(self.lib.gcs_ctx_set_map(self.h, L.dptr(m)), "set_map")
+
+    def get_scan_stats(self):
+        B = self.n_bins
+        s = np.zeros(L.SCAN_FIELDS * B)
+        self._chk(self.lib.gcs_ctx_get_scan_stats(self.h, L.dptr(s)), "get_scan_stats")
+        return s.reshape(L.SCAN_FIELDS, B)
+
+    def iw_state(self):
+        nu, Psi, Q = np.zeros(7), np.zeros(252), np.zeros(484)
+        self._chk(self.lib.gcs_ctx_get_iw_state(self.h, L.dptr(nu), L.dptr(Psi), L.dptr(Q)), "get_iw_state")
+        return nu, Psi.reshape(7, 6, 6), Q.reshape(22, 22)
+
+    def enable_timing(self, on=True):
+        self._chk(self.lib.gcs_ctx_enable_timing(self.h, int(on)), "enable_timing")
+
+    def stage_times(self, reset=False):
+        ms = np.zeros(6)
+        cnt = np.zeros(6, np.int64)
+        self._chk(self.lib.gcs_ctx_stage_times(self.h, L.dptr(ms), cnt.ctypes.data_as(L.c_int64_p), int(reset)),
+                  "stage_times")
+        return ms, cnt
+
+    def synchronize(self):
+        self._chk(self.lib.gcs_ctx_synchronize(self.h), "synchronize")
+
+    # ------------------------------------------------------------------ per-operator stages
+    def point_stage(self, xyz_dev, point_step, t_dev, w_dev, n_points, t0, t1, xi_body, want_outputs=True):
+        """Fused PointBudgetResample + DeskewConstantTwist + directions + soft-assign normalisers."""
+        torch = _torch()
+        cap = self.cap
+        dev = f"cuda:{self.device}"
+        p0 = torch.zeros((cap, 3), dtype=torch.float64, device=dev) if want_outputs else None
+        wo = torch.zeros(cap, dtype=torch.float64, device=dev) if want_outputs else None
+        wb = torch.zeros(cap, dtype=torch.float64, device=dev) if want_outputs else None
+        nearest = torch.zeros(cap, dtype=torch.int32, device=dev) if want_outputs else None
+        xi = np.ascontiguousarray(xi_body, np.float64)
+        cert = np.zeros(8)
+        ptr = lambda t: C.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        rc = self.lib.gcs_point_stage(self.h, C.c_void_p(xyz_dev.data_ptr()), int(point_step),
+                                      C.c_void_p(t_dev.data_ptr()), C.c_void_p(w_dev.data_ptr()), int(n_points),
+                                      float(t0), float(t1), L.dptr(xi), ptr(p0), ptr(wo), ptr(wb), ptr(nearest),
+                                      L.dptr(cert))
+        self._chk(rc, "point_stage")
+        return dict(points=p0, weights=wo, budget_weights=wb, nearest=nearest, cert=cert)
+
+    def bin_soft_assign(self):
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        if self.mode == "scale":
+            ids = torch.zeros((self.cap, self.cfg.k_cand), dtype=torch.int32, device=dev)
+            r = torch.zeros((self.cap, self.cfg.k_cand), dtype=torch.float64, device=dev)
+        else:
+            ids = None
+            r = torch.zeros((self.cap, self.n_bins), dtype=torch.float64, device=dev)
+        rc = self.lib.gcs_bin_soft_assign(self.h, C.c_void_p(ids.data_ptr()) if ids is not None else None,
+                                          C.c_void_p(r.data_ptr()))
+        self._chk(rc, "bin_soft_assign")
+        return ids, r
+
+    def scan_bin_moment_match(self):
+        cert = np.zeros(5)
+        self._chk(self.lib.gcs_scan_bin_moment_match(self.h, L.dptr(cert)), "scan_bin_moment_match")
+        return cert
+
+    def matrix_fisher_rotation(self):
+        out = np.zeros(42)
+        self._chk(self.lib.gcs_matrix_fisher_rotation(self.h, L.dptr(out)), "matrix_fisher_rotation")
+        return dict(H=out[0:9].reshape(3, 3), N_eff=out[9], map_scatter_total=out[10:19].reshape(3, 3),
+                    map_N_dir_total=out[19], scan_N_total=out[20], R_mf=out[21:30].reshape(3, 3),
+                    svd_s=out[30:33], V=out[33:42].reshape(3, 3))
+
+    def planar_translation(self, R_hat):
+        R = np.ascontiguousarray(R_hat, np.float64).reshape(9)
+        out = np.zeros(13)
+        self._chk(self.lib.gcs_planar_translation(self.h, L.dptr(R), L.dptr(out)), "planar_translation")
+        return dict(L_full=out[0:9].reshape(3, 3), h_full=out[9:12], N_eff=out[12])
+
+    def pushforward(self, z_t, Sigma_pose6, gamma):
+        z = np.ascontiguousarray(z_t, np.float64)
+        S = np.ascontiguousarray(Sigma_pose6, np.float64).reshape(36)
+        self._chk(self.lib.gcs_pushforward(self.h, L.dptr(z), L.dptr(S), float(gamma)), "pushforward")
+
+    # ------------------------------------------------------------------ the scan
+    def scan(self, xyz_dev, point_step, t_dev, w_dev, n_points, imu_stamps, imu_gyro, imu_accel,
+             scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None):
+        imu_stamps = np.ascontiguousarray(imu_stamps, np.float64)
+        imu_gyro = np.ascontiguousarray(imu_gyro, np.float64).reshape(-1)
+        imu_accel = np.ascontiguousarray(imu_accel, np.float64).reshape(-1)
+        inp = L.GcsScanInputs()
+        inp.xyz_dev = xyz_dev.data_ptr()
+        inp.point_step = int(point_step)
+        inp.timestamps_dev = t_dev.data_ptr()
+        inp.weights_dev = w_dev.data_ptr()
+        inp.n_points = int(n_points)
+        inp.imu_stamps = L.dptr(imu_stamps)
+        inp.imu_gyro = L.dptr(imu_gyro)
+        inp.imu_accel = L.dptr(imu_accel)
+        inp.imu_len = int(imu_stamps.shape[0])
+        inp.scan_start_time = float(scan_start_time)
+        inp.scan_end_time = float(scan_end_time)
+        inp.dt_sec = float(dt_sec)
+        keep = []
+        for name, arr in (("Q", Q), ("L_ext", L_ext), ("h_ext", h_ext)):
+            if arr is not None:
+                a = np.ascontiguousarray(arr, np.float64).reshape(-1)
+                keep.append(a)
+                setattr(inp, name, L.dptr(a))
+        out = L.GcsScanOutputs()
+        self._chk(self.lib.gcs_scan(self.h, C.byref(inp), C.byref(out)), "gcs_scan")
+        return out
+
+    # ------------------------------------------------------------------ hypotheses
+    def hypothesis_payload(self, w_iw, w_bary):
+        p = np.zeros(L.PAYLOAD_LEN)
+        self._chk(self.lib.gcs_hypothesis_payload(self.h, float(w_iw), float(w_bary), L.dptr(p)), "payload")
+        return p
+
+    def hypothesis_combine(self, payload_sum, scan_count):
+        p = np.ascontiguousarray(payload_sum, np.float64)
+        b = L.GcsBelief()
+        cert = np.zeros(4)
+        self._chk(self.lib.gcs_hypothesis_combine(self.h, L.dptr(p), int(scan_count), C.byref(b), L.dptr(cert)),
+                  "combine")
+        return L.struct_to_arrays(b), cert

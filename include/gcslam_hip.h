@@ -1,0 +1,191 @@
+/*
+ * gcslam_hip.h -- C-ABI of the MI355X (gfx950) GC-SLAM bin-path per-scan backend.
+ *
+ * Plain pointers and sizes only.  "dev" pointers are HIP device pointers (HBM), "host"
+ * pointers are ordinary host memory.  Every call returns 0 on success or a negative
+ * gcs_status; gcs_last_error(ctx) holds the message.  A context owns one hypothesis on one
+ * GPU (device buffers, HIP stream, belief, map-bin statistics); calls on one context must be
+ * serialised by the caller, distinct contexts are independent (no global mutable state).
+ *
+ * Reference interfaces replaced (paths relative to the reference repo,
+ * FS = fl_ws/src/fl_slam_poc/fl_slam_poc):
+ *   gcs_scan                    FS/backend/pipeline.py:316-1591 process_scan_single_hypothesis
+ *                               (14-step bin path, README.md:105-122)
+ *   gcs_point_stage             FS/backend/operators/point_budget.py:117-221 point_budget_resample
+ *                               + FS/backend/operators/deskew_constant_twist.py:72-117 (fused)
+ *   gcs_bin_soft_assign         archive/legacy_operators/binning.py:79-131 bin_soft_assign
+ *   gcs_scan_bin_moment_match   archive/legacy_operators/binning.py:212-324 (+ kappa.py:130-169)
+ *   gcs_matrix_fisher_rotation  archive/legacy_operators/matrix_fisher_evidence.py:264-394
+ *   gcs_planar_translation      archive/legacy_operators/matrix_fisher_evidence.py:502-671
+ *   gcs_pushforward             PoseCovInflationPushforward (source deleted; CHANGELOG.md:1246)
+ *                               + archive/bin_atlas.py:137-257 update/forgetting/derived stats
+ *   gcs_psd_project             FS/common/primitives.py:80-123 domain_projection_psd_core
+ *   gcs_info_fusion_additive    FS/backend/operators/fusion.py:150-230
+ *   gcs_predict_diffusion       FS/backend/operators/predict.py:106-214
+ *   gcs_preintegrate_imu        FS/backend/operators/imu_preintegration.py:47-147
+ *   gcs_hypothesis_payload /    FS/backend/backend_node.py:1999-2119 (IW accumulation) and
+ *   gcs_hypothesis_combine      FS/backend/operators/hypothesis.py:51-117 (barycenter)
+ *   gcs_fibonacci_atlas         archive/bin_atlas.py:40-61
+ */
+#ifndef GCSLAM_HIP_H
+#define GCSLAM_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GCS_ABI_VERSION 1
+#define GCS_D_Z 22
+#define GCS_SCAN_FIELDS 26   /* ScanBinStats, field-major: N, s_dir[3], S_dir_scatter[9], p_bar[3], Sigma_p[9], kappa */
+#define GCS_MAP_FIELDS 26    /* MapBinStats: S_dir[3], S_dir_scatter[9], N_dir, N_pos, sum_p[3], sum_ppT[9] */
+#define GCS_DERIVED_FIELDS 16 /* mu_dir[3], kappa, centroid[3], Sigma_c[9] */
+#define GCS_PAYLOAD_LEN 840  /* hypothesis all-reduce payload (f64) */
+
+typedef enum {
+  GCS_OK = 0,
+  GCS_ERR_ARG = -1,      /* maps to ValueError */
+  GCS_ERR_HIP = -2,      /* maps to RuntimeError */
+  GCS_ERR_NONFINITE = -3,/* maps to ValueError (reference fail-fast, pipeline.py:546-548) */
+  GCS_ERR_STATE = -4
+} gcs_status;
+
+typedef enum { GCS_MODE_DENSE = 0, GCS_MODE_SCALE = 1 } gcs_mode;
+
+typedef struct gcs_ctx gcs_ctx;
+
+typedef struct {
+  int32_t device;              /* HIP device ordinal */
+  int32_t n_bins;              /* B */
+  int32_t n_points_cap;        /* N_POINTS_CAP (constants.py:64; raised for C2/C3) */
+  int32_t max_raw_points;      /* capacity of the raw input */
+  int32_t mode;                /* gcs_mode */
+  int32_t k_cand;              /* K candidates per point in scale mode (16) */
+  double tau;                  /* soft-assign temperature (declared) */
+  double lidar_origin[3];      /* LiDAR origin in base (pipeline.py:589-593) */
+  int32_t deskew_rotation_only;/* pipeline.py:482-483 */
+  double forgetting_factor;    /* PipelineConfig.forgetting_factor (0.99) */
+  double gravity_W[3];         /* constants.py:80 */
+} gcs_config;
+
+typedef struct {
+  /* LiDAR scan resident on the device (PointCloud2-like: float x,y,z at offsets 0,4,8) */
+  const void* xyz_dev;
+  int32_t point_step;
+  const double* timestamps_dev;
+  const double* weights_dev;
+  int32_t n_points;
+  /* IMU window (host, padded to imu_len with zero stamps) */
+  const double* imu_stamps;    /* [imu_len] */
+  const double* imu_gyro;      /* [imu_len*3] */
+  const double* imu_accel;     /* [imu_len*3] */
+  int32_t imu_len;
+  double scan_start_time, scan_end_time, dt_sec;
+  const double* Q;             /* [22*22] host; NULL = context's IW-derived Q */
+  const double* L_ext;         /* optional external evidence [22*22] (IMU/odom family), may be NULL */
+  const double* h_ext;         /* [22] */
+} gcs_scan_inputs;
+
+typedef struct {
+  double X_anchor[6];
+  double stamp_sec;
+  double z_lin[GCS_D_Z];
+  double L[GCS_D_Z * GCS_D_Z];
+  double h[GCS_D_Z];
+} gcs_belief;
+
+/* Certificate / diagnostic scalars of one scan (indices documented in DESIGN.md). */
+#define GCS_CERT_LEN 64
+typedef struct {
+  gcs_belief belief;                 /* belief after AnchorDriftUpdate */
+  double iw_process_dPsi[7 * 36];
+  double iw_process_dnu[7];
+  double z_t[6];                     /* post-recompose world pose used by the map update */
+  double L_evidence[GCS_D_Z * GCS_D_Z];
+  double h_evidence[GCS_D_Z];
+  double R_mf[9];
+  double t_wls[3];
+  double cert[GCS_CERT_LEN];
+  double stage_ms[8];                /* host-measured stage times */
+} gcs_scan_outputs;
+
+/* ---------------------------------------------------------------- context */
+const char* gcs_version(void);
+int gcs_abi_version(void);
+int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out);
+int gcs_ctx_destroy(gcs_ctx* ctx);
+const char* gcs_last_error(const gcs_ctx* ctx);
+int gcs_ctx_set_stream(gcs_ctx* ctx, void* hip_stream);
+int gcs_ctx_synchronize(gcs_ctx* ctx);
+/* device stage timing with hipEvents on the context stream: stages
+ * [0 budget+points, 1 sort+bucket, 2 bin moment-match kernel, 3 MF, 4 planar, 5 pushforward] */
+int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t on);
+int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*6*/, int64_t* counts /*6*/, int32_t reset);
+int gcs_ctx_set_atlas(gcs_ctx* ctx, const double* dirs_host /*B*3*/);
+int gcs_ctx_get_atlas(gcs_ctx* ctx, double* dirs_host /*B*3*/, int32_t* knn_host /*B*K*/);
+int gcs_ctx_set_belief(gcs_ctx* ctx, const gcs_belief* b);
+int gcs_ctx_get_belief(gcs_ctx* ctx, gcs_belief* b);
+int gcs_ctx_set_map(gcs_ctx* ctx, const double* map_host /*26*B field-major*/);
+int gcs_ctx_get_map(gcs_ctx* ctx, double* map_host /*26*B*/, double* derived_host /*16*B*/);
+int gcs_ctx_get_scan_stats(gcs_ctx* ctx, double* scan_host /*26*B*/);
+/* device pointers of the resident per-bin arrays (field-major, length-B rows) */
+int gcs_ctx_device_arrays(gcs_ctx* ctx, double** scan_dev, double** map_dev, double** derived_dev);
+int gcs_ctx_set_iw_state(gcs_ctx* ctx, const double* nu7, const double* Psi7x36);
+int gcs_ctx_get_iw_state(gcs_ctx* ctx, double* nu7, double* Psi7x36, double* Q22x22);
+
+/* ---------------------------------------------------------------- the per-scan pipeline */
+int gcs_scan(gcs_ctx* ctx, const gcs_scan_inputs* in, gcs_scan_outputs* out);
+
+/* ---------------------------------------------------------------- per-operator device entry points */
+/* PointBudgetResample + DeskewConstantTwist + directions + BinSoftAssign normalisers, fused.
+ * Outputs (device, length n_points_cap; NULL to skip): deskewed points [cap*3], deskewed
+ * weights, budget weights, nearest bin (scale mode).  cert_host receives scalars
+ * [mass_in, mass_sel, mass_scale, sum_w_budget, sum_wn2, sum_w_deskew, sum_entropy, max_resp]. */
+int gcs_point_stage(gcs_ctx* ctx, const void* xyz_dev, int32_t point_step, const double* t_dev, const double* w_dev,
+                    int32_t n_points, double t0, double t1, const double* xi_body6,
+                    double* p0_dev, double* w_out_dev, double* w_budget_dev, int32_t* nearest_dev, double* cert_host);
+/* BinSoftAssign materialised for parity (scale: [cap*K] ids + responsibilities; dense: [cap*B]).
+ * Requires a preceding gcs_point_stage on the same context. */
+int gcs_bin_soft_assign(gcs_ctx* ctx, int32_t* ids_dev, double* resp_dev);
+/* ScanBinMomentMatch (+Kappa) over the last point stage; writes the context's ScanBinStats
+ * (gcs_ctx_device_arrays) and cert_host = [sum N, sum N^2, sum N/(N+eps), psd_delta, max eps ratio]. */
+int gcs_scan_bin_moment_match(gcs_ctx* ctx, double* cert_host);
+/* MatrixFisherRotation + PlanarTranslation over the context's scan and map stats.
+ * mf_host  = [H(9), N_eff, map_scatter_total(9), map_N_dir_total, scan_N_total, R_mf(9), s(3), V(9)]
+ * pt_host  = [L_full(9), h_full(3), N_eff] */
+int gcs_matrix_fisher_rotation(gcs_ctx* ctx, double* mf_host);
+int gcs_planar_translation(gcs_ctx* ctx, const double* R_hat9, double* pt_host);
+/* PoseCovInflationPushforward of the context's scan stats into its map at pose z_t. */
+int gcs_pushforward(gcs_ctx* ctx, const double* z_t6, const double* Sigma_pose36, double gamma);
+
+/* ---------------------------------------------------------------- host-side numerics (no GPU) */
+int gcs_psd_project(int32_t n, const double* M, double eps_psd, double* M_psd, double* cert6);
+int gcs_spd_solve_lifted(int32_t n, const double* L, const double* b, double eps_lift, double* x);
+int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps_lift, double* Linv);
+int gcs_svd3(const double* H, double* U, double* s, double* V);
+int gcs_predict_diffusion(const gcs_belief* prev, const double* Q, double dt_sec, gcs_belief* pred, double* cert4);
+int gcs_info_fusion_additive(const gcs_belief* pred, const double* L_ev, const double* h_ev, double alpha,
+                             gcs_belief* post, double* psd_delta);
+int gcs_preintegrate_imu(int32_t m, const double* stamps, const double* gyro, const double* accel, const double* weights,
+                         const double* rotvec_start, const double* gyro_bias, const double* accel_bias,
+                         const double* gravity_W, double* delta_pose6, double* ess);
+int gcs_belief_world_pose(const gcs_belief* b, double* pose6); /* belief.py:410-434 */
+int gcs_fibonacci_atlas(int32_t n_bins, double* dirs /*B*3*/);
+int gcs_knn_table(int32_t n_bins, const double* dirs, int32_t k, int32_t* knn /*B*k*/);
+int gcs_nearest_bins(int32_t n_bins, const double* dirs, int32_t n_query, const double* q /*n*3*/, int32_t* out);
+
+/* ---------------------------------------------------------------- hypotheses (multi-GPU combine) */
+/* Pack this hypothesis' contribution (weights pre-applied) for an RCCL sum all-reduce:
+ * [w_iw dPsi 252 | w_iw dnu 7 | w_iw dPsi_meas 27 | w_iw dnu_meas 3 | w L 484 | w h 22 | w z 22 | w mu 22 | w |mu|^2 1] */
+int gcs_hypothesis_payload(gcs_ctx* ctx, double w_iw, double w_bary, double* payload_host);
+/* Apply the summed payload: barycenter (PSD of L), IW apply + Q rebuild (stored in ctx).
+ * combined_out may be NULL; cert_out = [psd_delta, spread, iw_psd_delta, iw_nu_delta]. */
+int gcs_hypothesis_combine(gcs_ctx* ctx, const double* payload_sum, int32_t scan_count, gcs_belief* combined_out,
+                           double* cert_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GCSLAM_HIP_H */

@@ -1,0 +1,176 @@
+"""The 14-step bin-path per-scan pipeline, one hypothesis (test oracle only).
+
+Step order follows README.md:105-122 with the live calling convention of
+process_scan_single_hypothesis (FS/backend/pipeline.py:316-1591); see SURVEY.md
+section 3.3 for the reconstruction.  Out of scope this round: the
+IMU/odom evidence family of step 9 (pipeline.py:595-776) -- it enters as an
+optional external (L, h) term -- and the measurement-noise IW statistics.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import ops, se3
+from .primitives import psd_project, spd_inverse_lifted
+
+
+@dataclass
+class BinPathConfig:
+    n_points_cap: int = 8192
+    n_bins: int = 48
+    mode: str = "dense"            # "dense" (reference N x B softmax) or "scale" (K candidates)
+    k_cand: int = ops.K_CAND
+    tau: float | None = None       # None -> ops.tau_for_bins(n_bins)
+    lidar_origin: tuple = (0.0, 0.0, 0.0)
+    deskew_rotation_only: bool = False
+    forgetting_factor: float = ops.FORGETTING_FACTOR
+    gravity_W: tuple = ops.GRAVITY_W
+
+    def temperature(self):
+        return ops.tau_for_bins(self.n_bins) if self.tau is None else self.tau
+
+
+@dataclass
+class MapState:
+    stats: ops.MapBinStats
+    mu_dir: np.ndarray
+    kappa: np.ndarray
+    centroid: np.ndarray
+    Sigma_c: np.ndarray
+
+    @classmethod
+    def empty(cls, B):
+        st = ops.MapBinStats.empty(B)
+        return cls(st, *ops.map_derived_stats(st))
+
+
+def _aggregate_ess(certs):
+    return sum(c.get("ess_total", 0.0) for c in certs) / len(certs)
+
+
+def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathConfig, bins, knn,
+                          map_state: MapState, L_ext=None, h_ext=None):
+    """One hypothesis, one scan.  `scan` keys: points (N,3), timestamps, weights, imu_stamps,
+    imu_gyro, imu_accel, scan_start_time, scan_end_time, dt_sec."""
+    certs = []   # list of dicts: influence fields + ess_total (+ name)
+    # 1 PointBudgetResample (pipeline.py:399-418)
+    bud = ops.point_budget_resample(scan["points"], scan["timestamps"], scan["weights"],
+                                    n_points_cap=cfg.n_points_cap)
+    certs.append(dict(name="budget", mass_epsilon_ratio=bud["mass_epsilon_ratio"], ess_total=bud["ess"]))
+    # 2 PredictDiffusion (pipeline.py:423-430)
+    b_pred, infl = ops.predict_diffusion(belief_prev, Q, scan["dt_sec"])
+    certs.append(dict(name="predict", **infl))
+    # 3 IMU window, preintegration, deskew (pipeline.py:432-587)
+    cov_pred, _ = spd_inverse_lifted(b_pred.L, ops.EPS_LIFT)
+    sigma_warp = max(math.sqrt(cov_pred[15, 15]), 0.01)
+    w_imu = ops.smooth_window_weights(scan["imu_stamps"], scan["scan_start_time"], scan["scan_end_time"],
+                                      sigma_warp)
+    mu_inc = b_pred.mean_increment()
+    pose0 = belief_prev.mean_world_pose()
+    pre = ops.preintegrate_imu(scan["imu_stamps"], scan["imu_gyro"], scan["imu_accel"], w_imu, pose0[3:6],
+                               mu_inc[9:12], mu_inc[12:15], np.asarray(cfg.gravity_W))
+    xi = se3.se3_log(pre["delta_pose"])
+    if cfg.deskew_rotation_only:
+        xi[:3] = 0.0
+    dk = ops.deskew_constant_twist(bud["points"], bud["timestamps"], bud["weights"],
+                                   scan["scan_start_time"], scan["scan_end_time"], xi)
+    cert_deskew = dict(name="deskew", ess_total=pre["ess"])
+    certs.append(cert_deskew)
+    # 4-6 BinSoftAssign + ScanBinMomentMatch (+Kappa)
+    origin = np.asarray(cfg.lidar_origin, np.float64)
+    d = ops.point_directions(dk["points"], origin)
+    tau = cfg.temperature()
+    if cfg.mode == "dense":
+        sa = ops.bin_soft_assign_dense(d, bins, tau)
+        st = ops.scan_bin_moment_match_dense(dk["points"], dk["weights"], sa["responsibilities"], origin)
+    else:
+        sa = ops.bin_soft_assign_scale(d, bins, knn, tau)
+        st = ops.scan_bin_moment_match_scale(dk["points"], dk["weights"], sa["indices"],
+                                             sa["responsibilities"], origin, bins.shape[0])
+    cert_sa = dict(name="soft_assign", ess_total=sa["ess_total"])
+    cert_mm = dict(name="moment_match", ess_total=st["ess"], psd_projection_delta=st["psd_projection_delta"],
+                   mass_epsilon_ratio=st["mass_epsilon_ratio"])
+    # 7 MatrixFisherRotation, 8 PlanarTranslationEvidence
+    pose_pred = b_pred.mean_world_pose()
+    R_pred = se3.so3_exp(pose_pred[3:6])
+    m = map_state
+    mf = ops.matrix_fisher_rotation(R_pred, st["s_dir"], st["S_dir_scatter"], st["N"], m.stats.S_dir,
+                                    m.stats.S_dir_scatter, m.stats.N_dir)
+    pt = ops.planar_translation(pose_pred[:3], mf["R_mf"], st["p_bar"], st["Sigma_p"], st["N"], m.centroid,
+                                m.Sigma_c, m.stats.N_pos, m.stats.S_dir_scatter, m.stats.N_dir)
+    cert_mf = dict(name="mf", psd_projection_delta=mf["psd_projection_delta"],
+                   mass_epsilon_ratio=mf["mass_epsilon_ratio"])
+    cert_pt = dict(name="planar", psd_projection_delta=pt["psd_projection_delta"],
+                   mass_epsilon_ratio=pt["mass_epsilon_ratio"])
+    lidar_certs = [cert_deskew, cert_sa, cert_mm, cert_mf, cert_pt]
+    certs.extend([cert_sa, cert_mm, cert_mf, cert_pt])
+    # 9 evidence + power tempering (pipeline.py:1038-1117) + excitation scaling (:1119-1148)
+    L_lidar, h_lidar = ops.combined_lidar_evidence_22d(mf, pt)
+    L_raw = L_lidar + (0.0 if L_ext is None else L_ext)
+    h_raw = h_lidar + (0.0 if h_ext is None else h_ext)
+    eps = ops.EPS_MASS
+    dt_pose = np.linalg.norm(L_raw[15, 0:6]) + np.linalg.norm(L_raw[0:6, 15])
+    dt_vel = np.linalg.norm(L_raw[15, 6:9]) + np.linalg.norm(L_raw[6:9, 15])
+    dt_asym = min(max(abs(dt_vel - dt_pose) / (dt_vel + dt_pose + eps), 0.0), 1.0)
+    z_to_xy = abs(L_raw[2, 2]) / (0.5 * (abs(L_raw[0, 0]) + abs(L_raw[1, 1])) + eps)
+    ess_total = _aggregate_ess([dict(ess_total=_aggregate_ess(lidar_certs))])
+    exc_total = 0.0   # max dt_effect + max extrinsic_effect over the bin-path certs (all 0)
+    ess_to_exc = ess_total / (exc_total + eps)
+    s_z = z_to_xy / (z_to_xy + ops.POWER_BETA_Z_C)
+    s_exc = 1.0 / (1.0 + ess_to_exc / ops.POWER_BETA_EXC_C)
+    s = min(max(dt_asym * s_z * s_exc, 0.0), 1.0)
+    beta = ops.POWER_BETA_MIN + (1.0 - ops.POWER_BETA_MIN) * s
+    beta = min(max(beta, ops.POWER_BETA_MIN), 1.0)
+    L_ev, h_ev = beta * L_raw, beta * h_raw
+    certs.append(dict(name="temper", power_beta=beta))
+    s_dt, s_ex = ops.excitation_scales(L_ev, b_pred.L)
+    Lp, hp = ops.apply_excitation_scaling(b_pred.L, b_pred.h, s_dt, s_ex)
+    certs.append(dict(name="excitation", dt_scale=1.0 - s_dt, extrinsic_scale=1.0 - s_ex))
+    b_pred = ops.Belief(b_pred.X_anchor, b_pred.stamp_sec, b_pred.z_lin, Lp, hp)
+    # 10 FusionScaleFromCertificates: alpha_min = alpha_max = 1 (constants.py:89-90) -> alpha = 1
+    alpha = 1.0
+    certs.append(dict(name="fusion_scale", trust_alpha=alpha))
+    # 11 InfoFusionAdditive
+    b_post, infl = ops.info_fusion_additive(b_pred, L_ev, h_ev, alpha)
+    certs.append(dict(name="fusion", **infl))
+    # 12 PoseUpdateFrobeniusRecompose (T = sum of trigger magnitudes, pipeline.py:1211)
+    T = sum(ops.trigger_magnitude(c) for c in certs)
+    b_rec, rinfo = ops.frobenius_recompose(b_post, T)
+    certs.append(dict(name="recompose"))
+    dPsi, dnu = ops.process_noise_iw_suffstats(b_pred.L, b_pred.h, b_rec.L, b_rec.h)
+    # 13 PoseCovInflationPushforward (map update with z_t)
+    z_t = b_rec.mean_world_pose()
+    cov_rec, _ = spd_inverse_lifted(b_rec.L, ops.EPS_LIFT)
+    new_stats = ops.pose_cov_inflation_pushforward(m.stats, st, z_t, cov_rec[0:6, 0:6], cfg.forgetting_factor)
+    new_map = MapState(new_stats, *ops.map_derived_stats(new_stats))
+    # 14 AnchorDriftUpdate
+    b_fin, dinfo = ops.anchor_drift_update(b_rec)
+    certs.append(dict(name="anchor_drift", **dinfo))
+    return dict(belief=b_fin, map=new_map, iw_process_dPsi=dPsi, iw_process_dnu=dnu,
+                budget=bud, deskew=dk, soft_assign=sa, scan_bins=st, mf=mf, planar=pt,
+                L_evidence=L_ev, h_evidence=h_ev, beta=beta, total_trigger=T,
+                frobenius_strength=rinfo["frobenius_strength"], z_t=z_t, xi_body=xi, certs=certs,
+                belief_post=b_post, belief_recomposed=b_rec)
+
+
+def combine_and_update_noise(results, weights, iw_state, scan_count):
+    """Node-level post-loop (FS/backend/backend_node.py:1999-2119): IW accumulation with raw
+    weights, barycenter with floor-renormalised weights, IW apply, Q rebuild."""
+    nu, Psi = iw_state
+    acc = np.zeros((7, 6, 6))
+    accn = np.zeros(7)
+    for w, r in zip(weights, results):
+        acc += w * r["iw_process_dPsi"]
+        accn += w * r["iw_process_dnu"]
+    L = np.stack([r["belief"].L for r in results])
+    h = np.stack([r["belief"].h for r in results])
+    z = np.stack([r["belief"].z_lin for r in results])
+    combo = ops.hypothesis_barycenter(L, h, z, weights)
+    wp = min(1, scan_count)
+    nu2, Psi2, cert = ops.process_noise_iw_apply(nu, Psi, wp * acc, wp * accn)
+    Q = ops.process_noise_Q(nu2, Psi2)
+    return dict(combined=combo, iw_state=(nu2, Psi2), Q=Q, iw_cert=cert, acc_dPsi=acc, acc_dnu=accn)

@@ -1,0 +1,136 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol declared in include/gcslam_hip.h,
+and its host-side numerics / atlas tables match the oracle (no GPU compute calls here)."""
+
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from gcslam import _lib as L
+from oracle import ops, se3
+from oracle.primitives import psd_project, spd_inverse_lifted, spd_solve_lifted
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol(lib):
+    hdr = open(os.path.join(ROOT, "include", "gcslam_hip.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(gcs_\w+)\s*\(", hdr, re.M))
+    assert declared, "no declarations parsed"
+    assert declared == set(L.SYMBOLS), declared ^ set(L.SYMBOLS)
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.gcs_abi_version() == 1
+
+
+@pytest.mark.parametrize("n", [3, 6, 22])
+def test_psd_project_matches_oracle(lib, n):
+    rng = np.random.default_rng(n)
+    for shift in (-0.5, 0.0, 1.0):
+        A = rng.standard_normal((n, n))
+        M = np.ascontiguousarray(A @ A.T + shift * np.eye(n) + 1e-3 * rng.standard_normal((n, n)))
+        out = np.zeros((n, n))
+        cert = np.zeros(6)
+        assert lib.gcs_psd_project(n, L.dptr(M), 1e-12, L.dptr(out), L.dptr(cert)) == 0
+        ref, rc = psd_project(M)
+        scale = np.abs(M).max()
+        assert np.allclose(out, ref, atol=1e-13 * scale * n, rtol=0)
+        assert cert[0] == pytest.approx(rc[0], abs=1e-13 * scale * n)
+        assert cert[1] == pytest.approx(rc[1], rel=1e-12, abs=1e-300)
+
+
+def test_spd_solve_and_inverse_match_oracle(lib):
+    rng = np.random.default_rng(11)
+    A = rng.standard_normal((22, 22))
+    Lm = np.ascontiguousarray(A @ A.T + 0.1 * np.eye(22))
+    b = rng.standard_normal(22)
+    x = np.zeros(22)
+    inv = np.zeros((22, 22))
+    lib.gcs_spd_solve_lifted(22, L.dptr(Lm), L.dptr(b), 1e-9, L.dptr(x))
+    lib.gcs_spd_inverse_lifted(22, L.dptr(Lm), 1e-9, L.dptr(inv))
+    assert np.allclose(x, spd_solve_lifted(Lm, b)[0], rtol=1e-10, atol=1e-12)
+    assert np.allclose(inv, spd_inverse_lifted(Lm)[0], rtol=1e-10, atol=1e-12)
+
+
+def test_svd3_reconstructs_and_matches_numpy_singular_values(lib):
+    rng = np.random.default_rng(12)
+    for k in range(20):
+        H = rng.standard_normal((3, 3))
+        if k % 5 == 0:
+            H[:, 2] = H[:, 0] + H[:, 1]         # rank 2
+        H = np.ascontiguousarray(H)
+        U, s, V = np.zeros(9), np.zeros(3), np.zeros(9)
+        lib.gcs_svd3(L.dptr(H), L.dptr(U), L.dptr(s), L.dptr(V))
+        U, V = U.reshape(3, 3), V.reshape(3, 3)
+        assert np.allclose(U @ np.diag(s) @ V.T, H, atol=1e-13)
+        assert np.allclose(s, np.linalg.svd(H)[1], atol=1e-13)
+        assert np.allclose(U.T @ U, np.eye(3), atol=1e-12) and np.allclose(V.T @ V, np.eye(3), atol=1e-12)
+
+
+def test_predict_and_fusion_match_oracle(lib):
+    rng = np.random.default_rng(13)
+    b = ops.Belief.identity_prior()
+    b.L = b.L + np.diag(rng.uniform(1, 10, 22))
+    b.h = rng.standard_normal(22)
+    nu, Psi = ops.datasheet_process_noise_state()
+    Q = ops.process_noise_Q(nu, Psi)
+    s = L.belief_to_struct(b.X_anchor, b.stamp_sec, b.z_lin, b.L, b.h)
+    o = L.GcsBelief()
+    cert = np.zeros(4)
+    lib.gcs_predict_diffusion(C.byref(s), L.dptr(np.ascontiguousarray(Q)), 0.1, C.byref(o), L.dptr(cert))
+    ref, infl = ops.predict_diffusion(b, Q, 0.1)
+    X, st, z, Lm, h = L.struct_to_arrays(o)
+    assert np.allclose(Lm, ref.L, rtol=1e-9, atol=1e-9 * np.abs(ref.L).max())
+    assert np.allclose(h, ref.h, rtol=1e-9, atol=1e-12)
+    Lev = np.ascontiguousarray(np.diag(rng.uniform(0, 5, 22)))
+    hev = rng.standard_normal(22)
+    p2 = L.GcsBelief()
+    d = np.zeros(1)
+    lib.gcs_info_fusion_additive(C.byref(o), L.dptr(Lev), L.dptr(hev), 1.0, C.byref(p2), L.dptr(d))
+    r2, inf2 = ops.info_fusion_additive(ref, Lev, hev, 1.0)
+    assert np.allclose(L.struct_to_arrays(p2)[3], r2.L, rtol=1e-9, atol=1e-9 * np.abs(r2.L).max())
+
+
+def test_preintegration_matches_oracle(lib):
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "gc-slam_amd"))
+    from gcslam import synthetic
+    sc = synthetic.make_scan(256, 0)
+    w = ops.smooth_window_weights(sc["imu_stamps"], sc["scan_start_time"], sc["scan_end_time"], 0.01)
+    rv, gb, ab = np.array([0.01, -0.02, 0.3]), np.array([1e-3, 0, 0]), np.array([0, 1e-2, 0])
+    g = np.array(ops.GRAVITY_W)
+    ref = ops.preintegrate_imu(sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], w, rv, gb, ab, g)
+    dp = np.zeros(6)
+    ess = np.zeros(1)
+    args = [np.ascontiguousarray(a, np.float64) for a in (sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], w, rv,
+                                                            gb, ab, g)]
+    lib.gcs_preintegrate_imu(len(w), *[L.dptr(a) for a in args], L.dptr(dp), L.dptr(ess))
+    assert np.allclose(dp, ref["delta_pose"], rtol=1e-11, atol=1e-14)
+    assert ess[0] == pytest.approx(ref["ess"], rel=1e-13)
+
+
+@pytest.mark.parametrize("B", [48, 1000, 20000])
+def test_atlas_knn_nearest_bit_exact(lib, B):
+    d = np.zeros((B, 3))
+    lib.gcs_fibonacci_atlas(B, L.dptr(d))
+    assert np.allclose(d, ops.fibonacci_atlas(B), atol=2e-15, rtol=0)
+    K = min(16, B)
+    knn = np.zeros((B, K), np.int32)
+    lib.gcs_knn_table(B, L.dptr(d), K, L.iptr(knn))
+    assert np.array_equal(knn, ops.bin_knn_table(d, K))           # bit-exact indices
+    rng = np.random.default_rng(B)
+    q = np.ascontiguousarray(ops.point_directions(rng.standard_normal((3000, 3)), np.zeros(3)))
+    q[0] = 0.0                                                     # degenerate zero direction -> bin 0
+    nb = np.zeros(3000, np.int32)
+    lib.gcs_nearest_bins(B, L.dptr(d), 3000, L.dptr(q), L.iptr(nb))
+    assert np.array_equal(nb, ops.nearest_bin(q, d))
+
+
+def test_missing_library_fails_loudly(monkeypatch, tmp_path):
+    import importlib
+    monkeypatch.setattr(L, "LIB_PATH", str(tmp_path / "nope.so"))
+    monkeypatch.setattr(L, "_lib", None)
+    with pytest.raises(RuntimeError):
+        L.load()
