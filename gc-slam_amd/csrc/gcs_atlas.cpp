@@ -197,7 +197,8 @@ void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& 
     std::sort(L.begin(), L.end());
   });
   width = 1;
-  for (auto& L : lists) width = std::max(width, (int)L.size());
+  for (auto& L : lists) width = std::max(width, (int)L.size() + 1);  // >= one -1 terminator
+  width = (width + 3) & ~3;                                           // int4 loads
   pools.assign((size_t)ncell * width, -1);
   for (int c = 0; c < ncell; ++c)
     std::copy(lists[c].begin(), lists[c].end(), pools.begin() + (size_t)c * width);

@@ -41,12 +41,11 @@ struct gcs_ctx {
   std::vector<int> knn_host;
   // per-point
   PointRec* d_recs = nullptr;
-  uint32_t *d_keys = nullptr, *d_vals = nullptr, *d_keys_s = nullptr, *d_vals_s = nullptr;
-  void* d_sort_tmp = nullptr;
-  size_t sort_bytes = 0;
+  uint32_t *d_keys = nullptr, *d_slots = nullptr, *d_sorted = nullptr;
   int* d_nearest = nullptr;
-  // per-bin
-  int2* d_ranges = nullptr;
+  // per-bin bucketing
+  uint32_t *d_counts = nullptr /*B+1: last = big bucket count*/, *d_starts = nullptr, *d_tile_sums = nullptr,
+           *d_big_list = nullptr;
   uint8_t* d_flags = nullptr;
   double* d_scan = nullptr;
   double* d_map = nullptr;
@@ -197,12 +196,18 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.grid = c->G;
   a.recs = c->d_recs;
   a.keys = c->d_keys;
-  a.vals = c->d_vals;
+  a.slots = c->d_slots;
+  a.counts = c->d_counts;
+  a.flags = c->d_flags;
   a.scalars = c->d_scalars;
   a.p0_out = p0_out;
   a.w_out = w_out;
   a.w_budget_out = wb_out;
   a.nearest_out = c->d_nearest;
+  if (c->cfg.mode == GCS_MODE_SCALE) {
+    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, ((size_t)c->B + 1) * sizeof(uint32_t), s));
+    HIPCHK(c, hipMemsetAsync(c->d_flags, 0, (size_t)c->B, s));
+  }
   HIPCHK(c, launch_points(a, c->cfg.mode == GCS_MODE_SCALE, c->d_partials, red_blocks(c->cap), s));
   return GCS_OK;
 }
@@ -210,8 +215,9 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
 BinKernelArgs bin_args(gcs_ctx* c) {
   BinKernelArgs b{};
   b.recs = c->d_recs;
-  b.sorted_vals = c->d_vals_s;
-  b.ranges = c->d_ranges;
+  b.sorted_vals = c->d_sorted;
+  b.starts = c->d_starts;
+  b.counts = c->d_counts;
   b.flags = c->d_flags;
   b.rknn_off = c->d_rknn_off;
   b.rknn = c->d_rknn;
@@ -227,16 +233,12 @@ BinKernelArgs bin_args(gcs_ctx* c) {
 int stage_bins(gcs_ctx* c) {
   hipStream_t s = c->stream;
   BinKernelArgs b = bin_args(c);
-  int nblk = (c->B + 255) / 256;
+  int nblk = c->cfg.mode == GCS_MODE_SCALE ? bins_scale_blocks(c->B) : (c->B + 255) / 256;
   if (c->cfg.mode == GCS_MODE_SCALE) {
-    int end_bit = 1;
-    while ((1u << end_bit) <= (unsigned)c->B) ++end_bit;
     {
       StageTimer timer(c, ST_SORT);
-      HIPCHK(c, launch_sort(c->d_sort_tmp, c->sort_bytes, c->d_keys, c->d_keys_s, c->d_vals, c->d_vals_s, c->cap, end_bit, s));
-      HIPCHK(c, hipMemsetAsync(c->d_ranges, 0, (size_t)c->B * sizeof(int2), s));
-      HIPCHK(c, hipMemsetAsync(c->d_flags, 0, (size_t)c->B, s));
-      HIPCHK(c, launch_bucket_mark(c->d_keys_s, c->cap, c->B, c->d_knn, c->K, c->d_ranges, c->d_flags, s));
+      HIPCHK(c, launch_bucketing(c->d_counts, c->d_starts, c->d_tile_sums, c->d_keys, c->d_slots, c->cap, c->B,
+                                 c->d_sorted, c->d_big_list, c->d_counts + c->B, s));
     }
     StageTimer timer(c, ST_BINS);
     HIPCHK(c, launch_bins_scale(b, c->d_partials, s));
@@ -266,7 +268,17 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) 
   pa.t[0] = z_t[0];
   pa.t[1] = z_t[1];
   pa.t[2] = 0.0;  // t_z := 0 before the map update (CHANGELOG.md:575-578)
-  memcpy(pa.Sigma_pose, Sig6, 36 * sizeof(double));
+  double Srt[9], Srr[9], RS[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      pa.Stt[3 * i + j] = Sig6[6 * i + j];
+      Srt[3 * i + j] = Sig6[6 * (3 + i) + j];
+      Srr[3 * i + j] = Sig6[6 * (3 + i) + 3 + j];
+    }
+  mat3_mul(pa.R, Srt, pa.F);
+  mat3_mul(pa.R, Srr, RS);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) pa.G[3 * i + j] = RS[3 * i] * pa.R[3 * j] + RS[3 * i + 1] * pa.R[3 * j + 1] + RS[3 * i + 2] * pa.R[3 * j + 2];
   pa.gamma = gamma;
   StageTimer timer(c, ST_PUSH);
   HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->stream));
@@ -322,7 +334,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_derived, B * MD_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_map, 0, B * MF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scan, 0, B * SF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
-  c->partials_len = std::max<size_t>((size_t)kRedBlocks * 24, ((B + 255) / 256) * 5 + 64);
+  c->partials_len = std::max<size_t>((size_t)kRedBlocks * 24, ((B + 63) / 64) * 5 + 64);
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
@@ -332,13 +344,13 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMalloc(&c->d_rknn_off, (B + 1) * sizeof(int)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_rknn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_keys, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_vals, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_keys_s, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_vals_s, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_ranges, B * sizeof(int2)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_slots, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_sorted, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_counts, (B + 1) * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_starts, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_tile_sums, (B / 4096 + 2) * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_big_list, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_flags, B))) return GCS_ERR_HIP;
-    c->sort_bytes = sort_temp_bytes(c->cap);
-    if (bad(hipMalloc(&c->d_sort_tmp, std::max<size_t>(c->sort_bytes, 16)))) return GCS_ERR_HIP;
   } else {
     size_t nchunks = (cap + 255) / 256;
     if (bad(hipMalloc(&c->d_bin_partials, nchunks * 19 * B * sizeof(double)))) return GCS_ERR_HIP;
@@ -362,9 +374,9 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
 
 int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
-  void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_vals,
-                  c->d_keys_s, c->d_vals_s, c->d_sort_tmp, c->d_nearest, c->d_ranges, c->d_flags, c->d_scan,
-                  c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
+  void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
+                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_tile_sums, c->d_big_list, c->d_flags,
+                  c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
@@ -504,9 +516,7 @@ __global__ void k_materialize(const PointRec* recs, const int* nearest, const in
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
   PointRec pr = recs[i];
-  double rx = pr.x - ox, ry = pr.y - oy, rz = pr.z - oz;
-  double nrm = sqrt(dot3_exact(rx, ry, rz, rx, ry, rz)) + kEpsMass;
-  double d0 = rx / nrm, d1 = ry / nrm, d2 = rz / nrm;
+  double d0 = pr.dx, d1 = pr.dy, d2 = pr.dz;
   double it = 1.0 / tau;
   if (scale) {
     const int* row = knn + (size_t)nearest[i] * K;

@@ -66,6 +66,15 @@ double psd_project(int n, const double* M, double eps_psd, double* out, double* 
       double d = s[i * n + j] - M[i * n + j];
       sym2 += d * d;
     }
+  if (!cert6) {
+    // fast path (see gcs_math.h psd_project3): M_sym - eps I positive definite -> no clamping
+    std::vector<double> A(s), Lc(n * n);
+    for (int i = 0; i < n; ++i) A[i * n + i] -= eps_psd;
+    if (cholesky(n, A.data(), Lc.data())) {
+      for (int i = 0; i < n * n; ++i) out[i] = s[i];
+      return 0.0;
+    }
+  }
   bool zero = true;
   for (int i = 0; i < n * n; ++i) zero = zero && s[i] == 0.0;
   if (zero) {

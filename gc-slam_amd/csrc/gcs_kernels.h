@@ -30,7 +30,9 @@ struct PointKernelArgs {
   // outputs
   PointRec* recs;
   uint32_t* keys;
-  uint32_t* vals;
+  uint32_t* slots;
+  uint32_t* counts;  // per-bin bucket sizes (zeroed before the launch)
+  uint8_t* flags;    // active-bin flags (zeroed before the launch)
   double* scalars;
   // optional debug/parity outputs (may be null)
   double* p0_out;
@@ -42,7 +44,8 @@ struct PointKernelArgs {
 struct BinKernelArgs {
   const PointRec* recs;
   const uint32_t* sorted_vals;
-  const int2* ranges;
+  const uint32_t* starts;
+  const uint32_t* counts;
   const uint8_t* flags;
   const int* rknn_off;
   const int* rknn;
@@ -56,18 +59,19 @@ struct BinKernelArgs {
 struct PushArgs {
   double R[9];
   double t[3];
-  double Sigma_pose[36];
+  double Stt[9];  // translation block of the pose covariance
+  double F[9];    // R S_rt   (rotation rows, translation columns)
+  double G[9];    // R S_rr R^T
   double gamma;
 };
 
 hipError_t launch_budget(const double* w, int n_raw, int stride, double* partials, int nblk, double* scalars,
                          hipStream_t s);
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, hipStream_t s);
-size_t sort_temp_bytes(int n);
-hipError_t launch_sort(void* temp, size_t temp_bytes, uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
-                       uint32_t* vals_out, int n, int end_bit, hipStream_t s);
-hipError_t launch_bucket_mark(const uint32_t* keys, int n, int n_bins, const int* knn, int k, int2* ranges,
-                              uint8_t* flags, hipStream_t s);
+hipError_t launch_bucketing(uint32_t* counts, uint32_t* starts, uint32_t* tile_sums, const uint32_t* keys,
+                            const uint32_t* slots, int n, int n_bins, uint32_t* sorted, uint32_t* big_list,
+                            uint32_t* big_n, hipStream_t s);
+int bins_scale_blocks(int n_bins);
 hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s);
 hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* partials, hipStream_t s);
 hipError_t launch_bin_cert_final(const double* partials, int nblk, double* scalars, hipStream_t s);

@@ -5,8 +5,7 @@
 //                   K-candidate softmax normaliser (BinSoftAssign, scale mode) or dense
 //                   softmax normaliser, and the per-point certificate partials
 //                   deskew_constant_twist.py:31-69, pipeline.py:589-593, binning.py:56-76
-//   (radix sort of points by nearest bin: rocPRIM, stable -> deterministic buckets)
-//   k_bucket_mark   bucket ranges + active-bin flags
+//   k_scan_*, k_place, k_bucket_*   deterministic bucketing of points by nearest bin
 //   k_bins_scale    bin-centric gather: ScanBinMomentMatch + Kappa, finalize + write
 //                   binning.py:139-209, kappa.py:130-169
 //   k_dense_*       the reference's dense N x B form (legacy B=48)
@@ -20,8 +19,6 @@
 // so results are bitwise reproducible run to run (docs/GC_SLAM.md:1150).  No float atomics.
 #include <hip/hip_runtime.h>
 
-#include <cstring>
-#include <rocprim/rocprim.hpp>
 
 #include "gcs_kernels.h"
 #include "gcs_layout.h"
@@ -137,9 +134,18 @@ __global__ __launch_bounds__(kBlock) void k_budget_partial(const double* __restr
   }
 }
 
-__global__ void k_budget_scale(double* scalars) {
-  // mass_scale = total_mass_in / (total_mass_selected + eps_mass)   point_budget.py:80-84
-  scalars[SC_MASS_SCALE] = scalars[SC_MASS_IN] / (scalars[SC_MASS_SEL] + kEpsMass);
+__global__ __launch_bounds__(kBlock) void k_budget_final(const double* __restrict__ partials, int nblocks,
+                                                         double* scalars) {
+  __shared__ double lds[kWaves * 2];
+  double v[2] = {0.0, 0.0};
+  for (int b = threadIdx.x; b < nblocks; b += kBlock) { v[0] += partials[2 * b]; v[1] += partials[2 * b + 1]; }
+  block_sum<2>(v, lds);
+  if (threadIdx.x == 0) {
+    scalars[SC_MASS_IN] = v[0];
+    scalars[SC_MASS_SEL] = v[1];
+    // mass_scale = total_mass_in / (total_mass_selected + eps_mass)   point_budget.py:80-84
+    scalars[SC_MASS_SCALE] = v[0] / (v[1] + kEpsMass);
+  }
 }
 
 // ---------------------------------------------------------------- cube-map cell of a direction
@@ -168,7 +174,7 @@ __device__ __forceinline__ void ray_dir(double px, double py, double pz, const d
 
 // ---------------------------------------------------------------- row 1+3+5: the point kernel
 // One thread per budget output slot i in [0, cap).  SCALE = candidate-restricted softmax.
-template <bool SCALE>
+template <bool SCALE, int KC>
 __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* partials) {
   __shared__ double lds[kWaves * 5];
   const double mass_scale = a.scalars[SC_MASS_SCALE];
@@ -199,32 +205,51 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
       // exact nearest atlas bin: pool of the direction's cube cell, ascending ids, strict '>'
       bool zero = (d[0] == 0.0 && d[1] == 0.0 && d[2] == 0.0);
       if (!zero) {
-        const int* pool = a.pools + (size_t)cube_cell(d[0], d[1], d[2], a.grid) * a.pool_width;
+        const int4* pool = (const int4*)(a.pools + (size_t)cube_cell(d[0], d[1], d[2], a.grid) * a.pool_width);
         double best = -INFINITY;
-        for (int q = 0; q < a.pool_width; ++q) {
-          int b = pool[q];
-          if (b < 0) break;
-          const double* bd = a.bin_dirs + 4 * (size_t)b;
-          double s = dot3_exact(d[0], d[1], d[2], bd[0], bd[1], bd[2]);
-          if (s > best) { best = s; nearest = b; }
+        for (int q = 0; q < (a.pool_width >> 2); ++q) {
+          int4 id4 = pool[q];
+          int ids[4] = {id4.x, id4.y, id4.z, id4.w};
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (ids[u] >= 0) {
+              const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)ids[u]);
+              double s = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
+              if (s > best) { best = s; nearest = ids[u]; }
+            }
+          }
+          if (id4.w < 0) break;
         }
       }
-      const int* cand = a.knn + (size_t)nearest * a.k;
-      double sims[32];
-      for (int k = 0; k < a.k; ++k) {
-        const double* bd = a.bin_dirs + 4 * (size_t)cand[k];
-        sims[k] = dot3_exact(d[0], d[1], d[2], bd[0], bd[1], bd[2]);
+      const int* cand = a.knn + (size_t)nearest * KC;
+      double sims[KC];
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)cand[k]);
+        sims[k] = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
         m = fmax(m, sims[k]);
       }
-      for (int k = 0; k < a.k; ++k) Z += exp((sims[k] - m) * inv_tau);
+#pragma unroll
+      for (int k = 0; k < KC; ++k) Z += exp((sims[k] - m) * inv_tau);
       double iz = 1.0 / Z;
-      for (int k = 0; k < a.k; ++k) {
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
         double r = exp((sims[k] - m) * inv_tau) * iz;
         H -= r * log(r + kEpsMass);
         rm = fmax(rm, r);
       }
-      a.keys[i] = valid ? (uint32_t)nearest : (uint32_t)a.n_bins;
-      a.vals[i] = (uint32_t)i;
+      uint32_t key = (uint32_t)a.n_bins;
+      if (valid) {
+        // bucket slot: arrival order only (reordered by point index in k_bucket_order)
+        uint32_t slot = atomicAdd(a.counts + nearest, 1u);
+        a.slots[i] = slot;
+        key = (uint32_t)nearest;
+        if (slot == 0) {  // first arrival marks the bucket's candidate bins active
+#pragma unroll
+          for (int k = 0; k < KC; ++k) a.flags[cand[k]] = 1;
+        }
+      }
+      a.keys[i] = key;
       Z = iz;
     } else {
       for (int b = 0; b < a.n_bins; ++b) {
@@ -245,7 +270,9 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
       Z = iz;
     }
     PointRec pr;
-    pr.x = p0[0]; pr.y = p0[1]; pr.z = p0[2]; pr.w = wout; pr.m = m; pr.iz = Z;
+    pr.x = p0[0]; pr.y = p0[1]; pr.z = p0[2];
+    pr.dx = d[0]; pr.dy = d[1]; pr.dz = d[2];
+    pr.w = wout; pr.m = m; pr.iz = Z; pr.pad = 0.0;
     a.recs[i] = pr;
     if (a.p0_out) { a.p0_out[3 * (size_t)i] = p0[0]; a.p0_out[3 * (size_t)i + 1] = p0[1]; a.p0_out[3 * (size_t)i + 2] = p0[2]; }
     if (a.w_out) a.w_out[i] = wout;
@@ -266,21 +293,107 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
   }
 }
 
-// ---------------------------------------------------------------- bucket ranges + active flags
-__global__ __launch_bounds__(kBlock) void k_bucket_mark(const uint32_t* __restrict__ keys, int n, int n_bins,
-                                                        const int* __restrict__ knn, int k, int2* ranges,
-                                                        uint8_t* flags) {
+// ---------------------------------------------------------------- deterministic bucketing by nearest bin
+// counts[] were filled by atomic slots in k_points.  start[] = exclusive scan of counts in two
+// passes over 4096-bucket tiles; points are placed at start+slot, then every bucket is reordered
+// by ascending point index (insertion sort up to 64 entries, an in-order compaction over all
+// keys for larger buckets), so the bin gather sees a scheduling-independent order.
+constexpr int kScanTile = 4096;
+__global__ __launch_bounds__(kBlock) void k_scan_tiles(const uint32_t* __restrict__ counts, int n, uint32_t* tile_sums) {
+  __shared__ uint32_t ws[kWaves];
+  int base = blockIdx.x * kScanTile;
+  uint32_t s = 0;
+  for (int i = base + threadIdx.x; i < min(base + kScanTile, n); i += kBlock) s += counts[i];
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+__global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* __restrict__ counts, int n,
+                                                       const uint32_t* __restrict__ tile_sums, uint32_t* start) {
+  __shared__ uint32_t wsum[kWaves];
+  __shared__ uint32_t carry;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if (t == 0) {
+    uint32_t c = 0;
+    for (int b = 0; b < (int)blockIdx.x; ++b) c += tile_sums[b];
+    carry = c;
+  }
+  __syncthreads();
+  int base = blockIdx.x * kScanTile;
+  for (int c0 = base; c0 < min(base + kScanTile, n); c0 += kBlock) {
+    int i = c0 + t;
+    uint32_t v = i < n ? counts[i] : 0u;
+    uint32_t x = v;  // inclusive wave scan
+    for (int off = 1; off < 64; off <<= 1) {
+      uint32_t y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t pre = carry;
+    for (int w = 0; w < wid; ++w) pre += wsum[w];
+    if (i < n) start[i] = pre + x - v;
+    __syncthreads();
+    if (t == kBlock - 1) carry = pre + x;
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_place(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ slots,
+                                                  const uint32_t* __restrict__ start, int n, int n_bins,
+                                                  uint32_t* sorted) {
   for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     uint32_t key = keys[i];
-    if (key >= (uint32_t)n_bins) continue;
-    bool first = (i == 0) || keys[i - 1] != key;
-    bool last = (i == n - 1) || keys[i + 1] != key;
-    if (first) {
-      ranges[key].x = i;
-      const int* row = knn + (size_t)key * k;
-      for (int q = 0; q < k; ++q) flags[row[q]] = 1;
+    if (key < (uint32_t)n_bins) sorted[start[key] + slots[i]] = (uint32_t)i;
+  }
+}
+
+constexpr int kSmallBucket = 64;
+__global__ __launch_bounds__(kBlock) void k_bucket_order(const uint32_t* __restrict__ counts,
+                                                         const uint32_t* __restrict__ start, int n_bins,
+                                                         uint32_t* sorted, uint32_t* big_list, uint32_t* big_n) {
+  for (int a = blockIdx.x * kBlock + threadIdx.x; a < n_bins; a += gridDim.x * kBlock) {
+    uint32_t c = counts[a];
+    if (c < 2) continue;
+    if (c > (uint32_t)kSmallBucket) {
+      big_list[atomicAdd(big_n, 1u)] = (uint32_t)a;
+      continue;
     }
-    if (last) ranges[key].y = i + 1;
+    uint32_t* v = sorted + start[a];
+    for (uint32_t j = 1; j < c; ++j) {
+      uint32_t x = v[j];
+      int q = (int)j - 1;
+      while (q >= 0 && v[q] > x) { v[q + 1] = v[q]; --q; }
+      v[q + 1] = x;
+    }
+  }
+}
+
+// big buckets: one block rebuilds the bucket by an in-order compaction over all keys
+__global__ __launch_bounds__(kBlock) void k_bucket_big(const uint32_t* __restrict__ keys, int n,
+                                                       const uint32_t* __restrict__ start,
+                                                       const uint32_t* __restrict__ big_list,
+                                                       const uint32_t* __restrict__ big_n, uint32_t* sorted) {
+  __shared__ uint32_t wcnt[kWaves];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  uint32_t nb = *big_n;
+  for (uint32_t j = blockIdx.x; j < nb; j += gridDim.x) {
+    uint32_t a = big_list[j];
+    uint32_t pos = start[a];
+    for (int c0 = 0; c0 < n; c0 += kBlock) {
+      int i = c0 + t;
+      bool hit = i < n && keys[i] == a;
+      unsigned long long m = __ballot(hit);
+      if (lane == 0) wcnt[wid] = (uint32_t)__popcll(m);
+      __syncthreads();
+      uint32_t pre = pos;
+      for (int w = 0; w < wid; ++w) pre += wcnt[w];
+      if (hit) sorted[pre + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
+      pos += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      __syncthreads();
+    }
   }
 }
 
@@ -352,39 +465,28 @@ __device__ __forceinline__ void write_bin_cert(double* cert, double* lds, double
 }
 
 // ---------------------------------------------------------------- row 5+6 scale mode: bin-centric
-// One workgroup per tile of 256 consecutive bins.  Phase 1 compacts the active bins of the
-// tile; phase 2 gathers each active bin's contributions with a 16-lane group (fixed order:
-// reverse-kNN bucket order, then ascending point index, lane-strided, fixed xor tree);
-// phase 3 finalizes every bin of the tile and streams the 26 SoA fields.
+// One 256-thread workgroup per tile of 64 consecutive bins.  Phase 1 compacts the tile's active
+// bins (ballot, wave order).  Phase 2: a 16-lane group per active bin; lane l owns the bin's
+// reverse-kNN buckets l, l+16, ... (fixed order) and walks each bucket's points in ascending
+// point index (stable sort), so each lane's dependent chain is one bucket deep and the 16
+// buckets are fetched concurrently; the 16 lane sums meet in a fixed xor tree.  Phase 3: the
+// first wave finalizes the 64 bins (PSD, kappa) and streams the 26 field-major outputs.
+constexpr int kTile = 64;
 constexpr int kGroup = 16;
 __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* partials) {
-  __shared__ double sums[19 * kBlock];
-  __shared__ int active[kBlock];
+  __shared__ double sums[19 * kTile];
+  __shared__ int active[kTile];
   __shared__ int n_active;
   __shared__ double lds[kWaves * 4];
   const int t = threadIdx.x;
-  const int b0 = blockIdx.x * kBlock;
-  const int b = b0 + t;
-  for (int f = 0; f < 19; ++f) sums[f * kBlock + t] = 0.0;
-  if (t == 0) n_active = 0;
-  __syncthreads();
-  bool act = (b < a.n_bins) && a.flags[b];
-  // deterministic compaction: ballot per wave, prefix over waves in wave order
-  unsigned long long mask = __ballot(act);
-  int lane = t & 63, wid = t >> 6;
-  __shared__ int wcount[kWaves];
-  if (lane == 0) wcount[wid] = __popcll(mask);
-  __syncthreads();
-  int base = 0;
-  for (int w = 0; w < wid; ++w) base += wcount[w];
-  if (act) {
-    int rank = __popcll(mask & ((1ull << lane) - 1ull));
-    active[base + rank] = t;
-  }
-  if (t == 0) {
-    int s = 0;
-    for (int w = 0; w < kWaves; ++w) s += wcount[w];
-    n_active = s;
+  const int b0 = blockIdx.x * kTile;
+  for (int i = t; i < 19 * kTile; i += kBlock) sums[i] = 0.0;
+  if (t < 64) {
+    int b = b0 + t;
+    bool act = (b < a.n_bins) && a.flags[b];
+    unsigned long long mask = __ballot(act);
+    if (act) active[__popcll(mask & ((1ull << t) - 1ull))] = t;
+    if (t == 0) n_active = __popcll(mask);
   }
   __syncthreads();
   const int g = t / kGroup, l = t % kGroup;
@@ -392,22 +494,48 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   for (int j = g; j < n_active; j += kBlock / kGroup) {
     int lb = active[j];
     int bb = b0 + lb;
-    const double* bd = a.bin_dirs + 4 * (size_t)bb;
-    double bx = bd[0], by = bd[1], bz = bd[2];
+    const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)bb);
     double acc[19];
 #pragma unroll
     for (int f = 0; f < 19; ++f) acc[f] = 0.0;
-    int q0 = a.rknn_off[bb], q1 = a.rknn_off[bb + 1];
-    for (int q = q0; q < q1; ++q) {
-      int2 rg = a.ranges[a.rknn[q]];
-      for (int i = rg.x + l; i < rg.y; i += kGroup) {
-        PointRec pr = a.recs[a.sorted_vals[i]];
-        double p[3] = {pr.x, pr.y, pr.z};
-        double d[3];
-        ray_dir(pr.x, pr.y, pr.z, a.origin, d);
-        double s = dot3_exact(d[0], d[1], d[2], bx, by, bz);
-        double r = exp((s - pr.m) * inv_tau) * pr.iz;
-        add_contrib(acc, pr.w * r, d, p);
+    const int q0 = a.rknn_off[bb], q1 = a.rknn_off[bb + 1];
+    // reverse-kNN buckets in chunks of 16 (one per lane); contributions flattened over the
+    // group in (bucket order, ascending point index) and dealt to lanes round-robin
+    for (int qc = q0; qc < q1; qc += kGroup) {
+      int q = qc + l;
+      uint32_t st = 0, ct = 0;
+      if (q < q1) {
+        int src = a.rknn[q];
+        st = a.starts[src];
+        ct = a.counts[src];
+      }
+      uint32_t x = ct;  // inclusive scan over the 16 lanes of the group
+#pragma unroll
+      for (int off = 1; off < kGroup; off <<= 1) {
+        uint32_t y = __shfl_up(x, off, kGroup);
+        if (l >= off) x += y;
+      }
+      const uint32_t pre = x - ct;
+      const uint32_t tot = __shfl(x, kGroup - 1, kGroup);
+      for (uint32_t r0 = 0; r0 < tot; r0 += kGroup) {
+        uint32_t jj = r0 + (uint32_t)l;
+        // source lane = last lane whose exclusive prefix <= jj (binary search over the group)
+        int s = 0;
+#pragma unroll
+        for (int step = kGroup / 2; step >= 1; step >>= 1) {
+          uint32_t ps = __shfl(pre, s + step, kGroup);
+          if (ps <= jj && s + step < kGroup) s += step;
+        }
+        uint32_t s_st = __shfl(st, s, kGroup);
+        uint32_t s_pre = __shfl(pre, s, kGroup);
+        if (jj < tot) {
+          const PointRec pr = a.recs[a.sorted_vals[s_st + (jj - s_pre)]];
+          double d[3] = {pr.dx, pr.dy, pr.dz};
+          double p[3] = {pr.x, pr.y, pr.z};
+          double sim = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
+          double r = exp((sim - pr.m) * inv_tau) * pr.iz;
+          add_contrib(acc, pr.w * r, d, p);
+        }
       }
     }
 #pragma unroll
@@ -416,15 +544,15 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
       for (int f = 0; f < 19; ++f) acc[f] += __shfl_xor(acc[f], off, 64);
     if (l == 0)
 #pragma unroll
-      for (int f = 0; f < 19; ++f) sums[f * kBlock + lb] = acc[f];
+      for (int f = 0; f < 19; ++f) sums[f * kTile + lb] = acc[f];
   }
   __syncthreads();
   double cert[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
-  if (b < a.n_bins) {
+  if (t < kTile && b0 + t < a.n_bins) {
     double r[19];
 #pragma unroll
-    for (int f = 0; f < 19; ++f) r[f] = sums[f * kBlock + t];
-    finalize_bin(r, a.scan, a.n_bins, b, cert);
+    for (int f = 0; f < 19; ++f) r[f] = sums[f * kTile + t];
+    finalize_bin(r, a.scan, a.n_bins, b0 + t, cert);
   }
   write_bin_cert(cert, lds, partials);
 }
@@ -440,9 +568,7 @@ __global__ __launch_bounds__(kBlock) void k_dense_accum(BinKernelArgs a, double*
   if (i < a.cap) {
     PointRec pr = a.recs[i];
     pts[t] = pr;
-    double d[3];
-    ray_dir(pr.x, pr.y, pr.z, a.origin, d);
-    dirs[3 * t] = d[0]; dirs[3 * t + 1] = d[1]; dirs[3 * t + 2] = d[2];
+    dirs[3 * t] = pr.dx; dirs[3 * t + 1] = pr.dy; dirs[3 * t + 2] = pr.dz;
   }
   __syncthreads();
   int np = a.cap - blockIdx.x * kBlock;
@@ -622,112 +748,116 @@ __global__ __launch_bounds__(kBlock) void k_pt_final(const double* __restrict__ 
 }
 
 // ---------------------------------------------------------------- row 11: pushforward (declared)
+// Per bin: forgetting + world-frame increments at z_t = (R, t) + derived stats.  With u = R p_bar
+// and X = [u]x the pose-covariance pushforward J S J^T (J = [I, -R [p_bar]x]) is
+// S_tt - X F - (X F)^T + X G X^T with F = R S_rt, G = R S_rr R^T precomputed on the host.
+__device__ __forceinline__ void derive_bin(const double* sd, double nd, double np, const double* sp,
+                                           const double* spp, double* derived, size_t Bs, int b) {
+  double sn = sqrt(dot3_exact(sd[0], sd[1], sd[2], sd[0], sd[1], sd[2]));
+  double dn = sn + kEpsMass;
+#pragma unroll
+  for (int k = 0; k < 3; ++k) derived[(MD_MU + k) * Bs + b] = sd[k] / dn;
+  double invNd = 1.0 / (nd + kEpsMass + kF64Eps);
+  derived[MD_KAPPA * Bs + b] = kappa_from_rbar(sn * invNd);
+  double invNp = 1.0 / (np + kEpsMass + kF64Eps);
+  double c[3] = {sp[0] * invNp, sp[1] * invNp, sp[2] * invNp};
+  double raw[9], sig[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) raw[3 * i + j] = spp[3 * i + j] * invNp - c[i] * c[j];
+  psd_project3(raw, sig);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) derived[(MD_C + k) * Bs + b] = c[k];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) derived[(MD_SIG + k) * Bs + b] = sig[k];
+}
+
 __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict__ scan, double* map, double* derived,
                                                         int B, PushArgs pa) {
-  size_t Bs = (size_t)B;
+  const size_t Bs = (size_t)B;
   const double* R = pa.R;
-  const double* t = pa.t;
+  const double g = pa.gamma;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
-    double N = scan[SF_N * Bs + b];
-    double sd[3], S[9], pb[3], Sp[9];
+    const double N = scan[SF_N * Bs + b];
+    double pb[3], u[3], q[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { sd[k] = scan[(SF_SD + k) * Bs + b]; pb[k] = scan[(SF_PB + k) * Bs + b]; }
-#pragma unroll
-    for (int k = 0; k < 9; ++k) { S[k] = scan[(SF_S + k) * Bs + b]; Sp[k] = scan[(SF_SIG + k) * Bs + b]; }
-    // R s_dir, R S R^T
-    double Rsd[3], Rp[3];
+    for (int k = 0; k < 3; ++k) pb[k] = scan[(SF_PB + k) * Bs + b];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      Rsd[i] = R[3 * i] * sd[0] + R[3 * i + 1] * sd[1] + R[3 * i + 2] * sd[2];
-      Rp[i] = R[3 * i] * pb[0] + R[3 * i + 1] * pb[1] + R[3 * i + 2] * pb[2];
+      u[i] = R[3 * i] * pb[0] + R[3 * i + 1] * pb[1] + R[3 * i + 2] * pb[2];
+      q[i] = u[i] + pa.t[i];
     }
-    double RS[9], RSR[9], M2[9], RM[9], RMR[9];
-    mat3_mul(R, S, RS);
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) RSR[3 * i + j] = RS[3 * i] * R[3 * j] + RS[3 * i + 1] * R[3 * j + 1] + RS[3 * i + 2] * R[3 * j + 2];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) M2[3 * i + j] = Sp[3 * i + j] + pb[i] * pb[j];
-    mat3_mul(R, M2, RM);
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) RMR[3 * i + j] = RM[3 * i] * R[3 * j] + RM[3 * i + 1] * R[3 * j + 1] + RM[3 * i + 2] * R[3 * j + 2];
-    // J Sigma_pose J^T with J = [I, A], A = -R [p_bar]x
-    double K[9], A[9];
-    skew3(pb, K);
-    mat3_mul(R, K, A);
+    // S_dir += R s_dir
+    double sd[3];
+    {
+      double s0 = scan[(SF_SD + 0) * Bs + b], s1 = scan[(SF_SD + 1) * Bs + b], s2 = scan[(SF_SD + 2) * Bs + b];
 #pragma unroll
-    for (int k = 0; k < 9; ++k) A[k] = -A[k];
-    const double* P = pa.Sigma_pose;  // 6x6 row-major
-    double JSJ[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        double s = P[6 * i + j];
-        for (int k = 0; k < 3; ++k) {
-          s += A[3 * i + k] * P[6 * (3 + k) + j];      // A S_rt
-          s += P[6 * i + 3 + k] * A[3 * j + k];        // S_tr A^T
-        }
-        for (int k = 0; k < 3; ++k)
-          for (int l = 0; l < 3; ++l) s += A[3 * i + k] * P[6 * (3 + k) + 3 + l] * A[3 * j + l];
-        JSJ[3 * i + j] = s;
+      for (int i = 0; i < 3; ++i) {
+        sd[i] = g * map[(MF_SD + i) * Bs + b] + (R[3 * i] * s0 + R[3 * i + 1] * s1 + R[3 * i + 2] * s2);
+        map[(MF_SD + i) * Bs + b] = sd[i];
       }
-    double qv[3] = {Rp[0] + t[0], Rp[1] + t[1], Rp[2] + t[2]};
-    const double g = pa.gamma;
-    double nm[MF_COUNT];
+    }
+    // S_dir_scatter += R S R^T
+    {
+      double S[9], RS[9];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) nm[MF_SD + k] = g * map[(MF_SD + k) * Bs + b] + Rsd[k];
+      for (int k = 0; k < 9; ++k) S[k] = scan[(SF_S + k) * Bs + b];
+      mat3_mul(R, S, RS);
 #pragma unroll
-    for (int k = 0; k < 9; ++k) nm[MF_S + k] = g * map[(MF_S + k) * Bs + b] + RSR[k];
-    nm[MF_ND] = g * map[MF_ND * Bs + b] + N;
-    nm[MF_NP] = g * map[MF_NP * Bs + b] + N;
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int k = 0; k < 3; ++k) nm[MF_SP + k] = g * map[(MF_SP + k) * Bs + b] + N * qv[k];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j)
-        nm[MF_SPP + 3 * i + j] = g * map[(MF_SPP + 3 * i + j) * Bs + b] +
-                                 N * (RMR[3 * i + j] + JSJ[3 * i + j] + qv[i] * qv[j] - Rp[i] * Rp[j]);
+        for (int j = 0; j < 3; ++j) {
+          double v = RS[3 * i] * R[3 * j] + RS[3 * i + 1] * R[3 * j + 1] + RS[3 * i + 2] * R[3 * j + 2];
+          map[(MF_S + 3 * i + j) * Bs + b] = g * map[(MF_S + 3 * i + j) * Bs + b] + v;
+        }
+    }
+    const double nd = g * map[MF_ND * Bs + b] + N;
+    const double np = g * map[MF_NP * Bs + b] + N;
+    map[MF_ND * Bs + b] = nd;
+    map[MF_NP * Bs + b] = np;
+    double sp[3];
 #pragma unroll
-    for (int k = 0; k < MF_COUNT; ++k) map[k * Bs + b] = nm[k];
-    // derived stats (bin_atlas.py:166-200)
-    double sn = sqrt(dot3_exact(nm[0], nm[1], nm[2], nm[0], nm[1], nm[2]));
-    double dn = sn + kEpsMass;
-    derived[(MD_MU + 0) * Bs + b] = nm[0] / dn;
-    derived[(MD_MU + 1) * Bs + b] = nm[1] / dn;
-    derived[(MD_MU + 2) * Bs + b] = nm[2] / dn;
-    double invNd = 1.0 / (nm[MF_ND] + kEpsMass + kF64Eps);
-    derived[MD_KAPPA * Bs + b] = kappa_from_rbar(sn * invNd);
-    double invNp = 1.0 / (nm[MF_NP] + kEpsMass + kF64Eps);
-    double c[3] = {nm[MF_SP] * invNp, nm[MF_SP + 1] * invNp, nm[MF_SP + 2] * invNp};
-    double raw[9], sig[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) raw[3 * i + j] = nm[MF_SPP + 3 * i + j] * invNp - c[i] * c[j];
-    psd_project3(raw, sig);
+    for (int k = 0; k < 3; ++k) {
+      sp[k] = g * map[(MF_SP + k) * Bs + b] + N * q[k];
+      map[(MF_SP + k) * Bs + b] = sp[k];
+    }
+    // sum_ppT += N [ R (Sigma_p + p p^T) R^T + J S J^T + q q^T - u u^T ]
+    double spp[9];
+    {
+      double M2[9], RM[9];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) derived[(MD_C + k) * Bs + b] = c[k];
+      for (int i = 0; i < 3; ++i)
 #pragma unroll
-    for (int k = 0; k < 9; ++k) derived[(MD_SIG + k) * Bs + b] = sig[k];
+        for (int j = 0; j < 3; ++j) M2[3 * i + j] = scan[(SF_SIG + 3 * i + j) * Bs + b] + pb[i] * pb[j];
+      mat3_mul(R, M2, RM);
+      double X[9], XF[9], XG[9];
+      skew3(u, X);
+      mat3_mul(X, pa.F, XF);
+      mat3_mul(X, pa.G, XG);
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          double rmr = RM[3 * i] * R[3 * j] + RM[3 * i + 1] * R[3 * j + 1] + RM[3 * i + 2] * R[3 * j + 2];
+          double xgx = XG[3 * i] * X[3 * j] + XG[3 * i + 1] * X[3 * j + 1] + XG[3 * i + 2] * X[3 * j + 2];
+          double jsj = pa.Stt[3 * i + j] - XF[3 * i + j] - XF[3 * j + i] + xgx;
+          spp[3 * i + j] = g * map[(MF_SPP + 3 * i + j) * Bs + b] + N * (rmr + jsj + q[i] * q[j] - u[i] * u[j]);
+          map[(MF_SPP + 3 * i + j) * Bs + b] = spp[3 * i + j];
+        }
+    }
+    derive_bin(sd, nd, np, sp, spp, derived, Bs, b);
   }
 }
 
 // derived stats from map sufficient stats only (used after set_map / reset)
 __global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict__ map, double* derived, int B) {
-  PushArgs pa;
-  (void)pa;
-  size_t Bs = (size_t)B;
+  const size_t Bs = (size_t)B;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
-    double nm[MF_COUNT];
-    for (int k = 0; k < MF_COUNT; ++k) nm[k] = map[k * Bs + b];
-    double sn = sqrt(dot3_exact(nm[0], nm[1], nm[2], nm[0], nm[1], nm[2]));
-    double dn = sn + kEpsMass;
-    for (int k = 0; k < 3; ++k) derived[(MD_MU + k) * Bs + b] = nm[k] / dn;
-    double invNd = 1.0 / (nm[MF_ND] + kEpsMass + kF64Eps);
-    derived[MD_KAPPA * Bs + b] = kappa_from_rbar(sn * invNd);
-    double invNp = 1.0 / (nm[MF_NP] + kEpsMass + kF64Eps);
-    double c[3] = {nm[MF_SP] * invNp, nm[MF_SP + 1] * invNp, nm[MF_SP + 2] * invNp};
-    double raw[9], sig[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) raw[3 * i + j] = nm[MF_SPP + 3 * i + j] * invNp - c[i] * c[j];
-    psd_project3(raw, sig);
-    for (int k = 0; k < 3; ++k) derived[(MD_C + k) * Bs + b] = c[k];
-    for (int k = 0; k < 9; ++k) derived[(MD_SIG + k) * Bs + b] = sig[k];
+    double sd[3], sp[3], spp[9];
+    for (int k = 0; k < 3; ++k) { sd[k] = map[(MF_SD + k) * Bs + b]; sp[k] = map[(MF_SP + k) * Bs + b]; }
+    for (int k = 0; k < 9; ++k) spp[k] = map[(MF_SPP + k) * Bs + b];
+    derive_bin(sd, map[MF_ND * Bs + b], map[MF_NP * Bs + b], sp, spp, derived, Bs, b);
   }
 }
 
@@ -741,44 +871,47 @@ static int grid_for(long n, int cap_blocks) {
 hipError_t launch_budget(const double* w, int n_raw, int stride, double* partials, int nblk, double* scalars,
                          hipStream_t s) {
   hipLaunchKernelGGL(k_budget_partial, dim3(nblk), dim3(kBlock), 0, s, w, n_raw, stride, partials);
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_partials_final<2, 0u>), dim3(1), dim3(kBlock), 0, s, (const double*)partials, nblk,
-                     scalars, (int)SC_MASS_IN);
-  hipLaunchKernelGGL(k_budget_scale, dim3(1), dim3(1), 0, s, scalars);
+  hipLaunchKernelGGL(k_budget_final, dim3(1), dim3(kBlock), 0, s, (const double*)partials, nblk, scalars);
   return hipGetLastError();
 }
 
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, hipStream_t s) {
-  if (scale)
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<true>), dim3(nblk), dim3(kBlock), 0, s, a, partials);
-  else
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<false>), dim3(nblk), dim3(kBlock), 0, s, a, partials);
+  if (scale) {
+    switch (a.k) {
+      case 8: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<true, 8>), dim3(nblk), dim3(kBlock), 0, s, a, partials); break;
+      case 16: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<true, 16>), dim3(nblk), dim3(kBlock), 0, s, a, partials); break;
+      case 32: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<true, 32>), dim3(nblk), dim3(kBlock), 0, s, a, partials); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<false, 1>), dim3(nblk), dim3(kBlock), 0, s, a, partials);
+  }
   // per-point cert partials -> scalars[SC_DESKEW_WIN..]: (sum wb, sum wn^2, sum wout, sum H, max r)
   hipLaunchKernelGGL(HIP_KERNEL_NAME(k_partials_final<5, 16u>), dim3(1), dim3(kBlock), 0, s, (const double*)partials,
                      nblk, a.scalars, (int)SC_DESKEW_WIN);
   return hipGetLastError();
 }
 
-size_t sort_temp_bytes(int n) {
-  size_t bytes = 0;
-  (void)rocprim::radix_sort_pairs((void*)nullptr, bytes, (uint32_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                            (uint32_t*)nullptr, (size_t)n, 0, 32);
-  return bytes;
-}
-
-hipError_t launch_sort(void* temp, size_t temp_bytes, uint32_t* keys_in, uint32_t* keys_out, uint32_t* vals_in,
-                       uint32_t* vals_out, int n, int end_bit, hipStream_t s) {
-  size_t tb = temp_bytes;
-  return rocprim::radix_sort_pairs(temp, tb, keys_in, keys_out, vals_in, vals_out, (size_t)n, 0, end_bit, s);
-}
-
-hipError_t launch_bucket_mark(const uint32_t* keys, int n, int n_bins, const int* knn, int k, int2* ranges,
-                              uint8_t* flags, hipStream_t s) {
-  hipLaunchKernelGGL(k_bucket_mark, dim3(grid_for(n, 2048)), dim3(kBlock), 0, s, keys, n, n_bins, knn, k, ranges, flags);
+hipError_t launch_bucketing(uint32_t* counts, uint32_t* starts, uint32_t* tile_sums, const uint32_t* keys,
+                            const uint32_t* slots, int n, int n_bins, uint32_t* sorted, uint32_t* big_list,
+                            uint32_t* big_n, hipStream_t s) {
+  int tiles = (n_bins + kScanTile - 1) / kScanTile;
+  hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(kBlock), 0, s, (const uint32_t*)counts, n_bins, tile_sums);
+  hipLaunchKernelGGL(k_scan_apply, dim3(tiles), dim3(kBlock), 0, s, (const uint32_t*)counts, n_bins,
+                     (const uint32_t*)tile_sums, starts);
+  hipLaunchKernelGGL(k_place, dim3(grid_for(n, 2048)), dim3(kBlock), 0, s, keys, slots, (const uint32_t*)starts, n,
+                     n_bins, sorted);
+  hipLaunchKernelGGL(k_bucket_order, dim3(grid_for(n_bins, 2048)), dim3(kBlock), 0, s, (const uint32_t*)counts,
+                     (const uint32_t*)starts, n_bins, sorted, big_list, big_n);
+  hipLaunchKernelGGL(k_bucket_big, dim3(64), dim3(kBlock), 0, s, keys, n, (const uint32_t*)starts,
+                     (const uint32_t*)big_list, (const uint32_t*)big_n, sorted);
   return hipGetLastError();
 }
 
+int bins_scale_blocks(int n_bins) { return (n_bins + kTile - 1) / kTile; }
+
 hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s) {
-  int nblk = (a.n_bins + kBlock - 1) / kBlock;
+  int nblk = bins_scale_blocks(a.n_bins);
   hipLaunchKernelGGL(k_bins_scale, dim3(nblk), dim3(kBlock), 0, s, a, partials);
   return hipGetLastError();
 }

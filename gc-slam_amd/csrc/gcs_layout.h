@@ -38,10 +38,12 @@ enum MapDerived : int {
 
 // Per-point record written by the point kernel, gathered by the bin kernels (48 B).
 struct PointRec {
-  double x, y, z;  // deskewed point (scan-start base frame)
-  double w;        // weight after budget mass rescale and deskew time window
-  double m;        // max candidate similarity (softmax shift)
-  double iz;       // 1 / sum_k exp((s_k - m) / tau)
+  double x, y, z;     // deskewed point (scan-start base frame)
+  double dx, dy, dz;  // ray direction from the LiDAR origin (pipeline.py:589-593)
+  double w;           // weight after budget mass rescale and deskew time window
+  double m;           // max candidate similarity (softmax shift)
+  double iz;          // 1 / sum_k exp((s_k - m) / tau)
+  double pad;
 };
 
 // Scalar results slots (device buffer of doubles, copied to host once per scan).

@@ -231,6 +231,23 @@ GCS_HD double psd_project3(const double* M, double* out) {
     for (int i = 0; i < 9; ++i) out[i] = (i % 4 == 0) ? kEpsPsd : 0.0;
     return 1.7320508075688772e-12;
   }
+  // Fast path: if M_sym - eps I is positive definite no eigenvalue is clamped, so the exact
+  // projection is M_sym itself with delta 0 (the eigh rebuild differs only by rounding).
+  {
+    double a00 = s[0] - kEpsPsd;
+    if (a00 > 0.0) {
+      double l00 = sqrt(a00), l10 = s[3] / l00, l20 = s[6] / l00;
+      double a11 = s[4] - kEpsPsd - l10 * l10;
+      if (a11 > 0.0) {
+        double l11 = sqrt(a11), l21 = (s[7] - l20 * l10) / l11;
+        double a22 = s[8] - kEpsPsd - l20 * l20 - l21 * l21;
+        if (a22 > 0.0) {
+          for (int i = 0; i < 9; ++i) out[i] = s[i];
+          return 0.0;
+        }
+      }
+    }
+  }
   double w[3], V[9];
   eigh3_jacobi(s, w, V);
   for (int k = 0; k < 3; ++k) w[k] = w[k] > kEpsPsd ? w[k] : kEpsPsd;
