@@ -117,18 +117,24 @@ def main():
     torch.cuda.synchronize()
 
     state = dict(count=0)
+    host_ms = np.zeros(5)  # pre-device host, device submit+wait, host tail, whole gcs_scan, combine
 
     def step():
         sc, rec, t, w = scans[state["count"] % N_SCANS]
-        ctx.scan(rec, 16, t, w, N, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
-                 sc["scan_end_time"], sc["dt_sec"])
-        combine_allreduce(ctx, rank, world, state["count"], device=device)
+        out = ctx.scan(rec, 16, t, w, N, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
+                       sc["scan_end_time"], sc["dt_sec"])
+        tc = time.perf_counter()
+        combine_allreduce(ctx, rank, world, state["count"], device=device, want_belief=False)
+        host_ms[4] += (time.perf_counter() - tc) * 1e3
+        host_ms[:4] += np.asarray(out.stage_ms[:4])
         state["count"] += 1
 
     for _ in range(args.warmup):
         step()
-    ctx.enable_timing(True)
+    # timed region: only the roofline kernel carries event stamps (each timed stage costs queue time)
+    ctx.enable_timing(True, stages=["bins"])
     ctx.stage_times(reset=True)
+    host_ms[:] = 0.0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -144,13 +150,20 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    ms_sum, counts = ctx.stage_times()
+    ms_sum, counts = ctx.stage_times(reset=True)
+    bins_ms = float(ms_sum[2] / counts[2]) if counts[2] else None
+    host_avg = dict(zip(["pre_device", "device_wait", "tail", "gcs_scan", "combine"], (host_ms / args.steps).tolist()))
+    # diagnostic pass after the timed region: every device stage stamped (not part of `value`)
+    ctx.enable_timing(True)
+    for _ in range(min(args.steps, 20)):
+        step()
+    ctx.synchronize()
+    ms_sum, counts = ctx.stage_times(reset=True)
     stage_avg = {name: (float(ms_sum[i] / counts[i]) if counts[i] else None)
-                 for i, name in enumerate(["points", "sort_bucket", "bins", "matrix_fisher", "planar", "pushforward"])}
+                 for i, name in enumerate(ctx.STAGES)}
 
     if rank == 0:
         value = world * args.steps / elapsed
-        bins_ms = stage_avg["bins"]
         ach = bins_kernel_bytes(N, B) / (bins_ms * 1e-3) / 1e9 if bins_ms else None
         traffic = None
         pmc_path = os.path.join(ROOT, "profiles", f"pmc_bins_{args.config}.json")
@@ -171,6 +184,7 @@ def main():
                          "kernel": "k_bins_scale (BinSoftAssign+ScanBinMomentMatch+kappa)",
                          "algorithmic_bytes_per_launch": bins_kernel_bytes(N, B)},
             "stage_ms": stage_avg,
+            "host_ms": host_avg,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(cfg)

@@ -41,11 +41,15 @@ struct gcs_ctx {
   std::vector<int> knn_host;
   // per-point
   PointRec* d_recs = nullptr;
+  PointRec* d_recs_s = nullptr;  // bucket order (scale mode)
   uint32_t *d_keys = nullptr, *d_slots = nullptr, *d_sorted = nullptr;
   int* d_nearest = nullptr;
   // per-bin bucketing
-  uint32_t *d_counts = nullptr /*B+1: last = big bucket count*/, *d_starts = nullptr, *d_tile_sums = nullptr,
-           *d_big_list = nullptr;
+  // d_counts holds B counts, [B] = mid-list length, [B+1] pad, then one look-back word per
+  // 4096-bucket tile: the whole range is cleared by k_budget every scan
+  uint32_t *d_counts = nullptr, *d_starts = nullptr, *d_mid_list = nullptr;
+  int n_counts_words = 0;
+  uint32_t* d_tickets = nullptr;
   uint8_t* d_flags = nullptr;
   double* d_scan = nullptr;
   double* d_map = nullptr;
@@ -62,8 +66,10 @@ struct gcs_ctx {
   double last_dPsi[7 * 36], last_dnu[7];
   bool have_last = false;
   int last_n_sel = 0, last_stride = 1;
+  std::vector<double> wimu;  // IMU window weights (scratch)
   // device stage timing (hipEvents on the context stream; harvested lazily)
-  bool timing = false, pending = false;
+  uint32_t timing_mask = 0;
+  bool pending = false;
   hipEvent_t ev[kStages][2] = {};
   bool ev_rec[kStages] = {};
   double stage_ms_sum[kStages] = {};
@@ -83,7 +89,7 @@ int fail(gcs_ctx* c, int code, const std::string& m) {
     if (_e != hipSuccess) return fail((ctx), GCS_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
   } while (0)
 
-constexpr int kRedBlocks = 512;
+constexpr int kRedBlocks = 1024;
 int red_blocks(long n) { return (int)std::max(1L, std::min((long)kRedBlocks, (n + 255) / 256)); }
 
 void harvest(gcs_ctx* c) {
@@ -101,20 +107,24 @@ void harvest(gcs_ctx* c) {
   c->pending = false;
 }
 
-struct StageTimer {
-  gcs_ctx* c;
-  int st;
-  StageTimer(gcs_ctx* cc, int s) : c(cc), st(s) {
-    if (c->timing) (void)hipEventRecord(c->ev[st][0], c->stream);
-  }
-  ~StageTimer() {
-    if (c->timing) {
-      (void)hipEventRecord(c->ev[st][1], c->stream);
-      c->ev_rec[st] = true;
-      c->pending = true;
-    }
-  }
+// Stage events are stamped by the stage's own kernel dispatches (hipExtLaunchKernel), so timing
+// adds no marker packets (a hipEventRecord marker costs ~10 us of queue time per record).
+struct StageEv {
+  hipEvent_t e0 = nullptr, e1 = nullptr;
 };
+StageEv stage_ev(gcs_ctx* c, int st) {
+  StageEv e;
+  if ((c->timing_mask >> st) & 1u) {
+    e.e0 = c->ev[st][0];
+    e.e1 = c->ev[st][1];
+    c->ev_rec[st] = true;
+    c->pending = true;
+  }
+  return e;
+}
+uint32_t* ticket(gcs_ctx* c, int tk) { return c->d_tickets + (size_t)tk * kTicketStride; }
+// partials: nblocks*NV plus the group partials (nblocks/64 + 1)*NV
+size_t partials_need(long nblocks, int nv) { return (size_t)(nblocks + nblocks / 64 + 2) * nv; }
 
 void to_host_belief(const gcs_belief& in, Belief& b) {
   memcpy(b.X_anchor, in.X_anchor, sizeof(b.X_anchor));
@@ -167,12 +177,19 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   c->last_stride = stride;
   hipStream_t s = c->stream;
   harvest(c);
-  StageTimer timer(c, ST_POINTS);
-  if (n_raw > 0) {
-    HIPCHK(c, launch_budget(w, n_raw, stride, c->d_partials, red_blocks(n_raw), c->d_scalars, s));
-  } else {
-    HIPCHK(c, hipMemsetAsync(c->d_scalars, 0, 3 * sizeof(double), s));
-  }
+  StageEv ev = stage_ev(c, ST_POINTS);
+  BudgetArgs ba{};
+  ba.w = w;
+  ba.n_raw = n_raw;
+  ba.stride = stride;
+  ba.partials = c->d_partials;
+  ba.scalars = c->d_scalars;
+  ba.ticket = ticket(c, TK_BUDGET);
+  ba.zero32 = c->d_counts;  // counts only: the bucketing scratch after them is re-armed by k_bins_scale
+  ba.n_zero32 = c->d_counts ? c->B : 0;
+  ba.zero8 = c->d_flags;
+  ba.n_zero8 = c->d_flags ? c->B : 0;
+  HIPCHK(c, launch_budget(ba, red_blocks(std::max(n_raw, 1)), s, ev.e0, nullptr));
   PointKernelArgs a{};
   a.xyz = (const uint8_t*)xyz;
   a.point_step = point_step;
@@ -198,67 +215,86 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.keys = c->d_keys;
   a.slots = c->d_slots;
   a.counts = c->d_counts;
-  a.flags = c->d_flags;
   a.scalars = c->d_scalars;
+  a.ticket = ticket(c, TK_POINTS);
   a.p0_out = p0_out;
   a.w_out = w_out;
   a.w_budget_out = wb_out;
   a.nearest_out = c->d_nearest;
-  if (c->cfg.mode == GCS_MODE_SCALE) {
-    HIPCHK(c, hipMemsetAsync(c->d_counts, 0, ((size_t)c->B + 1) * sizeof(uint32_t), s));
-    HIPCHK(c, hipMemsetAsync(c->d_flags, 0, (size_t)c->B, s));
-  }
-  HIPCHK(c, launch_points(a, c->cfg.mode == GCS_MODE_SCALE, c->d_partials, red_blocks(c->cap), s));
+  HIPCHK(c, launch_points(a, c->cfg.mode == GCS_MODE_SCALE, c->d_partials, red_blocks(c->cap), s, nullptr, ev.e1));
   return GCS_OK;
 }
 
 BinKernelArgs bin_args(gcs_ctx* c) {
   BinKernelArgs b{};
   b.recs = c->d_recs;
-  b.sorted_vals = c->d_sorted;
+  b.recs_s = c->d_recs_s;
   b.starts = c->d_starts;
   b.counts = c->d_counts;
   b.flags = c->d_flags;
   b.rknn_off = c->d_rknn_off;
   b.rknn = c->d_rknn;
   b.bin_dirs = c->d_bin_dirs;
+  b.map = c->d_map;
   b.n_bins = c->B;
   b.cap = c->cap;
   memcpy(b.origin, c->cfg.lidar_origin, 3 * sizeof(double));
   b.tau = c->cfg.tau;
   b.scan = c->d_scan;
+  b.scalars = c->d_scalars;
+  b.ticket = ticket(c, c->cfg.mode == GCS_MODE_SCALE ? TK_BINS : TK_DENSE);
+  if (c->d_counts) {
+    b.zero_after = c->d_counts + c->B;
+    b.n_zero_after = c->n_counts_words - c->B;
+  }
   return b;
 }
 
 int stage_bins(gcs_ctx* c) {
   hipStream_t s = c->stream;
   BinKernelArgs b = bin_args(c);
-  int nblk = c->cfg.mode == GCS_MODE_SCALE ? bins_scale_blocks(c->B) : (c->B + 255) / 256;
   if (c->cfg.mode == GCS_MODE_SCALE) {
     {
-      StageTimer timer(c, ST_SORT);
-      HIPCHK(c, launch_bucketing(c->d_counts, c->d_starts, c->d_tile_sums, c->d_keys, c->d_slots, c->cap, c->B,
-                                 c->d_sorted, c->d_big_list, c->d_counts + c->B, s));
+      StageEv ev = stage_ev(c, ST_SORT);
+      BucketArgs ba{};
+      ba.n_bins = c->B;
+      ba.k = c->K;
+      ba.counts = c->d_counts;
+      ba.keys = c->d_keys;
+      ba.slots = c->d_slots;
+      ba.knn = c->d_knn;
+      ba.recs = c->d_recs;
+      ba.starts = c->d_starts;
+      ba.scan_status = c->d_counts + c->B + 2;
+      ba.scan_ticket = ticket(c, TK_SCAN);
+      ba.slot_idx = c->d_sorted;
+      ba.dest = c->d_slots;  // slots are consumed by k_place before k_bucket_rank writes destinations
+      ba.recs_s = c->d_recs_s;
+      ba.flags = c->d_flags;
+      ba.mid_list = c->d_mid_list;
+      ba.mid_n = c->d_counts + c->B;
+      HIPCHK(c, launch_bucketing(ba, c->cap, s, ev.e0, ev.e1));
     }
-    StageTimer timer(c, ST_BINS);
-    HIPCHK(c, launch_bins_scale(b, c->d_partials, s));
+    StageEv ev = stage_ev(c, ST_BINS);
+    HIPCHK(c, launch_bins_scale(b, c->d_partials, s, ev.e0, ev.e1));
   } else {
-    StageTimer timer(c, ST_BINS);
-    HIPCHK(c, launch_dense(b, c->d_bin_partials, c->d_partials, s));
+    StageEv ev = stage_ev(c, ST_BINS);
+    HIPCHK(c, launch_dense(b, c->d_bin_partials, c->d_partials, s, ev.e0, ev.e1));
   }
-  HIPCHK(c, launch_bin_cert_final(c->d_partials, nblk, c->d_scalars, s));
   return GCS_OK;
 }
 
 int stage_mf(gcs_ctx* c) {
-  StageTimer timer(c, ST_MF);
-  HIPCHK(c, launch_mf(c->d_scan, c->d_map, c->B, c->d_partials, red_blocks(c->B), c->d_scalars, c->stream));
+  StageEv ev = stage_ev(c, ST_MF);
+  HIPCHK(c, launch_mf(c->d_scan, c->d_map, c->B, c->d_partials, red_blocks(c->B), c->d_scalars, ticket(c, TK_MF),
+                      c->stream, ev.e0, ev.e1));
   return GCS_OK;
 }
 
 int stage_pt(gcs_ctx* c) {
-  StageTimer timer(c, ST_PT);
-  HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars, c->stream));
+  StageEv ev = stage_ev(c, ST_PT);
+  HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
+                      ticket(c, TK_PT), c->stream, ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -280,8 +316,9 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) 
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) pa.G[3 * i + j] = RS[3 * i] * pa.R[3 * j] + RS[3 * i + 1] * pa.R[3 * j + 1] + RS[3 * i + 2] * pa.R[3 * j + 2];
   pa.gamma = gamma;
-  StageTimer timer(c, ST_PUSH);
-  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->stream));
+  StageEv ev = stage_ev(c, ST_PUSH);
+  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->d_partials, c->d_scalars,
+                               ticket(c, TK_PUSH), c->stream, ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -334,10 +371,13 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_derived, B * MD_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_map, 0, B * MF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scan, 0, B * SF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
-  c->partials_len = std::max<size_t>((size_t)kRedBlocks * 24, ((B + 63) / 64) * 5 + 64);
+  c->partials_len = std::max<size_t>({partials_need(kRedBlocks, 24), partials_need(bins_scale_blocks(c->B), bins_partial_nv()),
+                                      partials_need(push_blocks(c->B), 10)});
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_tickets, (size_t)TK_COUNT * kTicketStride * sizeof(uint32_t)))) return GCS_ERR_HIP;
+  if (bad(hipMemset(c->d_tickets, 0, (size_t)TK_COUNT * kTicketStride * sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocDefault))) return GCS_ERR_HIP;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
@@ -346,10 +386,12 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMalloc(&c->d_keys, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_slots, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_sorted, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_counts, (B + 1) * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    c->n_counts_words = (int)B + 2 + scan_tiles(c->B);
+    if (bad(hipMalloc(&c->d_counts, (size_t)c->n_counts_words * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMemset(c->d_counts, 0, (size_t)c->n_counts_words * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_starts, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_tile_sums, (B / 4096 + 2) * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_big_list, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_mid_list, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_recs_s, cap * sizeof(PointRec)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_flags, B))) return GCS_ERR_HIP;
   } else {
     size_t nchunks = (cap + 255) / 256;
@@ -361,7 +403,9 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     gcs_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
-  if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->stream))) return GCS_ERR_HIP;
+  if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, ticket(c, TK_PUSH),
+                            c->stream)))
+    return GCS_ERR_HIP;
   if (bad(hipStreamSynchronize(c->stream))) return GCS_ERR_HIP;
   // identity prior (belief.py:320-358) and datasheet IW state
   memset(&c->belief, 0, sizeof(Belief));
@@ -375,7 +419,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
 int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
   void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
-                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_tile_sums, c->d_big_list, c->d_flags,
+                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_mid_list, c->d_flags, c->d_recs_s, c->d_tickets,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -402,12 +446,12 @@ int gcs_ctx_synchronize(gcs_ctx* c) {
   return GCS_OK;
 }
 
-int gcs_ctx_enable_timing(gcs_ctx* c, int32_t on) {
+int gcs_ctx_enable_timing(gcs_ctx* c, int32_t stage_mask) {
   if (!c) return GCS_ERR_ARG;
-  if (on && !c->ev[0][0])
+  if (stage_mask && !c->ev[0][0])
     for (int st = 0; st < kStages; ++st)
       for (int k = 0; k < 2; ++k) HIPCHK(c, hipEventCreate(&c->ev[st][k]));
-  c->timing = on != 0;
+  c->timing_mask = (uint32_t)stage_mask;
   return GCS_OK;
 }
 
@@ -450,7 +494,8 @@ int gcs_ctx_get_belief(gcs_ctx* c, gcs_belief* b) {
 int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
   if (!c || !map) return GCS_ERR_ARG;
   HIPCHK(c, hipMemcpyAsync(c->d_map, map, (size_t)c->B * MF_COUNT * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, launch_map_derive(c->d_map, c->d_derived, c->B, c->stream));
+  HIPCHK(c, launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, ticket(c, TK_PUSH),
+                              c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
 }
@@ -610,21 +655,25 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   double Tsum = 0.0;
   // 2 PredictDiffusion
   Belief prev = c->belief, pred;
-  double pinfl[3];
-  host::predict_diffusion(prev, Q, in->dt_sec, pred, pinfl);
+  double pinfl[3], mu_prev[DZ];
+  host::predict_diffusion(prev, Q, in->dt_sec, pred, pinfl, mu_prev);
   cert[6] = pinfl[0]; cert[7] = pinfl[1]; cert[8] = pinfl[2];
   Tsum += trig(pinfl[0], pinfl[1], 0, 0, 0, pinfl[2], 1, 1, 1);
   // 3 IMU membership window + preintegration -> deskew twist (pipeline.py:432-483)
-  std::vector<double> covp(DZ * DZ);
-  host::spd_inverse_lifted(DZ, pred.L, kEpsLift, covp.data());
-  double sigma_warp = std::max(sqrt(covp[15 * DZ + 15]), 0.01);
+  host::SpdFactor fpred;  // one factor of the predicted information for every solve below
+  host::spd_factor_lifted(DZ, pred.L, kEpsLift, fpred);
+  double e15[DZ] = {}, col15[DZ];
+  e15[15] = 1.0;
+  host::spd_factor_solve(fpred, e15, col15);  // column 15 of the predicted covariance
+  double sigma_warp = std::max(sqrt(col15[15]), 0.01);
   cert[38] = sigma_warp;
-  std::vector<double> wimu(in->imu_len);
+  std::vector<double>& wimu = c->wimu;
+  wimu.resize(in->imu_len);
   for (int i = 0; i < in->imu_len; ++i)
     wimu[i] = smooth_window(in->imu_stamps[i], in->scan_start_time, in->scan_end_time, sigma_warp);
   double mu_inc[DZ], pose0[6];
-  host::mean_increment(pred, mu_inc);
-  host::mean_world_pose(prev, pose0);
+  host::spd_factor_solve(fpred, pred.h, mu_inc);
+  host::world_pose_from_increment(prev, mu_prev, pose0);
   host::PreintOut pre;
   host::preintegrate_imu(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wimu.data(), pose0 + 3, mu_inc + 9,
                          mu_inc + 12, c->cfg.gravity_W, pre);
@@ -637,8 +686,8 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
                         in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr);
   if (rc) return rc;
-  if ((rc = stage_bins(c))) return rc;
-  if ((rc = stage_mf(c))) return rc;
+  if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
+  if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
   if ((rc = stage_pt(c))) return rc;
   if ((rc = pull_scalars(c))) return rc;
   auto T2 = clk::now();
@@ -671,7 +720,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   Tsum += S[SC_BIN_PSD] + S[SC_BIN_EPSR];
   // 7 MatrixFisherRotation tail (matrix_fisher_evidence.py:240-256,310-394)
   double pose_pred[6], R_pred[9];
-  host::mean_world_pose(pred, pose_pred);
+  host::world_pose_from_increment(pred, mu_inc, pose_pred);
   so3_exp(pose_pred + 3, R_pred);
   const double* sv = S + SC_MF_S;
   const double* V = S + SC_MF_V;
@@ -789,7 +838,9 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   double fs = Tsum / (Tsum + 1.0);
   cert[36] = fs;
   double dz[DZ], corr[6], dpc[6], e6[6];
-  host::mean_increment(post, dz);
+  host::SpdFactor fpost;  // recompose keeps L: one factor serves post, rec and the anchor drift
+  host::spd_factor_lifted(DZ, post.L, kEpsLift, fpost);
+  host::spd_factor_solve(fpost, post.h, dz);
   host::bch3(post.z_lin, dz, corr);
   for (int i = 0; i < 6; ++i) dpc[i] = dz[i] + fs * corr[i];
   Belief rec = post;
@@ -801,20 +852,22 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     for (int j = 0; j < 6; ++j) s += post.L[i * DZ + j] * dpc[j];
     rec.h[i] = post.h[i] - s;
   }
-  host::process_iw_suffstats(pred.L, pred.h, rec.L, rec.h, out->iw_process_dPsi, out->iw_process_dnu);
+  double mu_pred_x[DZ], mu_rec[DZ], covr[DZ * DZ];
+  host::spd_solve_lifted(DZ, pred.L, pred.h, kEpsLift, mu_pred_x);  // pred after excitation scaling
+  host::spd_factor_solve(fpost, rec.h, mu_rec);
+  host::spd_factor_inverse(fpost, covr);
+  host::process_iw_suffstats_from(mu_pred_x, mu_rec, covr, out->iw_process_dPsi, out->iw_process_dnu);
   memcpy(c->last_dPsi, out->iw_process_dPsi, sizeof(c->last_dPsi));
   memcpy(c->last_dnu, out->iw_process_dnu, sizeof(c->last_dnu));
   // 13 PoseCovInflationPushforward with z_t (pipeline.py:1244-1246)
-  double z_t[6], covr[DZ * DZ], Sig6[36];
-  host::mean_world_pose(rec, z_t);
-  host::spd_inverse_lifted(DZ, rec.L, kEpsLift, covr);
+  double z_t[6], Sig6[36];
+  host::world_pose_from_increment(rec, mu_rec, z_t);
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j < 6; ++j) Sig6[6 * i + j] = covr[i * DZ + j];
   if ((rc = stage_push(c, z_t, Sig6, c->cfg.forgetting_factor))) return rc;
   memcpy(out->z_t, z_t, sizeof(out->z_t));
   // 14 AnchorDriftUpdate (anchor_drift.py:93-191)
-  double dz2[DZ];
-  host::mean_increment(rec, dz2);
+  const double* dz2 = mu_rec;  // mean_increment(rec)
   double dm = sqrt(dz2[0] * dz2[0] + dz2[1] * dz2[1] + dz2[2] * dz2[2]);
   double dr = sqrt(dz2[3] * dz2[3] + dz2[4] * dz2[4] + dz2[5] * dz2[5]);
   double rho = std::min(std::max(std::max(dm / 0.5, dr / 0.2), 0.0), 1.0);

@@ -12,7 +12,8 @@ namespace gcs {
 namespace host {
 
 void jacobi_eigh(int n, const double* A, double* w, double* V) {
-  std::vector<double> a(A, A + n * n);
+  double a[kMaxN * kMaxN];
+  for (int i = 0; i < n * n; ++i) a[i] = A[i];
   for (int i = 0; i < n * n; ++i) V[i] = 0.0;
   for (int i = 0; i < n; ++i) V[i * n + i] = 1.0;
   double fro = 0.0;
@@ -58,7 +59,7 @@ void jacobi_eigh(int n, const double* A, double* w, double* V) {
 
 // domain_projection_psd_core, FS/common/primitives.py:80-123
 double psd_project(int n, const double* M, double eps_psd, double* out, double* cert6) {
-  std::vector<double> s(n * n), w(n), V(n * n);
+  double s[kMaxN * kMaxN];
   double sym2 = 0.0;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) {
@@ -67,21 +68,47 @@ double psd_project(int n, const double* M, double eps_psd, double* out, double* 
       sym2 += d * d;
     }
   if (!cert6) {
-    // fast path (see gcs_math.h psd_project3): M_sym - eps I positive definite -> no clamping
-    std::vector<double> A(s), Lc(n * n);
+    // Fast paths (declared, DESIGN.md "PSD fast path"); the certificate form always runs eigh.
+    // (a) exactly-zero rows/columns split off: eigh of [A 0; 0 0] is eigh(A) plus exact zero
+    //     eigenvalues, each clamped to eps_psd on the diagonal (IW padded blocks, masked evidence).
+    int act[kMaxN], na = 0;
+    for (int i = 0; i < n; ++i) {
+      bool z = true;
+      for (int j = 0; j < n && z; ++j) z = s[i * n + j] == 0.0;
+      if (!z) act[na++] = i;
+    }
+    if (na < n) {
+      for (int i = 0; i < n * n; ++i) out[i] = 0.0;
+      for (int i = 0; i < n; ++i) out[i * n + i] = eps_psd;
+      double d2 = (double)(n - na) * eps_psd * eps_psd;
+      if (na > 0) {
+        double sub[kMaxN * kMaxN], so[kMaxN * kMaxN];
+        for (int i = 0; i < na; ++i)
+          for (int j = 0; j < na; ++j) sub[i * na + j] = s[act[i] * n + act[j]];
+        double da = psd_project(na, sub, eps_psd, so, nullptr);
+        for (int i = 0; i < na; ++i)
+          for (int j = 0; j < na; ++j) out[act[i] * n + act[j]] = so[i * na + j];
+        d2 += da * da;
+      }
+      return sqrt(d2);
+    }
+    // (b) M_sym - eps I positive definite -> no eigenvalue is clamped: return M_sym, delta 0
+    double A[kMaxN * kMaxN], Lc[kMaxN * kMaxN];
+    for (int i = 0; i < n * n; ++i) A[i] = s[i];
     for (int i = 0; i < n; ++i) A[i * n + i] -= eps_psd;
-    if (cholesky(n, A.data(), Lc.data())) {
+    if (cholesky(n, A, Lc)) {
       for (int i = 0; i < n * n; ++i) out[i] = s[i];
       return 0.0;
     }
   }
+  double w[kMaxN], V[kMaxN * kMaxN];
   bool zero = true;
   for (int i = 0; i < n * n; ++i) zero = zero && s[i] == 0.0;
   if (zero) {
     for (int i = 0; i < n * n; ++i) V[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
     for (int i = 0; i < n; ++i) w[i] = 0.0;
   } else {
-    jacobi_eigh(n, s.data(), w.data(), V.data());
+    jacobi_eigh(n, s, w, V);
   }
   double emin = INFINITY, emax = -INFINITY, nn = 0.0;
   for (int k = 0; k < n; ++k) {
@@ -123,11 +150,19 @@ bool cholesky(int n, const double* A, double* Lc) {
   return true;
 }
 
-// spd_cholesky_solve_lifted_core, primitives.py:141-166
-void spd_solve_lifted(int n, const double* L, const double* b, double eps_lift, double* x) {
-  std::vector<double> A(L, L + n * n), Lc(n * n), y(n);
+// spd_cholesky_solve_lifted_core / spd_cholesky_inverse_lifted_core, primitives.py:141-192
+void spd_factor_lifted(int n, const double* L, double eps_lift, SpdFactor& f) {
+  double A[kMaxN * kMaxN];
+  for (int i = 0; i < n * n; ++i) A[i] = L[i];
   for (int i = 0; i < n; ++i) A[i * n + i] += eps_lift;
-  cholesky(n, A.data(), Lc.data());
+  f.n = n;
+  cholesky(n, A, f.Lc);
+}
+
+void spd_factor_solve(const SpdFactor& f, const double* b, double* x) {
+  const int n = f.n;
+  const double* Lc = f.Lc;
+  double y[kMaxN];
   for (int i = 0; i < n; ++i) {
     double s = b[i];
     for (int k = 0; k < i; ++k) s -= Lc[i * n + k] * y[k];
@@ -140,23 +175,36 @@ void spd_solve_lifted(int n, const double* L, const double* b, double eps_lift, 
   }
 }
 
-// spd_cholesky_inverse_lifted_core, primitives.py:169-192
-void spd_inverse_lifted(int n, const double* L, double eps_lift, double* Linv) {
-  std::vector<double> A(L, L + n * n), Lc(n * n), Ci(n * n, 0.0);
-  for (int i = 0; i < n; ++i) A[i * n + i] += eps_lift;
-  cholesky(n, A.data(), Lc.data());
+void spd_factor_inverse(const SpdFactor& f, double* Linv) {
+  const int n = f.n;
+  const double* Lc = f.Lc;
+  double Ci[kMaxN * kMaxN];  // Ci = Lc^{-1} (lower triangular)
   for (int c = 0; c < n; ++c)
     for (int i = 0; i < n; ++i) {
+      if (i < c) { Ci[i * n + c] = 0.0; continue; }
       double s = (i == c) ? 1.0 : 0.0;
-      for (int k = 0; k < i; ++k) s -= Lc[i * n + k] * Ci[k * n + c];
+      for (int k = c; k < i; ++k) s -= Lc[i * n + k] * Ci[k * n + c];
       Ci[i * n + c] = s / Lc[i * n + i];
     }
   for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
+    for (int j = i; j < n; ++j) {
       double s = 0.0;
-      for (int k = 0; k < n; ++k) s += Ci[k * n + i] * Ci[k * n + j];
+      for (int k = j; k < n; ++k) s += Ci[k * n + i] * Ci[k * n + j];
       Linv[i * n + j] = s;
+      Linv[j * n + i] = s;
     }
+}
+
+void spd_solve_lifted(int n, const double* L, const double* b, double eps_lift, double* x) {
+  SpdFactor f;
+  spd_factor_lifted(n, L, eps_lift, f);
+  spd_factor_solve(f, b, x);
+}
+
+void spd_inverse_lifted(int n, const double* L, double eps_lift, double* Linv) {
+  SpdFactor f;
+  spd_factor_lifted(n, L, eps_lift, f);
+  spd_factor_inverse(f, Linv);
 }
 
 void solve3(const double* A, const double* b, double* x) {
@@ -219,19 +267,27 @@ void se3_log(const double* T, double* out) {
 // BeliefGaussianInfo.mean_increment / mean_world_pose, belief.py:373-434
 void mean_increment(const Belief& b, double* dz) { spd_solve_lifted(DZ, b.L, b.h, kEpsLift, dz); }
 
-void mean_world_pose(const Belief& b, double* pose6) {
-  double dz[DZ], e[6];
-  mean_increment(b, dz);
+void world_pose_from_increment(const Belief& b, const double* dz, double* pose6) {
+  double e[6];
   se3_exp(dz, e);
   se3_compose(b.X_anchor, e, pose6);
 }
 
+void mean_world_pose(const Belief& b, double* pose6) {
+  double dz[DZ];
+  mean_increment(b, dz);
+  world_pose_from_increment(b, dz, pose6);
+}
+
 // _predict_diffusion_core, predict.py:43-103
-void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& pred, double* infl3) {
+void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& pred, double* infl3,
+                       double* mean_prev_out) {
   const int n = DZ;
   double mean_prev[DZ], cov_prev[DZ * DZ], cov_raw[DZ * DZ], cov_psd[DZ * DZ], Lp[DZ * DZ], Lpsd[DZ * DZ];
-  spd_solve_lifted(n, prev.L, prev.h, kEpsLift, mean_prev);
-  spd_inverse_lifted(n, prev.L, kEpsLift, cov_prev);
+  SpdFactor f;
+  spd_factor_lifted(n, prev.L, kEpsLift, f);
+  spd_factor_solve(f, prev.h, mean_prev);
+  spd_factor_inverse(f, cov_prev);
   const double lam = 0.1;  // GC_OU_DAMPING_LAMBDA, constants.py:248
   double ef = exp(-2.0 * lam * dt);
   double dc = (1.0 - ef) / (2.0 * lam + kF64Eps);
@@ -251,6 +307,7 @@ void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& p
   infl3[0] = 2.0 * kEpsLift * n;
   infl3[1] = d1 + d2;
   infl3[2] = dt;
+  if (mean_prev_out) memcpy(mean_prev_out, mean_prev, sizeof(mean_prev));
 }
 
 // preintegrate_imu_relative_pose_jax, imu_preintegration.py:47-147
@@ -264,6 +321,8 @@ void preintegrate_imu(int m, const double* stamps, const double* gyro, const dou
     double dt = (i + 1 < m) ? stamps[i + 1] - stamps[i] : 0.0;
     dt = dt > 0.0 ? dt : 0.0;
     double dte = w[i] * dt;
+    // dte == 0 (padding slots, last sample) is an exact identity step: Exp(0) = I, v and p unchanged
+    if (dte == 0.0) continue;
     double om[3] = {(gyro[3 * i] - gb[0]) * dte, (gyro[3 * i + 1] - gb[1]) * dte, (gyro[3 * i + 2] - gb[2]) * dte};
     double dR[9], Rn[9];
     so3_exp(om, dR);
@@ -295,8 +354,14 @@ void process_iw_suffstats(const double* L_pred, const double* h_pred, const doub
                           double* dPsi, double* dnu) {
   double mu0[DZ], mu1[DZ], Sig[DZ * DZ];
   spd_solve_lifted(DZ, L_pred, h_pred, kEpsLift, mu0);
-  spd_solve_lifted(DZ, L_post, h_post, kEpsLift, mu1);
-  spd_inverse_lifted(DZ, L_post, kEpsLift, Sig);
+  SpdFactor f;
+  spd_factor_lifted(DZ, L_post, kEpsLift, f);
+  spd_factor_solve(f, h_post, mu1);
+  spd_factor_inverse(f, Sig);
+  process_iw_suffstats_from(mu0, mu1, Sig, dPsi, dnu);
+}
+
+void process_iw_suffstats_from(const double* mu0, const double* mu1, const double* Sig, double* dPsi, double* dnu) {
   for (int i = 0; i < 7 * 36; ++i) dPsi[i] = 0.0;
   for (int b = 0; b < 7; ++b) {
     int s0 = kBlkStart[b], d = kBlkDim[b];

@@ -5,8 +5,6 @@
 #pragma once
 #include <stdint.h>
 
-#include <vector>
-
 namespace gcs {
 namespace host {
 
@@ -19,6 +17,17 @@ double psd_project(int n, const double* M, double eps_psd, double* out, double* 
 bool cholesky(int n, const double* A, double* Lc);
 void spd_solve_lifted(int n, const double* L, const double* b, double eps_lift, double* x);
 void spd_inverse_lifted(int n, const double* L, double eps_lift, double* Linv);
+
+// One Cholesky factor of L + eps_lift I (spd_cholesky_*_lifted_core, primitives.py:141-192),
+// reused by every solve / inverse of the same matrix in a scan.
+constexpr int kMaxN = 64;
+struct SpdFactor {
+  int n = 0;
+  double Lc[kMaxN * kMaxN];
+};
+void spd_factor_lifted(int n, const double* L, double eps_lift, SpdFactor& f);
+void spd_factor_solve(const SpdFactor& f, const double* b, double* x);
+void spd_factor_inverse(const SpdFactor& f, double* Linv);
 void solve3(const double* A, const double* b, double* x);  // LU with partial pivoting
 
 struct Belief {
@@ -33,9 +42,12 @@ void se3_compose(const double* a, const double* b, double* out);
 void se3_log(const double* T, double* out);
 void mean_increment(const Belief& b, double* dz);
 void mean_world_pose(const Belief& b, double* pose6);
+// world pose from an already solved mean increment (belief.py:400-434)
+void world_pose_from_increment(const Belief& b, const double* dz, double* pose6);
 
 // predict_diffusion (predict.py:43-103); infl = [lift_strength, psd_delta, dt_scale]
-void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& pred, double* infl3);
+void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& pred, double* infl3,
+                       double* mean_prev_out = nullptr /*DZ, optional: prev's mean increment*/);
 
 struct PreintOut {
   double delta_pose[6];
@@ -47,6 +59,9 @@ void preintegrate_imu(int m, const double* stamps, const double* gyro, const dou
 // IW process noise (inverse_wishart_jax.py)
 void process_iw_suffstats(const double* L_pred, const double* h_pred, const double* L_post, const double* h_post,
                           double* dPsi /*7x36*/, double* dnu /*7*/);
+// same from the solved means and posterior covariance (shared with the rest of the scan tail)
+void process_iw_suffstats_from(const double* mu_pred, const double* mu_post, const double* Sig_post, double* dPsi,
+                               double* dnu);
 void datasheet_iw_state(double* nu, double* Psi);
 void process_noise_Q(const double* nu, const double* Psi, double* Q);
 void process_iw_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double* nu_out,

@@ -8,6 +8,23 @@
 
 namespace gcs {
 
+// "last block finishes" tickets (device array, zeroed at context creation, self re-arming):
+// kTicketStride words per kernel (kernel-wide ticket + one per group of 64 blocks)
+enum { TK_BUDGET = 0, TK_POINTS, TK_SCAN, TK_BINS, TK_MF, TK_PT, TK_PUSH, TK_DENSE, TK_COUNT };
+constexpr int kTicketStride = 1024;
+
+struct BudgetArgs {
+  const double* w;
+  int n_raw, stride;
+  double* partials;
+  double* scalars;
+  uint32_t* ticket;
+  uint32_t* zero32;  // scale-mode bucketing state cleared for this scan (may be null)
+  int n_zero32;
+  uint8_t* zero8;
+  int n_zero8;
+};
+
 struct PointKernelArgs {
   // raw PointCloud2-like input (device)
   const uint8_t* xyz;  // float x,y,z at byte offsets 0,4,8 of each record
@@ -31,9 +48,9 @@ struct PointKernelArgs {
   PointRec* recs;
   uint32_t* keys;
   uint32_t* slots;
-  uint32_t* counts;  // per-bin bucket sizes (zeroed before the launch)
-  uint8_t* flags;    // active-bin flags (zeroed before the launch)
+  uint32_t* counts;  // per-bin bucket sizes (cleared by k_budget)
   double* scalars;
+  uint32_t* ticket;
   // optional debug/parity outputs (may be null)
   double* p0_out;
   double* w_out;
@@ -41,19 +58,42 @@ struct PointKernelArgs {
   int* nearest_out;
 };
 
-struct BinKernelArgs {
+struct BucketArgs {
+  int n_bins, k;
+  const uint32_t* counts;
+  const uint32_t* keys;
+  const uint32_t* slots;
+  const int* knn;
   const PointRec* recs;
-  const uint32_t* sorted_vals;
+  uint32_t* starts;
+  uint32_t* scan_status;  // per 4096-bucket tile look-back word (cleared by k_budget)
+  uint32_t* scan_ticket;
+  uint32_t* slot_idx;
+  uint32_t* dest;  // per point: bucket-ordered destination (aliases the slot array once placed)
+  PointRec* recs_s;
+  uint8_t* flags;      // active bins (cleared by k_budget)
+  uint32_t* mid_list;  // buckets with more than kLaneRank members
+  uint32_t* mid_n;     // (cleared by k_budget)
+};
+
+struct BinKernelArgs {
+  const PointRec* recs;    // point order (dense mode)
+  const PointRec* recs_s;  // bucket order (scale mode)
   const uint32_t* starts;
   const uint32_t* counts;
   const uint8_t* flags;
   const int* rknn_off;
   const int* rknn;
   const double* bin_dirs;
+  const double* map;  // map sufficient stats (fused Matrix-Fisher term, scale mode)
   int n_bins, cap;
   double origin[3];
   double tau;
   double* scan;  // 26 x B field-major
+  double* scalars;
+  uint32_t* ticket;
+  uint32_t* zero_after;  // bucketing scratch (mid-list length, look-back words) re-armed for the next scan
+  int n_zero_after;
 };
 
 struct PushArgs {
@@ -65,22 +105,27 @@ struct PushArgs {
   double gamma;
 };
 
-hipError_t launch_budget(const double* w, int n_raw, int stride, double* partials, int nblk, double* scalars,
-                         hipStream_t s);
-hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, hipStream_t s);
-hipError_t launch_bucketing(uint32_t* counts, uint32_t* starts, uint32_t* tile_sums, const uint32_t* keys,
-                            const uint32_t* slots, int n, int n_bins, uint32_t* sorted, uint32_t* big_list,
-                            uint32_t* big_n, hipStream_t s);
+// Launchers.  e0/e1 (may be null) are stamped with the first kernel's start and the last
+// kernel's end through hipExtLaunchKernel, so stage timing adds no marker packets to the queue.
+hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, hipStream_t s, hipEvent_t e0,
+                         hipEvent_t e1);
+int scan_tiles(int n_bins);
+hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 int bins_scale_blocks(int n_bins);
-hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s);
-hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* partials, hipStream_t s);
-hipError_t launch_bin_cert_final(const double* partials, int nblk, double* scalars, hipStream_t s);
+int bins_partial_nv();
+int push_blocks(int n_bins);
+hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* partials, hipStream_t s, hipEvent_t e0,
+                        hipEvent_t e1);
 hipError_t launch_mf(const double* scan, const double* map, int B, double* partials, int nblk, double* scalars,
-                     hipStream_t s);
+                     uint32_t* ticket, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, hipStream_t s);
+                     double* scalars, uint32_t* ticket, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
-                              hipStream_t s);
-hipError_t launch_map_derive(const double* map, double* derived, int B, hipStream_t s);
+                              double* partials, double* scalars, uint32_t* ticket, hipStream_t s, hipEvent_t e0,
+                              hipEvent_t e1);
+hipError_t launch_map_derive(const double* map, double* derived, int B, double* partials, double* scalars,
+                             uint32_t* ticket, hipStream_t s);
 
 }  // namespace gcs

@@ -21,6 +21,8 @@
 
 
 #include "gcs_kernels.h"
+
+#include <hip/hip_ext.h>
 #include "gcs_layout.h"
 #include "gcs_math.h"
 
@@ -79,19 +81,19 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
   return v;
 }
 
-// Final pass over per-block partials: one block, thread t sums partials t, t+256, ... in order,
-// then a fixed tree.  Bit k of MAXMASK selects max instead of sum for component k.
+// Final pass over per-block partials inside one block: thread t folds partials t, t+256, ... in
+// order, then a fixed tree; the result is valid in thread 0.  Bit k of MAXMASK selects max
+// instead of sum for component k.  lds must hold kWaves*NV doubles.
 template <int NV, unsigned MAXMASK>
-__global__ __launch_bounds__(kBlock) void k_partials_final(const double* __restrict__ partials, int nblocks,
-                                                           double* out, int out_off) {
-  __shared__ double lds[kWaves * NV];
-  double v[NV];
+__device__ __forceinline__ void reduce_partials(const double* __restrict__ partials, int nblocks, double (&v)[NV],
+                                                double* lds) {
 #pragma unroll
   for (int k = 0; k < NV; ++k) v[k] = ((MAXMASK >> k) & 1u) ? -INFINITY : 0.0;
   for (int b = threadIdx.x; b < nblocks; b += kBlock)
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-      double x = partials[(size_t)b * NV + k];
+      // device-coherent load (sc1): partials of other blocks were stored device-coherently
+      double x = __hip_atomic_load(partials + (size_t)b * NV + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       v[k] = ((MAXMASK >> k) & 1u) ? fmax(v[k], x) : v[k] + x;
     }
 #pragma unroll
@@ -112,39 +114,84 @@ __global__ __launch_bounds__(kBlock) void k_partials_final(const double* __restr
     for (int k = 0; k < NV; ++k) {
       double s = lds[k];
       for (int w = 1; w < kWaves; ++w) s = ((MAXMASK >> k) & 1u) ? fmax(s, lds[w * NV + k]) : s + lds[w * NV + k];
-      out[out_off + k] = s;
+      v[k] = s;
     }
   }
+  __syncthreads();
+}
+
+// "Last block finishes", two levels: thread 0 of every block stores the block partial
+// device-coherently (sc1 stores, no L2 write-back), waits for the stores to complete and draws a
+// ticket of its group of 64 blocks; the last block of a group folds the group's partials (fixed
+// order, sc1 loads) into a group partial and draws the kernel-wide ticket; the last group runs
+// the final fold.  No single block ever reads more than 64 partials, and a full
+// __threadfence() (buffer_wbl2: write-back of the XCD's whole L2, per block) is never needed.
+// Tickets re-arm themselves.  Layout: partials[nblocks*NV] then group partials[ngroups*NV];
+// tickets[0] kernel-wide, tickets[1 + g] per group.
+constexpr int kFinGroup = 64;  // kTicketStride (gcs_kernels.h) >= 1 + ngroups
+
+template <int NV>
+__device__ __forceinline__ void store_partials(const double (&v)[NV], double* base, int idx) {
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+      __hip_atomic_store(base + (size_t)idx * NV + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool ticket_last(uint32_t* ticket, uint32_t expected) {
+  __shared__ uint32_t s_last;
+  if (threadIdx.x == 0) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);  // this thread's partial stores have completed
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    uint32_t prev = atomicAdd(ticket, 1u);
+    uint32_t last = (prev == expected - 1u) ? 1u : 0u;
+    if (last) atomicExch(ticket, 0u);
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0u;
+}
+
+// v: block partial (valid in thread 0).  Returns true in the one block that finishes, with the
+// kernel-wide fold in v (thread 0).
+template <int NV, unsigned MAXMASK>
+__device__ bool finish_blocks(double (&v)[NV], double* partials, uint32_t* tickets, double* lds) {
+  const int nb = gridDim.x;
+  const int ng = (nb + kFinGroup - 1) / kFinGroup;
+  store_partials<NV>(v, partials, blockIdx.x);
+  const int g = blockIdx.x / kFinGroup;
+  const int gsz = min(kFinGroup, nb - g * kFinGroup);
+  if (!ticket_last(tickets + 1 + g, (uint32_t)gsz)) return false;
+  reduce_partials<NV, MAXMASK>(partials + (size_t)g * kFinGroup * NV, gsz, v, lds);
+  double* gp = partials + (size_t)nb * NV;
+  store_partials<NV>(v, gp, g);
+  if (!ticket_last(tickets, (uint32_t)ng)) return false;
+  reduce_partials<NV, MAXMASK>(gp, ng, v, lds);
+  return true;
 }
 
 // ---------------------------------------------------------------- row 1: budget mass sums
-__global__ __launch_bounds__(kBlock) void k_budget_partial(const double* __restrict__ w, int n_raw, int stride,
-                                                           double* partials) {
+// Also clears the scale-mode bucketing state of this scan (counts, flags, look-back status),
+// replacing three memsets.  mass_scale = total_mass_in / (total_mass_selected + eps_mass)
+// (point_budget.py:80-84) is produced by the last block.
+__global__ __launch_bounds__(kBlock) void k_budget(BudgetArgs a) {
   __shared__ double lds[kWaves * 2];
+  const int gid = blockIdx.x * kBlock + threadIdx.x, gsz = gridDim.x * kBlock;
+  for (int j = gid; j < a.n_zero32; j += gsz) a.zero32[j] = 0u;
+  for (int j = gid; j < a.n_zero8; j += gsz) a.zero8[j] = 0u;
   double v[2] = {0.0, 0.0};
-  for (int j = blockIdx.x * kBlock + threadIdx.x; j < n_raw; j += gridDim.x * kBlock) {
-    double x = w[j];
+  for (int j = gid; j < a.n_raw; j += gsz) {
+    double x = a.w[j];
     v[0] += x;
-    if (j % stride == 0) v[1] += x;
+    if (j % a.stride == 0) v[1] += x;
   }
   block_sum<2>(v, lds);
+  if (!finish_blocks<2, 0u>(v, a.partials, a.ticket, lds)) return;
   if (threadIdx.x == 0) {
-    partials[blockIdx.x * 2] = v[0];
-    partials[blockIdx.x * 2 + 1] = v[1];
-  }
-}
-
-__global__ __launch_bounds__(kBlock) void k_budget_final(const double* __restrict__ partials, int nblocks,
-                                                         double* scalars) {
-  __shared__ double lds[kWaves * 2];
-  double v[2] = {0.0, 0.0};
-  for (int b = threadIdx.x; b < nblocks; b += kBlock) { v[0] += partials[2 * b]; v[1] += partials[2 * b + 1]; }
-  block_sum<2>(v, lds);
-  if (threadIdx.x == 0) {
-    scalars[SC_MASS_IN] = v[0];
-    scalars[SC_MASS_SEL] = v[1];
-    // mass_scale = total_mass_in / (total_mass_selected + eps_mass)   point_budget.py:80-84
-    scalars[SC_MASS_SCALE] = v[0] / (v[1] + kEpsMass);
+    a.scalars[SC_MASS_IN] = v[0];
+    a.scalars[SC_MASS_SEL] = v[1];
+    a.scalars[SC_MASS_SCALE] = v[0] / (v[1] + kEpsMass);
   }
 }
 
@@ -174,6 +221,10 @@ __device__ __forceinline__ void ray_dir(double px, double py, double pz, const d
 
 // ---------------------------------------------------------------- row 1+3+5: the point kernel
 // One thread per budget output slot i in [0, cap).  SCALE = candidate-restricted softmax.
+// At C2 the grid is ~1 wave per SIMD, so the kernel is bound by each lane's dependent chain:
+// loads are issued in independent batches (whole pool row, whole candidate row) so the chain is
+// xyz -> pool ids -> pool dirs -> knn row -> candidate dirs -> slot atomic, and the softmax
+// evaluates one exp per candidate and no per-candidate log (entropy identity below).
 template <bool SCALE, int KC>
 __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* partials) {
   __shared__ double lds[kWaves * 5];
@@ -206,48 +257,67 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
       bool zero = (d[0] == 0.0 && d[1] == 0.0 && d[2] == 0.0);
       if (!zero) {
         const int4* pool = (const int4*)(a.pools + (size_t)cube_cell(d[0], d[1], d[2], a.grid) * a.pool_width);
+        const int nq = a.pool_width >> 2;
         double best = -INFINITY;
-        for (int q = 0; q < (a.pool_width >> 2); ++q) {
-          int4 id4 = pool[q];
-          int ids[4] = {id4.x, id4.y, id4.z, id4.w};
+        for (int q = 0; q < nq; q += 2) {  // 8 ids per batch: all loads in flight together
+          int4 u0 = pool[q];
+          int4 u1 = q + 1 < nq ? pool[q + 1] : make_int4(-1, -1, -1, -1);
+          int ids[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+          double s[8];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
+          for (int u = 0; u < 8; ++u) {
+            s[u] = -INFINITY;
             if (ids[u] >= 0) {
               const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)ids[u]);
-              double s = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
-              if (s > best) { best = s; nearest = ids[u]; }
+              s[u] = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
             }
           }
-          if (id4.w < 0) break;
+#pragma unroll
+          for (int u = 0; u < 8; ++u)
+            if (s[u] > best) { best = s[u]; nearest = ids[u]; }
+          if (u1.w < 0) break;
         }
       }
-      const int* cand = a.knn + (size_t)nearest * KC;
-      double sims[KC];
+      const int4* cand4 = (const int4*)(a.knn + (size_t)nearest * KC);
+      int cand[KC];
+#pragma unroll
+      for (int k = 0; k < KC / 4; ++k) {
+        int4 c4 = cand4[k];
+        cand[4 * k] = c4.x; cand[4 * k + 1] = c4.y; cand[4 * k + 2] = c4.z; cand[4 * k + 3] = c4.w;
+      }
+      double e[KC];
 #pragma unroll
       for (int k = 0; k < KC; ++k) {
         const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)cand[k]);
-        sims[k] = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
-        m = fmax(m, sims[k]);
+        e[k] = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
+        m = fmax(m, e[k]);
       }
-#pragma unroll
-      for (int k = 0; k < KC; ++k) Z += exp((sims[k] - m) * inv_tau);
-      double iz = 1.0 / Z;
+      // e_k = exp(x_k), x_k = (sim_k - m)/tau (binning.py:69 softmax, shifted by the max)
+      double sxe = 0.0;
 #pragma unroll
       for (int k = 0; k < KC; ++k) {
-        double r = exp((sims[k] - m) * inv_tau) * iz;
-        H -= r * log(r + kEpsMass);
+        double x = (e[k] - m) * inv_tau;
+        e[k] = exp(x);
+        Z += e[k];
+        sxe += x * e[k];
+      }
+      const double iz = 1.0 / Z;
+      // entropy of r_k = e_k/Z (binning.py:71-75): -sum r log(r + eps)
+      //   = log Z - sum r_k x_k - sum r_k log1p(eps/r_k),
+      // with r log1p(eps/r) in [0, eps] taken as eps r/(r + eps) (|error| < 0.2 eps per term)
+      double corr = 0.0;
+#pragma unroll
+      for (int k = 0; k < KC; ++k) {
+        double r = e[k] * iz;
+        corr += r * __builtin_amdgcn_rcp(r + kEpsMass);
         rm = fmax(rm, r);
       }
+      H = log(Z) - sxe * iz - kEpsMass * corr;
       uint32_t key = (uint32_t)a.n_bins;
       if (valid) {
-        // bucket slot: arrival order only (reordered by point index in k_bucket_order)
-        uint32_t slot = atomicAdd(a.counts + nearest, 1u);
-        a.slots[i] = slot;
+        // bucket slot: arrival order only (re-ranked by point index in k_bucket_build)
+        a.slots[i] = atomicAdd(a.counts + nearest, 1u);
         key = (uint32_t)nearest;
-        if (slot == 0) {  // first arrival marks the bucket's candidate bins active
-#pragma unroll
-          for (int k = 0; k < KC; ++k) a.flags[cand[k]] = 1;
-        }
       }
       a.keys[i] = key;
       Z = iz;
@@ -287,114 +357,178 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
   }
   block_sum<4>(acc, lds);
   rmax = block_max(rmax, lds);
-  if (threadIdx.x == 0) {
-    double* pp = partials + blockIdx.x * 5;
-    pp[0] = acc[0]; pp[1] = acc[1]; pp[2] = acc[2]; pp[3] = acc[3]; pp[4] = rmax;
-  }
+  double v[5] = {acc[0], acc[1], acc[2], acc[3], rmax};
+  // (sum wb, sum wn^2, sum w_out, sum H, max r) -> scalars[SC_DESKEW_WIN..]
+  if (!finish_blocks<5, 16u>(v, partials, a.ticket, lds)) return;
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 5; ++k) a.scalars[SC_DESKEW_WIN + k] = v[k];
 }
 
 // ---------------------------------------------------------------- deterministic bucketing by nearest bin
-// counts[] were filled by atomic slots in k_points.  start[] = exclusive scan of counts in two
-// passes over 4096-bucket tiles; points are placed at start+slot, then every bucket is reordered
-// by ascending point index (insertion sort up to 64 entries, an in-order compaction over all
-// keys for larger buckets), so the bin gather sees a scheduling-independent order.
+// k_points took an arrival slot per point (atomic per-bucket counts).  k_scan: start[] =
+// exclusive scan of the counts in one pass (decoupled look-back over 4096-bucket tiles, one
+// wave reading 64 predecessors per step).  k_place scatters point indices by slot.
+// k_bucket_rank gives every member its rank by point index inside its bucket (one lane per
+// bucket up to kLaneRank members, else one wave per bucket in k_bucket_mid; above kRankMax an
+// in-order compaction over all keys) and writes the member's destination start+rank; it also
+// marks the K candidate bins of every non-empty bucket active.  k_gather then moves every point
+// record to its destination, so each bucket's records are contiguous in point-index order and
+// the bin gather streams them in a scheduling-independent order.
 constexpr int kScanTile = 4096;
-__global__ __launch_bounds__(kBlock) void k_scan_tiles(const uint32_t* __restrict__ counts, int n, uint32_t* tile_sums) {
-  __shared__ uint32_t ws[kWaves];
-  int base = blockIdx.x * kScanTile;
-  uint32_t s = 0;
-  for (int i = base + threadIdx.x; i < min(base + kScanTile, n); i += kBlock) s += counts[i];
-  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
-  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) tile_sums[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
-}
+constexpr int kLaneRank = 16;
+constexpr int kRankMax = 8192;
+constexpr uint32_t kLbAgg = 1u << 30, kLbPre = 2u << 30, kLbVal = (1u << 30) - 1u;
 
-__global__ __launch_bounds__(kBlock) void k_scan_apply(const uint32_t* __restrict__ counts, int n,
-                                                       const uint32_t* __restrict__ tile_sums, uint32_t* start) {
+__global__ __launch_bounds__(kBlock) void k_scan(const uint32_t* __restrict__ counts, int n, uint32_t* status,
+                                                 uint32_t* ticket, uint32_t* start) {
   __shared__ uint32_t wsum[kWaves];
-  __shared__ uint32_t carry;
+  __shared__ uint32_t s_tile, s_excl;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  if (t == 0) {
-    uint32_t c = 0;
-    for (int b = 0; b < (int)blockIdx.x; ++b) c += tile_sums[b];
-    carry = c;
+  if (t == 0) s_tile = atomicAdd(ticket, 1u);  // tiles are numbered in start order (forward progress)
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const int base = (int)tile * kScanTile + 16 * t;
+  uint32_t v[16];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    v[j] = (base + j < n) ? counts[base + j] : 0u;
+    tot += v[j];
+  }
+  uint32_t x = tot;
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  if (wid == 0) {
+    const uint32_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    uint32_t excl = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(status, kLbPre | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(status + tile, kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // look back in windows of 64 predecessors: lane l reads tile (w0 - l)
+      uint32_t spins = 0;
+      int w0 = (int)tile - 1;
+      while (w0 >= 0) {
+        const int j = w0 - lane;
+        uint32_t s = j >= 0 ? __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
+        // the window is usable up to (and including) its nearest published prefix
+        const unsigned long long pre = __ballot((s & ~kLbVal) == kLbPre);
+        const int stop = pre ? (__ffsll((long long)pre) - 1) : 63;
+        const unsigned long long unpub = __ballot(s == 0u && lane <= stop);
+        if (unpub) {  // bounded so a broken invariant cannot hang the GPU
+          if (++spins > (1u << 22)) { excl = 0xffffffffu; break; }
+          continue;
+        }
+        uint32_t val = (lane <= stop && j >= 0) ? (s & kLbVal) : 0u;
+        for (int off = 32; off >= 1; off >>= 1) val += __shfl_xor(val, off, 64);
+        excl += val;
+        if (pre) break;
+        w0 -= 64;
+      }
+      if (lane == 0) __hip_atomic_store(status + tile, kLbPre | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_excl = excl;
+      if (tile == gridDim.x - 1) atomicExch(ticket, 0u);  // every tile has drawn its number by now
+    }
   }
   __syncthreads();
-  int base = blockIdx.x * kScanTile;
-  for (int c0 = base; c0 < min(base + kScanTile, n); c0 += kBlock) {
-    int i = c0 + t;
-    uint32_t v = i < n ? counts[i] : 0u;
-    uint32_t x = v;  // inclusive wave scan
-    for (int off = 1; off < 64; off <<= 1) {
-      uint32_t y = __shfl_up(x, off, 64);
-      if (lane >= off) x += y;
-    }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    uint32_t pre = carry;
-    for (int w = 0; w < wid; ++w) pre += wsum[w];
-    if (i < n) start[i] = pre + x - v;
-    __syncthreads();
-    if (t == kBlock - 1) carry = pre + x;
-    __syncthreads();
+  uint32_t pre = s_excl + x - tot;
+  for (int w = 0; w < wid; ++w) pre += wsum[w];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    if (base + j < n) start[base + j] = pre;
+    pre += v[j];
   }
 }
 
 __global__ __launch_bounds__(kBlock) void k_place(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ slots,
                                                   const uint32_t* __restrict__ start, int n, int n_bins,
-                                                  uint32_t* sorted) {
+                                                  uint32_t* slot_idx) {
   for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
     uint32_t key = keys[i];
-    if (key < (uint32_t)n_bins) sorted[start[key] + slots[i]] = (uint32_t)i;
+    if (key < (uint32_t)n_bins) slot_idx[start[key] + slots[i]] = (uint32_t)i;
   }
 }
 
-constexpr int kSmallBucket = 64;
-__global__ __launch_bounds__(kBlock) void k_bucket_order(const uint32_t* __restrict__ counts,
-                                                         const uint32_t* __restrict__ start, int n_bins,
-                                                         uint32_t* sorted, uint32_t* big_list, uint32_t* big_n) {
-  for (int a = blockIdx.x * kBlock + threadIdx.x; a < n_bins; a += gridDim.x * kBlock) {
-    uint32_t c = counts[a];
-    if (c < 2) continue;
-    if (c > (uint32_t)kSmallBucket) {
-      big_list[atomicAdd(big_n, 1u)] = (uint32_t)a;
-      continue;
-    }
-    uint32_t* v = sorted + start[a];
-    for (uint32_t j = 1; j < c; ++j) {
-      uint32_t x = v[j];
-      int q = (int)j - 1;
-      while (q >= 0 && v[q] > x) { v[q + 1] = v[q]; --q; }
-      v[q + 1] = x;
+// one lane per bucket (grid covers all buckets exactly once)
+__global__ __launch_bounds__(kBlock) void k_bucket_rank(BucketArgs b) {
+  const int a = blockIdx.x * kBlock + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const uint32_t c = a < b.n_bins ? b.counts[a] : 0u;
+  const bool mid = c > (uint32_t)kLaneRank;
+  const unsigned long long mm = __ballot(mid);
+  if (mm) {  // wave-aggregated append to the mid list
+    const int leader = __ffsll((long long)mm) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(b.mid_n, (uint32_t)__popcll(mm));
+    base = __shfl(base, leader, 64);
+    if (mid) b.mid_list[base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull))] = (uint32_t)a;
+  }
+  if (c == 0u) return;
+  const int* kr = b.knn + (size_t)a * b.k;
+  for (int q = 0; q < b.k; q += 4) {
+    int4 c4 = *(const int4*)(kr + q);
+    b.flags[c4.x] = 1; b.flags[c4.y] = 1; b.flags[c4.z] = 1; b.flags[c4.w] = 1;
+  }
+  if (mid) return;
+  const uint32_t st = b.starts[a];
+  const uint32_t* sl = b.slot_idx + st;
+  uint32_t idx[kLaneRank];
+#pragma unroll
+  for (int j = 0; j < kLaneRank; ++j) idx[j] = (uint32_t)j < c ? sl[j] : 0xffffffffu;
+#pragma unroll
+  for (int j = 0; j < kLaneRank; ++j) {
+    if ((uint32_t)j < c) {
+      uint32_t r = 0;
+#pragma unroll
+      for (int q = 0; q < kLaneRank; ++q) r += idx[q] < idx[j] ? 1u : 0u;
+      b.dest[idx[j]] = st + r;
     }
   }
 }
 
-// big buckets: one block rebuilds the bucket by an in-order compaction over all keys
-__global__ __launch_bounds__(kBlock) void k_bucket_big(const uint32_t* __restrict__ keys, int n,
-                                                       const uint32_t* __restrict__ start,
-                                                       const uint32_t* __restrict__ big_list,
-                                                       const uint32_t* __restrict__ big_n, uint32_t* sorted) {
-  __shared__ uint32_t wcnt[kWaves];
-  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  uint32_t nb = *big_n;
-  for (uint32_t j = blockIdx.x; j < nb; j += gridDim.x) {
-    uint32_t a = big_list[j];
-    uint32_t pos = start[a];
-    for (int c0 = 0; c0 < n; c0 += kBlock) {
-      int i = c0 + t;
-      bool hit = i < n && keys[i] == a;
-      unsigned long long m = __ballot(hit);
-      if (lane == 0) wcnt[wid] = (uint32_t)__popcll(m);
-      __syncthreads();
-      uint32_t pre = pos;
-      for (int w = 0; w < wid; ++w) pre += wcnt[w];
-      if (hit) sorted[pre + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
-      pos += wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
-      __syncthreads();
+// one wave per bucket with more than kLaneRank members
+__global__ __launch_bounds__(kBlock) void k_bucket_mid(BucketArgs b, int n) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t nb = *b.mid_n;
+  const uint32_t nw = gridDim.x * kWaves;
+  for (uint32_t w = blockIdx.x * kWaves + (threadIdx.x >> 6); w < nb; w += nw) {
+    const uint32_t a = b.mid_list[w];
+    const uint32_t c = b.counts[a], st = b.starts[a];
+    if (c <= (uint32_t)kRankMax) {
+      for (uint32_t j0 = 0; j0 < c; j0 += 64) {
+        uint32_t v = (j0 + lane < c) ? b.slot_idx[st + j0 + lane] : 0xffffffffu;
+        uint32_t rank = 0;
+        for (uint32_t k0 = 0; k0 < c; k0 += 64) {
+          uint32_t u = (k0 + lane < c) ? b.slot_idx[st + k0 + lane] : 0xffffffffu;
+          for (int jj = 0; jj < 64; ++jj) rank += (__shfl(u, jj, 64) < v) ? 1u : 0u;
+        }
+        if (j0 + lane < c) b.dest[v] = st + rank;
+      }
+    } else {  // in-order compaction over all keys
+      uint32_t pos = st;
+      for (int i0 = 0; i0 < n; i0 += 64) {
+        const int i = i0 + lane;
+        const bool hit = i < n && b.keys[i] == a;
+        const unsigned long long m = __ballot(hit);
+        if (hit) b.dest[i] = pos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        pos += (uint32_t)__popcll(m);
+      }
     }
   }
+}
+
+// every valid point record to its bucket-ordered destination
+__global__ __launch_bounds__(kBlock) void k_gather(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ dest,
+                                                   int n, int n_bins, const PointRec* __restrict__ recs,
+                                                   PointRec* __restrict__ recs_s) {
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+    if (keys[i] < (uint32_t)n_bins) recs_s[dest[i]] = recs[i];
 }
 
 // ---------------------------------------------------------------- bin finalize (shared)
@@ -458,28 +592,71 @@ __device__ __forceinline__ void write_bin_cert(double* cert, double* lds, double
   double v[4] = {cert[0], cert[1], cert[2], cert[3]};
   block_sum<4>(v, lds);
   double mx = block_max(cert[4], lds);
-  if (threadIdx.x == 0) {
-    double* pp = partials + blockIdx.x * 5;
-    pp[0] = v[0]; pp[1] = v[1]; pp[2] = v[2]; pp[3] = v[3]; pp[4] = mx;
-  }
+  cert[0] = v[0]; cert[1] = v[1]; cert[2] = v[2]; cert[3] = v[3]; cert[4] = mx;
 }
+
+// ---------------------------------------------------------------- row 7 helpers (Matrix-Fisher)
+// Per bin (matrix_fisher_evidence.py:181-211): w_b = sqrt(N_s N_m + eps), u = S/(|S|+eps),
+// conf = Rbar_s Rbar_m, H += w_b conf u_map u_scan^T; out[9] += w_b conf; out[10] += N_s.
+__device__ __forceinline__ void mf_bin_term(double Ns, double sx, double sy, double sz, const double* __restrict__ map,
+                                            int B, int b, double* out /*11*/) {
+  const size_t Bs = (size_t)B;
+  double Nm = map[MF_ND * Bs + b];
+  double mx = map[(MF_SD) * Bs + b], my = map[(MF_SD + 1) * Bs + b], mz = map[(MF_SD + 2) * Bs + b];
+  double wb = sqrt(Ns * Nm + kEpsMass);
+  double sn = sqrt(dot3_exact(sx, sy, sz, sx, sy, sz));
+  double mn = sqrt(dot3_exact(mx, my, mz, mx, my, mz));
+  double us[3] = {sx / (sn + kEpsMass), sy / (sn + kEpsMass), sz / (sn + kEpsMass)};
+  double um[3] = {mx / (mn + kEpsMass), my / (mn + kEpsMass), mz / (mn + kEpsMass)};
+  double conf = (sn * (1.0 / (Ns + kEpsMass))) * (mn * (1.0 / (Nm + kEpsMass)));
+  double wf = wb * conf;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) out[3 * i + j] += wf * um[i] * us[j];
+  out[9] += wf;
+  out[10] += Ns;
+}
+
+// H (9), sum w conf, sum N_s -> scalars; 3x3 SVD and the det-fixed R_mf (:215-222) on one thread
+__device__ void mf_finish(const double* v, double* scalars) {
+  for (int k = 0; k < 9; ++k) scalars[SC_MF_H + k] = v[k];
+  scalars[SC_MF_NEFF] = v[9];
+  scalars[SC_MF_SCANN] = v[10];
+  double U[9], s[3], V[9];
+  svd3(v, U, s, V);
+  double UVt[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) UVt[3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
+  double dt = det3(UVt);
+  double sg = dt > 0.0 ? 1.0 : (dt < 0.0 ? -1.0 : 0.0);
+  U[2] *= sg; U[5] *= sg; U[8] *= sg;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      scalars[SC_MF_R + 3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
+  for (int k = 0; k < 3; ++k) scalars[SC_MF_S + k] = s[k];
+  for (int k = 0; k < 9; ++k) scalars[SC_MF_V + k] = V[k];
+}
+
+// fused bin-kernel partial: [sum N, sum N^2, sum N/(N+eps), sum psd delta, max eps ratio | MF 11]
+constexpr int kBinNV = 16;
 
 // ---------------------------------------------------------------- row 5+6 scale mode: bin-centric
 // One 256-thread workgroup per tile of 64 consecutive bins.  Phase 1 compacts the tile's active
-// bins (ballot, wave order).  Phase 2: a 16-lane group per active bin; lane l owns the bin's
-// reverse-kNN buckets l, l+16, ... (fixed order) and walks each bucket's points in ascending
-// point index (stable sort), so each lane's dependent chain is one bucket deep and the 16
-// buckets are fetched concurrently; the 16 lane sums meet in a fixed xor tree.  Phase 3: the
+// bins (ballot).  Phase 2: a 4-lane group per active bin (all 64 bins of a tile in flight);
+// lane l owns the bin's reverse-kNN buckets l, l+4, ... and streams each bucket's contiguous
+// records (ascending point index); the 4 lane sums meet in a fixed xor tree.  Phase 3: the
 // first wave finalizes the 64 bins (PSD, kappa) and streams the 26 field-major outputs.
 constexpr int kTile = 64;
-constexpr int kGroup = 16;
+constexpr int kGroup = 4;
 __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* partials) {
   __shared__ double sums[19 * kTile];
   __shared__ int active[kTile];
   __shared__ int n_active;
-  __shared__ double lds[kWaves * 4];
+  __shared__ double lds[kWaves * kBinNV];
   const int t = threadIdx.x;
   const int b0 = blockIdx.x * kTile;
+  for (int j = blockIdx.x * kBlock + t; j < a.n_zero_after; j += gridDim.x * kBlock) a.zero_after[j] = 0u;
   for (int i = t; i < 19 * kTile; i += kBlock) sums[i] = 0.0;
   if (t < 64) {
     int b = b0 + t;
@@ -492,50 +669,25 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   const int g = t / kGroup, l = t % kGroup;
   const double inv_tau = 1.0 / a.tau;
   for (int j = g; j < n_active; j += kBlock / kGroup) {
-    int lb = active[j];
-    int bb = b0 + lb;
+    const int lb = active[j];
+    const int bb = b0 + lb;
     const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)bb);
     double acc[19];
 #pragma unroll
     for (int f = 0; f < 19; ++f) acc[f] = 0.0;
-    const int q0 = a.rknn_off[bb], q1 = a.rknn_off[bb + 1];
-    // reverse-kNN buckets in chunks of 16 (one per lane); contributions flattened over the
-    // group in (bucket order, ascending point index) and dealt to lanes round-robin
-    for (int qc = q0; qc < q1; qc += kGroup) {
-      int q = qc + l;
-      uint32_t st = 0, ct = 0;
-      if (q < q1) {
-        int src = a.rknn[q];
-        st = a.starts[src];
-        ct = a.counts[src];
-      }
-      uint32_t x = ct;  // inclusive scan over the 16 lanes of the group
-#pragma unroll
-      for (int off = 1; off < kGroup; off <<= 1) {
-        uint32_t y = __shfl_up(x, off, kGroup);
-        if (l >= off) x += y;
-      }
-      const uint32_t pre = x - ct;
-      const uint32_t tot = __shfl(x, kGroup - 1, kGroup);
-      for (uint32_t r0 = 0; r0 < tot; r0 += kGroup) {
-        uint32_t jj = r0 + (uint32_t)l;
-        // source lane = last lane whose exclusive prefix <= jj (binary search over the group)
-        int s = 0;
-#pragma unroll
-        for (int step = kGroup / 2; step >= 1; step >>= 1) {
-          uint32_t ps = __shfl(pre, s + step, kGroup);
-          if (ps <= jj && s + step < kGroup) s += step;
-        }
-        uint32_t s_st = __shfl(st, s, kGroup);
-        uint32_t s_pre = __shfl(pre, s, kGroup);
-        if (jj < tot) {
-          const PointRec pr = a.recs[a.sorted_vals[s_st + (jj - s_pre)]];
-          double d[3] = {pr.dx, pr.dy, pr.dz};
-          double p[3] = {pr.x, pr.y, pr.z};
-          double sim = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
-          double r = exp((sim - pr.m) * inv_tau) * pr.iz;
-          add_contrib(acc, pr.w * r, d, p);
-        }
+    const int q1 = a.rknn_off[bb + 1];
+    // lane l owns reverse-kNN buckets l, l+4, ...; each bucket streams its contiguous records
+    for (int q = a.rknn_off[bb] + l; q < q1; q += kGroup) {
+      const uint32_t src = (uint32_t)a.rknn[q];
+      const uint32_t c = a.counts[src];
+      const PointRec* rp = a.recs_s + a.starts[src];
+      for (uint32_t i = 0; i < c; ++i) {
+        const PointRec pr = rp[i];
+        double d[3] = {pr.dx, pr.dy, pr.dz};
+        double p[3] = {pr.x, pr.y, pr.z};
+        double sim = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
+        double r = exp((sim - pr.m) * inv_tau) * pr.iz;
+        add_contrib(acc, pr.w * r, d, p);
       }
     }
 #pragma unroll
@@ -547,14 +699,35 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
       for (int f = 0; f < 19; ++f) sums[f * kTile + lb] = acc[f];
   }
   __syncthreads();
-  double cert[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+  // phase 3: finalize + this bin's Matrix-Fisher term (row 7, matrix_fisher_evidence.py:181-211).
+  // A bin with no scan mass contributes exact zeros to H, so only active bins read the map.
+  double v[kBinNV];
+#pragma unroll
+  for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
+  v[4] = -INFINITY;
   if (t < kTile && b0 + t < a.n_bins) {
     double r[19];
 #pragma unroll
     for (int f = 0; f < 19; ++f) r[f] = sums[f * kTile + t];
-    finalize_bin(r, a.scan, a.n_bins, b0 + t, cert);
+    finalize_bin(r, a.scan, a.n_bins, b0 + t, v);
+    if (a.flags[b0 + t]) mf_bin_term(r[0], r[1], r[2], r[3], a.map, a.n_bins, b0 + t, v + 5);
   }
-  write_bin_cert(cert, lds, partials);
+  // block reduce: 4 sums, 1 max, 11 sums
+  double s4[4] = {v[0], v[1], v[2], v[3]};
+  block_sum<4>(s4, lds);
+  double mx = block_max(v[4], lds);
+  double m11[11];
+#pragma unroll
+  for (int f = 0; f < 11; ++f) m11[f] = v[5 + f];
+  block_sum<11>(m11, lds);
+  v[0] = s4[0]; v[1] = s4[1]; v[2] = s4[2]; v[3] = s4[3]; v[4] = mx;
+#pragma unroll
+  for (int f = 0; f < 11; ++f) v[5 + f] = m11[f];
+  if (!finish_blocks<kBinNV, 16u>(v, partials, a.ticket, lds)) return;
+  if (t == 0) {
+    for (int f = 0; f < 5; ++f) a.scalars[SC_BIN_NSUM + f] = v[f];
+    mf_finish(v + 5, a.scalars);
+  }
 }
 
 // ---------------------------------------------------------------- row 5+6 dense mode (B small)
@@ -594,7 +767,7 @@ __global__ __launch_bounds__(kBlock) void k_dense_accum(BinKernelArgs a, double*
 
 __global__ __launch_bounds__(kBlock) void k_dense_finalize(BinKernelArgs a, const double* __restrict__ bin_partials,
                                                            int nchunks, double* partials) {
-  __shared__ double lds[kWaves * 4];
+  __shared__ double lds[kWaves * 5];
   int b = blockIdx.x * kBlock + threadIdx.x;
   double cert[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
   if (b < a.n_bins) {
@@ -607,77 +780,38 @@ __global__ __launch_bounds__(kBlock) void k_dense_finalize(BinKernelArgs a, cons
     finalize_bin(r, a.scan, a.n_bins, b, cert);
   }
   write_bin_cert(cert, lds, partials);
+  double v5[5] = {cert[0], cert[1], cert[2], cert[3], cert[4]};
+  if (!finish_blocks<5, 16u>(v5, partials, a.ticket, lds)) return;
+  for (int f = 0; f < 5; ++f) cert[f] = v5[f];
+  if (threadIdx.x == 0)
+    for (int f = 0; f < 5; ++f) a.scalars[SC_BIN_NSUM + f] = cert[f];
 }
 
 // ---------------------------------------------------------------- row 7: Matrix-Fisher reduction
-// Per bin (matrix_fisher_evidence.py:181-211): w_b = sqrt(N_s N_m + eps), u = S/(|S|+eps),
-// conf = Rbar_s Rbar_m, H += w_b conf u_map u_scan^T.  Also sum map S_dir_scatter / N_dir
-// (z precision in planar evidence, :572-587) and sum scan N.
-constexpr int kMfNV = 22;
-__global__ __launch_bounds__(kBlock) void k_mf_partial(const double* __restrict__ scan, const double* __restrict__ map,
-                                                       int B, double* partials) {
+// Standalone form (dense mode and the per-operator entry point): H terms over every bin plus the
+// map totals sum S_dir_scatter / sum N_dir (planar z precision, :572-587).  In the scale-mode
+// scan the H terms are fused into k_bins_scale and the map totals come from the pushforward.
+constexpr int kMfNV = 21;
+__global__ __launch_bounds__(kBlock) void k_mf(const double* __restrict__ scan, const double* __restrict__ map, int B,
+                                               double* partials, double* scalars, uint32_t* ticket) {
   __shared__ double lds[kWaves * kMfNV];
   double v[kMfNV];
 #pragma unroll
   for (int k = 0; k < kMfNV; ++k) v[k] = 0.0;
-  size_t Bs = (size_t)B;
+  const size_t Bs = (size_t)B;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
-    double Ns = scan[SF_N * Bs + b];
-    double sx = scan[(SF_SD) * Bs + b], sy = scan[(SF_SD + 1) * Bs + b], sz = scan[(SF_SD + 2) * Bs + b];
-    double Nm = map[MF_ND * Bs + b];
-    double mx = map[(MF_SD) * Bs + b], my = map[(MF_SD + 1) * Bs + b], mz = map[(MF_SD + 2) * Bs + b];
-    double wb = sqrt(Ns * Nm + kEpsMass);
-    double sn = sqrt(dot3_exact(sx, sy, sz, sx, sy, sz));
-    double mn = sqrt(dot3_exact(mx, my, mz, mx, my, mz));
-    double us[3] = {sx / (sn + kEpsMass), sy / (sn + kEpsMass), sz / (sn + kEpsMass)};
-    double um[3] = {mx / (mn + kEpsMass), my / (mn + kEpsMass), mz / (mn + kEpsMass)};
-    double conf = (sn * (1.0 / (Ns + kEpsMass))) * (mn * (1.0 / (Nm + kEpsMass)));
-    double wf = wb * conf;
+    mf_bin_term(scan[SF_N * Bs + b], scan[SF_SD * Bs + b], scan[(SF_SD + 1) * Bs + b], scan[(SF_SD + 2) * Bs + b], map,
+                B, b, v);
 #pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) v[3 * i + j] += wf * um[i] * us[j];
-    v[9] += wf;
-#pragma unroll
-    for (int k = 0; k < 9; ++k) v[10 + k] += map[(MF_S + k) * Bs + b];
-    v[19] += Nm;
-    v[20] += Ns;
+    for (int k = 0; k < 9; ++k) v[11 + k] += map[(MF_S + k) * Bs + b];
+    v[20] += map[MF_ND * Bs + b];
   }
   block_sum<kMfNV>(v, lds);
-  if (threadIdx.x == 0)
-    for (int k = 0; k < kMfNV; ++k) partials[(size_t)blockIdx.x * kMfNV + k] = v[k];
-}
-
-// final MF: reduce partials (fixed order) then 3x3 SVD and the det-fixed R_mf on one thread.
-__global__ __launch_bounds__(kBlock) void k_mf_final(const double* __restrict__ partials, int nblocks, double* scalars) {
-  __shared__ double lds[kWaves * kMfNV];
-  double v[kMfNV];
-#pragma unroll
-  for (int k = 0; k < kMfNV; ++k) v[k] = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += kBlock)
-#pragma unroll
-    for (int k = 0; k < kMfNV; ++k) v[k] += partials[(size_t)b * kMfNV + k];
-  block_sum<kMfNV>(v, lds);
+  if (!finish_blocks<kMfNV, 0u>(v, partials, ticket, lds)) return;
   if (threadIdx.x == 0) {
-    for (int k = 0; k < 9; ++k) scalars[SC_MF_H + k] = v[k];
-    scalars[SC_MF_NEFF] = v[9];
-    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[10 + k];
-    scalars[SC_MF_MAPND] = v[19];
-    scalars[SC_MF_SCANN] = v[20];
-    double U[9], s[3], V[9];
-    svd3(v, U, s, V);
-    // det fix of U's last column, matrix_fisher_evidence.py:217-222
-    double UVt[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) UVt[3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
-    double dt = det3(UVt);
-    double sg = dt > 0.0 ? 1.0 : (dt < 0.0 ? -1.0 : 0.0);
-    U[2] *= sg; U[5] *= sg; U[8] *= sg;
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j)
-        scalars[SC_MF_R + 3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
-    for (int k = 0; k < 3; ++k) scalars[SC_MF_S + k] = s[k];
-    for (int k = 0; k < 9; ++k) scalars[SC_MF_V + k] = V[k];
+    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[11 + k];
+    scalars[SC_MF_MAPND] = v[20];
+    mf_finish(v, scalars);
   }
 }
 
@@ -685,9 +819,9 @@ __global__ __launch_bounds__(kBlock) void k_mf_final(const double* __restrict__ 
 // Per bin (matrix_fisher_evidence.py:442-475): t_b = c_map - R p_scan,
 // S_b = Sigma_map + R Sigma_scan R^T, W_b = w_b inv(S_b + eps I); L += W_b, h += W_b t_b.
 constexpr int kPtNV = 13;
-__global__ __launch_bounds__(kBlock) void k_pt_partial(const double* __restrict__ scan, const double* __restrict__ map,
-                                                       const double* __restrict__ derived, int B,
-                                                       const double* __restrict__ scalars, double* partials) {
+__global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, const double* __restrict__ map,
+                                               const double* __restrict__ derived, int B, double* scalars,
+                                               double* partials, uint32_t* ticket) {
   __shared__ double lds[kWaves * kPtNV];
   double R[9];
 #pragma unroll
@@ -727,19 +861,7 @@ __global__ __launch_bounds__(kBlock) void k_pt_partial(const double* __restrict_
     v[12] += wb;
   }
   block_sum<kPtNV>(v, lds);
-  if (threadIdx.x == 0)
-    for (int k = 0; k < kPtNV; ++k) partials[(size_t)blockIdx.x * kPtNV + k] = v[k];
-}
-
-__global__ __launch_bounds__(kBlock) void k_pt_final(const double* __restrict__ partials, int nblocks, double* scalars) {
-  __shared__ double lds[kWaves * kPtNV];
-  double v[kPtNV];
-#pragma unroll
-  for (int k = 0; k < kPtNV; ++k) v[k] = 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += kBlock)
-#pragma unroll
-    for (int k = 0; k < kPtNV; ++k) v[k] += partials[(size_t)b * kPtNV + k];
-  block_sum<kPtNV>(v, lds);
+  if (!finish_blocks<kPtNV, 0u>(v, partials, ticket, lds)) return;
   if (threadIdx.x == 0) {
     for (int k = 0; k < 9; ++k) scalars[SC_PT_L + k] = v[k];
     for (int k = 0; k < 3; ++k) scalars[SC_PT_H + k] = v[9 + k];
@@ -773,8 +895,26 @@ __device__ __forceinline__ void derive_bin(const double* sd, double nd, double n
   for (int k = 0; k < 9; ++k) derived[(MD_SIG + k) * Bs + b] = sig[k];
 }
 
+// Map totals for the next scan's planar z precision (sum S_dir_scatter, sum N_dir over bins),
+// reduced in fixed order by the last block.
+constexpr int kTotNV = 10;
+__device__ __forceinline__ void map_totals_finish(double (&tot)[kTotNV], double* lds, double* partials,
+                                                  double* scalars, uint32_t* ticket) {
+  block_sum<kTotNV>(tot, lds);
+  if (!finish_blocks<kTotNV, 0u>(tot, partials, ticket, lds)) return;
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = tot[k];
+    scalars[SC_MF_MAPND] = tot[9];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict__ scan, double* map, double* derived,
-                                                        int B, PushArgs pa) {
+                                                        int B, PushArgs pa, double* partials, double* scalars,
+                                                        uint32_t* ticket) {
+  __shared__ double lds[kWaves * kTotNV];
+  double tot[kTotNV];
+#pragma unroll
+  for (int k = 0; k < kTotNV; ++k) tot[k] = 0.0;
   const size_t Bs = (size_t)B;
   const double* R = pa.R;
   const double g = pa.gamma;
@@ -809,13 +949,16 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           double v = RS[3 * i] * R[3 * j] + RS[3 * i + 1] * R[3 * j + 1] + RS[3 * i + 2] * R[3 * j + 2];
-          map[(MF_S + 3 * i + j) * Bs + b] = g * map[(MF_S + 3 * i + j) * Bs + b] + v;
+          double sn = g * map[(MF_S + 3 * i + j) * Bs + b] + v;
+          map[(MF_S + 3 * i + j) * Bs + b] = sn;
+          tot[3 * i + j] += sn;
         }
     }
     const double nd = g * map[MF_ND * Bs + b] + N;
     const double np = g * map[MF_NP * Bs + b] + N;
     map[MF_ND * Bs + b] = nd;
     map[MF_NP * Bs + b] = np;
+    tot[9] += nd;
     double sp[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -848,17 +991,25 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
     }
     derive_bin(sd, nd, np, sp, spp, derived, Bs, b);
   }
+  map_totals_finish(tot, lds, partials, scalars, ticket);
 }
 
-// derived stats from map sufficient stats only (used after set_map / reset)
-__global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict__ map, double* derived, int B) {
+// derived stats + map totals from map sufficient stats only (used after set_map / reset)
+__global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict__ map, double* derived, int B,
+                                                       double* partials, double* scalars, uint32_t* ticket) {
+  __shared__ double lds[kWaves * kTotNV];
+  double tot[kTotNV];
+#pragma unroll
+  for (int k = 0; k < kTotNV; ++k) tot[k] = 0.0;
   const size_t Bs = (size_t)B;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
     double sd[3], sp[3], spp[9];
     for (int k = 0; k < 3; ++k) { sd[k] = map[(MF_SD + k) * Bs + b]; sp[k] = map[(MF_SP + k) * Bs + b]; }
-    for (int k = 0; k < 9; ++k) spp[k] = map[(MF_SPP + k) * Bs + b];
+    for (int k = 0; k < 9; ++k) { spp[k] = map[(MF_SPP + k) * Bs + b]; tot[k] += map[(MF_S + k) * Bs + b]; }
+    tot[9] += map[MF_ND * Bs + b];
     derive_bin(sd, map[MF_ND * Bs + b], map[MF_NP * Bs + b], sp, spp, derived, Bs, b);
   }
+  map_totals_finish(tot, lds, partials, scalars, ticket);
 }
 
 // ---------------------------------------------------------------- launchers
@@ -867,91 +1018,86 @@ static int grid_for(long n, int cap_blocks) {
   if (g < 1) g = 1;
   return (int)(g > cap_blocks ? cap_blocks : g);
 }
+int push_blocks(int n_bins) { return grid_for(n_bins, 4096); }
 
-hipError_t launch_budget(const double* w, int n_raw, int stride, double* partials, int nblk, double* scalars,
-                         hipStream_t s) {
-  hipLaunchKernelGGL(k_budget_partial, dim3(nblk), dim3(kBlock), 0, s, w, n_raw, stride, partials);
-  hipLaunchKernelGGL(k_budget_final, dim3(1), dim3(kBlock), 0, s, (const double*)partials, nblk, scalars);
+hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  hipExtLaunchKernelGGL(k_budget, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a);
   return hipGetLastError();
 }
 
-hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, hipStream_t s) {
+hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, hipStream_t s, hipEvent_t e0,
+                         hipEvent_t e1) {
   if (scale) {
     switch (a.k) {
-      case 8: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<true, 8>), dim3(nblk), dim3(kBlock), 0, s, a, partials); break;
-      case 16: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<true, 16>), dim3(nblk), dim3(kBlock), 0, s, a, partials); break;
-      case 32: hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<true, 32>), dim3(nblk), dim3(kBlock), 0, s, a, partials); break;
+      case 8: hipExtLaunchKernelGGL(k_points<true, 8>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials); break;
+      case 16: hipExtLaunchKernelGGL(k_points<true, 16>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials); break;
+      case 32: hipExtLaunchKernelGGL(k_points<true, 32>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials); break;
       default: return hipErrorInvalidValue;
     }
   } else {
-    hipLaunchKernelGGL(HIP_KERNEL_NAME(k_points<false, 1>), dim3(nblk), dim3(kBlock), 0, s, a, partials);
+    hipExtLaunchKernelGGL(k_points<false, 1>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
   }
-  // per-point cert partials -> scalars[SC_DESKEW_WIN..]: (sum wb, sum wn^2, sum wout, sum H, max r)
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_partials_final<5, 16u>), dim3(1), dim3(kBlock), 0, s, (const double*)partials,
-                     nblk, a.scalars, (int)SC_DESKEW_WIN);
   return hipGetLastError();
 }
 
-hipError_t launch_bucketing(uint32_t* counts, uint32_t* starts, uint32_t* tile_sums, const uint32_t* keys,
-                            const uint32_t* slots, int n, int n_bins, uint32_t* sorted, uint32_t* big_list,
-                            uint32_t* big_n, hipStream_t s) {
-  int tiles = (n_bins + kScanTile - 1) / kScanTile;
-  hipLaunchKernelGGL(k_scan_tiles, dim3(tiles), dim3(kBlock), 0, s, (const uint32_t*)counts, n_bins, tile_sums);
-  hipLaunchKernelGGL(k_scan_apply, dim3(tiles), dim3(kBlock), 0, s, (const uint32_t*)counts, n_bins,
-                     (const uint32_t*)tile_sums, starts);
-  hipLaunchKernelGGL(k_place, dim3(grid_for(n, 2048)), dim3(kBlock), 0, s, keys, slots, (const uint32_t*)starts, n,
-                     n_bins, sorted);
-  hipLaunchKernelGGL(k_bucket_order, dim3(grid_for(n_bins, 2048)), dim3(kBlock), 0, s, (const uint32_t*)counts,
-                     (const uint32_t*)starts, n_bins, sorted, big_list, big_n);
-  hipLaunchKernelGGL(k_bucket_big, dim3(64), dim3(kBlock), 0, s, keys, n, (const uint32_t*)starts,
-                     (const uint32_t*)big_list, (const uint32_t*)big_n, sorted);
+int scan_tiles(int n_bins) { return (n_bins + kScanTile - 1) / kScanTile; }
+
+hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  hipExtLaunchKernelGGL(k_scan, dim3(scan_tiles(b.n_bins)), dim3(kBlock), 0, s, e0, nullptr, 0,
+                        (const uint32_t*)b.counts, b.n_bins, b.scan_status, b.scan_ticket, b.starts);
+  hipLaunchKernelGGL(k_place, dim3(grid_for(n, 2048)), dim3(kBlock), 0, s, (const uint32_t*)b.keys,
+                     (const uint32_t*)b.slots, (const uint32_t*)b.starts, n, b.n_bins, b.slot_idx);
+  hipLaunchKernelGGL(k_bucket_rank, dim3((b.n_bins + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b);
+  hipLaunchKernelGGL(k_bucket_mid, dim3(256), dim3(kBlock), 0, s, b, n);
+  hipExtLaunchKernelGGL(k_gather, dim3(grid_for(n, 2048)), dim3(kBlock), 0, s, nullptr, e1, 0,
+                        (const uint32_t*)b.keys, (const uint32_t*)b.dest, n, b.n_bins, (const PointRec*)b.recs,
+                        b.recs_s);
   return hipGetLastError();
 }
 
 int bins_scale_blocks(int n_bins) { return (n_bins + kTile - 1) / kTile; }
+int bins_partial_nv() { return kBinNV; }
 
-hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s) {
-  int nblk = bins_scale_blocks(a.n_bins);
-  hipLaunchKernelGGL(k_bins_scale, dim3(nblk), dim3(kBlock), 0, s, a, partials);
+hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  hipExtLaunchKernelGGL(k_bins_scale, dim3(bins_scale_blocks(a.n_bins)), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
   return hipGetLastError();
 }
 
-hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* partials, hipStream_t s) {
+hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* partials, hipStream_t s, hipEvent_t e0,
+                        hipEvent_t e1) {
   int nchunks = (a.cap + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_dense_accum, dim3(nchunks), dim3(kBlock), 0, s, a, bin_partials);
+  hipExtLaunchKernelGGL(k_dense_accum, dim3(nchunks), dim3(kBlock), 0, s, e0, nullptr, 0, a, bin_partials);
   int nblk = (a.n_bins + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(k_dense_finalize, dim3(nblk), dim3(kBlock), 0, s, a, (const double*)bin_partials, nchunks, partials);
-  return hipGetLastError();
-}
-
-hipError_t launch_bin_cert_final(const double* partials, int nblk, double* scalars, hipStream_t s) {
-  hipLaunchKernelGGL(HIP_KERNEL_NAME(k_partials_final<5, 16u>), dim3(1), dim3(kBlock), 0, s, partials, nblk, scalars,
-                     (int)SC_BIN_NSUM);
+  hipExtLaunchKernelGGL(k_dense_finalize, dim3(nblk), dim3(kBlock), 0, s, nullptr, e1, 0, a,
+                        (const double*)bin_partials, nchunks, partials);
   return hipGetLastError();
 }
 
 hipError_t launch_mf(const double* scan, const double* map, int B, double* partials, int nblk, double* scalars,
-                     hipStream_t s) {
-  hipLaunchKernelGGL(k_mf_partial, dim3(nblk), dim3(kBlock), 0, s, scan, map, B, partials);
-  hipLaunchKernelGGL(k_mf_final, dim3(1), dim3(kBlock), 0, s, (const double*)partials, nblk, scalars);
+                     uint32_t* ticket, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  hipExtLaunchKernelGGL(k_mf, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, scan, map, B, partials, scalars, ticket);
   return hipGetLastError();
 }
 
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, hipStream_t s) {
-  hipLaunchKernelGGL(k_pt_partial, dim3(nblk), dim3(kBlock), 0, s, scan, map, derived, B, (const double*)scalars, partials);
-  hipLaunchKernelGGL(k_pt_final, dim3(1), dim3(kBlock), 0, s, (const double*)partials, nblk, scalars);
+                     double* scalars, uint32_t* ticket, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, scan, map, derived, B, scalars, partials,
+                        ticket);
   return hipGetLastError();
 }
 
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
-                              hipStream_t s) {
-  hipLaunchKernelGGL(k_pushforward, dim3(grid_for(B, 4096)), dim3(kBlock), 0, s, scan, map, derived, B, pa);
+                              double* partials, double* scalars, uint32_t* ticket, hipStream_t s, hipEvent_t e0,
+                              hipEvent_t e1) {
+  hipExtLaunchKernelGGL(k_pushforward, dim3(push_blocks(B)), dim3(kBlock), 0, s, e0, e1, 0, scan, map, derived, B, pa,
+                        partials, scalars, ticket);
   return hipGetLastError();
 }
 
-hipError_t launch_map_derive(const double* map, double* derived, int B, hipStream_t s) {
-  hipLaunchKernelGGL(k_map_derive, dim3(grid_for(B, 4096)), dim3(kBlock), 0, s, map, derived, B);
+hipError_t launch_map_derive(const double* map, double* derived, int B, double* partials, double* scalars,
+                             uint32_t* ticket, hipStream_t s) {
+  hipLaunchKernelGGL(k_map_derive, dim3(push_blocks(B)), dim3(kBlock), 0, s, map, derived, B, partials, scalars,
+                     ticket);
   return hipGetLastError();
 }
 

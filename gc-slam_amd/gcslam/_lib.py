@@ -158,5 +158,7 @@ def belief_to_struct(X_anchor, stamp, z_lin, L, h) -> GcsBelief:
 
 
 def struct_to_arrays(b: GcsBelief):
-    return (np.array(b.X_anchor[:]), float(b.stamp_sec), np.array(b.z_lin[:]),
-            np.array(b.L[:]).reshape(D_Z, D_Z), np.array(b.h[:]))
+    """Copy a belief struct out as numpy arrays (buffer views, no per-element Python floats)."""
+    view = np.ctypeslib.as_array
+    return (view(b.X_anchor).copy(), float(b.stamp_sec), view(b.z_lin).copy(),
+            view(b.L).reshape(D_Z, D_Z).copy(), view(b.h).copy())

@@ -120,8 +120,17 @@ class HypothesisContext:
         self._chk(self.lib.gcs_ctx_get_iw_state(self.h, L.dptr(nu), L.dptr(Psi), L.dptr(Q)), "get_iw_state")
         return nu, Psi.reshape(7, 6, 6), Q.reshape(22, 22)
 
-    def enable_timing(self, on=True):
-        self._chk(self.lib.gcs_ctx_enable_timing(self.h, int(on)), "enable_timing")
+    STAGES = ("points", "sort_bucket", "bins", "matrix_fisher", "planar", "pushforward")
+
+    def enable_timing(self, on=True, stages=None):
+        """Device stage timing (hipEvents stamped by the stage kernels).  stages: names from
+        STAGES to time (default all); on=False turns timing off."""
+        mask = 0
+        if on:
+            names = self.STAGES if stages is None else stages
+            for s in names:
+                mask |= 1 << self.STAGES.index(s)
+        self._chk(self.lib.gcs_ctx_enable_timing(self.h, mask), "enable_timing")
 
     def stage_times(self, reset=False):
         ms = np.zeros(6)
@@ -221,14 +230,16 @@ class HypothesisContext:
 
     # ------------------------------------------------------------------ hypotheses
     def hypothesis_payload(self, w_iw, w_bary):
-        p = np.zeros(L.PAYLOAD_LEN)
+        """Packed 840-f64 all-reduce payload of this hypothesis (a fresh array per call)."""
+        p = np.empty(L.PAYLOAD_LEN)
         self._chk(self.lib.gcs_hypothesis_payload(self.h, float(w_iw), float(w_bary), L.dptr(p)), "payload")
         return p
 
-    def hypothesis_combine(self, payload_sum, scan_count):
+    def hypothesis_combine(self, payload_sum, scan_count, want_belief=True):
+        """Barycenter + IW update from the summed payload; returns (belief arrays or None, cert)."""
         p = np.ascontiguousarray(payload_sum, np.float64)
         b = L.GcsBelief()
-        cert = np.zeros(4)
+        cert = np.empty(4)
         self._chk(self.lib.gcs_hypothesis_combine(self.h, L.dptr(p), int(scan_count), C.byref(b), L.dptr(cert)),
                   "combine")
-        return L.struct_to_arrays(b), cert
+        return (L.struct_to_arrays(b) if want_belief else None), cert

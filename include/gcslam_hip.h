@@ -119,9 +119,11 @@ int gcs_ctx_destroy(gcs_ctx* ctx);
 const char* gcs_last_error(const gcs_ctx* ctx);
 int gcs_ctx_set_stream(gcs_ctx* ctx, void* hip_stream);
 int gcs_ctx_synchronize(gcs_ctx* ctx);
-/* device stage timing with hipEvents on the context stream: stages
- * [0 budget+points, 1 sort+bucket, 2 bin moment-match kernel, 3 MF, 4 planar, 5 pushforward] */
-int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t on);
+/* device stage timing: hipEvents stamped by the stages' own kernel dispatches on the context
+ * stream.  stage_mask bit s enables stage s (0 = off): [0 budget+points, 1 sort+bucket,
+ * 2 bin moment-match kernel (+ fused Matrix-Fisher in scale mode), 3 MF (dense / per-op),
+ * 4 planar, 5 pushforward].  Each timed stage costs a few us of queue time. */
+int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
 int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*6*/, int64_t* counts /*6*/, int32_t reset);
 int gcs_ctx_set_atlas(gcs_ctx* ctx, const double* dirs_host /*B*3*/);
 int gcs_ctx_get_atlas(gcs_ctx* ctx, double* dirs_host /*B*3*/, int32_t* knn_host /*B*K*/);

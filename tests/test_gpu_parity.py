@@ -259,10 +259,11 @@ def test_bitwise_determinism_scale():
         assert np.array_equal(a, b)
 
 
-def test_degenerate_same_direction_points():
-    """All points on one ray (one giant bucket) and zero-weight points."""
-    ctx = _ctx(n_bins=20000, n_points_cap=4096, mode="scale")
-    n = 4096
+@pytest.mark.parametrize("n", [4096, 12288])
+def test_degenerate_same_direction_points(n):
+    """All points on one ray (one giant bucket: ranked in-wave at 4096, compacted at 12288)
+    and zero-weight points."""
+    ctx = _ctx(n_bins=20000, n_points_cap=n, mode="scale")
     p = np.tile(np.array([[5.0, 1.0, 0.5]], np.float32), (n, 1))
     rec = np.zeros((n, 4), np.float32)
     rec[:, :3] = p
