@@ -204,5 +204,66 @@ void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& 
     std::copy(lists[c].begin(), lists[c].end(), pools.begin() + (size_t)c * width);
 }
 
+namespace {
+// Hilbert index of (x, y) on an n x n grid (n a power of two)
+uint64_t hilbert_d(uint32_t n, uint32_t x, uint32_t y) {
+  uint64_t d = 0;
+  for (uint32_t s = n / 2; s > 0; s /= 2) {
+    uint32_t rx = (x & s) > 0, ry = (y & s) > 0;
+    d += (uint64_t)s * s * ((3 * rx) ^ ry);
+    if (ry == 0) {
+      if (rx == 1) { x = s - 1 - x; y = s - 1 - y; }
+      std::swap(x, y);
+    }
+  }
+  return d;
+}
+}  // namespace
+
+void hilbert_order(const double* dirs, int B, std::vector<int>& order) {
+  const uint32_t n = 1u << 15;
+  std::vector<uint64_t> key(B);
+  for (int b = 0; b < B; ++b) {
+    const double* d = dirs + 3 * b;
+    double ax = fabs(d[0]), ay = fabs(d[1]), az = fabs(d[2]);
+    int f;
+    double m, u, v;
+    if (ax >= ay && ax >= az) { f = d[0] >= 0.0 ? 0 : 1; m = ax; u = d[1]; v = d[2]; }
+    else if (ay >= az) { f = d[1] >= 0.0 ? 2 : 3; m = ay; u = d[0]; v = d[2]; }
+    else { f = d[2] >= 0.0 ? 4 : 5; m = az; u = d[0]; v = d[1]; }
+    if (!(m > 0.0)) { m = 1.0; u = v = 0.0; }
+    auto q = [&](double x) {
+      long c = (long)floor((x / m + 1.0) * 0.5 * n);
+      return (uint32_t)std::min<long>(std::max<long>(c, 0), n - 1);
+    };
+    key[b] = ((uint64_t)f << 40) | hilbert_d(n, q(u), q(v));
+  }
+  order.resize(B);
+  for (int b = 0; b < B; ++b) order[b] = b;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int c) { return key[a] < key[c]; });
+}
+
+int tile_sources(const std::vector<int>& off, const std::vector<int>& idx, int B, int tile, std::vector<int>& src_off,
+                 std::vector<int>& src, std::vector<uint16_t>& local) {
+  const int nt = (B + tile - 1) / tile;
+  src_off.assign(nt + 1, 0);
+  src.clear();
+  local.assign(idx.size(), 0);
+  int most = 0;
+  std::vector<int> u;
+  for (int t = 0; t < nt; ++t) {
+    const int b0 = t * tile, b1 = std::min(B, b0 + tile);
+    u.assign(idx.begin() + off[b0], idx.begin() + off[b1]);
+    std::sort(u.begin(), u.end());
+    u.erase(std::unique(u.begin(), u.end()), u.end());
+    for (int q = off[b0]; q < off[b1]; ++q)
+      local[q] = (uint16_t)(std::lower_bound(u.begin(), u.end(), idx[q]) - u.begin());
+    src.insert(src.end(), u.begin(), u.end());
+    src_off[t + 1] = (int)src.size();
+    most = std::max(most, (int)u.size());
+  }
+  return most;
+}
+
 }  // namespace atlas
 }  // namespace gcs

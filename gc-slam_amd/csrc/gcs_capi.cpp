@@ -37,8 +37,15 @@ struct gcs_ctx {
   int* d_rknn_off = nullptr;
   int* d_rknn = nullptr;
   int* d_pools = nullptr;
-  std::vector<double> dirs_host;
-  std::vector<int> knn_host;
+  std::vector<double> dirs_host;  // reference order
+  std::vector<int> knn_host;      // reference rows and ids
+  // device bin order (scale mode: Hilbert patches; dense: identity); order[dev] = reference id
+  std::vector<int> order, inv;
+  int* d_bin_ref = nullptr;  // device -> reference id (nearest / candidate ids reported in reference ids)
+  int* d_tile_src_off = nullptr;
+  int* d_tile_src = nullptr;
+  uint16_t* d_rknn_local = nullptr;
+  int max_tile_src = 0;
   // per-point
   PointRec* d_recs = nullptr;
   PointRec* d_recs_s = nullptr;  // bucket order (scale mode)
@@ -122,9 +129,7 @@ StageEv stage_ev(gcs_ctx* c, int st) {
   }
   return e;
 }
-uint32_t* ticket(gcs_ctx* c, int tk) { return c->d_tickets + (size_t)tk * kTicketStride; }
-// partials: nblocks*NV plus the group partials (nblocks/64 + 1)*NV
-size_t partials_need(long nblocks, int nv) { return (size_t)(nblocks + nblocks / 64 + 2) * nv; }
+size_t partials_need(long nblocks, int nv) { return (size_t)nblocks * nv; }
 
 void to_host_belief(const gcs_belief& in, Belief& b) {
   memcpy(b.X_anchor, in.X_anchor, sizeof(b.X_anchor));
@@ -142,26 +147,74 @@ void from_host_belief(const Belief& b, gcs_belief& out) {
   memcpy(out.h, b.h, sizeof(b.h));
 }
 
+template <class T>
+int upload(gcs_ctx* c, T*& dst, const std::vector<T>& src) {
+  if (dst) (void)hipFree(dst);
+  dst = nullptr;
+  HIPCHK(c, hipMalloc(&dst, std::max<size_t>(1, src.size()) * sizeof(T)));
+  if (!src.empty()) HIPCHK(c, hipMemcpy(dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+  return GCS_OK;
+}
+
+// Reference-order field-major rows (F x B) <-> device bin order
+void to_device_order(const gcs_ctx* c, int F, const double* ref, double* dev) {
+  const size_t B = c->B;
+  for (int f = 0; f < F; ++f)
+    for (size_t i = 0; i < B; ++i) dev[f * B + i] = ref[f * B + c->order[i]];
+}
+void to_reference_order(const gcs_ctx* c, int F, const double* dev, double* ref) {
+  const size_t B = c->B;
+  for (int f = 0; f < F; ++f)
+    for (size_t i = 0; i < B; ++i) ref[f * B + c->order[i]] = dev[f * B + i];
+}
+
 int upload_atlas(gcs_ctx* c) {
   const int B = c->B, K = c->K;
+  const bool scale = c->cfg.mode == GCS_MODE_SCALE;
+  // device order: Hilbert patches in scale mode (k_bins_scale tiles), identity in dense mode
+  if (scale) {
+    atlas::hilbert_order(c->dirs_host.data(), B, c->order);
+  } else {
+    c->order.resize(B);
+    for (int b = 0; b < B; ++b) c->order[b] = b;
+  }
+  c->inv.assign(B, 0);
+  for (int i = 0; i < B; ++i) c->inv[c->order[i]] = i;
   std::vector<double> d4((size_t)B * 4, 0.0);
-  for (int b = 0; b < B; ++b)
-    for (int k = 0; k < 3; ++k) d4[(size_t)b * 4 + k] = c->dirs_host[(size_t)b * 3 + k];
+  for (int i = 0; i < B; ++i)
+    for (int k = 0; k < 3; ++k) d4[(size_t)i * 4 + k] = c->dirs_host[(size_t)c->order[i] * 3 + k];
   HIPCHK(c, hipMemcpy(c->d_bin_dirs, d4.data(), d4.size() * sizeof(double), hipMemcpyHostToDevice));
-  if (c->cfg.mode == GCS_MODE_SCALE) {
+  if (int rc = upload(c, c->d_bin_ref, c->order)) return rc;
+  if (scale) {
+    // candidate rule on reference ids (ties -> lower reference id), then renamed to device ids
     c->knn_host.assign((size_t)B * K, 0);
     atlas::knn(c->dirs_host.data(), B, K, c->knn_host.data());
+    std::vector<int> knn_dev((size_t)B * K);
+    for (int i = 0; i < B; ++i)
+      for (int k = 0; k < K; ++k) knn_dev[(size_t)i * K + k] = c->inv[c->knn_host[(size_t)c->order[i] * K + k]];
     std::vector<int> off, idx, pools;
-    atlas::reverse(c->knn_host.data(), B, K, off, idx);
+    atlas::reverse(knn_dev.data(), B, K, off, idx);
+    std::vector<int> src_off, src;
+    std::vector<uint16_t> local;
+    c->max_tile_src = atlas::tile_sources(off, idx, B, bins_tile(), src_off, src, local);
+    if (c->max_tile_src > bins_max_tile_sources())
+      return fail(c, GCS_ERR_ARG, "bin atlas too irregular for the tiled bin kernel (tile source list too long)");
+    for (int b0 = 0; b0 < B; b0 += bins_tile())
+      if (off[std::min(B, b0 + bins_tile())] - off[b0] > bins_max_tile_entries())
+        return fail(c, GCS_ERR_ARG, "bin atlas too irregular for the tiled bin kernel (tile reverse-kNN list too long)");
     c->G = atlas::grid_for_bins(B);
     c->ncell = 6 * c->G * c->G;
+    // pools keep ascending reference ids (exact nearest-bin tie rule) and hold device ids
     atlas::cell_pools(c->dirs_host.data(), B, c->G, pools, c->pool_width);
-    if (c->d_pools) (void)hipFree(c->d_pools);
-    HIPCHK(c, hipMalloc(&c->d_pools, pools.size() * sizeof(int)));
-    HIPCHK(c, hipMemcpy(c->d_pools, pools.data(), pools.size() * sizeof(int), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemcpy(c->d_knn, c->knn_host.data(), c->knn_host.size() * sizeof(int), hipMemcpyHostToDevice));
+    for (int& id : pools)
+      if (id >= 0) id = c->inv[id];
+    if (int rc = upload(c, c->d_pools, pools)) return rc;
+    HIPCHK(c, hipMemcpy(c->d_knn, knn_dev.data(), knn_dev.size() * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_rknn_off, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_rknn, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
+    if (int rc = upload(c, c->d_tile_src_off, src_off)) return rc;
+    if (int rc = upload(c, c->d_tile_src, src)) return rc;
+    if (int rc = upload(c, c->d_rknn_local, local)) return rc;
   }
   return GCS_OK;
 }
@@ -184,7 +237,6 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   ba.stride = stride;
   ba.partials = c->d_partials;
   ba.scalars = c->d_scalars;
-  ba.ticket = ticket(c, TK_BUDGET);
   ba.zero32 = c->d_counts;  // counts only: the bucketing scratch after them is re-armed by k_bins_scale
   ba.n_zero32 = c->d_counts ? c->B : 0;
   ba.zero8 = c->d_flags;
@@ -216,11 +268,10 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.slots = c->d_slots;
   a.counts = c->d_counts;
   a.scalars = c->d_scalars;
-  a.ticket = ticket(c, TK_POINTS);
   a.p0_out = p0_out;
   a.w_out = w_out;
   a.w_budget_out = wb_out;
-  a.nearest_out = c->d_nearest;
+  a.nearest_out = c->d_nearest;  // device ids
   HIPCHK(c, launch_points(a, c->cfg.mode == GCS_MODE_SCALE, c->d_partials, red_blocks(c->cap), s, nullptr, ev.e1));
   return GCS_OK;
 }
@@ -234,6 +285,9 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   b.flags = c->d_flags;
   b.rknn_off = c->d_rknn_off;
   b.rknn = c->d_rknn;
+  b.rknn_local = c->d_rknn_local;
+  b.tile_src_off = c->d_tile_src_off;
+  b.tile_src = c->d_tile_src;
   b.bin_dirs = c->d_bin_dirs;
   b.map = c->d_map;
   b.n_bins = c->B;
@@ -242,7 +296,6 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   b.tau = c->cfg.tau;
   b.scan = c->d_scan;
   b.scalars = c->d_scalars;
-  b.ticket = ticket(c, c->cfg.mode == GCS_MODE_SCALE ? TK_BINS : TK_DENSE);
   if (c->d_counts) {
     b.zero_after = c->d_counts + c->B;
     b.n_zero_after = c->n_counts_words - c->B;
@@ -266,7 +319,7 @@ int stage_bins(gcs_ctx* c) {
       ba.recs = c->d_recs;
       ba.starts = c->d_starts;
       ba.scan_status = c->d_counts + c->B + 2;
-      ba.scan_ticket = ticket(c, TK_SCAN);
+      ba.scan_ticket = c->d_tickets;
       ba.slot_idx = c->d_sorted;
       ba.dest = c->d_slots;  // slots are consumed by k_place before k_bucket_rank writes destinations
       ba.recs_s = c->d_recs_s;
@@ -276,7 +329,7 @@ int stage_bins(gcs_ctx* c) {
       HIPCHK(c, launch_bucketing(ba, c->cap, s, ev.e0, ev.e1));
     }
     StageEv ev = stage_ev(c, ST_BINS);
-    HIPCHK(c, launch_bins_scale(b, c->d_partials, s, ev.e0, ev.e1));
+    HIPCHK(c, launch_bins_scale(b, c->d_partials, s, ev.e0, ev.e1, nullptr));  // stage = the bin kernel itself
   } else {
     StageEv ev = stage_ev(c, ST_BINS);
     HIPCHK(c, launch_dense(b, c->d_bin_partials, c->d_partials, s, ev.e0, ev.e1));
@@ -286,15 +339,15 @@ int stage_bins(gcs_ctx* c) {
 
 int stage_mf(gcs_ctx* c) {
   StageEv ev = stage_ev(c, ST_MF);
-  HIPCHK(c, launch_mf(c->d_scan, c->d_map, c->B, c->d_partials, red_blocks(c->B), c->d_scalars, ticket(c, TK_MF),
-                      c->stream, ev.e0, ev.e1));
+  HIPCHK(c, launch_mf(c->d_scan, c->d_map, c->B, c->d_partials, red_blocks(c->B), c->d_scalars, c->stream, ev.e0,
+                      ev.e1));
   return GCS_OK;
 }
 
 int stage_pt(gcs_ctx* c) {
   StageEv ev = stage_ev(c, ST_PT);
   HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
-                      ticket(c, TK_PT), c->stream, ev.e0, ev.e1));
+                      c->stream, ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -317,8 +370,8 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) 
     for (int j = 0; j < 3; ++j) pa.G[3 * i + j] = RS[3 * i] * pa.R[3 * j] + RS[3 * i + 1] * pa.R[3 * j + 1] + RS[3 * i + 2] * pa.R[3 * j + 2];
   pa.gamma = gamma;
   StageEv ev = stage_ev(c, ST_PUSH);
-  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->d_partials, c->d_scalars,
-                               ticket(c, TK_PUSH), c->stream, ev.e0, ev.e1));
+  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->d_partials, c->d_scalars, c->stream,
+                               ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -376,8 +429,8 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
-  if (bad(hipMalloc(&c->d_tickets, (size_t)TK_COUNT * kTicketStride * sizeof(uint32_t)))) return GCS_ERR_HIP;
-  if (bad(hipMemset(c->d_tickets, 0, (size_t)TK_COUNT * kTicketStride * sizeof(uint32_t)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_tickets, sizeof(uint32_t)))) return GCS_ERR_HIP;
+  if (bad(hipMemset(c->d_tickets, 0, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocDefault))) return GCS_ERR_HIP;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
@@ -403,7 +456,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     gcs_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
-  if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, ticket(c, TK_PUSH),
+  if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars,
                             c->stream)))
     return GCS_ERR_HIP;
   if (bad(hipStreamSynchronize(c->stream))) return GCS_ERR_HIP;
@@ -420,6 +473,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
   void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_mid_list, c->d_flags, c->d_recs_s, c->d_tickets,
+                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -493,26 +547,40 @@ int gcs_ctx_get_belief(gcs_ctx* c, gcs_belief* b) {
 
 int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
   if (!c || !map) return GCS_ERR_ARG;
-  HIPCHK(c, hipMemcpyAsync(c->d_map, map, (size_t)c->B * MF_COUNT * sizeof(double), hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, ticket(c, TK_PUSH),
+  std::vector<double> dev((size_t)c->B * MF_COUNT);
+  to_device_order(c, MF_COUNT, map, dev.data());
+  HIPCHK(c, hipMemcpy(c->d_map, dev.data(), dev.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars,
                               c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
 }
 
+int pull_rows(gcs_ctx* c, const double* dev_src, int F, double* ref_out) {
+  std::vector<double> dev((size_t)c->B * F);
+  HIPCHK(c, hipMemcpyAsync(dev.data(), dev_src, dev.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  to_reference_order(c, F, dev.data(), ref_out);
+  return GCS_OK;
+}
+
 int gcs_ctx_get_map(gcs_ctx* c, double* map, double* derived) {
   if (!c) return GCS_ERR_ARG;
-  if (map) HIPCHK(c, hipMemcpyAsync(map, c->d_map, (size_t)c->B * MF_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  if (map)
+    if (int rc = pull_rows(c, c->d_map, MF_COUNT, map)) return rc;
   if (derived)
-    HIPCHK(c, hipMemcpyAsync(derived, c->d_derived, (size_t)c->B * MD_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rc = pull_rows(c, c->d_derived, MD_COUNT, derived)) return rc;
   return GCS_OK;
 }
 
 int gcs_ctx_get_scan_stats(gcs_ctx* c, double* scan) {
   if (!c || !scan) return GCS_ERR_ARG;
-  HIPCHK(c, hipMemcpyAsync(scan, c->d_scan, (size_t)c->B * SF_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return pull_rows(c, c->d_scan, SF_COUNT, scan);
+}
+
+int gcs_ctx_get_bin_order(gcs_ctx* c, int32_t* order) {
+  if (!c || !order) return GCS_ERR_ARG;
+  for (int i = 0; i < c->B; ++i) order[i] = c->order[i];
   return GCS_OK;
 }
 
@@ -541,14 +609,24 @@ int gcs_ctx_get_iw_state(gcs_ctx* c, double* nu, double* Psi, double* Q) {
 }
 
 // ---------------------------------------------------------------- per-operator entry points
+namespace {
+__global__ void k_ref_ids(const int* dev_ids, const int* bin_ref, int n, int* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = bin_ref[dev_ids[i]];
+}
+}  // namespace
+
 int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const double* t, const double* w, int32_t n,
                     double t0, double t1, const double* xi, double* p0_dev, double* w_out_dev, double* w_budget_dev,
                     int32_t* nearest_dev, double* cert) {
   if (!c || !xi) return GCS_ERR_ARG;
   int rc = stage_points(c, xyz, point_step, t, w, n, t0, t1, xi, p0_dev, w_out_dev, w_budget_dev);
   if (rc) return rc;
-  if (nearest_dev)
-    HIPCHK(c, hipMemcpyAsync(nearest_dev, c->d_nearest, (size_t)c->cap * sizeof(int), hipMemcpyDeviceToDevice, c->stream));
+  if (nearest_dev) {  // reported in reference bin ids
+    hipLaunchKernelGGL(k_ref_ids, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, (const int*)c->d_nearest,
+                       (const int*)c->d_bin_ref, c->cap, nearest_dev);
+    HIPCHK(c, hipGetLastError());
+  }
   if ((rc = pull_scalars(c))) return rc;
   if (cert)
     for (int k = 0; k < 8; ++k) cert[k] = c->h_scalars[k];
@@ -556,19 +634,20 @@ int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const doubl
 }
 
 namespace {
-__global__ void k_materialize(const PointRec* recs, const int* nearest, const int* knn, const double* bin_dirs, int cap,
-                              int B, int K, bool scale, double ox, double oy, double oz, double tau, int* ids, double* r) {
+__global__ void k_materialize(const PointRec* recs, const int* nearest, const int* knn, const double* bin_dirs,
+                              const int* bin_ref, int cap, int B, int K, bool scale, double ox, double oy, double oz,
+                              double tau, int* ids, double* r) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
   PointRec pr = recs[i];
   double d0 = pr.dx, d1 = pr.dy, d2 = pr.dz;
   double it = 1.0 / tau;
   if (scale) {
-    const int* row = knn + (size_t)nearest[i] * K;
+    const int* row = knn + (size_t)nearest[i] * K;  // d_nearest holds device ids
     for (int k = 0; k < K; ++k) {
       const double* bd = bin_dirs + 4 * (size_t)row[k];
       double s = dot3_exact(d0, d1, d2, bd[0], bd[1], bd[2]);
-      if (ids) ids[(size_t)i * K + k] = row[k];
+      if (ids) ids[(size_t)i * K + k] = bin_ref[row[k]];
       if (r) r[(size_t)i * K + k] = exp((s - pr.m) * it) * pr.iz;
     }
   } else {
@@ -585,7 +664,8 @@ int gcs_bin_soft_assign(gcs_ctx* c, int32_t* ids, double* r) {
   if (!c) return GCS_ERR_ARG;
   bool scale = c->cfg.mode == GCS_MODE_SCALE;
   hipLaunchKernelGGL(k_materialize, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, (const PointRec*)c->d_recs,
-                     (const int*)c->d_nearest, (const int*)c->d_knn, (const double*)c->d_bin_dirs, c->cap, c->B, c->K,
+                     (const int*)c->d_nearest, (const int*)c->d_knn, (const double*)c->d_bin_dirs,
+                     (const int*)c->d_bin_ref, c->cap, c->B, c->K,
                      scale, c->cfg.lidar_origin[0], c->cfg.lidar_origin[1], c->cfg.lidar_origin[2], c->cfg.tau, ids, r);
   HIPCHK(c, hipGetLastError());
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -615,8 +695,10 @@ int gcs_matrix_fisher_rotation(gcs_ctx* c, double* mf) {
     mf[k++] = c->h_scalars[SC_MF_MAPND];
     mf[k++] = c->h_scalars[SC_MF_SCANN];
     for (int i = 0; i < 9; ++i) mf[k++] = c->h_scalars[SC_MF_R + i];
-    for (int i = 0; i < 3; ++i) mf[k++] = c->h_scalars[SC_MF_S + i];
-    for (int i = 0; i < 9; ++i) mf[k++] = c->h_scalars[SC_MF_V + i];
+    double U[9], s[3], V[9];
+    svd3(c->h_scalars + SC_MF_H, U, s, V);
+    for (int i = 0; i < 3; ++i) mf[k++] = s[i];
+    for (int i = 0; i < 9; ++i) mf[k++] = V[i];
   }
   return GCS_OK;
 }
@@ -722,8 +804,8 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   double pose_pred[6], R_pred[9];
   host::world_pose_from_increment(pred, mu_inc, pose_pred);
   so3_exp(pose_pred + 3, R_pred);
-  const double* sv = S + SC_MF_S;
-  const double* V = S + SC_MF_V;
+  double Umf[9], sv[3], V[9];
+  svd3(S + SC_MF_H, Umf, sv, V);  // L_rot needs s and V (host, same 3x3 SVD code as the device)
   const double* Rmf = S + SC_MF_R;
   double Lrot_raw[9], Lrot[9];
   double dg[3] = {sv[1] + sv[2], sv[0] + sv[2], sv[0] + sv[1]};
@@ -967,6 +1049,11 @@ int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps, double* Li) {
 int gcs_svd3(const double* H, double* U, double* s, double* V) {
   if (!H || !U || !s || !V) return GCS_ERR_ARG;
   svd3(H, U, s, V);
+  return GCS_OK;
+}
+int gcs_mf_rotation(const double* H, double* R) {
+  if (!H || !R) return GCS_ERR_ARG;
+  mf_rotation(H, R);
   return GCS_OK;
 }
 int gcs_predict_diffusion(const gcs_belief* prev, const double* Q, double dt, gcs_belief* pred, double* cert) {

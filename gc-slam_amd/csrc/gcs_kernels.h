@@ -8,17 +8,13 @@
 
 namespace gcs {
 
-// "last block finishes" tickets (device array, zeroed at context creation, self re-arming):
-// kTicketStride words per kernel (kernel-wide ticket + one per group of 64 blocks)
-enum { TK_BUDGET = 0, TK_POINTS, TK_SCAN, TK_BINS, TK_MF, TK_PT, TK_PUSH, TK_DENSE, TK_COUNT };
-constexpr int kTicketStride = 1024;
+// k_scan draws its tile numbers from a self re-arming ticket (device word, zeroed at creation)
 
 struct BudgetArgs {
   const double* w;
   int n_raw, stride;
   double* partials;
   double* scalars;
-  uint32_t* ticket;
   uint32_t* zero32;  // scale-mode bucketing state cleared for this scan (may be null)
   int n_zero32;
   uint8_t* zero8;
@@ -50,7 +46,6 @@ struct PointKernelArgs {
   uint32_t* slots;
   uint32_t* counts;  // per-bin bucket sizes (cleared by k_budget)
   double* scalars;
-  uint32_t* ticket;
   // optional debug/parity outputs (may be null)
   double* p0_out;
   double* w_out;
@@ -84,6 +79,9 @@ struct BinKernelArgs {
   const uint8_t* flags;
   const int* rknn_off;
   const int* rknn;
+  const uint16_t* rknn_local;  // per reverse-kNN entry: index in its tile's source list
+  const int* tile_src_off;     // per tile of bins_tile() bins: CSR into tile_src
+  const int* tile_src;         // ascending unique source buckets of the tile
   const double* bin_dirs;
   const double* map;  // map sufficient stats (fused Matrix-Fisher term, scale mode)
   int n_bins, cap;
@@ -91,7 +89,6 @@ struct BinKernelArgs {
   double tau;
   double* scan;  // 26 x B field-major
   double* scalars;
-  uint32_t* ticket;
   uint32_t* zero_after;  // bucketing scratch (mid-list length, look-back words) re-armed for the next scan
   int n_zero_after;
 };
@@ -113,19 +110,23 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
 int scan_tiles(int n_bins);
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 int bins_scale_blocks(int n_bins);
+int bins_tile();              // device bins per k_bins_scale workgroup
+int bins_max_tile_sources();  // capacity of its source list
+int bins_max_tile_entries();  // capacity of its reverse-kNN entry list
 int bins_partial_nv();
 int push_blocks(int n_bins);
-hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+// e0/e1 bracket k_bins_scale itself (the roofline kernel), e2 ends its one-block fold
+hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                             hipEvent_t e2);
 hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* partials, hipStream_t s, hipEvent_t e0,
                         hipEvent_t e1);
 hipError_t launch_mf(const double* scan, const double* map, int B, double* partials, int nblk, double* scalars,
-                     uint32_t* ticket, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+                     hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, uint32_t* ticket, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+                     double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
-                              double* partials, double* scalars, uint32_t* ticket, hipStream_t s, hipEvent_t e0,
-                              hipEvent_t e1);
+                              double* partials, double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_map_derive(const double* map, double* derived, int B, double* partials, double* scalars,
-                             uint32_t* ticket, hipStream_t s);
+                             hipStream_t s);
 
 }  // namespace gcs

@@ -81,8 +81,8 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
   return v;
 }
 
-// Final pass over per-block partials inside one block: thread t folds partials t, t+256, ... in
-// order, then a fixed tree; the result is valid in thread 0.  Bit k of MAXMASK selects max
+// Final pass over per-block partials (one-block k_final launch): thread t folds partials t,
+// t+256, ... in order, then a fixed tree; the result is valid in thread 0.  Bit k of MAXMASK selects max
 // instead of sum for component k.  lds must hold kWaves*NV doubles.
 template <int NV, unsigned MAXMASK>
 __device__ __forceinline__ void reduce_partials(const double* __restrict__ partials, int nblocks, double (&v)[NV],
@@ -92,8 +92,7 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
   for (int b = threadIdx.x; b < nblocks; b += kBlock)
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
-      // device-coherent load (sc1): partials of other blocks were stored device-coherently
-      double x = __hip_atomic_load(partials + (size_t)b * NV + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double x = partials[(size_t)b * NV + k];
       v[k] = ((MAXMASK >> k) & 1u) ? fmax(v[k], x) : v[k] + x;
     }
 #pragma unroll
@@ -120,61 +119,22 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
   __syncthreads();
 }
 
-// "Last block finishes", two levels: thread 0 of every block stores the block partial
-// device-coherently (sc1 stores, no L2 write-back), waits for the stores to complete and draws a
-// ticket of its group of 64 blocks; the last block of a group folds the group's partials (fixed
-// order, sc1 loads) into a group partial and draws the kernel-wide ticket; the last group runs
-// the final fold.  No single block ever reads more than 64 partials, and a full
-// __threadfence() (buffer_wbl2: write-back of the XCD's whole L2, per block) is never needed.
-// Tickets re-arm themselves.  Layout: partials[nblocks*NV] then group partials[ngroups*NV];
-// tickets[0] kernel-wide, tickets[1 + g] per group.
-constexpr int kFinGroup = 64;  // kTicketStride (gcs_kernels.h) >= 1 + ngroups
-
+// Block partials are folded by a separate one-block k_final launch queued right behind the
+// producer (back-to-back dispatch, no gap).  Measured against "last block finishes" tickets in the
+// producer (sc1 stores + ticket + in-kernel fold): the separate fold was 15 us faster on the bin
+// kernel, because the in-kernel form holds every block until its ticket returns and runs the
+// fold and the 3x3 polar factor as a serial tail of the producer.
 template <int NV>
 __device__ __forceinline__ void store_partials(const double (&v)[NV], double* base, int idx) {
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int k = 0; k < NV; ++k)
-      __hip_atomic_store(base + (size_t)idx * NV + k, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool ticket_last(uint32_t* ticket, uint32_t expected) {
-  __shared__ uint32_t s_last;
-  if (threadIdx.x == 0) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_waitcnt(0);  // this thread's partial stores have completed
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    uint32_t prev = atomicAdd(ticket, 1u);
-    uint32_t last = (prev == expected - 1u) ? 1u : 0u;
-    if (last) atomicExch(ticket, 0u);
-    s_last = last;
-  }
-  __syncthreads();
-  return s_last != 0u;
-}
-
-// v: block partial (valid in thread 0).  Returns true in the one block that finishes, with the
-// kernel-wide fold in v (thread 0).
-template <int NV, unsigned MAXMASK>
-__device__ bool finish_blocks(double (&v)[NV], double* partials, uint32_t* tickets, double* lds) {
-  const int nb = gridDim.x;
-  const int ng = (nb + kFinGroup - 1) / kFinGroup;
-  store_partials<NV>(v, partials, blockIdx.x);
-  const int g = blockIdx.x / kFinGroup;
-  const int gsz = min(kFinGroup, nb - g * kFinGroup);
-  if (!ticket_last(tickets + 1 + g, (uint32_t)gsz)) return false;
-  reduce_partials<NV, MAXMASK>(partials + (size_t)g * kFinGroup * NV, gsz, v, lds);
-  double* gp = partials + (size_t)nb * NV;
-  store_partials<NV>(v, gp, g);
-  if (!ticket_last(tickets, (uint32_t)ng)) return false;
-  reduce_partials<NV, MAXMASK>(gp, ng, v, lds);
-  return true;
+    for (int k = 0; k < NV; ++k) base[(size_t)idx * NV + k] = v[k];
 }
 
 // ---------------------------------------------------------------- row 1: budget mass sums
 // Also clears the scale-mode bucketing state of this scan (counts, flags, look-back status),
 // replacing three memsets.  mass_scale = total_mass_in / (total_mass_selected + eps_mass)
-// (point_budget.py:80-84) is produced by the last block.
+// (point_budget.py:80-84) is produced by k_final<FIN_BUDGET>.
 __global__ __launch_bounds__(kBlock) void k_budget(BudgetArgs a) {
   __shared__ double lds[kWaves * 2];
   const int gid = blockIdx.x * kBlock + threadIdx.x, gsz = gridDim.x * kBlock;
@@ -187,12 +147,7 @@ __global__ __launch_bounds__(kBlock) void k_budget(BudgetArgs a) {
     if (j % a.stride == 0) v[1] += x;
   }
   block_sum<2>(v, lds);
-  if (!finish_blocks<2, 0u>(v, a.partials, a.ticket, lds)) return;
-  if (threadIdx.x == 0) {
-    a.scalars[SC_MASS_IN] = v[0];
-    a.scalars[SC_MASS_SEL] = v[1];
-    a.scalars[SC_MASS_SCALE] = v[0] / (v[1] + kEpsMass);
-  }
+  store_partials<2>(v, a.partials, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- cube-map cell of a direction
@@ -358,10 +313,8 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
   block_sum<4>(acc, lds);
   rmax = block_max(rmax, lds);
   double v[5] = {acc[0], acc[1], acc[2], acc[3], rmax};
-  // (sum wb, sum wn^2, sum w_out, sum H, max r) -> scalars[SC_DESKEW_WIN..]
-  if (!finish_blocks<5, 16u>(v, partials, a.ticket, lds)) return;
-  if (threadIdx.x == 0)
-    for (int k = 0; k < 5; ++k) a.scalars[SC_DESKEW_WIN + k] = v[k];
+  // (sum wb, sum wn^2, sum w_out, sum H, max r) -> scalars[SC_DESKEW_WIN..] by k_final<FIN_POINTS>
+  store_partials<5>(v, partials, blockIdx.x);
 }
 
 // ---------------------------------------------------------------- deterministic bucketing by nearest bin
@@ -598,11 +551,16 @@ __device__ __forceinline__ void write_bin_cert(double* cert, double* lds, double
 // ---------------------------------------------------------------- row 7 helpers (Matrix-Fisher)
 // Per bin (matrix_fisher_evidence.py:181-211): w_b = sqrt(N_s N_m + eps), u = S/(|S|+eps),
 // conf = Rbar_s Rbar_m, H += w_b conf u_map u_scan^T; out[9] += w_b conf; out[10] += N_s.
-__device__ __forceinline__ void mf_bin_term(double Ns, double sx, double sy, double sz, const double* __restrict__ map,
-                                            int B, int b, double* out /*11*/) {
+struct MapDir {
+  double Nm, mx, my, mz;  // map N_dir, S_dir of the bin
+};
+__device__ __forceinline__ MapDir load_map_dir(const double* __restrict__ map, int B, int b) {
   const size_t Bs = (size_t)B;
-  double Nm = map[MF_ND * Bs + b];
-  double mx = map[(MF_SD) * Bs + b], my = map[(MF_SD + 1) * Bs + b], mz = map[(MF_SD + 2) * Bs + b];
+  return MapDir{map[MF_ND * Bs + b], map[MF_SD * Bs + b], map[(MF_SD + 1) * Bs + b], map[(MF_SD + 2) * Bs + b]};
+}
+__device__ __forceinline__ void mf_bin_term(double Ns, double sx, double sy, double sz, const MapDir& md,
+                                            double* out /*11*/) {
+  const double Nm = md.Nm, mx = md.mx, my = md.my, mz = md.mz;
   double wb = sqrt(Ns * Nm + kEpsMass);
   double sn = sqrt(dot3_exact(sx, sy, sz, sx, sy, sz));
   double mn = sqrt(dot3_exact(mx, my, mz, mx, my, mz));
@@ -618,100 +576,206 @@ __device__ __forceinline__ void mf_bin_term(double Ns, double sx, double sy, dou
   out[10] += Ns;
 }
 
-// H (9), sum w conf, sum N_s -> scalars; 3x3 SVD and the det-fixed R_mf (:215-222) on one thread
+// H (9), sum w conf, sum N_s -> scalars; the det-fixed R_mf = U diag(1,1,det(UV^T)) V^T
+// (:215-222) on one thread (polar Newton, Jacobi SVD fallback: gcs_math.h mf_rotation).  The host
+// recomputes the singular values / V it needs for L_rot from H.
 __device__ void mf_finish(const double* v, double* scalars) {
   for (int k = 0; k < 9; ++k) scalars[SC_MF_H + k] = v[k];
   scalars[SC_MF_NEFF] = v[9];
   scalars[SC_MF_SCANN] = v[10];
-  double U[9], s[3], V[9];
-  svd3(v, U, s, V);
-  double UVt[9];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) UVt[3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
-  double dt = det3(UVt);
-  double sg = dt > 0.0 ? 1.0 : (dt < 0.0 ? -1.0 : 0.0);
-  U[2] *= sg; U[5] *= sg; U[8] *= sg;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j)
-      scalars[SC_MF_R + 3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
-  for (int k = 0; k < 3; ++k) scalars[SC_MF_S + k] = s[k];
-  for (int k = 0; k < 9; ++k) scalars[SC_MF_V + k] = V[k];
+  double R[9];
+  mf_rotation(v, R);
+  for (int k = 0; k < 9; ++k) scalars[SC_MF_R + k] = R[k];
 }
 
 // fused bin-kernel partial: [sum N, sum N^2, sum N/(N+eps), sum psd delta, max eps ratio | MF 11]
 constexpr int kBinNV = 16;
 
 // ---------------------------------------------------------------- row 5+6 scale mode: bin-centric
-// One 256-thread workgroup per tile of 64 consecutive bins.  Phase 1 compacts the tile's active
-// bins (ballot).  Phase 2: a 4-lane group per active bin (all 64 bins of a tile in flight);
-// lane l owns the bin's reverse-kNN buckets l, l+4, ... and streams each bucket's contiguous
-// records (ascending point index); the 4 lane sums meet in a fixed xor tree.  Phase 3: the
-// first wave finalizes the 64 bins (PSD, kappa) and streams the 26 field-major outputs.
-constexpr int kTile = 64;
-constexpr int kGroup = 4;
+// One 256-thread workgroup per tile of 128 consecutive device bins (a compact Hilbert patch of
+// the sphere, gcs_atlas.h).
+//  A: the tile's bin directions, reverse-kNN ranges and local source indices go to LDS; the
+//     tile's unique source buckets (host table, ~2 per bin) get sizes, starts and staged offsets
+//     (block scan); each bin's work (records to visit) is summed.
+//  B: the sources' records, which each bin of the tile reads ~K/2 times, are staged once into LDS
+//     (64 B: p, d, m, w/Z); a tile with more than kStage records reads them from HBM/L2 instead.
+//  C: a lane pair per bin accumulates the bin's records in fixed order (the bin's sources in
+//     ascending bucket id, each source's points in ascending index; lane l takes the l-th half;
+//     one xor add) -- LDS traffic only.
+//  D: the sums go through LDS to one lane per bin (waves 0-1; waves 2-3 only join the block
+//     reduction): PSD, kappa, the bin's Matrix-Fisher term, coalesced 128-bin output rows.
+// LDS < 80 KiB: two workgroups per CU.
+constexpr int kBinTile = 128;
+constexpr int kBinLanes = kBlock / kBinTile;
+constexpr int kMaxSrc = 768;
+constexpr int kMaxRl = 3072;  // reverse-kNN entries of one tile (~K x kBinTile)
+constexpr int kStage = 896;
+constexpr int kRecD = 8;  // staged record: x y z dx dy dz m w/Z
+static_assert(kStage * kRecD >= 19 * kBinTile, "phase D reuses the record stage for the bin sums");
+int bins_tile() { return kBinTile; }
+int bins_max_tile_sources() { return kMaxSrc; }
+int bins_max_tile_entries() { return kMaxRl; }
+
+__device__ __forceinline__ void bin_contrib(double* acc, const double4& bd, double inv_tau, double px, double py,
+                                            double pz, double dx, double dy, double dz, double m, double wz) {
+  double d[3] = {dx, dy, dz};
+  double p[3] = {px, py, pz};
+  double sim = dot3_exact(dx, dy, dz, bd.x, bd.y, bd.z);
+  // w r = w exp((s - m)/tau) / Z   (binning.py:69 softmax, :159-160 weighting)
+  add_contrib(acc, wz * exp((sim - m) * inv_tau), d, p);
+}
+
+#ifdef GCS_PHASE_PROF
+__device__ unsigned long long g_prof[16384 * 8];
+extern "C" int gcs_debug_prof(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), (size_t)n * sizeof(unsigned long long));
+}
+#define PROF(k) \
+  if (threadIdx.x == 0) g_prof[blockIdx.x * 8 + (k)] = wall_clock64();
+#else
+#define PROF(k)
+#endif
+
 __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* partials) {
-  __shared__ double sums[19 * kTile];
-  __shared__ int active[kTile];
-  __shared__ int n_active;
+  __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
+  __shared__ uint16_t s_rl[kMaxRl];
+  __shared__ double s_rec[kStage * kRecD];
+  __shared__ double4 s_bd[kBinTile];
+  __shared__ int s_q[kBinTile + 1];
+  __shared__ uint32_t s_work[kBinTile];
+  __shared__ uint32_t s_wsum[kWaves];
   __shared__ double lds[kWaves * kBinNV];
-  const int t = threadIdx.x;
-  const int b0 = blockIdx.x * kTile;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int tile = blockIdx.x;
+  const int b0 = tile * kBinTile;
+  const int nb = min(kBinTile, a.n_bins - b0);
+  PROF(0);
   for (int j = blockIdx.x * kBlock + t; j < a.n_zero_after; j += gridDim.x * kBlock) a.zero_after[j] = 0u;
-  for (int i = t; i < 19 * kTile; i += kBlock) sums[i] = 0.0;
-  if (t < 64) {
-    int b = b0 + t;
-    bool act = (b < a.n_bins) && a.flags[b];
-    unsigned long long mask = __ballot(act);
-    if (act) active[__popcll(mask & ((1ull << t) - 1ull))] = t;
-    if (t == 0) n_active = __popcll(mask);
+  // phase D's bin (thread t < nb owns bin b0 + t): flag and map direction stats up front
+  const bool own = t < nb;
+  const bool own_act = own && a.flags[b0 + t];
+  MapDir mapv{0.0, 0.0, 0.0, 0.0};
+  if (own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + t);
+  // phase A
+  if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
+  if (t <= nb) s_q[t] = a.rknn_off[b0 + t];
+  const int q0 = a.rknn_off[b0], q1t = a.rknn_off[b0 + nb];
+  for (int q = q0 + t; q < q1t; q += kBlock) s_rl[q - q0] = a.rknn_local[q];
+  const int s0 = a.tile_src_off[tile];
+  const int ns = a.tile_src_off[tile + 1] - s0;
+  for (int j = t; j < ns; j += kBlock) {
+    const int src = a.tile_src[s0 + j];
+    s_cnt[j] = a.counts[src];
+    s_st[j] = a.starts[src];
   }
   __syncthreads();
-  const int g = t / kGroup, l = t % kGroup;
-  const double inv_tau = 1.0 / a.tau;
-  for (int j = g; j < n_active; j += kBlock / kGroup) {
-    const int lb = active[j];
-    const int bb = b0 + lb;
-    const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)bb);
-    double acc[19];
+  PROF(1);
+  if (t < kBinTile) {  // records each bin visits (0 for inactive / out-of-range bins)
+    uint32_t w = 0;
+    if (own_act)
+      for (int q = s_q[t]; q < s_q[t + 1]; ++q) w += s_cnt[s_rl[q - q0]];
+    s_work[t] = w;
+  }
+  const int chunk = (ns + kBlock - 1) / kBlock;
+  const int j0 = min(ns, t * chunk), j1 = min(ns, j0 + chunk);
+  uint32_t mine = 0;
+  for (int j = j0; j < j1; ++j) mine += s_cnt[j];
+  uint32_t x = mine;
+  for (int off = 1; off < 64; off <<= 1) {
+    uint32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wsum[wid] = x;
+  __syncthreads();
+  uint32_t run = x - mine;
+  for (int w = 0; w < wid; ++w) run += s_wsum[w];
+  for (int j = j0; j < j1; ++j) {
+    s_off[j] = run;
+    run += s_cnt[j];
+  }
+  const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  const bool staged = total <= (uint32_t)kStage;
+  __syncthreads();
+  PROF(2);
+  // phase B: stage the tile's records (record r belongs to the last source with s_off <= r)
+  if (staged) {
+    for (uint32_t r = t; r < total; r += kBlock) {
+      int lo = 0, hi = ns - 1;
+      while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= r) lo = mid; else hi = mid - 1;
+      }
+      const PointRec pr = a.recs_s[s_st[lo] + (r - s_off[lo])];
+      double* d = s_rec + (size_t)r * kRecD;
+      d[0] = pr.x; d[1] = pr.y; d[2] = pr.z; d[3] = pr.dx; d[4] = pr.dy; d[5] = pr.dz;
+      d[6] = pr.m; d[7] = pr.w * pr.iz;
+    }
+  }
+  __syncthreads();
+  PROF(3);
+  // phase C: lane pair per bin; the bin's records (sources in order, points in order) are one
+  // flattened list and lane l takes the l-th half, so every lane's trip count is its own share
+  // (no per-source max over the wave's lanes).
+  const int lb = t / kBinLanes, l = t % kBinLanes;
+  double acc[19];
 #pragma unroll
-    for (int f = 0; f < 19; ++f) acc[f] = 0.0;
-    const int q1 = a.rknn_off[bb + 1];
-    // lane l owns reverse-kNN buckets l, l+4, ...; each bucket streams its contiguous records
-    for (int q = a.rknn_off[bb] + l; q < q1; q += kGroup) {
-      const uint32_t src = (uint32_t)a.rknn[q];
-      const uint32_t c = a.counts[src];
-      const PointRec* rp = a.recs_s + a.starts[src];
-      for (uint32_t i = 0; i < c; ++i) {
-        const PointRec pr = rp[i];
-        double d[3] = {pr.dx, pr.dy, pr.dz};
-        double p[3] = {pr.x, pr.y, pr.z};
-        double sim = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
-        double r = exp((sim - pr.m) * inv_tau) * pr.iz;
-        add_contrib(acc, pr.w * r, d, p);
+  for (int f = 0; f < 19; ++f) acc[f] = 0.0;
+  const uint32_t work = s_work[lb];
+  if (work > 0) {
+    const double4 bd = s_bd[lb];
+    const double inv_tau = 1.0 / a.tau;
+    const uint32_t i0 = l == 0 ? 0u : work / 2u, i1 = l == 0 ? work / 2u : work;
+    // cursor: source q (local j), record k within it
+    int q = s_q[lb];
+    uint32_t skip = i0;
+    int j = s_rl[q - q0];
+    uint32_t c = s_cnt[j];
+    while (skip >= c) {
+      skip -= c;
+      ++q;
+      j = s_rl[q - q0];
+      c = s_cnt[j];
+    }
+    uint32_t kk = skip;
+    for (uint32_t i = i0; i < i1; ++i) {
+      if (staged) {
+        const double* rp = s_rec + (size_t)(s_off[j] + kk) * kRecD;
+        bin_contrib(acc, bd, inv_tau, rp[0], rp[1], rp[2], rp[3], rp[4], rp[5], rp[6], rp[7]);
+      } else {
+        const PointRec pr = a.recs_s[s_st[j] + kk];
+        bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, pr.dx, pr.dy, pr.dz, pr.m, pr.w * pr.iz);
+      }
+      if (++kk == c && i + 1 < i1) {  // next non-empty source
+        kk = 0;
+        do {
+          ++q;
+          j = s_rl[q - q0];
+          c = s_cnt[j];
+        } while (c == 0);
       }
     }
-#pragma unroll
-    for (int off = kGroup / 2; off >= 1; off >>= 1)
-#pragma unroll
-      for (int f = 0; f < 19; ++f) acc[f] += __shfl_xor(acc[f], off, 64);
-    if (l == 0)
-#pragma unroll
-      for (int f = 0; f < 19; ++f) sums[f * kTile + lb] = acc[f];
   }
+#pragma unroll
+  for (int f = 0; f < 19; ++f) acc[f] += __shfl_xor(acc[f], 1, 64);
+  PROF(4);
+  __syncthreads();  // the record stage is free: it now carries the bin sums [19][kBinTile]
+  if (l == 0)
+#pragma unroll
+    for (int f = 0; f < 19; ++f) s_rec[f * kBinTile + lb] = acc[f];
   __syncthreads();
-  // phase 3: finalize + this bin's Matrix-Fisher term (row 7, matrix_fisher_evidence.py:181-211).
+  // phase D: finalize + this bin's Matrix-Fisher term (row 7, matrix_fisher_evidence.py:181-211).
   // A bin with no scan mass contributes exact zeros to H, so only active bins read the map.
   double v[kBinNV];
 #pragma unroll
   for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
   v[4] = -INFINITY;
-  if (t < kTile && b0 + t < a.n_bins) {
-    double r[19];
+  if (own) {
 #pragma unroll
-    for (int f = 0; f < 19; ++f) r[f] = sums[f * kTile + t];
-    finalize_bin(r, a.scan, a.n_bins, b0 + t, v);
-    if (a.flags[b0 + t]) mf_bin_term(r[0], r[1], r[2], r[3], a.map, a.n_bins, b0 + t, v + 5);
+    for (int f = 0; f < 19; ++f) acc[f] = s_rec[f * kBinTile + t];
+    finalize_bin(acc, a.scan, a.n_bins, b0 + t, v);
+    if (own_act) mf_bin_term(acc[0], acc[1], acc[2], acc[3], mapv, v + 5);
   }
+  PROF(5);
   // block reduce: 4 sums, 1 max, 11 sums
   double s4[4] = {v[0], v[1], v[2], v[3]};
   block_sum<4>(s4, lds);
@@ -723,11 +787,8 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   v[0] = s4[0]; v[1] = s4[1]; v[2] = s4[2]; v[3] = s4[3]; v[4] = mx;
 #pragma unroll
   for (int f = 0; f < 11; ++f) v[5 + f] = m11[f];
-  if (!finish_blocks<kBinNV, 16u>(v, partials, a.ticket, lds)) return;
-  if (t == 0) {
-    for (int f = 0; f < 5; ++f) a.scalars[SC_BIN_NSUM + f] = v[f];
-    mf_finish(v + 5, a.scalars);
-  }
+  store_partials<kBinNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_BINS>
+  PROF(6);
 }
 
 // ---------------------------------------------------------------- row 5+6 dense mode (B small)
@@ -781,10 +842,7 @@ __global__ __launch_bounds__(kBlock) void k_dense_finalize(BinKernelArgs a, cons
   }
   write_bin_cert(cert, lds, partials);
   double v5[5] = {cert[0], cert[1], cert[2], cert[3], cert[4]};
-  if (!finish_blocks<5, 16u>(v5, partials, a.ticket, lds)) return;
-  for (int f = 0; f < 5; ++f) cert[f] = v5[f];
-  if (threadIdx.x == 0)
-    for (int f = 0; f < 5; ++f) a.scalars[SC_BIN_NSUM + f] = cert[f];
+  store_partials<5>(v5, partials, blockIdx.x);  // folded by k_final<FIN_DENSE>
 }
 
 // ---------------------------------------------------------------- row 7: Matrix-Fisher reduction
@@ -793,26 +851,21 @@ __global__ __launch_bounds__(kBlock) void k_dense_finalize(BinKernelArgs a, cons
 // scan the H terms are fused into k_bins_scale and the map totals come from the pushforward.
 constexpr int kMfNV = 21;
 __global__ __launch_bounds__(kBlock) void k_mf(const double* __restrict__ scan, const double* __restrict__ map, int B,
-                                               double* partials, double* scalars, uint32_t* ticket) {
+                                               double* partials) {
   __shared__ double lds[kWaves * kMfNV];
   double v[kMfNV];
 #pragma unroll
   for (int k = 0; k < kMfNV; ++k) v[k] = 0.0;
   const size_t Bs = (size_t)B;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
-    mf_bin_term(scan[SF_N * Bs + b], scan[SF_SD * Bs + b], scan[(SF_SD + 1) * Bs + b], scan[(SF_SD + 2) * Bs + b], map,
-                B, b, v);
+    mf_bin_term(scan[SF_N * Bs + b], scan[SF_SD * Bs + b], scan[(SF_SD + 1) * Bs + b], scan[(SF_SD + 2) * Bs + b],
+                load_map_dir(map, B, b), v);
 #pragma unroll
     for (int k = 0; k < 9; ++k) v[11 + k] += map[(MF_S + k) * Bs + b];
     v[20] += map[MF_ND * Bs + b];
   }
   block_sum<kMfNV>(v, lds);
-  if (!finish_blocks<kMfNV, 0u>(v, partials, ticket, lds)) return;
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[11 + k];
-    scalars[SC_MF_MAPND] = v[20];
-    mf_finish(v, scalars);
-  }
+  store_partials<kMfNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_MF>
 }
 
 // ---------------------------------------------------------------- row 8: planar translation
@@ -820,8 +873,8 @@ __global__ __launch_bounds__(kBlock) void k_mf(const double* __restrict__ scan, 
 // S_b = Sigma_map + R Sigma_scan R^T, W_b = w_b inv(S_b + eps I); L += W_b, h += W_b t_b.
 constexpr int kPtNV = 13;
 __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, const double* __restrict__ map,
-                                               const double* __restrict__ derived, int B, double* scalars,
-                                               double* partials, uint32_t* ticket) {
+                                               const double* __restrict__ derived, int B,
+                                               const double* __restrict__ scalars, double* partials) {
   __shared__ double lds[kWaves * kPtNV];
   double R[9];
 #pragma unroll
@@ -861,12 +914,7 @@ __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, 
     v[12] += wb;
   }
   block_sum<kPtNV>(v, lds);
-  if (!finish_blocks<kPtNV, 0u>(v, partials, ticket, lds)) return;
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 9; ++k) scalars[SC_PT_L + k] = v[k];
-    for (int k = 0; k < 3; ++k) scalars[SC_PT_H + k] = v[9 + k];
-    scalars[SC_PT_NEFF] = v[12];
-  }
+  store_partials<kPtNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_PT>
 }
 
 // ---------------------------------------------------------------- row 11: pushforward (declared)
@@ -898,19 +946,13 @@ __device__ __forceinline__ void derive_bin(const double* sd, double nd, double n
 // Map totals for the next scan's planar z precision (sum S_dir_scatter, sum N_dir over bins),
 // reduced in fixed order by the last block.
 constexpr int kTotNV = 10;
-__device__ __forceinline__ void map_totals_finish(double (&tot)[kTotNV], double* lds, double* partials,
-                                                  double* scalars, uint32_t* ticket) {
+__device__ __forceinline__ void map_totals_partial(double (&tot)[kTotNV], double* lds, double* partials) {
   block_sum<kTotNV>(tot, lds);
-  if (!finish_blocks<kTotNV, 0u>(tot, partials, ticket, lds)) return;
-  if (threadIdx.x == 0) {
-    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = tot[k];
-    scalars[SC_MF_MAPND] = tot[9];
-  }
+  store_partials<kTotNV>(tot, partials, blockIdx.x);  // folded by k_final<FIN_TOTALS>
 }
 
 __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict__ scan, double* map, double* derived,
-                                                        int B, PushArgs pa, double* partials, double* scalars,
-                                                        uint32_t* ticket) {
+                                                        int B, PushArgs pa, double* partials) {
   __shared__ double lds[kWaves * kTotNV];
   double tot[kTotNV];
 #pragma unroll
@@ -991,12 +1033,12 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
     }
     derive_bin(sd, nd, np, sp, spp, derived, Bs, b);
   }
-  map_totals_finish(tot, lds, partials, scalars, ticket);
+  map_totals_partial(tot, lds, partials);
 }
 
 // derived stats + map totals from map sufficient stats only (used after set_map / reset)
 __global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict__ map, double* derived, int B,
-                                                       double* partials, double* scalars, uint32_t* ticket) {
+                                                       double* partials) {
   __shared__ double lds[kWaves * kTotNV];
   double tot[kTotNV];
 #pragma unroll
@@ -1009,8 +1051,46 @@ __global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict_
     tot[9] += map[MF_ND * Bs + b];
     derive_bin(sd, map[MF_ND * Bs + b], map[MF_NP * Bs + b], sp, spp, derived, Bs, b);
   }
-  map_totals_finish(tot, lds, partials, scalars, ticket);
+  map_totals_partial(tot, lds, partials);
 }
+
+// ---------------------------------------------------------------- one-block folds of block partials
+enum FinalKind : int { FIN_BUDGET, FIN_POINTS, FIN_BINS, FIN_DENSE, FIN_MF, FIN_PT, FIN_TOTALS };
+
+template <int NV, unsigned MAXMASK, int KIND>
+__global__ __launch_bounds__(kBlock) void k_final(const double* __restrict__ partials, int nblocks, double* scalars) {
+  __shared__ double lds[kWaves * NV];
+  double v[NV];
+  reduce_partials<NV, MAXMASK>(partials, nblocks, v, lds);
+  if (threadIdx.x != 0) return;
+  if (KIND == FIN_BUDGET) {
+    scalars[SC_MASS_IN] = v[0];
+    scalars[SC_MASS_SEL] = v[1];
+    scalars[SC_MASS_SCALE] = v[0] / (v[1] + kEpsMass);  // point_budget.py:80-84
+  } else if (KIND == FIN_POINTS) {
+    for (int k = 0; k < 5; ++k) scalars[SC_DESKEW_WIN + k] = v[k];
+  } else if (KIND == FIN_BINS) {
+    for (int k = 0; k < 5; ++k) scalars[SC_BIN_NSUM + k] = v[k];
+    mf_finish(v + 5, scalars);
+  } else if (KIND == FIN_DENSE) {
+    for (int k = 0; k < 5; ++k) scalars[SC_BIN_NSUM + k] = v[k];
+  } else if (KIND == FIN_MF) {
+    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[11 + k];
+    scalars[SC_MF_MAPND] = v[20];
+    mf_finish(v, scalars);
+  } else if (KIND == FIN_PT) {
+    for (int k = 0; k < 9; ++k) scalars[SC_PT_L + k] = v[k];
+    for (int k = 0; k < 3; ++k) scalars[SC_PT_H + k] = v[9 + k];
+    scalars[SC_PT_NEFF] = v[12];
+  } else if (KIND == FIN_TOTALS) {
+    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[k];
+    scalars[SC_MF_MAPND] = v[9];
+  }
+}
+
+#define GCS_FINAL(NV, MASK, KIND, nblk, s, e1, partials, scalars)                                                   \
+  hipExtLaunchKernelGGL(k_final<NV, MASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0, (const double*)partials, \
+                        (int)(nblk), scalars)
 
 // ---------------------------------------------------------------- launchers
 static int grid_for(long n, int cap_blocks) {
@@ -1021,7 +1101,8 @@ static int grid_for(long n, int cap_blocks) {
 int push_blocks(int n_bins) { return grid_for(n_bins, 4096); }
 
 hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  hipExtLaunchKernelGGL(k_budget, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a);
+  hipExtLaunchKernelGGL(k_budget, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a);
+  GCS_FINAL(2, 0u, FIN_BUDGET, nblk, s, e1, a.partials, a.scalars);
   return hipGetLastError();
 }
 
@@ -1029,14 +1110,15 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
                          hipEvent_t e1) {
   if (scale) {
     switch (a.k) {
-      case 8: hipExtLaunchKernelGGL(k_points<true, 8>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials); break;
-      case 16: hipExtLaunchKernelGGL(k_points<true, 16>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials); break;
-      case 32: hipExtLaunchKernelGGL(k_points<true, 32>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials); break;
+      case 8: hipExtLaunchKernelGGL(k_points<true, 8>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
+      case 16: hipExtLaunchKernelGGL(k_points<true, 16>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
+      case 32: hipExtLaunchKernelGGL(k_points<true, 32>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
       default: return hipErrorInvalidValue;
     }
   } else {
-    hipExtLaunchKernelGGL(k_points<false, 1>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL(k_points<false, 1>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials);
   }
+  GCS_FINAL(5, 16u, FIN_POINTS, nblk, s, e1, partials, a.scalars);
   return hipGetLastError();
 }
 
@@ -1055,11 +1137,14 @@ hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_
   return hipGetLastError();
 }
 
-int bins_scale_blocks(int n_bins) { return (n_bins + kTile - 1) / kTile; }
+int bins_scale_blocks(int n_bins) { return (n_bins + kBinTile - 1) / kBinTile; }
 int bins_partial_nv() { return kBinNV; }
 
-hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  hipExtLaunchKernelGGL(k_bins_scale, dim3(bins_scale_blocks(a.n_bins)), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
+hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
+                             hipEvent_t e2) {
+  const int nblk = bins_scale_blocks(a.n_bins);
+  hipExtLaunchKernelGGL(k_bins_scale, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
+  GCS_FINAL(kBinNV, 16u, FIN_BINS, nblk, s, e2, partials, a.scalars);
   return hipGetLastError();
 }
 
@@ -1068,36 +1153,41 @@ hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* pa
   int nchunks = (a.cap + kBlock - 1) / kBlock;
   hipExtLaunchKernelGGL(k_dense_accum, dim3(nchunks), dim3(kBlock), 0, s, e0, nullptr, 0, a, bin_partials);
   int nblk = (a.n_bins + kBlock - 1) / kBlock;
-  hipExtLaunchKernelGGL(k_dense_finalize, dim3(nblk), dim3(kBlock), 0, s, nullptr, e1, 0, a,
+  hipExtLaunchKernelGGL(k_dense_finalize, dim3(nblk), dim3(kBlock), 0, s, nullptr, nullptr, 0, a,
                         (const double*)bin_partials, nchunks, partials);
+  GCS_FINAL(5, 16u, FIN_DENSE, nblk, s, e1, partials, a.scalars);
   return hipGetLastError();
 }
 
 hipError_t launch_mf(const double* scan, const double* map, int B, double* partials, int nblk, double* scalars,
-                     uint32_t* ticket, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  hipExtLaunchKernelGGL(k_mf, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, scan, map, B, partials, scalars, ticket);
+                     hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  hipExtLaunchKernelGGL(k_mf, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, B, partials);
+  GCS_FINAL(kMfNV, 0u, FIN_MF, nblk, s, e1, partials, scalars);
   return hipGetLastError();
 }
 
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, uint32_t* ticket, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, scan, map, derived, B, scalars, partials,
-                        ticket);
+                     double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B,
+                        (const double*)scalars, partials);
+  GCS_FINAL(kPtNV, 0u, FIN_PT, nblk, s, e1, partials, scalars);
   return hipGetLastError();
 }
 
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
-                              double* partials, double* scalars, uint32_t* ticket, hipStream_t s, hipEvent_t e0,
-                              hipEvent_t e1) {
-  hipExtLaunchKernelGGL(k_pushforward, dim3(push_blocks(B)), dim3(kBlock), 0, s, e0, e1, 0, scan, map, derived, B, pa,
-                        partials, scalars, ticket);
+                              double* partials, double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  const int nblk = push_blocks(B);
+  hipExtLaunchKernelGGL(k_pushforward, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B, pa,
+                        partials);
+  GCS_FINAL(kTotNV, 0u, FIN_TOTALS, nblk, s, e1, partials, scalars);
   return hipGetLastError();
 }
 
 hipError_t launch_map_derive(const double* map, double* derived, int B, double* partials, double* scalars,
-                             uint32_t* ticket, hipStream_t s) {
-  hipLaunchKernelGGL(k_map_derive, dim3(push_blocks(B)), dim3(kBlock), 0, s, map, derived, B, partials, scalars,
-                     ticket);
+                             hipStream_t s) {
+  const int nblk = push_blocks(B);
+  hipLaunchKernelGGL(k_map_derive, dim3(nblk), dim3(kBlock), 0, s, map, derived, B, partials);
+  GCS_FINAL(kTotNV, 0u, FIN_TOTALS, nblk, s, nullptr, partials, scalars);
   return hipGetLastError();
 }
 

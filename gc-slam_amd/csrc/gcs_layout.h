@@ -36,7 +36,8 @@ enum MapDerived : int {
   MD_COUNT = 16
 };
 
-// Per-point record written by the point kernel, gathered by the bin kernels (48 B).
+// Per-point record written by the point kernel, gathered by the bin kernels (80 B; the bin
+// kernel stages the first 72 B of each record in LDS).
 struct PointRec {
   double x, y, z;     // deskewed point (scan-start base frame)
   double dx, dy, dz;  // ray direction from the LiDAR origin (pipeline.py:589-593)

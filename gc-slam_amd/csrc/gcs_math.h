@@ -370,4 +370,59 @@ GCS_HD double det3(const double* m) {
   return m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) + m[2] * (m[3] * m[7] - m[4] * m[6]);
 }
 
+// R_mf = U' V^T with U' = U with its last column multiplied by sign(det(U V^T)), H = U S V^T
+// (matrix_fisher_evidence.py:215-222), through the Jacobi SVD.
+GCS_HD void mf_rotation_svd(const double* H, double* R) {
+  double U[9], s[3], V[9], UVt[9];
+  svd3(H, U, s, V);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) UVt[3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
+  double dt = det3(UVt);
+  double sg = dt > 0.0 ? 1.0 : (dt < 0.0 ? -1.0 : 0.0);
+  U[2] *= sg; U[5] *= sg; U[8] *= sg;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) R[3 * i + j] = U[3 * i] * V[3 * j] + U[3 * i + 1] * V[3 * j + 1] + U[3 * i + 2] * V[3 * j + 2];
+}
+
+// Same R_mf.  When det(H) > 0 and H is not nearly singular, det(U V^T) = +1 and R_mf is the
+// orthogonal polar factor of H: the scaled Newton iteration X <- (g X + X^{-T} / g) / 2,
+// g = (|X^{-1}|_F / |X|_F)^{1/2}, reaches it in a handful of 3x3 adjugate steps (quadratic
+// convergence) -- a short dependent chain on one GPU thread.  Reflections and rank-deficient H
+// take the SVD.
+GCS_HD void mf_rotation(const double* H, double* R) {
+  double fro2 = 0.0;
+  for (int k = 0; k < 9; ++k) fro2 += H[k] * H[k];
+  const double fro = sqrt(fro2);
+  const double d0 = det3(H);
+  if (!(fro > 0.0) || !(d0 > 1e-6 * fro2 * fro)) {
+    mf_rotation_svd(H, R);
+    return;
+  }
+  double X[9];
+  for (int k = 0; k < 9; ++k) X[k] = H[k];
+  bool polish = false;
+  for (int it = 0; it < 60; ++it) {
+    double C[9] = {X[4] * X[8] - X[5] * X[7], X[5] * X[6] - X[3] * X[8], X[3] * X[7] - X[4] * X[6],
+                   X[2] * X[7] - X[1] * X[8], X[0] * X[8] - X[2] * X[6], X[1] * X[6] - X[0] * X[7],
+                   X[1] * X[5] - X[2] * X[4], X[2] * X[3] - X[0] * X[5], X[0] * X[4] - X[1] * X[3]};
+    const double dx = X[0] * C[0] + X[1] * C[1] + X[2] * C[2];  // C / dx = X^{-T}
+    double g = 1.0;
+    if (!polish) {
+      double nx = 0.0, nc = 0.0;
+      for (int k = 0; k < 9; ++k) { nx += X[k] * X[k]; nc += C[k] * C[k]; }
+      g = sqrt(sqrt(nc / nx) / fabs(dx));
+    }
+    const double a = 0.5 * g, b = 0.5 / (g * dx);
+    double diff = 0.0;
+    for (int k = 0; k < 9; ++k) {
+      const double xn = a * X[k] + b * C[k];
+      diff += (xn - X[k]) * (xn - X[k]);
+      X[k] = xn;
+    }
+    if (polish) break;             // one unscaled step after convergence
+    if (diff <= 1e-24) polish = true;
+  }
+  for (int k = 0; k < 9; ++k) R[k] = X[k];
+}
+
 }  // namespace gcs

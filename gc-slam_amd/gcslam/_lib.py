@@ -73,6 +73,7 @@ _SIGS = [
     ("gcs_ctx_set_map", C.c_int, [C.c_void_p, c_double_p]),
     ("gcs_ctx_get_map", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
     ("gcs_ctx_get_scan_stats", C.c_int, [C.c_void_p, c_double_p]),
+    ("gcs_ctx_get_bin_order", C.c_int, [C.c_void_p, c_int32_p]),
     ("gcs_ctx_device_arrays", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                         C.POINTER(C.c_void_p)]),
     ("gcs_ctx_set_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
@@ -89,6 +90,7 @@ _SIGS = [
     ("gcs_spd_solve_lifted", C.c_int, [C.c_int32, c_double_p, c_double_p, C.c_double, c_double_p]),
     ("gcs_spd_inverse_lifted", C.c_int, [C.c_int32, c_double_p, C.c_double, c_double_p]),
     ("gcs_svd3", C.c_int, [c_double_p, c_double_p, c_double_p, c_double_p]),
+    ("gcs_mf_rotation", C.c_int, [c_double_p, c_double_p]),
     ("gcs_predict_diffusion", C.c_int, [C.POINTER(GcsBelief), c_double_p, C.c_double, C.POINTER(GcsBelief),
                                         c_double_p]),
     ("gcs_info_fusion_additive", C.c_int, [C.POINTER(GcsBelief), c_double_p, c_double_p, C.c_double,

@@ -132,8 +132,11 @@ int gcs_ctx_get_belief(gcs_ctx* ctx, gcs_belief* b);
 int gcs_ctx_set_map(gcs_ctx* ctx, const double* map_host /*26*B field-major*/);
 int gcs_ctx_get_map(gcs_ctx* ctx, double* map_host /*26*B*/, double* derived_host /*16*B*/);
 int gcs_ctx_get_scan_stats(gcs_ctx* ctx, double* scan_host /*26*B*/);
-/* device pointers of the resident per-bin arrays (field-major, length-B rows) */
+/* device pointers of the resident per-bin arrays (field-major, length-B rows) in DEVICE bin
+ * order; set/get_map and get_scan_stats convert to reference (atlas) order */
 int gcs_ctx_device_arrays(gcs_ctx* ctx, double** scan_dev, double** map_dev, double** derived_dev);
+/* order[device bin] = reference bin id (scale mode: Hilbert patches of the sphere; dense: identity) */
+int gcs_ctx_get_bin_order(gcs_ctx* ctx, int32_t* order /*B*/);
 int gcs_ctx_set_iw_state(gcs_ctx* ctx, const double* nu7, const double* Psi7x36);
 int gcs_ctx_get_iw_state(gcs_ctx* ctx, double* nu7, double* Psi7x36, double* Q22x22);
 
@@ -167,6 +170,9 @@ int gcs_psd_project(int32_t n, const double* M, double eps_psd, double* M_psd, d
 int gcs_spd_solve_lifted(int32_t n, const double* L, const double* b, double eps_lift, double* x);
 int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps_lift, double* Linv);
 int gcs_svd3(const double* H, double* U, double* s, double* V);
+/* det-fixed Matrix-Fisher rotation R = U diag(1,1,det(UV^T)) V^T of H (matrix_fisher_evidence.py:215-222):
+ * the same routine the device fold runs (polar Newton, SVD for reflections / rank deficiency) */
+int gcs_mf_rotation(const double* H /*3x3*/, double* R /*3x3*/);
 int gcs_predict_diffusion(const gcs_belief* prev, const double* Q, double dt_sec, gcs_belief* pred, double* cert4);
 int gcs_info_fusion_additive(const gcs_belief* pred, const double* L_ev, const double* h_ev, double alpha,
                              gcs_belief* post, double* psd_delta);

@@ -69,6 +69,43 @@ def test_svd3_reconstructs_and_matches_numpy_singular_values(lib):
         assert np.allclose(U.T @ U, np.eye(3), atol=1e-12) and np.allclose(V.T @ V, np.eye(3), atol=1e-12)
 
 
+def _mf_rotation_numpy(H):
+    """matrix_fisher_evidence.py:215-222: SVD, det fix of U's last column, R = U' Vt."""
+    U, s, Vt = np.linalg.svd(H)
+    U[:, 2] *= np.sign(np.linalg.det(U @ Vt))
+    return U @ Vt
+
+
+@pytest.mark.parametrize("kind", ["random", "near_rotation", "reflection", "rank2", "zero"])
+def test_mf_rotation_matches_svd_rule(lib, kind):
+    rng = np.random.default_rng(21)
+    for k in range(25):
+        if kind == "near_rotation":   # well aligned scans: H close to R diag(s)
+            Q, _ = np.linalg.qr(rng.standard_normal((3, 3)))
+            Q *= np.sign(np.linalg.det(Q))
+            H = Q @ np.diag(rng.uniform(0.5, 50.0, 3)) + 1e-3 * rng.standard_normal((3, 3))
+        elif kind == "reflection":
+            H = rng.standard_normal((3, 3))
+            if np.linalg.det(H) > 0:
+                H[:, 0] *= -1
+        elif kind == "rank2":
+            H = rng.standard_normal((3, 3))
+            H[:, 2] = H[:, 0] - 2 * H[:, 1]
+        elif kind == "zero":
+            H = np.zeros((3, 3))
+        else:
+            H = rng.standard_normal((3, 3))
+        H = np.ascontiguousarray(H)
+        R = np.zeros(9)
+        lib.gcs_mf_rotation(L.dptr(H), L.dptr(R))
+        R = R.reshape(3, 3)
+        assert np.allclose(R @ R.T, np.eye(3), atol=1e-12) and np.linalg.det(R) == pytest.approx(1.0, abs=1e-12)
+        if kind == "zero":
+            assert np.allclose(R, np.eye(3))
+        elif kind != "rank2":           # rank-deficient H: R is not unique; only the rule above holds
+            assert np.allclose(R, _mf_rotation_numpy(H), atol=1e-11)
+
+
 def test_predict_and_fusion_match_oracle(lib):
     rng = np.random.default_rng(13)
     b = ops.Belief.identity_prior()
