@@ -48,13 +48,12 @@ struct gcs_ctx {
   int max_tile_src = 0;
   // per-point
   PointRec* d_recs = nullptr;
-  PointRec* d_recs_s = nullptr;  // bucket order (scale mode)
   uint32_t *d_keys = nullptr, *d_slots = nullptr, *d_sorted = nullptr;
   int* d_nearest = nullptr;
   // per-bin bucketing
   // d_counts holds B counts, [B] = mid-list length, [B+1] pad, then one look-back word per
   // 4096-bucket tile: the whole range is cleared by k_budget every scan
-  uint32_t *d_counts = nullptr, *d_starts = nullptr, *d_mid_list = nullptr;
+  uint32_t *d_counts = nullptr, *d_starts = nullptr, *d_perm = nullptr;
   int n_counts_words = 0;
   uint32_t* d_tickets = nullptr;
   uint8_t* d_flags = nullptr;
@@ -65,8 +64,12 @@ struct gcs_ctx {
   // reductions
   double* d_partials = nullptr;
   size_t partials_len = 0;
+  double* d_part_pts = nullptr;  // k_points block partials (folded later in the scale-mode scan)
+  int pts_blocks = 0;
+  bool pts_fold_pending = false;
   double* d_scalars = nullptr;
-  double* h_scalars = nullptr;  // pinned
+  double* h_scalars = nullptr;  // pinned, mapped
+  double* d_scalars_mirror = nullptr;  // device view of h_scalars
   // host state
   Belief belief{};
   double iw_nu[7], iw_Psi[7 * 36], Q[DZ * DZ];
@@ -129,7 +132,7 @@ StageEv stage_ev(gcs_ctx* c, int st) {
   }
   return e;
 }
-size_t partials_need(long nblocks, int nv) { return (size_t)nblocks * nv; }
+size_t partials_need(long nblocks, int nv) { return (size_t)nblocks * partial_stride(nv); }
 
 void to_host_belief(const gcs_belief& in, Belief& b) {
   memcpy(b.X_anchor, in.X_anchor, sizeof(b.X_anchor));
@@ -220,8 +223,9 @@ int upload_atlas(gcs_ctx* c) {
 }
 
 // ---------------------------------------------------------------- device stages
+// fold_later: leave k_points' cert fold to block 0 of the next k_bins_scale (scale-mode scan)
 int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, const double* w, int n_raw, double t0,
-                 double t1, const double* xi, double* p0_out, double* w_out, double* wb_out) {
+                 double t1, const double* xi, double* p0_out, double* w_out, double* wb_out, bool fold_later = false) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
   if (point_step < 12) return fail(c, GCS_ERR_ARG, "point_step must be >= 12 bytes");
   int stride = std::max(1, (int)((n_raw + (long)c->cap - 1) / c->cap));  // ceil(N/cap), point_budget.py:160
@@ -241,7 +245,8 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   ba.n_zero32 = c->d_counts ? c->B : 0;
   ba.zero8 = c->d_flags;
   ba.n_zero8 = c->d_flags ? c->B : 0;
-  HIPCHK(c, launch_budget(ba, red_blocks(std::max(n_raw, 1)), s, ev.e0, nullptr));
+  const int budget_blocks = red_blocks(std::max(n_raw, 1));
+  HIPCHK(c, launch_budget(ba, budget_blocks, s, ev.e0, nullptr));
   PointKernelArgs a{};
   a.xyz = (const uint8_t*)xyz;
   a.point_step = point_step;
@@ -267,19 +272,24 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.keys = c->d_keys;
   a.slots = c->d_slots;
   a.counts = c->d_counts;
+  a.budget_partials = c->d_partials;
+  a.budget_blocks = budget_blocks;
   a.scalars = c->d_scalars;
   a.p0_out = p0_out;
   a.w_out = w_out;
   a.w_budget_out = wb_out;
   a.nearest_out = c->d_nearest;  // device ids
-  HIPCHK(c, launch_points(a, c->cfg.mode == GCS_MODE_SCALE, c->d_partials, red_blocks(c->cap), s, nullptr, ev.e1));
+  const bool scale = c->cfg.mode == GCS_MODE_SCALE;
+  c->pts_blocks = red_blocks(c->cap);
+  c->pts_fold_pending = scale && fold_later;
+  HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, nullptr, ev.e1));
   return GCS_OK;
 }
 
 BinKernelArgs bin_args(gcs_ctx* c) {
   BinKernelArgs b{};
   b.recs = c->d_recs;
-  b.recs_s = c->d_recs_s;
+  b.perm = c->d_perm;
   b.starts = c->d_starts;
   b.counts = c->d_counts;
   b.flags = c->d_flags;
@@ -296,6 +306,10 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   b.tau = c->cfg.tau;
   b.scan = c->d_scan;
   b.scalars = c->d_scalars;
+  if (c->pts_fold_pending) {
+    b.pts_partials = c->d_part_pts;
+    b.pts_blocks = c->pts_blocks;
+  }
   if (c->d_counts) {
     b.zero_after = c->d_counts + c->B;
     b.n_zero_after = c->n_counts_words - c->B;
@@ -316,20 +330,17 @@ int stage_bins(gcs_ctx* c) {
       ba.keys = c->d_keys;
       ba.slots = c->d_slots;
       ba.knn = c->d_knn;
-      ba.recs = c->d_recs;
       ba.starts = c->d_starts;
       ba.scan_status = c->d_counts + c->B + 2;
       ba.scan_ticket = c->d_tickets;
       ba.slot_idx = c->d_sorted;
-      ba.dest = c->d_slots;  // slots are consumed by k_place before k_bucket_rank writes destinations
-      ba.recs_s = c->d_recs_s;
+      ba.perm = c->d_perm;
       ba.flags = c->d_flags;
-      ba.mid_list = c->d_mid_list;
-      ba.mid_n = c->d_counts + c->B;
       HIPCHK(c, launch_bucketing(ba, c->cap, s, ev.e0, ev.e1));
     }
     StageEv ev = stage_ev(c, ST_BINS);
     HIPCHK(c, launch_bins_scale(b, c->d_partials, s, ev.e0, ev.e1, nullptr));  // stage = the bin kernel itself
+    c->pts_fold_pending = false;
   } else {
     StageEv ev = stage_ev(c, ST_BINS);
     HIPCHK(c, launch_dense(b, c->d_bin_partials, c->d_partials, s, ev.e0, ev.e1));
@@ -344,10 +355,12 @@ int stage_mf(gcs_ctx* c) {
   return GCS_OK;
 }
 
-int stage_pt(gcs_ctx* c) {
+// to_host: the fold also writes the whole scalar block into the mapped host mirror (the scan
+// then only synchronizes; per-operator calls copy with pull_scalars)
+int stage_pt(gcs_ctx* c, bool to_host = false) {
   StageEv ev = stage_ev(c, ST_PT);
   HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
-                      c->stream, ev.e0, ev.e1));
+                      to_host ? c->d_scalars_mirror : nullptr, c->stream, ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -427,11 +440,13 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   c->partials_len = std::max<size_t>({partials_need(kRedBlocks, 24), partials_need(bins_scale_blocks(c->B), bins_partial_nv()),
                                       partials_need(push_blocks(c->B), 10)});
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_part_pts, partials_need(kRedBlocks, 5) * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_tickets, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_tickets, 0, sizeof(uint32_t)))) return GCS_ERR_HIP;
-  if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocDefault))) return GCS_ERR_HIP;
+  if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocMapped))) return GCS_ERR_HIP;
+  if (bad(hipHostGetDevicePointer((void**)&c->d_scalars_mirror, c->h_scalars, 0))) return GCS_ERR_HIP;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_rknn_off, (B + 1) * sizeof(int)))) return GCS_ERR_HIP;
@@ -443,8 +458,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMalloc(&c->d_counts, (size_t)c->n_counts_words * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMemset(c->d_counts, 0, (size_t)c->n_counts_words * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_starts, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_mid_list, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_recs_s, cap * sizeof(PointRec)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_perm, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_flags, B))) return GCS_ERR_HIP;
   } else {
     size_t nchunks = (cap + 255) / 256;
@@ -472,8 +486,8 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
 int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
   void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
-                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_mid_list, c->d_flags, c->d_recs_s, c->d_tickets,
-                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local,
+                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags, c->d_tickets,
+                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -766,12 +780,12 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   auto T1 = clk::now();
   // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
   int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
-                        in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr);
+                        in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, /*fold_later=*/true);
   if (rc) return rc;
   if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
   if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
-  if ((rc = stage_pt(c))) return rc;
-  if ((rc = pull_scalars(c))) return rc;
+  if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the PT fold has written the scalars to h_scalars
   auto T2 = clk::now();
   const double* S = c->h_scalars;
   // budget cert (point_budget.py:182-212)

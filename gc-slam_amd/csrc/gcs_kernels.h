@@ -45,6 +45,8 @@ struct PointKernelArgs {
   uint32_t* keys;
   uint32_t* slots;
   uint32_t* counts;  // per-bin bucket sizes (cleared by k_budget)
+  const double* budget_partials;  // k_budget block partials (folded by every k_points block)
+  int budget_blocks;
   double* scalars;
   // optional debug/parity outputs (may be null)
   double* p0_out;
@@ -59,21 +61,17 @@ struct BucketArgs {
   const uint32_t* keys;
   const uint32_t* slots;
   const int* knn;
-  const PointRec* recs;
   uint32_t* starts;
-  uint32_t* scan_status;  // per 4096-bucket tile look-back word (cleared by k_budget)
+  uint32_t* scan_status;  // per 4096-bucket tile look-back word (re-armed by k_bins_scale)
   uint32_t* scan_ticket;
-  uint32_t* slot_idx;
-  uint32_t* dest;  // per point: bucket-ordered destination (aliases the slot array once placed)
-  PointRec* recs_s;
-  uint8_t* flags;      // active bins (cleared by k_budget)
-  uint32_t* mid_list;  // buckets with more than kLaneRank members
-  uint32_t* mid_n;     // (cleared by k_budget)
+  uint32_t* slot_idx;     // bucket-ordered point indices, arrival order within a bucket
+  uint32_t* perm;         // bucket-ordered point indices, point-index order within a bucket
+  uint8_t* flags;         // active bins (cleared by k_budget)
 };
 
 struct BinKernelArgs {
-  const PointRec* recs;    // point order (dense mode)
-  const PointRec* recs_s;  // bucket order (scale mode)
+  const PointRec* recs;   // point order
+  const uint32_t* perm;   // bucket order -> point index (scale mode)
   const uint32_t* starts;
   const uint32_t* counts;
   const uint8_t* flags;
@@ -89,6 +87,8 @@ struct BinKernelArgs {
   double tau;
   double* scan;  // 26 x B field-major
   double* scalars;
+  const double* pts_partials;  // if set: k_points' partial rows, folded by block 0
+  int pts_blocks;
   uint32_t* zero_after;  // bucketing scratch (mid-list length, look-back words) re-armed for the next scan
   int n_zero_after;
 };
@@ -105,11 +105,13 @@ struct PushArgs {
 // Launchers.  e0/e1 (may be null) are stamped with the first kernel's start and the last
 // kernel's end through hipExtLaunchKernel, so stage timing adds no marker packets to the queue.
 hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
-hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, hipStream_t s, hipEvent_t e0,
-                         hipEvent_t e1);
+// fold: run k_points' cert fold now (else k_bins_scale block 0 folds it, BinKernelArgs.pts_partials)
+hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
+                         hipEvent_t e0, hipEvent_t e1);
 int scan_tiles(int n_bins);
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 int bins_scale_blocks(int n_bins);
+int partial_stride(int nv);  // doubles per block-partial row
 int bins_tile();              // device bins per k_bins_scale workgroup
 int bins_max_tile_sources();  // capacity of its source list
 int bins_max_tile_entries();  // capacity of its reverse-kNN entry list
@@ -122,8 +124,9 @@ hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* pa
                         hipEvent_t e1);
 hipError_t launch_mf(const double* scan, const double* map, int B, double* partials, int nblk, double* scalars,
                      hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+// mirror (may be null): mapped host buffer that receives the whole scalar block after the fold
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+                     double* scalars, double* mirror, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
                               double* partials, double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_map_derive(const double* map, double* derived, int B, double* partials, double* scalars,

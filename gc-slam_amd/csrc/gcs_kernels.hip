@@ -1,19 +1,19 @@
 // HIP kernels for the GC-SLAM bin-path hot path on gfx950 (MI355X).
 //
-//   k_budget_*      PointBudgetResample mass sums   point_budget.py:50-109
-//   k_points        budget gather + DeskewConstantTwist + ray direction + nearest bin +
+//   k_budget        PointBudgetResample mass sums (+ clears the bucketing state)  point_budget.py:50-109
+//   k_points        budget fold + gather + DeskewConstantTwist + ray direction + nearest bin +
 //                   K-candidate softmax normaliser (BinSoftAssign, scale mode) or dense
 //                   softmax normaliser, and the per-point certificate partials
 //                   deskew_constant_twist.py:31-69, pipeline.py:589-593, binning.py:56-76
-//   k_scan_*, k_place, k_bucket_*   deterministic bucketing of points by nearest bin
-//   k_bins_scale    bin-centric gather: ScanBinMomentMatch + Kappa, finalize + write
-//                   binning.py:139-209, kappa.py:130-169
+//   k_scan, k_place, k_bucket_rank   deterministic bucketing of points by nearest bin
+//   k_bins_scale    tiled bin-centric gather: ScanBinMomentMatch + Kappa + Matrix-Fisher terms
+//                   binning.py:139-209, kappa.py:130-169, matrix_fisher_evidence.py:181-211
 //   k_dense_*       the reference's dense N x B form (legacy B=48)
-//   k_mf_*          MatrixFisherRotation bin reduction + device 3x3 SVD
-//                   matrix_fisher_evidence.py:155-256
-//   k_pt_*          PlanarTranslationEvidence bin reduction   matrix_fisher_evidence.py:413-499
-//   k_pushforward   PoseCovInflationPushforward + forgetting + derived map stats
+//   k_mf            MatrixFisherRotation bin reduction (dense mode / per-operator entry point)
+//   k_pt            PlanarTranslationEvidence bin reduction   matrix_fisher_evidence.py:413-499
+//   k_pushforward   PoseCovInflationPushforward + forgetting + derived map stats + map totals
 //                   (declared; bin_atlas.py:137-257)
+//   k_final         one-block folds of block partials (+ R_mf by polar Newton)
 //
 // All reductions are fixed-shape (fixed grid, fixed lane/LDS trees, fixed-order final pass),
 // so results are bitwise reproducible run to run (docs/GC_SLAM.md:1150).  No float atomics.
@@ -81,38 +81,44 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
   return v;
 }
 
-// Final pass over per-block partials (one-block k_final launch): thread t folds partials t,
-// t+256, ... in order, then a fixed tree; the result is valid in thread 0.  Bit k of MAXMASK selects max
-// instead of sum for component k.  lds must hold kWaves*NV doubles.
+// Block partials are stored as rows of pstride(NV) doubles (16, or 32 for NV > 16), so in the
+// fold thread t always owns column t % stride: the block sweeps the partial rows with coalesced,
+// independent loads (rows t / stride, + 256 / stride, ...) and the lanes of one column meet in a
+// fixed xor tree, then a fixed cross-wave order.  The result is valid in thread 0.  Bit k of
+// MAXMASK selects max instead of sum for component k.  lds must hold kWaves * pstride(NV).
+template <int NV>
+__host__ __device__ constexpr int pstride() { return NV <= 16 ? 16 : 32; }
+int partial_stride(int nv) { return nv <= 16 ? 16 : 32; }
+
 template <int NV, unsigned MAXMASK>
 __device__ __forceinline__ void reduce_partials(const double* __restrict__ partials, int nblocks, double (&v)[NV],
                                                 double* lds) {
-#pragma unroll
-  for (int k = 0; k < NV; ++k) v[k] = ((MAXMASK >> k) & 1u) ? -INFINITY : 0.0;
-  for (int b = threadIdx.x; b < nblocks; b += kBlock)
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      double x = partials[(size_t)b * NV + k];
-      v[k] = ((MAXMASK >> k) & 1u) ? fmax(v[k], x) : v[k] + x;
-    }
-#pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    if ((MAXMASK >> k) & 1u) {
-      v[k] = wave_max(v[k]);
-    } else {
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) v[k] += __shfl_xor(v[k], off, 64);
+  constexpr int S = pstride<NV>();
+  constexpr int R = kBlock / S;
+  const int c = threadIdx.x % S, r0 = threadIdx.x / S;
+  const bool is_max = c < NV && ((MAXMASK >> c) & 1u);
+  double a = is_max ? -INFINITY : 0.0;
+  if (c < NV) {
+#pragma unroll 16
+    for (int b = r0; b < nblocks; b += R) {
+      const double x = partials[(size_t)b * S + c];
+      a = is_max ? fmax(a, x) : a + x;
     }
   }
-  int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0)
 #pragma unroll
-    for (int k = 0; k < NV; ++k) lds[wid * NV + k] = v[k];
+  for (int off = S; off < 64; off <<= 1) {
+    const double y = __shfl_xor(a, off, 64);
+    a = is_max ? fmax(a, y) : a + y;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane < S) lds[wid * S + lane] = a;
   __syncthreads();
   if (threadIdx.x == 0) {
+#pragma unroll
     for (int k = 0; k < NV; ++k) {
+      const bool mx = (MAXMASK >> k) & 1u;
       double s = lds[k];
-      for (int w = 1; w < kWaves; ++w) s = ((MAXMASK >> k) & 1u) ? fmax(s, lds[w * NV + k]) : s + lds[w * NV + k];
+      for (int w = 1; w < kWaves; ++w) s = mx ? fmax(s, lds[w * S + k]) : s + lds[w * S + k];
       v[k] = s;
     }
   }
@@ -128,7 +134,7 @@ template <int NV>
 __device__ __forceinline__ void store_partials(const double (&v)[NV], double* base, int idx) {
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int k = 0; k < NV; ++k) base[(size_t)idx * NV + k] = v[k];
+    for (int k = 0; k < NV; ++k) base[(size_t)idx * pstride<NV>() + k] = v[k];
 }
 
 // ---------------------------------------------------------------- row 1: budget mass sums
@@ -183,8 +189,29 @@ __device__ __forceinline__ void ray_dir(double px, double py, double pz, const d
 template <bool SCALE, int KC>
 __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* partials) {
   __shared__ double lds[kWaves * 5];
-  const double mass_scale = a.scalars[SC_MASS_SCALE];
-  const double mass_in = a.scalars[SC_MASS_IN];
+  __shared__ double s_mass[2];
+  // budget mass sums: every block folds k_budget's partial rows itself (same fixed order in every
+  // block), so no separate fold launch sits between the two kernels; block 0 publishes them
+  {
+    double v[2] = {0.0, 0.0};
+    for (int r = threadIdx.x; r < a.budget_blocks; r += kBlock) {
+      v[0] += a.budget_partials[(size_t)r * pstride<2>()];
+      v[1] += a.budget_partials[(size_t)r * pstride<2>() + 1];
+    }
+    block_sum<2>(v, lds);
+    if (threadIdx.x == 0) {
+      s_mass[0] = v[0];
+      s_mass[1] = v[0] / (v[1] + kEpsMass);  // mass_scale, point_budget.py:80-84
+      if (blockIdx.x == 0) {
+        a.scalars[SC_MASS_IN] = v[0];
+        a.scalars[SC_MASS_SEL] = v[1];
+        a.scalars[SC_MASS_SCALE] = s_mass[1];
+      }
+    }
+    __syncthreads();
+  }
+  const double mass_scale = s_mass[1];
+  const double mass_in = s_mass[0];
   const double denom = a.t1 - a.t0 > 1e-12 ? a.t1 - a.t0 : 1e-12;
   const double inv_tau = 1.0 / a.tau;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sum w_budget, sum wn^2, sum w_out, sum H
@@ -321,20 +348,21 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
 // k_points took an arrival slot per point (atomic per-bucket counts).  k_scan: start[] =
 // exclusive scan of the counts in one pass (decoupled look-back over 4096-bucket tiles, one
 // wave reading 64 predecessors per step).  k_place scatters point indices by slot.
-// k_bucket_rank gives every member its rank by point index inside its bucket (one lane per
-// bucket up to kLaneRank members, else one wave per bucket in k_bucket_mid; above kRankMax an
-// in-order compaction over all keys) and writes the member's destination start+rank; it also
-// marks the K candidate bins of every non-empty bucket active.  k_gather then moves every point
-// record to its destination, so each bucket's records are contiguous in point-index order and
-// the bin gather streams them in a scheduling-independent order.
-constexpr int kScanTile = 4096;
+// k_bucket_rank ranks every bucket's members by point index (one lane per bucket up to
+// kLaneRank members, the lane's wave for larger ones) into perm[], so perm lists each bucket's
+// points contiguously in point-index order and the bin kernel visits them in a
+// scheduling-independent order; it also marks the K candidate bins of every non-empty bucket
+// active.
+constexpr int kScanThreads = 256;
+constexpr int kScanTile = 16 * kScanThreads;  // 16 counts per thread (4 x 16-B loads)
 constexpr int kLaneRank = 16;
 constexpr int kRankMax = 8192;
 constexpr uint32_t kLbAgg = 1u << 30, kLbPre = 2u << 30, kLbVal = (1u << 30) - 1u;
 
-__global__ __launch_bounds__(kBlock) void k_scan(const uint32_t* __restrict__ counts, int n, uint32_t* status,
-                                                 uint32_t* ticket, uint32_t* start) {
-  __shared__ uint32_t wsum[kWaves];
+__global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restrict__ counts, int n, uint32_t* status,
+                                                       uint32_t* ticket, uint32_t* start) {
+  constexpr int kSW = kScanThreads / 64;
+  __shared__ uint32_t wsum[kSW];
   __shared__ uint32_t s_tile, s_excl;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   if (t == 0) s_tile = atomicAdd(ticket, 1u);  // tiles are numbered in start order (forward progress)
@@ -342,12 +370,19 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint32_t* __restrict__ co
   const uint32_t tile = s_tile;
   const int base = (int)tile * kScanTile + 16 * t;
   uint32_t v[16];
+  if (base + 16 <= n) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 u = *(const uint4*)(counts + base + 4 * q);
+      v[4 * q] = u.x; v[4 * q + 1] = u.y; v[4 * q + 2] = u.z; v[4 * q + 3] = u.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = (base + j < n) ? counts[base + j] : 0u;
+  }
   uint32_t tot = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    v[j] = (base + j < n) ? counts[base + j] : 0u;
-    tot += v[j];
-  }
+  for (int j = 0; j < 16; ++j) tot += v[j];
   uint32_t x = tot;
   for (int off = 1; off < 64; off <<= 1) {
     uint32_t y = __shfl_up(x, off, 64);
@@ -356,7 +391,8 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint32_t* __restrict__ co
   if (lane == 63) wsum[wid] = x;
   __syncthreads();
   if (wid == 0) {
-    const uint32_t agg = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    uint32_t agg = 0;
+    for (int w = 0; w < kSW; ++w) agg += wsum[w];
     uint32_t excl = 0;
     if (tile == 0) {
       if (lane == 0) __hip_atomic_store(status, kLbPre | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -392,10 +428,19 @@ __global__ __launch_bounds__(kBlock) void k_scan(const uint32_t* __restrict__ co
   __syncthreads();
   uint32_t pre = s_excl + x - tot;
   for (int w = 0; w < wid; ++w) pre += wsum[w];
+  uint32_t o[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    if (base + j < n) start[base + j] = pre;
+    o[j] = pre;
     pre += v[j];
+  }
+  if (base + 16 <= n) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(uint4*)(start + base + 4 * q) = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (base + j < n) start[base + j] = o[j];
   }
 }
 
@@ -408,80 +453,64 @@ __global__ __launch_bounds__(kBlock) void k_place(const uint32_t* __restrict__ k
   }
 }
 
-// one lane per bucket (grid covers all buckets exactly once)
-__global__ __launch_bounds__(kBlock) void k_bucket_rank(BucketArgs b) {
+// One lane per bucket (grid covers all buckets exactly once).  Buckets of up to kLaneRank members
+// are ranked in the lane's registers; larger ones are ranked afterwards by the whole wave (64
+// members per step by shuffles), and above kRankMax by an in-order compaction over all keys (one
+// wave, O(N): a degenerate case).  perm[start + rank] = point index.
+__global__ __launch_bounds__(kBlock) void k_bucket_rank(BucketArgs b, int n) {
   const int a = blockIdx.x * kBlock + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const uint32_t c = a < b.n_bins ? b.counts[a] : 0u;
-  const bool mid = c > (uint32_t)kLaneRank;
-  const unsigned long long mm = __ballot(mid);
-  if (mm) {  // wave-aggregated append to the mid list
-    const int leader = __ffsll((long long)mm) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(b.mid_n, (uint32_t)__popcll(mm));
-    base = __shfl(base, leader, 64);
-    if (mid) b.mid_list[base + (uint32_t)__popcll(mm & ((1ull << lane) - 1ull))] = (uint32_t)a;
-  }
-  if (c == 0u) return;
-  const int* kr = b.knn + (size_t)a * b.k;
-  for (int q = 0; q < b.k; q += 4) {
-    int4 c4 = *(const int4*)(kr + q);
-    b.flags[c4.x] = 1; b.flags[c4.y] = 1; b.flags[c4.z] = 1; b.flags[c4.w] = 1;
-  }
-  if (mid) return;
-  const uint32_t st = b.starts[a];
-  const uint32_t* sl = b.slot_idx + st;
-  uint32_t idx[kLaneRank];
-#pragma unroll
-  for (int j = 0; j < kLaneRank; ++j) idx[j] = (uint32_t)j < c ? sl[j] : 0xffffffffu;
-#pragma unroll
-  for (int j = 0; j < kLaneRank; ++j) {
-    if ((uint32_t)j < c) {
-      uint32_t r = 0;
-#pragma unroll
-      for (int q = 0; q < kLaneRank; ++q) r += idx[q] < idx[j] ? 1u : 0u;
-      b.dest[idx[j]] = st + r;
+  const uint32_t st = c ? b.starts[a] : 0u;
+  if (c) {
+    const int* kr = b.knn + (size_t)a * b.k;
+    for (int q = 0; q < b.k; q += 4) {
+      int4 c4 = *(const int4*)(kr + q);
+      b.flags[c4.x] = 1; b.flags[c4.y] = 1; b.flags[c4.z] = 1; b.flags[c4.w] = 1;
     }
   }
-}
-
-// one wave per bucket with more than kLaneRank members
-__global__ __launch_bounds__(kBlock) void k_bucket_mid(BucketArgs b, int n) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t nb = *b.mid_n;
-  const uint32_t nw = gridDim.x * kWaves;
-  for (uint32_t w = blockIdx.x * kWaves + (threadIdx.x >> 6); w < nb; w += nw) {
-    const uint32_t a = b.mid_list[w];
-    const uint32_t c = b.counts[a], st = b.starts[a];
-    if (c <= (uint32_t)kRankMax) {
-      for (uint32_t j0 = 0; j0 < c; j0 += 64) {
-        uint32_t v = (j0 + lane < c) ? b.slot_idx[st + j0 + lane] : 0xffffffffu;
+  if (c && c <= (uint32_t)kLaneRank) {
+    const uint32_t* sl = b.slot_idx + st;
+    uint32_t idx[kLaneRank];
+#pragma unroll
+    for (int j = 0; j < kLaneRank; ++j) idx[j] = (uint32_t)j < c ? sl[j] : 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < kLaneRank; ++j) {
+      if ((uint32_t)j < c) {
+        uint32_t r = 0;
+#pragma unroll
+        for (int q = 0; q < kLaneRank; ++q) r += idx[q] < idx[j] ? 1u : 0u;
+        b.perm[st + r] = idx[j];
+      }
+    }
+  }
+  unsigned long long big = __ballot(c > (uint32_t)kLaneRank);
+  while (big) {  // wave-cooperative ranking of this wave's large buckets, one at a time
+    const int src = __ffsll((long long)big) - 1;
+    big &= big - 1ull;
+    const uint32_t cb = __shfl(c, src, 64), sb = __shfl(st, src, 64);
+    const uint32_t ab = (uint32_t)__shfl(a, src, 64);
+    if (cb <= (uint32_t)kRankMax) {
+      for (uint32_t j0 = 0; j0 < cb; j0 += 64) {
+        const uint32_t v = (j0 + lane < cb) ? b.slot_idx[sb + j0 + lane] : 0xffffffffu;
         uint32_t rank = 0;
-        for (uint32_t k0 = 0; k0 < c; k0 += 64) {
-          uint32_t u = (k0 + lane < c) ? b.slot_idx[st + k0 + lane] : 0xffffffffu;
+        for (uint32_t k0 = 0; k0 < cb; k0 += 64) {
+          const uint32_t u = (k0 + lane < cb) ? b.slot_idx[sb + k0 + lane] : 0xffffffffu;
           for (int jj = 0; jj < 64; ++jj) rank += (__shfl(u, jj, 64) < v) ? 1u : 0u;
         }
-        if (j0 + lane < c) b.dest[v] = st + rank;
+        if (j0 + lane < cb) b.perm[sb + rank] = v;
       }
-    } else {  // in-order compaction over all keys
-      uint32_t pos = st;
+    } else {
+      uint32_t pos = sb;
       for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
-        const bool hit = i < n && b.keys[i] == a;
+        const bool hit = i < n && b.keys[i] == ab;
         const unsigned long long m = __ballot(hit);
-        if (hit) b.dest[i] = pos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (hit) b.perm[pos + (uint32_t)__popcll(m & ((1ull << lane) - 1ull))] = (uint32_t)i;
         pos += (uint32_t)__popcll(m);
       }
     }
   }
-}
-
-// every valid point record to its bucket-ordered destination
-__global__ __launch_bounds__(kBlock) void k_gather(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ dest,
-                                                   int n, int n_bins, const PointRec* __restrict__ recs,
-                                                   PointRec* __restrict__ recs_s) {
-  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-    if (keys[i] < (uint32_t)n_bins) recs_s[dest[i]] = recs[i];
 }
 
 // ---------------------------------------------------------------- bin finalize (shared)
@@ -651,6 +680,12 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   const int nb = min(kBinTile, a.n_bins - b0);
   PROF(0);
   for (int j = blockIdx.x * kBlock + t; j < a.n_zero_after; j += gridDim.x * kBlock) a.zero_after[j] = 0u;
+  if (blockIdx.x == 0 && a.pts_partials) {  // k_points' cert partials (off the critical path here)
+    double pv[5];
+    reduce_partials<5, 16u>(a.pts_partials, a.pts_blocks, pv, lds);
+    if (t == 0)
+      for (int f = 0; f < 5; ++f) a.scalars[SC_DESKEW_WIN + f] = pv[f];
+  }
   // phase D's bin (thread t < nb owns bin b0 + t): flag and map direction stats up front
   const bool own = t < nb;
   const bool own_act = own && a.flags[b0 + t];
@@ -705,7 +740,7 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
         int mid = (lo + hi + 1) >> 1;
         if (s_off[mid] <= r) lo = mid; else hi = mid - 1;
       }
-      const PointRec pr = a.recs_s[s_st[lo] + (r - s_off[lo])];
+      const PointRec pr = a.recs[a.perm[s_st[lo] + (r - s_off[lo])]];
       double* d = s_rec + (size_t)r * kRecD;
       d[0] = pr.x; d[1] = pr.y; d[2] = pr.z; d[3] = pr.dx; d[4] = pr.dy; d[5] = pr.dz;
       d[6] = pr.m; d[7] = pr.w * pr.iz;
@@ -742,7 +777,7 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
         const double* rp = s_rec + (size_t)(s_off[j] + kk) * kRecD;
         bin_contrib(acc, bd, inv_tau, rp[0], rp[1], rp[2], rp[3], rp[4], rp[5], rp[6], rp[7]);
       } else {
-        const PointRec pr = a.recs_s[s_st[j] + kk];
+        const PointRec pr = a.recs[a.perm[s_st[j] + kk]];
         bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, pr.dx, pr.dy, pr.dz, pr.m, pr.w * pr.iz);
       }
       if (++kk == c && i + 1 < i1) {  // next non-empty source
@@ -1057,12 +1092,8 @@ __global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict_
 // ---------------------------------------------------------------- one-block folds of block partials
 enum FinalKind : int { FIN_BUDGET, FIN_POINTS, FIN_BINS, FIN_DENSE, FIN_MF, FIN_PT, FIN_TOTALS };
 
-template <int NV, unsigned MAXMASK, int KIND>
-__global__ __launch_bounds__(kBlock) void k_final(const double* __restrict__ partials, int nblocks, double* scalars) {
-  __shared__ double lds[kWaves * NV];
-  double v[NV];
-  reduce_partials<NV, MAXMASK>(partials, nblocks, v, lds);
-  if (threadIdx.x != 0) return;
+template <int NV, int KIND>
+__device__ __forceinline__ void final_epilogue(const double (&v)[NV], double* scalars) {
   if (KIND == FIN_BUDGET) {
     scalars[SC_MASS_IN] = v[0];
     scalars[SC_MASS_SEL] = v[1];
@@ -1088,9 +1119,26 @@ __global__ __launch_bounds__(kBlock) void k_final(const double* __restrict__ par
   }
 }
 
-#define GCS_FINAL(NV, MASK, KIND, nblk, s, e1, partials, scalars)                                                   \
+// mirror (may be null): after the epilogue the whole scalar block is copied to this mapped host
+// buffer, so the host reads the scan's results without a separate D2H copy.
+template <int NV, unsigned MAXMASK, int KIND>
+__global__ __launch_bounds__(kBlock) void k_final(const double* __restrict__ partials, int nblocks, double* scalars,
+                                                  double* mirror) {
+  __shared__ double lds[kWaves * pstride<NV>()];
+  double v[NV];
+  reduce_partials<NV, MAXMASK>(partials, nblocks, v, lds);
+  if (threadIdx.x == 0) final_epilogue<NV, KIND>(v, scalars);
+  if (mirror) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < SC_COUNT; i += kBlock) mirror[i] = scalars[i];
+  }
+}
+
+#define GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, mirror)                                         \
   hipExtLaunchKernelGGL(k_final<NV, MASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0, (const double*)partials, \
-                        (int)(nblk), scalars)
+                        (int)(nblk), scalars, (double*)(mirror))
+#define GCS_FINAL(NV, MASK, KIND, nblk, s, e1, partials, scalars) \
+  GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, nullptr)
 
 // ---------------------------------------------------------------- launchers
 static int grid_for(long n, int cap_blocks) {
@@ -1101,13 +1149,12 @@ static int grid_for(long n, int cap_blocks) {
 int push_blocks(int n_bins) { return grid_for(n_bins, 4096); }
 
 hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  hipExtLaunchKernelGGL(k_budget, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a);
-  GCS_FINAL(2, 0u, FIN_BUDGET, nblk, s, e1, a.partials, a.scalars);
+  hipExtLaunchKernelGGL(k_budget, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a);  // folded inside k_points
   return hipGetLastError();
 }
 
-hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, hipStream_t s, hipEvent_t e0,
-                         hipEvent_t e1) {
+hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
+                         hipEvent_t e0, hipEvent_t e1) {
   if (scale) {
     switch (a.k) {
       case 8: hipExtLaunchKernelGGL(k_points<true, 8>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
@@ -1118,22 +1165,23 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
   } else {
     hipExtLaunchKernelGGL(k_points<false, 1>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials);
   }
-  GCS_FINAL(5, 16u, FIN_POINTS, nblk, s, e1, partials, a.scalars);
+  if (fold) {
+    GCS_FINAL(5, 16u, FIN_POINTS, nblk, s, e1, partials, a.scalars);
+  } else if (e1) {  // the fold rides in k_bins_scale's block 0; close the stage on an empty marker
+    (void)hipEventRecord(e1, s);
+  }
   return hipGetLastError();
 }
 
 int scan_tiles(int n_bins) { return (n_bins + kScanTile - 1) / kScanTile; }
 
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  hipExtLaunchKernelGGL(k_scan, dim3(scan_tiles(b.n_bins)), dim3(kBlock), 0, s, e0, nullptr, 0,
+  hipExtLaunchKernelGGL(k_scan, dim3(scan_tiles(b.n_bins)), dim3(kScanThreads), 0, s, e0, nullptr, 0,
                         (const uint32_t*)b.counts, b.n_bins, b.scan_status, b.scan_ticket, b.starts);
   hipLaunchKernelGGL(k_place, dim3(grid_for(n, 2048)), dim3(kBlock), 0, s, (const uint32_t*)b.keys,
                      (const uint32_t*)b.slots, (const uint32_t*)b.starts, n, b.n_bins, b.slot_idx);
-  hipLaunchKernelGGL(k_bucket_rank, dim3((b.n_bins + kBlock - 1) / kBlock), dim3(kBlock), 0, s, b);
-  hipLaunchKernelGGL(k_bucket_mid, dim3(256), dim3(kBlock), 0, s, b, n);
-  hipExtLaunchKernelGGL(k_gather, dim3(grid_for(n, 2048)), dim3(kBlock), 0, s, nullptr, e1, 0,
-                        (const uint32_t*)b.keys, (const uint32_t*)b.dest, n, b.n_bins, (const PointRec*)b.recs,
-                        b.recs_s);
+  hipExtLaunchKernelGGL(k_bucket_rank, dim3((b.n_bins + kBlock - 1) / kBlock), dim3(kBlock), 0, s, nullptr, e1, 0, b,
+                        n);
   return hipGetLastError();
 }
 
@@ -1167,10 +1215,10 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 }
 
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+                     double* scalars, double* mirror, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B,
                         (const double*)scalars, partials);
-  GCS_FINAL(kPtNV, 0u, FIN_PT, nblk, s, e1, partials, scalars);
+  GCS_FINAL_M(kPtNV, 0u, FIN_PT, nblk, s, e1, partials, scalars, mirror);
   return hipGetLastError();
 }
 
