@@ -57,6 +57,7 @@ struct gcs_ctx {
   int n_counts_words = 0;
   uint32_t* d_tickets = nullptr;
   uint8_t* d_flags = nullptr;
+  uint8_t* d_touched = nullptr;  // per bin: the map holds mass (k_map_derive / k_pushforward)
   double* d_scan = nullptr;
   double* d_map = nullptr;
   double* d_derived = nullptr;
@@ -132,7 +133,6 @@ StageEv stage_ev(gcs_ctx* c, int st) {
   }
   return e;
 }
-size_t partials_need(long nblocks, int nv) { return (size_t)nblocks * partial_stride(nv); }
 
 void to_host_belief(const gcs_belief& in, Belief& b) {
   memcpy(b.X_anchor, in.X_anchor, sizeof(b.X_anchor));
@@ -244,7 +244,7 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   ba.zero32 = c->d_counts;  // counts only: the bucketing scratch after them is re-armed by k_bins_scale
   ba.n_zero32 = c->d_counts ? c->B : 0;
   ba.zero8 = c->d_flags;
-  ba.n_zero8 = c->d_flags ? c->B : 0;
+  ba.n_zero8 = c->d_flags ? c->B + bins_scale_blocks(c->B) : 0;
   const int budget_blocks = red_blocks(std::max(n_raw, 1));
   HIPCHK(c, launch_budget(ba, budget_blocks, s, ev.e0, nullptr));
   PointKernelArgs a{};
@@ -360,7 +360,7 @@ int stage_mf(gcs_ctx* c) {
 int stage_pt(gcs_ctx* c, bool to_host = false) {
   StageEv ev = stage_ev(c, ST_PT);
   HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
-                      to_host ? c->d_scalars_mirror : nullptr, c->stream, ev.e0, ev.e1));
+                      to_host ? c->d_scalars_mirror : nullptr, c->d_flags, c->d_touched, c->stream, ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -383,8 +383,8 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) 
     for (int j = 0; j < 3; ++j) pa.G[3 * i + j] = RS[3 * i] * pa.R[3 * j] + RS[3 * i + 1] * pa.R[3 * j + 1] + RS[3 * i + 2] * pa.R[3 * j + 2];
   pa.gamma = gamma;
   StageEv ev = stage_ev(c, ST_PUSH);
-  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->d_partials, c->d_scalars, c->stream,
-                               ev.e0, ev.e1));
+  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->d_partials, c->d_scalars, c->d_flags,
+                               c->d_touched, c->stream, ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -437,6 +437,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_derived, B * MD_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_map, 0, B * MF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scan, 0, B * SF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_touched, B))) return GCS_ERR_HIP;
   c->partials_len = std::max<size_t>({partials_need(kRedBlocks, 24), partials_need(bins_scale_blocks(c->B), bins_partial_nv()),
                                       partials_need(push_blocks(c->B), 10)});
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
@@ -459,7 +460,9 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMemset(c->d_counts, 0, (size_t)c->n_counts_words * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_starts, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_perm, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_flags, B))) return GCS_ERR_HIP;
+    // bin flags, then one flag per k_bins_scale tile (both cleared by k_budget every scan)
+    if (bad(hipMalloc(&c->d_flags, B + bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
+    if (bad(hipMemset(c->d_flags, 0, B + bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
   } else {
     size_t nchunks = (cap + 255) / 256;
     if (bad(hipMalloc(&c->d_bin_partials, nchunks * 19 * B * sizeof(double)))) return GCS_ERR_HIP;
@@ -470,7 +473,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     gcs_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
-  if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars,
+  if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, c->d_touched,
                             c->stream)))
     return GCS_ERR_HIP;
   if (bad(hipStreamSynchronize(c->stream))) return GCS_ERR_HIP;
@@ -486,7 +489,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
 int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
   void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
-                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags, c->d_tickets,
+                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags, c->d_touched, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
@@ -564,7 +567,7 @@ int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
   std::vector<double> dev((size_t)c->B * MF_COUNT);
   to_device_order(c, MF_COUNT, map, dev.data());
   HIPCHK(c, hipMemcpy(c->d_map, dev.data(), dev.size() * sizeof(double), hipMemcpyHostToDevice));
-  HIPCHK(c, launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars,
+  HIPCHK(c, launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, c->d_touched,
                               c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
@@ -1063,6 +1066,12 @@ int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps, double* Li) {
 int gcs_svd3(const double* H, double* U, double* s, double* V) {
   if (!H || !U || !s || !V) return GCS_ERR_ARG;
   svd3(H, U, s, V);
+  return GCS_OK;
+}
+int gcs_psd_project3(const double* M, double* out, double* delta) {
+  if (!M || !out) return GCS_ERR_ARG;
+  const double d = psd_project3(M, out);
+  if (delta) *delta = d;
   return GCS_OK;
 }
 int gcs_mf_rotation(const double* H, double* R) {

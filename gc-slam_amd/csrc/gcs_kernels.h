@@ -112,6 +112,8 @@ int scan_tiles(int n_bins);
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 int bins_scale_blocks(int n_bins);
 int partial_stride(int nv);  // doubles per block-partial row
+// doubles a partials buffer needs for nblocks rows of nv values (+ the two-level fold's rows)
+size_t partials_need(long nblocks, int nv);
 int bins_tile();              // device bins per k_bins_scale workgroup
 int bins_max_tile_sources();  // capacity of its source list
 int bins_max_tile_entries();  // capacity of its reverse-kNN entry list
@@ -125,11 +127,16 @@ hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* pa
 hipError_t launch_mf(const double* scan, const double* map, int B, double* partials, int nblk, double* scalars,
                      hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 // mirror (may be null): mapped host buffer that receives the whole scalar block after the fold
+// act (scan-active bin flags, null = all) and touched (bin has map mass) let k_pt and
+// k_pushforward skip bins that are zero in both the scan and the map
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, double* mirror, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
+                     hipEvent_t e0, hipEvent_t e1);
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
-                              double* partials, double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+                              double* partials, double* scalars, const uint8_t* act, uint8_t* touched, hipStream_t s,
+                              hipEvent_t e0, hipEvent_t e1);
+// also rebuilds touched from the map
 hipError_t launch_map_derive(const double* map, double* derived, int B, double* partials, double* scalars,
-                             hipStream_t s);
+                             uint8_t* touched, hipStream_t s);
 
 }  // namespace gcs

@@ -30,6 +30,7 @@ namespace gcs {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
+constexpr int kBinTile = 64;  // device bins per k_bins_scale workgroup (a Hilbert patch, gcs_atlas.h)
 
 // ---------------------------------------------------------------- reductions
 template <int NV>
@@ -81,11 +82,13 @@ __device__ __forceinline__ double block_max(double v, double* lds) {
   return v;
 }
 
-// Block partials are stored as rows of pstride(NV) doubles (16, or 32 for NV > 16), so in the
-// fold thread t always owns column t % stride: the block sweeps the partial rows with coalesced,
-// independent loads (rows t / stride, + 256 / stride, ...) and the lanes of one column meet in a
-// fixed xor tree, then a fixed cross-wave order.  The result is valid in thread 0.  Bit k of
-// MAXMASK selects max instead of sum for component k.  lds must hold kWaves * pstride(NV).
+// Block partials are stored as rows of pstride(NV) doubles (16, or 32 for NV > 16).  In the fold
+// G = stride / 4 threads share a row, thread t loading columns 4 (t % G) .. +3 (one 32-B load) of
+// rows t / G, t / G + 256 / G, ...: the block sweeps 64 (or 32) rows per pass with coalesced,
+// independent loads, the lanes of one column group meet in a fixed xor tree, then a fixed
+// cross-wave order.
+// The result is valid in thread 0.  Bit k of MAXMASK selects max instead of sum for component k.
+// lds must hold kWaves * pstride(NV).  Columns >= NV are never read back.
 template <int NV>
 __host__ __device__ constexpr int pstride() { return NV <= 16 ? 16 : 32; }
 int partial_stride(int nv) { return nv <= 16 ? 16 : 32; }
@@ -94,24 +97,35 @@ template <int NV, unsigned MAXMASK>
 __device__ __forceinline__ void reduce_partials(const double* __restrict__ partials, int nblocks, double (&v)[NV],
                                                 double* lds) {
   constexpr int S = pstride<NV>();
-  constexpr int R = kBlock / S;
-  const int c = threadIdx.x % S, r0 = threadIdx.x / S;
-  const bool is_max = c < NV && ((MAXMASK >> c) & 1u);
-  double a = is_max ? -INFINITY : 0.0;
-  if (c < NV) {
-#pragma unroll 16
-    for (int b = r0; b < nblocks; b += R) {
-      const double x = partials[(size_t)b * S + c];
-      a = is_max ? fmax(a, x) : a + x;
-    }
+  constexpr int G = S / 4;
+  constexpr int R = kBlock / G;
+  const int c0 = 4 * (threadIdx.x % G), r0 = threadIdx.x / G;
+  bool mx[4];
+  double a[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    mx[k] = c0 + k < NV && ((MAXMASK >> (c0 + k)) & 1u);
+    a[k] = mx[k] ? -INFINITY : 0.0;
+  }
+#pragma unroll 8
+  for (int b = r0; b < nblocks; b += R) {
+    const double4 x = *(const double4*)(partials + (size_t)b * S + c0);
+    a[0] = mx[0] ? fmax(a[0], x.x) : a[0] + x.x;
+    a[1] = mx[1] ? fmax(a[1], x.y) : a[1] + x.y;
+    a[2] = mx[2] ? fmax(a[2], x.z) : a[2] + x.z;
+    a[3] = mx[3] ? fmax(a[3], x.w) : a[3] + x.w;
   }
 #pragma unroll
-  for (int off = S; off < 64; off <<= 1) {
-    const double y = __shfl_xor(a, off, 64);
-    a = is_max ? fmax(a, y) : a + y;
-  }
+  for (int off = G; off < 64; off <<= 1)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double y = __shfl_xor(a[k], off, 64);
+      a[k] = mx[k] ? fmax(a[k], y) : a[k] + y;
+    }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane < S) lds[wid * S + lane] = a;
+  if (lane < G)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lds[wid * S + c0 + k] = a[k];
   __syncthreads();
   if (threadIdx.x == 0) {
 #pragma unroll
@@ -462,11 +476,13 @@ __global__ __launch_bounds__(kBlock) void k_bucket_rank(BucketArgs b, int n) {
   const int lane = threadIdx.x & 63;
   const uint32_t c = a < b.n_bins ? b.counts[a] : 0u;
   const uint32_t st = c ? b.starts[a] : 0u;
-  if (c) {
+  if (c) {  // candidate bins active, and their k_bins_scale tiles (flags[n_bins + tile])
     const int* kr = b.knn + (size_t)a * b.k;
+    uint8_t* tf = b.flags + b.n_bins;
     for (int q = 0; q < b.k; q += 4) {
       int4 c4 = *(const int4*)(kr + q);
       b.flags[c4.x] = 1; b.flags[c4.y] = 1; b.flags[c4.z] = 1; b.flags[c4.w] = 1;
+      tf[c4.x / kBinTile] = 1; tf[c4.y / kBinTile] = 1; tf[c4.z / kBinTile] = 1; tf[c4.w / kBinTile] = 1;
     }
   }
   if (c && c <= (uint32_t)kLaneRank) {
@@ -621,26 +637,33 @@ __device__ void mf_finish(const double* v, double* scalars) {
 constexpr int kBinNV = 16;
 
 // ---------------------------------------------------------------- row 5+6 scale mode: bin-centric
-// One 256-thread workgroup per tile of 128 consecutive device bins (a compact Hilbert patch of
-// the sphere, gcs_atlas.h).
+// One 256-thread workgroup per tile of kBinTile = 64 consecutive device bins (a compact Hilbert
+// patch of the sphere, gcs_atlas.h).
+//  0: a tile none of whose bins is a candidate of a non-empty bucket (tile flag, set by
+//     k_bucket_rank) has exact-zero sums: wave 0 writes the zero-bin rows and the tile's partial
+//     row in closed form; A-D are skipped.  With the VLP-16-like scans (rings within +-15 deg)
+//     most tiles of the sphere are such.
 //  A: the tile's bin directions, reverse-kNN ranges and local source indices go to LDS; the
-//     tile's unique source buckets (host table, ~2 per bin) get sizes, starts and staged offsets
-//     (block scan); each bin's work (records to visit) is summed.
-//  B: the sources' records, which each bin of the tile reads ~K/2 times, are staged once into LDS
-//     (64 B: p, d, m, w/Z); a tile with more than kStage records reads them from HBM/L2 instead.
-//  C: a lane pair per bin accumulates the bin's records in fixed order (the bin's sources in
-//     ascending bucket id, each source's points in ascending index; lane l takes the l-th half;
-//     one xor add) -- LDS traffic only.
-//  D: the sums go through LDS to one lane per bin (waves 0-1; waves 2-3 only join the block
-//     reduction): PSD, kappa, the bin's Matrix-Fisher term, coalesced 128-bin output rows.
-// LDS < 80 KiB: two workgroups per CU.
-constexpr int kBinTile = 128;
+//     tile's unique source buckets (host table, ~2.3 per bin) get sizes, starts and staged
+//     offsets (block scan); each bin's work (records to visit) is summed.
+//  B: the sources' records, which each bin of the tile reads ~K/2.3 times, are staged once into
+//     LDS (64 B: p, d, m, w/Z); a tile with more than STAGE records reads them from HBM/L2.
+//  C: four lanes per bin accumulate the bin's records in fixed order (the bin's sources in
+//     ascending bucket id, each source's points in ascending index, as one flattened list; lane l
+//     takes the l-th quarter; two xor adds) -- LDS traffic only.  (Work-proportional lane groups
+//     were measured slower: the group bookkeeping and the deeper shuffle trees cost more than the
+//     balance bought back)
+//  D: wave 0, one lane per bin: PSD, kappa, the bin's Matrix-Fisher term, coalesced 64-bin output
+//     rows, the tile's partial row by a wave reduction.
+// STAGE: kStageBig when the scan is dense in the map (cap >= 0.4 B, C2: 42 KiB of LDS, three
+// workgroups per CU), kStageSmall otherwise (C3: 26 KiB; four per CU, register-limited).
+constexpr int kMaxSrc = 320;   // atlas tables for B = 1k .. 1M have at most 199 per 64-bin tile
+constexpr int kMaxRl = 1280;   // reverse-kNN entries of one tile (~K x kBinTile; at most 1070)
 constexpr int kBinLanes = kBlock / kBinTile;
-constexpr int kMaxSrc = 768;
-constexpr int kMaxRl = 3072;  // reverse-kNN entries of one tile (~K x kBinTile)
-constexpr int kStage = 896;
+constexpr int kStageBig = 512, kStageSmall = 256;
 constexpr int kRecD = 8;  // staged record: x y z dx dy dz m w/Z
-static_assert(kStage * kRecD >= 19 * kBinTile, "phase D reuses the record stage for the bin sums");
+static_assert(kBinLanes == 4, "phase C splits each bin over four lanes");
+static_assert(kStageSmall * kRecD >= 19 * kBinTile, "phase D reuses the record stage for the bin sums");
 int bins_tile() { return kBinTile; }
 int bins_max_tile_sources() { return kMaxSrc; }
 int bins_max_tile_entries() { return kMaxRl; }
@@ -655,25 +678,41 @@ __device__ __forceinline__ void bin_contrib(double* acc, const double4& bd, doub
 }
 
 #ifdef GCS_PHASE_PROF
-__device__ unsigned long long g_prof[16384 * 8];
+__device__ unsigned long long g_prof[32768 * 16];
 extern "C" int gcs_debug_prof(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), (size_t)n * sizeof(unsigned long long));
 }
 #define PROF(k) \
-  if (threadIdx.x == 0) g_prof[blockIdx.x * 8 + (k)] = wall_clock64();
+  if (threadIdx.x == 0) g_prof[blockIdx.x * 16 + (k)] = wall_clock64();
+#define PROFV(k, v) \
+  if (threadIdx.x == 0) g_prof[blockIdx.x * 16 + (k)] = (unsigned long long)(v);
 #else
 #define PROF(k)
+#define PROFV(k, v)
 #endif
 
+// Wave 0's reduction of the per-bin cert / Matrix-Fisher terms into the tile's partial row:
+// [sum N, sum N^2, sum N/(N+eps), sum psd delta, max eps ratio | MF 11] (fixed xor tree).
+__device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < kBinNV; ++k) {
+      const double y = __shfl_xor(v[k], off, 64);
+      v[k] = k == 4 ? fmax(v[k], y) : v[k] + y;
+    }
+}
+
+template <int STAGE>
 __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* partials) {
   __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
   __shared__ uint16_t s_rl[kMaxRl];
-  __shared__ double s_rec[kStage * kRecD];
+  __shared__ double s_rec[STAGE * kRecD];
   __shared__ double4 s_bd[kBinTile];
   __shared__ int s_q[kBinTile + 1];
   __shared__ uint32_t s_work[kBinTile];
   __shared__ uint32_t s_wsum[kWaves];
-  __shared__ double lds[kWaves * kBinNV];
+  __shared__ double lds[kWaves * 16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int tile = blockIdx.x;
   const int b0 = tile * kBinTile;
@@ -686,18 +725,42 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
     if (t == 0)
       for (int f = 0; f < 5; ++f) a.scalars[SC_DESKEW_WIN + f] = pv[f];
   }
-  // phase D's bin (thread t < nb owns bin b0 + t): flag and map direction stats up front
+  // the tile flag and phase A's first-level table loads are issued together
+  const bool tile_active = a.flags[a.n_bins + tile] != 0;  // block-uniform
+  const int q_t = t <= nb ? a.rknn_off[b0 + t] : 0;
+  const int q0 = a.rknn_off[b0], q1t = a.rknn_off[b0 + nb];
+  const int s0 = a.tile_src_off[tile];
+  const int ns = a.tile_src_off[tile + 1] - s0;
+  if (!tile_active) {
+    // every bin of the tile has exact-zero sums: the zero-bin finalize writes its rows (N = 0,
+    // Sigma = eps I, ...); partial row = nb x the zero bin's terms, no MF term
+    if (wid == 0) {
+      double z[19], c5[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
+#pragma unroll
+      for (int f = 0; f < 19; ++f) z[f] = 0.0;
+      if (t < nb) finalize_bin(z, a.scan, a.n_bins, b0 + t, c5);
+      if (t == 0) {
+        double v[kBinNV];
+#pragma unroll
+        for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
+        v[3] = (double)nb * c5[3];
+        v[4] = c5[4];
+        store_partials<kBinNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_BINS>
+      }
+    }
+    PROF(6);
+    PROFV(7, 0);
+    return;
+  }
+  // phase D's bin (wave 0: thread t < nb owns bin b0 + t): flag and map direction stats up front
   const bool own = t < nb;
   const bool own_act = own && a.flags[b0 + t];
   MapDir mapv{0.0, 0.0, 0.0, 0.0};
   if (own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + t);
   // phase A
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
-  if (t <= nb) s_q[t] = a.rknn_off[b0 + t];
-  const int q0 = a.rknn_off[b0], q1t = a.rknn_off[b0 + nb];
+  if (t <= nb) s_q[t] = q_t;
   for (int q = q0 + t; q < q1t; q += kBlock) s_rl[q - q0] = a.rknn_local[q];
-  const int s0 = a.tile_src_off[tile];
-  const int ns = a.tile_src_off[tile + 1] - s0;
   for (int j = t; j < ns; j += kBlock) {
     const int src = a.tile_src[s0 + j];
     s_cnt[j] = a.counts[src];
@@ -705,7 +768,7 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   }
   __syncthreads();
   PROF(1);
-  if (t < kBinTile) {  // records each bin visits (0 for inactive / out-of-range bins)
+  if (t < kBinTile) {  // wave 0, lane = bin: records each bin visits (0: inactive / out of range)
     uint32_t w = 0;
     if (own_act)
       for (int q = s_q[t]; q < s_q[t + 1]; ++q) w += s_cnt[s_rl[q - q0]];
@@ -729,7 +792,16 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
     run += s_cnt[j];
   }
   const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-  const bool staged = total <= (uint32_t)kStage;
+  const bool staged = total <= (uint32_t)STAGE;
+  PROFV(8, total);
+#ifdef GCS_PHASE_PROF
+  if (t == 0) {
+    uint32_t mx = 0, sm = 0;
+    for (int i = 0; i < kBinTile; ++i) { mx = max(mx, s_work[i]); sm += s_work[i]; }
+    g_prof[blockIdx.x * 16 + 9] = mx;
+    g_prof[blockIdx.x * 16 + 10] = sm;
+  }
+#endif
   __syncthreads();
   PROF(2);
   // phase B: stage the tile's records (record r belongs to the last source with s_off <= r)
@@ -748,18 +820,18 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   }
   __syncthreads();
   PROF(3);
-  // phase C: lane pair per bin; the bin's records (sources in order, points in order) are one
-  // flattened list and lane l takes the l-th half, so every lane's trip count is its own share
+  // phase C: four lanes per bin; the bin's records (sources in order, points in order) are one
+  // flattened list and lane l takes the l-th quarter, so every lane's trip count is its own share
   // (no per-source max over the wave's lanes).
   const int lb = t / kBinLanes, l = t % kBinLanes;
   double acc[19];
 #pragma unroll
   for (int f = 0; f < 19; ++f) acc[f] = 0.0;
   const uint32_t work = s_work[lb];
-  if (work > 0) {
+  const uint32_t i0 = work * (uint32_t)l / 4u, i1 = work * (uint32_t)(l + 1) / 4u;
+  if (i1 > i0) {
     const double4 bd = s_bd[lb];
     const double inv_tau = 1.0 / a.tau;
-    const uint32_t i0 = l == 0 ? 0u : work / 2u, i1 = l == 0 ? work / 2u : work;
     // cursor: source q (local j), record k within it
     int q = s_q[lb];
     uint32_t skip = i0;
@@ -772,32 +844,58 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
       c = s_cnt[j];
     }
     uint32_t kk = skip;
-    for (uint32_t i = i0; i < i1; ++i) {
-      if (staged) {
-        const double* rp = s_rec + (size_t)(s_off[j] + kk) * kRecD;
-        bin_contrib(acc, bd, inv_tau, rp[0], rp[1], rp[2], rp[3], rp[4], rp[5], rp[6], rp[7]);
-      } else {
+    if (staged) {
+      // a source's records are one contiguous LDS run: the record index advances by one and is
+      // re-based only at source boundaries, and the next record is loaded (double2 x 4) while the
+      // current one is accumulated
+      uint32_t r = s_off[j] + kk, left = c - kk;
+      const double2* rp = (const double2*)(s_rec + (size_t)r * kRecD);
+      double2 x0 = rp[0], x1 = rp[1], x2 = rp[2], x3 = rp[3];
+      for (uint32_t i = i0; i < i1; ++i) {
+        const double2 c0 = x0, c1 = x1, c2 = x2, c3 = x3;
+        if (i + 1 < i1) {
+          if (--left == 0) {  // next non-empty source
+            do {
+              ++q;
+              j = s_rl[q - q0];
+              left = s_cnt[j];
+            } while (left == 0);
+            r = s_off[j];
+          } else {
+            ++r;
+          }
+          const double2* np = (const double2*)(s_rec + (size_t)r * kRecD);
+          x0 = np[0]; x1 = np[1]; x2 = np[2]; x3 = np[3];
+        }
+        bin_contrib(acc, bd, inv_tau, c0.x, c0.y, c1.x, c1.y, c2.x, c2.y, c3.x, c3.y);
+      }
+    } else {
+      for (uint32_t i = i0; i < i1; ++i) {
         const PointRec pr = a.recs[a.perm[s_st[j] + kk]];
         bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, pr.dx, pr.dy, pr.dz, pr.m, pr.w * pr.iz);
-      }
-      if (++kk == c && i + 1 < i1) {  // next non-empty source
-        kk = 0;
-        do {
-          ++q;
-          j = s_rl[q - q0];
-          c = s_cnt[j];
-        } while (c == 0);
+        if (++kk == c && i + 1 < i1) {  // next non-empty source
+          kk = 0;
+          do {
+            ++q;
+            j = s_rl[q - q0];
+            c = s_cnt[j];
+          } while (c == 0);
+        }
       }
     }
   }
 #pragma unroll
-  for (int f = 0; f < 19; ++f) acc[f] += __shfl_xor(acc[f], 1, 64);
+  for (int f = 0; f < 19; ++f) {  // quarters in fixed order: (q0 + q1) + (q2 + q3)
+    acc[f] += __shfl_xor(acc[f], 1, 64);
+    acc[f] += __shfl_xor(acc[f], 2, 64);
+  }
   PROF(4);
   __syncthreads();  // the record stage is free: it now carries the bin sums [19][kBinTile]
   if (l == 0)
 #pragma unroll
     for (int f = 0; f < 19; ++f) s_rec[f * kBinTile + lb] = acc[f];
   __syncthreads();
+  if (wid != 0) return;
   // phase D: finalize + this bin's Matrix-Fisher term (row 7, matrix_fisher_evidence.py:181-211).
   // A bin with no scan mass contributes exact zeros to H, so only active bins read the map.
   double v[kBinNV];
@@ -811,19 +909,10 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
     if (own_act) mf_bin_term(acc[0], acc[1], acc[2], acc[3], mapv, v + 5);
   }
   PROF(5);
-  // block reduce: 4 sums, 1 max, 11 sums
-  double s4[4] = {v[0], v[1], v[2], v[3]};
-  block_sum<4>(s4, lds);
-  double mx = block_max(v[4], lds);
-  double m11[11];
-#pragma unroll
-  for (int f = 0; f < 11; ++f) m11[f] = v[5 + f];
-  block_sum<11>(m11, lds);
-  v[0] = s4[0]; v[1] = s4[1]; v[2] = s4[2]; v[3] = s4[3]; v[4] = mx;
-#pragma unroll
-  for (int f = 0; f < 11; ++f) v[5 + f] = m11[f];
+  wave_reduce_bin_terms(v);
   store_partials<kBinNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_BINS>
   PROF(6);
+  PROFV(7, 1);
 }
 
 // ---------------------------------------------------------------- row 5+6 dense mode (B small)
@@ -906,10 +995,15 @@ __global__ __launch_bounds__(kBlock) void k_mf(const double* __restrict__ scan, 
 // ---------------------------------------------------------------- row 8: planar translation
 // Per bin (matrix_fisher_evidence.py:442-475): t_b = c_map - R p_scan,
 // S_b = Sigma_map + R Sigma_scan R^T, W_b = w_b inv(S_b + eps I); L += W_b, h += W_b t_b.
+// A bin that is empty in the scan (not a candidate: act = 0) and has never received map mass
+// (touched = 0) holds the finalize constants of a zero bin in both (N = 0, p_bar = c = 0,
+// Sigma = eps I, gcs_math.h psd_project3): its term is computed from those constants without
+// reading the bin (bitwise the same term).  act == nullptr (dense mode): every bin is read.
 constexpr int kPtNV = 13;
 __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, const double* __restrict__ map,
                                                const double* __restrict__ derived, int B,
-                                               const double* __restrict__ scalars, double* partials) {
+                                               const double* __restrict__ scalars, double* partials,
+                                               const uint8_t* __restrict__ act, const uint8_t* __restrict__ touched) {
   __shared__ double lds[kWaves * kPtNV];
   double R[9];
 #pragma unroll
@@ -919,13 +1013,18 @@ __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, 
   for (int k = 0; k < kPtNV; ++k) v[k] = 0.0;
   size_t Bs = (size_t)B;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
-    double Ns = scan[SF_N * Bs + b];
-    double Nm = map[MF_NP * Bs + b];
-    double pb[3], Sp[9], c[3], Sc[9];
+    double Ns = 0.0, Nm = 0.0;
+    double pb[3] = {0.0, 0.0, 0.0}, c[3] = {0.0, 0.0, 0.0};
+    double Sp[9] = {kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd};
+    double Sc[9] = {kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd};
+    if (!act || act[b] || touched[b]) {
+      Ns = scan[SF_N * Bs + b];
+      Nm = map[MF_NP * Bs + b];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) { pb[k] = scan[(SF_PB + k) * Bs + b]; c[k] = derived[(MD_C + k) * Bs + b]; }
+      for (int k = 0; k < 3; ++k) { pb[k] = scan[(SF_PB + k) * Bs + b]; c[k] = derived[(MD_C + k) * Bs + b]; }
 #pragma unroll
-    for (int k = 0; k < 9; ++k) { Sp[k] = scan[(SF_SIG + k) * Bs + b]; Sc[k] = derived[(MD_SIG + k) * Bs + b]; }
+      for (int k = 0; k < 9; ++k) { Sp[k] = scan[(SF_SIG + k) * Bs + b]; Sc[k] = derived[(MD_SIG + k) * Bs + b]; }
+    }
     double tb[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) tb[i] = c[i] - (R[3 * i] * pb[0] + R[3 * i + 1] * pb[1] + R[3 * i + 2] * pb[2]);
@@ -986,8 +1085,13 @@ __device__ __forceinline__ void map_totals_partial(double (&tot)[kTotNV], double
   store_partials<kTotNV>(tot, partials, blockIdx.x);  // folded by k_final<FIN_TOTALS>
 }
 
+// A bin with no scan mass (act = 0: exact-zero scan sums) and a map that never received mass
+// (touched = 0: all-zero stats) stays exactly zero under forgetting + push, and its derived stats
+// keep the zero-bin constants: it is skipped (adds exact zeros to the totals).  act == nullptr
+// (dense mode): every bin is updated.
 __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict__ scan, double* map, double* derived,
-                                                        int B, PushArgs pa, double* partials) {
+                                                        int B, PushArgs pa, double* partials,
+                                                        const uint8_t* __restrict__ act, uint8_t* touched) {
   __shared__ double lds[kWaves * kTotNV];
   double tot[kTotNV];
 #pragma unroll
@@ -996,6 +1100,13 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
   const double* R = pa.R;
   const double g = pa.gamma;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
+    if (act) {
+      if (act[b]) {
+        if (!touched[b]) touched[b] = 1;
+      } else if (!touched[b]) {
+        continue;
+      }
+    }
     const double N = scan[SF_N * Bs + b];
     double pb[3], u[3], q[3];
 #pragma unroll
@@ -1073,13 +1184,16 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
 
 // derived stats + map totals from map sufficient stats only (used after set_map / reset)
 __global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict__ map, double* derived, int B,
-                                                       double* partials) {
+                                                       double* partials, uint8_t* touched) {
   __shared__ double lds[kWaves * kTotNV];
   double tot[kTotNV];
 #pragma unroll
   for (int k = 0; k < kTotNV; ++k) tot[k] = 0.0;
   const size_t Bs = (size_t)B;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
+    bool nz = false;
+    for (int f = 0; f < MF_COUNT; ++f) nz = nz || map[f * Bs + b] != 0.0;
+    if (touched) touched[b] = nz ? 1 : 0;  // any map mass: k_pt / k_pushforward must read the bin
     double sd[3], sp[3], spp[9];
     for (int k = 0; k < 3; ++k) { sd[k] = map[(MF_SD + k) * Bs + b]; sp[k] = map[(MF_SP + k) * Bs + b]; }
     for (int k = 0; k < 9; ++k) { spp[k] = map[(MF_SPP + k) * Bs + b]; tot[k] += map[(MF_S + k) * Bs + b]; }
@@ -1134,9 +1248,40 @@ __global__ __launch_bounds__(kBlock) void k_final(const double* __restrict__ par
   }
 }
 
-#define GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, mirror)                                         \
-  hipExtLaunchKernelGGL(k_final<NV, MASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0, (const double*)partials, \
-                        (int)(nblk), scalars, (double*)(mirror))
+// First level of a two-level fold: block j folds partial rows [64 j, 64 j + 64) into row j of out.
+// One block reads ~10 B/clk from HBM, so a single-block fold of the 8192 rows (1 MiB) of the
+// bin kernel at C3 took 30 us; with a first level on 128 CUs the one-block tail folds 128 rows.
+constexpr int kFoldRows = 64;
+constexpr int kFoldDirect = 1024;  // up to this many rows a single block folds directly
+template <int NV, unsigned MAXMASK>
+__global__ __launch_bounds__(kBlock) void k_fold(const double* __restrict__ partials, int nblocks, double* out) {
+  __shared__ double lds[kWaves * pstride<NV>()];
+  const int r0 = blockIdx.x * kFoldRows;
+  double v[NV];
+  reduce_partials<NV, MAXMASK>(partials + (size_t)r0 * pstride<NV>(), min(kFoldRows, nblocks - r0), v, lds);
+  store_partials<NV>(v, out, blockIdx.x);
+}
+
+// Fold nblk partial rows into the scalars (one or two levels).  The level-1 rows are written
+// behind the nblk rows of `partials` (partials_need() reserves them).
+template <int NV, unsigned MAXMASK, int KIND>
+void launch_fold(const double* partials, int nblk, hipStream_t s, hipEvent_t e1, double* scalars, double* mirror) {
+  if (nblk > kFoldDirect) {
+    double* lvl = (double*)partials + (size_t)nblk * pstride<NV>();
+    const int g = (nblk + kFoldRows - 1) / kFoldRows;
+    hipExtLaunchKernelGGL(k_fold<NV, MAXMASK>, dim3(g), dim3(kBlock), 0, s, nullptr, nullptr, 0, partials, nblk, lvl);
+    hipExtLaunchKernelGGL(k_final<NV, MAXMASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0,
+                          (const double*)lvl, g, scalars, mirror);
+  } else {
+    hipExtLaunchKernelGGL(k_final<NV, MAXMASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0, partials, nblk,
+                          scalars, mirror);
+  }
+}
+size_t partials_need(long nblocks, int nv) {
+  return (size_t)(nblocks + (nblocks + kFoldRows - 1) / kFoldRows + 1) * partial_stride(nv);
+}
+#define GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, mirror) \
+  launch_fold<NV, MASK, KIND>((const double*)(partials), (int)(nblk), s, e1, scalars, (double*)(mirror))
 #define GCS_FINAL(NV, MASK, KIND, nblk, s, e1, partials, scalars) \
   GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, nullptr)
 
@@ -1191,7 +1336,10 @@ int bins_partial_nv() { return kBinNV; }
 hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                              hipEvent_t e2) {
   const int nblk = bins_scale_blocks(a.n_bins);
-  hipExtLaunchKernelGGL(k_bins_scale, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
+  if ((long)a.cap * 5 >= (long)a.n_bins * 2)
+    hipExtLaunchKernelGGL(k_bins_scale<kStageBig>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
+  else
+    hipExtLaunchKernelGGL(k_bins_scale<kStageSmall>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
   GCS_FINAL(kBinNV, 16u, FIN_BINS, nblk, s, e2, partials, a.scalars);
   return hipGetLastError();
 }
@@ -1215,26 +1363,28 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 }
 
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, double* mirror, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
+                     hipEvent_t e0, hipEvent_t e1) {
   hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B,
-                        (const double*)scalars, partials);
+                        (const double*)scalars, partials, act, touched);
   GCS_FINAL_M(kPtNV, 0u, FIN_PT, nblk, s, e1, partials, scalars, mirror);
   return hipGetLastError();
 }
 
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
-                              double* partials, double* scalars, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+                              double* partials, double* scalars, const uint8_t* act, uint8_t* touched, hipStream_t s,
+                              hipEvent_t e0, hipEvent_t e1) {
   const int nblk = push_blocks(B);
   hipExtLaunchKernelGGL(k_pushforward, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B, pa,
-                        partials);
+                        partials, act, touched);
   GCS_FINAL(kTotNV, 0u, FIN_TOTALS, nblk, s, e1, partials, scalars);
   return hipGetLastError();
 }
 
 hipError_t launch_map_derive(const double* map, double* derived, int B, double* partials, double* scalars,
-                             hipStream_t s) {
+                             uint8_t* touched, hipStream_t s) {
   const int nblk = push_blocks(B);
-  hipLaunchKernelGGL(k_map_derive, dim3(nblk), dim3(kBlock), 0, s, map, derived, B, partials);
+  hipLaunchKernelGGL(k_map_derive, dim3(nblk), dim3(kBlock), 0, s, map, derived, B, partials, touched);
   GCS_FINAL(kTotNV, 0u, FIN_TOTALS, nblk, s, nullptr, partials, scalars);
   return hipGetLastError();
 }

@@ -216,6 +216,131 @@ GCS_HD void eigh3_jacobi(const double* A, double* w, double* V) {
   w[0] = a[0]; w[1] = a[4]; w[2] = a[8];
 }
 
+GCS_HD void cross3(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// Clamped-eigenpair form of the 3x3 PSD projection, for a symmetric s that failed the fast
+// paths (rank-deficient scatter: bins with one to three points).  With w_i, v_i the eigenpairs,
+// V diag(max(w, eps)) V^T = s + sum_{w_i < eps} (eps - w_i) v_i v_i^T and the projection delta is
+// sqrt(sum_{w_i < eps} (eps - w_i)^2), so only the clamped pairs are needed:
+//   * the top eigenvalue by Newton's method on the characteristic cubic from the Gershgorin
+//     bound (monotone from above; no transcendental calls) and its vector as the longest cross
+//     product of two rows of s - w_1 I;
+//   * the two small eigenpairs from the 2x2 projection of s onto the complement of that vector
+//     (closed form, absolute accuracy ~ 1e-16 |s|, far below eps = 1e-12).
+// Returns false (caller falls back to Jacobi) when the top eigenvalue is (near) double.
+GCS_HD bool psd3_deflate(const double* s, double* out, double* delta) {
+  const double c2 = s[0] + s[4] + s[8];
+  const double c1 = (s[0] * s[4] - s[1] * s[1]) + (s[0] * s[8] - s[2] * s[2]) + (s[4] * s[8] - s[5] * s[5]);
+  const double c0 = s[0] * (s[4] * s[8] - s[5] * s[5]) - s[1] * (s[1] * s[8] - s[5] * s[2]) +
+                    s[2] * (s[1] * s[5] - s[4] * s[2]);
+  double lam = fmax(fmax(s[0] + fabs(s[1]) + fabs(s[2]), s[4] + fabs(s[1]) + fabs(s[5])),
+                    s[8] + fabs(s[2]) + fabs(s[5]));
+  if (!(lam > -1e300 && lam < 1e300)) return false;  // NaN / inf
+  for (int it = 0; it < 100; ++it) {
+    const double f = ((lam - c2) * lam + c1) * lam - c0;
+    const double fp = (3.0 * lam - 2.0 * c2) * lam + c1;
+    if (!(fp > 0.0) || !(f > 0.0)) break;
+    const double step = f / fp;
+    lam -= step;
+    if (step <= 1e-15 * fabs(lam)) break;
+  }
+  const double m0 = s[0] - lam, m4 = s[4] - lam, m8 = s[8] - lam;
+  // cross products of the rows (m0 s1 s2), (s1 m4 s5), (s2 s5 m8)
+  const double x0 = s[1] * s[5] - s[2] * m4, x1 = s[2] * s[1] - m0 * s[5], x2 = m0 * m4 - s[1] * s[1];
+  const double y0 = s[1] * m8 - s[2] * s[5], y1 = s[2] * s[2] - m0 * m8, y2 = m0 * s[5] - s[1] * s[2];
+  const double z0 = m4 * m8 - s[5] * s[5], z1 = s[5] * s[2] - s[1] * m8, z2 = s[1] * s[5] - m4 * s[2];
+  const double nx = x0 * x0 + x1 * x1 + x2 * x2, ny = y0 * y0 + y1 * y1 + y2 * y2, nz = z0 * z0 + z1 * z1 + z2 * z2;
+  double u0 = x0, u1 = x1, u2 = x2, nmax = nx;
+  if (ny > nmax) { u0 = y0; u1 = y1; u2 = y2; nmax = ny; }
+  if (nz > nmax) { u0 = z0; u1 = z1; u2 = z2; nmax = nz; }
+  const double mf2 = m0 * m0 + m4 * m4 + m8 * m8 + 2.0 * (s[1] * s[1] + s[2] * s[2] + s[5] * s[5]);
+  if (!(nmax > 1e-12 * mf2 * mf2)) return false;  // (near) double top eigenvalue: Jacobi
+  const double in = 1.0 / sqrt(nmax);
+  u0 *= in; u1 *= in; u2 *= in;
+  // orthonormal complement e, f of u: e = u x (axis of the smallest |u_k|), f = u x e
+  const double a0 = fabs(u0), a1 = fabs(u1), a2 = fabs(u2);
+  double e0, e1, e2;
+  if (a0 <= a1 && a0 <= a2) { e0 = 0.0; e1 = u2; e2 = -u1; }        // u x (1,0,0)
+  else if (a1 <= a2) { e0 = -u2; e1 = 0.0; e2 = u0; }               // u x (0,1,0)
+  else { e0 = u1; e1 = -u0; e2 = 0.0; }                             // u x (0,0,1)
+  const double ie = 1.0 / sqrt(e0 * e0 + e1 * e1 + e2 * e2);
+  e0 *= ie; e1 *= ie; e2 *= ie;
+  const double f0 = u1 * e2 - u2 * e1, f1 = u2 * e0 - u0 * e2, f2 = u0 * e1 - u1 * e0;
+  // 2x2 projection [[a b] [b c]] of s onto span(e, f)
+  const double se0 = s[0] * e0 + s[1] * e1 + s[2] * e2, se1 = s[1] * e0 + s[4] * e1 + s[5] * e2,
+               se2 = s[2] * e0 + s[5] * e1 + s[8] * e2;
+  const double sf0 = s[0] * f0 + s[1] * f1 + s[2] * f2, sf1 = s[1] * f0 + s[4] * f1 + s[5] * f2,
+               sf2 = s[2] * f0 + s[5] * f1 + s[8] * f2;
+  const double a = e0 * se0 + e1 * se1 + e2 * se2;
+  const double c = f0 * sf0 + f1 * sf1 + f2 * sf2;
+  const double b = 0.5 * ((e0 * sf0 + e1 * sf1 + e2 * sf2) + (f0 * se0 + f1 * se1 + f2 * se2));
+  const double mean = 0.5 * (a + c), h = 0.5 * (a - c);
+  const double d = sqrt(h * h + b * b);
+  const double mu_hi = mean + d, mu_lo = mean - d;
+  // eigenvector (p, q) of mu_hi in the (e, f) plane: the longer of (b, mu - a) and (mu - c, b)
+  double p = b, q = mu_hi - a;
+  const double p2 = mu_hi - c, q2 = b;
+  if (p2 * p2 + q2 * q2 > p * p + q * q) { p = p2; q = q2; }
+  const double pn = p * p + q * q;
+  if (pn > 0.0) {
+    const double ipn = 1.0 / sqrt(pn);
+    p *= ipn; q *= ipn;
+  } else {
+    p = 1.0; q = 0.0;  // a multiple of the identity in the plane: any basis
+  }
+  // v_hi = p e + q f, v_lo = -q e + p f
+  const double vh0 = p * e0 + q * f0, vh1 = p * e1 + q * f1, vh2 = p * e2 + q * f2;
+  const double vl0 = p * f0 - q * e0, vl1 = p * f1 - q * e1, vl2 = p * f2 - q * e2;
+  for (int k = 0; k < 9; ++k) out[k] = s[k];
+  double d2 = 0.0;
+  if (lam < kEpsPsd) {  // every eigenvalue clamped: V eps I V^T
+    for (int k = 0; k < 9; ++k) out[k] = (k % 4 == 0) ? kEpsPsd : 0.0;
+    d2 = (kEpsPsd - lam) * (kEpsPsd - lam) + (kEpsPsd - mu_hi) * (kEpsPsd - mu_hi) +
+         (kEpsPsd - mu_lo) * (kEpsPsd - mu_lo);
+  } else {
+    if (mu_hi < kEpsPsd) {
+      const double g = kEpsPsd - mu_hi;
+      d2 += g * g;
+      out[0] += g * vh0 * vh0; out[1] += g * vh0 * vh1; out[2] += g * vh0 * vh2;
+      out[3] += g * vh1 * vh0; out[4] += g * vh1 * vh1; out[5] += g * vh1 * vh2;
+      out[6] += g * vh2 * vh0; out[7] += g * vh2 * vh1; out[8] += g * vh2 * vh2;
+    }
+    if (mu_lo < kEpsPsd) {
+      const double g = kEpsPsd - mu_lo;
+      d2 += g * g;
+      out[0] += g * vl0 * vl0; out[1] += g * vl0 * vl1; out[2] += g * vl0 * vl2;
+      out[3] += g * vl1 * vl0; out[4] += g * vl1 * vl1; out[5] += g * vl1 * vl2;
+      out[6] += g * vl2 * vl0; out[7] += g * vl2 * vl1; out[8] += g * vl2 * vl2;
+    }
+  }
+  *delta = sqrt(d2);
+  return true;
+}
+
+// The PSD projection of a symmetric s that failed the fast paths: deflation, else Jacobi.  Kept
+// out of line so its registers do not weigh on the callers' main paths (it runs for a minority
+// of bins: those with one to three points).
+__host__ __device__ inline __attribute__((noinline)) double psd_project3_slow(const double* s, double* out) {
+  double dl;
+  if (psd3_deflate(s, out, &dl)) return dl;
+  double w[3], V[9];
+  eigh3_jacobi(s, w, V);
+  for (int k = 0; k < 3; ++k) w[k] = w[k] > kEpsPsd ? w[k] : kEpsPsd;
+  double d2 = 0.0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double v = V[3 * i] * w[0] * V[3 * j] + V[3 * i + 1] * w[1] * V[3 * j + 1] + V[3 * i + 2] * w[2] * V[3 * j + 2];
+      out[3 * i + j] = v;
+      double dd = v - s[3 * i + j];
+      d2 += dd * dd;
+    }
+  return sqrt(d2);
+}
+
 // DomainProjectionPSD for a 3x3 (primitives.py:80-123).  M_psd = V diag(max(w,eps)) V^T
 // and the projection delta ||M_psd - M_sym||_F.  Exact fast path for the all-zero matrix
 // (LAPACK returns V = I there, so the reference gives eps*I and delta = sqrt(3) eps exactly).
@@ -248,18 +373,7 @@ GCS_HD double psd_project3(const double* M, double* out) {
       }
     }
   }
-  double w[3], V[9];
-  eigh3_jacobi(s, w, V);
-  for (int k = 0; k < 3; ++k) w[k] = w[k] > kEpsPsd ? w[k] : kEpsPsd;
-  double d2 = 0.0;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) {
-      double v = V[3 * i] * w[0] * V[3 * j] + V[3 * i + 1] * w[1] * V[3 * j + 1] + V[3 * i + 2] * w[2] * V[3 * j + 2];
-      out[3 * i + j] = v;
-      double dd = v - s[3 * i + j];
-      d2 += dd * dd;
-    }
-  return sqrt(d2);
+  return psd_project3_slow(s, out);
 }
 
 // Inverse of a general 3x3 via adjugate / determinant (jnp.linalg.inv restated).
@@ -278,12 +392,6 @@ GCS_HD void inv3(const double* m, double* o) {
   o[6] = c02 * id;
   o[7] = (m[1] * m[6] - m[0] * m[7]) * id;
   o[8] = (m[0] * m[4] - m[1] * m[3]) * id;
-}
-
-GCS_HD void cross3(const double* a, const double* b, double* c) {
-  c[0] = a[1] * b[2] - a[2] * b[1];
-  c[1] = a[2] * b[0] - a[0] * b[2];
-  c[2] = a[0] * b[1] - a[1] * b[0];
 }
 
 // 3x3 SVD H = U diag(s) V^T by one-sided (Hestenes) Jacobi, s sorted descending.

@@ -90,6 +90,7 @@ _SIGS = [
     ("gcs_spd_solve_lifted", C.c_int, [C.c_int32, c_double_p, c_double_p, C.c_double, c_double_p]),
     ("gcs_spd_inverse_lifted", C.c_int, [C.c_int32, c_double_p, C.c_double, c_double_p]),
     ("gcs_svd3", C.c_int, [c_double_p, c_double_p, c_double_p, c_double_p]),
+    ("gcs_psd_project3", C.c_int, [c_double_p, c_double_p, c_double_p]),
     ("gcs_mf_rotation", C.c_int, [c_double_p, c_double_p]),
     ("gcs_predict_diffusion", C.c_int, [C.POINTER(GcsBelief), c_double_p, C.c_double, C.POINTER(GcsBelief),
                                         c_double_p]),
@@ -115,10 +116,12 @@ def load():
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(LIB_PATH):
-        raise RuntimeError(f"{LIB_PATH} not found: build it with __graft_entry__.build() "
+    # GCSLAM_LIB: an instrumented build of the same library (tools/phase_prof.py), never a fallback
+    path = os.environ.get("GCSLAM_LIB", LIB_PATH)
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} not found: build it with __graft_entry__.build() "
                            "(make -C gc-slam_amd); there is no CPU fallback")
-    lib = C.CDLL(LIB_PATH)
+    lib = C.CDLL(path)
     for name, res, args in _SIGS:
         fn = getattr(lib, name)
         fn.restype = res

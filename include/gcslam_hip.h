@@ -170,6 +170,10 @@ int gcs_psd_project(int32_t n, const double* M, double eps_psd, double* M_psd, d
 int gcs_spd_solve_lifted(int32_t n, const double* L, const double* b, double eps_lift, double* x);
 int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps_lift, double* Linv);
 int gcs_svd3(const double* H, double* U, double* s, double* V);
+/* The kernels' 3x3 DomainProjectionPSD (primitives.py:80-123; gcs_math.h psd_project3: exact-zero
+ * and Cholesky fast paths, clamped-eigenpair deflation, Jacobi fallback), host build of the same
+ * code; delta = ||M_psd - M_sym||_F. */
+int gcs_psd_project3(const double* M /*3x3*/, double* M_psd /*3x3*/, double* delta);
 /* det-fixed Matrix-Fisher rotation R = U diag(1,1,det(UV^T)) V^T of H (matrix_fisher_evidence.py:215-222):
  * the same routine the device fold runs (polar Newton, SVD for reflections / rank deficiency) */
 int gcs_mf_rotation(const double* H /*3x3*/, double* R /*3x3*/);

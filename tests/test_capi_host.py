@@ -41,6 +41,40 @@ def test_psd_project_matches_oracle(lib, n):
         assert cert[1] == pytest.approx(rc[1], rel=1e-12, abs=1e-300)
 
 
+def _psd3_cases():
+    """Symmetric 3x3 inputs of the bin finalize: full-rank scatter, one to three clamped
+    eigenvalues (one, two or three points), near-double roots, negative noise, large norms."""
+    rng = np.random.default_rng(3)
+    out = []
+    for scale in (1e-6, 1e-3, 1.0, 1e2):
+        for rank in (0, 1, 2, 3):
+            for _ in range(40):
+                X = rng.standard_normal((rank, 3)) * scale ** 0.5
+                M = X.T @ X
+                M = M + 1e-17 * scale * rng.standard_normal((3, 3))        # rounding-level noise
+                out.append(M)
+    for lam in ([1e-3, 1e-3, 0.0], [1.0, 1e-13, -1e-13], [2e-12, 1e-12, 5e-13], [1e-3, 1e-3, 1e-3],
+                [1e-3, 2e-12, 0.9e-12], [-1e-14, -1e-14, 1e-4]):
+        Q, _ = np.linalg.qr(rng.standard_normal((3, 3)))
+        out.append(Q @ np.diag(lam) @ Q.T)
+    out.append(np.zeros((3, 3)))
+    return out
+
+
+def test_psd_project3_matches_oracle(lib):
+    """The device 3x3 PSD projection (host build) against primitives.psd_project (numpy eigh)."""
+    for M in _psd3_cases():
+        M = np.ascontiguousarray(M)
+        out = np.zeros((3, 3))
+        d = np.zeros(1)
+        assert lib.gcs_psd_project3(L.dptr(M), L.dptr(out), L.dptr(d)) == 0
+        ref, rc = psd_project(M)
+        s = np.abs(M).max() + 1e-12
+        assert np.allclose(out, ref, atol=1e-14 * s + 1e-22, rtol=0), (M, out, ref)
+        assert d[0] == pytest.approx(rc[0], abs=1e-14 * s + 1e-22), (M, d[0], rc[0])
+        assert np.linalg.eigvalsh(0.5 * (out + out.T)).min() >= 1e-12 * (1 - 1e-6) - 1e-15 * s
+
+
 def test_spd_solve_and_inverse_match_oracle(lib):
     rng = np.random.default_rng(11)
     A = rng.standard_normal((22, 22))
