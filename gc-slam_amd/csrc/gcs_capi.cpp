@@ -57,7 +57,9 @@ struct gcs_ctx {
   int n_counts_words = 0;
   uint32_t* d_tickets = nullptr;
   uint8_t* d_flags = nullptr;
-  uint8_t* d_touched = nullptr;  // per bin: the map holds mass (k_map_derive / k_pushforward)
+  uint8_t* d_touched = nullptr;
+  uint8_t* d_tile_dirty = nullptr;  // k_bins_scale: tile output not the zero-bin values (persistent)
+  double* d_bins_part = nullptr;    // k_bins_scale partial rows (persistent: clean tiles keep theirs)  // per bin: the map holds mass (k_map_derive / k_pushforward)
   double* d_scan = nullptr;
   double* d_map = nullptr;
   double* d_derived = nullptr;
@@ -293,6 +295,7 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   b.starts = c->d_starts;
   b.counts = c->d_counts;
   b.flags = c->d_flags;
+  b.tile_dirty = c->d_tile_dirty;
   b.rknn_off = c->d_rknn_off;
   b.rknn = c->d_rknn;
   b.rknn_local = c->d_rknn_local;
@@ -339,7 +342,7 @@ int stage_bins(gcs_ctx* c) {
       HIPCHK(c, launch_bucketing(ba, c->cap, s, ev.e0, ev.e1));
     }
     StageEv ev = stage_ev(c, ST_BINS);
-    HIPCHK(c, launch_bins_scale(b, c->d_partials, s, ev.e0, ev.e1, nullptr));  // stage = the bin kernel itself
+    HIPCHK(c, launch_bins_scale(b, c->d_bins_part, s, ev.e0, ev.e1, nullptr));  // stage = the bin kernel itself
     c->pts_fold_pending = false;
   } else {
     StageEv ev = stage_ev(c, ST_BINS);
@@ -463,6 +466,11 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     // bin flags, then one flag per k_bins_scale tile (both cleared by k_budget every scan)
     if (bad(hipMalloc(&c->d_flags, B + bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
     if (bad(hipMemset(c->d_flags, 0, B + bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
+    // every tile starts dirty: the first scan writes all ScanBinStats rows and partial rows
+    if (bad(hipMalloc(&c->d_tile_dirty, bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
+    if (bad(hipMemset(c->d_tile_dirty, 1, bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_bins_part, partials_need(bins_scale_blocks(c->B), bins_partial_nv()) * sizeof(double))))
+      return GCS_ERR_HIP;
   } else {
     size_t nchunks = (cap + 255) / 256;
     if (bad(hipMalloc(&c->d_bin_partials, nchunks * 19 * B * sizeof(double)))) return GCS_ERR_HIP;
@@ -489,7 +497,8 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
 int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
   void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
-                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags, c->d_touched, c->d_tickets,
+                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags, c->d_touched,
+                  c->d_tile_dirty, c->d_bins_part, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)

@@ -75,6 +75,7 @@ struct BinKernelArgs {
   const uint32_t* starts;
   const uint32_t* counts;
   const uint8_t* flags;
+  uint8_t* tile_dirty;     // per tile: rows / partial row differ from the zero-bin values (persistent)
   const int* rknn_off;
   const int* rknn;
   const uint16_t* rknn_local;  // per reverse-kNN entry: index in its tile's source list

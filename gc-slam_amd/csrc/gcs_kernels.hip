@@ -642,7 +642,9 @@ constexpr int kBinNV = 16;
 //  0: a tile none of whose bins is a candidate of a non-empty bucket (tile flag, set by
 //     k_bucket_rank) has exact-zero sums: wave 0 writes the zero-bin rows and the tile's partial
 //     row in closed form; A-D are skipped.  With the VLP-16-like scans (rings within +-15 deg)
-//     most tiles of the sphere are such.
+//     most tiles of the sphere are such.  A per-tile dirty byte (persistent across scans) records
+//     whether the tile's rows and partial row differ from those zero-bin values: a tile inactive
+//     in this scan and the last one exits without writing (its output is already in place).
 //  A: the tile's bin directions, reverse-kNN ranges and local source indices go to LDS; the
 //     tile's unique source buckets (host table, ~2.3 per bin) get sizes, starts and staged
 //     offsets (block scan); each bin's work (records to visit) is summed.
@@ -681,6 +683,14 @@ __device__ __forceinline__ void bin_contrib(double* acc, const double4& bd, doub
 __device__ unsigned long long g_prof[32768 * 16];
 extern "C" int gcs_debug_prof(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), (size_t)n * sizeof(unsigned long long));
+}
+extern "C" int gcs_debug_psd_count(unsigned long long* out /*4*/, int reset) {
+  int e = (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_psd_count), 4 * sizeof(unsigned long long));
+  if (reset) {
+    unsigned long long z[4] = {0, 0, 0, 0};
+    e |= (int)hipMemcpyToSymbol(HIP_SYMBOL(g_psd_count), z, sizeof(z));
+  }
+  return e;
 }
 #define PROF(k) \
   if (threadIdx.x == 0) g_prof[blockIdx.x * 16 + (k)] = wall_clock64();
@@ -725,12 +735,19 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
     if (t == 0)
       for (int f = 0; f < 5; ++f) a.scalars[SC_DESKEW_WIN + f] = pv[f];
   }
-  // the tile flag and phase A's first-level table loads are issued together
+  // the tile flags and phase A's first-level table loads are issued together
   const bool tile_active = a.flags[a.n_bins + tile] != 0;  // block-uniform
+  const bool tile_dirty = a.tile_dirty[tile] != 0;
   const int q_t = t <= nb ? a.rknn_off[b0 + t] : 0;
   const int q0 = a.rknn_off[b0], q1t = a.rknn_off[b0 + nb];
   const int s0 = a.tile_src_off[tile];
   const int ns = a.tile_src_off[tile + 1] - s0;
+  if (!tile_active && !tile_dirty) {
+    PROF(6);
+    PROFV(7, 2);
+    return;
+  }
+  if (t == 0 && tile_active != tile_dirty) a.tile_dirty[tile] = tile_active ? 1 : 0;
   if (!tile_active) {
     // every bin of the tile has exact-zero sums: the zero-bin finalize writes its rows (N = 0,
     // Sigma = eps I, ...); partial row = nb x the zero bin's terms, no MF term
@@ -890,12 +907,16 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
     acc[f] += __shfl_xor(acc[f], 2, 64);
   }
   PROF(4);
+#ifdef GCS_PHASE_PROF
+  if (lane == 0 && wid > 0) g_prof[blockIdx.x * 16 + 10 + wid] = wall_clock64();  // waves 1-3 gather end
+#endif
   __syncthreads();  // the record stage is free: it now carries the bin sums [19][kBinTile]
   if (l == 0)
 #pragma unroll
     for (int f = 0; f < 19; ++f) s_rec[f * kBinTile + lb] = acc[f];
   __syncthreads();
   if (wid != 0) return;
+  PROF(14);
   // phase D: finalize + this bin's Matrix-Fisher term (row 7, matrix_fisher_evidence.py:181-211).
   // A bin with no scan mass contributes exact zeros to H, so only active bins read the map.
   double v[kBinNV];
@@ -906,6 +927,7 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
 #pragma unroll
     for (int f = 0; f < 19; ++f) acc[f] = s_rec[f * kBinTile + t];
     finalize_bin(acc, a.scan, a.n_bins, b0 + t, v);
+    PROF(15);
     if (own_act) mf_bin_term(acc[0], acc[1], acc[2], acc[3], mapv, v + 5);
   }
   PROF(5);

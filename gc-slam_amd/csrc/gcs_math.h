@@ -8,6 +8,17 @@
 #include <math.h>
 #include <stdint.h>
 
+// instrumented build only (make prof): device counters of the 3x3 PSD paths
+#ifdef GCS_PHASE_PROF
+__device__ unsigned long long g_psd_count[4];  // non-zero inputs, slow path, Jacobi fallback
+#ifdef __HIP_DEVICE_COMPILE__
+#define GCS_PSD_COUNT(k) atomicAdd(&g_psd_count[k], 1ull)
+#endif
+#endif
+#ifndef GCS_PSD_COUNT
+#define GCS_PSD_COUNT(k)
+#endif
+
 #define GCS_HD __host__ __device__ __forceinline__
 
 namespace gcs {
@@ -232,7 +243,7 @@ GCS_HD void cross3(const double* a, const double* b, double* c) {
 //   * the two small eigenpairs from the 2x2 projection of s onto the complement of that vector
 //     (closed form, absolute accuracy ~ 1e-16 |s|, far below eps = 1e-12).
 // Returns false (caller falls back to Jacobi) when the top eigenvalue is (near) double.
-GCS_HD bool psd3_deflate(const double* s, double* out, double* delta) {
+GCS_HD __attribute__((always_inline)) bool psd3_deflate(const double* s, double* out, double* delta) {
   const double c2 = s[0] + s[4] + s[8];
   const double c1 = (s[0] * s[4] - s[1] * s[1]) + (s[0] * s[8] - s[2] * s[2]) + (s[4] * s[8] - s[5] * s[5]);
   const double c0 = s[0] * (s[4] * s[8] - s[5] * s[5]) - s[1] * (s[1] * s[8] - s[5] * s[2]) +
@@ -321,12 +332,11 @@ GCS_HD bool psd3_deflate(const double* s, double* out, double* delta) {
   return true;
 }
 
-// The PSD projection of a symmetric s that failed the fast paths: deflation, else Jacobi.  Kept
-// out of line so its registers do not weigh on the callers' main paths (it runs for a minority
-// of bins: those with one to three points).
+// Jacobi PSD projection of a symmetric s whose top eigenvalue is (near) double, where the
+// deflation cannot pick an eigenvector.  Kept out of line: it is rare (no bin of the benchmark
+// scans takes it) and its indexed arrays live in scratch.
 __host__ __device__ inline __attribute__((noinline)) double psd_project3_slow(const double* s, double* out) {
-  double dl;
-  if (psd3_deflate(s, out, &dl)) return dl;
+  GCS_PSD_COUNT(2);
   double w[3], V[9];
   eigh3_jacobi(s, w, V);
   for (int k = 0; k < 3; ++k) w[k] = w[k] > kEpsPsd ? w[k] : kEpsPsd;
@@ -356,6 +366,7 @@ GCS_HD double psd_project3(const double* M, double* out) {
     for (int i = 0; i < 9; ++i) out[i] = (i % 4 == 0) ? kEpsPsd : 0.0;
     return 1.7320508075688772e-12;
   }
+  GCS_PSD_COUNT(0);
   // Fast path: if M_sym - eps I is positive definite no eigenvalue is clamped, so the exact
   // projection is M_sym itself with delta 0 (the eigh rebuild differs only by rounding).
   {
@@ -373,7 +384,19 @@ GCS_HD double psd_project3(const double* M, double* out) {
       }
     }
   }
-  return psd_project3_slow(s, out);
+  // the out-of-line call takes private copies, so s / out themselves never leave registers
+  // (an escaping address would put them in scratch on every bin, fast path included)
+  // deflation inline: at C3 about 6% of the non-empty bins (one to three points) come here, so
+  // nearly every wave has such a lane, and a call would save and restore its live registers
+  // through scratch on every wave
+  GCS_PSD_COUNT(1);
+  double dl;
+  if (psd3_deflate(s, out, &dl)) return dl;
+  double si[9], so[9];
+  for (int i = 0; i < 9; ++i) si[i] = s[i];
+  double d = psd_project3_slow(si, so);
+  for (int i = 0; i < 9; ++i) out[i] = so[i];
+  return d;
 }
 
 // Inverse of a general 3x3 via adjugate / determinant (jnp.linalg.inv restated).

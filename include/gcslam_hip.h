@@ -133,7 +133,9 @@ int gcs_ctx_set_map(gcs_ctx* ctx, const double* map_host /*26*B field-major*/);
 int gcs_ctx_get_map(gcs_ctx* ctx, double* map_host /*26*B*/, double* derived_host /*16*B*/);
 int gcs_ctx_get_scan_stats(gcs_ctx* ctx, double* scan_host /*26*B*/);
 /* device pointers of the resident per-bin arrays (field-major, length-B rows) in DEVICE bin
- * order; set/get_map and get_scan_stats convert to reference (atlas) order */
+ * order; set/get_map and get_scan_stats convert to reference (atlas) order.  scan_dev is
+ * read-only for the caller: in scale mode the rows of bin tiles empty in consecutive scans are
+ * left in place rather than rewritten. */
 int gcs_ctx_device_arrays(gcs_ctx* ctx, double** scan_dev, double** map_dev, double** derived_dev);
 /* order[device bin] = reference bin id (scale mode: Hilbert patches of the sphere; dense: identity) */
 int gcs_ctx_get_bin_order(gcs_ctx* ctx, int32_t* order /*B*/);

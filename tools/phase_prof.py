@@ -33,19 +33,23 @@ def main():
         ctx.scan(rec, 16, t, w, N, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
                  sc["scan_end_time"], sc["dt_sec"])
     ctx.synchronize()
+    pc = (C.c_ulonglong * 4)()
+    ctx.lib.gcs_debug_psd_count.argtypes = [C.c_void_p, C.c_int]
+    assert ctx.lib.gcs_debug_psd_count(pc, 1) == 0
+    print(f"3x3 PSD over 3 scans: non-zero inputs {pc[0]}, slow path {pc[1]}, Jacobi fallback {pc[2]}")
     nblk = (B + 63) // 64
     buf = (C.c_ulonglong * (nblk * 16))()
     fn = ctx.lib.gcs_debug_prof
     fn.argtypes = [C.c_void_p, C.c_int]
     assert fn(buf, nblk * 16) == 0
     g = np.frombuffer(buf, dtype=np.uint64).reshape(nblk, 16).astype(np.int64)
-    act = g[:, 7] == 1
+    act = g[:, 7] == 1  # slot 7: 1 active, 0 inactive (zero rows written), 2 inactive and clean
     us = lambda x: x / 100.0  # noqa: E731  (100 MHz)
     t0 = g[:, 0].min()
     print(f"tiles {nblk}, active {act.sum()} ({act.mean():.1%})")
     print(f"kernel span {us(g[:, 6].max() - t0):.1f} us")
     life = us(g[:, 6] - g[:, 0])
-    for name, m in (("active", act), ("inactive", ~act)):
+    for name, m in (("active", act), ("inactive", g[:, 7] == 0), ("clean inactive", g[:, 7] == 2)):
         if not m.any():
             continue
         print(f"{name}: block life mean {life[m].mean():.2f} p90 {np.percentile(life[m], 90):.2f} max {life[m].max():.2f}")
@@ -55,12 +59,16 @@ def main():
                   np.round(d.mean(0), 2), "p90", np.round(np.percentile(d, 90, axis=0), 2))
             print(f"  staged records mean {g[m, 8].mean():.0f} p90 {np.percentile(g[m, 8], 90):.0f} max {g[m, 8].max()}"
                   f"; bin work max mean {g[m, 9].mean():.0f} max {g[m, 9].max()}; tile work mean {g[m, 10].mean():.0f}")
+            ge = us(g[m][:, 11:14].max(1) - g[m][:, 4])
+            print(f"  gather end, slowest of waves 1-3 minus wave 0: mean {ge.mean():.2f} p90 {np.percentile(ge, 90):.2f}")
+            dd = us(np.diff(g[m][:, [4, 14, 15, 5]], axis=1))
+            print("  phase D split (barriers, finalize_bin, MF term) mean", np.round(dd.mean(0), 2),
+                  "p90", np.round(np.percentile(dd, 90, axis=0), 2))
             big = life[m] > np.percentile(life[m], 90)
             print(f"  slowest 10%: staged mean {g[m][big, 8].mean():.0f}, max-bin work mean {g[m][big, 9].mean():.0f}, "
                   f"tile work mean {g[m][big, 10].mean():.0f}")
         else:
-            d = us(g[m][:, 6] - g[m][:, 5])
-            print(f"  reduce+store mean {d.mean():.2f}; finalize {us(g[m][:, 5] - g[m][:, 0]).mean():.2f}")
+            print(f"  count {m.sum()}")
     st = us(g[:, 0] - t0)
     print("block start percentiles (us) 0/10/25/50/75/90/100:", np.round(np.percentile(st, [0, 10, 25, 50, 75, 90, 100]), 2))
     ctx.close()
