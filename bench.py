@@ -130,7 +130,7 @@ def main():
                 ctx.enable_timing(False)
         sc, rec, t, w = scans[state["count"] % N_SCANS]
         out = ctx.scan(rec, 16, t, w, N, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
-                       sc["scan_end_time"], sc["dt_sec"])
+                       sc["scan_end_time"], sc["dt_sec"], t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"])
         tc = time.perf_counter()
         combine_allreduce(ctx, rank, world, state["count"], device=device, want_belief=False)
         host_ms[4] += (time.perf_counter() - tc) * 1e3

@@ -57,9 +57,9 @@ struct gcs_ctx {
   int n_counts_words = 0;
   uint32_t* d_tickets = nullptr;
   uint8_t* d_flags = nullptr;
-  uint8_t* d_touched = nullptr;
+  uint8_t* d_touched = nullptr;     // per bin: the map holds mass (k_map_derive / k_pushforward)
   uint8_t* d_tile_dirty = nullptr;  // k_bins_scale: tile output not the zero-bin values (persistent)
-  double* d_bins_part = nullptr;    // k_bins_scale partial rows (persistent: clean tiles keep theirs)  // per bin: the map holds mass (k_map_derive / k_pushforward)
+  double* d_bins_part = nullptr;    // k_bins_scale partial rows (persistent: clean tiles keep theirs)
   double* d_scan = nullptr;
   double* d_map = nullptr;
   double* d_derived = nullptr;
@@ -77,9 +77,11 @@ struct gcs_ctx {
   Belief belief{};
   double iw_nu[7], iw_Psi[7 * 36], Q[DZ * DZ];
   double last_dPsi[7 * 36], last_dnu[7];
+  double meas_nu[3], meas_Psi[3 * 9], meas_cert[2] = {0.0, 0.0};  // measurement-noise IW state
+  double last_meas_dPsi[3 * 9], last_meas_dnu[3];
   bool have_last = false;
   int last_n_sel = 0, last_stride = 1;
-  std::vector<double> wimu;  // IMU window weights (scratch)
+  std::vector<double> wimu, wint;  // IMU window weights: within-scan, scan-to-scan (scratch)
   // device stage timing (hipEvents on the context stream; harvested lazily)
   uint32_t timing_mask = 0;
   bool pending = false;
@@ -490,6 +492,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   for (int i = 0; i < DZ; ++i) c->belief.L[i * DZ + i] = 1e-6;
   host::datasheet_iw_state(c->iw_nu, c->iw_Psi);
   host::process_noise_Q(c->iw_nu, c->iw_Psi, c->Q);
+  host::datasheet_meas_iw_state(c->meas_nu, c->meas_Psi);
   *out = c;
   return GCS_OK;
 }
@@ -631,6 +634,21 @@ int gcs_ctx_get_iw_state(gcs_ctx* c, double* nu, double* Psi, double* Q) {
   if (nu) memcpy(nu, c->iw_nu, sizeof(c->iw_nu));
   if (Psi) memcpy(Psi, c->iw_Psi, sizeof(c->iw_Psi));
   if (Q) memcpy(Q, c->Q, sizeof(c->Q));
+  return GCS_OK;
+}
+
+int gcs_ctx_set_meas_iw_state(gcs_ctx* c, const double* nu, const double* Psi) {
+  if (!c || !nu || !Psi) return GCS_ERR_ARG;
+  memcpy(c->meas_nu, nu, sizeof(c->meas_nu));
+  memcpy(c->meas_Psi, Psi, sizeof(c->meas_Psi));
+  return GCS_OK;
+}
+
+int gcs_ctx_get_meas_iw_state(gcs_ctx* c, double* nu, double* Psi, double* cert2) {
+  if (!c) return GCS_ERR_ARG;
+  if (nu) memcpy(nu, c->meas_nu, sizeof(c->meas_nu));
+  if (Psi) memcpy(Psi, c->meas_Psi, sizeof(c->meas_Psi));
+  if (cert2) memcpy(cert2, c->meas_cert, sizeof(c->meas_cert));
   return GCS_OK;
 }
 
@@ -789,6 +807,18 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   host::se3_log(pre.delta_pose, xi);
   if (c->cfg.deskew_rotation_only) xi[0] = xi[1] = xi[2] = 0.0;
   cert[10] = pre.ess;
+  // 13 measurement-noise IW statistics over the scan-to-scan IMU window (pipeline.py:448-453,
+  // 522-566); padded samples (stamp <= 0) carry weight 0 (the reference's valid mask)
+  std::vector<double>& wint = c->wint;
+  wint.resize(in->imu_len);
+  for (int i = 0; i < in->imu_len; ++i)
+    wint[i] = in->imu_stamps[i] > 0.0 ? smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, sigma_warp) : 0.0;
+  host::imu_meas_iw_suffstats(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wint.data(), mu_inc + 9,
+                              mu_inc + 12, pose0 + 3, c->cfg.gravity_W, out->iw_meas_dPsi, out->iw_meas_dnu);
+  for (int k = 0; k < 27; ++k)
+    if (!std::isfinite(out->iw_meas_dPsi[k])) return fail(c, GCS_ERR_NONFINITE, "omega_avg / IMU residuals non-finite");
+  memcpy(c->last_meas_dPsi, out->iw_meas_dPsi, sizeof(c->last_meas_dPsi));
+  memcpy(c->last_meas_dnu, out->iw_meas_dnu, sizeof(c->last_meas_dnu));
   auto T1 = clk::now();
   // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
   int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
@@ -1014,7 +1044,8 @@ int gcs_hypothesis_payload(gcs_ctx* c, double w_iw, double w_bary, double* p) {
   int k = 0;
   for (int i = 0; i < 252; ++i) p[k++] = w_iw * (c->have_last ? c->last_dPsi[i] : 0.0);
   for (int i = 0; i < 7; ++i) p[k++] = w_iw * (c->have_last ? c->last_dnu[i] : 0.0);
-  k += 27 + 3;  // measurement-noise IW stats: out of scope this round (zeros)
+  for (int i = 0; i < 27; ++i) p[k++] = w_iw * (c->have_last ? c->last_meas_dPsi[i] : 0.0);
+  for (int i = 0; i < 3; ++i) p[k++] = w_iw * (c->have_last ? c->last_meas_dnu[i] : 0.0);
   const Belief& b = c->belief;
   for (int i = 0; i < DZ * DZ; ++i) p[k++] = w_bary * b.L[i];
   for (int i = 0; i < DZ; ++i) p[k++] = w_bary * b.h[i];
@@ -1051,6 +1082,11 @@ int gcs_hypothesis_combine(gcs_ctx* c, const double* p, int32_t scan_count, gcs_
   memcpy(c->iw_nu, nu2, sizeof(nu2));
   memcpy(c->iw_Psi, Psi2, sizeof(Psi2));
   host::process_noise_Q(c->iw_nu, c->iw_Psi, c->Q);
+  // measurement-noise IW apply, weight 1 every scan (backend_node.py:2105,2114-2119)
+  double mnu2[3], mPsi2[27];
+  host::meas_iw_apply(c->meas_nu, c->meas_Psi, p + 259, p + 286, mnu2, mPsi2, c->meas_cert);
+  memcpy(c->meas_nu, mnu2, sizeof(mnu2));
+  memcpy(c->meas_Psi, mPsi2, sizeof(mPsi2));
   if (comb) from_host_belief(out, *comb);
   if (cert) { cert[0] = delta; cert[1] = n2 - m2; cert[2] = c2[0]; cert[3] = c2[1]; }
   return GCS_OK;
@@ -1075,6 +1111,21 @@ int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps, double* Li) {
 int gcs_svd3(const double* H, double* U, double* s, double* V) {
   if (!H || !U || !s || !V) return GCS_ERR_ARG;
   svd3(H, U, s, V);
+  return GCS_OK;
+}
+int gcs_imu_meas_iw_suffstats(int32_t m, const double* stamps, const double* gyro, const double* accel,
+                              const double* w_int, const double* gb, const double* ab, const double* rv,
+                              const double* g, double* dPsi, double* dnu) {
+  if (m < 0 || !stamps || !gyro || !accel || !w_int || !gb || !ab || !rv || !g || !dPsi || !dnu) return GCS_ERR_ARG;
+  host::imu_meas_iw_suffstats(m, stamps, gyro, accel, w_int, gb, ab, rv, g, dPsi, dnu);
+  return GCS_OK;
+}
+int gcs_meas_iw_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double* nu_out,
+                      double* Psi_out, double* cert2) {
+  if (!nu || !Psi || !dPsi || !dnu || !nu_out || !Psi_out) return GCS_ERR_ARG;
+  double c2[2];
+  host::meas_iw_apply(nu, Psi, dPsi, dnu, nu_out, Psi_out, c2);
+  if (cert2) { cert2[0] = c2[0]; cert2[1] = c2[1]; }
   return GCS_OK;
 }
 int gcs_psd_project3(const double* M, double* out, double* delta) {

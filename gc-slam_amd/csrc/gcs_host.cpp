@@ -425,6 +425,99 @@ void process_iw_apply(const double* nu, const double* Psi, const double* dPsi, c
   cert2[1] = nsum;
 }
 
+// sum_m w_m r_m r_m^T / (sum w + eps), symmetrised, PSD-projected, times dt
+// (measurement_noise_iw_jax.py:150-162 / :202-213)
+static void weighted_outer_psd(double wsum, const double* S_acc, double dt, double* out) {
+  double S[9];
+  const double inv = 1.0 / (wsum + kEpsMass);
+  for (int k = 0; k < 9; ++k) S[k] = S_acc[k] * inv;
+  double Ss[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Ss[3 * i + j] = 0.5 * (S[3 * i + j] + S[3 * j + i]);
+  psd_project(3, Ss, kEpsPsd, out);
+  for (int k = 0; k < 9; ++k) out[k] *= dt;
+}
+
+// The pipeline's dt_imu / valid mask / omega_avg (pipeline.py:522-548) around
+// imu_gyro_meas_iw_suffstats_from_avg_rate_jax (measurement_noise_iw_jax.py:130-167) and
+// imu_accel_meas_iw_suffstats_from_gravity_dir_jax (:170-218); gyro + accel summed (pipeline.py:1024-1025).
+void imu_meas_iw_suffstats(int m, const double* stamps, const double* gyro, const double* accel, const double* w_int,
+                           const double* gb, const double* ab, const double* rotvec0, const double* g, double* dPsi,
+                           double* dnu) {
+  int n_valid = 0;
+  double tmin = INFINITY, tmax = -INFINITY, wsum = 0.0, om[3] = {0.0, 0.0, 0.0};
+  for (int i = 0; i < m; ++i) {
+    if (!(stamps[i] > 0.0)) continue;
+    ++n_valid;
+    tmin = std::min(tmin, stamps[i]);
+    tmax = std::max(tmax, stamps[i]);
+    wsum += w_int[i];
+  }
+  double dt = n_valid >= 2 ? (tmax - tmin) / std::max(n_valid - 1, 1) : 0.0;
+  dt = std::max(dt, 1e-12);
+  const double inv = 1.0 / (wsum + kEpsMass);
+  for (int i = 0; i < m; ++i) {
+    if (!(stamps[i] > 0.0)) continue;
+    const double wn = w_int[i] * inv;
+    for (int k = 0; k < 3; ++k) om[k] += wn * (gyro[3 * i + k] - gb[k]);
+  }
+  double R0[9], f[3];
+  so3_exp(rotvec0, R0);
+  for (int k = 0; k < 3; ++k) f[k] = -(R0[k] * g[0] + R0[3 + k] * g[1] + R0[6 + k] * g[2]);  // -R0^T g
+  double Sg[9] = {}, Sa[9] = {};
+  for (int i = 0; i < m; ++i) {
+    if (!(stamps[i] > 0.0)) continue;
+    const double w = w_int[i];
+    double rg[3], ra[3];
+    for (int k = 0; k < 3; ++k) {
+      rg[k] = (gyro[3 * i + k] - gb[k]) - om[k];
+      ra[k] = (accel[3 * i + k] - ab[k]) - f[k];
+    }
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) {
+        Sg[3 * a + b] += w * rg[a] * rg[b];
+        Sa[3 * a + b] += w * ra[a] * ra[b];
+      }
+  }
+  for (int k = 0; k < 27; ++k) dPsi[k] = 0.0;
+  weighted_outer_psd(wsum, Sg, dt, dPsi);
+  weighted_outer_psd(wsum, Sa, dt, dPsi + 9);
+  dnu[0] = 1.0;
+  dnu[1] = 1.0;
+  dnu[2] = 0.0;
+}
+
+// create_datasheet_measurement_noise_state, structures/measurement_noise_iw_jax.py:37-68
+void datasheet_meas_iw_state(double* nu, double* Psi) {
+  const double sig[3] = {8.7e-7, 9.5e-5, 0.01};  // constants.py:190,201,210
+  for (int b = 0; b < 3; ++b) {
+    nu[b] = 3.0 + 1.0 + 0.5;
+    for (int k = 0; k < 9; ++k) Psi[9 * b + k] = (k % 4 == 0) ? sig[b] * 0.5 : 0.0;
+  }
+}
+
+// measurement_noise_apply_suffstats_jax, measurement_noise_iw_jax.py:59-100
+void meas_iw_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double* nu_out,
+                   double* Psi_out, double* cert2) {
+  const double rho[3] = {0.995, 0.995, 0.99};  // constants.py:279-281
+  double dsum = 0.0, nsum = 0.0;
+  for (int b = 0; b < 3; ++b) {
+    double raw[9], sym[9];
+    for (int k = 0; k < 9; ++k) raw[k] = rho[b] * Psi[9 * b + k] + dPsi[9 * b + k];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) sym[3 * i + j] = 0.5 * (raw[3 * i + j] + raw[3 * j + i]);
+    dsum += psd_project(3, sym, kEpsPsd, Psi_out + 9 * b);
+    const double nu_raw = rho[b] * nu[b] + dnu[b];
+    const double nu_min = 3.0 + 1.0 + 0.5;
+    const double nu_floor = nu_min + softplus(nu_raw - nu_min);
+    const double nn = 1000.0 - softplus(1000.0 - nu_floor);
+    nsum += fabs(nn - nu_raw);
+    nu_out[b] = nn;
+  }
+  cert2[0] = dsum;
+  cert2[1] = nsum;
+}
+
 // _bch3_correction, recompose.py:50-91
 void bch3(const double* xi1, const double* xi2, double* out) {
   double c1[3], c2[3], c3[3];

@@ -67,6 +67,15 @@ void process_noise_Q(const double* nu, const double* Psi, double* Q);
 void process_iw_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double* nu_out,
                       double* Psi_out, double* cert2);
 
+// IW measurement noise, blocks [gyro, accel, lidar] (measurement_noise_iw_jax.py).  w_int: the
+// scan-to-scan IMU window weights (padded samples, stamp <= 0, are masked here).
+void imu_meas_iw_suffstats(int m, const double* stamps, const double* gyro, const double* accel, const double* w_int,
+                           const double* gyro_bias, const double* accel_bias, const double* rotvec0,
+                           const double* gravity_W, double* dPsi /*3x9*/, double* dnu /*3*/);
+void datasheet_meas_iw_state(double* nu /*3*/, double* Psi /*3x9*/);
+void meas_iw_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double* nu_out,
+                   double* Psi_out, double* cert2);
+
 void bch3(const double* xi1, const double* xi2, double* out);
 
 }  // namespace host

@@ -1039,13 +1039,22 @@ __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, 
     double pb[3] = {0.0, 0.0, 0.0}, c[3] = {0.0, 0.0, 0.0};
     double Sp[9] = {kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd};
     double Sc[9] = {kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd};
-    if (!act || act[b] || touched[b]) {
+    // scan rows of a bin without scan mass hold the zero-bin values the defaults above restate,
+    // map / derived rows of a bin the map never reached hold them too: only the rest is read
+    const bool sc = !act || act[b];
+    if (sc) {
       Ns = scan[SF_N * Bs + b];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) pb[k] = scan[(SF_PB + k) * Bs + b];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) Sp[k] = scan[(SF_SIG + k) * Bs + b];
+    }
+    if (sc || touched[b]) {
       Nm = map[MF_NP * Bs + b];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) { pb[k] = scan[(SF_PB + k) * Bs + b]; c[k] = derived[(MD_C + k) * Bs + b]; }
+      for (int k = 0; k < 3; ++k) c[k] = derived[(MD_C + k) * Bs + b];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) { Sp[k] = scan[(SF_SIG + k) * Bs + b]; Sc[k] = derived[(MD_SIG + k) * Bs + b]; }
+      for (int k = 0; k < 9; ++k) Sc[k] = derived[(MD_SIG + k) * Bs + b];
     }
     double tb[3];
 #pragma unroll
@@ -1122,17 +1131,23 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
   const double* R = pa.R;
   const double g = pa.gamma;
   for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
+    // sc: the bin has scan mass.  Without it the scan rows hold the zero-bin values (N = 0, zero
+    // sums, p_bar = 0, Sigma_p = eps I) and every scan term below is an exact zero (each is
+    // multiplied by N or is R 0 R^T), so the update is the forgetting alone: those rows are not
+    // read (masked loads of zeros; the arithmetic is unchanged bit for bit).
+    bool sc = true;
     if (act) {
-      if (act[b]) {
+      sc = act[b] != 0;
+      if (sc) {
         if (!touched[b]) touched[b] = 1;
       } else if (!touched[b]) {
         continue;
       }
     }
-    const double N = scan[SF_N * Bs + b];
+    const double N = sc ? scan[SF_N * Bs + b] : 0.0;
     double pb[3], u[3], q[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) pb[k] = scan[(SF_PB + k) * Bs + b];
+    for (int k = 0; k < 3; ++k) pb[k] = sc ? scan[(SF_PB + k) * Bs + b] : 0.0;
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       u[i] = R[3 * i] * pb[0] + R[3 * i + 1] * pb[1] + R[3 * i + 2] * pb[2];
@@ -1141,7 +1156,12 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
     // S_dir += R s_dir
     double sd[3];
     {
-      double s0 = scan[(SF_SD + 0) * Bs + b], s1 = scan[(SF_SD + 1) * Bs + b], s2 = scan[(SF_SD + 2) * Bs + b];
+      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
+      if (sc) {
+        s0 = scan[(SF_SD + 0) * Bs + b];
+        s1 = scan[(SF_SD + 1) * Bs + b];
+        s2 = scan[(SF_SD + 2) * Bs + b];
+      }
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         sd[i] = g * map[(MF_SD + i) * Bs + b] + (R[3 * i] * s0 + R[3 * i + 1] * s1 + R[3 * i + 2] * s2);
@@ -1152,7 +1172,7 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
     {
       double S[9], RS[9];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) S[k] = scan[(SF_S + k) * Bs + b];
+      for (int k = 0; k < 9; ++k) S[k] = sc ? scan[(SF_S + k) * Bs + b] : 0.0;
       mat3_mul(R, S, RS);
 #pragma unroll
       for (int i = 0; i < 3; ++i)
@@ -1182,7 +1202,8 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j) M2[3 * i + j] = scan[(SF_SIG + 3 * i + j) * Bs + b] + pb[i] * pb[j];
+        for (int j = 0; j < 3; ++j)
+          M2[3 * i + j] = (sc ? scan[(SF_SIG + 3 * i + j) * Bs + b] : (i == j ? kEpsPsd : 0.0)) + pb[i] * pb[j];
       mat3_mul(R, M2, RM);
       double X[9], XF[9], XG[9];
       skew3(u, X);

@@ -58,7 +58,11 @@ GCS_HD double sigmoid(double x) {
 // smooth_window_weights, imu_preintegration.py:20-43
 GCS_HD double smooth_window(double t, double start, double end, double sigma) {
   double sig = sigma > 1e-6 ? sigma : 1e-6;
-  double w = sigmoid((t - start) / sig) * sigmoid((end - t) / sig);
+  const double a = (t - start) / sig, b = (end - t) / sig;
+  // exp underflows to exactly 0 below -745.2, so a factor is exactly 0 there and w is the floor
+  // (padded IMU samples, stamp 0): the same value without the two exps
+  if (a < -746.0 || b < -746.0) return kWeightFloor;
+  double w = sigmoid(a) * sigmoid(b);
   return w * (1.0 - kWeightFloor) + kWeightFloor;
 }
 

@@ -40,7 +40,8 @@ class GcsScanInputs(C.Structure):
                 ("weights_dev", C.c_void_p), ("n_points", C.c_int32), ("imu_stamps", c_double_p),
                 ("imu_gyro", c_double_p), ("imu_accel", c_double_p), ("imu_len", C.c_int32),
                 ("scan_start_time", C.c_double), ("scan_end_time", C.c_double), ("dt_sec", C.c_double),
-                ("Q", c_double_p), ("L_ext", c_double_p), ("h_ext", c_double_p)]
+                ("Q", c_double_p), ("L_ext", c_double_p), ("h_ext", c_double_p),
+                ("t_last_scan", C.c_double), ("t_scan", C.c_double)]
 
 
 class GcsBelief(C.Structure):
@@ -52,7 +53,7 @@ class GcsScanOutputs(C.Structure):
     _fields_ = [("belief", GcsBelief), ("iw_process_dPsi", C.c_double * 252), ("iw_process_dnu", C.c_double * 7),
                 ("z_t", C.c_double * 6), ("L_evidence", C.c_double * (D_Z * D_Z)), ("h_evidence", C.c_double * D_Z),
                 ("R_mf", C.c_double * 9), ("t_wls", C.c_double * 3), ("cert", C.c_double * CERT_LEN),
-                ("stage_ms", C.c_double * 8)]
+                ("stage_ms", C.c_double * 8), ("iw_meas_dPsi", C.c_double * 27), ("iw_meas_dnu", C.c_double * 3)]
 
 
 # (name, restype, argtypes) for every symbol declared in include/gcslam_hip.h
@@ -78,6 +79,8 @@ _SIGS = [
                                         C.POINTER(C.c_void_p)]),
     ("gcs_ctx_set_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
     ("gcs_ctx_get_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p]),
+    ("gcs_ctx_set_meas_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
+    ("gcs_ctx_get_meas_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p]),
     ("gcs_scan", C.c_int, [C.c_void_p, C.POINTER(GcsScanInputs), C.POINTER(GcsScanOutputs)]),
     ("gcs_point_stage", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_double,
                                   C.c_double, c_double_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, c_double_p]),
@@ -99,6 +102,8 @@ _SIGS = [
     ("gcs_preintegrate_imu", C.c_int, [C.c_int32, c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
                                        c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
     ("gcs_belief_world_pose", C.c_int, [C.POINTER(GcsBelief), c_double_p]),
+    ("gcs_imu_meas_iw_suffstats", C.c_int, [C.c_int32] + [c_double_p] * 10),
+    ("gcs_meas_iw_apply", C.c_int, [c_double_p] * 7),
     ("gcs_fibonacci_atlas", C.c_int, [C.c_int32, c_double_p]),
     ("gcs_knn_table", C.c_int, [C.c_int32, c_double_p, C.c_int32, c_int32_p]),
     ("gcs_nearest_bins", C.c_int, [C.c_int32, c_double_p, C.c_int32, c_double_p, c_int32_p]),

@@ -120,6 +120,18 @@ class HypothesisContext:
         self._chk(self.lib.gcs_ctx_get_iw_state(self.h, L.dptr(nu), L.dptr(Psi), L.dptr(Q)), "get_iw_state")
         return nu, Psi.reshape(7, 6, 6), Q.reshape(22, 22)
 
+    def meas_iw_state(self):
+        """Measurement-noise IW state: nu (3,), Psi (3,3,3), cert [psd_delta, nu_delta] of the last apply."""
+        nu, Psi, cert = np.zeros(3), np.zeros(27), np.zeros(2)
+        self._chk(self.lib.gcs_ctx_get_meas_iw_state(self.h, L.dptr(nu), L.dptr(Psi), L.dptr(cert)),
+                  "get_meas_iw_state")
+        return nu, Psi.reshape(3, 3, 3), cert
+
+    def set_meas_iw_state(self, nu, Psi):
+        n = np.ascontiguousarray(nu, np.float64).reshape(3)
+        P = np.ascontiguousarray(Psi, np.float64).reshape(27)
+        self._chk(self.lib.gcs_ctx_set_meas_iw_state(self.h, L.dptr(n), L.dptr(P)), "set_meas_iw_state")
+
     STAGES = ("points", "sort_bucket", "bins", "matrix_fisher", "planar", "pushforward")
 
     def enable_timing(self, on=True, stages=None):
@@ -201,7 +213,9 @@ class HypothesisContext:
 
     # ------------------------------------------------------------------ the scan
     def scan(self, xyz_dev, point_step, t_dev, w_dev, n_points, imu_stamps, imu_gyro, imu_accel,
-             scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None):
+             scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None, t_last_scan=None, t_scan=None):
+        """gcs_scan.  t_last_scan / t_scan bound the scan-to-scan IMU window of the measurement-noise
+        IW statistics (pipeline.py:331-332); default: the scan window."""
         imu_stamps = np.ascontiguousarray(imu_stamps, np.float64)
         imu_gyro = np.ascontiguousarray(imu_gyro, np.float64).reshape(-1)
         imu_accel = np.ascontiguousarray(imu_accel, np.float64).reshape(-1)
@@ -218,6 +232,8 @@ class HypothesisContext:
         inp.scan_start_time = float(scan_start_time)
         inp.scan_end_time = float(scan_end_time)
         inp.dt_sec = float(dt_sec)
+        inp.t_last_scan = float(scan_start_time if t_last_scan is None else t_last_scan)
+        inp.t_scan = float(scan_end_time if t_scan is None else t_scan)
         keep = []
         for name, arr in (("Q", Q), ("L_ext", L_ext), ("h_ext", h_ext)):
             if arr is not None:

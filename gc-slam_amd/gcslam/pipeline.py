@@ -145,7 +145,7 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
     ctx.set_belief(belief_prev.X_anchor, belief_prev.stamp_sec, belief_prev.z_lin, belief_prev.L, belief_prev.h)
     rec, t, w = _as_device_scan(raw_points, raw_timestamps, raw_weights, config.device)
     out = ctx.scan(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
-                   dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext)
+                   dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan)
     X, stamp, z, Lm, h = ctx.get_belief()
     cert = np.array(out.cert[:])
     certs = _certs_from_vector(cert, CHART_ID, belief_prev.anchor_id)
@@ -155,7 +155,7 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
         belief_updated=bel,
         iw_process_dPsi=np.array(out.iw_process_dPsi[:]).reshape(7, 6, 6),
         iw_process_dnu=np.array(out.iw_process_dnu[:]),
-        iw_meas_dPsi=np.zeros((3, 3, 3)), iw_meas_dnu=np.zeros(3),
+        iw_meas_dPsi=np.array(out.iw_meas_dPsi[:]).reshape(3, 3, 3), iw_meas_dnu=np.array(out.iw_meas_dnu[:]),
         iw_lidar_bucket_dPsi=np.zeros((64, 3, 3)), iw_lidar_bucket_dnu=np.zeros(64),
         all_certs=certs, aggregated_cert=agg,
         diagnostics_tape=dict(stage_ms=list(out.stage_ms[:4]), total_trigger=cert[35], beta=cert[30]),

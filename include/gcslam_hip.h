@@ -86,6 +86,8 @@ typedef struct {
   const double* Q;             /* [22*22] host; NULL = context's IW-derived Q */
   const double* L_ext;         /* optional external evidence [22*22] (IMU/odom family), may be NULL */
   const double* h_ext;         /* [22] */
+  /* scan-to-scan IMU window of the measurement-noise IW statistics (pipeline.py:331-332,448-453) */
+  double t_last_scan, t_scan;
 } gcs_scan_inputs;
 
 typedef struct {
@@ -109,6 +111,8 @@ typedef struct {
   double t_wls[3];
   double cert[GCS_CERT_LEN];
   double stage_ms[8];                /* host-measured stage times */
+  double iw_meas_dPsi[3 * 9];        /* measurement-noise IW statistics [gyro, accel, lidar] 3x3 blocks */
+  double iw_meas_dnu[3];
 } gcs_scan_outputs;
 
 /* ---------------------------------------------------------------- context */
@@ -141,6 +145,10 @@ int gcs_ctx_device_arrays(gcs_ctx* ctx, double** scan_dev, double** map_dev, dou
 int gcs_ctx_get_bin_order(gcs_ctx* ctx, int32_t* order /*B*/);
 int gcs_ctx_set_iw_state(gcs_ctx* ctx, const double* nu7, const double* Psi7x36);
 int gcs_ctx_get_iw_state(gcs_ctx* ctx, double* nu7, double* Psi7x36, double* Q22x22);
+/* measurement-noise IW state [gyro, accel, lidar] (structures/measurement_noise_iw_jax.py:29-68);
+ * cert2 = [psd_delta, nu_delta] of the last apply in gcs_hypothesis_combine (may be NULL) */
+int gcs_ctx_set_meas_iw_state(gcs_ctx* ctx, const double* nu3, const double* Psi3x9);
+int gcs_ctx_get_meas_iw_state(gcs_ctx* ctx, double* nu3, double* Psi3x9, double* cert2);
 
 /* ---------------------------------------------------------------- the per-scan pipeline */
 int gcs_scan(gcs_ctx* ctx, const gcs_scan_inputs* in, gcs_scan_outputs* out);
@@ -186,6 +194,14 @@ int gcs_preintegrate_imu(int32_t m, const double* stamps, const double* gyro, co
                          const double* rotvec_start, const double* gyro_bias, const double* accel_bias,
                          const double* gravity_W, double* delta_pose6, double* ess);
 int gcs_belief_world_pose(const gcs_belief* b, double* pose6); /* belief.py:410-434 */
+/* gyro + accel measurement-noise IW statistics of one IMU window (pipeline.py:522-566;
+ * measurement_noise_iw_jax.py:130-218); w_int = scan-to-scan window weights, stamps <= 0 are padding */
+int gcs_imu_meas_iw_suffstats(int32_t m, const double* stamps, const double* gyro, const double* accel,
+                              const double* w_int, const double* gyro_bias, const double* accel_bias,
+                              const double* rotvec0, const double* gravity_W, double* dPsi3x9, double* dnu3);
+/* measurement_noise_apply_suffstats_jax (measurement_noise_iw_jax.py:59-100) */
+int gcs_meas_iw_apply(const double* nu3, const double* Psi3x9, const double* dPsi3x9, const double* dnu3,
+                      double* nu_out, double* Psi_out, double* cert2);
 int gcs_fibonacci_atlas(int32_t n_bins, double* dirs /*B*3*/);
 int gcs_knn_table(int32_t n_bins, const double* dirs, int32_t k, int32_t* knn /*B*k*/);
 int gcs_nearest_bins(int32_t n_bins, const double* dirs, int32_t n_query, const double* q /*n*3*/, int32_t* out);
@@ -194,7 +210,8 @@ int gcs_nearest_bins(int32_t n_bins, const double* dirs, int32_t n_query, const 
 /* Pack this hypothesis' contribution (weights pre-applied) for an RCCL sum all-reduce:
  * [w_iw dPsi 252 | w_iw dnu 7 | w_iw dPsi_meas 27 | w_iw dnu_meas 3 | w L 484 | w h 22 | w z 22 | w mu 22 | w |mu|^2 1] */
 int gcs_hypothesis_payload(gcs_ctx* ctx, double w_iw, double w_bary, double* payload_host);
-/* Apply the summed payload: barycenter (PSD of L), IW apply + Q rebuild (stored in ctx).
+/* Apply the summed payload: barycenter (PSD of L), process IW apply + Q rebuild and
+ * measurement-noise IW apply (backend_node.py:2102-2119; both stored in ctx).
  * combined_out may be NULL; cert_out = [psd_delta, spread, iw_psd_delta, iw_nu_delta]. */
 int gcs_hypothesis_combine(gcs_ctx* ctx, const double* payload_sum, int32_t scan_count, gcs_belief* combined_out,
                            double* cert_out);

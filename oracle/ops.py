@@ -625,6 +625,66 @@ def process_noise_iw_apply(nu, Psi, dPsi, dnu, nu_max=1000.0):
     return nu_new, Psi_new, np.array([dsum, np.abs(nu_new - nu_raw).sum()])
 
 
+# ================================================================ row 13: IW measurement noise
+MEAS_RHO = (0.995, 0.995, 0.99)            # gyro, accel, lidar: constants.py:279-281
+MEAS_SIGMA = (8.7e-7, 9.5e-5, 0.01)        # constants.py:190,201,210
+
+
+def datasheet_measurement_noise_state():
+    """create_datasheet_measurement_noise_state, structures/measurement_noise_iw_jax.py:37-68:
+    nu = p + 1 + 0.5, Psi = Sigma_prior * 0.5 per block [gyro, accel, lidar]."""
+    nu = np.full(3, 3.0 + 1.0 + IW_NU_WEAK_ADD)
+    Psi = np.stack([np.eye(3) * s * IW_NU_WEAK_ADD for s in MEAS_SIGMA])
+    return nu, Psi
+
+
+def _weighted_outer_psd(w, r):
+    """sum_m w_norm[m] r_m r_m^T symmetrised and PSD-projected (measurement_noise_iw_jax.py:150-157)."""
+    w_norm = w / (w.sum() + EPS_MASS)
+    rrT = np.einsum("m,mi,mj->ij", w_norm, r, r)
+    return psd_project(0.5 * (rrT + rrT.T), EPS_PSD)[0]
+
+
+def imu_meas_iw_suffstats(imu_stamps, imu_gyro, imu_accel, w_int, gyro_bias, accel_bias, rotvec0, gravity_W):
+    """Gyro + accel measurement-noise IW statistics of one scan: the pipeline's dt_imu, valid mask
+    and omega_avg (FS/backend/pipeline.py:522-566, summed at :1024-1025) around
+    imu_gyro_meas_iw_suffstats_from_avg_rate_jax (measurement_noise_iw_jax.py:130-167) and
+    imu_accel_meas_iw_suffstats_from_gravity_dir_jax (:170-218).  Returns dPsi (3,3,3), dnu (3,)."""
+    stamps = np.asarray(imu_stamps, np.float64).reshape(-1)
+    valid = stamps > 0.0
+    n_valid = int(valid.sum())
+    dt_imu = float((stamps[valid].max() - stamps[valid].min()) / max(n_valid - 1, 1)) if n_valid >= 2 else 0.0
+    dt_imu = max(dt_imu, 1e-12)
+    w = np.asarray(w_int, np.float64) * valid.astype(np.float64)
+    g_db = np.asarray(imu_gyro, np.float64) - np.asarray(gyro_bias)[None, :]
+    omega_avg = np.einsum("m,mi->i", w / (w.sum() + EPS_MASS), g_db)
+    if not np.all(np.isfinite(omega_avg)):
+        raise ValueError(f"omega_avg contains non-finite values: {omega_avg}")
+    dPsi = np.zeros((3, 3, 3))
+    dPsi[0] = _weighted_outer_psd(w, g_db - omega_avg[None, :]) * dt_imu
+    f_pred = -(se3.so3_exp(np.asarray(rotvec0, np.float64)).T @ np.asarray(gravity_W, np.float64))
+    r_a = (np.asarray(imu_accel, np.float64) - np.asarray(accel_bias)[None, :]) - f_pred[None, :]
+    dPsi[1] = _weighted_outer_psd(w, r_a) * dt_imu
+    return dPsi, np.array([1.0, 1.0, 0.0])
+
+
+def measurement_noise_iw_apply(nu, Psi, dPsi, dnu, nu_max=1000.0):
+    """measurement_noise_apply_suffstats_jax, measurement_noise_iw_jax.py:59-100."""
+    rho = np.array(MEAS_RHO)
+    raw = rho[:, None, None] * Psi + dPsi
+    raw = 0.5 * (raw + np.swapaxes(raw, -1, -2))
+    Psi_new = np.zeros_like(raw)
+    dsum = 0.0
+    for i in range(3):
+        Psi_new[i], c = psd_project(raw[i], EPS_PSD)
+        dsum += c[0]
+    nu_raw = rho * nu + dnu
+    nu_min = 3.0 + 1.0 + IW_NU_WEAK_ADD
+    nu_floor = nu_min + softplus(nu_raw - nu_min)
+    nu_new = nu_max - softplus(nu_max - nu_floor)
+    return nu_new, Psi_new, np.array([dsum, np.abs(nu_new - nu_raw).sum()])
+
+
 # ================================================================ row 14: hypothesis combine
 def hypothesis_barycenter(L_stack, h_stack, z_stack, weights):
     """_hypothesis_barycenter_core, hypothesis.py:51-117."""

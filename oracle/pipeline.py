@@ -4,7 +4,8 @@ Step order follows README.md:105-122 with the live calling convention of
 process_scan_single_hypothesis (FS/backend/pipeline.py:316-1591); see SURVEY.md
 section 3.3 for the reconstruction.  Out of scope this round: the
 IMU/odom evidence family of step 9 (pipeline.py:595-776) -- it enters as an
-optional external (L, h) term -- and the measurement-noise IW statistics.
+optional external (L, h) term.  Scans without t_last_scan / t_scan keys use the scan window
+(scan_start_time, scan_end_time) for the scan-to-scan IMU window.
 """
 
 from __future__ import annotations
@@ -74,6 +75,12 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
     pre = ops.preintegrate_imu(scan["imu_stamps"], scan["imu_gyro"], scan["imu_accel"], w_imu, pose0[3:6],
                                mu_inc[9:12], mu_inc[12:15], np.asarray(cfg.gravity_W))
     xi = se3.se3_log(pre["delta_pose"])
+    # measurement-noise IW statistics over the scan-to-scan window (pipeline.py:448-453,522-566)
+    w_int = ops.smooth_window_weights(scan["imu_stamps"], scan.get("t_last_scan", scan["scan_start_time"]),
+                                      scan.get("t_scan", scan["scan_end_time"]), sigma_warp)
+    meas_dPsi, meas_dnu = ops.imu_meas_iw_suffstats(scan["imu_stamps"], scan["imu_gyro"], scan["imu_accel"], w_int,
+                                                    mu_inc[9:12], mu_inc[12:15], pose0[3:6],
+                                                    np.asarray(cfg.gravity_W))
     if cfg.deskew_rotation_only:
         xi[:3] = 0.0
     dk = ops.deskew_constant_twist(bud["points"], bud["timestamps"], bud["weights"],
@@ -151,21 +158,29 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
     b_fin, dinfo = ops.anchor_drift_update(b_rec)
     certs.append(dict(name="anchor_drift", **dinfo))
     return dict(belief=b_fin, map=new_map, iw_process_dPsi=dPsi, iw_process_dnu=dnu,
-                budget=bud, deskew=dk, soft_assign=sa, scan_bins=st, mf=mf, planar=pt,
+                iw_meas_dPsi=meas_dPsi, iw_meas_dnu=meas_dnu, budget=bud, deskew=dk, soft_assign=sa, scan_bins=st, mf=mf, planar=pt,
                 L_evidence=L_ev, h_evidence=h_ev, beta=beta, total_trigger=T,
                 frobenius_strength=rinfo["frobenius_strength"], z_t=z_t, xi_body=xi, certs=certs,
                 belief_post=b_post, belief_recomposed=b_rec)
 
 
-def combine_and_update_noise(results, weights, iw_state, scan_count):
+def combine_and_update_noise(results, weights, iw_state, scan_count, meas_state=None):
     """Node-level post-loop (FS/backend/backend_node.py:1999-2119): IW accumulation with raw
-    weights, barycenter with floor-renormalised weights, IW apply, Q rebuild."""
+    weights, barycenter with floor-renormalised weights, process IW apply (weight min(1, scan)),
+    Q rebuild, measurement-noise IW apply (weight 1, :2105,2114-2119)."""
     nu, Psi = iw_state
     acc = np.zeros((7, 6, 6))
     accn = np.zeros(7)
+    accm = np.zeros((3, 3, 3))
+    accmn = np.zeros(3)
     for w, r in zip(weights, results):
         acc += w * r["iw_process_dPsi"]
         accn += w * r["iw_process_dnu"]
+        accm += w * r["iw_meas_dPsi"]
+        accmn += w * r["iw_meas_dnu"]
+    if meas_state is None:
+        meas_state = ops.datasheet_measurement_noise_state()
+    mnu, mPsi, mcert = ops.measurement_noise_iw_apply(meas_state[0], meas_state[1], accm, accmn)
     L = np.stack([r["belief"].L for r in results])
     h = np.stack([r["belief"].h for r in results])
     z = np.stack([r["belief"].z_lin for r in results])
@@ -173,4 +188,5 @@ def combine_and_update_noise(results, weights, iw_state, scan_count):
     wp = min(1, scan_count)
     nu2, Psi2, cert = ops.process_noise_iw_apply(nu, Psi, wp * acc, wp * accn)
     Q = ops.process_noise_Q(nu2, Psi2)
-    return dict(combined=combo, iw_state=(nu2, Psi2), Q=Q, iw_cert=cert, acc_dPsi=acc, acc_dnu=accn)
+    return dict(combined=combo, iw_state=(nu2, Psi2), Q=Q, iw_cert=cert, acc_dPsi=acc, acc_dnu=accn,
+                meas_state=(mnu, mPsi), meas_cert=mcert, acc_meas_dPsi=accm, acc_meas_dnu=accmn)

@@ -97,13 +97,14 @@ def scan_steps(mode, B, cap, n_raw, n_scans=3):
     ms = opipe.MapState.empty(B)
     out = dict(mode=mode, n_bins=B, cap=cap, n_raw=n_raw, Q=Q, tau=cfg.tau)
     keys = ("xyz_record", "timestamps", "weights", "imu_stamps", "imu_gyro", "imu_accel")
-    rec = {k: [] for k in ("z_t", "X_anchor", "L", "h", "z_lin", "beta", "T", "dPsi", "dnu", "L_ev", "h_ev",
-                           "scan_N", "map")}
-    for k in keys + ("scan_start_time", "scan_end_time", "dt_sec"):
+    rec = {k: [] for k in ("z_t", "X_anchor", "L", "h", "z_lin", "beta", "T", "dPsi", "dnu", "meas_dPsi",
+                           "meas_dnu", "L_ev", "h_ev", "scan_N", "map")}
+    times = ("scan_start_time", "scan_end_time", "dt_sec", "t_last_scan", "t_scan")
+    for k in keys + times:
         out[f"in_{k}"] = []
     for s in range(n_scans):
         sc = synthetic.make_scan(n_raw, 20 + s)
-        for k in keys + ("scan_start_time", "scan_end_time", "dt_sec"):
+        for k in keys + times:
             out[f"in_{k}"].append(np.asarray(sc[k]))
         r = opipe.process_scan_bin_path(b, sc, Q, cfg, bins, knn, ms)
         rec["z_t"].append(r["z_t"])
@@ -115,6 +116,8 @@ def scan_steps(mode, B, cap, n_raw, n_scans=3):
         rec["T"].append(r["total_trigger"])
         rec["dPsi"].append(r["iw_process_dPsi"])
         rec["dnu"].append(r["iw_process_dnu"])
+        rec["meas_dPsi"].append(r["iw_meas_dPsi"])
+        rec["meas_dnu"].append(r["iw_meas_dnu"])
         rec["L_ev"].append(r["L_evidence"])
         rec["h_ev"].append(r["h_evidence"])
         rec["scan_N"].append(r["scan_bins"]["N"])
@@ -130,8 +133,9 @@ def scan_steps(mode, B, cap, n_raw, n_scans=3):
 
 
 def combine():
-    """Hypothesis combine + IW apply (hypothesis.py:51-117, inverse_wishart_jax.py:126-185,
-    backend_node.py:1999-2119) over 4 hypotheses with distinct beliefs."""
+    """Hypothesis combine + IW applies (hypothesis.py:51-117, inverse_wishart_jax.py:126-185,
+    measurement_noise_iw_jax.py:59-100, backend_node.py:1999-2119) over 4 hypotheses with distinct
+    beliefs; the measurement-noise statistics come from 4 synthetic IMU windows."""
     rng = np.random.default_rng(5)
     H = 4
     results = []
@@ -141,15 +145,25 @@ def combine():
         bel = ops.Belief(rng.normal(0, 0.05, 6), 1.0, rng.normal(0, 1e-3, 22), L, rng.normal(size=22))
         dPsi = np.stack([np.outer(v, v) for v in rng.normal(size=(7, 6))])
         results.append(dict(belief=bel, iw_process_dPsi=dPsi, iw_process_dnu=np.ones(7)))
+    for k, res in enumerate(results):  # after the draws above, so those inputs are unchanged
+        sc = synthetic.make_scan(16, 30 + k)
+        w_int = ops.smooth_window_weights(sc["imu_stamps"], sc["t_last_scan"], sc["t_scan"], 0.01)
+        res["iw_meas_dPsi"], res["iw_meas_dnu"] = ops.imu_meas_iw_suffstats(
+            sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], w_int, 1e-3 * np.ones(3), np.array([0.0, 1e-2, 0.0]),
+            np.array([0.01, -0.02, 0.3 * k]), np.array(ops.GRAVITY_W))
     w = np.array([0.5, 0.3, 0.199, 0.001])
     nu, Psi = ops.datasheet_process_noise_state()
-    r = opipe.combine_and_update_noise(results, w, (nu, Psi), 3)
+    mnu, mPsi = ops.datasheet_measurement_noise_state()
+    r = opipe.combine_and_update_noise(results, w, (nu, Psi), 3, (mnu, mPsi))
     return dict(weights=w, L=np.stack([x["belief"].L for x in results]), h=np.stack([x["belief"].h for x in results]),
                 z_lin=np.stack([x["belief"].z_lin for x in results]),
                 X_anchor=np.stack([x["belief"].X_anchor for x in results]),
                 dPsi=np.stack([x["iw_process_dPsi"] for x in results]), nu0=nu, Psi0=Psi,
                 out_L=r["combined"]["L"], out_h=r["combined"]["h"], out_z_lin=r["combined"]["z_lin"],
-                out_nu=r["iw_state"][0], out_Psi=r["iw_state"][1], out_Q=r["Q"])
+                out_nu=r["iw_state"][0], out_Psi=r["iw_state"][1], out_Q=r["Q"],
+                meas_dPsi=np.stack([x["iw_meas_dPsi"] for x in results]),
+                meas_dnu=np.stack([x["iw_meas_dnu"] for x in results]), meas_nu0=mnu, meas_Psi0=mPsi,
+                out_meas_nu=r["meas_state"][0], out_meas_Psi=r["meas_state"][1], out_meas_cert=r["meas_cert"])
 
 
 FIXTURES = {

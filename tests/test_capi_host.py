@@ -75,6 +75,53 @@ def test_psd_project3_matches_oracle(lib):
         assert np.linalg.eigvalsh(0.5 * (out + out.T)).min() >= 1e-12 * (1 - 1e-6) - 1e-15 * s
 
 
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_imu_meas_iw_suffstats_match_oracle(lib, seed):
+    """Gyro + accel measurement-noise IW statistics (measurement_noise_iw_jax.py:130-218 with the
+    pipeline's dt_imu / valid mask / omega_avg, pipeline.py:522-566) on a padded IMU window."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "gc-slam_amd"))
+    from gcslam import synthetic
+    rng = np.random.default_rng(seed)
+    sc = synthetic.make_scan(16, seed)
+    w_int = ops.smooth_window_weights(sc["imu_stamps"], sc["t_last_scan"], sc["t_scan"], 0.01 + 0.02 * seed)
+    w_int = np.where(sc["imu_stamps"] > 0.0, w_int, 0.0)
+    gb, ab = 1e-3 * rng.standard_normal(3), 1e-2 * rng.standard_normal(3)
+    rv = rng.standard_normal(3) * 0.3
+    g = np.array(ops.GRAVITY_W)
+    ref, ref_nu = ops.imu_meas_iw_suffstats(sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], w_int, gb, ab, rv, g)
+    args = [np.ascontiguousarray(a, np.float64) for a in (sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], w_int,
+                                                            gb, ab, rv, g)]
+    dPsi, dnu = np.zeros(27), np.zeros(3)
+    assert lib.gcs_imu_meas_iw_suffstats(len(w_int), *[L.dptr(a) for a in args], L.dptr(dPsi), L.dptr(dnu)) == 0
+    assert np.allclose(dPsi.reshape(3, 3, 3), ref, rtol=1e-11, atol=1e-22)
+    assert np.array_equal(dnu, ref_nu)
+    assert np.all(dPsi.reshape(3, 3, 3)[2] == 0.0)                     # lidar block untouched here
+
+
+def test_meas_iw_apply_matches_oracle(lib):
+    """measurement_noise_apply_suffstats_jax (measurement_noise_iw_jax.py:59-100): forgetting, PSD,
+    softplus projection of nu into [p + 1.5, 1000]."""
+    rng = np.random.default_rng(4)
+    nu, Psi = ops.datasheet_measurement_noise_state()
+    for it in range(4):
+        dP = np.stack([np.outer(v, v) * s for v, s in zip(rng.standard_normal((3, 3)), (1e-8, 1e-4, 1e-3))])
+        if it == 3:
+            dP[0] -= 1e-6 * np.eye(3)                                        # forces a PSD clamp
+        dn = np.array([1.0, 1.0, float(it % 2)])
+        ref = ops.measurement_noise_iw_apply(nu, Psi, dP, dn)
+        nu_o, Psi_o, c = np.zeros(3), np.zeros(27), np.zeros(2)
+        a = [np.ascontiguousarray(x, np.float64).reshape(-1) for x in (nu, Psi, dP, dn)]
+        assert lib.gcs_meas_iw_apply(*[L.dptr(x) for x in a], L.dptr(nu_o), L.dptr(Psi_o), L.dptr(c)) == 0
+        # unclamped blocks: the host PSD fast path returns sym(M) with delta 0, the oracle's eigh
+        # rebuild differs by rounding (~1e-16 |M|), so absolute bars scale with the block norm
+        s = np.abs(ref[1]).max()
+        assert np.allclose(nu_o, ref[0], rtol=1e-14, atol=0)
+        assert np.allclose(Psi_o.reshape(3, 3, 3), ref[1], rtol=1e-12, atol=1e-14 * s)
+        assert c[0] == pytest.approx(ref[2][0], rel=1e-9, abs=1e-13 * s) and c[1] == pytest.approx(ref[2][1], rel=1e-12)
+        nu, Psi = ref[0], ref[1]
+
+
 def test_spd_solve_and_inverse_match_oracle(lib):
     rng = np.random.default_rng(11)
     A = rng.standard_normal((22, 22))

@@ -42,12 +42,15 @@ def _iw_stats(k):
     return rng.normal(size=252), np.ones(7)
 
 
-def pack_payload(b, dPsi, dnu, w_iw, w_bary):
+def pack_payload(b, dPsi, dnu, w_iw, w_bary, meas_dPsi=None, meas_dnu=None):
     """Layout of gcs_hypothesis_payload: [dPsi 252 | dnu 7 | meas dPsi 27 | meas dnu 3 | L 484 | h 22 |
     z_lin 22 | mu 22 | |mu|^2 1]."""
     p = np.zeros(PAYLOAD_LEN)
     p[0:252] = w_iw * dPsi
     p[252:259] = w_iw * dnu
+    if meas_dPsi is not None:
+        p[259:286] = w_iw * np.asarray(meas_dPsi).reshape(27)
+        p[286:289] = w_iw * np.asarray(meas_dnu)
     mu = b.mean_increment()
     p[289:773] = w_bary * b.L.ravel()
     p[773:795] = w_bary * b.h

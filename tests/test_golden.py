@@ -83,14 +83,20 @@ def test_golden_scan_steps(name):
         _close(r["belief"].L, g["out_L"][s], rtol=1e-10, atol=1e-10 * np.abs(g["out_L"][s]).max())
         _close(r["scan_bins"]["N"], g["out_scan_N"][s], atol=1e-14)
         assert r["beta"] == pytest.approx(float(g["out_beta"][s]), rel=RT)
+        _close(r["iw_meas_dPsi"], g["out_meas_dPsi"][s], rtol=1e-10, atol=1e-22)
+        _close(r["iw_meas_dnu"], g["out_meas_dnu"][s])
         b, ms = r["belief"], r["map"]
 
 
 def test_golden_combine():
     g = load("combine_h4")
     results = [dict(belief=ops.Belief(g["X_anchor"][k], 1.0, g["z_lin"][k], g["L"][k], g["h"][k]),
-                    iw_process_dPsi=g["dPsi"][k], iw_process_dnu=np.ones(7)) for k in range(4)]
-    r = opipe.combine_and_update_noise(results, g["weights"], (g["nu0"], g["Psi0"]), 3)
+                    iw_process_dPsi=g["dPsi"][k], iw_process_dnu=np.ones(7), iw_meas_dPsi=g["meas_dPsi"][k],
+                    iw_meas_dnu=g["meas_dnu"][k]) for k in range(4)]
+    r = opipe.combine_and_update_noise(results, g["weights"], (g["nu0"], g["Psi0"]), 3,
+                                       (g["meas_nu0"], g["meas_Psi0"]))
+    _close(r["meas_state"][0], g["out_meas_nu"])
+    _close(r["meas_state"][1], g["out_meas_Psi"], atol=1e-20)
     _close(r["combined"]["L"], g["out_L"], atol=1e-12)
     _close(r["combined"]["h"], g["out_h"])
     _close(r["iw_state"][1], g["out_Psi"], atol=1e-15)

@@ -89,7 +89,8 @@ def test_gpu_golden_scan_steps(name):
         sc = scan_dict(g, s)
         rec, t, w = device_scan(sc)
         out = ctx.scan(rec, 16, t, w, int(g["n_raw"]), sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"],
-                       sc["scan_start_time"], sc["scan_end_time"], sc["dt_sec"], Q=g["Q"])
+                       sc["scan_start_time"], sc["scan_end_time"], sc["dt_sec"], Q=g["Q"],
+                       t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"])
         X, _, z, Lm, h = ctx.get_belief()
         cert = np.array(out.cert[:])
         assert cert[30] == pytest.approx(float(g["out_beta"][s]), rel=1e-12)
@@ -103,6 +104,11 @@ def test_gpu_golden_scan_steps(name):
         assert_close(f"scan{s} mean increment", mu_dev, mu_ref, rtol=1e-6, atol=ta)
         assert_close(f"scan{s} dPsi", np.array(out.iw_process_dPsi[:]).reshape(7, 6, 6), g["out_dPsi"][s],
                      rtol=1e-6, atol=1e-12)
+        # host PSD fast path vs the oracle's eigh rebuild: rounding ~1e-16 of the block norm
+        mref = g["out_meas_dPsi"][s]
+        assert_close(f"scan{s} meas dPsi", np.array(out.iw_meas_dPsi[:]).reshape(3, 3, 3), mref,
+                     rtol=1e-9, atol=1e-13 * np.abs(mref).max())
+        assert np.array_equal(np.array(out.iw_meas_dnu[:]), g["out_meas_dnu"][s])
         assert_close(f"scan{s} scan N", ctx.get_scan_stats()[0], g["out_scan_N"][s], rtol=1e-11, atol=1e-14)
         mref = g["out_map"][s]
         assert_close(f"scan{s} map", ctx.get_map()[0], mref, rtol=1e-7, atol=1e-9 * max(np.abs(mref).max(), 1.0))
@@ -120,11 +126,13 @@ def test_gpu_golden_combine():
     total = np.zeros(840)
     for k in range(4):
         b = ops.Belief(g["X_anchor"][k], 1.0, g["z_lin"][k], g["L"][k], g["h"][k])
-        total += pack_payload(b, g["dPsi"][k].reshape(-1), np.ones(7), float(w[k]), float(wn[k]))
+        total += pack_payload(b, g["dPsi"][k].reshape(-1), np.ones(7), float(w[k]), float(wn[k]), g["meas_dPsi"][k],
+                              g["meas_dnu"][k])
     ctx = _ctx(n_bins=48, n_points_cap=64, mode="dense")
     nu0 = np.ascontiguousarray(g["nu0"], np.float64)
     Psi0 = np.ascontiguousarray(g["Psi0"], np.float64).reshape(-1).copy()
     assert ctx.lib.gcs_ctx_set_iw_state(ctx.h, L.dptr(nu0), L.dptr(Psi0)) == 0
+    ctx.set_meas_iw_state(g["meas_nu0"], g["meas_Psi0"])
     (X, _, z, Lm, h), _ = ctx.hypothesis_combine(total, 3)
     assert_close("combined L", Lm, g["out_L"], rtol=1e-12, atol=1e-12)
     assert_close("combined h", h, g["out_h"], rtol=1e-12, atol=1e-14)
@@ -133,4 +141,9 @@ def test_gpu_golden_combine():
     assert_close("IW nu", nu, g["out_nu"], rtol=1e-13, atol=0)
     assert_close("IW Psi", Psi, g["out_Psi"], rtol=1e-12, atol=1e-16)
     assert_close("Q", Q, g["out_Q"], rtol=1e-12, atol=1e-18)
+    mnu, mPsi, mcert = ctx.meas_iw_state()
+    assert_close("meas IW nu", mnu, g["out_meas_nu"], rtol=1e-13, atol=0)
+    ps = np.abs(g["out_meas_Psi"]).max()
+    assert_close("meas IW Psi", mPsi, g["out_meas_Psi"], rtol=1e-12, atol=1e-14 * ps)
+    assert_close("meas IW cert", mcert, g["out_meas_cert"], rtol=1e-9, atol=1e-13 * ps)
     ctx.close()

@@ -215,7 +215,8 @@ def test_full_pipeline_matches_oracle(mode, B, cap, n_raw):
         ref = opipe.process_scan_bin_path(b, sc, Q, cfg, dirs, knn, ms)
         rec, t, w = device_scan(sc)
         out = ctx.scan(rec, 16, t, w, n_raw, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"],
-                       sc["scan_start_time"], sc["scan_end_time"], sc["dt_sec"], Q=Q)
+                       sc["scan_start_time"], sc["scan_end_time"], sc["dt_sec"], Q=Q,
+                       t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"])
         X, stamp, z, Lm, h = ctx.get_belief()
         cert = np.array(out.cert[:])
         assert cert[30] == pytest.approx(ref["beta"], rel=1e-12)
@@ -235,6 +236,8 @@ def test_full_pipeline_matches_oracle(mode, B, cap, n_raw):
         assert_close(f"scan{k} z_lin", z, ref["belief"].z_lin, rtol=1e-6, atol=1e-9)
         assert_close(f"scan{k} dPsi", np.array(out.iw_process_dPsi[:]).reshape(7, 6, 6), ref["iw_process_dPsi"],
                      rtol=1e-6, atol=1e-12)
+        assert_close(f"scan{k} meas dPsi", np.array(out.iw_meas_dPsi[:]).reshape(3, 3, 3), ref["iw_meas_dPsi"],
+                     rtol=1e-9, atol=1e-13 * np.abs(ref["iw_meas_dPsi"]).max())
         _check_scan_stats(ctx.get_scan_stats(), ref["scan_bins"])
         m_dev, _ = ctx.get_map()
         mref = map_fields(ref["map"].stats)
