@@ -93,12 +93,12 @@ template <int NV>
 __host__ __device__ constexpr int pstride() { return NV <= 16 ? 16 : 32; }
 int partial_stride(int nv) { return nv <= 16 ? 16 : 32; }
 
-template <int NV, unsigned MAXMASK>
+template <int NV, unsigned MAXMASK, int NT = kBlock>
 __device__ __forceinline__ void reduce_partials(const double* __restrict__ partials, int nblocks, double (&v)[NV],
                                                 double* lds) {
   constexpr int S = pstride<NV>();
   constexpr int G = S / 4;
-  constexpr int R = kBlock / G;
+  constexpr int R = NT / G;
   const int c0 = 4 * (threadIdx.x % G), r0 = threadIdx.x / G;
   bool mx[4];
   double a[4];
@@ -132,7 +132,7 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
     for (int k = 0; k < NV; ++k) {
       const bool mx = (MAXMASK >> k) & 1u;
       double s = lds[k];
-      for (int w = 1; w < kWaves; ++w) s = mx ? fmax(s, lds[w * S + k]) : s + lds[w * S + k];
+      for (int w = 1; w < NT / 64; ++w) s = mx ? fmax(s, lds[w * S + k]) : s + lds[w * S + k];
       v[k] = s;
     }
   }
@@ -650,9 +650,12 @@ constexpr int kBinNV = 16;
 //     offsets (block scan); each bin's work (records to visit) is summed.
 //  B: the sources' records, which each bin of the tile reads ~K/2.3 times, are staged once into
 //     LDS (64 B: p, d, m, w/Z); a tile with more than STAGE records reads them from HBM/L2.
-//  C: four lanes per bin accumulate the bin's records in fixed order (the bin's sources in
+//  C: LANES lanes per bin accumulate the bin's records in fixed order (the bin's sources in
 //     ascending bucket id, each source's points in ascending index, as one flattened list; lane l
-//     takes the l-th quarter; two xor adds) -- LDS traffic only.  (Work-proportional lane groups
+//     takes the l-th share; a fixed xor tree) -- LDS traffic only.  LANES = 4 for both scan
+//     densities.  (LANES = 8, 512-thread workgroups, was measured at C2: the active tile's life
+//     fell 23 -> 20 us, but at 122 VGPRs only two such workgroups fit a CU, the 540 active tiles
+//     no longer started together and the kernel went 32 -> 40 us.)  (Work-proportional lane groups
 //     were measured slower: the group bookkeeping and the deeper shuffle trees cost more than the
 //     balance bought back)
 //  D: wave 0, one lane per bin: PSD, kappa, the bin's Matrix-Fisher term, coalesced 64-bin output
@@ -661,10 +664,8 @@ constexpr int kBinNV = 16;
 // workgroups per CU), kStageSmall otherwise (C3: 26 KiB; four per CU, register-limited).
 constexpr int kMaxSrc = 320;   // atlas tables for B = 1k .. 1M have at most 199 per 64-bin tile
 constexpr int kMaxRl = 1280;   // reverse-kNN entries of one tile (~K x kBinTile; at most 1070)
-constexpr int kBinLanes = kBlock / kBinTile;
 constexpr int kStageBig = 512, kStageSmall = 256;
 constexpr int kRecD = 8;  // staged record: x y z dx dy dz m w/Z
-static_assert(kBinLanes == 4, "phase C splits each bin over four lanes");
 static_assert(kStageSmall * kRecD >= 19 * kBinTile, "phase D reuses the record stage for the bin sums");
 int bins_tile() { return kBinTile; }
 int bins_max_tile_sources() { return kMaxSrc; }
@@ -713,25 +714,27 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
     }
 }
 
-template <int STAGE>
-__global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* partials) {
+template <int STAGE, int LANES>
+__global__ __launch_bounds__(kBinTile * LANES) void k_bins_scale(BinKernelArgs a, double* partials) {
+  constexpr int NT = kBinTile * LANES, NW = NT / 64;
+  static_assert(LANES == 4 || LANES == 8, "phase C splits each bin over 4 or 8 lanes");
   __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
   __shared__ uint16_t s_rl[kMaxRl];
   __shared__ double s_rec[STAGE * kRecD];
   __shared__ double4 s_bd[kBinTile];
   __shared__ int s_q[kBinTile + 1];
   __shared__ uint32_t s_work[kBinTile];
-  __shared__ uint32_t s_wsum[kWaves];
-  __shared__ double lds[kWaves * 16];
+  __shared__ uint32_t s_wsum[NW];
+  __shared__ double lds[NW * 16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int tile = blockIdx.x;
   const int b0 = tile * kBinTile;
   const int nb = min(kBinTile, a.n_bins - b0);
   PROF(0);
-  for (int j = blockIdx.x * kBlock + t; j < a.n_zero_after; j += gridDim.x * kBlock) a.zero_after[j] = 0u;
+  for (int j = blockIdx.x * NT + t; j < a.n_zero_after; j += gridDim.x * NT) a.zero_after[j] = 0u;
   if (blockIdx.x == 0 && a.pts_partials) {  // k_points' cert partials (off the critical path here)
     double pv[5];
-    reduce_partials<5, 16u>(a.pts_partials, a.pts_blocks, pv, lds);
+    reduce_partials<5, 16u, NT>(a.pts_partials, a.pts_blocks, pv, lds);
     if (t == 0)
       for (int f = 0; f < 5; ++f) a.scalars[SC_DESKEW_WIN + f] = pv[f];
   }
@@ -777,8 +780,8 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   // phase A
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
   if (t <= nb) s_q[t] = q_t;
-  for (int q = q0 + t; q < q1t; q += kBlock) s_rl[q - q0] = a.rknn_local[q];
-  for (int j = t; j < ns; j += kBlock) {
+  for (int q = q0 + t; q < q1t; q += NT) s_rl[q - q0] = a.rknn_local[q];
+  for (int j = t; j < ns; j += NT) {
     const int src = a.tile_src[s0 + j];
     s_cnt[j] = a.counts[src];
     s_st[j] = a.starts[src];
@@ -791,7 +794,7 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
       for (int q = s_q[t]; q < s_q[t + 1]; ++q) w += s_cnt[s_rl[q - q0]];
     s_work[t] = w;
   }
-  const int chunk = (ns + kBlock - 1) / kBlock;
+  const int chunk = (ns + NT - 1) / NT;
   const int j0 = min(ns, t * chunk), j1 = min(ns, j0 + chunk);
   uint32_t mine = 0;
   for (int j = j0; j < j1; ++j) mine += s_cnt[j];
@@ -808,7 +811,9 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
     s_off[j] = run;
     run += s_cnt[j];
   }
-  const uint32_t total = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+  uint32_t total = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) total += s_wsum[w];
   const bool staged = total <= (uint32_t)STAGE;
   PROFV(8, total);
 #ifdef GCS_PHASE_PROF
@@ -823,7 +828,7 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   PROF(2);
   // phase B: stage the tile's records (record r belongs to the last source with s_off <= r)
   if (staged) {
-    for (uint32_t r = t; r < total; r += kBlock) {
+    for (uint32_t r = t; r < total; r += NT) {
       int lo = 0, hi = ns - 1;
       while (lo < hi) {
         int mid = (lo + hi + 1) >> 1;
@@ -840,12 +845,12 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
   // phase C: four lanes per bin; the bin's records (sources in order, points in order) are one
   // flattened list and lane l takes the l-th quarter, so every lane's trip count is its own share
   // (no per-source max over the wave's lanes).
-  const int lb = t / kBinLanes, l = t % kBinLanes;
+  const int lb = t / LANES, l = t % LANES;
   double acc[19];
 #pragma unroll
   for (int f = 0; f < 19; ++f) acc[f] = 0.0;
   const uint32_t work = s_work[lb];
-  const uint32_t i0 = work * (uint32_t)l / 4u, i1 = work * (uint32_t)(l + 1) / 4u;
+  const uint32_t i0 = work * (uint32_t)l / (uint32_t)LANES, i1 = work * (uint32_t)(l + 1) / (uint32_t)LANES;
   if (i1 > i0) {
     const double4 bd = s_bd[lb];
     const double inv_tau = 1.0 / a.tau;
@@ -902,13 +907,12 @@ __global__ __launch_bounds__(kBlock) void k_bins_scale(BinKernelArgs a, double* 
     }
   }
 #pragma unroll
-  for (int f = 0; f < 19; ++f) {  // quarters in fixed order: (q0 + q1) + (q2 + q3)
-    acc[f] += __shfl_xor(acc[f], 1, 64);
-    acc[f] += __shfl_xor(acc[f], 2, 64);
-  }
+  for (int f = 0; f < 19; ++f)  // the lanes' shares in a fixed xor tree: ((s0 + s1) + (s2 + s3)) + ...
+#pragma unroll
+    for (int off = 1; off < LANES; off <<= 1) acc[f] += __shfl_xor(acc[f], off, 64);
   PROF(4);
 #ifdef GCS_PHASE_PROF
-  if (lane == 0 && wid > 0) g_prof[blockIdx.x * 16 + 10 + wid] = wall_clock64();  // waves 1-3 gather end
+  if (lane == 0 && wid > 0 && wid < 4) g_prof[blockIdx.x * 16 + 10 + wid] = wall_clock64();  // waves 1-3 gather end
 #endif
   __syncthreads();  // the record stage is free: it now carries the bin sums [19][kBinTile]
   if (l == 0)
@@ -1380,9 +1384,9 @@ hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream
                              hipEvent_t e2) {
   const int nblk = bins_scale_blocks(a.n_bins);
   if ((long)a.cap * 5 >= (long)a.n_bins * 2)
-    hipExtLaunchKernelGGL(k_bins_scale<kStageBig>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL(k_bins_scale<kStageBig, 4>, dim3(nblk), dim3(kBinTile * 4), 0, s, e0, e1, 0, a, partials);
   else
-    hipExtLaunchKernelGGL(k_bins_scale<kStageSmall>, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL(k_bins_scale<kStageSmall, 4>, dim3(nblk), dim3(kBinTile * 4), 0, s, e0, e1, 0, a, partials);
   GCS_FINAL(kBinNV, 16u, FIN_BINS, nblk, s, e2, partials, a.scalars);
   return hipGetLastError();
 }
