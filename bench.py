@@ -62,7 +62,7 @@ def cpu_baseline(cfg, seconds_target=15.0):
     ms = opipe.MapState.empty(B)
     scans = [synthetic.make_scan(N, k) for k in range(2)]
     n, t_tot = 0, 0.0
-    while n < 2 or (t_tot < seconds_target and n < 6):
+    while n < 2 or (t_tot < seconds_target and n < 16):
         sc = scans[n % 2]
         t0 = time.perf_counter()
         r = opipe.process_scan_bin_path(b, sc, Q, pc, bins, knn, ms)

@@ -807,18 +807,6 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   host::se3_log(pre.delta_pose, xi);
   if (c->cfg.deskew_rotation_only) xi[0] = xi[1] = xi[2] = 0.0;
   cert[10] = pre.ess;
-  // 13 measurement-noise IW statistics over the scan-to-scan IMU window (pipeline.py:448-453,
-  // 522-566); padded samples (stamp <= 0) carry weight 0 (the reference's valid mask)
-  std::vector<double>& wint = c->wint;
-  wint.resize(in->imu_len);
-  for (int i = 0; i < in->imu_len; ++i)
-    wint[i] = in->imu_stamps[i] > 0.0 ? smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, sigma_warp) : 0.0;
-  host::imu_meas_iw_suffstats(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wint.data(), mu_inc + 9,
-                              mu_inc + 12, pose0 + 3, c->cfg.gravity_W, out->iw_meas_dPsi, out->iw_meas_dnu);
-  for (int k = 0; k < 27; ++k)
-    if (!std::isfinite(out->iw_meas_dPsi[k])) return fail(c, GCS_ERR_NONFINITE, "omega_avg / IMU residuals non-finite");
-  memcpy(c->last_meas_dPsi, out->iw_meas_dPsi, sizeof(c->last_meas_dPsi));
-  memcpy(c->last_meas_dnu, out->iw_meas_dnu, sizeof(c->last_meas_dnu));
   auto T1 = clk::now();
   // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
   int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
@@ -827,7 +815,20 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
   if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
   if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+  // 13 measurement-noise IW statistics over the scan-to-scan IMU window (pipeline.py:448-453,
+  // 522-566), computed while the device stages run (they need no device result); padded samples
+  // (stamp <= 0) carry weight 0 (the reference's valid mask)
+  std::vector<double>& wint = c->wint;
+  wint.resize(in->imu_len);
+  for (int i = 0; i < in->imu_len; ++i)
+    wint[i] = in->imu_stamps[i] > 0.0 ? smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, sigma_warp) : 0.0;
+  host::imu_meas_iw_suffstats(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wint.data(), mu_inc + 9,
+                              mu_inc + 12, pose0 + 3, c->cfg.gravity_W, out->iw_meas_dPsi, out->iw_meas_dnu);
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the PT fold has written the scalars to h_scalars
+  for (int k = 0; k < 27; ++k)
+    if (!std::isfinite(out->iw_meas_dPsi[k])) return fail(c, GCS_ERR_NONFINITE, "omega_avg / IMU residuals non-finite");
+  memcpy(c->last_meas_dPsi, out->iw_meas_dPsi, sizeof(c->last_meas_dPsi));
+  memcpy(c->last_meas_dnu, out->iw_meas_dnu, sizeof(c->last_meas_dnu));
   auto T2 = clk::now();
   const double* S = c->h_scalars;
   // budget cert (point_budget.py:182-212)
@@ -1094,17 +1095,17 @@ int gcs_hypothesis_combine(gcs_ctx* c, const double* p, int32_t scan_count, gcs_
 
 // ---------------------------------------------------------------- host numerics
 int gcs_psd_project(int32_t n, const double* M, double eps, double* out, double* cert6) {
-  if (n < 1 || n > 64 || !M || !out) return GCS_ERR_ARG;
+  if (n < 1 || n > host::kMaxN || !M || !out) return GCS_ERR_ARG;
   host::psd_project(n, M, eps, out, cert6);
   return GCS_OK;
 }
 int gcs_spd_solve_lifted(int32_t n, const double* L, const double* b, double eps, double* x) {
-  if (n < 1 || n > 64 || !L || !b || !x) return GCS_ERR_ARG;
+  if (n < 1 || n > host::kMaxN || !L || !b || !x) return GCS_ERR_ARG;
   host::spd_solve_lifted(n, L, b, eps, x);
   return GCS_OK;
 }
 int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps, double* Li) {
-  if (n < 1 || n > 64 || !L || !Li) return GCS_ERR_ARG;
+  if (n < 1 || n > host::kMaxN || !L || !Li) return GCS_ERR_ARG;
   host::spd_inverse_lifted(n, L, eps, Li);
   return GCS_OK;
 }

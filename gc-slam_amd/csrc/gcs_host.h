@@ -20,7 +20,9 @@ void spd_inverse_lifted(int n, const double* L, double eps_lift, double* Linv);
 
 // One Cholesky factor of L + eps_lift I (spd_cholesky_*_lifted_core, primitives.py:141-192),
 // reused by every solve / inverse of the same matrix in a scan.
-constexpr int kMaxN = 64;
+// Largest matrix order of the host numerics (the 22-D state; public entry points reject larger n);
+// it sizes the stack working arrays.
+constexpr int kMaxN = 24;
 struct SpdFactor {
   int n = 0;
   double Lc[kMaxN * kMaxN];

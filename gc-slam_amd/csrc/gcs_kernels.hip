@@ -665,7 +665,16 @@ constexpr int kBinNV = 16;
 constexpr int kMaxSrc = 320;   // atlas tables for B = 1k .. 1M have at most 199 per 64-bin tile
 constexpr int kMaxRl = 1280;   // reverse-kNN entries of one tile (~K x kBinTile; at most 1070)
 constexpr int kStageBig = 512, kStageSmall = 256;
-constexpr int kRecD = 8;  // staged record: x y z dx dy dz m w/Z
+// staged record: x y z dx dy dz m w/Z as four double2 chunks (+ GCS_REC_PAD doubles of stride
+// padding); GCS_REC_SWZ stores chunk c of record r at slot c ^ ((r >> 2) & 3) (LDS bank spread)
+#ifndef GCS_REC_PAD
+#define GCS_REC_PAD 0
+#endif
+#ifndef GCS_REC_SWZ
+#define GCS_REC_SWZ 1  // A/B at C2: 33.0 -> 31.0 us; C3 unchanged (LDS conflicts are ~1/3 of LDS cycles)
+#endif
+constexpr int kRecD = 8 + GCS_REC_PAD;
+__device__ __forceinline__ uint32_t rec_swz(uint32_t r) { return GCS_REC_SWZ ? ((r >> 2) & 3u) : 0u; }
 static_assert(kStageSmall * kRecD >= 19 * kBinTile, "phase D reuses the record stage for the bin sums");
 int bins_tile() { return kBinTile; }
 int bins_max_tile_sources() { return kMaxSrc; }
@@ -835,9 +844,12 @@ __global__ __launch_bounds__(kBinTile * LANES) void k_bins_scale(BinKernelArgs a
         if (s_off[mid] <= r) lo = mid; else hi = mid - 1;
       }
       const PointRec pr = a.recs[a.perm[s_st[lo] + (r - s_off[lo])]];
-      double* d = s_rec + (size_t)r * kRecD;
-      d[0] = pr.x; d[1] = pr.y; d[2] = pr.z; d[3] = pr.dx; d[4] = pr.dy; d[5] = pr.dz;
-      d[6] = pr.m; d[7] = pr.w * pr.iz;
+      double2* d = (double2*)(s_rec + (size_t)r * kRecD);
+      const uint32_t sw = rec_swz(r);
+      d[0 ^ sw] = make_double2(pr.x, pr.y);
+      d[1 ^ sw] = make_double2(pr.z, pr.dx);
+      d[2 ^ sw] = make_double2(pr.dy, pr.dz);
+      d[3 ^ sw] = make_double2(pr.m, pr.w * pr.iz);
     }
   }
   __syncthreads();
@@ -872,7 +884,8 @@ __global__ __launch_bounds__(kBinTile * LANES) void k_bins_scale(BinKernelArgs a
       // current one is accumulated
       uint32_t r = s_off[j] + kk, left = c - kk;
       const double2* rp = (const double2*)(s_rec + (size_t)r * kRecD);
-      double2 x0 = rp[0], x1 = rp[1], x2 = rp[2], x3 = rp[3];
+      uint32_t sw = rec_swz(r);
+      double2 x0 = rp[0 ^ sw], x1 = rp[1 ^ sw], x2 = rp[2 ^ sw], x3 = rp[3 ^ sw];
       for (uint32_t i = i0; i < i1; ++i) {
         const double2 c0 = x0, c1 = x1, c2 = x2, c3 = x3;
         if (i + 1 < i1) {
@@ -887,7 +900,8 @@ __global__ __launch_bounds__(kBinTile * LANES) void k_bins_scale(BinKernelArgs a
             ++r;
           }
           const double2* np = (const double2*)(s_rec + (size_t)r * kRecD);
-          x0 = np[0]; x1 = np[1]; x2 = np[2]; x3 = np[3];
+          sw = rec_swz(r);
+          x0 = np[0 ^ sw]; x1 = np[1 ^ sw]; x2 = np[2 ^ sw]; x3 = np[3 ^ sw];
         }
         bin_contrib(acc, bd, inv_tau, c0.x, c0.y, c1.x, c1.y, c2.x, c2.y, c3.x, c3.y);
       }

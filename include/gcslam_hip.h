@@ -176,6 +176,7 @@ int gcs_planar_translation(gcs_ctx* ctx, const double* R_hat9, double* pt_host);
 int gcs_pushforward(gcs_ctx* ctx, const double* z_t6, const double* Sigma_pose36, double gamma);
 
 /* ---------------------------------------------------------------- host-side numerics (no GPU) */
+/* matrix orders n <= 24 (the 22-D state and its blocks); larger n returns GCS_ERR_ARG */
 int gcs_psd_project(int32_t n, const double* M, double eps_psd, double* M_psd, double* cert6);
 int gcs_spd_solve_lifted(int32_t n, const double* L, const double* b, double eps_lift, double* x);
 int gcs_spd_inverse_lifted(int32_t n, const double* L, double eps_lift, double* Linv);

@@ -58,7 +58,8 @@ def main():
             print("  phases (A loads, rank+scan, stage, gather, finalize, reduce+store) mean",
                   np.round(d.mean(0), 2), "p90", np.round(np.percentile(d, 90, axis=0), 2))
             print(f"  staged records mean {g[m, 8].mean():.0f} p90 {np.percentile(g[m, 8], 90):.0f} max {g[m, 8].max()}"
-                  f"; bin work max mean {g[m, 9].mean():.0f} max {g[m, 9].max()}; tile work mean {g[m, 10].mean():.0f}")
+                  f"; bin work max mean {g[m, 9].mean():.0f} max {g[m, 9].max()}; tile work mean {g[m, 10].mean():.0f}"
+                  f" p90 {np.percentile(g[m, 10], 90):.0f} p99 {np.percentile(g[m, 10], 99):.0f} max {g[m, 10].max()}")
             ge = us(g[m][:, 11:14].max(1) - g[m][:, 4])
             print(f"  gather end, slowest of waves 1-3 minus wave 0: mean {ge.mean():.2f} p90 {np.percentile(ge, 90):.2f}")
             dd = us(np.diff(g[m][:, [4, 14, 15, 5]], axis=1))
