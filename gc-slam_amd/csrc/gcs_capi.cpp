@@ -56,7 +56,11 @@ struct gcs_ctx {
   uint32_t *d_counts = nullptr, *d_starts = nullptr, *d_perm = nullptr;
   int n_counts_words = 0;
   uint32_t* d_tickets = nullptr;
+  // active-bin flags, double-buffered by scan: the next scan's k_budget clears one buffer while the
+  // previous scan's k_pushforward (on push_stream) still reads the other
   uint8_t* d_flags = nullptr;
+  uint8_t* d_flags_buf[2] = {nullptr, nullptr};
+  int flags_cur = 0;
   uint8_t* d_touched = nullptr;     // per bin: the map holds mass (k_map_derive / k_pushforward)
   uint8_t* d_tile_dirty = nullptr;  // k_bins_scale: tile output not the zero-bin values (persistent)
   double* d_bins_part = nullptr;    // k_bins_scale partial rows (persistent: clean tiles keep theirs)
@@ -68,6 +72,12 @@ struct gcs_ctx {
   double* d_partials = nullptr;
   size_t partials_len = 0;
   double* d_part_pts = nullptr;  // k_points block partials (folded later in the scale-mode scan)
+  double* d_part_push = nullptr; // k_pushforward block partials (its fold runs on push_stream)
+  // gcs_scan launches k_pushforward on its own stream, so it overlaps the next scan's point and
+  // bucketing kernels; the main stream waits for ev_push before the next bin kernel (join)
+  hipStream_t push_stream = nullptr;
+  hipEvent_t ev_push = nullptr;
+  bool push_pending = false;
   int pts_blocks = 0;
   bool pts_fold_pending = false;
   double* d_scalars = nullptr;
@@ -96,6 +106,13 @@ namespace {
 int fail(gcs_ctx* c, int code, const std::string& m) {
   if (c) c->err = m;
   return code;
+}
+
+// order the main stream after an in-flight scan pushforward (map, derived, touched, map totals)
+void join_push(gcs_ctx* c) {
+  if (!c->push_pending) return;
+  (void)hipStreamWaitEvent(c->stream, c->ev_push, 0);
+  c->push_pending = false;
 }
 
 #define HIPCHK(ctx, expr)                                                                         \
@@ -238,6 +255,10 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   c->last_stride = stride;
   hipStream_t s = c->stream;
   harvest(c);
+  if (c->d_flags_buf[0]) {  // this scan's flag buffer (the other may still be read by k_pushforward)
+    c->flags_cur ^= 1;
+    c->d_flags = c->d_flags_buf[c->flags_cur];
+  }
   StageEv ev = stage_ev(c, ST_POINTS);
   BudgetArgs ba{};
   ba.w = w;
@@ -369,7 +390,7 @@ int stage_pt(gcs_ctx* c, bool to_host = false) {
   return GCS_OK;
 }
 
-int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) {
+int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, hipStream_t s, double* partials) {
   PushArgs pa{};
   so3_exp(z_t + 3, pa.R);
   pa.t[0] = z_t[0];
@@ -388,8 +409,12 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) 
     for (int j = 0; j < 3; ++j) pa.G[3 * i + j] = RS[3 * i] * pa.R[3 * j] + RS[3 * i + 1] * pa.R[3 * j + 1] + RS[3 * i + 2] * pa.R[3 * j + 2];
   pa.gamma = gamma;
   StageEv ev = stage_ev(c, ST_PUSH);
-  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, c->d_partials, c->d_scalars, c->d_flags,
-                               c->d_touched, c->stream, ev.e0, ev.e1));
+  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, partials, c->d_scalars, c->d_flags,
+                               c->d_touched, s, ev.e0, ev.e1));
+  if (s != c->stream) {
+    HIPCHK(c, hipEventRecord(c->ev_push, s));
+    c->push_pending = true;
+  }
   return GCS_OK;
 }
 
@@ -433,6 +458,8 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipSetDevice(cfg->device))) return GCS_ERR_HIP;
   if (bad(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
   c->own_stream = true;
+  if (bad(hipStreamCreateWithFlags(&c->push_stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
+  if (bad(hipEventCreateWithFlags(&c->ev_push, hipEventDisableTiming))) return GCS_ERR_HIP;
   const size_t B = c->B, cap = c->cap;
   if (bad(hipMalloc(&c->d_bin_dirs, B * 4 * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_recs, cap * sizeof(PointRec)))) return GCS_ERR_HIP;
@@ -447,6 +474,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
                                       partials_need(push_blocks(c->B), 10)});
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_part_pts, partials_need(kRedBlocks, 5) * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_part_push, partials_need(push_blocks(c->B), 10) * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_tickets, sizeof(uint32_t)))) return GCS_ERR_HIP;
@@ -466,8 +494,11 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMalloc(&c->d_starts, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_perm, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     // bin flags, then one flag per k_bins_scale tile (both cleared by k_budget every scan)
-    if (bad(hipMalloc(&c->d_flags, B + bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
-    if (bad(hipMemset(c->d_flags, 0, B + bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
+    const size_t nflags = B + bins_scale_blocks(c->B);
+    if (bad(hipMalloc(&c->d_flags_buf[0], 2 * nflags))) return GCS_ERR_HIP;
+    if (bad(hipMemset(c->d_flags_buf[0], 0, 2 * nflags))) return GCS_ERR_HIP;
+    c->d_flags_buf[1] = c->d_flags_buf[0] + nflags;
+    c->d_flags = c->d_flags_buf[0];
     // every tile starts dirty: the first scan writes all ScanBinStats rows and partial rows
     if (bad(hipMalloc(&c->d_tile_dirty, bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
     if (bad(hipMemset(c->d_tile_dirty, 1, bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
@@ -499,10 +530,12 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
 
 int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
+  if (c->push_stream) (void)hipStreamSynchronize(c->push_stream);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
-                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags, c->d_touched,
+                  c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_bins_part, c->d_tickets,
-                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts,
+                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -510,6 +543,8 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   for (int st = 0; st < kStages; ++st)
     for (int k = 0; k < 2; ++k)
       if (c->ev[st][k]) (void)hipEventDestroy(c->ev[st][k]);
+  if (c->ev_push) (void)hipEventDestroy(c->ev_push);
+  if (c->push_stream) (void)hipStreamDestroy(c->push_stream);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return GCS_OK;
@@ -517,6 +552,8 @@ int gcs_ctx_destroy(gcs_ctx* c) {
 
 int gcs_ctx_set_stream(gcs_ctx* c, void* s) {
   if (!c) return GCS_ERR_ARG;
+  HIPCHK(c, hipStreamSynchronize(c->push_stream));
+  c->push_pending = false;
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   c->stream = (hipStream_t)s;
   c->own_stream = false;
@@ -525,6 +562,7 @@ int gcs_ctx_set_stream(gcs_ctx* c, void* s) {
 
 int gcs_ctx_synchronize(gcs_ctx* c) {
   if (!c) return GCS_ERR_ARG;
+  join_push(c);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
 }
@@ -551,6 +589,8 @@ int gcs_ctx_stage_times(gcs_ctx* c, double* ms_sum, int64_t* counts, int32_t res
 
 int gcs_ctx_set_atlas(gcs_ctx* c, const double* dirs) {
   if (!c || !dirs) return GCS_ERR_ARG;
+  join_push(c);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   c->dirs_host.assign(dirs, dirs + (size_t)c->B * 3);
   return upload_atlas(c);
 }
@@ -576,6 +616,8 @@ int gcs_ctx_get_belief(gcs_ctx* c, gcs_belief* b) {
 
 int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
   if (!c || !map) return GCS_ERR_ARG;
+  join_push(c);
+  HIPCHK(c, hipStreamSynchronize(c->stream));
   std::vector<double> dev((size_t)c->B * MF_COUNT);
   to_device_order(c, MF_COUNT, map, dev.data());
   HIPCHK(c, hipMemcpy(c->d_map, dev.data(), dev.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -586,6 +628,7 @@ int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
 }
 
 int pull_rows(gcs_ctx* c, const double* dev_src, int F, double* ref_out) {
+  join_push(c);
   std::vector<double> dev((size_t)c->B * F);
   HIPCHK(c, hipMemcpyAsync(dev.data(), dev_src, dev.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -615,6 +658,8 @@ int gcs_ctx_get_bin_order(gcs_ctx* c, int32_t* order) {
 
 int gcs_ctx_device_arrays(gcs_ctx* c, double** scan, double** map, double** derived) {
   if (!c) return GCS_ERR_ARG;
+  join_push(c);
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the arrays are final when the pointers are handed out
   if (scan) *scan = c->d_scan;
   if (map) *map = c->d_map;
   if (derived) *derived = c->d_derived;
@@ -664,6 +709,7 @@ int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const doubl
                     double t0, double t1, const double* xi, double* p0_dev, double* w_out_dev, double* w_budget_dev,
                     int32_t* nearest_dev, double* cert) {
   if (!c || !xi) return GCS_ERR_ARG;
+  join_push(c);
   int rc = stage_points(c, xyz, point_step, t, w, n, t0, t1, xi, p0_dev, w_out_dev, w_budget_dev);
   if (rc) return rc;
   if (nearest_dev) {  // reported in reference bin ids
@@ -706,6 +752,7 @@ __global__ void k_materialize(const PointRec* recs, const int* nearest, const in
 
 int gcs_bin_soft_assign(gcs_ctx* c, int32_t* ids, double* r) {
   if (!c) return GCS_ERR_ARG;
+  join_push(c);
   bool scale = c->cfg.mode == GCS_MODE_SCALE;
   hipLaunchKernelGGL(k_materialize, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, (const PointRec*)c->d_recs,
                      (const int*)c->d_nearest, (const int*)c->d_knn, (const double*)c->d_bin_dirs,
@@ -718,6 +765,7 @@ int gcs_bin_soft_assign(gcs_ctx* c, int32_t* ids, double* r) {
 
 int gcs_scan_bin_moment_match(gcs_ctx* c, double* cert) {
   if (!c) return GCS_ERR_ARG;
+  join_push(c);
   int rc = stage_bins(c);
   if (rc) return rc;
   if ((rc = pull_scalars(c))) return rc;
@@ -728,6 +776,7 @@ int gcs_scan_bin_moment_match(gcs_ctx* c, double* cert) {
 
 int gcs_matrix_fisher_rotation(gcs_ctx* c, double* mf) {
   if (!c) return GCS_ERR_ARG;
+  join_push(c);
   int rc = stage_mf(c);
   if (rc) return rc;
   if ((rc = pull_scalars(c))) return rc;
@@ -749,6 +798,7 @@ int gcs_matrix_fisher_rotation(gcs_ctx* c, double* mf) {
 
 int gcs_planar_translation(gcs_ctx* c, const double* R_hat, double* pt) {
   if (!c || !R_hat) return GCS_ERR_ARG;
+  join_push(c);
   HIPCHK(c, hipMemcpyAsync(c->d_scalars + SC_MF_R, R_hat, 9 * sizeof(double), hipMemcpyHostToDevice, c->stream));
   int rc = stage_pt(c);
   if (rc) return rc;
@@ -763,7 +813,8 @@ int gcs_planar_translation(gcs_ctx* c, const double* R_hat, double* pt) {
 
 int gcs_pushforward(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) {
   if (!c || !z_t || !Sig6) return GCS_ERR_ARG;
-  int rc = stage_push(c, z_t, Sig6, gamma);
+  join_push(c);
+  int rc = stage_push(c, z_t, Sig6, gamma, c->stream, c->d_partials);
   if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
@@ -812,6 +863,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
                         in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, /*fold_later=*/true);
   if (rc) return rc;
+  join_push(c);  // the bin kernel reads the map the previous scan's pushforward wrote
   if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
   if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
   if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
@@ -1003,7 +1055,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   host::world_pose_from_increment(rec, mu_rec, z_t);
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j < 6; ++j) Sig6[6 * i + j] = covr[i * DZ + j];
-  if ((rc = stage_push(c, z_t, Sig6, c->cfg.forgetting_factor))) return rc;
+  if ((rc = stage_push(c, z_t, Sig6, c->cfg.forgetting_factor, c->push_stream, c->d_part_push))) return rc;
   memcpy(out->z_t, z_t, sizeof(out->z_t));
   // 14 AnchorDriftUpdate (anchor_drift.py:93-191)
   const double* dz2 = mu_rec;  // mean_increment(rec)

@@ -1313,7 +1313,7 @@ __global__ __launch_bounds__(kBlock) void k_final(const double* __restrict__ par
 // One block reads ~10 B/clk from HBM, so a single-block fold of the 8192 rows (1 MiB) of the
 // bin kernel at C3 took 30 us; with a first level on 128 CUs the one-block tail folds 128 rows.
 constexpr int kFoldRows = 64;
-constexpr int kFoldDirect = 1024;  // up to this many rows a single block folds directly
+constexpr int kFoldDirect = 2048;  // up to this many rows a single block folds directly (C2 bins: 1563)
 template <int NV, unsigned MAXMASK>
 __global__ __launch_bounds__(kBlock) void k_fold(const double* __restrict__ partials, int nblocks, double* out) {
   __shared__ double lds[kWaves * pstride<NV>()];
