@@ -205,45 +205,41 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
   __shared__ double lds[kWaves * 5];
   __shared__ double s_mass[2];
   // budget mass sums: every block folds k_budget's partial rows itself (same fixed order in every
-  // block), so no separate fold launch sits between the two kernels; block 0 publishes them
-  {
-    double v[2] = {0.0, 0.0};
-    for (int r = threadIdx.x; r < a.budget_blocks; r += kBlock) {
-      v[0] += a.budget_partials[(size_t)r * pstride<2>()];
-      v[1] += a.budget_partials[(size_t)r * pstride<2>() + 1];
-    }
-    block_sum<2>(v, lds);
-    if (threadIdx.x == 0) {
-      s_mass[0] = v[0];
-      s_mass[1] = v[0] / (v[1] + kEpsMass);  // mass_scale, point_budget.py:80-84
-      if (blockIdx.x == 0) {
-        a.scalars[SC_MASS_IN] = v[0];
-        a.scalars[SC_MASS_SEL] = v[1];
-        a.scalars[SC_MASS_SCALE] = s_mass[1];
-      }
-    }
-    __syncthreads();
+  // block), so no separate fold launch sits between the two kernels; block 0 publishes them.  The
+  // rows are loaded here and folded after the first point's geometry (which needs no weight), so
+  // their latency and the fold's barriers overlap the point's dependent chain.
+  static_assert(kBlock * 4 >= 1024, "k_budget launches at most 1024 blocks: four rows per thread");
+  double2 brow[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = threadIdx.x + k * kBlock;
+    brow[k] = r < a.budget_blocks ? *(const double2*)(a.budget_partials + (size_t)r * pstride<2>())
+                                  : make_double2(0.0, 0.0);
   }
-  const double mass_scale = s_mass[1];
-  const double mass_in = s_mass[0];
   const double denom = a.t1 - a.t0 > 1e-12 ? a.t1 - a.t0 : 1e-12;
   const double inv_tau = 1.0 / a.tau;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sum w_budget, sum wn^2, sum w_out, sum H
   double rmax = -INFINITY;
-  for (int i = blockIdx.x * kBlock + threadIdx.x; i < a.cap; i += gridDim.x * kBlock) {
-    double p[3] = {0.0, 0.0, 0.0}, t = 0.0, wb = 0.0;
-    bool valid = i < a.n_sel;
+  double mass_scale = 0.0, mass_in = 0.0;
+  // uniform trip count (the budget fold inside the first iteration has barriers)
+  const int gstride = gridDim.x * kBlock;
+  const int niter = (a.cap + gstride - 1) / gstride;
+  for (int it = 0; it < niter; ++it) {
+    const int i = blockIdx.x * kBlock + threadIdx.x + it * gstride;
+    const bool live = i < a.cap;
+    double p[3] = {0.0, 0.0, 0.0}, t = 0.0, w_raw = 0.0;
+    bool valid = live && i < a.n_sel;
     if (valid) {
       size_t src = (size_t)i * (size_t)a.stride;
       const float* rec = (const float*)(a.xyz + src * (size_t)a.point_step);
       p[0] = (double)rec[0]; p[1] = (double)rec[1]; p[2] = (double)rec[2];
       t = a.timestamps[src];
-      wb = a.weights[src] * mass_scale;
+      w_raw = a.weights[src];
     }
     double alpha = (t - a.t0) / denom;
     double p0[3];
     deskew_point(alpha, a.xi, p, p0);
-    double wout = wb * smooth_window(t, a.t0, a.t1, kTimeWarpSigmaFrac * denom);
+    const double win = smooth_window(t, a.t0, a.t1, kTimeWarpSigmaFrac * denom);
     double d[3];
     ray_dir(p0[0], p0[1], p0[2], a.origin, d);
     double m = -INFINITY, Z = 0.0, H = 0.0, rm = 0.0;
@@ -315,7 +311,7 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
         a.slots[i] = atomicAdd(a.counts + nearest, 1u);
         key = (uint32_t)nearest;
       }
-      a.keys[i] = key;
+      if (live) a.keys[i] = key;
       Z = iz;
     } else {
       for (int b = 0; b < a.n_bins; ++b) {
@@ -335,6 +331,30 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
       }
       Z = iz;
     }
+    if (it == 0) {  // block-uniform: the budget fold
+      double v[2] = {0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[0] += brow[k].x;
+        v[1] += brow[k].y;
+      }
+      block_sum<2>(v, lds);
+      if (threadIdx.x == 0) {
+        s_mass[0] = v[0];
+        s_mass[1] = v[0] / (v[1] + kEpsMass);  // mass_scale, point_budget.py:80-84
+        if (blockIdx.x == 0) {
+          a.scalars[SC_MASS_IN] = v[0];
+          a.scalars[SC_MASS_SEL] = v[1];
+          a.scalars[SC_MASS_SCALE] = s_mass[1];
+        }
+      }
+      __syncthreads();
+      mass_scale = s_mass[1];
+      mass_in = s_mass[0];
+    }
+    if (!live) continue;
+    const double wb = w_raw * mass_scale;
+    const double wout = wb * win;
     PointRec pr;
     pr.x = p0[0]; pr.y = p0[1]; pr.z = p0[2];
     pr.dx = d[0]; pr.dy = d[1]; pr.dz = d[2];

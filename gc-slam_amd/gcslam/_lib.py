@@ -36,11 +36,12 @@ class GcsConfig(C.Structure):
 
 
 class GcsScanInputs(C.Structure):
+    # host arrays as plain addresses (arr.ctypes.data): a typed-pointer conversion costs ~2 us each
     _fields_ = [("xyz_dev", C.c_void_p), ("point_step", C.c_int32), ("timestamps_dev", C.c_void_p),
-                ("weights_dev", C.c_void_p), ("n_points", C.c_int32), ("imu_stamps", c_double_p),
-                ("imu_gyro", c_double_p), ("imu_accel", c_double_p), ("imu_len", C.c_int32),
+                ("weights_dev", C.c_void_p), ("n_points", C.c_int32), ("imu_stamps", C.c_void_p),
+                ("imu_gyro", C.c_void_p), ("imu_accel", C.c_void_p), ("imu_len", C.c_int32),
                 ("scan_start_time", C.c_double), ("scan_end_time", C.c_double), ("dt_sec", C.c_double),
-                ("Q", c_double_p), ("L_ext", c_double_p), ("h_ext", c_double_p),
+                ("Q", C.c_void_p), ("L_ext", C.c_void_p), ("h_ext", C.c_void_p),
                 ("t_last_scan", C.c_double), ("t_scan", C.c_double)]
 
 
@@ -107,8 +108,8 @@ _SIGS = [
     ("gcs_fibonacci_atlas", C.c_int, [C.c_int32, c_double_p]),
     ("gcs_knn_table", C.c_int, [C.c_int32, c_double_p, C.c_int32, c_int32_p]),
     ("gcs_nearest_bins", C.c_int, [C.c_int32, c_double_p, C.c_int32, c_double_p, c_int32_p]),
-    ("gcs_hypothesis_payload", C.c_int, [C.c_void_p, C.c_double, C.c_double, c_double_p]),
-    ("gcs_hypothesis_combine", C.c_int, [C.c_void_p, c_double_p, C.c_int32, C.POINTER(GcsBelief), c_double_p]),
+    ("gcs_hypothesis_payload", C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_void_p]),
+    ("gcs_hypothesis_combine", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]

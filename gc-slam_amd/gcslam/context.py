@@ -225,9 +225,9 @@ class HypothesisContext:
         inp.timestamps_dev = t_dev.data_ptr()
         inp.weights_dev = w_dev.data_ptr()
         inp.n_points = int(n_points)
-        inp.imu_stamps = L.dptr(imu_stamps)
-        inp.imu_gyro = L.dptr(imu_gyro)
-        inp.imu_accel = L.dptr(imu_accel)
+        inp.imu_stamps = imu_stamps.ctypes.data
+        inp.imu_gyro = imu_gyro.ctypes.data
+        inp.imu_accel = imu_accel.ctypes.data
         inp.imu_len = int(imu_stamps.shape[0])
         inp.scan_start_time = float(scan_start_time)
         inp.scan_end_time = float(scan_end_time)
@@ -239,7 +239,7 @@ class HypothesisContext:
             if arr is not None:
                 a = np.ascontiguousarray(arr, np.float64).reshape(-1)
                 keep.append(a)
-                setattr(inp, name, L.dptr(a))
+                setattr(inp, name, a.ctypes.data)
         out = L.GcsScanOutputs()
         self._chk(self.lib.gcs_scan(self.h, C.byref(inp), C.byref(out)), "gcs_scan")
         return out
@@ -248,7 +248,7 @@ class HypothesisContext:
     def hypothesis_payload(self, w_iw, w_bary):
         """Packed 840-f64 all-reduce payload of this hypothesis (a fresh array per call)."""
         p = np.empty(L.PAYLOAD_LEN)
-        self._chk(self.lib.gcs_hypothesis_payload(self.h, float(w_iw), float(w_bary), L.dptr(p)), "payload")
+        self._chk(self.lib.gcs_hypothesis_payload(self.h, float(w_iw), float(w_bary), p.ctypes.data), "payload")
         return p
 
     def hypothesis_combine(self, payload_sum, scan_count, want_belief=True):
@@ -256,6 +256,6 @@ class HypothesisContext:
         p = np.ascontiguousarray(payload_sum, np.float64)
         b = L.GcsBelief()
         cert = np.empty(4)
-        self._chk(self.lib.gcs_hypothesis_combine(self.h, L.dptr(p), int(scan_count), C.byref(b), L.dptr(cert)),
+        self._chk(self.lib.gcs_hypothesis_combine(self.h, p.ctypes.data, int(scan_count), C.addressof(b), cert.ctypes.data),
                   "combine")
         return (L.struct_to_arrays(b) if want_belief else None), cert
