@@ -73,6 +73,7 @@ struct gcs_ctx {
   size_t partials_len = 0;
   double* d_part_pts = nullptr;  // k_points block partials (folded later in the scale-mode scan)
   double* d_part_push = nullptr; // k_pushforward block partials (its fold runs on push_stream)
+  uint32_t* d_parse_flag = nullptr;  // PointCloud2 parse: some per-point time > 1e6 (ns)
   // gcs_scan launches k_pushforward on its own stream, so it overlaps the next scan's point and
   // bucketing kernels; the main stream waits for ev_push before the next bin kernel (join)
   hipStream_t push_stream = nullptr;
@@ -246,9 +247,10 @@ int upload_atlas(gcs_ctx* c) {
 // ---------------------------------------------------------------- device stages
 // fold_later: leave k_points' cert fold to block 0 of the next k_bins_scale (scale-mode scan)
 int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, const double* w, int n_raw, double t0,
-                 double t1, const double* xi, double* p0_out, double* w_out, double* wb_out, bool fold_later = false) {
+                 double t1, const double* xi, double* p0_out, double* w_out, double* wb_out, bool fold_later = false,
+                 bool xyz_f64 = false) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
-  if (point_step < 12) return fail(c, GCS_ERR_ARG, "point_step must be >= 12 bytes");
+  if (point_step < (xyz_f64 ? 24 : 12)) return fail(c, GCS_ERR_ARG, "point_step too small for x, y, z");
   int stride = std::max(1, (int)((n_raw + (long)c->cap - 1) / c->cap));  // ceil(N/cap), point_budget.py:160
   int n_sel = (n_raw + stride - 1) / stride;
   c->last_n_sel = n_sel;
@@ -275,6 +277,7 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   PointKernelArgs a{};
   a.xyz = (const uint8_t*)xyz;
   a.point_step = point_step;
+  a.xyz_f64 = xyz_f64 ? 1 : 0;
   a.timestamps = t;
   a.weights = w;
   a.n_raw = n_raw;
@@ -478,6 +481,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_tickets, sizeof(uint32_t)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_parse_flag, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_tickets, 0, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocMapped))) return GCS_ERR_HIP;
   if (bad(hipHostGetDevicePointer((void**)&c->d_scalars_mirror, c->h_scalars, 0))) return GCS_ERR_HIP;
@@ -535,7 +539,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_bins_part, c->d_tickets,
-                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push,
+                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -705,6 +709,35 @@ __global__ void k_ref_ids(const int* dev_ids, const int* bin_ref, int n, int* ou
 }
 }  // namespace
 
+int gcs_parse_pointcloud2(gcs_ctx* c, const void* data_dev, const gcs_pointcloud2_layout* L, double* points_dev,
+                          double* t_dev, double* w_dev, uint8_t* ring_dev) {
+  if (!c || !L || (L->n_points > 0 && (!data_dev || !points_dev || !t_dev || !w_dev))) return GCS_ERR_ARG;
+  if (L->n_points < 0 || L->point_step < 1) return GCS_ERR_ARG;
+  auto fits = [&](int off, int bytes) { return off >= 0 && off + bytes <= L->point_step; };
+  auto width = [](int dt) { return dt <= 2 ? 1 : dt <= 4 ? 2 : dt <= 7 ? 4 : 8; };
+  if (!fits(L->off_x, 4) || !fits(L->off_y, 4) || !fits(L->off_z, 4))
+    return fail(c, GCS_ERR_ARG, "PointCloud2 x/y/z FLOAT32 fields outside point_step");
+  if (L->ring_datatype < 1 || L->ring_datatype > 8 || !fits(L->off_ring, width(L->ring_datatype)))
+    return fail(c, GCS_ERR_ARG, "PointCloud2 (VLP-16 layout) ring field missing or outside point_step");
+  if (L->off_t >= 0 && (L->t_datatype < 1 || L->t_datatype > 8 || !fits(L->off_t, width(L->t_datatype))))
+    return fail(c, GCS_ERR_ARG, "PointCloud2 time field outside point_step");
+  join_push(c);
+  ParseArgs a{};
+  a.data = (const uint8_t*)data_dev;
+  a.n = L->n_points;
+  a.point_step = L->point_step;
+  a.off_x = L->off_x; a.off_y = L->off_y; a.off_z = L->off_z;
+  a.off_ring = L->off_ring; a.ring_datatype = L->ring_datatype;
+  a.off_t = L->off_t; a.t_datatype = L->t_datatype;
+  a.header_stamp = L->header_stamp_sec;
+  memcpy(a.R, L->R_base_lidar, sizeof(a.R));
+  memcpy(a.tb, L->t_base_lidar, sizeof(a.tb));
+  a.points = points_dev; a.t = t_dev; a.w = w_dev; a.ring = ring_dev;
+  a.ns_flag = c->d_parse_flag;
+  HIPCHK(c, launch_parse(a, c->stream));
+  return GCS_OK;
+}
+
 int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const double* t, const double* w, int32_t n,
                     double t0, double t1, const double* xi, double* p0_dev, double* w_out_dev, double* w_budget_dev,
                     int32_t* nearest_dev, double* cert) {
@@ -861,7 +894,8 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   auto T1 = clk::now();
   // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
   int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
-                        in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, /*fold_later=*/true);
+                        in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, /*fold_later=*/true,
+                        in->xyz_format == 1);
   if (rc) return rc;
   join_push(c);  // the bin kernel reads the map the previous scan's pushforward wrote
   if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in

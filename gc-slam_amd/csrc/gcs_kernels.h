@@ -10,6 +10,19 @@ namespace gcs {
 
 // k_scan draws its tile numbers from a self re-arming ticket (device word, zeroed at creation)
 
+struct ParseArgs {
+  const uint8_t* data;  // raw PointCloud2 bytes (device)
+  int n, point_step;
+  int off_x, off_y, off_z, off_ring, ring_datatype, off_t, t_datatype;
+  double header_stamp;
+  double R[9], tb[3];   // R_base_lidar, t_base_lidar
+  double* points;       // n x 3 base frame
+  double* t;
+  double* w;
+  uint8_t* ring;        // may be null
+  uint32_t* ns_flag;
+};
+
 struct BudgetArgs {
   const double* w;
   int n_raw, stride;
@@ -23,8 +36,9 @@ struct BudgetArgs {
 
 struct PointKernelArgs {
   // raw PointCloud2-like input (device)
-  const uint8_t* xyz;  // float x,y,z at byte offsets 0,4,8 of each record
+  const uint8_t* xyz;  // float x,y,z at byte offsets 0,4,8 of each record (double when xyz_f64)
   int point_step;      // bytes per record
+  int xyz_f64;
   const double* timestamps;
   const double* weights;
   int n_raw, n_sel, stride, cap;
@@ -105,6 +119,7 @@ struct PushArgs {
 
 // Launchers.  e0/e1 (may be null) are stamped with the first kernel's start and the last
 // kernel's end through hipExtLaunchKernel, so stage timing adds no marker packets to the queue.
+hipError_t launch_parse(const ParseArgs& a, hipStream_t s);
 hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 // fold: run k_points' cert fold now (else k_bins_scale block 0 folds it, BinKernelArgs.pts_partials)
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,

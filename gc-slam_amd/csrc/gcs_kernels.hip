@@ -151,6 +151,60 @@ __device__ __forceinline__ void store_partials(const double (&v)[NV], double* ba
     for (int k = 0; k < NV; ++k) base[(size_t)idx * pstride<NV>() + k] = v[k];
 }
 
+// ---------------------------------------------------------------- PointCloud2 parse (before row 1)
+// parse_pointcloud2_vlp16 (backend_node.py:377-468) + the base transform (:1677-1680), one thread
+// per point over the raw message bytes: x/y/z FLOAT32 with the non-finite sentinel (nan_to_num),
+// ring, per-point time (seconds, or ns when any value exceeds 1e6: an integer flag word reduced
+// with atomicOr, applied by k_parse_time_scale), range-sigmoid weights on the lidar-frame range,
+// points in the base frame (f64, 3 per point).  numpy's operation order, no contraction.
+__device__ __forceinline__ double pc2_field(const uint8_t* p, int datatype) {
+  switch (datatype) {  // sensor_msgs/PointField codes, little endian
+    case 1: { int8_t v; __builtin_memcpy(&v, p, 1); return (double)v; }
+    case 2: { uint8_t v; __builtin_memcpy(&v, p, 1); return (double)v; }
+    case 3: { int16_t v; __builtin_memcpy(&v, p, 2); return (double)v; }
+    case 4: { uint16_t v; __builtin_memcpy(&v, p, 2); return (double)v; }
+    case 5: { int32_t v; __builtin_memcpy(&v, p, 4); return (double)v; }
+    case 6: { uint32_t v; __builtin_memcpy(&v, p, 4); return (double)v; }
+    case 7: { float v; __builtin_memcpy(&v, p, 4); return (double)v; }
+    default: { double v; __builtin_memcpy(&v, p, 8); return v; }
+  }
+}
+__device__ __forceinline__ double nan_to_num_sentinel(double v) {
+  if (v != v) return 1e6;  // GC_NONFINITE_SENTINEL, constants.py:256-262
+  if (v == INFINITY) return 1e6;
+  if (v == -INFINITY) return -1e6;
+  return v;
+}
+__global__ __launch_bounds__(kBlock) void k_parse_pc2(ParseArgs a) {
+#pragma clang fp contract(off)
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= a.n) return;
+  const uint8_t* rec = a.data + (size_t)i * (size_t)a.point_step;
+  const double x = nan_to_num_sentinel(pc2_field(rec + a.off_x, 7));
+  const double y = nan_to_num_sentinel(pc2_field(rec + a.off_y, 7));
+  const double z = nan_to_num_sentinel(pc2_field(rec + a.off_z, 7));
+  if (a.ring) a.ring[i] = (uint8_t)(int64_t)pc2_field(rec + a.off_ring, a.ring_datatype);
+  double t = a.header_stamp;
+  if (a.off_t >= 0) {
+    t = pc2_field(rec + a.off_t, a.t_datatype);
+    if (t > 1e6) atomicOr(a.ns_flag, 1u);
+  }
+  a.t[i] = t;
+  const double dist = sqrt((x * x + y * y) + z * z);
+  const double ra = (dist - 0.5) / 0.25, rb = (50.0 - dist) / 0.25;  // constants.py:256-262
+  const double w_raw = (1.0 / (1.0 + exp(-ra))) * (1.0 / (1.0 + exp(-rb)));
+  a.w[i] = w_raw * (1.0 - kWeightFloor) + kWeightFloor;
+  const double* R = a.R;
+  double* o = a.points + 3 * (size_t)i;
+  o[0] = ((R[0] * x + R[1] * y) + R[2] * z) + a.tb[0];
+  o[1] = ((R[3] * x + R[4] * y) + R[5] * z) + a.tb[1];
+  o[2] = ((R[6] * x + R[7] * y) + R[8] * z) + a.tb[2];
+}
+__global__ __launch_bounds__(kBlock) void k_parse_time_scale(double* t, int n, const uint32_t* ns_flag) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n && *ns_flag) t[i] = t[i] * 1e-9;
+}
+
 // ---------------------------------------------------------------- row 1: budget mass sums
 // Also clears the scale-mode bucketing state of this scan (counts, flags, look-back status),
 // replacing three memsets.  mass_scale = total_mass_in / (total_mass_selected + eps_mass)
@@ -231,8 +285,13 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
     bool valid = live && i < a.n_sel;
     if (valid) {
       size_t src = (size_t)i * (size_t)a.stride;
-      const float* rec = (const float*)(a.xyz + src * (size_t)a.point_step);
-      p[0] = (double)rec[0]; p[1] = (double)rec[1]; p[2] = (double)rec[2];
+      if (a.xyz_f64) {  // parsed base-frame points (k_parse_pc2)
+        const double* rec = (const double*)(a.xyz + src * (size_t)a.point_step);
+        p[0] = rec[0]; p[1] = rec[1]; p[2] = rec[2];
+      } else {
+        const float* rec = (const float*)(a.xyz + src * (size_t)a.point_step);
+        p[0] = (double)rec[0]; p[1] = (double)rec[1]; p[2] = (double)rec[2];
+      }
       t = a.timestamps[src];
       w_raw = a.weights[src];
     }
@@ -1373,6 +1432,17 @@ static int grid_for(long n, int cap_blocks) {
   return (int)(g > cap_blocks ? cap_blocks : g);
 }
 int push_blocks(int n_bins) { return grid_for(n_bins, 4096); }
+
+hipError_t launch_parse(const ParseArgs& a, hipStream_t s) {
+  if (a.n <= 0) return hipSuccess;
+  const int nblk = (a.n + kBlock - 1) / kBlock;
+  hipError_t e = hipMemsetAsync(a.ns_flag, 0, sizeof(uint32_t), s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_parse_pc2, dim3(nblk), dim3(kBlock), 0, s, a);
+  if (a.off_t >= 0)
+    hipLaunchKernelGGL(k_parse_time_scale, dim3(nblk), dim3(kBlock), 0, s, a.t, a.n, (const uint32_t*)a.ns_flag);
+  return hipGetLastError();
+}
 
 hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   hipExtLaunchKernelGGL(k_budget, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a);  // folded inside k_points

@@ -42,7 +42,14 @@ class GcsScanInputs(C.Structure):
                 ("imu_gyro", C.c_void_p), ("imu_accel", C.c_void_p), ("imu_len", C.c_int32),
                 ("scan_start_time", C.c_double), ("scan_end_time", C.c_double), ("dt_sec", C.c_double),
                 ("Q", C.c_void_p), ("L_ext", C.c_void_p), ("h_ext", C.c_void_p),
-                ("t_last_scan", C.c_double), ("t_scan", C.c_double)]
+                ("t_last_scan", C.c_double), ("t_scan", C.c_double), ("xyz_format", C.c_int32)]
+
+
+class GcsPointCloud2Layout(C.Structure):
+    _fields_ = [("n_points", C.c_int32), ("point_step", C.c_int32), ("off_x", C.c_int32), ("off_y", C.c_int32),
+                ("off_z", C.c_int32), ("off_ring", C.c_int32), ("ring_datatype", C.c_int32), ("off_t", C.c_int32),
+                ("t_datatype", C.c_int32), ("header_stamp_sec", C.c_double), ("R_base_lidar", C.c_double * 9),
+                ("t_base_lidar", C.c_double * 3)]
 
 
 class GcsBelief(C.Structure):
@@ -83,6 +90,8 @@ _SIGS = [
     ("gcs_ctx_set_meas_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
     ("gcs_ctx_get_meas_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p]),
     ("gcs_scan", C.c_int, [C.c_void_p, C.POINTER(GcsScanInputs), C.POINTER(GcsScanOutputs)]),
+    ("gcs_parse_pointcloud2", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(GcsPointCloud2Layout), C.c_void_p,
+                                        C.c_void_p, C.c_void_p, C.c_void_p]),
     ("gcs_point_stage", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_double,
                                   C.c_double, c_double_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, c_double_p]),
     ("gcs_bin_soft_assign", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),

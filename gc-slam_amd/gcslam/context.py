@@ -213,9 +213,11 @@ class HypothesisContext:
 
     # ------------------------------------------------------------------ the scan
     def scan(self, xyz_dev, point_step, t_dev, w_dev, n_points, imu_stamps, imu_gyro, imu_accel,
-             scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None, t_last_scan=None, t_scan=None):
+             scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None, t_last_scan=None, t_scan=None,
+             xyz_f64=False):
         """gcs_scan.  t_last_scan / t_scan bound the scan-to-scan IMU window of the measurement-noise
-        IW statistics (pipeline.py:331-332); default: the scan window."""
+        IW statistics (pipeline.py:331-332); default: the scan window.  xyz_f64: xyz_dev holds f64
+        x, y, z per point_step record (gcs_parse_pointcloud2 output, point_step 24)."""
         imu_stamps = np.ascontiguousarray(imu_stamps, np.float64)
         imu_gyro = np.ascontiguousarray(imu_gyro, np.float64).reshape(-1)
         imu_accel = np.ascontiguousarray(imu_accel, np.float64).reshape(-1)
@@ -234,6 +236,7 @@ class HypothesisContext:
         inp.dt_sec = float(dt_sec)
         inp.t_last_scan = float(scan_start_time if t_last_scan is None else t_last_scan)
         inp.t_scan = float(scan_end_time if t_scan is None else t_scan)
+        inp.xyz_format = 1 if xyz_f64 else 0
         keep = []
         for name, arr in (("Q", Q), ("L_ext", L_ext), ("h_ext", h_ext)):
             if arr is not None:

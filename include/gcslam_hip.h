@@ -11,6 +11,7 @@
  * FS = fl_ws/src/fl_slam_poc/fl_slam_poc):
  *   gcs_scan                    FS/backend/pipeline.py:316-1591 process_scan_single_hypothesis
  *                               (14-step bin path, README.md:105-122)
+ *   gcs_parse_pointcloud2       FS/backend/backend_node.py:377-468 parse_pointcloud2_vlp16 (+ :1677-1680)
  *   gcs_point_stage             FS/backend/operators/point_budget.py:117-221 point_budget_resample
  *                               + FS/backend/operators/deskew_constant_twist.py:72-117 (fused)
  *   gcs_bin_soft_assign         archive/legacy_operators/binning.py:79-131 bin_soft_assign
@@ -88,7 +89,22 @@ typedef struct {
   const double* h_ext;         /* [22] */
   /* scan-to-scan IMU window of the measurement-noise IW statistics (pipeline.py:331-332,448-453) */
   double t_last_scan, t_scan;
+  /* 0: float32 x,y,z at bytes 0,4,8 of each point_step record; 1: float64 x,y,z (gcs_parse_pointcloud2) */
+  int32_t xyz_format;
 } gcs_scan_inputs;
+
+/* Layout of a PointCloud2 message (sensor_msgs/PointField offsets and datatype codes) for
+ * gcs_parse_pointcloud2; the VLP-16 layout has FLOAT32 x, y, z and a ring field. */
+typedef struct {
+  int32_t n_points;             /* width * height */
+  int32_t point_step;
+  int32_t off_x, off_y, off_z;  /* FLOAT32 */
+  int32_t off_ring, ring_datatype;
+  int32_t off_t, t_datatype;    /* per-point "t" (else "time") field; off_t < 0: none (header stamp) */
+  double header_stamp_sec;
+  double R_base_lidar[9];       /* row-major; points are returned in the base frame */
+  double t_base_lidar[3];
+} gcs_pointcloud2_layout;
 
 typedef struct {
   double X_anchor[6];
@@ -154,6 +170,12 @@ int gcs_ctx_get_meas_iw_state(gcs_ctx* ctx, double* nu3, double* Psi3x9, double*
 int gcs_scan(gcs_ctx* ctx, const gcs_scan_inputs* in, gcs_scan_outputs* out);
 
 /* ---------------------------------------------------------------- per-operator device entry points */
+/* parse_pointcloud2_vlp16 (FS/backend/backend_node.py:377-468) + the no-TF base transform
+ * (:1677-1680) on the device, over the raw message bytes: points_dev [n*3] f64 base frame (feed
+ * gcs_scan with xyz_format = 1, point_step = 24), t_dev (s; ns converted when any value exceeds
+ * 1e6), w_dev (range-sigmoid weights), ring_dev (u8, may be NULL).  Async on the context stream. */
+int gcs_parse_pointcloud2(gcs_ctx* ctx, const void* data_dev, const gcs_pointcloud2_layout* layout,
+                          double* points_dev, double* t_dev, double* w_dev, uint8_t* ring_dev);
 /* PointBudgetResample + DeskewConstantTwist + directions + BinSoftAssign normalisers, fused.
  * Outputs (device, length n_points_cap; NULL to skip): deskewed points [cap*3], deskewed
  * weights, budget weights, nearest bin (scale mode).  cert_host receives scalars

@@ -62,6 +62,47 @@ def dot3(a, b):
     return (a[..., 0] * b[..., 0] + a[..., 1] * b[..., 1]) + a[..., 2] * b[..., 2]
 
 
+# ================================================================ before row 1: PointCloud2 parse
+NONFINITE_SENTINEL = 1e6                           # constants.py:256-262
+RANGE_WEIGHT_SIGMA, RANGE_WEIGHT_MIN_R, RANGE_WEIGHT_MAX_R = 0.25, 0.5, 50.0
+PC2_DTYPES = {1: "i1", 2: "u1", 3: "<i2", 4: "<u2", 5: "<i4", 6: "<u4", 7: "<f4", 8: "<f8"}  # PointField codes
+
+
+def parse_pointcloud2_vlp16(data, fields, point_step, n_points, header_stamp_sec):
+    """parse_pointcloud2_vlp16, FS/backend/backend_node.py:377-468.  fields: {name: (offset,
+    datatype)}.  Returns points (n,3) f64 (lidar frame), t, w, ring (u8), tag (u8)."""
+    if n_points <= 0:
+        return (np.zeros((0, 3)), np.zeros(0), np.zeros(0), np.zeros(0, np.uint8), np.zeros(0, np.uint8))
+    missing = [k for k in ("x", "y", "z", "ring") if k not in fields]
+    if missing:
+        raise RuntimeError(f"PointCloud2 (VLP-16 layout) missing required fields: {missing}")
+    time_field = "t" if "t" in fields else ("time" if "time" in fields else None)
+    names = ["x", "y", "z", "ring"] + ([time_field] if time_field else [])
+    dt = np.dtype({"names": names, "formats": [PC2_DTYPES[fields[k][1]] for k in names],
+                   "offsets": [fields[k][0] for k in names], "itemsize": point_step})
+    arr = np.frombuffer(bytes(data), dtype=dt, count=n_points)
+    s = NONFINITE_SENTINEL
+    x, y, z = (np.nan_to_num(np.asarray(arr[k], np.float64), nan=s, posinf=s, neginf=-s) for k in "xyz")
+    ring = np.asarray(arr["ring"]).astype(np.uint8)
+    if time_field is not None:
+        t_raw = np.asarray(arr[time_field], np.float64)
+        t = t_raw * 1e-9 if np.any(t_raw > 1e6) else t_raw
+    else:
+        t = np.full(n_points, header_stamp_sec, np.float64)
+    dist = np.sqrt(x * x + y * y + z * z)
+    a = (dist - RANGE_WEIGHT_MIN_R) / RANGE_WEIGHT_SIGMA
+    b = (RANGE_WEIGHT_MAX_R - dist) / RANGE_WEIGHT_SIGMA
+    with np.errstate(over="ignore"):  # sentinel ranges: exp overflows to inf, the weight to 0 (as in numpy there)
+        w_raw = (1.0 / (1.0 + np.exp(-a))) * (1.0 / (1.0 + np.exp(-b)))
+    w = w_raw * (1.0 - WEIGHT_FLOOR) + WEIGHT_FLOOR
+    return np.stack([x, y, z], axis=1), t, w, ring, np.zeros(n_points, np.uint8)
+
+
+def lidar_to_base(points, R_base_lidar, t_base_lidar):
+    """No-TF mode transform before inference, backend_node.py:1677-1680."""
+    return (np.asarray(R_base_lidar) @ points.T).T + np.asarray(t_base_lidar)[None, :]
+
+
 # ================================================================ row 1: PointBudgetResample
 def point_budget_resample(points, timestamps, weights, ring=None, tag=None, n_points_cap=8192):
     """FS/backend/operators/point_budget.py:50-109 (core) and :117-221 (wrapper)."""
