@@ -15,6 +15,7 @@ import numpy as np
 
 from .certificates import CertBundle, InfluenceCert, SupportCert, aggregate_certificates
 from .context import HypothesisContext
+from .outputs import tape_from_result
 
 CHART_ID = "GC-RIGHT-01"
 D_Z = 22
@@ -80,7 +81,7 @@ class ScanPipelineResult:
     iw_lidar_bucket_dnu: np.ndarray
     all_certs: List[CertBundle]
     aggregated_cert: CertBundle
-    diagnostics_tape: Optional[dict] = None
+    diagnostics_tape: Optional[object] = None   # gcslam.outputs.MinimalScanTape (diagnostics.py:19-160)
     map_bins_updated: Optional[HypothesisContext] = None
     z_t: Optional[np.ndarray] = None
     raw_cert: Optional[np.ndarray] = None
@@ -151,15 +152,19 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
     certs = _certs_from_vector(cert, CHART_ID, belief_prev.anchor_id)
     agg = aggregate_certificates(certs)
     bel = BeliefGaussianInfo(CHART_ID, belief_prev.anchor_id, X, stamp, z, Lm, h, certs[-1])
-    return ScanPipelineResult(
+    res = ScanPipelineResult(
         belief_updated=bel,
         iw_process_dPsi=np.array(out.iw_process_dPsi[:]).reshape(7, 6, 6),
         iw_process_dnu=np.array(out.iw_process_dnu[:]),
         iw_meas_dPsi=np.array(out.iw_meas_dPsi[:]).reshape(3, 3, 3), iw_meas_dnu=np.array(out.iw_meas_dnu[:]),
         iw_lidar_bucket_dPsi=np.zeros((64, 3, 3)), iw_lidar_bucket_dnu=np.zeros(64),
         all_certs=certs, aggregated_cert=agg,
-        diagnostics_tape=dict(stage_ms=list(out.stage_ms[:4]), total_trigger=cert[35], beta=cert[30]),
+        diagnostics_tape=dict(stage_ms=list(out.stage_ms[:4])),
         map_bins_updated=ctx, z_t=np.array(out.z_t[:]), raw_cert=cert)
+    # the reference's per-scan MinimalScanTape (pipeline.py:1504-1570)
+    res.diagnostics_tape = tape_from_result(res, scan_seq, scan_end_time, dt_sec, rec.shape[0],
+                                            np.array(out.L_evidence[:]))
+    return res
 
 
 def process_hypotheses(hypotheses: List[BeliefGaussianInfo], weights, config: PipelineConfig,
