@@ -92,6 +92,8 @@ struct gcs_ctx {
   double last_meas_dPsi[3 * 9], last_meas_dnu[3];
   bool have_last = false;
   int last_n_sel = 0, last_stride = 1;
+  int budget_blocks = 0;
+  bool budget_pending = false;  // k_budget already queued for the coming point stage (gcs_scan)
   std::vector<double> wimu, wint;  // IMU window weights: within-scan, scan-to-scan (scratch)
   // device stage timing (hipEvents on the context stream; harvested lazily)
   uint32_t timing_mask = 0;
@@ -246,22 +248,19 @@ int upload_atlas(gcs_ctx* c) {
 
 // ---------------------------------------------------------------- device stages
 // fold_later: leave k_points' cert fold to block 0 of the next k_bins_scale (scale-mode scan)
-int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, const double* w, int n_raw, double t0,
-                 double t1, const double* xi, double* p0_out, double* w_out, double* wb_out, bool fold_later = false,
-                 bool xyz_f64 = false) {
+// Row 1's mass sums (k_budget) need only the weights: gcs_scan queues them before its host
+// prologue so they run while the host predicts and preintegrates.  e0: stage timing start (may be null).
+int stage_budget(gcs_ctx* c, const double* w, int n_raw, hipEvent_t e0) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
-  if (point_step < (xyz_f64 ? 24 : 12)) return fail(c, GCS_ERR_ARG, "point_step too small for x, y, z");
   int stride = std::max(1, (int)((n_raw + (long)c->cap - 1) / c->cap));  // ceil(N/cap), point_budget.py:160
   int n_sel = (n_raw + stride - 1) / stride;
   c->last_n_sel = n_sel;
   c->last_stride = stride;
   hipStream_t s = c->stream;
-  harvest(c);
   if (c->d_flags_buf[0]) {  // this scan's flag buffer (the other may still be read by k_pushforward)
     c->flags_cur ^= 1;
     c->d_flags = c->d_flags_buf[c->flags_cur];
   }
-  StageEv ev = stage_ev(c, ST_POINTS);
   BudgetArgs ba{};
   ba.w = w;
   ba.n_raw = n_raw;
@@ -272,8 +271,25 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   ba.n_zero32 = c->d_counts ? c->B : 0;
   ba.zero8 = c->d_flags;
   ba.n_zero8 = c->d_flags ? c->B + bins_scale_blocks(c->B) : 0;
-  const int budget_blocks = red_blocks(std::max(n_raw, 1));
-  HIPCHK(c, launch_budget(ba, budget_blocks, s, ev.e0, nullptr));
+  c->budget_blocks = red_blocks(std::max(n_raw, 1));
+  HIPCHK(c, launch_budget(ba, c->budget_blocks, s, e0, nullptr));
+  c->budget_pending = true;
+  return GCS_OK;
+}
+
+int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, const double* w, int n_raw, double t0,
+                 double t1, const double* xi, double* p0_out, double* w_out, double* wb_out, bool fold_later = false,
+                 bool xyz_f64 = false) {
+  if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
+  if (point_step < (xyz_f64 ? 24 : 12)) return fail(c, GCS_ERR_ARG, "point_step too small for x, y, z");
+  harvest(c);
+  StageEv ev = stage_ev(c, ST_POINTS);
+  const bool hoisted = c->budget_pending;  // k_budget queued earlier by gcs_scan: the stage starts at k_points
+  if (!hoisted)
+    if (int rc = stage_budget(c, w, n_raw, ev.e0)) return rc;
+  c->budget_pending = false;
+  const int n_sel = c->last_n_sel, stride = c->last_stride;
+  hipStream_t s = c->stream;
   PointKernelArgs a{};
   a.xyz = (const uint8_t*)xyz;
   a.point_step = point_step;
@@ -301,7 +317,7 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.slots = c->d_slots;
   a.counts = c->d_counts;
   a.budget_partials = c->d_partials;
-  a.budget_blocks = budget_blocks;
+  a.budget_blocks = c->budget_blocks;
   a.scalars = c->d_scalars;
   a.p0_out = p0_out;
   a.w_out = w_out;
@@ -310,7 +326,8 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   const bool scale = c->cfg.mode == GCS_MODE_SCALE;
   c->pts_blocks = red_blocks(c->cap);
   c->pts_fold_pending = scale && fold_later;
-  HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, nullptr, ev.e1));
+  HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, hoisted ? ev.e0 : nullptr,
+                          ev.e1));
   return GCS_OK;
 }
 
@@ -743,6 +760,7 @@ int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const doubl
                     int32_t* nearest_dev, double* cert) {
   if (!c || !xi) return GCS_ERR_ARG;
   join_push(c);
+  c->budget_pending = false;  // a k_budget queued by a gcs_scan that failed later is stale
   int rc = stage_points(c, xyz, point_step, t, w, n, t0, t1, xi, p0_dev, w_out_dev, w_budget_dev);
   if (rc) return rc;
   if (nearest_dev) {  // reported in reference bin ids
@@ -859,6 +877,8 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   if (!c || !in || !out) return fail(c, GCS_ERR_ARG, "null argument");
   if (in->imu_len < 1 || !in->imu_stamps || !in->imu_gyro || !in->imu_accel) return fail(c, GCS_ERR_ARG, "IMU window required");
   auto T0 = clk::now();
+  c->budget_pending = false;
+  if (int rc0 = stage_budget(c, in->weights_dev, in->n_points, nullptr)) return rc0;  // runs during the prologue
   const double* Q = in->Q ? in->Q : c->Q;
   double* cert = out->cert;
   memset(cert, 0, sizeof(out->cert));
