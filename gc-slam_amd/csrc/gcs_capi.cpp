@@ -324,7 +324,7 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.w_budget_out = wb_out;
   a.nearest_out = c->d_nearest;  // device ids
   const bool scale = c->cfg.mode == GCS_MODE_SCALE;
-  c->pts_blocks = red_blocks(c->cap);
+  c->pts_blocks = points_blocks(c->cap, scale);
   c->pts_fold_pending = scale && fold_later;
   HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, hoisted ? ev.e0 : nullptr,
                           ev.e1));
@@ -493,7 +493,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   c->partials_len = std::max<size_t>({partials_need(kRedBlocks, 24), partials_need(bins_scale_blocks(c->B), bins_partial_nv()),
                                       partials_need(push_blocks(c->B), 10)});
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
-  if (bad(hipMalloc(&c->d_part_pts, partials_need(kRedBlocks, 5) * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_part_pts, partials_need(std::max(kRedBlocks, points_max_blocks()), 5) * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_part_push, partials_need(push_blocks(c->B), 10) * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;

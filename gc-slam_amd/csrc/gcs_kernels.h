@@ -122,6 +122,8 @@ struct PushArgs {
 hipError_t launch_parse(const ParseArgs& a, hipStream_t s);
 hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 // fold: run k_points' cert fold now (else k_bins_scale block 0 folds it, BinKernelArgs.pts_partials)
+int points_blocks(long cap, bool scale);  // k_points grid (lanes per point in scale mode)
+int points_max_blocks();
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
                          hipEvent_t e0, hipEvent_t e1);
 int scan_tiles(int n_bins);

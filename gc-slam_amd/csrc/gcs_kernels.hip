@@ -254,8 +254,23 @@ __device__ __forceinline__ void ray_dir(double px, double py, double pz, const d
 // loads are issued in independent batches (whole pool row, whole candidate row) so the chain is
 // xyz -> pool ids -> pool dirs -> knn row -> candidate dirs -> slot atomic, and the softmax
 // evaluates one exp per candidate and no per-candidate log (entropy identity below).
-template <bool SCALE, int KC>
-__global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* partials) {
+// LP > 1 (scale mode): LP lanes per point.  Each lane scans every LP-th chunk of the pool row and
+// takes KC/LP of the candidates, so the chain's load batches are LP times narrower per lane and
+// the register file holds KC/LP candidate terms; the lanes' nearest bins meet in a (dot, lower
+// id) max, their softmax terms in fixed xor trees (identical on every lane of the point).  One
+// lane per point takes the slot atomic and writes the record.
+#ifndef GCS_POINT_WAVES
+#define GCS_POINT_WAVES 0  // register target (waves per SIMD) of k_points; 0: compiler default
+#endif
+template <bool SCALE, int KC, int LP>
+__global__ __launch_bounds__(kBlock)
+#if GCS_POINT_WAVES
+__attribute__((amdgpu_waves_per_eu(GCS_POINT_WAVES)))
+#endif
+void k_points(PointKernelArgs a, double* partials) {
+  static_assert(LP == 1 || (SCALE && (LP == 2 || LP == 4) && KC % LP == 0), "lanes per point");
+  constexpr int KL = KC / LP, kPB = kBlock / LP;  // candidates per lane, points per block
+  const int sub = threadIdx.x % LP;
   __shared__ double lds[kWaves * 5];
   __shared__ double s_mass[2];
   // budget mass sums: every block folds k_budget's partial rows itself (same fixed order in every
@@ -276,10 +291,10 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
   double rmax = -INFINITY;
   double mass_scale = 0.0, mass_in = 0.0;
   // uniform trip count (the budget fold inside the first iteration has barriers)
-  const int gstride = gridDim.x * kBlock;
+  const int gstride = gridDim.x * kPB;
   const int niter = (a.cap + gstride - 1) / gstride;
   for (int it = 0; it < niter; ++it) {
-    const int i = blockIdx.x * kBlock + threadIdx.x + it * gstride;
+    const int i = blockIdx.x * kPB + (int)threadIdx.x / LP + it * gstride;
     const bool live = i < a.cap;
     double p[3] = {0.0, 0.0, 0.0}, t = 0.0, w_raw = 0.0;
     bool valid = live && i < a.n_sel;
@@ -310,13 +325,15 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
         const int4* pool = (const int4*)(a.pools + (size_t)cube_cell(d[0], d[1], d[2], a.grid) * a.pool_width);
         const int nq = a.pool_width >> 2;
         double best = -INFINITY;
-        for (int q = 0; q < nq; q += 2) {  // 8 ids per batch: all loads in flight together
+        // 4 * CH ids per batch and lane: all loads in flight together
+        constexpr int CH = LP >= 4 ? 1 : 2;
+        for (int q = sub; q < nq; q += CH * LP) {
           int4 u0 = pool[q];
-          int4 u1 = q + 1 < nq ? pool[q + 1] : make_int4(-1, -1, -1, -1);
+          int4 u1 = CH == 2 && q + LP < nq ? pool[q + LP] : make_int4(-1, -1, -1, -1);
           int ids[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
           double s[8];
 #pragma unroll
-          for (int u = 0; u < 8; ++u) {
+          for (int u = 0; u < 4 * CH; ++u) {
             s[u] = -INFINITY;
             if (ids[u] >= 0) {
               const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)ids[u]);
@@ -324,33 +341,51 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
             }
           }
 #pragma unroll
-          for (int u = 0; u < 8; ++u)
+          for (int u = 0; u < 4 * CH; ++u)
             if (s[u] > best) { best = s[u]; nearest = ids[u]; }
-          if (u1.w < 0) break;
+          if ((CH == 2 ? u1.w : u0.w) < 0) break;
+        }
+#pragma unroll
+        for (int off = 1; off < LP; off <<= 1) {  // first maximum in ascending-id order
+          const double ob = __shfl_xor(best, off, 64);
+          const int oi = __shfl_xor(nearest, off, 64);
+          if (ob > best || (ob == best && oi < nearest)) { best = ob; nearest = oi; }
         }
       }
-      const int4* cand4 = (const int4*)(a.knn + (size_t)nearest * KC);
-      int cand[KC];
+      int cand[KL];
+      if constexpr (KL % 4 == 0) {
+        const int4* cand4 = (const int4*)(a.knn + (size_t)nearest * KC + sub * KL);
 #pragma unroll
-      for (int k = 0; k < KC / 4; ++k) {
-        int4 c4 = cand4[k];
-        cand[4 * k] = c4.x; cand[4 * k + 1] = c4.y; cand[4 * k + 2] = c4.z; cand[4 * k + 3] = c4.w;
+        for (int k = 0; k < KL / 4; ++k) {
+          int4 c4 = cand4[k];
+          cand[4 * k] = c4.x; cand[4 * k + 1] = c4.y; cand[4 * k + 2] = c4.z; cand[4 * k + 3] = c4.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < KL; ++k) cand[k] = a.knn[(size_t)nearest * KC + sub * KL + k];
       }
-      double e[KC];
+      double e[KL];
 #pragma unroll
-      for (int k = 0; k < KC; ++k) {
+      for (int k = 0; k < KL; ++k) {
         const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)cand[k]);
         e[k] = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
         m = fmax(m, e[k]);
       }
+#pragma unroll
+      for (int off = 1; off < LP; off <<= 1) m = fmax(m, __shfl_xor(m, off, 64));
       // e_k = exp(x_k), x_k = (sim_k - m)/tau (binning.py:69 softmax, shifted by the max)
       double sxe = 0.0;
 #pragma unroll
-      for (int k = 0; k < KC; ++k) {
+      for (int k = 0; k < KL; ++k) {
         double x = (e[k] - m) * inv_tau;
         e[k] = exp(x);
         Z += e[k];
         sxe += x * e[k];
+      }
+#pragma unroll
+      for (int off = 1; off < LP; off <<= 1) {
+        Z += __shfl_xor(Z, off, 64);
+        sxe += __shfl_xor(sxe, off, 64);
       }
       const double iz = 1.0 / Z;
       // entropy of r_k = e_k/Z (binning.py:71-75): -sum r log(r + eps)
@@ -358,19 +393,24 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
       // with r log1p(eps/r) in [0, eps] taken as eps r/(r + eps) (|error| < 0.2 eps per term)
       double corr = 0.0;
 #pragma unroll
-      for (int k = 0; k < KC; ++k) {
+      for (int k = 0; k < KL; ++k) {
         double r = e[k] * iz;
         corr += r * __builtin_amdgcn_rcp(r + kEpsMass);
         rm = fmax(rm, r);
       }
+#pragma unroll
+      for (int off = 1; off < LP; off <<= 1) {
+        corr += __shfl_xor(corr, off, 64);
+        rm = fmax(rm, __shfl_xor(rm, off, 64));
+      }
       H = log(Z) - sxe * iz - kEpsMass * corr;
       uint32_t key = (uint32_t)a.n_bins;
-      if (valid) {
+      if (valid && sub == 0) {
         // bucket slot: arrival order only (re-ranked by point index in k_bucket_build)
         a.slots[i] = atomicAdd(a.counts + nearest, 1u);
         key = (uint32_t)nearest;
       }
-      if (live) a.keys[i] = key;
+      if (live && sub == 0) a.keys[i] = key;
       Z = iz;
     } else {
       for (int b = 0; b < a.n_bins; ++b) {
@@ -411,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void k_points(PointKernelArgs a, double* pa
       mass_scale = s_mass[1];
       mass_in = s_mass[0];
     }
-    if (!live) continue;
+    if (!live || sub != 0) continue;
     const double wb = w_raw * mass_scale;
     const double wout = wb * win;
     PointRec pr;
@@ -802,8 +842,21 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
     }
 }
 
+#ifndef GCS_GATHER_PIPE
+#define GCS_GATHER_PIPE 1  // phase C loads the next staged record while accumulating the current one
+#endif
+#ifndef GCS_MAPV_EARLY
+#define GCS_MAPV_EARLY 1  // phase D's map direction stats are loaded before phase A
+#endif
+#ifndef GCS_BINS_WAVES
+#define GCS_BINS_WAVES 0  // waves per SIMD the register allocation targets (0: compiler default)
+#endif
 template <int STAGE, int LANES>
-__global__ __launch_bounds__(kBinTile * LANES) void k_bins_scale(BinKernelArgs a, double* partials) {
+__global__ __launch_bounds__(kBinTile * LANES)
+#if GCS_BINS_WAVES
+__attribute__((amdgpu_waves_per_eu(GCS_BINS_WAVES)))
+#endif
+void k_bins_scale(BinKernelArgs a, double* partials) {
   constexpr int NT = kBinTile * LANES, NW = NT / 64;
   static_assert(LANES == 4 || LANES == 8, "phase C splits each bin over 4 or 8 lanes");
   __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
@@ -864,7 +917,7 @@ __global__ __launch_bounds__(kBinTile * LANES) void k_bins_scale(BinKernelArgs a
   const bool own = t < nb;
   const bool own_act = own && a.flags[b0 + t];
   MapDir mapv{0.0, 0.0, 0.0, 0.0};
-  if (own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + t);
+  if (GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + t);
   // phase A
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
   if (t <= nb) s_q[t] = q_t;
@@ -957,7 +1010,25 @@ __global__ __launch_bounds__(kBinTile * LANES) void k_bins_scale(BinKernelArgs a
       c = s_cnt[j];
     }
     uint32_t kk = skip;
-    if (staged) {
+    if (staged && !GCS_GATHER_PIPE) {
+      uint32_t r = s_off[j] + kk, left = c - kk;
+      for (uint32_t i = i0; i < i1; ++i) {
+        const double2* rp = (const double2*)(s_rec + (size_t)r * kRecD);
+        const uint32_t sw = rec_swz(r);
+        const double2 c0 = rp[0 ^ sw], c1 = rp[1 ^ sw], c2 = rp[2 ^ sw], c3 = rp[3 ^ sw];
+        bin_contrib(acc, bd, inv_tau, c0.x, c0.y, c1.x, c1.y, c2.x, c2.y, c3.x, c3.y);
+        if (--left == 0 && i + 1 < i1) {  // next non-empty source
+          do {
+            ++q;
+            j = s_rl[q - q0];
+            left = s_cnt[j];
+          } while (left == 0);
+          r = s_off[j];
+        } else {
+          ++r;
+        }
+      }
+    } else if (staged) {
       // a source's records are one contiguous LDS run: the record index advances by one and is
       // re-based only at source boundaries, and the next record is loaded (double2 x 4) while the
       // current one is accumulated
@@ -1025,6 +1096,7 @@ __global__ __launch_bounds__(kBinTile * LANES) void k_bins_scale(BinKernelArgs a
     for (int f = 0; f < 19; ++f) acc[f] = s_rec[f * kBinTile + t];
     finalize_bin(acc, a.scan, a.n_bins, b0 + t, v);
     PROF(15);
+    if (!GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + t);
     if (own_act) mf_bin_term(acc[0], acc[1], acc[2], acc[3], mapv, v + 5);
   }
   PROF(5);
@@ -1217,9 +1289,10 @@ __device__ __forceinline__ void map_totals_partial(double (&tot)[kTotNV], double
 // (touched = 0: all-zero stats) stays exactly zero under forgetting + push, and its derived stats
 // keep the zero-bin constants: it is skipped (adds exact zeros to the totals).  act == nullptr
 // (dense mode): every bin is updated.
-__global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict__ scan, double* map, double* derived,
-                                                        int B, PushArgs pa, double* partials,
-                                                        const uint8_t* __restrict__ act, uint8_t* touched) {
+__global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict__ scan, double* __restrict__ map,
+                                                        double* __restrict__ derived, int B, PushArgs pa,
+                                                        double* __restrict__ partials,
+                                                        const uint8_t* __restrict__ act, uint8_t* __restrict__ touched) {
   __shared__ double lds[kWaves * kTotNV];
   double tot[kTotNV];
 #pragma unroll
@@ -1241,10 +1314,40 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
         continue;
       }
     }
-    const double N = sc ? scan[SF_N * Bs + b] : 0.0;
-    double pb[3], u[3], q[3];
+    // every load of the bin is issued before any store: the map rows are read and written in
+    // place, so loads placed after a store could not be hoisted above it and each field would cost
+    // its own memory round trip
+    double ms[26];  // map row: S_dir 3 | S_dir_scatter 9 | N_dir | N_pos | sum p 3 | sum ppT 9
 #pragma unroll
-    for (int k = 0; k < 3; ++k) pb[k] = sc ? scan[(SF_PB + k) * Bs + b] : 0.0;
+    for (int k = 0; k < 3; ++k) ms[k] = map[(MF_SD + k) * Bs + b];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) ms[3 + k] = map[(MF_S + k) * Bs + b];
+    ms[12] = map[MF_ND * Bs + b];
+    ms[13] = map[MF_NP * Bs + b];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ms[14 + k] = map[(MF_SP + k) * Bs + b];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) ms[17 + k] = map[(MF_SPP + k) * Bs + b];
+    double N = 0.0, pb[3] = {0.0, 0.0, 0.0}, s_d[3] = {0.0, 0.0, 0.0}, S[9], Sg[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      S[k] = 0.0;
+      Sg[k] = (k % 4 == 0) ? kEpsPsd : 0.0;
+    }
+    if (sc) {
+      N = scan[SF_N * Bs + b];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        pb[k] = scan[(SF_PB + k) * Bs + b];
+        s_d[k] = scan[(SF_SD + k) * Bs + b];
+      }
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        S[k] = scan[(SF_S + k) * Bs + b];
+        Sg[k] = scan[(SF_SIG + k) * Bs + b];
+      }
+    }
+    double u[3], q[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       u[i] = R[3 * i] * pb[0] + R[3 * i + 1] * pb[1] + R[3 * i + 2] * pb[2];
@@ -1252,44 +1355,34 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
     }
     // S_dir += R s_dir
     double sd[3];
-    {
-      double s0 = 0.0, s1 = 0.0, s2 = 0.0;
-      if (sc) {
-        s0 = scan[(SF_SD + 0) * Bs + b];
-        s1 = scan[(SF_SD + 1) * Bs + b];
-        s2 = scan[(SF_SD + 2) * Bs + b];
-      }
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        sd[i] = g * map[(MF_SD + i) * Bs + b] + (R[3 * i] * s0 + R[3 * i + 1] * s1 + R[3 * i + 2] * s2);
-        map[(MF_SD + i) * Bs + b] = sd[i];
-      }
+    for (int i = 0; i < 3; ++i) {
+      sd[i] = g * ms[i] + (R[3 * i] * s_d[0] + R[3 * i + 1] * s_d[1] + R[3 * i + 2] * s_d[2]);
+      map[(MF_SD + i) * Bs + b] = sd[i];
     }
     // S_dir_scatter += R S R^T
     {
-      double S[9], RS[9];
-#pragma unroll
-      for (int k = 0; k < 9; ++k) S[k] = sc ? scan[(SF_S + k) * Bs + b] : 0.0;
+      double RS[9];
       mat3_mul(R, S, RS);
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
           double v = RS[3 * i] * R[3 * j] + RS[3 * i + 1] * R[3 * j + 1] + RS[3 * i + 2] * R[3 * j + 2];
-          double sn = g * map[(MF_S + 3 * i + j) * Bs + b] + v;
+          double sn = g * ms[3 + 3 * i + j] + v;
           map[(MF_S + 3 * i + j) * Bs + b] = sn;
           tot[3 * i + j] += sn;
         }
     }
-    const double nd = g * map[MF_ND * Bs + b] + N;
-    const double np = g * map[MF_NP * Bs + b] + N;
+    const double nd = g * ms[12] + N;
+    const double np = g * ms[13] + N;
     map[MF_ND * Bs + b] = nd;
     map[MF_NP * Bs + b] = np;
     tot[9] += nd;
     double sp[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      sp[k] = g * map[(MF_SP + k) * Bs + b] + N * q[k];
+      sp[k] = g * ms[14 + k] + N * q[k];
       map[(MF_SP + k) * Bs + b] = sp[k];
     }
     // sum_ppT += N [ R (Sigma_p + p p^T) R^T + J S J^T + q q^T - u u^T ]
@@ -1299,8 +1392,7 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
 #pragma unroll
       for (int i = 0; i < 3; ++i)
 #pragma unroll
-        for (int j = 0; j < 3; ++j)
-          M2[3 * i + j] = (sc ? scan[(SF_SIG + 3 * i + j) * Bs + b] : (i == j ? kEpsPsd : 0.0)) + pb[i] * pb[j];
+        for (int j = 0; j < 3; ++j) M2[3 * i + j] = Sg[3 * i + j] + pb[i] * pb[j];
       mat3_mul(R, M2, RM);
       double X[9], XF[9], XG[9];
       skew3(u, X);
@@ -1313,7 +1405,7 @@ __global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict
           double rmr = RM[3 * i] * R[3 * j] + RM[3 * i + 1] * R[3 * j + 1] + RM[3 * i + 2] * R[3 * j + 2];
           double xgx = XG[3 * i] * X[3 * j] + XG[3 * i + 1] * X[3 * j + 1] + XG[3 * i + 2] * X[3 * j + 2];
           double jsj = pa.Stt[3 * i + j] - XF[3 * i + j] - XF[3 * j + i] + xgx;
-          spp[3 * i + j] = g * map[(MF_SPP + 3 * i + j) * Bs + b] + N * (rmr + jsj + q[i] * q[j] - u[i] * u[j]);
+          spp[3 * i + j] = g * ms[17 + 3 * i + j] + N * (rmr + jsj + q[i] * q[j] - u[i] * u[j]);
           map[(MF_SPP + 3 * i + j) * Bs + b] = spp[3 * i + j];
         }
     }
@@ -1449,17 +1541,29 @@ hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_
   return hipGetLastError();
 }
 
+#ifndef GCS_POINT_LANES
+#define GCS_POINT_LANES 1  // lanes per point (scale mode); 2 and 4 measured slower, DESIGN.md section 5
+#endif
+constexpr int kPointLanes = GCS_POINT_LANES;
+constexpr int kPointsMaxBlocks = 4096;
+int points_max_blocks() { return kPointsMaxBlocks; }
+int points_blocks(long cap, bool scale) {
+  const long lanes = scale ? kPointLanes : 1;
+  const long need = (cap * lanes + kBlock - 1) / kBlock;
+  return (int)std::max(1L, std::min((long)(scale ? kPointsMaxBlocks : 1024), need));
+}
+
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
                          hipEvent_t e0, hipEvent_t e1) {
   if (scale) {
     switch (a.k) {
-      case 8: hipExtLaunchKernelGGL(k_points<true, 8>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
-      case 16: hipExtLaunchKernelGGL(k_points<true, 16>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
-      case 32: hipExtLaunchKernelGGL(k_points<true, 32>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
+      case 8: hipExtLaunchKernelGGL((k_points<true, 8, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
+      case 16: hipExtLaunchKernelGGL((k_points<true, 16, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
+      case 32: hipExtLaunchKernelGGL((k_points<true, 32, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
       default: return hipErrorInvalidValue;
     }
   } else {
-    hipExtLaunchKernelGGL(k_points<false, 1>, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials);
+    hipExtLaunchKernelGGL((k_points<false, 1, 1>), dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials);
   }
   if (fold) {
     GCS_FINAL(5, 16u, FIN_POINTS, nblk, s, e1, partials, a.scalars);
