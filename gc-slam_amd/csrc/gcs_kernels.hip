@@ -969,19 +969,38 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   PROF(2);
   // phase B: stage the tile's records (record r belongs to the last source with s_off <= r)
   if (staged) {
-    for (uint32_t r = t; r < total; r += NT) {
-      int lo = 0, hi = ns - 1;
-      while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (s_off[mid] <= r) lo = mid; else hi = mid - 1;
+    // at most RPT records per thread: every perm load is issued before any record load, so a
+    // tile with more records than threads still pays two dependent round trips, not 2 x RPT
+    constexpr int RPT = (STAGE + NT - 1) / NT;
+    uint32_t pi[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const uint32_t r = t + k * NT;
+      pi[k] = 0u;
+      if (r < total) {
+        int lo = 0, hi = ns - 1;
+        while (lo < hi) {
+          int mid = (lo + hi + 1) >> 1;
+          if (s_off[mid] <= r) lo = mid; else hi = mid - 1;
+        }
+        pi[k] = a.perm[s_st[lo] + (r - s_off[lo])];
       }
-      const PointRec pr = a.recs[a.perm[s_st[lo] + (r - s_off[lo])]];
-      double2* d = (double2*)(s_rec + (size_t)r * kRecD);
-      const uint32_t sw = rec_swz(r);
-      d[0 ^ sw] = make_double2(pr.x, pr.y);
-      d[1 ^ sw] = make_double2(pr.z, pr.dx);
-      d[2 ^ sw] = make_double2(pr.dy, pr.dz);
-      d[3 ^ sw] = make_double2(pr.m, pr.w * pr.iz);
+    }
+    PointRec pr[RPT];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k)
+      if (t + k * NT < total) pr[k] = a.recs[pi[k]];
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const uint32_t r = t + k * NT;
+      if (r < total) {
+        double2* d = (double2*)(s_rec + (size_t)r * kRecD);
+        const uint32_t sw = rec_swz(r);
+        d[0 ^ sw] = make_double2(pr[k].x, pr[k].y);
+        d[1 ^ sw] = make_double2(pr[k].z, pr[k].dx);
+        d[2 ^ sw] = make_double2(pr[k].dy, pr[k].dz);
+        d[3 ^ sw] = make_double2(pr[k].m, pr[k].w * pr[k].iz);
+      }
     }
   }
   __syncthreads();
