@@ -921,11 +921,35 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   // phase A
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
   if (t <= nb) s_q[t] = q_t;
-  for (int q = q0 + t; q < q1t; q += NT) s_rl[q - q0] = a.rknn_local[q];
-  for (int j = t; j < ns; j += NT) {
-    const int src = a.tile_src[s0 + j];
-    s_cnt[j] = a.counts[src];
-    s_st[j] = a.starts[src];
+  {
+    // fixed trip counts: every thread issues all of its table loads before the first LDS write,
+    // so the reverse-kNN entries (up to kMaxRl / NT per thread) cost one round trip, not one each,
+    // and the sources two (tile_src, then their counts / starts)
+    constexpr int RL = (kMaxRl + NT - 1) / NT, SR = (kMaxSrc + NT - 1) / NT;
+    uint16_t rl[RL];
+#pragma unroll
+    for (int k = 0; k < RL; ++k) {
+      const int q = q0 + t + k * NT;
+      rl[k] = q < q1t ? a.rknn_local[q] : (uint16_t)0;
+    }
+    int src[SR];
+#pragma unroll
+    for (int k = 0; k < SR; ++k) src[k] = t + k * NT < ns ? a.tile_src[s0 + t + k * NT] : 0;
+    uint32_t cn[SR], st[SR];
+#pragma unroll
+    for (int k = 0; k < SR; ++k) {
+      cn[k] = t + k * NT < ns ? a.counts[src[k]] : 0u;
+      st[k] = t + k * NT < ns ? a.starts[src[k]] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < RL; ++k)
+      if (q0 + t + k * NT < q1t) s_rl[t + k * NT] = rl[k];
+#pragma unroll
+    for (int k = 0; k < SR; ++k)
+      if (t + k * NT < ns) {
+        s_cnt[t + k * NT] = cn[k];
+        s_st[t + k * NT] = st[k];
+      }
   }
   __syncthreads();
   PROF(1);
