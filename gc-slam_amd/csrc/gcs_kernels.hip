@@ -332,13 +332,14 @@ void k_points(PointKernelArgs a, double* partials) {
           int4 u1 = CH == 2 && q + LP < nq ? pool[q + LP] : make_int4(-1, -1, -1, -1);
           int ids[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
           double s[8];
+          // branch-free: a guarded load per id compiled to one branch and one wait per id (the
+          // batch's loads went out one round trip at a time); padding ids (-1) read bin 0 and
+          // are masked to -inf after the loads
 #pragma unroll
           for (int u = 0; u < 4 * CH; ++u) {
-            s[u] = -INFINITY;
-            if (ids[u] >= 0) {
-              const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)ids[u]);
-              s[u] = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
-            }
+            const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)(ids[u] >= 0 ? ids[u] : 0));
+            const double sv = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
+            s[u] = ids[u] >= 0 ? sv : -INFINITY;
           }
 #pragma unroll
           for (int u = 0; u < 4 * CH; ++u)
