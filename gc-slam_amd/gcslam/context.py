@@ -257,8 +257,9 @@ class HypothesisContext:
     def hypothesis_combine(self, payload_sum, scan_count, want_belief=True):
         """Barycenter + IW update from the summed payload; returns (belief arrays or None, cert)."""
         p = np.ascontiguousarray(payload_sum, np.float64)
-        b = L.GcsBelief()
+        b = L.GcsBelief() if want_belief else None  # combined_out may be NULL (gcslam_hip.h)
         cert = np.empty(4)
-        self._chk(self.lib.gcs_hypothesis_combine(self.h, p.ctypes.data, int(scan_count), C.addressof(b), cert.ctypes.data),
+        self._chk(self.lib.gcs_hypothesis_combine(self.h, p.ctypes.data, int(scan_count),
+                                                  C.addressof(b) if want_belief else None, cert.ctypes.data),
                   "combine")
         return (L.struct_to_arrays(b) if want_belief else None), cert
