@@ -1333,7 +1333,14 @@ __device__ __forceinline__ void map_totals_partial(double (&tot)[kTotNV], double
 // (touched = 0: all-zero stats) stays exactly zero under forgetting + push, and its derived stats
 // keep the zero-bin constants: it is skipped (adds exact zeros to the totals).  act == nullptr
 // (dense mode): every bin is updated.
-__global__ __launch_bounds__(kBlock) void k_pushforward(const double* __restrict__ scan, double* __restrict__ map,
+#ifndef GCS_PUSH_WAVES
+#define GCS_PUSH_WAVES 0  // register target (waves per SIMD) of k_pushforward; 0: compiler default
+#endif
+__global__ __launch_bounds__(kBlock)
+#if GCS_PUSH_WAVES
+__attribute__((amdgpu_waves_per_eu(GCS_PUSH_WAVES)))
+#endif
+void k_pushforward(const double* __restrict__ scan, double* __restrict__ map,
                                                         double* __restrict__ derived, int B, PushArgs pa,
                                                         double* __restrict__ partials,
                                                         const uint8_t* __restrict__ act, uint8_t* __restrict__ touched) {
