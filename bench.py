@@ -50,6 +50,7 @@ def cpu_baseline(cfg, seconds_target=15.0):
     14-step scans at the same N, B, K on one host core."""
     sys.path.insert(0, ROOT)
     from gcslam import synthetic
+    from gcslam.synthetic import scan_kwargs
     from oracle import ops, pipeline as opipe
     N, B = cfg["N"], cfg["B"]
     bins = ops.fibonacci_atlas(B)
@@ -97,6 +98,7 @@ def main():
     torch.cuda.set_device(local_rank)
 
     from gcslam import synthetic
+    from gcslam.synthetic import scan_kwargs
     from gcslam.context import HypothesisContext
     from gcslam.distributed import combine_allreduce
 
@@ -129,8 +131,7 @@ def main():
             elif phase == 1:
                 ctx.enable_timing(False)
         sc, rec, t, w = scans[state["count"] % N_SCANS]
-        out = ctx.scan(rec, 16, t, w, N, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
-                       sc["scan_end_time"], sc["dt_sec"], t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"])
+        out = ctx.scan(rec, 16, t, w, N, **scan_kwargs(sc))
         tc = time.perf_counter()
         combine_allreduce(ctx, rank, world, state["count"], device=device, want_belief=False)
         host_ms[4] += (time.perf_counter() - tc) * 1e3

@@ -84,6 +84,12 @@ struct gcs_ctx {
   double* d_scalars = nullptr;
   double* h_scalars = nullptr;  // pinned, mapped
   double* d_scalars_mirror = nullptr;  // device view of h_scalars
+  // bucketing error words (pinned, mapped; BucketArgs.err): [0] look-back bound exhausted, [1]
+  // degenerate-bucket compaction taken.  Debug knobs (gcs_ctx_set_debug).
+  uint32_t* h_err = nullptr;
+  uint32_t* d_err = nullptr;
+  uint32_t spin_limit = 1u << 22;
+  int inject_scan_fail = 0;
   // host state
   Belief belief{};
   double iw_nu[7], iw_Psi[7 * 36], Q[DZ * DZ];
@@ -95,6 +101,8 @@ struct gcs_ctx {
   int budget_blocks = 0;
   bool budget_pending = false;  // k_budget already queued for the coming point stage (gcs_scan)
   std::vector<double> wimu, wint;  // IMU window weights: within-scan, scan-to-scan (scratch)
+  host::ImuOdomOut io;             // step 9 IMU/odometry evidence of the current scan (scratch)
+  double grav[3] = {0.0, 0.0, 0.0};  // gravity_W * imu_gravity_scale
   // device stage timing (hipEvents on the context stream; harvested lazily)
   uint32_t timing_mask = 0;
   bool pending = false;
@@ -382,6 +390,9 @@ int stage_bins(gcs_ctx* c) {
       ba.slot_idx = c->d_sorted;
       ba.perm = c->d_perm;
       ba.flags = c->d_flags;
+      ba.err = c->d_err;
+      ba.spin_limit = c->spin_limit;
+      ba.inject_scan_fail = c->inject_scan_fail;
       HIPCHK(c, launch_bucketing(ba, c->cap, s, ev.e0, ev.e1));
     }
     StageEv ev = stage_ev(c, ST_BINS);
@@ -438,11 +449,55 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, 
   return GCS_OK;
 }
 
+// after a stream sync: a k_scan whose look-back bound ran out left wrong bucket starts
+int check_bucket_err(gcs_ctx* c) {
+  if (c->h_err && c->h_err[0]) {
+    c->h_err[0] = 0u;
+    return fail(c, GCS_ERR_HIP, "k_scan: decoupled look-back exceeded its spin bound; bucket starts invalid, scan failed");
+  }
+  return GCS_OK;
+}
+
 int pull_scalars(gcs_ctx* c) {
   HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, SC_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
 }
+
+// The IMU/odometry branch from the quantities the reference reads (pipeline.py:442-566,595-776):
+// dt_int, dt_imu, omega_avg and the scan-to-scan preintegration, then the eleven factors.
+// extra = [dt_int, dt_imu, omega_avg(3)]
+void run_imu_odom(const gcs_imu_odom_inputs& in, host::ImuOdomOut& io, double* extra) {
+  const double dt_int = host::imu_integration_time(in.m, in.stamps, in.t_last_scan, in.t_scan);
+  double dt_imu, om[3];
+  host::imu_rate_stats(in.m, in.stamps, in.gyro, in.w_int, in.mu_inc + 9, &dt_imu, om);
+  host::PreintOut pre;
+  host::preintegrate_imu(in.m, in.stamps, in.gyro, in.accel, in.w_int, in.pose0 + 3, in.mu_inc + 9, in.mu_inc + 12,
+                         in.gravity_W, pre);
+  host::ImuOdomInputs a{};
+  a.m = in.m;
+  a.stamps = in.stamps; a.gyro = in.gyro; a.accel = in.accel; a.w_int = in.w_int;
+  a.dt_imu = dt_imu; a.dt_int = dt_int; a.dt_sec = in.dt_sec;
+  a.omega_avg = om;
+  a.drot_int = pre.delta_pose + 3; a.dp_int = pre.delta_pose; a.dv_int = pre.delta_v;
+  a.pose0 = in.pose0; a.pose_pred = in.pose_pred; a.mu_prev = in.mu_prev; a.mu_inc = in.mu_inc;
+  a.accel_bias = in.mu_inc + 12;
+  a.gravity = in.gravity_W;
+  a.Sigma_g = in.Sigma_g; a.Sigma_a = in.Sigma_a;
+  a.odom_pose = in.odom_pose; a.odom_cov = in.odom_cov_se3; a.odom_twist = in.odom_twist;
+  a.odom_twist_cov = in.odom_twist_cov;
+  a.planar_z_ref = in.planar_z_ref; a.planar_z_sigma = in.planar_z_sigma; a.planar_vz_sigma = in.planar_vz_sigma;
+  host::imu_odom_branch(a, io);
+  if (extra) { extra[0] = dt_int; extra[1] = dt_imu; extra[2] = om[0]; extra[3] = om[1]; extra[4] = om[2]; }
+}
+
+// node defaults when no odometry has arrived (backend_node.py:939-940,2047-2051)
+const double kZero6[6] = {0, 0, 0, 0, 0, 0};
+struct BigCov6 {
+  double v[36];
+  BigCov6() { for (int i = 0; i < 36; ++i) v[i] = (i % 7 == 0) ? 1e12 : 0.0; }
+};
+const BigCov6 kBigCov6;
 
 double trig(double lift, double psd, double nu, double mer, double rho, double dts, double exs, double alpha, double beta) {
   return lift + psd + nu + mer + rho + fabs(1.0 - dts) + fabs(1.0 - exs) + fabs(1.0 - alpha) + fabs(1.0 - beta);
@@ -456,11 +511,38 @@ const char* gcs_version(void) { return "gcslam-mi355x 0.1.0 (gfx950)"; }
 int gcs_abi_version(void) { return GCS_ABI_VERSION; }
 const char* gcs_last_error(const gcs_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
+int gcs_config_defaults(gcs_config* c) {
+  if (!c) return GCS_ERR_ARG;
+  memset(c, 0, sizeof(*c));
+  c->n_bins = 48;            // legacy B_BINS (CHANGELOG.md:492)
+  c->n_points_cap = 8192;    // constants.py:64
+  c->max_raw_points = 1 << 16;
+  c->mode = GCS_MODE_DENSE;
+  c->k_cand = 16;
+  c->tau = 0.1;              // DECLARED tau at B = 48
+  c->forgetting_factor = 0.99;
+  c->gravity_W[2] = -9.81;   // constants.py:80
+  c->use_imu_odom = 1;
+  c->imu_gravity_scale = 1.0;
+  c->planar_z_ref = 0.0;
+  c->planar_z_sigma = 0.1;
+  c->planar_vz_sigma = 0.01;
+  c->alpha_min = 1.0;
+  c->alpha_max = 1.0;
+  c->c0_cond = 1e6;
+  return GCS_OK;
+}
+
 int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (!cfg || !out) return GCS_ERR_ARG;
   *out = nullptr;
+  if (!(cfg->planar_z_sigma > 0.0) || !(cfg->planar_vz_sigma > 0.0) || !(cfg->alpha_min <= cfg->alpha_max) ||
+      !(cfg->c0_cond > 0.0))
+    return GCS_ERR_ARG;  // gcs_config_defaults() fills these
   if (cfg->n_bins < 1 || cfg->n_points_cap < 1 || cfg->max_raw_points < 0) return GCS_ERR_ARG;
-  if (cfg->mode == GCS_MODE_SCALE && (cfg->k_cand < 1 || cfg->k_cand > 32 || cfg->k_cand > cfg->n_bins)) return GCS_ERR_ARG;
+  // scale mode: the point kernel is instantiated for K = 8, 16, 32 and the bucketing reads kNN rows as int4
+  if (cfg->mode == GCS_MODE_SCALE && ((cfg->k_cand != 8 && cfg->k_cand != 16 && cfg->k_cand != 32) || cfg->k_cand > cfg->n_bins))
+    return GCS_ERR_ARG;
   if (!(cfg->tau > 0.0)) return GCS_ERR_ARG;
   gcs_ctx* c = new gcs_ctx();
   c->cfg = *cfg;
@@ -468,6 +550,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   c->cap = cfg->n_points_cap;
   c->K = cfg->mode == GCS_MODE_SCALE ? cfg->k_cand : 0;
   c->max_raw = cfg->max_raw_points;
+  for (int k = 0; k < 3; ++k) c->grav[k] = cfg->gravity_W[k] * cfg->imu_gravity_scale;
   auto bad = [&](hipError_t e) {
     if (e != hipSuccess) {
       gcs_ctx_destroy(c);
@@ -502,6 +585,9 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMemset(c->d_tickets, 0, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocMapped))) return GCS_ERR_HIP;
   if (bad(hipHostGetDevicePointer((void**)&c->d_scalars_mirror, c->h_scalars, 0))) return GCS_ERR_HIP;
+  if (bad(hipHostMalloc(&c->h_err, 2 * sizeof(uint32_t), hipHostMallocMapped))) return GCS_ERR_HIP;
+  c->h_err[0] = c->h_err[1] = 0u;
+  if (bad(hipHostGetDevicePointer((void**)&c->d_err, c->h_err, 0))) return GCS_ERR_HIP;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_rknn_off, (B + 1) * sizeof(int)))) return GCS_ERR_HIP;
@@ -514,6 +600,9 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMemset(c->d_counts, 0, (size_t)c->n_counts_words * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_starts, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_perm, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    // zeroed so every slot holds a valid point index even when a failed scan leaves holes
+    if (bad(hipMemset(c->d_perm, 0, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMemset(c->d_sorted, 0, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     // bin flags, then one flag per k_bins_scale tile (both cleared by k_budget every scan)
     const size_t nflags = B + bins_scale_blocks(c->B);
     if (bad(hipMalloc(&c->d_flags_buf[0], 2 * nflags))) return GCS_ERR_HIP;
@@ -561,6 +650,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
+  if (c->h_err) (void)hipHostFree(c->h_err);
   for (int st = 0; st < kStages; ++st)
     for (int k = 0; k < 2; ++k)
       if (c->ev[st][k]) (void)hipEventDestroy(c->ev[st][k]);
@@ -575,6 +665,7 @@ int gcs_ctx_set_stream(gcs_ctx* c, void* s) {
   if (!c) return GCS_ERR_ARG;
   HIPCHK(c, hipStreamSynchronize(c->push_stream));
   c->push_pending = false;
+  if (c->stream) HIPCHK(c, hipStreamSynchronize(c->stream));  // work queued on the old stream completes first
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   c->stream = (hipStream_t)s;
   c->own_stream = false;
@@ -586,6 +677,21 @@ int gcs_ctx_synchronize(gcs_ctx* c) {
   join_push(c);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
+}
+
+int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
+  if (!c) return GCS_ERR_ARG;
+  switch (key) {
+    case GCS_DEBUG_SCAN_SPIN_LIMIT:
+      if (value < 0 || value > 0xffffffffLL) return fail(c, GCS_ERR_ARG, "spin limit out of range");
+      c->spin_limit = (uint32_t)value;
+      return GCS_OK;
+    case GCS_DEBUG_INJECT_SCAN_FAIL:
+      c->inject_scan_fail = value ? 1 : 0;
+      return GCS_OK;
+    default:
+      return fail(c, GCS_ERR_ARG, "unknown debug key");
+  }
 }
 
 int gcs_ctx_enable_timing(gcs_ctx* c, int32_t stage_mask) {
@@ -820,6 +926,7 @@ int gcs_scan_bin_moment_match(gcs_ctx* c, double* cert) {
   int rc = stage_bins(c);
   if (rc) return rc;
   if ((rc = pull_scalars(c))) return rc;
+  if ((rc = check_bucket_err(c))) return rc;
   if (cert)
     for (int k = 0; k < 5; ++k) cert[k] = c->h_scalars[SC_BIN_NSUM + k];
   return GCS_OK;
@@ -906,7 +1013,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   host::world_pose_from_increment(prev, mu_prev, pose0);
   host::PreintOut pre;
   host::preintegrate_imu(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wimu.data(), pose0 + 3, mu_inc + 9,
-                         mu_inc + 12, c->cfg.gravity_W, pre);
+                         mu_inc + 12, c->grav, pre);
   double xi[6];
   host::se3_log(pre.delta_pose, xi);
   if (c->cfg.deskew_rotation_only) xi[0] = xi[1] = xi[2] = 0.0;
@@ -924,13 +1031,48 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   // 13 measurement-noise IW statistics over the scan-to-scan IMU window (pipeline.py:448-453,
   // 522-566), computed while the device stages run (they need no device result); padded samples
   // (stamp <= 0) carry weight 0 (the reference's valid mask)
+  // w_imu_int unmasked as in the reference (padding gets the 1e-12 floor); the IW statistics mask
+  // stamps <= 0 themselves
   std::vector<double>& wint = c->wint;
   wint.resize(in->imu_len);
   for (int i = 0; i < in->imu_len; ++i)
-    wint[i] = in->imu_stamps[i] > 0.0 ? smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, sigma_warp) : 0.0;
+    wint[i] = smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, sigma_warp);
   host::imu_meas_iw_suffstats(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wint.data(), mu_inc + 9,
-                              mu_inc + 12, pose0 + 3, c->cfg.gravity_W, out->iw_meas_dPsi, out->iw_meas_dnu);
+                              mu_inc + 12, pose0 + 3, c->grav, out->iw_meas_dPsi, out->iw_meas_dnu);
+  // 9 (pipeline.py:595-776) IMU/odometry evidence, also while the device stages run
+  double pose_pred[6];
+  host::world_pose_from_increment(pred, mu_inc, pose_pred);
+  const bool use_io = c->cfg.use_imu_odom != 0;
+  double io_extra[5] = {0, 0, 0, 0, 0};
+  if (use_io) {
+    if (in->imu_len < 2) return fail(c, GCS_ERR_ARG, "IMU window of at least 2 samples required");
+    double Sg[9], Sa[9];
+    if (in->Sigma_g) memcpy(Sg, in->Sigma_g, sizeof(Sg)); else host::meas_iw_mode(c->meas_nu, c->meas_Psi, 0, Sg);
+    if (in->Sigma_a) memcpy(Sa, in->Sigma_a, sizeof(Sa)); else host::meas_iw_mode(c->meas_nu, c->meas_Psi, 1, Sa);
+    gcs_imu_odom_inputs ii{};
+    ii.m = in->imu_len;
+    ii.stamps = in->imu_stamps; ii.gyro = in->imu_gyro; ii.accel = in->imu_accel; ii.w_int = wint.data();
+    ii.t_last_scan = in->t_last_scan; ii.t_scan = in->t_scan; ii.dt_sec = in->dt_sec;
+    ii.pose0 = pose0; ii.pose_pred = pose_pred; ii.mu_prev = mu_prev; ii.mu_inc = mu_inc;
+    ii.gravity_W = c->grav;
+    ii.Sigma_g = Sg; ii.Sigma_a = Sa;
+    ii.odom_pose = in->odom_pose ? in->odom_pose : kZero6;
+    ii.odom_cov_se3 = in->odom_cov_se3 ? in->odom_cov_se3 : kBigCov6.v;
+    ii.odom_twist = in->odom_twist ? in->odom_twist : kZero6;
+    ii.odom_twist_cov = in->odom_twist_cov ? in->odom_twist_cov : kBigCov6.v;
+    ii.planar_z_ref = c->cfg.planar_z_ref; ii.planar_z_sigma = c->cfg.planar_z_sigma;
+    ii.planar_vz_sigma = c->cfg.planar_vz_sigma;
+    run_imu_odom(ii, c->io, io_extra);
+    for (int k = 0; k < DZ * DZ; ++k)
+      if (!std::isfinite(c->io.L[k])) return fail(c, GCS_ERR_NONFINITE, "IMU/odometry evidence contains NaN");
+  } else {
+    memset(c->io.L, 0, sizeof(c->io.L));
+    memset(c->io.h, 0, sizeof(c->io.h));
+  }
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the PT fold has written the scalars to h_scalars
+  if ((rc = check_bucket_err(c))) return rc;
+  cert[41] = c->h_err[1] ? 1.0 : 0.0;  // a bucket above the ranking capacity took the compaction path
+  c->h_err[1] = 0u;
   for (int k = 0; k < 27; ++k)
     if (!std::isfinite(out->iw_meas_dPsi[k])) return fail(c, GCS_ERR_NONFINITE, "omega_avg / IMU residuals non-finite");
   memcpy(c->last_meas_dPsi, out->iw_meas_dPsi, sizeof(c->last_meas_dPsi));
@@ -964,8 +1106,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   cert[17] = S[SC_BIN_EPSR];
   Tsum += S[SC_BIN_PSD] + S[SC_BIN_EPSR];
   // 7 MatrixFisherRotation tail (matrix_fisher_evidence.py:240-256,310-394)
-  double pose_pred[6], R_pred[9];
-  host::world_pose_from_increment(pred, mu_inc, pose_pred);
+  double R_pred[9];
   so3_exp(pose_pred + 3, R_pred);
   double Umf[9], sv[3], V[9];
   svd3(S + SC_MF_H, Umf, sv, V);  // L_rot needs s and V (host, same 3x3 SVD code as the device)
@@ -1021,8 +1162,21 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   memcpy(out->t_wls, twls, sizeof(out->t_wls));
   // 9 evidence (build_combined_lidar_evidence_22d) + external + power tempering (pipeline.py:1038-1117)
   double Lraw[DZ * DZ], hraw[DZ];
-  for (int i = 0; i < DZ * DZ; ++i) Lraw[i] = in->L_ext ? in->L_ext[i] : 0.0;
-  for (int i = 0; i < DZ; ++i) hraw[i] = in->h_ext ? in->h_ext[i] : 0.0;
+  for (int i = 0; i < DZ * DZ; ++i) Lraw[i] = (in->L_ext ? in->L_ext[i] : 0.0) + c->io.L[i];
+  for (int i = 0; i < DZ; ++i) hraw[i] = (in->h_ext ? in->h_ext[i] : 0.0) + c->io.h[i];
+  memcpy(out->L_imu_odom, c->io.L, sizeof(out->L_imu_odom));
+  {
+    const host::EvCert* cs[11] = {&c->io.odom, &c->io.imu, &c->io.dep, &c->io.gyro, &c->io.preint, &c->io.planar,
+                                  &c->io.vz, &c->io.vel, &c->io.wz, &c->io.kin, &c->io.odom_dep};
+    for (int k = 0; k < 11; ++k) {
+      double* o = out->imu_odom_certs + 7 * k;
+      if (!use_io) { for (int j = 0; j < 7; ++j) o[j] = 0.0; continue; }
+      o[0] = cs[k]->ess; o[1] = cs[k]->support; o[2] = cs[k]->nll; o[3] = cs[k]->lift; o[4] = cs[k]->psd;
+      o[5] = cs[k]->mer; o[6] = cs[k]->trust_alpha;
+    }
+  }
+  memcpy(out->h_imu_odom, c->io.h, sizeof(out->h_imu_odom));
+  if (use_io) Tsum += c->io.trigger;  // the eleven IMU/odometry certs are in all_certs (pipeline.py:964)
   for (int i = 0; i < 3; ++i) {
     hraw[i] += htr[i];
     hraw[3 + i] += hrot[i];
@@ -1041,8 +1195,12 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   double dt_asym = fabs(dt_vel - dt_pose) / (dt_vel + dt_pose + kEpsMass);
   dt_asym = std::min(std::max(dt_asym, 0.0), 1.0);
   double z_to_xy = fabs(Lraw[2 * DZ + 2]) / (0.5 * (fabs(Lraw[0]) + fabs(Lraw[DZ + 1])) + kEpsMass);
-  // combined evidence cert: aggregate of the LiDAR certs [deskew, soft assign, moment match, MF, planar]
-  double ess_total = (pre.ess + cert[12] + mm_ess + 0.0 + 0.0) / 5.0;
+  // combined evidence cert (pipeline.py:1057-1067): aggregate([aggregate(LiDAR certs [deskew, soft
+  // assign, moment match, MF, planar]), odom, imu, gyro]); ExcitationCert is never filled -> 0
+  const double ev_ess = (pre.ess + cert[12] + mm_ess + 0.0 + 0.0) / 5.0;
+  const double ev_nll = cert[24] / (mf_neff + kEpsMass) + cert[29] / (pt_neff + kEpsMass);
+  const double ess_total = use_io ? (ev_ess + c->io.odom.ess + c->io.imu.ess + c->io.gyro.ess) / 4.0 : ev_ess;
+  const double nll_total = use_io ? ev_nll + c->io.odom.nll + c->io.imu.nll + c->io.gyro.nll : ev_nll;
   double ess_to_exc = ess_total / (0.0 + kEpsMass);
   double s_z = z_to_xy / (z_to_xy + 1.0);
   double s_exc = 1.0 / (1.0 + ess_to_exc / 50.0);
@@ -1067,9 +1225,29 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   for (int r = 16; r < 22; ++r) pred.h[r] *= a_ex;
   cert[31] = s_dt; cert[32] = s_ex;
   Tsum += fabs(s_dt) + fabs(s_ex);
-  // 10 FusionScaleFromCertificates: alpha_min = alpha_max = 1 (constants.py:89-90)
-  const double alpha = 1.0;
+  // 10 FusionScaleFromCertificates on the pose-6 conditioning of the tempered evidence
+  // (pipeline.py:1150-1192, fusion.py:46-142)
+  double c6min, c6max, c6cond, c6nn, quality;
+  host::pose6_conditioning(Lev, &c6min, &c6max, &c6cond, &c6nn);
+  const double alpha = host::fusion_scale(c6cond, ess_total, nll_total, beta, dt_asym, z_to_xy, 0.0, c->cfg.alpha_min,
+                                          c->cfg.alpha_max, c->cfg.c0_cond, &quality);
   cert[33] = alpha;
+  Tsum += fabs(1.0 - alpha);
+  cert[42] = use_io ? c->io.trigger : 0.0;
+  cert[43] = io_extra[0];            // dt_int
+  cert[44] = io_extra[1];            // dt_imu
+  cert[45] = c->io.transport_sigma;
+  cert[46] = c->io.kappa;            // IMU gravity vMF kappa
+  cert[47] = c->io.imu_scale;        // imu_dependence_inflation scale
+  cert[48] = c->io.odom_scale;       // odom_dependence_inflation scale
+  cert[49] = c6cond;                 // pose-6 conditioning
+  cert[50] = c6nn;
+  cert[51] = ess_total;
+  cert[52] = quality;
+  cert[53] = c->io.ess_weighted;
+  cert[54] = c->io.mean_reliability;
+  cert[55] = nll_total;
+  cert[56] = io_extra[4];            // omega_avg z
   // 11 InfoFusionAdditive (fusion.py:186-191)
   Belief post = pred;
   double Lsum[DZ * DZ];
@@ -1199,6 +1377,104 @@ int gcs_hypothesis_combine(gcs_ctx* c, const double* p, int32_t scan_count, gcs_
   return GCS_OK;
 }
 
+int gcs_hypothesis_barycenter(int32_t n, const double* Ls, const double* hs, const double* zs, const double* w,
+                              double* Lo, double* ho, double* zo, double* cert) {
+  if (n < 1 || !Ls || !hs || !zs || !w || !Lo || !ho || !zo) return GCS_ERR_ARG;
+  std::vector<double> wn(n);
+  double wsum = 0.0, floor_adj = 0.0;
+  for (int k = 0; k < n; ++k) {  // weight floor + renormalise (hypothesis.py:83-87)
+    const double wf = std::max(w[k], 0.0025);
+    floor_adj += fabs(wf - w[k]);
+    wn[k] = wf;
+    wsum += wf;
+  }
+  for (int k = 0; k < n; ++k) wn[k] /= wsum;
+  double Lr[DZ * DZ] = {};
+  for (int i = 0; i < DZ; ++i) { ho[i] = 0.0; zo[i] = 0.0; }
+  for (int k = 0; k < n; ++k) {  // barycenter (:92-99)
+    for (int i = 0; i < DZ * DZ; ++i) Lr[i] += wn[k] * Ls[(size_t)k * DZ * DZ + i];
+    for (int i = 0; i < DZ; ++i) {
+      ho[i] += wn[k] * hs[(size_t)k * DZ + i];
+      zo[i] += wn[k] * zs[(size_t)k * DZ + i];
+    }
+  }
+  double c6[6];
+  host::psd_project(DZ, Lr, kEpsPsd, Lo, c6);
+  // spread proxy (:103-115): sum w ||mu_k - sum w mu||^2
+  std::vector<double> mus((size_t)n * DZ);
+  double mom[DZ] = {};
+  for (int k = 0; k < n; ++k) {
+    host::spd_solve_lifted(DZ, Ls + (size_t)k * DZ * DZ, hs + (size_t)k * DZ, kEpsLift, &mus[(size_t)k * DZ]);
+    for (int i = 0; i < DZ; ++i) mom[i] += wn[k] * mus[(size_t)k * DZ + i];
+  }
+  double spread = 0.0, ess_den = 0.0, supp = 0.0;
+  for (int k = 0; k < n; ++k) {
+    double d2 = 0.0;
+    for (int i = 0; i < DZ; ++i) {
+      const double d = mus[(size_t)k * DZ + i] - mom[i];
+      d2 += d * d;
+    }
+    spread += wn[k] * d2;
+    ess_den += wn[k] * wn[k];
+    supp += wn[k] > 0.0025 ? 1.0 : 0.0;
+  }
+  if (cert) {
+    cert[0] = c6[0]; cert[1] = floor_adj; cert[2] = 1.0 / ess_den; cert[3] = supp / n; cert[4] = spread; cert[5] = c6[4];
+  }
+  return GCS_OK;
+}
+
+int gcs_process_iw_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double* nu_out,
+                         double* Psi_out, double* cert2) {
+  if (!nu || !Psi || !dPsi || !dnu || !nu_out || !Psi_out) return GCS_ERR_ARG;
+  double c2[2];
+  host::process_iw_apply(nu, Psi, dPsi, dnu, nu_out, Psi_out, c2);
+  if (cert2) { cert2[0] = c2[0]; cert2[1] = c2[1]; }
+  return GCS_OK;
+}
+
+int gcs_process_noise_Q(const double* nu, const double* Psi, double* Q) {
+  if (!nu || !Psi || !Q) return GCS_ERR_ARG;
+  host::process_noise_Q(nu, Psi, Q);
+  return GCS_OK;
+}
+
+int gcs_meas_iw_mode(const double* nu, const double* Psi, int32_t idx, double* Sigma) {
+  if (!nu || !Psi || !Sigma || idx < 0 || idx > 2) return GCS_ERR_ARG;
+  host::meas_iw_mode(nu, Psi, idx, Sigma);
+  return GCS_OK;
+}
+
+int gcs_ctx_describe(gcs_ctx* c, char* buf, int32_t len) {
+  if (!c || !buf || len < 1) return GCS_ERR_ARG;
+  const gcs_config& f = c->cfg;
+  const bool scale = f.mode == GCS_MODE_SCALE;
+  char tmp[2048];
+  int n = snprintf(tmp, sizeof(tmp),
+      "{\"library\": \"%s\", \"abi\": %d, \"device\": %d, \"arch\": \"gfx950\", \"N_POINTS_CAP\": %d, "
+      "\"B_BINS\": %d, \"soft_assign_mode\": \"%s\", \"k_cand\": %d, \"tau_soft_assign\": %.17g, "
+      "\"tau_rule\": \"tau_B = 0.1 * 48 / B (declared)\", \"candidate_rule\": \"%s\", "
+      "\"map_mode\": \"per-hypothesis MapBinStats (declared; reference couples through hypothesis 0)\", "
+      "\"pushforward_form\": \"gamma forgetting + N[R(Sigma_p + pbar pbar^T)R^T + J Sigma_pose J^T + q q^T - u u^T], t_z := 0 (declared)\", "
+      "\"forgetting_factor\": %.17g, \"deskew_rotation_only\": %s, \"gravity_W\": [%.17g, %.17g, %.17g], "
+      "\"imu_gravity_scale\": %.17g, \"use_imu_odom\": %s, \"planar_z_ref\": %.17g, \"planar_z_sigma\": %.17g, "
+      "\"planar_vz_sigma\": %.17g, \"alpha_min\": %.17g, \"alpha_max\": %.17g, \"c0_cond\": %.17g, "
+      "\"eps_psd\": 1e-12, \"eps_lift\": 1e-09, \"eps_mass\": 1e-12, \"eps_r\": 1e-06, "
+      "\"power_beta_min\": 0.25, \"power_beta_exc_c\": 50, \"power_beta_z_c\": 1, \"c_frob\": 1, "
+      "\"MAX_IMU_PREINT_LEN\": 512, \"precision\": \"f64 state and accumulation, f32 xyz stream\", "
+      "\"backends\": {\"points\": \"k_points (HIP)\", \"moment_match\": \"%s\", \"pushforward\": \"k_pushforward (HIP)\", "
+      "\"tail_22d\": \"host C++\", \"imu_odom_evidence\": \"host C++ (gcs_evidence.cpp)\", "
+      "\"hypothesis_combine\": \"payload sum all-reduce (RCCL) + host apply\"}}",
+      gcs_version(), GCS_ABI_VERSION, f.device, f.n_points_cap, f.n_bins, scale ? "scale" : "dense", scale ? f.k_cand : 0,
+      f.tau, scale ? "K nearest atlas bins of the exact nearest bin, ties -> lower id (declared)" : "dense N x B softmax (reference)",
+      f.forgetting_factor, f.deskew_rotation_only ? "true" : "false", f.gravity_W[0], f.gravity_W[1], f.gravity_W[2],
+      f.imu_gravity_scale, f.use_imu_odom ? "true" : "false", f.planar_z_ref, f.planar_z_sigma, f.planar_vz_sigma,
+      f.alpha_min, f.alpha_max, f.c0_cond, scale ? "bucketing + k_bins_scale (HIP)" : "k_dense_accum + k_dense_finalize (HIP)");
+  if (n < 0 || n >= len) return fail(c, GCS_ERR_ARG, "describe buffer too short");
+  memcpy(buf, tmp, (size_t)n + 1);
+  return GCS_OK;
+}
+
 // ---------------------------------------------------------------- host numerics
 int gcs_psd_project(int32_t n, const double* M, double eps, double* out, double* cert6) {
   if (n < 1 || n > host::kMaxN || !M || !out) return GCS_ERR_ARG;
@@ -1220,6 +1496,27 @@ int gcs_svd3(const double* H, double* U, double* s, double* V) {
   svd3(H, U, s, V);
   return GCS_OK;
 }
+int gcs_imu_odom_evidence(const gcs_imu_odom_inputs* in, double* L, double* h, double* cert) {
+  if (!in || !L || !h || in->m < 2 || !in->stamps || !in->gyro || !in->accel || !in->w_int || !in->pose0 ||
+      !in->pose_pred || !in->mu_prev || !in->mu_inc || !in->gravity_W || !in->Sigma_g || !in->Sigma_a ||
+      !in->odom_pose || !in->odom_cov_se3 || !in->odom_twist || !in->odom_twist_cov || !(in->planar_z_sigma > 0.0) ||
+      !(in->planar_vz_sigma > 0.0))
+    return GCS_ERR_ARG;
+  host::ImuOdomOut* io = new host::ImuOdomOut();
+  double ex[5];
+  run_imu_odom(*in, *io, ex);
+  memcpy(L, io->L, sizeof(io->L));
+  memcpy(h, io->h, sizeof(io->h));
+  if (cert) {
+    const double v[GCS_IMU_ODOM_CERT_LEN] = {io->trigger, io->ess_weighted, io->kappa, io->transport_sigma,
+                                             io->imu_scale, io->odom_scale, io->mean_reliability, io->odom.nll,
+                                             io->imu.nll, io->gyro.nll, ex[0], ex[1], ex[2], ex[3], ex[4]};
+    memcpy(cert, v, sizeof(v));
+  }
+  delete io;
+  return GCS_OK;
+}
+
 int gcs_imu_meas_iw_suffstats(int32_t m, const double* stamps, const double* gyro, const double* accel,
                               const double* w_int, const double* gb, const double* ab, const double* rv,
                               const double* g, double* dPsi, double* dnu) {

@@ -241,6 +241,16 @@ void se3_compose(const double* a, const double* b, double* out) {
   so3_log(R, out + 3);
 }
 
+// se3_inverse, se3_jax.py:427-438
+void se3_inverse(const double* a, double* out) {
+  double R[9], Rt[9];
+  so3_exp(a + 3, R);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Rt[3 * i + j] = R[3 * j + i];
+  for (int i = 0; i < 3; ++i) out[i] = -(Rt[3 * i] * a[0] + Rt[3 * i + 1] * a[1] + Rt[3 * i + 2] * a[2]);
+  so3_log(Rt, out + 3);
+}
+
 // se3_log, se3_jax.py:210-245 (with _se3_V_inv, :169-207)
 void se3_log(const double* T, double* out) {
   double R[9], phi[3];
@@ -342,6 +352,7 @@ void preintegrate_imu(int m, const double* stamps, const double* gyro, const dou
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) dR[3 * i + j] = R0[i] * R[j] + R0[3 + i] * R[3 + j] + R0[6 + i] * R[6 + j];
   for (int i = 0; i < 3; ++i) out.delta_pose[i] = R0[i] * p[0] + R0[3 + i] * p[1] + R0[6 + i] * p[2];
+  for (int i = 0; i < 3; ++i) out.delta_v[i] = R0[i] * v[0] + R0[3 + i] * v[1] + R0[6 + i] * v[2];
   so3_log(dR, out.delta_pose + 3);
   out.ess = ess;
 }

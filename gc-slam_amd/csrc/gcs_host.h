@@ -41,6 +41,7 @@ struct Belief {
 };
 
 void se3_compose(const double* a, const double* b, double* out);
+void se3_inverse(const double* a, double* out);
 void se3_log(const double* T, double* out);
 void mean_increment(const Belief& b, double* dz);
 void mean_world_pose(const Belief& b, double* pose6);
@@ -52,7 +53,8 @@ void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& p
                        double* mean_prev_out = nullptr /*DZ, optional: prev's mean increment*/);
 
 struct PreintOut {
-  double delta_pose[6];
+  double delta_pose[6];  // [R0^T p, Log(R0^T R_end)]: delta_pose[0:3] is delta_p_body
+  double delta_v[3];     // R0^T v_end
   double ess;
 };
 void preintegrate_imu(int m, const double* stamps, const double* gyro, const double* accel, const double* w,
@@ -79,6 +81,50 @@ void meas_iw_apply(const double* nu, const double* Psi, const double* dPsi, cons
                    double* Psi_out, double* cert2);
 
 void bch3(const double* xi1, const double* xi2, double* out);
+
+// ---------------------------------------------------------------- step 9 IMU / odometry family
+// (gcs_evidence.cpp; FS/backend/pipeline.py:595-776)
+// The CertBundle fields the pipeline reads back from one operator (FS/common/certificates.py:22-109):
+// support, mismatch and the influence fields of total_trigger_magnitude (identity defaults).
+struct EvCert {
+  double ess = 0.0, support = 1.0, nll = 0.0;
+  double lift = 0.0, psd = 0.0, mer = 0.0, trust_alpha = 1.0;
+};
+struct ImuOdomInputs {
+  int m;                                  // IMU window length (>= 2)
+  const double *stamps, *gyro, *accel;    // [m], [m*3], [m*3]
+  const double* w_int;                    // scan-to-scan window weights [m] (unmasked)
+  double dt_imu, dt_int, dt_sec;
+  const double* omega_avg;                // [3] (pipeline.py:536-548)
+  const double* drot_int;                 // scan-to-scan preintegration: delta rotvec [3]
+  const double* dp_int;                   //   delta p (start body frame) [3]
+  const double* dv_int;                   //   delta v (start body frame) [3]
+  const double* pose0;                    // belief_prev.mean_world_pose [6]
+  const double* pose_pred;                // belief_pred.mean_world_pose [6]
+  const double* mu_prev;                  // belief_prev.mean_increment [22]
+  const double* mu_inc;                   // belief_pred.mean_increment [22]
+  const double* accel_bias;               // mu_inc[12:15]
+  const double* gravity;                  // gravity_W * imu_gravity_scale
+  const double *Sigma_g, *Sigma_a;        // 3x3
+  const double *odom_pose, *odom_cov;     // [6], 6x6
+  const double *odom_twist, *odom_twist_cov;  // [6], 6x6
+  double planar_z_ref, planar_z_sigma, planar_vz_sigma;
+};
+struct ImuOdomOut {
+  double L[DZ * DZ], h[DZ];  // L_imu_odom, h_imu_odom (pipeline.py:745-750)
+  EvCert odom, imu, dep, gyro, preint, planar, vz, vel, wz, kin, odom_dep;  // all_certs order
+  double trigger;            // sum of the eleven certs' trigger magnitudes
+  double kappa, transport_sigma, ess_weighted, mean_reliability, imu_scale, odom_scale;
+};
+double imu_integration_time(int m, const double* stamps, double t_start, double t_end);
+void imu_rate_stats(int m, const double* stamps, const double* gyro, const double* w_int, const double* gyro_bias,
+                    double* dt_imu, double* omega_avg);
+void meas_iw_mode(const double* nu3, const double* Psi3x9, int idx, double* Sigma3x3);
+double kappa_scalar(double R_bar);
+void imu_odom_branch(const ImuOdomInputs& in, ImuOdomOut& out);
+double fusion_scale(double cond, double ess, double nll, double power_beta, double dt_asym, double z_to_xy,
+                    double excitation_total, double alpha_min, double alpha_max, double c0_cond, double* quality);
+void pose6_conditioning(const double* L_ev, double* eig_min, double* eig_max, double* cond, double* near_null);
 
 }  // namespace host
 }  // namespace gcs

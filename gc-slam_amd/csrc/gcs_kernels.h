@@ -81,6 +81,12 @@ struct BucketArgs {
   uint32_t* slot_idx;     // bucket-ordered point indices, arrival order within a bucket
   uint32_t* perm;         // bucket-ordered point indices, point-index order within a bucket
   uint8_t* flags;         // active bins (cleared by k_budget)
+  // error words in host-mapped memory, written only on the rare paths: [0] k_scan look-back spin
+  // bound exhausted (the scan's bucket starts are invalid -> gcs_scan fails), [1] k_bucket_rank took
+  // the in-order compaction path for a bucket above kRankMax members (correct, degenerate; reported)
+  uint32_t* err;
+  uint32_t spin_limit;    // look-back spin bound (gcs_ctx_set_debug; default 1 << 22)
+  int inject_scan_fail;   // test hook: tile 1 behaves as if its look-back bound were exhausted
 };
 
 struct BinKernelArgs {

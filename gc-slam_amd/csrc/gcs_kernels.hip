@@ -494,7 +494,8 @@ constexpr int kRankMax = 8192;
 constexpr uint32_t kLbAgg = 1u << 30, kLbPre = 2u << 30, kLbVal = (1u << 30) - 1u;
 
 __global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restrict__ counts, int n, uint32_t* status,
-                                                       uint32_t* ticket, uint32_t* start) {
+                                                       uint32_t* ticket, uint32_t* start, uint32_t* err,
+                                                       uint32_t spin_limit, int inject_fail) {
   constexpr int kSW = kScanThreads / 64;
   __shared__ uint32_t wsum[kSW];
   __shared__ uint32_t s_tile, s_excl;
@@ -533,8 +534,12 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restric
     } else {
       if (lane == 0) __hip_atomic_store(status + tile, kLbAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // look back in windows of 64 predecessors: lane l reads tile (w0 - l)
+      // On spin exhaustion the tile reports failure and continues with excl = 0: every start then
+      // stays below the scan's point count, so k_place / k_bucket_rank / k_bins_scale index in
+      // bounds (with wrong bucket ranges) and the host fails the scan from err[0].
       uint32_t spins = 0;
-      int w0 = (int)tile - 1;
+      bool failed = inject_fail && tile == 1;
+      int w0 = failed ? -1 : (int)tile - 1;
       while (w0 >= 0) {
         const int j = w0 - lane;
         uint32_t s = j >= 0 ? __hip_atomic_load(status + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLbPre;
@@ -542,8 +547,8 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restric
         const unsigned long long pre = __ballot((s & ~kLbVal) == kLbPre);
         const int stop = pre ? (__ffsll((long long)pre) - 1) : 63;
         const unsigned long long unpub = __ballot(s == 0u && lane <= stop);
-        if (unpub) {  // bounded so a broken invariant cannot hang the GPU
-          if (++spins > (1u << 22)) { excl = 0xffffffffu; break; }
+        if (unpub) {  // bounded so a broken invariant cannot hang the GPU; the host fails the scan
+          if (++spins > spin_limit) { excl = 0u; failed = true; break; }
           continue;
         }
         uint32_t val = (lane <= stop && j >= 0) ? (s & kLbVal) : 0u;
@@ -553,6 +558,7 @@ __global__ __launch_bounds__(kScanThreads) void k_scan(const uint32_t* __restric
         w0 -= 64;
       }
       if (lane == 0) __hip_atomic_store(status + tile, kLbPre | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (failed && lane == 0) err[0] = 1u;  // vector store to host-mapped memory, checked by gcs_scan
     }
     if (lane == 0) {
       s_excl = excl;
@@ -637,6 +643,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_rank(BucketArgs b, int n) {
         if (j0 + lane < cb) b.perm[sb + rank] = v;
       }
     } else {
+      if (lane == 0) b.err[1] = 1u;  // degenerate bucket: reported in the scan certificate
       uint32_t pos = sb;
       for (int i0 = 0; i0 < n; i0 += 64) {
         const int i = i0 + lane;
@@ -1628,7 +1635,8 @@ int scan_tiles(int n_bins) { return (n_bins + kScanTile - 1) / kScanTile; }
 
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   hipExtLaunchKernelGGL(k_scan, dim3(scan_tiles(b.n_bins)), dim3(kScanThreads), 0, s, e0, nullptr, 0,
-                        (const uint32_t*)b.counts, b.n_bins, b.scan_status, b.scan_ticket, b.starts);
+                        (const uint32_t*)b.counts, b.n_bins, b.scan_status, b.scan_ticket, b.starts, b.err,
+                        b.spin_limit, b.inject_scan_fail);
   hipLaunchKernelGGL(k_place, dim3(grid_for(n, 2048)), dim3(kBlock), 0, s, (const uint32_t*)b.keys,
                      (const uint32_t*)b.slots, (const uint32_t*)b.starts, n, b.n_bins, b.slot_idx);
   hipExtLaunchKernelGGL(k_bucket_rank, dim3((b.n_bins + kBlock - 1) / kBlock), dim3(kBlock), 0, s, nullptr, e1, 0, b,

@@ -32,7 +32,10 @@ class GcsConfig(C.Structure):
     _fields_ = [("device", C.c_int32), ("n_bins", C.c_int32), ("n_points_cap", C.c_int32),
                 ("max_raw_points", C.c_int32), ("mode", C.c_int32), ("k_cand", C.c_int32),
                 ("tau", C.c_double), ("lidar_origin", C.c_double * 3), ("deskew_rotation_only", C.c_int32),
-                ("forgetting_factor", C.c_double), ("gravity_W", C.c_double * 3)]
+                ("forgetting_factor", C.c_double), ("gravity_W", C.c_double * 3),
+                ("use_imu_odom", C.c_int32), ("imu_gravity_scale", C.c_double), ("planar_z_ref", C.c_double),
+                ("planar_z_sigma", C.c_double), ("planar_vz_sigma", C.c_double), ("alpha_min", C.c_double),
+                ("alpha_max", C.c_double), ("c0_cond", C.c_double)]
 
 
 class GcsScanInputs(C.Structure):
@@ -42,7 +45,9 @@ class GcsScanInputs(C.Structure):
                 ("imu_gyro", C.c_void_p), ("imu_accel", C.c_void_p), ("imu_len", C.c_int32),
                 ("scan_start_time", C.c_double), ("scan_end_time", C.c_double), ("dt_sec", C.c_double),
                 ("Q", C.c_void_p), ("L_ext", C.c_void_p), ("h_ext", C.c_void_p),
-                ("t_last_scan", C.c_double), ("t_scan", C.c_double), ("xyz_format", C.c_int32)]
+                ("t_last_scan", C.c_double), ("t_scan", C.c_double), ("xyz_format", C.c_int32),
+                ("odom_pose", C.c_void_p), ("odom_cov_se3", C.c_void_p), ("odom_twist", C.c_void_p),
+                ("odom_twist_cov", C.c_void_p), ("Sigma_g", C.c_void_p), ("Sigma_a", C.c_void_p)]
 
 
 class GcsPointCloud2Layout(C.Structure):
@@ -61,19 +66,37 @@ class GcsScanOutputs(C.Structure):
     _fields_ = [("belief", GcsBelief), ("iw_process_dPsi", C.c_double * 252), ("iw_process_dnu", C.c_double * 7),
                 ("z_t", C.c_double * 6), ("L_evidence", C.c_double * (D_Z * D_Z)), ("h_evidence", C.c_double * D_Z),
                 ("R_mf", C.c_double * 9), ("t_wls", C.c_double * 3), ("cert", C.c_double * CERT_LEN),
-                ("stage_ms", C.c_double * 8), ("iw_meas_dPsi", C.c_double * 27), ("iw_meas_dnu", C.c_double * 3)]
+                ("stage_ms", C.c_double * 8), ("iw_meas_dPsi", C.c_double * 27), ("iw_meas_dnu", C.c_double * 3),
+                ("L_imu_odom", C.c_double * (D_Z * D_Z)), ("h_imu_odom", C.c_double * D_Z),
+                ("imu_odom_certs", C.c_double * 77)]
+
+
+class GcsImuOdomInputs(C.Structure):
+    _fields_ = [("m", C.c_int32), ("stamps", C.c_void_p), ("gyro", C.c_void_p), ("accel", C.c_void_p),
+                ("w_int", C.c_void_p), ("t_last_scan", C.c_double), ("t_scan", C.c_double), ("dt_sec", C.c_double),
+                ("pose0", C.c_void_p), ("pose_pred", C.c_void_p), ("mu_prev", C.c_void_p), ("mu_inc", C.c_void_p),
+                ("gravity_W", C.c_void_p), ("Sigma_g", C.c_void_p), ("Sigma_a", C.c_void_p),
+                ("odom_pose", C.c_void_p), ("odom_cov_se3", C.c_void_p), ("odom_twist", C.c_void_p),
+                ("odom_twist_cov", C.c_void_p), ("planar_z_ref", C.c_double), ("planar_z_sigma", C.c_double),
+                ("planar_vz_sigma", C.c_double)]
+
+
+IMU_ODOM_CERT_LEN = 15
+DEBUG_SCAN_SPIN_LIMIT, DEBUG_INJECT_SCAN_FAIL = 1, 2
 
 
 # (name, restype, argtypes) for every symbol declared in include/gcslam_hip.h
 _SIGS = [
     ("gcs_version", C.c_char_p, []),
     ("gcs_abi_version", C.c_int, []),
+    ("gcs_config_defaults", C.c_int, [C.POINTER(GcsConfig)]),
     ("gcs_ctx_create", C.c_int, [C.POINTER(GcsConfig), C.POINTER(C.c_void_p)]),
     ("gcs_ctx_destroy", C.c_int, [C.c_void_p]),
     ("gcs_last_error", C.c_char_p, [C.c_void_p]),
     ("gcs_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("gcs_ctx_synchronize", C.c_int, [C.c_void_p]),
     ("gcs_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int32]),
+    ("gcs_ctx_set_debug", C.c_int, [C.c_void_p, C.c_int32, C.c_int64]),
     ("gcs_ctx_stage_times", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int32]),
     ("gcs_ctx_set_atlas", C.c_int, [C.c_void_p, c_double_p]),
     ("gcs_ctx_get_atlas", C.c_int, [C.c_void_p, c_double_p, c_int32_p]),
@@ -112,6 +135,7 @@ _SIGS = [
     ("gcs_preintegrate_imu", C.c_int, [C.c_int32, c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
                                        c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
     ("gcs_belief_world_pose", C.c_int, [C.POINTER(GcsBelief), c_double_p]),
+    ("gcs_imu_odom_evidence", C.c_int, [C.POINTER(GcsImuOdomInputs), c_double_p, c_double_p, c_double_p]),
     ("gcs_imu_meas_iw_suffstats", C.c_int, [C.c_int32] + [c_double_p] * 10),
     ("gcs_meas_iw_apply", C.c_int, [c_double_p] * 7),
     ("gcs_fibonacci_atlas", C.c_int, [C.c_int32, c_double_p]),
@@ -119,6 +143,11 @@ _SIGS = [
     ("gcs_nearest_bins", C.c_int, [C.c_int32, c_double_p, C.c_int32, c_double_p, c_int32_p]),
     ("gcs_hypothesis_payload", C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_void_p]),
     ("gcs_hypothesis_combine", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+    ("gcs_hypothesis_barycenter", C.c_int, [C.c_int32] + [c_double_p] * 8),
+    ("gcs_process_iw_apply", C.c_int, [c_double_p] * 7),
+    ("gcs_process_noise_Q", C.c_int, [c_double_p] * 3),
+    ("gcs_meas_iw_mode", C.c_int, [c_double_p, c_double_p, C.c_int32, c_double_p]),
+    ("gcs_ctx_describe", C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]
@@ -136,6 +165,15 @@ def load():
     if not os.path.exists(path):
         raise RuntimeError(f"{path} not found: build it with __graft_entry__.build() "
                            "(make -C gc-slam_amd); there is no CPU fallback")
+    # One HIP runtime per process: torch wheels ship their own libamdhip64 (SONAME libamdhip64.so.7,
+    # found through their RPATH as "libamdhip64.so").  Loaded after this library, torch would map a
+    # second runtime next to /opt/rocm's and fail to initialise ("No HIP GPUs are available");
+    # loaded first, this library's libamdhip64.so.7 dependency resolves to torch's copy, and the
+    # streams and device pointers torch hands over belong to the same runtime.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     for name, res, args in _SIGS:
         fn = getattr(lib, name)

@@ -27,9 +27,12 @@ def tau_for_bins(n_bins: int, tau_48: float = 0.1) -> float:
 class HypothesisContext:
     def __init__(self, n_bins=48, n_points_cap=8192, max_raw_points=None, mode="dense", k_cand=16, tau=None,
                  lidar_origin=(0.0, 0.0, 0.0), deskew_rotation_only=False, forgetting_factor=0.99,
-                 gravity_W=(0.0, 0.0, -9.81), device=0, use_torch_stream=True):
+                 gravity_W=(0.0, 0.0, -9.81), device=0, use_torch_stream=True, use_imu_odom=True,
+                 imu_gravity_scale=1.0, planar_z_ref=0.0, planar_z_sigma=0.1, planar_vz_sigma=0.01, alpha_min=1.0,
+                 alpha_max=1.0, c0_cond=1e6):
         self.lib = L.load()
         cfg = L.GcsConfig()
+        L.check(self.lib.gcs_config_defaults(C.byref(cfg)), None, "gcs_config_defaults")
         cfg.device = int(device)
         cfg.n_bins = int(n_bins)
         cfg.n_points_cap = int(n_points_cap)
@@ -41,6 +44,14 @@ class HypothesisContext:
         cfg.deskew_rotation_only = int(bool(deskew_rotation_only))
         cfg.forgetting_factor = float(forgetting_factor)
         cfg.gravity_W[:] = [float(x) for x in gravity_W]
+        cfg.use_imu_odom = int(bool(use_imu_odom))
+        cfg.imu_gravity_scale = float(imu_gravity_scale)
+        cfg.planar_z_ref = float(planar_z_ref)
+        cfg.planar_z_sigma = float(planar_z_sigma)
+        cfg.planar_vz_sigma = float(planar_vz_sigma)
+        cfg.alpha_min = float(alpha_min)
+        cfg.alpha_max = float(alpha_max)
+        cfg.c0_cond = float(c0_cond)
         self.cfg = cfg
         self.mode = mode
         self.device = int(device)
@@ -151,6 +162,17 @@ class HypothesisContext:
                   "stage_times")
         return ms, cnt
 
+    def describe(self):
+        """gcs_ctx_describe: the library's runtime description of this context (RuntimeManifest)."""
+        import json
+        buf = C.create_string_buffer(4096)
+        self._chk(self.lib.gcs_ctx_describe(self.h, buf, len(buf)), "describe")
+        return json.loads(buf.value.decode())
+
+    def set_debug(self, key, value):
+        """gcs_ctx_set_debug (test knobs: L.DEBUG_SCAN_SPIN_LIMIT, L.DEBUG_INJECT_SCAN_FAIL)."""
+        self._chk(self.lib.gcs_ctx_set_debug(self.h, int(key), int(value)), "set_debug")
+
     def synchronize(self):
         self._chk(self.lib.gcs_ctx_synchronize(self.h), "synchronize")
 
@@ -214,10 +236,13 @@ class HypothesisContext:
     # ------------------------------------------------------------------ the scan
     def scan(self, xyz_dev, point_step, t_dev, w_dev, n_points, imu_stamps, imu_gyro, imu_accel,
              scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None, t_last_scan=None, t_scan=None,
-             xyz_f64=False):
+             xyz_f64=False, odom_pose=None, odom_cov_se3=None, odom_twist=None, odom_twist_cov=None, Sigma_g=None,
+             Sigma_a=None):
         """gcs_scan.  t_last_scan / t_scan bound the scan-to-scan IMU window of the measurement-noise
-        IW statistics (pipeline.py:331-332); default: the scan window.  xyz_f64: xyz_dev holds f64
-        x, y, z per point_step record (gcs_parse_pointcloud2 output, point_step 24)."""
+        IW statistics and the IMU evidence (pipeline.py:331-332); default: the scan window.  xyz_f64:
+        xyz_dev holds f64 x, y, z per point_step record (gcs_parse_pointcloud2 output, point_step 24).
+        Odometry arguments left None take the node's "no odometry yet" inputs (backend_node.py:
+        2047-2051); Sigma_g / Sigma_a None take the IW modes of the context's measurement state."""
         imu_stamps = np.ascontiguousarray(imu_stamps, np.float64)
         imu_gyro = np.ascontiguousarray(imu_gyro, np.float64).reshape(-1)
         imu_accel = np.ascontiguousarray(imu_accel, np.float64).reshape(-1)
@@ -238,7 +263,9 @@ class HypothesisContext:
         inp.t_scan = float(scan_end_time if t_scan is None else t_scan)
         inp.xyz_format = 1 if xyz_f64 else 0
         keep = []
-        for name, arr in (("Q", Q), ("L_ext", L_ext), ("h_ext", h_ext)):
+        for name, arr in (("Q", Q), ("L_ext", L_ext), ("h_ext", h_ext), ("odom_pose", odom_pose),
+                          ("odom_cov_se3", odom_cov_se3), ("odom_twist", odom_twist), ("odom_twist_cov", odom_twist_cov),
+                          ("Sigma_g", Sigma_g), ("Sigma_a", Sigma_a)):
             if arr is not None:
                 a = np.ascontiguousarray(arr, np.float64).reshape(-1)
                 keep.append(a)

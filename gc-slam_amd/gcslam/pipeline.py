@@ -1,6 +1,8 @@
 """L2 drop-in: process_scan_single_hypothesis / process_hypotheses with the reference calling
 convention (FS/backend/pipeline.py:316-340, :1594-1621), running the 14-step bin path
-(README.md:105-122) on the MI355X through libgcslam_hip.so.
+(README.md:105-122) on the MI355X through libgcslam_hip.so, plus the node-level noise updates the
+reference's backend node calls after the hypothesis loop (backend_node.py:2093-2119) and the
+RuntimeManifest (pipeline.py:1629-1793).
 
 `primitive_map` is replaced by `map_bins`, a HypothesisContext that owns the device-resident
 MapBinStats of this hypothesis (the legacy pipeline took bin_atlas/map_stats, CHANGELOG.md:280).
@@ -8,17 +10,22 @@ MapBinStats of this hypothesis (the legacy pipeline took bin_atlas/map_stats, CH
 
 from __future__ import annotations
 
+import json
+import warnings
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import Dict, List, Optional
 
 import numpy as np
 
-from .certificates import CertBundle, InfluenceCert, SupportCert, aggregate_certificates
+from . import _lib as L
+from .certificates import (CertBundle, ConditioningCert, ExpectedEffect, InfluenceCert, MismatchCert, SupportCert,
+                           aggregate_certificates)
 from .context import HypothesisContext
 from .outputs import tape_from_result
 
 CHART_ID = "GC-RIGHT-01"
 D_Z = 22
+HYP_WEIGHT_FLOOR = 0.0025   # constants.py:63
 
 
 @dataclass
@@ -52,21 +59,40 @@ class PipelineConfig:
     eps_psd: float = 1e-12
     eps_lift: float = 1e-9
     eps_mass: float = 1e-12
+    alpha_min: float = 1.0            # constants.py:89-90
+    alpha_max: float = 1.0
+    c0_cond: float = 1e6              # constants.py:92
+    power_beta_min: float = 0.25      # pipeline.py:119-121 (fixed in the library)
+    power_beta_exc_c: float = 50.0
+    power_beta_z_c: float = 1.0
     c_frob: float = 1.0
     forgetting_factor: float = 0.99
+    Sigma_g: Optional[np.ndarray] = None   # node sets these per scan from the IW state (backend_node.py:2020-2023)
+    Sigma_a: Optional[np.ndarray] = None   # None: the IW mode of the context's measurement-noise state
+    imu_gravity_scale: float = 1.0
     deskew_rotation_only: bool = False
     lidar_origin_base: tuple = (0.0, 0.0, 0.0)
     gravity_W: tuple = (0.0, 0.0, -9.81)
+    planar_z_ref: float = 0.0         # constants.py:294-310
+    planar_z_sigma: float = 0.1
+    planar_vz_sigma: float = 0.01
+    enable_imu_odom: bool = True      # False: LiDAR-only ablation (the reference always runs the branch)
+    camera_batch_policy: str = "warn"  # camera evidence is out of scope here: "warn" once | "raise" | "ignore"
     max_raw_points: int = 1 << 20
     device: int = 0
 
+    def context_kwargs(self) -> dict:
+        return dict(n_bins=self.B_BINS, n_points_cap=self.N_POINTS_CAP, max_raw_points=self.max_raw_points,
+                    mode=self.soft_assign_mode, k_cand=self.k_cand, tau=self.tau_soft_assign,
+                    lidar_origin=self.lidar_origin_base, deskew_rotation_only=self.deskew_rotation_only,
+                    forgetting_factor=self.forgetting_factor, gravity_W=self.gravity_W, device=self.device,
+                    use_imu_odom=self.enable_imu_odom, imu_gravity_scale=self.imu_gravity_scale,
+                    planar_z_ref=self.planar_z_ref, planar_z_sigma=self.planar_z_sigma,
+                    planar_vz_sigma=self.planar_vz_sigma, alpha_min=self.alpha_min, alpha_max=self.alpha_max,
+                    c0_cond=self.c0_cond)
+
     def make_context(self) -> HypothesisContext:
-        return HypothesisContext(n_bins=self.B_BINS, n_points_cap=self.N_POINTS_CAP,
-                                 max_raw_points=self.max_raw_points, mode=self.soft_assign_mode, k_cand=self.k_cand,
-                                 tau=self.tau_soft_assign, lidar_origin=self.lidar_origin_base,
-                                 deskew_rotation_only=self.deskew_rotation_only,
-                                 forgetting_factor=self.forgetting_factor, gravity_W=self.gravity_W,
-                                 device=self.device)
+        return HypothesisContext(**self.context_kwargs())
 
 
 @dataclass
@@ -85,17 +111,38 @@ class ScanPipelineResult:
     map_bins_updated: Optional[HypothesisContext] = None
     z_t: Optional[np.ndarray] = None
     raw_cert: Optional[np.ndarray] = None
+    L_evidence: Optional[np.ndarray] = None
+    h_evidence: Optional[np.ndarray] = None
+    L_imu_odom: Optional[np.ndarray] = None
+    h_imu_odom: Optional[np.ndarray] = None
 
 
-def _certs_from_vector(c, chart, anchor):
-    """Rebuild the per-operator certificates from the scan's cert vector (DESIGN.md cert slots)."""
+IMU_ODOM_CERTS = (("OdomEvidenceGaussian",), ("ImuAccelDirectionTimeResolved", "TransportConsistencyWeighting"),
+                  ("ImuDependenceInflation",), ("ImuGyroRotationGaussian",), ("ImuPreintegrationVelPos",),
+                  ("PlanarZPrior",), ("VelocityZPrior",), ("OdomVelocityEvidence",), ("OdomYawRateEvidence",),
+                  ("PoseTwistKinematicConsistency",), ("OdomDependenceInflation",))
+
+
+def _certs_from_vector(c, io, chart, anchor):
+    """Rebuild the per-operator certificates in the reference's all_certs order from the scan's
+    cert vector and the eleven IMU/odometry certificate rows (DESIGN.md cert slots)."""
     I = InfluenceCert
-    return [
+    certs = [
         CertBundle.create_approx(chart, anchor, ["PointBudgetResample"], support=SupportCert(c[0], c[1]),
                                  influence=I(mass_epsilon_ratio=c[2])),
         CertBundle.create_approx(chart, anchor, ["PredictDiffusion"],
                                  influence=I(lift_strength=c[6], psd_projection_delta=c[7], dt_scale=c[8])),
         CertBundle.create_exact(chart, anchor, support=SupportCert(c[10], c[9])),
+    ]
+    for k, trig in enumerate(IMU_ODOM_CERTS):
+        r = io[7 * k:7 * k + 7]
+        if not np.any(r):
+            continue   # branch disabled
+        certs.append(CertBundle.create_approx(chart, anchor, list(trig), support=SupportCert(r[0], r[1]),
+                                              mismatch=MismatchCert(nll_per_ess=r[2]),
+                                              influence=I(lift_strength=r[3], psd_projection_delta=r[4],
+                                                          mass_epsilon_ratio=r[5], trust_alpha=r[6])))
+    certs += [
         CertBundle.create_exact(chart, anchor, support=SupportCert(c[12], c[13])),
         CertBundle.create_approx(chart, anchor, ["ScanBinMomentMatch"], support=SupportCert(c[14], c[15]),
                                  influence=I(psd_projection_delta=c[16], mass_epsilon_ratio=c[17])),
@@ -103,33 +150,75 @@ def _certs_from_vector(c, chart, anchor):
                                  influence=I(psd_projection_delta=c[18], mass_epsilon_ratio=c[19])),
         CertBundle.create_approx(chart, anchor, ["PlanarTranslationEvidence"],
                                  influence=I(psd_projection_delta=c[25], mass_epsilon_ratio=c[26])),
-        CertBundle.create_approx(chart, anchor, ["PowerTempering"], influence=I(power_beta=c[30])),
+        CertBundle.create_approx(chart, anchor, ["PowerTempering"], frobenius_applied=abs(1.0 - c[30]) > 0.0,
+                                 influence=I(power_beta=c[30])),
         CertBundle.create_approx(chart, anchor, ["ExcitationPriorScaling"],
                                  influence=I(dt_scale=1.0 - c[31], extrinsic_scale=1.0 - c[32])),
-        CertBundle.create_exact(chart, anchor, influence=I(trust_alpha=c[33])),
+        CertBundle.create_exact(chart, anchor, influence=I(trust_alpha=c[33]),
+                                conditioning=ConditioningCert(cond=c[49], near_null_count=int(c[50]))),
         CertBundle.create_approx(chart, anchor, ["InfoFusionAdditive"],
                                  influence=I(psd_projection_delta=c[34], trust_alpha=c[33])),
         CertBundle.create_approx(chart, anchor, ["PoseUpdateFrobeniusRecompose"], frobenius_applied=c[36] > 0),
         CertBundle.create_approx(chart, anchor, ["AnchorDriftUpdate"], influence=I(anchor_drift_rho=c[37])),
     ]
+    return certs
+
+
+_pinned = {}
+
+
+def _to_device(a, dtype, device, role):
+    """Host array -> device tensor through a pinned staging buffer per (role, shape), reused across
+    scans: one async H2D, and before a buffer is refilled the event of its previous copy is waited
+    on (the copy may still be reading it)."""
+    import torch
+    if isinstance(a, torch.Tensor):
+        return a.to(f"cuda:{device}", dtype=dtype).contiguous()
+    a = np.ascontiguousarray(a)
+    key = (role, device, dtype, a.shape)
+    ent = _pinned.get(key)
+    if ent is None:
+        ent = _pinned[key] = [torch.empty(a.shape, dtype=dtype).pin_memory(), None]
+    buf, ev = ent
+    if ev is not None:
+        ev.synchronize()
+    buf.numpy()[...] = a
+    out = buf.to(f"cuda:{device}", non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(device))
+    ent[1] = ev
+    return out
 
 
 def _as_device_scan(raw_points, raw_timestamps, raw_weights, device):
+    """The node's parsed cloud (backend_node.py:1675-1690) as device inputs: xyz as the float32
+    PointCloud2 record the point kernel reads (x, y, z, pad), t and w f64."""
     import torch
-    dev = f"cuda:{device}"
     if isinstance(raw_points, torch.Tensor) and raw_points.dim() == 2 and raw_points.shape[1] == 4 \
             and raw_points.dtype == torch.float32:
-        rec = raw_points.to(dev)
+        rec = raw_points.to(f"cuda:{device}").contiguous()
     else:
-        p = torch.as_tensor(np.asarray(raw_points), dtype=torch.float64).reshape(-1, 3)
-        rec = torch.zeros((p.shape[0], 4), dtype=torch.float32)
-        rec[:, :3] = p.to(torch.float32)   # PointCloud2 x,y,z are float32 (backend_node.py:377-468)
-        rec = rec.to(dev)
-    t = torch.as_tensor(np.asarray(raw_timestamps, np.float64) if not isinstance(raw_timestamps, torch.Tensor)
-                        else raw_timestamps, dtype=torch.float64).to(dev).contiguous()
-    w = torch.as_tensor(np.asarray(raw_weights, np.float64) if not isinstance(raw_weights, torch.Tensor)
-                        else raw_weights, dtype=torch.float64).to(dev).contiguous()
-    return rec.contiguous(), t, w
+        p = np.asarray(raw_points.cpu() if isinstance(raw_points, torch.Tensor) else raw_points,
+                       np.float64).reshape(-1, 3)
+        r = np.zeros((p.shape[0], 4), np.float32)
+        r[:, :3] = p   # PointCloud2 x,y,z are float32 (backend_node.py:377-468)
+        rec = _to_device(r, torch.float32, device, "xyz")
+    t = _to_device(raw_timestamps, torch.float64, device, "t")
+    w = _to_device(raw_weights, torch.float64, device, "w")
+    return rec, t, w
+
+
+_camera_warned = False
+
+
+def _camera_batch_has_content(camera_batch):
+    if camera_batch is None:
+        return False
+    for attr in ("n_valid", "n", "count"):
+        v = getattr(camera_batch, attr, None)
+        if v is not None:
+            return int(v) > 0
+    return True
 
 
 def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, raw_timestamps, raw_weights,
@@ -140,49 +229,203 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
                                    L_ext=None, h_ext=None) -> ScanPipelineResult:
     """FS/backend/pipeline.py:316-1591 with the bin path of README.md:105-122.
 
-    odom/IMU evidence factors (pipeline.py:595-776) are not computed this round; callers may pass
-    their summed information as L_ext/h_ext (DESIGN.md "out of scope")."""
+    Every reference input is consumed: the point stream, the IMU window (deskew, scan-to-scan
+    preintegration, measurement-noise statistics, IMU evidence), odometry pose / covariance /
+    twist (the step-9 odometry factors; None takes the node's "no odometry yet" inputs,
+    backend_node.py:939-940,2047-2051).  raw_ring / raw_tag are only gathered by the reference's
+    budget step for the primitive path; the bin path does not read them.  camera_batch feeds the
+    live primitive path's visual evidence, which this backend does not build (DESIGN.md out of
+    scope): config.camera_batch_policy says whether a non-empty batch warns (default), raises or is
+    ignored.  L_ext / h_ext add further caller evidence to step 9."""
+    global _camera_warned
+    if _camera_batch_has_content(camera_batch):
+        if config.camera_batch_policy == "raise":
+            raise NotImplementedError("camera_batch: visual evidence is not part of the bin-path backend")
+        if config.camera_batch_policy == "warn" and not _camera_warned:
+            warnings.warn("camera_batch ignored: the bin-path backend has no visual evidence (DESIGN.md section 9)")
+            _camera_warned = True
     ctx = map_bins if map_bins is not None else config.make_context()
     ctx.set_belief(belief_prev.X_anchor, belief_prev.stamp_sec, belief_prev.z_lin, belief_prev.L, belief_prev.h)
     rec, t, w = _as_device_scan(raw_points, raw_timestamps, raw_weights, config.device)
     out = ctx.scan(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
-                   dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan)
+                   dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
+                   odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
+                   odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a)
     X, stamp, z, Lm, h = ctx.get_belief()
     cert = np.array(out.cert[:])
-    certs = _certs_from_vector(cert, CHART_ID, belief_prev.anchor_id)
+    certs = _certs_from_vector(cert, np.array(out.imu_odom_certs[:]), CHART_ID, belief_prev.anchor_id)
     agg = aggregate_certificates(certs)
     bel = BeliefGaussianInfo(CHART_ID, belief_prev.anchor_id, X, stamp, z, Lm, h, certs[-1])
+    view = np.ctypeslib.as_array
     res = ScanPipelineResult(
         belief_updated=bel,
-        iw_process_dPsi=np.array(out.iw_process_dPsi[:]).reshape(7, 6, 6),
-        iw_process_dnu=np.array(out.iw_process_dnu[:]),
-        iw_meas_dPsi=np.array(out.iw_meas_dPsi[:]).reshape(3, 3, 3), iw_meas_dnu=np.array(out.iw_meas_dnu[:]),
+        iw_process_dPsi=view(out.iw_process_dPsi).copy().reshape(7, 6, 6),
+        iw_process_dnu=view(out.iw_process_dnu).copy(),
+        iw_meas_dPsi=view(out.iw_meas_dPsi).copy().reshape(3, 3, 3), iw_meas_dnu=view(out.iw_meas_dnu).copy(),
         iw_lidar_bucket_dPsi=np.zeros((64, 3, 3)), iw_lidar_bucket_dnu=np.zeros(64),
         all_certs=certs, aggregated_cert=agg,
         diagnostics_tape=dict(stage_ms=list(out.stage_ms[:4])),
-        map_bins_updated=ctx, z_t=np.array(out.z_t[:]), raw_cert=cert)
+        map_bins_updated=ctx, z_t=view(out.z_t).copy(), raw_cert=cert,
+        L_evidence=view(out.L_evidence).copy().reshape(D_Z, D_Z), h_evidence=view(out.h_evidence).copy(),
+        L_imu_odom=view(out.L_imu_odom).copy().reshape(D_Z, D_Z), h_imu_odom=view(out.h_imu_odom).copy())
     # the reference's per-scan MinimalScanTape (pipeline.py:1504-1570)
-    res.diagnostics_tape = tape_from_result(res, scan_seq, scan_end_time, dt_sec, rec.shape[0],
-                                            np.array(out.L_evidence[:]))
+    res.diagnostics_tape = tape_from_result(res, scan_seq, scan_end_time, dt_sec, rec.shape[0], res.L_evidence)
+    if map_bins is None:
+        ctx.close()
+        res.map_bins_updated = None
     return res
 
 
-def process_hypotheses(hypotheses: List[BeliefGaussianInfo], weights, config: PipelineConfig,
-                       ctx: Optional[HypothesisContext] = None):
-    """FS/backend/pipeline.py:1594-1621 -> hypothesis_barycenter_projection (hypothesis.py:51-117),
-    single-process form: sum the per-hypothesis payloads on the host (the multi-GPU form is
-    gcslam.distributed.combine_allreduce)."""
-    from . import _lib as L
-    w = np.maximum(np.asarray(weights, np.float64), 0.0025)
-    wn = w / w.sum()
-    total = np.zeros(L.PAYLOAD_LEN)
-    own = ctx is None
-    ctx = ctx or config.make_context()
-    for k, b in enumerate(hypotheses):
-        ctx.set_belief(b.X_anchor, b.stamp_sec, b.z_lin, b.L, b.h)
-        total += ctx.hypothesis_payload(float(weights[k]), float(wn[k]))
-    (X, stamp, z, Lm, h), cert = ctx.hypothesis_combine(total, 0)
-    if own:
-        ctx.close()
-    return BeliefGaussianInfo(CHART_ID, hypotheses[0].anchor_id, hypotheses[0].X_anchor, hypotheses[0].stamp_sec,
-                              z, Lm, h), cert
+def process_hypotheses(hypotheses: List[BeliefGaussianInfo], weights, config: PipelineConfig):
+    """FS/backend/pipeline.py:1594-1621 -> hypothesis_barycenter_projection (hypothesis.py:125-236):
+    returns (combined BeliefGaussianInfo, CertBundle, ExpectedEffect).  Host numerics through
+    gcs_hypothesis_barycenter: no context, no device, no state change (the IW applies are separate
+    calls, as in the node).  The multi-GPU form is gcslam.distributed.combine_allreduce."""
+    lib = L.load()
+    w = np.ascontiguousarray(weights, np.float64).reshape(-1)
+    if len(hypotheses) != config.K_HYP:
+        raise ValueError(f"Expected {config.K_HYP} hypotheses, got {len(hypotheses)}")
+    if w.shape != (config.K_HYP,):
+        raise ValueError(f"Expected weights shape ({config.K_HYP},), got {w.shape}")
+    Ls = np.ascontiguousarray(np.stack([b.L for b in hypotheses]), np.float64)
+    hs = np.ascontiguousarray(np.stack([b.h for b in hypotheses]), np.float64)
+    zs = np.ascontiguousarray(np.stack([b.z_lin for b in hypotheses]), np.float64)
+    Lo, ho, zo, c = np.zeros((D_Z, D_Z)), np.zeros(D_Z), np.zeros(D_Z), np.zeros(6)
+    L.check(lib.gcs_hypothesis_barycenter(len(hypotheses), L.dptr(Ls), L.dptr(hs), L.dptr(zs), L.dptr(w),
+                                          L.dptr(Lo), L.dptr(ho), L.dptr(zo), L.dptr(c)), None,
+            "gcs_hypothesis_barycenter")
+    t = hypotheses[0]
+    wf = np.maximum(w, HYP_WEIGHT_FLOOR)
+    wn = wf / wf.sum()
+    cert = CertBundle.create_approx(
+        CHART_ID, t.anchor_id, ["HypothesisProjection", "I-projection-info-barycenter"],
+        conditioning=ConditioningCert(cond=float(c[5])),
+        support=SupportCert(ess_total=float(c[2]), support_frac=float(c[3])),
+        influence=InfluenceCert(psd_projection_delta=float(c[0]), mass_epsilon_ratio=float(c[1]) / config.K_HYP))
+    belief = BeliefGaussianInfo(CHART_ID, t.anchor_id, t.X_anchor, t.stamp_sec, zo, Lo, ho, cert)
+    effect = ExpectedEffect("predicted_projection_spread_proxy", float(c[4]), None)
+    assert np.isclose(wn.sum(), 1.0)
+    return belief, cert, effect
+
+
+# ---------------------------------------------------------------- node-level noise updates
+@dataclass
+class ProcessNoiseIWState:
+    """FS/backend/structures/inverse_wishart_jax.py:28-39 (7 blocks, dims [3,3,3,3,3,1,6])."""
+    nu: np.ndarray
+    Psi_blocks: np.ndarray   # (7, 6, 6)
+
+
+@dataclass
+class MeasurementNoiseIWState:
+    """FS/backend/structures/measurement_noise_iw_jax.py:29-34 (blocks gyro, accel, lidar)."""
+    nu: np.ndarray
+    Psi_blocks: np.ndarray   # (3, 3, 3)
+
+
+def process_noise_iw_apply_suffstats(state: ProcessNoiseIWState, dPsi, dnu):
+    """process_noise_iw_apply_suffstats_jax (inverse_wishart_jax.py:126-185) -> (state, cert2)."""
+    lib = L.load()
+    nu, Psi = np.ascontiguousarray(state.nu, np.float64), np.ascontiguousarray(state.Psi_blocks, np.float64)
+    dP, dn = np.ascontiguousarray(dPsi, np.float64), np.ascontiguousarray(dnu, np.float64)
+    nu2, Psi2, c = np.zeros(7), np.zeros((7, 6, 6)), np.zeros(2)
+    L.check(lib.gcs_process_iw_apply(L.dptr(nu), L.dptr(Psi), L.dptr(dP), L.dptr(dn), L.dptr(nu2), L.dptr(Psi2),
+                                     L.dptr(c)), None, "gcs_process_iw_apply")
+    return ProcessNoiseIWState(nu2, Psi2), c
+
+
+def process_noise_state_to_Q(state: ProcessNoiseIWState):
+    """process_noise_state_to_Q_jax (inverse_wishart_jax.py:35-68)."""
+    lib = L.load()
+    nu, Psi = np.ascontiguousarray(state.nu, np.float64), np.ascontiguousarray(state.Psi_blocks, np.float64)
+    Q = np.zeros((D_Z, D_Z))
+    L.check(lib.gcs_process_noise_Q(L.dptr(nu), L.dptr(Psi), L.dptr(Q)), None, "gcs_process_noise_Q")
+    return Q
+
+
+def measurement_noise_apply_suffstats(state: MeasurementNoiseIWState, dPsi_blocks, dnu):
+    """measurement_noise_apply_suffstats_jax (measurement_noise_iw_jax.py:59-100) -> (state, cert2)."""
+    lib = L.load()
+    nu, Psi = np.ascontiguousarray(state.nu, np.float64), np.ascontiguousarray(state.Psi_blocks, np.float64)
+    dP, dn = np.ascontiguousarray(dPsi_blocks, np.float64), np.ascontiguousarray(dnu, np.float64)
+    nu2, Psi2, c = np.zeros(3), np.zeros((3, 3, 3)), np.zeros(2)
+    L.check(lib.gcs_meas_iw_apply(L.dptr(nu), L.dptr(Psi), L.dptr(dP), L.dptr(dn), L.dptr(nu2), L.dptr(Psi2),
+                                  L.dptr(c)), None, "gcs_meas_iw_apply")
+    return MeasurementNoiseIWState(nu2, Psi2), c
+
+
+def measurement_noise_mean(state: MeasurementNoiseIWState, idx: int):
+    """measurement_noise_mean_jax (measurement_noise_iw_jax.py:38-56): the IW mode of block idx."""
+    lib = L.load()
+    nu, Psi = np.ascontiguousarray(state.nu, np.float64), np.ascontiguousarray(state.Psi_blocks, np.float64)
+    S = np.zeros((3, 3))
+    L.check(lib.gcs_meas_iw_mode(L.dptr(nu), L.dptr(Psi), int(idx), L.dptr(S)), None, "gcs_meas_iw_mode")
+    return S
+
+
+def datasheet_process_noise_state() -> ProcessNoiseIWState:
+    """create_datasheet_process_noise_state (structures/inverse_wishart_jax.py:42-80)."""
+    dims = (3, 3, 3, 3, 3, 1, 6)
+    sig = (1e-4, 8.7e-7, 9.5e-5, 1e-8, 1e-6, 1e-6, 1e-8)   # constants.py:225-237
+    Psi = np.zeros((7, 6, 6))
+    for i, d in enumerate(dims):
+        Psi[i, :d, :d] = np.eye(d) * sig[i] * 0.5
+    return ProcessNoiseIWState(np.array(dims, np.float64) + 1.5, Psi)
+
+
+def datasheet_measurement_noise_state() -> MeasurementNoiseIWState:
+    """create_datasheet_measurement_noise_state (structures/measurement_noise_iw_jax.py:37-68)."""
+    return MeasurementNoiseIWState(np.full(3, 4.5), np.stack([np.eye(3) * s * 0.5 for s in (8.7e-7, 9.5e-5, 0.01)]))
+
+
+# ---------------------------------------------------------------- RuntimeManifest
+@dataclass
+class RuntimeManifest:
+    """RuntimeManifest (FS/backend/pipeline.py:1629-1793) for the bin-path backend: the reference's
+    constants plus every declared item (tau rule, candidate rule, K, N_POINTS_CAP, map mode,
+    pushforward form) and the library's own description of a live context (gcs_ctx_describe)."""
+    config: PipelineConfig = field(default_factory=PipelineConfig)
+    chart_id: str = CHART_ID
+    D_Z: int = D_Z
+    D_DESKEW: int = 22
+    HYP_WEIGHT_FLOOR: float = HYP_WEIGHT_FLOOR
+    eps_r: float = 1e-6
+    eps_den: float = 1e-12
+    kappa_scale: float = 1.0
+    c_dt: float = 1.0
+    c_ex: float = 1.0
+    MAX_IMU_PREINT_LEN: int = 512
+    pose_evidence_backend: str = "bins"       # legacy bin path (README.md:105-122), not primitives
+    map_backend: str = "map_bin_stats"
+    topics: Dict[str, str] = field(default_factory=dict)
+    context_description: Optional[dict] = None
+
+    @classmethod
+    def from_context(cls, config: PipelineConfig, ctx: HypothesisContext):
+        return cls(config=config, context_description=ctx.describe())
+
+    def to_dict(self) -> dict:
+        c = self.config
+        d = dict(chart_id=self.chart_id, pose_evidence_backend=self.pose_evidence_backend,
+                 map_backend=self.map_backend, topics=dict(self.topics), D_Z=self.D_Z, D_DESKEW=self.D_DESKEW,
+                 K_HYP=c.K_HYP, HYP_WEIGHT_FLOOR=self.HYP_WEIGHT_FLOOR, N_POINTS_CAP=c.N_POINTS_CAP,
+                 B_BINS=c.B_BINS, soft_assign_mode=c.soft_assign_mode, k_cand=c.k_cand,
+                 tau_soft_assign=(c.tau_soft_assign if c.tau_soft_assign is not None else 0.1 * 48.0 / c.B_BINS),
+                 tau_rule="tau_B = 0.1 * 48 / B (declared; GC_TAU_SOFT_ASSIGN is undefined in the reference)",
+                 candidate_rule=("dense N x B softmax (reference)" if c.soft_assign_mode == "dense" else
+                                 "K nearest atlas bins of the exact nearest bin, ties -> lower id (declared)"),
+                 map_mode="per-hypothesis MapBinStats (declared)",
+                 pushforward_form="declared (DESIGN.md section 3 item 3)",
+                 eps_psd=c.eps_psd, eps_lift=c.eps_lift, eps_mass=c.eps_mass, eps_r=self.eps_r, eps_den=self.eps_den,
+                 alpha_min=c.alpha_min, alpha_max=c.alpha_max, kappa_scale=self.kappa_scale, c0_cond=c.c0_cond,
+                 c_dt=self.c_dt, c_ex=self.c_ex, c_frob=c.c_frob, imu_gravity_scale=c.imu_gravity_scale,
+                 deskew_rotation_only=c.deskew_rotation_only, power_beta_min=c.power_beta_min,
+                 power_beta_exc_c=c.power_beta_exc_c, power_beta_z_c=c.power_beta_z_c,
+                 enable_parallel_stages=False, MAX_IMU_PREINT_LEN=self.MAX_IMU_PREINT_LEN,
+                 backends={"core_array": "HIP (gfx950) + host C++", "library": L.load().gcs_version().decode()})
+        if self.context_description is not None:
+            d["context"] = self.context_description
+        return d
+
+    def to_json(self) -> str:
+        return json.dumps(self.to_dict())

@@ -6,6 +6,9 @@ y=+-6 m, floor z=0, ceiling z=3 m) from a sensor 0.5 m above the base origin, wi
 noise.  The body moves with a constant twist (v=(1,0,0) m/s, w=(0,0,0.3) rad/s) so deskew has
 work to do; points are expressed in the base frame at their own capture time.  Weights follow
 the reference parse law (FS/backend/backend_node.py:448-459).  IMU at 200 Hz, padded to 512.
+Odometry (the node's odom_pose / odom_cov_se3 / odom_twist / odom_twist_cov, backend_node.py:
+1453-1535): the true base pose at the scan stamp t_scan plus N(0, (1 cm, 0.2 deg)) noise, and the
+true body twist plus N(0, (2 cm/s, 0.5 deg/s)) noise, with matching diagonal covariances.
 """
 
 from __future__ import annotations
@@ -90,7 +93,35 @@ def make_scan(n_points: int, scan_index: int = 0, seed: int = 0, noise: float = 
     gyro[:m] = W_BODY[None, :] + 1e-3 * rng.standard_normal((m, 3))
     a_body = np.cross(W_BODY, V_BODY) + np.array([0.0, 0.0, 9.81])
     accel[:m] = a_body[None, :] + 1e-2 * rng.standard_normal((m, 3))
+    # odometry at the scan stamp (drawn after the LiDAR and IMU noise, so those inputs are unchanged)
+    t_scan = t_start + SCAN_PERIOD
+    p_w, _ = body_pose(t_scan)
+    sd_pose = np.array([0.01, 0.01, 0.01, np.deg2rad(0.2), np.deg2rad(0.2), np.deg2rad(0.2)])
+    odom_pose = np.concatenate([p_w, [0.0, 0.0, W_BODY[2] * (t_scan - T0)]]) + sd_pose * rng.standard_normal(6)
+    sd_twist = np.array([0.02, 0.02, 0.02, np.deg2rad(0.5), np.deg2rad(0.5), np.deg2rad(0.5)])
+    odom_twist = np.concatenate([V_BODY, W_BODY]) + sd_twist * rng.standard_normal(6)
     return dict(xyz_record=rec, points=rec[:, :3].astype(np.float64), timestamps=t, weights=w,
                 imu_stamps=imu_t, imu_gyro=gyro, imu_accel=accel, scan_start_time=t_start,
                 scan_end_time=t_start + SCAN_PERIOD, dt_sec=SCAN_PERIOD,
-                t_last_scan=t_start - SCAN_PERIOD, t_scan=t_start + SCAN_PERIOD)
+                t_last_scan=t_start - SCAN_PERIOD, t_scan=t_scan,
+                odom_pose=odom_pose, odom_cov_se3=np.diag(sd_pose ** 2), odom_twist=odom_twist,
+                odom_twist_cov=np.diag(sd_twist ** 2))
+
+
+ODOM_KEYS = ("odom_pose", "odom_cov_se3", "odom_twist", "odom_twist_cov")
+
+
+def odom_kwargs(sc):
+    """The scan's odometry as HypothesisContext.scan keyword arguments."""
+    return {k: sc[k] for k in ODOM_KEYS if k in sc}
+
+
+def scan_kwargs(sc):
+    """Every host-side input of HypothesisContext.scan held by a scan dict (IMU window, times,
+    scan-to-scan window, odometry)."""
+    kw = {k: sc[k] for k in ("imu_stamps", "imu_gyro", "imu_accel", "scan_start_time", "scan_end_time", "dt_sec")}
+    for k in ("t_last_scan", "t_scan"):
+        if k in sc:
+            kw[k] = sc[k]
+    kw.update(odom_kwargs(sc))
+    return kw

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define GCS_ABI_VERSION 1
+#define GCS_ABI_VERSION 2
 #define GCS_D_Z 22
 #define GCS_SCAN_FIELDS 26   /* ScanBinStats, field-major: N, s_dir[3], S_dir_scatter[9], p_bar[3], Sigma_p[9], kappa */
 #define GCS_MAP_FIELDS 26    /* MapBinStats: S_dir[3], S_dir_scatter[9], N_dir, N_pos, sum_p[3], sum_ppT[9] */
@@ -69,6 +69,13 @@ typedef struct {
   int32_t deskew_rotation_only;/* pipeline.py:482-483 */
   double forgetting_factor;    /* PipelineConfig.forgetting_factor (0.99) */
   double gravity_W[3];         /* constants.py:80 */
+  /* step 9 IMU / odometry evidence family (pipeline.py:595-776) and fusion scale (fusion.py:46-142);
+   * PipelineConfig fields (pipeline.py:96-223).  Fill with gcs_config_defaults() first. */
+  int32_t use_imu_odom;        /* 1: the reference's branch (default); 0: LiDAR-only ablation */
+  double imu_gravity_scale;    /* PipelineConfig.imu_gravity_scale (1.0) */
+  double planar_z_ref, planar_z_sigma, planar_vz_sigma;  /* constants.py:294-310 (0, 0.1, 0.01) */
+  double alpha_min, alpha_max; /* constants.py:89-90 (1, 1) */
+  double c0_cond;              /* constants.py:92 (1e6) */
 } gcs_config;
 
 typedef struct {
@@ -91,6 +98,17 @@ typedef struct {
   double t_last_scan, t_scan;
   /* 0: float32 x,y,z at bytes 0,4,8 of each point_step record; 1: float64 x,y,z (gcs_parse_pointcloud2) */
   int32_t xyz_format;
+  /* odometry (host; NULL = the node's "no odometry yet" inputs: identity pose, 1e12 I covariances,
+   * backend_node.py:939-940,2047-2051).  Pose [t, rotvec] relative to the first odometry pose,
+   * covariances row-major 6x6 in ROS [x,y,z,roll,pitch,yaw] order, twist [vx,vy,vz,wx,wy,wz] body. */
+  const double* odom_pose;     /* [6] */
+  const double* odom_cov_se3;  /* [36] */
+  const double* odom_twist;    /* [6] */
+  const double* odom_twist_cov;/* [36] */
+  /* IMU noise proxies (3x3); NULL = IW mode of the context's measurement-noise state
+   * (backend_node.py:2020-2023, measurement_noise_iw_jax.py:38-56) */
+  const double* Sigma_g;
+  const double* Sigma_a;
 } gcs_scan_inputs;
 
 /* Layout of a PointCloud2 message (sensor_msgs/PointField offsets and datatype codes) for
@@ -129,11 +147,36 @@ typedef struct {
   double stage_ms[8];                /* host-measured stage times */
   double iw_meas_dPsi[3 * 9];        /* measurement-noise IW statistics [gyro, accel, lidar] 3x3 blocks */
   double iw_meas_dnu[3];
+  double L_imu_odom[GCS_D_Z * GCS_D_Z]; /* summed IMU/odometry evidence (pipeline.py:745-750), untempered */
+  double h_imu_odom[GCS_D_Z];
+  /* the eleven IMU/odometry certificates in all_certs order [odom, imu, imu_dep, gyro, preint, planar,
+   * vz, odom_vel, odom_wz, kinematic, odom_dep], 7 fields each: [ess_total, support_frac, nll_per_ess,
+   * lift_strength, psd_projection_delta, mass_epsilon_ratio, trust_alpha] */
+  double imu_odom_certs[11 * 7];
 } gcs_scan_outputs;
+
+/* Inputs of the IMU/odometry evidence branch on its own (gcs_imu_odom_evidence): every quantity
+ * the reference's _compute_imu_odom_branch reads (pipeline.py:595-776). */
+typedef struct {
+  int32_t m;                               /* IMU window length (>= 2) */
+  const double *stamps, *gyro, *accel;     /* [m], [m*3], [m*3]; stamps <= 0 are padding */
+  const double* w_int;                     /* scan-to-scan window weights [m] */
+  double t_last_scan, t_scan, dt_sec;
+  const double* pose0;                     /* belief_prev.mean_world_pose [6] */
+  const double* pose_pred;                 /* belief_pred.mean_world_pose [6] */
+  const double* mu_prev;                   /* belief_prev.mean_increment [22] */
+  const double* mu_inc;                    /* belief_pred.mean_increment [22] */
+  const double* gravity_W;                 /* [3], gravity scale applied */
+  const double *Sigma_g, *Sigma_a;         /* [9] each */
+  const double *odom_pose, *odom_cov_se3, *odom_twist, *odom_twist_cov;
+  double planar_z_ref, planar_z_sigma, planar_vz_sigma;
+} gcs_imu_odom_inputs;
 
 /* ---------------------------------------------------------------- context */
 const char* gcs_version(void);
 int gcs_abi_version(void);
+/* the reference's PipelineConfig / constants.py defaults (dense mode, B=48, cap 8192, K=16) */
+int gcs_config_defaults(gcs_config* cfg);
 int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out);
 int gcs_ctx_destroy(gcs_ctx* ctx);
 const char* gcs_last_error(const gcs_ctx* ctx);
@@ -144,6 +187,12 @@ int gcs_ctx_synchronize(gcs_ctx* ctx);
  * 2 bin moment-match kernel (+ fused Matrix-Fisher in scale mode), 3 MF (dense / per-op),
  * 4 planar, 5 pushforward].  Each timed stage costs a few us of queue time. */
 int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
+/* Debug knobs (tests): GCS_DEBUG_SCAN_SPIN_LIMIT bounds k_scan's decoupled look-back spin (default
+ * 1 << 22; when it runs out the scan returns GCS_ERR_HIP), GCS_DEBUG_INJECT_SCAN_FAIL != 0 makes
+ * one look-back tile take that failure path on every scan. */
+#define GCS_DEBUG_SCAN_SPIN_LIMIT 1
+#define GCS_DEBUG_INJECT_SCAN_FAIL 2
+int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*6*/, int64_t* counts /*6*/, int32_t reset);
 int gcs_ctx_set_atlas(gcs_ctx* ctx, const double* dirs_host /*B*3*/);
 int gcs_ctx_get_atlas(gcs_ctx* ctx, double* dirs_host /*B*3*/, int32_t* knn_host /*B*K*/);
@@ -219,6 +268,11 @@ int gcs_preintegrate_imu(int32_t m, const double* stamps, const double* gyro, co
 int gcs_belief_world_pose(const gcs_belief* b, double* pose6); /* belief.py:410-434 */
 /* gyro + accel measurement-noise IW statistics of one IMU window (pipeline.py:522-566;
  * measurement_noise_iw_jax.py:130-218); w_int = scan-to-scan window weights, stamps <= 0 are padding */
+/* _compute_imu_odom_branch (pipeline.py:595-776): L [22*22], h [22] (dependence scales applied);
+ * cert = [trigger sum of the eleven certs, ess_imu_weighted, kappa, transport_sigma, imu scale,
+ *         odom scale, mean reliability, odom nll, imu nll/ess, gyro nll, dt_int, dt_imu, omega_avg(3)] */
+#define GCS_IMU_ODOM_CERT_LEN 15
+int gcs_imu_odom_evidence(const gcs_imu_odom_inputs* in, double* L, double* h, double* cert);
 int gcs_imu_meas_iw_suffstats(int32_t m, const double* stamps, const double* gyro, const double* accel,
                               const double* w_int, const double* gyro_bias, const double* accel_bias,
                               const double* rotvec0, const double* gravity_W, double* dPsi3x9, double* dnu3);
@@ -233,6 +287,23 @@ int gcs_nearest_bins(int32_t n_bins, const double* dirs, int32_t n_query, const 
 /* Pack this hypothesis' contribution (weights pre-applied) for an RCCL sum all-reduce:
  * [w_iw dPsi 252 | w_iw dnu 7 | w_iw dPsi_meas 27 | w_iw dnu_meas 3 | w L 484 | w h 22 | w z 22 | w mu 22 | w |mu|^2 1] */
 int gcs_hypothesis_payload(gcs_ctx* ctx, double w_iw, double w_bary, double* payload_host);
+/* hypothesis_barycenter_projection (hypothesis.py:51-236) on host arrays, no context and no side
+ * effects: weights floored at 0.0025 and renormalised, L = PSD(sum w L_k), h, z_lin = sum w (h, z).
+ * cert6 = [psd_delta, floor_adjustment, ess = 1/sum w^2, support_frac, spread_proxy, cond] */
+int gcs_hypothesis_barycenter(int32_t n_hyp, const double* L_stack /*n*484*/, const double* h_stack /*n*22*/,
+                              const double* z_stack /*n*22*/, const double* weights /*n*/, double* L_out, double* h_out,
+                              double* z_out, double* cert6);
+/* process_noise_iw_apply_suffstats_jax (inverse_wishart_jax.py:126-185): state (nu7, Psi 7x36) <- apply
+ * (dPsi, dnu); cert2 = [psd_delta, nu_delta].  process_noise_state_to_Q_jax (:35-68). */
+int gcs_process_iw_apply(const double* nu7, const double* Psi7x36, const double* dPsi7x36, const double* dnu7,
+                         double* nu_out, double* Psi_out, double* cert2);
+int gcs_process_noise_Q(const double* nu7, const double* Psi7x36, double* Q22x22);
+/* measurement_noise_mean_jax (IW mode, measurement_noise_iw_jax.py:38-56) of block idx (0 gyro, 1 accel, 2 lidar) */
+int gcs_meas_iw_mode(const double* nu3, const double* Psi3x9, int32_t idx, double* Sigma3x3);
+/* Runtime description of a context (RuntimeManifest, pipeline.py:1629-1793, for the bin path): JSON
+ * with the library version, device, declared parameters (tau rule, K, cap, map mode, pushforward
+ * form) and kernel set.  Writes at most len bytes (NUL-terminated); returns GCS_ERR_ARG if too short. */
+int gcs_ctx_describe(gcs_ctx* ctx, char* buf, int32_t len);
 /* Apply the summed payload: barycenter (PSD of L), process IW apply + Q rebuild and
  * measurement-noise IW apply (backend_node.py:2102-2119; both stored in ctx).
  * combined_out may be NULL; cert_out = [psd_delta, spread, iw_psd_delta, iw_nu_delta]. */

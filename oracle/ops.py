@@ -458,7 +458,8 @@ def matrix_fisher_rotation(R_pred, scan_s_dir, scan_S, scan_N, map_S_dir, map_S,
     return dict(R_mf=R_mf, L_rot=L_rot, h_rot=h_rot, delta_rot=delta_rot, svd_s=s, H=H, N_eff=N_eff,
                 scan_scatter_total=scan_S.sum(0), map_scatter_total=map_S.sum(0),
                 psd_projection_delta=cert[0], mass_epsilon_ratio=eps / (N_eff + eps),
-                nll=0.5 * float(delta_rot @ L_rot @ delta_rot))
+                nll=0.5 * float(delta_rot @ L_rot @ delta_rot),
+                nll_per_ess=0.5 * float(delta_rot @ L_rot @ delta_rot) / (N_eff + eps))  # cert :355-375
 
 
 # ================================================================ row 8: PlanarTranslationEvidence
@@ -487,7 +488,8 @@ def planar_translation(t_pred, R_hat, scan_p_bar, scan_Sigma_p, scan_N, map_cent
     return dict(t_wls=t_wls, L_trans=L_trans, h_trans=h_trans, delta_trans=delta, z_scale=z_scale,
                 L_full=L_full, h_full=h_full, N_eff=N_eff, psd_projection_delta=cert[0],
                 mass_epsilon_ratio=eps / (N_eff + eps),
-                nll=0.5 * float(delta @ L_trans @ delta))
+                nll=0.5 * float(delta @ L_trans @ delta),
+                nll_per_ess=0.5 * float(delta @ L_trans @ delta) / (N_eff + eps))  # cert :630-653
 
 
 def combined_lidar_evidence_22d(mf, pt):

@@ -2,10 +2,11 @@
 
 Step order follows README.md:105-122 with the live calling convention of
 process_scan_single_hypothesis (FS/backend/pipeline.py:316-1591); see SURVEY.md
-section 3.3 for the reconstruction.  Out of scope this round: the
-IMU/odom evidence family of step 9 (pipeline.py:595-776) -- it enters as an
-optional external (L, h) term.  Scans without t_last_scan / t_scan keys use the scan window
-(scan_start_time, scan_end_time) for the scan-to-scan IMU window.
+section 3.3 for the reconstruction.  Step 9 sums the LiDAR bin evidence with the IMU/odometry
+evidence family (pipeline.py:595-776, oracle/imu_odom.py) and an optional external (L, h) term.
+Scans without t_last_scan / t_scan keys use the scan window (scan_start_time, scan_end_time) for
+the scan-to-scan IMU window; scans without odometry get the node's "no odometry yet" inputs
+(identity pose, 1e12 I covariances; backend_node.py:939-940,2047-2051).
 """
 
 from __future__ import annotations
@@ -15,7 +16,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from . import ops, se3
+from . import imu_odom, ops, se3
 from .primitives import psd_project, spd_inverse_lifted
 
 
@@ -30,6 +31,14 @@ class BinPathConfig:
     deskew_rotation_only: bool = False
     forgetting_factor: float = ops.FORGETTING_FACTOR
     gravity_W: tuple = ops.GRAVITY_W
+    # step 9 IMU/odometry family (PipelineConfig, FS/backend/pipeline.py:96-223)
+    use_imu_odom: bool = True
+    planar_z_ref: float = imu_odom.PLANAR_Z_REF
+    planar_z_sigma: float = imu_odom.PLANAR_Z_SIGMA
+    planar_vz_sigma: float = imu_odom.PLANAR_VZ_SIGMA
+    alpha_min: float = imu_odom.ALPHA_MIN
+    alpha_max: float = imu_odom.ALPHA_MAX
+    c0_cond: float = imu_odom.C0_COND
 
     def temperature(self):
         return ops.tau_for_bins(self.n_bins) if self.tau is None else self.tau
@@ -53,10 +62,21 @@ def _aggregate_ess(certs):
     return sum(c.get("ess_total", 0.0) for c in certs) / len(certs)
 
 
+def scan_odometry(scan):
+    """Odometry inputs of a scan, or the node's defaults when it carries none."""
+    big = imu_odom.ODOM_COV_MISSING * np.eye(6)
+    return (np.asarray(scan.get("odom_pose", np.zeros(6)), np.float64),
+            np.asarray(scan.get("odom_cov_se3", big), np.float64),
+            np.asarray(scan.get("odom_twist", np.zeros(6)), np.float64),
+            np.asarray(scan.get("odom_twist_cov", big), np.float64))
+
+
 def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathConfig, bins, knn,
-                          map_state: MapState, L_ext=None, h_ext=None):
+                          map_state: MapState, L_ext=None, h_ext=None, meas_state=None, Sigma_g=None, Sigma_a=None):
     """One hypothesis, one scan.  `scan` keys: points (N,3), timestamps, weights, imu_stamps,
-    imu_gyro, imu_accel, scan_start_time, scan_end_time, dt_sec."""
+    imu_gyro, imu_accel, scan_start_time, scan_end_time, dt_sec (+ t_last_scan, t_scan, odom_pose,
+    odom_cov_se3, odom_twist, odom_twist_cov).  Sigma_g / Sigma_a default to the IW modes of
+    meas_state (datasheet state when None), as the node sets them per scan (backend_node.py:2020-2023)."""
     certs = []   # list of dicts: influence fields + ess_total (+ name)
     # 1 PointBudgetResample (pipeline.py:399-418)
     bud = ops.point_budget_resample(scan["points"], scan["timestamps"], scan["weights"],
@@ -76,8 +96,8 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
                                mu_inc[9:12], mu_inc[12:15], np.asarray(cfg.gravity_W))
     xi = se3.se3_log(pre["delta_pose"])
     # measurement-noise IW statistics over the scan-to-scan window (pipeline.py:448-453,522-566)
-    w_int = ops.smooth_window_weights(scan["imu_stamps"], scan.get("t_last_scan", scan["scan_start_time"]),
-                                      scan.get("t_scan", scan["scan_end_time"]), sigma_warp)
+    t_last, t_scan = scan.get("t_last_scan", scan["scan_start_time"]), scan.get("t_scan", scan["scan_end_time"])
+    w_int = ops.smooth_window_weights(scan["imu_stamps"], t_last, t_scan, sigma_warp)
     meas_dPsi, meas_dnu = ops.imu_meas_iw_suffstats(scan["imu_stamps"], scan["imu_gyro"], scan["imu_accel"], w_int,
                                                     mu_inc[9:12], mu_inc[12:15], pose0[3:6],
                                                     np.asarray(cfg.gravity_W))
@@ -87,6 +107,28 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
                                    scan["scan_start_time"], scan["scan_end_time"], xi)
     cert_deskew = dict(name="deskew", ess_total=pre["ess"])
     certs.append(cert_deskew)
+    # step 9 IMU + odometry evidence (pipeline.py:595-776)
+    io = None
+    if cfg.use_imu_odom:
+        if meas_state is None:
+            meas_state = ops.datasheet_measurement_noise_state()
+        Sg = imu_odom.measurement_noise_mean(*meas_state, 0) if Sigma_g is None else np.asarray(Sigma_g)
+        Sa = imu_odom.measurement_noise_mean(*meas_state, 1) if Sigma_a is None else np.asarray(Sigma_a)
+        dt_int = imu_odom.compute_imu_integration_time(scan["imu_stamps"], t_last, t_scan)
+        dt_imu, omega_avg = imu_odom.dt_imu_and_omega_avg(scan["imu_stamps"], scan["imu_gyro"], w_int, mu_inc[9:12])
+        pre_int = ops.preintegrate_imu(scan["imu_stamps"], scan["imu_gyro"], scan["imu_accel"], w_int, pose0[3:6],
+                                       mu_inc[9:12], mu_inc[12:15], np.asarray(cfg.gravity_W))
+        op, oc, ot, otc = scan_odometry(scan)
+        L_io, h_io, io_certs, io_named, io_info = imu_odom.imu_odom_branch(
+            pose0=pose0, pose_pred=b_pred.mean_world_pose(), mu_prev=belief_prev.mean_increment(), mu_inc=mu_inc,
+            imu_stamps=scan["imu_stamps"], imu_gyro=scan["imu_gyro"], imu_accel=scan["imu_accel"], w_int=w_int,
+            dt_imu=dt_imu, omega_avg=omega_avg, dt_int=dt_int, pre_int=pre_int, gravity_W=np.asarray(cfg.gravity_W),
+            Sigma_g=Sg, Sigma_a=Sa, odom_pose=op, odom_cov=oc, odom_twist=ot, odom_twist_cov=otc,
+            dt_sec=scan["dt_sec"], planar_z_ref=cfg.planar_z_ref, planar_z_sigma=cfg.planar_z_sigma,
+            planar_vz_sigma=cfg.planar_vz_sigma)
+        certs.extend(io_certs)
+        io = dict(L=L_io, h=h_io, certs=io_certs, named=io_named, info=io_info, dt_int=dt_int, dt_imu=dt_imu,
+                  omega_avg=omega_avg, pre_int=pre_int)
     # 4-6 BinSoftAssign + ScanBinMomentMatch (+Kappa)
     origin = np.asarray(cfg.lidar_origin, np.float64)
     d = ops.point_directions(dk["points"], origin)
@@ -117,15 +159,23 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
     certs.extend([cert_sa, cert_mm, cert_mf, cert_pt])
     # 9 evidence + power tempering (pipeline.py:1038-1117) + excitation scaling (:1119-1148)
     L_lidar, h_lidar = ops.combined_lidar_evidence_22d(mf, pt)
-    L_raw = L_lidar + (0.0 if L_ext is None else L_ext)
-    h_raw = h_lidar + (0.0 if h_ext is None else h_ext)
+    L_raw = L_lidar + (0.0 if L_ext is None else L_ext) + (0.0 if io is None else io["L"])
+    h_raw = h_lidar + (0.0 if h_ext is None else h_ext) + (0.0 if io is None else io["h"])
     eps = ops.EPS_MASS
     dt_pose = np.linalg.norm(L_raw[15, 0:6]) + np.linalg.norm(L_raw[0:6, 15])
     dt_vel = np.linalg.norm(L_raw[15, 6:9]) + np.linalg.norm(L_raw[6:9, 15])
     dt_asym = min(max(abs(dt_vel - dt_pose) / (dt_vel + dt_pose + eps), 0.0), 1.0)
     z_to_xy = abs(L_raw[2, 2]) / (0.5 * (abs(L_raw[0, 0]) + abs(L_raw[1, 1])) + eps)
-    ess_total = _aggregate_ess([dict(ess_total=_aggregate_ess(lidar_certs))])
-    exc_total = 0.0   # max dt_effect + max extrinsic_effect over the bin-path certs (all 0)
+    # combined evidence cert = aggregate([aggregate(lidar certs), odom, imu, gyro]) (pipeline.py:1057-1067)
+    ev_ess = _aggregate_ess(lidar_certs)
+    ev_nll = mf["nll_per_ess"] + pt["nll_per_ess"]
+    if io is None:
+        ess_total, nll_total = ev_ess, ev_nll
+    else:
+        named = io["named"]
+        ess_total = (ev_ess + named["odom"]["ess_total"] + named["imu"]["ess_total"] + named["gyro"]["ess_total"]) / 4.0
+        nll_total = ev_nll + named["odom"]["nll_per_ess"] + named["imu"]["nll_per_ess"] + named["gyro"]["nll_per_ess"]
+    exc_total = 0.0   # no reference operator fills an ExcitationCert (certificates.py:564-567 aggregates zeros)
     ess_to_exc = ess_total / (exc_total + eps)
     s_z = z_to_xy / (z_to_xy + ops.POWER_BETA_Z_C)
     s_exc = 1.0 / (1.0 + ess_to_exc / ops.POWER_BETA_EXC_C)
@@ -138,8 +188,13 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
     Lp, hp = ops.apply_excitation_scaling(b_pred.L, b_pred.h, s_dt, s_ex)
     certs.append(dict(name="excitation", dt_scale=1.0 - s_dt, extrinsic_scale=1.0 - s_ex))
     b_pred = ops.Belief(b_pred.X_anchor, b_pred.stamp_sec, b_pred.z_lin, Lp, hp)
-    # 10 FusionScaleFromCertificates: alpha_min = alpha_max = 1 (constants.py:89-90) -> alpha = 1
-    alpha = 1.0
+    # 10 FusionScaleFromCertificates with the pose-6 conditioning of the tempered evidence
+    # (pipeline.py:1150-1192, fusion.py:46-142)
+    cond6 = imu_odom.pose6_conditioning(L_ev)
+    alpha, quality = imu_odom.fusion_scale_from_certificates(
+        dict(cond=cond6["cond"], ess_total=ess_total, nll_per_ess=nll_total, power_beta=beta),
+        alpha_min=cfg.alpha_min, alpha_max=cfg.alpha_max, c0_cond=cfg.c0_cond, excitation_total=exc_total,
+        dt_asymmetry=dt_asym, z_to_xy_ratio=z_to_xy)
     certs.append(dict(name="fusion_scale", trust_alpha=alpha))
     # 11 InfoFusionAdditive
     b_post, infl = ops.info_fusion_additive(b_pred, L_ev, h_ev, alpha)
@@ -161,7 +216,8 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
                 iw_meas_dPsi=meas_dPsi, iw_meas_dnu=meas_dnu, budget=bud, deskew=dk, soft_assign=sa, scan_bins=st, mf=mf, planar=pt,
                 L_evidence=L_ev, h_evidence=h_ev, beta=beta, total_trigger=T,
                 frobenius_strength=rinfo["frobenius_strength"], z_t=z_t, xi_body=xi, certs=certs,
-                belief_post=b_post, belief_recomposed=b_rec)
+                belief_post=b_post, belief_recomposed=b_rec, imu_odom=io, alpha=alpha, fusion_quality=quality,
+                cond_pose6=cond6, ess_total=ess_total, nll_total=nll_total)
 
 
 def combine_and_update_noise(results, weights, iw_state, scan_count, meas_state=None):

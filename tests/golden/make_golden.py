@@ -96,9 +96,10 @@ def scan_steps(mode, B, cap, n_raw, n_scans=3):
     Q = ops.process_noise_Q(nu, Psi)
     ms = opipe.MapState.empty(B)
     out = dict(mode=mode, n_bins=B, cap=cap, n_raw=n_raw, Q=Q, tau=cfg.tau)
-    keys = ("xyz_record", "timestamps", "weights", "imu_stamps", "imu_gyro", "imu_accel")
+    keys = ("xyz_record", "timestamps", "weights", "imu_stamps", "imu_gyro", "imu_accel", "odom_pose", "odom_cov_se3",
+            "odom_twist", "odom_twist_cov")
     rec = {k: [] for k in ("z_t", "X_anchor", "L", "h", "z_lin", "beta", "T", "dPsi", "dnu", "meas_dPsi",
-                           "meas_dnu", "L_ev", "h_ev", "scan_N", "map")}
+                           "meas_dnu", "L_ev", "h_ev", "scan_N", "map", "L_io", "h_io", "alpha")}
     times = ("scan_start_time", "scan_end_time", "dt_sec", "t_last_scan", "t_scan")
     for k in keys + times:
         out[f"in_{k}"] = []
@@ -121,6 +122,9 @@ def scan_steps(mode, B, cap, n_raw, n_scans=3):
         rec["L_ev"].append(r["L_evidence"])
         rec["h_ev"].append(r["h_evidence"])
         rec["scan_N"].append(r["scan_bins"]["N"])
+        rec["L_io"].append(r["imu_odom"]["L"])   # step 9 IMU/odometry evidence (pipeline.py:745-750)
+        rec["h_io"].append(r["imu_odom"]["h"])
+        rec["alpha"].append(r["alpha"])
         st = r["map"].stats
         rec["map"].append(np.concatenate([st.S_dir.T, st.S_dir_scatter.reshape(B, 9).T, st.N_dir[None],
                                           st.N_pos[None], st.sum_p.T, st.sum_ppT.reshape(B, 9).T], axis=0))

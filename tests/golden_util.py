@@ -20,4 +20,6 @@ def scan_dict(g, s):
                 weights=g["in_weights"][s], imu_stamps=g["in_imu_stamps"][s], imu_gyro=g["in_imu_gyro"][s],
                 imu_accel=g["in_imu_accel"][s], scan_start_time=float(g["in_scan_start_time"][s]),
                 scan_end_time=float(g["in_scan_end_time"][s]), dt_sec=float(g["in_dt_sec"][s]),
-                t_last_scan=float(g["in_t_last_scan"][s]), t_scan=float(g["in_t_scan"][s]))
+                t_last_scan=float(g["in_t_last_scan"][s]), t_scan=float(g["in_t_scan"][s]),
+                **{k: g[f"in_{k}"][s] for k in ("odom_pose", "odom_cov_se3", "odom_twist", "odom_twist_cov")
+                   if f"in_{k}" in g})

@@ -11,6 +11,7 @@ import pytest
 torch = pytest.importorskip("torch")
 
 from golden_util import ORIGIN, load, scan_dict
+from gcslam.synthetic import scan_kwargs
 from gpu_util import assert_close, device_scan, scan_fields
 from test_distributed_gloo import pack_payload
 
@@ -88,9 +89,7 @@ def test_gpu_golden_scan_steps(name):
     for s in range(g["out_z_t"].shape[0]):
         sc = scan_dict(g, s)
         rec, t, w = device_scan(sc)
-        out = ctx.scan(rec, 16, t, w, int(g["n_raw"]), sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"],
-                       sc["scan_start_time"], sc["scan_end_time"], sc["dt_sec"], Q=g["Q"],
-                       t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"])
+        out = ctx.scan(rec, 16, t, w, int(g["n_raw"]), **scan_kwargs(sc), Q=g["Q"])
         X, _, z, Lm, h = ctx.get_belief()
         cert = np.array(out.cert[:])
         assert cert[30] == pytest.approx(float(g["out_beta"][s]), rel=1e-12)
@@ -109,6 +108,13 @@ def test_gpu_golden_scan_steps(name):
         assert_close(f"scan{s} meas dPsi", np.array(out.iw_meas_dPsi[:]).reshape(3, 3, 3), mref,
                      rtol=1e-9, atol=1e-13 * np.abs(mref).max())
         assert np.array_equal(np.array(out.iw_meas_dnu[:]), g["out_meas_dnu"][s])
+        # step 9 IMU/odometry evidence (pipeline.py:595-776) and the fusion scale
+        Lio = g["out_L_io"][s]
+        assert_close(f"scan{s} L_imu_odom", np.array(out.L_imu_odom[:]).reshape(22, 22), Lio, rtol=1e-7,
+                     atol=1e-9 * np.abs(Lio).max())
+        assert_close(f"scan{s} h_imu_odom", np.array(out.h_imu_odom[:]), g["out_h_io"][s], rtol=1e-6,
+                     atol=1e-9 * max(np.abs(g["out_h_io"][s]).max(), 1.0))
+        assert cert[33] == pytest.approx(float(g["out_alpha"][s]), rel=1e-12)
         assert_close(f"scan{s} scan N", ctx.get_scan_stats()[0], g["out_scan_N"][s], rtol=1e-11, atol=1e-14)
         mref = g["out_map"][s]
         assert_close(f"scan{s} map", ctx.get_map()[0], mref, rtol=1e-7, atol=1e-9 * max(np.abs(mref).max(), 1.0))

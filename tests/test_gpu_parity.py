@@ -10,6 +10,7 @@ torch = pytest.importorskip("torch")
 from gpu_util import (assert_close, derived_fields, device_scan, map_fields, map_from_fields, scan_fields,
                       scan_from_fields)
 from oracle import ops, pipeline as opipe, se3
+from gcslam.synthetic import scan_kwargs
 
 pytestmark = pytest.mark.gpu
 
@@ -214,9 +215,7 @@ def test_full_pipeline_matches_oracle(mode, B, cap, n_raw):
         sc = syn.make_scan(n_raw, k)
         ref = opipe.process_scan_bin_path(b, sc, Q, cfg, dirs, knn, ms)
         rec, t, w = device_scan(sc)
-        out = ctx.scan(rec, 16, t, w, n_raw, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"],
-                       sc["scan_start_time"], sc["scan_end_time"], sc["dt_sec"], Q=Q,
-                       t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"])
+        out = ctx.scan(rec, 16, t, w, n_raw, **scan_kwargs(sc), Q=Q)
         X, stamp, z, Lm, h = ctx.get_belief()
         cert = np.array(out.cert[:])
         assert cert[30] == pytest.approx(ref["beta"], rel=1e-12)
@@ -254,8 +253,7 @@ def test_bitwise_determinism_scale():
         ctx = _ctx(n_bins=20000, n_points_cap=8192, mode="scale")
         sc = syn.make_scan(8192, 7)
         rec, t, w = device_scan(sc)
-        o = ctx.scan(rec, 16, t, w, 8192, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
-                     sc["scan_end_time"], sc["dt_sec"])
+        o = ctx.scan(rec, 16, t, w, 8192, **scan_kwargs(sc))
         outs.append((ctx.get_scan_stats(), ctx.get_map()[0], np.array(o.belief.L[:]), np.array(o.cert[:])))
         ctx.close()
     for a, b in zip(outs[0], outs[1]):
@@ -288,8 +286,7 @@ def test_empty_scan_and_zero_twist():
     syn = _synthetic()
     sc = syn.make_scan(64, 0)
     rec, t, w = device_scan(sc)
-    o = ctx.scan(rec, 16, t, w, 0, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
-                 sc["scan_end_time"], sc["dt_sec"])
+    o = ctx.scan(rec, 16, t, w, 0, **scan_kwargs(sc))
     assert np.all(np.isfinite(np.array(o.belief.L[:])))
     st = ctx.get_scan_stats()
     assert np.all(st[0] == 0.0)

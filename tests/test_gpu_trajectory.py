@@ -19,6 +19,7 @@ import pytest
 torch = pytest.importorskip("torch")
 
 from golden_util import ORIGIN
+from gcslam.synthetic import scan_kwargs
 
 pytestmark = pytest.mark.gpu
 
@@ -42,7 +43,7 @@ def oracle_trajectory(mode, B, cap, n_raw, scans):
     ms = opipe.MapState.empty(B)
     zs = []
     for s, sc in enumerate(scans):
-        r = opipe.process_scan_bin_path(b, sc, Q, cfg, bins, knn, ms)
+        r = opipe.process_scan_bin_path(b, sc, Q, cfg, bins, knn, ms, meas_state=meas)
         zs.append(np.asarray(r["z_t"], np.float64))
         c = opipe.combine_and_update_noise([r], np.array([1.0]), iw, s, meas)
         Q, iw, meas = c["Q"], c["iw_state"], c["meas_state"]
@@ -61,9 +62,7 @@ def hip_trajectory(mode, B, cap, n_raw, scans):
             rec = torch.from_numpy(sc["xyz_record"]).cuda()
             t = torch.from_numpy(sc["timestamps"]).cuda()
             w = torch.from_numpy(sc["weights"]).cuda()
-            out = ctx.scan(rec, 16, t, w, n_raw, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"],
-                           sc["scan_start_time"], sc["scan_end_time"], sc["dt_sec"],
-                           t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"])
+            out = ctx.scan(rec, 16, t, w, n_raw, **scan_kwargs(sc))
             zs.append(np.array(out.z_t[:], np.float64))
             combine_allreduce(ctx, 0, 1, s, want_belief=False)
     finally:

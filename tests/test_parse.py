@@ -9,6 +9,7 @@ import numpy as np
 import pytest
 
 from oracle import ops
+from gcslam.synthetic import scan_kwargs
 
 F32, F64, U16, U32 = 7, 8, 4, 6
 NP = {F32: "<f4", F64: "<f8", U16: "<u2", U32: "<u4"}
@@ -137,8 +138,7 @@ def test_gpu_scan_from_parsed_cloud_matches_oracle():
         p_ref, t_ref, w_ref, _, _ = ops.parse_pointcloud2_vlp16(data, fields, step, 4096, 0.0)
         sref = dict(sc, points=ops.lidar_to_base(p_ref, np.eye(3), tb), timestamps=t_ref, weights=w_ref)
         ref = opipe.process_scan_bin_path(b, sref, Q, cfg, dirs, knn, ms)
-        out = ctx.scan(pts, 24, t, w, 4096, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
-                       sc["scan_end_time"], sc["dt_sec"], Q=Q, t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"],
+        out = ctx.scan(pts, 24, t, w, 4096, **scan_kwargs(sc), Q=Q,
                        xyz_f64=True)
         np.testing.assert_allclose(np.array(out.z_t[:]), ref["z_t"], rtol=1e-7, atol=1e-9)
         np.testing.assert_allclose(ctx.get_scan_stats()[0], ref["scan_bins"]["N"], rtol=1e-11, atol=1e-14)

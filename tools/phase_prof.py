@@ -20,6 +20,7 @@ os.environ.setdefault("GCSLAM_LIB", os.path.join(ROOT, "gc-slam_amd", "gcslam", 
 def main():
     import torch
     from gcslam import synthetic
+    from gcslam.synthetic import scan_kwargs
     from gcslam.context import HypothesisContext
     cfg = {"c2": (65536, 100000), "c3": (262144, 1048576)}[sys.argv[1] if len(sys.argv) > 1 else "c2"]
     N, B = cfg
@@ -30,8 +31,7 @@ def main():
         rec = torch.from_numpy(sc["xyz_record"]).cuda()
         t = torch.from_numpy(sc["timestamps"]).cuda()
         w = torch.from_numpy(sc["weights"]).cuda()
-        ctx.scan(rec, 16, t, w, N, sc["imu_stamps"], sc["imu_gyro"], sc["imu_accel"], sc["scan_start_time"],
-                 sc["scan_end_time"], sc["dt_sec"])
+        ctx.scan(rec, 16, t, w, N, **scan_kwargs(sc))
     ctx.synchronize()
     pc = (C.c_ulonglong * 4)()
     ctx.lib.gcs_debug_psd_count.argtypes = [C.c_void_p, C.c_int]
