@@ -122,11 +122,14 @@ def _mm_reference(ctx, p0, wout):
     return ops.scan_bin_moment_match_dense(p0, wout, sa["responsibilities"], np.array(ORIGIN))
 
 
-def _check_scan_stats(got, st):
+def _check_scan_stats(got, st, amp=1.0):
+    """amp scales the responsibility-driven bars: the soft-assign logits are (s - m) / tau, so a
+    1-ulp difference in a direction cosine moves a responsibility by ~ulp / tau relative (tau =
+    4.6e-6 at B = 1M, DESIGN.md declared tau rule); callers pass amp = max(1, 10 ulp / tau / 1e-11)."""
     ref = scan_fields(st)
-    assert_close("N", got[0], ref[0], rtol=1e-11, atol=1e-14)
-    assert_close("s_dir", got[1:4], ref[1:4], rtol=1e-10, atol=1e-13)
-    assert_close("S_dir_scatter", got[4:13], ref[4:13], rtol=1e-10, atol=1e-13)
+    assert_close("N", got[0], ref[0], rtol=1e-11 * amp, atol=1e-14)
+    assert_close("s_dir", got[1:4], ref[1:4], rtol=1e-10 * amp, atol=1e-13)
+    assert_close("S_dir_scatter", got[4:13], ref[4:13], rtol=1e-10 * amp, atol=1e-13)
     assert_close("p_bar", got[13:16], ref[13:16], rtol=1e-9, atol=1e-10)
     assert_close("Sigma_p", got[16:25], ref[16:25], rtol=1e-7, atol=1e-10)       # m^2, PSD-projected
     assert_close("kappa", got[25], ref[25], rtol=1e-8, atol=1e-10)
