@@ -266,9 +266,11 @@ def main():
     device = f"cuda:{local_rank}"
     torch.cuda.set_device(local_rank)
 
-    from gcslam.distributed import combine_allreduce
+    from gcslam.distributed import HypothesisComm, combine_allreduce
     from gcslam.synthetic import scan_kwargs
 
+    # the per-scan exchange runs in the library over RCCL (torch.distributed only broadcasts the id)
+    comm = HypothesisComm(rank, world, local_rank) if world > 1 else None
     cfg = CONFIGS[args.config]
     N, B, K = cfg["N"], cfg["B"], cfg["K"]
     ctx = make_ctx(cfg, local_rank)
@@ -291,7 +293,7 @@ def main():
         sc, rec, t, w = scans[state["count"] % N_SCANS]
         out = ctx.scan(rec, 16, t, w, N, **scan_kwargs(sc))
         tc = time.perf_counter()
-        combine_allreduce(ctx, rank, world, state["count"], device=device, want_belief=False)
+        combine_allreduce(ctx, rank, world, state["count"], comm=comm, want_belief=False)
         host_ms[4] += (time.perf_counter() - tc) * 1e3
         host_ms[:4] += np.asarray(out.stage_ms[:4])
         state["count"] += 1
@@ -364,6 +366,8 @@ def main():
             line["roofline_c3"] = c3_roofline(local_rank)
         line["cpu_baseline"] = cpu_baseline(cfg) if (world == 1 and not args.no_cpu_baseline) else None
         print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime.h>
 #include <math.h>
+#include <rccl/rccl.h>
 #include <string.h>
 
 #include <algorithm>
@@ -90,6 +91,9 @@ struct gcs_ctx {
   uint32_t* d_err = nullptr;
   uint32_t spin_limit = 1u << 22;
   int inject_scan_fail = 0;
+  // hypothesis all-reduce payload (gcs_combine_allreduce): pinned host staging + device buffer
+  double* h_payload = nullptr;
+  double* d_payload = nullptr;
   // host state
   Belief belief{};
   double iw_nu[7], iw_Psi[7 * 36], Q[DZ * DZ];
@@ -651,6 +655,8 @@ int gcs_ctx_destroy(gcs_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
   if (c->h_err) (void)hipHostFree(c->h_err);
+  if (c->h_payload) (void)hipHostFree(c->h_payload);
+  if (c->d_payload) (void)hipFree(c->d_payload);
   for (int st = 0; st < kStages; ++st)
     for (int k = 0; k < 2; ++k)
       if (c->ev[st][k]) (void)hipEventDestroy(c->ev[st][k]);
@@ -1323,15 +1329,16 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
 }
 
 // ---------------------------------------------------------------- hypothesis payload / combine
-int gcs_hypothesis_payload(gcs_ctx* c, double w_iw, double w_bary, double* p) {
-  if (!c || !p) return GCS_ERR_ARG;
-  memset(p, 0, GCS_PAYLOAD_LEN * sizeof(double));
+namespace {
+// Payload layout: [w_iw dPsi 252 | w_iw dnu 7 | w_iw dPsi_meas 27 | w_iw dnu_meas 3 |
+// w L 484 | w h 22 | w z 22 | w mu 22 | w |mu|^2 1]
+void pack_payload(const Belief& b, const double* dPsi, const double* dnu, const double* mdPsi, const double* mdnu,
+                  double w_iw, double w_bary, double* p) {
   int k = 0;
-  for (int i = 0; i < 252; ++i) p[k++] = w_iw * (c->have_last ? c->last_dPsi[i] : 0.0);
-  for (int i = 0; i < 7; ++i) p[k++] = w_iw * (c->have_last ? c->last_dnu[i] : 0.0);
-  for (int i = 0; i < 27; ++i) p[k++] = w_iw * (c->have_last ? c->last_meas_dPsi[i] : 0.0);
-  for (int i = 0; i < 3; ++i) p[k++] = w_iw * (c->have_last ? c->last_meas_dnu[i] : 0.0);
-  const Belief& b = c->belief;
+  for (int i = 0; i < 252; ++i) p[k++] = w_iw * (dPsi ? dPsi[i] : 0.0);
+  for (int i = 0; i < 7; ++i) p[k++] = w_iw * (dnu ? dnu[i] : 0.0);
+  for (int i = 0; i < 27; ++i) p[k++] = w_iw * (mdPsi ? mdPsi[i] : 0.0);
+  for (int i = 0; i < 3; ++i) p[k++] = w_iw * (mdnu ? mdnu[i] : 0.0);
   for (int i = 0; i < DZ * DZ; ++i) p[k++] = w_bary * b.L[i];
   for (int i = 0; i < DZ; ++i) p[k++] = w_bary * b.h[i];
   for (int i = 0; i < DZ; ++i) p[k++] = w_bary * b.z_lin[i];
@@ -1339,42 +1346,138 @@ int gcs_hypothesis_payload(gcs_ctx* c, double w_iw, double w_bary, double* p) {
   host::mean_increment(b, mu);
   for (int i = 0; i < DZ; ++i) { p[k++] = w_bary * mu[i]; n2 += mu[i] * mu[i]; }
   p[k++] = w_bary * n2;
-  return k == GCS_PAYLOAD_LEN ? GCS_OK : fail(c, GCS_ERR_STATE, "payload size mismatch");
 }
 
-int gcs_hypothesis_combine(gcs_ctx* c, const double* p, int32_t scan_count, gcs_belief* comb, double* cert) {
-  if (!c || !p) return GCS_ERR_ARG;
+// The summed payload -> barycenter (PSD of L, hypothesis.py:92-115) + process IW apply with
+// weight min(1, scan_count) + Q rebuild + measurement IW apply with weight 1 (backend_node.py:2102-2119)
+void apply_payload(const double* p, int32_t scan_count, const double* X_anchor, double stamp, const double* nu7,
+                   const double* Psi, const double* mnu, const double* mPsi, Belief& out, double* nu_out,
+                   double* Psi_out, double* Q_out, double* mnu_out, double* mPsi_out, double* cert4,
+                   double* meas_cert2) {
   const double* dPsi = p;
   const double* dnu = p + 252;
   const double* L = p + 289;
   const double* h = L + 484;
   const double* z = h + 22;
   const double* mu = z + 22;
-  double n2 = mu[22];
-  Belief out{};
-  double delta = host::psd_project(DZ, L, kEpsPsd, out.L);
+  const double n2 = mu[22];
+  memset(&out, 0, sizeof(out));
+  const double delta = host::psd_project(DZ, L, kEpsPsd, out.L);
   memcpy(out.h, h, sizeof(out.h));
   memcpy(out.z_lin, z, sizeof(out.z_lin));
-  memcpy(out.X_anchor, c->belief.X_anchor, sizeof(out.X_anchor));
-  out.stamp = c->belief.stamp;
+  memcpy(out.X_anchor, X_anchor, sizeof(out.X_anchor));
+  out.stamp = stamp;
   double m2 = 0.0;
   for (int i = 0; i < DZ; ++i) m2 += mu[i] * mu[i];
-  double wp = std::min(1, scan_count);
-  double dP[252], dn[7], nu2[7], Psi2[252], c2[2];
+  const double wp = std::min(1, scan_count);
+  double dP[252], dn[7], c2[2];
   for (int i = 0; i < 252; ++i) dP[i] = wp * dPsi[i];
   for (int i = 0; i < 7; ++i) dn[i] = wp * dnu[i];
-  host::process_iw_apply(c->iw_nu, c->iw_Psi, dP, dn, nu2, Psi2, c2);
+  host::process_iw_apply(nu7, Psi, dP, dn, nu_out, Psi_out, c2);
+  host::process_noise_Q(nu_out, Psi_out, Q_out);
+  double mc[2];
+  host::meas_iw_apply(mnu, mPsi, p + 259, p + 286, mnu_out, mPsi_out, mc);
+  if (meas_cert2) { meas_cert2[0] = mc[0]; meas_cert2[1] = mc[1]; }
+  if (cert4) { cert4[0] = delta; cert4[1] = n2 - m2; cert4[2] = c2[0]; cert4[3] = c2[1]; }
+}
+
+int combine_into_ctx(gcs_ctx* c, const double* p, int32_t scan_count, gcs_belief* comb, double* cert) {
+  Belief out;
+  double nu2[7], Psi2[252], Q2[DZ * DZ], mnu2[3], mPsi2[27], c4[4];
+  apply_payload(p, scan_count, c->belief.X_anchor, c->belief.stamp, c->iw_nu, c->iw_Psi, c->meas_nu, c->meas_Psi,
+                out, nu2, Psi2, Q2, mnu2, mPsi2, c4, c->meas_cert);
   memcpy(c->iw_nu, nu2, sizeof(nu2));
   memcpy(c->iw_Psi, Psi2, sizeof(Psi2));
-  host::process_noise_Q(c->iw_nu, c->iw_Psi, c->Q);
-  // measurement-noise IW apply, weight 1 every scan (backend_node.py:2105,2114-2119)
-  double mnu2[3], mPsi2[27];
-  host::meas_iw_apply(c->meas_nu, c->meas_Psi, p + 259, p + 286, mnu2, mPsi2, c->meas_cert);
+  memcpy(c->Q, Q2, sizeof(Q2));
   memcpy(c->meas_nu, mnu2, sizeof(mnu2));
   memcpy(c->meas_Psi, mPsi2, sizeof(mPsi2));
   if (comb) from_host_belief(out, *comb);
-  if (cert) { cert[0] = delta; cert[1] = n2 - m2; cert[2] = c2[0]; cert[3] = c2[1]; }
+  if (cert) memcpy(cert, c4, sizeof(c4));
   return GCS_OK;
+}
+}  // namespace
+
+int gcs_hypothesis_payload(gcs_ctx* c, double w_iw, double w_bary, double* p) {
+  if (!c || !p) return GCS_ERR_ARG;
+  const bool h = c->have_last;
+  pack_payload(c->belief, h ? c->last_dPsi : nullptr, h ? c->last_dnu : nullptr, h ? c->last_meas_dPsi : nullptr,
+               h ? c->last_meas_dnu : nullptr, w_iw, w_bary, p);
+  return GCS_OK;
+}
+
+int gcs_hypothesis_combine(gcs_ctx* c, const double* p, int32_t scan_count, gcs_belief* comb, double* cert) {
+  if (!c || !p) return GCS_ERR_ARG;
+  return combine_into_ctx(c, p, scan_count, comb, cert);
+}
+
+int gcs_payload_pack(const gcs_belief* b, const double* dPsi, const double* dnu, const double* mdPsi,
+                     const double* mdnu, double w_iw, double w_bary, double* payload) {
+  if (!b || !payload) return GCS_ERR_ARG;
+  Belief hb;
+  to_host_belief(*b, hb);
+  pack_payload(hb, dPsi, dnu, mdPsi, mdnu, w_iw, w_bary, payload);
+  return GCS_OK;
+}
+
+int gcs_payload_apply(const double* p, int32_t scan_count, const double* X_anchor, double stamp, const double* nu7,
+                      const double* Psi, const double* mnu, const double* mPsi, gcs_belief* comb, double* nu_out,
+                      double* Psi_out, double* Q_out, double* mnu_out, double* mPsi_out, double* cert4) {
+  if (!p || !X_anchor || !nu7 || !Psi || !mnu || !mPsi || !nu_out || !Psi_out || !Q_out || !mnu_out || !mPsi_out)
+    return GCS_ERR_ARG;
+  Belief out;
+  apply_payload(p, scan_count, X_anchor, stamp, nu7, Psi, mnu, mPsi, out, nu_out, Psi_out, Q_out, mnu_out, mPsi_out,
+                cert4, nullptr);
+  if (comb) from_host_belief(out, *comb);
+  return GCS_OK;
+}
+
+// ---------------------------------------------------------------- RCCL
+int gcs_rccl_get_unique_id(uint8_t* id) {
+  if (!id) return GCS_ERR_ARG;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return GCS_ERR_HIP;
+  static_assert(sizeof(u) == GCS_RCCL_ID_BYTES, "ncclUniqueId size");
+  memcpy(id, &u, sizeof(u));
+  return GCS_OK;
+}
+
+int gcs_rccl_comm_init(int32_t device, int32_t n_ranks, int32_t rank, const uint8_t* id, void** comm) {
+  if (!id || !comm || n_ranks < 1 || rank < 0 || rank >= n_ranks) return GCS_ERR_ARG;
+  *comm = nullptr;
+  if (hipSetDevice(device) != hipSuccess) return GCS_ERR_HIP;
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof(u));
+  ncclComm_t cm = nullptr;
+  if (ncclCommInitRank(&cm, n_ranks, u, rank) != ncclSuccess) return GCS_ERR_HIP;
+  *comm = (void*)cm;
+  return GCS_OK;
+}
+
+int gcs_rccl_comm_destroy(void* comm) {
+  if (!comm) return GCS_OK;
+  return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? GCS_OK : GCS_ERR_HIP;
+}
+
+int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, int32_t scan_count,
+                          gcs_belief* comb, double* cert) {
+  if (!c) return GCS_ERR_ARG;
+  if (!c->h_payload) {
+    HIPCHK(c, hipHostMalloc(&c->h_payload, GCS_PAYLOAD_LEN * sizeof(double), hipHostMallocDefault));
+    HIPCHK(c, hipMalloc(&c->d_payload, GCS_PAYLOAD_LEN * sizeof(double)));
+  }
+  if (int rc = gcs_hypothesis_payload(c, w_iw, w_bary, c->h_payload)) return rc;
+  if (comm) {
+    // the reduction rides the context stream; the previous scan's pushforward keeps running on
+    // push_stream underneath it
+    hipStream_t s = c->stream;
+    HIPCHK(c, hipMemcpyAsync(c->d_payload, c->h_payload, GCS_PAYLOAD_LEN * sizeof(double), hipMemcpyHostToDevice, s));
+    ncclResult_t r = ncclAllReduce(c->d_payload, c->d_payload, GCS_PAYLOAD_LEN, ncclDouble, ncclSum,
+                                   (ncclComm_t)comm, s);
+    if (r != ncclSuccess) return fail(c, GCS_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    HIPCHK(c, hipMemcpyAsync(c->h_payload, c->d_payload, GCS_PAYLOAD_LEN * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipStreamSynchronize(s));
+  }
+  return combine_into_ctx(c, c->h_payload, scan_count, comb, cert);
 }
 
 int gcs_hypothesis_barycenter(int32_t n, const double* Ls, const double* hs, const double* zs, const double* w,

@@ -82,6 +82,7 @@ class GcsImuOdomInputs(C.Structure):
 
 
 IMU_ODOM_CERT_LEN = 15
+RCCL_ID_BYTES = 128
 DEBUG_SCAN_SPIN_LIMIT, DEBUG_INJECT_SCAN_FAIL = 1, 2
 
 
@@ -144,6 +145,15 @@ _SIGS = [
     ("gcs_hypothesis_payload", C.c_int, [C.c_void_p, C.c_double, C.c_double, C.c_void_p]),
     ("gcs_hypothesis_combine", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
     ("gcs_hypothesis_barycenter", C.c_int, [C.c_int32] + [c_double_p] * 8),
+    ("gcs_payload_pack", C.c_int, [C.POINTER(GcsBelief), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
+                                   C.c_double, C.c_void_p]),
+    ("gcs_payload_apply", C.c_int, [C.c_void_p, C.c_int32, C.c_void_p, C.c_double] + [C.c_void_p] * 4 +
+     [C.POINTER(GcsBelief)] + [C.c_void_p] * 6),
+    ("gcs_rccl_get_unique_id", C.c_int, [C.c_void_p]),
+    ("gcs_rccl_comm_init", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("gcs_rccl_comm_destroy", C.c_int, [C.c_void_p]),
+    ("gcs_combine_allreduce", C.c_int, [C.c_void_p, C.c_void_p, C.c_double, C.c_double, C.c_int32, C.c_void_p,
+                                        C.c_void_p]),
     ("gcs_process_iw_apply", C.c_int, [c_double_p] * 7),
     ("gcs_process_noise_Q", C.c_int, [c_double_p] * 3),
     ("gcs_meas_iw_mode", C.c_int, [c_double_p, c_double_p, C.c_int32, c_double_p]),

@@ -281,6 +281,16 @@ class HypothesisContext:
         self._chk(self.lib.gcs_hypothesis_payload(self.h, float(w_iw), float(w_bary), p.ctypes.data), "payload")
         return p
 
+    def combine_allreduce(self, comm, w_iw, w_bary, scan_count, want_belief=True):
+        """gcs_combine_allreduce: payload pack + RCCL sum all-reduce on the context stream (comm =
+        HypothesisComm handle; None = single rank) + combine and IW updates."""
+        b = L.GcsBelief() if want_belief else None
+        cert = np.empty(4)
+        self._chk(self.lib.gcs_combine_allreduce(self.h, comm, float(w_iw), float(w_bary), int(scan_count),
+                                                 C.addressof(b) if want_belief else None, cert.ctypes.data),
+                  "combine_allreduce")
+        return (L.struct_to_arrays(b) if want_belief else None), cert
+
     def hypothesis_combine(self, payload_sum, scan_count, want_belief=True):
         """Barycenter + IW update from the summed payload; returns (belief arrays or None, cert)."""
         p = np.ascontiguousarray(payload_sum, np.float64)

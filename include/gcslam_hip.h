@@ -310,6 +310,29 @@ int gcs_ctx_describe(gcs_ctx* ctx, char* buf, int32_t len);
 int gcs_hypothesis_combine(gcs_ctx* ctx, const double* payload_sum, int32_t scan_count, gcs_belief* combined_out,
                            double* cert_out);
 
+/* Context-free forms of the same payload (host numerics, no GPU): pack one hypothesis' contribution
+ * (any stats pointer may be NULL = zeros) and apply a summed payload to explicit IW states. */
+int gcs_payload_pack(const gcs_belief* b, const double* dPsi252, const double* dnu7, const double* meas_dPsi27,
+                     const double* meas_dnu3, double w_iw, double w_bary, double* payload /*840*/);
+int gcs_payload_apply(const double* payload_sum, int32_t scan_count, const double* X_anchor6, double stamp_sec,
+                      const double* nu7, const double* Psi7x36, const double* meas_nu3, const double* meas_Psi3x9,
+                      gcs_belief* combined_out /*may be NULL*/, double* nu_out, double* Psi_out, double* Q_out,
+                      double* meas_nu_out, double* meas_Psi_out, double* cert4);
+
+/* ---------------------------------------------------------------- RCCL (one rank per GPU) */
+/* The per-scan hypothesis exchange (backend_node.py:1999-2119, hypothesis.py:92-115):
+ * gcs_combine_allreduce packs this context's payload, sum-all-reduces it over the RCCL communicator
+ * on the context stream (xGMI between MI355X GPUs), and applies the combine + IW updates, so every
+ * rank holds bitwise-identical Q and IW states.  comm NULL = a single rank (no exchange).  The
+ * communicator comes from gcs_rccl_comm_init with an id from gcs_rccl_get_unique_id on one rank,
+ * broadcast by the launcher. */
+#define GCS_RCCL_ID_BYTES 128
+int gcs_rccl_get_unique_id(uint8_t* id /*GCS_RCCL_ID_BYTES*/);
+int gcs_rccl_comm_init(int32_t device, int32_t n_ranks, int32_t rank, const uint8_t* id, void** comm);
+int gcs_rccl_comm_destroy(void* comm);
+int gcs_combine_allreduce(gcs_ctx* ctx, void* comm, double w_iw, double w_bary, int32_t scan_count,
+                          gcs_belief* combined_out /*may be NULL*/, double* cert4 /*may be NULL*/);
+
 #ifdef __cplusplus
 }
 #endif

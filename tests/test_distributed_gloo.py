@@ -6,8 +6,11 @@ hypothesis weights (backend_node.py:1999-2002, 2085-2090) and the barycenter sum
 hypothesis_barycenter_projection weighted by the floor-renormalised weights (hypothesis.py:83-99,
 spread :103-115).  Here two gloo ranks build the payload of their own hypothesis, all-reduce it
 through gcslam.distributed.allreduce_payload (the function bench.py calls over RCCL), and the
-decoded sums are checked against the oracle's barycenter on the same beliefs.  The payload packing
-below restates gcs_hypothesis_payload (gcs_capi.cpp); the GPU suite checks the C packing against it.
+decoded sums are checked against the oracle's barycenter on the same beliefs (the payload packing
+below restates gcs_hypothesis_payload; the GPU suite checks the C packing against it).  A second
+test runs the library's own context-free pack / apply (gcs_payload_pack / gcs_payload_apply) on
+both ranks for three scans.  tests/test_gpu_distributed.py runs the same exchange between two
+gcs_ctx on one GPU.
 """
 
 import os
@@ -105,11 +108,98 @@ def test_gloo_world2_payload_allreduce_matches_oracle_barycenter():
     mom = tot[817:839]
     spread = tot[839] - float(mom @ mom)   # sum w |mu|^2 - |sum w mu|^2 (hypothesis.py:110-115)
     assert spread == pytest.approx(bary["spread"], rel=1e-9, abs=1e-15)
-    # IW statistics: raw weights 1/H (backend_node.py:2086-2090)
     exp_dPsi = sum(_iw_stats(k)[0] for k in range(WORLD)) / WORLD
     np.testing.assert_allclose(tot[0:252], exp_dPsi, rtol=1e-14, atol=1e-15)
     np.testing.assert_allclose(tot[252:259], np.ones(7), rtol=1e-14)
-    assert not np.any(tot[259:289])   # measurement-noise IW slots (out of scope this round)
+
+
+def _lib_worker(rank, port, q):
+    """One rank of the library-level exchange on CPU: gcs_payload_pack of this rank's hypothesis
+    (belief, process and measurement IW statistics), gloo sum, gcs_payload_apply on the summed
+    payload, three scans in a row with the IW states carried over (backend_node.py:2085-2119)."""
+    import ctypes as C
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in (root, os.path.join(root, "gc-slam_amd")):
+        sys.path.insert(0, p)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from gcslam import _lib as L
+    from gcslam.distributed import allreduce_payload, hypothesis_weights
+    from oracle import ops
+    lib = L.load()
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        w, wn = hypothesis_weights(WORLD)
+        nu, Psi = (np.ascontiguousarray(a) for a in ops.datasheet_process_noise_state())
+        mnu, mPsi = (np.ascontiguousarray(a) for a in ops.datasheet_measurement_noise_state())
+        outs = []
+        for s in range(3):
+            b = _beliefs(WORLD + s)[rank + s]
+            dPsi, dnu = _iw_stats(10 * s + rank)
+            mdPsi = np.ascontiguousarray(np.stack([np.outer(v, v) for v in np.random.default_rng(s + 7 * rank)
+                                                   .normal(0, 1e-3, (3, 3))]))
+            mdnu = np.array([1.0, 1.0, 0.0])
+            bs = L.belief_to_struct(b.X_anchor, b.stamp_sec, b.z_lin, b.L, b.h)
+            p = np.zeros(840)
+            assert lib.gcs_payload_pack(C.byref(bs), dPsi.ctypes.data, dnu.ctypes.data, mdPsi.ctypes.data,
+                                        mdnu.ctypes.data, float(w[rank]), float(wn[rank]), p.ctypes.data) == 0
+            tot = np.ascontiguousarray(allreduce_payload(p))
+            comb = L.GcsBelief()
+            nu2, Psi2, Q2, mnu2, mPsi2, c4 = (np.zeros(7), np.zeros(252), np.zeros(484), np.zeros(3), np.zeros(27),
+                                              np.zeros(4))
+            X0 = np.zeros(6)
+            assert lib.gcs_payload_apply(tot.ctypes.data, s, X0.ctypes.data, 0.0, nu.ctypes.data, Psi.ctypes.data,
+                                         mnu.ctypes.data, mPsi.ctypes.data, C.byref(comb), nu2.ctypes.data,
+                                         Psi2.ctypes.data, Q2.ctypes.data, mnu2.ctypes.data, mPsi2.ctypes.data,
+                                         c4.ctypes.data) == 0
+            nu, Psi, mnu, mPsi = nu2, Psi2.reshape(7, 6, 6), mnu2, mPsi2.reshape(3, 3, 3)
+            X, _, z, Lm, h = L.struct_to_arrays(comb)
+            outs.append(dict(L=Lm, h=h, z=z, nu=nu.copy(), Psi=Psi.copy(), Q=Q2.reshape(22, 22), mnu=mnu.copy(),
+                             mPsi=mPsi.copy(), dPsi=dPsi, mdPsi=mdPsi))
+        q.put((rank, outs))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_library_combine_matches_oracle():
+    """The library's own payload pack / apply meet a second rank (gloo, CPU): both ranks end with
+    bitwise-identical combined belief, process and measurement IW states and Q, equal to the
+    oracle's 2-hypothesis node update (hypothesis.py:51-117; backend_node.py:2085-2119)."""
+    import torch.multiprocessing as mp
+    from oracle import ops, pipeline as opipe
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_lib_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    iw = ops.datasheet_process_noise_state()
+    meas = ops.datasheet_measurement_noise_state()
+    for s in range(3):
+        a, b = got[0][s], got[1][s]
+        for k in a:
+            assert np.array_equal(a[k], b[k]) or k in ("dPsi", "mdPsi"), k
+        bs = _beliefs(WORLD + s)
+        results = []
+        for r in range(WORLD):
+            dPsi, dnu = _iw_stats(10 * s + r)
+            results.append(dict(belief=bs[r + s], iw_process_dPsi=dPsi.reshape(7, 6, 6), iw_process_dnu=dnu,
+                                iw_meas_dPsi=got[r][s]["mdPsi"], iw_meas_dnu=np.array([1.0, 1.0, 0.0])))
+        ref = opipe.combine_and_update_noise(results, np.full(WORLD, 1.0 / WORLD), iw, s, meas)
+        iw, meas = ref["iw_state"], ref["meas_state"]
+        Lr = ref["combined"]["L"]
+        np.testing.assert_allclose(a["L"], Lr, rtol=1e-12, atol=1e-12 * np.abs(Lr).max())
+        np.testing.assert_allclose(a["h"], ref["combined"]["h"], rtol=1e-13, atol=1e-15)
+        np.testing.assert_allclose(a["nu"], iw[0], rtol=1e-14)
+        np.testing.assert_allclose(a["Psi"], iw[1], rtol=1e-9, atol=1e-20)
+        np.testing.assert_allclose(a["Q"], ref["Q"], rtol=1e-9, atol=1e-12 * np.abs(ref["Q"]).max())
+        np.testing.assert_allclose(a["mPsi"], meas[1], rtol=1e-9, atol=1e-20)
 
 
 def test_hypothesis_weights_floor():
