@@ -281,7 +281,9 @@ def main():
     scans = resident_scans(N, device)
 
     state = dict(count=0, sample=False)
-    host_ms = np.zeros(5)  # pre-device host, device submit+wait, host tail, whole gcs_scan, combine
+    # pre-device host, device submit+wait, host tail, whole gcs_scan, combine, then the sub-spans
+    # (budget launch + predict, device launch calls, tail numerics, pushforward launch calls)
+    host_ms = np.zeros(9)
 
     def step():
         if state["sample"]:  # roofline-kernel event stamps on every TIMING_STRIDE-th scan
@@ -296,6 +298,7 @@ def main():
         combine_allreduce(ctx, rank, world, state["count"], comm=comm, want_belief=False)
         host_ms[4] += (time.perf_counter() - tc) * 1e3
         host_ms[:4] += np.asarray(out.stage_ms[:4])
+        host_ms[5:9] += np.asarray(out.stage_ms[4:8])
         state["count"] += 1
 
     for _ in range(args.warmup):
@@ -325,7 +328,8 @@ def main():
     ms_sum, counts = ctx.stage_times(reset=True)
     bins_ms = float(ms_sum[2] / counts[2]) if counts[2] else None
     bins_samples = int(counts[2])
-    host_avg = dict(zip(["pre_device", "device_wait", "tail", "gcs_scan", "combine"], (host_ms / args.steps).tolist()))
+    host_avg = dict(zip(["pre_device", "device_wait", "tail", "gcs_scan", "combine", "pre_predict", "launch_calls",
+                         "tail_numerics", "push_launch"], (host_ms / args.steps).tolist()))
     # diagnostic pass after the timed region: every device stage stamped (not part of `value`)
     ctx.enable_timing(True)
     for _ in range(min(args.steps, 20)):

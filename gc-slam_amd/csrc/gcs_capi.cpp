@@ -80,6 +80,7 @@ struct gcs_ctx {
   hipStream_t push_stream = nullptr;
   hipEvent_t ev_push = nullptr;
   bool push_pending = false;
+  bool push_main = false;  // experiment knob (GCSLAM_PUSH_MAIN=1): k_pushforward on the main stream
   int pts_blocks = 0;
   bool pts_fold_pending = false;
   double* d_scalars = nullptr;
@@ -567,6 +568,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   c->own_stream = true;
   if (bad(hipStreamCreateWithFlags(&c->push_stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
   if (bad(hipEventCreateWithFlags(&c->ev_push, hipEventDisableTiming))) return GCS_ERR_HIP;
+  if (const char* pm = getenv("GCSLAM_PUSH_MAIN")) c->push_main = atoi(pm) != 0;
   const size_t B = c->B, cap = c->cap;
   if (bad(hipMalloc(&c->d_bin_dirs, B * 4 * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_recs, cap * sizeof(PointRec)))) return GCS_ERR_HIP;
@@ -1002,6 +1004,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   host::predict_diffusion(prev, Q, in->dt_sec, pred, pinfl, mu_prev);
   cert[6] = pinfl[0]; cert[7] = pinfl[1]; cert[8] = pinfl[2];
   Tsum += trig(pinfl[0], pinfl[1], 0, 0, 0, pinfl[2], 1, 1, 1);
+  auto Tp = clk::now();
   // 3 IMU membership window + preintegration -> deskew twist (pipeline.py:432-483)
   host::SpdFactor fpred;  // one factor of the predicted information for every solve below
   host::spd_factor_lifted(DZ, pred.L, kEpsLift, fpred);
@@ -1034,6 +1037,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
   if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
   if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+  auto Ts = clk::now();
   // 13 measurement-noise IW statistics over the scan-to-scan IMU window (pipeline.py:448-453,
   // 522-566), computed while the device stages run (they need no device result); padded samples
   // (stamp <= 0) carry weight 0 (the reference's valid mask)
@@ -1293,7 +1297,11 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   host::world_pose_from_increment(rec, mu_rec, z_t);
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j < 6; ++j) Sig6[6 * i + j] = covr[i * DZ + j];
-  if ((rc = stage_push(c, z_t, Sig6, c->cfg.forgetting_factor, c->push_stream, c->d_part_push))) return rc;
+  auto Tq = clk::now();
+  if ((rc = stage_push(c, z_t, Sig6, c->cfg.forgetting_factor, c->push_main ? c->stream : c->push_stream,
+                       c->d_part_push)))
+    return rc;
+  auto Tr = clk::now();
   memcpy(out->z_t, z_t, sizeof(out->z_t));
   // 14 AnchorDriftUpdate (anchor_drift.py:93-191)
   const double* dz2 = mu_rec;  // mean_increment(rec)
@@ -1325,6 +1333,10 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   out->stage_ms[1] = ms(T1, T2);
   out->stage_ms[2] = ms(T2, T3);
   out->stage_ms[3] = ms(T0, T3);
+  out->stage_ms[4] = ms(T0, Tp);  // of [0]: budget launch + PredictDiffusion
+  out->stage_ms[5] = ms(T1, Ts);  // of [1]: the device stages' launch calls
+  out->stage_ms[6] = ms(T2, Tq);  // of [2]: tail numerics up to the pushforward launch
+  out->stage_ms[7] = ms(Tq, Tr);  // of [2]: pushforward launch calls
   return GCS_OK;
 }
 

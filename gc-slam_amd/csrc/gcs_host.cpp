@@ -133,21 +133,60 @@ double psd_project(int n, const double* M, double eps_psd, double* out, double* 
   return delta;
 }
 
-bool cholesky(int n, const double* A, double* Lc) {
+// Cholesky / triangular solves / inverse, specialised on the size (22 for the belief, 6 and 3 for
+// the blocks) so the inner products unroll over contiguous rows; reciprocal diagonals replace the
+// divisions.  Row-major lower factor; Ct holds Lc^{-1} transposed (row c = column c of Lc^{-1}).
+template <int N>
+static bool cholesky_n(const double* A, double* Lc, double* rd) {
+  for (int i = 0; i < N * N; ++i) Lc[i] = 0.0;
+  for (int j = 0; j < N; ++j) {
+    const double* Lj = Lc + j * N;
+    double s = A[j * N + j];
+    for (int k = 0; k < j; ++k) s -= Lj[k] * Lj[k];
+    if (!(s > 0.0)) return false;
+    const double d = sqrt(s), r = 1.0 / d;
+    Lc[j * N + j] = d;
+    rd[j] = r;
+    for (int i = j + 1; i < N; ++i) {
+      const double* Li = Lc + i * N;
+      double t = A[i * N + j];
+      for (int k = 0; k < j; ++k) t -= Li[k] * Lj[k];
+      Lc[i * N + j] = t * r;
+    }
+  }
+  return true;
+}
+
+static bool cholesky_dyn(int n, const double* A, double* Lc, double* rd) {
   for (int i = 0; i < n * n; ++i) Lc[i] = 0.0;
   for (int j = 0; j < n; ++j) {
     double s = A[j * n + j];
     for (int k = 0; k < j; ++k) s -= Lc[j * n + k] * Lc[j * n + k];
     if (!(s > 0.0)) return false;
-    double d = sqrt(s);
+    const double d = sqrt(s), r = 1.0 / d;
     Lc[j * n + j] = d;
+    rd[j] = r;
     for (int i = j + 1; i < n; ++i) {
       double t = A[i * n + j];
       for (int k = 0; k < j; ++k) t -= Lc[i * n + k] * Lc[j * n + k];
-      Lc[i * n + j] = t / d;
+      Lc[i * n + j] = t * r;
     }
   }
   return true;
+}
+
+static bool cholesky_rd(int n, const double* A, double* Lc, double* rd) {
+  switch (n) {
+    case DZ: return cholesky_n<DZ>(A, Lc, rd);
+    case 6: return cholesky_n<6>(A, Lc, rd);
+    case 3: return cholesky_n<3>(A, Lc, rd);
+    default: return cholesky_dyn(n, A, Lc, rd);
+  }
+}
+
+bool cholesky(int n, const double* A, double* Lc) {
+  double rd[kMaxN];
+  return cholesky_rd(n, A, Lc, rd);
 }
 
 // spd_cholesky_solve_lifted_core / spd_cholesky_inverse_lifted_core, primitives.py:141-192
@@ -156,40 +195,97 @@ void spd_factor_lifted(int n, const double* L, double eps_lift, SpdFactor& f) {
   for (int i = 0; i < n * n; ++i) A[i] = L[i];
   for (int i = 0; i < n; ++i) A[i * n + i] += eps_lift;
   f.n = n;
-  cholesky(n, A, f.Lc);
+  if (!cholesky_rd(n, A, f.Lc, f.rd))  // not PD even lifted: NaN propagates to the callers' checks
+    for (int i = 0; i < n; ++i) f.rd[i] = NAN;
+}
+
+template <int N>
+static void factor_solve_n(const double* Lc, const double* rd, const double* b, double* x) {
+  double y[N];
+  for (int i = 0; i < N; ++i) {
+    const double* Li = Lc + i * N;
+    double s = b[i];
+    for (int k = 0; k < i; ++k) s -= Li[k] * y[k];
+    y[i] = s * rd[i];
+  }
+  // back substitution by columns of Lc (row-major rows of Lc^T): x_i = (y_i - sum_k>i Lc[k][i] x_k) / Lc[i][i]
+  for (int i = N - 1; i >= 0; --i) {
+    const double xi = y[i] * rd[i];
+    x[i] = xi;
+    const double* Li = Lc + i * N;
+    for (int k = 0; k < i; ++k) y[k] -= Li[k] * xi;
+  }
 }
 
 void spd_factor_solve(const SpdFactor& f, const double* b, double* x) {
   const int n = f.n;
+  if (n == DZ) return factor_solve_n<DZ>(f.Lc, f.rd, b, x);
+  if (n == 6) return factor_solve_n<6>(f.Lc, f.rd, b, x);
   const double* Lc = f.Lc;
   double y[kMaxN];
   for (int i = 0; i < n; ++i) {
     double s = b[i];
     for (int k = 0; k < i; ++k) s -= Lc[i * n + k] * y[k];
-    y[i] = s / Lc[i * n + i];
+    y[i] = s * f.rd[i];
   }
   for (int i = n - 1; i >= 0; --i) {
-    double s = y[i];
-    for (int k = i + 1; k < n; ++k) s -= Lc[k * n + i] * x[k];
-    x[i] = s / Lc[i * n + i];
+    const double xi = y[i] * f.rd[i];
+    x[i] = xi;
+    for (int k = 0; k < i; ++k) y[k] -= Lc[i * n + k] * xi;
   }
+}
+
+template <int N>
+static void factor_inverse_n(const double* Lc, const double* rd, double* Linv) {
+  // X = Lc^{-1} row by row (X_i = (e_i - sum_k<i Lc[i][k] X_k) / Lc[i][i]: row AXPYs), then
+  // Linv = X^T X as rank-1 updates over the rows of X; both inner loops are contiguous and independent
+  double X[N * N];
+  for (int i = 0; i < N; ++i) {
+    double* Xi = X + i * N;
+    for (int c = 0; c < N; ++c) Xi[c] = 0.0;
+    const double* Li = Lc + i * N;
+    for (int k = 0; k < i; ++k) {
+      const double l = Li[k];
+      const double* Xk = X + k * N;
+      for (int c = 0; c <= k; ++c) Xi[c] -= l * Xk[c];
+    }
+    Xi[i] = 1.0;
+    for (int c = 0; c <= i; ++c) Xi[c] *= rd[i];
+  }
+  for (int i = 0; i < N * N; ++i) Linv[i] = 0.0;
+  for (int k = 0; k < N; ++k) {
+    const double* Xk = X + k * N;
+    for (int i = 0; i <= k; ++i) {
+      const double xi = Xk[i];
+      double* Ri = Linv + i * N;
+      for (int j = 0; j <= i; ++j) Ri[j] += xi * Xk[j];
+    }
+  }
+  for (int i = 0; i < N; ++i)
+    for (int j = i + 1; j < N; ++j) Linv[i * N + j] = Linv[j * N + i];
 }
 
 void spd_factor_inverse(const SpdFactor& f, double* Linv) {
   const int n = f.n;
+  if (n == DZ) return factor_inverse_n<DZ>(f.Lc, f.rd, Linv);
+  if (n == 6) return factor_inverse_n<6>(f.Lc, f.rd, Linv);
+  if (n == 3) return factor_inverse_n<3>(f.Lc, f.rd, Linv);
   const double* Lc = f.Lc;
-  double Ci[kMaxN * kMaxN];  // Ci = Lc^{-1} (lower triangular)
-  for (int c = 0; c < n; ++c)
-    for (int i = 0; i < n; ++i) {
-      if (i < c) { Ci[i * n + c] = 0.0; continue; }
-      double s = (i == c) ? 1.0 : 0.0;
-      for (int k = c; k < i; ++k) s -= Lc[i * n + k] * Ci[k * n + c];
-      Ci[i * n + c] = s / Lc[i * n + i];
+  double Ct[kMaxN * kMaxN];
+  for (int c = 0; c < n; ++c) {
+    double* C = Ct + c * n;
+    for (int i = 0; i < c; ++i) C[i] = 0.0;
+    C[c] = f.rd[c];
+    for (int i = c + 1; i < n; ++i) {
+      double s = 0.0;
+      for (int k = c; k < i; ++k) s -= Lc[i * n + k] * C[k];
+      C[i] = s * f.rd[i];
     }
+  }
   for (int i = 0; i < n; ++i)
     for (int j = i; j < n; ++j) {
       double s = 0.0;
-      for (int k = j; k < n; ++k) s += Ci[k * n + i] * Ci[k * n + j];
+      for (int k = j; k < n; ++k) s += Ct[i * n + k] * Ct[j * n + k];
       Linv[i * n + j] = s;
       Linv[j * n + i] = s;
     }

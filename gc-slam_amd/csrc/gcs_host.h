@@ -26,6 +26,7 @@ constexpr int kMaxN = 24;
 struct SpdFactor {
   int n = 0;
   double Lc[kMaxN * kMaxN];
+  double rd[kMaxN];  // 1 / diag(Lc)
 };
 void spd_factor_lifted(int n, const double* L, double eps_lift, SpdFactor& f);
 void spd_factor_solve(const SpdFactor& f, const double* b, double* x);

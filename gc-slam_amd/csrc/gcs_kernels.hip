@@ -962,9 +962,29 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   __syncthreads();
   PROF(1);
   if (t < kBinTile) {  // wave 0, lane = bin: records each bin visits (0: inactive / out of range)
+    // The bin's reverse-kNN sources are compacted in place to the non-empty ones (same order):
+    // most sources of a bin are empty buckets, and phase C's cursor then never walks them (each
+    // visit was two dependent LDS reads).  Entries are read four at a time ahead of the writes
+    // (a write never passes a read: e <= q).
     uint32_t w = 0;
-    if (own_act)
-      for (int q = s_q[t]; q < s_q[t + 1]; ++q) w += s_cnt[s_rl[q - q0]];
+    int e = s_q[t] - q0;
+    if (own_act) {
+      const int qa = s_q[t] - q0, qb = s_q[t + 1] - q0;
+      for (int q = qa; q < qb; q += 4) {
+        uint16_t j[4];
+        uint32_t c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) j[u] = q + u < qb ? s_rl[q + u] : (uint16_t)0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = q + u < qb ? s_cnt[j[u]] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (c[u]) {
+            s_rl[e++] = j[u];
+            w += c[u];
+          }
+      }
+    }
     s_work[t] = w;
   }
   const int chunk = (ns + NT - 1) / NT;
@@ -1068,12 +1088,10 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         const uint32_t sw = rec_swz(r);
         const double2 c0 = rp[0 ^ sw], c1 = rp[1 ^ sw], c2 = rp[2 ^ sw], c3 = rp[3 ^ sw];
         bin_contrib(acc, bd, inv_tau, c0.x, c0.y, c1.x, c1.y, c2.x, c2.y, c3.x, c3.y);
-        if (--left == 0 && i + 1 < i1) {  // next non-empty source
-          do {
-            ++q;
-            j = s_rl[q - q0];
-            left = s_cnt[j];
-          } while (left == 0);
+        if (--left == 0 && i + 1 < i1) {  // next source (compacted: non-empty)
+          ++q;
+          j = s_rl[q - q0];
+          left = s_cnt[j];
           r = s_off[j];
         } else {
           ++r;
@@ -1090,12 +1108,10 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       for (uint32_t i = i0; i < i1; ++i) {
         const double2 c0 = x0, c1 = x1, c2 = x2, c3 = x3;
         if (i + 1 < i1) {
-          if (--left == 0) {  // next non-empty source
-            do {
-              ++q;
-              j = s_rl[q - q0];
-              left = s_cnt[j];
-            } while (left == 0);
+          if (--left == 0) {  // next source (compacted: non-empty)
+            ++q;
+            j = s_rl[q - q0];
+            left = s_cnt[j];
             r = s_off[j];
           } else {
             ++r;
@@ -1110,13 +1126,11 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       for (uint32_t i = i0; i < i1; ++i) {
         const PointRec pr = a.recs[a.perm[s_st[j] + kk]];
         bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, pr.dx, pr.dy, pr.dz, pr.m, pr.w * pr.iz);
-        if (++kk == c && i + 1 < i1) {  // next non-empty source
+        if (++kk == c && i + 1 < i1) {  // next source (compacted: non-empty)
           kk = 0;
-          do {
-            ++q;
-            j = s_rl[q - q0];
-            c = s_cnt[j];
-          } while (c == 0);
+          ++q;
+          j = s_rl[q - q0];
+          c = s_cnt[j];
         }
       }
     }

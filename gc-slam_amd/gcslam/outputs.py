@@ -239,3 +239,90 @@ class DiagnosticsLog:
             vals = [getattr(t, f.name) for t in self.tape]
             data[f.name] = np.stack(vals) if f.name == "L_pose6" else np.array(vals)
         np.savez_compressed(path, **data)
+
+
+# ---------------------------------------------------------------- trajectory error (evaluation side)
+def pose6_to_matrix(pose6):
+    """[t, rotvec] -> 4x4 homogeneous transform."""
+    p = np.asarray(pose6, float)
+    T = np.eye(4)
+    T[:3, :3] = _so3_exp(p[3:])
+    T[:3, 3] = p[:3]
+    return T
+
+
+def associate_stamps(t_ref, t_est, max_diff=0.01):
+    """Index pairs (i_ref, i_est) of stamps within max_diff, each est stamp used once, in ref order
+    (evo sync.associate_trajectories, as called by tools/evaluate_slam.py:254)."""
+    t_ref, t_est = np.asarray(t_ref, float), np.asarray(t_est, float)
+    pairs, used = [], set()
+    for i, t in enumerate(t_ref):
+        if t_est.size == 0:
+            break
+        j = int(np.argmin(np.abs(t_est - t)))
+        if abs(t_est[j] - t) <= max_diff and j not in used:
+            used.add(j)
+            pairs.append((i, j))
+    return pairs
+
+
+def align_initial(T_gt, T_est):
+    """tools/evaluate_slam.py:220-232: GT moved into the estimate frame so that the first associated
+    GT pose equals the first estimate (T_gt_i <- T_est0 T_gt0^-1 T_gt_i)."""
+    if len(T_gt) == 0 or len(T_est) == 0:
+        return [np.array(T) for T in T_gt]
+    A = np.asarray(T_est[0], float) @ np.linalg.inv(np.asarray(T_gt[0], float))
+    return [A @ np.asarray(T, float) for T in T_gt]
+
+
+def align_umeyama(T_gt, T_est):
+    """SE(3) Umeyama fit of the estimate positions to GT, scale fixed (evo PoseTrajectory3D.align
+    with correct_scale=False, tools/evaluate_slam.py:260); returns the aligned estimate poses."""
+    X = np.array([np.asarray(T, float)[:3, 3] for T in T_est])
+    Y = np.array([np.asarray(T, float)[:3, 3] for T in T_gt])
+    mx, my = X.mean(0), Y.mean(0)
+    S = (Y - my).T @ (X - mx) / len(X)
+    U, _, Vt = np.linalg.svd(S)
+    D = np.eye(3)
+    if np.linalg.det(U) * np.linalg.det(Vt) < 0:
+        D[2, 2] = -1.0
+    R = U @ D @ Vt
+    A = np.eye(4)
+    A[:3, :3] = R
+    A[:3, 3] = my - R @ mx
+    return [A @ np.asarray(T, float) for T in T_est]
+
+
+def _stats(e):
+    e = np.asarray(e, float)
+    return dict(rmse=float(np.sqrt(np.mean(e * e))), mean=float(e.mean()), median=float(np.median(e)),
+                std=float(e.std()), min=float(e.min()), max=float(e.max()), sse=float(np.sum(e * e)))
+
+
+def ate(stamps_gt, poses_gt, stamps_est, poses_est, align="initial", max_diff=0.01):
+    """Absolute trajectory error as tools/evaluate_slam.py:235-270 computes it with evo: associate
+    by stamp, align ("initial": GT into the estimate frame at the first pose; "umeyama": SE(3)
+    fit, no scale), then APE of E_i = P_gt_i^-1 P_est_i: translation |t(E_i)| (m) and rotation
+    angle |angle(R(E_i))| (deg).  Poses are [t, rotvec] rows or 4x4 matrices."""
+    def mats(P):
+        P = np.asarray(P, float)
+        return [T for T in P] if P.ndim == 3 else [pose6_to_matrix(p) for p in P]
+    Tg, Te = mats(poses_gt), mats(poses_est)
+    pairs = associate_stamps(stamps_gt, stamps_est, max_diff)
+    if not pairs:
+        raise ValueError("no associated poses")
+    Tg = [Tg[i] for i, _ in pairs]
+    Te = [Te[j] for _, j in pairs]
+    if align == "initial":
+        Tg = align_initial(Tg, Te)
+    elif align == "umeyama":
+        Te = align_umeyama(Tg, Te)
+    elif align != "none":
+        raise ValueError(f"align must be 'initial', 'umeyama' or 'none', got {align!r}")
+    et, er = [], []
+    for A, B in zip(Tg, Te):
+        E = np.linalg.inv(A) @ B
+        et.append(float(np.linalg.norm(E[:3, 3])))
+        c = min(1.0, max(-1.0, (np.trace(E[:3, :3]) - 1.0) * 0.5))
+        er.append(math.degrees(math.acos(c)))
+    return dict(align=align, n=len(pairs), trans=_stats(et), rot_deg=_stats(er))
