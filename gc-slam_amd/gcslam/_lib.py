@@ -87,6 +87,23 @@ DEBUG_SCAN_SPIN_LIMIT, DEBUG_INJECT_SCAN_FAIL = 1, 2
 
 
 # (name, restype, argtypes) for every symbol declared in include/gcslam_hip.h
+class GcsSurfelConfig(C.Structure):
+    _fields_ = [("n_surfel", C.c_int32), ("n_feat", C.c_int32), ("voxel_size_m", C.c_double),
+                ("num_cells_1", C.c_int32), ("num_cells_2", C.c_int32), ("num_cells_z", C.c_int32),
+                ("max_occupants", C.c_int32), ("min_points_per_voxel", C.c_int32),
+                ("sensor_noise_var_per_axis", C.c_double), ("wishart_nu", C.c_double),
+                ("wishart_psi_scale", C.c_double), ("kappa_main_scale", C.c_double), ("kappa_min", C.c_double),
+                ("kappa_max", C.c_double), ("eig_min", C.c_double), ("eps_lift", C.c_double),
+                ("max_points", C.c_int32), ("device", C.c_int32)]
+
+
+class GcsSurfelOutputs(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("positions", "covariances", "normals", "kappas", "weights", "timestamps",
+                                          "Lambdas", "thetas", "etas", "colors", "valid_mask", "source_indices",
+                                          "cell_ids", "bucket", "count")] + \
+               [("center", C.c_double * 3), ("n_valid", C.c_int32), ("cert", C.c_double * 2)]
+
+
 _SIGS = [
     ("gcs_version", C.c_char_p, []),
     ("gcs_abi_version", C.c_int, []),
@@ -158,6 +175,13 @@ _SIGS = [
     ("gcs_process_noise_Q", C.c_int, [c_double_p] * 3),
     ("gcs_meas_iw_mode", C.c_int, [c_double_p, c_double_p, C.c_int32, c_double_p]),
     ("gcs_ctx_describe", C.c_int, [C.c_void_p, C.c_char_p, C.c_int32]),
+    ("gcs_surfel_config_defaults", C.c_int, [C.POINTER(GcsSurfelConfig)]),
+    ("gcs_surfel_ctx_create", C.c_int, [C.POINTER(GcsSurfelConfig), C.POINTER(C.c_void_p)]),
+    ("gcs_surfel_ctx_destroy", C.c_int, [C.c_void_p]),
+    ("gcs_surfel_last_error", C.c_char_p, [C.c_void_p]),
+    ("gcs_surfel_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("gcs_extract_lidar_surfels", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
+                                            C.POINTER(GcsSurfelOutputs)]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]

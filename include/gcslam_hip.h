@@ -27,6 +27,9 @@
  *   gcs_hypothesis_payload /    FS/backend/backend_node.py:1999-2119 (IW accumulation) and
  *   gcs_hypothesis_combine      FS/backend/operators/hypothesis.py:51-117 (barycenter)
  *   gcs_fibonacci_atlas         archive/bin_atlas.py:40-61
+ *   gcs_extract_lidar_surfels   FS/backend/operators/lidar_surfel_extraction.py:339-431
+ *                               extract_lidar_surfels (+ FS/common/ma_hex_web.py:243-303
+ *                               bin_points_3d, FS/backend/structures/measurement_batch.py:272-381)
  */
 #ifndef GCSLAM_HIP_H
 #define GCSLAM_HIP_H
@@ -332,6 +335,67 @@ int gcs_rccl_comm_init(int32_t device, int32_t n_ranks, int32_t rank, const uint
 int gcs_rccl_comm_destroy(void* comm);
 int gcs_combine_allreduce(gcs_ctx* ctx, void* comm, double w_iw, double w_bary, int32_t scan_count,
                           gcs_belief* combined_out /*may be NULL*/, double* cert4 /*may be NULL*/);
+
+
+/* ---------------------------------------------------------------- primitive path: LiDAR surfels */
+/* extract_lidar_surfels (lidar_surfel_extraction.py:339-431) on the GPU: sentinel mask and weighted
+ * centre, MA-hex 3D hash-grid cell of every point (ma_hex_web.py:221-303), the first max_occupants
+ * points of each cell in index order (stable radix sort by cell), one weighted plane fit per cell
+ * (3x3 eigh, Wishart-regularised covariance, kappa; :84-163), the valid cells in cell-id order
+ * into n_surfel slots (:297-321) and the LiDAR slice of the MeasurementBatch in information form
+ * (measurement_batch.py:298-331).  A surfel context owns the workspace for up to max_points points
+ * on one GPU; calls on one context must be serialised. */
+typedef struct gcs_surfel_ctx gcs_surfel_ctx;
+
+typedef struct {
+  int32_t n_surfel;                   /* lidar_surfel_extraction.py:46 (GC_N_SURFEL = 1024) */
+  int32_t n_feat;                     /* :47 (GC_N_FEAT = 512): the LiDAR slice starts there */
+  double voxel_size_m;                /* :48 */
+  int32_t num_cells_1, num_cells_2, num_cells_z, max_occupants;  /* :50-53 (32, 32, 8, 32) */
+  int32_t min_points_per_voxel;       /* :54 */
+  double sensor_noise_var_per_axis;   /* :55 */
+  double wishart_nu, wishart_psi_scale;          /* :56-57 */
+  double kappa_main_scale, kappa_min, kappa_max; /* :58-60 */
+  double eig_min;                     /* :61 */
+  double eps_lift;                    /* :62 (GC_EPS_LIFT) */
+  int32_t max_points;                 /* capacity of the context (points per call) */
+  int32_t device;
+} gcs_surfel_config;
+
+/* Outputs: device pointers, each may be NULL (not written).  Row counts: n_surfel unless noted.
+ * Slots past n_valid hold the reference's padding (positions / normals / kappas / weights /
+ * timestamps 0, covariances I; batch rows 0, cell_ids -1). */
+typedef struct {
+  double* positions;     /* n_surfel x 3   surfel centroids (lidar_surfel_extraction.py:307) */
+  double* covariances;   /* n_surfel x 9   Wishart-regularised Sigma */
+  double* normals;       /* n_surfel x 3 */
+  double* kappas;        /* n_surfel */
+  double* weights;       /* n_surfel       sum of member weights */
+  double* timestamps;    /* n_surfel */
+  double* Lambdas;       /* n_surfel x 9   MeasurementBatch LiDAR slice: inv(Sigma + eps_lift I) */
+  double* thetas;        /* n_surfel x 3   Lambda mu */
+  double* etas;          /* n_surfel x 3 lobes x 3: lobe 0 = kappa n, others 0 */
+  double* colors;        /* n_surfel x 3   grey from normal z (measurement_batch.py:262-269) */
+  uint8_t* valid_mask;   /* n_surfel */
+  int32_t* source_indices; /* n_surfel */
+  int32_t* cell_ids;     /* n_surfel       MA-hex cell of each slot (-1 past n_valid) */
+  int32_t* bucket;       /* n_cells x max_occupants point indices (-1 padding) */
+  int32_t* count;        /* n_cells        occupancy clipped to max_occupants */
+  /* host results */
+  double center[3];      /* the weighted centre the cells are hashed around (:264-267) */
+  int32_t n_valid;       /* surfels in the LiDAR slice */
+  double cert[2];        /* SupportCert: ess_total = n_valid, support_frac = n_valid / n_surfel */
+} gcs_surfel_outputs;
+
+int gcs_surfel_config_defaults(gcs_surfel_config* cfg);
+int gcs_surfel_ctx_create(const gcs_surfel_config* cfg, gcs_surfel_ctx** out);
+int gcs_surfel_ctx_destroy(gcs_surfel_ctx* ctx);
+const char* gcs_surfel_last_error(const gcs_surfel_ctx* ctx);
+/* stream: a hipStream_t (NULL = the context's own); work on it is ordered after the caller's */
+int gcs_surfel_ctx_set_stream(gcs_surfel_ctx* ctx, void* stream);
+/* points: n x 3 f64, timestamps / weights: n f64 (device); n <= max_points.  Synchronises. */
+int gcs_extract_lidar_surfels(gcs_surfel_ctx* ctx, const double* points_dev, const double* timestamps_dev,
+                              const double* weights_dev, int32_t n, gcs_surfel_outputs* out);
 
 #ifdef __cplusplus
 }
