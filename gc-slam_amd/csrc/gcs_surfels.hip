@@ -3,17 +3,21 @@
 // 339-431, with the MA-hex 3D bucketing of FS/common/ma_hex_web.py:221-303 and the LiDAR slice of
 // FS/backend/structures/measurement_batch.py:272-381.
 //
-//   k_sf_partials   weighted centre partial sums (sentinel mask, :259-266), fixed-order block trees
-//   k_sf_keys       every block folds the partials in the same order (the centre), then per point
-//                   the hash-grid cell of the centred point (masked points -> key n_cells)
+//   k_sf_partials   weighted centre partial sums (sentinel mask, :259-266), fixed-order block trees;
+//                   also clears the per-cell run bounds
+//   k_sf_keys       every block folds the partials in the same fixed tree (the centre), then per
+//                   point the hash-grid cell of the centred point (masked points -> key n_cells)
 //   radix sort      stable (rocPRIM LSD radix sort on the cell key, point index as value): the
 //                   reference's stable argsort by (masked, cell) (ma_hex_web.py:276-280)
-//   k_sf_cells      per cell: run bounds by binary search, the first max_occupants indices, the
-//                   clipped count (:284-303)
-//   k_sf_fit        per cell: weighted plane fit, eigh, Wishart-regularised covariance, kappa
-//                   (lidar_surfel_extraction.py:84-163)
-//   k_sf_select     one workgroup: valid cells in cell-id order into n_surfel slots (:297-321),
-//                   the information form of the LiDAR slice (measurement_batch.py:298-331)
+//   k_sf_bounds     per sorted point: the first / last position of each cell's run
+//   k_sf_cells      per cell: the first max_occupants indices, the clipped count (:284-303)
+//   k_sf_moments    one wave per occupied cell: weight, centroid, time and scatter sums over the
+//                   occupants in fixed xor trees (lidar_surfel_extraction.py:113-126)
+//   k_sf_fit        one lane per cell: eigh, normal, in-plane variances, Wishart-regularised
+//                   covariance, kappa, validity (:126-163)
+//   k_sf_slots      one workgroup: valid cells in cell-id order -> slots (:297-305)
+//   k_sf_write      one lane per slot: the surfel rows and the information form of the LiDAR
+//                   slice (:307-321, measurement_batch.py:298-331), padding past n_valid
 // Everything is fixed-order (no floating-point atomics): results are bitwise reproducible.
 #include <hip/hip_runtime.h>
 
@@ -51,8 +55,10 @@ __device__ __forceinline__ bool sf_mask(double x, double y, double z) {
 // per block: sum over its grid-stride points of (x w_eff, y w_eff, z w_eff, w_eff), w_eff = w * mask
 __global__ __launch_bounds__(kSfThreads) void k_sf_partials(const double* __restrict__ p,
                                                              const double* __restrict__ w, int n,
-                                                             double* __restrict__ partials) {
+                                                             double* __restrict__ partials, int32_t* __restrict__ run,
+                                                             int n_run) {
   __shared__ double lds[kSfThreads / 64][4];
+  for (int j = blockIdx.x * kSfThreads + threadIdx.x; j < n_run; j += gridDim.x * kSfThreads) run[j] = 0;
   double v[4] = {0.0, 0.0, 0.0, 0.0};
   for (int i = blockIdx.x * kSfThreads + threadIdx.x; i < n; i += gridDim.x * kSfThreads) {
     const double x = p[3 * (size_t)i], y = p[3 * (size_t)i + 1], z = p[3 * (size_t)i + 2];
@@ -85,19 +91,40 @@ __global__ __launch_bounds__(kSfThreads) void k_sf_partials(const double* __rest
 __global__ __launch_bounds__(kSfThreads) void k_sf_keys(const double* __restrict__ p, int n,
                                                          const double* __restrict__ partials, int nblk,
                                                          SfParams a, uint32_t* __restrict__ keys,
-                                                         uint32_t* __restrict__ vals, double* __restrict__ center_out) {
+                                                         uint32_t* __restrict__ vals, double* __restrict__ center_out,
+                                                         double* __restrict__ center_host) {
 #pragma clang fp contract(off)
   __shared__ double s_c[3];
-  if (threadIdx.x == 0) {
-    double s[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int b = 0; b < nblk; ++b)
-      for (int k = 0; k < 4; ++k) s[k] += partials[4 * b + k];
-    const double ws = s[3] + a.eig_min;
-    for (int k = 0; k < 3; ++k) s_c[k] = s[k] / ws;
-    if (blockIdx.x == 0)
-      for (int k = 0; k < 3; ++k) center_out[k] = s_c[k];
+  __shared__ double lds[kSfThreads / 64][4];
+  {  // the partial rows in one fixed tree (row t on thread t, nblk <= kSfThreads), same in every block
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    if ((int)threadIdx.x < nblk)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = partials[4 * threadIdx.x + k];
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] += __shfl_xor(v[k], off, 64);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) lds[threadIdx.x >> 6][k] = v[k];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sm[4];
+      for (int k = 0; k < 4; ++k) {
+        sm[k] = lds[0][k];
+        for (int q = 1; q < kSfThreads / 64; ++q) sm[k] += lds[q][k];
+      }
+      const double ws = sm[3] + a.eig_min;
+      for (int k = 0; k < 3; ++k) s_c[k] = sm[k] / ws;
+      if (blockIdx.x == 0)
+        for (int k = 0; k < 3; ++k) {
+          center_out[k] = s_c[k];
+          center_host[k] = s_c[k];
+        }
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const double cx = s_c[0], cy = s_c[1], cz = s_c[2];
   for (int i = blockIdx.x * kSfThreads + threadIdx.x; i < n; i += gridDim.x * kSfThreads) {
     const double x = p[3 * (size_t)i], y = p[3 * (size_t)i + 1], z = p[3 * (size_t)i + 2];
@@ -116,23 +143,24 @@ __global__ __launch_bounds__(kSfThreads) void k_sf_keys(const double* __restrict
   }
 }
 
-__device__ __forceinline__ int lower_bound_u32(const uint32_t* __restrict__ a, int n, uint32_t v) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (a[mid] < v) lo = mid + 1; else hi = mid;
-  }
-  return lo;
+// run bounds of every cell in the sorted keys: start and end (one past), 0/0 = empty
+__global__ __launch_bounds__(kSfThreads) void k_sf_bounds(const uint32_t* __restrict__ keys_s, int n, int n_cells,
+                                                           int32_t* __restrict__ run) {
+  const int q = blockIdx.x * kSfThreads + threadIdx.x;
+  if (q >= n) return;
+  const uint32_t k = keys_s[q];
+  if (k >= (uint32_t)n_cells) return;  // masked points sort last
+  if (q == 0 || keys_s[q - 1] != k) run[2 * k] = q;
+  if (q == n - 1 || keys_s[q + 1] != k) run[2 * k + 1] = q + 1;
 }
 
-// per cell: its run in the sorted keys, the first max_occ point indices, the clipped count
-__global__ __launch_bounds__(kSfThreads) void k_sf_cells(const uint32_t* __restrict__ keys_s,
-                                                          const uint32_t* __restrict__ vals_s, int n, SfParams a,
+// per cell: the first max_occ point indices of its run (stable: index order), the clipped count
+__global__ __launch_bounds__(kSfThreads) void k_sf_cells(const int32_t* __restrict__ run,
+                                                          const uint32_t* __restrict__ vals_s, SfParams a,
                                                           int32_t* __restrict__ bucket, int32_t* __restrict__ count) {
   const int k = blockIdx.x * kSfThreads + threadIdx.x;
   if (k >= a.n_cells) return;
-  const int s = lower_bound_u32(keys_s, n, (uint32_t)k);
-  const int e = lower_bound_u32(keys_s, n, (uint32_t)k + 1u);
+  const int s = run[2 * k], e = run[2 * k + 1];
   const int c = min(e - s, a.max_occ);
   count[k] = c;
   int32_t* row = bucket + (size_t)k * a.max_occ;
@@ -150,50 +178,90 @@ __device__ __forceinline__ void sym_plus_diag(double* M, double d) {
   M[0] += d; M[4] += d; M[8] += d;
 }
 
-// _fit_one_cell (lidar_surfel_extraction.py:84-163) on the cell's present slots (absent slots carry
-// zero weight in the reference and add exact zeros); fit row = centroid (+ centre) | Sigma_reg |
-// normal | kappa | w_surfel | t_surfel
-__global__ __launch_bounds__(kSfThreads) void k_sf_fit(const double* __restrict__ p, const double* __restrict__ t,
-                                                        const double* __restrict__ w, const double* __restrict__ center,
-                                                        const int32_t* __restrict__ bucket,
+template <int NV>
+__device__ __forceinline__ void sf_wave_sum(double (&v)[NV]) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += __shfl_xor(v[k], off, 64);
+}
+
+// Occupant sums of one cell per wave (lidar_surfel_extraction.py:113-126; absent slots carry zero
+// weight in the reference and add exact zeros): lane r holds occupant r, the sums meet in fixed
+// xor trees.  Moment row = sum w, centroid (3), sum t, sum w d d^T (xx xy xz yy yz zz).
+constexpr int kMomFields = 11;
+constexpr int kCellsPerBlock = kSfThreads / 64;
+__global__ __launch_bounds__(kSfThreads) void k_sf_moments(const double* __restrict__ p, const double* __restrict__ t,
+                                                            const double* __restrict__ w,
+                                                            const double* __restrict__ center,
+                                                            const int32_t* __restrict__ bucket,
+                                                            const int32_t* __restrict__ count, SfParams a,
+                                                            double* __restrict__ mom) {
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * kCellsPerBlock + (threadIdx.x >> 6);
+  if (k >= a.n_cells) return;  // wave-uniform
+  const int c = count[k];
+  if (c == 0) return;          // k_sf_fit does not read the row of an empty cell
+  const int32_t* row = bucket + (size_t)k * a.max_occ;
+  const double cx = center[0], cy = center[1], cz = center[2];
+  double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // w, w x, w y, w z, t
+  double px[2] = {0.0, 0.0}, py[2] = {0.0, 0.0}, pz[2] = {0.0, 0.0}, pw[2] = {0.0, 0.0};
+  for (int r = lane, u = 0; r < c; r += 64, ++u) {
+    const int i = row[r];
+    const double x = p[3 * (size_t)i], y = p[3 * (size_t)i + 1], z = p[3 * (size_t)i + 2];
+    const double we = w[i];  // occupants are unmasked points: w_eff = w * 1
+    s5[0] += we;
+    s5[1] += (x - cx) * we;
+    s5[2] += (y - cy) * we;
+    s5[3] += (z - cz) * we;
+    s5[4] += t[i];
+    if (u < 2) { px[u] = x - cx; py[u] = y - cy; pz[u] = z - cz; pw[u] = we; }
+  }
+  sf_wave_sum<5>(s5);
+  const double wsum = s5[0] + kFitEps;
+  const double m[3] = {s5[1] / wsum, s5[2] / wsum, s5[3] / wsum};
+  double c6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int r = lane, u = 0; r < c; r += 64, ++u) {
+    double x, y, z, we;
+    if (u < 2) { x = px[u]; y = py[u]; z = pz[u]; we = pw[u]; }
+    else {
+      const int i = row[r];
+      x = p[3 * (size_t)i] - cx; y = p[3 * (size_t)i + 1] - cy; z = p[3 * (size_t)i + 2] - cz;
+      we = w[i];
+    }
+    const double d0 = x - m[0], d1 = y - m[1], d2 = z - m[2];
+    c6[0] += d0 * we * d0; c6[1] += d0 * we * d1; c6[2] += d0 * we * d2;
+    c6[3] += d1 * we * d1; c6[4] += d1 * we * d2; c6[5] += d2 * we * d2;
+  }
+  sf_wave_sum<6>(c6);
+  double f = 0.0;
+  if (lane == 0) f = s5[0];
+  else if (lane < 4) f = m[lane - 1];
+  else if (lane == 4) f = s5[4];
+  else if (lane < 11) f = c6[lane - 5];
+  if (lane < kMomFields) mom[(size_t)k * kMomFields + lane] = f;
+}
+
+// The rest of _fit_one_cell (:126-163), one lane per cell.  The in-plane variances are the
+// quadratic forms e^T (sum w d d^T) e / w_sum (the reference sums w (d.e)^2 point by point: equal
+// up to rounding).  Fit row = centroid (+ centre) | Sigma_reg | normal | kappa | w_surfel | t_surfel.
+__global__ __launch_bounds__(kSfThreads) void k_sf_fit(const double* __restrict__ mom,
+                                                        const double* __restrict__ center,
                                                         const int32_t* __restrict__ count, SfParams a,
                                                         double* __restrict__ fit, uint8_t* __restrict__ valid) {
   const int k = blockIdx.x * kSfThreads + threadIdx.x;
   if (k >= a.n_cells) return;
   const int c = count[k];
-  double* out = fit + (size_t)k * kFitFields;
-  if (c == 0) {  // never valid (w_surfel = 0): the row is not read
+  if (c == 0) {  // never valid (w_surfel = 0): the fit row is not read
     valid[k] = 0;
     return;
   }
-  const int32_t* row = bucket + (size_t)k * a.max_occ;
-  const double cx = center[0], cy = center[1], cz = center[2];
-  double ws = 0.0, sx = 0.0, sy = 0.0, sz = 0.0, st = 0.0;
-  for (int r = 0; r < c; ++r) {
-    const int i = row[r];
-    const double x = p[3 * (size_t)i], y = p[3 * (size_t)i + 1], z = p[3 * (size_t)i + 2];
-    const double we = w[i] * (sf_mask(x, y, z) ? 1.0 : 0.0);
-    ws += we;
-    sx += (x - cx) * we;
-    sy += (y - cy) * we;
-    sz += (z - cz) * we;
-    st += t[i];
-  }
-  const double wsum = ws + kFitEps;
-  const double m[3] = {sx / wsum, sy / wsum, sz / wsum};
-  double C[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = 0; r < c; ++r) {
-    const int i = row[r];
-    const double x = p[3 * (size_t)i], y = p[3 * (size_t)i + 1], z = p[3 * (size_t)i + 2];
-    const double we = w[i] * (sf_mask(x, y, z) ? 1.0 : 0.0);
-    const double d[3] = {(x - cx) - m[0], (y - cy) - m[1], (z - cz) - m[2]};
-#pragma unroll
-    for (int u = 0; u < 3; ++u)
-#pragma unroll
-      for (int v = 0; v < 3; ++v) C[3 * u + v] += d[u] * we * d[v];
-  }
-#pragma unroll
-  for (int q = 0; q < 9; ++q) C[q] /= wsum;
+  const double* mo = mom + (size_t)k * kMomFields;
+  const double ws = mo[0], wsum = ws + kFitEps;
+  const double m[3] = {mo[1], mo[2], mo[3]};
+  const double* c6 = mo + 5;
+  double C[9] = {c6[0] / wsum, c6[1] / wsum, c6[2] / wsum, c6[1] / wsum, c6[3] / wsum,
+                 c6[4] / wsum, c6[2] / wsum, c6[4] / wsum, c6[5] / wsum};
   sym_plus_diag(C, a.eig_min);
   double ev[3], V[9];
   eigh3_jacobi(C, ev, V);
@@ -213,18 +281,14 @@ __global__ __launch_bounds__(kSfThreads) void k_sf_fit(const double* __restrict_
   double e2[3];
   cross3(n2, e1, e2);
   normalize3(e2);
-  double v1 = 0.0, v2 = 0.0;
-  for (int r = 0; r < c; ++r) {
-    const int i = row[r];
-    const double x = p[3 * (size_t)i], y = p[3 * (size_t)i + 1], z = p[3 * (size_t)i + 2];
-    const double we = w[i] * (sf_mask(x, y, z) ? 1.0 : 0.0);
-    const double d[3] = {(x - cx) - m[0], (y - cy) - m[1], (z - cz) - m[2]};
-    const double q1 = d[0] * e1[0] + d[1] * e1[1] + d[2] * e1[2];
-    const double q2 = d[0] * e2[0] + d[1] * e2[1] + d[2] * e2[2];
-    v1 += we * (q1 * q1);
-    v2 += we * (q2 * q2);
-  }
-  const double var_e1 = v1 / wsum + a.sensor_var, var_e2 = v2 / wsum + a.sensor_var;
+  const double S6[9] = {c6[0], c6[1], c6[2], c6[1], c6[3], c6[4], c6[2], c6[4], c6[5]};
+  auto quad = [&](const double* e) {
+    double q = 0.0;
+#pragma unroll
+    for (int u = 0; u < 3; ++u) q += e[u] * (S6[3 * u] * e[0] + S6[3 * u + 1] * e[1] + S6[3 * u + 2] * e[2]);
+    return q;
+  };
+  const double var_e1 = quad(e1) / wsum + a.sensor_var, var_e2 = quad(e2) / wsum + a.sensor_var;
   const double sps = fmax(ev[im], a.eig_min);
   const double var_perp = sps + a.sensor_var;
   const double D[3] = {fmax(var_e1, a.eig_min), fmax(var_e2, a.eig_min), fmax(var_perp, a.eig_min)};
@@ -251,15 +315,16 @@ __global__ __launch_bounds__(kSfThreads) void k_sf_fit(const double* __restrict_
   sym_plus_diag(Sr, a.eig_min);
   double kap = a.kappa_scale / sqrt(fmax(sps, a.eig_min));
   kap = fmin(fmax(kap, a.kappa_min), a.kappa_max);
-  out[0] = m[0] + cx;
-  out[1] = m[1] + cy;
-  out[2] = m[2] + cz;
+  double* out = fit + (size_t)k * kFitFields;
+  out[0] = m[0] + center[0];
+  out[1] = m[1] + center[1];
+  out[2] = m[2] + center[2];
 #pragma unroll
   for (int q = 0; q < 9; ++q) out[3 + q] = Sr[q];
   out[12] = nrm[0]; out[13] = nrm[1]; out[14] = nrm[2];
   out[15] = kap;
   out[16] = ws;
-  out[17] = st / wsum;
+  out[17] = mo[4] / wsum;
   valid[k] = (c >= a.min_points && ws > 0.0) ? 1 : 0;
 }
 
@@ -268,14 +333,13 @@ struct SelOut {
   double *Lambdas, *thetas, *etas, *colors;
   uint8_t* valid_mask;
   int32_t *source_indices, *cell_ids;
-  int32_t* n_valid;  // device scalar
 };
 
-// one workgroup: valid cells (cell-id order) -> slots, then the padded tail
-__global__ __launch_bounds__(kSelThreads) void k_sf_select(const double* __restrict__ fit,
-                                                            const uint8_t* __restrict__ valid, SfParams a, SelOut o) {
+// one workgroup: valid cells in cell-id order -> slot_cell[slot], n_valid (device + mapped host)
+__global__ __launch_bounds__(kSelThreads) void k_sf_slots(const uint8_t* __restrict__ valid, SfParams a,
+                                                           int32_t* __restrict__ slot_cell, int32_t* __restrict__ nv_dev,
+                                                           int32_t* __restrict__ nv_host) {
   __shared__ int s_wsum[kSelThreads / 64];
-  __shared__ int s_total;
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int per = (a.n_cells + kSelThreads - 1) / kSelThreads;
   const int k0 = min(a.n_cells, t * per), k1 = min(a.n_cells, k0 + per);
@@ -290,45 +354,25 @@ __global__ __launch_bounds__(kSelThreads) void k_sf_select(const double* __restr
   __syncthreads();
   int run = x - mine;
   for (int q = 0; q < wid; ++q) run += s_wsum[q];
-  if (t == kSelThreads - 1) s_total = run + mine;
-  for (int k = k0; k < k1; ++k) {
-    if (!valid[k]) continue;
-    const int s = run++;
-    if (s >= a.n_surfel) break;
-    const double* f = fit + (size_t)k * kFitFields;
-    const double* pos = f;
-    const double* S = f + 3;
-    const double* nrm = f + 12;
-    const double kap = f[15];
-    if (o.positions) for (int q = 0; q < 3; ++q) o.positions[3 * s + q] = pos[q];
-    if (o.covariances) for (int q = 0; q < 9; ++q) o.covariances[9 * s + q] = S[q];
-    if (o.normals) for (int q = 0; q < 3; ++q) o.normals[3 * s + q] = nrm[q];
-    if (o.kappas) o.kappas[s] = kap;
-    if (o.weights) o.weights[s] = f[16];
-    if (o.timestamps) o.timestamps[s] = f[17];
-    if (o.cell_ids) o.cell_ids[s] = k;
-    // measurement_batch_add_lidar_surfels (measurement_batch.py:298-312)
-    double A[9], L[9];
-    for (int q = 0; q < 9; ++q) A[q] = S[q];
-    A[0] += a.eps_lift; A[4] += a.eps_lift; A[8] += a.eps_lift;
-    inv3(A, L);
-    if (o.Lambdas) for (int q = 0; q < 9; ++q) o.Lambdas[9 * s + q] = L[q];
-    if (o.thetas)
-      for (int q = 0; q < 3; ++q) o.thetas[3 * s + q] = L[3 * q] * pos[0] + L[3 * q + 1] * pos[1] + L[3 * q + 2] * pos[2];
-    if (o.etas)
-      for (int q = 0; q < 9; ++q) o.etas[9 * s + q] = q < 3 ? kap * nrm[q] : 0.0;
-    if (o.colors) {
-      const double nz = fmin(fmax(nrm[2], -1.0), 1.0);
-      const double g = 0.25 + 0.5 * (nz + 1.0) / 2.0;
-      for (int q = 0; q < 3; ++q) o.colors[3 * s + q] = g;
-    }
-    if (o.valid_mask) o.valid_mask[s] = 1;
-    if (o.source_indices) o.source_indices[s] = s;
+  for (int k = k0; k < k1 && run < a.n_surfel; ++k)
+    if (valid[k]) slot_cell[run++] = k;
+  if (t == kSelThreads - 1) {
+    int tot = 0;
+    for (int q = 0; q < kSelThreads / 64; ++q) tot += s_wsum[q];
+    const int nv = min(tot, a.n_surfel);
+    *nv_dev = nv;
+    *nv_host = nv;
   }
-  __syncthreads();
-  const int nv = min(s_total, a.n_surfel);
-  if (t == 0) *o.n_valid = nv;
-  for (int s = nv + t; s < a.n_surfel; s += kSelThreads) {  // the reference's padding
+}
+
+// one lane per slot: the surfel row of its cell and the LiDAR slice in information form, or the
+// reference's padding past n_valid
+__global__ __launch_bounds__(kSfThreads) void k_sf_write(const double* __restrict__ fit,
+                                                          const int32_t* __restrict__ slot_cell,
+                                                          const int32_t* __restrict__ nv_dev, SfParams a, SelOut o) {
+  const int s = blockIdx.x * kSfThreads + threadIdx.x;
+  if (s >= a.n_surfel) return;
+  if (s >= *nv_dev) {
     if (o.positions) for (int q = 0; q < 3; ++q) o.positions[3 * s + q] = 0.0;
     if (o.covariances) for (int q = 0; q < 9; ++q) o.covariances[9 * s + q] = (q % 4 == 0) ? 1.0 : 0.0;
     if (o.normals) for (int q = 0; q < 3; ++q) o.normals[3 * s + q] = 0.0;
@@ -342,7 +386,41 @@ __global__ __launch_bounds__(kSelThreads) void k_sf_select(const double* __restr
     if (o.colors) for (int q = 0; q < 3; ++q) o.colors[3 * s + q] = 0.0;
     if (o.valid_mask) o.valid_mask[s] = 0;
     if (o.source_indices) o.source_indices[s] = 0;
+    return;
   }
+  const int k = slot_cell[s];
+  const double* f = fit + (size_t)k * kFitFields;
+  double pos[3], S[9], nrm[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) { pos[q] = f[q]; nrm[q] = f[12 + q]; }
+#pragma unroll
+  for (int q = 0; q < 9; ++q) S[q] = f[3 + q];
+  const double kap = f[15];
+  if (o.positions) for (int q = 0; q < 3; ++q) o.positions[3 * s + q] = pos[q];
+  if (o.covariances) for (int q = 0; q < 9; ++q) o.covariances[9 * s + q] = S[q];
+  if (o.normals) for (int q = 0; q < 3; ++q) o.normals[3 * s + q] = nrm[q];
+  if (o.kappas) o.kappas[s] = kap;
+  if (o.weights) o.weights[s] = f[16];
+  if (o.timestamps) o.timestamps[s] = f[17];
+  if (o.cell_ids) o.cell_ids[s] = k;
+  // measurement_batch_add_lidar_surfels (measurement_batch.py:298-312)
+  double A[9], L[9];
+#pragma unroll
+  for (int q = 0; q < 9; ++q) A[q] = S[q];
+  A[0] += a.eps_lift; A[4] += a.eps_lift; A[8] += a.eps_lift;
+  inv3(A, L);
+  if (o.Lambdas) for (int q = 0; q < 9; ++q) o.Lambdas[9 * s + q] = L[q];
+  if (o.thetas)
+    for (int q = 0; q < 3; ++q) o.thetas[3 * s + q] = L[3 * q] * pos[0] + L[3 * q + 1] * pos[1] + L[3 * q + 2] * pos[2];
+  if (o.etas)
+    for (int q = 0; q < 9; ++q) o.etas[9 * s + q] = q < 3 ? kap * nrm[q] : 0.0;
+  if (o.colors) {
+    const double nz = fmin(fmax(nrm[2], -1.0), 1.0);
+    const double g = 0.25 + 0.5 * (nz + 1.0) / 2.0;
+    for (int q = 0; q < 3; ++q) o.colors[3 * s + q] = g;
+  }
+  if (o.valid_mask) o.valid_mask[s] = 1;
+  if (o.source_indices) o.source_indices[s] = s;
 }
 
 }  // namespace
@@ -361,11 +439,12 @@ struct gcs_surfel_ctx {
   void* d_temp = nullptr;
   size_t temp_bytes = 0;
   unsigned end_bit = 1;
-  int32_t *d_bucket = nullptr, *d_count = nullptr;
-  double* d_fit = nullptr;
+  int32_t *d_bucket = nullptr, *d_count = nullptr, *d_run = nullptr, *d_slot_cell = nullptr;
+  double *d_mom = nullptr, *d_fit = nullptr;
   uint8_t* d_valid = nullptr;
-  double* d_scal = nullptr;   // center[3], n_valid (as int32 in the 4th slot)
-  double* h_scal = nullptr;   // pinned
+  double* d_scal = nullptr;   // device: center[3], n_valid (int32 in the 4th slot)
+  double* h_scal = nullptr;   // pinned, mapped: the same, written by the kernels (no copy)
+  double* h_scal_dev = nullptr;
 };
 
 namespace {
@@ -413,7 +492,7 @@ int gcs_surfel_ctx_destroy(gcs_surfel_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_partials, c->d_keys, c->d_vals, c->d_keys_s, c->d_vals_s, c->d_temp,
-                  c->d_bucket, c->d_count, c->d_fit, c->d_valid, c->d_scal};
+                  c->d_bucket, c->d_count, c->d_run, c->d_slot_cell, c->d_mom, c->d_fit, c->d_valid, c->d_scal};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_scal) (void)hipHostFree(c->h_scal);
@@ -458,7 +537,10 @@ int gcs_surfel_ctx_create(const gcs_surfel_config* cfg, gcs_surfel_ctx** out) {
       bad(hipMalloc(&c->d_bucket, (size_t)n_cells * a.max_occ * 4)) || bad(hipMalloc(&c->d_count, n_cells * 4)) ||
       bad(hipMalloc(&c->d_fit, (size_t)n_cells * kFitFields * sizeof(double))) ||
       bad(hipMalloc(&c->d_valid, n_cells)) || bad(hipMalloc(&c->d_scal, 4 * sizeof(double))) ||
-      bad(hipHostMalloc(&c->h_scal, 4 * sizeof(double), hipHostMallocDefault))) {
+      bad(hipMalloc(&c->d_run, (size_t)n_cells * 2 * 4)) || bad(hipMalloc(&c->d_slot_cell, (size_t)cfg->n_surfel * 4)) ||
+      bad(hipMalloc(&c->d_mom, (size_t)n_cells * kMomFields * sizeof(double))) ||
+      bad(hipHostMalloc(&c->h_scal, 4 * sizeof(double), hipHostMallocMapped)) ||
+      bad(hipHostGetDevicePointer((void**)&c->h_scal_dev, c->h_scal, 0))) {
     gcs_surfel_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
@@ -492,29 +574,35 @@ int gcs_extract_lidar_surfels(gcs_surfel_ctx* c, const double* points, const dou
   const SfParams& a = c->prm;
   hipStream_t s = c->stream;
   const int nblk = std::max(1, std::min(kSfMaxPartials, (n + kSfThreads - 1) / kSfThreads));
-  hipLaunchKernelGGL(k_sf_partials, dim3(nblk), dim3(kSfThreads), 0, s, points, weights, n, c->d_partials);
+  hipLaunchKernelGGL(k_sf_partials, dim3(nblk), dim3(kSfThreads), 0, s, points, weights, n, c->d_partials, c->d_run,
+                     2 * a.n_cells);
   hipLaunchKernelGGL(k_sf_keys, dim3(nblk), dim3(kSfThreads), 0, s, points, n, (const double*)c->d_partials, nblk, a,
-                     c->d_keys, c->d_vals, c->d_scal);
+                     c->d_keys, c->d_vals, c->d_scal, c->h_scal_dev);
   if (n > 0) {
     size_t tb = c->temp_bytes;
     SFCHK(c, rocprim::radix_sort_pairs(c->d_temp, tb, c->d_keys, c->d_keys_s, c->d_vals, c->d_vals_s, (unsigned)n, 0u,
                                        c->end_bit, s));
+    hipLaunchKernelGGL(k_sf_bounds, dim3((n + kSfThreads - 1) / kSfThreads), dim3(kSfThreads), 0, s,
+                       (const uint32_t*)c->d_keys_s, n, a.n_cells, c->d_run);
   }
   const int cblk = (a.n_cells + kSfThreads - 1) / kSfThreads;
-  hipLaunchKernelGGL(k_sf_cells, dim3(cblk), dim3(kSfThreads), 0, s, (const uint32_t*)c->d_keys_s,
-                     (const uint32_t*)c->d_vals_s, n, a, c->d_bucket, c->d_count);
-  hipLaunchKernelGGL(k_sf_fit, dim3(cblk), dim3(kSfThreads), 0, s, points, timestamps, weights,
-                     (const double*)c->d_scal, (const int32_t*)c->d_bucket, (const int32_t*)c->d_count, a, c->d_fit,
-                     c->d_valid);
+  hipLaunchKernelGGL(k_sf_cells, dim3(cblk), dim3(kSfThreads), 0, s, (const int32_t*)c->d_run,
+                     (const uint32_t*)c->d_vals_s, a, c->d_bucket, c->d_count);
+  hipLaunchKernelGGL(k_sf_moments, dim3((a.n_cells + kCellsPerBlock - 1) / kCellsPerBlock), dim3(kSfThreads), 0, s,
+                     points, timestamps, weights, (const double*)c->d_scal, (const int32_t*)c->d_bucket,
+                     (const int32_t*)c->d_count, a, c->d_mom);
+  hipLaunchKernelGGL(k_sf_fit, dim3(cblk), dim3(kSfThreads), 0, s, (const double*)c->d_mom, (const double*)c->d_scal,
+                     (const int32_t*)c->d_count, a, c->d_fit, c->d_valid);
+  hipLaunchKernelGGL(k_sf_slots, dim3(1), dim3(kSelThreads), 0, s, (const uint8_t*)c->d_valid, a, c->d_slot_cell,
+                     (int32_t*)(c->d_scal + 3), (int32_t*)(c->h_scal_dev + 3));
   SelOut so{o->positions, o->covariances, o->normals, o->kappas, o->weights, o->timestamps, o->Lambdas, o->thetas,
-            o->etas, o->colors, o->valid_mask, o->source_indices, o->cell_ids, (int32_t*)(c->d_scal + 3)};
-  hipLaunchKernelGGL(k_sf_select, dim3(1), dim3(kSelThreads), 0, s, (const double*)c->d_fit,
-                     (const uint8_t*)c->d_valid, a, so);
+            o->etas, o->colors, o->valid_mask, o->source_indices, o->cell_ids};
+  hipLaunchKernelGGL(k_sf_write, dim3((a.n_surfel + kSfThreads - 1) / kSfThreads), dim3(kSfThreads), 0, s,
+                     (const double*)c->d_fit, (const int32_t*)c->d_slot_cell, (const int32_t*)(c->d_scal + 3), a, so);
   SFCHK(c, hipGetLastError());
   if (o->bucket)
     SFCHK(c, hipMemcpyAsync(o->bucket, c->d_bucket, (size_t)a.n_cells * a.max_occ * 4, hipMemcpyDeviceToDevice, s));
   if (o->count) SFCHK(c, hipMemcpyAsync(o->count, c->d_count, (size_t)a.n_cells * 4, hipMemcpyDeviceToDevice, s));
-  SFCHK(c, hipMemcpyAsync(c->h_scal, c->d_scal, 4 * sizeof(double), hipMemcpyDeviceToHost, s));
   SFCHK(c, hipStreamSynchronize(s));
   for (int k = 0; k < 3; ++k) o->center[k] = c->h_scal[k];
   int32_t nv;

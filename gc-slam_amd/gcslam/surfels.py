@@ -120,6 +120,7 @@ class SurfelExtractor:
         self.h = h
         self.device = int(device)
         self.max_points = int(max_points)
+        self._bufs = {}
 
     def close(self):
         if getattr(self, "h", None):
@@ -138,7 +139,8 @@ class SurfelExtractor:
             raise (ValueError if rc in (-1, -3) else RuntimeError)(f"{what} failed ({rc}): {msg}")
 
     def extract(self, points, timestamps, weights, want_intermediates=False):
-        """Surfel arrays (device tensors) + n_valid + centre; points (N,3) / timestamps / weights f64."""
+        """Surfel arrays (device tensors) + n_valid + centre; points (N,3) / timestamps / weights f64.
+        The output tensors belong to the extractor and are overwritten by its next call."""
         torch = _torch()
         dev = f"cuda:{self.device}"
         cf = self.config
@@ -148,18 +150,23 @@ class SurfelExtractor:
         n = int(p.shape[0])
         if t.shape[0] != n or w.shape[0] != n:
             raise ValueError("points, timestamps and weights must have the same length")
-        ns = cf.n_surfel
-        f = lambda *sh, dt=torch.float64: torch.empty(sh, dtype=dt, device=dev)  # noqa: E731
-        out = dict(positions=f(ns, 3), covariances=f(ns, 3, 3), normals=f(ns, 3), kappas=f(ns), weights=f(ns),
-                   timestamps=f(ns), Lambdas=f(ns, 3, 3), thetas=f(ns, 3), etas=f(ns, GC_VMF_N_LOBES, 3),
-                   colors=f(ns, 3), valid_mask=f(ns, dt=torch.uint8), source_indices=f(ns, dt=torch.int32),
-                   cell_ids=f(ns, dt=torch.int32))
-        if want_intermediates:
-            out["bucket"] = f(cf.n_cells, cf.hex3d_max_occupants, dt=torch.int32)
-            out["count"] = f(cf.n_cells, dt=torch.int32)
-        o = L.GcsSurfelOutputs()
-        for k, v in out.items():
-            setattr(o, k, v.data_ptr())
+        key = bool(want_intermediates)
+        if key not in self._bufs:  # allocated once per extractor (and per intermediates flag)
+            ns = cf.n_surfel
+            f = lambda *sh, dt=torch.float64: torch.empty(sh, dtype=dt, device=dev)  # noqa: E731
+            out = dict(positions=f(ns, 3), covariances=f(ns, 3, 3), normals=f(ns, 3), kappas=f(ns), weights=f(ns),
+                       timestamps=f(ns), Lambdas=f(ns, 3, 3), thetas=f(ns, 3), etas=f(ns, GC_VMF_N_LOBES, 3),
+                       colors=f(ns, 3), valid_mask=f(ns, dt=torch.uint8), source_indices=f(ns, dt=torch.int32),
+                       cell_ids=f(ns, dt=torch.int32))
+            if want_intermediates:
+                out["bucket"] = f(cf.n_cells, cf.hex3d_max_occupants, dt=torch.int32)
+                out["count"] = f(cf.n_cells, dt=torch.int32)
+            o = L.GcsSurfelOutputs()
+            for k, v in out.items():
+                setattr(o, k, v.data_ptr())
+            self._bufs[key] = (out, o)
+        out, o = self._bufs[key]
+        out = dict(out)
         self._chk(self.lib.gcs_surfel_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
                   "gcs_surfel_ctx_set_stream")
         self._chk(self.lib.gcs_extract_lidar_surfels(self.h, C.c_void_p(p.data_ptr()), C.c_void_p(t.data_ptr()),
