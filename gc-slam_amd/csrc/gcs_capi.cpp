@@ -9,7 +9,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -81,6 +85,24 @@ struct gcs_ctx {
   hipEvent_t ev_push = nullptr;
   bool push_pending = false;
   bool push_main = false;  // experiment knob (GCSLAM_PUSH_MAIN=1): k_pushforward on the main stream
+  // Asynchronous pushforward launch (GCSLAM_PUSH_THREAD=0 turns it off): the launch calls of
+  // k_pushforward and its fold (~10 us of host time per scan, on the scan's critical path) are made
+  // by a per-context worker thread; every later use of the map, the flags or the push event first
+  // waits for the worker (push_wait), so the device order is the synchronous one.
+  bool push_async = true;
+  std::thread push_thread;
+  std::atomic<uint64_t> push_req{0}, push_done{0};
+  std::atomic<bool> push_stop{false}, push_sleeping{false};
+  std::mutex push_mu;
+  std::condition_variable push_cv;
+  struct PushJob {
+    double z_t[6], Sig6[36], gamma;
+    hipStream_t s;
+    double* partials;
+    uint8_t* flags;
+  } push_job{};
+  int push_rc = 0;
+  std::string push_err;
   int pts_blocks = 0;
   bool pts_fold_pending = false;
   double* d_scalars = nullptr;
@@ -124,11 +146,26 @@ int fail(gcs_ctx* c, int code, const std::string& m) {
   return code;
 }
 
+// wait until the push worker has made the launch calls of the last submitted pushforward
+int push_wait(gcs_ctx* c) {
+  if (!c->push_thread.joinable()) return GCS_OK;
+  const uint64_t r = c->push_req.load(std::memory_order_acquire);
+  while (c->push_done.load(std::memory_order_acquire) != r) __builtin_ia32_pause();
+  if (c->push_rc) {
+    const int rc = c->push_rc;
+    c->push_rc = 0;
+    return fail(c, rc, c->push_err);
+  }
+  return GCS_OK;
+}
+
 // order the main stream after an in-flight scan pushforward (map, derived, touched, map totals)
-void join_push(gcs_ctx* c) {
-  if (!c->push_pending) return;
+int join_push(gcs_ctx* c) {
+  if (int rc = push_wait(c)) return rc;
+  if (!c->push_pending) return GCS_OK;
   (void)hipStreamWaitEvent(c->stream, c->ev_push, 0);
   c->push_pending = false;
+  return GCS_OK;
 }
 
 #define HIPCHK(ctx, expr)                                                                         \
@@ -426,7 +463,10 @@ int stage_pt(gcs_ctx* c, bool to_host = false) {
   return GCS_OK;
 }
 
-int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, hipStream_t s, double* partials) {
+// on_worker: called by the push worker; errors are returned, not written to the context's message
+int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, hipStream_t s, double* partials,
+               uint8_t* flags, bool on_worker = false) {
+  gcs_ctx* ec = on_worker ? nullptr : c;
   PushArgs pa{};
   so3_exp(z_t + 3, pa.R);
   pa.t[0] = z_t[0];
@@ -445,11 +485,71 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, 
     for (int j = 0; j < 3; ++j) pa.G[3 * i + j] = RS[3 * i] * pa.R[3 * j] + RS[3 * i + 1] * pa.R[3 * j + 1] + RS[3 * i + 2] * pa.R[3 * j + 2];
   pa.gamma = gamma;
   StageEv ev = stage_ev(c, ST_PUSH);
-  HIPCHK(c, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, partials, c->d_scalars, c->d_flags,
+  HIPCHK(ec, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, partials, c->d_scalars, flags,
                                c->d_touched, s, ev.e0, ev.e1));
   if (s != c->stream) {
-    HIPCHK(c, hipEventRecord(c->ev_push, s));
+    HIPCHK(ec, hipEventRecord(c->ev_push, s));
     c->push_pending = true;
+  }
+  return GCS_OK;
+}
+
+// The push worker: waits (spin, then sleep) for a submitted job and makes its launch calls with the
+// job's captured arguments (the flags buffer of that scan; the context's device buffers are fixed).
+void push_worker(gcs_ctx* c) {
+  (void)hipSetDevice(c->cfg.device);
+  uint64_t seen = 0;
+  for (;;) {
+    // spin for up to 2 ms after the last job (a scan every 0.1-0.3 ms keeps the worker awake: a
+    // futex wake-up costs tens of microseconds, which at C3 delayed the pushforward behind the
+    // next scan's bin kernel), then sleep until the next submission
+    int spins = 0;
+    auto t_idle = std::chrono::steady_clock::now();
+    while (c->push_req.load() == seen && !c->push_stop.load()) {
+      __builtin_ia32_pause();
+      if ((++spins & 255) != 0 || std::chrono::steady_clock::now() - t_idle < std::chrono::milliseconds(2))
+        continue;
+      std::unique_lock<std::mutex> lk(c->push_mu);
+      c->push_sleeping.store(true);
+      c->push_cv.wait(lk, [&] { return c->push_req.load() != seen || c->push_stop.load(); });
+      c->push_sleeping.store(false);
+      t_idle = std::chrono::steady_clock::now();
+    }
+    const uint64_t r = c->push_req.load(std::memory_order_acquire);
+    if (r == seen) return;  // stop requested, nothing pending
+    seen = r;
+    const gcs_ctx::PushJob& j = c->push_job;
+    int rc = GCS_OK;
+    {
+      rc = stage_push(c, j.z_t, j.Sig6, j.gamma, j.s, j.partials, j.flags, true);
+      if (rc) c->push_err = "pushforward launch (worker): " + std::string(hipGetErrorString(hipGetLastError()));
+    }
+    c->push_rc = rc;
+    c->push_done.store(r, std::memory_order_release);
+  }
+}
+
+// launch the scan's pushforward: on the worker (default) or inline (timing the push stage, or
+// GCSLAM_PUSH_THREAD=0)
+int submit_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, hipStream_t s, double* partials) {
+  const bool timed = (c->timing_mask >> ST_PUSH) & 1u;
+  if (!c->push_async || timed) {
+    if (int rc = push_wait(c)) return rc;
+    return stage_push(c, z_t, Sig6, gamma, s, partials, c->d_flags);
+  }
+  if (int rc = push_wait(c)) return rc;  // the previous job is launched: its slot is free
+  if (!c->push_thread.joinable()) c->push_thread = std::thread(push_worker, c);
+  gcs_ctx::PushJob& j = c->push_job;
+  memcpy(j.z_t, z_t, sizeof(j.z_t));
+  memcpy(j.Sig6, Sig6, sizeof(j.Sig6));
+  j.gamma = gamma;
+  j.s = s;
+  j.partials = partials;
+  j.flags = c->d_flags;
+  c->push_req.fetch_add(1);
+  if (c->push_sleeping.load()) {
+    std::lock_guard<std::mutex> lk(c->push_mu);
+    c->push_cv.notify_one();
   }
   return GCS_OK;
 }
@@ -569,6 +669,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipStreamCreateWithFlags(&c->push_stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
   if (bad(hipEventCreateWithFlags(&c->ev_push, hipEventDisableTiming))) return GCS_ERR_HIP;
   if (const char* pm = getenv("GCSLAM_PUSH_MAIN")) c->push_main = atoi(pm) != 0;
+  if (const char* pt = getenv("GCSLAM_PUSH_THREAD")) c->push_async = atoi(pt) != 0;
   const size_t B = c->B, cap = c->cap;
   if (bad(hipMalloc(&c->d_bin_dirs, B * 4 * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_recs, cap * sizeof(PointRec)))) return GCS_ERR_HIP;
@@ -646,6 +747,15 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
 
 int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
+  if (c->push_thread.joinable()) {
+    (void)push_wait(c);
+    {
+      std::lock_guard<std::mutex> lk(c->push_mu);
+      c->push_stop.store(true);
+    }
+    c->push_cv.notify_one();
+    c->push_thread.join();
+  }
   if (c->push_stream) (void)hipStreamSynchronize(c->push_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
@@ -671,6 +781,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
 
 int gcs_ctx_set_stream(gcs_ctx* c, void* s) {
   if (!c) return GCS_ERR_ARG;
+  if (int rc = push_wait(c)) return rc;
   HIPCHK(c, hipStreamSynchronize(c->push_stream));
   c->push_pending = false;
   if (c->stream) HIPCHK(c, hipStreamSynchronize(c->stream));  // work queued on the old stream completes first
@@ -682,7 +793,7 @@ int gcs_ctx_set_stream(gcs_ctx* c, void* s) {
 
 int gcs_ctx_synchronize(gcs_ctx* c) {
   if (!c) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
 }
@@ -724,7 +835,7 @@ int gcs_ctx_stage_times(gcs_ctx* c, double* ms_sum, int64_t* counts, int32_t res
 
 int gcs_ctx_set_atlas(gcs_ctx* c, const double* dirs) {
   if (!c || !dirs) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   c->dirs_host.assign(dirs, dirs + (size_t)c->B * 3);
   return upload_atlas(c);
@@ -751,7 +862,7 @@ int gcs_ctx_get_belief(gcs_ctx* c, gcs_belief* b) {
 
 int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
   if (!c || !map) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   std::vector<double> dev((size_t)c->B * MF_COUNT);
   to_device_order(c, MF_COUNT, map, dev.data());
@@ -763,7 +874,7 @@ int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
 }
 
 int pull_rows(gcs_ctx* c, const double* dev_src, int F, double* ref_out) {
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   std::vector<double> dev((size_t)c->B * F);
   HIPCHK(c, hipMemcpyAsync(dev.data(), dev_src, dev.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -793,7 +904,7 @@ int gcs_ctx_get_bin_order(gcs_ctx* c, int32_t* order) {
 
 int gcs_ctx_device_arrays(gcs_ctx* c, double** scan, double** map, double** derived) {
   if (!c) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the arrays are final when the pointers are handed out
   if (scan) *scan = c->d_scan;
   if (map) *map = c->d_map;
@@ -852,7 +963,7 @@ int gcs_parse_pointcloud2(gcs_ctx* c, const void* data_dev, const gcs_pointcloud
     return fail(c, GCS_ERR_ARG, "PointCloud2 (VLP-16 layout) ring field missing or outside point_step");
   if (L->off_t >= 0 && (L->t_datatype < 1 || L->t_datatype > 8 || !fits(L->off_t, width(L->t_datatype))))
     return fail(c, GCS_ERR_ARG, "PointCloud2 time field outside point_step");
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   ParseArgs a{};
   a.data = (const uint8_t*)data_dev;
   a.n = L->n_points;
@@ -873,7 +984,7 @@ int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const doubl
                     double t0, double t1, const double* xi, double* p0_dev, double* w_out_dev, double* w_budget_dev,
                     int32_t* nearest_dev, double* cert) {
   if (!c || !xi) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   c->budget_pending = false;  // a k_budget queued by a gcs_scan that failed later is stale
   int rc = stage_points(c, xyz, point_step, t, w, n, t0, t1, xi, p0_dev, w_out_dev, w_budget_dev);
   if (rc) return rc;
@@ -917,7 +1028,7 @@ __global__ void k_materialize(const PointRec* recs, const int* nearest, const in
 
 int gcs_bin_soft_assign(gcs_ctx* c, int32_t* ids, double* r) {
   if (!c) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   bool scale = c->cfg.mode == GCS_MODE_SCALE;
   hipLaunchKernelGGL(k_materialize, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, (const PointRec*)c->d_recs,
                      (const int*)c->d_nearest, (const int*)c->d_knn, (const double*)c->d_bin_dirs,
@@ -930,7 +1041,7 @@ int gcs_bin_soft_assign(gcs_ctx* c, int32_t* ids, double* r) {
 
 int gcs_scan_bin_moment_match(gcs_ctx* c, double* cert) {
   if (!c) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   int rc = stage_bins(c);
   if (rc) return rc;
   if ((rc = pull_scalars(c))) return rc;
@@ -942,7 +1053,7 @@ int gcs_scan_bin_moment_match(gcs_ctx* c, double* cert) {
 
 int gcs_matrix_fisher_rotation(gcs_ctx* c, double* mf) {
   if (!c) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   int rc = stage_mf(c);
   if (rc) return rc;
   if ((rc = pull_scalars(c))) return rc;
@@ -964,7 +1075,7 @@ int gcs_matrix_fisher_rotation(gcs_ctx* c, double* mf) {
 
 int gcs_planar_translation(gcs_ctx* c, const double* R_hat, double* pt) {
   if (!c || !R_hat) return GCS_ERR_ARG;
-  join_push(c);
+  if (int rc_ = join_push(c)) return rc_;
   HIPCHK(c, hipMemcpyAsync(c->d_scalars + SC_MF_R, R_hat, 9 * sizeof(double), hipMemcpyHostToDevice, c->stream));
   int rc = stage_pt(c);
   if (rc) return rc;
@@ -979,8 +1090,8 @@ int gcs_planar_translation(gcs_ctx* c, const double* R_hat, double* pt) {
 
 int gcs_pushforward(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma) {
   if (!c || !z_t || !Sig6) return GCS_ERR_ARG;
-  join_push(c);
-  int rc = stage_push(c, z_t, Sig6, gamma, c->stream, c->d_partials);
+  if (int rc_ = join_push(c)) return rc_;
+  int rc = stage_push(c, z_t, Sig6, gamma, c->stream, c->d_partials, c->d_flags);
   if (rc) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return GCS_OK;
@@ -1033,7 +1144,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
                         in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, /*fold_later=*/true,
                         in->xyz_format == 1);
   if (rc) return rc;
-  join_push(c);  // the bin kernel reads the map the previous scan's pushforward wrote
+  if (int rc_ = join_push(c)) return rc_;  // the bin kernel reads the map the previous scan's pushforward wrote
   if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
   if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
   if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
@@ -1298,8 +1409,8 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j < 6; ++j) Sig6[6 * i + j] = covr[i * DZ + j];
   auto Tq = clk::now();
-  if ((rc = stage_push(c, z_t, Sig6, c->cfg.forgetting_factor, c->push_main ? c->stream : c->push_stream,
-                       c->d_part_push)))
+  if ((rc = submit_push(c, z_t, Sig6, c->cfg.forgetting_factor, c->push_main ? c->stream : c->push_stream,
+                        c->d_part_push)))
     return rc;
   auto Tr = clk::now();
   memcpy(out->z_t, z_t, sizeof(out->z_t));

@@ -46,7 +46,9 @@ GCS_HD double dot3_exact(double ax, double ay, double az, double bx, double by, 
 }
 
 GCS_HD double sigmoid(double x) {
-  // numerically symmetric logistic
+  // numerically symmetric logistic; above 40, exp(-x) < 2^-57 and 1 / (1 + exp(-x)) rounds to
+  // exactly 1.0, which is returned without the exp (bitwise the same value)
+  if (x > 40.0) return 1.0;
   if (x >= 0.0) {
     double e = exp(-x);
     return 1.0 / (1.0 + e);

@@ -6,7 +6,7 @@ Correction (MI355X_MICROARCH.md, section HBM): FETCH_SIZE and WRITE_SIZE are rep
 on gfx950 FETCH_SIZE counts one half of the bytes of a 16-B-per-lane coalesced streaming read, so
 the read bytes are FETCH_SIZE x 2.  WRITE_SIZE is exact for 16-B-per-lane streaming stores.
 
-Usage: python tools/pmc_summary.py gpurun_out/pmc [c2 c3]
+Usage: python tools/pmc_summary.py gpurun_out/pmc [c2 c3]   (PMC_ROUND=r02 labels the round)
 """
 
 import csv
@@ -48,7 +48,8 @@ def main():
                           "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes": rd + wr,
                           "launches": [nf.get(k, 0), nw.get(k, 0)]}
         bins = next((v for k, v in kernels.items() if "k_bins_scale" in k), None)
-        out = {"config": cfg, "hbm_bytes_per_launch": bins["hbm_bytes"] if bins else None,
+        out = {"config": cfg, "round": os.environ.get("PMC_ROUND", "r02"),
+               "hbm_bytes_per_launch": bins["hbm_bytes"] if bins else None,
                "correction": "read = FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count of 16-B/lane reads); "
                              "write = WRITE_SIZE KiB x 1024",
                "kernels": kernels}
