@@ -47,7 +47,9 @@ def main():
             kernels[k] = {"fetch_size_kib": fetch.get(k), "write_size_kib": write.get(k),
                           "read_bytes_corrected": rd, "write_bytes": wr, "hbm_bytes": rd + wr,
                           "launches": [nf.get(k, 0), nw.get(k, 0)]}
-        bins = next((v for k, v in kernels.items() if "k_bins_scale" in k), None)
+        # the roofline kernel's instance for this config (C2 stages 512 records per tile, C3 256)
+        want = {"c2": "k_bins_scale<512", "c3": "k_bins_scale<256"}.get(cfg, "k_bins_scale")
+        bins = next((v for k, v in kernels.items() if want in k.replace(" ", "")), None)
         out = {"config": cfg, "round": os.environ.get("PMC_ROUND", "r02"),
                "hbm_bytes_per_launch": bins["hbm_bytes"] if bins else None,
                "correction": "read = FETCH_SIZE KiB x 1024 x 2 (gfx950 half-count of 16-B/lane reads); "

@@ -9,7 +9,7 @@ RE='k_bins_scale|k_points|k_pt|k_pushforward'
 run() {  # config, name, counters...
   local cfg=$1 name=$2; shift 2
   timeout -s KILL 120 rocprofv3 --pmc "$@" --kernel-include-regex "$RE" -d "$OUT/${cfg}_$name" -o run \
-    --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline \
+    --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline --no-c3 \
     > "$OUT/${cfg}_$name.log" 2>&1
 }
 for cfg in ${PMC_CONFIGS:-c2 c3}; do
