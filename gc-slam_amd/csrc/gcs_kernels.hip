@@ -850,6 +850,9 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
     }
 }
 
+#ifndef GCS_RANK_LANES
+#define GCS_RANK_LANES 4  // phase A's per-bin work sum + source compaction: 4 lanes per bin (1: wave 0 alone)
+#endif
 #ifndef GCS_GATHER_PIPE
 #define GCS_GATHER_PIPE 1  // phase C loads the next staged record while accumulating the current one
 #endif
@@ -869,6 +872,13 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   static_assert(LANES == 4 || LANES == 8, "phase C splits each bin over 4 or 8 lanes");
   __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
   __shared__ uint16_t s_rl[kMaxRl];
+#if GCS_RANK_LANES == 4
+  __shared__ uint16_t s_rlc[kMaxRl];  // each bin's non-empty sources, compacted (phase C's list)
+  __shared__ uint8_t s_act[kBinTile];
+  uint16_t* const rlist = s_rlc;
+#else
+  uint16_t* const rlist = s_rl;
+#endif
   __shared__ double s_rec[STAGE * kRecD];
   __shared__ double4 s_bd[kBinTile];
   __shared__ int s_q[kBinTile + 1];
@@ -929,6 +939,9 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   // phase A
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
   if (t <= nb) s_q[t] = q_t;
+#if GCS_RANK_LANES == 4
+  if (t < kBinTile) s_act[t] = own_act ? 1 : 0;
+#endif
   {
     // fixed trip counts: every thread issues all of its table loads before the first LDS write,
     // so the reverse-kNN entries (up to kMaxRl / NT per thread) cost one round trip, not one each,
@@ -961,6 +974,53 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   }
   __syncthreads();
   PROF(1);
+#if GCS_RANK_LANES == 4
+  {
+    // Records each bin visits (0: inactive / out of range), on the bin's four phase-C lanes: lane l
+    // takes the l-th quarter of the bin's reverse-kNN entries; the non-empty sources are written,
+    // in order, to the compacted list s_rlc (offsets by a prefix over the four lanes), so phase C's
+    // cursor never walks an empty bucket (each visit was two dependent LDS reads).
+    const int rb = t >> 2, rq = t & 3;
+    int qa = 0, lo = 0, hi = 0;
+    if (s_act[rb]) {
+      qa = s_q[rb] - q0;
+      const int n = s_q[rb + 1] - q0 - qa;
+      lo = qa + n * rq / 4;
+      hi = qa + n * (rq + 1) / 4;
+    }
+    uint32_t w = 0;
+    int nz = 0;
+    for (int q = lo; q < hi; q += 4) {
+      uint16_t j[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) j[u] = q + u < hi ? s_rl[q + u] : (uint16_t)0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t c = q + u < hi ? s_cnt[j[u]] : 0u;
+        w += c;
+        nz += c ? 1 : 0;
+      }
+    }
+    int x = nz;
+#pragma unroll
+    for (int off = 1; off < 4; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (rq >= off) x += y;
+    }
+    int e = qa + (x - nz);
+    for (int q = lo; q < hi; q += 4) {
+      uint16_t j[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) j[u] = q + u < hi ? s_rl[q + u] : (uint16_t)0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (q + u < hi && s_cnt[j[u]]) s_rlc[e++] = j[u];
+    }
+    w += (uint32_t)__shfl_xor((int)w, 1, 64);
+    w += (uint32_t)__shfl_xor((int)w, 2, 64);
+    if (rq == 0) s_work[rb] = w;
+  }
+#else
   if (t < kBinTile) {  // wave 0, lane = bin: records each bin visits (0: inactive / out of range)
     // The bin's reverse-kNN sources are compacted in place to the non-empty ones (same order):
     // most sources of a bin are empty buckets, and phase C's cursor then never walks them (each
@@ -987,6 +1047,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     }
     s_work[t] = w;
   }
+#endif
   const int chunk = (ns + NT - 1) / NT;
   const int j0 = min(ns, t * chunk), j1 = min(ns, j0 + chunk);
   uint32_t mine = 0;
@@ -1072,12 +1133,12 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     // cursor: source q (local j), record k within it
     int q = s_q[lb];
     uint32_t skip = i0;
-    int j = s_rl[q - q0];
+    int j = rlist[q - q0];
     uint32_t c = s_cnt[j];
     while (skip >= c) {
       skip -= c;
       ++q;
-      j = s_rl[q - q0];
+      j = rlist[q - q0];
       c = s_cnt[j];
     }
     uint32_t kk = skip;
@@ -1090,7 +1151,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         bin_contrib(acc, bd, inv_tau, c0.x, c0.y, c1.x, c1.y, c2.x, c2.y, c3.x, c3.y);
         if (--left == 0 && i + 1 < i1) {  // next source (compacted: non-empty)
           ++q;
-          j = s_rl[q - q0];
+          j = rlist[q - q0];
           left = s_cnt[j];
           r = s_off[j];
         } else {
@@ -1110,7 +1171,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         if (i + 1 < i1) {
           if (--left == 0) {  // next source (compacted: non-empty)
             ++q;
-            j = s_rl[q - q0];
+            j = rlist[q - q0];
             left = s_cnt[j];
             r = s_off[j];
           } else {
@@ -1129,7 +1190,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         if (++kk == c && i + 1 < i1) {  // next source (compacted: non-empty)
           kk = 0;
           ++q;
-          j = s_rl[q - q0];
+          j = rlist[q - q0];
           c = s_cnt[j];
         }
       }
