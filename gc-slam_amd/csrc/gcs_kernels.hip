@@ -787,11 +787,14 @@ constexpr int kBinNV = 16;
 //     balance bought back)
 //  D: wave 0, one lane per bin: PSD, kappa, the bin's Matrix-Fisher term, coalesced 64-bin output
 //     rows, the tile's partial row by a wave reduction.
-// STAGE: kStageBig when the scan is dense in the map (cap >= 0.4 B, C2: 42 KiB of LDS, three
-// workgroups per CU), kStageSmall otherwise (C3: 26 KiB; four per CU, register-limited).
+// STAGE: kStageBig when the scan is dense in the map (cap >= 0.4 B, C2: 41 KiB of LDS, three
+// workgroups per CU), kStageSmall otherwise (C3: 25 KiB; four per CU, register-limited).
 constexpr int kMaxSrc = 320;   // atlas tables for B = 1k .. 1M have at most 199 per 64-bin tile
 constexpr int kMaxRl = 1280;   // reverse-kNN entries of one tile (~K x kBinTile; at most 1070)
-constexpr int kStageBig = 512, kStageSmall = 256;
+#ifndef GCS_STAGE_BIG
+#define GCS_STAGE_BIG 512  // 480 (four workgroups per CU in LDS instead of three) measured slower at C2: 27.2 -> 30.5 us
+#endif
+constexpr int kStageBig = GCS_STAGE_BIG, kStageSmall = 256;
 // staged record: x y z dx dy dz m w/Z as four double2 chunks (+ GCS_REC_PAD doubles of stride
 // padding); GCS_REC_SWZ stores chunk c of record r at slot c ^ ((r >> 2) & 3) (LDS bank spread)
 #ifndef GCS_REC_PAD
@@ -854,7 +857,9 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
 #define GCS_RANK_LANES 4  // phase A's per-bin work sum + source compaction: 4 lanes per bin (1: wave 0 alone)
 #endif
 #ifndef GCS_GATHER_PIPE
-#define GCS_GATHER_PIPE 1  // phase C loads the next staged record while accumulating the current one
+// phase C: 1 loads the next staged record while accumulating the current one; 2 takes two
+// records per trip (two independent exp chains in flight)
+#define GCS_GATHER_PIPE 2
 #endif
 #ifndef GCS_MAPV_EARLY
 #define GCS_MAPV_EARLY 1  // phase D's map direction stats are loaded before phase A
@@ -871,15 +876,19 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   constexpr int NT = kBinTile * LANES, NW = NT / 64;
   static_assert(LANES == 4 || LANES == 8, "phase C splits each bin over 4 or 8 lanes");
   __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
-  __shared__ uint16_t s_rl[kMaxRl];
+  __shared__ double s_rec[STAGE * kRecD];
 #if GCS_RANK_LANES == 4
+  // the raw reverse-kNN list is dead once phase A has compacted it, before phase B stages the
+  // records: it lives in the record stage (2.5 KiB less LDS per workgroup)
+  static_assert(kMaxRl * sizeof(uint16_t) <= STAGE * kRecD * sizeof(double), "raw list fits the stage");
+  uint16_t* const s_rl = reinterpret_cast<uint16_t*>(s_rec);
   __shared__ uint16_t s_rlc[kMaxRl];  // each bin's non-empty sources, compacted (phase C's list)
   __shared__ uint8_t s_act[kBinTile];
   uint16_t* const rlist = s_rlc;
 #else
+  __shared__ uint16_t s_rl[kMaxRl];
   uint16_t* const rlist = s_rl;
 #endif
-  __shared__ double s_rec[STAGE * kRecD];
   __shared__ double4 s_bd[kBinTile];
   __shared__ int s_q[kBinTile + 1];
   __shared__ uint32_t s_work[kBinTile];
@@ -1157,6 +1166,55 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         } else {
           ++r;
         }
+      }
+    } else if (staged && GCS_GATHER_PIPE == 2) {
+      // two records per trip: both records' dot / exp chains are independent, so they issue
+      // interleaved (the exp chain, not the loads, is the gather's latency); the sums still take
+      // record i before record i + 1, so the accumulation order is the one-record loop's
+      uint32_t r = s_off[j] + kk, left = c - kk;
+      uint32_t i = i0;
+      for (; i + 2 <= i1; i += 2) {
+        const uint32_t ra = r;
+        if (--left == 0) {  // next source (compacted: non-empty); record i + 1 exists
+          ++q;
+          j = rlist[q - q0];
+          left = s_cnt[j];
+          r = s_off[j];
+        } else {
+          ++r;
+        }
+        const uint32_t rb = r;
+        if (i + 2 < i1) {
+          if (--left == 0) {
+            ++q;
+            j = rlist[q - q0];
+            left = s_cnt[j];
+            r = s_off[j];
+          } else {
+            ++r;
+          }
+        }
+        const double2* pa = (const double2*)(s_rec + (size_t)ra * kRecD);
+        const double2* pb = (const double2*)(s_rec + (size_t)rb * kRecD);
+        const uint32_t sa = rec_swz(ra), sb = rec_swz(rb);
+        const double2 a0 = pa[0 ^ sa], a1 = pa[1 ^ sa], a2 = pa[2 ^ sa], a3 = pa[3 ^ sa];
+        const double2 b0 = pb[0 ^ sb], b1 = pb[1 ^ sb], b2 = pb[2 ^ sb], b3 = pb[3 ^ sb];
+        const double ea = exp((dot3_exact(a1.y, a2.x, a2.y, bd.x, bd.y, bd.z) - a3.x) * inv_tau);
+        const double eb = exp((dot3_exact(b1.y, b2.x, b2.y, bd.x, bd.y, bd.z) - b3.x) * inv_tau);
+        {
+          const double d[3] = {a1.y, a2.x, a2.y}, p[3] = {a0.x, a0.y, a1.x};
+          add_contrib(acc, a3.y * ea, d, p);
+        }
+        {
+          const double d[3] = {b1.y, b2.x, b2.y}, p[3] = {b0.x, b0.y, b1.x};
+          add_contrib(acc, b3.y * eb, d, p);
+        }
+      }
+      if (i < i1) {
+        const double2* rp = (const double2*)(s_rec + (size_t)r * kRecD);
+        const uint32_t sw = rec_swz(r);
+        const double2 c0 = rp[0 ^ sw], c1 = rp[1 ^ sw], c2 = rp[2 ^ sw], c3 = rp[3 ^ sw];
+        bin_contrib(acc, bd, inv_tau, c0.x, c0.y, c1.x, c1.y, c2.x, c2.y, c3.x, c3.y);
       }
     } else if (staged) {
       // a source's records are one contiguous LDS run: the record index advances by one and is
@@ -1600,16 +1658,16 @@ __device__ __forceinline__ void final_epilogue(const double (&v)[NV], double* sc
 
 // mirror (may be null): after the epilogue the whole scalar block is copied to this mapped host
 // buffer, so the host reads the scan's results without a separate D2H copy.
-template <int NV, unsigned MAXMASK, int KIND>
-__global__ __launch_bounds__(kBlock) void k_final(const double* __restrict__ partials, int nblocks, double* scalars,
-                                                  double* mirror) {
-  __shared__ double lds[kWaves * pstride<NV>()];
+template <int NV, unsigned MAXMASK, int KIND, int NT = kBlock>
+__global__ __launch_bounds__(NT) void k_final(const double* __restrict__ partials, int nblocks, double* scalars,
+                                              double* mirror) {
+  __shared__ double lds[(NT / 64) * pstride<NV>()];
   double v[NV];
-  reduce_partials<NV, MAXMASK>(partials, nblocks, v, lds);
+  reduce_partials<NV, MAXMASK, NT>(partials, nblocks, v, lds);
   if (threadIdx.x == 0) final_epilogue<NV, KIND>(v, scalars);
   if (mirror) {
     __syncthreads();
-    for (int i = threadIdx.x; i < SC_COUNT; i += kBlock) mirror[i] = scalars[i];
+    for (int i = threadIdx.x; i < SC_COUNT; i += NT) mirror[i] = scalars[i];
   }
 }
 
@@ -1618,6 +1676,7 @@ __global__ __launch_bounds__(kBlock) void k_final(const double* __restrict__ par
 // bin kernel at C3 took 30 us; with a first level on 128 CUs the one-block tail folds 128 rows.
 constexpr int kFoldRows = 64;
 constexpr int kFoldDirect = 2048;  // up to this many rows a single block folds directly (C2 bins: 1563)
+// (a 1024-thread direct fold measured slower: C2 bins fold 8.1 -> 10.1 us, the 391-row folds +0.3-0.7 us)
 template <int NV, unsigned MAXMASK>
 __global__ __launch_bounds__(kBlock) void k_fold(const double* __restrict__ partials, int nblocks, double* out) {
   __shared__ double lds[kWaves * pstride<NV>()];
