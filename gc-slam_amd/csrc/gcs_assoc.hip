@@ -1,0 +1,802 @@
+// Primitive association by unbalanced optimal transport on gfx950 -- the live primitive path's
+// second operator: associate_primitives_ot,
+// FS/backend/operators/primitive_association.py:239-553.
+//
+//   k_as_prep      one lane per measurement row: mean position ((Lambda + eps I)^-1 theta, partial
+//                  pivoting), resultant direction and kappa (measurement_batch.py:389-411), A_vmf of
+//                  kappa, the MA-hex stencil tile ids (tiling.py:148-186, :309-336) and their index in
+//                  the view's tile list (first match, -1 none: :338-344); one lane per view entry: A_vmf
+//                  of its kappa and the valid count
+//   k_as_pool      one workgroup per row: the row's pool (n_stencil x m_tile_view entries) costed
+//                  (:351-365; ||dx||^2 + beta H^2_vMF, 1e12 where invalid or the tile is missing), the
+//                  k_assoc smallest by (cost, pool position) -- lax.sort with num_keys=1 is stable on
+//                  cost alone (:376) -- per-thread sorted lists merged by k rounds of a block argmin;
+//                  then per candidate the unmasked cost + recency, row-min subtraction, addressing
+//                  (:377-403)
+//   k_as_sinkhorn  one 1024-thread workgroup: marginals a (policy) and b (uniform), the optional median
+//                  scaling, k_sinkhorn fixed unbalanced iterations (:105-138) with the K_mat rows in
+//                  registers and the column sums in a fixed tree, pi, row masses, responsibilities and
+//                  the OTCert / Support / Influence scalars (:465-551) -- the p95 order statistics by an
+//                  8-pass radix select -- into mapped host memory
+// No floating-point atomics; every sum has a fixed order: bitwise reproducible.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+
+#include "gcslam_hip.h"
+
+namespace gcs {
+namespace {
+
+constexpr int kAsThreads = 256;
+constexpr int kShThreads = 1024;
+constexpr int kMaxStencil = 64;
+constexpr double kLog4Pi = 2.5310242469692907;     // np.log(4.0 * np.pi)
+constexpr double kLog2 = 0.6931471805599453;       // np.log(2.0)
+constexpr double kSqrt3Half = 0.8660254037844386;  // jnp.sqrt(3.0) * 0.5 (:319)
+constexpr double kCostInvalid = 1e12;              // :365
+constexpr double kEigMin = 1e-12;                  // _compute_sparse_cost_matrix_jax eig_min
+constexpr int kBitsPerAxis = 21;                   // tiling.py:80
+constexpr int64_t kBias = 1LL << 20;               // tiling.py:81
+constexpr int64_t kMask = (1LL << kBitsPerAxis) - 1;
+
+struct AsParams {
+  int n, m_view, n_tiles, n_stencil, k, iters, m_pool;
+  int a_policy, row_min, med;
+  double beta, eps, tau_a, tau_b, eps_mass, eps_lift, eps_dir, h, lam, eps_lam;
+  long long scan_seq;
+};
+
+struct AsWork {
+  double *pos, *dir, *kap, *A1, *A2, *dt;
+  int32_t* tix;
+  int32_t* cand;
+  uint32_t* mvalid;
+};
+
+struct AsIn {
+  const double *Lambdas, *thetas, *etas, *weights;
+  const uint8_t* valid;
+  int n_lobes;
+  const int64_t* tile_ids;
+  const double *vpos, *vdir, *vkap;
+  const uint8_t* vvalid;
+  const int64_t *vlast, *vtile;
+  const int32_t* vslot;
+};
+
+struct AsOut {
+  double *resp, *rmass, *cost;
+  int32_t* cand;
+  int64_t *tile, *slot;
+  double* cert;  // mapped host
+};
+
+// A_vmf(k) = log(4 pi) + log sinh(k) - log k with the stable log-sinh (:141-149); k**3 is
+// lax.integer_pow (k k k)
+__device__ __forceinline__ double a_vmf(double k) {
+#pragma clang fp contract(off)
+  k = fmax(k, kEigMin);
+  double ls;
+  if (k > 20.0) ls = k - kLog2;
+  else if (k >= 1e-2) ls = log(sinh(k));
+  else ls = log(k + (k * k * k) / 6.0);
+  return (kLog4Pi + ls) - log(k);
+}
+
+// cost of measurement (p, d, k, A1) against view entry e (:166-197)
+__device__ __forceinline__ double pair_cost(const double* mp, const double* md, double mk, double A1,
+                                            const double* __restrict__ vpos, const double* __restrict__ vdir,
+                                            const double* __restrict__ vkap, const double* __restrict__ A2, int e,
+                                            double beta) {
+#pragma clang fp contract(off)
+  const double dx = mp[0] - vpos[3 * e], dy = mp[1] - vpos[3 * e + 1], dz = mp[2] - vpos[3 * e + 2];
+  const double d_pos = (dx * dx + dy * dy) + dz * dz;
+  const double vk = vkap[e];
+  const double s0 = mk * md[0] + vk * vdir[3 * e], s1 = mk * md[1] + vk * vdir[3 * e + 1],
+               s2 = mk * md[2] + vk * vdir[3 * e + 2];
+  const double km = 0.5 * sqrt((s0 * s0 + s1 * s1) + s2 * s2);
+  const double bc = exp(a_vmf(fmax(km, kEigMin)) - 0.5 * (A1 + A2[e]));
+  double d_dir = fmax(0.0, 1.0 - bc);
+  if (!(mk > 0.0 && vk > 0.0)) d_dir = 0.0;
+  return d_pos + beta * d_dir;
+}
+
+// total order of doubles as unsigned keys (NaN last, as lax.sort / numpy argsort place it)
+__device__ __forceinline__ unsigned long long order_key(double x) {
+  if (isnan(x)) return ~0ULL;
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+
+__device__ __forceinline__ int64_t pack_tile(int64_t c1, int64_t c2, int64_t cz) {
+  return (((c1 + kBias) & kMask) << (2 * kBitsPerAxis)) | (((c2 + kBias) & kMask) << kBitsPerAxis) |
+         ((cz + kBias) & kMask);
+}
+
+// x = (L + eps I)^-1 th: Gaussian elimination with partial pivoting (jnp.linalg.solve is LU)
+__device__ __forceinline__ void solve3_pivot(const double* L, double eps, const double* th, double* x) {
+#pragma clang fp contract(off)
+  double A[3][4];
+  for (int r = 0; r < 3; ++r) {
+    for (int c = 0; c < 3; ++c) A[r][c] = L[3 * r + c] + (r == c ? eps : 0.0);
+    A[r][3] = th[r];
+  }
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    int pr = c;
+#pragma unroll
+    for (int r = c + 1; r < 3; ++r)
+      if (fabs(A[r][c]) > fabs(A[pr][c])) pr = r;
+    if (pr != c)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double tmp = A[c][q];
+        A[c][q] = A[pr][q];
+        A[pr][q] = tmp;
+      }
+#pragma unroll
+    for (int r = c + 1; r < 3; ++r) {
+      const double f = A[r][c] / A[c][c];
+#pragma unroll
+      for (int q = c; q < 4; ++q) A[r][q] = A[r][q] - f * A[c][q];
+    }
+  }
+  x[2] = A[2][3] / A[2][2];
+  x[1] = (A[1][3] - A[1][2] * x[2]) / A[1][1];
+  x[0] = ((A[0][3] - A[0][1] * x[1]) - A[0][2] * x[2]) / A[0][0];
+}
+
+__global__ __launch_bounds__(kAsThreads) void k_as_prep(AsIn in, AsParams p, AsWork w, const int8_t* __restrict__ st) {
+#pragma clang fp contract(off)
+  const int g = blockIdx.x * kAsThreads + threadIdx.x;
+  if (g < p.n) {
+    const int i = g;
+    double L[9], th[3], x[3];
+    for (int k = 0; k < 9; ++k) L[k] = in.Lambdas[9 * i + k];
+    for (int k = 0; k < 3; ++k) th[k] = in.thetas[3 * i + k];
+    solve3_pivot(L, p.eps_lift, th, x);
+    double es[3];
+    for (int c = 0; c < 3; ++c) es[c] = in.etas[(size_t)i * in.n_lobes * 3 + c];
+    for (int b = 1; b < in.n_lobes; ++b)
+      for (int c = 0; c < 3; ++c) es[c] = es[c] + in.etas[((size_t)i * in.n_lobes + b) * 3 + c];
+    const double kap = sqrt((es[0] * es[0] + es[1] * es[1]) + es[2] * es[2]);
+    for (int c = 0; c < 3; ++c) {
+      w.pos[3 * i + c] = x[c];
+      w.dir[3 * i + c] = es[c] / (kap + p.eps_dir);
+    }
+    w.kap[i] = kap;
+    w.A1[i] = a_vmf(fmax(kap, kEigMin));
+    // stencil tiles (:317-336) and their view tile index (first match, :341-344)
+    const double s1 = x[0];
+    const double s2 = x[0] * 0.5 + x[1] * kSqrt3Half;
+    const int64_t c1 = (int64_t)floor(s1 / p.h), c2 = (int64_t)floor(s2 / p.h), cz = (int64_t)floor(x[2] / p.h);
+    for (int s = 0; s < p.n_stencil; ++s) {
+      const int64_t id = pack_tile(c1 + st[3 * s], c2 + st[3 * s + 1], cz + st[3 * s + 2]);
+      int hit = -1;
+      for (int q = 0; q < p.n_tiles; ++q)
+        if (in.tile_ids[q] == id) {
+          hit = q;
+          break;
+        }
+      w.tix[(size_t)i * p.n_stencil + s] = hit;
+    }
+  } else if (g < p.n + p.m_pool) {
+    const int e = g - p.n;
+    w.A2[e] = a_vmf(fmax(in.vkap[e], kEigMin));
+    if (in.vvalid[e]) atomicAdd(w.mvalid, 1u);  // integer count (order-free)
+  }
+}
+
+template <int KM>
+__device__ __forceinline__ void list_insert(unsigned long long (&key)[KM], int (&idx)[KM], unsigned long long k, int p) {
+  // sorted ascending by (key, idx); the new entry is dropped if it is not below the last
+  if (k > key[KM - 1] || (k == key[KM - 1] && p >= idx[KM - 1])) return;
+  key[KM - 1] = k;
+  idx[KM - 1] = p;
+#pragma unroll
+  for (int j = KM - 1; j > 0; --j) {
+    const bool sw = key[j] < key[j - 1] || (key[j] == key[j - 1] && idx[j] < idx[j - 1]);
+    if (sw) {
+      const unsigned long long tk = key[j];
+      key[j] = key[j - 1];
+      key[j - 1] = tk;
+      const int ti = idx[j];
+      idx[j] = idx[j - 1];
+      idx[j - 1] = ti;
+    }
+  }
+}
+
+__device__ __forceinline__ bool kless(unsigned long long ka, int pa, unsigned long long kb, int pb) {
+  return ka < kb || (ka == kb && pa < pb);
+}
+
+// one workgroup per measurement row
+template <int KM>
+__global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsWork w, AsOut o) {
+#pragma clang fp contract(off)
+  __shared__ int s_tix[kMaxStencil];
+  __shared__ unsigned long long s_wk[2][kAsThreads / 64];
+  __shared__ int s_wp[2][kAsThreads / 64];
+  __shared__ int s_sel[32];
+  const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const bool row_valid = in.valid[i] != 0;
+  if (t < p.n_stencil) s_tix[t] = w.tix[(size_t)i * p.n_stencil + t];
+  __syncthreads();
+  const double mp[3] = {w.pos[3 * i], w.pos[3 * i + 1], w.pos[3 * i + 2]};
+  const double md[3] = {w.dir[3 * i], w.dir[3 * i + 1], w.dir[3 * i + 2]};
+  const double mk = w.kap[i], A1 = w.A1[i];
+  if (row_valid) {
+    unsigned long long key[KM];
+    int idx[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+      key[j] = ~0ULL;
+      idx[j] = 0x7fffffff;
+    }
+    const int P = p.n_stencil * p.m_view;
+    int s = t / p.m_view, off = t % p.m_view;
+    const int ds = kAsThreads / p.m_view, doff = kAsThreads % p.m_view;
+    for (int q = t; q < P; q += kAsThreads) {
+      const int ti = s_tix[s];
+      const int e = (ti < 0 ? 0 : ti) * p.m_view + off;
+      double c = kCostInvalid;
+      if (ti >= 0 && in.vvalid[e]) c = pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e, p.beta);
+      list_insert<KM>(key, idx, order_key(c), q);
+      s += ds;
+      off += doff;
+      if (off >= p.m_view) {
+        off -= p.m_view;
+        ++s;
+      }
+    }
+    // k rounds of a block argmin over the lists' heads; the winner's owner pops its head
+    for (int r = 0; r < p.k; ++r) {
+      unsigned long long bk = key[0];
+      int bp = idx[0];
+#pragma unroll
+      for (int sh = 32; sh >= 1; sh >>= 1) {
+        const unsigned long long ok = __shfl_xor(bk, sh, 64);
+        const int op = __shfl_xor(bp, sh, 64);
+        if (kless(ok, op, bk, bp)) {
+          bk = ok;
+          bp = op;
+        }
+      }
+      const int buf = r & 1;
+      if (lane == 0) {
+        s_wk[buf][wid] = bk;
+        s_wp[buf][wid] = bp;
+      }
+      __syncthreads();
+      bk = s_wk[buf][0];
+      bp = s_wp[buf][0];
+#pragma unroll
+      for (int v = 1; v < kAsThreads / 64; ++v)
+        if (kless(s_wk[buf][v], s_wp[buf][v], bk, bp)) {
+          bk = s_wk[buf][v];
+          bp = s_wp[buf][v];
+        }
+      if (t == 0) s_sel[r] = bp;
+      if (idx[0] == bp && key[0] == bk) {  // pool positions are unique: exactly one owner
+#pragma unroll
+        for (int j = 0; j < KM - 1; ++j) {
+          key[j] = key[j + 1];
+          idx[j] = idx[j + 1];
+        }
+        key[KM - 1] = ~0ULL;
+        idx[KM - 1] = 0x7fffffff;
+      }
+    }
+    __syncthreads();
+  }
+  if (wid != 0) return;
+  // per candidate (lane k < K): view index, unmasked cost + recency, row min (:377-403)
+  const bool act = lane < p.k;
+  int e = 0;
+  if (act && row_valid) {
+    const int q = s_sel[lane];
+    const int ti = s_tix[q / p.m_view];
+    e = (ti < 0 ? 0 : ti) * p.m_view + q % p.m_view;
+  }
+  double c = INFINITY, dt = 0.0;
+  if (act) {
+    c = pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e, p.beta);
+    const long long last = (long long)in.vlast[e];
+    dt = (double)(p.scan_seq - last > 0 ? p.scan_seq - last : 0);
+    c = c + p.eps_lam * dt;
+  }
+  double mn = c;
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1) mn = fmin(mn, __shfl_xor(mn, sh, 64));
+  if (act) {
+    if (p.row_min) c = c - mn;
+    const size_t o_ = (size_t)i * p.k + lane;
+    o.cost[o_] = c;
+    w.cand[o_] = e;
+    w.dt[o_] = dt;
+    if (o.cand) o.cand[o_] = e;
+    if (o.tile) o.tile[o_] = in.vtile[e];
+    if (o.slot) o.slot[o_] = (int64_t)in.vslot[e];
+  }
+}
+
+// ---------------------------------------------------------------- single-workgroup Sinkhorn
+template <int NV>
+__device__ __forceinline__ void bsum(double (&v)[NV], double* lds /*16*NV*/) {
+  // fixed xor tree in each wave, then the 16 wave rows in order (valid in every thread)
+#pragma unroll
+  for (int sh = 32; sh >= 1; sh >>= 1)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) v[k] += __shfl_xor(v[k], sh, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < NV; ++k) lds[wid * NV + k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    double s = lds[k];
+    for (int q = 1; q < kShThreads / 64; ++q) s += lds[q * NV + k];
+    v[k] = s;
+  }
+}
+
+// k-th smallest (0-based) of the values the threads hold (slot j of a thread counts when bit j of
+// its mask is set), MSB-first radix select over the total-order keys, 8 bits per pass; the result
+// is returned in every thread
+template <int CAP>
+__device__ __forceinline__ double radix_select(const double (&vals)[CAP], uint32_t okmask, int k, uint32_t* hist /*256*/,
+                               uint32_t* sel /*4*/) {
+  static_assert(CAP <= 32, "slot mask is 32 bits");
+  unsigned long long prefix = 0, mask = 0;
+  const int t = threadIdx.x, lane = t & 63;
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    __syncthreads();
+    if (t < 256) hist[t] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < CAP; ++j)
+      if ((okmask >> j) & 1u) {
+        const unsigned long long kk = order_key(vals[j]);
+        if ((kk & mask) == prefix) atomicAdd(&hist[(kk >> shift) & 255ULL], 1u);
+      }
+    __syncthreads();
+    if (t < 64) {
+      const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+      const uint32_t mine = h0 + h1 + h2 + h3;
+      uint32_t inc = mine;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+      }
+      const uint32_t exc = inc - mine;
+      if ((uint32_t)k >= exc && (uint32_t)k < inc) {  // exactly one lane
+        uint32_t below = exc, d = 4 * lane;
+        const uint32_t hs[4] = {h0, h1, h2, h3};
+        for (int q = 0; q < 4; ++q) {
+          if ((uint32_t)k < below + hs[q]) {
+            d = 4 * lane + q;
+            break;
+          }
+          below += hs[q];
+        }
+        sel[0] = d;
+        sel[1] = below;
+      }
+    }
+    __syncthreads();
+    prefix |= (unsigned long long)sel[0] << shift;
+    mask |= 255ULL << shift;
+    k -= (int)sel[1];
+  }
+  // invert the key map
+  const unsigned long long b = (prefix >> 63) ? (prefix & 0x7fffffffffffffffULL) : ~prefix;
+  return prefix == ~0ULL ? NAN : __longlong_as_double((long long)b);
+}
+
+enum CertSlot : int {
+  CE_DEFECT_A, CE_DEFECT_B, CE_MASS_TOTAL, CE_SUM_A, CE_SUM_B, CE_SUM_M, CE_SUM_NOVEL, CE_P95_A, CE_P95_B,
+  CE_NONZERO_A, CE_NONZERO_B, CE_B_P95, CE_ESS, CE_MASS_EPS, CE_TOTAL_COST, CE_SUPPORT, CE_EXACT, CE_MVALID,
+  CE_COUNT
+};
+
+template <int KM, int RPT>
+__global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p, AsWork w, AsOut o, int n_valid_host) {
+#pragma clang fp contract(off)
+  __shared__ double s_red[16 * (KM + 8)];
+  __shared__ double s_col[2][16 * KM];
+  __shared__ uint32_t s_hist[256], s_sel[4];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int N = p.n, K = p.k;
+  const bool empty = n_valid_host == 0 || *w.mvalid == 0u;
+  if (empty) {  // :272-287 -- zeros, exact cert
+    for (int q = t; q < N * K; q += kShThreads) {
+      o.resp[q] = 0.0;
+      o.cost[q] = 0.0;
+      if (o.cand) o.cand[q] = 0;
+      if (o.tile) o.tile[q] = 0;
+      if (o.slot) o.slot[q] = 0;
+    }
+    for (int q = t; q < N; q += kShThreads) o.rmass[q] = 0.0;
+    if (t < CE_COUNT) o.cert[t] = t == CE_EXACT ? 1.0 : (t == CE_MVALID ? (double)*w.mvalid : 0.0);
+    return;
+  }
+  // marginal a (:412-424)
+  double va[RPT], X[RPT * KM];  // X: the cost rows, then K_mat = exp(-C / eps) in place
+  double part[1] = {0.0};
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int r = t + j * kShThreads;
+    va[j] = 0.0;
+    if (r < N) {
+      va[j] = in.valid[r] ? 1.0 : 0.0;
+      if (p.a_policy == 1) va[j] = va[j] * in.weights[r];
+    }
+    part[0] += va[j];
+  }
+  bsum<1>(part, s_red);
+  const double sum_a = fmax(part[0], p.eps_mass);
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) va[j] = va[j] / sum_a;
+  uint32_t okm = 0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const int r = t + j * kShThreads;
+      const bool ok = r < N && k < K;
+      X[j * KM + k] = ok ? o.cost[(size_t)r * K + k] : 0.0;
+      if (ok) okm |= 1u << (j * KM + k);
+    }
+  if (p.med) {  // cost_scale_by_median (:405-407)
+    const int tot = N * K;
+    double med;
+    if (tot & 1) {
+      med = radix_select<RPT * KM>(X, okm, tot / 2, s_hist, s_sel);
+    } else {
+      const double lo = radix_select<RPT * KM>(X, okm, tot / 2 - 1, s_hist, s_sel);
+      const double hi = radix_select<RPT * KM>(X, okm, tot / 2, s_hist, s_sel);
+      med = (lo + hi) * 0.5;  // jnp.median: mean of the two middle values
+    }
+#pragma unroll
+    for (int q = 0; q < RPT * KM; ++q) {
+      X[q] = X[q] / (med + 1e-12);
+      if ((okm >> q) & 1u) o.cost[(size_t)(t + (q / KM) * kShThreads) * K + q % KM] = X[q];  // result.cost_matrix
+    }
+  }
+  const double eps = fmax(p.eps, 1e-12);
+  const double ua = 1.0 / (1.0 + p.tau_a / eps), vb = 1.0 / (1.0 + p.tau_b / eps);
+  const double bk = 1.0 / (double)K;
+#pragma unroll
+  for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
+  double u[RPT], v[KM];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) u[j] = 1.0;
+#pragma unroll
+  for (int k = 0; k < KM; ++k) v[k] = 1.0;
+  for (int it = 0; it < p.iters; ++it) {
+    double cp[KM];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) cp[k] = 0.0;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      double kv = 0.0;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) kv += X[j * KM + k] * v[k];
+      u[j] = (t + j * kShThreads < N) ? pow(va[j] / (kv + 1e-12), ua) : 0.0;
+#pragma unroll
+      for (int k = 0; k < KM; ++k) cp[k] += X[j * KM + k] * u[j];
+    }
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1)
+#pragma unroll
+      for (int k = 0; k < KM; ++k) cp[k] += __shfl_xor(cp[k], sh, 64);
+    double* col = s_col[it & 1];
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < KM; ++k) col[wid * KM + k] = cp[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      double s = col[k];
+      for (int q = 1; q < kShThreads / 64; ++q) s += col[q * KM + k];
+      v[k] = k < K ? pow(bk / (s + 1e-12), vb) : 0.0;
+    }
+  }
+  // pi, row masses, responsibilities and the cert sums
+  // acc: [sum rm, sum rm^2, sum novel, defect_a^2, sum pi C, nonzero_a, sum pi | col masses K]
+  double acc[7 + KM];
+#pragma unroll
+  for (int q = 0; q < 7 + KM; ++q) acc[q] = 0.0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int r = t + j * kShThreads;
+    if (r >= N) continue;
+    const bool rv = in.valid[r] != 0;
+    double rm = 0.0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (k >= K) continue;
+      const double pik = (u[j] * X[j * KM + k]) * v[k];
+      rm += pik;
+      acc[4] += pik * o.cost[(size_t)r * K + k];
+      acc[6] += pik;
+      acc[7 + k] += pik;
+      o.resp[(size_t)r * K + k] = rv ? pik : 0.0;
+    }
+    o.rmass[r] = rm;
+    acc[0] += rm;
+    acc[1] += rm * rm;
+    acc[2] += fmax(va[j] - rm, 0.0);
+    acc[3] += (rm - va[j]) * (rm - va[j]);
+    acc[5] += va[j] > p.eps_mass ? 1.0 : 0.0;
+  }
+  bsum<7 + KM>(acc, s_red);
+  // recency-weighted b rows (:441-446): exp(-lambda dt) normalised per row
+  double brow[RPT * KM];
+  uint32_t okb = 0, oka = 0;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int r = t + j * kShThreads;
+    double dsum = 0.0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      double dd = 0.0;
+      if (r < N && k < K) {
+        dd = exp(-p.lam * w.dt[(size_t)r * K + k]);
+        dd = dd > 0.0 ? dd : 0.0;
+        okb |= 1u << (j * KM + k);
+      }
+      brow[j * KM + k] = dd;
+      dsum += dd;
+    }
+    const double den = fmax(dsum, p.eps_mass);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) brow[j * KM + k] = brow[j * KM + k] / den;
+    if (r < N) oka |= 1u << j;
+  }
+  // p95 of a (:488-493) and of the b rows (:445-446)
+  const double p95_a = radix_select<RPT>(va, oka, std::min((int)(0.95 * (double)N), N - 1), s_hist, s_sel);
+  const int nbt = N * K;
+  const double p95_b_row = radix_select<RPT * KM>(brow, okb, std::min((int)(0.95 * (double)nbt), nbt - 1), s_hist, s_sel);
+  if (t == 0) {
+    double db = 0.0;
+    for (int k = 0; k < K; ++k) db += (acc[7 + k] - bk) * (acc[7 + k] - bk);
+    const double tm = acc[6];
+    o.cert[CE_DEFECT_A] = sqrt(acc[3]);
+    o.cert[CE_DEFECT_B] = sqrt(db);
+    o.cert[CE_MASS_TOTAL] = tm;
+    o.cert[CE_SUM_A] = sum_a;
+    o.cert[CE_SUM_B] = bk * (double)K;
+    o.cert[CE_SUM_M] = acc[0];
+    o.cert[CE_SUM_NOVEL] = acc[2];
+    o.cert[CE_P95_A] = p95_a;
+    o.cert[CE_P95_B] = bk;  // b uniform: every entry is 1 / K
+    o.cert[CE_NONZERO_A] = acc[5];
+    o.cert[CE_NONZERO_B] = bk > p.eps_mass ? (double)K : 0.0;
+    o.cert[CE_B_P95] = p95_b_row;
+    o.cert[CE_ESS] = acc[0] * acc[0] / (acc[1] + p.eps_mass);
+    o.cert[CE_MASS_EPS] = p.eps_mass / (tm + p.eps_mass);
+    o.cert[CE_TOTAL_COST] = acc[4];
+    o.cert[CE_SUPPORT] = acc[5] / (double)std::max(N, 1);
+    o.cert[CE_EXACT] = 0.0;
+    o.cert[CE_MVALID] = (double)*w.mvalid;
+  }
+}
+
+}  // namespace
+}  // namespace gcs
+
+using namespace gcs;
+
+struct gcs_assoc_ctx {
+  int device = 0;
+  int max_meas = 0, max_pool = 0, max_k = 0;
+  std::string err;
+  hipStream_t own = nullptr, stream = nullptr;
+  double *d_pos = nullptr, *d_dir = nullptr, *d_kap = nullptr, *d_A1 = nullptr, *d_A2 = nullptr, *d_dt = nullptr;
+  int32_t *d_tix = nullptr, *d_cand = nullptr;
+  uint32_t* d_mvalid = nullptr;
+  int8_t* d_st = nullptr;
+  double* h_cert = nullptr;  // pinned, mapped
+  double* h_cert_dev = nullptr;
+};
+
+namespace {
+int as_fail(gcs_assoc_ctx* c, int code, const std::string& m) {
+  if (c) c->err = m;
+  return code;
+}
+#define ASCHK(ctx, expr)                                                                          \
+  do {                                                                                            \
+    hipError_t _e = (expr);                                                                       \
+    if (_e != hipSuccess) return as_fail((ctx), GCS_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
+  } while (0)
+
+// rows per Sinkhorn thread for k_assoc <= KM: the K_mat rows stay in registers
+constexpr int rpt_for(int km) { return km <= 8 ? 2 : 1; }
+}  // namespace
+
+extern "C" {
+
+int gcs_assoc_config_defaults(gcs_assoc_config* c) {
+  if (!c) return GCS_ERR_ARG;
+  memset(c, 0, sizeof(*c));
+  c->k_assoc = 8;       // GC_K_ASSOC, constants.py:356
+  c->k_sinkhorn = 50;   // GC_K_SINKHORN, constants.py:357
+  c->beta = 0.5;        // primitive_association.py:219-222
+  c->epsilon = 0.1;
+  c->tau_a = 0.5;
+  c->tau_b = 0.5;
+  c->cost_subtract_row_min = 1;
+  c->cost_scale_by_median = 0;
+  c->a_policy = GCS_ASSOC_A_UNIFORM;
+  c->b_policy = GCS_ASSOC_B_UNIFORM;
+  c->eps_mass = 1e-12;  // GC_EPS_MASS
+  c->eps_lift = 1e-9;   // GC_EPS_LIFT
+  c->eps_mass_dir = 1e-12;
+  c->h_tile = 2.0;      // GC_H_TILE, constants.py:408
+  c->r_stencil_tiles_xy = 1;  // constants.py:415-416
+  c->r_stencil_tiles_z = 0;
+  c->scan_seq = 0;
+  c->recency_decay_lambda = 0.02;  // GC_RECENCY_DECAY_LAMBDA, constants.py:419
+  return GCS_OK;
+}
+
+const char* gcs_assoc_last_error(const gcs_assoc_ctx* c) { return c ? c->err.c_str() : "null association context"; }
+
+int gcs_assoc_ctx_destroy(gcs_assoc_ctx* c) {
+  if (!c) return GCS_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* bufs[] = {c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, c->d_mvalid, c->d_st};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->h_cert) (void)hipHostFree(c->h_cert);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+  return GCS_OK;
+}
+
+int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int32_t device, gcs_assoc_ctx** out) {
+  if (!out) return GCS_ERR_ARG;
+  *out = nullptr;
+  if (max_meas < 1 || max_pool < 1 || max_k < 1 || max_k > 32 || max_meas > kShThreads * rpt_for(max_k))
+    return GCS_ERR_ARG;
+  auto* c = new gcs_assoc_ctx();
+  c->device = device;
+  c->max_meas = max_meas;
+  c->max_pool = max_pool;
+  c->max_k = max_k;
+  auto bad = [](hipError_t e) { return e != hipSuccess; };
+  const size_t N = (size_t)max_meas, M = (size_t)max_pool, NK = N * (size_t)max_k;
+  if (bad(hipSetDevice(device)) || bad(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) ||
+      bad(hipMalloc(&c->d_pos, N * 3 * 8)) || bad(hipMalloc(&c->d_dir, N * 3 * 8)) || bad(hipMalloc(&c->d_kap, N * 8)) ||
+      bad(hipMalloc(&c->d_A1, N * 8)) || bad(hipMalloc(&c->d_A2, M * 8)) || bad(hipMalloc(&c->d_dt, NK * 8)) ||
+      bad(hipMalloc(&c->d_tix, N * kMaxStencil * 4)) || bad(hipMalloc(&c->d_cand, NK * 4)) ||
+      bad(hipMalloc(&c->d_mvalid, 4)) || bad(hipMalloc(&c->d_st, kMaxStencil * 3)) ||
+      bad(hipHostMalloc(&c->h_cert, GCS_ASSOC_CERT_LEN * sizeof(double), hipHostMallocMapped)) ||
+      bad(hipHostGetDevicePointer((void**)&c->h_cert_dev, c->h_cert, 0))) {
+    gcs_assoc_ctx_destroy(c);
+    return GCS_ERR_HIP;
+  }
+  c->stream = c->own;
+  *out = c;
+  return GCS_OK;
+}
+
+int gcs_assoc_ctx_set_stream(gcs_assoc_ctx* c, void* stream) {
+  if (!c) return GCS_ERR_ARG;
+  ASCHK(c, hipSetDevice(c->device));
+  ASCHK(c, hipStreamSynchronize(c->stream));  // work queued on the old stream completes first
+  c->stream = stream ? (hipStream_t)stream : c->own;
+  return GCS_OK;
+}
+
+int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_meas* m,
+                                const gcs_assoc_view* v, gcs_assoc_outputs* o) {
+  if (!c || !cfg || !m || !v || !o) return GCS_ERR_ARG;
+  if (!o->responsibilities || !o->row_masses || !o->cost_matrix)
+    return as_fail(c, GCS_ERR_ARG, "responsibilities, row_masses and cost_matrix are required outputs");
+  const int K = cfg->k_assoc;
+  if (K < 1 || K > c->max_k) return as_fail(c, GCS_ERR_ARG, "k_assoc outside [1, max_k] of the context");
+  if (m->n_total < 1 || m->n_total > c->max_meas) return as_fail(c, GCS_ERR_ARG, "n_total outside [1, max_meas]");
+  if (m->n_lobes < 1) return as_fail(c, GCS_ERR_ARG, "n_lobes < 1");
+  // an unsupported policy raises only past the empty-case return, as in the reference (:272 vs :413-437)
+  const char* bad_policy = nullptr;
+  if (cfg->a_policy != GCS_ASSOC_A_UNIFORM && cfg->a_policy != GCS_ASSOC_A_WEIGHT)
+    bad_policy = "Unsupported measurement mass policy: only UNIFORM and WEIGHT_PROPORTIONAL are implemented";
+  else if (cfg->b_policy != GCS_ASSOC_B_UNIFORM)
+    bad_policy = "Unsupported map mass policy: only UNIFORM is implemented";
+  if (v->m_tile_view <= 0) return as_fail(c, GCS_ERR_ARG, "m_tile_view must be > 0");
+  if (v->n_tiles < 1) return as_fail(c, GCS_ERR_ARG, "the view needs at least one tile");
+  const long pool = (long)v->n_tiles * v->m_tile_view;
+  if (pool > c->max_pool) return as_fail(c, GCS_ERR_ARG, "view entries exceed max_pool");
+  if (cfg->r_stencil_tiles_xy < 0 || cfg->r_stencil_tiles_z < 0 || cfg->k_sinkhorn < 0)
+    return as_fail(c, GCS_ERR_ARG, "negative stencil radius or iteration count");
+  // stencil offsets, z slab outer, sorted axial disk inner (tiling.py:171-186; :309-336)
+  int8_t st[kMaxStencil * 3];
+  int ns = 0;
+  const int rxy = cfg->r_stencil_tiles_xy, rz = cfg->r_stencil_tiles_z;
+  for (int z = -rz; z <= rz; ++z)
+    for (int q = -rxy; q <= rxy; ++q)
+      for (int r = std::max(-rxy, -q - rxy); r <= std::min(rxy, -q + rxy); ++r) {
+        if (ns >= kMaxStencil) return as_fail(c, GCS_ERR_ARG, "stencil exceeds 64 tiles");
+        st[3 * ns] = (int8_t)q;
+        st[3 * ns + 1] = (int8_t)r;
+        st[3 * ns + 2] = (int8_t)z;
+        ++ns;
+      }
+  if ((long)ns * v->m_tile_view < K) return as_fail(c, GCS_ERR_ARG, "pool smaller than k_assoc");
+  ASCHK(c, hipSetDevice(c->device));
+  hipStream_t s = c->stream;
+  AsParams p{};
+  p.n = m->n_total;
+  p.m_view = v->m_tile_view;
+  p.n_tiles = v->n_tiles;
+  p.n_stencil = ns;
+  p.k = K;
+  p.iters = cfg->k_sinkhorn;
+  p.m_pool = (int)pool;
+  p.a_policy = cfg->a_policy == GCS_ASSOC_A_WEIGHT ? 1 : 0;
+  p.row_min = cfg->cost_subtract_row_min != 0;
+  p.med = cfg->cost_scale_by_median != 0;
+  p.beta = cfg->beta;
+  p.eps = cfg->epsilon;
+  p.tau_a = cfg->tau_a;
+  p.tau_b = cfg->tau_b;
+  p.eps_mass = cfg->eps_mass;
+  p.eps_lift = cfg->eps_lift;
+  p.eps_dir = cfg->eps_mass_dir;
+  p.h = std::max(cfg->h_tile, 1e-12);
+  p.lam = cfg->recency_decay_lambda;
+  p.eps_lam = cfg->epsilon * cfg->recency_decay_lambda;  // float(epsilon) * float(lambda) first (:397)
+  p.scan_seq = (long long)cfg->scan_seq;
+  AsIn in{m->Lambdas, m->thetas, m->etas, m->weights, m->valid_mask, m->n_lobes, v->tile_ids, v->positions,
+          v->directions, v->kappas, v->valid_mask, v->last_supported_scan_seq, v->candidate_tile_ids,
+          v->candidate_slots};
+  AsWork w{c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, c->d_mvalid};
+  AsOut out{o->responsibilities, o->row_masses, o->cost_matrix, o->candidate_pool_indices, o->candidate_tile_ids,
+            o->candidate_slots, c->h_cert_dev};
+  ASCHK(c, hipMemcpyAsync(c->d_st, st, (size_t)ns * 3, hipMemcpyHostToDevice, s));
+  ASCHK(c, hipMemsetAsync(c->d_mvalid, 0, 4, s));
+  const int nprep = (int)((p.n + pool + kAsThreads - 1) / kAsThreads);
+  hipLaunchKernelGGL(k_as_prep, dim3(nprep), dim3(kAsThreads), 0, s, in, p, w, (const int8_t*)c->d_st);
+  const int km = K <= 8 ? 8 : (K <= 16 ? 16 : 32);
+  if (bad_policy) {
+    uint32_t mv = 0;
+    ASCHK(c, hipMemcpyAsync(&mv, c->d_mvalid, 4, hipMemcpyDeviceToHost, s));
+    ASCHK(c, hipStreamSynchronize(s));
+    if (m->n_valid != 0 && mv != 0) return as_fail(c, GCS_ERR_ARG, bad_policy);
+    // empty: the Sinkhorn kernel's zero path writes the reference's empty result
+  }
+  if (bad_policy) {
+    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(1), dim3(kShThreads), 0, s, in, p, w, out, 0);
+  } else if (km == 8) {
+    hipLaunchKernelGGL(k_as_pool<8>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(1), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+  } else if (km == 16) {
+    hipLaunchKernelGGL(k_as_pool<16>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(1), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+  } else {
+    hipLaunchKernelGGL(k_as_pool<32>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(1), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+  }
+  ASCHK(c, hipGetLastError());
+  ASCHK(c, hipStreamSynchronize(s));
+  for (int q = 0; q < GCS_ASSOC_CERT_LEN; ++q) o->cert[q] = c->h_cert[q];
+  o->exact = c->h_cert[CE_EXACT] != 0.0;
+  o->n_map_valid = (int32_t)c->h_cert[CE_MVALID];
+  return GCS_OK;
+}
+
+}  // extern "C"

@@ -104,6 +104,38 @@ class GcsSurfelOutputs(C.Structure):
                [("center", C.c_double * 3), ("n_valid", C.c_int32), ("cert", C.c_double * 2)]
 
 
+GCS_ASSOC_CERT_LEN = 18
+ASSOC_CERT_FIELDS = ("marginal_defect_a", "marginal_defect_b", "transport_mass_total", "sum_a", "sum_b", "sum_m",
+                     "sum_novel", "p95_a", "p95_b", "nonzero_a", "nonzero_b", "b_recency_p95", "ess_total",
+                     "mass_epsilon_ratio", "total_cost", "support_frac", "exact", "map_valid")
+
+
+class GcsAssocConfig(C.Structure):
+    _fields_ = [("k_assoc", C.c_int32), ("k_sinkhorn", C.c_int32), ("beta", C.c_double), ("epsilon", C.c_double),
+                ("tau_a", C.c_double), ("tau_b", C.c_double), ("cost_subtract_row_min", C.c_int32),
+                ("cost_scale_by_median", C.c_int32), ("a_policy", C.c_int32), ("b_policy", C.c_int32),
+                ("eps_mass", C.c_double), ("eps_lift", C.c_double), ("eps_mass_dir", C.c_double), ("h_tile", C.c_double),
+                ("r_stencil_tiles_xy", C.c_int32), ("r_stencil_tiles_z", C.c_int32), ("scan_seq", C.c_int64),
+                ("recency_decay_lambda", C.c_double)]
+
+
+class GcsAssocMeas(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("Lambdas", "thetas", "etas", "weights", "valid_mask")] + \
+               [("n_total", C.c_int32), ("n_lobes", C.c_int32), ("n_valid", C.c_int32)]
+
+
+class GcsAssocView(C.Structure):
+    _fields_ = [("tile_ids", C.c_void_p), ("n_tiles", C.c_int32), ("m_tile_view", C.c_int32)] + \
+               [(n, C.c_void_p) for n in ("positions", "directions", "kappas", "valid_mask",
+                                          "last_supported_scan_seq", "candidate_tile_ids", "candidate_slots")]
+
+
+class GcsAssocOutputs(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("responsibilities", "candidate_pool_indices", "candidate_tile_ids",
+                                          "candidate_slots", "row_masses", "cost_matrix")] + \
+               [("cert", C.c_double * GCS_ASSOC_CERT_LEN), ("exact", C.c_int32), ("n_map_valid", C.c_int32)]
+
+
 _SIGS = [
     ("gcs_version", C.c_char_p, []),
     ("gcs_abi_version", C.c_int, []),
@@ -182,6 +214,13 @@ _SIGS = [
     ("gcs_surfel_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("gcs_extract_lidar_surfels", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                             C.POINTER(GcsSurfelOutputs)]),
+    ("gcs_assoc_config_defaults", C.c_int, [C.POINTER(GcsAssocConfig)]),
+    ("gcs_assoc_ctx_create", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    ("gcs_assoc_ctx_destroy", C.c_int, [C.c_void_p]),
+    ("gcs_assoc_last_error", C.c_char_p, [C.c_void_p]),
+    ("gcs_assoc_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("gcs_associate_primitives_ot", C.c_int, [C.c_void_p, C.POINTER(GcsAssocConfig), C.POINTER(GcsAssocMeas),
+                                              C.POINTER(GcsAssocView), C.POINTER(GcsAssocOutputs)]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]

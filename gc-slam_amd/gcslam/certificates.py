@@ -48,6 +48,38 @@ class InfluenceCert:             # certificates.py:78-109
 
 
 @dataclass
+class ComputeCert:               # certificates.py:318-329 (shape / allocation accounting)
+    alloc_bytes_est: int = 0
+    largest_tensor_shape: tuple = (0, 0)
+    segment_sum_k: int = 0
+    psd_projection_count: int = 0
+    chol_solve_count: int = 0
+
+
+@dataclass
+class OTCert:                    # certificates.py:152-181 (association diagnostics)
+    marginal_defect_a: float = 0.0
+    marginal_defect_b: float = 0.0
+    transport_mass_total: float = 0.0
+    dual_gap_proxy: float = 0.0
+    sum_a: float = 0.0
+    sum_b: float = 0.0
+    sum_m: float = 0.0
+    sum_novel: float = 0.0
+    p95_a: float = 0.0
+    p95_b: float = 0.0
+    nonzero_a: int = 0
+    nonzero_b: int = 0
+    epsilon: float = 0.0
+    tau_a: float = 0.0
+    tau_b: float = 0.0
+    n_iters: int = 0
+    b_policy: str = ""
+    b_recency_decay_lambda: float = 0.0
+    b_recency_p95: float = 0.0
+
+
+@dataclass
 class CertBundle:                # certificates.py:349-486
     chart_id: str
     anchor_id: str
@@ -58,6 +90,8 @@ class CertBundle:                # certificates.py:349-486
     support: SupportCert = field(default_factory=SupportCert)
     mismatch: MismatchCert = field(default_factory=MismatchCert)
     influence: InfluenceCert = field(default_factory=InfluenceCert)
+    compute: ComputeCert = field(default_factory=ComputeCert)
+    ot: Optional[OTCert] = None  # populated by the association operator
 
     @classmethod
     def create_exact(cls, chart_id, anchor_id, **kw):

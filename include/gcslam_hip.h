@@ -27,6 +27,8 @@
  *   gcs_hypothesis_payload /    FS/backend/backend_node.py:1999-2119 (IW accumulation) and
  *   gcs_hypothesis_combine      FS/backend/operators/hypothesis.py:51-117 (barycenter)
  *   gcs_fibonacci_atlas         archive/bin_atlas.py:40-61
+ *   gcs_associate_primitives_ot FS/backend/operators/primitive_association.py:239-553
+ *                               associate_primitives_ot (+ tiling.py:148-186, measurement_batch.py:389-411)
  *   gcs_extract_lidar_surfels   FS/backend/operators/lidar_surfel_extraction.py:339-431
  *                               extract_lidar_surfels (+ FS/common/ma_hex_web.py:243-303
  *                               bin_points_3d, FS/backend/structures/measurement_batch.py:272-381)
@@ -396,6 +398,87 @@ int gcs_surfel_ctx_set_stream(gcs_surfel_ctx* ctx, void* stream);
 /* points: n x 3 f64, timestamps / weights: n f64 (device); n <= max_points.  Synchronises. */
 int gcs_extract_lidar_surfels(gcs_surfel_ctx* ctx, const double* points_dev, const double* timestamps_dev,
                               const double* weights_dev, int32_t n, gcs_surfel_outputs* out);
+
+/* ---------------------------------------------------------------- primitive path: OT association */
+/* associate_primitives_ot (primitive_association.py:239-553) on the GPU: per measurement the MA-hex
+ * stencil pool (n_stencil x m_tile_view view entries) costed by ||x_i - x_j||^2 + beta H^2_vMF
+ * (:152-197; 1e12 where the view entry is invalid or the stencil tile is not in the view), the
+ * k_assoc cheapest by (cost, pool position) (lax.sort with num_keys=1 is stable on cost alone, :376),
+ * the selected candidates' unmasked cost + recency (eps lambda dt) with the row minimum subtracted,
+ * then k_sinkhorn fixed iterations of unbalanced Sinkhorn (:105-138) on one workgroup; the OTCert /
+ * SupportCert / InfluenceCert scalars land in cert[] (GCS_ASSOC_CERT_* slots).  An association
+ * context owns the workspace for up to max_meas rows, max_pool view entries and k_assoc <= max_k
+ * (<= 32; max_meas <= 2048 for max_k <= 8, 1024 above). */
+#define GCS_ASSOC_CERT_LEN 18
+enum {
+  GCS_ASSOC_CERT_DEFECT_A = 0, GCS_ASSOC_CERT_DEFECT_B, GCS_ASSOC_CERT_MASS_TOTAL, GCS_ASSOC_CERT_SUM_A,
+  GCS_ASSOC_CERT_SUM_B, GCS_ASSOC_CERT_SUM_M, GCS_ASSOC_CERT_SUM_NOVEL, GCS_ASSOC_CERT_P95_A, GCS_ASSOC_CERT_P95_B,
+  GCS_ASSOC_CERT_NONZERO_A, GCS_ASSOC_CERT_NONZERO_B, GCS_ASSOC_CERT_B_RECENCY_P95, GCS_ASSOC_CERT_ESS,
+  GCS_ASSOC_CERT_MASS_EPS_RATIO, GCS_ASSOC_CERT_TOTAL_COST, GCS_ASSOC_CERT_SUPPORT_FRAC, GCS_ASSOC_CERT_EXACT,
+  GCS_ASSOC_CERT_MAP_VALID
+};
+enum { GCS_ASSOC_A_UNIFORM = 0, GCS_ASSOC_A_WEIGHT = 1 };  /* MeasurementMassPolicy (:40-48) */
+enum { GCS_ASSOC_B_UNIFORM = 0 };                          /* MapMassPolicy (:51-59): only UNIFORM runs */
+typedef struct gcs_assoc_ctx gcs_assoc_ctx;
+
+typedef struct {            /* AssociationConfig, primitive_association.py:206-236 */
+  int32_t k_assoc, k_sinkhorn;                     /* GC_K_ASSOC = 8, GC_K_SINKHORN = 50 */
+  double beta, epsilon, tau_a, tau_b;              /* 0.5, 0.1, 0.5, 0.5 */
+  int32_t cost_subtract_row_min, cost_scale_by_median;  /* 1, 0 */
+  int32_t a_policy, b_policy;                      /* GCS_ASSOC_A_*, GCS_ASSOC_B_* */
+  double eps_mass;                                 /* AssociationConfig.eps_mass: marginals, b rows, ESS */
+  double eps_lift, eps_mass_dir;                   /* operator arguments eps_lift / eps_mass: measurement
+                                                      means and directions (:296-297) */
+  double h_tile;                                   /* GC_H_TILE = 2.0 */
+  int32_t r_stencil_tiles_xy, r_stencil_tiles_z;   /* 1, 0 */
+  int64_t scan_seq;
+  double recency_decay_lambda;                     /* 0.02 */
+} gcs_assoc_config;
+
+typedef struct {            /* MeasurementBatch (measurement_batch.py:68-135), device pointers */
+  const double* Lambdas;    /* n_total x 9 */
+  const double* thetas;     /* n_total x 3 */
+  const double* etas;       /* n_total x n_lobes x 3 */
+  const double* weights;    /* n_total */
+  const uint8_t* valid_mask;/* n_total */
+  int32_t n_total, n_lobes;
+  int32_t n_valid;          /* n_camera_valid + n_lidar_valid (host count, :272) */
+} gcs_assoc_meas;
+
+typedef struct {            /* AtlasMapView (primitive_map.py:270-300), device pointers */
+  const int64_t* tile_ids;  /* n_tiles, view order */
+  int32_t n_tiles, m_tile_view;     /* view entries = n_tiles x m_tile_view */
+  const double* positions;  /* entries x 3 */
+  const double* directions; /* entries x 3 */
+  const double* kappas;     /* entries */
+  const uint8_t* valid_mask;/* entries */
+  const int64_t* last_supported_scan_seq;  /* entries */
+  const int64_t* candidate_tile_ids;       /* entries */
+  const int32_t* candidate_slots;          /* entries */
+} gcs_assoc_view;
+
+typedef struct {            /* PrimitiveAssociationResult (:71-92): device pointers, n_total x k_assoc */
+  double* responsibilities; /* required */
+  int32_t* candidate_pool_indices;  /* may be NULL */
+  int64_t* candidate_tile_ids;      /* may be NULL */
+  int64_t* candidate_slots;         /* may be NULL */
+  double* row_masses;       /* n_total, required */
+  double* cost_matrix;      /* required */
+  /* host results */
+  double cert[GCS_ASSOC_CERT_LEN];
+  int32_t exact;            /* 1: the empty case (no valid measurement or map entry, :272-287) */
+  int32_t n_map_valid;
+} gcs_assoc_outputs;
+
+int gcs_assoc_config_defaults(gcs_assoc_config* cfg);
+int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int32_t device, gcs_assoc_ctx** out);
+int gcs_assoc_ctx_destroy(gcs_assoc_ctx* ctx);
+const char* gcs_assoc_last_error(const gcs_assoc_ctx* ctx);
+/* stream: a hipStream_t (NULL = the context's own); work on it is ordered after the caller's */
+int gcs_assoc_ctx_set_stream(gcs_assoc_ctx* ctx, void* stream);
+/* Synchronises; unsupported policies return GCS_ERR_ARG with the reference's message. */
+int gcs_associate_primitives_ot(gcs_assoc_ctx* ctx, const gcs_assoc_config* cfg, const gcs_assoc_meas* meas,
+                                const gcs_assoc_view* view, gcs_assoc_outputs* out);
 
 #ifdef __cplusplus
 }
