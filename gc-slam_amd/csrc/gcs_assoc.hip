@@ -13,7 +13,7 @@
 //                  cost alone (:376) -- per-thread sorted lists merged by k rounds of a block argmin;
 //                  then per candidate the unmasked cost + recency, row-min subtraction, addressing
 //                  (:377-403)
-//   k_as_sinkhorn  one 1024-thread workgroup: marginals a (policy) and b (uniform), the optional median
+//   k_as_sinkhorn  one 512-thread workgroup: marginals a (policy) and b (uniform), the optional median
 //                  scaling, k_sinkhorn fixed unbalanced iterations (:105-138) with the K_mat rows in
 //                  registers and the column sums in a fixed tree, pi, row masses, responsibilities and
 //                  the OTCert / Support / Influence scalars (:465-551) -- the p95 order statistics by an
@@ -33,7 +33,8 @@ namespace gcs {
 namespace {
 
 constexpr int kAsThreads = 256;
-constexpr int kShThreads = 1024;
+constexpr int kShThreads = 512;  // 2 waves per SIMD: up to 256 VGPRs for both K_mat copies, no spills
+constexpr int kShCR = 32;        // rows per lane in the Sinkhorn column sums: N <= kShCR * 512 / KM
 constexpr int kMaxStencil = 64;
 constexpr double kLog4Pi = 2.5310242469692907;     // np.log(4.0 * np.pi)
 constexpr double kLog2 = 0.6931471805599453;       // np.log(2.0)
@@ -111,6 +112,12 @@ __device__ __forceinline__ unsigned long long order_key(double x) {
   if (isnan(x)) return ~0ULL;
   const unsigned long long b = (unsigned long long)__double_as_longlong(x);
   return (b >> 63) ? ~b : (b | 0x8000000000000000ULL);
+}
+
+// inverse of order_key (the empty key ~0 gives NaN, which compares false)
+__device__ __forceinline__ double key_value(unsigned long long k) {
+  if (k == ~0ULL) return NAN;
+  return __longlong_as_double((long long)((k >> 63) ? (k & 0x7fffffffffffffffULL) : ~k));
 }
 
 __device__ __forceinline__ int64_t pack_tile(int64_t c1, int64_t c2, int64_t cz) {
@@ -245,9 +252,17 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
     for (int q = t; q < P; q += kAsThreads) {
       const int ti = s_tix[s];
       const int e = (ti < 0 ? 0 : ti) * p.m_view + off;
-      double c = kCostInvalid;
-      if (ti >= 0 && in.vvalid[e]) c = pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e, p.beta);
-      list_insert<KM>(key, idx, order_key(c), q);
+      if (ti >= 0 && in.vvalid[e]) {
+        // cost = d_pos + beta d_dir >= d_pos (beta >= 0, d_dir >= 0): an entry whose d_pos alone does
+        // not beat the list's last (and comes later in the pool) cannot enter; skip its vMF term
+        const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
+        const double d_pos = (dx * dx + dy * dy) + dz * dz;
+        if (!(p.beta >= 0.0 && d_pos >= key_value(key[KM - 1])))
+          list_insert<KM>(key, idx, order_key(pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e, p.beta)),
+                          q);
+      } else {
+        list_insert<KM>(key, idx, order_key(kCostInvalid), q);
+      }
       s += ds;
       off += doff;
       if (off >= p.m_view) {
@@ -413,7 +428,9 @@ template <int KM, int RPT>
 __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p, AsWork w, AsOut o, int n_valid_host) {
 #pragma clang fp contract(off)
   __shared__ double s_red[16 * (KM + 8)];
-  __shared__ double s_col[2][16 * KM];
+  __shared__ double s_u[kShThreads * RPT];
+  __shared__ double s_colp[kShThreads / 32];
+  __shared__ double s_v[KM];
   __shared__ uint32_t s_hist[256], s_sel[4];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int N = p.n, K = p.k;
@@ -478,39 +495,56 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const double bk = 1.0 / (double)K;
 #pragma unroll
   for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
+  // column-major copy of K_mat for the column sums: thread t owns column t / TPC and rows
+  // t % TPC + TPC j (the same values: exp of the same cost entries)
+  constexpr int TPC = kShThreads / KM, CR = kShCR;
+  const int kc = t / TPC, cc = t % TPC;
+  __syncthreads();  // the median-scaled costs written back above are visible to every thread
+  double XC[CR];
+#pragma unroll
+  for (int j = 0; j < CR; ++j) {
+    const int r = cc + TPC * j;
+    XC[j] = (r < N && kc < K) ? exp(-o.cost[(size_t)r * K + kc] / eps) : 0.0;
+  }
   double u[RPT], v[KM];
 #pragma unroll
   for (int j = 0; j < RPT; ++j) u[j] = 1.0;
 #pragma unroll
   for (int k = 0; k < KM; ++k) v[k] = 1.0;
+  constexpr int GW = TPC < 64 ? TPC : 64;  // lanes of one column group inside a wave
   for (int it = 0; it < p.iters; ++it) {
-    double cp[KM];
-#pragma unroll
-    for (int k = 0; k < KM; ++k) cp[k] = 0.0;
+    // u = (a / (K v + 1e-12))^ua, one lane per row (K v in column order)
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
+      const int r = t + j * kShThreads;
       double kv = 0.0;
 #pragma unroll
       for (int k = 0; k < KM; ++k) kv += X[j * KM + k] * v[k];
-      u[j] = (t + j * kShThreads < N) ? pow(va[j] / (kv + 1e-12), ua) : 0.0;
+      u[j] = r < N ? pow(va[j] / (kv + 1e-12), ua) : 0.0;
+      if (r < N) s_u[r] = u[j];
+    }
+    __syncthreads();
+    // K^T u: TPC lanes per column, rows in the fixed order cc, cc + TPC, ..., then a fixed xor tree
+    double cs = 0.0;
 #pragma unroll
-      for (int k = 0; k < KM; ++k) cp[k] += X[j * KM + k] * u[j];
+    for (int j = 0; j < CR; ++j) {
+      const int r = cc + TPC * j;
+      cs += XC[j] * (r < N ? s_u[r] : 0.0);
     }
 #pragma unroll
-    for (int sh = 32; sh >= 1; sh >>= 1)
+    for (int sh = GW / 2; sh >= 1; sh >>= 1) cs += __shfl_xor(cs, sh, 64);
+    if ((lane & (GW - 1)) == 0) s_colp[t / GW] = cs;
+    __syncthreads();
+    if (t < K) {  // v = (b / (K^T u + 1e-12))^vb: column t's group partials in order
+      constexpr int G = TPC / GW;
+      double sum = s_colp[t * G];
 #pragma unroll
-      for (int k = 0; k < KM; ++k) cp[k] += __shfl_xor(cp[k], sh, 64);
-    double* col = s_col[it & 1];
-    if (lane == 0)
-#pragma unroll
-      for (int k = 0; k < KM; ++k) col[wid * KM + k] = cp[k];
+      for (int g = 1; g < G; ++g) sum += s_colp[t * G + g];
+      s_v[t] = pow(bk / (sum + 1e-12), vb);
+    }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      double s = col[k];
-      for (int q = 1; q < kShThreads / 64; ++q) s += col[q * KM + k];
-      v[k] = k < K ? pow(bk / (s + 1e-12), vb) : 0.0;
-    }
+    for (int k = 0; k < KM; ++k) v[k] = k < K ? s_v[k] : 0.0;
   }
   // pi, row masses, responsibilities and the cert sums
   // acc: [sum rm, sum rm^2, sum novel, defect_a^2, sum pi C, nonzero_a, sum pi | col masses K]
@@ -622,8 +656,9 @@ int as_fail(gcs_assoc_ctx* c, int code, const std::string& m) {
     if (_e != hipSuccess) return as_fail((ctx), GCS_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e)); \
   } while (0)
 
-// rows per Sinkhorn thread for k_assoc <= KM: the K_mat rows stay in registers
-constexpr int rpt_for(int km) { return km <= 8 ? 2 : 1; }
+// rows per Sinkhorn thread for k_assoc <= KM: the K_mat rows stay in registers (both layouts)
+constexpr int rpt_for(int km) { return km <= 8 ? 4 : (km <= 16 ? 2 : 1); }
+constexpr int max_rows_for(int max_k) { return kShCR * kShThreads / (max_k <= 8 ? 8 : (max_k <= 16 ? 16 : 32)); }
 }  // namespace
 
 extern "C" {
@@ -670,7 +705,7 @@ int gcs_assoc_ctx_destroy(gcs_assoc_ctx* c) {
 int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int32_t device, gcs_assoc_ctx** out) {
   if (!out) return GCS_ERR_ARG;
   *out = nullptr;
-  if (max_meas < 1 || max_pool < 1 || max_k < 1 || max_k > 32 || max_meas > kShThreads * rpt_for(max_k))
+  if (max_meas < 1 || max_pool < 1 || max_k < 1 || max_k > 32 || max_meas > max_rows_for(max_k))
     return GCS_ERR_ARG;
   auto* c = new gcs_assoc_ctx();
   c->device = device;

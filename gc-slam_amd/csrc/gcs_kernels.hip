@@ -867,10 +867,17 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
 #ifndef GCS_BINS_WAVES
 #define GCS_BINS_WAVES 0  // waves per SIMD the register allocation targets (0: compiler default)
 #endif
+#ifndef GCS_BINS_WAVES_SMALL
+// the small-stage instantiation (C3: 25 KiB of LDS, six workgroups per CU by LDS) is register-bound:
+// 5 waves per SIMD needs <= 96 VGPRs (the register allocator spills ~28 dwords to reach it)
+#define GCS_BINS_WAVES_SMALL 0
+#endif
 template <int STAGE, int LANES>
 __global__ __launch_bounds__(kBinTile * LANES)
 #if GCS_BINS_WAVES
 __attribute__((amdgpu_waves_per_eu(GCS_BINS_WAVES)))
+#elif GCS_BINS_WAVES_SMALL
+__attribute__((amdgpu_waves_per_eu(STAGE == kStageSmall ? GCS_BINS_WAVES_SMALL : 1)))
 #endif
 void k_bins_scale(BinKernelArgs a, double* partials) {
   constexpr int NT = kBinTile * LANES, NW = NT / 64;

@@ -338,13 +338,61 @@ GCS_HD __attribute__((always_inline)) bool psd3_deflate(const double* s, double*
   return true;
 }
 
+// eigh3_jacobi with its loops kept rolled (indexed arrays in scratch): the same arithmetic in the
+// same order, but few registers -- an out-of-line callee's register count bounds every kernel that
+// calls it, and the unrolled form took 114 VGPRs, which held the bin kernel at 4 waves per SIMD.
+__host__ __device__ inline __attribute__((noinline)) void eigh3_jacobi_rolled(const double* A, double* w, double* V) {
+  double a[9];
+#pragma clang loop unroll(disable)
+  for (int i = 0; i < 9; ++i) { a[i] = A[i]; V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
+#pragma clang loop unroll(disable)
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    double off = a[1] * a[1] + a[2] * a[2] + a[5] * a[5];
+    double diag = a[0] * a[0] + a[4] * a[4] + a[8] * a[8];
+    if (off <= 1e-40 * diag || off == 0.0) break;
+#pragma clang loop unroll(disable)
+    for (int pq = 0; pq < 3; ++pq) {
+      int p = pq == 2 ? 1 : 0;
+      int q = pq == 0 ? 1 : 2;
+      double apq = a[3 * p + q];
+      if (apq == 0.0) continue;
+      double app = a[4 * p], aqq = a[4 * q];
+      double theta = (aqq - app) / (2.0 * apq);
+      double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+      double c = 1.0 / sqrt(t * t + 1.0);
+      double s = t * c;
+#pragma clang loop unroll(disable)
+      for (int k = 0; k < 3; ++k) {
+        double akp = a[3 * k + p], akq = a[3 * k + q];
+        a[3 * k + p] = c * akp - s * akq;
+        a[3 * k + q] = s * akp + c * akq;
+      }
+#pragma clang loop unroll(disable)
+      for (int k = 0; k < 3; ++k) {
+        double apk = a[3 * p + k], aqk = a[3 * q + k];
+        a[3 * p + k] = c * apk - s * aqk;
+        a[3 * q + k] = s * apk + c * aqk;
+      }
+      a[3 * p + q] = 0.0;
+      a[3 * q + p] = 0.0;
+#pragma clang loop unroll(disable)
+      for (int k = 0; k < 3; ++k) {
+        double vkp = V[3 * k + p], vkq = V[3 * k + q];
+        V[3 * k + p] = c * vkp - s * vkq;
+        V[3 * k + q] = s * vkp + c * vkq;
+      }
+    }
+  }
+  w[0] = a[0]; w[1] = a[4]; w[2] = a[8];
+}
+
 // Jacobi PSD projection of a symmetric s whose top eigenvalue is (near) double, where the
 // deflation cannot pick an eigenvector.  Kept out of line: it is rare (no bin of the benchmark
 // scans takes it) and its indexed arrays live in scratch.
 __host__ __device__ inline __attribute__((noinline)) double psd_project3_slow(const double* s, double* out) {
   GCS_PSD_COUNT(2);
   double w[3], V[9];
-  eigh3_jacobi(s, w, V);
+  eigh3_jacobi_rolled(s, w, V);
   for (int k = 0; k < 3; ++k) w[k] = w[k] > kEpsPsd ? w[k] : kEpsPsd;
   double d2 = 0.0;
   for (int i = 0; i < 3; ++i)

@@ -408,7 +408,7 @@ int gcs_extract_lidar_surfels(gcs_surfel_ctx* ctx, const double* points_dev, con
  * then k_sinkhorn fixed iterations of unbalanced Sinkhorn (:105-138) on one workgroup; the OTCert /
  * SupportCert / InfluenceCert scalars land in cert[] (GCS_ASSOC_CERT_* slots).  An association
  * context owns the workspace for up to max_meas rows, max_pool view entries and k_assoc <= max_k
- * (<= 32; max_meas <= 2048 for max_k <= 8, 1024 above). */
+ * (<= 32; max_meas <= 2048 / 1024 / 512 for max_k <= 8 / 16 / 32). */
 #define GCS_ASSOC_CERT_LEN 18
 enum {
   GCS_ASSOC_CERT_DEFECT_A = 0, GCS_ASSOC_CERT_DEFECT_B, GCS_ASSOC_CERT_MASS_TOTAL, GCS_ASSOC_CERT_SUM_A,

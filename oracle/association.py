@@ -153,6 +153,8 @@ def extract_atlas_map_view(tiles, tile_ids, m_tile_view, eps_lift=GC_EPS_LIFT, e
                              "last_supported_scan_seq", "candidate_slots", "candidate_tile_ids")}
     for tid in tile_ids:
         t = tiles[int(tid)]
+        if t["weights"].shape[0] < k:
+            raise ValueError("m_tile_view exceeds the tile size (the reference's view would be short)")
         score = np.where(t["valid_mask"], t["weights"], -1e30)
         slots = np.argsort(-score, kind="stable")[:k].astype(np.int32)
         for f in ("Lambdas", "thetas", "etas", "weights", "primitive_ids", "valid_mask", "last_supported_scan_seq"):

@@ -29,9 +29,10 @@ def _unit(rng, n):
     return d / np.linalg.norm(d, axis=1, keepdims=True)
 
 
-def make_scene(seed=0, n_feat=512, n_surfel=1024, n_valid_cam=300, n_valid_lidar=900, m_tile=256, m_tile_view=1024,
-               tile_span=2, h=2.0, fill=(0, 256), n_lobes=3, scan_seq=10, missing_tiles=1, dup_tile=False):
+def make_scene(seed=0, n_feat=512, n_surfel=1024, n_valid_cam=300, n_valid_lidar=900, m_tile=1024, m_tile_view=1024,
+               tile_span=2, h=2.0, fill=(0, 700), n_lobes=3, scan_seq=10, missing_tiles=1, dup_tile=False):
     """Returns (batch dict, view dict, tiles dict)."""
+    assert m_tile >= m_tile_view, "a tile view selects m_tile_view of the tile's m_tile slots"
     rng = np.random.default_rng(seed)
     coords = [(a, b, 0) for a in range(-tile_span, tile_span + 1) for b in range(-tile_span, tile_span + 1)]
     tiles = {}

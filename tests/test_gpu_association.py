@@ -99,7 +99,7 @@ def test_association_matches_oracle_reference_sizes(seed):
 
 @pytest.mark.parametrize("variant", ["weight_proportional", "median_no_rowmin", "k16_r2", "dup_tile"])
 def test_association_config_variants(variant):
-    kw = dict(seed=7, n_feat=128, n_surfel=256, n_valid_cam=60, n_valid_lidar=200, m_tile=128, m_tile_view=256)
+    kw = dict(seed=7, n_feat=128, n_surfel=256, n_valid_cam=60, n_valid_lidar=200, m_tile=256, m_tile_view=256)
     cfg = OA.AssociationConfig(scan_seq=4)
     if variant == "weight_proportional":
         cfg.a_policy = "weight_proportional"
@@ -148,7 +148,7 @@ def test_unsupported_policy_raises_unless_empty():
 
 
 def test_association_deterministic():
-    batch, view, _ = make_scene(seed=9, n_feat=128, n_surfel=256, n_valid_cam=60, n_valid_lidar=200, m_tile=128,
+    batch, view, _ = make_scene(seed=9, n_feat=128, n_surfel=256, n_valid_cam=60, n_valid_lidar=200, m_tile=256,
                                 m_tile_view=256)
     b, v = _batch(batch), _view(view)
     r1, _, _ = GA.associate_primitives_ot(b, v)
