@@ -266,6 +266,7 @@ def main():
     device = f"cuda:{local_rank}"
     torch.cuda.set_device(local_rank)
 
+    from gcslam import _lib as L
     from gcslam.distributed import HypothesisComm, combine_allreduce
     from gcslam.synthetic import scan_kwargs
 
@@ -282,6 +283,7 @@ def main():
     scan_kw = [scan_kwargs(sc) for sc, _, _, _ in scans]  # the per-scan host arguments, built once
 
     state = dict(count=0, sample=False, sampled=0)
+    scan_out = L.GcsScanOutputs()  # one output record for every scan (the caller-owned buffer form)
     # pre-device host, device submit+wait, host tail, whole gcs_scan, combine, then the sub-spans
     # (budget launch + predict, device launch calls, tail numerics, pushforward launch calls)
     host_ms = np.zeros(9)
@@ -295,7 +297,7 @@ def main():
                 ctx.enable_timing(False)
         i = state["count"] % N_SCANS
         _, rec, t, w = scans[i]
-        out = ctx.scan(rec, 16, t, w, N, **scan_kw[i])
+        out = ctx.scan(rec, 16, t, w, N, out=scan_out, **scan_kw[i])
         if state["count"] % TIMING_STRIDE == TIMING_STRIDE // 2:  # host sub-spans: sampled scans without event stamps
             tc = time.perf_counter()
             combine_allreduce(ctx, rank, world, state["count"], comm=comm, want_belief=False)

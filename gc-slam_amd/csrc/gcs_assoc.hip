@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <string>
 
+#include "gcs_math.h"
 #include "gcslam_hip.h"
 
 namespace gcs {
@@ -46,7 +47,7 @@ constexpr int64_t kBias = 1LL << 20;               // tiling.py:81
 constexpr int64_t kMask = (1LL << kBitsPerAxis) - 1;
 
 struct AsParams {
-  int n, m_view, n_tiles, n_stencil, k, iters, m_pool;
+  int n, m_view, m_shift, n_tiles, n_stencil, k, iters, m_pool;
   int a_policy, row_min, med;
   double beta, eps, tau_a, tau_b, eps_mass, eps_lift, eps_dir, h, lam, eps_lam;
   long long scan_seq;
@@ -247,27 +248,47 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
       idx[j] = 0x7fffffff;
     }
     const int P = p.n_stencil * p.m_view;
-    int s = t / p.m_view, off = t % p.m_view;
-    const int ds = kAsThreads / p.m_view, doff = kAsThreads % p.m_view;
-    for (int q = t; q < P; q += kAsThreads) {
-      const int ti = s_tix[s];
-      const int e = (ti < 0 ? 0 : ti) * p.m_view + off;
-      if (ti >= 0 && in.vvalid[e]) {
-        // cost = d_pos + beta d_dir >= d_pos (beta >= 0, d_dir >= 0): an entry whose d_pos alone does
-        // not beat the list's last (and comes later in the pool) cannot enter; skip its vMF term
-        const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
-        const double d_pos = (dx * dx + dy * dy) + dz * dz;
-        if (!(p.beta >= 0.0 && d_pos >= key_value(key[KM - 1])))
-          list_insert<KM>(key, idx, order_key(pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e, p.beta)),
-                          q);
-      } else {
-        list_insert<KM>(key, idx, order_key(kCostInvalid), q);
+    const bool prune = p.beta >= 0.0;
+    // four pool entries per trip, in increasing pool position: their table loads issue together
+    constexpr int PB = 4;
+    for (int q0 = t; q0 < P; q0 += PB * kAsThreads) {
+      int e[PB];
+      bool ok[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int q = q0 + u * kAsThreads;
+        // stencil tile and offset of pool position q (shift / mask when m_tile_view is a power of two)
+        const int sq = p.m_shift >= 0 ? (q >> p.m_shift) : q / p.m_view;
+        const int oq = q - sq * p.m_view;
+        const int ti = q < P ? s_tix[sq] : -1;
+        e[u] = (ti < 0 ? 0 : ti) * p.m_view + (q < P ? oq : 0);
+        ok[u] = ti >= 0;
       }
-      s += ds;
-      off += doff;
-      if (off >= p.m_view) {
-        off -= p.m_view;
-        ++s;
+      uint8_t vv[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) vv[u] = ok[u] ? in.vvalid[e[u]] : (uint8_t)0;
+      double px[PB], py[PB], pz[PB];
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        px[u] = in.vpos[3 * e[u]];
+        py[u] = in.vpos[3 * e[u] + 1];
+        pz[u] = in.vpos[3 * e[u] + 2];
+      }
+#pragma unroll
+      for (int u = 0; u < PB; ++u) {
+        const int q = q0 + u * kAsThreads;
+        if (q >= P) break;
+        if (ok[u] && vv[u]) {
+          // cost = d_pos + beta d_dir >= d_pos (beta >= 0, d_dir >= 0): an entry whose d_pos alone does
+          // not beat the list's last (and comes later in the pool) cannot enter; skip its vMF term
+          const double dx = mp[0] - px[u], dy = mp[1] - py[u], dz = mp[2] - pz[u];
+          const double d_pos = (dx * dx + dy * dy) + dz * dz;
+          if (!(prune && d_pos >= key_value(key[KM - 1])))
+            list_insert<KM>(key, idx,
+                            order_key(pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e[u], p.beta)), q);
+        } else {
+          list_insert<KM>(key, idx, order_key(kCostInvalid), q);
+        }
       }
     }
     // k rounds of a block argmin over the lists' heads; the winner's owner pops its head
@@ -520,7 +541,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
       double kv = 0.0;
 #pragma unroll
       for (int k = 0; k < KM; ++k) kv += X[j * KM + k] * v[k];
-      u[j] = r < N ? pow(va[j] / (kv + 1e-12), ua) : 0.0;
+      u[j] = r < N ? pow_sinkhorn(va[j] / (kv + 1e-12), ua) : 0.0;
       if (r < N) s_u[r] = u[j];
     }
     __syncthreads();
@@ -540,7 +561,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
       double sum = s_colp[t * G];
 #pragma unroll
       for (int g = 1; g < G; ++g) sum += s_colp[t * G + g];
-      s_v[t] = pow(bk / (sum + 1e-12), vb);
+      s_v[t] = pow_sinkhorn(bk / (sum + 1e-12), vb);
     }
     __syncthreads();
 #pragma unroll
@@ -663,6 +684,16 @@ constexpr int max_rows_for(int max_k) { return kShCR * kShThreads / (max_k <= 8 
 
 extern "C" {
 
+int gcs_debug_short_log_exp(const double* x, int32_t n, double y, double* log_out, double* exp_out, double* pow_out) {
+  if (n < 0 || (n > 0 && (!x || !log_out || !exp_out || !pow_out))) return GCS_ERR_ARG;
+  for (int i = 0; i < n; ++i) {
+    log_out[i] = x[i] > 0.0 ? gcs::log_short(x[i]) : NAN;
+    exp_out[i] = fabs(x[i]) < 700.0 ? gcs::exp_short(x[i]) : NAN;
+    pow_out[i] = gcs::pow_sinkhorn(x[i], y);
+  }
+  return GCS_OK;
+}
+
 int gcs_assoc_config_defaults(gcs_assoc_config* c) {
   if (!c) return GCS_ERR_ARG;
   memset(c, 0, sizeof(*c));
@@ -777,6 +808,9 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   AsParams p{};
   p.n = m->n_total;
   p.m_view = v->m_tile_view;
+  p.m_shift = -1;
+  for (int b = 0; b < 31; ++b)
+    if ((1 << b) == p.m_view) p.m_shift = b;
   p.n_tiles = v->n_tiles;
   p.n_stencil = ns;
   p.k = K;

@@ -96,10 +96,13 @@ struct gcs_ctx {
   std::mutex push_mu;
   std::condition_variable push_cv;
   struct PushJob {
+    int kind;  // 0: the scan's pushforward, 1: the next scan's k_budget (row 1 mass sums)
     double z_t[6], Sig6[36], gamma;
     hipStream_t s;
     double* partials;
     uint8_t* flags;
+    BudgetArgs ba;
+    int nblk;
   } push_job{};
   int push_rc = 0;
   std::string push_err;
@@ -112,6 +115,15 @@ struct gcs_ctx {
   // degenerate-bucket compaction taken.  Debug knobs (gcs_ctx_set_debug).
   uint32_t* h_err = nullptr;
   uint32_t* d_err = nullptr;
+  // direct buckets (gcs_scan, scale mode): k_points writes each bucket's members into a fixed row of
+  // capb slots and marks the active bins itself; the bin kernel ranks them while staging, so the
+  // sorted bucketing (k_scan, k_place, k_bucket_rank) is skipped.  A bucket past capb members sets
+  // h_err[2]: that scan is redone with the sorted bucketing, and so are the context's later scans.
+  uint32_t* d_members = nullptr;
+  int capb = 32, capb_eff = 32;
+  bool direct_buckets = true;   // GCSLAM_SORTED_BUCKETS=1 / GCS_DEBUG_SORTED_BUCKETS: always sorted
+  bool sorted_sticky = false;   // a bucket overflowed: sorted bucketing from now on
+  bool use_direct = false;      // the stages of the current gcs_scan call
   uint32_t spin_limit = 1u << 22;
   int inject_scan_fail = 0;
   // hypothesis all-reduce payload (gcs_combine_allreduce): pinned host staging + device buffer
@@ -296,18 +308,20 @@ int upload_atlas(gcs_ctx* c) {
   return GCS_OK;
 }
 
+int submit_budget(gcs_ctx* c, const BudgetArgs& ba, int nblk, hipStream_t s);
+
 // ---------------------------------------------------------------- device stages
 // fold_later: leave k_points' cert fold to block 0 of the next k_bins_scale (scale-mode scan)
 // Row 1's mass sums (k_budget) need only the weights: gcs_scan queues them before its host
 // prologue so they run while the host predicts and preintegrates.  e0: stage timing start (may be null).
-int stage_budget(gcs_ctx* c, const double* w, int n_raw, hipEvent_t e0) {
+int stage_budget(gcs_ctx* c, const double* w, int n_raw, hipEvent_t e0, bool toggle = true) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
   int stride = std::max(1, (int)((n_raw + (long)c->cap - 1) / c->cap));  // ceil(N/cap), point_budget.py:160
   int n_sel = (n_raw + stride - 1) / stride;
   c->last_n_sel = n_sel;
   c->last_stride = stride;
   hipStream_t s = c->stream;
-  if (c->d_flags_buf[0]) {  // this scan's flag buffer (the other may still be read by k_pushforward)
+  if (c->d_flags_buf[0] && toggle) {  // this scan's flag buffer (the other may still be read by k_pushforward)
     c->flags_cur ^= 1;
     c->d_flags = c->d_flags_buf[c->flags_cur];
   }
@@ -322,8 +336,9 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, hipEvent_t e0) {
   ba.zero8 = c->d_flags;
   ba.n_zero8 = c->d_flags ? c->B + bins_scale_blocks(c->B) : 0;
   c->budget_blocks = red_blocks(std::max(n_raw, 1));
-  HIPCHK(c, launch_budget(ba, c->budget_blocks, s, e0, nullptr));
   c->budget_pending = true;
+  if (!e0 && c->push_async) return submit_budget(c, ba, c->budget_blocks, s);
+  HIPCHK(c, launch_budget(ba, c->budget_blocks, s, e0, nullptr));
   return GCS_OK;
 }
 
@@ -337,6 +352,7 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   const bool hoisted = c->budget_pending;  // k_budget queued earlier by gcs_scan: the stage starts at k_points
   if (!hoisted)
     if (int rc = stage_budget(c, w, n_raw, ev.e0)) return rc;
+  if (int rc = push_wait(c)) return rc;  // k_budget's launch call (worker) precedes k_points on the stream
   c->budget_pending = false;
   const int n_sel = c->last_n_sel, stride = c->last_stride;
   hipStream_t s = c->stream;
@@ -366,6 +382,12 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.keys = c->d_keys;
   a.slots = c->d_slots;
   a.counts = c->d_counts;
+  if (c->use_direct) {
+    a.members = c->d_members;
+    a.capb = c->capb_eff;
+    a.flags = c->d_flags;
+    a.overflow = c->d_err + 2;
+  }
   a.budget_partials = c->d_partials;
   a.budget_blocks = c->budget_blocks;
   a.scalars = c->d_scalars;
@@ -385,6 +407,10 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   BinKernelArgs b{};
   b.recs = c->d_recs;
   b.perm = c->d_perm;
+  if (c->use_direct) {
+    b.members = c->d_members;
+    b.capb = c->capb_eff;
+  }
   b.starts = c->d_starts;
   b.counts = c->d_counts;
   b.flags = c->d_flags;
@@ -417,7 +443,7 @@ int stage_bins(gcs_ctx* c) {
   hipStream_t s = c->stream;
   BinKernelArgs b = bin_args(c);
   if (c->cfg.mode == GCS_MODE_SCALE) {
-    {
+    if (!c->use_direct) {  // sorted bucketing (direct buckets: k_points placed and flagged them)
       StageEv ev = stage_ev(c, ST_SORT);
       BucketArgs ba{};
       ba.n_bins = c->B;
@@ -520,7 +546,13 @@ void push_worker(gcs_ctx* c) {
     seen = r;
     const gcs_ctx::PushJob& j = c->push_job;
     int rc = GCS_OK;
-    {
+    if (j.kind == 1) {
+      const hipError_t e = launch_budget(j.ba, j.nblk, j.s, nullptr, nullptr);
+      if (e != hipSuccess) {
+        rc = GCS_ERR_HIP;
+        c->push_err = "k_budget launch (worker): " + std::string(hipGetErrorString(e));
+      }
+    } else {
       rc = stage_push(c, j.z_t, j.Sig6, j.gamma, j.s, j.partials, j.flags, true);
       if (rc) c->push_err = "pushforward launch (worker): " + std::string(hipGetErrorString(hipGetLastError()));
     }
@@ -540,12 +572,32 @@ int submit_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma,
   if (int rc = push_wait(c)) return rc;  // the previous job is launched: its slot is free
   if (!c->push_thread.joinable()) c->push_thread = std::thread(push_worker, c);
   gcs_ctx::PushJob& j = c->push_job;
+  j.kind = 0;
   memcpy(j.z_t, z_t, sizeof(j.z_t));
   memcpy(j.Sig6, Sig6, sizeof(j.Sig6));
   j.gamma = gamma;
   j.s = s;
   j.partials = partials;
   j.flags = c->d_flags;
+  c->push_req.fetch_add(1);
+  if (c->push_sleeping.load()) {
+    std::lock_guard<std::mutex> lk(c->push_mu);
+    c->push_cv.notify_one();
+  }
+  return GCS_OK;
+}
+
+// k_budget's launch call on the worker too (gcs_scan queues it before its host prologue): the main
+// thread goes straight to PredictDiffusion; stage_points waits for the worker (push_wait) before it
+// queues k_points behind it on the same stream, so the device order is the synchronous one.
+int submit_budget(gcs_ctx* c, const BudgetArgs& ba, int nblk, hipStream_t s) {
+  if (int rc = push_wait(c)) return rc;  // the previous job (the last scan's pushforward) is launched
+  if (!c->push_thread.joinable()) c->push_thread = std::thread(push_worker, c);
+  gcs_ctx::PushJob& j = c->push_job;
+  j.kind = 1;
+  j.ba = ba;
+  j.nblk = nblk;
+  j.s = s;
   c->push_req.fetch_add(1);
   if (c->push_sleeping.load()) {
     std::lock_guard<std::mutex> lk(c->push_mu);
@@ -670,6 +722,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipEventCreateWithFlags(&c->ev_push, hipEventDisableTiming))) return GCS_ERR_HIP;
   if (const char* pm = getenv("GCSLAM_PUSH_MAIN")) c->push_main = atoi(pm) != 0;
   if (const char* pt = getenv("GCSLAM_PUSH_THREAD")) c->push_async = atoi(pt) != 0;
+  if (const char* sb = getenv("GCSLAM_SORTED_BUCKETS")) c->direct_buckets = atoi(sb) == 0;
   const size_t B = c->B, cap = c->cap;
   if (bad(hipMalloc(&c->d_bin_dirs, B * 4 * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_recs, cap * sizeof(PointRec)))) return GCS_ERR_HIP;
@@ -692,8 +745,8 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMemset(c->d_tickets, 0, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocMapped))) return GCS_ERR_HIP;
   if (bad(hipHostGetDevicePointer((void**)&c->d_scalars_mirror, c->h_scalars, 0))) return GCS_ERR_HIP;
-  if (bad(hipHostMalloc(&c->h_err, 2 * sizeof(uint32_t), hipHostMallocMapped))) return GCS_ERR_HIP;
-  c->h_err[0] = c->h_err[1] = 0u;
+  if (bad(hipHostMalloc(&c->h_err, 4 * sizeof(uint32_t), hipHostMallocMapped))) return GCS_ERR_HIP;
+  c->h_err[0] = c->h_err[1] = c->h_err[2] = c->h_err[3] = 0u;
   if (bad(hipHostGetDevicePointer((void**)&c->d_err, c->h_err, 0))) return GCS_ERR_HIP;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
@@ -707,6 +760,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMemset(c->d_counts, 0, (size_t)c->n_counts_words * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_starts, B * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_perm, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_members, B * (size_t)c->capb * sizeof(uint32_t)))) return GCS_ERR_HIP;
     // zeroed so every slot holds a valid point index even when a failed scan leaves holes
     if (bad(hipMemset(c->d_perm, 0, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMemset(c->d_sorted, 0, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
@@ -758,7 +812,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   }
   if (c->push_stream) (void)hipStreamSynchronize(c->push_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
+  void* ptrs[] = {c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_bins_part, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,
@@ -801,6 +855,14 @@ int gcs_ctx_synchronize(gcs_ctx* c) {
 int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
   if (!c) return GCS_ERR_ARG;
   switch (key) {
+    case GCS_DEBUG_SORTED_BUCKETS:
+      c->direct_buckets = value == 0;
+      return GCS_OK;
+    case GCS_DEBUG_BUCKET_CAPACITY:
+      if (value < 4 || value > c->capb || (value & 3)) return fail(c, GCS_ERR_ARG, "bucket capacity: a multiple of 4 in [4, 32]");
+      c->capb_eff = (int)value;
+      c->sorted_sticky = false;
+      return GCS_OK;
     case GCS_DEBUG_SCAN_SPIN_LIMIT:
       if (value < 0 || value > 0xffffffffLL) return fail(c, GCS_ERR_ARG, "spin limit out of range");
       c->spin_limit = (uint32_t)value;
@@ -1104,6 +1166,12 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   if (in->imu_len < 1 || !in->imu_stamps || !in->imu_gyro || !in->imu_accel) return fail(c, GCS_ERR_ARG, "IMU window required");
   auto T0 = clk::now();
   c->budget_pending = false;
+  // direct buckets for this call's stages (scale mode, unless a bucket overflowed before)
+  c->use_direct = c->cfg.mode == GCS_MODE_SCALE && c->direct_buckets && !c->sorted_sticky && c->d_members;
+  struct DirectOff {
+    gcs_ctx* c;
+    ~DirectOff() { c->use_direct = false; }  // per-operator entry points always take the sorted path
+  } direct_off{c};
   if (int rc0 = stage_budget(c, in->weights_dev, in->n_points, nullptr)) return rc0;  // runs during the prologue
   const double* Q = in->Q ? in->Q : c->Q;
   double* cert = out->cert;
@@ -1192,6 +1260,24 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));  // the PT fold has written the scalars to h_scalars
   if ((rc = check_bucket_err(c))) return rc;
+  bool redone = false;
+  if (c->use_direct && c->h_err[2]) {
+    // a bucket exceeded the direct rows: redo the device stages with the sorted bucketing (same
+    // flags buffer: the previous scan's pushforward may still read the other), and keep it
+    c->h_err[2] = 0u;
+    c->sorted_sticky = true;
+    c->use_direct = false;
+    redone = true;
+    if ((rc = stage_budget(c, in->weights_dev, in->n_points, nullptr, /*toggle=*/false))) return rc;
+    if ((rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
+                           in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, true,
+                           in->xyz_format == 1)))
+      return rc;
+    if ((rc = stage_bins(c))) return rc;
+    if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((rc = check_bucket_err(c))) return rc;
+  }
   cert[41] = c->h_err[1] ? 1.0 : 0.0;  // a bucket above the ranking capacity took the compaction path
   c->h_err[1] = 0u;
   for (int k = 0; k < 27; ++k)
@@ -1369,6 +1455,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   cert[54] = c->io.mean_reliability;
   cert[55] = nll_total;
   cert[56] = io_extra[4];            // omega_avg z
+  cert[57] = redone ? 1.0 : 0.0;     // a bucket overflowed the direct rows: redone sorted
   // 11 InfoFusionAdditive (fusion.py:186-191)
   Belief post = pred;
   double Lsum[DZ * DZ];

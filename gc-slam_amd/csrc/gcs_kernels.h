@@ -59,6 +59,13 @@ struct PointKernelArgs {
   uint32_t* keys;
   uint32_t* slots;
   uint32_t* counts;  // per-bin bucket sizes (cleared by k_budget)
+  // direct buckets (scale mode, gcs_scan): members[b * capb + slot] = point index for slot < capb;
+  // the first arrival of a bucket marks its K candidate bins and their tiles active (flags); a slot
+  // >= capb sets *overflow (host-mapped) and the scan is redone with the sorted bucketing
+  uint32_t* members;
+  int capb;
+  uint8_t* flags;
+  uint32_t* overflow;
   const double* budget_partials;  // k_budget block partials (folded by every k_points block)
   int budget_blocks;
   double* scalars;
@@ -91,7 +98,9 @@ struct BucketArgs {
 
 struct BinKernelArgs {
   const PointRec* recs;   // point order
-  const uint32_t* perm;   // bucket order -> point index (scale mode)
+  const uint32_t* perm;   // bucket order -> point index (scale mode, sorted bucketing)
+  const uint32_t* members;  // direct buckets (k_points): bucket b's members at b * capb, arrival order
+  int capb;
   const uint32_t* starts;
   const uint32_t* counts;
   const uint8_t* flags;

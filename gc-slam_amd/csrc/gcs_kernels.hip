@@ -127,14 +127,18 @@ __device__ __forceinline__ void reduce_partials(const double* __restrict__ parti
 #pragma unroll
     for (int k = 0; k < 4; ++k) lds[wid * S + c0 + k] = a[k];
   __syncthreads();
-  if (threadIdx.x == 0) {
+  // the cross-wave fold: lane k of wave 0 folds component k over the waves in order (the serial
+  // fold by thread 0 was NV x waves dependent LDS reads: the tail of a 1024-thread fold)
+  double s = 0.0;
+  if (threadIdx.x < NV) {
+    const int k = threadIdx.x;
+    const bool mx = (MAXMASK >> k) & 1u;
+    s = lds[k];
+    for (int w = 1; w < NT / 64; ++w) s = mx ? fmax(s, lds[w * S + k]) : s + lds[w * S + k];
+  }
+  if (threadIdx.x < 64) {
 #pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const bool mx = (MAXMASK >> k) & 1u;
-      double s = lds[k];
-      for (int w = 1; w < NT / 64; ++w) s = mx ? fmax(s, lds[w * S + k]) : s + lds[w * S + k];
-      v[k] = s;
-    }
+    for (int k = 0; k < NV; ++k) v[k] = __shfl(s, k, 64);
   }
   __syncthreads();
 }
@@ -407,9 +411,25 @@ void k_points(PointKernelArgs a, double* partials) {
       H = log(Z) - sxe * iz - kEpsMass * corr;
       uint32_t key = (uint32_t)a.n_bins;
       if (valid && sub == 0) {
-        // bucket slot: arrival order only (re-ranked by point index in k_bucket_build)
-        a.slots[i] = atomicAdd(a.counts + nearest, 1u);
+        // bucket slot: arrival order only (re-ranked by point index by k_bucket_rank, or by the bin
+        // kernel's staging for the direct buckets)
+        const uint32_t sl = atomicAdd(a.counts + nearest, 1u);
+        a.slots[i] = sl;
         key = (uint32_t)nearest;
+        if (a.members) {
+          if (sl < (uint32_t)a.capb) a.members[(size_t)nearest * a.capb + sl] = (uint32_t)i;
+          else *a.overflow = 1u;  // vector store to host-mapped memory; gcs_scan redoes the scan sorted
+          if (sl == 0u) {  // the bucket's first arrival marks its candidate bins and their tiles
+            const int* kr = a.knn + (size_t)nearest * a.k;
+            uint8_t* tf = a.flags + a.n_bins;
+#pragma unroll
+            for (int q = 0; q < KC; q += 4) {
+              const int4 c4 = *(const int4*)(kr + q);
+              a.flags[c4.x] = 1; a.flags[c4.y] = 1; a.flags[c4.z] = 1; a.flags[c4.w] = 1;
+              tf[c4.x / kBinTile] = 1; tf[c4.y / kBinTile] = 1; tf[c4.z / kBinTile] = 1; tf[c4.w / kBinTile] = 1;
+            }
+          }
+        }
       }
       if (live && sub == 0) a.keys[i] = key;
       Z = iz;
@@ -976,7 +996,9 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #pragma unroll
     for (int k = 0; k < SR; ++k) {
       cn[k] = t + k * NT < ns ? a.counts[src[k]] : 0u;
-      st[k] = t + k * NT < ns ? a.starts[src[k]] : 0u;
+      if (a.members) cn[k] = min(cn[k], (uint32_t)a.capb);  // an overflowing scan is redone (rows in bounds)
+      // sorted bucketing: the bucket's start in perm; direct buckets: its member row
+      st[k] = t + k * NT < ns ? (a.members ? (uint32_t)src[k] * (uint32_t)a.capb : a.starts[src[k]]) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < RL; ++k)
@@ -1101,18 +1123,35 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     // at most RPT records per thread: every perm load is issued before any record load, so a
     // tile with more records than threads still pays two dependent round trips, not 2 x RPT
     constexpr int RPT = (STAGE + NT - 1) / NT;
-    uint32_t pi[RPT];
+    uint32_t pi[RPT], dst[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint32_t r = t + k * NT;
       pi[k] = 0u;
+      dst[k] = r;
       if (r < total) {
         int lo = 0, hi = ns - 1;
         while (lo < hi) {
           int mid = (lo + hi + 1) >> 1;
           if (s_off[mid] <= r) lo = mid; else hi = mid - 1;
         }
-        pi[k] = a.perm[s_st[lo] + (r - s_off[lo])];
+        const uint32_t pos = s_st[lo] + (r - s_off[lo]);
+        if (a.members) {
+          // direct buckets hold arrival order: the record's slot is its source's offset + the rank
+          // of its point index among the source's members (the sorted bucketing's order, bit for bit)
+          const uint32_t c = s_cnt[lo];
+          const uint4* row = (const uint4*)(a.members + s_st[lo]);
+          const uint32_t me = a.members[pos];
+          uint32_t rank = 0;
+          for (uint32_t q = 0; q < c; q += 4) {
+            const uint4 m4 = row[q >> 2];
+            rank += (m4.x < me) + (q + 1 < c && m4.y < me) + (q + 2 < c && m4.z < me) + (q + 3 < c && m4.w < me);
+          }
+          pi[k] = me;
+          dst[k] = s_off[lo] + rank;
+        } else {
+          pi[k] = a.perm[pos];
+        }
       }
     }
     PointRec pr[RPT];
@@ -1121,8 +1160,8 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       if (t + k * NT < total) pr[k] = a.recs[pi[k]];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
-      const uint32_t r = t + k * NT;
-      if (r < total) {
+      const uint32_t r = dst[k];
+      if (t + k * NT < total) {
         double2* d = (double2*)(s_rec + (size_t)r * kRecD);
         const uint32_t sw = rec_swz(r);
         d[0 ^ sw] = make_double2(pr[k].x, pr[k].y);
@@ -1250,7 +1289,20 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       }
     } else {
       for (uint32_t i = i0; i < i1; ++i) {
-        const PointRec pr = a.recs[a.perm[s_st[j] + kk]];
+        uint32_t pidx;
+        if (a.members) {  // the kk-th smallest member (a tile over its stage: rare)
+          const uint32_t* row = a.members + s_st[j];
+          pidx = row[0];
+          for (uint32_t q = 0; q < c; ++q) {
+            const uint32_t m = row[q];
+            uint32_t rk = 0;
+            for (uint32_t q2 = 0; q2 < c; ++q2) rk += row[q2] < m ? 1u : 0u;
+            if (rk == kk) pidx = m;
+          }
+        } else {
+          pidx = a.perm[s_st[j] + kk];
+        }
+        const PointRec pr = a.recs[pidx];
         bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, pr.dx, pr.dy, pr.dz, pr.m, pr.w * pr.iz);
         if (++kk == c && i + 1 < i1) {  // next source (compacted: non-empty)
           kk = 0;
@@ -1683,7 +1735,10 @@ __global__ __launch_bounds__(NT) void k_final(const double* __restrict__ partial
 // bin kernel at C3 took 30 us; with a first level on 128 CUs the one-block tail folds 128 rows.
 constexpr int kFoldRows = 64;
 constexpr int kFoldDirect = 2048;  // up to this many rows a single block folds directly (C2 bins: 1563)
-// (a 1024-thread direct fold measured slower: C2 bins fold 8.1 -> 10.1 us, the 391-row folds +0.3-0.7 us)
+#ifndef GCS_FINAL_WIDE
+#define GCS_FINAL_WIDE 1024  // threads of a direct fold over more than kFinalWideRows rows (kBlock: off)
+#endif
+constexpr int kFinalWide = GCS_FINAL_WIDE, kFinalWideRows = 512;
 template <int NV, unsigned MAXMASK>
 __global__ __launch_bounds__(kBlock) void k_fold(const double* __restrict__ partials, int nblocks, double* out) {
   __shared__ double lds[kWaves * pstride<NV>()];
@@ -1703,6 +1758,9 @@ void launch_fold(const double* partials, int nblk, hipStream_t s, hipEvent_t e1,
     hipExtLaunchKernelGGL(k_fold<NV, MAXMASK>, dim3(g), dim3(kBlock), 0, s, nullptr, nullptr, 0, partials, nblk, lvl);
     hipExtLaunchKernelGGL(k_final<NV, MAXMASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0,
                           (const double*)lvl, g, scalars, mirror);
+  } else if (kFinalWide != kBlock && nblk > kFinalWideRows) {  // C2 bins: 1563 rows in one or two round trips
+    hipExtLaunchKernelGGL((k_final<NV, MAXMASK, KIND, kFinalWide>), dim3(1), dim3(kFinalWide), 0, s, nullptr, e1, 0,
+                          partials, nblk, scalars, mirror);
   } else {
     hipExtLaunchKernelGGL(k_final<NV, MAXMASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0, partials, nblk,
                           scalars, mirror);

@@ -610,4 +610,58 @@ GCS_HD void mf_rotation(const double* H, double* R) {
   for (int k = 0; k < 9; ++k) R[k] = X[k];
 }
 
+// ---------------------------------------------------------------------------- short log / exp
+// f64 log and exp for finite arguments in the Sinkhorn scalings' range (the classic
+// reduction + minimax polynomials of the 4.4BSD / fdlibm e_log.c and e_exp.c, < 1 ulp): about a
+// third of the library's instruction count (its log carries double-double steps), which is what a
+// one-workgroup Sinkhorn iteration spends its time on.  No contraction: host and device round alike.
+GCS_HD double log_short(double x) {  // x > 0, finite, normal
+#pragma clang fp contract(off)
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01, Lg3 = 2.857142874366239149e-01,
+               Lg4 = 2.222219843214978396e-01, Lg5 = 1.818357216161805012e-01, Lg6 = 1.531383769920937332e-01,
+               Lg7 = 1.479819860511658591e-01;
+  int e;
+  double m = frexp(x, &e);  // [0.5, 1)
+  if (m < 0.70710678118654752440) {
+    m = m * 2.0;
+    e -= 1;
+  }
+  const double f = m - 1.0;
+  const double hfsq = 0.5 * f * f;
+  const double s = f / (2.0 + f);
+  const double dk = (double)e;
+  const double z = s * s, w = z * z;
+  const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
+  const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+  const double R = t2 + t1;
+  return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+}
+
+GCS_HD double exp_short(double x) {  // |x| < 700
+#pragma clang fp contract(off)
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
+               invln2 = 1.44269504088896338700e+00;
+  const double P1 = 1.66666666666666019037e-01, P2 = -2.77777777770155933842e-03, P3 = 6.61375632143793436117e-05,
+               P4 = -1.65339022054652515390e-06, P5 = 4.13813679705723846039e-08;
+  const int k = (int)(invln2 * x + (x < 0.0 ? -0.5 : 0.5));
+  const double t = (double)k;
+  const double hi = x - t * ln2_hi, lo = t * ln2_lo;
+  const double r = hi - lo;
+  const double rr = r * r;
+  const double c = r - rr * (P1 + rr * (P2 + rr * (P3 + rr * (P4 + rr * P5))));
+  const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
+  return ldexp(y, k);
+}
+
+// x^y for the Sinkhorn scalings: 0 at x = 0, exp_short(y log_short(x)) for positive finite normal
+// x and |y log x| < 700, the library pow otherwise (a few ulps from pow: |y log x| < ~40 here)
+GCS_HD double pow_sinkhorn(double x, double y) {
+  if (x == 0.0) return 0.0;
+  if (!(x >= 2.2250738585072014e-308) || !(x <= 1.7976931348623157e308)) return pow(x, y);
+  const double a = y * log_short(x);
+  if (!(fabs(a) < 700.0)) return pow(x, y);
+  return exp_short(a);
+}
+
 }  // namespace gcs

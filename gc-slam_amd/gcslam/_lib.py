@@ -84,6 +84,7 @@ class GcsImuOdomInputs(C.Structure):
 IMU_ODOM_CERT_LEN = 15
 RCCL_ID_BYTES = 128
 DEBUG_SCAN_SPIN_LIMIT, DEBUG_INJECT_SCAN_FAIL = 1, 2
+DEBUG_SORTED_BUCKETS, DEBUG_BUCKET_CAPACITY = 3, 4
 
 
 # (name, restype, argtypes) for every symbol declared in include/gcslam_hip.h
@@ -215,6 +216,7 @@ _SIGS = [
     ("gcs_extract_lidar_surfels", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32,
                                             C.POINTER(GcsSurfelOutputs)]),
     ("gcs_assoc_config_defaults", C.c_int, [C.POINTER(GcsAssocConfig)]),
+    ("gcs_debug_short_log_exp", C.c_int, [c_double_p, C.c_int32, C.c_double, c_double_p, c_double_p, c_double_p]),
     ("gcs_assoc_ctx_create", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     ("gcs_assoc_ctx_destroy", C.c_int, [C.c_void_p]),
     ("gcs_assoc_last_error", C.c_char_p, [C.c_void_p]),

@@ -246,12 +246,13 @@ class HypothesisContext:
     def scan(self, xyz_dev, point_step, t_dev, w_dev, n_points, imu_stamps, imu_gyro, imu_accel,
              scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None, t_last_scan=None, t_scan=None,
              xyz_f64=False, odom_pose=None, odom_cov_se3=None, odom_twist=None, odom_twist_cov=None, Sigma_g=None,
-             Sigma_a=None):
+             Sigma_a=None, out=None):
         """gcs_scan.  t_last_scan / t_scan bound the scan-to-scan IMU window of the measurement-noise
         IW statistics and the IMU evidence (pipeline.py:331-332); default: the scan window.  xyz_f64:
         xyz_dev holds f64 x, y, z per point_step record (gcs_parse_pointcloud2 output, point_step 24).
         Odometry arguments left None take the node's "no odometry yet" inputs (backend_node.py:
-        2047-2051); Sigma_g / Sigma_a None take the IW modes of the context's measurement state."""
+        2047-2051); Sigma_g / Sigma_a None take the IW modes of the context's measurement state.
+        out: a GcsScanOutputs to fill (the caller's, reused across scans); default a fresh one."""
         imu_stamps = np.ascontiguousarray(imu_stamps, np.float64)
         imu_gyro = np.ascontiguousarray(imu_gyro, np.float64).reshape(-1)
         imu_accel = np.ascontiguousarray(imu_accel, np.float64).reshape(-1)
@@ -279,7 +280,8 @@ class HypothesisContext:
                 a = np.ascontiguousarray(arr, np.float64).reshape(-1)
                 keep.append(a)
                 setattr(inp, name, _addr(a))
-        out = L.GcsScanOutputs()
+        if out is None:
+            out = L.GcsScanOutputs()
         self._chk(self.lib.gcs_scan(self.h, C.byref(inp), C.byref(out)), "gcs_scan")
         return out
 

@@ -197,6 +197,11 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * one look-back tile take that failure path on every scan. */
 #define GCS_DEBUG_SCAN_SPIN_LIMIT 1
 #define GCS_DEBUG_INJECT_SCAN_FAIL 2
+/* GCS_DEBUG_SORTED_BUCKETS != 0: gcs_scan buckets points by the sorted path (k_scan, k_place,
+ * k_bucket_rank) instead of the direct buckets; GCS_DEBUG_BUCKET_CAPACITY (4..32, multiple of 4)
+ * lowers the direct buckets' row capacity so a test can force the overflow redo (cert[57] = 1). */
+#define GCS_DEBUG_SORTED_BUCKETS 3
+#define GCS_DEBUG_BUCKET_CAPACITY 4
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*6*/, int64_t* counts /*6*/, int32_t reset);
 int gcs_ctx_set_atlas(gcs_ctx* ctx, const double* dirs_host /*B*3*/);
@@ -471,6 +476,9 @@ typedef struct {            /* PrimitiveAssociationResult (:71-92): device point
 } gcs_assoc_outputs;
 
 int gcs_assoc_config_defaults(gcs_assoc_config* cfg);
+/* Host evaluation of the Sinkhorn's short log / exp / x^y (gcs_math.h log_short, exp_short,
+ * pow_sinkhorn; the device runs the same code) for the accuracy test against numpy. */
+int gcs_debug_short_log_exp(const double* x, int32_t n, double y, double* log_out, double* exp_out, double* pow_out);
 int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int32_t device, gcs_assoc_ctx** out);
 int gcs_assoc_ctx_destroy(gcs_assoc_ctx* ctx);
 const char* gcs_assoc_last_error(const gcs_assoc_ctx* ctx);

@@ -105,3 +105,29 @@ def test_assoc_ctx_argument_checks(lib):
     assert lib.gcs_assoc_ctx_create(0, 16, 8, 0, C.byref(h)) == -1       # no rows
     assert lib.gcs_assoc_ctx_create(16, 16, 33, 0, C.byref(h)) == -1     # k_assoc > 32
     assert lib.gcs_assoc_ctx_create(4096, 16, 8, 0, C.byref(h)) == -1    # past the one-workgroup Sinkhorn
+
+
+def test_short_log_exp_pow_accuracy(lib):
+    """The Sinkhorn's short log / exp (fdlibm reductions + minimax polynomials, gcs_math.h): within
+    1 ulp of numpy's over the scalings' range, and x^y within 12 ulps of numpy's pow there."""
+    from gcslam import _lib as L
+    rng = np.random.default_rng(0)
+    x = np.concatenate([np.exp(rng.uniform(-40.0, 40.0, 100000)), rng.uniform(0.5, 2.0, 10000),
+                        np.array([1.0, 0.5, 2.0, np.sqrt(0.5), 1e-300, 1e300])])
+    lo, ex, pw = np.empty_like(x), np.empty_like(x), np.empty_like(x)
+    y = 1.0 / 6.0
+    assert lib.gcs_debug_short_log_exp(L.dptr(x), x.size, y, L.dptr(lo), L.dptr(ex), L.dptr(pw)) == 0
+    ulp = lambda a, b: np.abs(a - b) / np.spacing(np.abs(b))  # noqa: E731
+    assert ulp(lo, np.log(x)).max() <= 1.0
+    xe = rng.uniform(-40.0, 40.0, 100000)
+    lo2, ex2, pw2 = np.empty_like(xe), np.empty_like(xe), np.empty_like(xe)
+    assert lib.gcs_debug_short_log_exp(L.dptr(xe), xe.size, y, L.dptr(lo2), L.dptr(ex2), L.dptr(pw2)) == 0
+    assert ulp(ex2, np.exp(xe)).max() <= 1.0
+    # the rounding of y log x (an ulp of |y log x|, up to 6.7 over exp(+-40)) carries into exp; at
+    # 1e+-300 (|y log x| = 115, far outside the scalings' range) it is ~20 ulps
+    assert ulp(pw[:-2], np.power(x[:-2], y)).max() <= 12.0
+    np.testing.assert_allclose(pw[-2:], np.power(x[-2:], y), rtol=1e-14)
+    z = np.zeros(1)
+    o1, o2, o3 = np.empty(1), np.empty(1), np.empty(1)
+    assert lib.gcs_debug_short_log_exp(L.dptr(z), 1, y, L.dptr(o1), L.dptr(o2), L.dptr(o3)) == 0
+    assert o3[0] == 0.0

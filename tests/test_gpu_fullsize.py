@@ -101,10 +101,12 @@ def test_c3_subsample_point_stage_and_moment_match():
 def test_scan_lookback_failure_is_reported():
     """k_scan's bounded look-back spin: when it runs out the scan fails loudly (GCS_ERR_HIP ->
     RuntimeError) instead of returning results built on wrong bucket starts; the next scan is
-    unaffected (gcs_ctx_set_debug test hook forces the failure path on one look-back tile)."""
+    unaffected (gcs_ctx_set_debug test hook forces the failure path on one look-back tile).  gcs_scan
+    runs the sorted bucketing here (its direct buckets have no look-back)."""
     from gcslam import _lib as L
     syn = _synthetic()
     ctx = _ctx(n_bins=20000, n_points_cap=8192, mode="scale")     # 5 look-back tiles
+    ctx.set_debug(L.DEBUG_SORTED_BUCKETS, 1)
     sc = syn.make_scan(8192, 5)
     rec, t, w = device_scan(sc)
     ctx.set_debug(L.DEBUG_INJECT_SCAN_FAIL, 1)

@@ -263,6 +263,39 @@ def test_bitwise_determinism_scale():
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("capacity", [32, 4])
+def test_direct_buckets_match_sorted_bitwise(capacity):
+    """gcs_scan's direct buckets (k_points' fixed member rows, ranked by point index while the bin
+    kernel stages) against the sorted bucketing (k_scan, k_place, k_bucket_rank): the accumulation
+    order is the same, so three consecutive scans agree bit for bit.  capacity 4: buckets overflow
+    the rows, the first scan is redone sorted (cert[57] = 1) and later scans stay sorted."""
+    from gcslam import _lib as L
+    syn = _synthetic()
+    outs = []
+    for sorted_path in (False, True):
+        # capacity 4: 2,000 bins, so the occupied buckets hold several points each and overflow
+        ctx = _ctx(n_bins=20000 if capacity == 32 else 2000, n_points_cap=8192, mode="scale")
+        if sorted_path:
+            ctx.set_debug(L.DEBUG_SORTED_BUCKETS, 1)
+        elif capacity != 32:
+            ctx.set_debug(L.DEBUG_BUCKET_CAPACITY, capacity)
+        res = []
+        for k in range(3):
+            sc = syn.make_scan(8192, 11 + k)
+            rec, t, w = device_scan(sc)
+            o = ctx.scan(rec, 16, t, w, 8192, **scan_kwargs(sc))
+            res.append((ctx.get_scan_stats(), ctx.get_map()[0], np.array(o.belief.L[:]), np.array(o.cert[:])))
+        outs.append(res)
+        ctx.close()
+    for k in range(3):
+        for a, b in zip(outs[0][k][:3], outs[1][k][:3]):
+            assert np.array_equal(a, b)
+        ca, cb = outs[0][k][3], outs[1][k][3]
+        assert ca[57] == (1.0 if (capacity == 4 and k == 0) else 0.0) and cb[57] == 0.0
+        ca[57] = cb[57] = 0.0
+        assert np.array_equal(ca, cb)
+
+
 @pytest.mark.parametrize("n", [4096, 12288])
 def test_degenerate_same_direction_points(n):
     """All points on one ray (one giant bucket: ranked in-wave at 4096, compacted at 12288)
