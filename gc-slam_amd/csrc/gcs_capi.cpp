@@ -51,6 +51,8 @@ struct gcs_ctx {
   int* d_tile_src = nullptr;
   uint16_t* d_rknn_local = nullptr;
   int max_tile_src = 0;
+  int tile_bins = 64;  // bins per k_bins_scale tile (bins_tile_for)
+  int tile_shift = 6;
   // per-point
   PointRec* d_recs = nullptr;
   uint32_t *d_keys = nullptr, *d_slots = nullptr, *d_sorted = nullptr;
@@ -285,11 +287,11 @@ int upload_atlas(gcs_ctx* c) {
     atlas::reverse(knn_dev.data(), B, K, off, idx);
     std::vector<int> src_off, src;
     std::vector<uint16_t> local;
-    c->max_tile_src = atlas::tile_sources(off, idx, B, bins_tile(), src_off, src, local);
+    c->max_tile_src = atlas::tile_sources(off, idx, B, c->tile_bins, src_off, src, local);
     if (c->max_tile_src > bins_max_tile_sources())
       return fail(c, GCS_ERR_ARG, "bin atlas too irregular for the tiled bin kernel (tile source list too long)");
-    for (int b0 = 0; b0 < B; b0 += bins_tile())
-      if (off[std::min(B, b0 + bins_tile())] - off[b0] > bins_max_tile_entries())
+    for (int b0 = 0; b0 < B; b0 += c->tile_bins)
+      if (off[std::min(B, b0 + c->tile_bins)] - off[b0] > bins_max_tile_entries())
         return fail(c, GCS_ERR_ARG, "bin atlas too irregular for the tiled bin kernel (tile reverse-kNN list too long)");
     c->G = atlas::grid_for_bins(B);
     c->ncell = 6 * c->G * c->G;
@@ -334,7 +336,7 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, hipEvent_t e0, bool tog
   ba.zero32 = c->d_counts;  // counts only: the bucketing scratch after them is re-armed by k_bins_scale
   ba.n_zero32 = c->d_counts ? c->B : 0;
   ba.zero8 = c->d_flags;
-  ba.n_zero8 = c->d_flags ? c->B + bins_scale_blocks(c->B) : 0;
+  ba.n_zero8 = c->d_flags ? c->B + bins_scale_blocks(c->B, c->tile_bins) : 0;
   c->budget_blocks = red_blocks(std::max(n_raw, 1));
   c->budget_pending = true;
   if (!e0 && c->push_async) return submit_budget(c, ba, c->budget_blocks, s);
@@ -386,6 +388,7 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
     a.members = c->d_members;
     a.capb = c->capb_eff;
     a.flags = c->d_flags;
+    a.tile_shift = c->tile_shift;
     a.overflow = c->d_err + 2;
   }
   a.budget_partials = c->d_partials;
@@ -424,6 +427,7 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   b.map = c->d_map;
   b.n_bins = c->B;
   b.cap = c->cap;
+  b.tile_bins = c->tile_bins;
   memcpy(b.origin, c->cfg.lidar_origin, 3 * sizeof(double));
   b.tau = c->cfg.tau;
   b.scan = c->d_scan;
@@ -458,6 +462,7 @@ int stage_bins(gcs_ctx* c) {
       ba.slot_idx = c->d_sorted;
       ba.perm = c->d_perm;
       ba.flags = c->d_flags;
+      ba.tile_shift = c->tile_shift;
       ba.err = c->d_err;
       ba.spin_limit = c->spin_limit;
       ba.inject_scan_fail = c->inject_scan_fail;
@@ -705,6 +710,8 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   c->cfg = *cfg;
   c->B = cfg->n_bins;
   c->cap = cfg->n_points_cap;
+  c->tile_bins = bins_tile_for(c->cap, c->B);
+  c->tile_shift = c->tile_bins == 32 ? 5 : 6;
   c->K = cfg->mode == GCS_MODE_SCALE ? cfg->k_cand : 0;
   c->max_raw = cfg->max_raw_points;
   for (int k = 0; k < 3; ++k) c->grav[k] = cfg->gravity_W[k] * cfg->imu_gravity_scale;
@@ -733,7 +740,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMemset(c->d_map, 0, B * MF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scan, 0, B * SF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_touched, B))) return GCS_ERR_HIP;
-  c->partials_len = std::max<size_t>({partials_need(kRedBlocks, 24), partials_need(bins_scale_blocks(c->B), bins_partial_nv()),
+  c->partials_len = std::max<size_t>({partials_need(kRedBlocks, 24), partials_need(bins_scale_blocks(c->B, c->tile_bins), bins_partial_nv()),
                                       partials_need(push_blocks(c->B), 10)});
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_part_pts, partials_need(std::max(kRedBlocks, points_max_blocks()), 5) * sizeof(double)))) return GCS_ERR_HIP;
@@ -765,15 +772,15 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMemset(c->d_perm, 0, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     if (bad(hipMemset(c->d_sorted, 0, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     // bin flags, then one flag per k_bins_scale tile (both cleared by k_budget every scan)
-    const size_t nflags = B + bins_scale_blocks(c->B);
+    const size_t nflags = B + bins_scale_blocks(c->B, c->tile_bins);
     if (bad(hipMalloc(&c->d_flags_buf[0], 2 * nflags))) return GCS_ERR_HIP;
     if (bad(hipMemset(c->d_flags_buf[0], 0, 2 * nflags))) return GCS_ERR_HIP;
     c->d_flags_buf[1] = c->d_flags_buf[0] + nflags;
     c->d_flags = c->d_flags_buf[0];
     // every tile starts dirty: the first scan writes all ScanBinStats rows and partial rows
-    if (bad(hipMalloc(&c->d_tile_dirty, bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
-    if (bad(hipMemset(c->d_tile_dirty, 1, bins_scale_blocks(c->B)))) return GCS_ERR_HIP;
-    if (bad(hipMalloc(&c->d_bins_part, partials_need(bins_scale_blocks(c->B), bins_partial_nv()) * sizeof(double))))
+    if (bad(hipMalloc(&c->d_tile_dirty, bins_scale_blocks(c->B, c->tile_bins)))) return GCS_ERR_HIP;
+    if (bad(hipMemset(c->d_tile_dirty, 1, bins_scale_blocks(c->B, c->tile_bins)))) return GCS_ERR_HIP;
+    if (bad(hipMalloc(&c->d_bins_part, partials_need(bins_scale_blocks(c->B, c->tile_bins), bins_partial_nv()) * sizeof(double))))
       return GCS_ERR_HIP;
   } else {
     size_t nchunks = (cap + 255) / 256;
@@ -1782,7 +1789,9 @@ int gcs_ctx_describe(gcs_ctx* c, char* buf, int32_t len) {
       f.tau, scale ? "K nearest atlas bins of the exact nearest bin, ties -> lower id (declared)" : "dense N x B softmax (reference)",
       f.forgetting_factor, f.deskew_rotation_only ? "true" : "false", f.gravity_W[0], f.gravity_W[1], f.gravity_W[2],
       f.imu_gravity_scale, f.use_imu_odom ? "true" : "false", f.planar_z_ref, f.planar_z_sigma, f.planar_vz_sigma,
-      f.alpha_min, f.alpha_max, f.c0_cond, scale ? "bucketing + k_bins_scale (HIP)" : "k_dense_accum + k_dense_finalize (HIP)");
+      f.alpha_min, f.alpha_max, f.c0_cond, scale ? (c->tile_bins == 32 ? "bucketing + k_bins_scale, 32-bin tiles x 8 lanes per bin (HIP)"
+                                 : "bucketing + k_bins_scale, 64-bin tiles x 4 lanes per bin (HIP)")
+            : "k_dense_accum + k_dense_finalize (HIP)");
   if (n < 0 || n >= len) return fail(c, GCS_ERR_ARG, "describe buffer too short");
   memcpy(buf, tmp, (size_t)n + 1);
   return GCS_OK;

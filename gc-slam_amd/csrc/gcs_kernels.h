@@ -65,6 +65,7 @@ struct PointKernelArgs {
   uint32_t* members;
   int capb;
   uint8_t* flags;
+  int tile_shift;  // log2 of the bin kernel's tile (flags[n_bins + (bin >> tile_shift)] marks active tiles)
   uint32_t* overflow;
   const double* budget_partials;  // k_budget block partials (folded by every k_points block)
   int budget_blocks;
@@ -88,6 +89,7 @@ struct BucketArgs {
   uint32_t* slot_idx;     // bucket-ordered point indices, arrival order within a bucket
   uint32_t* perm;         // bucket-ordered point indices, point-index order within a bucket
   uint8_t* flags;         // active bins (cleared by k_budget)
+  int tile_shift;         // log2 of the bin kernel's tile
   // error words in host-mapped memory, written only on the rare paths: [0] k_scan look-back spin
   // bound exhausted (the scan's bucket starts are invalid -> gcs_scan fails), [1] k_bucket_rank took
   // the in-order compaction path for a bucket above kRankMax members (correct, degenerate; reported)
@@ -113,6 +115,7 @@ struct BinKernelArgs {
   const double* bin_dirs;
   const double* map;  // map sufficient stats (fused Matrix-Fisher term, scale mode)
   int n_bins, cap;
+  int tile_bins;  // bins per k_bins_scale workgroup (bins_tile_for)
   double origin[3];
   double tau;
   double* scan;  // 26 x B field-major
@@ -143,11 +146,13 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
                          hipEvent_t e0, hipEvent_t e1);
 int scan_tiles(int n_bins);
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
-int bins_scale_blocks(int n_bins);
+// Bins per k_bins_scale tile: 64 (four lanes per bin); GCSLAM_BIN_TILE=32 selects 32-bin tiles with
+// eight lanes per bin (measured slower at C2, kept for A/B and parity-tested).
+int bins_tile_for(long cap, int n_bins);
+int bins_scale_blocks(int n_bins, int tile_bins);
 int partial_stride(int nv);  // doubles per block-partial row
 // doubles a partials buffer needs for nblocks rows of nv values (+ the two-level fold's rows)
 size_t partials_need(long nblocks, int nv);
-int bins_tile();              // device bins per k_bins_scale workgroup
 int bins_max_tile_sources();  // capacity of its source list
 int bins_max_tile_entries();  // capacity of its reverse-kNN entry list
 int bins_partial_nv();

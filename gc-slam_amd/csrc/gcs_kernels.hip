@@ -30,7 +30,6 @@ namespace gcs {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
-constexpr int kBinTile = 64;  // device bins per k_bins_scale workgroup (a Hilbert patch, gcs_atlas.h)
 
 // ---------------------------------------------------------------- reductions
 template <int NV>
@@ -426,7 +425,8 @@ void k_points(PointKernelArgs a, double* partials) {
             for (int q = 0; q < KC; q += 4) {
               const int4 c4 = *(const int4*)(kr + q);
               a.flags[c4.x] = 1; a.flags[c4.y] = 1; a.flags[c4.z] = 1; a.flags[c4.w] = 1;
-              tf[c4.x / kBinTile] = 1; tf[c4.y / kBinTile] = 1; tf[c4.z / kBinTile] = 1; tf[c4.w / kBinTile] = 1;
+              const int ts = a.tile_shift;
+              tf[c4.x >> ts] = 1; tf[c4.y >> ts] = 1; tf[c4.z >> ts] = 1; tf[c4.w >> ts] = 1;
             }
           }
         }
@@ -628,7 +628,8 @@ __global__ __launch_bounds__(kBlock) void k_bucket_rank(BucketArgs b, int n) {
     for (int q = 0; q < b.k; q += 4) {
       int4 c4 = *(const int4*)(kr + q);
       b.flags[c4.x] = 1; b.flags[c4.y] = 1; b.flags[c4.z] = 1; b.flags[c4.w] = 1;
-      tf[c4.x / kBinTile] = 1; tf[c4.y / kBinTile] = 1; tf[c4.z / kBinTile] = 1; tf[c4.w / kBinTile] = 1;
+      const int ts = b.tile_shift;
+      tf[c4.x >> ts] = 1; tf[c4.y >> ts] = 1; tf[c4.z >> ts] = 1; tf[c4.w >> ts] = 1;
     }
   }
   if (c && c <= (uint32_t)kLaneRank) {
@@ -784,8 +785,12 @@ __device__ void mf_finish(const double* v, double* scalars) {
 constexpr int kBinNV = 16;
 
 // ---------------------------------------------------------------- row 5+6 scale mode: bin-centric
-// One 256-thread workgroup per tile of kBinTile = 64 consecutive device bins (a compact Hilbert
-// patch of the sphere, gcs_atlas.h).
+// One 256-thread workgroup per tile of TB consecutive device bins (a compact Hilbert patch of the
+// sphere, gcs_atlas.h): TB = 64 with four lanes per bin.  TB = 32 with eight lanes per bin
+// (GCSLAM_BIN_TILE=32) was measured at C2 and dropped: 1,019 active tiles no longer start together
+// (a quarter start after 15 us), the gather phase did not shorten (5.7 vs 5.9 us with half the
+// records per lane), and a tile over its 256-record stage took the unstaged path (69 us): kernel
+// 69.7 vs 28.3 us.
 //  0: a tile none of whose bins is a candidate of a non-empty bucket (tile flag, set by
 //     k_bucket_rank) has exact-zero sums: wave 0 writes the zero-bin rows and the tile's partial
 //     row in closed form; A-D are skipped.  With the VLP-16-like scans (rings within +-15 deg)
@@ -810,7 +815,7 @@ constexpr int kBinNV = 16;
 // STAGE: kStageBig when the scan is dense in the map (cap >= 0.4 B, C2: 41 KiB of LDS, three
 // workgroups per CU), kStageSmall otherwise (C3: 25 KiB; four per CU, register-limited).
 constexpr int kMaxSrc = 320;   // atlas tables for B = 1k .. 1M have at most 199 per 64-bin tile
-constexpr int kMaxRl = 1280;   // reverse-kNN entries of one tile (~K x kBinTile; at most 1070)
+constexpr int kMaxRl = 1280;   // reverse-kNN entries of one tile (~K x 64; at most 1070)
 #ifndef GCS_STAGE_BIG
 #define GCS_STAGE_BIG 512  // 480 (four workgroups per CU in LDS instead of three) measured slower at C2: 27.2 -> 30.5 us
 #endif
@@ -825,8 +830,6 @@ constexpr int kStageBig = GCS_STAGE_BIG, kStageSmall = 256;
 #endif
 constexpr int kRecD = 8 + GCS_REC_PAD;
 __device__ __forceinline__ uint32_t rec_swz(uint32_t r) { return GCS_REC_SWZ ? ((r >> 2) & 3u) : 0u; }
-static_assert(kStageSmall * kRecD >= 19 * kBinTile, "phase D reuses the record stage for the bin sums");
-int bins_tile() { return kBinTile; }
 int bins_max_tile_sources() { return kMaxSrc; }
 int bins_max_tile_entries() { return kMaxRl; }
 
@@ -892,16 +895,18 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
 // 5 waves per SIMD needs <= 96 VGPRs (the register allocator spills ~28 dwords to reach it)
 #define GCS_BINS_WAVES_SMALL 0
 #endif
-template <int STAGE, int LANES>
-__global__ __launch_bounds__(kBinTile * LANES)
+template <int STAGE, int TB, int LANES>
+__global__ __launch_bounds__(TB * LANES)
 #if GCS_BINS_WAVES
 __attribute__((amdgpu_waves_per_eu(GCS_BINS_WAVES)))
 #elif GCS_BINS_WAVES_SMALL
 __attribute__((amdgpu_waves_per_eu(STAGE == kStageSmall ? GCS_BINS_WAVES_SMALL : 1)))
 #endif
 void k_bins_scale(BinKernelArgs a, double* partials) {
-  constexpr int NT = kBinTile * LANES, NW = NT / 64;
+  constexpr int NT = TB * LANES, NW = NT / 64;
   static_assert(LANES == 4 || LANES == 8, "phase C splits each bin over 4 or 8 lanes");
+  static_assert(TB <= 64, "phase D: one lane of wave 0 per bin");
+  static_assert(STAGE * kRecD >= 19 * TB, "phase D reuses the record stage for the bin sums");
   __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
   __shared__ double s_rec[STAGE * kRecD];
 #if GCS_RANK_LANES == 4
@@ -910,21 +915,21 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   static_assert(kMaxRl * sizeof(uint16_t) <= STAGE * kRecD * sizeof(double), "raw list fits the stage");
   uint16_t* const s_rl = reinterpret_cast<uint16_t*>(s_rec);
   __shared__ uint16_t s_rlc[kMaxRl];  // each bin's non-empty sources, compacted (phase C's list)
-  __shared__ uint8_t s_act[kBinTile];
+  __shared__ uint8_t s_act[TB];
   uint16_t* const rlist = s_rlc;
 #else
   __shared__ uint16_t s_rl[kMaxRl];
   uint16_t* const rlist = s_rl;
 #endif
-  __shared__ double4 s_bd[kBinTile];
-  __shared__ int s_q[kBinTile + 1];
-  __shared__ uint32_t s_work[kBinTile];
+  __shared__ double4 s_bd[TB];
+  __shared__ int s_q[TB + 1];
+  __shared__ uint32_t s_work[TB];
   __shared__ uint32_t s_wsum[NW];
   __shared__ double lds[NW * 16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int tile = blockIdx.x;
-  const int b0 = tile * kBinTile;
-  const int nb = min(kBinTile, a.n_bins - b0);
+  const int b0 = tile * TB;
+  const int nb = min(TB, a.n_bins - b0);
   PROF(0);
   for (int j = blockIdx.x * NT + t; j < a.n_zero_after; j += gridDim.x * NT) a.zero_after[j] = 0u;
   if (blockIdx.x == 0 && a.pts_partials) {  // k_points' cert partials (off the critical path here)
@@ -976,7 +981,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
   if (t <= nb) s_q[t] = q_t;
 #if GCS_RANK_LANES == 4
-  if (t < kBinTile) s_act[t] = own_act ? 1 : 0;
+  if (t < TB) s_act[t] = own_act ? 1 : 0;
 #endif
   {
     // fixed trip counts: every thread issues all of its table loads before the first LDS write,
@@ -1018,13 +1023,13 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     // takes the l-th quarter of the bin's reverse-kNN entries; the non-empty sources are written,
     // in order, to the compacted list s_rlc (offsets by a prefix over the four lanes), so phase C's
     // cursor never walks an empty bucket (each visit was two dependent LDS reads).
-    const int rb = t >> 2, rq = t & 3;
+    const int rb = t / LANES, rq = t % LANES;
     int qa = 0, lo = 0, hi = 0;
     if (s_act[rb]) {
       qa = s_q[rb] - q0;
       const int n = s_q[rb + 1] - q0 - qa;
-      lo = qa + n * rq / 4;
-      hi = qa + n * (rq + 1) / 4;
+      lo = qa + n * rq / LANES;
+      hi = qa + n * (rq + 1) / LANES;
     }
     uint32_t w = 0;
     int nz = 0;
@@ -1041,7 +1046,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     }
     int x = nz;
 #pragma unroll
-    for (int off = 1; off < 4; off <<= 1) {
+    for (int off = 1; off < LANES; off <<= 1) {
       const int y = __shfl_up(x, off, 64);
       if (rq >= off) x += y;
     }
@@ -1054,12 +1059,12 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       for (int u = 0; u < 4; ++u)
         if (q + u < hi && s_cnt[j[u]]) s_rlc[e++] = j[u];
     }
-    w += (uint32_t)__shfl_xor((int)w, 1, 64);
-    w += (uint32_t)__shfl_xor((int)w, 2, 64);
+#pragma unroll
+    for (int off = 1; off < LANES; off <<= 1) w += (uint32_t)__shfl_xor((int)w, off, 64);
     if (rq == 0) s_work[rb] = w;
   }
 #else
-  if (t < kBinTile) {  // wave 0, lane = bin: records each bin visits (0: inactive / out of range)
+  if (t < TB) {  // wave 0, lane = bin: records each bin visits (0: inactive / out of range)
     // The bin's reverse-kNN sources are compacted in place to the non-empty ones (same order):
     // most sources of a bin are empty buckets, and phase C's cursor then never walks them (each
     // visit was two dependent LDS reads).  Entries are read four at a time ahead of the writes
@@ -1111,7 +1116,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #ifdef GCS_PHASE_PROF
   if (t == 0) {
     uint32_t mx = 0, sm = 0;
-    for (int i = 0; i < kBinTile; ++i) { mx = max(mx, s_work[i]); sm += s_work[i]; }
+    for (int i = 0; i < TB; ++i) { mx = max(mx, s_work[i]); sm += s_work[i]; }
     g_prof[blockIdx.x * 16 + 9] = mx;
     g_prof[blockIdx.x * 16 + 10] = sm;
   }
@@ -1321,10 +1326,10 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #ifdef GCS_PHASE_PROF
   if (lane == 0 && wid > 0 && wid < 4) g_prof[blockIdx.x * 16 + 10 + wid] = wall_clock64();  // waves 1-3 gather end
 #endif
-  __syncthreads();  // the record stage is free: it now carries the bin sums [19][kBinTile]
+  __syncthreads();  // the record stage is free: it now carries the bin sums [19][TB]
   if (l == 0)
 #pragma unroll
-    for (int f = 0; f < 19; ++f) s_rec[f * kBinTile + lb] = acc[f];
+    for (int f = 0; f < 19; ++f) s_rec[f * TB + lb] = acc[f];
   __syncthreads();
   if (wid != 0) return;
   PROF(14);
@@ -1336,7 +1341,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   v[4] = -INFINITY;
   if (own) {
 #pragma unroll
-    for (int f = 0; f < 19; ++f) acc[f] = s_rec[f * kBinTile + t];
+    for (int f = 0; f < 19; ++f) acc[f] = s_rec[f * TB + t];
     finalize_bin(acc, a.scan, a.n_bins, b0 + t, v);
     PROF(15);
     if (!GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + t);
@@ -1843,16 +1848,28 @@ hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_
   return hipGetLastError();
 }
 
-int bins_scale_blocks(int n_bins) { return (n_bins + kBinTile - 1) / kBinTile; }
+int bins_tile_for(long cap, int n_bins) {
+  if (const char* e = getenv("GCSLAM_BIN_TILE")) {
+    const int v = atoi(e);
+    if (v == 32 || v == 64) return v;
+  }
+  (void)cap;
+  (void)n_bins;
+  return 64;
+}
+int bins_scale_blocks(int n_bins, int tile_bins) { return (n_bins + tile_bins - 1) / tile_bins; }
 int bins_partial_nv() { return kBinNV; }
 
 hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
                              hipEvent_t e2) {
-  const int nblk = bins_scale_blocks(a.n_bins);
-  if ((long)a.cap * 5 >= (long)a.n_bins * 2)
-    hipExtLaunchKernelGGL(k_bins_scale<kStageBig, 4>, dim3(nblk), dim3(kBinTile * 4), 0, s, e0, e1, 0, a, partials);
+  const int nblk = bins_scale_blocks(a.n_bins, a.tile_bins);
+  const bool big = (long)a.cap * 5 >= (long)a.n_bins * 2;  // C2-like: dense in the map
+  if (a.tile_bins == 32)  // half the records of a 64-bin tile: the small stage holds them
+    hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 32, 8>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+  else if (big)
+    hipExtLaunchKernelGGL((k_bins_scale<kStageBig, 64, 4>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else
-    hipExtLaunchKernelGGL(k_bins_scale<kStageSmall, 4>, dim3(nblk), dim3(kBinTile * 4), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 64, 4>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   GCS_FINAL(kBinNV, 16u, FIN_BINS, nblk, s, e2, partials, a.scalars);
   return hipGetLastError();
 }

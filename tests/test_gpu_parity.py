@@ -263,6 +263,33 @@ def test_bitwise_determinism_scale():
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("tile", [32, 64])
+def test_bin_tile_sizes_match_oracle(tile, monkeypatch):
+    """k_bins_scale's two tile shapes (32 bins x 8 lanes, chosen when the scan is dense in the map;
+    64 bins x 4 lanes) forced through GCSLAM_BIN_TILE on the same scans: ScanBinStats and the
+    scan's z_t against the oracle at the moment-match bars, and the manifest names the shape."""
+    monkeypatch.setenv("GCSLAM_BIN_TILE", str(tile))
+    syn = _synthetic()
+    B, cap, n_raw = 20000, 8192, 8192
+    ctx = _ctx(n_bins=B, n_points_cap=cap, mode="scale")
+    assert f"{tile}-bin tiles" in ctx.describe()["backends"]["moment_match"]
+    dirs, knn = ctx.atlas()
+    cfg = opipe.BinPathConfig(n_points_cap=cap, n_bins=B, mode="scale", lidar_origin=ORIGIN, tau=ctx.cfg.tau)
+    b = ops.Belief.identity_prior()
+    nu, Psi = ops.datasheet_process_noise_state()
+    Q = ops.process_noise_Q(nu, Psi)
+    ms = opipe.MapState.empty(B)
+    for k in range(2):
+        sc = syn.make_scan(n_raw, 20 + k)
+        ref = opipe.process_scan_bin_path(b, sc, Q, cfg, dirs, knn, ms)
+        rec, t, w = device_scan(sc)
+        out = ctx.scan(rec, 16, t, w, n_raw, **scan_kwargs(sc), Q=Q)
+        _check_scan_stats(ctx.get_scan_stats(), ref["scan_bins"])
+        assert_close(f"tile {tile} scan{k} z_t", np.array(out.z_t[:]), ref["z_t"], rtol=1e-7, atol=1e-9)
+        b, ms = ref["belief"], ref["map"]
+    ctx.close()
+
+
 @pytest.mark.parametrize("capacity", [32, 4])
 def test_direct_buckets_match_sorted_bitwise(capacity):
     """gcs_scan's direct buckets (k_points' fixed member rows, ranked by point index while the bin

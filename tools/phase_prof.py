@@ -37,7 +37,9 @@ def main():
     ctx.lib.gcs_debug_psd_count.argtypes = [C.c_void_p, C.c_int]
     assert ctx.lib.gcs_debug_psd_count(pc, 1) == 0
     print(f"3x3 PSD over 3 scans: non-zero inputs {pc[0]}, slow path {pc[1]}, Jacobi fallback {pc[2]}")
-    nblk = (B + 63) // 64
+    tb = 32 if "32-bin tiles" in ctx.describe()["backends"]["moment_match"] else 64
+    nblk = (B + tb - 1) // tb
+    print(f"tile: {tb} bins")
     buf = (C.c_ulonglong * (nblk * 16))()
     fn = ctx.lib.gcs_debug_prof
     fn.argtypes = [C.c_void_p, C.c_int]
