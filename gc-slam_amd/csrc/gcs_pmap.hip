@@ -1,0 +1,1105 @@
+// The primitive map resident in HBM and its maintenance operators on gfx950 -- the live primitive
+// path's map side, FS/backend/structures/primitive_map.py:
+//
+//   storage        max_tiles tiles x m_tile slots; per field [tile][slot][width] (the reference's
+//                  PrimitiveMapTile array shapes, :98-174), f64 / i64 / u8
+//   k_pm_keys      one lane per slot: the single sort key of _select_topk_slots_fixed (-score, :316-319)
+//                  or _select_lowest_mass_slots_fixed (retention, :345-351) in order-preserving u64 bits
+//                  (-0.0 and 0.0 equal, as lax.sort's comparator), value = slot; then a stable
+//                  segmented radix sort (rocPRIM), one segment per tile
+//   k_pm_view      one lane per view entry: the tile's r-th slot, mean (LU solve of Lambda + eps I),
+//                  covariance, resultant direction and kappa (:474-498)
+//   k_pm_insert    one workgroup: tile by tile, the masked proposals into the K lowest-retention slots,
+//                  ids by a prefix over the mask from next_global_id (:852-934)
+//   fuse           rows keyed by (tile, slot) (masked rows dropped), stable radix sort, one lane per key
+//                  run sums its rows in input order (the reference's .at[].add order) and adds the sums
+//                  to the slot (:1037-1123); every listed tile's rgb is rebuilt and the rows' slots get
+//                  the timestamp (:1097-1112)
+//   k_pm_cull / k_pm_recency / k_pm_forget  one workgroup per tile (fixed-order sums) / elementwise
+//   merge          per-slot mean / covariance / det, all triu pairs' Bhattacharyya distance
+//                  (:1907-1930), max_pairs rounds of a (distance, pair index) argmin over eligible pairs
+//                  -- the greedy walk of the stable argsort (:1554-1585) -- then the moment-matched
+//                  merges of the selected (disjoint) pairs (:1603-1707)
+// No floating-point atomics; every sum has a fixed order.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "gcs_math.h"
+#include "gcslam_hip.h"
+
+namespace gcs {
+namespace {
+
+constexpr int kPmThreads = 256;
+constexpr int kPmRed = 1024;  // one-workgroup-per-tile reductions
+constexpr uint32_t kNoKey = 0xffffffffu;
+
+struct PmStore {
+  double *lam, *th, *eta, *w, *ts, *cts, *col, *cam, *lid, *acc, *den, *rgb;
+  int64_t *lsup, *lupd, *ids;
+  uint8_t* valid;
+  int M, nl;  // slots per tile, vMF lobes
+};
+
+__device__ __forceinline__ size_t sidx(const PmStore& s, int t, int q) { return (size_t)t * s.M + q; }
+
+// ascending order of a double as unsigned bits; -0.0 folds onto 0.0 (lax.sort's float comparator)
+__device__ __forceinline__ uint64_t ord_key(double x) {
+  if (x == 0.0) x = 0.0;
+  const uint64_t u = (uint64_t)__double_as_longlong(x);
+  return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+
+// LU with partial pivoting on A + eps I (jnp.linalg.solve / inv / det are LU), n_rhs right-hand sides
+__device__ void lu3(const double* A, double eps, double (&a)[3][3], int (&perm)[3], double& det) {
+#pragma clang fp contract(off)
+  for (int r = 0; r < 3; ++r) {
+    perm[r] = r;
+    for (int c = 0; c < 3; ++c) a[r][c] = A[3 * r + c] + (r == c ? eps : 0.0);
+  }
+  double sgn = 1.0;
+  for (int c = 0; c < 3; ++c) {
+    int pr = c;
+    for (int r = c + 1; r < 3; ++r)
+      if (fabs(a[r][c]) > fabs(a[pr][c])) pr = r;
+    if (pr != c) {
+      for (int q = 0; q < 3; ++q) {
+        const double t = a[c][q];
+        a[c][q] = a[pr][q];
+        a[pr][q] = t;
+      }
+      const int t = perm[c];
+      perm[c] = perm[pr];
+      perm[pr] = t;
+      sgn = -sgn;
+    }
+    for (int r = c + 1; r < 3; ++r) {
+      a[r][c] = a[r][c] / a[c][c];
+      for (int q = c + 1; q < 3; ++q) a[r][q] = a[r][q] - a[r][c] * a[c][q];
+    }
+  }
+  det = sgn * (a[0][0] * a[1][1] * a[2][2]);
+}
+
+__device__ void lu3_solve(const double (&a)[3][3], const int (&perm)[3], const double* b, double* x) {
+#pragma clang fp contract(off)
+  double y[3];
+  for (int r = 0; r < 3; ++r) {
+    double v = b[perm[r]];
+    for (int q = 0; q < r; ++q) v = v - a[r][q] * y[q];
+    y[r] = v;
+  }
+  for (int r = 2; r >= 0; --r) {
+    double v = y[r];
+    for (int q = r + 1; q < 3; ++q) v = v - a[r][q] * x[q];
+    x[r] = v / a[r][r];
+  }
+}
+
+__device__ void lu3_inv(const double (&a)[3][3], const int (&perm)[3], double* inv) {
+  for (int c = 0; c < 3; ++c) {
+    const double e[3] = {c == 0 ? 1.0 : 0.0, c == 1 ? 1.0 : 0.0, c == 2 ? 1.0 : 0.0};
+    double x[3];
+    lu3_solve(a, perm, e, x);
+    for (int r = 0; r < 3; ++r) inv[3 * r + c] = x[r];
+  }
+}
+
+__device__ __forceinline__ double clip01(double x) { return fmin(fmax(x, 0.0), 1.0); }
+
+// fixed-order block sum (thread-strided partials, xor tree, waves in order); result in all threads
+template <int NT>
+__device__ double block_sum_d(double v, double* lds) {
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  double s = lds[0];
+  for (int w = 1; w < NT / 64; ++w) s += lds[w];
+  return s;
+}
+
+__global__ __launch_bounds__(kPmThreads) void k_pm_clear(PmStore st, int t) {
+  const int q = blockIdx.x * kPmThreads + threadIdx.x;
+  if (q >= st.M) return;
+  const size_t i = sidx(st, t, q);
+  for (int k = 0; k < 9; ++k) st.lam[9 * i + k] = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    st.th[3 * i + k] = 0.0;
+    st.col[3 * i + k] = 0.0;
+    st.acc[3 * i + k] = 0.0;
+    st.rgb[3 * i + k] = 0.5;
+  }
+  for (int k = 0; k < 3 * st.nl; ++k) st.eta[(size_t)3 * st.nl * i + k] = 0.0;
+  st.w[i] = st.ts[i] = st.cts[i] = st.cam[i] = st.lid[i] = st.den[i] = 0.0;
+  st.lsup[i] = st.lupd[i] = st.ids[i] = 0;
+  st.valid[i] = 0;
+}
+
+// mode 0: -score (score = w, -1e30 where invalid), mode 1: retention w exp(-lam dt) (-inf where invalid)
+__global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_t* tiles, int n, int mode,
+                                                        long long seq, double lam, uint64_t* keys, uint32_t* vals,
+                                                        int32_t* offs) {
+  const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
+  if (g <= n) offs[g] = (int32_t)(g * st.M);  // segment bounds
+  if (g >= (long)n * st.M) return;
+  const int t = (int)(g / st.M), q = (int)(g % st.M);
+  const int ti = tiles[t];
+  bool v = false;
+  double w = 0.0;
+  long long last = 0;
+  if (ti >= 0) {
+    const size_t i = sidx(st, ti, q);
+    v = st.valid[i] != 0;
+    w = st.w[i];
+    last = st.lsup[i];
+  }
+  double key;
+  if (mode == 0) {
+    key = -(v ? w : -1e30);
+  } else {
+    const long long dt = max(0ll, seq - last);
+    const double decay = exp(-lam * (double)dt);
+    key = v ? w * decay : -INFINITY;
+  }
+  keys[g] = ord_key(key);
+  vals[g] = (uint32_t)q;
+}
+
+struct PmViewOut {
+  double *pos, *cov, *dir, *kap, *w, *eta, *col;
+  int64_t *ids, *lsup, *tid;
+  uint8_t* valid;
+  int32_t* slots;
+};
+
+__global__ __launch_bounds__(kPmThreads) void k_pm_view(PmStore st, const int32_t* tiles, const int64_t* tile_ids,
+                                                        int n, int k, const uint32_t* sorted, double eps_lift,
+                                                        double eps_mass, PmViewOut o) {
+#pragma clang fp contract(off)
+  const int g = blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= n * k) return;
+  const int t = g / k, r = g % k;
+  const int ti = tiles[t];
+  const int q = ti >= 0 ? (int)sorted[(size_t)t * st.M + r] : r;  // a missing tile: all keys equal
+  double L[9], th[3], es[3] = {0.0, 0.0, 0.0}, rgb[3] = {0.5, 0.5, 0.5}, w = 0.0;
+  long long id = 0, last = 0;
+  uint8_t v = 0;
+  for (int c = 0; c < 9; ++c) L[c] = 0.0;
+  for (int c = 0; c < 3; ++c) th[c] = 0.0;
+  const int ne = 3 * st.nl;
+  if (ti >= 0) {
+    const size_t i = sidx(st, ti, q);
+    for (int c = 0; c < 9; ++c) L[c] = st.lam[9 * i + c];
+    for (int c = 0; c < 3; ++c) {
+      th[c] = st.th[3 * i + c];
+      rgb[c] = st.rgb[3 * i + c];
+    }
+    for (int b = 0; b < st.nl; ++b)
+      for (int c = 0; c < 3; ++c) {
+        const double e = st.eta[(size_t)ne * i + 3 * b + c];
+        es[c] = b == 0 ? e : es[c] + e;
+        if (o.eta) o.eta[(size_t)ne * g + 3 * b + c] = e;
+      }
+    w = st.w[i];
+    id = st.ids[i];
+    last = st.lsup[i];
+    v = st.valid[i];
+  } else if (o.eta) {
+    for (int c = 0; c < ne; ++c) o.eta[(size_t)ne * g + c] = 0.0;
+  }
+  double a[3][3], det;
+  int perm[3];
+  lu3(L, eps_lift, a, perm, det);
+  double mu[3];
+  lu3_solve(a, perm, th, mu);
+  if (o.pos)
+    for (int c = 0; c < 3; ++c) o.pos[3 * g + c] = mu[c];
+  if (o.cov) {
+    double S[9];
+    lu3_inv(a, perm, S);
+    for (int c = 0; c < 9; ++c) o.cov[9 * g + c] = S[c];
+  }
+  const double kap = sqrt((es[0] * es[0] + es[1] * es[1]) + es[2] * es[2]);
+  if (o.dir)
+    for (int c = 0; c < 3; ++c) o.dir[3 * g + c] = es[c] / (kap + eps_mass);
+  if (o.kap) o.kap[g] = kap;
+  if (o.w) o.w[g] = w;
+  if (o.col)
+    for (int c = 0; c < 3; ++c) o.col[3 * g + c] = rgb[c];
+  if (o.ids) o.ids[g] = id;
+  if (o.lsup) o.lsup[g] = last;
+  if (o.valid) o.valid[g] = v;
+  if (o.slots) o.slots[g] = q;
+  if (o.tid) o.tid[g] = tile_ids[t];
+}
+
+struct PmRows {
+  const double *lam, *th, *eta, *w, *resp, *col;
+  const uint8_t* valid;
+  const int32_t *src, *tpos, *slots;
+  int n;
+};
+
+// one workgroup: tile by tile, the masked proposals land in the K lowest-retention slots
+__global__ __launch_bounds__(kPmThreads) void k_pm_insert(PmStore st, const int32_t* tiles, int n, int K,
+                                                          const uint32_t* sorted, PmRows r, double ts, long long seq,
+                                                          long long next_id, int64_t* ids_out, int32_t* n_ins) {
+  __shared__ int s_w[kPmThreads / 64];
+  long long base = next_id;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int ne = 3 * st.nl;
+  for (int t = 0; t < n; ++t) {
+    const int ti = tiles[t];
+    int run = 0;
+    for (int q0 = 0; q0 < K; q0 += kPmThreads) {
+      const int q = q0 + threadIdx.x;
+      const int row = t * K + q;
+      const int d = q < K && r.valid[row] ? 1 : 0;
+      int x = d;
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      __syncthreads();
+      if (lane == 63) s_w[wid] = x;
+      __syncthreads();
+      int pre = run + x - d;
+      for (int w = 0; w < wid; ++w) pre += s_w[w];
+      int tot = 0;
+      for (int w = 0; w < kPmThreads / 64; ++w) tot += s_w[w];
+      if (q < K) {
+        const long long id = d ? base + pre : -1;
+        if (ids_out) ids_out[row] = id;
+        if (d) {
+          const size_t i = sidx(st, ti, (int)sorted[(size_t)t * st.M + q]);
+          for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = r.lam[9 * (size_t)row + c];
+          for (int c = 0; c < 3; ++c) st.th[3 * i + c] = r.th[3 * (size_t)row + c];
+          for (int c = 0; c < ne; ++c) st.eta[(size_t)ne * i + c] = r.eta[(size_t)ne * row + c];
+          const double wn = r.w[row];
+          const int s = r.src ? r.src[row] : 1;
+          const double cam = wn * (s == 0 ? 1.0 : 0.0), lid = wn * (s == 1 ? 1.0 : 0.0);
+          double cn[3] = {0.0, 0.0, 0.0};
+          if (r.col)
+            for (int c = 0; c < 3; ++c) cn[c] = r.col[3 * (size_t)row + c];
+          for (int c = 0; c < 3; ++c) {
+            const double rg = cam > 0.0 ? clip01(cn[c]) : 0.5;
+            st.acc[3 * i + c] = cn[c] * cam;
+            st.col[3 * i + c] = rg;
+            st.rgb[3 * i + c] = rg;
+          }
+          st.w[i] = wn;
+          st.ids[i] = id;
+          st.cam[i] = cam;
+          st.lid[i] = lid;
+          st.den[i] = cam;
+          st.ts[i] = ts;
+          st.cts[i] = ts;
+          st.lsup[i] = seq;
+          st.lupd[i] = seq;
+          st.valid[i] = 1;
+        }
+      }
+      run += tot;
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) n_ins[t] = run;
+    base += run;
+  }
+}
+
+// fuse: key = (tile position, slot) for the rows that contribute (valid, tile listed)
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys(PmRows r, int n_tiles, int M, uint32_t* keys,
+                                                             uint32_t* vals, uint32_t* err) {
+  const int g = blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= r.n) return;
+  const int tp = r.tpos[g], q = r.slots[g];
+  const bool ok = q >= 0 && q < M;
+  if (!ok) err[0] = 1u;
+  const bool v = (r.valid ? r.valid[g] != 0 : true) && tp >= 0 && tp < n_tiles && ok;
+  keys[g] = v ? (uint32_t)tp * (uint32_t)M + (uint32_t)q : kNoKey;
+  vals[g] = (uint32_t)g;
+}
+
+// one lane per key run (sorted stable: rows in input order): d = sum r x from 0, then slot += d
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply(PmStore st, const int32_t* tiles, PmRows r,
+                                                              const uint32_t* keys, const uint32_t* vals,
+                                                              long long seq) {
+#pragma clang fp contract(off)
+  const int g = blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= r.n) return;
+  const uint32_t key = keys[g];
+  if (key == kNoKey || (g > 0 && keys[g - 1] == key)) return;
+  const int ne = 3 * st.nl;
+  double dL[9], dth[3], de[3 * 8], dw = 0.0, drs = 0.0, dcam = 0.0, dlid = 0.0, dacc[3] = {0.0, 0.0, 0.0}, dden = 0.0;
+  for (int c = 0; c < 9; ++c) dL[c] = 0.0;
+  for (int c = 0; c < 3; ++c) dth[c] = 0.0;
+  for (int c = 0; c < ne; ++c) de[c] = 0.0;
+  for (int p = g; p < r.n && keys[p] == key; ++p) {
+    const size_t row = vals[p];
+    const double rr = r.resp[row] * 1.0;  // resp * valid (valid here)
+    for (int c = 0; c < 9; ++c) dL[c] = dL[c] + rr * r.lam[9 * row + c];
+    for (int c = 0; c < 3; ++c) dth[c] = dth[c] + rr * r.th[3 * row + c];
+    for (int c = 0; c < ne; ++c) de[c] = de[c] + rr * r.eta[(size_t)ne * row + c];
+    const double rw = rr * r.w[row];
+    dw = dw + rw;
+    drs = drs + rr;
+    if (r.src) {
+      const int s = r.src[row];
+      const double wc = rw * (s == 0 ? 1.0 : 0.0);
+      dcam = dcam + wc;
+      dlid = dlid + rw * (s == 1 ? 1.0 : 0.0);
+      if (r.col) {
+        for (int c = 0; c < 3; ++c) dacc[c] = dacc[c] + clip01(r.col[3 * row + c]) * wc;
+        dden = dden + wc;
+      }
+    }
+  }
+  const int t = (int)(key / (uint32_t)st.M), q = (int)(key % (uint32_t)st.M);
+  const size_t i = sidx(st, tiles[t], q);
+  for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = st.lam[9 * i + c] + dL[c];
+  for (int c = 0; c < 3; ++c) {
+    st.th[3 * i + c] = st.th[3 * i + c] + dth[c];
+    st.acc[3 * i + c] = st.acc[3 * i + c] + dacc[c];
+  }
+  for (int c = 0; c < ne; ++c) st.eta[(size_t)ne * i + c] = st.eta[(size_t)ne * i + c] + de[c];
+  st.w[i] = st.w[i] + dw;
+  st.cam[i] = st.cam[i] + dcam;
+  st.lid[i] = st.lid[i] + dlid;
+  st.den[i] = st.den[i] + dden;
+  if (drs > 0.0) {
+    st.lsup[i] = seq;
+    st.lupd[i] = seq;
+  }
+}
+
+// every listed tile: rgb = where(cam > 0, clip(accum / max(denom, eps)), gray), colors = rgb (:1097-1105)
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_rgb(PmStore st, const int32_t* tiles, int n, double eps) {
+#pragma clang fp contract(off)
+  const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= (long)n * st.M) return;
+  const size_t i = sidx(st, tiles[g / st.M], (int)(g % st.M));
+  const double den = fmax(st.den[i], eps);
+  const bool cam = st.cam[i] > 0.0;
+  for (int c = 0; c < 3; ++c) {
+    const double v = cam ? clip01(st.acc[3 * i + c] / den) : 0.5;
+    st.rgb[3 * i + c] = v;
+    st.col[3 * i + c] = v;
+  }
+}
+
+// timestamps.at[unique(target_slots)].set(ts) in every listed tile (all rows' slots, :1112) and
+// the unique-slot flags for n_fused
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_ts(PmStore st, const int32_t* tiles, int n, PmRows r,
+                                                           double ts, uint8_t* mark) {
+  const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= (long)n * r.n) return;
+  const int t = (int)(g / r.n), row = (int)(g % r.n);
+  const int q = r.slots[row];
+  if (q < 0 || q >= st.M) return;
+  st.ts[sidx(st, tiles[t], q)] = ts;
+  if (t == 0) mark[q] = 1;
+}
+
+__global__ __launch_bounds__(kPmRed) void k_pm_count_marks(const uint8_t* mark, int M, int32_t* out) {
+  __shared__ double lds[kPmRed / 64];
+  double c = 0.0;
+  for (int q = threadIdx.x; q < M; q += kPmRed) c += mark[q] ? 1.0 : 0.0;
+  c = block_sum_d<kPmRed>(c, lds);
+  if (threadIdx.x == 0) out[0] = (int32_t)c;
+}
+
+// one workgroup per listed tile: valid count
+__global__ __launch_bounds__(kPmRed) void k_pm_count(PmStore st, const int32_t* tiles, int32_t* out) {
+  __shared__ double lds[kPmRed / 64];
+  const int ti = tiles[blockIdx.x];
+  double c = 0.0;
+  for (int q = threadIdx.x; q < st.M; q += kPmRed) c += st.valid[sidx(st, ti, q)] ? 1.0 : 0.0;
+  c = block_sum_d<kPmRed>(c, lds);
+  if (threadIdx.x == 0) out[blockIdx.x] = (int32_t)c;
+}
+
+// cull (:1217-1250): below = valid & w < thr -> invalid; culled count, mass dropped, sum of all weights,
+// valid count after (one workgroup per tile, fixed-order sums)
+__global__ __launch_bounds__(kPmRed) void k_pm_cull(PmStore st, const int32_t* tiles, double thr, int32_t* n_out,
+                                                    double* mass, double* wsum, int32_t* cnt) {
+  __shared__ double lds[kPmRed / 64];
+  const int ti = tiles[blockIdx.x];
+  double nb = 0.0, md = 0.0, ws = 0.0, nv = 0.0;
+  for (int q = threadIdx.x; q < st.M; q += kPmRed) {
+    const size_t i = sidx(st, ti, q);
+    const double w = st.w[i];
+    const bool v = st.valid[i] != 0;
+    const bool b = v && w < thr;
+    nb += b ? 1.0 : 0.0;
+    md += w * (b ? 1.0 : 0.0);
+    ws += w;
+    nv += (v && !b) ? 1.0 : 0.0;
+    if (b) st.valid[i] = 0;
+  }
+  nb = block_sum_d<kPmRed>(nb, lds);
+  md = block_sum_d<kPmRed>(md, lds);
+  ws = block_sum_d<kPmRed>(ws, lds);
+  nv = block_sum_d<kPmRed>(nv, lds);
+  if (threadIdx.x == 0) {
+    n_out[blockIdx.x] = (int32_t)nb;
+    mass[blockIdx.x] = md;
+    wsum[blockIdx.x] = ws;
+    cnt[blockIdx.x] = (int32_t)nv;
+  }
+}
+
+__global__ __launch_bounds__(kPmThreads) void k_pm_forget(PmStore st, const int32_t* tiles, int n, double gamma) {
+  const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= (long)n * st.M) return;
+  const size_t i = sidx(st, tiles[g / st.M], (int)(g % st.M));
+  st.w[i] = gamma * st.w[i];
+}
+
+// recency inflate (:1425-1463): decay = clip(exp(-lam dt), min_scale, 1) on valid slots; Lambda, theta
+// scaled; per tile [sum (1 - decay) valid, sum (1/decay - 1) valid, n_valid]
+__global__ __launch_bounds__(kPmRed) void k_pm_recency(PmStore st, const int32_t* tiles, long long seq, double lam,
+                                                       double min_scale, double* out) {
+#pragma clang fp contract(off)
+  __shared__ double lds[kPmRed / 64];
+  const int ti = tiles[blockIdx.x];
+  double dn = 0.0, inf = 0.0, nv = 0.0;
+  for (int q = threadIdx.x; q < st.M; q += kPmRed) {
+    const size_t i = sidx(st, ti, q);
+    const bool v = st.valid[i] != 0;
+    const long long dt = max(0ll, seq - st.lsup[i]);
+    double d = fmin(fmax(exp(-lam * (double)dt), min_scale), 1.0);
+    d = v ? d : 1.0;
+    for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = st.lam[9 * i + c] * d;
+    for (int c = 0; c < 3; ++c) st.th[3 * i + c] = st.th[3 * i + c] * d;
+    const double vf = v ? 1.0 : 0.0;
+    nv += vf;
+    dn += (1.0 - d) * vf;
+    inf += ((1.0 / d) - 1.0) * vf;
+  }
+  dn = block_sum_d<kPmRed>(dn, lds);
+  inf = block_sum_d<kPmRed>(inf, lds);
+  nv = block_sum_d<kPmRed>(nv, lds);
+  if (threadIdx.x == 0) {
+    out[3 * blockIdx.x] = dn;
+    out[3 * blockIdx.x + 1] = inf;
+    out[3 * blockIdx.x + 2] = nv;
+  }
+}
+
+// ---------------------------------------------------------------- merge-reduce
+__global__ __launch_bounds__(kPmThreads) void k_pm_merge_prep(PmStore st, int ti, double eps_lift, double* mu,
+                                                              double* Sig, double* det) {
+  const int q = blockIdx.x * kPmThreads + threadIdx.x;
+  if (q >= st.M) return;
+  const size_t i = sidx(st, ti, q);
+  double a[3][3], d;
+  int perm[3];
+  lu3(st.lam + 9 * i, eps_lift, a, perm, d);
+  lu3_solve(a, perm, st.th + 3 * i, mu + 3 * q);
+  double S[9];
+  lu3_inv(a, perm, S);
+  for (int c = 0; c < 9; ++c) Sig[9 * q + c] = S[c];
+  double b[3][3], dS;
+  int pb[3];
+  lu3(S, 0.0, b, pb, dS);
+  det[q] = dS;
+}
+
+// pair p of triu_indices(M, 1), row-major
+__device__ __forceinline__ void pair_ij(long p, int M, int& i, int& j) {
+  const double m2 = 2.0 * M - 1.0;
+  int ii = (int)floor((m2 - sqrt(m2 * m2 - 8.0 * (double)p)) * 0.5);
+  ii = max(0, min(ii, M - 2));
+  auto start = [M](long r) { return r * (2L * M - r - 1) / 2; };
+  while (ii > 0 && start(ii) > p) --ii;
+  while (ii < M - 2 && start(ii + 1) <= p) ++ii;
+  i = ii;
+  j = (int)(p - start(ii)) + ii + 1;
+}
+
+__global__ __launch_bounds__(kPmThreads) void k_pm_merge_dist(PmStore st, int ti, long P, double eps_lift,
+                                                              const double* mu, const double* Sig, const double* det,
+                                                              double* dist) {
+#pragma clang fp contract(off)
+  const long p = (long)blockIdx.x * kPmThreads + threadIdx.x;
+  if (p >= P) return;
+  int i, j;
+  pair_ij(p, st.M, i, j);
+  if (!(st.valid[sidx(st, ti, i)] && st.valid[sidx(st, ti, j)])) {
+    dist[p] = INFINITY;
+    return;
+  }
+  double S[9];
+  for (int c = 0; c < 9; ++c) S[c] = 0.5 * (Sig[9 * i + c] + Sig[9 * j + c]);
+  double a[3][3], dS;
+  int perm[3];
+  lu3(S, 0.0, a, perm, dS);
+  double b[3][3], dd;
+  int pb[3];
+  lu3(S, eps_lift, b, pb, dd);
+  double Si[9];
+  lu3_inv(b, pb, Si);
+  const double dm[3] = {mu[3 * i] - mu[3 * j], mu[3 * i + 1] - mu[3 * j + 1], mu[3 * i + 2] - mu[3 * j + 2]};
+  double row[3];
+  for (int c = 0; c < 3; ++c) row[c] = (dm[0] * Si[c] + dm[1] * Si[3 + c]) + dm[2] * Si[6 + c];
+  const double quad = 0.125 * ((row[0] * dm[0] + row[1] * dm[1]) + row[2] * dm[2]);
+  const double lt = 0.5 * log(dS / sqrt(det[i] * det[j] + 1e-24));
+  dist[p] = quad + lt;
+}
+
+struct MinKey {
+  double d;
+  long p;
+};
+__device__ __forceinline__ bool key_less(double d1, long p1, double d2, long p2) {
+  return d1 < d2 || (d1 == d2 && p1 < p2);
+}
+
+// one round: block argmin of (distance, pair) over the eligible pairs -> partials
+__global__ __launch_bounds__(kPmThreads) void k_pm_merge_min(PmStore st, long P, const double* dist, double thr,
+                                                             const uint8_t* used, double* pd, long long* pp) {
+  __shared__ double sd[kPmThreads];
+  __shared__ long long sp[kPmThreads];
+  double bd = INFINITY;
+  long bp = -1;
+  for (long p = (long)blockIdx.x * kPmThreads + threadIdx.x; p < P; p += (long)gridDim.x * kPmThreads) {
+    const double d = dist[p];
+    if (!(isfinite(d) && d < thr)) continue;
+    int i, j;
+    pair_ij(p, st.M, i, j);
+    if (used[i] || used[j]) continue;
+    if (bp < 0 || key_less(d, p, bd, bp)) {
+      bd = d;
+      bp = p;
+    }
+  }
+  sd[threadIdx.x] = bd;
+  sp[threadIdx.x] = bp;
+  __syncthreads();
+  for (int s = kPmThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      const long p2 = sp[threadIdx.x + s];
+      if (p2 >= 0 && (sp[threadIdx.x] < 0 || key_less(sd[threadIdx.x + s], p2, sd[threadIdx.x], sp[threadIdx.x]))) {
+        sd[threadIdx.x] = sd[threadIdx.x + s];
+        sp[threadIdx.x] = p2;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    pd[blockIdx.x] = sd[0];
+    pp[blockIdx.x] = sp[0];
+  }
+}
+
+__global__ void k_pm_merge_pick(int M, const double* pd, const long long* pp, int nblk, uint8_t* used, int32_t* sel,
+                                int32_t* n_sel) {
+  if (threadIdx.x != 0) return;
+  double bd = INFINITY;
+  long bp = -1;
+  for (int b = 0; b < nblk; ++b)
+    if (pp[b] >= 0 && (bp < 0 || key_less(pd[b], pp[b], bd, bp))) {
+      bd = pd[b];
+      bp = pp[b];
+    }
+  if (bp < 0) return;
+  int i, j;
+  pair_ij(bp, M, i, j);
+  used[i] = used[j] = 1;
+  const int k = n_sel[0];
+  sel[2 * k] = i;
+  sel[2 * k + 1] = j;
+  n_sel[0] = k + 1;
+}
+
+__global__ void k_pm_merge_apply(PmStore st, int ti, const int32_t* sel, const int32_t* n_sel, const double* mu,
+                                 const double* Sig, double eps_psd) {
+#pragma clang fp contract(off)
+  const int k = threadIdx.x;
+  if (k >= n_sel[0]) return;
+  const int qi = sel[2 * k], qj = sel[2 * k + 1];
+  const size_t i = sidx(st, ti, qi), j = sidx(st, ti, qj);
+  const double w1 = st.w[i], w2 = st.w[j], ws = w1 + w2;
+  if (!(ws > 0.0)) return;
+  double mm[3], d1[3], d2[3];
+  for (int c = 0; c < 3; ++c) mm[c] = (w1 * mu[3 * qi + c] + w2 * mu[3 * qj + c]) / ws;
+  for (int c = 0; c < 3; ++c) {
+    d1[c] = mu[3 * qi + c] - mm[c];
+    d2[c] = mu[3 * qj + c] - mm[c];
+  }
+  double Sm[9];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      Sm[3 * r + c] = (w1 * (Sig[9 * qi + 3 * r + c] + d1[r] * d1[c]) + w2 * (Sig[9 * qj + 3 * r + c] + d2[r] * d2[c])) /
+                          ws + (r == c ? eps_psd : 0.0);
+  double a[3][3], dt;
+  int perm[3];
+  lu3(Sm, 0.0, a, perm, dt);
+  double Lm[9];
+  lu3_inv(a, perm, Lm);
+  for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = Lm[c];
+  for (int r = 0; r < 3; ++r) st.th[3 * i + r] = (Lm[3 * r] * mm[0] + Lm[3 * r + 1] * mm[1]) + Lm[3 * r + 2] * mm[2];
+  const int ne = 3 * st.nl;
+  for (int c = 0; c < ne; ++c)
+    st.eta[(size_t)ne * i + c] = (w1 * st.eta[(size_t)ne * i + c] + w2 * st.eta[(size_t)ne * j + c]) / ws;
+  const double cam = st.cam[i] + st.cam[j];
+  const double den = st.den[i] + st.den[j];
+  for (int c = 0; c < 3; ++c) {
+    const double acc = st.acc[3 * i + c] + st.acc[3 * j + c];
+    const double rg = cam > 0.0 ? clip01(acc / fmax(den, eps_psd)) : 0.5;
+    st.acc[3 * i + c] = acc;
+    st.col[3 * i + c] = rg;
+    st.rgb[3 * i + c] = rg;
+  }
+  st.cam[i] = cam;
+  st.lid[i] = st.lid[i] + st.lid[j];
+  st.den[i] = den;
+  st.w[i] = ws;
+  st.ts[i] = fmax(st.ts[i], st.ts[j]);
+  st.cts[i] = fmin(st.cts[i], st.cts[j]);
+  st.lsup[i] = max(st.lsup[i], st.lsup[j]);
+  st.lupd[i] = max(st.lupd[i], st.lupd[j]);
+  st.w[j] = 0.0;
+  st.valid[j] = 0;
+}
+
+constexpr int kMergeBlocks = 512;
+
+}  // namespace
+}  // namespace gcs
+
+using namespace gcs;
+
+struct gcs_pmap {
+  int device = 0, M = 0, T = 0, nl = 3, max_merge = 0;
+  hipStream_t own = nullptr, stream = nullptr;
+  PmStore st{};
+  void* fields[GCS_PM_NFIELDS] = {};
+  // sort scratch (view / insert: T tiles x M slots)
+  uint64_t *keys = nullptr, *keys_s = nullptr;
+  uint32_t *vals = nullptr, *vals_s = nullptr;
+  int32_t *offs = nullptr, *d_tiles = nullptr;
+  int64_t* d_tids = nullptr;
+  void* temp = nullptr;
+  size_t temp_bytes = 0;
+  // fuse scratch (grown on demand)
+  uint32_t *fk = nullptr, *fk_s = nullptr, *fv = nullptr, *fv_s = nullptr;
+  void* ftemp = nullptr;
+  size_t ftemp_bytes = 0;
+  int frows = 0;
+  uint8_t* mark = nullptr;
+  // merge scratch
+  double *mmu = nullptr, *msig = nullptr, *mdet = nullptr, *mdist = nullptr, *mpd = nullptr;
+  long long* mpp = nullptr;
+  uint8_t* mused = nullptr;
+  int32_t *msel = nullptr, *mnsel = nullptr;
+  // small host-mapped results
+  char* h_small = nullptr;
+  char* d_small = nullptr;
+  std::string err;
+};
+
+namespace {
+constexpr size_t kSmall = 1 << 16;
+const int kFieldWidth[GCS_PM_NFIELDS] = {9, 3, -1, 1, 1, 1, 3, 1, 1, 3, 1, 3, 1, 1, 1, 1};
+const int kFieldBytes[GCS_PM_NFIELDS] = {8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 1};
+
+int pm_fail(gcs_pmap* p, int rc, const std::string& m) {
+  p->err = m;
+  return rc;
+}
+#define PMCHK(p, call)                                                                                   \
+  do {                                                                                                   \
+    hipError_t e_ = (call);                                                                              \
+    if (e_ != hipSuccess) return pm_fail(p, GCS_ERR_HIP, std::string(#call ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+size_t field_elems(const gcs_pmap* p, int f) {
+  const int w = kFieldWidth[f] < 0 ? 3 * p->nl : kFieldWidth[f];
+  return (size_t)p->M * w;
+}
+
+int check_tiles(gcs_pmap* p, const int32_t* tiles, int n, bool allow_missing) {
+  if (n < 0 || n > p->T) return pm_fail(p, GCS_ERR_ARG, "tile list longer than max_tiles");
+  if (n > 0 && !tiles) return pm_fail(p, GCS_ERR_ARG, "null tile list");
+  std::vector<char> seen(p->T, 0);
+  for (int i = 0; i < n; ++i) {
+    if (tiles[i] < 0 && allow_missing) continue;
+    if (tiles[i] < 0 || tiles[i] >= p->T) return pm_fail(p, GCS_ERR_ARG, "tile storage index out of range");
+    if (!allow_missing && seen[tiles[i]]) return pm_fail(p, GCS_ERR_ARG, "tile listed twice");
+    seen[tiles[i]] = 1;
+  }
+  return GCS_OK;
+}
+
+int upload_tiles(gcs_pmap* p, const int32_t* tiles, int n) {
+  if (n > 0) PMCHK(p, hipMemcpyAsync(p->d_tiles, tiles, n * sizeof(int32_t), hipMemcpyHostToDevice, p->stream));
+  return GCS_OK;
+}
+
+// stable per-tile sort of the slot keys (mode 0 view, 1 eviction); result in vals_s
+int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam) {
+  const long total = (long)n * p->M;
+  hipLaunchKernelGGL(k_pm_keys, dim3((unsigned)((std::max(total, (long)n + 1) + kPmThreads - 1) / kPmThreads)),
+                     dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, mode, seq, lam, p->keys,
+                     p->vals, p->offs);
+  size_t tb = p->temp_bytes;
+  PMCHK(p, rocprim::segmented_radix_sort_pairs(p->temp, tb, p->keys, p->keys_s, p->vals, p->vals_s, (unsigned)total,
+                                               (unsigned)n, p->offs, p->offs + 1, 0u, 64u, p->stream));
+  return GCS_OK;
+}
+
+PmRows rows_of(const gcs_pmap_rows* r) {
+  PmRows o{};
+  o.lam = r->Lambdas;
+  o.th = r->thetas;
+  o.eta = r->etas;
+  o.w = r->weights;
+  o.resp = r->responsibilities;
+  o.col = r->colors;
+  o.valid = r->valid;
+  o.src = r->sources;
+  o.tpos = r->tile_pos;
+  o.slots = r->slots;
+  o.n = r->n;
+  return o;
+}
+}  // namespace
+
+extern "C" {
+
+int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t max_merge, int32_t device,
+                    gcs_pmap** out) {
+  if (!out || m_tile < 1 || max_tiles < 1 || n_lobes < 1 || n_lobes > 8 || max_merge < 0) return GCS_ERR_ARG;
+  if ((long)m_tile * max_tiles >= (1L << 31)) return GCS_ERR_ARG;
+  gcs_pmap* p = new gcs_pmap();
+  p->device = device;
+  p->M = m_tile;
+  p->T = max_tiles;
+  p->nl = n_lobes;
+  p->max_merge = std::min(max_merge, m_tile);
+  auto bad = [&](hipError_t e) { return e != hipSuccess; };
+  auto fail = [&]() {
+    gcs_pmap_destroy(p);
+    return GCS_ERR_HIP;
+  };
+  if (bad(hipSetDevice(device)) || bad(hipStreamCreateWithFlags(&p->own, hipStreamNonBlocking))) return fail();
+  p->stream = p->own;
+  for (int f = 0; f < GCS_PM_NFIELDS; ++f)
+    if (bad(hipMalloc(&p->fields[f], field_elems(p, f) * kFieldBytes[f] * (size_t)max_tiles))) return fail();
+  PmStore& s = p->st;
+  s.lam = (double*)p->fields[GCS_PM_LAMBDAS];
+  s.th = (double*)p->fields[GCS_PM_THETAS];
+  s.eta = (double*)p->fields[GCS_PM_ETAS];
+  s.w = (double*)p->fields[GCS_PM_WEIGHTS];
+  s.ts = (double*)p->fields[GCS_PM_TIMESTAMPS];
+  s.cts = (double*)p->fields[GCS_PM_CREATED];
+  s.col = (double*)p->fields[GCS_PM_COLORS];
+  s.cam = (double*)p->fields[GCS_PM_CAM_MASS];
+  s.lid = (double*)p->fields[GCS_PM_LIDAR_MASS];
+  s.acc = (double*)p->fields[GCS_PM_RGB_ACCUM];
+  s.den = (double*)p->fields[GCS_PM_RGB_DENOM];
+  s.rgb = (double*)p->fields[GCS_PM_RGB];
+  s.lsup = (int64_t*)p->fields[GCS_PM_LAST_SUPPORTED];
+  s.lupd = (int64_t*)p->fields[GCS_PM_LAST_UPDATE];
+  s.ids = (int64_t*)p->fields[GCS_PM_IDS];
+  s.valid = (uint8_t*)p->fields[GCS_PM_VALID];
+  s.M = m_tile;
+  s.nl = n_lobes;
+  const size_t tot = (size_t)m_tile * max_tiles;
+  if (bad(hipMalloc(&p->keys, tot * 8)) || bad(hipMalloc(&p->keys_s, tot * 8)) || bad(hipMalloc(&p->vals, tot * 4)) ||
+      bad(hipMalloc(&p->vals_s, tot * 4)) || bad(hipMalloc(&p->offs, (max_tiles + 1) * 4)) ||
+      bad(hipMalloc(&p->d_tiles, max_tiles * 4)) || bad(hipMalloc(&p->d_tids, max_tiles * 8)) ||
+      bad(hipMalloc(&p->mark, m_tile)) ||
+      bad(hipHostMalloc((void**)&p->h_small, kSmall, hipHostMallocMapped)) ||
+      bad(hipHostGetDevicePointer((void**)&p->d_small, p->h_small, 0)))
+    return fail();
+  size_t tb = 0;
+  if (bad(rocprim::segmented_radix_sort_pairs(nullptr, tb, p->keys, p->keys_s, p->vals, p->vals_s, (unsigned)tot,
+                                              (unsigned)max_tiles, p->offs, p->offs + 1, 0u, 64u, p->stream)) ||
+      bad(hipMalloc(&p->temp, std::max<size_t>(tb, 16))))
+    return fail();
+  p->temp_bytes = std::max<size_t>(tb, 16);
+  if (p->max_merge >= 2) {
+    const long P = (long)p->max_merge * (p->max_merge - 1) / 2;
+    if (bad(hipMalloc(&p->mmu, (size_t)p->max_merge * 3 * 8)) || bad(hipMalloc(&p->msig, (size_t)p->max_merge * 9 * 8)) ||
+        bad(hipMalloc(&p->mdet, (size_t)p->max_merge * 8)) || bad(hipMalloc(&p->mdist, (size_t)P * 8)) ||
+        bad(hipMalloc(&p->mpd, kMergeBlocks * 8)) || bad(hipMalloc(&p->mpp, kMergeBlocks * 8)) ||
+        bad(hipMalloc(&p->mused, p->max_merge)) || bad(hipMalloc(&p->msel, 2 * 1024 * 4)) ||
+        bad(hipMalloc(&p->mnsel, 4)))
+      return fail();
+  }
+  for (int t = 0; t < max_tiles; ++t)
+    hipLaunchKernelGGL(k_pm_clear, dim3((m_tile + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream, p->st, t);
+  if (bad(hipStreamSynchronize(p->stream))) return fail();
+  *out = p;
+  return GCS_OK;
+}
+
+int gcs_pmap_destroy(gcs_pmap* p) {
+  if (!p) return GCS_ERR_ARG;
+  (void)hipSetDevice(p->device);
+  if (p->stream) (void)hipStreamSynchronize(p->stream);
+  for (void* f : p->fields)
+    if (f) (void)hipFree(f);
+  void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->offs, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
+                  p->fv, p->fv_s, p->ftemp, p->mark, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
+                  p->msel, p->mnsel};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (p->h_small) (void)hipHostFree(p->h_small);
+  if (p->own) (void)hipStreamDestroy(p->own);
+  delete p;
+  return GCS_OK;
+}
+
+const char* gcs_pmap_last_error(const gcs_pmap* p) { return p ? p->err.c_str() : "null map"; }
+
+int gcs_pmap_set_stream(gcs_pmap* p, void* stream) {
+  if (!p) return GCS_ERR_ARG;
+  PMCHK(p, hipSetDevice(p->device));
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  p->stream = stream ? (hipStream_t)stream : p->own;
+  return GCS_OK;
+}
+
+int gcs_pmap_clear_tile(gcs_pmap* p, int32_t tile) {
+  if (!p) return GCS_ERR_ARG;
+  if (tile < 0 || tile >= p->T) return pm_fail(p, GCS_ERR_ARG, "tile storage index out of range");
+  PMCHK(p, hipSetDevice(p->device));
+  hipLaunchKernelGGL(k_pm_clear, dim3((p->M + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream, p->st,
+                     tile);
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  return GCS_OK;
+}
+
+int gcs_pmap_read(gcs_pmap* p, int32_t tile, int32_t field, void* host) {
+  if (!p || !host || field < 0 || field >= GCS_PM_NFIELDS) return GCS_ERR_ARG;
+  if (tile < 0 || tile >= p->T) return pm_fail(p, GCS_ERR_ARG, "tile storage index out of range");
+  PMCHK(p, hipSetDevice(p->device));
+  const size_t b = field_elems(p, field) * kFieldBytes[field];
+  PMCHK(p, hipMemcpyAsync(host, (char*)p->fields[field] + b * tile, b, hipMemcpyDeviceToHost, p->stream));
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  return GCS_OK;
+}
+
+int gcs_pmap_write(gcs_pmap* p, int32_t tile, int32_t field, const void* host) {
+  if (!p || !host || field < 0 || field >= GCS_PM_NFIELDS) return GCS_ERR_ARG;
+  if (tile < 0 || tile >= p->T) return pm_fail(p, GCS_ERR_ARG, "tile storage index out of range");
+  PMCHK(p, hipSetDevice(p->device));
+  const size_t b = field_elems(p, field) * kFieldBytes[field];
+  PMCHK(p, hipMemcpyAsync((char*)p->fields[field] + b * tile, host, b, hipMemcpyHostToDevice, p->stream));
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  return GCS_OK;
+}
+
+int gcs_pmap_extract_view(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_ids, int32_t n, int32_t m_view,
+                          double eps_lift, double eps_mass, gcs_pmap_view* o) {
+  if (!p || !o || !tile_ids) return GCS_ERR_ARG;
+  if (m_view <= 0) return pm_fail(p, GCS_ERR_ARG, "extract_atlas_map_view: m_tile_view must be > 0");
+  if (m_view > p->M) return pm_fail(p, GCS_ERR_ARG, "m_tile_view exceeds the tile size");
+  if (int rc = check_tiles(p, tiles, n, true)) return rc;
+  if (n == 0) return GCS_OK;
+  PMCHK(p, hipSetDevice(p->device));
+  if (int rc = upload_tiles(p, tiles, n)) return rc;
+  PMCHK(p, hipMemcpyAsync(p->d_tids, tile_ids, n * sizeof(int64_t), hipMemcpyHostToDevice, p->stream));
+  if (int rc = sort_tiles(p, n, 0, 0, 0.0)) return rc;
+  PmViewOut v{o->positions, o->covariances, o->directions, o->kappas, o->weights, o->etas, o->colors,
+              o->primitive_ids, o->last_supported_scan_seq, o->candidate_tile_ids, o->valid_mask,
+              o->candidate_slots};
+  hipLaunchKernelGGL(k_pm_view, dim3((n * m_view + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream,
+                     p->st, (const int32_t*)p->d_tiles, (const int64_t*)p->d_tids, n, m_view,
+                     (const uint32_t*)p->vals_s, eps_lift, eps_mass, v);
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  return GCS_OK;
+}
+
+int gcs_pmap_insert_masked(gcs_pmap* p, const int32_t* tiles, int32_t n, int32_t K, const gcs_pmap_rows* rows,
+                           double timestamp, int64_t scan_seq, double lam, int64_t next_global_id, int64_t* new_ids,
+                           int32_t* n_inserted, int32_t* count) {
+  if (!p || !rows || !n_inserted || !count) return GCS_ERR_ARG;
+  if (int rc = check_tiles(p, tiles, n, false)) return rc;
+  if (K < 0 || K > p->M) return pm_fail(p, GCS_ERR_ARG, "K proposals exceed the tile size");
+  if (rows->n != n * K) return pm_fail(p, GCS_ERR_ARG, "rows.n must be n_tiles x K");
+  if (n * K > 0 && (!rows->Lambdas || !rows->thetas || !rows->etas || !rows->weights || !rows->valid))
+    return pm_fail(p, GCS_ERR_ARG, "null proposal array");
+  if (n == 0) return GCS_OK;
+  PMCHK(p, hipSetDevice(p->device));
+  if (int rc = upload_tiles(p, tiles, n)) return rc;
+  int32_t* d_ins = (int32_t*)p->d_small;
+  int32_t* d_cnt = (int32_t*)(p->d_small + 4096);
+  if (K > 0) {
+    if (int rc = sort_tiles(p, n, 1, scan_seq, lam)) return rc;
+    hipLaunchKernelGGL(k_pm_insert, dim3(1), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, K,
+                       (const uint32_t*)p->vals_s, rows_of(rows), timestamp, (long long)scan_seq,
+                       (long long)next_global_id, new_ids, d_ins);
+  } else {
+    PMCHK(p, hipMemsetAsync(d_ins, 0, n * sizeof(int32_t), p->stream));
+  }
+  hipLaunchKernelGGL(k_pm_count, dim3(n), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles, d_cnt);
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  memcpy(n_inserted, p->h_small, n * sizeof(int32_t));
+  memcpy(count, p->h_small + 4096, n * sizeof(int32_t));
+  return GCS_OK;
+}
+
+int gcs_pmap_fuse(gcs_pmap* p, const int32_t* tiles, int32_t n, const gcs_pmap_rows* rows, double timestamp,
+                  int64_t scan_seq, double eps_mass, int32_t* n_fused) {
+  if (!p || !rows || !n_fused) return GCS_ERR_ARG;
+  if (int rc = check_tiles(p, tiles, n, false)) return rc;
+  const int R = rows->n;
+  if (R < 0) return GCS_ERR_ARG;
+  *n_fused = 0;
+  if (R == 0 || n == 0) return GCS_OK;  // K == 0: the reference's exact no-op
+  if (!rows->Lambdas || !rows->thetas || !rows->etas || !rows->weights || !rows->responsibilities ||
+      !rows->tile_pos || !rows->slots)
+    return pm_fail(p, GCS_ERR_ARG, "null contribution array");
+  PMCHK(p, hipSetDevice(p->device));
+  if (R > p->frows) {
+    for (void* b : {(void*)p->fk, (void*)p->fk_s, (void*)p->fv, (void*)p->fv_s, p->ftemp})
+      if (b) (void)hipFree(b);
+    p->fk = p->fk_s = p->fv = p->fv_s = nullptr;
+    p->ftemp = nullptr;
+    const int cap = std::max(R, 16384);
+    PMCHK(p, hipMalloc(&p->fk, cap * 4));
+    PMCHK(p, hipMalloc(&p->fk_s, cap * 4));
+    PMCHK(p, hipMalloc(&p->fv, cap * 4));
+    PMCHK(p, hipMalloc(&p->fv_s, cap * 4));
+    size_t tb = 0;
+    PMCHK(p, rocprim::radix_sort_pairs(nullptr, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)cap, 0u, 32u, p->stream));
+    p->ftemp_bytes = std::max<size_t>(tb, 16);
+    PMCHK(p, hipMalloc(&p->ftemp, p->ftemp_bytes));
+    p->frows = cap;
+  }
+  if (int rc = upload_tiles(p, tiles, n)) return rc;
+  uint32_t* d_err = (uint32_t*)(p->d_small + 8192);
+  int32_t* d_nf = (int32_t*)(p->d_small + 8200);
+  *(uint32_t*)(p->h_small + 8192) = 0u;
+  const PmRows r = rows_of(rows);
+  const int rb = (R + kPmThreads - 1) / kPmThreads;
+  hipLaunchKernelGGL(k_pm_fuse_keys, dim3(rb), dim3(kPmThreads), 0, p->stream, r, n, p->M, p->fk, p->fv, d_err);
+  size_t tb = p->ftemp_bytes;
+  PMCHK(p, rocprim::radix_sort_pairs(p->ftemp, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)R, 0u, 32u, p->stream));
+  hipLaunchKernelGGL(k_pm_fuse_apply, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, r,
+                     (const uint32_t*)p->fk_s, (const uint32_t*)p->fv_s, (long long)scan_seq);
+  const long tm = (long)n * p->M;
+  hipLaunchKernelGGL(k_pm_fuse_rgb, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
+                     p->stream, p->st, (const int32_t*)p->d_tiles, n, eps_mass);
+  PMCHK(p, hipMemsetAsync(p->mark, 0, p->M, p->stream));
+  const long tr = (long)n * R;
+  hipLaunchKernelGGL(k_pm_fuse_ts, dim3((unsigned)((tr + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
+                     p->stream, p->st, (const int32_t*)p->d_tiles, n, r, timestamp, p->mark);
+  hipLaunchKernelGGL(k_pm_count_marks, dim3(1), dim3(kPmRed), 0, p->stream, (const uint8_t*)p->mark, p->M, d_nf);
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  if (*(uint32_t*)(p->h_small + 8192)) return pm_fail(p, GCS_ERR_ARG, "target slot out of range (rows skipped)");
+  *n_fused = *(int32_t*)(p->h_small + 8200);
+  return GCS_OK;
+}
+
+int gcs_pmap_cull(gcs_pmap* p, const int32_t* tiles, int32_t n, double thr, int32_t* n_culled, double* mass_dropped,
+                  double* weight_sum, int32_t* count) {
+  if (!p || !n_culled || !mass_dropped || !weight_sum || !count) return GCS_ERR_ARG;
+  if (int rc = check_tiles(p, tiles, n, false)) return rc;
+  if (n == 0) return GCS_OK;
+  PMCHK(p, hipSetDevice(p->device));
+  if (int rc = upload_tiles(p, tiles, n)) return rc;
+  char* d = p->d_small + 16384;
+  hipLaunchKernelGGL(k_pm_cull, dim3(n), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles, thr,
+                     (int32_t*)d, (double*)(d + 4096), (double*)(d + 8192), (int32_t*)(d + 12288));
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  const char* h = p->h_small + 16384;
+  memcpy(n_culled, h, n * 4);
+  memcpy(mass_dropped, h + 4096, n * 8);
+  memcpy(weight_sum, h + 8192, n * 8);
+  memcpy(count, h + 12288, n * 4);
+  return GCS_OK;
+}
+
+int gcs_pmap_forget(gcs_pmap* p, const int32_t* tiles, int32_t n, double gamma) {
+  if (!p) return GCS_ERR_ARG;
+  if (int rc = check_tiles(p, tiles, n, false)) return rc;
+  if (n == 0) return GCS_OK;
+  PMCHK(p, hipSetDevice(p->device));
+  if (int rc = upload_tiles(p, tiles, n)) return rc;
+  const long tm = (long)n * p->M;
+  hipLaunchKernelGGL(k_pm_forget, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
+                     p->stream, p->st, (const int32_t*)p->d_tiles, n, gamma);
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  return GCS_OK;
+}
+
+int gcs_pmap_recency_inflate(gcs_pmap* p, const int32_t* tiles, int32_t n, int64_t scan_seq, double lam,
+                             double min_scale, double* stats) {
+  if (!p || !stats) return GCS_ERR_ARG;
+  if (int rc = check_tiles(p, tiles, n, false)) return rc;
+  stats[0] = stats[1] = stats[2] = 0.0;
+  if (n == 0) return GCS_OK;
+  PMCHK(p, hipSetDevice(p->device));
+  if (int rc = upload_tiles(p, tiles, n)) return rc;
+  double* d = (double*)(p->d_small + 32768);
+  hipLaunchKernelGGL(k_pm_recency, dim3(n), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
+                     (long long)scan_seq, lam, min_scale, d);
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  const double* h = (const double*)(p->h_small + 32768);
+  for (int t = 0; t < n; ++t)  // the reference's Python float sums, tile by tile
+    for (int k = 0; k < 3; ++k) stats[k] += h[3 * t + k];
+  return GCS_OK;
+}
+
+int gcs_pmap_merge_reduce(gcs_pmap* p, int32_t tile, double thr, int32_t max_pairs, double eps_psd, double eps_lift,
+                          int32_t* n_merged, int32_t* pairs, int32_t* count) {
+  if (!p || !n_merged || !count || (max_pairs > 0 && !pairs)) return GCS_ERR_ARG;
+  if (tile < 0 || tile >= p->T) return pm_fail(p, GCS_ERR_ARG, "tile storage index out of range");
+  if (p->M > p->max_merge) return pm_fail(p, GCS_ERR_ARG, "tile larger than the context's max_merge");
+  if (max_pairs > 1024) return pm_fail(p, GCS_ERR_ARG, "max_pairs above 1024");
+  *n_merged = 0;
+  PMCHK(p, hipSetDevice(p->device));
+  const int32_t tl[1] = {tile};
+  if (int rc = upload_tiles(p, tl, 1)) return rc;
+  const int M = p->M;
+  const long P = (long)M * (M - 1) / 2;
+  if (max_pairs > 0 && P > 0) {
+    hipLaunchKernelGGL(k_pm_merge_prep, dim3((M + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream,
+                       p->st, tile, eps_lift, p->mmu, p->msig, p->mdet);
+    hipLaunchKernelGGL(k_pm_merge_dist, dim3((unsigned)((P + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
+                       p->stream, p->st, tile, P, eps_lift, (const double*)p->mmu, (const double*)p->msig,
+                       (const double*)p->mdet, p->mdist);
+    PMCHK(p, hipMemsetAsync(p->mused, 0, M, p->stream));
+    PMCHK(p, hipMemsetAsync(p->mnsel, 0, 4, p->stream));
+    const int nb = (int)std::min<long>(kMergeBlocks, (P + kPmThreads - 1) / kPmThreads);
+    for (int k = 0; k < max_pairs; ++k) {
+      hipLaunchKernelGGL(k_pm_merge_min, dim3(nb), dim3(kPmThreads), 0, p->stream, p->st, P, (const double*)p->mdist,
+                         thr, (const uint8_t*)p->mused, p->mpd, p->mpp);
+      hipLaunchKernelGGL(k_pm_merge_pick, dim3(1), dim3(64), 0, p->stream, M, (const double*)p->mpd,
+                         (const long long*)p->mpp, nb, p->mused, p->msel, p->mnsel);
+    }
+    hipLaunchKernelGGL(k_pm_merge_apply, dim3(1), dim3(1024), 0, p->stream, p->st, tile, (const int32_t*)p->msel,
+                       (const int32_t*)p->mnsel, (const double*)p->mmu, (const double*)p->msig, eps_psd);
+    PMCHK(p, hipMemcpyAsync(n_merged, p->mnsel, 4, hipMemcpyDeviceToHost, p->stream));
+    PMCHK(p, hipMemcpyAsync(pairs, p->msel, 2 * max_pairs * 4, hipMemcpyDeviceToHost, p->stream));
+  }
+  hipLaunchKernelGGL(k_pm_count, dim3(1), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
+                     (int32_t*)(p->d_small + 40960));
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  *count = *(int32_t*)(p->h_small + 40960);
+  return GCS_OK;
+}
+
+}  // extern "C"

@@ -131,6 +131,23 @@ class GcsAssocView(C.Structure):
                                           "last_supported_scan_seq", "candidate_tile_ids", "candidate_slots")]
 
 
+# primitive map (gcs_pmap_*): field codes, view outputs and proposal / contribution rows
+PM_FIELDS = ("Lambdas", "thetas", "etas", "weights", "timestamps", "created_timestamps", "colors", "cam_mass",
+             "lidar_mass", "rgb_cam_accum", "rgb_cam_denom", "rgb", "last_supported_scan_seq", "last_update_scan_seq",
+             "primitive_ids", "valid_mask")
+
+
+class GcsPmapView(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("positions", "covariances", "directions", "kappas", "weights",
+                                          "primitive_ids", "valid_mask", "last_supported_scan_seq", "etas", "colors",
+                                          "candidate_slots", "candidate_tile_ids")]
+
+
+class GcsPmapRows(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("Lambdas", "thetas", "etas", "weights", "responsibilities", "valid",
+                                          "colors", "sources", "tile_pos", "slots")] + [("n", C.c_int32)]
+
+
 class GcsAssocOutputs(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("responsibilities", "candidate_pool_indices", "candidate_tile_ids",
                                           "candidate_slots", "row_masses", "cost_matrix")] + \
@@ -223,6 +240,27 @@ _SIGS = [
     ("gcs_assoc_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("gcs_associate_primitives_ot", C.c_int, [C.c_void_p, C.POINTER(GcsAssocConfig), C.POINTER(GcsAssocMeas),
                                               C.POINTER(GcsAssocView), C.POINTER(GcsAssocOutputs)]),
+    ("gcs_pmap_create", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
+    ("gcs_pmap_destroy", C.c_int, [C.c_void_p]),
+    ("gcs_pmap_last_error", C.c_char_p, [C.c_void_p]),
+    ("gcs_pmap_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("gcs_pmap_clear_tile", C.c_int, [C.c_void_p, C.c_int32]),
+    ("gcs_pmap_read", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
+    ("gcs_pmap_write", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
+    ("gcs_pmap_extract_view", C.c_int, [C.c_void_p, c_int32_p, c_int64_p, C.c_int32, C.c_int32, C.c_double,
+                                        C.c_double, C.POINTER(GcsPmapView)]),
+    ("gcs_pmap_insert_masked", C.c_int, [C.c_void_p, c_int32_p, C.c_int32, C.c_int32, C.POINTER(GcsPmapRows),
+                                         C.c_double, C.c_int64, C.c_double, C.c_int64, C.c_void_p, c_int32_p,
+                                         c_int32_p]),
+    ("gcs_pmap_fuse", C.c_int, [C.c_void_p, c_int32_p, C.c_int32, C.POINTER(GcsPmapRows), C.c_double, C.c_int64,
+                                C.c_double, c_int32_p]),
+    ("gcs_pmap_cull", C.c_int, [C.c_void_p, c_int32_p, C.c_int32, C.c_double, c_int32_p, c_double_p, c_double_p,
+                                c_int32_p]),
+    ("gcs_pmap_forget", C.c_int, [C.c_void_p, c_int32_p, C.c_int32, C.c_double]),
+    ("gcs_pmap_recency_inflate", C.c_int, [C.c_void_p, c_int32_p, C.c_int32, C.c_int64, C.c_double, C.c_double,
+                                           c_double_p]),
+    ("gcs_pmap_merge_reduce", C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_int32, C.c_double, C.c_double,
+                                        c_int32_p, c_int32_p, c_int32_p]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]

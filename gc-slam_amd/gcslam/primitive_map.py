@@ -1,0 +1,497 @@
+"""The live primitive path's map on the MI355X: the AtlasMap's tiles resident
+in HBM and the maintenance operators with the reference's calling conventions
+(FS/backend/structures/primitive_map.py), running gcs_pmap_* (libgcslam_hip.so):
+
+  extract_atlas_map_view         :356-450   -> gcslam.association.AtlasMapView (device tensors)
+  primitive_map_insert_masked    :807-981   (+ primitive_map_insert_masked_tiles: several tiles, one call)
+  primitive_map_fuse             :992-1163  (+ primitive_map_fuse_tiles: the pipeline's active-tile loop,
+                                             pipeline.py:1301-1327, in one call)
+  primitive_map_cull             :1175-1304
+  primitive_map_forget           :1314-1384
+  primitive_map_recency_inflate  :1400-1484
+  primitive_map_merge_reduce     :1809-2031
+
+Each operator returns the reference's (result, CertBundle, ExpectedEffect).  The reference's
+AtlasMap is immutable (every operator returns a new one); this one is updated in place on the GPU
+and result.atlas_map is the same object.  Inputs may be numpy arrays or device tensors.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib as L
+from .association import AtlasMapView
+from .certificates import CertBundle, ExpectedEffect, InfluenceCert
+
+CHART_ID = "GC-RIGHT-01"
+GC_EPS_LIFT = 1e-9
+GC_EPS_MASS = 1e-12
+GC_EPS_PSD = 1e-12
+GC_VMF_N_LOBES = 3                          # constants.py:463
+GC_PRIMITIVE_MAP_MAX_SIZE = 50000           # constants.py:392 (= GC_M_TILE)
+GC_RECENCY_DECAY_LAMBDA = 0.02              # constants.py:419
+GC_RECENCY_MIN_SCALE = 0.05                 # constants.py:420
+GC_PRIMITIVE_FORGETTING_FACTOR = 0.995      # constants.py:442
+GC_PRIMITIVE_MERGE_THRESHOLD = 0.1          # constants.py:445
+GC_K_MERGE_PAIRS_PER_TILE = 4               # constants.py:448
+GC_PRIMITIVE_MERGE_MAX_TILE_SIZE = 2048     # constants.py:450
+GC_PRIMITIVE_CULL_WEIGHT_THRESHOLD = 1e-4   # constants.py:453
+GC_FUSE_CHUNK_SIZE = 1024                   # constants.py:470
+
+_DT = {"f": np.float64, "i": np.int64, "u": np.uint8}
+_KIND = ["f"] * 12 + ["i"] * 3 + ["u"]
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class AtlasMap:
+    """primitive_map.py:182-211: tile_id -> tile; here the tiles live in one gcs_pmap context on
+    `device` (max_tiles storage slots of m_tile primitives) and `tiles` maps tile ids to storage
+    indices.  next_global_id / total_count follow the reference's bookkeeping."""
+
+    def __init__(self, m_tile: int = GC_PRIMITIVE_MAP_MAX_SIZE, max_tiles: int = 64, n_lobes: int = GC_VMF_N_LOBES,
+                 max_merge: int = GC_PRIMITIVE_MERGE_MAX_TILE_SIZE, device: int = 0):
+        self.lib = L.load()
+        h = C.c_void_p()
+        rc = self.lib.gcs_pmap_create(int(m_tile), int(max_tiles), int(n_lobes), int(max_merge), int(device),
+                                      C.byref(h))
+        if rc != 0:
+            raise (ValueError if rc == -1 else RuntimeError)(f"gcs_pmap_create failed ({rc})")
+        self.h = h
+        self.m_tile, self.max_tiles, self.n_lobes, self.device = int(m_tile), int(max_tiles), int(n_lobes), int(device)
+        self.tiles = {}
+        self.counts = {}
+        self.next_global_id = 0
+        self.total_count = 0
+        self._free = list(range(self.max_tiles))
+
+    # ------------------------------------------------------------------ plumbing
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.gcs_pmap_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc, what):
+        if rc != 0:
+            msg = self.lib.gcs_pmap_last_error(self.h).decode(errors="replace")
+            raise (ValueError if rc in (-1, -3) else RuntimeError)(f"{what} failed ({rc}): {msg}")
+
+    def _stream(self):
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        self._chk(self.lib.gcs_pmap_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                  "gcs_pmap_set_stream")
+
+    @property
+    def n_tiles(self) -> int:
+        return len(self.tiles)
+
+    @property
+    def tile_ids(self) -> List[int]:
+        return list(self.tiles.keys())
+
+    def index(self, tile_id: int, create: bool = True) -> int:
+        """Storage index of tile_id (create_empty_tile on first use, :148-174); -1 if absent."""
+        tid = int(tile_id)
+        if tid in self.tiles:
+            return self.tiles[tid]
+        if not create:
+            return -1
+        if not self._free:
+            raise RuntimeError(f"primitive map holds max_tiles={self.max_tiles} tiles")
+        idx = self._free.pop(0)
+        self._chk(self.lib.gcs_pmap_clear_tile(self.h, idx), "gcs_pmap_clear_tile")
+        self.tiles[tid] = idx
+        self.counts[tid] = 0
+        return idx
+
+    def _width(self, f):
+        return {"Lambdas": (3, 3), "thetas": (3,), "etas": (self.n_lobes, 3), "colors": (3,), "rgb_cam_accum": (3,),
+                "rgb": (3,)}.get(f, ())
+
+    def read_tile(self, tile_id: int) -> dict:
+        """The tile's arrays (reference field names and shapes) as numpy."""
+        idx = self.index(tile_id, create=False)
+        if idx < 0:
+            raise KeyError(tile_id)
+        out = {}
+        for k, f in enumerate(L.PM_FIELDS):
+            a = np.empty((self.m_tile,) + self._width(f), dtype=_DT[_KIND[k]])
+            self._chk(self.lib.gcs_pmap_read(self.h, idx, k, a.ctypes.data), "gcs_pmap_read")
+            out[f] = a.astype(bool) if f == "valid_mask" else a
+        return out
+
+    def write_tile(self, tile_id: int, arrays: dict):
+        """Upload a tile (reference field names; missing fields keep their values)."""
+        idx = self.index(tile_id, create=True)
+        for k, f in enumerate(L.PM_FIELDS):
+            if f in arrays:
+                a = np.ascontiguousarray(np.asarray(arrays[f]).astype(_DT[_KIND[k]]).reshape(
+                    (self.m_tile,) + self._width(f)))
+                self._chk(self.lib.gcs_pmap_write(self.h, idx, k, a.ctypes.data), "gcs_pmap_write")
+        if "valid_mask" in arrays:
+            n = int(np.asarray(arrays["valid_mask"]).sum())
+            self.total_count += n - self.counts.get(int(tile_id), 0)
+            self.counts[int(tile_id)] = n
+
+
+def create_empty_atlas_map(m_tile: int = GC_PRIMITIVE_MAP_MAX_SIZE, max_tiles: int = 64, device: int = 0) -> AtlasMap:
+    """primitive_map.py:214-227 (tiles are created on demand)."""
+    return AtlasMap(m_tile=m_tile, max_tiles=max_tiles, device=device)
+
+
+# ---------------------------------------------------------------------- results (reference dataclasses)
+@dataclass
+class PrimitiveMapInsertResult:      # :642-648
+    atlas_map: AtlasMap
+    tile_id: int
+    n_inserted: int
+    new_ids: object
+
+
+@dataclass
+class PrimitiveMapFuseResult:        # :984-989
+    atlas_map: AtlasMap
+    tile_id: int
+    n_fused: int
+
+
+@dataclass
+class PrimitiveMapCullResult:        # :1166-1172
+    atlas_map: AtlasMap
+    tile_id: int
+    n_culled: int
+    mass_dropped: float
+
+
+@dataclass
+class PrimitiveMapForgetResult:      # :1307-1311
+    atlas_map: AtlasMap
+    tile_id: int
+
+
+@dataclass
+class PrimitiveMapRecencyInflateStats:   # :1392-1397
+    staleness_inflation_strength: float
+    staleness_cov_inflation_trace: float
+    stale_precision_downscale_total: float
+
+
+@dataclass
+class PrimitiveMapMergeReduceResult:     # :1492-1498
+    atlas_map: AtlasMap
+    tile_id: int
+    n_merged: int
+    frobenius_correction: float
+
+
+def _exact(chart_id, anchor_id, name, predicted=0.0, realized=0.0):
+    return CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id), ExpectedEffect(name, predicted, realized)
+
+
+class _Rows:
+    """Device staging of proposal / contribution rows (kept alive for the call)."""
+
+    def __init__(self, atlas: AtlasMap, n: int, Lambdas, thetas, etas, weights, valid=None, responsibilities=None,
+                 colors=None, sources=None, tile_pos=None, slots=None):
+        torch = _torch()
+        dev = f"cuda:{atlas.device}"
+        f64 = lambda x: torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x,  # noqa: E731
+                                        device=dev).to(torch.float64).contiguous()
+        i32 = lambda x: torch.as_tensor(np.asarray(x) if not torch.is_tensor(x) else x,  # noqa: E731
+                                        device=dev).to(torch.int32).contiguous()
+        self.keep = []
+        r = L.GcsPmapRows()
+        r.n = int(n)
+
+        def put(name, t):
+            self.keep.append(t)
+            setattr(r, name, t.data_ptr() if t.numel() else None)
+
+        put("Lambdas", f64(Lambdas).reshape(n, 9))
+        put("thetas", f64(thetas).reshape(n, 3))
+        put("etas", f64(etas).reshape(n, -1) if n else f64(etas))
+        put("weights", f64(weights).reshape(n))
+        if valid is not None:
+            put("valid", torch.as_tensor(np.asarray(valid) if not torch.is_tensor(valid) else valid,
+                                         device=dev).to(torch.uint8).reshape(n).contiguous())
+        if responsibilities is not None:
+            put("responsibilities", f64(responsibilities).reshape(n))
+        if colors is not None:
+            put("colors", f64(colors).reshape(n, 3))
+        if sources is not None:
+            put("sources", i32(sources).reshape(n))
+        if tile_pos is not None:
+            put("tile_pos", i32(tile_pos).reshape(n))
+        if slots is not None:
+            put("slots", i32(slots).reshape(n))
+        self.rows = r
+
+
+def _tiles_arg(idx):
+    a = np.ascontiguousarray(np.asarray(idx, dtype=np.int32))
+    return a, L.iptr(a)
+
+
+# ---------------------------------------------------------------------- operators
+def extract_atlas_map_view(atlas_map: AtlasMap, tile_ids: List[int], m_tile_view: int,
+                           eps_lift: float = GC_EPS_LIFT, eps_mass: float = GC_EPS_MASS) -> AtlasMapView:
+    """:356-450: per listed tile the top m_tile_view slots by weight (stable on -score; a missing tile
+    is viewed as empty), stitched in tile order, with means, covariances, resultant directions and
+    kappas (:474-498)."""
+    if int(m_tile_view) <= 0:
+        raise ValueError(f"extract_atlas_map_view: m_tile_view must be > 0, got {m_tile_view}")
+    torch = _torch()
+    dev = f"cuda:{atlas_map.device}"
+    n, k = len(tile_ids), int(m_tile_view)
+    R = n * k
+    t = dict(positions=torch.empty((R, 3), dtype=torch.float64, device=dev),
+             covariances=torch.empty((R, 3, 3), dtype=torch.float64, device=dev),
+             directions=torch.empty((R, 3), dtype=torch.float64, device=dev),
+             kappas=torch.empty((R,), dtype=torch.float64, device=dev),
+             weights=torch.empty((R,), dtype=torch.float64, device=dev),
+             primitive_ids=torch.empty((R,), dtype=torch.int64, device=dev),
+             valid_mask=torch.empty((R,), dtype=torch.uint8, device=dev),
+             last_supported_scan_seq=torch.empty((R,), dtype=torch.int64, device=dev),
+             etas=torch.empty((R, atlas_map.n_lobes, 3), dtype=torch.float64, device=dev),
+             colors=torch.empty((R, 3), dtype=torch.float64, device=dev),
+             candidate_slots=torch.empty((R,), dtype=torch.int32, device=dev),
+             candidate_tile_ids=torch.empty((R,), dtype=torch.int64, device=dev))
+    v = L.GcsPmapView()
+    for name, x in t.items():
+        setattr(v, name, x.data_ptr() if R else None)
+    idx, ip = _tiles_arg([atlas_map.index(tid, create=False) for tid in tile_ids])
+    tids = np.ascontiguousarray(np.asarray(tile_ids, dtype=np.int64))
+    atlas_map._stream()
+    atlas_map._chk(atlas_map.lib.gcs_pmap_extract_view(atlas_map.h, ip, tids.ctypes.data_as(L.c_int64_p), n, k,
+                                                       float(eps_lift), float(eps_mass), C.byref(v)),
+                   "gcs_pmap_extract_view")
+    t["valid_mask"] = t["valid_mask"].to(torch.bool)
+    return AtlasMapView(tile_ids=torch.as_tensor(tids, device=dev), m_tile_view=k, **t)
+
+
+def primitive_map_insert_masked_tiles(atlas_map: AtlasMap, tile_ids: List[int], Lambdas_new, thetas_new, etas_new,
+                                      weights_new, timestamp: float, valid_new_mask, scan_seq: int = 0,
+                                      recency_decay_lambda: float = GC_RECENCY_DECAY_LAMBDA, colors_new=None,
+                                      sources_new=None, chart_id: str = CHART_ID,
+                                      anchor_id: str = "primitive_map_insert_masked"):
+    """primitive_map_insert_masked on each listed tile in order with its K proposals (arrays
+    (n_tiles, K, ...)); ids continue from next_global_id tile by tile, as the pipeline's loop
+    (pipeline.py:1348-1392).  Returns one (result, cert, effect) per tile."""
+    torch = _torch()
+    n = len(tile_ids)
+    wn = weights_new if torch.is_tensor(weights_new) else np.asarray(weights_new, np.float64)
+    K = int(wn.shape[1]) if n else 0
+    if K > atlas_map.m_tile:
+        raise ValueError("K proposals exceed the tile size")
+    idx, ip = _tiles_arg([atlas_map.index(tid, create=True) for tid in tile_ids])
+    rows = _Rows(atlas_map, n * K, Lambdas_new, thetas_new, etas_new, weights_new, valid=valid_new_mask,
+                 colors=colors_new, sources=sources_new)
+    dev = f"cuda:{atlas_map.device}"
+    new_ids = torch.empty((n, K), dtype=torch.int64, device=dev)
+    n_ins = np.zeros(n, np.int32)
+    cnt = np.zeros(n, np.int32)
+    atlas_map._stream()
+    atlas_map._chk(atlas_map.lib.gcs_pmap_insert_masked(
+        atlas_map.h, ip, n, K, C.byref(rows.rows), float(timestamp), int(scan_seq), float(recency_decay_lambda),
+        int(atlas_map.next_global_id), C.c_void_p(new_ids.data_ptr() if n * K else None), L.iptr(n_ins),
+        L.iptr(cnt)), "gcs_pmap_insert_masked")
+    vm = valid_new_mask.detach().cpu().numpy() if torch.is_tensor(valid_new_mask) else np.asarray(valid_new_mask)
+    vm = vm.reshape(n, K).astype(bool) if n else vm
+    out = []
+    for t, tid in enumerate(tile_ids):
+        ni = int(n_ins[t])
+        atlas_map.next_global_id += ni
+        atlas_map.total_count += ni
+        atlas_map.counts[int(tid)] = int(cnt[t])
+        dropped = int((~vm[t]).sum())
+        cert = (CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=["insert_unfilled_budget"],
+                                         frobenius_applied=False) if dropped > 0
+                else CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id))
+        eff = ExpectedEffect("primitive_map_insert_masked", float(int(vm[t].sum())), float(ni))
+        out.append((PrimitiveMapInsertResult(atlas_map, int(tid), ni, new_ids[t]), cert, eff))
+    return out
+
+
+def primitive_map_insert_masked(atlas_map: AtlasMap, tile_id: int, Lambdas_new, thetas_new, etas_new, weights_new,
+                                timestamp: float, valid_new_mask, scan_seq: int = 0,
+                                recency_decay_lambda: float = GC_RECENCY_DECAY_LAMBDA, colors_new=None,
+                                sources_new=None, chart_id: str = CHART_ID,
+                                anchor_id: str = "primitive_map_insert_masked"):
+    """:807-981: up to K masked proposals into the tile's K lowest-retention slots (empty first)."""
+    add = lambda x: None if x is None else (x[None] if _torch().is_tensor(x) else np.asarray(x)[None])  # noqa: E731
+    return primitive_map_insert_masked_tiles(atlas_map, [tile_id], add(Lambdas_new), add(thetas_new), add(etas_new),
+                                             add(weights_new), timestamp, add(valid_new_mask), scan_seq,
+                                             recency_decay_lambda, add(colors_new), add(sources_new), chart_id,
+                                             anchor_id)[0]
+
+
+def primitive_map_fuse_tiles(atlas_map: AtlasMap, active_tile_ids: List[int], tile_ids_flat, target_slots,
+                             Lambdas_meas, thetas_meas, etas_meas, weights_meas, responsibilities, timestamp: float,
+                             scan_seq: int = 0, valid_mask=None, colors_meas=None, sources_meas=None,
+                             eps_mass: float = GC_EPS_MASS, chart_id: str = CHART_ID, anchor_id: str = "primitive_map"):
+    """The pipeline's per-active-tile fuse loop (pipeline.py:1301-1327) in one call: tile t fuses the
+    rows with tile_ids_flat == t (and valid); each (result, cert, effect) as primitive_map_fuse's."""
+    torch = _torch()
+    K = int((target_slots.shape if torch.is_tensor(target_slots) else np.asarray(target_slots).shape)[0])
+    if K == 0 or not active_tile_ids:
+        return [(PrimitiveMapFuseResult(atlas_map, int(t), 0),) + _exact(chart_id, anchor_id, "primitive_map_fuse")
+                for t in active_tile_ids]
+    idx, ip = _tiles_arg([atlas_map.index(tid, create=True) for tid in active_tile_ids])
+    pos = {int(t): i for i, t in enumerate(active_tile_ids)}
+    tf = tile_ids_flat.detach().cpu().numpy() if torch.is_tensor(tile_ids_flat) else np.asarray(tile_ids_flat)
+    tpos = np.array([pos.get(int(t), -1) for t in tf.reshape(-1)], dtype=np.int32)
+    rows = _Rows(atlas_map, K, Lambdas_meas, thetas_meas, etas_meas, weights_meas, valid=valid_mask,
+                 responsibilities=responsibilities, colors=colors_meas, sources=sources_meas, tile_pos=tpos,
+                 slots=target_slots)
+    nf = np.zeros(1, np.int32)
+    atlas_map._stream()
+    atlas_map._chk(atlas_map.lib.gcs_pmap_fuse(atlas_map.h, ip, len(active_tile_ids), C.byref(rows.rows),
+                                               float(timestamp), int(scan_seq), float(eps_mass), L.iptr(nf)),
+                   "gcs_pmap_fuse")
+    return [(PrimitiveMapFuseResult(atlas_map, int(t), int(nf[0])),
+             CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
+             ExpectedEffect("primitive_map_fuse", float(K), float(nf[0]))) for t in active_tile_ids]
+
+
+def primitive_map_fuse(atlas_map: AtlasMap, tile_id: int, target_slots, Lambdas_meas, thetas_meas, etas_meas,
+                       weights_meas, responsibilities, timestamp: float, scan_seq: int = 0, valid_mask=None,
+                       colors_meas=None, sources_meas=None, eps_psd: float = GC_EPS_PSD, eps_mass: float = GC_EPS_MASS,
+                       fuse_chunk_size: int = GC_FUSE_CHUNK_SIZE, chart_id: str = CHART_ID,
+                       anchor_id: str = "primitive_map"):
+    """:992-1163: PoE fuse of K rows into the tile's target slots (sums in row order; the chunking
+    of the reference does not change that order)."""
+    torch = _torch()
+    K = int((target_slots.shape if torch.is_tensor(target_slots) else np.asarray(target_slots).shape)[0])
+    return primitive_map_fuse_tiles(atlas_map, [tile_id], np.full(K, int(tile_id), np.int64), target_slots,
+                                    Lambdas_meas, thetas_meas, etas_meas, weights_meas, responsibilities, timestamp,
+                                    scan_seq, valid_mask, colors_meas, sources_meas, eps_mass, chart_id, anchor_id)[0]
+
+
+def primitive_map_cull(atlas_map: AtlasMap, tile_id: int,
+                       weight_threshold: float = GC_PRIMITIVE_CULL_WEIGHT_THRESHOLD,
+                       max_primitives: Optional[int] = None, chart_id: str = CHART_ID, anchor_id: str = "primitive_map"):
+    """:1175-1304: valid primitives below the weight threshold are dropped (budgeting, mass logged)."""
+    idx = atlas_map.index(tile_id, create=True)
+    no_op = lambda: (PrimitiveMapCullResult(atlas_map, int(tile_id), 0, 0.0),) + _exact(  # noqa: E731
+        chart_id, anchor_id, "primitive_map_cull")
+    if atlas_map.counts.get(int(tile_id), 0) == 0:
+        return no_op()
+    thr = float(weight_threshold)
+    if max_primitives is not None:   # :1220-1228: effective threshold from the sorted weights (host)
+        t = atlas_map.read_tile(tile_id)
+        below = t["valid_mask"] & (t["weights"] < thr)
+        if atlas_map.counts[int(tile_id)] - int(below.sum()) > max_primitives:
+            sw = np.sort(t["weights"] * t["valid_mask"].astype(np.float64))[::-1]
+            if max_primitives < len(sw):
+                thr = float(sw[max_primitives])
+    ip = _tiles_arg([idx])
+    nc, cnt = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    md, ws = np.zeros(1), np.zeros(1)
+    atlas_map._stream()
+    atlas_map._chk(atlas_map.lib.gcs_pmap_cull(atlas_map.h, ip[1], 1, thr, L.iptr(nc), L.dptr(md), L.dptr(ws),
+                                               L.iptr(cnt)), "gcs_pmap_cull")
+    n = int(nc[0])
+    if n == 0:
+        return no_op()
+    atlas_map.counts[int(tile_id)] = int(cnt[0])
+    atlas_map.total_count -= n
+    cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=["budgeting", "mass_drop"],
+                                    influence=InfluenceCert.identity().with_overrides(
+                                        mass_epsilon_ratio=float(md[0]) / (float(ws[0]) + GC_EPS_MASS)))
+    return (PrimitiveMapCullResult(atlas_map, int(tile_id), n, float(md[0])), cert,
+            ExpectedEffect("primitive_map_cull", float(n), float(n)))
+
+
+def primitive_map_forget(atlas_map: AtlasMap, tile_id: int,
+                         forgetting_factor: float = GC_PRIMITIVE_FORGETTING_FACTOR, chart_id: str = CHART_ID,
+                         anchor_id: str = "primitive_map"):
+    """:1314-1384: weights *= gamma (a missing tile: exact no-op)."""
+    idx = atlas_map.index(tile_id, create=False)
+    if idx < 0:
+        return (PrimitiveMapForgetResult(atlas_map, int(tile_id)),) + _exact(chart_id, anchor_id,
+                                                                             "primitive_map_forget")
+    ip = _tiles_arg([idx])
+    atlas_map._stream()
+    atlas_map._chk(atlas_map.lib.gcs_pmap_forget(atlas_map.h, ip[1], 1, float(forgetting_factor)),
+                   "gcs_pmap_forget")
+    g = float(forgetting_factor)
+    return (PrimitiveMapForgetResult(atlas_map, int(tile_id)), CertBundle.create_exact(chart_id, anchor_id),
+            ExpectedEffect("primitive_map_forget", 1.0 - g, 1.0 - g))
+
+
+def primitive_map_recency_inflate(atlas_map: AtlasMap, tile_ids: List[int], scan_seq: int,
+                                  recency_decay_lambda: float = GC_RECENCY_DECAY_LAMBDA,
+                                  min_scale: float = GC_RECENCY_MIN_SCALE, chart_id: str = CHART_ID,
+                                  anchor_id: str = "primitive_map_recency_inflate"):
+    """:1400-1484: precision (Lambda, theta) of stale primitives scaled by clip(exp(-lambda dt))."""
+    present = [atlas_map.tiles[int(t)] for t in tile_ids if int(t) in atlas_map.tiles]
+    st = np.zeros(3)
+    if present:
+        ip = _tiles_arg(present)
+        atlas_map._stream()
+        atlas_map._chk(atlas_map.lib.gcs_pmap_recency_inflate(atlas_map.h, ip[1], len(present), int(scan_seq),
+                                                              float(recency_decay_lambda), float(min_scale),
+                                                              L.dptr(st)), "gcs_pmap_recency_inflate")
+    down, infl, nv = float(st[0]), float(st[1]), float(st[2])
+    stats = PrimitiveMapRecencyInflateStats(down / max(nv, 1.0), infl, down)
+    return (atlas_map, CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
+            ExpectedEffect("primitive_map_recency_inflate", nv, nv), stats)
+
+
+def primitive_map_merge_reduce(atlas_map: AtlasMap, tile_id: int,
+                               merge_threshold: float = GC_PRIMITIVE_MERGE_THRESHOLD,
+                               max_pairs: int = GC_K_MERGE_PAIRS_PER_TILE,
+                               max_tile_size: int = GC_PRIMITIVE_MERGE_MAX_TILE_SIZE, eps_psd: float = GC_EPS_PSD,
+                               eps_lift: float = GC_EPS_LIFT, chart_id: str = CHART_ID,
+                               anchor_id: str = "primitive_map"):
+    """:1809-2031: greedy disjoint pairs by Bhattacharyya distance below the threshold, moment-matched
+    (Frobenius-corrected approximation).  A tile over max_tile_size returns the budget-cap cert."""
+    def no_op(predicted, triggers=None, influence=None):
+        res = PrimitiveMapMergeReduceResult(atlas_map, int(tile_id), 0, 0.0)
+        cert = (CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=triggers,
+                                         frobenius_applied=True, influence=influence or InfluenceCert.identity())
+                if triggers else CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id))
+        return res, cert, ExpectedEffect("primitive_map_merge_reduce", predicted, 0.0)
+
+    idx = atlas_map.index(tile_id, create=False)
+    if idx < 0:
+        return no_op(0.0)
+    M = atlas_map.m_tile
+    if M < 2 or atlas_map.counts.get(int(tile_id), 0) < 2 or int(max_pairs) <= 0:
+        return no_op(float(max_pairs))
+    if int(max_tile_size) > 0 and M > int(max_tile_size):
+        over = float(M - int(max_tile_size)) / float(max(M, 1))
+        return no_op(float(max_pairs), ["merge_reduce_budget_cap"],
+                     InfluenceCert.identity().with_overrides(mass_epsilon_ratio=over))
+    nm, cnt = np.zeros(1, np.int32), np.zeros(1, np.int32)
+    pairs = np.zeros(2 * int(max_pairs), np.int32)
+    atlas_map._stream()
+    atlas_map._chk(atlas_map.lib.gcs_pmap_merge_reduce(atlas_map.h, idx, float(merge_threshold), int(max_pairs),
+                                                       float(eps_psd), float(eps_lift), L.iptr(nm), L.iptr(pairs),
+                                                       L.iptr(cnt)), "gcs_pmap_merge_reduce")
+    n = int(nm[0])
+    atlas_map.last_merge_pairs = [(int(pairs[2 * k]), int(pairs[2 * k + 1])) for k in range(n)]
+    if n <= 0:
+        return no_op(float(max_pairs))
+    atlas_map.counts[int(tile_id)] = int(cnt[0])
+    atlas_map.total_count -= n
+    cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=["primitive_map_merge_reduce"],
+                                    frobenius_applied=True, influence=InfluenceCert.identity().with_overrides(
+                                        mass_epsilon_ratio=float(n) / float(max(M, 1))))
+    return (PrimitiveMapMergeReduceResult(atlas_map, int(tile_id), n, float(n)), cert,
+            ExpectedEffect("primitive_map_merge_reduce", float(max_pairs), float(n)))

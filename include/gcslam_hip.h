@@ -29,6 +29,9 @@
  *   gcs_fibonacci_atlas         archive/bin_atlas.py:40-61
  *   gcs_associate_primitives_ot FS/backend/operators/primitive_association.py:239-553
  *                               associate_primitives_ot (+ tiling.py:148-186, measurement_batch.py:389-411)
+ *   gcs_pmap_*                  FS/backend/structures/primitive_map.py:98-2031 (AtlasMap tiles in HBM;
+ *                               extract_atlas_map_view, insert_masked, fuse, cull, forget,
+ *                               recency_inflate, merge_reduce)
  *   gcs_extract_lidar_surfels   FS/backend/operators/lidar_surfel_extraction.py:339-431
  *                               extract_lidar_surfels (+ FS/common/ma_hex_web.py:243-303
  *                               bin_points_3d, FS/backend/structures/measurement_batch.py:272-381)
@@ -487,6 +490,111 @@ int gcs_assoc_ctx_set_stream(gcs_assoc_ctx* ctx, void* stream);
 /* Synchronises; unsupported policies return GCS_ERR_ARG with the reference's message. */
 int gcs_associate_primitives_ot(gcs_assoc_ctx* ctx, const gcs_assoc_config* cfg, const gcs_assoc_meas* meas,
                                 const gcs_assoc_view* view, gcs_assoc_outputs* out);
+
+/* ---------------------------------------------------------------- primitive path: the primitive map */
+/* The AtlasMap's tile storage (FS/backend/structures/primitive_map.py:98-227) resident in HBM, and
+ * its maintenance operators on the GPU:
+ *   gcs_pmap_extract_view      extract_atlas_map_view (:356-450, top m_view slots by weight per tile,
+ *                              _select_topk_slots_fixed :303-322; view core :474-498)
+ *   gcs_pmap_insert_masked     primitive_map_insert_masked (:807-981; eviction targets by
+ *                              _select_lowest_mass_slots_fixed :325-353), several tiles per call
+ *   gcs_pmap_fuse              primitive_map_fuse (:992-1163), the pipeline's per-active-tile loop
+ *                              (pipeline.py:1301-1327) in one call
+ *   gcs_pmap_cull              primitive_map_cull (:1175-1304, weight threshold)
+ *   gcs_pmap_forget            primitive_map_forget (:1314-1384)
+ *   gcs_pmap_recency_inflate   primitive_map_recency_inflate (:1400-1484)
+ *   gcs_pmap_merge_reduce      primitive_map_merge_reduce (:1501-2031) for tiles of <= max_merge slots
+ * A map context holds max_tiles tiles of m_tile slots (tile storage index 0..max_tiles-1; the caller
+ * maps MA-hex tile ids to storage indices, as the AtlasMap dict does).  Per field the storage is
+ * [tile][slot][width] (the reference's array shapes).  Sorts are stable radix sorts on the
+ * reference's single key (lax.sort with num_keys = 1; -0.0 == 0.0); scatter-adds accumulate in
+ * input order; no floating-point atomics: bitwise reproducible.  Every call synchronises. */
+typedef struct gcs_pmap gcs_pmap;
+enum {  /* field codes for gcs_pmap_read / gcs_pmap_write: element type and width per slot */
+  GCS_PM_LAMBDAS = 0,  /* f64 x 9 */
+  GCS_PM_THETAS,       /* f64 x 3 */
+  GCS_PM_ETAS,         /* f64 x n_lobes*3 */
+  GCS_PM_WEIGHTS,      /* f64 */
+  GCS_PM_TIMESTAMPS,   /* f64 */
+  GCS_PM_CREATED,      /* f64 */
+  GCS_PM_COLORS,       /* f64 x 3 */
+  GCS_PM_CAM_MASS,     /* f64 */
+  GCS_PM_LIDAR_MASS,   /* f64 */
+  GCS_PM_RGB_ACCUM,    /* f64 x 3 */
+  GCS_PM_RGB_DENOM,    /* f64 */
+  GCS_PM_RGB,          /* f64 x 3 */
+  GCS_PM_LAST_SUPPORTED, /* i64 */
+  GCS_PM_LAST_UPDATE,  /* i64 */
+  GCS_PM_IDS,          /* i64 */
+  GCS_PM_VALID,        /* u8 */
+  GCS_PM_NFIELDS
+};
+
+typedef struct {            /* AtlasMapView outputs (device pointers, n_tiles x m_view rows; any may be NULL) */
+  double* positions;        /* x 3 */
+  double* covariances;      /* x 9 */
+  double* directions;       /* x 3 */
+  double* kappas;
+  double* weights;
+  int64_t* primitive_ids;
+  uint8_t* valid_mask;
+  int64_t* last_supported_scan_seq;
+  double* etas;             /* x n_lobes*3 */
+  double* colors;           /* x 3 (the tile's rgb) */
+  int32_t* candidate_slots;
+  int64_t* candidate_tile_ids;
+} gcs_pmap_view;
+
+typedef struct {            /* one row per proposal / contribution (device pointers; optional ones may be NULL) */
+  const double* Lambdas;    /* n x 9 (world frame) */
+  const double* thetas;     /* n x 3 */
+  const double* etas;       /* n x n_lobes*3 */
+  const double* weights;    /* n */
+  const double* responsibilities; /* n (fuse) */
+  const uint8_t* valid;     /* n: fuse valid_mask / insert valid_new_mask */
+  const double* colors;     /* n x 3, optional */
+  const int32_t* sources;   /* n (0 camera, 1 LiDAR), optional */
+  const int32_t* tile_pos;  /* fuse: n, index into the call's tile list (-1: no tile) */
+  const int32_t* slots;     /* fuse: n, target slot */
+  int32_t n;
+} gcs_pmap_rows;
+
+int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t max_merge, int32_t device,
+                    gcs_pmap** out);
+int gcs_pmap_destroy(gcs_pmap* pm);
+const char* gcs_pmap_last_error(const gcs_pmap* pm);
+int gcs_pmap_set_stream(gcs_pmap* pm, void* stream);
+/* create_empty_tile (:148-174) into storage index tile */
+int gcs_pmap_clear_tile(gcs_pmap* pm, int32_t tile);
+/* one field of one tile, host buffer of m_tile x width elements */
+int gcs_pmap_read(gcs_pmap* pm, int32_t tile, int32_t field, void* host);
+int gcs_pmap_write(gcs_pmap* pm, int32_t tile, int32_t field, const void* host);
+/* tiles: n host storage indices in view order (-1: a tile missing from the map, viewed as empty);
+ * tile_ids: the n MA-hex ids written to candidate_tile_ids */
+int gcs_pmap_extract_view(gcs_pmap* pm, const int32_t* tiles, const int64_t* tile_ids, int32_t n, int32_t m_view,
+                          double eps_lift, double eps_mass, gcs_pmap_view* out);
+/* primitive_map_insert_masked for n tiles, K proposals each (rows tile-major, rows.n = n K); ids from
+ * next_global_id in tile order.  new_ids (device, n K, -1 where masked) may be NULL; n_inserted and
+ * count (host, n each): proposals inserted and the tile's valid count afterwards. */
+int gcs_pmap_insert_masked(gcs_pmap* pm, const int32_t* tiles, int32_t n, int32_t K, const gcs_pmap_rows* rows,
+                           double timestamp, int64_t scan_seq, double recency_decay_lambda, int64_t next_global_id,
+                           int64_t* new_ids, int32_t* n_inserted, int32_t* count);
+/* primitive_map_fuse on each of the n tiles with the rows whose tile_pos names it (valid & tile
+ * match, pipeline.py:1304-1305); every listed tile gets the call's timestamp at every row's slot and
+ * its rgb rebuilt, as the reference's per-tile call does.  n_fused (host): unique row slots. */
+int gcs_pmap_fuse(gcs_pmap* pm, const int32_t* tiles, int32_t n, const gcs_pmap_rows* rows, double timestamp,
+                  int64_t scan_seq, double eps_mass, int32_t* n_fused);
+/* per tile (host, n each): culled count, mass dropped, sum of all weights, valid count afterwards */
+int gcs_pmap_cull(gcs_pmap* pm, const int32_t* tiles, int32_t n, double weight_threshold, int32_t* n_culled,
+                  double* mass_dropped, double* weight_sum, int32_t* count);
+int gcs_pmap_forget(gcs_pmap* pm, const int32_t* tiles, int32_t n, double forgetting_factor);
+/* stats (host): [downscale total, cov inflation trace, valid count] over the n tiles */
+int gcs_pmap_recency_inflate(gcs_pmap* pm, const int32_t* tiles, int32_t n, int64_t scan_seq,
+                             double recency_decay_lambda, double min_scale, double* stats);
+/* the whole tile's Bhattacharyya pairs (m_tile <= max_merge); pairs (host, 2 x max_pairs): the merged
+ * (kept, removed) slots in selection order */
+int gcs_pmap_merge_reduce(gcs_pmap* pm, int32_t tile, double merge_threshold, int32_t max_pairs, double eps_psd,
+                          double eps_lift, int32_t* n_merged, int32_t* pairs, int32_t* count);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,213 @@
+"""GPU parity of the primitive map (gcs_pmap_* through gcslam.primitive_map) against the numpy
+oracle (oracle/primitive_map.py) on seeded random tiles: slot selections, ids, masks and integer
+fields bit-exact; floating fields within the bars written at each assertion."""
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+from oracle import primitive_map as opm
+
+pytestmark = pytest.mark.gpu
+
+M = 4096
+NL = 3
+
+
+def _rand_tile(rng, m=M, frac=0.6, seq_hi=40):
+    t = opm.create_empty_tile(m)
+    v = rng.random(m) < frac
+    t["valid_mask"][:] = v
+    w = rng.random(m) * 2.0
+    w[rng.random(m) < 0.1] = 0.5          # exact ties (stable order by slot)
+    w[rng.random(m) < 0.05] = 0.0
+    t["weights"][:] = w
+    A = rng.normal(size=(m, 3, 3)) * 0.3
+    t["Lambdas"][:] = np.einsum("nij,nkj->nik", A, A) + np.eye(3)[None] * rng.uniform(0.5, 4.0, size=(m, 1, 1))
+    t["thetas"][:] = rng.normal(size=(m, 3)) * 3.0
+    t["etas"][:] = rng.normal(size=(m, NL, 3))
+    t["timestamps"][:] = rng.uniform(0, 10, m)
+    t["created_timestamps"][:] = rng.uniform(0, 10, m)
+    t["last_supported_scan_seq"][:] = rng.integers(0, seq_hi, m)
+    t["last_update_scan_seq"][:] = rng.integers(0, seq_hi, m)
+    t["primitive_ids"][:] = rng.permutation(10 * m)[:m]
+    t["colors"][:] = rng.random((m, 3))
+    cam = np.where(rng.random(m) < 0.3, rng.random(m), 0.0)
+    t["cam_mass"][:] = cam
+    t["lidar_mass"][:] = rng.random(m)
+    t["rgb_cam_accum"][:] = rng.random((m, 3)) * cam[:, None]
+    t["rgb_cam_denom"][:] = cam
+    t["rgb"][:] = np.where((cam > 0)[:, None], rng.random((m, 3)), 0.5)
+    return t
+
+
+def _map(tiles, m=M, max_merge=0):
+    from gcslam.primitive_map import AtlasMap
+    am = AtlasMap(m_tile=m, max_tiles=8, n_lobes=NL, max_merge=max_merge)
+    for tid, t in tiles.items():
+        am.write_tile(tid, t)
+    return am
+
+
+def _same_tile(got, ref, rtol=0.0, what=""):
+    for f in opm.FIELDS_I64 + ("valid_mask",):
+        assert np.array_equal(got[f], ref[f]), f"{what} {f}"
+    for f in opm.FIELDS_F64:
+        a, b = got[f], ref[f]
+        if rtol == 0.0:
+            assert np.array_equal(a, b), f"{what} {f}: max |diff| {np.abs(a - b).max()}"
+        else:
+            np.testing.assert_allclose(a, b, rtol=rtol, atol=rtol * max(1.0, np.abs(b).max()), err_msg=f"{what} {f}")
+
+
+def test_view_matches_oracle():
+    rng = np.random.default_rng(1)
+    tiles = {11: _rand_tile(rng), 12: _rand_tile(rng, frac=0.2)}
+    am = _map(tiles)
+    v = opm.extract_atlas_map_view(tiles, [11, 99, 12], 1024, M)
+    g = __import__("gcslam.primitive_map", fromlist=["x"]).extract_atlas_map_view(am, [11, 99, 12], 1024)
+    cpu = lambda x: x.detach().cpu().numpy()  # noqa: E731
+    assert np.array_equal(cpu(g.candidate_slots), v["candidate_slots"])          # stable top-k, ties by slot
+    assert np.array_equal(cpu(g.candidate_tile_ids), v["candidate_tile_ids"])
+    assert np.array_equal(cpu(g.valid_mask), v["valid_mask"])
+    assert np.array_equal(cpu(g.primitive_ids), v["primitive_ids"])
+    assert np.array_equal(cpu(g.last_supported_scan_seq), v["last_supported_scan_seq"])
+    assert np.array_equal(cpu(g.weights), v["weights"])
+    assert np.array_equal(cpu(g.etas), v["etas"]) and np.array_equal(cpu(g.colors), v["colors"])
+    # LU solve / inverse of (Lambda + eps I): the pivot order is LAPACK's, the rounding may differ
+    np.testing.assert_allclose(cpu(g.positions), v["positions"], rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(cpu(g.covariances), v["covariances"], rtol=1e-12, atol=1e-13)
+    np.testing.assert_allclose(cpu(g.kappas), v["kappas"], rtol=1e-15, atol=0)   # same sum order, no FMA
+    np.testing.assert_allclose(cpu(g.directions), v["directions"], rtol=1e-15, atol=1e-16)
+    am.close()
+
+
+def test_insert_masked_matches_oracle():
+    from gcslam import primitive_map as gpm
+    rng = np.random.default_rng(2)
+    tiles = {1: _rand_tile(rng, frac=0.99), 2: _rand_tile(rng, frac=0.3), 3: _rand_tile(rng, frac=1.0)}
+    tiles[3]["weights"][:] = 0.25                     # retention ties everywhere in tile 3
+    tiles[3]["last_supported_scan_seq"][:] = 7
+    am = _map(tiles)
+    am.next_global_id = 1000
+    K = 64
+    ids_t = [2, 1, 3]
+    P = dict(L=rng.normal(size=(3, K, 3, 3)), th=rng.normal(size=(3, K, 3)), e=rng.normal(size=(3, K, NL, 3)),
+             w=rng.random((3, K)), v=rng.random((3, K)) < 0.7, c=rng.random((3, K, 3)) * 1.4 - 0.2,
+             s=rng.integers(0, 2, (3, K)).astype(np.int32))
+    res = gpm.primitive_map_insert_masked_tiles(am, ids_t, P["L"], P["th"], P["e"], P["w"], 5.5, P["v"], scan_seq=41,
+                                                colors_new=P["c"], sources_new=P["s"])
+    nxt = 1000
+    for k, tid in enumerate(ids_t):
+        n, ids, dropped, nxt = opm.insert_masked(tiles[tid], nxt, P["L"][k], P["th"][k], P["e"][k], P["w"][k], 5.5,
+                                                 P["v"][k], scan_seq=41, colors_new=P["c"][k], sources_new=P["s"][k])
+        r, cert, eff = res[k]
+        assert r.n_inserted == n and eff.realized == n and (cert.exact == (dropped == 0))
+        assert np.array_equal(r.new_ids.cpu().numpy(), ids)
+        _same_tile(am.read_tile(tid), tiles[tid], what=f"tile {tid}")      # copies and products: bitwise
+        assert am.counts[tid] == int(tiles[tid]["valid_mask"].sum())
+    assert am.next_global_id == nxt
+    am.close()
+
+
+def test_fuse_matches_oracle():
+    from gcslam import primitive_map as gpm
+    rng = np.random.default_rng(3)
+    tiles = {5: _rand_tile(rng), 6: _rand_tile(rng), 7: _rand_tile(rng)}
+    am = _map(tiles)
+    R = 3000
+    tile_flat = rng.choice([5, 6, 7, 8], size=R)      # tile 8 is not active: its rows do nothing
+    slots = rng.integers(0, 300, R)                   # many repeated targets
+    Lm = rng.normal(size=(R, 3, 3))
+    th, et, w = rng.normal(size=(R, 3)), rng.normal(size=(R, NL, 3)), rng.random(R)
+    resp, valid = rng.random(R), rng.random(R) < 0.8
+    cols, srcs = rng.random((R, 3)) * 1.5 - 0.25, rng.integers(0, 2, R).astype(np.int32)
+    active = [6, 5, 7]
+    res = gpm.primitive_map_fuse_tiles(am, active, tile_flat, slots, Lm, th, et, w, resp, 9.25, scan_seq=50,
+                                       valid_mask=valid, colors_meas=cols, sources_meas=srcs)
+    for k, tid in enumerate(active):
+        n = opm.fuse(tiles[tid], slots, Lm, th, et, w, resp, 9.25, scan_seq=50, valid_mask=valid & (tile_flat == tid),
+                     colors_meas=cols, sources_meas=srcs)
+        assert res[k][0].n_fused == n
+        _same_tile(am.read_tile(tid), tiles[tid], what=f"tile {tid}")      # same sum order: bitwise
+    am.close()
+
+
+def test_cull_forget_recency_match_oracle():
+    from gcslam import primitive_map as gpm
+    rng = np.random.default_rng(4)
+    tiles = {1: _rand_tile(rng), 2: _rand_tile(rng)}
+    tiles[1]["weights"][rng.random(M) < 0.2] = 5e-5
+    am = _map(tiles)
+    r, cert, eff = gpm.primitive_map_cull(am, 1, 1e-4)
+    n, dropped, ratio = opm.cull(tiles[1], 1e-4)
+    assert r.n_culled == n and n > 0
+    assert r.mass_dropped == pytest.approx(dropped, rel=1e-13)               # fixed-order tree vs numpy pairwise
+    assert cert.influence.mass_epsilon_ratio == pytest.approx(ratio, rel=1e-13)
+    gpm.primitive_map_forget(am, 2, 0.995)
+    opm.forget(tiles[2], 0.995)
+    _, _, _, st = gpm.primitive_map_recency_inflate(am, [2, 1, 77], 45, 0.02, 0.05)
+    s_ref = opm.recency_inflate(tiles, [2, 1, 77], 45, 0.02, 0.05)
+    assert st.staleness_inflation_strength == pytest.approx(s_ref[0], rel=1e-12)
+    assert st.staleness_cov_inflation_trace == pytest.approx(s_ref[1], rel=1e-12)
+    assert st.stale_precision_downscale_total == pytest.approx(s_ref[2], rel=1e-12)
+    for tid in (1, 2):   # exp on the device vs numpy: 1 ulp in the decay
+        _same_tile(am.read_tile(tid), tiles[tid], rtol=1e-15, what=f"tile {tid}")
+    am.close()
+
+
+def test_merge_reduce_matches_oracle():
+    from gcslam import primitive_map as gpm
+    rng = np.random.default_rng(5)
+    m = 512
+    t = _rand_tile(rng, m=m, frac=0.9)
+    # well-separated primitives plus a few close pairs (distinct distances)
+    mu = rng.uniform(-50, 50, size=(m, 3))
+    t["Lambdas"][:] = np.eye(3)[None] * rng.uniform(1.0, 2.0, size=(m, 1, 1))
+    for a, b, d in ((3, 40, 0.01), (7, 8, 0.02), (100, 300, 0.005), (40, 41, 0.003), (200, 201, 0.015)):
+        mu[b] = mu[a] + d
+        t["Lambdas"][b] = t["Lambdas"][a]
+        t["valid_mask"][[a, b]] = True
+    t["thetas"][:] = np.einsum("nij,nj->ni", t["Lambdas"], mu)
+    am = _map({0: t}, m=m, max_merge=m)
+    r, cert, eff = gpm.primitive_map_merge_reduce(am, 0, merge_threshold=0.1, max_pairs=4, max_tile_size=2048)
+    n, status, pairs = opm.merge_reduce(t, merge_threshold=0.1, max_pairs=4, max_tile_size=2048)
+    assert r.n_merged == n >= 3 and am.last_merge_pairs == pairs and cert.frobenius_applied
+    _same_tile(am.read_tile(0), t, rtol=1e-12, what="merged tile")
+    am.close()
+
+
+def test_reference_merge_and_color_tests_on_gpu():
+    """test_primitive_map_merge_reduce.py:76-98 and test_map_color_provenance.py:69-82 through the
+    device operators."""
+    from gcslam import primitive_map as gpm
+    t = opm.create_empty_tile(3)
+    t["Lambdas"][:] = np.eye(3)
+    t["thetas"][:] = [[0.0, 0, 0], [0.01, 0, 0], [10.0, 0, 0]]
+    t["weights"][:] = 1.0
+    t["primitive_ids"][:] = [0, 1, 2]
+    t["valid_mask"][:] = True
+    t["cam_mass"][:] = [1.0, 0.0, 0.0]
+    t["lidar_mass"][:] = [0.0, 1.0, 1.0]
+    t["rgb_cam_accum"][0] = [1.0, 0.0, 0.0]
+    t["rgb_cam_denom"][:] = [1.0, 0.0, 0.0]
+    t["rgb"][0] = [1.0, 0.0, 0.0]
+    am = _map({0: t}, m=3, max_merge=3)
+    am.next_global_id, am.total_count = 3, 3
+    r, cert, eff = gpm.primitive_map_merge_reduce(am, 0, merge_threshold=0.5, max_pairs=1, max_tile_size=10)
+    g = am.read_tile(0)
+    assert r.n_merged == 1 and g["valid_mask"].tolist() == [True, False, True]
+    assert np.isclose(g["weights"][0], 2.0) and am.total_count == 2 and cert.frobenius_applied and eff.realized == 1.0
+    am.close()
+    for first, second, want in (((1.0, 0.0, 0.0), 0, (0.2, 0.2, 0.2)), ((0.2, 0.2, 0.2), 1, (0.0, 1.0, 0.0))):
+        am = gpm.AtlasMap(m_tile=1, max_tiles=1, n_lobes=NL, max_merge=0)
+        gpm.primitive_map_insert_masked(am, 0, np.eye(3)[None], np.zeros((1, 3)), np.zeros((1, NL, 3)),
+                                        np.array([1.0]), 0.0, np.array([True]), colors_new=np.array([first]),
+                                        sources_new=np.array([second]))
+        gpm.primitive_map_fuse(am, 0, np.array([0]), np.eye(3)[None], np.zeros((1, 3)), np.zeros((1, NL, 3)),
+                               np.array([1.0]), np.array([1.0]), 1.0, scan_seq=1, valid_mask=np.array([True]),
+                               colors_meas=np.array([want]), sources_meas=np.array([1 - second]))
+        expect = first if second == 0 else want
+        assert np.allclose(am.read_tile(0)["rgb"][0], expect, atol=1e-6)
+        am.close()
