@@ -1741,7 +1741,9 @@ __global__ __launch_bounds__(NT) void k_final(const double* __restrict__ partial
 constexpr int kFoldRows = 64;
 constexpr int kFoldDirect = 2048;  // up to this many rows a single block folds directly (C2 bins: 1563)
 #ifndef GCS_FINAL_WIDE
-#define GCS_FINAL_WIDE 1024  // threads of a direct fold over more than kFinalWideRows rows (kBlock: off)
+// threads of a direct fold over more than kFinalWideRows rows (kBlock: off).  Same-box rocprof at C2
+// (1,563 rows, profiles/r02/foldab/): 1024 threads 9.9 us, 256 threads 7.8 us -> off
+#define GCS_FINAL_WIDE 256
 #endif
 constexpr int kFinalWide = GCS_FINAL_WIDE, kFinalWideRows = 512;
 template <int NV, unsigned MAXMASK>

@@ -675,6 +675,159 @@ __global__ void k_pm_merge_apply(PmStore st, int ti, const int32_t* sel, const i
 
 constexpr int kMergeBlocks = 512;
 
+// ---------------------------------------------------------------- step 12b (pipeline.py:1244-1447)
+struct PmMeas {
+  const double *lam, *th, *eta, *w, *col;
+  const uint8_t* valid;
+  const int32_t* src;
+  int n;
+  const double* resp;
+  const int64_t *ctile, *cslot;
+  const double* rmass;
+  int k;
+};
+
+struct PmWorld {
+  double R[9], t[3], eps_lift;
+};
+
+// Lambda_w = (R Lambda) R^T, mu_w = R (Lambda + eps I)^-1 theta + t, theta_w = Lambda_w mu_w, eta_w = R eta
+__device__ void world_row(const PmWorld& W, const double* L, const double* th, const double* eta, int nl, double* Lw,
+                          double* thw, double* ew, double* muw) {
+#pragma clang fp contract(off)
+  double RL[9];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) RL[3 * r + c] = (W.R[3 * r] * L[c] + W.R[3 * r + 1] * L[3 + c]) + W.R[3 * r + 2] * L[6 + c];
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c)
+      Lw[3 * r + c] = (RL[3 * r] * W.R[3 * c] + RL[3 * r + 1] * W.R[3 * c + 1]) + RL[3 * r + 2] * W.R[3 * c + 2];
+  double a[3][3], det, mb[3];
+  int perm[3];
+  lu3(L, W.eps_lift, a, perm, det);
+  lu3_solve(a, perm, th, mb);
+  for (int r = 0; r < 3; ++r) muw[r] = ((W.R[3 * r] * mb[0] + W.R[3 * r + 1] * mb[1]) + W.R[3 * r + 2] * mb[2]) + W.t[r];
+  if (thw)
+    for (int r = 0; r < 3; ++r) thw[r] = (Lw[3 * r] * muw[0] + Lw[3 * r + 1] * muw[1]) + Lw[3 * r + 2] * muw[2];
+  if (ew)
+    for (int b = 0; b < nl; ++b)
+      for (int r = 0; r < 3; ++r)
+        ew[3 * b + r] = (W.R[3 * r] * eta[3 * b] + W.R[3 * r + 1] * eta[3 * b + 1]) + W.R[3 * r + 2] * eta[3 * b + 2];
+}
+
+struct PmRowBuf {
+  double *lam, *th, *eta, *w, *resp, *col, *fm;
+  uint8_t* valid;
+  int32_t *src, *tpos, *slots;
+};
+
+// block_associations_for_fuse (primitive_association.py:561-588) + the world transform, rows in
+// (block, measurement, candidate) order; fm = w r [valid and tile active] (fused mass terms)
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_rows(PmMeas m, PmWorld W, int nl, int block, int nrows,
+                                                             const int64_t* act_ids, int n_act, PmRowBuf o) {
+  const int g = blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= nrows) return;
+  const int row = g / m.k, k = g % m.k;  // row = b * block + i
+  const int mi = min(row, m.n - 1);
+  const bool vr = row < m.n && m.valid[mi] != 0;
+  const int64_t tid = m.ctile[(size_t)mi * m.k + k];
+  int tp = -1;
+  for (int q = 0; q < n_act; ++q)
+    if (act_ids[q] == tid) {
+      tp = q;
+      break;
+    }
+  const double r = m.resp[(size_t)mi * m.k + k] * (vr ? 1.0 : 0.0);
+  double Lw[9], thw[3], ew[24], muw[3];
+  world_row(W, m.lam + 9 * (size_t)mi, m.th + 3 * (size_t)mi, m.eta + (size_t)3 * nl * mi, nl, Lw, thw, ew, muw);
+  for (int c = 0; c < 9; ++c) o.lam[9 * (size_t)g + c] = Lw[c];
+  for (int c = 0; c < 3; ++c) {
+    o.th[3 * (size_t)g + c] = thw[c];
+    o.col[3 * (size_t)g + c] = m.col ? m.col[3 * (size_t)mi + c] : 0.0;
+  }
+  for (int c = 0; c < 3 * nl; ++c) o.eta[(size_t)3 * nl * g + c] = ew[c];
+  const double w = m.w[mi];
+  o.w[g] = w;
+  o.resp[g] = r;
+  o.valid[g] = vr ? 1 : 0;
+  o.src[g] = m.src ? m.src[mi] : 1;
+  o.tpos[g] = tp;
+  o.slots[g] = (int32_t)m.cslot[(size_t)mi * m.k + k];
+  o.fm[g] = (vr && tp >= 0) ? (w * r) * 1.0 : 0.0;
+  (void)block;
+}
+
+// Novelty proposals per active tile (pipeline.py:1331-1375): one 1024-thread workgroup per tile;
+// the stable argsort of -score_t is a rank count over (key, index); rows in (tile, rank) order.
+constexpr int kPropThreads = 1024;
+__global__ __launch_bounds__(kPropThreads) void k_pm_proposals(PmMeas m, PmWorld W, int nl, double eps_mass,
+                                                               double h_tile, const int64_t* act_ids, int kins,
+                                                               double* score_buf, int64_t* tile_buf, PmRowBuf o) {
+#pragma clang fp contract(off)
+  __shared__ double lds[kPropThreads / 64];
+  __shared__ int s_any;
+  const int t = blockIdx.x;
+  const int64_t tid = act_ids[t];
+  double* sc = score_buf + (size_t)t * m.n;
+  double nv = 0.0;
+  for (int i = threadIdx.x; i < m.n; i += kPropThreads) nv += m.valid[i] ? 1.0 : 0.0;
+  nv = block_sum_d<kPropThreads>(nv, lds);
+  const double asum = fmax(nv, eps_mass);
+  for (int i = threadIdx.x; i < m.n; i += kPropThreads) {  // the measurement's tile at z_t (tiling.py:126-145)
+    double Lw[9], muw[3];
+    world_row(W, m.lam + 9 * (size_t)i, m.th + 3 * (size_t)i, nullptr, 0, Lw, nullptr, nullptr, muw);
+    const double h = fmax(h_tile, 1e-12);
+    const double s2 = muw[0] * 0.5 + muw[1] * (1.7320508075688772 * 0.5);
+    const long long c1 = (long long)floor(muw[0] / h), c2 = (long long)floor(s2 / h), cz = (long long)floor(muw[2] / h);
+    const long long M21 = (1LL << 21) - 1, B21 = 1LL << 20;
+    const int64_t mt = (((c1 + B21) & M21) << 42) | (((c2 + B21) & M21) << 21) | ((cz + B21) & M21);
+    if (t == 0) tile_buf[i] = mt;
+    const double vf = m.valid[i] ? 1.0 : 0.0;
+    const double a = vf / asum;
+    const double nov = fmax(a - m.rmass[i], 0.0);
+    const double score = nov * m.w[i] - (1.0 - vf) * 1e6;
+    sc[i] = mt == tid ? score : -1e30;
+  }
+  __syncthreads();
+  // rank of each measurement under (-score_t ascending, index); ranks < kins are the proposals
+  int* slot_of = (int*)(score_buf + (size_t)gridDim.x * m.n) + (size_t)t * kins;
+  for (int i = threadIdx.x; i < m.n; i += kPropThreads) {
+    const double ki = -sc[i];
+    int rank = 0;
+    for (int j = 0; j < m.n; ++j) {
+      const double kj = -sc[j];
+      rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+      if (rank >= kins) break;
+    }
+    if (rank < kins) slot_of[rank] = i;
+  }
+  if (threadIdx.x == 0) s_any = 0;
+  __syncthreads();
+  for (int q = threadIdx.x; q < kins; q += kPropThreads) {
+    const int i = slot_of[q];
+    if (q < m.n && sc[i] > -1e20) s_any = 1;  // in_tile[ins] & (score_t[ins] > -1e20) (plain store: one value)
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < kins; q += kPropThreads) {
+    const size_t g = (size_t)t * kins + q;
+    const int i = q < m.n ? slot_of[q] : 0;
+    const bool in_tile = q < m.n && sc[i] > -1e29;  // score_t == -1e30 exactly where out of tile
+    const bool vn = s_any ? (in_tile && sc[i] > -1e20) : true;
+    double Lw[9], thw[3], ew[24], muw[3];
+    world_row(W, m.lam + 9 * (size_t)i, m.th + 3 * (size_t)i, m.eta + (size_t)3 * nl * i, nl, Lw, thw, ew, muw);
+    for (int c = 0; c < 9; ++c) o.lam[9 * g + c] = Lw[c];
+    for (int c = 0; c < 3; ++c) {
+      o.th[3 * g + c] = thw[c];
+      o.col[3 * g + c] = m.col ? m.col[3 * (size_t)i + c] : 0.0;
+    }
+    for (int c = 0; c < 3 * nl; ++c) o.eta[(size_t)3 * nl * g + c] = ew[c];
+    const double vf = m.valid[i] ? 1.0 : 0.0;
+    const double nov = fmax(vf / asum - m.rmass[i], 0.0);
+    o.w[g] = in_tile ? nov * m.w[i] : 0.0;
+    o.valid[g] = vn ? 1 : 0;
+    o.src[g] = m.src ? m.src[i] : 1;
+  }
+}
+
 }  // namespace
 }  // namespace gcs
 
@@ -698,6 +851,9 @@ struct gcs_pmap {
   size_t ftemp_bytes = 0;
   int frows = 0;
   uint8_t* mark = nullptr;
+  // step-12b scratch (grown on demand)
+  void* ub = nullptr;
+  size_t ub_bytes = 0;
   // merge scratch
   double *mmu = nullptr, *msig = nullptr, *mdet = nullptr, *mdist = nullptr, *mpd = nullptr;
   long long* mpp = nullptr;
@@ -854,7 +1010,7 @@ int gcs_pmap_destroy(gcs_pmap* p) {
     if (f) (void)hipFree(f);
   void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->offs, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
                   p->fv, p->fv_s, p->ftemp, p->mark, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
-                  p->msel, p->mnsel};
+                  p->msel, p->mnsel, p->ub};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (p->h_small) (void)hipHostFree(p->h_small);
@@ -1099,6 +1255,152 @@ int gcs_pmap_merge_reduce(gcs_pmap* p, int32_t tile, double thr, int32_t max_pai
   PMCHK(p, hipGetLastError());
   PMCHK(p, hipStreamSynchronize(p->stream));
   *count = *(int32_t*)(p->h_small + 40960);
+  return GCS_OK;
+}
+
+int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_ids, int32_t n, const double* z_t6,
+                        double timestamp, int64_t scan_seq, int64_t* next_global_id,
+                        const gcs_pmap_update_config* cfg, const gcs_pmap_update_inputs* in,
+                        gcs_pmap_update_stats* st, int32_t* counts) {
+  if (!p || !z_t6 || !next_global_id || !cfg || !in || !st || !counts || !tile_ids) return GCS_ERR_ARG;
+  if (int rc = check_tiles(p, tiles, n, false)) return rc;
+  if (in->n_total < 1 || in->k_assoc < 1 || !in->Lambdas || !in->thetas || !in->etas || !in->weights || !in->valid ||
+      !in->responsibilities || !in->candidate_tile_ids || !in->candidate_slots || !in->row_masses)
+    return pm_fail(p, GCS_ERR_ARG, "map update: missing measurement or association array");
+  if (cfg->block_size < 1 || cfg->k_insert_tile < 0 || in->n_lobes != p->nl)
+    return pm_fail(p, GCS_ERR_ARG, "map update: bad block size, insert budget or lobe count");
+  memset(st, 0, sizeof(*st));
+  if (n == 0) return GCS_OK;
+  PMCHK(p, hipSetDevice(p->device));
+  PmWorld W{};
+  so3_exp(z_t6 + 3, W.R);
+  for (int k = 0; k < 3; ++k) W.t[k] = z_t6[k];
+  W.eps_lift = cfg->eps_lift;
+  PmMeas m{in->Lambdas, in->thetas, in->etas, in->weights, in->colors, in->valid, in->sources, in->n_total,
+           in->responsibilities, in->candidate_tile_ids, in->candidate_slots, in->row_masses, in->k_assoc};
+  const int N = in->n_total, K = in->k_assoc, B = cfg->block_size, nl = p->nl;
+  const int nb = (N + B - 1) / B;
+  const int nrows = nb * B * K;
+  const int kins = std::min(cfg->k_insert_tile, N);
+  const int nprop = n * kins;
+  const int R = std::max(nrows, nprop);
+  // row buffers: lam 9, th 3, eta 3 nl, w, resp, col 3, fm (f64); valid (u8); src, tpos, slots (i32)
+  const size_t f64s = (size_t)R * (9 + 3 + 3 * nl + 1 + 1 + 3 + 1);
+  const size_t need = f64s * 8 + (size_t)R * (1 + 12) + (size_t)n * N * 8 + (size_t)n * kins * 4 + (size_t)N * 8 +
+                      n * 8 + 256;
+  if (need > p->ub_bytes) {
+    if (p->ub) PMCHK(p, hipFree(p->ub));
+    p->ub = nullptr;
+    PMCHK(p, hipMalloc(&p->ub, need));
+    p->ub_bytes = need;
+  }
+  double* f = (double*)p->ub;
+  PmRowBuf o{};
+  o.lam = f; f += (size_t)R * 9;
+  o.th = f; f += (size_t)R * 3;
+  o.eta = f; f += (size_t)R * 3 * nl;
+  o.w = f; f += R;
+  o.resp = f; f += R;
+  o.col = f; f += (size_t)R * 3;
+  o.fm = f; f += R;
+  double* score = f; f += (size_t)n * N;
+  int32_t* slot_of = (int32_t*)f;  // behind the scores (k_pm_proposals' layout)
+  int64_t* mtile = (int64_t*)((char*)slot_of + (((size_t)n * kins * 4 + 7) & ~(size_t)7));
+  int64_t* act = mtile + N;
+  char* c8 = (char*)(act + n);
+  o.valid = (uint8_t*)c8;
+  int32_t* i32 = (int32_t*)(c8 + (((size_t)R + 7) & ~(size_t)7));
+  o.src = i32; i32 += R;
+  o.tpos = i32; i32 += R;
+  o.slots = i32;
+  (void)slot_of;
+  PMCHK(p, hipMemcpyAsync(act, tile_ids, n * sizeof(int64_t), hipMemcpyHostToDevice, p->stream));
+  // fuse: per association block, every active tile (pipeline.py:1265-1327)
+  hipLaunchKernelGGL(k_pm_fuse_rows, dim3((nrows + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream, m, W,
+                     nl, B, nrows, (const int64_t*)act, n, o);
+  PMCHK(p, hipGetLastError());
+  std::vector<double> fm(nrows);
+  std::vector<int32_t> tp(nrows);
+  PMCHK(p, hipMemcpyAsync(fm.data(), o.fm, nrows * 8, hipMemcpyDeviceToHost, p->stream));
+  PMCHK(p, hipMemcpyAsync(tp.data(), o.tpos, nrows * 4, hipMemcpyDeviceToHost, p->stream));
+  for (int b = 0; b < nb; ++b) {
+    const size_t r0 = (size_t)b * B * K;
+    gcs_pmap_rows rb{};
+    rb.Lambdas = o.lam + 9 * r0;
+    rb.thetas = o.th + 3 * r0;
+    rb.etas = o.eta + (size_t)3 * nl * r0;
+    rb.weights = o.w + r0;
+    rb.responsibilities = o.resp + r0;
+    rb.valid = o.valid + r0;
+    rb.colors = o.col + 3 * r0;
+    rb.sources = o.src + r0;
+    rb.tile_pos = o.tpos + r0;
+    rb.slots = o.slots + r0;
+    rb.n = B * K;
+    int32_t nf = 0;
+    if (int rc = gcs_pmap_fuse(p, tiles, n, &rb, timestamp, scan_seq, cfg->eps_mass, &nf)) return rc;
+    st->fused_count += n * nf;
+    for (int t = 0; t < n; ++t) {  // fused_mass_total: per (block, tile) sums (pipeline.py:1306-1308)
+      double sm = 0.0;
+      for (int q = 0; q < B * K; ++q)
+        if (tp[r0 + q] == t) sm += fm[r0 + q];
+      st->fused_mass_total += sm;
+    }
+  }
+  // novelty insertion per active tile (pipeline.py:1331-1392)
+  if (kins > 0) {
+    hipLaunchKernelGGL(k_pm_proposals, dim3(n), dim3(kPropThreads), 0, p->stream, m, W, nl, cfg->eps_mass, cfg->h_tile,
+                       (const int64_t*)act, kins, score, mtile, o);
+    PMCHK(p, hipGetLastError());
+    std::vector<double> wi(nprop);
+    PMCHK(p, hipMemcpyAsync(wi.data(), o.w, nprop * 8, hipMemcpyDeviceToHost, p->stream));
+    gcs_pmap_rows rp{};
+    rp.Lambdas = o.lam;
+    rp.thetas = o.th;
+    rp.etas = o.eta;
+    rp.weights = o.w;
+    rp.valid = o.valid;
+    rp.colors = o.col;
+    rp.sources = o.src;
+    rp.n = nprop;
+    std::vector<int32_t> ni(n);
+    if (int rc = gcs_pmap_insert_masked(p, tiles, n, kins, &rp, timestamp, scan_seq, cfg->recency_decay_lambda,
+                                        *next_global_id, nullptr, ni.data(), counts))
+      return rc;
+    for (int t = 0; t < n; ++t) {
+      st->insert_count_total += ni[t];
+      *next_global_id += ni[t];
+      std::vector<double> ws(wi.begin() + (size_t)t * kins, wi.begin() + (size_t)(t + 1) * kins);
+      double sm = 0.0;
+      for (double x : ws) sm += x;
+      st->insert_mass_total += sm;
+      std::sort(ws.begin(), ws.end());
+      const int i95 = std::min((int)(0.95 * (double)kins), kins - 1);
+      st->insert_mass_p95 = std::max(st->insert_mass_p95, ws[i95]);
+    }
+  }
+  // per tile: cull, forget, merge-reduce (pipeline.py:1413-1447)
+  std::vector<int32_t> nc(n);
+  std::vector<double> md(n), wsum(n);
+  if (int rc = gcs_pmap_cull(p, tiles, n, cfg->cull_threshold, nc.data(), md.data(), wsum.data(), counts)) return rc;
+  for (int t = 0; t < n; ++t) {
+    st->evicted_count += nc[t];
+    st->evicted_mass_total += nc[t] ? md[t] : 0.0;
+  }
+  if (int rc = gcs_pmap_forget(p, tiles, n, cfg->forgetting_factor)) return rc;
+  const bool capped = cfg->merge_max_tile_size > 0 && p->M > cfg->merge_max_tile_size;
+  if (!capped && cfg->k_merge_pairs > 0 && p->M >= 2) {
+    if (p->M > p->max_merge) return pm_fail(p, GCS_ERR_ARG, "map update: merge needs max_merge >= m_tile");
+    std::vector<int32_t> pairs(2 * (size_t)cfg->k_merge_pairs);
+    for (int t = 0; t < n; ++t) {
+      if (counts[t] < 2) continue;
+      int32_t nm = 0;
+      if (int rc = gcs_pmap_merge_reduce(p, tiles[t], cfg->merge_threshold, cfg->k_merge_pairs, cfg->eps_psd,
+                                         cfg->eps_lift, &nm, pairs.data(), &counts[t]))
+        return rc;
+      st->merged_count += nm;
+    }
+  }
   return GCS_OK;
 }
 

@@ -148,6 +148,26 @@ class GcsPmapRows(C.Structure):
                                           "colors", "sources", "tile_pos", "slots")] + [("n", C.c_int32)]
 
 
+class GcsPmapUpdateConfig(C.Structure):
+    _fields_ = [("k_insert_tile", C.c_int32), ("block_size", C.c_int32), ("k_merge_pairs", C.c_int32),
+                ("merge_max_tile_size", C.c_int32), ("h_tile", C.c_double), ("recency_decay_lambda", C.c_double),
+                ("cull_threshold", C.c_double), ("forgetting_factor", C.c_double), ("merge_threshold", C.c_double),
+                ("eps_lift", C.c_double), ("eps_mass", C.c_double), ("eps_psd", C.c_double)]
+
+
+class GcsPmapUpdateInputs(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in ("Lambdas", "thetas", "etas", "weights", "valid", "colors", "sources")] + \
+               [("n_total", C.c_int32), ("n_lobes", C.c_int32)] + \
+               [(n, C.c_void_p) for n in ("responsibilities", "candidate_tile_ids", "candidate_slots", "row_masses")] + \
+               [("k_assoc", C.c_int32)]
+
+
+class GcsPmapUpdateStats(C.Structure):
+    _fields_ = [("fused_count", C.c_int32), ("insert_count_total", C.c_int32), ("evicted_count", C.c_int32),
+                ("merged_count", C.c_int32), ("fused_mass_total", C.c_double), ("insert_mass_total", C.c_double),
+                ("insert_mass_p95", C.c_double), ("evicted_mass_total", C.c_double)]
+
+
 class GcsAssocOutputs(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("responsibilities", "candidate_pool_indices", "candidate_tile_ids",
                                           "candidate_slots", "row_masses", "cost_matrix")] + \
@@ -261,6 +281,9 @@ _SIGS = [
                                            c_double_p]),
     ("gcs_pmap_merge_reduce", C.c_int, [C.c_void_p, C.c_int32, C.c_double, C.c_int32, C.c_double, C.c_double,
                                         c_int32_p, c_int32_p, c_int32_p]),
+    ("gcs_pmap_map_update", C.c_int, [C.c_void_p, c_int32_p, c_int64_p, C.c_int32, c_double_p, C.c_double, C.c_int64,
+                                      c_int64_p, C.POINTER(GcsPmapUpdateConfig), C.POINTER(GcsPmapUpdateInputs),
+                                      C.POINTER(GcsPmapUpdateStats), c_int32_p]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]

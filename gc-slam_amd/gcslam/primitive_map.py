@@ -10,6 +10,8 @@ in HBM and the maintenance operators with the reference's calling conventions
   primitive_map_forget           :1314-1384
   primitive_map_recency_inflate  :1400-1484
   primitive_map_merge_reduce     :1809-2031
+  primitive_map_update           pipeline.py:1232-1492 (step 12b: fuse per association block, novelty
+                                 insertion, cull / forget / merge per active tile) in one library call
 
 Each operator returns the reference's (result, CertBundle, ExpectedEffect).  The reference's
 AtlasMap is immutable (every operator returns a new one); this one is updated in place on the GPU
@@ -495,3 +497,70 @@ def primitive_map_merge_reduce(atlas_map: AtlasMap, tile_id: int,
                                         mass_epsilon_ratio=float(n) / float(max(M, 1))))
     return (PrimitiveMapMergeReduceResult(atlas_map, int(tile_id), n, float(n)), cert,
             ExpectedEffect("primitive_map_merge_reduce", float(max_pairs), float(n)))
+
+
+@dataclass
+class PrimitiveMapUpdateConfig:
+    """The PipelineConfig fields step 12b reads (pipeline.py:187-206)."""
+    k_insert_tile: int = 64                  # GC_K_INSERT_TILE
+    block_size: int = 256                    # GC_ASSOC_BLOCK_SIZE
+    k_merge_pairs_tile: int = GC_K_MERGE_PAIRS_PER_TILE
+    primitive_merge_max_tile_size: int = GC_PRIMITIVE_MERGE_MAX_TILE_SIZE
+    H_TILE: float = 2.0
+    RECENCY_DECAY_LAMBDA: float = GC_RECENCY_DECAY_LAMBDA
+    primitive_cull_weight_threshold: float = GC_PRIMITIVE_CULL_WEIGHT_THRESHOLD
+    primitive_forgetting_factor: float = GC_PRIMITIVE_FORGETTING_FACTOR
+    primitive_merge_threshold: float = GC_PRIMITIVE_MERGE_THRESHOLD
+    eps_lift: float = GC_EPS_LIFT
+    eps_mass: float = GC_EPS_MASS
+    eps_psd: float = GC_EPS_PSD
+
+
+def primitive_map_update(atlas_map: AtlasMap, measurement_batch, assoc_result, z_t, active_tile_ids: List[int],
+                         timestamp: float, scan_seq: int, config: Optional[PrimitiveMapUpdateConfig] = None) -> dict:
+    """pipeline.py:1244-1447 (step 12b) on the GPU: the scan's MeasurementBatch (body frame) fused into
+    the active tiles at z_t = [t, rotvec] through the association result, novelty insertion, then
+    cull / forget / merge-reduce per tile.  Returns the MapUpdateCert counters (:1457-1486)."""
+    torch = _torch()
+    cfg = config or PrimitiveMapUpdateConfig()
+    dev = f"cuda:{atlas_map.device}"
+    f64 = lambda x: torch.as_tensor(x, device=dev).to(torch.float64).contiguous()  # noqa: E731
+    i64 = lambda x: torch.as_tensor(x, device=dev).to(torch.int64).contiguous()  # noqa: E731
+    b, a = measurement_batch, assoc_result
+    keep = [f64(b.Lambdas), f64(b.thetas), f64(b.etas), f64(b.weights),
+            torch.as_tensor(b.valid_mask, device=dev).to(torch.uint8).contiguous(),
+            f64(b.colors) if getattr(b, "colors", None) is not None else None,
+            torch.as_tensor(b.sources, device=dev).to(torch.int32).contiguous()
+            if getattr(b, "sources", None) is not None else None,
+            f64(a.responsibilities), i64(a.candidate_tile_ids), i64(a.candidate_slots), f64(a.row_masses)]
+    N, K = int(keep[7].shape[0]), int(keep[7].shape[1])
+    inp = L.GcsPmapUpdateInputs()
+    for name, t in zip(("Lambdas", "thetas", "etas", "weights", "valid", "colors", "sources", "responsibilities",
+                        "candidate_tile_ids", "candidate_slots", "row_masses"), keep):
+        setattr(inp, name, t.data_ptr() if t is not None else None)
+    inp.n_total, inp.n_lobes, inp.k_assoc = N, int(keep[2].reshape(N, -1, 3).shape[1]), K
+    c = L.GcsPmapUpdateConfig(int(cfg.k_insert_tile), int(cfg.block_size), int(cfg.k_merge_pairs_tile),
+                              int(cfg.primitive_merge_max_tile_size), float(cfg.H_TILE), float(cfg.RECENCY_DECAY_LAMBDA),
+                              float(cfg.primitive_cull_weight_threshold), float(cfg.primitive_forgetting_factor),
+                              float(cfg.primitive_merge_threshold), float(cfg.eps_lift), float(cfg.eps_mass),
+                              float(cfg.eps_psd))
+    idx, ip = _tiles_arg([atlas_map.index(t, create=True) for t in active_tile_ids])
+    tids = np.ascontiguousarray(np.asarray(active_tile_ids, dtype=np.int64))
+    z = np.ascontiguousarray(np.asarray(z_t, dtype=np.float64).reshape(6))
+    nxt = np.array([atlas_map.next_global_id], dtype=np.int64)
+    cnt = np.zeros(max(len(active_tile_ids), 1), np.int32)
+    st = L.GcsPmapUpdateStats()
+    atlas_map._stream()
+    atlas_map._chk(atlas_map.lib.gcs_pmap_map_update(
+        atlas_map.h, ip, tids.ctypes.data_as(L.c_int64_p), len(active_tile_ids), L.dptr(z), float(timestamp),
+        int(scan_seq), nxt.ctypes.data_as(L.c_int64_p), C.byref(c), C.byref(inp), C.byref(st), L.iptr(cnt)),
+        "gcs_pmap_map_update")
+    atlas_map.total_count += int(st.insert_count_total) - int(st.evicted_count) - int(st.merged_count)
+    atlas_map.next_global_id = int(nxt[0])
+    for k, t in enumerate(active_tile_ids):
+        atlas_map.counts[int(t)] = int(cnt[k])
+    return dict(n_active_tiles=len(active_tile_ids), tile_ids_active=[int(t) for t in active_tile_ids],
+                insert_count_total=int(st.insert_count_total), insert_mass_total=float(st.insert_mass_total),
+                insert_mass_p95=float(st.insert_mass_p95), evicted_count=int(st.evicted_count),
+                evicted_mass_total=float(st.evicted_mass_total), fused_count=int(st.fused_count),
+                fused_mass_total=float(st.fused_mass_total), merged_count=int(st.merged_count))

@@ -596,6 +596,53 @@ int gcs_pmap_recency_inflate(gcs_pmap* pm, const int32_t* tiles, int32_t n, int6
 int gcs_pmap_merge_reduce(gcs_pmap* pm, int32_t tile, double merge_threshold, int32_t max_pairs, double eps_psd,
                           double eps_lift, int32_t* n_merged, int32_t* pairs, int32_t* count);
 
+/* Step 12b of process_scan_single_hypothesis (pipeline.py:1232-1492): the map update at z_t from the
+ * scan's MeasurementBatch and PrimitiveAssociationResult over the n active tiles (storage indices +
+ * MA-hex ids, the association stencil's tiles): per association block (block_associations_for_fuse,
+ * primitive_association.py:561-588) the world-frame rows fused into every active tile; the novelty
+ * proposals (a - row mass)+ w of the measurements whose world mean falls in the tile, k_insert_tile
+ * per tile by a stable rank, inserted masked (ids from *next_global_id, advanced); then cull, forget
+ * and merge-reduce per tile (the merge only when m_tile <= merge_max_tile_size, else the reference's
+ * budget cap).  counts (host, n): the tiles' valid counts afterwards. */
+typedef struct {            /* PipelineConfig fields (pipeline.py:187-206) and operator epsilons */
+  int32_t k_insert_tile;    /* GC_K_INSERT_TILE = 64 */
+  int32_t block_size;       /* GC_ASSOC_BLOCK_SIZE = 256 */
+  int32_t k_merge_pairs;    /* GC_K_MERGE_PAIRS_PER_TILE = 4 */
+  int32_t merge_max_tile_size;  /* GC_PRIMITIVE_MERGE_MAX_TILE_SIZE = 2048 */
+  double h_tile;            /* GC_H_TILE = 2.0 */
+  double recency_decay_lambda;  /* 0.02 */
+  double cull_threshold;    /* 1e-4 */
+  double forgetting_factor; /* 0.995 */
+  double merge_threshold;   /* 0.1 */
+  double eps_lift, eps_mass, eps_psd;  /* 1e-9, 1e-12, 1e-12 */
+} gcs_pmap_update_config;
+
+typedef struct {            /* device pointers */
+  const double* Lambdas;    /* MeasurementBatch: n_total x 9 (body frame) */
+  const double* thetas;     /* n_total x 3 */
+  const double* etas;       /* n_total x n_lobes x 3 */
+  const double* weights;    /* n_total */
+  const uint8_t* valid;     /* n_total */
+  const double* colors;     /* n_total x 3, may be NULL */
+  const int32_t* sources;   /* n_total, may be NULL (LiDAR) */
+  int32_t n_total, n_lobes;
+  const double* responsibilities;    /* PrimitiveAssociationResult: n_total x k_assoc */
+  const int64_t* candidate_tile_ids; /* n_total x k_assoc */
+  const int64_t* candidate_slots;    /* n_total x k_assoc */
+  const double* row_masses;          /* n_total */
+  int32_t k_assoc;
+} gcs_pmap_update_inputs;
+
+typedef struct {            /* MapUpdateCert counters (pipeline.py:1454-1487) */
+  int32_t fused_count, insert_count_total, evicted_count, merged_count;
+  double fused_mass_total, insert_mass_total, insert_mass_p95, evicted_mass_total;
+} gcs_pmap_update_stats;
+
+int gcs_pmap_map_update(gcs_pmap* pm, const int32_t* tiles, const int64_t* tile_ids, int32_t n, const double* z_t6,
+                        double timestamp, int64_t scan_seq, int64_t* next_global_id,
+                        const gcs_pmap_update_config* cfg, const gcs_pmap_update_inputs* in,
+                        gcs_pmap_update_stats* stats, int32_t* counts);
+
 #ifdef __cplusplus
 }
 #endif

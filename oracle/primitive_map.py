@@ -304,3 +304,98 @@ def merge_reduce(tile, merge_threshold=GC_PRIMITIVE_MERGE_THRESHOLD, max_pairs=G
         tile["valid_mask"][j] = False
     n = len(pairs)
     return n, ("merged" if n > 0 else "noop"), pairs
+
+
+GC_K_INSERT_TILE = 64        # constants.py:476-477
+GC_ASSOC_BLOCK_SIZE = 256    # constants.py:473
+BITS_PER_AXIS, BIAS = 21, 1 << 20   # tiling.py:80-81
+MASK = (1 << BITS_PER_AXIS) - 1
+
+
+def tile_ids_from_xyz(X, h_tile):
+    """tiling.py:126-145 (packed MA-hex tile ids of world points)."""
+    X = np.asarray(X, np.float64).reshape(-1, 3)
+    h = max(float(h_tile), 1e-12)
+    s2 = X[:, 0] * 0.5 + X[:, 1] * (np.sqrt(3.0) * 0.5)
+    c1, c2, cz = (np.floor(X[:, 0] / h).astype(np.int64), np.floor(s2 / h).astype(np.int64),
+                  np.floor(X[:, 2] / h).astype(np.int64))
+    return (((c1 + BIAS) & MASK) << (2 * BITS_PER_AXIS)) | (((c2 + BIAS) & MASK) << BITS_PER_AXIS) | ((cz + BIAS) & MASK)
+
+
+def to_world(R, t, Lambdas, thetas, etas, eps_lift=GC_EPS_LIFT):
+    """pipeline.py:1248-1256 transform_gaussian_to_world, vmapped: (R Lambda) R^T, R mu + t, Lambda_w mu_w,
+    each lobe R eta."""
+    Lw = (R[None] @ np.asarray(Lambdas, np.float64)) @ R.T[None]
+    mu_b = _solve(np.asarray(Lambdas, np.float64) + eps_lift * np.eye(3)[None], np.asarray(thetas, np.float64))
+    mu_w = (R[None] @ mu_b[..., None])[..., 0] + t[None]
+    return Lw, (Lw @ mu_w[..., None])[..., 0], (R[None, None] @ np.asarray(etas, np.float64)[..., None])[..., 0]
+
+
+def map_update_step(tiles, next_global_id, batch, assoc, R, t, active_tile_ids, m_tile, timestamp, scan_seq,
+                    k_insert_tile=GC_K_INSERT_TILE, h_tile=2.0, block_size=GC_ASSOC_BLOCK_SIZE,
+                    recency_decay_lambda=GC_RECENCY_DECAY_LAMBDA, cull_threshold=GC_PRIMITIVE_CULL_WEIGHT_THRESHOLD,
+                    forgetting_factor=GC_PRIMITIVE_FORGETTING_FACTOR, merge_threshold=GC_PRIMITIVE_MERGE_THRESHOLD,
+                    k_merge_pairs=GC_K_MERGE_PAIRS_PER_TILE, merge_max_tile_size=GC_PRIMITIVE_MERGE_MAX_TILE_SIZE,
+                    eps_lift=GC_EPS_LIFT, eps_mass=GC_EPS_MASS, eps_psd=GC_EPS_PSD):
+    """pipeline.py:1244-1447 (step 12b): fuse per association block and active tile, novelty
+    insertion per active tile, then cull / forget / merge-reduce per active tile.  batch: dict
+    Lambdas, thetas, etas, weights, valid_mask, colors, sources; assoc: dict responsibilities,
+    candidate_tile_ids, candidate_slots, row_masses.  tiles: dict id -> tile (missing active tiles are
+    created).  Returns (next_global_id, MapUpdateCert counters dict)."""
+    for tid in active_tile_ids:
+        tiles.setdefault(int(tid), create_empty_tile(m_tile, np.asarray(batch["etas"]).shape[1]))
+    valid = np.asarray(batch["valid_mask"], bool)
+    N, K = np.asarray(assoc["responsibilities"]).shape
+    st = dict(fused_count=0, fused_mass_total=0.0, insert_count_total=0, insert_mass_total=0.0, insert_mass_p95=0.0,
+              evicted_count=0, evicted_mass_total=0.0, merged_count=0)
+    nb = (N + block_size - 1) // block_size
+    for b in range(nb):   # block_associations_for_fuse (primitive_association.py:561-588)
+        idx = np.arange(b * block_size, (b + 1) * block_size)
+        mi = np.minimum(idx, N - 1)
+        vr = (idx < N) & valid[mi]
+        tile_flat = np.asarray(assoc["candidate_tile_ids"])[mi].reshape(-1).astype(np.int64)
+        slot_flat = np.asarray(assoc["candidate_slots"])[mi].reshape(-1).astype(np.int32)
+        resp = (np.asarray(assoc["responsibilities"])[mi] * vr[:, None]).reshape(-1)
+        vflat = np.repeat(vr, K)
+        rep = lambda x: np.repeat(np.asarray(x)[mi], K, axis=0)  # noqa: E731
+        Lw, thw, ew = to_world(R, t, rep(batch["Lambdas"]), rep(batch["thetas"]), rep(batch["etas"]), eps_lift)
+        wm = rep(batch["weights"])
+        for tid in active_tile_ids:
+            vt = vflat & (tile_flat == int(tid))
+            st["fused_mass_total"] += float(np.sum(wm * resp * vt.astype(np.float64)))
+            st["fused_count"] += fuse(tiles[int(tid)], slot_flat, Lw, thw, ew, wm, resp, timestamp, scan_seq,
+                                      valid_mask=vt, colors_meas=rep(batch["colors"]),
+                                      sources_meas=rep(batch["sources"]), eps_mass=eps_mass)
+    a = valid.astype(np.float64)
+    a = a / max(np.sum(a), eps_mass)
+    novelty = np.maximum(a - np.asarray(assoc["row_masses"], np.float64), 0.0)
+    w = np.asarray(batch["weights"], np.float64)
+    score = novelty * w - (1.0 - valid.astype(np.float64)) * 1e6
+    mu_b = _solve(np.asarray(batch["Lambdas"]) + eps_lift * np.eye(3)[None], np.asarray(batch["thetas"]))
+    mtid = tile_ids_from_xyz((R[None] @ mu_b[..., None])[..., 0] + t[None], h_tile)
+    for tid in active_tile_ids:
+        it = mtid == int(tid)
+        sc = np.where(it, score, -1e30)
+        ins = np.argsort(-sc, kind="stable")[:k_insert_tile]
+        vn = it[ins] & (sc[ins] > -1e20)
+        if not vn.any():
+            vn = np.ones_like(vn)
+        wi = np.where(it[ins], novelty[ins] * w[ins], 0.0)
+        st["insert_mass_total"] += float(np.sum(wi))
+        ws = np.sort(wi)
+        if ws.shape[0] > 0:
+            st["insert_mass_p95"] = max(st["insert_mass_p95"], float(ws[min(int(0.95 * ws.shape[0]), ws.shape[0] - 1)]))
+        Lw, thw, ew = to_world(R, t, np.asarray(batch["Lambdas"])[ins], np.asarray(batch["thetas"])[ins],
+                               np.asarray(batch["etas"])[ins], eps_lift)
+        n, _, _, next_global_id = insert_masked(tiles[int(tid)], next_global_id, Lw, thw, ew, wi, timestamp, vn,
+                                                scan_seq, recency_decay_lambda, np.asarray(batch["colors"])[ins],
+                                                np.asarray(batch["sources"])[ins])
+        st["insert_count_total"] += n
+    for tid in active_tile_ids:
+        n, dropped, _ = cull(tiles[int(tid)], cull_threshold, eps_mass)
+        st["evicted_count"] += n
+        st["evicted_mass_total"] += dropped
+        forget(tiles[int(tid)], forgetting_factor)
+        st["merged_count"] += merge_reduce(tiles[int(tid)], merge_threshold, k_merge_pairs, merge_max_tile_size,
+                                           eps_psd, eps_lift)[0]
+    return next_global_id, st

@@ -211,3 +211,45 @@ def test_reference_merge_and_color_tests_on_gpu():
         expect = first if second == 0 else want
         assert np.allclose(am.read_tile(0)["rgb"][0], expect, atol=1e-6)
         am.close()
+
+
+def test_map_update_step_matches_oracle():
+    """Step 12b (pipeline.py:1244-1447) through gcs_pmap_map_update against the oracle's restatement:
+    per-block fuse into the active tiles, novelty insertion, cull / forget; a second scan merges
+    (m_tile <= merge_max_tile_size)."""
+    from types import SimpleNamespace
+    from gcslam import primitive_map as gpm
+    from oracle import se3
+    rng = np.random.default_rng(6)
+    m, N, K = 1024, 600, 8
+    tiles = {}
+    am = gpm.AtlasMap(m_tile=m, max_tiles=16, n_lobes=NL, max_merge=m)
+    z = np.array([1.5, -0.7, 0.3, 0.02, -0.01, 0.4])
+    R, t = se3.so3_exp(z[3:]), z[:3]
+    for scan in range(2):
+        p_body = rng.uniform(-5, 5, size=(N, 3))
+        A = rng.normal(size=(N, 3, 3)) * 0.2
+        Lam = np.einsum("nij,nkj->nik", A, A) + np.eye(3)[None] * rng.uniform(1, 5, size=(N, 1, 1))
+        batch = dict(Lambdas=Lam, thetas=np.einsum("nij,nj->ni", Lam, p_body), etas=rng.normal(size=(N, NL, 3)),
+                     weights=rng.random(N), valid_mask=rng.random(N) < 0.9, colors=rng.random((N, 3)),
+                     sources=rng.integers(0, 2, N).astype(np.int32))
+        wtid = opm.tile_ids_from_xyz(p_body @ R.T + t[None], 2.0)
+        uniq, cnts = np.unique(wtid, return_counts=True)
+        active = [int(x) for x in uniq[np.argsort(-cnts, kind="stable")][:6]] + [12345]
+        ctile = rng.choice(np.array(active[:6] + [777], dtype=np.int64), size=(N, K))
+        assoc = dict(responsibilities=rng.random((N, K)) / K, candidate_tile_ids=ctile,
+                     candidate_slots=rng.integers(0, m, size=(N, K)), row_masses=rng.random(N) * 2.0 / N)
+        nxt_ref, st_ref = opm.map_update_step(tiles, am.next_global_id, batch, assoc, R, t, active, m, 3.0 + scan,
+                                              10 + scan, k_insert_tile=64, h_tile=2.0)
+        st = gpm.primitive_map_update(am, SimpleNamespace(**batch), SimpleNamespace(**assoc), z, active, 3.0 + scan,
+                                      10 + scan)
+        assert am.next_global_id == nxt_ref
+        for k in ("fused_count", "insert_count_total", "evicted_count", "merged_count"):
+            assert st[k] == st_ref[k], k
+        for k in ("fused_mass_total", "insert_mass_total", "insert_mass_p95", "evicted_mass_total"):
+            assert st[k] == pytest.approx(st_ref[k], rel=1e-12, abs=1e-300), k
+        for tid in active:   # world transforms: so3_exp and LU rounding -> 1e-12 relative
+            _same_tile(am.read_tile(tid), tiles[tid], rtol=1e-11, what=f"scan {scan} tile {tid}")
+            assert am.counts[tid] == int(tiles[tid]["valid_mask"].sum())
+    assert st_ref["insert_count_total"] > 0 and st_ref["fused_count"] > 0
+    am.close()
