@@ -648,6 +648,114 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   }
 }
 
+// ---------------------------------------------------------------- visual pose evidence
+// visual_pose_evidence (FS/backend/operators/visual_pose_evidence.py:260-412) over the first n_meas
+// valid rows: one 1024-thread workgroup, each thread sums its strided rows in order, then a fixed
+// tree.  Per row i (body mean p, direction u, kappa k, Lambda_reg = Lambda + eps I) and candidate j
+// (view position m, direction v, kappa kv, responsibility r):
+//   L_t += (sum_j r) Lambda_reg; h_t += Lambda_reg sum_j r (m - R p); cost_t += r q^T Lambda_reg q,
+//   q = m - R p - t (:121-148);  w = r sqrt(k kv + 1e-12), S += w v u^T, cost_r += w (1 - (R u).v)
+//   (:209-222).  out: L_t 9, h_t 3, cost_t, S 9, cost_r, sum row masses, rows used, map valid count.
+constexpr int kVpeThreads = 1024;
+constexpr int kVpeVals = 27;
+struct VpeIn {
+  const double *Lambdas, *thetas, *etas;
+  const uint8_t* valid;
+  int n, n_lobes, n_meas;
+  const double *vpos, *vdir, *vkap;
+  const uint8_t* vvalid;
+  int m_view;
+  const double *resp, *rmass;
+  const int32_t* cand;
+  int k;
+  double R[9], t[3], eps_lift, eps_mass;
+};
+
+__global__ __launch_bounds__(kVpeThreads) void k_as_vpe(VpeIn in, double* out) {
+#pragma clang fp contract(off)
+  __shared__ int s_w[kVpeThreads / 64];
+  __shared__ double lds[kVpeThreads / 64];
+  double acc[kVpeVals];
+  for (int q = 0; q < kVpeVals; ++q) acc[q] = 0.0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int base = 0;  // valid rows before this chunk
+  for (int c0 = 0; c0 < in.n; c0 += kVpeThreads) {
+    const int i = c0 + threadIdx.x;
+    const int v = i < in.n && in.valid[i] ? 1 : 0;
+    int x = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    __syncthreads();
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    int rank = base + x - v;
+    for (int w = 0; w < wid; ++w) rank += s_w[w];
+    int tot = 0;
+    for (int w = 0; w < kVpeThreads / 64; ++w) tot += s_w[w];
+    base += tot;
+    if (!v || rank >= in.n_meas) continue;
+    double p[3];
+    solve3_pivot(in.Lambdas + 9 * (size_t)i, in.eps_lift, in.thetas + 3 * (size_t)i, p);
+    double es[3] = {0.0, 0.0, 0.0};
+    for (int b = 0; b < in.n_lobes; ++b)
+      for (int c = 0; c < 3; ++c) {
+        const double e = in.etas[(size_t)3 * in.n_lobes * i + 3 * b + c];
+        es[c] = b == 0 ? e : es[c] + e;
+      }
+    const double kap = sqrt((es[0] * es[0] + es[1] * es[1]) + es[2] * es[2]);
+    const double u[3] = {es[0] / (kap + in.eps_mass), es[1] / (kap + in.eps_mass), es[2] / (kap + in.eps_mass)};
+    double Lr[9];
+    for (int c = 0; c < 9; ++c) Lr[c] = in.Lambdas[9 * (size_t)i + c] + ((c % 4) == 0 ? in.eps_lift : 0.0);
+    double Rp[3], Ru[3];
+    for (int r = 0; r < 3; ++r) {
+      Rp[r] = (in.R[3 * r] * p[0] + in.R[3 * r + 1] * p[1]) + in.R[3 * r + 2] * p[2];
+      Ru[r] = (in.R[3 * r] * u[0] + in.R[3 * r + 1] * u[1]) + in.R[3 * r + 2] * u[2];
+    }
+    double rs = 0.0, wt[3] = {0.0, 0.0, 0.0}, ct = 0.0, cr = 0.0, S[9];
+    for (int c = 0; c < 9; ++c) S[c] = 0.0;
+    for (int j = 0; j < in.k; ++j) {
+      const double r = in.resp[(size_t)i * in.k + j];
+      const int e = in.cand[(size_t)i * in.k + j];
+      const double m[3] = {in.vpos[3 * (size_t)e], in.vpos[3 * (size_t)e + 1], in.vpos[3 * (size_t)e + 2]};
+      const double vd[3] = {in.vdir[3 * (size_t)e], in.vdir[3 * (size_t)e + 1], in.vdir[3 * (size_t)e + 2]};
+      rs = rs + r;
+      double q[3], Lq[3];
+      for (int c = 0; c < 3; ++c) {
+        wt[c] = wt[c] + r * (m[c] - Rp[c]);
+        q[c] = (m[c] - Rp[c]) - in.t[c];
+      }
+      for (int a = 0; a < 3; ++a) Lq[a] = (Lr[3 * a] * q[0] + Lr[3 * a + 1] * q[1]) + Lr[3 * a + 2] * q[2];
+      ct = ct + r * ((q[0] * Lq[0] + q[1] * Lq[1]) + q[2] * Lq[2]);
+      const double w = r * sqrt(kap * in.vkap[e] + 1e-12);
+      for (int a = 0; a < 3; ++a)
+        for (int b = 0; b < 3; ++b) S[3 * a + b] = S[3 * a + b] + (w * vd[a]) * u[b];
+      cr = cr + w * (1.0 - ((Ru[0] * vd[0] + Ru[1] * vd[1]) + Ru[2] * vd[2]));
+    }
+    for (int c = 0; c < 9; ++c) acc[c] += rs * Lr[c];
+    for (int a = 0; a < 3; ++a) acc[9 + a] += (Lr[3 * a] * wt[0] + Lr[3 * a + 1] * wt[1]) + Lr[3 * a + 2] * wt[2];
+    acc[12] += ct;
+    for (int c = 0; c < 9; ++c) acc[13 + c] += S[c];
+    acc[22] += cr;
+    acc[23] += in.rmass[i];
+    acc[24] += 1.0;
+  }
+  for (int e = threadIdx.x; e < in.m_view; e += kVpeThreads) acc[25] += in.vvalid[e] ? 1.0 : 0.0;
+  for (int q = 0; q < kVpeVals; ++q) {
+    double v = acc[q];
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+    __syncthreads();
+    if (lane == 0) lds[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double sum = lds[0];
+      for (int w = 1; w < kVpeThreads / 64; ++w) sum += lds[w];
+      out[q] = sum;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace gcs
 
@@ -664,6 +772,8 @@ struct gcs_assoc_ctx {
   int8_t* d_st = nullptr;
   double* h_cert = nullptr;  // pinned, mapped
   double* h_cert_dev = nullptr;
+  double* h_vpe = nullptr;   // pinned, mapped: k_as_vpe's sums
+  double* h_vpe_dev = nullptr;
 };
 
 namespace {
@@ -728,6 +838,7 @@ int gcs_assoc_ctx_destroy(gcs_assoc_ctx* c) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_cert) (void)hipHostFree(c->h_cert);
+  if (c->h_vpe) (void)hipHostFree(c->h_vpe);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
   return GCS_OK;
@@ -751,7 +862,9 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
       bad(hipMalloc(&c->d_tix, N * kMaxStencil * 4)) || bad(hipMalloc(&c->d_cand, NK * 4)) ||
       bad(hipMalloc(&c->d_mvalid, 4)) || bad(hipMalloc(&c->d_st, kMaxStencil * 3)) ||
       bad(hipHostMalloc(&c->h_cert, GCS_ASSOC_CERT_LEN * sizeof(double), hipHostMallocMapped)) ||
-      bad(hipHostGetDevicePointer((void**)&c->h_cert_dev, c->h_cert, 0))) {
+      bad(hipHostGetDevicePointer((void**)&c->h_cert_dev, c->h_cert, 0)) ||
+      bad(hipHostMalloc(&c->h_vpe, 32 * sizeof(double), hipHostMallocMapped)) ||
+      bad(hipHostGetDevicePointer((void**)&c->h_vpe_dev, c->h_vpe, 0))) {
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
@@ -865,6 +978,87 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   for (int q = 0; q < GCS_ASSOC_CERT_LEN; ++q) o->cert[q] = c->h_cert[q];
   o->exact = c->h_cert[CE_EXACT] != 0.0;
   o->n_map_valid = (int32_t)c->h_cert[CE_MVALID];
+  return GCS_OK;
+}
+
+int gcs_visual_pose_evidence(gcs_assoc_ctx* c, const gcs_assoc_meas* m, const gcs_assoc_view* v,
+                             const double* responsibilities, const int32_t* candidate_pool_indices,
+                             const double* row_masses, int32_t k_assoc, const double* z_lin_pose, double eps_lift,
+                             double eps_mass, gcs_vpe_outputs* o) {
+  if (!c || !m || !v || !o || !z_lin_pose) return GCS_ERR_ARG;
+  if (m->n_total < 1 || k_assoc < 1 || !responsibilities || !candidate_pool_indices || !row_masses || !m->Lambdas ||
+      !m->thetas || !m->etas || !m->valid_mask || !v->positions || !v->directions || !v->kappas || !v->valid_mask)
+    return as_fail(c, GCS_ERR_ARG, "visual_pose_evidence: missing measurement, view or association array");
+  ASCHK(c, hipSetDevice(c->device));
+  VpeIn in{};
+  in.Lambdas = m->Lambdas;
+  in.thetas = m->thetas;
+  in.etas = m->etas;
+  in.valid = m->valid_mask;
+  in.n = m->n_total;
+  in.n_lobes = m->n_lobes;
+  in.n_meas = std::max(0, m->n_valid);
+  in.vpos = v->positions;
+  in.vdir = v->directions;
+  in.vkap = v->kappas;
+  in.vvalid = v->valid_mask;
+  in.m_view = v->n_tiles * v->m_tile_view;
+  in.resp = responsibilities;
+  in.rmass = row_masses;
+  in.cand = candidate_pool_indices;
+  in.k = k_assoc;
+  so3_exp(z_lin_pose + 3, in.R);
+  for (int q = 0; q < 3; ++q) in.t[q] = z_lin_pose[q];
+  in.eps_lift = eps_lift;
+  in.eps_mass = eps_mass;
+  hipLaunchKernelGGL(k_as_vpe, dim3(1), dim3(kVpeThreads), 0, c->stream, in, c->h_vpe_dev);
+  ASCHK(c, hipGetLastError());
+  ASCHK(c, hipStreamSynchronize(c->stream));
+  const double* a = c->h_vpe;
+  memset(o, 0, sizeof(*o));
+  for (int q = 0; q < 22; ++q) o->L_pose[23 * q] = eps_lift;
+  const int rows = (int)a[24];
+  if (m->n_valid == 0 || rows == 0 || a[25] == 0.0) {  // the empty case (:293-318)
+    o->exact = 1;
+    return GCS_OK;
+  }
+  for (int q = 0; q < 9; ++q) o->L_trans[q] = a[q] + ((q % 4) == 0 ? eps_lift : 0.0);
+  for (int q = 0; q < 3; ++q) o->h_trans[q] = a[9 + q];
+  // rotation: SVD of the scatter, det-fixed U V^T, R_delta = R_scatter R_pred^T, h = diag(s + eps) log(R_delta)
+  double U[9], sv[3], V[9];
+  svd3(a + 13, U, sv, V);
+  double Rs[9];
+  for (int r = 0; r < 3; ++r)
+    for (int q = 0; q < 3; ++q) Rs[3 * r + q] = (U[3 * r] * V[3 * q] + U[3 * r + 1] * V[3 * q + 1]) + U[3 * r + 2] * V[3 * q + 2];
+  if (det3(Rs) < 0.0)
+    for (int r = 0; r < 3; ++r)
+      for (int q = 0; q < 3; ++q)
+        Rs[3 * r + q] = (U[3 * r] * V[3 * q] + U[3 * r + 1] * V[3 * q + 1]) - U[3 * r + 2] * V[3 * q + 2];
+  double Rd[9];
+  for (int r = 0; r < 3; ++r)
+    for (int q = 0; q < 3; ++q)
+      Rd[3 * r + q] = (Rs[3 * r] * in.R[3 * q] + Rs[3 * r + 1] * in.R[3 * q + 1]) + Rs[3 * r + 2] * in.R[3 * q + 2];
+  double w[3];
+  so3_log(Rd, w);
+  for (int q = 0; q < 3; ++q) {
+    o->L_rot[4 * q] = sv[q] + eps_lift;
+    o->h_rot[q] = o->L_rot[4 * q] * w[q];
+  }
+  for (int r = 0; r < 3; ++r)
+    for (int q = 0; q < 3; ++q) {
+      o->L_pose[22 * r + q] = o->L_trans[3 * r + q];
+      o->L_pose[22 * (3 + r) + 3 + q] = o->L_rot[3 * r + q];
+    }
+  for (int q = 0; q < 3; ++q) {
+    o->h_pose[q] = o->h_trans[q];
+    o->h_pose[3 + q] = o->h_rot[q];
+  }
+  o->total_weighted_cost = a[12] + a[22];
+  o->n_associations = rows * k_assoc;
+  o->mean_transported_mass = a[23] / (double)rows;
+  o->ess_total = a[23];
+  o->support_frac = (double)rows / (double)std::max(m->n_valid, 1);
+  o->exact = 0;
   return GCS_OK;
 }
 

@@ -168,6 +168,13 @@ class GcsPmapUpdateStats(C.Structure):
                 ("insert_mass_p95", C.c_double), ("evicted_mass_total", C.c_double)]
 
 
+class GcsVpeOutputs(C.Structure):
+    _fields_ = [("L_pose", C.c_double * (D_Z * D_Z)), ("h_pose", C.c_double * D_Z), ("L_trans", C.c_double * 9),
+                ("h_trans", C.c_double * 3), ("L_rot", C.c_double * 9), ("h_rot", C.c_double * 3),
+                ("total_weighted_cost", C.c_double), ("mean_transported_mass", C.c_double), ("ess_total", C.c_double),
+                ("support_frac", C.c_double), ("n_associations", C.c_int32), ("exact", C.c_int32)]
+
+
 class GcsAssocOutputs(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("responsibilities", "candidate_pool_indices", "candidate_tile_ids",
                                           "candidate_slots", "row_masses", "cost_matrix")] + \
@@ -260,6 +267,9 @@ _SIGS = [
     ("gcs_assoc_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("gcs_associate_primitives_ot", C.c_int, [C.c_void_p, C.POINTER(GcsAssocConfig), C.POINTER(GcsAssocMeas),
                                               C.POINTER(GcsAssocView), C.POINTER(GcsAssocOutputs)]),
+    ("gcs_visual_pose_evidence", C.c_int, [C.c_void_p, C.POINTER(GcsAssocMeas), C.POINTER(GcsAssocView), C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_int32, c_double_p, C.c_double, C.c_double,
+                                           C.POINTER(GcsVpeOutputs)]),
     ("gcs_pmap_create", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     ("gcs_pmap_destroy", C.c_int, [C.c_void_p]),
     ("gcs_pmap_last_error", C.c_char_p, [C.c_void_p]),

@@ -180,6 +180,37 @@ class Associator:
         return out, cert, bool(o.exact)
 
 
+    def pose_evidence(self, batch, view: AtlasMapView, result, k_assoc: int, z_lin_pose, eps_lift=GC_EPS_LIFT,
+                      eps_mass=GC_EPS_MASS):
+        """gcs_visual_pose_evidence: the 22-D pose evidence of an association result (host struct)."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        f64 = lambda x: torch.as_tensor(x, device=dev).to(torch.float64).contiguous()  # noqa: E731
+        u8 = lambda x: torch.as_tensor(x, device=dev).to(torch.uint8).contiguous()  # noqa: E731
+        keep = [f64(batch.Lambdas), f64(batch.thetas), f64(batch.etas), u8(batch.valid_mask), f64(view.positions),
+                f64(view.directions), f64(view.kappas), u8(view.valid_mask), f64(result.responsibilities),
+                torch.as_tensor(result.candidate_pool_indices, device=dev).to(torch.int32).contiguous(),
+                f64(result.row_masses)]
+        N = int(keep[0].shape[0])
+        m = L.GcsAssocMeas()
+        m.Lambdas, m.thetas, m.etas, m.valid_mask = (t.data_ptr() for t in keep[:4])
+        m.n_total = N
+        m.n_lobes = int(keep[2].reshape(N, -1, 3).shape[1])
+        m.n_valid = int(batch.n_valid)
+        v = L.GcsAssocView()
+        v.positions, v.directions, v.kappas, v.valid_mask = (t.data_ptr() for t in keep[4:8])
+        v.n_tiles, v.m_tile_view = 1, int(keep[7].shape[0])
+        o = L.GcsVpeOutputs()
+        z = np.ascontiguousarray(np.asarray(z_lin_pose, dtype=np.float64).ravel()[:6])
+        self._chk(self.lib.gcs_assoc_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                  "gcs_assoc_ctx_set_stream")
+        self._chk(self.lib.gcs_visual_pose_evidence(self.h, C.byref(m), C.byref(v), C.c_void_p(keep[8].data_ptr()),
+                                                    C.c_void_p(keep[9].data_ptr()), C.c_void_p(keep[10].data_ptr()),
+                                                    int(k_assoc), L.dptr(z), float(eps_lift), float(eps_mass),
+                                                    C.byref(o)), "gcs_visual_pose_evidence")
+        return o
+
+
 _associators = {}
 
 
@@ -228,3 +259,56 @@ def associate_primitives_ot(measurement_batch, map_view: AtlasMapView, config: O
     effect = ExpectedEffect(objective_name="primitive_association_ot", predicted=cv["total_cost"],
                             realized=cv["total_cost"])
     return result, cert, effect
+
+
+@dataclass
+class VisualPoseEvidenceResult:      # visual_pose_evidence.py:46-66
+    L_pose: np.ndarray
+    h_pose: np.ndarray
+    L_trans: np.ndarray
+    h_trans: np.ndarray
+    L_rot: np.ndarray
+    h_rot: np.ndarray
+    total_weighted_cost: float
+    n_associations: int
+    mean_transported_mass: float
+
+
+def visual_pose_evidence(association_result: PrimitiveAssociationResult, measurement_batch, map_view: AtlasMapView,
+                         belief_pred=None, eps_lift: float = GC_EPS_LIFT, eps_mass: float = GC_EPS_MASS,
+                         chart_id: str = CHART_ID, anchor_id: str = "visual_pose_evidence", z_lin_pose=None,
+                         device: int = 0, associator: Associator = None):
+    """visual_pose_evidence.py:260-412: 22-D pose evidence from the OT soft correspondences at
+    z_lin_pose (or belief_pred.mean_world_pose()).  Returns (VisualPoseEvidenceResult, CertBundle,
+    ExpectedEffect); the sums run on the GPU (gcs_visual_pose_evidence), the 3x3 SVD on the host."""
+    if z_lin_pose is None:
+        if belief_pred is None:
+            raise ValueError("visual_pose_evidence needs z_lin_pose or belief_pred")
+        z_lin_pose = belief_pred.mean_world_pose(eps_lift=eps_lift)
+    torch = _torch()
+    r = association_result.responsibilities
+    N, K = (int(x) for x in (r.shape if torch.is_tensor(r) else np.asarray(r).shape))
+    pool = int(np.asarray(map_view.valid_mask.shape)[0])
+    a = associator or _associator_for(max(N, 1), pool, max(K, 1), device)
+    o = a.pose_evidence(measurement_batch, map_view, association_result, K, z_lin_pose, eps_lift, eps_mass)
+    view = np.ctypeslib.as_array
+    res = VisualPoseEvidenceResult(L_pose=view(o.L_pose).reshape(22, 22).copy(), h_pose=view(o.h_pose).copy(),
+                                   L_trans=view(o.L_trans).reshape(3, 3).copy(), h_trans=view(o.h_trans).copy(),
+                                   L_rot=view(o.L_rot).reshape(3, 3).copy(), h_rot=view(o.h_rot).copy(),
+                                   total_weighted_cost=float(o.total_weighted_cost),
+                                   n_associations=int(o.n_associations),
+                                   mean_transported_mass=float(o.mean_transported_mass))
+    if o.exact:
+        return res, CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id), ExpectedEffect(
+            objective_name="visual_pose_evidence", predicted=0.0, realized=0.0)
+    cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id,
+                                    triggers=["linearization", "ot_soft_correspondence"], frobenius_applied=True,
+                                    support=SupportCert(ess_total=float(o.ess_total), support_frac=float(o.support_frac)),
+                                    influence=InfluenceCert.identity().with_overrides(lift_strength=eps_lift))
+    c = float(o.total_weighted_cost)
+    return res, cert, ExpectedEffect(objective_name="visual_pose_evidence", predicted=c, realized=c)
+
+
+def build_visual_pose_evidence_22d(visual_result: VisualPoseEvidenceResult):
+    """visual_pose_evidence.py:420-433."""
+    return visual_result.L_pose, visual_result.h_pose

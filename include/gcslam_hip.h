@@ -29,6 +29,7 @@
  *   gcs_fibonacci_atlas         archive/bin_atlas.py:40-61
  *   gcs_associate_primitives_ot FS/backend/operators/primitive_association.py:239-553
  *                               associate_primitives_ot (+ tiling.py:148-186, measurement_batch.py:389-411)
+ *   gcs_visual_pose_evidence    FS/backend/operators/visual_pose_evidence.py:260-412 visual_pose_evidence
  *   gcs_pmap_*                  FS/backend/structures/primitive_map.py:98-2031 (AtlasMap tiles in HBM;
  *                               extract_atlas_map_view, insert_masked, fuse, cull, forget,
  *                               recency_inflate, merge_reduce)
@@ -490,6 +491,24 @@ int gcs_assoc_ctx_set_stream(gcs_assoc_ctx* ctx, void* stream);
 /* Synchronises; unsupported policies return GCS_ERR_ARG with the reference's message. */
 int gcs_associate_primitives_ot(gcs_assoc_ctx* ctx, const gcs_assoc_config* cfg, const gcs_assoc_meas* meas,
                                 const gcs_assoc_view* view, gcs_assoc_outputs* out);
+
+/* visual_pose_evidence (visual_pose_evidence.py:260-412): 22-D pose evidence from the association's
+ * soft correspondences at z_lin_pose = [t, rotvec] -- WLS translation (L_t = sum_i (sum_k pi) Lambda_i,
+ * h_t, cost; :104-148) and the vMF scatter rotation (S = sum pi sqrt(k_i k_m) mu_m mu_i^T, SVD,
+ * det-fixed U V^T, so3_log of R_scatter R_pred^T, L_rot = diag(s + eps); :150-240) -- summed in a
+ * fixed order over the first n_valid valid rows on the association context's stream; the 3x3 SVD
+ * and so3_log on the host.  exact = 1: the empty case (L = eps I, h = 0; :293-318). */
+typedef struct {
+  double L_pose[GCS_D_Z * GCS_D_Z], h_pose[GCS_D_Z];
+  double L_trans[9], h_trans[3], L_rot[9], h_rot[3];
+  double total_weighted_cost, mean_transported_mass;
+  double ess_total, support_frac;   /* SupportCert */
+  int32_t n_associations, exact;
+} gcs_vpe_outputs;
+int gcs_visual_pose_evidence(gcs_assoc_ctx* ctx, const gcs_assoc_meas* meas, const gcs_assoc_view* view,
+                             const double* responsibilities, const int32_t* candidate_pool_indices,
+                             const double* row_masses, int32_t k_assoc, const double* z_lin_pose, double eps_lift,
+                             double eps_mass, gcs_vpe_outputs* out);
 
 /* ---------------------------------------------------------------- primitive path: the primitive map */
 /* The AtlasMap's tile storage (FS/backend/structures/primitive_map.py:98-227) resident in HBM, and

@@ -130,3 +130,28 @@ def test_view_top_weights_stable():
     assert v["candidate_tile_ids"].tolist() == [7] * 4 + [8] * 4
     assert v["valid_mask"].tolist() == [True] * 4 + [False] * 4
     assert np.allclose(v["kappas"][:4], 3.0) and np.allclose(v["directions"][0], [0, 0, 3.0 / (3.0 + 1e-12)])
+
+
+def test_visual_pose_evidence_oracle_closed_form():
+    """visual_pose_evidence.py:104-240 on exact correspondences: map = R p + t with one candidate per
+    row -> L_t^{-1} h_t = t, the scatter's rotation is R itself (h_rot = 0), and both costs vanish."""
+    from oracle import primitive_evidence as OE, se3
+    rng = np.random.default_rng(0)
+    N = 40
+    z = np.array([0.5, -1.0, 0.2, 0.1, -0.05, 0.3])
+    R, t = se3.so3_exp(z[3:]), z[:3]
+    p = rng.normal(size=(N, 3))
+    u = rng.normal(size=(N, 3))
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    Lam = np.tile(np.eye(3), (N, 1, 1))
+    etas = np.zeros((N, 3, 3))
+    etas[:, 0] = 5.0 * u
+    batch = dict(Lambdas=Lam, thetas=p, etas=etas, valid_mask=np.ones(N, bool), n_valid=N)
+    view = dict(positions=p @ R.T + t, directions=u @ R.T, kappas=np.full(N, 5.0), valid_mask=np.ones(N, bool))
+    assoc = dict(responsibilities=np.full((N, 1), 1.0 / N), candidate_pool_indices=np.arange(N)[:, None],
+                 row_masses=np.full(N, 1.0 / N))
+    # the measurement mean is (I + eps) ^-1 p: evaluate at the linearisation of the exact pose
+    r = OE.visual_pose_evidence(batch, view, assoc, z, eps_lift=0.0, eps_mass=0.0)
+    assert np.allclose(np.linalg.solve(r["L_trans"], r["h_trans"]), t, atol=1e-12)
+    assert np.allclose(r["h_rot"], 0.0, atol=1e-12) and r["total_weighted_cost"] == pytest.approx(0.0, abs=1e-12)
+    assert r["support_frac"] == 1.0 and r["n_associations"] == N
