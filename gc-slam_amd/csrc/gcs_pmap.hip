@@ -6,7 +6,8 @@
 //   k_pm_keys      one lane per slot: the single sort key of _select_topk_slots_fixed (-score, :316-319)
 //                  or _select_lowest_mass_slots_fixed (retention, :345-351) in order-preserving u64 bits
 //                  (-0.0 and 0.0 equal, as lax.sort's comparator), value = slot; then a stable
-//                  segmented radix sort (rocPRIM), one segment per tile
+//                  radix sort (rocPRIM) of all listed tiles' keys followed by a stable radix sort on the
+//                  tile position: per tile, the key order with ties by slot
 //   k_pm_view      one lane per view entry: the tile's r-th slot, mean (LU solve of Lambda + eps I),
 //                  covariance, resultant direction and kappa (:474-498)
 //   k_pm_insert    one workgroup: tile by tile, the masked proposals into the K lowest-retention slots,
@@ -23,7 +24,6 @@
 // No floating-point atomics; every sum has a fixed order.
 #include <hip/hip_runtime.h>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_segmented_radix_sort.hpp>
 
 #include <math.h>
 #include <string.h>
@@ -39,6 +39,7 @@ namespace gcs {
 namespace {
 
 constexpr int kPmThreads = 256;
+constexpr int kNL = 3;  // vMF lobes per primitive (GC_VMF_N_LOBES, constants.py:463); the context requires it
 constexpr int kPmRed = 1024;  // one-workgroup-per-tile reductions
 constexpr uint32_t kNoKey = 0xffffffffu;
 
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_clear(PmStore st, int t) {
     st.acc[3 * i + k] = 0.0;
     st.rgb[3 * i + k] = 0.5;
   }
-  for (int k = 0; k < 3 * st.nl; ++k) st.eta[(size_t)3 * st.nl * i + k] = 0.0;
+  for (int k = 0; k < 3 * kNL; ++k) st.eta[(size_t)3 * kNL * i + k] = 0.0;
   st.w[i] = st.ts[i] = st.cts[i] = st.cam[i] = st.lid[i] = st.den[i] = 0.0;
   st.lsup[i] = st.lupd[i] = st.ids[i] = 0;
   st.valid[i] = 0;
@@ -147,10 +148,8 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_clear(PmStore st, int t) {
 
 // mode 0: -score (score = w, -1e30 where invalid), mode 1: retention w exp(-lam dt) (-inf where invalid)
 __global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_t* tiles, int n, int mode,
-                                                        long long seq, double lam, uint64_t* keys, uint32_t* vals,
-                                                        int32_t* offs) {
+                                                        long long seq, double lam, uint64_t* keys, uint32_t* vals) {
   const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
-  if (g <= n) offs[g] = (int32_t)(g * st.M);  // segment bounds
   if (g >= (long)n * st.M) return;
   const int t = (int)(g / st.M), q = (int)(g % st.M);
   const int ti = tiles[t];
@@ -172,7 +171,13 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_
     key = v ? w * decay : -INFINITY;
   }
   keys[g] = ord_key(key);
-  vals[g] = (uint32_t)q;
+  vals[g] = (uint32_t)g;  // tile position x M + slot
+}
+
+// second (stable) pass of the per-tile sort: key = the entry's tile position
+__global__ __launch_bounds__(kPmThreads) void k_pm_segkeys(const uint32_t* vals, long total, int M, uint32_t* seg) {
+  const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
+  if (g < total) seg[g] = vals[g] / (uint32_t)M;
 }
 
 struct PmViewOut {
@@ -190,13 +195,13 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_view(PmStore st, const int32_
   if (g >= n * k) return;
   const int t = g / k, r = g % k;
   const int ti = tiles[t];
-  const int q = ti >= 0 ? (int)sorted[(size_t)t * st.M + r] : r;  // a missing tile: all keys equal
+  const int q = ti >= 0 ? (int)(sorted[(size_t)t * st.M + r] % (uint32_t)st.M) : r;  // missing tile: all keys equal
   double L[9], th[3], es[3] = {0.0, 0.0, 0.0}, rgb[3] = {0.5, 0.5, 0.5}, w = 0.0;
   long long id = 0, last = 0;
   uint8_t v = 0;
   for (int c = 0; c < 9; ++c) L[c] = 0.0;
   for (int c = 0; c < 3; ++c) th[c] = 0.0;
-  const int ne = 3 * st.nl;
+  constexpr int ne = 3 * kNL;
   if (ti >= 0) {
     const size_t i = sidx(st, ti, q);
     for (int c = 0; c < 9; ++c) L[c] = st.lam[9 * i + c];
@@ -204,7 +209,7 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_view(PmStore st, const int32_
       th[c] = st.th[3 * i + c];
       rgb[c] = st.rgb[3 * i + c];
     }
-    for (int b = 0; b < st.nl; ++b)
+    for (int b = 0; b < kNL; ++b)
       for (int c = 0; c < 3; ++c) {
         const double e = st.eta[(size_t)ne * i + 3 * b + c];
         es[c] = b == 0 ? e : es[c] + e;
@@ -257,7 +262,7 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_insert(PmStore st, const int3
   __shared__ int s_w[kPmThreads / 64];
   long long base = next_id;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int ne = 3 * st.nl;
+  constexpr int ne = 3 * kNL;
   for (int t = 0; t < n; ++t) {
     const int ti = tiles[t];
     int run = 0;
@@ -281,7 +286,7 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_insert(PmStore st, const int3
         const long long id = d ? base + pre : -1;
         if (ids_out) ids_out[row] = id;
         if (d) {
-          const size_t i = sidx(st, ti, (int)sorted[(size_t)t * st.M + q]);
+          const size_t i = sidx(st, ti, (int)(sorted[(size_t)t * st.M + q] % (uint32_t)st.M));
           for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = r.lam[9 * (size_t)row + c];
           for (int c = 0; c < 3; ++c) st.th[3 * i + c] = r.th[3 * (size_t)row + c];
           for (int c = 0; c < ne; ++c) st.eta[(size_t)ne * i + c] = r.eta[(size_t)ne * row + c];
@@ -339,8 +344,8 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply(PmStore st, const 
   if (g >= r.n) return;
   const uint32_t key = keys[g];
   if (key == kNoKey || (g > 0 && keys[g - 1] == key)) return;
-  const int ne = 3 * st.nl;
-  double dL[9], dth[3], de[3 * 8], dw = 0.0, drs = 0.0, dcam = 0.0, dlid = 0.0, dacc[3] = {0.0, 0.0, 0.0}, dden = 0.0;
+  constexpr int ne = 3 * kNL;
+  double dL[9], dth[3], de[3 * kNL], dw = 0.0, drs = 0.0, dcam = 0.0, dlid = 0.0, dacc[3] = {0.0, 0.0, 0.0}, dden = 0.0;
   for (int c = 0; c < 9; ++c) dL[c] = 0.0;
   for (int c = 0; c < 3; ++c) dth[c] = 0.0;
   for (int c = 0; c < ne; ++c) de[c] = 0.0;
@@ -400,42 +405,46 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_rgb(PmStore st, const in
 // timestamps.at[unique(target_slots)].set(ts) in every listed tile (all rows' slots, :1112) and
 // the unique-slot flags for n_fused
 __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_ts(PmStore st, const int32_t* tiles, int n, PmRows r,
-                                                           double ts, uint8_t* mark) {
+                                                           double ts, uint32_t* mark) {
   const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
   if (g >= (long)n * r.n) return;
   const int t = (int)(g / r.n), row = (int)(g % r.n);
   const int q = r.slots[row];
   if (q < 0 || q >= st.M) return;
   st.ts[sidx(st, tiles[t], q)] = ts;
-  if (t == 0) mark[q] = 1;
+  if (t == 0) mark[q] = 1u;
 }
 
-__global__ __launch_bounds__(kPmRed) void k_pm_count_marks(const uint8_t* mark, int M, int32_t* out) {
-  __shared__ double lds[kPmRed / 64];
-  double c = 0.0;
-  for (int q = threadIdx.x; q < M; q += kPmRed) c += mark[q] ? 1.0 : 0.0;
-  c = block_sum_d<kPmRed>(c, lds);
-  if (threadIdx.x == 0) out[0] = (int32_t)c;
+// unique target slots: per-block counts of the marks, added with an integer atomic (exact in any order)
+__global__ __launch_bounds__(kPmThreads) void k_pm_count_marks(const uint32_t* mark, int M, uint32_t* n_unique) {
+  __shared__ double lds[kPmThreads / 64];
+  const int q = blockIdx.x * kPmThreads + threadIdx.x;
+  double c = q < M && mark[q] ? 1.0 : 0.0;
+  c = block_sum_d<kPmThreads>(c, lds);
+  if (threadIdx.x == 0 && c > 0.0) atomicAdd(n_unique, (uint32_t)c);
 }
 
-// one workgroup per listed tile: valid count
-__global__ __launch_bounds__(kPmRed) void k_pm_count(PmStore st, const int32_t* tiles, int32_t* out) {
+// grid (tiles, blocks per tile): block b of tile t covers slots b*kPmRed + j*gridDim.y*kPmRed
+__device__ __forceinline__ int part_row() { return blockIdx.x * gridDim.y + blockIdx.y; }
+
+// valid counts (partials: one per block)
+__global__ __launch_bounds__(kPmRed) void k_pm_count(PmStore st, const int32_t* tiles, double* part) {
   __shared__ double lds[kPmRed / 64];
   const int ti = tiles[blockIdx.x];
   double c = 0.0;
-  for (int q = threadIdx.x; q < st.M; q += kPmRed) c += st.valid[sidx(st, ti, q)] ? 1.0 : 0.0;
+  for (int q = blockIdx.y * kPmRed + threadIdx.x; q < st.M; q += gridDim.y * kPmRed)
+    c += st.valid[sidx(st, ti, q)] ? 1.0 : 0.0;
   c = block_sum_d<kPmRed>(c, lds);
-  if (threadIdx.x == 0) out[blockIdx.x] = (int32_t)c;
+  if (threadIdx.x == 0) part[part_row()] = c;
 }
 
 // cull (:1217-1250): below = valid & w < thr -> invalid; culled count, mass dropped, sum of all weights,
 // valid count after (one workgroup per tile, fixed-order sums)
-__global__ __launch_bounds__(kPmRed) void k_pm_cull(PmStore st, const int32_t* tiles, double thr, int32_t* n_out,
-                                                    double* mass, double* wsum, int32_t* cnt) {
+__global__ __launch_bounds__(kPmRed) void k_pm_cull(PmStore st, const int32_t* tiles, double thr, double* part) {
   __shared__ double lds[kPmRed / 64];
   const int ti = tiles[blockIdx.x];
   double nb = 0.0, md = 0.0, ws = 0.0, nv = 0.0;
-  for (int q = threadIdx.x; q < st.M; q += kPmRed) {
+  for (int q = blockIdx.y * kPmRed + threadIdx.x; q < st.M; q += gridDim.y * kPmRed) {
     const size_t i = sidx(st, ti, q);
     const double w = st.w[i];
     const bool v = st.valid[i] != 0;
@@ -451,10 +460,11 @@ __global__ __launch_bounds__(kPmRed) void k_pm_cull(PmStore st, const int32_t* t
   ws = block_sum_d<kPmRed>(ws, lds);
   nv = block_sum_d<kPmRed>(nv, lds);
   if (threadIdx.x == 0) {
-    n_out[blockIdx.x] = (int32_t)nb;
-    mass[blockIdx.x] = md;
-    wsum[blockIdx.x] = ws;
-    cnt[blockIdx.x] = (int32_t)nv;
+    double* o = part + 4 * part_row();
+    o[0] = nb;
+    o[1] = md;
+    o[2] = ws;
+    o[3] = nv;
   }
 }
 
@@ -473,7 +483,7 @@ __global__ __launch_bounds__(kPmRed) void k_pm_recency(PmStore st, const int32_t
   __shared__ double lds[kPmRed / 64];
   const int ti = tiles[blockIdx.x];
   double dn = 0.0, inf = 0.0, nv = 0.0;
-  for (int q = threadIdx.x; q < st.M; q += kPmRed) {
+  for (int q = blockIdx.y * kPmRed + threadIdx.x; q < st.M; q += gridDim.y * kPmRed) {
     const size_t i = sidx(st, ti, q);
     const bool v = st.valid[i] != 0;
     const long long dt = max(0ll, seq - st.lsup[i]);
@@ -490,9 +500,9 @@ __global__ __launch_bounds__(kPmRed) void k_pm_recency(PmStore st, const int32_t
   inf = block_sum_d<kPmRed>(inf, lds);
   nv = block_sum_d<kPmRed>(nv, lds);
   if (threadIdx.x == 0) {
-    out[3 * blockIdx.x] = dn;
-    out[3 * blockIdx.x + 1] = inf;
-    out[3 * blockIdx.x + 2] = nv;
+    out[3 * part_row()] = dn;
+    out[3 * part_row() + 1] = inf;
+    out[3 * part_row() + 2] = nv;
   }
 }
 
@@ -649,7 +659,7 @@ __global__ void k_pm_merge_apply(PmStore st, int ti, const int32_t* sel, const i
   lu3_inv(a, perm, Lm);
   for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = Lm[c];
   for (int r = 0; r < 3; ++r) st.th[3 * i + r] = (Lm[3 * r] * mm[0] + Lm[3 * r + 1] * mm[1]) + Lm[3 * r + 2] * mm[2];
-  const int ne = 3 * st.nl;
+  constexpr int ne = 3 * kNL;
   for (int c = 0; c < ne; ++c)
     st.eta[(size_t)ne * i + c] = (w1 * st.eta[(size_t)ne * i + c] + w2 * st.eta[(size_t)ne * j + c]) / ws;
   const double cam = st.cam[i] + st.cam[j];
@@ -692,7 +702,7 @@ struct PmWorld {
 };
 
 // Lambda_w = (R Lambda) R^T, mu_w = R (Lambda + eps I)^-1 theta + t, theta_w = Lambda_w mu_w, eta_w = R eta
-__device__ void world_row(const PmWorld& W, const double* L, const double* th, const double* eta, int nl, double* Lw,
+__device__ __forceinline__ void world_row(const PmWorld& W, const double* L, const double* th, const double* eta, int nl, double* Lw,
                           double* thw, double* ew, double* muw) {
 #pragma clang fp contract(off)
   double RL[9];
@@ -737,14 +747,14 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_rows(PmMeas m, PmWorld W
       break;
     }
   const double r = m.resp[(size_t)mi * m.k + k] * (vr ? 1.0 : 0.0);
-  double Lw[9], thw[3], ew[24], muw[3];
-  world_row(W, m.lam + 9 * (size_t)mi, m.th + 3 * (size_t)mi, m.eta + (size_t)3 * nl * mi, nl, Lw, thw, ew, muw);
+  double Lw[9], thw[3], ew[3 * kNL], muw[3];
+  world_row(W, m.lam + 9 * (size_t)mi, m.th + 3 * (size_t)mi, m.eta + (size_t)3 * kNL * mi, kNL, Lw, thw, ew, muw);
   for (int c = 0; c < 9; ++c) o.lam[9 * (size_t)g + c] = Lw[c];
   for (int c = 0; c < 3; ++c) {
     o.th[3 * (size_t)g + c] = thw[c];
     o.col[3 * (size_t)g + c] = m.col ? m.col[3 * (size_t)mi + c] : 0.0;
   }
-  for (int c = 0; c < 3 * nl; ++c) o.eta[(size_t)3 * nl * g + c] = ew[c];
+  for (int c = 0; c < 3 * kNL; ++c) o.eta[(size_t)3 * kNL * g + c] = ew[c];
   const double w = m.w[mi];
   o.w[g] = w;
   o.resp[g] = r;
@@ -759,11 +769,16 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_rows(PmMeas m, PmWorld W
 // Novelty proposals per active tile (pipeline.py:1331-1375): one 1024-thread workgroup per tile;
 // the stable argsort of -score_t is a rank count over (key, index); rows in (tile, rank) order.
 constexpr int kPropThreads = 1024;
+constexpr int kPropLds = 2048;     // measurement rows a map update handles (scores and ranks in LDS)
+constexpr int kPropMaxIns = 1024;  // k_insert_tile bound
 __global__ __launch_bounds__(kPropThreads) void k_pm_proposals(PmMeas m, PmWorld W, int nl, double eps_mass,
                                                                double h_tile, const int64_t* act_ids, int kins,
                                                                double* score_buf, int64_t* tile_buf, PmRowBuf o) {
 #pragma clang fp contract(off)
   __shared__ double lds[kPropThreads / 64];
+  __shared__ double s_sc[kPropLds];
+  __shared__ int s_in[kPropLds], s_pre[kPropLds], s_slot[kPropMaxIns];
+  __shared__ int s_wsum[kPropThreads / 64];
   __shared__ int s_any;
   const int t = blockIdx.x;
   const int64_t tid = act_ids[t];
@@ -786,18 +801,51 @@ __global__ __launch_bounds__(kPropThreads) void k_pm_proposals(PmMeas m, PmWorld
     const double nov = fmax(a - m.rmass[i], 0.0);
     const double score = nov * m.w[i] - (1.0 - vf) * 1e6;
     sc[i] = mt == tid ? score : -1e30;
+    s_sc[i] = sc[i];
   }
   __syncthreads();
-  // rank of each measurement under (-score_t ascending, index); ranks < kins are the proposals
-  int* slot_of = (int*)(score_buf + (size_t)gridDim.x * m.n) + (size_t)t * kins;
-  for (int i = threadIdx.x; i < m.n; i += kPropThreads) {
-    const double ki = -sc[i];
-    int rank = 0;
-    for (int j = 0; j < m.n; ++j) {
-      const double kj = -sc[j];
-      rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
-      if (rank >= kins) break;
+  const double* scr = s_sc;
+  // rank of each measurement under (-score_t ascending, index); ranks < kins are the proposals.  The
+  // tile's measurements (score_t > -1e29) are compacted in index order and ranked among themselves;
+  // every other row has the key 1e30, above all of them, so its rank is c + (its index among them).
+  int* slot_of = s_slot;
+  int run = 0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int c0 = 0; c0 < m.n; c0 += kPropThreads) {
+    const int i = c0 + threadIdx.x;
+    const int f = i < m.n && scr[i] > -1e29 ? 1 : 0;
+    int x = f;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
     }
+    __syncthreads();
+    if (lane == 63) s_wsum[wid] = x;
+    __syncthreads();
+    int pre = run + x - f;
+    for (int w = 0; w < wid; ++w) pre += s_wsum[w];
+    int tot = 0;
+    for (int w = 0; w < kPropThreads / 64; ++w) tot += s_wsum[w];
+    if (f) s_in[pre] = i;
+    s_pre[i < m.n ? i : 0] = i < m.n ? pre : 0;  // in-tile rows before i
+    run += tot;
+  }
+  __syncthreads();
+  const int c = run;
+  for (int a = threadIdx.x; a < c; a += kPropThreads) {
+    const int i = s_in[a];
+    const double ki = -scr[i];
+    int rank = 0;
+    for (int b = 0; b < c && rank < kins; ++b) {
+      const int j = s_in[b];
+      const double kj = -scr[j];
+      rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+    }
+    if (rank < kins) slot_of[rank] = i;
+  }
+  for (int i = threadIdx.x; i < m.n; i += kPropThreads) {
+    if (scr[i] > -1e29) continue;
+    const int rank = c + (i - s_pre[i]);
     if (rank < kins) slot_of[rank] = i;
   }
   if (threadIdx.x == 0) s_any = 0;
@@ -812,14 +860,14 @@ __global__ __launch_bounds__(kPropThreads) void k_pm_proposals(PmMeas m, PmWorld
     const int i = q < m.n ? slot_of[q] : 0;
     const bool in_tile = q < m.n && sc[i] > -1e29;  // score_t == -1e30 exactly where out of tile
     const bool vn = s_any ? (in_tile && sc[i] > -1e20) : true;
-    double Lw[9], thw[3], ew[24], muw[3];
-    world_row(W, m.lam + 9 * (size_t)i, m.th + 3 * (size_t)i, m.eta + (size_t)3 * nl * i, nl, Lw, thw, ew, muw);
+    double Lw[9], thw[3], ew[3 * kNL], muw[3];
+    world_row(W, m.lam + 9 * (size_t)i, m.th + 3 * (size_t)i, m.eta + (size_t)3 * kNL * i, kNL, Lw, thw, ew, muw);
     for (int c = 0; c < 9; ++c) o.lam[9 * g + c] = Lw[c];
     for (int c = 0; c < 3; ++c) {
       o.th[3 * g + c] = thw[c];
       o.col[3 * g + c] = m.col ? m.col[3 * (size_t)i + c] : 0.0;
     }
-    for (int c = 0; c < 3 * nl; ++c) o.eta[(size_t)3 * nl * g + c] = ew[c];
+    for (int c = 0; c < 3 * kNL; ++c) o.eta[(size_t)3 * kNL * g + c] = ew[c];
     const double vf = m.valid[i] ? 1.0 : 0.0;
     const double nov = fmax(vf / asum - m.rmass[i], 0.0);
     o.w[g] = in_tile ? nov * m.w[i] : 0.0;
@@ -841,7 +889,8 @@ struct gcs_pmap {
   // sort scratch (view / insert: T tiles x M slots)
   uint64_t *keys = nullptr, *keys_s = nullptr;
   uint32_t *vals = nullptr, *vals_s = nullptr;
-  int32_t *offs = nullptr, *d_tiles = nullptr;
+  uint32_t* seg = nullptr;  // tile positions of the key-sorted entries
+  int32_t* d_tiles = nullptr;
   int64_t* d_tids = nullptr;
   void* temp = nullptr;
   size_t temp_bytes = 0;
@@ -850,7 +899,8 @@ struct gcs_pmap {
   void* ftemp = nullptr;
   size_t ftemp_bytes = 0;
   int frows = 0;
-  uint8_t* mark = nullptr;
+  uint32_t* mark = nullptr;  // fuse: slots seen (n_fused)
+  uint32_t* dcnt = nullptr;  // fuse: unique-slot counter (device memory: atomics stay off the mapped buffer)
   // step-12b scratch (grown on demand)
   void* ub = nullptr;
   size_t ub_bytes = 0;
@@ -866,7 +916,10 @@ struct gcs_pmap {
 };
 
 namespace {
-constexpr size_t kSmall = 1 << 16;
+constexpr size_t kSmall = 1 << 20;
+constexpr size_t kPartOff = 1 << 16;  // per-(tile, block) reduction partials in the mapped buffer
+constexpr int kMaxBlocksPerTile = 64;
+int blocks_per_tile(int M) { return std::max(1, std::min(kMaxBlocksPerTile, (M + kPmRed - 1) / kPmRed)); }
 const int kFieldWidth[GCS_PM_NFIELDS] = {9, 3, -1, 1, 1, 1, 3, 1, 1, 3, 1, 3, 1, 1, 1, 1};
 const int kFieldBytes[GCS_PM_NFIELDS] = {8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 1};
 
@@ -903,15 +956,43 @@ int upload_tiles(gcs_pmap* p, const int32_t* tiles, int n) {
   return GCS_OK;
 }
 
-// stable per-tile sort of the slot keys (mode 0 view, 1 eviction); result in vals_s
+// stable per-tile sort of the slot keys (mode 0 view, 1 eviction): one radix sort of every listed
+// tile's (key, tile position x M + slot), then a stable radix sort on the tile position -- per tile the
+// key order with ties by slot (LSD composition).  Result (tile position x M + slot) in vals.
 int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam) {
   const long total = (long)n * p->M;
-  hipLaunchKernelGGL(k_pm_keys, dim3((unsigned)((std::max(total, (long)n + 1) + kPmThreads - 1) / kPmThreads)),
-                     dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, mode, seq, lam, p->keys,
-                     p->vals, p->offs);
+  const unsigned gb = (unsigned)((total + kPmThreads - 1) / kPmThreads);
+  hipLaunchKernelGGL(k_pm_keys, dim3(gb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, mode,
+                     seq, lam, p->keys, p->vals);
   size_t tb = p->temp_bytes;
-  PMCHK(p, rocprim::segmented_radix_sort_pairs(p->temp, tb, p->keys, p->keys_s, p->vals, p->vals_s, (unsigned)total,
-                                               (unsigned)n, p->offs, p->offs + 1, 0u, 64u, p->stream));
+  PMCHK(p, rocprim::radix_sort_pairs(p->temp, tb, p->keys, p->keys_s, p->vals, p->vals_s, (unsigned)total, 0u, 64u,
+                                     p->stream));
+  if (n > 1) {
+    unsigned bits = 1;
+    while ((1u << bits) < (unsigned)n) ++bits;
+    hipLaunchKernelGGL(k_pm_segkeys, dim3(gb), dim3(kPmThreads), 0, p->stream, (const uint32_t*)p->vals_s, total, p->M,
+                       (uint32_t*)p->keys);
+    tb = p->temp_bytes;
+    PMCHK(p, rocprim::radix_sort_pairs(p->temp, tb, (uint32_t*)p->keys, p->seg, p->vals_s, p->vals, (unsigned)total, 0u,
+                                       bits, p->stream));
+  } else {
+    PMCHK(p, hipMemcpyAsync(p->vals, p->vals_s, total * 4, hipMemcpyDeviceToDevice, p->stream));
+  }
+  return GCS_OK;
+}
+
+// valid counts of the n listed tiles (host, after a sync)
+int count_tiles(gcs_pmap* p, const int32_t* d_tiles, int n, int32_t* count) {
+  const int nbt = blocks_per_tile(p->M);
+  hipLaunchKernelGGL(k_pm_count, dim3(n, nbt), dim3(kPmRed), 0, p->stream, p->st, d_tiles, (double*)(p->d_small + kPartOff));
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  const double* h = (const double*)(p->h_small + kPartOff);
+  for (int t = 0; t < n; ++t) {
+    double c = 0.0;
+    for (int b = 0; b < nbt; ++b) c += h[t * nbt + b];
+    count[t] = (int32_t)c;
+  }
   return GCS_OK;
 }
 
@@ -936,8 +1017,9 @@ extern "C" {
 
 int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t max_merge, int32_t device,
                     gcs_pmap** out) {
-  if (!out || m_tile < 1 || max_tiles < 1 || n_lobes < 1 || n_lobes > 8 || max_merge < 0) return GCS_ERR_ARG;
+  if (!out || m_tile < 1 || max_tiles < 1 || n_lobes != kNL || max_merge < 0) return GCS_ERR_ARG;
   if ((long)m_tile * max_tiles >= (1L << 31)) return GCS_ERR_ARG;
+  if ((size_t)max_tiles * kMaxBlocksPerTile * 4 * sizeof(double) > kSmall - kPartOff) return GCS_ERR_ARG;
   gcs_pmap* p = new gcs_pmap();
   p->device = device;
   p->M = m_tile;
@@ -974,18 +1056,20 @@ int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t 
   s.nl = n_lobes;
   const size_t tot = (size_t)m_tile * max_tiles;
   if (bad(hipMalloc(&p->keys, tot * 8)) || bad(hipMalloc(&p->keys_s, tot * 8)) || bad(hipMalloc(&p->vals, tot * 4)) ||
-      bad(hipMalloc(&p->vals_s, tot * 4)) || bad(hipMalloc(&p->offs, (max_tiles + 1) * 4)) ||
+      bad(hipMalloc(&p->vals_s, tot * 4)) || bad(hipMalloc(&p->seg, tot * 4)) ||
       bad(hipMalloc(&p->d_tiles, max_tiles * 4)) || bad(hipMalloc(&p->d_tids, max_tiles * 8)) ||
-      bad(hipMalloc(&p->mark, m_tile)) ||
+      bad(hipMalloc(&p->mark, (size_t)m_tile * 4)) || bad(hipMalloc(&p->dcnt, 4)) ||
       bad(hipHostMalloc((void**)&p->h_small, kSmall, hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&p->d_small, p->h_small, 0)))
     return fail();
-  size_t tb = 0;
-  if (bad(rocprim::segmented_radix_sort_pairs(nullptr, tb, p->keys, p->keys_s, p->vals, p->vals_s, (unsigned)tot,
-                                              (unsigned)max_tiles, p->offs, p->offs + 1, 0u, 64u, p->stream)) ||
-      bad(hipMalloc(&p->temp, std::max<size_t>(tb, 16))))
+  size_t tb = 0, tb2 = 0;
+  if (bad(rocprim::radix_sort_pairs(nullptr, tb, p->keys, p->keys_s, p->vals, p->vals_s, (unsigned)tot, 0u, 64u,
+                                    p->stream)) ||
+      bad(rocprim::radix_sort_pairs(nullptr, tb2, (uint32_t*)p->keys, p->seg, p->vals_s, p->vals, (unsigned)tot, 0u,
+                                    16u, p->stream)) ||
+      bad(hipMalloc(&p->temp, std::max<size_t>(std::max(tb, tb2), 16))))
     return fail();
-  p->temp_bytes = std::max<size_t>(tb, 16);
+  p->temp_bytes = std::max<size_t>(std::max(tb, tb2), 16);
   if (p->max_merge >= 2) {
     const long P = (long)p->max_merge * (p->max_merge - 1) / 2;
     if (bad(hipMalloc(&p->mmu, (size_t)p->max_merge * 3 * 8)) || bad(hipMalloc(&p->msig, (size_t)p->max_merge * 9 * 8)) ||
@@ -1008,8 +1092,8 @@ int gcs_pmap_destroy(gcs_pmap* p) {
   if (p->stream) (void)hipStreamSynchronize(p->stream);
   for (void* f : p->fields)
     if (f) (void)hipFree(f);
-  void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->offs, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
-                  p->fv, p->fv_s, p->ftemp, p->mark, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
+  void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->seg, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
+                  p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
                   p->msel, p->mnsel, p->ub};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -1075,7 +1159,7 @@ int gcs_pmap_extract_view(gcs_pmap* p, const int32_t* tiles, const int64_t* tile
               o->candidate_slots};
   hipLaunchKernelGGL(k_pm_view, dim3((n * m_view + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream,
                      p->st, (const int32_t*)p->d_tiles, (const int64_t*)p->d_tids, n, m_view,
-                     (const uint32_t*)p->vals_s, eps_lift, eps_mass, v);
+                     (const uint32_t*)p->vals, eps_lift, eps_mass, v);
   PMCHK(p, hipGetLastError());
   PMCHK(p, hipStreamSynchronize(p->stream));
   return GCS_OK;
@@ -1094,25 +1178,34 @@ int gcs_pmap_insert_masked(gcs_pmap* p, const int32_t* tiles, int32_t n, int32_t
   PMCHK(p, hipSetDevice(p->device));
   if (int rc = upload_tiles(p, tiles, n)) return rc;
   int32_t* d_ins = (int32_t*)p->d_small;
-  int32_t* d_cnt = (int32_t*)(p->d_small + 4096);
   if (K > 0) {
     if (int rc = sort_tiles(p, n, 1, scan_seq, lam)) return rc;
     hipLaunchKernelGGL(k_pm_insert, dim3(1), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, K,
-                       (const uint32_t*)p->vals_s, rows_of(rows), timestamp, (long long)scan_seq,
+                       (const uint32_t*)p->vals, rows_of(rows), timestamp, (long long)scan_seq,
                        (long long)next_global_id, new_ids, d_ins);
   } else {
     PMCHK(p, hipMemsetAsync(d_ins, 0, n * sizeof(int32_t), p->stream));
   }
-  hipLaunchKernelGGL(k_pm_count, dim3(n), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles, d_cnt);
-  PMCHK(p, hipGetLastError());
-  PMCHK(p, hipStreamSynchronize(p->stream));
+  if (int rc = count_tiles(p, (const int32_t*)p->d_tiles, n, count)) return rc;
   memcpy(n_inserted, p->h_small, n * sizeof(int32_t));
-  memcpy(count, p->h_small + 4096, n * sizeof(int32_t));
   return GCS_OK;
 }
 
+namespace {
+int fuse_impl(gcs_pmap* p, const int32_t* tiles, int32_t n, const gcs_pmap_rows* rows, double timestamp,
+              int64_t scan_seq, double eps_mass, int32_t* n_fused, bool rebuild_rgb);
+}
 int gcs_pmap_fuse(gcs_pmap* p, const int32_t* tiles, int32_t n, const gcs_pmap_rows* rows, double timestamp,
                   int64_t scan_seq, double eps_mass, int32_t* n_fused) {
+  return fuse_impl(p, tiles, n, rows, timestamp, scan_seq, eps_mass, n_fused, true);
+}
+}  // extern "C"
+
+namespace {
+// rebuild_rgb = false: a later call on the same tiles rebuilds it (rgb is a function of the slot's
+// accumulators alone, so only the last rebuild of a sequence is observable)
+int fuse_impl(gcs_pmap* p, const int32_t* tiles, int32_t n, const gcs_pmap_rows* rows, double timestamp,
+              int64_t scan_seq, double eps_mass, int32_t* n_fused, bool rebuild_rgb) {
   if (!p || !rows || !n_fused) return GCS_ERR_ARG;
   if (int rc = check_tiles(p, tiles, n, false)) return rc;
   const int R = rows->n;
@@ -1141,8 +1234,9 @@ int gcs_pmap_fuse(gcs_pmap* p, const int32_t* tiles, int32_t n, const gcs_pmap_r
   }
   if (int rc = upload_tiles(p, tiles, n)) return rc;
   uint32_t* d_err = (uint32_t*)(p->d_small + 8192);
-  int32_t* d_nf = (int32_t*)(p->d_small + 8200);
+  uint32_t* d_nf = p->dcnt;
   *(uint32_t*)(p->h_small + 8192) = 0u;
+  PMCHK(p, hipMemsetAsync(p->dcnt, 0, 4, p->stream));
   const PmRows r = rows_of(rows);
   const int rb = (R + kPmThreads - 1) / kPmThreads;
   hipLaunchKernelGGL(k_pm_fuse_keys, dim3(rb), dim3(kPmThreads), 0, p->stream, r, n, p->M, p->fk, p->fv, d_err);
@@ -1151,19 +1245,25 @@ int gcs_pmap_fuse(gcs_pmap* p, const int32_t* tiles, int32_t n, const gcs_pmap_r
   hipLaunchKernelGGL(k_pm_fuse_apply, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, r,
                      (const uint32_t*)p->fk_s, (const uint32_t*)p->fv_s, (long long)scan_seq);
   const long tm = (long)n * p->M;
-  hipLaunchKernelGGL(k_pm_fuse_rgb, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
-                     p->stream, p->st, (const int32_t*)p->d_tiles, n, eps_mass);
-  PMCHK(p, hipMemsetAsync(p->mark, 0, p->M, p->stream));
+  if (rebuild_rgb)
+    hipLaunchKernelGGL(k_pm_fuse_rgb, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
+                       p->stream, p->st, (const int32_t*)p->d_tiles, n, eps_mass);
+  PMCHK(p, hipMemsetAsync(p->mark, 0, (size_t)p->M * 4, p->stream));
   const long tr = (long)n * R;
   hipLaunchKernelGGL(k_pm_fuse_ts, dim3((unsigned)((tr + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
                      p->stream, p->st, (const int32_t*)p->d_tiles, n, r, timestamp, p->mark);
-  hipLaunchKernelGGL(k_pm_count_marks, dim3(1), dim3(kPmRed), 0, p->stream, (const uint8_t*)p->mark, p->M, d_nf);
+  hipLaunchKernelGGL(k_pm_count_marks, dim3((p->M + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream,
+                     (const uint32_t*)p->mark, p->M, d_nf);
+  PMCHK(p, hipMemcpyAsync(p->h_small + 8200, p->dcnt, 4, hipMemcpyDeviceToHost, p->stream));
   PMCHK(p, hipGetLastError());
   PMCHK(p, hipStreamSynchronize(p->stream));
   if (*(uint32_t*)(p->h_small + 8192)) return pm_fail(p, GCS_ERR_ARG, "target slot out of range (rows skipped)");
-  *n_fused = *(int32_t*)(p->h_small + 8200);
+  *n_fused = (int32_t)*(uint32_t*)(p->h_small + 8200);
   return GCS_OK;
 }
+}  // namespace
+
+extern "C" {
 
 int gcs_pmap_cull(gcs_pmap* p, const int32_t* tiles, int32_t n, double thr, int32_t* n_culled, double* mass_dropped,
                   double* weight_sum, int32_t* count) {
@@ -1172,16 +1272,21 @@ int gcs_pmap_cull(gcs_pmap* p, const int32_t* tiles, int32_t n, double thr, int3
   if (n == 0) return GCS_OK;
   PMCHK(p, hipSetDevice(p->device));
   if (int rc = upload_tiles(p, tiles, n)) return rc;
-  char* d = p->d_small + 16384;
-  hipLaunchKernelGGL(k_pm_cull, dim3(n), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles, thr,
-                     (int32_t*)d, (double*)(d + 4096), (double*)(d + 8192), (int32_t*)(d + 12288));
+  const int nbt = blocks_per_tile(p->M);
+  hipLaunchKernelGGL(k_pm_cull, dim3(n, nbt), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles, thr,
+                     (double*)(p->d_small + kPartOff));
   PMCHK(p, hipGetLastError());
   PMCHK(p, hipStreamSynchronize(p->stream));
-  const char* h = p->h_small + 16384;
-  memcpy(n_culled, h, n * 4);
-  memcpy(mass_dropped, h + 4096, n * 8);
-  memcpy(weight_sum, h + 8192, n * 8);
-  memcpy(count, h + 12288, n * 4);
+  const double* h = (const double*)(p->h_small + kPartOff);
+  for (int t = 0; t < n; ++t) {  // block partials folded in block order
+    double a[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int b = 0; b < nbt; ++b)
+      for (int k = 0; k < 4; ++k) a[k] += h[4 * (t * nbt + b) + k];
+    n_culled[t] = (int32_t)a[0];
+    mass_dropped[t] = a[1];
+    weight_sum[t] = a[2];
+    count[t] = (int32_t)a[3];
+  }
   return GCS_OK;
 }
 
@@ -1207,14 +1312,18 @@ int gcs_pmap_recency_inflate(gcs_pmap* p, const int32_t* tiles, int32_t n, int64
   if (n == 0) return GCS_OK;
   PMCHK(p, hipSetDevice(p->device));
   if (int rc = upload_tiles(p, tiles, n)) return rc;
-  double* d = (double*)(p->d_small + 32768);
-  hipLaunchKernelGGL(k_pm_recency, dim3(n), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
-                     (long long)scan_seq, lam, min_scale, d);
+  const int nbt = blocks_per_tile(p->M);
+  hipLaunchKernelGGL(k_pm_recency, dim3(n, nbt), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
+                     (long long)scan_seq, lam, min_scale, (double*)(p->d_small + kPartOff));
   PMCHK(p, hipGetLastError());
   PMCHK(p, hipStreamSynchronize(p->stream));
-  const double* h = (const double*)(p->h_small + 32768);
-  for (int t = 0; t < n; ++t)  // the reference's Python float sums, tile by tile
-    for (int k = 0; k < 3; ++k) stats[k] += h[3 * t + k];
+  const double* h = (const double*)(p->h_small + kPartOff);
+  for (int t = 0; t < n; ++t) {  // per tile (block partials in order), then the reference's sums over tiles
+    double a[3] = {0.0, 0.0, 0.0};
+    for (int b = 0; b < nbt; ++b)
+      for (int k = 0; k < 3; ++k) a[k] += h[3 * (t * nbt + b) + k];
+    for (int k = 0; k < 3; ++k) stats[k] += a[k];
+  }
   return GCS_OK;
 }
 
@@ -1250,12 +1359,7 @@ int gcs_pmap_merge_reduce(gcs_pmap* p, int32_t tile, double thr, int32_t max_pai
     PMCHK(p, hipMemcpyAsync(n_merged, p->mnsel, 4, hipMemcpyDeviceToHost, p->stream));
     PMCHK(p, hipMemcpyAsync(pairs, p->msel, 2 * max_pairs * 4, hipMemcpyDeviceToHost, p->stream));
   }
-  hipLaunchKernelGGL(k_pm_count, dim3(1), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
-                     (int32_t*)(p->d_small + 40960));
-  PMCHK(p, hipGetLastError());
-  PMCHK(p, hipStreamSynchronize(p->stream));
-  *count = *(int32_t*)(p->h_small + 40960);
-  return GCS_OK;
+  return count_tiles(p, (const int32_t*)p->d_tiles, 1, count);
 }
 
 int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_ids, int32_t n, const double* z_t6,
@@ -1267,8 +1371,9 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   if (in->n_total < 1 || in->k_assoc < 1 || !in->Lambdas || !in->thetas || !in->etas || !in->weights || !in->valid ||
       !in->responsibilities || !in->candidate_tile_ids || !in->candidate_slots || !in->row_masses)
     return pm_fail(p, GCS_ERR_ARG, "map update: missing measurement or association array");
-  if (cfg->block_size < 1 || cfg->k_insert_tile < 0 || in->n_lobes != p->nl)
-    return pm_fail(p, GCS_ERR_ARG, "map update: bad block size, insert budget or lobe count");
+  if (cfg->block_size < 1 || cfg->k_insert_tile < 0 || cfg->k_insert_tile > kPropMaxIns || in->n_lobes != p->nl)
+    return pm_fail(p, GCS_ERR_ARG, "map update: bad block size, insert budget (<= 1024) or lobe count");
+  if (in->n_total > kPropLds) return pm_fail(p, GCS_ERR_ARG, "map update: more than 2048 measurement rows");
   memset(st, 0, sizeof(*st));
   if (n == 0) return GCS_OK;
   PMCHK(p, hipSetDevice(p->device));
@@ -1338,7 +1443,7 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
     rb.slots = o.slots + r0;
     rb.n = B * K;
     int32_t nf = 0;
-    if (int rc = gcs_pmap_fuse(p, tiles, n, &rb, timestamp, scan_seq, cfg->eps_mass, &nf)) return rc;
+    if (int rc = fuse_impl(p, tiles, n, &rb, timestamp, scan_seq, cfg->eps_mass, &nf, b == nb - 1)) return rc;
     st->fused_count += n * nf;
     for (int t = 0; t < n; ++t) {  // fused_mass_total: per (block, tile) sums (pipeline.py:1306-1308)
       double sm = 0.0;
