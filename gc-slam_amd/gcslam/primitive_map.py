@@ -499,6 +499,26 @@ def primitive_map_merge_reduce(atlas_map: AtlasMap, tile_id: int,
             ExpectedEffect("primitive_map_merge_reduce", float(max_pairs), float(n)))
 
 
+def ma_hex_stencil_tile_ids(center_xyz, h_tile: float, radius_xy: int, radius_z: int) -> List[int]:
+    """tiling.py:167-209: the packed MA-hex tile ids of the hex disk (radius_xy, sorted axial order) x
+    z slab (radius_z, outer) around the cell of center_xyz -- the active / stencil tiles of a scan."""
+    x, y, z = (float(v) for v in np.asarray(center_xyz, dtype=np.float64).ravel()[:3])
+    h = max(float(h_tile), 1e-12)
+    c1 = int(np.floor(x / h))
+    c2 = int(np.floor((x * 0.5 + y * (np.sqrt(3.0) * 0.5)) / h))
+    cz = int(np.floor(z / h))
+    r = int(radius_xy)
+    disk = sorted((q, rr) for q in range(-r, r + 1) for rr in range(max(-r, -q - r), min(r, -q + r) + 1))
+    bits, bias = 21, 1 << 20
+    mask = (1 << bits) - 1
+
+    def pack(a, b, c):
+        return (((a + bias) & mask) << (2 * bits)) | (((b + bias) & mask) << bits) | ((c + bias) & mask)
+
+    return [int(pack(c1 + dq, c2 + dr, cz + dz)) for dz in range(-int(radius_z), int(radius_z) + 1)
+            for dq, dr in disk]
+
+
 @dataclass
 class PrimitiveMapUpdateConfig:
     """The PipelineConfig fields step 12b reads (pipeline.py:187-206)."""

@@ -399,3 +399,16 @@ def map_update_step(tiles, next_global_id, batch, assoc, R, t, active_tile_ids, 
         st["merged_count"] += merge_reduce(tiles[int(tid)], merge_threshold, k_merge_pairs, merge_max_tile_size,
                                            eps_psd, eps_lift)[0]
     return next_global_id, st
+
+
+def ma_hex_stencil_tile_ids(center_xyz, h_tile, radius_xy, radius_z):
+    """tiling.py:167-209: packed tile ids of the hex disk (sorted axial (q, r)) x z slab around the
+    centre's MA-hex cell, z outer."""
+    x, y, z = (float(v) for v in np.asarray(center_xyz, np.float64).ravel()[:3])
+    h = max(float(h_tile), 1e-12)
+    c1, c2, cz = int(np.floor(x / h)), int(np.floor((x * 0.5 + y * (np.sqrt(3.0) * 0.5)) / h)), int(np.floor(z / h))
+    r = int(radius_xy)
+    disk = sorted((q, rr) for q in range(-r, r + 1) for rr in range(max(-r, -q - r), min(r, -q + r) + 1))
+    pack = lambda a, b, c: (((a + BIAS) & MASK) << (2 * BITS_PER_AXIS)) | (((b + BIAS) & MASK) << BITS_PER_AXIS) | (  # noqa: E731
+        (c + BIAS) & MASK)
+    return [int(pack(c1 + dq, c2 + dr, cz + dz)) for dz in range(-int(radius_z), int(radius_z) + 1) for dq, dr in disk]
