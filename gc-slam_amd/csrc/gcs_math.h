@@ -249,13 +249,24 @@ GCS_HD void cross3(const double* a, const double* b, double* c) {
 //   * the two small eigenpairs from the 2x2 projection of s onto the complement of that vector
 //     (closed form, absolute accuracy ~ 1e-16 |s|, far below eps = 1e-12).
 // Returns false (caller falls back to Jacobi) when the top eigenvalue is (near) double.
+#ifndef GCS_DEFLATE_FROB
+#define GCS_DEFLATE_FROB 1  // Newton's start (above); 0: the Gershgorin bound alone
+#endif
 GCS_HD __attribute__((always_inline)) bool psd3_deflate(const double* s, double* out, double* delta) {
   const double c2 = s[0] + s[4] + s[8];
   const double c1 = (s[0] * s[4] - s[1] * s[1]) + (s[0] * s[8] - s[2] * s[2]) + (s[4] * s[8] - s[5] * s[5]);
   const double c0 = s[0] * (s[4] * s[8] - s[5] * s[5]) - s[1] * (s[1] * s[8] - s[5] * s[2]) +
                     s[2] * (s[1] * s[5] - s[4] * s[2]);
-  double lam = fmax(fmax(s[0] + fabs(s[1]) + fabs(s[2]), s[4] + fabs(s[1]) + fabs(s[5])),
-                    s[8] + fabs(s[2]) + fabs(s[5]));
+  // start: the smaller of the Gershgorin bound and the Frobenius norm (|lambda| <= ||s||_F for a
+  // symmetric s; exact for rank 1, within sqrt 2 for rank 2 -- the scatters of one to three points
+  // that come here), so Newton starts at or above the top root and converges in a few steps
+#if GCS_DEFLATE_FROB
+  const double fro = sqrt((s[0] * s[0] + s[4] * s[4] + s[8] * s[8]) + 2.0 * ((s[1] * s[1] + s[2] * s[2]) + s[5] * s[5]));
+#else
+  const double fro = 1e308;
+#endif
+  double lam = fmin(fmax(fmax(s[0] + fabs(s[1]) + fabs(s[2]), s[4] + fabs(s[1]) + fabs(s[5])),
+                         s[8] + fabs(s[2]) + fabs(s[5])), fro);
   if (!(lam > -1e300 && lam < 1e300)) return false;  // NaN / inf
   for (int it = 0; it < 100; ++it) {
     const double f = ((lam - c2) * lam + c1) * lam - c0;

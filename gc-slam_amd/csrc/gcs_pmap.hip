@@ -415,6 +415,90 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_ts(PmStore st, const int
   if (t == 0) mark[q] = 1u;
 }
 
+// Step 12b's per-block fuse calls in one pass: key = ((tile position x M + slot) x nb + block) for
+// the contributing rows, so a (tile, slot) group's rows sort by block and, within a block, by row.
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmRows r, int n_tiles, int M, int nb, int rpb,
+                                                                    uint32_t* keys, uint32_t* vals, uint8_t* mark,
+                                                                    uint32_t* err) {
+  const int g = blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= r.n) return;
+  const int tp = r.tpos[g], q = r.slots[g], b = g / rpb;
+  const bool ok = q >= 0 && q < M;
+  if (!ok) err[0] = 1u;
+  else mark[(size_t)b * M + q] = 1;  // every row's slot counts for n_fused (np.unique(target_slots))
+  const bool v = (r.valid ? r.valid[g] != 0 : true) && tp >= 0 && tp < n_tiles && ok;
+  keys[g] = v ? ((uint32_t)tp * (uint32_t)M + (uint32_t)q) * (uint32_t)nb + (uint32_t)b : kNoKey;
+  vals[g] = (uint32_t)g;
+}
+
+// one lane per (tile, slot) group: for each block in order, d = the block's rows summed in row order,
+// then slot += d -- the reference's block-by-block fuse calls (pipeline.py:1272-1327)
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st, const int32_t* tiles, PmRows r,
+                                                                     const uint32_t* keys, const uint32_t* vals,
+                                                                     int nb, long long seq) {
+#pragma clang fp contract(off)
+  const int g = blockIdx.x * kPmThreads + threadIdx.x;
+  if (g >= r.n) return;
+  const uint32_t key = keys[g];
+  if (key == kNoKey) return;
+  const uint32_t grp = key / (uint32_t)nb;
+  if (g > 0 && keys[g - 1] != kNoKey && keys[g - 1] / (uint32_t)nb == grp) return;
+  constexpr int ne = 3 * kNL;
+  const int t = (int)(grp / (uint32_t)st.M), q = (int)(grp % (uint32_t)st.M);
+  const size_t i = sidx(st, tiles[t], q);
+  int pos = g;
+  while (pos < r.n && keys[pos] != kNoKey && keys[pos] / (uint32_t)nb == grp) {
+    const uint32_t kb = keys[pos];
+    double dL[9], dth[3], de[ne], dw = 0.0, drs = 0.0, dcam = 0.0, dlid = 0.0, dacc[3] = {0.0, 0.0, 0.0}, dden = 0.0;
+    for (int c = 0; c < 9; ++c) dL[c] = 0.0;
+    for (int c = 0; c < 3; ++c) dth[c] = 0.0;
+    for (int c = 0; c < ne; ++c) de[c] = 0.0;
+    for (; pos < r.n && keys[pos] == kb; ++pos) {
+      const size_t row = vals[pos];
+      const double rr = r.resp[row] * 1.0;
+      for (int c = 0; c < 9; ++c) dL[c] = dL[c] + rr * r.lam[9 * row + c];
+      for (int c = 0; c < 3; ++c) dth[c] = dth[c] + rr * r.th[3 * row + c];
+      for (int c = 0; c < ne; ++c) de[c] = de[c] + rr * r.eta[(size_t)ne * row + c];
+      const double rw = rr * r.w[row];
+      dw = dw + rw;
+      drs = drs + rr;
+      if (r.src) {
+        const int sv = r.src[row];
+        const double wc = rw * (sv == 0 ? 1.0 : 0.0);
+        dcam = dcam + wc;
+        dlid = dlid + rw * (sv == 1 ? 1.0 : 0.0);
+        if (r.col) {
+          for (int c = 0; c < 3; ++c) dacc[c] = dacc[c] + clip01(r.col[3 * row + c]) * wc;
+          dden = dden + wc;
+        }
+      }
+    }
+    for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = st.lam[9 * i + c] + dL[c];
+    for (int c = 0; c < 3; ++c) {
+      st.th[3 * i + c] = st.th[3 * i + c] + dth[c];
+      st.acc[3 * i + c] = st.acc[3 * i + c] + dacc[c];
+    }
+    for (int c = 0; c < ne; ++c) st.eta[(size_t)ne * i + c] = st.eta[(size_t)ne * i + c] + de[c];
+    st.w[i] = st.w[i] + dw;
+    st.cam[i] = st.cam[i] + dcam;
+    st.lid[i] = st.lid[i] + dlid;
+    st.den[i] = st.den[i] + dden;
+    if (drs > 0.0) {
+      st.lsup[i] = seq;
+      st.lupd[i] = seq;
+    }
+  }
+}
+
+// unique slots per block (grid: blocks of slots x nb): integer atomics into device counters
+__global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(const uint8_t* mark, int M, uint32_t* cnt) {
+  __shared__ double lds[kPmThreads / 64];
+  const int q = blockIdx.x * kPmThreads + threadIdx.x, b = blockIdx.y;
+  double c = q < M && mark[(size_t)b * M + q] ? 1.0 : 0.0;
+  c = block_sum_d<kPmThreads>(c, lds);
+  if (threadIdx.x == 0 && c > 0.0) atomicAdd(cnt + b, (uint32_t)c);
+}
+
 // unique target slots: per-block counts of the marks, added with an integer atomic (exact in any order)
 __global__ __launch_bounds__(kPmThreads) void k_pm_count_marks(const uint32_t* mark, int M, uint32_t* n_unique) {
   __shared__ double lds[kPmThreads / 64];
@@ -901,6 +985,9 @@ struct gcs_pmap {
   int frows = 0;
   uint32_t* mark = nullptr;  // fuse: slots seen (n_fused)
   uint32_t* dcnt = nullptr;  // fuse: unique-slot counter (device memory: atomics stay off the mapped buffer)
+  uint8_t* bmark = nullptr;   // step 12b: slots seen per association block (grown)
+  size_t bmark_bytes = 0;
+  uint32_t* bcnt = nullptr;   // step 12b: unique slots per block (kMaxFuseBlocks)
   // step-12b scratch (grown on demand)
   void* ub = nullptr;
   size_t ub_bytes = 0;
@@ -919,6 +1006,7 @@ namespace {
 constexpr size_t kSmall = 1 << 20;
 constexpr size_t kPartOff = 1 << 16;  // per-(tile, block) reduction partials in the mapped buffer
 constexpr int kMaxBlocksPerTile = 64;
+constexpr int kMaxFuseBlocks = 256;  // association blocks of one map update
 int blocks_per_tile(int M) { return std::max(1, std::min(kMaxBlocksPerTile, (M + kPmRed - 1) / kPmRed)); }
 const int kFieldWidth[GCS_PM_NFIELDS] = {9, 3, -1, 1, 1, 1, 3, 1, 1, 3, 1, 3, 1, 1, 1, 1};
 const int kFieldBytes[GCS_PM_NFIELDS] = {8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 8, 1};
@@ -1059,6 +1147,7 @@ int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t 
       bad(hipMalloc(&p->vals_s, tot * 4)) || bad(hipMalloc(&p->seg, tot * 4)) ||
       bad(hipMalloc(&p->d_tiles, max_tiles * 4)) || bad(hipMalloc(&p->d_tids, max_tiles * 8)) ||
       bad(hipMalloc(&p->mark, (size_t)m_tile * 4)) || bad(hipMalloc(&p->dcnt, 4)) ||
+      bad(hipMalloc(&p->bcnt, kMaxFuseBlocks * 4)) ||
       bad(hipHostMalloc((void**)&p->h_small, kSmall, hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&p->d_small, p->h_small, 0)))
     return fail();
@@ -1093,7 +1182,7 @@ int gcs_pmap_destroy(gcs_pmap* p) {
   for (void* f : p->fields)
     if (f) (void)hipFree(f);
   void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->seg, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
-                  p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
+                  p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->bmark, p->bcnt, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
                   p->msel, p->mnsel, p->ub};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -1259,6 +1348,69 @@ int fuse_impl(gcs_pmap* p, const int32_t* tiles, int32_t n, const gcs_pmap_rows*
   PMCHK(p, hipStreamSynchronize(p->stream));
   if (*(uint32_t*)(p->h_small + 8192)) return pm_fail(p, GCS_ERR_ARG, "target slot out of range (rows skipped)");
   *n_fused = (int32_t)*(uint32_t*)(p->h_small + 8200);
+  return GCS_OK;
+}
+
+// Step 12b's fuse: nb association blocks of rpb rows each (rows block-major), every listed tile
+// (already uploaded to d_tiles), in one sort + one apply (no host syncs between the blocks);
+// nf (host, nb): each block's unique target slots.  One sync at the end.
+int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int rpb, double timestamp, int64_t scan_seq,
+                double eps_mass, int32_t* nf) {
+  const int R = rows->n;
+  if (nb > kMaxFuseBlocks) return pm_fail(p, GCS_ERR_ARG, "map update: more than 256 association blocks");
+  if ((double)n * p->M * nb >= 4294967295.0) return pm_fail(p, GCS_ERR_ARG, "map update: fuse key space");
+  if (R > p->frows) {
+    for (void* b : {(void*)p->fk, (void*)p->fk_s, (void*)p->fv, (void*)p->fv_s, p->ftemp})
+      if (b) (void)hipFree(b);
+    p->fk = p->fk_s = p->fv = p->fv_s = nullptr;
+    p->ftemp = nullptr;
+    const int cap = std::max(R, 16384);
+    PMCHK(p, hipMalloc(&p->fk, cap * 4));
+    PMCHK(p, hipMalloc(&p->fk_s, cap * 4));
+    PMCHK(p, hipMalloc(&p->fv, cap * 4));
+    PMCHK(p, hipMalloc(&p->fv_s, cap * 4));
+    size_t tb = 0;
+    PMCHK(p, rocprim::radix_sort_pairs(nullptr, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)cap, 0u, 32u, p->stream));
+    p->ftemp_bytes = std::max<size_t>(tb, 16);
+    PMCHK(p, hipMalloc(&p->ftemp, p->ftemp_bytes));
+    p->frows = cap;
+  }
+  const size_t mb = (size_t)nb * p->M;
+  if (mb > p->bmark_bytes) {
+    if (p->bmark) PMCHK(p, hipFree(p->bmark));
+    p->bmark = nullptr;
+    PMCHK(p, hipMalloc(&p->bmark, mb));
+    p->bmark_bytes = mb;
+  }
+  uint32_t* d_err = (uint32_t*)(p->d_small + 8192);
+  *(uint32_t*)(p->h_small + 8192) = 0u;
+  PMCHK(p, hipMemsetAsync(p->bmark, 0, mb, p->stream));
+  PMCHK(p, hipMemsetAsync(p->bcnt, 0, nb * 4, p->stream));
+  const PmRows r = rows_of(rows);
+  const int rb = (R + kPmThreads - 1) / kPmThreads;
+  hipLaunchKernelGGL(k_pm_fuse_keys_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, r, n, p->M, nb, rpb, p->fk, p->fv,
+                     p->bmark, d_err);
+  unsigned bits = 1;
+  while (bits < 32 && ((double)(1ull << bits)) < (double)n * p->M * nb + 1.0) ++bits;
+  size_t tb = p->ftemp_bytes;
+  PMCHK(p, rocprim::radix_sort_pairs(p->ftemp, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)R, 0u, 32u, p->stream));
+  (void)bits;
+  hipLaunchKernelGGL(k_pm_fuse_apply_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
+                     r, (const uint32_t*)p->fk_s, (const uint32_t*)p->fv_s, nb, (long long)scan_seq);
+  const long tm = (long)n * p->M;
+  hipLaunchKernelGGL(k_pm_fuse_rgb, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
+                     p->stream, p->st, (const int32_t*)p->d_tiles, n, eps_mass);
+  const long tr = (long)n * R;
+  PMCHK(p, hipMemsetAsync(p->mark, 0, (size_t)p->M * 4, p->stream));  // k_pm_fuse_ts marks (unused here)
+  hipLaunchKernelGGL(k_pm_fuse_ts, dim3((unsigned)((tr + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
+                     p->stream, p->st, (const int32_t*)p->d_tiles, n, r, timestamp, p->mark);
+  hipLaunchKernelGGL(k_pm_count_marks_blocks, dim3((p->M + kPmThreads - 1) / kPmThreads, nb), dim3(kPmThreads), 0,
+                     p->stream, (const uint8_t*)p->bmark, p->M, p->bcnt);
+  PMCHK(p, hipMemcpyAsync(p->h_small + 9216, p->bcnt, nb * 4, hipMemcpyDeviceToHost, p->stream));
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  if (*(uint32_t*)(p->h_small + 8192)) return pm_fail(p, GCS_ERR_ARG, "target slot out of range (rows skipped)");
+  for (int b = 0; b < nb; ++b) nf[b] = (int32_t)((const uint32_t*)(p->h_small + 9216))[b];
   return GCS_OK;
 }
 }  // namespace
@@ -1428,23 +1580,24 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   std::vector<int32_t> tp(nrows);
   PMCHK(p, hipMemcpyAsync(fm.data(), o.fm, nrows * 8, hipMemcpyDeviceToHost, p->stream));
   PMCHK(p, hipMemcpyAsync(tp.data(), o.tpos, nrows * 4, hipMemcpyDeviceToHost, p->stream));
+  if (int rc = upload_tiles(p, tiles, n)) return rc;
+  gcs_pmap_rows ra{};
+  ra.Lambdas = o.lam;
+  ra.thetas = o.th;
+  ra.etas = o.eta;
+  ra.weights = o.w;
+  ra.responsibilities = o.resp;
+  ra.valid = o.valid;
+  ra.colors = o.col;
+  ra.sources = o.src;
+  ra.tile_pos = o.tpos;
+  ra.slots = o.slots;
+  ra.n = nrows;
+  std::vector<int32_t> nfb(nb);
+  if (int rc = fuse_blocks(p, n, &ra, nb, B * K, timestamp, scan_seq, cfg->eps_mass, nfb.data())) return rc;
   for (int b = 0; b < nb; ++b) {
     const size_t r0 = (size_t)b * B * K;
-    gcs_pmap_rows rb{};
-    rb.Lambdas = o.lam + 9 * r0;
-    rb.thetas = o.th + 3 * r0;
-    rb.etas = o.eta + (size_t)3 * nl * r0;
-    rb.weights = o.w + r0;
-    rb.responsibilities = o.resp + r0;
-    rb.valid = o.valid + r0;
-    rb.colors = o.col + 3 * r0;
-    rb.sources = o.src + r0;
-    rb.tile_pos = o.tpos + r0;
-    rb.slots = o.slots + r0;
-    rb.n = B * K;
-    int32_t nf = 0;
-    if (int rc = fuse_impl(p, tiles, n, &rb, timestamp, scan_seq, cfg->eps_mass, &nf, b == nb - 1)) return rc;
-    st->fused_count += n * nf;
+    st->fused_count += n * nfb[b];
     for (int t = 0; t < n; ++t) {  // fused_mass_total: per (block, tile) sums (pipeline.py:1306-1308)
       double sm = 0.0;
       for (int q = 0; q < B * K; ++q)
