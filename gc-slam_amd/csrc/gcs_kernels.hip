@@ -879,6 +879,9 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
 #ifndef GCS_RANK_LANES
 #define GCS_RANK_LANES 4  // phase A's per-bin work sum + source compaction: 4 lanes per bin (1: wave 0 alone)
 #endif
+#ifndef GCS_UNSTAGED_IDX
+#define GCS_UNSTAGED_IDX 1  // direct buckets, tile over its record stage: stage point indices (phase B)
+#endif
 #ifndef GCS_GATHER_PIPE
 // phase C: 1 loads the next staged record while accumulating the current one; 2 takes two
 // records per trip (two independent exp chains in flight)
@@ -1176,6 +1179,33 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       }
     }
   }
+#if GCS_UNSTAGED_IDX
+  // a tile over its record stage with direct buckets: stage the records' point indices instead (4 B
+  // each, in the stage's memory), ranked by point index within each source as above, so phase C
+  // gathers records from L2 without re-ranking members per record
+  const bool idx_staged = !staged && a.members && total <= (uint32_t)(STAGE * kRecD * 2);
+  if (idx_staged) {
+    uint32_t* s_idx = reinterpret_cast<uint32_t*>(s_rec);
+    for (uint32_t r = t; r < total; r += NT) {
+      int lo = 0, hi = ns - 1;
+      while (lo < hi) {
+        int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= r) lo = mid; else hi = mid - 1;
+      }
+      const uint32_t c = s_cnt[lo];
+      const uint4* row = (const uint4*)(a.members + s_st[lo]);
+      const uint32_t me = a.members[s_st[lo] + (r - s_off[lo])];
+      uint32_t rank = 0;
+      for (uint32_t q = 0; q < c; q += 4) {
+        const uint4 m4 = row[q >> 2];
+        rank += (m4.x < me) + (q + 1 < c && m4.y < me) + (q + 2 < c && m4.z < me) + (q + 3 < c && m4.w < me);
+      }
+      s_idx[s_off[lo] + rank] = me;
+    }
+  }
+#else
+  constexpr bool idx_staged = false;
+#endif
   __syncthreads();
   PROF(3);
   // phase C: four lanes per bin; the bin's records (sources in order, points in order) are one
@@ -1295,7 +1325,9 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     } else {
       for (uint32_t i = i0; i < i1; ++i) {
         uint32_t pidx;
-        if (a.members) {  // the kk-th smallest member (a tile over its stage: rare)
+        if (idx_staged) {
+          pidx = reinterpret_cast<const uint32_t*>(s_rec)[s_off[j] + kk];
+        } else if (a.members) {  // the kk-th smallest member (a tile over even the index stage: rarer)
           const uint32_t* row = a.members + s_st[j];
           pidx = row[0];
           for (uint32_t q = 0; q < c; ++q) {
