@@ -261,18 +261,18 @@ def extract_atlas_map_view(atlas_map: AtlasMap, tile_ids: List[int], m_tile_view
     dev = f"cuda:{atlas_map.device}"
     n, k = len(tile_ids), int(m_tile_view)
     R = n * k
-    # one device allocation carved into the view's arrays (8-B aligned slices)
-    nl = atlas_map.n_lobes
-    spec = [("positions", (R, 3), torch.float64), ("covariances", (R, 3, 3), torch.float64),
-            ("directions", (R, 3), torch.float64), ("kappas", (R,), torch.float64), ("weights", (R,), torch.float64),
-            ("etas", (R, nl, 3), torch.float64), ("colors", (R, 3), torch.float64),
-            ("primitive_ids", (R,), torch.int64), ("last_supported_scan_seq", (R,), torch.int64),
-            ("candidate_tile_ids", (R,), torch.int64), ("candidate_slots", (R,), torch.int32),
-            ("valid_mask", (R,), torch.uint8)]
-    sizes = [int(np.prod(sh)) * torch.empty((), dtype=dt).element_size() for _, sh, dt in spec]
-    offs = np.concatenate([[0], np.cumsum([(b + 7) // 8 * 8 for b in sizes])])
-    buf = torch.empty((int(offs[-1]),), dtype=torch.uint8, device=dev)
-    t = {name: buf[int(offs[i]):int(offs[i]) + sizes[i]].view(dt).view(sh) for i, (name, sh, dt) in enumerate(spec)}
+    t = dict(positions=torch.empty((R, 3), dtype=torch.float64, device=dev),
+             covariances=torch.empty((R, 3, 3), dtype=torch.float64, device=dev),
+             directions=torch.empty((R, 3), dtype=torch.float64, device=dev),
+             kappas=torch.empty((R,), dtype=torch.float64, device=dev),
+             weights=torch.empty((R,), dtype=torch.float64, device=dev),
+             primitive_ids=torch.empty((R,), dtype=torch.int64, device=dev),
+             valid_mask=torch.empty((R,), dtype=torch.uint8, device=dev),
+             last_supported_scan_seq=torch.empty((R,), dtype=torch.int64, device=dev),
+             etas=torch.empty((R, atlas_map.n_lobes, 3), dtype=torch.float64, device=dev),
+             colors=torch.empty((R, 3), dtype=torch.float64, device=dev),
+             candidate_slots=torch.empty((R,), dtype=torch.int32, device=dev),
+             candidate_tile_ids=torch.empty((R,), dtype=torch.int64, device=dev))
     v = L.GcsPmapView()
     for name, x in t.items():
         setattr(v, name, x.data_ptr() if R else None)
