@@ -773,9 +773,10 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     if (bad(hipMemset(c->d_sorted, 0, cap * sizeof(uint32_t)))) return GCS_ERR_HIP;
     // bin flags, then one flag per k_bins_scale tile (both cleared by k_budget every scan)
     const size_t nflags = B + bins_scale_blocks(c->B, c->tile_bins);
-    if (bad(hipMalloc(&c->d_flags_buf[0], 2 * nflags))) return GCS_ERR_HIP;
-    if (bad(hipMemset(c->d_flags_buf[0], 0, 2 * nflags))) return GCS_ERR_HIP;
-    c->d_flags_buf[1] = c->d_flags_buf[0] + nflags;
+    const size_t nflags16 = (nflags + 15) & ~(size_t)15;  // both buffers 16-B aligned (k_budget's clear)
+    if (bad(hipMalloc(&c->d_flags_buf[0], 2 * nflags16))) return GCS_ERR_HIP;
+    if (bad(hipMemset(c->d_flags_buf[0], 0, 2 * nflags16))) return GCS_ERR_HIP;
+    c->d_flags_buf[1] = c->d_flags_buf[0] + nflags16;
     c->d_flags = c->d_flags_buf[0];
     // every tile starts dirty: the first scan writes all ScanBinStats rows and partial rows
     if (bad(hipMalloc(&c->d_tile_dirty, bins_scale_blocks(c->B, c->tile_bins)))) return GCS_ERR_HIP;
