@@ -253,3 +253,85 @@ def test_map_update_step_matches_oracle():
             assert am.counts[tid] == int(tiles[tid]["valid_mask"].sum())
     assert st_ref["insert_count_total"] > 0 and st_ref["fused_count"] > 0
     am.close()
+
+
+@pytest.mark.parametrize("case", ["all_invalid", "ragged_blocks", "no_insert", "populated", "empty_active"])
+def test_map_update_edge_cases(case):
+    """Step 12b edge cases against the oracle: an all-invalid MeasurementBatch (zero fused and
+    inserted mass, cull / forget still run), a ragged last association block (N = 301, block 128), a zero
+    insert budget, tiles already holding primitives (retention evictions on insert, merges), and an
+    empty active-tile list (exact no-op)."""
+    from types import SimpleNamespace
+    from gcslam import primitive_map as gpm
+    from oracle import se3
+    rng = np.random.default_rng(20 + ["all_invalid", "ragged_blocks", "no_insert", "populated", "empty_active"].index(case))
+    m, N, K = 1024, (301 if case == "ragged_blocks" else 400), 8
+    block = 128 if case == "ragged_blocks" else 256
+    kins = 0 if case == "no_insert" else 64
+    cfg = gpm.PrimitiveMapUpdateConfig(k_insert_tile=kins, block_size=block)
+    z = np.array([0.4, 0.2, -0.3, -0.03, 0.02, 0.9])
+    R, t = se3.so3_exp(z[3:]), z[:3]
+    p_body = rng.uniform(-4, 4, size=(N, 3))
+    A = rng.normal(size=(N, 3, 3)) * 0.2
+    Lam = np.einsum("nij,nkj->nik", A, A) + np.eye(3)[None] * rng.uniform(1, 5, size=(N, 1, 1))
+    valid = np.zeros(N, bool) if case == "all_invalid" else rng.random(N) < 0.85
+    batch = dict(Lambdas=Lam, thetas=np.einsum("nij,nj->ni", Lam, p_body), etas=rng.normal(size=(N, NL, 3)),
+                 weights=rng.random(N), valid_mask=valid, colors=rng.random((N, 3)),
+                 sources=rng.integers(0, 2, N).astype(np.int32))
+    wtid = opm.tile_ids_from_xyz(p_body @ R.T + t[None], 2.0)
+    uniq, cnts = np.unique(wtid, return_counts=True)
+    active = [] if case == "empty_active" else [int(x) for x in uniq[np.argsort(-cnts, kind="stable")][:5]]
+    tiles = {}
+    if case in ("populated", "all_invalid", "empty_active"):
+        for tid in (active or [int(uniq[0])]):
+            tt = _rand_tile(rng, m=m, frac=0.97 if case == "populated" else 0.5, seq_hi=30)
+            tt["weights"][rng.random(m) < 0.05] = 1e-6      # below the cull threshold
+            tiles[tid] = tt
+    am = gpm.AtlasMap(m_tile=m, max_tiles=16, n_lobes=NL, max_merge=m)
+    for tid, tt in tiles.items():
+        am.write_tile(tid, tt)
+    am.next_global_id = 50_000
+    before = {tid: {k: v.copy() for k, v in tt.items()} for tid, tt in tiles.items()}
+    ctile = rng.choice(np.array(active + [777], dtype=np.int64), size=(N, K))
+    assoc = dict(responsibilities=rng.random((N, K)) / K, candidate_tile_ids=ctile,
+                 candidate_slots=rng.integers(0, m, size=(N, K)), row_masses=rng.random(N) * 2.0 / N)
+    nxt_ref, st_ref = opm.map_update_step(tiles, 50_000, batch, assoc, R, t, active, m, 7.0, 33,
+                                          k_insert_tile=kins, h_tile=2.0, block_size=block)
+    st = gpm.primitive_map_update(am, SimpleNamespace(**batch), SimpleNamespace(**assoc), z, active, 7.0, 33, cfg)
+    assert am.next_global_id == nxt_ref
+    for k in ("fused_count", "insert_count_total", "evicted_count", "merged_count"):
+        assert st[k] == st_ref[k], k
+    for k in ("fused_mass_total", "insert_mass_total", "insert_mass_p95", "evicted_mass_total"):
+        assert st[k] == pytest.approx(st_ref[k], rel=1e-12, abs=1e-300), k
+    for tid in active:
+        _same_tile(am.read_tile(tid), tiles[tid], rtol=1e-11, what=f"{case} tile {tid}")
+        assert am.counts[tid] == int(tiles[tid]["valid_mask"].sum())
+    if case == "all_invalid":   # the mask zeroes responsibilities and novelty; counts still follow the reference
+        assert st["fused_mass_total"] == 0.0 and st["insert_mass_total"] == 0.0 and st["evicted_count"] > 0
+    if case == "no_insert":
+        assert st["insert_count_total"] == 0 and st["fused_count"] > 0
+    if case == "populated":
+        assert st["insert_count_total"] > 0
+    if case == "empty_active":
+        assert all(v == 0 for k, v in st.items() if k not in ("tile_ids_active",))
+        for tid, tt in before.items():   # untouched
+            _same_tile(am.read_tile(tid), tt, what=f"untouched tile {tid}")
+    am.close()
+
+
+def test_view_sparse_and_empty_tiles():
+    """extract_atlas_map_view when a tile holds fewer valid primitives than m_tile_view (the top-k
+    falls through to invalid slots in slot order) and when a tile is empty or absent."""
+    from gcslam import primitive_map as gpm
+    rng = np.random.default_rng(9)
+    tiles = {3: _rand_tile(rng, frac=0.002), 4: _rand_tile(rng, frac=0.0)}
+    am = _map(tiles)
+    order = [4, 3, 55]
+    v = opm.extract_atlas_map_view(tiles, order, 1024, M)
+    g = gpm.extract_atlas_map_view(am, order, 1024)
+    cpu = lambda x: x.detach().cpu().numpy()  # noqa: E731
+    assert int(tiles[3]["valid_mask"].sum()) < 1024
+    for f in ("candidate_slots", "candidate_tile_ids", "valid_mask", "primitive_ids", "weights"):
+        assert np.array_equal(cpu(getattr(g, f)), v[f]), f
+    np.testing.assert_allclose(cpu(g.positions), v["positions"], rtol=1e-12, atol=1e-12)
+    am.close()
