@@ -174,6 +174,131 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_
   vals[g] = (uint32_t)g;  // tile position x M + slot
 }
 
+// the first k (<= kSelMax) entries of each tile's stable key order without sorting the tile: one
+// workgroup per tile finds the k-th smallest key T by an MSB radix select (8 passes of 8 bits over
+// the tile's keys), collects the keys below T and the first ties at T in slot order (exactly the
+// entries a stable sort puts first), and orders those k by (key, slot) with a bitonic sort in LDS.
+// Writes sorted[t M + r] = t M + slot for r < k (what k_pm_view / k_pm_insert read).
+constexpr int kSelMax = 1024;
+__global__ __launch_bounds__(kPmRed) void k_pm_select(const uint64_t* __restrict__ keys, int M, int k,
+                                                       uint32_t* __restrict__ sorted) {
+  __shared__ uint32_t s_hist[256];
+  __shared__ uint64_t s_key[kSelMax];
+  __shared__ uint32_t s_slot[kSelMax];
+  __shared__ uint32_t s_wl[kPmRed / 64], s_we[kPmRed / 64];
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_need;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint64_t* kt = keys + (size_t)t * M;
+  uint64_t prefix = 0, pmask = 0;
+  uint32_t need = (uint32_t)k;  // rank (1-based) of T among the keys that match the prefix
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += kPmRed) s_hist[i] = 0u;
+    __syncthreads();
+    for (int q = tid; q < M; q += kPmRed) {
+      const uint64_t x = kt[q];
+      if ((x & pmask) == prefix) atomicAdd(&s_hist[(x >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: the digit whose cumulative count reaches need
+      uint32_t h[4], sum = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        h[j] = s_hist[4 * tid + j];
+        sum += h[j];
+      }
+      uint32_t inc = sum;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+      }
+      const uint32_t exc = inc - sum;
+      if (exc < need && inc >= need) {
+        uint32_t c = exc;
+        int d = 4 * tid;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          if (c + h[j] >= need) {
+            d = 4 * tid + j;
+            break;
+          }
+          c += h[j];
+        }
+        s_need = need - c;
+        s_prefix = prefix | ((uint64_t)d << shift);
+      }
+    }
+    __syncthreads();
+    need = s_need;
+    prefix = s_prefix;
+    pmask |= (uint64_t)255u << shift;
+    __syncthreads();
+  }
+  // keys < T: exactly k - need of them; keys == T: the first `need` in slot order
+  const uint32_t nless = (uint32_t)k - need;
+  const uint64_t below = (1ull << lane) - 1ull;
+  uint32_t base_l = 0, base_e = 0;
+  for (int c0 = 0; c0 < M; c0 += kPmRed) {
+    const int q = c0 + tid;
+    const uint64_t x = q < M ? kt[q] : ~0ull;
+    const bool lt = q < M && x < prefix, eq = q < M && x == prefix;
+    const uint64_t bl = __ballot(lt), be = __ballot(eq);
+    if (lane == 0) {
+      s_wl[wid] = (uint32_t)__popcll(bl);
+      s_we[wid] = (uint32_t)__popcll(be);
+    }
+    __syncthreads();
+    uint32_t ol = 0, oe = 0, tl = 0, te = 0;
+    for (int w = 0; w < kPmRed / 64; ++w) {
+      if (w < wid) {
+        ol += s_wl[w];
+        oe += s_we[w];
+      }
+      tl += s_wl[w];
+      te += s_we[w];
+    }
+    if (lt) {
+      const uint32_t pos = base_l + ol + (uint32_t)__popcll(bl & below);
+      s_key[pos] = x;
+      s_slot[pos] = (uint32_t)q;
+    }
+    if (eq) {
+      const uint32_t r = base_e + oe + (uint32_t)__popcll(be & below);
+      if (r < need) {
+        s_key[nless + r] = x;
+        s_slot[nless + r] = (uint32_t)q;
+      }
+    }
+    base_l += tl;
+    base_e += te;
+    __syncthreads();
+  }
+  int P = 1;
+  while (P < k) P <<= 1;
+  for (int i = k + tid; i < P; i += kPmRed) {
+    s_key[i] = ~0ull;
+    s_slot[i] = ~0u;
+  }
+  for (int size = 2; size <= P; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      const int i = tid, j = tid ^ stride;
+      if (i < P && j > i) {
+        const uint64_t ki = s_key[i], kj = s_key[j];
+        const uint32_t si = s_slot[i], sj = s_slot[j];
+        const bool gt = ki > kj || (ki == kj && si > sj);
+        if (gt == ((i & size) == 0)) {
+          s_key[i] = kj;
+          s_key[j] = ki;
+          s_slot[i] = sj;
+          s_slot[j] = si;
+        }
+      }
+    }
+  __syncthreads();
+  for (int r = tid; r < k; r += kPmRed) sorted[(size_t)t * M + r] = (uint32_t)((size_t)t * M) + s_slot[r];
+}
+
 // second (stable) pass of the per-tile sort: key = the entry's tile position
 __global__ __launch_bounds__(kPmThreads) void k_pm_segkeys(const uint32_t* vals, long total, int M, uint32_t* seg) {
   const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
@@ -1047,11 +1172,22 @@ int upload_tiles(gcs_pmap* p, const int32_t* tiles, int n) {
 // stable per-tile sort of the slot keys (mode 0 view, 1 eviction): one radix sort of every listed
 // tile's (key, tile position x M + slot), then a stable radix sort on the tile position -- per tile the
 // key order with ties by slot (LSD composition).  Result (tile position x M + slot) in vals.
-int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam) {
+int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam, int k) {
   const long total = (long)n * p->M;
   const unsigned gb = (unsigned)((total + kPmThreads - 1) / kPmThreads);
   hipLaunchKernelGGL(k_pm_keys, dim3(gb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, mode,
                      seq, lam, p->keys, p->vals);
+  // only the first k of each tile are read: a per-tile select + LDS sort replaces the full radix sort
+  // (GCSLAM_PM_FULLSORT=1 keeps the full sort, for A/B)
+  static const bool full = [] {
+    const char* e = getenv("GCSLAM_PM_FULLSORT");
+    return e && e[0] == '1';
+  }();
+  if (k >= 1 && k <= kSelMax && !full) {
+    hipLaunchKernelGGL(k_pm_select, dim3(n), dim3(kPmRed), 0, p->stream, (const uint64_t*)p->keys, p->M, k, p->vals);
+    PMCHK(p, hipGetLastError());
+    return GCS_OK;
+  }
   size_t tb = p->temp_bytes;
   PMCHK(p, rocprim::radix_sort_pairs(p->temp, tb, p->keys, p->keys_s, p->vals, p->vals_s, (unsigned)total, 0u, 64u,
                                      p->stream));
@@ -1242,7 +1378,7 @@ int gcs_pmap_extract_view(gcs_pmap* p, const int32_t* tiles, const int64_t* tile
   PMCHK(p, hipSetDevice(p->device));
   if (int rc = upload_tiles(p, tiles, n)) return rc;
   PMCHK(p, hipMemcpyAsync(p->d_tids, tile_ids, n * sizeof(int64_t), hipMemcpyHostToDevice, p->stream));
-  if (int rc = sort_tiles(p, n, 0, 0, 0.0)) return rc;
+  if (int rc = sort_tiles(p, n, 0, 0, 0.0, m_view)) return rc;
   PmViewOut v{o->positions, o->covariances, o->directions, o->kappas, o->weights, o->etas, o->colors,
               o->primitive_ids, o->last_supported_scan_seq, o->candidate_tile_ids, o->valid_mask,
               o->candidate_slots};
@@ -1268,7 +1404,7 @@ int gcs_pmap_insert_masked(gcs_pmap* p, const int32_t* tiles, int32_t n, int32_t
   if (int rc = upload_tiles(p, tiles, n)) return rc;
   int32_t* d_ins = (int32_t*)p->d_small;
   if (K > 0) {
-    if (int rc = sort_tiles(p, n, 1, scan_seq, lam)) return rc;
+    if (int rc = sort_tiles(p, n, 1, scan_seq, lam, K)) return rc;
     hipLaunchKernelGGL(k_pm_insert, dim3(1), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, K,
                        (const uint32_t*)p->vals, rows_of(rows), timestamp, (long long)scan_seq,
                        (long long)next_global_id, new_ids, d_ins);
