@@ -175,14 +175,15 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_
 }
 
 // the first k (<= kSelMax) entries of each tile's stable key order without sorting the tile: one
-// workgroup per tile finds the k-th smallest key T by an MSB radix select (8 passes of 8 bits over
+// workgroup per tile finds the k-th smallest key T by an MSB radix select (6 passes of 11 bits over
 // the tile's keys), collects the keys below T and the first ties at T in slot order (exactly the
 // entries a stable sort puts first), and orders those k by (key, slot) with a bitonic sort in LDS.
 // Writes sorted[t M + r] = t M + slot for r < k (what k_pm_view / k_pm_insert read).
 constexpr int kSelMax = 1024;
+constexpr int kSelBits = 11;  // digit width of the select passes (6 passes over 64-bit keys)
 __global__ __launch_bounds__(kPmRed) void k_pm_select(const uint64_t* __restrict__ keys, int M, int k,
                                                        uint32_t* __restrict__ sorted) {
-  __shared__ uint32_t s_hist[256];
+  __shared__ uint32_t s_hist[1 << kSelBits];
   __shared__ uint64_t s_key[kSelMax];
   __shared__ uint32_t s_slot[kSelMax];
   __shared__ uint32_t s_wl[kPmRed / 64], s_we[kPmRed / 64];
@@ -192,21 +193,20 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select(const uint64_t* __restrict
   const uint64_t* kt = keys + (size_t)t * M;
   uint64_t prefix = 0, pmask = 0;
   uint32_t need = (uint32_t)k;  // rank (1-based) of T among the keys that match the prefix
-  for (int shift = 56; shift >= 0; shift -= 8) {
-    for (int i = tid; i < 256; i += kPmRed) s_hist[i] = 0u;
+  for (int hi = 64; hi > 0; hi -= kSelBits) {
+    const int bits = hi < kSelBits ? hi : kSelBits, shift = hi - bits;
+    const uint32_t dmask = (1u << bits) - 1u;
+    for (int i = tid; i < (1 << kSelBits); i += kPmRed) s_hist[i] = 0u;
     __syncthreads();
     for (int q = tid; q < M; q += kPmRed) {
       const uint64_t x = kt[q];
-      if ((x & pmask) == prefix) atomicAdd(&s_hist[(x >> shift) & 255u], 1u);
+      if ((x & pmask) == prefix) atomicAdd(&s_hist[(uint32_t)(x >> shift) & dmask], 1u);
     }
     __syncthreads();
-    if (tid < 64) {  // wave 0: the digit whose cumulative count reaches need
-      uint32_t h[4], sum = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        h[j] = s_hist[4 * tid + j];
-        sum += h[j];
-      }
+    if (tid < 64) {  // wave 0: the digit whose cumulative count reaches need (kSelPer bins per lane)
+      constexpr int kSelPer = (1 << kSelBits) / 64;
+      uint32_t sum = 0;
+      for (int j = 0; j < kSelPer; ++j) sum += s_hist[kSelPer * tid + j];
       uint32_t inc = sum;
       for (int off = 1; off < 64; off <<= 1) {
         const uint32_t y = __shfl_up(inc, off, 64);
@@ -215,14 +215,14 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select(const uint64_t* __restrict
       const uint32_t exc = inc - sum;
       if (exc < need && inc >= need) {
         uint32_t c = exc;
-        int d = 4 * tid;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (c + h[j] >= need) {
-            d = 4 * tid + j;
+        int d = kSelPer * tid;
+        for (int j = 0; j < kSelPer; ++j) {
+          const uint32_t h = s_hist[kSelPer * tid + j];
+          if (c + h >= need) {
+            d = kSelPer * tid + j;
             break;
           }
-          c += h[j];
+          c += h;
         }
         s_need = need - c;
         s_prefix = prefix | ((uint64_t)d << shift);
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select(const uint64_t* __restrict
     __syncthreads();
     need = s_need;
     prefix = s_prefix;
-    pmask |= (uint64_t)255u << shift;
+    pmask |= (uint64_t)dmask << shift;
     __syncthreads();
   }
   // keys < T: exactly k - need of them; keys == T: the first `need` in slot order
