@@ -15,7 +15,11 @@ the roofline kernel at C3 (configs[2], `roofline_c3`), the pinned-host H2D of on
 the C1-equivalent N=8192 x B=48 dense case).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3] [--no-cpu-baseline] [--no-c3]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Multi-GPU: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N, or plain
+`python bench.py --gpus N`: without a launcher's WORLD_SIZE this process starts the N rank processes
+itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, 127.0.0.1) before touching any GPU, and exits
+with their status.  `--cpu-rehearsal` runs the launcher + per-scan payload exchange on CPU over gloo
+(library pack / apply on synthetic hypotheses; tests/test_bench_launcher.py), not a benchmark.
 """
 
 from __future__ import annotations
@@ -48,6 +52,24 @@ def bins_kernel_bytes(N, B):
     kernel with responsibilities not materialised: N (3 s_p + 8 + 8) [xyz f32, t, w] + B 3 s_d
     [bin directions, f64] read; B 26 s_o [ScanBinStats, f64] written.  Returns (read, write)."""
     return N * (3 * 4 + 8 + 8) + B * 3 * 8, B * 26 * 8
+
+
+def roofline_chain(N, B, stage_avg, label):
+    """The north star's "BinSoftAssign + ScanBinMomentMatch" as the kernel chain that implements it:
+    k_budget (row 1) + k_points (rows 1, 3, 5: gather, deskew, direction, nearest bin, K-candidate
+    softmax normaliser) + k_bins_scale (rows 4-6 + MF terms) + the bin kernel's partial-row fold,
+    each timed by its own dispatch events, against the same SURVEY 8(d) bytes as `roofline`."""
+    names = ("budget", "points", "bins", "bins_fold")
+    if any(stage_avg.get(k) is None for k in names):
+        return None
+    ms = sum(stage_avg[k] for k in names)
+    rd, wr = bins_kernel_bytes(N, B)
+    s = ms * 1e-3
+    ach = (rd + wr) / s / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "read_frac": rd / s / 1e9 / HBM_PEAK_GBS, "write_frac": wr / s / 1e9 / HBM_PEAK_GBS,
+            "chain_us": ms * 1e3, "kernels_us": {k: stage_avg[k] * 1e3 for k in names},
+            "algorithmic_bytes": rd + wr, "config": label}
 
 
 def roofline(N, B, kernel_ms, traffic=None, traffic_source=None):
@@ -140,7 +162,8 @@ def cpu_baseline(cfg):
                sample=f"{n1} full 14-step scans (numpy oracle, scale mode) at N={N}, B={B}, K={cfg['K']} on 1 "
                       f"pinned host core (threadpoolctl limit 1), {t1:.1f} s",
                cpu_model=_cpu_model(), cpu_count=os.cpu_count(), cpus_allowed=len(allowed))
-    # all cores: one independent hypothesis stream per core (processes pinned one per core)
+    # multi-core: one independent hypothesis stream per core (processes pinned one per core), on the
+    # box's CPU share per GPU (16: os.cpu_count() reports the whole host's CPUs there)
     P = min(len(allowed), int(os.environ.get("GCS_BASELINE_PROCS", "16")))
     try:
         ctx = mp.get_context("spawn")
@@ -152,12 +175,13 @@ def cpu_baseline(cfg):
             wall = time.perf_counter() - t0
         nsc = sum(r[0] for r in res)
         tmax = max(r[1] for r in res)
-        out["all_cores"] = dict(value=nsc / tmax, unit="scans/s", cores=P,
-                                sample=f"{P} processes x 2 scans (one hypothesis stream per pinned core), timed "
-                                       f"from a common barrier; {wall:.1f} s wall incl. setup")
+        out["multi_core"] = dict(value=nsc / tmax, unit="scans/s", cores=P,
+                                 sample=f"{P} processes x 2 scans (one hypothesis stream per pinned core, {P} of the "
+                                        f"{len(allowed)} CPUs this process may use: the GPU box's per-GPU CPU "
+                                        f"share), timed from a common barrier; {wall:.1f} s wall incl. setup")
         mgr.shutdown()
     except Exception as e:  # the baseline is reported, never the thing measured
-        out["all_cores"] = dict(value=None, error=repr(e)[:200])
+        out["multi_core"] = dict(value=None, error=repr(e)[:200])
     n3, t3 = _oracle_scans(8192, 48, "dense", 40, 3.0, core=allowed[0])
     os.sched_setaffinity(0, prev)
     out["c1_equivalent"] = dict(value=n3 / t3, unit="scans/s", cores=1,
@@ -225,7 +249,7 @@ def c3_roofline(device, steps=16, warmup=3):
         sc, rec, t, w = scans[k % 2]
         ctx.scan(rec, 16, t, w, cfg["N"], **scan_kwargs(sc))
     ctx.synchronize()
-    ctx.enable_timing(True, stages=["bins"])
+    ctx.enable_timing(True, stages=["budget", "points", "bins", "bins_fold"])
     ctx.stage_times(reset=True)
     t0 = time.perf_counter()
     for k in range(steps):
@@ -235,32 +259,161 @@ def c3_roofline(device, steps=16, warmup=3):
     el = time.perf_counter() - t0
     ms_sum, cnt = ctx.stage_times(reset=True)
     ctx.close()
-    kms = float(ms_sum[2] / cnt[2]) if cnt[2] else None
-    r = roofline(cfg["N"], cfg["B"], kms, *pmc_traffic("c3"))
+    avg = {name: (float(ms_sum[i] / cnt[i]) if cnt[i] else None) for i, name in enumerate(ctx.STAGES)}
+    r = roofline(cfg["N"], cfg["B"], avg["bins"], *pmc_traffic("c3"))
+    label = "c3: 262144-pt scans vs 1048576-bin map, K=16"
     if r:
-        r.update(config="c3: 262144-pt scans vs 1048576-bin map, K=16", timed_launches=int(cnt[2]),
-                 scans_per_s_with_bins_stamps=steps / el)
-    return r
+        r.update(config=label, timed_launches=int(cnt[2]), scans_per_s_with_chain_stamps=steps / el)
+    return r, roofline_chain(cfg["N"], cfg["B"], avg, label)
+
+
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, cpu):
+    """`bench.py --gpus N` with no launcher: start N rank processes of this script (the one-process-per-GPU
+    layout torch.distributed.run gives) and return their exit status.  Nothing here touches a GPU:
+    torch.cuda.device_count() counts devices without initialising one on this image, and each rank
+    initialises only its own device."""
+    import subprocess
+    if not cpu:
+        import torch
+        vis = torch.cuda.device_count()
+        if n > vis:
+            print(f"bench.py: --gpus {n} but only {vis} visible GPU(s)", file=sys.stderr, flush=True)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.1)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                for q in live:  # one rank failed: the others would block in the next collective
+                    q.terminate()
+    for p in procs:
+        try:
+            p.wait(timeout=30)
+        except subprocess.TimeoutExpired:
+            p.kill()
+    return rc
+
+
+def cpu_rehearsal(args, rank, world):
+    """The multi-rank path without GPUs (gloo): each rank packs its hypothesis' payload with the library
+    (gcs_payload_pack: IW statistics with the raw weights, barycenter sums with the floor-renormalised
+    ones, backend_node.py:1999-2002,2085-2090, hypothesis.py:83-99), the payloads are summed over
+    torch.distributed, and every rank applies the sum (gcs_payload_apply: barycenter, both IW applies,
+    Q), carrying the IW states to the next step.  The per-rank payloads are all-gathered once to check
+    the sum.  A rehearsal of the launcher and the exchange, not a benchmark."""
+    import ctypes as C
+    import torch
+    import torch.distributed as dist
+    from gcslam import _lib as L
+    from gcslam.distributed import allreduce_payload, hypothesis_weights
+    lib = L.load()
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    w, wn = hypothesis_weights(world)
+    rng = np.random.default_rng(1000 + rank)
+    nu, Psi = np.zeros(7), np.zeros(252)
+    mnu, mPsi = np.zeros(3), np.zeros(27)
+    assert lib.gcs_datasheet_noise_states(nu.ctypes.data, Psi.ctypes.data, mnu.ctypes.data, mPsi.ctypes.data) == 0
+    err, payloads = 0.0, None
+    t0 = time.perf_counter()
+    for step in range(args.warmup + args.steps):
+        if step == args.warmup:
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+        A = rng.normal(size=(22, 22))
+        Lm = A @ A.T + 22.0 * np.eye(22)
+        bs = L.belief_to_struct(rng.normal(0, 0.05, 6), float(step), rng.normal(0, 1e-3, 22), Lm, rng.normal(size=22))
+        dPsi = np.ascontiguousarray(np.stack([np.outer(v, v) for v in rng.normal(0, 1e-2, (7, 6))]).reshape(252))
+        dnu = np.ones(7)
+        mdPsi = np.ascontiguousarray(np.stack([np.outer(v, v) for v in rng.normal(0, 1e-3, (3, 3))]).reshape(27))
+        mdnu = np.array([1.0, 1.0, 0.0])
+        p = np.zeros(840)
+        assert lib.gcs_payload_pack(C.byref(bs), dPsi.ctypes.data, dnu.ctypes.data, mdPsi.ctypes.data,
+                                    mdnu.ctypes.data, float(w[rank]), float(wn[rank]), p.ctypes.data) == 0
+        if step == 0:  # every rank's own payload, gathered before the sum (the transport reduces in place)
+            if world > 1:
+                got = [torch.zeros(840, dtype=torch.float64) for _ in range(world)]
+                dist.all_gather(got, torch.from_numpy(p.copy()))
+                payloads = np.stack([g.numpy() for g in got])
+            else:
+                payloads = p[None].copy()
+        tot = np.ascontiguousarray(allreduce_payload(p))
+        if step == 0:
+            err = float(np.abs(payloads.sum(0) - tot).max())
+        comb = L.GcsBelief()
+        out = [np.zeros(n) for n in (7, 252, 484, 3, 27, 4)]
+        assert lib.gcs_payload_apply(tot.ctypes.data, step, np.zeros(6).ctypes.data, 0.0, nu.ctypes.data,
+                                     Psi.ctypes.data, mnu.ctypes.data, mPsi.ctypes.data, C.byref(comb),
+                                     *[o.ctypes.data for o in out]) == 0
+        nu, Psi, _, mnu, mPsi, _ = out
+    el = time.perf_counter() - t0
+    ranks = [rank]
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+        allr = [None] * world
+        dist.all_gather_object(allr, dict(rank=rank, pid=os.getpid(), Q_sum=float(out[2].sum())))
+        ranks = allr
+    if rank == 0:
+        print(json.dumps({
+            "metric": "payload exchanges/s (CPU rehearsal of the multi-rank path; not the benchmark)",
+            "value": args.steps / el, "unit": "exchanges/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "higher_is_better": True, "rehearsal": True, "transport": "gloo" if world > 1 else None,
+            "ranks": ranks, "payload_sum_max_abs_err": err,
+            "payload_sum_check": bool(err <= 1e-12 * max(1.0, float(np.abs(payloads).sum(0).max())))}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c3", action="store_true")
+    ap.add_argument("--cpu-rehearsal", action="store_true",
+                    help="launcher + payload exchange over gloo on CPU (test of the multi-rank path)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, args.cpu_rehearsal))  # before any GPU call in this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if args.cpu_rehearsal:
+        return cpu_rehearsal(args, rank, world)
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
     device = f"cuda:{local_rank}"
@@ -272,6 +425,15 @@ def main():
 
     # the per-scan exchange runs in the library over RCCL (torch.distributed only broadcasts the id)
     comm = HypothesisComm(rank, world, local_rank) if world > 1 else None
+    rccl = None
+    if comm is not None:
+        n_comm, r_comm = comm.count()
+        cnt = torch.tensor([n_comm, r_comm], dtype=torch.int64, device=device)
+        allc = [torch.zeros_like(cnt) for _ in range(world)]
+        dist.all_gather(allc, cnt)
+        rccl = dict(comm_count=n_comm, user_ranks=[int(c[1]) for c in allc], counts=[int(c[0]) for c in allc])
+        if any(int(c[0]) != world for c in allc):
+            raise RuntimeError(f"RCCL communicator holds {rccl['counts']} ranks, expected {world}")
     cfg = CONFIGS[args.config]
     N, B, K = cfg["N"], cfg["B"], cfg["K"]
     ctx = make_ctx(cfg, local_rank)
@@ -331,10 +493,13 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    per_rank_s = [elapsed]
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        allt = [torch.zeros_like(tt) for _ in range(world)]
+        dist.all_gather(allt, tt)
+        per_rank_s = [float(x.item()) for x in allt]
+        elapsed = max(per_rank_s)  # the slowest rank's clock
     state["sample"] = False
     ms_sum, counts = ctx.stage_times(reset=True)
     bins_ms = float(ms_sum[2] / counts[2]) if counts[2] else None
@@ -368,9 +533,14 @@ def main():
             "value_definition": "hypothesis-scans/s of the whole job: every GPU runs its own hypothesis of each scan "
                                 "(weak scaling); the node's scans/s is scans_per_s_node = value / n_gpus",
             "scans_per_s_node": args.steps / elapsed,
+            # the per-GPU rate SCALE compares across N (value / n_gpus; at N = 1 it equals value)
+            "value_per_gpu": args.steps / elapsed,
+            "per_rank_ms_per_step": [t / args.steps * 1e3 for t in per_rank_s],
+            "rccl": rccl,
             "step_ms": {"median": float(np.median(per_step) * 1e3), "p90": float(np.percentile(per_step, 90) * 1e3),
                         "min": float(per_step.min() * 1e3), "max": float(per_step.max() * 1e3)},
             "roofline": dict(roofline(N, B, bins_ms, *pmc_traffic(args.config)) or {}, timed_launches=bins_samples),
+            "roofline_chain": roofline_chain(N, B, stage_avg, f"{args.config} (diagnostic pass, every stage stamped)"),
             "stage_ms": stage_avg,
             "host_ms": host_avg,
             "pcie_inclusive": {"h2d_bytes_per_scan": h2d_bytes, "scans_per_s": 1e3 / (ms_step / world + h2d) * world,
@@ -378,7 +548,7 @@ def main():
             "manifest": manifest,
         }
         if world == 1 and args.config == "c2" and not args.no_c3:
-            line["roofline_c3"] = c3_roofline(local_rank)
+            line["roofline_c3"], line["roofline_chain_c3"] = c3_roofline(local_rank)
         line["cpu_baseline"] = cpu_baseline(cfg) if (world == 1 and not args.no_cpu_baseline) else None
         print(json.dumps(line), flush=True)
     if comm is not None:

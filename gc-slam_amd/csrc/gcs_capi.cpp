@@ -28,7 +28,9 @@ using host::Belief;
 using host::DZ;
 
 // device stages timed with hipEvents when timing is enabled
-enum { ST_POINTS = 0, ST_SORT = 1, ST_BINS = 2, ST_MF = 3, ST_PT = 4, ST_PUSH = 5, kStages = 6 };
+enum { ST_POINTS = 0, ST_SORT = 1, ST_BINS = 2, ST_MF = 3, ST_PT = 4, ST_PUSH = 5, ST_BUDGET = 6, ST_BINS_FOLD = 7,
+       kStages = 8 };
+static_assert(kStages == GCS_N_STAGES, "stage count of the C-ABI");
 
 struct gcs_ctx {
   gcs_config cfg{};
@@ -315,8 +317,9 @@ int submit_budget(gcs_ctx* c, const BudgetArgs& ba, int nblk, hipStream_t s);
 // ---------------------------------------------------------------- device stages
 // fold_later: leave k_points' cert fold to block 0 of the next k_bins_scale (scale-mode scan)
 // Row 1's mass sums (k_budget) need only the weights: gcs_scan queues them before its host
-// prologue so they run while the host predicts and preintegrates.  e0: stage timing start (may be null).
-int stage_budget(gcs_ctx* c, const double* w, int n_raw, hipEvent_t e0, bool toggle = true) {
+// prologue so they run while the host predicts and preintegrates.  Timed (stage ST_BUDGET), the launch
+// is made here with the kernel's own start / end events; otherwise by the worker thread.
+int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
   int stride = std::max(1, (int)((n_raw + (long)c->cap - 1) / c->cap));  // ceil(N/cap), point_budget.py:160
   int n_sel = (n_raw + stride - 1) / stride;
@@ -339,8 +342,10 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, hipEvent_t e0, bool tog
   ba.n_zero8 = c->d_flags ? c->B + bins_scale_blocks(c->B, c->tile_bins) : 0;
   c->budget_blocks = red_blocks(std::max(n_raw, 1));
   c->budget_pending = true;
-  if (!e0 && c->push_async) return submit_budget(c, ba, c->budget_blocks, s);
-  HIPCHK(c, launch_budget(ba, c->budget_blocks, s, e0, nullptr));
+  StageEv ev = stage_ev(c, ST_BUDGET);
+  if (!ev.e0 && c->push_async) return submit_budget(c, ba, c->budget_blocks, s);
+  if (int rc = push_wait(c)) return rc;  // the worker's queued launches precede this one on the stream
+  HIPCHK(c, launch_budget(ba, c->budget_blocks, s, ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -351,9 +356,8 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   if (point_step < (xyz_f64 ? 24 : 12)) return fail(c, GCS_ERR_ARG, "point_step too small for x, y, z");
   harvest(c);
   StageEv ev = stage_ev(c, ST_POINTS);
-  const bool hoisted = c->budget_pending;  // k_budget queued earlier by gcs_scan: the stage starts at k_points
-  if (!hoisted)
-    if (int rc = stage_budget(c, w, n_raw, ev.e0)) return rc;
+  if (!c->budget_pending)  // k_budget not queued earlier by gcs_scan
+    if (int rc = stage_budget(c, w, n_raw)) return rc;
   if (int rc = push_wait(c)) return rc;  // k_budget's launch call (worker) precedes k_points on the stream
   c->budget_pending = false;
   const int n_sel = c->last_n_sel, stride = c->last_stride;
@@ -401,8 +405,7 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   const bool scale = c->cfg.mode == GCS_MODE_SCALE;
   c->pts_blocks = points_blocks(c->cap, scale);
   c->pts_fold_pending = scale && fold_later;
-  HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, hoisted ? ev.e0 : nullptr,
-                          ev.e1));
+  HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, ev.e0, ev.e1));
   return GCS_OK;
 }
 
@@ -468,8 +471,9 @@ int stage_bins(gcs_ctx* c) {
       ba.inject_scan_fail = c->inject_scan_fail;
       HIPCHK(c, launch_bucketing(ba, c->cap, s, ev.e0, ev.e1));
     }
-    StageEv ev = stage_ev(c, ST_BINS);
-    HIPCHK(c, launch_bins_scale(b, c->d_bins_part, s, ev.e0, ev.e1, nullptr));  // stage = the bin kernel itself
+    StageEv ev = stage_ev(c, ST_BINS), evf = stage_ev(c, ST_BINS_FOLD);
+    // stage = the bin kernel itself; ST_BINS_FOLD = its partial-row fold (+ R_mf)
+    HIPCHK(c, launch_bins_scale(b, c->d_bins_part, s, ev.e0, ev.e1, evf.e0, evf.e1));
     c->pts_fold_pending = false;
   } else {
     StageEv ev = stage_ev(c, ST_BINS);
@@ -1180,7 +1184,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     gcs_ctx* c;
     ~DirectOff() { c->use_direct = false; }  // per-operator entry points always take the sorted path
   } direct_off{c};
-  if (int rc0 = stage_budget(c, in->weights_dev, in->n_points, nullptr)) return rc0;  // runs during the prologue
+  if (int rc0 = stage_budget(c, in->weights_dev, in->n_points)) return rc0;  // runs during the prologue
   const double* Q = in->Q ? in->Q : c->Q;
   double* cert = out->cert;
   memset(cert, 0, sizeof(out->cert));
@@ -1276,7 +1280,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     c->sorted_sticky = true;
     c->use_direct = false;
     redone = true;
-    if ((rc = stage_budget(c, in->weights_dev, in->n_points, nullptr, /*toggle=*/false))) return rc;
+    if ((rc = stage_budget(c, in->weights_dev, in->n_points, /*toggle=*/false))) return rc;
     if ((rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
                            in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, true,
                            in->xyz_format == 1)))
@@ -1637,6 +1641,13 @@ int gcs_payload_pack(const gcs_belief* b, const double* dPsi, const double* dnu,
   return GCS_OK;
 }
 
+int gcs_datasheet_noise_states(double* nu7, double* Psi252, double* mnu3, double* mPsi27) {
+  if (!nu7 || !Psi252 || !mnu3 || !mPsi27) return GCS_ERR_ARG;
+  host::datasheet_iw_state(nu7, Psi252);
+  host::datasheet_meas_iw_state(mnu3, mPsi27);
+  return GCS_OK;
+}
+
 int gcs_payload_apply(const double* p, int32_t scan_count, const double* X_anchor, double stamp, const double* nu7,
                       const double* Psi, const double* mnu, const double* mPsi, gcs_belief* comb, double* nu_out,
                       double* Psi_out, double* Q_out, double* mnu_out, double* mPsi_out, double* cert4) {
@@ -1674,6 +1685,16 @@ int gcs_rccl_comm_init(int32_t device, int32_t n_ranks, int32_t rank, const uint
 int gcs_rccl_comm_destroy(void* comm) {
   if (!comm) return GCS_OK;
   return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? GCS_OK : GCS_ERR_HIP;
+}
+
+int gcs_rccl_comm_count(void* comm, int32_t* count, int32_t* user_rank) {
+  if (!comm || !count || !user_rank) return GCS_ERR_ARG;
+  int n = 0, r = 0;
+  if (ncclCommCount((ncclComm_t)comm, &n) != ncclSuccess) return GCS_ERR_HIP;
+  if (ncclCommUserRank((ncclComm_t)comm, &r) != ncclSuccess) return GCS_ERR_HIP;
+  *count = n;
+  *user_rank = r;
+  return GCS_OK;
 }
 
 int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, int32_t scan_count,

@@ -157,9 +157,9 @@ int bins_max_tile_sources();  // capacity of its source list
 int bins_max_tile_entries();  // capacity of its reverse-kNN entry list
 int bins_partial_nv();
 int push_blocks(int n_bins);
-// e0/e1 bracket k_bins_scale itself (the roofline kernel), e2 ends its one-block fold
+// e0/e1 bracket k_bins_scale itself (the roofline kernel), f0/f1 its partial-row fold
 hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
-                             hipEvent_t e2);
+                             hipEvent_t f0, hipEvent_t f1);
 hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* partials, hipStream_t s, hipEvent_t e0,
                         hipEvent_t e1);
 hipError_t launch_mf(const double* scan, const double* map, int B, double* partials, int nblk, double* scalars,

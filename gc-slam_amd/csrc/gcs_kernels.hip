@@ -1811,19 +1811,21 @@ __global__ __launch_bounds__(kBlock) void k_fold(const double* __restrict__ part
 
 // Fold nblk partial rows into the scalars (one or two levels).  The level-1 rows are written
 // behind the nblk rows of `partials` (partials_need() reserves them).
+// e0 / e1 (may be null): the first kernel's start / the last kernel's end.
 template <int NV, unsigned MAXMASK, int KIND>
-void launch_fold(const double* partials, int nblk, hipStream_t s, hipEvent_t e1, double* scalars, double* mirror) {
+void launch_fold(const double* partials, int nblk, hipStream_t s, hipEvent_t e1, double* scalars, double* mirror,
+                 hipEvent_t e0 = nullptr) {
   if (nblk > kFoldDirect) {
     double* lvl = (double*)partials + (size_t)nblk * pstride<NV>();
     const int g = (nblk + kFoldRows - 1) / kFoldRows;
-    hipExtLaunchKernelGGL(k_fold<NV, MAXMASK>, dim3(g), dim3(kBlock), 0, s, nullptr, nullptr, 0, partials, nblk, lvl);
+    hipExtLaunchKernelGGL(k_fold<NV, MAXMASK>, dim3(g), dim3(kBlock), 0, s, e0, nullptr, 0, partials, nblk, lvl);
     hipExtLaunchKernelGGL(k_final<NV, MAXMASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0,
                           (const double*)lvl, g, scalars, mirror);
   } else if (kFinalWide != kBlock && nblk > kFinalWideRows) {  // C2 bins: 1563 rows in one or two round trips
-    hipExtLaunchKernelGGL((k_final<NV, MAXMASK, KIND, kFinalWide>), dim3(1), dim3(kFinalWide), 0, s, nullptr, e1, 0,
+    hipExtLaunchKernelGGL((k_final<NV, MAXMASK, KIND, kFinalWide>), dim3(1), dim3(kFinalWide), 0, s, e0, e1, 0,
                           partials, nblk, scalars, mirror);
   } else {
-    hipExtLaunchKernelGGL(k_final<NV, MAXMASK, KIND>, dim3(1), dim3(kBlock), 0, s, nullptr, e1, 0, partials, nblk,
+    hipExtLaunchKernelGGL(k_final<NV, MAXMASK, KIND>, dim3(1), dim3(kBlock), 0, s, e0, e1, 0, partials, nblk,
                           scalars, mirror);
   }
 }
@@ -1873,21 +1875,19 @@ int points_blocks(long cap, bool scale) {
 
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
                          hipEvent_t e0, hipEvent_t e1) {
+  // without the fold (it rides in k_bins_scale's block 0) the stage ends with k_points itself
+  hipEvent_t ek = fold ? nullptr : e1;
   if (scale) {
     switch (a.k) {
-      case 8: hipExtLaunchKernelGGL((k_points<true, 8, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
-      case 16: hipExtLaunchKernelGGL((k_points<true, 16, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
-      case 32: hipExtLaunchKernelGGL((k_points<true, 32, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials); break;
+      case 8: hipExtLaunchKernelGGL((k_points<true, 8, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
+      case 16: hipExtLaunchKernelGGL((k_points<true, 16, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
+      case 32: hipExtLaunchKernelGGL((k_points<true, 32, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
       default: return hipErrorInvalidValue;
     }
   } else {
-    hipExtLaunchKernelGGL((k_points<false, 1, 1>), dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, a, partials);
+    hipExtLaunchKernelGGL((k_points<false, 1, 1>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
   }
-  if (fold) {
-    GCS_FINAL(5, 16u, FIN_POINTS, nblk, s, e1, partials, a.scalars);
-  } else if (e1) {  // the fold rides in k_bins_scale's block 0; close the stage on an empty marker
-    (void)hipEventRecord(e1, s);
-  }
+  if (fold) GCS_FINAL(5, 16u, FIN_POINTS, nblk, s, e1, partials, a.scalars);
   return hipGetLastError();
 }
 
@@ -1917,7 +1917,7 @@ int bins_scale_blocks(int n_bins, int tile_bins) { return (n_bins + tile_bins - 
 int bins_partial_nv() { return kBinNV; }
 
 hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream_t s, hipEvent_t e0, hipEvent_t e1,
-                             hipEvent_t e2) {
+                             hipEvent_t f0, hipEvent_t f1) {
   const int nblk = bins_scale_blocks(a.n_bins, a.tile_bins);
   const bool big = (long)a.cap * 5 >= (long)a.n_bins * 2;  // C2-like: dense in the map
   if (a.tile_bins == 32)  // half the records of a 64-bin tile: the small stage holds them
@@ -1926,7 +1926,7 @@ hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream
     hipExtLaunchKernelGGL((k_bins_scale<kStageBig, 64, 4>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else
     hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 64, 4>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
-  GCS_FINAL(kBinNV, 16u, FIN_BINS, nblk, s, e2, partials, a.scalars);
+  launch_fold<kBinNV, 16u, FIN_BINS>(partials, nblk, s, f1, a.scalars, nullptr, f0);
   return hipGetLastError();
 }
 

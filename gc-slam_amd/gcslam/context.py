@@ -152,7 +152,7 @@ class HypothesisContext:
         P = np.ascontiguousarray(Psi, np.float64).reshape(27)
         self._chk(self.lib.gcs_ctx_set_meas_iw_state(self.h, L.dptr(n), L.dptr(P)), "set_meas_iw_state")
 
-    STAGES = ("points", "sort_bucket", "bins", "matrix_fisher", "planar", "pushforward")
+    STAGES = ("points", "sort_bucket", "bins", "matrix_fisher", "planar", "pushforward", "budget", "bins_fold")
 
     def enable_timing(self, on=True, stages=None):
         """Device stage timing (hipEvents stamped by the stage kernels).  stages: names from
@@ -165,8 +165,8 @@ class HypothesisContext:
         self._chk(self.lib.gcs_ctx_enable_timing(self.h, mask), "enable_timing")
 
     def stage_times(self, reset=False):
-        ms = np.zeros(6)
-        cnt = np.zeros(6, np.int64)
+        ms = np.zeros(len(self.STAGES))
+        cnt = np.zeros(len(self.STAGES), np.int64)
         self._chk(self.lib.gcs_ctx_stage_times(self.h, L.dptr(ms), cnt.ctypes.data_as(L.c_int64_p), int(reset)),
                   "stage_times")
         return ms, cnt

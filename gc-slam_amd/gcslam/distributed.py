@@ -57,6 +57,12 @@ class HypothesisComm:
         self.h = h
         self.rank, self.world = rank, world
 
+    def count(self):
+        """(ranks in the RCCL communicator, this rank's index in it): ncclCommCount / ncclCommUserRank."""
+        n, r = C.c_int32(0), C.c_int32(0)
+        L.check(self.lib.gcs_rccl_comm_count(self.h, C.byref(n), C.byref(r)), None, "gcs_rccl_comm_count")
+        return int(n.value), int(r.value)
+
     def close(self):
         if getattr(self, "h", None):
             self.lib.gcs_rccl_comm_destroy(self.h)

@@ -192,9 +192,13 @@ const char* gcs_last_error(const gcs_ctx* ctx);
 int gcs_ctx_set_stream(gcs_ctx* ctx, void* hip_stream);
 int gcs_ctx_synchronize(gcs_ctx* ctx);
 /* device stage timing: hipEvents stamped by the stages' own kernel dispatches on the context
- * stream.  stage_mask bit s enables stage s (0 = off): [0 budget+points, 1 sort+bucket,
- * 2 bin moment-match kernel (+ fused Matrix-Fisher in scale mode), 3 MF (dense / per-op),
- * 4 planar, 5 pushforward].  Each timed stage costs a few us of queue time. */
+ * stream.  stage_mask bit s enables stage s (0 = off): [0 point kernel (+ its fold when not
+ * deferred), 1 sort+bucket, 2 bin moment-match kernel (+ fused Matrix-Fisher in scale mode),
+ * 3 MF (dense / per-op), 4 planar, 5 pushforward, 6 budget kernel (row 1 mass sums),
+ * 7 the bin kernel's partial-row fold (+ R_mf)].  Stages 6 + 0 + 2 + 7 are the
+ * BinSoftAssign + ScanBinMomentMatch chain (bench.py roofline_chain).  Each timed stage costs a
+ * few us of queue time. */
+#define GCS_N_STAGES 8
 int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
 /* Debug knobs (tests): GCS_DEBUG_SCAN_SPIN_LIMIT bounds k_scan's decoupled look-back spin (default
  * 1 << 22; when it runs out the scan returns GCS_ERR_HIP), GCS_DEBUG_INJECT_SCAN_FAIL != 0 makes
@@ -207,7 +211,8 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
 #define GCS_DEBUG_SORTED_BUCKETS 3
 #define GCS_DEBUG_BUCKET_CAPACITY 4
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
-int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*6*/, int64_t* counts /*6*/, int32_t reset);
+int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*GCS_N_STAGES*/, int64_t* counts /*GCS_N_STAGES*/,
+                        int32_t reset);
 int gcs_ctx_set_atlas(gcs_ctx* ctx, const double* dirs_host /*B*3*/);
 int gcs_ctx_get_atlas(gcs_ctx* ctx, double* dirs_host /*B*3*/, int32_t* knn_host /*B*K*/);
 int gcs_ctx_set_belief(gcs_ctx* ctx, const gcs_belief* b);
@@ -324,6 +329,11 @@ int gcs_ctx_describe(gcs_ctx* ctx, char* buf, int32_t len);
 int gcs_hypothesis_combine(gcs_ctx* ctx, const double* payload_sum, int32_t scan_count, gcs_belief* combined_out,
                            double* cert_out);
 
+/* The node's initial noise states (create_datasheet_process_noise_state,
+ * structures/inverse_wishart_jax.py:42-80; create_datasheet_measurement_noise_state,
+ * structures/measurement_noise_iw_jax.py:37-68): process nu[7], Psi[7*36]; measurement nu[3], Psi[3*9]. */
+int gcs_datasheet_noise_states(double* nu7, double* Psi252, double* mnu3, double* mPsi27);
+
 /* Context-free forms of the same payload (host numerics, no GPU): pack one hypothesis' contribution
  * (any stats pointer may be NULL = zeros) and apply a summed payload to explicit IW states. */
 int gcs_payload_pack(const gcs_belief* b, const double* dPsi252, const double* dnu7, const double* meas_dPsi27,
@@ -344,6 +354,9 @@ int gcs_payload_apply(const double* payload_sum, int32_t scan_count, const doubl
 int gcs_rccl_get_unique_id(uint8_t* id /*GCS_RCCL_ID_BYTES*/);
 int gcs_rccl_comm_init(int32_t device, int32_t n_ranks, int32_t rank, const uint8_t* id, void** comm);
 int gcs_rccl_comm_destroy(void* comm);
+/* Ranks the communicator holds (ncclCommCount) and this rank's index in it (ncclCommUserRank):
+ * bench.py reports them so a multi-GPU line shows RCCL saw every rank. */
+int gcs_rccl_comm_count(void* comm, int32_t* count, int32_t* user_rank);
 int gcs_combine_allreduce(gcs_ctx* ctx, void* comm, double w_iw, double w_bary, int32_t scan_count,
                           gcs_belief* combined_out /*may be NULL*/, double* cert4 /*may be NULL*/);
 

@@ -1,0 +1,81 @@
+#!/bin/bash
+# One entry point for the GPU-box steps (run through gpurun from the repo root):
+#   bash tools/gpu.sh STEP [STEP ...]
+# Steps (each under its own time limit, stopping at the first failure; outputs under $O):
+#   tests        pytest -m gpu (the parity suite)          smoke      __graft_entry__.smoke()
+#   bench        bench.py C2 headline line (+ C3 roofline + CPU baseline)
+#   bench3       bench.py --config c3
+#   prof2/prof3  rocprofv3 --kernel-trace --stats of bench at C2 / C3
+#   pmc          FETCH_SIZE / WRITE_SIZE passes (one counter per run) at C2 and C3 (PMC_CONFIGS)
+#   sq           SQ instruction-mix / wave-state passes of the hot kernels
+#   phase        per-phase clocks of the bin kernel (needs `make -C gc-slam_amd prof`)
+#   pmap         primitive-map timing (tools/pmap_bench.py)    assoc   association timing
+#   ab           same-box A/B of two builds: A = libgcslam_hip.so, B = libgcslam_hip_$B.so
+#   envab        same-box A/B of an environment knob: B runs with $ENVB
+# Env: O (output dir, default gpurun_out/run), REPS (A/B alternations), PYTEST_K (pytest -k filter).
+cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
+export TMPDIR=/tmp
+O=${O:-gpurun_out/run}
+mkdir -p "$O"
+RE='k_bins_scale|k_points|k_budget|k_pt|k_pushforward|k_final|k_fold'
+
+step() {
+  case "$1" in
+    tests)
+      local k=(); [ -n "$PYTEST_K" ] && k=(-k "$PYTEST_K")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 120 --timeout-method thread "${k[@]}" \
+        > "$O/pytest_gpu.log" 2>&1 ;;
+    smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    bench) timeout -k 10 400 python bench.py > "$O/bench_c2.log" 2>&1 ;;
+    bench3) timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline \
+              > "$O/bench_c3.log" 2>&1 ;;
+    prof2) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c2" -o run --output-format csv -- \
+             python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-c3 > "$O/prof_c2.log" 2>&1 ;;
+    prof3) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c3" -o run --output-format csv -- \
+             python3 bench.py --config c3 --steps 30 --warmup 5 --no-cpu-baseline > "$O/prof_c3.log" 2>&1 ;;
+    pmc)
+      for cfg in ${PMC_CONFIGS:-c2 c3}; do
+        for ctr in FETCH_SIZE WRITE_SIZE; do
+          timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "$RE" -d "$O/pmc/${cfg}_$ctr" -o run \
+            --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline --no-c3 \
+            > "$O/pmc_${cfg}_$ctr.log" 2>&1 || return $?
+        done
+      done ;;
+    sq)
+      for cfg in c2 c3; do
+        timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES \
+          SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY --kernel-include-regex "$RE" -d "$O/sq/${cfg}" -o run \
+          --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline --no-c3 \
+          > "$O/sq_$cfg.log" 2>&1 || return $?
+      done ;;
+    phase) for cfg in c2 c3; do timeout -k 10 180 python tools/phase_prof.py $cfg > "$O/phase_$cfg.txt" 2>&1 || return $?; done ;;
+    pmap) timeout -k 10 300 python tools/pmap_bench.py 30 > "$O/pmap_bench.txt" 2>&1 ;;
+    assoc) timeout -k 10 300 python tools/assoc_bench.py > "$O/assoc_bench.txt" 2>&1 ;;
+    ab)
+      for rep in $(seq 1 "${REPS:-2}"); do
+        for v in A B; do
+          lib=gc-slam_amd/gcslam/libgcslam_hip.so; [ $v = B ] && lib=gc-slam_amd/gcslam/libgcslam_hip_${B:-prev}.so
+          GCSLAM_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-c3 \
+            > "$O/ab_${v}_c2_$rep.log" 2>&1 || return $?
+          GCSLAM_LIB=$PWD/$lib timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline \
+            > "$O/ab_${v}_c3_$rep.log" 2>&1 || return $?
+        done
+      done ;;
+    envab)
+      for rep in $(seq 1 "${REPS:-2}"); do
+        for v in A B; do
+          e=""; [ $v = B ] && e="$ENVB"
+          env $e timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-c3 \
+            > "$O/envab_${v}_c2_$rep.log" 2>&1 || return $?
+          env $e timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline \
+            > "$O/envab_${v}_c3_$rep.log" 2>&1 || return $?
+        done
+      done ;;
+    *) echo "unknown step $1" >&2; return 2 ;;
+  esac
+}
+
+for s in "$@"; do
+  echo "[gpu.sh] $s $(date +%T)"
+  step "$s" || { rc=$?; echo "[gpu.sh] step $s failed rc=$rc"; exit $rc; }
+done
