@@ -32,6 +32,26 @@ enum { ST_POINTS = 0, ST_SORT = 1, ST_BINS = 2, ST_MF = 3, ST_PT = 4, ST_PUSH = 
        kStages = 8 };
 static_assert(kStages == GCS_N_STAGES, "stage count of the C-ABI");
 
+namespace {
+using clk = std::chrono::steady_clock;
+double ms_between(clk::time_point a, clk::time_point b) {
+  return std::chrono::duration<double, std::milli>(b - a).count();
+}
+}  // namespace
+
+struct gcs_scan_state {
+  Belief prev, pred;
+  double mu_prev[DZ], mu_inc[DZ], pose0[6], pose_pred[6], xi[6];
+  double sigma_warp = 0.0;
+  host::PreintOut pre;
+  bool use_io = false;
+  double io_extra[5] = {0, 0, 0, 0, 0};
+  double Tsum = 0.0;
+  double cert[GCS_CERT_LEN] = {};
+  double Lext[DZ * DZ] = {}, hext[DZ] = {};
+  clk::time_point T0, Tp, T1, Ts, T2;
+};
+
 struct gcs_ctx {
   gcs_config cfg{};
   int B = 0, cap = 0, K = 0, G = 0, pool_width = 0, ncell = 0, max_raw = 0;
@@ -57,6 +77,14 @@ struct gcs_ctx {
   int tile_shift = 6;
   // per-point
   PointRec* d_recs = nullptr;
+  double* d_iz = nullptr;  // 1 / Z per point, written by the per-operator point stage (gcs_bin_soft_assign)
+  bool iz_valid = false;
+  // live primitive path (gcs_scan_begin / gcs_scan_finish): deskewed points (cap x 3), weights and
+  // budget timestamps on the device, the prologue's state carried to the tail
+  double *d_live_p0 = nullptr, *d_live_w = nullptr, *d_live_t = nullptr;
+  gcs_scan_state* scan_st = nullptr;
+  gcs_scan_outputs* live_out = nullptr;
+  bool live_pending = false;
   uint32_t *d_keys = nullptr, *d_slots = nullptr, *d_sorted = nullptr;
   int* d_nearest = nullptr;
   // per-bin bucketing
@@ -157,8 +185,13 @@ struct gcs_ctx {
 
 namespace {
 
+// Without a context (the push worker's calls) the message goes to this thread's slot, so the
+// worker reports the failing call's own error text rather than a later hipGetLastError().
+thread_local std::string t_fail_msg;
+
 int fail(gcs_ctx* c, int code, const std::string& m) {
   if (c) c->err = m;
+  else t_fail_msg = m;
   return code;
 }
 
@@ -290,10 +323,10 @@ int upload_atlas(gcs_ctx* c) {
     std::vector<int> src_off, src;
     std::vector<uint16_t> local;
     c->max_tile_src = atlas::tile_sources(off, idx, B, c->tile_bins, src_off, src, local);
-    if (c->max_tile_src > bins_max_tile_sources())
+    if (c->max_tile_src > bins_max_tile_sources(c->tile_bins))
       return fail(c, GCS_ERR_ARG, "bin atlas too irregular for the tiled bin kernel (tile source list too long)");
     for (int b0 = 0; b0 < B; b0 += c->tile_bins)
-      if (off[std::min(B, b0 + c->tile_bins)] - off[b0] > bins_max_tile_entries())
+      if (off[std::min(B, b0 + c->tile_bins)] - off[b0] > bins_max_tile_entries(c->tile_bins))
         return fail(c, GCS_ERR_ARG, "bin atlas too irregular for the tiled bin kernel (tile reverse-kNN list too long)");
     c->G = atlas::grid_for_bins(B);
     c->ncell = 6 * c->G * c->G;
@@ -349,9 +382,11 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true) {
   return GCS_OK;
 }
 
+// deskew_only: the live primitive path's point stage (gcs_scan_begin): budget gather + deskew into
+// p0_out / w_out / t_out, no soft assign
 int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, const double* w, int n_raw, double t0,
                  double t1, const double* xi, double* p0_out, double* w_out, double* wb_out, bool fold_later = false,
-                 bool xyz_f64 = false) {
+                 bool xyz_f64 = false, double* iz_out = nullptr, bool deskew_only = false, double* t_out = nullptr) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
   if (point_step < (xyz_f64 ? 24 : 12)) return fail(c, GCS_ERR_ARG, "point_step too small for x, y, z");
   harvest(c);
@@ -402,7 +437,15 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.w_out = w_out;
   a.w_budget_out = wb_out;
   a.nearest_out = c->d_nearest;  // device ids
-  const bool scale = c->cfg.mode == GCS_MODE_SCALE;
+  a.iz_out = iz_out;
+  a.t_out = t_out;
+  c->iz_valid = false;
+  const bool scale = c->cfg.mode == GCS_MODE_SCALE && !deskew_only;
+  if (deskew_only) {
+    a.n_bins = 0;  // k_points<false, 0, 1>: no soft assign, no record, no bucketing
+    a.nearest_out = nullptr;
+    a.members = nullptr;
+  }
   c->pts_blocks = points_blocks(c->cap, scale);
   c->pts_fold_pending = scale && fold_later;
   HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, ev.e0, ev.e1));
@@ -563,7 +606,7 @@ void push_worker(gcs_ctx* c) {
       }
     } else {
       rc = stage_push(c, j.z_t, j.Sig6, j.gamma, j.s, j.partials, j.flags, true);
-      if (rc) c->push_err = "pushforward launch (worker): " + std::string(hipGetErrorString(hipGetLastError()));
+      if (rc) c->push_err = "pushforward launch (worker): " + t_fail_msg;
     }
     c->push_rc = rc;
     c->push_done.store(r, std::memory_order_release);
@@ -711,11 +754,13 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     return GCS_ERR_ARG;
   if (!(cfg->tau > 0.0)) return GCS_ERR_ARG;
   gcs_ctx* c = new gcs_ctx();
+  c->scan_st = new gcs_scan_state();
+  c->live_out = new gcs_scan_outputs();
   c->cfg = *cfg;
   c->B = cfg->n_bins;
   c->cap = cfg->n_points_cap;
   c->tile_bins = bins_tile_for(c->cap, c->B);
-  c->tile_shift = c->tile_bins == 32 ? 5 : 6;
+  c->tile_shift = __builtin_ctz((unsigned)c->tile_bins);
   c->K = cfg->mode == GCS_MODE_SCALE ? cfg->k_cand : 0;
   c->max_raw = cfg->max_raw_points;
   for (int k = 0; k < 3; ++k) c->grav[k] = cfg->gravity_W[k] * cfg->imu_gravity_scale;
@@ -737,6 +782,10 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   const size_t B = c->B, cap = c->cap;
   if (bad(hipMalloc(&c->d_bin_dirs, B * 4 * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_recs, cap * sizeof(PointRec)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_iz, cap * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_live_p0, 3 * cap * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_live_w, cap * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_live_t, cap * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_nearest, cap * sizeof(int)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scan, B * SF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_map, B * MF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
@@ -824,7 +873,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   }
   if (c->push_stream) (void)hipStreamSynchronize(c->push_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_keys, c->d_slots,
+  void* ptrs[] = {c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_bins_part, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,
@@ -841,6 +890,8 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (c->ev_push) (void)hipEventDestroy(c->ev_push);
   if (c->push_stream) (void)hipStreamDestroy(c->push_stream);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
+  delete c->scan_st;
+  delete c->live_out;
   delete c;
   return GCS_OK;
 }
@@ -1060,8 +1111,10 @@ int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const doubl
   if (!c || !xi) return GCS_ERR_ARG;
   if (int rc_ = join_push(c)) return rc_;
   c->budget_pending = false;  // a k_budget queued by a gcs_scan that failed later is stale
-  int rc = stage_points(c, xyz, point_step, t, w, n, t0, t1, xi, p0_dev, w_out_dev, w_budget_dev);
+  int rc = stage_points(c, xyz, point_step, t, w, n, t0, t1, xi, p0_dev, w_out_dev, w_budget_dev, false, false,
+                        c->d_iz);
   if (rc) return rc;
+  c->iz_valid = true;
   if (nearest_dev) {  // reported in reference bin ids
     hipLaunchKernelGGL(k_ref_ids, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, (const int*)c->d_nearest,
                        (const int*)c->d_bin_ref, c->cap, nearest_dev);
@@ -1074,12 +1127,13 @@ int gcs_point_stage(gcs_ctx* c, const void* xyz, int32_t point_step, const doubl
 }
 
 namespace {
-__global__ void k_materialize(const PointRec* recs, const int* nearest, const int* knn, const double* bin_dirs,
-                              const int* bin_ref, int cap, int B, int K, bool scale, double ox, double oy, double oz,
-                              double tau, int* ids, double* r) {
+__global__ void k_materialize(const PointRec* recs, const double* iz, const int* nearest, const int* knn,
+                              const double* bin_dirs, const int* bin_ref, int cap, int B, int K, bool scale, double ox,
+                              double oy, double oz, double tau, int* ids, double* r) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
   PointRec pr = recs[i];
+  const double izi = iz[i];
   double d0 = pr.dx, d1 = pr.dy, d2 = pr.dz;
   double it = 1.0 / tau;
   if (scale) {
@@ -1088,13 +1142,13 @@ __global__ void k_materialize(const PointRec* recs, const int* nearest, const in
       const double* bd = bin_dirs + 4 * (size_t)row[k];
       double s = dot3_exact(d0, d1, d2, bd[0], bd[1], bd[2]);
       if (ids) ids[(size_t)i * K + k] = bin_ref[row[k]];
-      if (r) r[(size_t)i * K + k] = exp((s - pr.m) * it) * pr.iz;
+      if (r) r[(size_t)i * K + k] = exp((s - pr.m) * it) * izi;
     }
   } else {
     for (int b = 0; b < B; ++b) {
       const double* bd = bin_dirs + 4 * (size_t)b;
       double s = dot3_exact(d0, d1, d2, bd[0], bd[1], bd[2]);
-      if (r) r[(size_t)i * B + b] = exp((s - pr.m) * it) * pr.iz;
+      if (r) r[(size_t)i * B + b] = exp((s - pr.m) * it) * izi;
     }
   }
 }
@@ -1103,9 +1157,10 @@ __global__ void k_materialize(const PointRec* recs, const int* nearest, const in
 int gcs_bin_soft_assign(gcs_ctx* c, int32_t* ids, double* r) {
   if (!c) return GCS_ERR_ARG;
   if (int rc_ = join_push(c)) return rc_;
+  if (!c->iz_valid) return fail(c, GCS_ERR_STATE, "gcs_bin_soft_assign needs gcs_point_stage first");
   bool scale = c->cfg.mode == GCS_MODE_SCALE;
   hipLaunchKernelGGL(k_materialize, dim3((c->cap + 255) / 256), dim3(256), 0, c->stream, (const PointRec*)c->d_recs,
-                     (const int*)c->d_nearest, (const int*)c->d_knn, (const double*)c->d_bin_dirs,
+                     (const double*)c->d_iz, (const int*)c->d_nearest, (const int*)c->d_knn, (const double*)c->d_bin_dirs,
                      (const int*)c->d_bin_ref, c->cap, c->B, c->K,
                      scale, c->cfg.lidar_origin[0], c->cfg.lidar_origin[1], c->cfg.lidar_origin[2], c->cfg.tau, ids, r);
   HIPCHK(c, hipGetLastError());
@@ -1172,80 +1227,79 @@ int gcs_pushforward(gcs_ctx* c, const double* z_t, const double* Sig6, double ga
 }
 
 // ---------------------------------------------------------------- the per-scan pipeline
-int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
-  using clk = std::chrono::steady_clock;
-  if (!c || !in || !out) return fail(c, GCS_ERR_ARG, "null argument");
-  if (in->imu_len < 1 || !in->imu_stamps || !in->imu_gyro || !in->imu_accel) return fail(c, GCS_ERR_ARG, "IMU window required");
-  auto T0 = clk::now();
+// gcs_scan runs the whole bin-path scan in one call.  gcs_scan_begin / gcs_scan_finish split the
+// same steps around the caller's LiDAR evidence for the live primitive path (pipeline.py:778-1011:
+// surfels, recency, view, association and visual pose evidence run between them on the device
+// through their own entry points).  The pieces below are shared, so both forms run one code path.
+
+namespace {
+
+// LiDAR evidence of step 9 and its certificate terms: the bin path's MF + planar blocks, or the live
+// path's visual pose evidence (the caller's gcs_lidar_evidence)
+struct LidarTerms {
+  double L[DZ * DZ] = {}, h[DZ] = {};
+  double ev_ess = 0.0;  // support.ess_total of aggregate(LiDAR certs)
+  double ev_nll = 0.0;  // mismatch.nll_per_ess of aggregate(LiDAR certs)
+};
+
+// 1 (launch), 2 PredictDiffusion, 3 IMU membership window + preintegration -> deskew twist
+// (pipeline.py:399-483)
+int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st) {
+  st.T0 = clk::now();
   c->budget_pending = false;
-  // direct buckets for this call's stages (scale mode, unless a bucket overflowed before)
-  c->use_direct = c->cfg.mode == GCS_MODE_SCALE && c->direct_buckets && !c->sorted_sticky && c->d_members;
-  struct DirectOff {
-    gcs_ctx* c;
-    ~DirectOff() { c->use_direct = false; }  // per-operator entry points always take the sorted path
-  } direct_off{c};
   if (int rc0 = stage_budget(c, in->weights_dev, in->n_points)) return rc0;  // runs during the prologue
   const double* Q = in->Q ? in->Q : c->Q;
-  double* cert = out->cert;
-  memset(cert, 0, sizeof(out->cert));
-  double Tsum = 0.0;
+  double* cert = st.cert;
+  memset(cert, 0, sizeof(st.cert));
+  st.Tsum = 0.0;
+  if (in->L_ext) memcpy(st.Lext, in->L_ext, sizeof(st.Lext)); else memset(st.Lext, 0, sizeof(st.Lext));
+  if (in->h_ext) memcpy(st.hext, in->h_ext, sizeof(st.hext)); else memset(st.hext, 0, sizeof(st.hext));
   // 2 PredictDiffusion
-  Belief prev = c->belief, pred;
-  double pinfl[3], mu_prev[DZ];
-  host::predict_diffusion(prev, Q, in->dt_sec, pred, pinfl, mu_prev);
+  st.prev = c->belief;
+  double pinfl[3];
+  host::predict_diffusion(st.prev, Q, in->dt_sec, st.pred, pinfl, st.mu_prev);
   cert[6] = pinfl[0]; cert[7] = pinfl[1]; cert[8] = pinfl[2];
-  Tsum += trig(pinfl[0], pinfl[1], 0, 0, 0, pinfl[2], 1, 1, 1);
-  auto Tp = clk::now();
+  st.Tsum += trig(pinfl[0], pinfl[1], 0, 0, 0, pinfl[2], 1, 1, 1);
+  st.Tp = clk::now();
   // 3 IMU membership window + preintegration -> deskew twist (pipeline.py:432-483)
   host::SpdFactor fpred;  // one factor of the predicted information for every solve below
-  host::spd_factor_lifted(DZ, pred.L, kEpsLift, fpred);
+  host::spd_factor_lifted(DZ, st.pred.L, kEpsLift, fpred);
   double e15[DZ] = {}, col15[DZ];
   e15[15] = 1.0;
   host::spd_factor_solve(fpred, e15, col15);  // column 15 of the predicted covariance
-  double sigma_warp = std::max(sqrt(col15[15]), 0.01);
-  cert[38] = sigma_warp;
+  st.sigma_warp = std::max(sqrt(col15[15]), 0.01);
+  cert[38] = st.sigma_warp;
   std::vector<double>& wimu = c->wimu;
   wimu.resize(in->imu_len);
   for (int i = 0; i < in->imu_len; ++i)
-    wimu[i] = smooth_window(in->imu_stamps[i], in->scan_start_time, in->scan_end_time, sigma_warp);
-  double mu_inc[DZ], pose0[6];
-  host::spd_factor_solve(fpred, pred.h, mu_inc);
-  host::world_pose_from_increment(prev, mu_prev, pose0);
-  host::PreintOut pre;
-  host::preintegrate_imu(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wimu.data(), pose0 + 3, mu_inc + 9,
-                         mu_inc + 12, c->grav, pre);
-  double xi[6];
-  host::se3_log(pre.delta_pose, xi);
-  if (c->cfg.deskew_rotation_only) xi[0] = xi[1] = xi[2] = 0.0;
-  cert[10] = pre.ess;
-  auto T1 = clk::now();
-  // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
-  int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
-                        in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, /*fold_later=*/true,
-                        in->xyz_format == 1);
-  if (rc) return rc;
-  if (int rc_ = join_push(c)) return rc_;  // the bin kernel reads the map the previous scan's pushforward wrote
-  if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
-  if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
-  if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
-  auto Ts = clk::now();
-  // 13 measurement-noise IW statistics over the scan-to-scan IMU window (pipeline.py:448-453,
-  // 522-566), computed while the device stages run (they need no device result); padded samples
-  // (stamp <= 0) carry weight 0 (the reference's valid mask)
-  // w_imu_int unmasked as in the reference (padding gets the 1e-12 floor); the IW statistics mask
-  // stamps <= 0 themselves
+    wimu[i] = smooth_window(in->imu_stamps[i], in->scan_start_time, in->scan_end_time, st.sigma_warp);
+  host::spd_factor_solve(fpred, st.pred.h, st.mu_inc);
+  host::world_pose_from_increment(st.prev, st.mu_prev, st.pose0);
+  host::preintegrate_imu(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wimu.data(), st.pose0 + 3,
+                         st.mu_inc + 9, st.mu_inc + 12, c->grav, st.pre);
+  host::se3_log(st.pre.delta_pose, st.xi);
+  if (c->cfg.deskew_rotation_only) st.xi[0] = st.xi[1] = st.xi[2] = 0.0;
+  cert[10] = st.pre.ess;
+  st.T1 = clk::now();
+  return GCS_OK;
+}
+
+// 13 measurement-noise IW statistics over the scan-to-scan IMU window (pipeline.py:448-453, 522-566)
+// and 9 the IMU/odometry evidence branch (pipeline.py:595-776), computed while the device stages
+// run (they need no device result); padded samples (stamp <= 0) carry weight 0 (the reference's
+// valid mask).  w_imu_int unmasked as in the reference (padding gets the 1e-12 floor); the IW
+// statistics mask stamps <= 0 themselves.
+int scan_imu_odom(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st, gcs_scan_outputs* out) {
   std::vector<double>& wint = c->wint;
   wint.resize(in->imu_len);
   for (int i = 0; i < in->imu_len; ++i)
-    wint[i] = smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, sigma_warp);
-  host::imu_meas_iw_suffstats(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wint.data(), mu_inc + 9,
-                              mu_inc + 12, pose0 + 3, c->grav, out->iw_meas_dPsi, out->iw_meas_dnu);
-  // 9 (pipeline.py:595-776) IMU/odometry evidence, also while the device stages run
-  double pose_pred[6];
-  host::world_pose_from_increment(pred, mu_inc, pose_pred);
-  const bool use_io = c->cfg.use_imu_odom != 0;
-  double io_extra[5] = {0, 0, 0, 0, 0};
-  if (use_io) {
+    wint[i] = smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, st.sigma_warp);
+  host::imu_meas_iw_suffstats(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wint.data(), st.mu_inc + 9,
+                              st.mu_inc + 12, st.pose0 + 3, c->grav, out->iw_meas_dPsi, out->iw_meas_dnu);
+  host::world_pose_from_increment(st.pred, st.mu_inc, st.pose_pred);
+  st.use_io = c->cfg.use_imu_odom != 0;
+  memset(st.io_extra, 0, sizeof(st.io_extra));
+  if (st.use_io) {
     if (in->imu_len < 2) return fail(c, GCS_ERR_ARG, "IMU window of at least 2 samples required");
     double Sg[9], Sa[9];
     if (in->Sigma_g) memcpy(Sg, in->Sigma_g, sizeof(Sg)); else host::meas_iw_mode(c->meas_nu, c->meas_Psi, 0, Sg);
@@ -1254,7 +1308,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     ii.m = in->imu_len;
     ii.stamps = in->imu_stamps; ii.gyro = in->imu_gyro; ii.accel = in->imu_accel; ii.w_int = wint.data();
     ii.t_last_scan = in->t_last_scan; ii.t_scan = in->t_scan; ii.dt_sec = in->dt_sec;
-    ii.pose0 = pose0; ii.pose_pred = pose_pred; ii.mu_prev = mu_prev; ii.mu_inc = mu_inc;
+    ii.pose0 = st.pose0; ii.pose_pred = st.pose_pred; ii.mu_prev = st.mu_prev; ii.mu_inc = st.mu_inc;
     ii.gravity_W = c->grav;
     ii.Sigma_g = Sg; ii.Sigma_a = Sa;
     ii.odom_pose = in->odom_pose ? in->odom_pose : kZero6;
@@ -1263,42 +1317,24 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     ii.odom_twist_cov = in->odom_twist_cov ? in->odom_twist_cov : kBigCov6.v;
     ii.planar_z_ref = c->cfg.planar_z_ref; ii.planar_z_sigma = c->cfg.planar_z_sigma;
     ii.planar_vz_sigma = c->cfg.planar_vz_sigma;
-    run_imu_odom(ii, c->io, io_extra);
+    run_imu_odom(ii, c->io, st.io_extra);
     for (int k = 0; k < DZ * DZ; ++k)
       if (!std::isfinite(c->io.L[k])) return fail(c, GCS_ERR_NONFINITE, "IMU/odometry evidence contains NaN");
   } else {
     memset(c->io.L, 0, sizeof(c->io.L));
     memset(c->io.h, 0, sizeof(c->io.h));
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // the PT fold has written the scalars to h_scalars
-  if ((rc = check_bucket_err(c))) return rc;
-  bool redone = false;
-  if (c->use_direct && c->h_err[2]) {
-    // a bucket exceeded the direct rows: redo the device stages with the sorted bucketing (same
-    // flags buffer: the previous scan's pushforward may still read the other), and keep it
-    c->h_err[2] = 0u;
-    c->sorted_sticky = true;
-    c->use_direct = false;
-    redone = true;
-    if ((rc = stage_budget(c, in->weights_dev, in->n_points, /*toggle=*/false))) return rc;
-    if ((rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
-                           in->scan_start_time, in->scan_end_time, xi, nullptr, nullptr, nullptr, true,
-                           in->xyz_format == 1)))
-      return rc;
-    if ((rc = stage_bins(c))) return rc;
-    if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    if ((rc = check_bucket_err(c))) return rc;
-  }
-  cert[41] = c->h_err[1] ? 1.0 : 0.0;  // a bucket above the ranking capacity took the compaction path
-  c->h_err[1] = 0u;
   for (int k = 0; k < 27; ++k)
     if (!std::isfinite(out->iw_meas_dPsi[k])) return fail(c, GCS_ERR_NONFINITE, "omega_avg / IMU residuals non-finite");
   memcpy(c->last_meas_dPsi, out->iw_meas_dPsi, sizeof(c->last_meas_dPsi));
   memcpy(c->last_meas_dnu, out->iw_meas_dnu, sizeof(c->last_meas_dnu));
-  auto T2 = clk::now();
+  return GCS_OK;
+}
+
+// budget (point_budget.py:182-212) and deskew certificates from the point stage's scalars
+int scan_point_certs(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st) {
   const double* S = c->h_scalars;
-  // budget cert (point_budget.py:182-212)
+  double* cert = st.cert;
   double mass_in = S[SC_MASS_IN];
   double budget_ess = 1.0 / (S[SC_BUDGET_W2] + (double)c->cap * kEpsMass);
   double budget_mer = kEpsMass / (mass_in + kEpsMass);
@@ -1308,25 +1344,30 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   cert[3] = mass_in;
   cert[4] = c->last_n_sel;
   cert[5] = c->last_stride;
-  Tsum += budget_mer;
+  st.Tsum += budget_mer;
   if (!std::isfinite(mass_in)) return fail(c, GCS_ERR_NONFINITE, "non-finite point weights");
-  // deskew cert
   cert[9] = S[SC_DESKEW_WOUT] / (S[SC_DESKEW_WIN] + kEpsMass);
-  // soft assign cert (binning.py:71-75,118-125)
+  return GCS_OK;
+}
+
+// soft assign, moment match, 7 MatrixFisherRotation and 8 PlanarTranslationEvidence tails
+// (binning.py:71-75,118-125,193-196; matrix_fisher_evidence.py:240-256,310-394,565-671) and the
+// combined 22-D LiDAR evidence (build_combined_lidar_evidence_22d, :729-756)
+void scan_bin_lidar(gcs_ctx* c, gcs_scan_state& st, LidarTerms& lt, gcs_scan_outputs* out) {
+  const double* S = c->h_scalars;
+  double* cert = st.cert;
   double avg_ent = S[SC_ENTROPY] / ((double)c->cap + kEpsMass);
   cert[11] = avg_ent;
   cert[12] = exp(avg_ent);
   cert[13] = S[SC_MAXRESP];
-  // moment match cert (binning.py:193-196)
   double mm_ess = S[SC_BIN_NSUM] * S[SC_BIN_NSUM] / (S[SC_BIN_N2SUM] + kEpsMass);
   cert[14] = mm_ess;
   cert[15] = S[SC_BIN_SUPP] / (double)c->B;
   cert[16] = S[SC_BIN_PSD];
   cert[17] = S[SC_BIN_EPSR];
-  Tsum += S[SC_BIN_PSD] + S[SC_BIN_EPSR];
-  // 7 MatrixFisherRotation tail (matrix_fisher_evidence.py:240-256,310-394)
+  st.Tsum += S[SC_BIN_PSD] + S[SC_BIN_EPSR];
   double R_pred[9];
-  so3_exp(pose_pred + 3, R_pred);
+  so3_exp(st.pose_pred + 3, R_pred);
   double Umf[9], sv[3], V[9];
   svd3(S + SC_MF_H, Umf, sv, V);  // L_rot needs s and V (host, same 3x3 SVD code as the device)
   const double* Rmf = S + SC_MF_R;
@@ -1346,8 +1387,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   cert[18] = mf_delta; cert[19] = mf_mer; cert[20] = mf_neff;
   cert[21] = sv[0]; cert[22] = sv[1]; cert[23] = sv[2];
   cert[24] = 0.5 * (drot[0] * hrot[0] + drot[1] * hrot[1] + drot[2] * hrot[2]);
-  Tsum += mf_delta + mf_mer;
-  // 8 PlanarTranslationEvidence tail (matrix_fisher_evidence.py:565-671)
+  st.Tsum += mf_delta + mf_mer;
   double Tmap[9], ev[3], Vt[9];
   double nd = S[SC_MF_MAPND] + kEpsMass;
   for (int k = 0; k < 9; ++k) Tmap[k] = S[SC_MF_MAPSCAT + k] / nd;
@@ -1369,41 +1409,56 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) Ltr_raw[3 * i + j] = Lf[3 * i + j] * mask[i] * mask[j];
   double pt_delta = host::psd_project(3, Ltr_raw, kEpsPsd, Ltr);
-  double dtr[3] = {twls[0] - pose_pred[0], twls[1] - pose_pred[1], twls[2] - pose_pred[2]};
+  double dtr[3] = {twls[0] - st.pose_pred[0], twls[1] - st.pose_pred[1], twls[2] - st.pose_pred[2]};
   double htr[3];
   for (int i = 0; i < 3; ++i) htr[i] = Ltr[3 * i] * dtr[0] + Ltr[3 * i + 1] * dtr[1] + Ltr[3 * i + 2] * dtr[2];
   double pt_neff = S[SC_PT_NEFF];
   double pt_mer = kEpsMass / (pt_neff + kEpsMass);
   cert[25] = pt_delta; cert[26] = pt_mer; cert[27] = pt_neff; cert[28] = zs;
   cert[29] = 0.5 * (dtr[0] * htr[0] + dtr[1] * htr[1] + dtr[2] * htr[2]);
-  Tsum += pt_delta + pt_mer;
+  st.Tsum += pt_delta + pt_mer;
   memcpy(out->R_mf, Rmf, sizeof(out->R_mf));
   memcpy(out->t_wls, twls, sizeof(out->t_wls));
-  // 9 evidence (build_combined_lidar_evidence_22d) + external + power tempering (pipeline.py:1038-1117)
+  memset(lt.L, 0, sizeof(lt.L));
+  memset(lt.h, 0, sizeof(lt.h));
+  for (int i = 0; i < 3; ++i) {
+    lt.h[i] = htr[i];
+    lt.h[3 + i] = hrot[i];
+    for (int j = 0; j < 3; ++j) {
+      lt.L[i * DZ + j] = Ltr[3 * i + j];
+      lt.L[(3 + i) * DZ + 3 + j] = Lrot[3 * i + j];
+    }
+  }
+  // aggregate of the LiDAR certs [deskew, soft assign, moment match, MF, planar] (pipeline.py:1057)
+  lt.ev_ess = (st.pre.ess + cert[12] + mm_ess + 0.0 + 0.0) / 5.0;
+  lt.ev_nll = cert[24] / (mf_neff + kEpsMass) + cert[29] / (pt_neff + kEpsMass);
+}
+
+// 9 evidence sum + power tempering + excitation scaling, 10 FusionScaleFromCertificates, 11
+// InfoFusionAdditive, 12 PoseUpdateFrobeniusRecompose, process IW statistics, 13 the bin map's
+// PoseCovInflationPushforward (push: the bin path; the live path's map update is the caller's step
+// 12b), 14 AnchorDriftUpdate (pipeline.py:1038-1230, 1494-1502)
+int scan_tail(gcs_ctx* c, gcs_scan_state& st, const LidarTerms& lt, gcs_scan_outputs* out, bool push) {
+  double* cert = st.cert;
+  Belief& pred = st.pred;
   double Lraw[DZ * DZ], hraw[DZ];
-  for (int i = 0; i < DZ * DZ; ++i) Lraw[i] = (in->L_ext ? in->L_ext[i] : 0.0) + c->io.L[i];
-  for (int i = 0; i < DZ; ++i) hraw[i] = (in->h_ext ? in->h_ext[i] : 0.0) + c->io.h[i];
+  for (int i = 0; i < DZ * DZ; ++i) Lraw[i] = st.Lext[i] + c->io.L[i];
+  for (int i = 0; i < DZ; ++i) hraw[i] = st.hext[i] + c->io.h[i];
   memcpy(out->L_imu_odom, c->io.L, sizeof(out->L_imu_odom));
   {
     const host::EvCert* cs[11] = {&c->io.odom, &c->io.imu, &c->io.dep, &c->io.gyro, &c->io.preint, &c->io.planar,
                                   &c->io.vz, &c->io.vel, &c->io.wz, &c->io.kin, &c->io.odom_dep};
     for (int k = 0; k < 11; ++k) {
       double* o = out->imu_odom_certs + 7 * k;
-      if (!use_io) { for (int j = 0; j < 7; ++j) o[j] = 0.0; continue; }
+      if (!st.use_io) { for (int j = 0; j < 7; ++j) o[j] = 0.0; continue; }
       o[0] = cs[k]->ess; o[1] = cs[k]->support; o[2] = cs[k]->nll; o[3] = cs[k]->lift; o[4] = cs[k]->psd;
       o[5] = cs[k]->mer; o[6] = cs[k]->trust_alpha;
     }
   }
   memcpy(out->h_imu_odom, c->io.h, sizeof(out->h_imu_odom));
-  if (use_io) Tsum += c->io.trigger;  // the eleven IMU/odometry certs are in all_certs (pipeline.py:964)
-  for (int i = 0; i < 3; ++i) {
-    hraw[i] += htr[i];
-    hraw[3 + i] += hrot[i];
-    for (int j = 0; j < 3; ++j) {
-      Lraw[i * DZ + j] += Ltr[3 * i + j];
-      Lraw[(3 + i) * DZ + 3 + j] += Lrot[3 * i + j];
-    }
-  }
+  if (st.use_io) st.Tsum += c->io.trigger;  // the eleven IMU/odometry certs are in all_certs (pipeline.py:964)
+  for (int i = 0; i < DZ * DZ; ++i) Lraw[i] += lt.L[i];
+  for (int i = 0; i < DZ; ++i) hraw[i] += lt.h[i];
   auto nrm = [](const double* v, int n, int stride) {
     double s = 0.0;
     for (int i = 0; i < n; ++i) s += v[i * stride] * v[i * stride];
@@ -1414,12 +1469,10 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   double dt_asym = fabs(dt_vel - dt_pose) / (dt_vel + dt_pose + kEpsMass);
   dt_asym = std::min(std::max(dt_asym, 0.0), 1.0);
   double z_to_xy = fabs(Lraw[2 * DZ + 2]) / (0.5 * (fabs(Lraw[0]) + fabs(Lraw[DZ + 1])) + kEpsMass);
-  // combined evidence cert (pipeline.py:1057-1067): aggregate([aggregate(LiDAR certs [deskew, soft
-  // assign, moment match, MF, planar]), odom, imu, gyro]); ExcitationCert is never filled -> 0
-  const double ev_ess = (pre.ess + cert[12] + mm_ess + 0.0 + 0.0) / 5.0;
-  const double ev_nll = cert[24] / (mf_neff + kEpsMass) + cert[29] / (pt_neff + kEpsMass);
-  const double ess_total = use_io ? (ev_ess + c->io.odom.ess + c->io.imu.ess + c->io.gyro.ess) / 4.0 : ev_ess;
-  const double nll_total = use_io ? ev_nll + c->io.odom.nll + c->io.imu.nll + c->io.gyro.nll : ev_nll;
+  // combined evidence cert (pipeline.py:1057-1067): aggregate([aggregate(LiDAR certs), odom, imu,
+  // gyro]); ExcitationCert is never filled -> 0
+  const double ess_total = st.use_io ? (lt.ev_ess + c->io.odom.ess + c->io.imu.ess + c->io.gyro.ess) / 4.0 : lt.ev_ess;
+  const double nll_total = st.use_io ? lt.ev_nll + c->io.odom.nll + c->io.imu.nll + c->io.gyro.nll : lt.ev_nll;
   double ess_to_exc = ess_total / (0.0 + kEpsMass);
   double s_z = z_to_xy / (z_to_xy + 1.0);
   double s_exc = 1.0 / (1.0 + ess_to_exc / 50.0);
@@ -1427,7 +1480,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   double beta = 0.25 + 0.75 * sc;
   beta = std::min(std::max(beta, 0.25), 1.0);
   cert[30] = beta; cert[39] = dt_asym; cert[40] = z_to_xy;
-  Tsum += fabs(1.0 - beta);
+  st.Tsum += fabs(1.0 - beta);
   double Lev[DZ * DZ], hev[DZ];
   for (int i = 0; i < DZ * DZ; ++i) Lev[i] = beta * Lraw[i];
   for (int i = 0; i < DZ; ++i) hev[i] = beta * hraw[i];
@@ -1443,7 +1496,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   for (int i = 0; i < DZ; ++i) for (int r = 16; r < 22; ++r) pred.L[i * DZ + r] *= a_ex;
   for (int r = 16; r < 22; ++r) pred.h[r] *= a_ex;
   cert[31] = s_dt; cert[32] = s_ex;
-  Tsum += fabs(s_dt) + fabs(s_ex);
+  st.Tsum += fabs(s_dt) + fabs(s_ex);
   // 10 FusionScaleFromCertificates on the pose-6 conditioning of the tempered evidence
   // (pipeline.py:1150-1192, fusion.py:46-142)
   double c6min, c6max, c6cond, c6nn, quality;
@@ -1451,10 +1504,10 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   const double alpha = host::fusion_scale(c6cond, ess_total, nll_total, beta, dt_asym, z_to_xy, 0.0, c->cfg.alpha_min,
                                           c->cfg.alpha_max, c->cfg.c0_cond, &quality);
   cert[33] = alpha;
-  Tsum += fabs(1.0 - alpha);
-  cert[42] = use_io ? c->io.trigger : 0.0;
-  cert[43] = io_extra[0];            // dt_int
-  cert[44] = io_extra[1];            // dt_imu
+  st.Tsum += fabs(1.0 - alpha);
+  cert[42] = st.use_io ? c->io.trigger : 0.0;
+  cert[43] = st.io_extra[0];         // dt_int
+  cert[44] = st.io_extra[1];         // dt_imu
   cert[45] = c->io.transport_sigma;
   cert[46] = c->io.kappa;            // IMU gravity vMF kappa
   cert[47] = c->io.imu_scale;        // imu_dependence_inflation scale
@@ -1466,8 +1519,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   cert[53] = c->io.ess_weighted;
   cert[54] = c->io.mean_reliability;
   cert[55] = nll_total;
-  cert[56] = io_extra[4];            // omega_avg z
-  cert[57] = redone ? 1.0 : 0.0;     // a bucket overflowed the direct rows: redone sorted
+  cert[56] = st.io_extra[4];         // omega_avg z
   // 11 InfoFusionAdditive (fusion.py:186-191)
   Belief post = pred;
   double Lsum[DZ * DZ];
@@ -1475,10 +1527,10 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   double fdelta = host::psd_project(DZ, Lsum, kEpsPsd, post.L);
   for (int i = 0; i < DZ; ++i) post.h[i] = pred.h[i] + alpha * hev[i];
   cert[34] = fdelta;
-  Tsum += fdelta;
+  st.Tsum += fdelta;
   // 12 PoseUpdateFrobeniusRecompose (recompose.py:94-205)
-  cert[35] = Tsum;
-  double fs = Tsum / (Tsum + 1.0);
+  cert[35] = st.Tsum;
+  double fs = st.Tsum / (st.Tsum + 1.0);
   cert[36] = fs;
   double dz[DZ], corr[6], dpc[6], e6[6];
   host::SpdFactor fpost;  // recompose keeps L: one factor serves post, rec and the anchor drift
@@ -1508,9 +1560,10 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j < 6; ++j) Sig6[6 * i + j] = covr[i * DZ + j];
   auto Tq = clk::now();
-  if ((rc = submit_push(c, z_t, Sig6, c->cfg.forgetting_factor, c->push_main ? c->stream : c->push_stream,
-                        c->d_part_push)))
-    return rc;
+  if (push)
+    if (int rc = submit_push(c, z_t, Sig6, c->cfg.forgetting_factor, c->push_main ? c->stream : c->push_stream,
+                             c->d_part_push))
+      return rc;
   auto Tr = clk::now();
   memcpy(out->z_t, z_t, sizeof(out->z_t));
   // 14 AnchorDriftUpdate (anchor_drift.py:93-191)
@@ -1537,17 +1590,139 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   c->belief = fin;
   from_host_belief(fin, out->belief);
   c->have_last = true;
+  memcpy(out->cert, cert, sizeof(out->cert));
   auto T3 = clk::now();
-  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-  out->stage_ms[0] = ms(T0, T1);
-  out->stage_ms[1] = ms(T1, T2);
-  out->stage_ms[2] = ms(T2, T3);
-  out->stage_ms[3] = ms(T0, T3);
-  out->stage_ms[4] = ms(T0, Tp);  // of [0]: budget launch + PredictDiffusion
-  out->stage_ms[5] = ms(T1, Ts);  // of [1]: the device stages' launch calls
-  out->stage_ms[6] = ms(T2, Tq);  // of [2]: tail numerics up to the pushforward launch
-  out->stage_ms[7] = ms(Tq, Tr);  // of [2]: pushforward launch calls
+  out->stage_ms[0] = ms_between(st.T0, st.T1);
+  out->stage_ms[1] = ms_between(st.T1, st.T2);
+  out->stage_ms[2] = ms_between(st.T2, T3);
+  out->stage_ms[3] = ms_between(st.T0, T3);
+  out->stage_ms[4] = ms_between(st.T0, st.Tp);  // of [0]: budget launch + PredictDiffusion
+  out->stage_ms[5] = ms_between(st.T1, st.Ts);  // of [1]: the device stages' launch calls
+  out->stage_ms[6] = ms_between(st.T2, Tq);     // of [2]: tail numerics up to the pushforward launch
+  out->stage_ms[7] = ms_between(Tq, Tr);        // of [2]: pushforward launch calls
   return GCS_OK;
+}
+
+}  // namespace
+
+int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
+  if (!c || !in || !out) return fail(c, GCS_ERR_ARG, "null argument");
+  if (in->imu_len < 1 || !in->imu_stamps || !in->imu_gyro || !in->imu_accel) return fail(c, GCS_ERR_ARG, "IMU window required");
+  c->live_pending = false;
+  // direct buckets for this call's stages (scale mode, unless a bucket overflowed before)
+  c->use_direct = c->cfg.mode == GCS_MODE_SCALE && c->direct_buckets && !c->sorted_sticky && c->d_members;
+  struct DirectOff {
+    gcs_ctx* c;
+    ~DirectOff() { c->use_direct = false; }  // per-operator entry points always take the sorted path
+  } direct_off{c};
+  gcs_scan_state& st = *c->scan_st;
+  if (int rc = scan_prologue(c, in, st)) return rc;
+  // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
+  int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
+                        in->scan_start_time, in->scan_end_time, st.xi, nullptr, nullptr, nullptr, /*fold_later=*/true,
+                        in->xyz_format == 1);
+  if (rc) return rc;
+  if (int rc_ = join_push(c)) return rc_;  // the bin kernel reads the map the previous scan's pushforward wrote
+  if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
+  if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
+  if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+  st.Ts = clk::now();
+  if ((rc = scan_imu_odom(c, in, st, out))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));  // the PT fold has written the scalars to h_scalars
+  if ((rc = check_bucket_err(c))) return rc;
+  bool redone = false;
+  if (c->use_direct && c->h_err[2]) {
+    // a bucket exceeded the direct rows: redo the device stages with the sorted bucketing (same
+    // flags buffer: the previous scan's pushforward may still read the other), and keep it
+    c->h_err[2] = 0u;
+    c->sorted_sticky = true;
+    c->use_direct = false;
+    redone = true;
+    if ((rc = stage_budget(c, in->weights_dev, in->n_points, /*toggle=*/false))) return rc;
+    if ((rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
+                           in->scan_start_time, in->scan_end_time, st.xi, nullptr, nullptr, nullptr, true,
+                           in->xyz_format == 1)))
+      return rc;
+    if ((rc = stage_bins(c))) return rc;
+    if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((rc = check_bucket_err(c))) return rc;
+  }
+  st.cert[41] = c->h_err[1] ? 1.0 : 0.0;  // a bucket above the ranking capacity took the compaction path
+  st.cert[57] = redone ? 1.0 : 0.0;       // a bucket overflowed the direct rows: redone sorted
+  c->h_err[1] = 0u;
+  st.T2 = clk::now();
+  if ((rc = scan_point_certs(c, in, st))) return rc;
+  LidarTerms lt;
+  scan_bin_lidar(c, st, lt, out);
+  return scan_tail(c, st, lt, out, /*push=*/true);
+}
+
+// ---------------------------------------------------------------- live primitive path: begin / finish
+int gcs_scan_begin(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs* out) {
+  if (!c || !in || !out) return fail(c, GCS_ERR_ARG, "null argument");
+  if (in->imu_len < 1 || !in->imu_stamps || !in->imu_gyro || !in->imu_accel) return fail(c, GCS_ERR_ARG, "IMU window required");
+  c->live_pending = false;
+  c->use_direct = false;
+  gcs_scan_state& st = *c->scan_st;
+  if (int rc = scan_prologue(c, in, st)) return rc;
+  // 1 + 3 on the device: budget gather, deskew, window weights (no soft assign, no bins)
+  double* p0 = out->points_dev ? out->points_dev : c->d_live_p0;
+  double* tt = out->timestamps_dev ? out->timestamps_dev : c->d_live_t;
+  double* ww = out->weights_dev ? out->weights_dev : c->d_live_w;
+  int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
+                        in->scan_start_time, in->scan_end_time, st.xi, p0, ww, nullptr,
+                        /*fold_later=*/false, in->xyz_format == 1, nullptr, /*deskew_only=*/true, tt);
+  if (rc) return rc;
+  st.Ts = clk::now();
+  if ((rc = scan_imu_odom(c, in, st, c->live_out))) return rc;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if ((rc = pull_scalars(c))) return rc;
+  st.T2 = clk::now();
+  if ((rc = scan_point_certs(c, in, st))) return rc;
+  // the map branch's linearisation point: z_lin = solve(PSD(L_pred + L_imu_odom), h_pred + h_imu_odom),
+  // its pose block (pipeline.py:751-755); read by visual_pose_evidence as [t, rotvec] (:318-322)
+  double Lf[DZ * DZ], Lp[DZ * DZ], hf[DZ], zl[DZ];
+  for (int i = 0; i < DZ * DZ; ++i) Lf[i] = st.pred.L[i] + c->io.L[i];
+  for (int i = 0; i < DZ; ++i) hf[i] = st.pred.h[i] + c->io.h[i];
+  host::psd_project(DZ, Lf, kEpsPsd, Lp);
+  host::spd_solve_lifted(DZ, Lp, hf, kEpsLift, zl);
+  memcpy(out->z_lin_pose, zl, sizeof(out->z_lin_pose));
+  memcpy(out->pose_pred, st.pose_pred, sizeof(out->pose_pred));
+  out->n_points = c->cap;
+  out->n_selected = c->last_n_sel;
+  out->points_dev = p0;
+  out->timestamps_dev = tt;
+  out->weights_dev = ww;
+  out->deskew_ess = st.pre.ess;  // the deskew certificate's support (deskew_constant_twist.py:95-104)
+  out->deskew_support = st.cert[9];
+  memcpy(out->cert, st.cert, sizeof(out->cert));
+  c->live_pending = true;
+  return GCS_OK;
+}
+
+int gcs_scan_finish(gcs_ctx* c, const gcs_lidar_evidence* ev, gcs_scan_outputs* out) {
+  if (!c || !ev || !out || !ev->L_lidar || !ev->h_lidar) return fail(c, GCS_ERR_ARG, "null argument");
+  if (!c->live_pending) return fail(c, GCS_ERR_STATE, "gcs_scan_finish without gcs_scan_begin");
+  c->live_pending = false;
+  gcs_scan_state& st = *c->scan_st;
+  memcpy(out->iw_meas_dPsi, c->live_out->iw_meas_dPsi, sizeof(out->iw_meas_dPsi));
+  memcpy(out->iw_meas_dnu, c->live_out->iw_meas_dnu, sizeof(out->iw_meas_dnu));
+  memset(out->R_mf, 0, sizeof(out->R_mf));
+  memset(out->t_wls, 0, sizeof(out->t_wls));
+  LidarTerms lt;
+  for (int i = 0; i < DZ * DZ; ++i) {
+    lt.L[i] = ev->L_lidar[i];
+    if (!std::isfinite(lt.L[i])) return fail(c, GCS_ERR_NONFINITE, "L_lidar contains NaN");
+  }
+  memcpy(lt.h, ev->h_lidar, sizeof(lt.h));
+  // aggregate(LiDAR certs) = aggregate([deskew, surfel, association, visual]) (pipeline.py:1049-1056):
+  // mean ess_total, summed nll_per_ess (the deskew cert has neither a mismatch term)
+  lt.ev_ess = (st.pre.ess + ev->ess_sum) / (1.0 + (double)ev->n_certs);
+  lt.ev_nll = ev->nll_sum;
+  st.Tsum += ev->trigger_sum;  // the map branch's and the visual certs in all_certs (pipeline.py:964-1002)
+  st.cert[58] = ev->trigger_sum;
+  return scan_tail(c, st, lt, out, /*push=*/false);
 }
 
 // ---------------------------------------------------------------- hypothesis payload / combine
@@ -1791,6 +1966,9 @@ int gcs_ctx_describe(gcs_ctx* c, char* buf, int32_t len) {
   if (!c || !buf || len < 1) return GCS_ERR_ARG;
   const gcs_config& f = c->cfg;
   const bool scale = f.mode == GCS_MODE_SCALE;
+  char tile_desc[160];
+  snprintf(tile_desc, sizeof(tile_desc), "%sk_bins_scale, %d-bin tiles x %d lanes per bin (HIP)",
+           c->use_direct || c->direct_buckets ? "direct buckets + " : "bucketing + ", c->tile_bins, 256 / c->tile_bins);
   char tmp[2048];
   int n = snprintf(tmp, sizeof(tmp),
       "{\"library\": \"%s\", \"abi\": %d, \"device\": %d, \"arch\": \"gfx950\", \"N_POINTS_CAP\": %d, "
@@ -1811,9 +1989,7 @@ int gcs_ctx_describe(gcs_ctx* c, char* buf, int32_t len) {
       f.tau, scale ? "K nearest atlas bins of the exact nearest bin, ties -> lower id (declared)" : "dense N x B softmax (reference)",
       f.forgetting_factor, f.deskew_rotation_only ? "true" : "false", f.gravity_W[0], f.gravity_W[1], f.gravity_W[2],
       f.imu_gravity_scale, f.use_imu_odom ? "true" : "false", f.planar_z_ref, f.planar_z_sigma, f.planar_vz_sigma,
-      f.alpha_min, f.alpha_max, f.c0_cond, scale ? (c->tile_bins == 32 ? "bucketing + k_bins_scale, 32-bin tiles x 8 lanes per bin (HIP)"
-                                 : "bucketing + k_bins_scale, 64-bin tiles x 4 lanes per bin (HIP)")
-            : "k_dense_accum + k_dense_finalize (HIP)");
+      f.alpha_min, f.alpha_max, f.c0_cond, scale ? tile_desc : "k_dense_accum + k_dense_finalize (HIP)");
   if (n < 0 || n >= len) return fail(c, GCS_ERR_ARG, "describe buffer too short");
   memcpy(buf, tmp, (size_t)n + 1);
   return GCS_OK;

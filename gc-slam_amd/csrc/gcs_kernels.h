@@ -75,6 +75,8 @@ struct PointKernelArgs {
   double* w_out;
   double* w_budget_out;
   int* nearest_out;
+  double* iz_out;  // 1 / Z per point (per-operator soft-assign materialisation; the record holds w / Z)
+  double* t_out;   // budget-selected timestamps (deskew-only stage: n_bins == 0)
 };
 
 struct BucketArgs {
@@ -147,14 +149,15 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
 int scan_tiles(int n_bins);
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 // Bins per k_bins_scale tile: 64 (four lanes per bin); GCSLAM_BIN_TILE=32 selects 32-bin tiles with
-// eight lanes per bin (measured slower at C2, kept for A/B and parity-tested).
+// eight lanes per bin (measured slower at C2, kept for A/B and parity-tested); 128 / 256 select wider
+// tiles with two lanes / one lane per bin and phase D on every wave.
 int bins_tile_for(long cap, int n_bins);
 int bins_scale_blocks(int n_bins, int tile_bins);
 int partial_stride(int nv);  // doubles per block-partial row
 // doubles a partials buffer needs for nblocks rows of nv values (+ the two-level fold's rows)
 size_t partials_need(long nblocks, int nv);
-int bins_max_tile_sources();  // capacity of its source list
-int bins_max_tile_entries();  // capacity of its reverse-kNN entry list
+int bins_max_tile_sources(int tile_bins);  // capacity of its source list
+int bins_max_tile_entries(int tile_bins);  // capacity of its reverse-kNN entry list
 int bins_partial_nv();
 int push_blocks(int n_bins);
 // e0/e1 bracket k_bins_scale itself (the roofline kernel), f0/f1 its partial-row fold

@@ -287,6 +287,9 @@ __device__ __forceinline__ void ray_dir(double px, double py, double pz, const d
 #ifndef GCS_POINT_WAVES
 #define GCS_POINT_WAVES 0  // register target (waves per SIMD) of k_points; 0: compiler default
 #endif
+// KC == 0 (!SCALE): deskew only -- the live primitive path's point stage (pipeline.py:399-418,
+// 568-587): budget gather, deskew, window weights and the budget / deskew certificate partials, no
+// soft assign and no record (the surfel extraction reads p0_out / w_out / t_out).
 template <bool SCALE, int KC, int LP>
 __global__ __launch_bounds__(kBlock)
 #if GCS_POINT_WAVES
@@ -343,7 +346,9 @@ void k_points(PointKernelArgs a, double* partials) {
     ray_dir(p0[0], p0[1], p0[2], a.origin, d);
     double m = -INFINITY, Z = 0.0, H = 0.0, rm = 0.0;
     int nearest = 0;
-    if (SCALE) {
+    if constexpr (!SCALE && KC == 0) {
+      // deskew only: no soft assign
+    } else if constexpr (SCALE) {
       // exact nearest atlas bin: pool of the direction's cube cell, ascending ids, strict '>'
       bool zero = (d[0] == 0.0 && d[1] == 0.0 && d[2] == 0.0);
       if (!zero) {
@@ -497,11 +502,13 @@ void k_points(PointKernelArgs a, double* partials) {
     if (!live || sub != 0) continue;
     const double wb = w_raw * mass_scale;
     const double wout = wb * win;
+    if (a.t_out) a.t_out[i] = t;
     PointRec pr;
     pr.x = p0[0]; pr.y = p0[1]; pr.z = p0[2];
     pr.dx = d[0]; pr.dy = d[1]; pr.dz = d[2];
-    pr.w = wout; pr.m = m; pr.iz = Z; pr.pad = 0.0;
-    a.recs[i] = pr;
+    pr.m = m; pr.wz = wout * Z;
+    if (KC != 0) a.recs[i] = pr;
+    if (a.iz_out) a.iz_out[i] = Z;
     if (a.p0_out) { a.p0_out[3 * (size_t)i] = p0[0]; a.p0_out[3 * (size_t)i + 1] = p0[1]; a.p0_out[3 * (size_t)i + 2] = p0[2]; }
     if (a.w_out) a.w_out[i] = wout;
     if (a.w_budget_out) a.w_budget_out[i] = wb;
@@ -836,12 +843,32 @@ constexpr int kBinNV = 16;
 //     rows, the tile's partial row by a wave reduction.
 // STAGE: kStageBig when the scan is dense in the map (cap >= 0.4 B, C2: 41 KiB of LDS, three
 // workgroups per CU), kStageSmall otherwise (C3: 25 KiB; four per CU, register-limited).
-constexpr int kMaxSrc = 320;   // atlas tables for B = 1k .. 1M have at most 199 per 64-bin tile
-constexpr int kMaxRl = 1280;   // reverse-kNN entries of one tile (~K x 64; at most 1070)
+// per-tile table capacities, proportional to the tile: for 64-bin tiles 320 sources (the atlas tables
+// for B = 1k .. 1M have at most 199) and 1280 reverse-kNN entries (~K x 64; at most 1070)
+__host__ __device__ constexpr int max_src(int tb) { return 5 * tb; }
+__host__ __device__ constexpr int max_rl(int tb) { return 20 * tb; }
 #ifndef GCS_STAGE_BIG
 #define GCS_STAGE_BIG 512  // 480 (four workgroups per CU in LDS instead of three) measured slower at C2: 27.2 -> 30.5 us
 #endif
 constexpr int kStageBig = GCS_STAGE_BIG, kStageSmall = 256;
+// record stages of the wider tiles (LDS per workgroup: tables + stage x 64 B)
+#ifndef GCS_STAGE_128_BIG
+#define GCS_STAGE_128_BIG 768
+#endif
+#ifndef GCS_STAGE_128_SMALL
+#define GCS_STAGE_128_SMALL 320
+#endif
+#ifndef GCS_STAGE_256_BIG
+#define GCS_STAGE_256_BIG 1024
+#endif
+#ifndef GCS_STAGE_256_SMALL
+#define GCS_STAGE_256_SMALL 640
+#endif
+#ifndef GCS_DALL64
+#define GCS_DALL64 false  // 64-bin tiles: phase D on wave 0 (every wave measured slower in round 1)
+#endif
+constexpr int kStage128Big = GCS_STAGE_128_BIG, kStage128Small = GCS_STAGE_128_SMALL;
+constexpr int kStage256Big = GCS_STAGE_256_BIG, kStage256Small = GCS_STAGE_256_SMALL;
 // staged record: x y z dx dy dz m w/Z as four double2 chunks (+ GCS_REC_PAD doubles of stride
 // padding); GCS_REC_SWZ stores chunk c of record r at slot c ^ ((r >> 2) & 3) (LDS bank spread)
 #ifndef GCS_REC_PAD
@@ -852,8 +879,8 @@ constexpr int kStageBig = GCS_STAGE_BIG, kStageSmall = 256;
 #endif
 constexpr int kRecD = 8 + GCS_REC_PAD;
 __device__ __forceinline__ uint32_t rec_swz(uint32_t r) { return GCS_REC_SWZ ? ((r >> 2) & 3u) : 0u; }
-int bins_max_tile_sources() { return kMaxSrc; }
-int bins_max_tile_entries() { return kMaxRl; }
+int bins_max_tile_sources(int tile_bins) { return max_src(tile_bins); }
+int bins_max_tile_entries(int tile_bins) { return max_rl(tile_bins); }
 
 __device__ __forceinline__ void bin_contrib(double* acc, const double4& bd, double inv_tau, double px, double py,
                                             double pz, double dx, double dy, double dz, double m, double wz) {
@@ -920,7 +947,10 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
 // 5 waves per SIMD needs <= 96 VGPRs (the register allocator spills ~28 dwords to reach it)
 #define GCS_BINS_WAVES_SMALL 0
 #endif
-template <int STAGE, int TB, int LANES>
+// DALL: phase D on every wave -- the first lane of each bin's lane group finalizes the bin from its
+// registers right after the lanes' xor tree (no LDS hand-off, no idle waves); required for tiles
+// wider than one wave (TB > 64).  !DALL: wave 0 alone, one lane per bin (the 64-bin tile's form).
+template <int STAGE, int TB, int LANES, bool DALL>
 __global__ __launch_bounds__(TB * LANES)
 #if GCS_BINS_WAVES
 __attribute__((amdgpu_waves_per_eu(GCS_BINS_WAVES)))
@@ -929,9 +959,10 @@ __attribute__((amdgpu_waves_per_eu(STAGE == kStageSmall ? GCS_BINS_WAVES_SMALL :
 #endif
 void k_bins_scale(BinKernelArgs a, double* partials) {
   constexpr int NT = TB * LANES, NW = NT / 64;
-  static_assert(LANES == 4 || LANES == 8, "phase C splits each bin over 4 or 8 lanes");
-  static_assert(TB <= 64, "phase D: one lane of wave 0 per bin");
-  static_assert(STAGE * kRecD >= 19 * TB, "phase D reuses the record stage for the bin sums");
+  constexpr int kMaxSrc = max_src(TB), kMaxRl = max_rl(TB);
+  static_assert(LANES == 1 || LANES == 2 || LANES == 4 || LANES == 8, "phase C splits each bin over 1-8 lanes");
+  static_assert(DALL || TB <= 64, "phase D on wave 0: one lane per bin");
+  static_assert(DALL || STAGE * kRecD >= 19 * TB, "phase D reuses the record stage for the bin sums");
   __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
   __shared__ double s_rec[STAGE * kRecD];
 #if GCS_RANK_LANES == 4
@@ -943,6 +974,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   __shared__ uint8_t s_act[TB];
   uint16_t* const rlist = s_rlc;
 #else
+  static_assert(!DALL, "the wave-0 work sum assumes TB <= 64");
   __shared__ uint16_t s_rl[kMaxRl];
   uint16_t* const rlist = s_rl;
 #endif
@@ -966,7 +998,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   // the tile flags and phase A's first-level table loads are issued together
   const bool tile_active = a.flags[a.n_bins + tile] != 0;  // block-uniform
   const bool tile_dirty = a.tile_dirty[tile] != 0;
-  const int q_t = t <= nb ? a.rknn_off[b0 + t] : 0;
+  const int q_t = t < nb ? a.rknn_off[b0 + t] : 0;
   const int q0 = a.rknn_off[b0], q1t = a.rknn_off[b0 + nb];
   const int s0 = a.tile_src_off[tile];
   const int ns = a.tile_src_off[tile + 1] - s0;
@@ -979,12 +1011,12 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   if (!tile_active) {
     // every bin of the tile has exact-zero sums: the zero-bin finalize writes its rows (N = 0,
     // Sigma = eps I, ...); partial row = nb x the zero bin's terms, no MF term
-    if (wid == 0) {
+    if (DALL || wid == 0) {
       double z[19], c5[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
 #pragma unroll
       for (int f = 0; f < 19; ++f) z[f] = 0.0;
       if (t < nb) finalize_bin(z, a.scan, a.n_bins, b0 + t, c5);
-      if (t == 0) {
+      if (t == 0) {  // every zero bin has the same terms: the partial row is nb x thread 0's
         double v[kBinNV];
 #pragma unroll
         for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
@@ -997,16 +1029,20 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     PROFV(7, 0);
     return;
   }
-  // phase D's bin (wave 0: thread t < nb owns bin b0 + t): flag and map direction stats up front
-  const bool own = t < nb;
-  const bool own_act = own && a.flags[b0 + t];
+  // phase D's bin (wave 0: thread t < nb owns bin b0 + t; DALL: lane 0 of the bin's lane group owns
+  // bin b0 + t / LANES): flag and map direction stats up front
+  const int own_b = DALL ? t / LANES : t;
+  const bool own = DALL ? (t % LANES == 0 && own_b < nb) : t < nb;
+  const bool act_t = t < nb && a.flags[b0 + t];  // bin b0 + t (the phase-A rank's table)
+  const bool own_act = DALL ? own && a.flags[b0 + own_b] : act_t;
   MapDir mapv{0.0, 0.0, 0.0, 0.0};
-  if (GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + t);
+  if (GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + own_b);
   // phase A
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
-  if (t <= nb) s_q[t] = q_t;
+  if (t < nb) s_q[t] = q_t;
+  if (t == 0) s_q[nb] = q1t;
 #if GCS_RANK_LANES == 4
-  if (t < TB) s_act[t] = own_act ? 1 : 0;
+  if (t < TB) s_act[t] = act_t ? 1 : 0;
 #endif
   {
     // fixed trip counts: every thread issues all of its table loads before the first LDS write,
@@ -1197,7 +1233,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         d[0 ^ sw] = make_double2(pr[k].x, pr[k].y);
         d[1 ^ sw] = make_double2(pr[k].z, pr[k].dx);
         d[2 ^ sw] = make_double2(pr[k].dy, pr[k].dz);
-        d[3 ^ sw] = make_double2(pr[k].m, pr[k].w * pr[k].iz);
+        d[3 ^ sw] = make_double2(pr[k].m, pr[k].wz);
       }
     }
   }
@@ -1362,7 +1398,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
           pidx = a.perm[s_st[j] + kk];
         }
         const PointRec pr = a.recs[pidx];
-        bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, pr.dx, pr.dy, pr.dz, pr.m, pr.w * pr.iz);
+        bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, pr.dx, pr.dy, pr.dz, pr.m, pr.wz);
         if (++kk == c && i + 1 < i1) {  // next source (compacted: non-empty)
           kk = 0;
           ++q;
@@ -1377,6 +1413,33 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #pragma unroll
     for (int off = 1; off < LANES; off <<= 1) acc[f] += __shfl_xor(acc[f], off, 64);
   PROF(4);
+  if constexpr (DALL) {
+    // phase D on every wave: the group's first lane finalizes its bin from the summed registers
+    double v[kBinNV];
+#pragma unroll
+    for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
+    v[4] = -INFINITY;
+    if (own) {
+      finalize_bin(acc, a.scan, a.n_bins, b0 + own_b, v);
+      if (!GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + own_b);
+      if (own_act) mf_bin_term(acc[0], acc[1], acc[2], acc[3], mapv, v + 5);
+    }
+    PROF(5);
+    // the tile's partial row: a fixed xor tree per wave, then the waves in order
+    wave_reduce_bin_terms(v);
+    if (lane == 0)
+#pragma unroll
+      for (int f = 0; f < kBinNV; ++f) lds[wid * 16 + f] = v[f];
+    __syncthreads();
+    if (t < kBinNV) {
+      double x = lds[t];
+      for (int w = 1; w < NW; ++w) x = t == 4 ? fmax(x, lds[w * 16 + t]) : x + lds[w * 16 + t];
+      partials[(size_t)blockIdx.x * pstride<kBinNV>() + t] = x;  // folded by k_final<FIN_BINS>
+    }
+    PROF(6);
+    PROFV(7, 1);
+    return;
+  }
 #ifdef GCS_PHASE_PROF
   if (lane == 0 && wid > 0 && wid < 4) g_prof[blockIdx.x * 16 + 10 + wid] = wall_clock64();  // waves 1-3 gather end
 #endif
@@ -1433,9 +1496,8 @@ __global__ __launch_bounds__(kBlock) void k_dense_accum(BinKernelArgs a, double*
     for (int j = 0; j < np; ++j) {
       const double* d = dirs + 3 * j;
       double s = dot3_exact(d[0], d[1], d[2], bd[0], bd[1], bd[2]);
-      double r = exp((s - pts[j].m) * inv_tau) * pts[j].iz;
       double p[3] = {pts[j].x, pts[j].y, pts[j].z};
-      add_contrib(acc, pts[j].w * r, d, p);
+      add_contrib(acc, pts[j].wz * exp((s - pts[j].m) * inv_tau), d, p);  // w r = (w / Z) exp(x)
     }
     size_t nb = gridDim.x;
 #pragma unroll
@@ -1884,6 +1946,8 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
       case 32: hipExtLaunchKernelGGL((k_points<true, 32, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
       default: return hipErrorInvalidValue;
     }
+  } else if (a.n_bins == 0) {  // deskew only (gcs_scan_begin)
+    hipExtLaunchKernelGGL((k_points<false, 0, 1>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
   } else {
     hipExtLaunchKernelGGL((k_points<false, 1, 1>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
   }
@@ -1907,7 +1971,7 @@ hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_
 int bins_tile_for(long cap, int n_bins) {
   if (const char* e = getenv("GCSLAM_BIN_TILE")) {
     const int v = atoi(e);
-    if (v == 32 || v == 64) return v;
+    if (v == 32 || v == 64 || v == 128 || v == 256) return v;
   }
   (void)cap;
   (void)n_bins;
@@ -1921,11 +1985,19 @@ hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream
   const int nblk = bins_scale_blocks(a.n_bins, a.tile_bins);
   const bool big = (long)a.cap * 5 >= (long)a.n_bins * 2;  // C2-like: dense in the map
   if (a.tile_bins == 32)  // half the records of a 64-bin tile: the small stage holds them
-    hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 32, 8>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 32, 8, false>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+  else if (a.tile_bins == 128 && big)
+    hipExtLaunchKernelGGL((k_bins_scale<kStage128Big, 128, 2, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+  else if (a.tile_bins == 128)
+    hipExtLaunchKernelGGL((k_bins_scale<kStage128Small, 128, 2, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+  else if (a.tile_bins == 256 && big)
+    hipExtLaunchKernelGGL((k_bins_scale<kStage256Big, 256, 1, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+  else if (a.tile_bins == 256)
+    hipExtLaunchKernelGGL((k_bins_scale<kStage256Small, 256, 1, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else if (big)
-    hipExtLaunchKernelGGL((k_bins_scale<kStageBig, 64, 4>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL((k_bins_scale<kStageBig, 64, 4, GCS_DALL64>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else
-    hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 64, 4>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 64, 4, GCS_DALL64>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   launch_fold<kBinNV, 16u, FIN_BINS>(partials, nblk, s, f1, a.scalars, nullptr, f0);
   return hipGetLastError();
 }

@@ -36,16 +36,16 @@ enum MapDerived : int {
   MD_COUNT = 16
 };
 
-// Per-point record written by the point kernel, gathered by the bin kernels (80 B; the bin
-// kernel stages the first 72 B of each record in LDS).
+// Per-point record written by the point kernel, gathered by the bin kernels (64 B, exactly what the
+// bin kernel stages in LDS: four 16-B loads per record).
 struct PointRec {
   double x, y, z;     // deskewed point (scan-start base frame)
   double dx, dy, dz;  // ray direction from the LiDAR origin (pipeline.py:589-593)
-  double w;           // weight after budget mass rescale and deskew time window
   double m;           // max candidate similarity (softmax shift)
-  double iz;          // 1 / sum_k exp((s_k - m) / tau)
-  double pad;
+  double wz;          // w / Z: weight after budget mass rescale and deskew time window (w), times
+                      // 1 / Z, Z = sum_k exp((s_k - m) / tau); w r_k = wz exp((s_k - m) / tau)
 };
+static_assert(sizeof(PointRec) == 64, "point record");
 
 // Scalar results slots (device buffer of doubles, copied to host once per scan).
 enum Scalar : int {

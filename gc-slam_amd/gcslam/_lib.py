@@ -71,6 +71,18 @@ class GcsScanOutputs(C.Structure):
                 ("imu_odom_certs", C.c_double * 77)]
 
 
+class GcsScanBeginOutputs(C.Structure):
+    _fields_ = [("z_lin_pose", C.c_double * 6), ("pose_pred", C.c_double * 6), ("n_points", C.c_int32),
+                ("n_selected", C.c_int32), ("points_dev", C.c_void_p), ("timestamps_dev", C.c_void_p),
+                ("weights_dev", C.c_void_p), ("deskew_ess", C.c_double), ("deskew_support", C.c_double),
+                ("cert", C.c_double * CERT_LEN)]
+
+
+class GcsLidarEvidence(C.Structure):
+    _fields_ = [("L_lidar", C.c_void_p), ("h_lidar", C.c_void_p), ("trigger_sum", C.c_double),
+                ("ess_sum", C.c_double), ("n_certs", C.c_int32), ("nll_sum", C.c_double)]
+
+
 class GcsImuOdomInputs(C.Structure):
     _fields_ = [("m", C.c_int32), ("stamps", C.c_void_p), ("gyro", C.c_void_p), ("accel", C.c_void_p),
                 ("w_int", C.c_void_p), ("t_last_scan", C.c_double), ("t_scan", C.c_double), ("dt_sec", C.c_double),
@@ -208,6 +220,8 @@ _SIGS = [
     ("gcs_ctx_set_meas_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p]),
     ("gcs_ctx_get_meas_iw_state", C.c_int, [C.c_void_p, c_double_p, c_double_p, c_double_p]),
     ("gcs_scan", C.c_int, [C.c_void_p, C.POINTER(GcsScanInputs), C.POINTER(GcsScanOutputs)]),
+    ("gcs_scan_begin", C.c_int, [C.c_void_p, C.POINTER(GcsScanInputs), C.POINTER(GcsScanBeginOutputs)]),
+    ("gcs_scan_finish", C.c_int, [C.c_void_p, C.POINTER(GcsLidarEvidence), C.POINTER(GcsScanOutputs)]),
     ("gcs_parse_pointcloud2", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(GcsPointCloud2Layout), C.c_void_p,
                                         C.c_void_p, C.c_void_p, C.c_void_p]),
     ("gcs_point_stage", C.c_int, [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_double,

@@ -243,6 +243,69 @@ class HypothesisContext:
         self._chk(self.lib.gcs_pushforward(self.h, L.dptr(z), L.dptr(S), float(gamma)), "pushforward")
 
     # ------------------------------------------------------------------ the scan
+    def _scan_inputs(self, xyz_dev, point_step, t_dev, w_dev, n_points, imu_stamps, imu_gyro, imu_accel,
+                     scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None, t_last_scan=None,
+                     t_scan=None, xyz_f64=False, odom_pose=None, odom_cov_se3=None, odom_twist=None,
+                     odom_twist_cov=None, Sigma_g=None, Sigma_a=None):
+        """gcs_scan_inputs for gcs_scan / gcs_scan_begin; returns (struct, arrays to keep alive)."""
+        imu_stamps = np.ascontiguousarray(imu_stamps, np.float64)
+        imu_gyro = np.ascontiguousarray(imu_gyro, np.float64).reshape(-1)
+        imu_accel = np.ascontiguousarray(imu_accel, np.float64).reshape(-1)
+        inp = L.GcsScanInputs()
+        inp.xyz_dev = xyz_dev.data_ptr()
+        inp.point_step = int(point_step)
+        inp.timestamps_dev = t_dev.data_ptr()
+        inp.weights_dev = w_dev.data_ptr()
+        inp.n_points = int(n_points)
+        inp.imu_stamps = _addr(imu_stamps)
+        inp.imu_gyro = _addr(imu_gyro)
+        inp.imu_accel = _addr(imu_accel)
+        inp.imu_len = int(imu_stamps.shape[0])
+        inp.scan_start_time = float(scan_start_time)
+        inp.scan_end_time = float(scan_end_time)
+        inp.dt_sec = float(dt_sec)
+        inp.t_last_scan = float(scan_start_time if t_last_scan is None else t_last_scan)
+        inp.t_scan = float(scan_end_time if t_scan is None else t_scan)
+        inp.xyz_format = 1 if xyz_f64 else 0
+        keep = [imu_stamps, imu_gyro, imu_accel]
+        for name, arr in (("Q", Q), ("L_ext", L_ext), ("h_ext", h_ext), ("odom_pose", odom_pose),
+                          ("odom_cov_se3", odom_cov_se3), ("odom_twist", odom_twist), ("odom_twist_cov", odom_twist_cov),
+                          ("Sigma_g", Sigma_g), ("Sigma_a", Sigma_a)):
+            if arr is not None:
+                a = np.ascontiguousarray(arr, np.float64).reshape(-1)
+                keep.append(a)
+                setattr(inp, name, _addr(a))
+        return inp, keep
+
+    def scan_begin(self, *args, **kw):
+        """gcs_scan_begin (the live primitive path's first half; same arguments as scan()): returns a
+        GcsScanBeginOutputs with z_lin_pose, pose_pred and the device arrays of the deskewed points,
+        budget timestamps and deskewed weights (context-owned, valid until the next scan)."""
+        import torch
+        bufs = kw.pop("buffers", None)
+        inp, keep = self._scan_inputs(*args, **kw)
+        out = L.GcsScanBeginOutputs()
+        if bufs is not None:  # caller-owned (points (cap,3), timestamps (cap,), weights (cap,)) f64 tensors
+            p, t, w = bufs
+            for x, n in ((p, 3 * self.cfg.n_points_cap), (t, self.cfg.n_points_cap), (w, self.cfg.n_points_cap)):
+                if x.dtype != torch.float64 or not x.is_contiguous() or x.numel() != n:
+                    raise ValueError("scan_begin buffers: contiguous f64 tensors of N_POINTS_CAP rows")
+            out.points_dev, out.timestamps_dev, out.weights_dev = p.data_ptr(), t.data_ptr(), w.data_ptr()
+        self._chk(self.lib.gcs_scan_begin(self.h, C.byref(inp), C.byref(out)), "gcs_scan_begin")
+        del keep
+        return out
+
+    def scan_finish(self, L_lidar, h_lidar, trigger_sum, ess_sum, n_certs, nll_sum, out=None):
+        """gcs_scan_finish with the live path's LiDAR evidence (visual_pose_evidence L_pose / h_pose) and
+        the terms of its certificates (gcs_lidar_evidence)."""
+        Lm = np.ascontiguousarray(L_lidar, np.float64).reshape(-1)
+        hv = np.ascontiguousarray(h_lidar, np.float64).reshape(-1)
+        ev = L.GcsLidarEvidence(_addr(Lm), _addr(hv), float(trigger_sum), float(ess_sum), int(n_certs), float(nll_sum))
+        if out is None:
+            out = L.GcsScanOutputs()
+        self._chk(self.lib.gcs_scan_finish(self.h, C.byref(ev), C.byref(out)), "gcs_scan_finish")
+        return out
+
     def scan(self, xyz_dev, point_step, t_dev, w_dev, n_points, imu_stamps, imu_gyro, imu_accel,
              scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None, t_last_scan=None, t_scan=None,
              xyz_f64=False, odom_pose=None, odom_cov_se3=None, odom_twist=None, odom_twist_cov=None, Sigma_g=None,

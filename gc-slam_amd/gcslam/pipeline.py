@@ -1,11 +1,16 @@
 """L2 drop-in: process_scan_single_hypothesis / process_hypotheses with the reference calling
-convention (FS/backend/pipeline.py:316-340, :1594-1621), running the 14-step bin path
-(README.md:105-122) on the MI355X through libgcslam_hip.so, plus the node-level noise updates the
-reference's backend node calls after the hypothesis loop (backend_node.py:2093-2119) and the
-RuntimeManifest (pipeline.py:1629-1793).
+convention (FS/backend/pipeline.py:316-340, :1594-1621) on the MI355X through libgcslam_hip.so, plus
+the node-level noise updates the reference's backend node calls after the hypothesis loop
+(backend_node.py:2093-2119) and the RuntimeManifest (pipeline.py:1629-1793).
 
-`primitive_map` is replaced by `map_bins`, a HypothesisContext that owns the device-resident
-MapBinStats of this hypothesis (the legacy pipeline took bin_atlas/map_stats, CHANGELOG.md:280).
+Two LiDAR evidence paths behind the one signature:
+  * the 14-step bin path (README.md:105-122): `map_bins`, a HypothesisContext that owns the
+    device-resident MapBinStats of this hypothesis (the legacy pipeline took bin_atlas/map_stats,
+    CHANGELOG.md:280);
+  * the live primitive path (pipeline.py:778-1011, 1232-1492) when `primitive_map` (an AtlasMap) is
+    given: surfels, recency inflation, the map view, OT association and visual pose evidence between
+    gcs_scan_begin and gcs_scan_finish, then step 12b at z_t; the result carries the updated map
+    (`map`, the node's result.map hand-off, backend_node.py:2079-2083) and its MapUpdateCert.
 """
 
 from __future__ import annotations
@@ -80,6 +85,28 @@ class PipelineConfig:
     camera_batch_policy: str = "warn"  # camera evidence is out of scope here: "warn" once | "raise" | "ignore"
     max_raw_points: int = 1 << 20
     device: int = 0
+    # live primitive path (pipeline.py:179-211; constants.py:350-477)
+    n_feat: int = 512
+    n_surfel: int = 1024
+    surfel_voxel_size_m: float = 0.1
+    surfel_min_points_per_voxel: int = 3
+    k_assoc: int = 8
+    k_sinkhorn: int = 50
+    ot_epsilon: float = 0.1
+    ot_tau_a: float = 0.5
+    ot_tau_b: float = 0.5
+    primitive_map_max_size: int = 50000
+    k_insert_tile: int = 64
+    H_TILE: float = 2.0
+    R_ACTIVE_TILES_XY: int = 1
+    R_ACTIVE_TILES_Z: int = 0
+    M_TILE_VIEW: int = 1024
+    R_STENCIL_TILES_XY: int = 1
+    R_STENCIL_TILES_Z: int = 0
+    N_ACTIVE_TILES: int = 7
+    N_STENCIL_TILES: int = 7
+    RECENCY_DECAY_LAMBDA: float = 0.02
+    RECENCY_MIN_SCALE: float = 0.05
 
     def context_kwargs(self) -> dict:
         return dict(n_bins=self.B_BINS, n_points_cap=self.N_POINTS_CAP, max_raw_points=self.max_raw_points,
@@ -93,6 +120,31 @@ class PipelineConfig:
 
     def make_context(self) -> HypothesisContext:
         return HypothesisContext(**self.context_kwargs())
+
+
+@dataclass
+class MapUpdateCert:
+    """FS/common/certificates.py MapUpdateCert, as step 12b fills it (pipeline.py:1454-1487)."""
+    n_active_tiles: int = 0
+    tile_ids_active: List[int] = field(default_factory=list)
+    n_inactive_tiles: int = 0
+    staleness_inflation_strength: float = 0.0
+    staleness_cov_inflation_trace: float = 0.0
+    stale_precision_downscale_total: float = 0.0
+    tile_ids_inactive: List[int] = field(default_factory=list)
+    tile_cache_hits: int = 0
+    tile_cache_misses: int = 0
+    candidate_tiles_per_meas_mean: float = 0.0
+    candidate_primitives_per_meas_mean: float = 0.0
+    candidate_primitives_per_meas_p95: float = 0.0
+    insert_count_total: int = 0
+    insert_mass_total: float = 0.0
+    insert_mass_p95: float = 0.0
+    evicted_count: int = 0
+    evicted_mass_total: float = 0.0
+    fused_count: int = 0
+    fused_mass_total: float = 0.0
+    merged_count: int = 0
 
 
 @dataclass
@@ -115,6 +167,14 @@ class ScanPipelineResult:
     h_evidence: Optional[np.ndarray] = None
     L_imu_odom: Optional[np.ndarray] = None
     h_imu_odom: Optional[np.ndarray] = None
+    # live primitive path (pipeline.py:230-254): the updated map, the scan's measurement batch, the
+    # map-update certificate and the association / view it fused through
+    map: Optional[object] = None
+    measurement_batch: Optional[object] = None
+    map_update_cert: Optional[MapUpdateCert] = None
+    association: Optional[object] = None
+    map_view: Optional[object] = None
+    z_lin_pose: Optional[np.ndarray] = None
 
 
 IMU_ODOM_CERTS = (("OdomEvidenceGaussian",), ("ImuAccelDirectionTimeResolved", "TransportConsistencyWeighting"),
@@ -123,9 +183,10 @@ IMU_ODOM_CERTS = (("OdomEvidenceGaussian",), ("ImuAccelDirectionTimeResolved", "
                   ("PoseTwistKinematicConsistency",), ("OdomDependenceInflation",))
 
 
-def _certs_from_vector(c, io, chart, anchor):
+def _certs_from_vector(c, io, chart, anchor, live_certs=None):
     """Rebuild the per-operator certificates in the reference's all_certs order from the scan's
-    cert vector and the eleven IMU/odometry certificate rows (DESIGN.md cert slots)."""
+    cert vector and the eleven IMU/odometry certificate rows (DESIGN.md cert slots).  live_certs: the
+    live path's map-branch + visual certs, which take the place of the bin path's LiDAR certs."""
     I = InfluenceCert
     certs = [
         CertBundle.create_approx(chart, anchor, ["PointBudgetResample"], support=SupportCert(c[0], c[1]),
@@ -142,14 +203,19 @@ def _certs_from_vector(c, io, chart, anchor):
                                               mismatch=MismatchCert(nll_per_ess=r[2]),
                                               influence=I(lift_strength=r[3], psd_projection_delta=r[4],
                                                           mass_epsilon_ratio=r[5], trust_alpha=r[6])))
+    if live_certs is not None:
+        certs += list(live_certs)
+    else:
+        certs += [
+            CertBundle.create_exact(chart, anchor, support=SupportCert(c[12], c[13])),
+            CertBundle.create_approx(chart, anchor, ["ScanBinMomentMatch"], support=SupportCert(c[14], c[15]),
+                                     influence=I(psd_projection_delta=c[16], mass_epsilon_ratio=c[17])),
+            CertBundle.create_approx(chart, anchor, ["MatrixFisherRotationEvidence"],
+                                     influence=I(psd_projection_delta=c[18], mass_epsilon_ratio=c[19])),
+            CertBundle.create_approx(chart, anchor, ["PlanarTranslationEvidence"],
+                                     influence=I(psd_projection_delta=c[25], mass_epsilon_ratio=c[26])),
+        ]
     certs += [
-        CertBundle.create_exact(chart, anchor, support=SupportCert(c[12], c[13])),
-        CertBundle.create_approx(chart, anchor, ["ScanBinMomentMatch"], support=SupportCert(c[14], c[15]),
-                                 influence=I(psd_projection_delta=c[16], mass_epsilon_ratio=c[17])),
-        CertBundle.create_approx(chart, anchor, ["MatrixFisherRotationEvidence"],
-                                 influence=I(psd_projection_delta=c[18], mass_epsilon_ratio=c[19])),
-        CertBundle.create_approx(chart, anchor, ["PlanarTranslationEvidence"],
-                                 influence=I(psd_projection_delta=c[25], mass_epsilon_ratio=c[26])),
         CertBundle.create_approx(chart, anchor, ["PowerTempering"], frobenius_applied=abs(1.0 - c[30]) > 0.0,
                                  influence=I(power_beta=c[30])),
         CertBundle.create_approx(chart, anchor, ["ExcitationPriorScaling"],
@@ -221,11 +287,113 @@ def _camera_batch_has_content(camera_batch):
     return True
 
 
+def _candidate_stats(batch, view, res, eps_mass):
+    """The map branch's candidate statistics for the MapUpdateCert (pipeline.py:879-905), on the device."""
+    import torch
+    valid = batch.valid_mask.to(torch.bool)
+    nv = int(valid.sum().item())
+    if nv == 0:
+        return 0.0, 0.0, 0.0
+    cp = res.candidate_pool_indices.to(torch.int64)
+    cand_valid = view.valid_mask.to(torch.bool)[cp]
+    cand_tiles = torch.where(cand_valid, res.candidate_tile_ids.to(torch.int64), torch.full_like(cp, -1))
+    cand_counts = cand_valid.to(torch.float64).sum(1)
+    ts = torch.sort(cand_tiles, dim=1).values
+    is_new = torch.cat([torch.ones_like(ts[:, :1], dtype=torch.bool), ts[:, 1:] != ts[:, :-1]], dim=1)
+    distinct = ((is_new & (ts != -1)).to(torch.float64)).sum(1)
+    vr = valid.to(torch.float64)
+    denom = max(float(vr.sum().item()), eps_mass)
+    tiles_mean = float((distinct * vr).sum().item()) / denom
+    prims_mean = float((cand_counts * vr).sum().item()) / denom
+    cs = torch.sort(torch.where(valid, cand_counts, torch.full_like(cand_counts, -1.0))).values
+    i95 = min(int(0.95 * float(cs.shape[0])), int(cs.shape[0]) - 1)
+    return tiles_mean, prims_mean, float(cs[i95].item())
+
+
+def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, rec, t, w, imu_stamps, imu_gyro,
+                            imu_accel, odom_pose, odom_cov_se3, scan_start_time, scan_end_time, dt_sec, t_last_scan,
+                            t_scan, Q, config: PipelineConfig, odom_twist, odom_twist_cov, scan_seq, L_ext, h_ext):
+    """The live pipeline (pipeline.py:316-1591) on the device: gcs_scan_begin (budget, predict, IMU
+    preintegration, deskew, IMU/odometry branch, z_lin_pose) -> the map branch (:778-926) -> visual
+    pose evidence (:980-1010) -> gcs_scan_finish (tempering, fusion, recompose, anchor drift) ->
+    step 12b at z_t (:1232-1492)."""
+    import torch
+    from . import association as GA, primitive_map as GPM
+    from .surfels import SurfelExtractionConfig, extract_lidar_surfels
+    cap = ctx.cfg.n_points_cap
+    dev = f"cuda:{config.device}"
+    bufs = getattr(ctx, "_live_bufs", None)
+    if bufs is None:
+        bufs = ctx._live_bufs = (torch.empty((cap, 3), dtype=torch.float64, device=dev),
+                                 torch.empty(cap, dtype=torch.float64, device=dev),
+                                 torch.empty(cap, dtype=torch.float64, device=dev))
+    b = ctx.scan_begin(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
+                       dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
+                       odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
+                       odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a, buffers=bufs)
+    # the map branch (pipeline.py:778-926)
+    scfg = SurfelExtractionConfig(n_surfel=config.n_surfel, n_feat=config.n_feat,
+                                  voxel_size_m=config.surfel_voxel_size_m,
+                                  min_points_per_voxel=config.surfel_min_points_per_voxel, eps_lift=config.eps_lift)
+    batch, c_surf, _ = extract_lidar_surfels(bufs[0], bufs[1], bufs[2], config=scfg, chart_id=CHART_ID,
+                                             device=config.device)
+    centre = np.array(b.pose_pred[:3])
+    active = GPM.ma_hex_stencil_tile_ids(centre, config.H_TILE, config.R_ACTIVE_TILES_XY, config.R_ACTIVE_TILES_Z)
+    stencil = GPM.ma_hex_stencil_tile_ids(centre, config.H_TILE, config.R_STENCIL_TILES_XY, config.R_STENCIL_TILES_Z)
+    if len(active) != int(config.N_ACTIVE_TILES):
+        raise ValueError(f"active tile stencil size mismatch: expected N_ACTIVE_TILES={config.N_ACTIVE_TILES}, "
+                         f"got {len(active)}")
+    if len(stencil) != int(config.N_STENCIL_TILES):
+        raise ValueError(f"stencil tile size mismatch: expected N_STENCIL_TILES={config.N_STENCIL_TILES}, "
+                         f"got {len(stencil)}")
+    am, c_infl, _, infl = GPM.primitive_map_recency_inflate(primitive_map, active, int(scan_seq),
+                                                            config.RECENCY_DECAY_LAMBDA, config.RECENCY_MIN_SCALE)
+    view = GPM.extract_atlas_map_view(am, stencil, int(config.M_TILE_VIEW), config.eps_lift, config.eps_mass)
+    acfg = GA.AssociationConfig(k_assoc=config.k_assoc, k_sinkhorn=config.k_sinkhorn, epsilon=config.ot_epsilon,
+                                tau_a=config.ot_tau_a, tau_b=config.ot_tau_b, eps_mass=config.eps_mass,
+                                h_tile=config.H_TILE, r_stencil_tiles_xy=config.R_STENCIL_TILES_XY,
+                                r_stencil_tiles_z=config.R_STENCIL_TILES_Z, scan_seq=int(scan_seq),
+                                recency_decay_lambda=config.RECENCY_DECAY_LAMBDA)
+    res, c_assoc, _ = GA.associate_primitives_ot(batch, view, acfg, chart_id=CHART_ID, device=config.device)
+    cand = _candidate_stats(batch, view, res, config.eps_mass)
+    z_lin_pose = np.array(b.z_lin_pose[:])
+    vis, c_vis, _ = GA.visual_pose_evidence(res, batch, view, eps_lift=config.eps_lift, eps_mass=config.eps_mass,
+                                            chart_id=CHART_ID, z_lin_pose=z_lin_pose, device=config.device)
+    L_lidar, h_lidar = GA.build_visual_pose_evidence_22d(vis)
+    # the map branch's + visual certs enter all_certs (T, pipeline.py:1211); the LiDAR evidence aggregate
+    # is [deskew, surfel, association, visual] (:1049-1056)
+    trig = sum(c.total_trigger_magnitude() for c in (c_surf, c_infl, c_assoc, c_vis))
+    lid = (c_surf, c_assoc, c_vis)
+    out = ctx.scan_finish(L_lidar, h_lidar, trig, sum(c.support.ess_total for c in lid), len(lid),
+                          sum(c.mismatch.nll_per_ess for c in lid))
+    z_t = np.array(out.z_t[:])
+    # step 12b: the primitive map update at z_t (pipeline.py:1232-1492)
+    ucfg = GPM.PrimitiveMapUpdateConfig(k_insert_tile=config.k_insert_tile, H_TILE=config.H_TILE,
+                                        RECENCY_DECAY_LAMBDA=config.RECENCY_DECAY_LAMBDA, eps_lift=config.eps_lift,
+                                        eps_mass=config.eps_mass, eps_psd=config.eps_psd)
+    st = GPM.primitive_map_update(am, batch, res, z_t, active, float(scan_end_time), int(scan_seq), config=ucfg)
+    act = set(active)
+    inactive = [int(x) for x in am.tile_ids if int(x) not in act]
+    hits = len([x for x in active if int(x) in set(am.tile_ids)])
+    muc = MapUpdateCert(n_active_tiles=len(active), tile_ids_active=[int(x) for x in active],
+                        n_inactive_tiles=len(inactive), staleness_inflation_strength=infl.staleness_inflation_strength,
+                        staleness_cov_inflation_trace=infl.staleness_cov_inflation_trace,
+                        stale_precision_downscale_total=infl.stale_precision_downscale_total,
+                        tile_ids_inactive=inactive, tile_cache_hits=hits, tile_cache_misses=len(act) - hits,
+                        candidate_tiles_per_meas_mean=cand[0], candidate_primitives_per_meas_mean=cand[1],
+                        candidate_primitives_per_meas_p95=cand[2],
+                        **{k: st[k] for k in ("insert_count_total", "insert_mass_total", "insert_mass_p95",
+                                              "evicted_count", "evicted_mass_total", "fused_count", "fused_mass_total",
+                                              "merged_count")})
+    return out, dict(map=am, batch=batch, map_update_cert=muc, certs=[c_surf, c_infl, c_assoc, c_vis],
+                     association=res, view=view, z_lin_pose=z_lin_pose)
+
+
 def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, raw_timestamps, raw_weights,
                                    raw_ring, raw_tag, imu_stamps, imu_gyro, imu_accel, odom_pose, odom_cov_se3,
                                    scan_start_time, scan_end_time, dt_sec, t_last_scan, t_scan, Q,
                                    config: PipelineConfig, odom_twist=None, odom_twist_cov=None, camera_batch=None,
-                                   scan_seq=0, map_bins: Optional[HypothesisContext] = None,
+                                   scan_seq=0, primitive_map=None, map_bins: Optional[HypothesisContext] = None,
                                    L_ext=None, h_ext=None) -> ScanPipelineResult:
     """FS/backend/pipeline.py:316-1591 with the bin path of README.md:105-122.
 
@@ -236,7 +404,11 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
     budget step for the primitive path; the bin path does not read them.  camera_batch feeds the
     live primitive path's visual evidence, which this backend does not build (DESIGN.md out of
     scope): config.camera_batch_policy says whether a non-empty batch warns (default), raises or is
-    ignored.  L_ext / h_ext add further caller evidence to step 9."""
+    ignored.  L_ext / h_ext add further caller evidence to step 9.
+
+    primitive_map (an AtlasMap): the live primitive path (pipeline.py:778-1011, 1232-1492) replaces the
+    bin evidence; map_bins then only carries the hypothesis state (belief, IW), and result.map is the
+    updated AtlasMap (the node keeps hypothesis 0's, backend_node.py:2079-2083)."""
     global _camera_warned
     if _camera_batch_has_content(camera_batch):
         if config.camera_batch_policy == "raise":
@@ -247,13 +419,21 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
     ctx = map_bins if map_bins is not None else config.make_context()
     ctx.set_belief(belief_prev.X_anchor, belief_prev.stamp_sec, belief_prev.z_lin, belief_prev.L, belief_prev.h)
     rec, t, w = _as_device_scan(raw_points, raw_timestamps, raw_weights, config.device)
-    out = ctx.scan(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
-                   dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
-                   odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
-                   odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a)
+    live = None
+    if primitive_map is not None:
+        out, live = _process_scan_primitive(ctx, primitive_map, belief_prev, rec, t, w, imu_stamps, imu_gyro,
+                                            imu_accel, odom_pose, odom_cov_se3, scan_start_time, scan_end_time, dt_sec,
+                                            t_last_scan, t_scan, Q, config, odom_twist, odom_twist_cov, scan_seq,
+                                            L_ext, h_ext)
+    else:
+        out = ctx.scan(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
+                       dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
+                       odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
+                       odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a)
     X, stamp, z, Lm, h = ctx.get_belief()
     cert = np.array(out.cert[:])
-    certs = _certs_from_vector(cert, np.array(out.imu_odom_certs[:]), CHART_ID, belief_prev.anchor_id)
+    certs = _certs_from_vector(cert, np.array(out.imu_odom_certs[:]), CHART_ID, belief_prev.anchor_id,
+                               live["certs"] if live else None)
     agg = aggregate_certificates(certs)
     bel = BeliefGaussianInfo(CHART_ID, belief_prev.anchor_id, X, stamp, z, Lm, h, certs[-1])
     view = np.ctypeslib.as_array
@@ -268,6 +448,14 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
         map_bins_updated=ctx, z_t=view(out.z_t).copy(), raw_cert=cert,
         L_evidence=view(out.L_evidence).copy().reshape(D_Z, D_Z), h_evidence=view(out.h_evidence).copy(),
         L_imu_odom=view(out.L_imu_odom).copy().reshape(D_Z, D_Z), h_imu_odom=view(out.h_imu_odom).copy())
+    if live is not None:
+        res.map = live["map"]
+        res.measurement_batch = live["batch"]
+        res.map_update_cert = live["map_update_cert"]
+        res.association = live["association"]
+        res.map_view = live["view"]
+        res.z_lin_pose = live["z_lin_pose"]
+        res.map_bins_updated = None
     # the reference's per-scan MinimalScanTape (pipeline.py:1504-1570)
     res.diagnostics_tape = tape_from_result(res, scan_seq, scan_end_time, dt_sec, rec.shape[0], res.L_evidence)
     if map_bins is None:

@@ -237,6 +237,48 @@ int gcs_ctx_get_meas_iw_state(gcs_ctx* ctx, double* nu3, double* Psi3x9, double*
 /* ---------------------------------------------------------------- the per-scan pipeline */
 int gcs_scan(gcs_ctx* ctx, const gcs_scan_inputs* in, gcs_scan_outputs* out);
 
+/* ---------------------------------------------------------------- live primitive path
+ * The same scan split around the live path's LiDAR evidence (FS/backend/pipeline.py:778-1011), which
+ * the caller builds with the primitive-path entry points between the two calls:
+ *   gcs_scan_begin: budget (device), PredictDiffusion, IMU window + preintegration, deskew (device:
+ *     deskewed points / weights / budget timestamps into context-owned device arrays), the
+ *     measurement-noise IW statistics and the IMU/odometry branch with its z_lin_pose (:751-755);
+ *   the caller: extract_lidar_surfels on those arrays, recency inflation + map view at pose_pred,
+ *     associate_primitives_ot, visual_pose_evidence at z_lin_pose -> L_lidar, h_lidar (:778-1011);
+ *   gcs_scan_finish: evidence sum + power tempering with the LiDAR certificates' terms, excitation
+ *     scaling, FusionScaleFromCertificates, InfoFusionAdditive, recompose, process IW statistics,
+ *     AnchorDriftUpdate (:1038-1230, 1494-1502); no bin-map pushforward: the caller runs step 12b
+ *     (the primitive map update) at out->z_t (:1232-1492).
+ * Any context mode works (its bin atlas is not used). */
+typedef struct {
+  double z_lin_pose[6];          /* [t, rotvec] read by visual_pose_evidence (pipeline.py:755, :318-322) */
+  double pose_pred[6];           /* belief_pred.mean_world_pose: the map branch's stencil centre (:801-802) */
+  int32_t n_points;              /* rows of the arrays below (N_POINTS_CAP: selected rows + zero padding) */
+  int32_t n_selected;
+  /* in: caller-owned device buffers of N_POINTS_CAP rows, or NULL for the context's own (valid until
+   * its next scan); out: the buffers written */
+  double* points_dev;            /* [n_points*3] deskewed points */
+  double* timestamps_dev;        /* [n_points] budget timestamps */
+  double* weights_dev;           /* [n_points] deskewed weights */
+  double deskew_ess;             /* the deskew certificate: ess_total (IMU preintegration ESS), */
+  double deskew_support;         /* support_frac (retained weight fraction) */
+  double cert[GCS_CERT_LEN];     /* the scan's certificate slots filled so far */
+} gcs_scan_begin_outputs;
+
+typedef struct {
+  const double* L_lidar;         /* [22*22] visual_pose_evidence L_pose (build_visual_pose_evidence_22d) */
+  const double* h_lidar;         /* [22] */
+  double trigger_sum;            /* sum of total_trigger_magnitude over the map-branch certs (surfel,
+                                    recency inflation, association) and the visual cert (pipeline.py:1211) */
+  double ess_sum;                /* sum of support.ess_total over the LiDAR certs after deskew (surfel,
+                                    association, visual; aggregate_certificates, pipeline.py:1049-1056) */
+  int32_t n_certs;               /* their count */
+  double nll_sum;                /* sum of mismatch.nll_per_ess over the same certs */
+} gcs_lidar_evidence;
+
+int gcs_scan_begin(gcs_ctx* ctx, const gcs_scan_inputs* in, gcs_scan_begin_outputs* out);
+int gcs_scan_finish(gcs_ctx* ctx, const gcs_lidar_evidence* ev, gcs_scan_outputs* out);
+
 /* ---------------------------------------------------------------- per-operator device entry points */
 /* parse_pointcloud2_vlp16 (FS/backend/backend_node.py:377-468) + the no-TF base transform
  * (:1677-1680) on the device, over the raw message bytes: points_dev [n*3] f64 base frame (feed

@@ -17,7 +17,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import imu_odom, ops, se3
-from .primitives import psd_project, spd_inverse_lifted
+from .primitives import psd_project, spd_inverse_lifted, spd_solve_lifted
 
 
 @dataclass
@@ -71,12 +71,9 @@ def scan_odometry(scan):
             np.asarray(scan.get("odom_twist_cov", big), np.float64))
 
 
-def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathConfig, bins, knn,
-                          map_state: MapState, L_ext=None, h_ext=None, meas_state=None, Sigma_g=None, Sigma_a=None):
-    """One hypothesis, one scan.  `scan` keys: points (N,3), timestamps, weights, imu_stamps,
-    imu_gyro, imu_accel, scan_start_time, scan_end_time, dt_sec (+ t_last_scan, t_scan, odom_pose,
-    odom_cov_se3, odom_twist, odom_twist_cov).  Sigma_g / Sigma_a default to the IW modes of
-    meas_state (datasheet state when None), as the node sets them per scan (backend_node.py:2020-2023)."""
+def _scan_prologue(belief_prev: ops.Belief, scan: dict, Q, cfg, meas_state=None, Sigma_g=None, Sigma_a=None):
+    """Steps 1-3 and the step-9 IMU/odometry branch, shared by the bin path and the live primitive
+    path (pipeline.py:399-776).  Returns the state the LiDAR evidence and the tail read."""
     certs = []   # list of dicts: influence fields + ess_total (+ name)
     # 1 PointBudgetResample (pipeline.py:399-418)
     bud = ops.point_budget_resample(scan["points"], scan["timestamps"], scan["weights"],
@@ -129,36 +126,15 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
         certs.extend(io_certs)
         io = dict(L=L_io, h=h_io, certs=io_certs, named=io_named, info=io_info, dt_int=dt_int, dt_imu=dt_imu,
                   omega_avg=omega_avg, pre_int=pre_int)
-    # 4-6 BinSoftAssign + ScanBinMomentMatch (+Kappa)
-    origin = np.asarray(cfg.lidar_origin, np.float64)
-    d = ops.point_directions(dk["points"], origin)
-    tau = cfg.temperature()
-    if cfg.mode == "dense":
-        sa = ops.bin_soft_assign_dense(d, bins, tau)
-        st = ops.scan_bin_moment_match_dense(dk["points"], dk["weights"], sa["responsibilities"], origin)
-    else:
-        sa = ops.bin_soft_assign_scale(d, bins, knn, tau)
-        st = ops.scan_bin_moment_match_scale(dk["points"], dk["weights"], sa["indices"],
-                                             sa["responsibilities"], origin, bins.shape[0])
-    cert_sa = dict(name="soft_assign", ess_total=sa["ess_total"])
-    cert_mm = dict(name="moment_match", ess_total=st["ess"], psd_projection_delta=st["psd_projection_delta"],
-                   mass_epsilon_ratio=st["mass_epsilon_ratio"])
-    # 7 MatrixFisherRotation, 8 PlanarTranslationEvidence
-    pose_pred = b_pred.mean_world_pose()
-    R_pred = se3.so3_exp(pose_pred[3:6])
-    m = map_state
-    mf = ops.matrix_fisher_rotation(R_pred, st["s_dir"], st["S_dir_scatter"], st["N"], m.stats.S_dir,
-                                    m.stats.S_dir_scatter, m.stats.N_dir)
-    pt = ops.planar_translation(pose_pred[:3], mf["R_mf"], st["p_bar"], st["Sigma_p"], st["N"], m.centroid,
-                                m.Sigma_c, m.stats.N_pos, m.stats.S_dir_scatter, m.stats.N_dir)
-    cert_mf = dict(name="mf", psd_projection_delta=mf["psd_projection_delta"],
-                   mass_epsilon_ratio=mf["mass_epsilon_ratio"])
-    cert_pt = dict(name="planar", psd_projection_delta=pt["psd_projection_delta"],
-                   mass_epsilon_ratio=pt["mass_epsilon_ratio"])
-    lidar_certs = [cert_deskew, cert_sa, cert_mm, cert_mf, cert_pt]
-    certs.extend([cert_sa, cert_mm, cert_mf, cert_pt])
-    # 9 evidence + power tempering (pipeline.py:1038-1117) + excitation scaling (:1119-1148)
-    L_lidar, h_lidar = ops.combined_lidar_evidence_22d(mf, pt)
+    return dict(certs=certs, bud=bud, b_pred=b_pred, pre=pre, xi=xi, dk=dk, cert_deskew=cert_deskew, io=io,
+                meas_dPsi=meas_dPsi, meas_dnu=meas_dnu, pose_pred=b_pred.mean_world_pose())
+
+
+def _scan_tail(st, cfg, L_lidar, h_lidar, ev_ess, ev_nll, L_ext=None, h_ext=None):
+    """Steps 9 (evidence sum, power tempering, excitation scaling) to 12 (recompose) and the process
+    IW statistics (pipeline.py:1038-1230).  ev_ess / ev_nll: support.ess_total / mismatch.nll_per_ess
+    of aggregate(LiDAR certs)."""
+    certs, io, b_pred = st["certs"], st["io"], st["b_pred"]
     L_raw = L_lidar + (0.0 if L_ext is None else L_ext) + (0.0 if io is None else io["L"])
     h_raw = h_lidar + (0.0 if h_ext is None else h_ext) + (0.0 if io is None else io["h"])
     eps = ops.EPS_MASS
@@ -167,8 +143,6 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
     dt_asym = min(max(abs(dt_vel - dt_pose) / (dt_vel + dt_pose + eps), 0.0), 1.0)
     z_to_xy = abs(L_raw[2, 2]) / (0.5 * (abs(L_raw[0, 0]) + abs(L_raw[1, 1])) + eps)
     # combined evidence cert = aggregate([aggregate(lidar certs), odom, imu, gyro]) (pipeline.py:1057-1067)
-    ev_ess = _aggregate_ess(lidar_certs)
-    ev_nll = mf["nll_per_ess"] + pt["nll_per_ess"]
     if io is None:
         ess_total, nll_total = ev_ess, ev_nll
     else:
@@ -204,20 +178,151 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
     b_rec, rinfo = ops.frobenius_recompose(b_post, T)
     certs.append(dict(name="recompose"))
     dPsi, dnu = ops.process_noise_iw_suffstats(b_pred.L, b_pred.h, b_rec.L, b_rec.h)
+    return dict(b_rec=b_rec, b_post=b_post, L_evidence=L_ev, h_evidence=h_ev, beta=beta, total_trigger=T,
+                frobenius_strength=rinfo["frobenius_strength"], z_t=b_rec.mean_world_pose(), alpha=alpha,
+                fusion_quality=quality, cond_pose6=cond6, ess_total=ess_total, nll_total=nll_total,
+                iw_process_dPsi=dPsi, iw_process_dnu=dnu)
+
+
+def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathConfig, bins, knn,
+                          map_state: MapState, L_ext=None, h_ext=None, meas_state=None, Sigma_g=None, Sigma_a=None):
+    """One hypothesis, one scan.  `scan` keys: points (N,3), timestamps, weights, imu_stamps,
+    imu_gyro, imu_accel, scan_start_time, scan_end_time, dt_sec (+ t_last_scan, t_scan, odom_pose,
+    odom_cov_se3, odom_twist, odom_twist_cov).  Sigma_g / Sigma_a default to the IW modes of
+    meas_state (datasheet state when None), as the node sets them per scan (backend_node.py:2020-2023)."""
+    st = _scan_prologue(belief_prev, scan, Q, cfg, meas_state, Sigma_g, Sigma_a)
+    certs, dk, cert_deskew = st["certs"], st["dk"], st["cert_deskew"]
+    # 4-6 BinSoftAssign + ScanBinMomentMatch (+Kappa)
+    origin = np.asarray(cfg.lidar_origin, np.float64)
+    d = ops.point_directions(dk["points"], origin)
+    tau = cfg.temperature()
+    if cfg.mode == "dense":
+        sa = ops.bin_soft_assign_dense(d, bins, tau)
+        st_b = ops.scan_bin_moment_match_dense(dk["points"], dk["weights"], sa["responsibilities"], origin)
+    else:
+        sa = ops.bin_soft_assign_scale(d, bins, knn, tau)
+        st_b = ops.scan_bin_moment_match_scale(dk["points"], dk["weights"], sa["indices"],
+                                               sa["responsibilities"], origin, bins.shape[0])
+    cert_sa = dict(name="soft_assign", ess_total=sa["ess_total"])
+    cert_mm = dict(name="moment_match", ess_total=st_b["ess"], psd_projection_delta=st_b["psd_projection_delta"],
+                   mass_epsilon_ratio=st_b["mass_epsilon_ratio"])
+    # 7 MatrixFisherRotation, 8 PlanarTranslationEvidence
+    pose_pred = st["pose_pred"]
+    R_pred = se3.so3_exp(pose_pred[3:6])
+    m = map_state
+    mf = ops.matrix_fisher_rotation(R_pred, st_b["s_dir"], st_b["S_dir_scatter"], st_b["N"], m.stats.S_dir,
+                                    m.stats.S_dir_scatter, m.stats.N_dir)
+    pt = ops.planar_translation(pose_pred[:3], mf["R_mf"], st_b["p_bar"], st_b["Sigma_p"], st_b["N"], m.centroid,
+                                m.Sigma_c, m.stats.N_pos, m.stats.S_dir_scatter, m.stats.N_dir)
+    cert_mf = dict(name="mf", psd_projection_delta=mf["psd_projection_delta"],
+                   mass_epsilon_ratio=mf["mass_epsilon_ratio"])
+    cert_pt = dict(name="planar", psd_projection_delta=pt["psd_projection_delta"],
+                   mass_epsilon_ratio=pt["mass_epsilon_ratio"])
+    lidar_certs = [cert_deskew, cert_sa, cert_mm, cert_mf, cert_pt]
+    certs.extend([cert_sa, cert_mm, cert_mf, cert_pt])
+    # 9-12 evidence, tempering, fusion, recompose
+    L_lidar, h_lidar = ops.combined_lidar_evidence_22d(mf, pt)
+    tl = _scan_tail(st, cfg, L_lidar, h_lidar, _aggregate_ess(lidar_certs), mf["nll_per_ess"] + pt["nll_per_ess"],
+                    L_ext, h_ext)
+    b_rec = tl["b_rec"]
     # 13 PoseCovInflationPushforward (map update with z_t)
-    z_t = b_rec.mean_world_pose()
+    z_t = tl["z_t"]
     cov_rec, _ = spd_inverse_lifted(b_rec.L, ops.EPS_LIFT)
-    new_stats = ops.pose_cov_inflation_pushforward(m.stats, st, z_t, cov_rec[0:6, 0:6], cfg.forgetting_factor)
+    new_stats = ops.pose_cov_inflation_pushforward(m.stats, st_b, z_t, cov_rec[0:6, 0:6], cfg.forgetting_factor)
     new_map = MapState(new_stats, *ops.map_derived_stats(new_stats))
     # 14 AnchorDriftUpdate
     b_fin, dinfo = ops.anchor_drift_update(b_rec)
     certs.append(dict(name="anchor_drift", **dinfo))
-    return dict(belief=b_fin, map=new_map, iw_process_dPsi=dPsi, iw_process_dnu=dnu,
-                iw_meas_dPsi=meas_dPsi, iw_meas_dnu=meas_dnu, budget=bud, deskew=dk, soft_assign=sa, scan_bins=st, mf=mf, planar=pt,
-                L_evidence=L_ev, h_evidence=h_ev, beta=beta, total_trigger=T,
-                frobenius_strength=rinfo["frobenius_strength"], z_t=z_t, xi_body=xi, certs=certs,
-                belief_post=b_post, belief_recomposed=b_rec, imu_odom=io, alpha=alpha, fusion_quality=quality,
-                cond_pose6=cond6, ess_total=ess_total, nll_total=nll_total)
+    return dict(belief=b_fin, map=new_map, iw_process_dPsi=tl["iw_process_dPsi"], iw_process_dnu=tl["iw_process_dnu"],
+                iw_meas_dPsi=st["meas_dPsi"], iw_meas_dnu=st["meas_dnu"], budget=st["bud"], deskew=dk, soft_assign=sa,
+                scan_bins=st_b, mf=mf, planar=pt, L_evidence=tl["L_evidence"], h_evidence=tl["h_evidence"],
+                beta=tl["beta"], total_trigger=tl["total_trigger"], frobenius_strength=tl["frobenius_strength"],
+                z_t=z_t, xi_body=st["xi"], certs=certs, belief_post=tl["b_post"], belief_recomposed=b_rec,
+                imu_odom=st["io"], alpha=tl["alpha"], fusion_quality=tl["fusion_quality"], cond_pose6=tl["cond_pose6"],
+                ess_total=tl["ess_total"], nll_total=tl["nll_total"])
+
+
+@dataclass
+class PrimitivePathConfig(BinPathConfig):
+    """The live path's map-branch parameters (PipelineConfig, FS/backend/pipeline.py:179-211, with
+    the reference constants, FS/common/constants.py:350-477)."""
+    n_surfel: int = 1024
+    n_feat: int = 512
+    m_tile: int = 50000
+    m_tile_view: int = 1024
+    h_tile: float = 2.0
+    r_active_xy: int = 1
+    r_active_z: int = 0
+    r_stencil_xy: int = 1
+    r_stencil_z: int = 0
+    k_assoc: int = 8
+    k_sinkhorn: int = 50
+    ot_epsilon: float = 0.1
+    ot_tau_a: float = 0.5
+    ot_tau_b: float = 0.5
+    k_insert_tile: int = 64
+    recency_decay_lambda: float = 0.02
+    recency_min_scale: float = 0.05
+
+
+def process_scan_primitive_path(belief_prev: ops.Belief, scan: dict, Q, cfg: PrimitivePathConfig, tiles: dict,
+                                next_global_id: int, scan_seq: int, meas_state=None, Sigma_g=None, Sigma_a=None):
+    """One hypothesis, one scan of the live pipeline (FS/backend/pipeline.py:316-1591): the shared
+    prologue, the map branch (:778-926: surfels on the deskewed budget points, recency inflation of
+    the active tiles, the view over the stencil, OT association), visual pose evidence at z_lin_pose
+    (:980-1010) as the LiDAR evidence, the shared tail (:1038-1230), step 12b at z_t (:1232-1492)
+    and AnchorDriftUpdate.  `tiles` (dict tile id -> tile) is updated in place; returns the result
+    dict with next_global_id.  The camera batch is empty (out of scope)."""
+    from . import association as OA, primitive_evidence as OE, primitive_map as OPM, surfels as OS
+    st = _scan_prologue(belief_prev, scan, Q, cfg, meas_state, Sigma_g, Sigma_a)
+    certs, dk, io, b_pred = st["certs"], st["dk"], st["io"], st["b_pred"]
+    # z_lin_pose (pipeline.py:745-755)
+    L_f = b_pred.L + (0.0 if io is None else io["L"])
+    h_f = b_pred.h + (0.0 if io is None else io["h"])
+    z_lin_pose = spd_solve_lifted(psd_project(L_f, ops.EPS_PSD)[0], h_f, ops.EPS_LIFT)[0][0:6]
+    # map branch (:778-926)
+    scfg = OS.SurfelExtractionConfig(n_surfel=cfg.n_surfel, n_feat=cfg.n_feat)
+    batch, c_surf, _ = OS.extract_lidar_surfels(dk["points"], st["bud"]["timestamps"], dk["weights"], scfg)
+    batch["n_valid"] = batch["n_camera_valid"] + batch["n_lidar_valid"]
+    centre = st["pose_pred"][:3]
+    active = OPM.ma_hex_stencil_tile_ids(centre, cfg.h_tile, cfg.r_active_xy, cfg.r_active_z)
+    stencil = OPM.ma_hex_stencil_tile_ids(centre, cfg.h_tile, cfg.r_stencil_xy, cfg.r_stencil_z)
+    infl = OPM.recency_inflate(tiles, active, scan_seq, cfg.recency_decay_lambda, cfg.recency_min_scale)
+    view = OPM.extract_atlas_map_view(tiles, stencil, cfg.m_tile_view, cfg.m_tile)
+    view.update(m_tile_view=cfg.m_tile_view)
+    acfg = OA.AssociationConfig(k_assoc=cfg.k_assoc, k_sinkhorn=cfg.k_sinkhorn, epsilon=cfg.ot_epsilon,
+                                tau_a=cfg.ot_tau_a, tau_b=cfg.ot_tau_b, h_tile=cfg.h_tile,
+                                r_stencil_tiles_xy=cfg.r_stencil_xy, r_stencil_tiles_z=cfg.r_stencil_z,
+                                scan_seq=scan_seq, recency_decay_lambda=cfg.recency_decay_lambda)
+    assoc, c_assoc = OA.associate_primitives_ot(batch, view, acfg)
+    vis = OE.visual_pose_evidence(batch, view, assoc, z_lin_pose)
+    # certificates (surfel: support only; recency inflation: exact; association: mass_epsilon_ratio;
+    # visual: lift_strength eps_lift, support = transported mass), in all_certs order
+    cert_surf = dict(name="surfel", ess_total=c_surf["ess_total"])
+    cert_infl = dict(name="recency_inflate")
+    cert_assoc = dict(name="association") if c_assoc.get("exact") else dict(
+        name="association", ess_total=c_assoc["ess_total"], mass_epsilon_ratio=c_assoc["mass_epsilon_ratio"])
+    cert_vis = dict(name="visual") if vis["exact"] else dict(name="visual", ess_total=vis["ess_total"],
+                                                               lift_strength=ops.EPS_LIFT)
+    certs.extend([cert_surf, cert_infl, cert_assoc, cert_vis])
+    lidar_certs = [st["cert_deskew"], cert_surf, cert_assoc, cert_vis]
+    tl = _scan_tail(st, cfg, vis["L_pose"], vis["h_pose"], _aggregate_ess(lidar_certs), 0.0)
+    b_rec, z_t = tl["b_rec"], tl["z_t"]
+    # 12b the primitive map update at z_t (:1232-1492)
+    next_global_id, mstats = OPM.map_update_step(tiles, next_global_id, batch, assoc, se3.so3_exp(z_t[3:6]), z_t[:3],
+                                                 active, cfg.m_tile, float(scan["scan_end_time"]), scan_seq,
+                                                 k_insert_tile=cfg.k_insert_tile, h_tile=cfg.h_tile,
+                                                 recency_decay_lambda=cfg.recency_decay_lambda)
+    # 13 AnchorDriftUpdate
+    b_fin, dinfo = ops.anchor_drift_update(b_rec)
+    certs.append(dict(name="anchor_drift", **dinfo))
+    return dict(belief=b_fin, next_global_id=next_global_id, map_update=mstats, active_tile_ids=active,
+                stencil_tile_ids=stencil, recency=infl, surfels=batch, view=view, assoc=assoc, assoc_cert=c_assoc,
+                visual=vis, z_lin_pose=z_lin_pose, iw_process_dPsi=tl["iw_process_dPsi"],
+                iw_process_dnu=tl["iw_process_dnu"], iw_meas_dPsi=st["meas_dPsi"], iw_meas_dnu=st["meas_dnu"],
+                L_evidence=tl["L_evidence"], h_evidence=tl["h_evidence"], beta=tl["beta"],
+                total_trigger=tl["total_trigger"], z_t=z_t, certs=certs, belief_recomposed=b_rec, deskew=dk,
+                budget=st["bud"], imu_odom=io, alpha=tl["alpha"], ess_total=tl["ess_total"])
 
 
 def combine_and_update_noise(results, weights, iw_state, scan_count, meas_state=None):

@@ -263,14 +263,17 @@ def test_bitwise_determinism_scale():
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("tile", [32, 64])
-def test_bin_tile_sizes_match_oracle(tile, monkeypatch):
-    """k_bins_scale's two tile shapes (32 bins x 8 lanes, chosen when the scan is dense in the map;
-    64 bins x 4 lanes) forced through GCSLAM_BIN_TILE on the same scans: ScanBinStats and the
-    scan's z_t against the oracle at the moment-match bars, and the manifest names the shape."""
+@pytest.mark.parametrize("tile,B", [(32, 20000), (64, 20000), (128, 20000), (256, 20000), (128, 60000),
+                                    (256, 60000)])
+def test_bin_tile_sizes_match_oracle(tile, B, monkeypatch):
+    """k_bins_scale's tile shapes (32 bins x 8 lanes; 64 x 4 with phase D on wave 0; 128 x 2 and
+    256 x 1 with phase D on every wave) forced through GCSLAM_BIN_TILE on the same scans, with the
+    large record stage (B = 20,000: the scan is dense in the map) and the small one (B = 60,000):
+    ScanBinStats and the scan's z_t against the oracle at the moment-match bars, and the manifest
+    names the shape."""
     monkeypatch.setenv("GCSLAM_BIN_TILE", str(tile))
     syn = _synthetic()
-    B, cap, n_raw = 20000, 8192, 8192
+    cap, n_raw = 8192, 8192
     ctx = _ctx(n_bins=B, n_points_cap=cap, mode="scale")
     assert f"{tile}-bin tiles" in ctx.describe()["backends"]["moment_match"]
     dirs, knn = ctx.atlas()
@@ -285,7 +288,11 @@ def test_bin_tile_sizes_match_oracle(tile, monkeypatch):
         rec, t, w = device_scan(sc)
         out = ctx.scan(rec, 16, t, w, n_raw, **scan_kwargs(sc), Q=Q)
         _check_scan_stats(ctx.get_scan_stats(), ref["scan_bins"])
-        assert_close(f"tile {tile} scan{k} z_t", np.array(out.z_t[:]), ref["z_t"], rtol=1e-7, atol=1e-9)
+        # B = 60,000 (0.14 points per bin): scan 0 meets an empty map, so the planar WLS is weighted by
+        # eps-level per-bin terms and amplifies last-ulp differences of the bin sums (the lane split of
+        # the gather changes their rounding) to ~5e-9 m: the B = 1024 golden's bar
+        atol = 1e-9 if B == 20000 else 5e-8
+        assert_close(f"tile {tile} scan{k} z_t", np.array(out.z_t[:]), ref["z_t"], rtol=1e-7, atol=atol)
         b, ms = ref["belief"], ref["map"]
     ctx.close()
 

@@ -37,7 +37,8 @@ def main():
     ctx.lib.gcs_debug_psd_count.argtypes = [C.c_void_p, C.c_int]
     assert ctx.lib.gcs_debug_psd_count(pc, 1) == 0
     print(f"3x3 PSD over 3 scans: non-zero inputs {pc[0]}, slow path {pc[1]}, Jacobi fallback {pc[2]}")
-    tb = 32 if "32-bin tiles" in ctx.describe()["backends"]["moment_match"] else 64
+    import re
+    tb = int(re.search(r"(\d+)-bin tiles", ctx.describe()["backends"]["moment_match"]).group(1))
     nblk = (B + tb - 1) // tb
     print(f"tile: {tb} bins")
     buf = (C.c_ulonglong * (nblk * 16))()
@@ -62,11 +63,12 @@ def main():
             print(f"  staged records mean {g[m, 8].mean():.0f} p90 {np.percentile(g[m, 8], 90):.0f} max {g[m, 8].max()}"
                   f"; bin work max mean {g[m, 9].mean():.0f} max {g[m, 9].max()}; tile work mean {g[m, 10].mean():.0f}"
                   f" p90 {np.percentile(g[m, 10], 90):.0f} p99 {np.percentile(g[m, 10], 99):.0f} max {g[m, 10].max()}")
-            ge = us(g[m][:, 11:14].max(1) - g[m][:, 4])
-            print(f"  gather end, slowest of waves 1-3 minus wave 0: mean {ge.mean():.2f} p90 {np.percentile(ge, 90):.2f}")
-            dd = us(np.diff(g[m][:, [4, 14, 15, 5]], axis=1))
-            print("  phase D split (barriers, finalize_bin, MF term) mean", np.round(dd.mean(0), 2),
-                  "p90", np.round(np.percentile(dd, 90, axis=0), 2))
+            if tb <= 64:  # phase D on wave 0 (wider tiles finalize on every wave: no hand-off stamps)
+                ge = us(g[m][:, 11:14].max(1) - g[m][:, 4])
+                print(f"  gather end, slowest of waves 1-3 minus wave 0: mean {ge.mean():.2f} p90 {np.percentile(ge, 90):.2f}")
+                dd = us(np.diff(g[m][:, [4, 14, 15, 5]], axis=1))
+                print("  phase D split (barriers, finalize_bin, MF term) mean", np.round(dd.mean(0), 2),
+                      "p90", np.round(np.percentile(dd, 90, axis=0), 2))
             big = life[m] > np.percentile(life[m], 90)
             print(f"  slowest 10%: staged mean {g[m][big, 8].mean():.0f}, max-bin work mean {g[m][big, 9].mean():.0f}, "
                   f"tile work mean {g[m][big, 10].mean():.0f}")
