@@ -10,6 +10,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cmath>
 #include <thread>
 #include <vector>
 
@@ -166,11 +167,12 @@ int grid_for_bins(int B) {
   return std::max(1, (int)ceil(2.0 / s));
 }
 
-void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& width) {
+void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& width, std::vector<float>* bounds) {
   int ncell = 6 * G * G;
   Grid g;
   g.build(dirs, B, grid_h(B, 4));
   std::vector<std::vector<int>> lists(ncell);
+  std::vector<std::vector<float>> blists(bounds ? ncell : 0);
   parallel_for(ncell, [&](int c) {
     int face = c / (G * G), iu = (c / G) % G, iv = c % G;
     double du = 2.0 / G;
@@ -194,7 +196,25 @@ void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& 
       double s = ctr[0] * dirs[3 * b] + ctr[1] * dirs[3 * b + 1] + ctr[2] * dirs[3 * b + 2];
       if (s >= cosR) L.push_back(b);
     });
-    std::sort(L.begin(), L.end());
+    if (!bounds) {
+      std::sort(L.begin(), L.end());
+      return;
+    }
+    // nearest-first order (angle from the cell centre, ties by id) with, per entry, an upper bound of
+    // the dot of any direction in the cell with that bin and every later one: a direction within rc
+    // of the centre is at least theta_b - rc from bin b, so dot <= cos(max(theta_b - rc, 0)); the
+    // bound is rounded up to float with a 1e-6 margin, so a search may stop once the next entry's
+    // bound is below its best dot (no later bin can reach or tie it)
+    std::vector<std::pair<double, int>> th(L.size());
+    for (size_t k = 0; k < L.size(); ++k) th[k] = {angle(ctr, dirs + 3 * L[k]), L[k]};
+    std::sort(th.begin(), th.end());
+    std::vector<float>& F = blists[c];
+    F.resize(L.size());
+    for (size_t k = 0; k < L.size(); ++k) {
+      L[k] = th[k].second;
+      const double bd = cos(std::max(th[k].first - rc, 0.0)) + 1e-6;
+      F[k] = std::nextafter((float)bd, 2.0f);
+    }
   });
   width = 1;
   for (auto& L : lists) width = std::max(width, (int)L.size() + 1);  // >= one -1 terminator
@@ -202,6 +222,11 @@ void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& 
   pools.assign((size_t)ncell * width, -1);
   for (int c = 0; c < ncell; ++c)
     std::copy(lists[c].begin(), lists[c].end(), pools.begin() + (size_t)c * width);
+  if (bounds) {
+    bounds->assign((size_t)ncell * width, -2.0f);  // padding: below any dot, ends the search
+    for (int c = 0; c < ncell; ++c)
+      std::copy(blists[c].begin(), blists[c].end(), bounds->begin() + (size_t)c * width);
+  }
 }
 
 namespace {

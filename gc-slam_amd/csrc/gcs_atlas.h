@@ -18,7 +18,11 @@ void knn(const double* dirs, int B, int K, int* out /*B*K*/);
 void nearest(const double* dirs, int B, int nq, const double* q, int* out);
 void reverse(const int* knn, int B, int K, std::vector<int>& off, std::vector<int>& idx);
 int grid_for_bins(int B);
-void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& width);
+// Per cube-map cell the bins that can be nearest to a direction in the cell.  bounds == nullptr:
+// ascending ids.  Otherwise nearest-first order (angle from the cell centre) and, per entry, a float
+// upper bound of the dot of any in-cell direction with that entry and every later one (-2 padding).
+void cell_pools(const double* dirs, int B, int G, std::vector<int>& pools, int& width,
+                std::vector<float>* bounds = nullptr);
 
 // Device bin order (declared layout, DESIGN.md "bin order"): bins sorted by cube face and the
 // Hilbert index of their face coordinates, so consecutive device bins form compact patches and a

@@ -64,6 +64,7 @@ struct gcs_ctx {
   int* d_rknn_off = nullptr;
   int* d_rknn = nullptr;
   int* d_pools = nullptr;
+  float* d_pool_bound = nullptr;  // per pool entry: dot upper bound of it and every later entry
   std::vector<double> dirs_host;  // reference order
   std::vector<int> knn_host;      // reference rows and ids
   // device bin order (scale mode: Hilbert patches; dense: identity); order[dev] = reference id
@@ -331,7 +332,9 @@ int upload_atlas(gcs_ctx* c) {
     c->G = atlas::grid_for_bins(B);
     c->ncell = 6 * c->G * c->G;
     // pools keep ascending reference ids (exact nearest-bin tie rule) and hold device ids
-    atlas::cell_pools(c->dirs_host.data(), B, c->G, pools, c->pool_width);
+    std::vector<float> pbound;  // nearest-first pools with early-exit bounds (k_points' nearest-bin search)
+    atlas::cell_pools(c->dirs_host.data(), B, c->G, pools, c->pool_width, &pbound);
+    if (int rc = upload(c, c->d_pool_bound, pbound)) return rc;
     for (int& id : pools)
       if (id >= 0) id = c->inv[id];
     if (int rc = upload(c, c->d_pools, pools)) return rc;
@@ -417,6 +420,8 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.knn = c->d_knn;
   a.k = c->K;
   a.pools = c->d_pools;
+  a.pool_bound = c->d_pool_bound;
+  a.bin_ref = c->d_bin_ref;
   a.pool_width = c->pool_width;
   a.grid = c->G;
   a.recs = c->d_recs;
@@ -873,7 +878,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   }
   if (c->push_stream) (void)hipStreamSynchronize(c->push_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
+  void* ptrs[] = {c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_bins_part, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,

@@ -52,7 +52,9 @@ struct PointKernelArgs {
   int n_bins;
   const int* knn;          // B x k
   int k;
-  const int* pools;        // ncell x pool_width, ascending ids, -1 padded
+  const int* pools;        // ncell x pool_width, nearest-first (angle from the cell centre), -1 padded
+  const float* pool_bound; // per entry: upper bound of the dot with it and every later entry (-2 padded)
+  const int* bin_ref;      // device id -> reference id (the nearest-bin tie rule: lower reference id)
   int pool_width, grid;
   // outputs
   PointRec* recs;

@@ -287,6 +287,12 @@ __device__ __forceinline__ void ray_dir(double px, double py, double pz, const d
 #ifndef GCS_POINT_WAVES
 #define GCS_POINT_WAVES 0  // register target (waves per SIMD) of k_points; 0: compiler default
 #endif
+#ifndef GCS_PROBE_NOPOOL
+#define GCS_PROBE_NOPOOL 0
+#endif
+#ifndef GCS_CAND_GROUP
+#define GCS_CAND_GROUP 16  // candidate direction loads in flight per group (16: all at once)
+#endif
 // KC == 0 (!SCALE): deskew only -- the live primitive path's point stage (pipeline.py:399-418,
 // 568-587): budget gather, deskew, window weights and the budget / deskew certificate partials, no
 // soft assign and no record (the surfel extraction reads p0_out / w_out / t_out).
@@ -298,6 +304,7 @@ __attribute__((amdgpu_waves_per_eu(GCS_POINT_WAVES)))
 void k_points(PointKernelArgs a, double* partials) {
   static_assert(LP == 1 || (SCALE && (LP == 2 || LP == 4) && KC % LP == 0), "lanes per point");
   constexpr int KL = KC / LP, kPB = kBlock / LP;  // candidates per lane, points per block
+  constexpr int kCandGroup = KL < GCS_CAND_GROUP ? (KL > 0 ? KL : 1) : GCS_CAND_GROUP;
   const int sub = threadIdx.x % LP;
   __shared__ double lds[kWaves * 5];
   __shared__ double s_mass[2];
@@ -349,17 +356,26 @@ void k_points(PointKernelArgs a, double* partials) {
     if constexpr (!SCALE && KC == 0) {
       // deskew only: no soft assign
     } else if constexpr (SCALE) {
-      // exact nearest atlas bin: pool of the direction's cube cell, ascending ids, strict '>'
+      // exact nearest atlas bin: the first maximum of the exact dot in reference-id order over the
+      // pool of the direction's cube cell.  The pool is nearest-first (angle from the cell centre)
+      // with a per-entry upper bound of the dot of any in-cell direction with that entry and every
+      // later one: the search stops at the first batch whose successor's bound is below the best dot
+      // (no later bin can reach or tie it), typically after one batch of 8 instead of the whole row.
       bool zero = (d[0] == 0.0 && d[1] == 0.0 && d[2] == 0.0);
       if (!zero) {
-        const int4* pool = (const int4*)(a.pools + (size_t)cube_cell(d[0], d[1], d[2], a.grid) * a.pool_width);
+        const size_t prow = (size_t)cube_cell(d[0], d[1], d[2], a.grid) * a.pool_width;
+        const int4* pool = (const int4*)(a.pools + prow);
+        const float* pbound = a.pool_bound + prow;
         const int nq = a.pool_width >> 2;
         double best = -INFINITY;
         // 4 * CH ids per batch and lane: all loads in flight together
         constexpr int CH = LP >= 4 ? 1 : 2;
-        for (int q = sub; q < nq; q += CH * LP) {
+        // GCS_PROBE_NOPOOL (timing probe, not a parity build): the first pool id only
+        for (int q = sub; q < (GCS_PROBE_NOPOOL ? 1 : nq); q += CH * LP) {
           int4 u0 = pool[q];
           int4 u1 = CH == 2 && q + LP < nq ? pool[q + LP] : make_int4(-1, -1, -1, -1);
+          const int qn = q + CH * LP;  // this lane's next batch
+          const float bnext = qn < nq ? pbound[4 * qn] : -2.0f;
           int ids[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
           double s[8];
           // branch-free: a guarded load per id compiled to one branch and one wait per id (the
@@ -372,15 +388,21 @@ void k_points(PointKernelArgs a, double* partials) {
             s[u] = ids[u] >= 0 ? sv : -INFINITY;
           }
 #pragma unroll
-          for (int u = 0; u < 4 * CH; ++u)
-            if (s[u] > best) { best = s[u]; nearest = ids[u]; }
-          if ((CH == 2 ? u1.w : u0.w) < 0) break;
+          for (int u = 0; u < 4 * CH; ++u) {
+            if (s[u] > best) {
+              best = s[u];
+              nearest = ids[u];
+            } else if (s[u] == best && ids[u] >= 0 && a.bin_ref[ids[u]] < a.bin_ref[nearest]) {
+              nearest = ids[u];  // an exact tie (measure zero): the lower reference id
+            }
+          }
+          if ((CH == 2 ? u1.w : u0.w) < 0 || (double)bnext < best) break;
         }
 #pragma unroll
-        for (int off = 1; off < LP; off <<= 1) {  // first maximum in ascending-id order
+        for (int off = 1; off < LP; off <<= 1) {  // first maximum in reference-id order
           const double ob = __shfl_xor(best, off, 64);
           const int oi = __shfl_xor(nearest, off, 64);
-          if (ob > best || (ob == best && oi < nearest)) { best = ob; nearest = oi; }
+          if (ob > best || (ob == best && a.bin_ref[oi] < a.bin_ref[nearest])) { best = ob; nearest = oi; }
         }
       }
       int cand[KL];
@@ -396,11 +418,22 @@ void k_points(PointKernelArgs a, double* partials) {
         for (int k = 0; k < KL; ++k) cand[k] = a.knn[(size_t)nearest * KC + sub * KL + k];
       }
       double e[KL];
+      // the candidates' directions in groups of GCS_CAND_GROUP loads in flight (x, y, z only: 24 B)
 #pragma unroll
-      for (int k = 0; k < KL; ++k) {
-        const double4 bd = *(const double4*)(a.bin_dirs + 4 * (size_t)cand[k]);
-        e[k] = dot3_exact(d[0], d[1], d[2], bd.x, bd.y, bd.z);
-        m = fmax(m, e[k]);
+      for (int k0 = 0; k0 < KL; k0 += kCandGroup) {
+        double3 bd[kCandGroup];
+#pragma unroll
+        for (int k = 0; k < kCandGroup; ++k) {
+          const double* p = a.bin_dirs + 4 * (size_t)cand[k0 + k];
+          const double2 xy = *(const double2*)p;
+          bd[k] = make_double3(xy.x, xy.y, p[2]);
+        }
+#pragma unroll
+        for (int k = 0; k < kCandGroup; ++k) {
+          e[k0 + k] = dot3_exact(d[0], d[1], d[2], bd[k].x, bd[k].y, bd[k].z);
+          m = fmax(m, e[k0 + k]);
+        }
+        if (kCandGroup < KL) __builtin_amdgcn_sched_barrier(0);  // keep the groups apart (registers)
       }
 #pragma unroll
       for (int off = 1; off < LP; off <<= 1) m = fmax(m, __shfl_xor(m, off, 64));

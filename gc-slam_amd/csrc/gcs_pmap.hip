@@ -198,9 +198,23 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select(const uint64_t* __restrict
     const uint32_t dmask = (1u << bits) - 1u;
     for (int i = tid; i < (1 << kSelBits); i += kPmRed) s_hist[i] = 0u;
     __syncthreads();
-    for (int q = tid; q < M; q += kPmRed) {
-      const uint64_t x = kt[q];
-      if ((x & pmask) == prefix) atomicAdd(&s_hist[(uint32_t)(x >> shift) & dmask], 1u);
+    for (int q0 = 0; q0 < M; q0 += kPmRed) {  // block-uniform trip count (the wave votes below)
+      const int q = q0 + tid;
+      const uint64_t x = q < M ? kt[q] : 0ull;
+      const bool act = q < M && (x & pmask) == prefix;
+      const uint32_t dg = (uint32_t)(x >> shift) & dmask;
+      // wave-aggregated when every counted lane has the same digit (an empty or freshly activated tile
+      // holds one key value everywhere: per-lane atomics on one LDS word serialise the whole tile)
+      const uint64_t am = __ballot(act);
+      if (am) {
+        const int l0 = __ffsll((long long)am) - 1;
+        const uint32_t d0 = (uint32_t)__shfl((int)dg, l0, 64);
+        if (__ballot(act && dg != d0) == 0ull) {
+          if (lane == l0) atomicAdd(&s_hist[d0], (uint32_t)__popcll(am));
+        } else if (act) {
+          atomicAdd(&s_hist[dg], 1u);
+        }
+      }
     }
     __syncthreads();
     if (tid < 64) {  // wave 0: the digit whose cumulative count reaches need (kSelPer bins per lane)
@@ -242,6 +256,175 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select(const uint64_t* __restrict
     const int q = c0 + tid;
     const uint64_t x = q < M ? kt[q] : ~0ull;
     const bool lt = q < M && x < prefix, eq = q < M && x == prefix;
+    const uint64_t bl = __ballot(lt), be = __ballot(eq);
+    if (lane == 0) {
+      s_wl[wid] = (uint32_t)__popcll(bl);
+      s_we[wid] = (uint32_t)__popcll(be);
+    }
+    __syncthreads();
+    uint32_t ol = 0, oe = 0, tl = 0, te = 0;
+    for (int w = 0; w < kPmRed / 64; ++w) {
+      if (w < wid) {
+        ol += s_wl[w];
+        oe += s_we[w];
+      }
+      tl += s_wl[w];
+      te += s_we[w];
+    }
+    if (lt) {
+      const uint32_t pos = base_l + ol + (uint32_t)__popcll(bl & below);
+      s_key[pos] = x;
+      s_slot[pos] = (uint32_t)q;
+    }
+    if (eq) {
+      const uint32_t r = base_e + oe + (uint32_t)__popcll(be & below);
+      if (r < need) {
+        s_key[nless + r] = x;
+        s_slot[nless + r] = (uint32_t)q;
+      }
+    }
+    base_l += tl;
+    base_e += te;
+    __syncthreads();
+  }
+  int P = 1;
+  while (P < k) P <<= 1;
+  for (int i = k + tid; i < P; i += kPmRed) {
+    s_key[i] = ~0ull;
+    s_slot[i] = ~0u;
+  }
+  for (int size = 2; size <= P; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      const int i = tid, j = tid ^ stride;
+      if (i < P && j > i) {
+        const uint64_t ki = s_key[i], kj = s_key[j];
+        const uint32_t si = s_slot[i], sj = s_slot[j];
+        const bool gt = ki > kj || (ki == kj && si > sj);
+        if (gt == ((i & size) == 0)) {
+          s_key[i] = kj;
+          s_key[j] = ki;
+          s_slot[i] = sj;
+          s_slot[j] = si;
+        }
+      }
+    }
+  __syncthreads();
+  for (int r = tid; r < k; r += kPmRed) sorted[(size_t)t * M + r] = (uint32_t)((size_t)t * M) + s_slot[r];
+}
+
+// The same select with the high 32 bits of the tile's keys held in registers (KPT per thread, slots
+// tid + j * kPmRed): one global pass loads them, the digit passes over the high word and the
+// collection run on registers and LDS; the low word is read from memory only for keys whose high word
+// equals the k-th key's (ties of the high word: typically a handful).  Histogram adds are
+// wave-aggregated when every counted lane of the wave has the same digit (an empty or freshly
+// activated tile has one key value everywhere: per-lane atomics on one LDS word serialise the tile),
+// else one LDS atomic per key.
+template <int KPT>
+__global__ __launch_bounds__(kPmRed) void k_pm_select_reg(const uint64_t* __restrict__ keys, int M, int k,
+                                                           uint32_t* __restrict__ sorted) {
+  __shared__ uint32_t s_hist[1 << kSelBits];
+  __shared__ uint64_t s_key[kSelMax];
+  __shared__ uint32_t s_slot[kSelMax];
+  __shared__ uint32_t s_wl[kPmRed / 64], s_we[kPmRed / 64];
+  __shared__ uint64_t s_prefix;
+  __shared__ uint32_t s_need;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint64_t* kt = keys + (size_t)t * M;
+  const uint32_t* kw = reinterpret_cast<const uint32_t*>(kt);  // little endian: [2q] low, [2q + 1] high word
+  uint32_t xh[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int q = tid + j * kPmRed;
+    xh[j] = q < M ? kw[2 * q + 1] : 0u;
+  }
+  uint64_t prefix = 0, pmask = 0;
+  uint32_t need = (uint32_t)k;  // rank (1-based) of T among the keys that match the prefix
+  // digits aligned to the words: 11, 11, 10 bits of the high word, then 11, 11, 10 of the low word
+  constexpr int kShift[6] = {53, 42, 32, 21, 10, 0}, kBits[6] = {11, 11, 10, 11, 11, 10};
+  for (int pass = 0; pass < 6; ++pass) {
+    const int bits = kBits[pass], shift = kShift[pass];
+    const uint32_t dmask = (1u << bits) - 1u;
+    const bool hiword = shift >= 32;  // this pass reads only high-word bits (prefix bits are high too)
+    for (int i = tid; i < (1 << kSelBits); i += kPmRed) s_hist[i] = 0u;
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int q = tid + j * kPmRed;
+      bool act = q < M;
+      uint32_t dg = 0;
+      if (hiword) {
+        act = act && (xh[j] & (uint32_t)(pmask >> 32)) == (uint32_t)(prefix >> 32);
+        dg = (xh[j] >> (shift - 32)) & dmask;
+      } else {
+        act = act && xh[j] == (uint32_t)(prefix >> 32);  // high word fixed by now: its ties only
+        if (act) {
+          const uint64_t x = ((uint64_t)xh[j] << 32) | kw[2 * q];
+          act = (x & pmask) == prefix;
+          dg = (uint32_t)(x >> shift) & dmask;
+        }
+      }
+      const uint64_t am = __ballot(act);
+      if (am) {  // wave-uniform
+        const int l0 = __ffsll((long long)am) - 1;
+        const uint32_t d0 = (uint32_t)__shfl((int)dg, l0, 64);
+        if (__ballot(act && dg != d0) == 0ull) {
+          if (lane == l0) atomicAdd(&s_hist[d0], (uint32_t)__popcll(am));
+        } else if (act) {
+          atomicAdd(&s_hist[dg], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < 64) {  // wave 0: the digit whose cumulative count reaches need (kSelPer bins per lane)
+      constexpr int kSelPer = (1 << kSelBits) / 64;
+      uint32_t sum = 0;
+      for (int j = 0; j < kSelPer; ++j) sum += s_hist[kSelPer * tid + j];
+      uint32_t inc = sum;
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+      }
+      const uint32_t exc = inc - sum;
+      if (exc < need && inc >= need) {
+        uint32_t c = exc;
+        int d = kSelPer * tid;
+        for (int j = 0; j < kSelPer; ++j) {
+          const uint32_t h = s_hist[kSelPer * tid + j];
+          if (c + h >= need) {
+            d = kSelPer * tid + j;
+            break;
+          }
+          c += h;
+        }
+        s_need = need - c;
+        s_prefix = prefix | ((uint64_t)d << shift);
+      }
+    }
+    __syncthreads();
+    need = s_need;
+    prefix = s_prefix;
+    pmask |= (uint64_t)dmask << shift;
+    __syncthreads();
+  }
+  // keys < T: exactly k - need of them; keys == T: the first `need` in slot order (slots ascend with j
+  // within a thread and with the thread within a chunk of kPmRed slots)
+  const uint32_t nless = (uint32_t)k - need;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const uint32_t th = (uint32_t)(prefix >> 32);
+  uint32_t base_l = 0, base_e = 0;
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    const int q = tid + j * kPmRed;
+    bool lt = q < M && xh[j] < th, eq = false;
+    uint64_t x = (uint64_t)xh[j] << 32;
+    if (q < M && xh[j] == th) {  // high-word tie: the full key decides
+      x |= kw[2 * q];
+      lt = x < prefix;
+      eq = x == prefix;
+    } else if (lt) {
+      x |= kw[2 * q];
+    }
     const uint64_t bl = __ballot(lt), be = __ballot(eq);
     if (lane == 0) {
       s_wl[wid] = (uint32_t)__popcll(bl);
@@ -1184,7 +1367,16 @@ int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam, int k) {
     return e && e[0] == '1';
   }();
   if (k >= 1 && k <= kSelMax && !full) {
-    hipLaunchKernelGGL(k_pm_select, dim3(n), dim3(kPmRed), 0, p->stream, (const uint64_t*)p->keys, p->M, k, p->vals);
+    // high key words in registers up to 8 per thread (M <= 8,192; 52 per thread spills at 1024 threads)
+    static const bool glob = [] {
+      const char* e = getenv("GCSLAM_PM_SELECT_GLOBAL");  // A/B: the global-memory passes
+      return e && e[0] == '1';
+    }();
+    const uint64_t* kk = (const uint64_t*)p->keys;
+    if (!glob && p->M <= 8 * kPmRed)
+      hipLaunchKernelGGL(k_pm_select_reg<8>, dim3(n), dim3(kPmRed), 0, p->stream, kk, p->M, k, p->vals);
+    else
+      hipLaunchKernelGGL(k_pm_select, dim3(n), dim3(kPmRed), 0, p->stream, kk, p->M, k, p->vals);
     PMCHK(p, hipGetLastError());
     return GCS_OK;
   }

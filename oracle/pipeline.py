@@ -31,6 +31,9 @@ class BinPathConfig:
     deskew_rotation_only: bool = False
     forgetting_factor: float = ops.FORGETTING_FACTOR
     gravity_W: tuple = ops.GRAVITY_W
+    # sensitivity of the declared pushforward inflation form: the pose
+    # covariance J Sigma J^T enters scaled by this factor (1.0: the declared form)
+    pushforward_inflation_scale: float = 1.0
     # step 9 IMU/odometry family (PipelineConfig, FS/backend/pipeline.py:96-223)
     use_imu_odom: bool = True
     planar_z_ref: float = imu_odom.PLANAR_Z_REF
@@ -228,7 +231,8 @@ def process_scan_bin_path(belief_prev: ops.Belief, scan: dict, Q, cfg: BinPathCo
     # 13 PoseCovInflationPushforward (map update with z_t)
     z_t = tl["z_t"]
     cov_rec, _ = spd_inverse_lifted(b_rec.L, ops.EPS_LIFT)
-    new_stats = ops.pose_cov_inflation_pushforward(m.stats, st_b, z_t, cov_rec[0:6, 0:6], cfg.forgetting_factor)
+    new_stats = ops.pose_cov_inflation_pushforward(m.stats, st_b, z_t, cfg.pushforward_inflation_scale * cov_rec[0:6, 0:6],
+                                                   cfg.forgetting_factor)
     new_map = MapState(new_stats, *ops.map_derived_stats(new_stats))
     # 14 AnchorDriftUpdate
     b_fin, dinfo = ops.anchor_drift_update(b_rec)
@@ -266,13 +270,18 @@ class PrimitivePathConfig(BinPathConfig):
 
 
 def process_scan_primitive_path(belief_prev: ops.Belief, scan: dict, Q, cfg: PrimitivePathConfig, tiles: dict,
-                                next_global_id: int, scan_seq: int, meas_state=None, Sigma_g=None, Sigma_a=None):
+                                next_global_id: int, scan_seq: int, meas_state=None, Sigma_g=None, Sigma_a=None,
+                                batch=None):
     """One hypothesis, one scan of the live pipeline (FS/backend/pipeline.py:316-1591): the shared
     prologue, the map branch (:778-926: surfels on the deskewed budget points, recency inflation of
     the active tiles, the view over the stencil, OT association), visual pose evidence at z_lin_pose
     (:980-1010) as the LiDAR evidence, the shared tail (:1038-1230), step 12b at z_t (:1232-1492)
     and AnchorDriftUpdate.  `tiles` (dict tile id -> tile) is updated in place; returns the result
-    dict with next_global_id.  The camera batch is empty (out of scope)."""
+    dict with next_global_id.  The camera batch is empty (out of scope).  batch: a MeasurementBatch
+    dict to use instead of this oracle's surfel extraction (a plane fit whose two smallest
+    eigenvalues coincide -- cells of two or three collinear points -- has no unique normal, and
+    lidar_surfel_extraction.py:129-130 then orients it by the sign of a rounding-level z component,
+    so a closed-loop check feeds both sides the same batch and checks the extraction on its own)."""
     from . import association as OA, primitive_evidence as OE, primitive_map as OPM, surfels as OS
     st = _scan_prologue(belief_prev, scan, Q, cfg, meas_state, Sigma_g, Sigma_a)
     certs, dk, io, b_pred = st["certs"], st["dk"], st["io"], st["b_pred"]
@@ -282,8 +291,12 @@ def process_scan_primitive_path(belief_prev: ops.Belief, scan: dict, Q, cfg: Pri
     z_lin_pose = spd_solve_lifted(psd_project(L_f, ops.EPS_PSD)[0], h_f, ops.EPS_LIFT)[0][0:6]
     # map branch (:778-926)
     scfg = OS.SurfelExtractionConfig(n_surfel=cfg.n_surfel, n_feat=cfg.n_feat)
-    batch, c_surf, _ = OS.extract_lidar_surfels(dk["points"], st["bud"]["timestamps"], dk["weights"], scfg)
-    batch["n_valid"] = batch["n_camera_valid"] + batch["n_lidar_valid"]
+    if batch is None:
+        batch, c_surf, _ = OS.extract_lidar_surfels(dk["points"], st["bud"]["timestamps"], dk["weights"], scfg)
+        batch["n_valid"] = batch["n_camera_valid"] + batch["n_lidar_valid"]
+    else:
+        nv = int(batch["n_valid"])
+        c_surf = dict(ess_total=float(nv), support_frac=float(nv) / float(max(cfg.n_surfel, 1)))
     centre = st["pose_pred"][:3]
     active = OPM.ma_hex_stencil_tile_ids(centre, cfg.h_tile, cfg.r_active_xy, cfg.r_active_z)
     stencil = OPM.ma_hex_stencil_tile_ids(centre, cfg.h_tile, cfg.r_stencil_xy, cfg.r_stencil_z)

@@ -98,6 +98,37 @@ def test_c3_subsample_point_stage_and_moment_match():
     ctx.close()
 
 
+def test_c3_full_scans_value_parity():
+    """BASELINE.json configs[2] at full size: two consecutive 262,144-point scans against a
+    1,048,576-bin map from the identity prior (the second meets the map the first pushed), each against
+    oracle.pipeline.process_scan_bin_path: z_t, X_anchor, L, every bin's ScanBinStats and the map."""
+    syn = _synthetic()
+    N, B = 262144, 1048576
+    ctx = _ctx(n_bins=B, n_points_cap=N, mode="scale", k_cand=16)
+    dirs, knn = ctx.atlas()
+    cfg = opipe.BinPathConfig(n_points_cap=N, n_bins=B, mode="scale", lidar_origin=ORIGIN, tau=ctx.cfg.tau)
+    b = ops.Belief.identity_prior()
+    Q = ops.process_noise_Q(*ops.datasheet_process_noise_state())
+    ms = opipe.MapState.empty(B)
+    amp = max(1.0, 10 * 2.2e-16 / ctx.cfg.tau / 1e-11)   # tau = 4.6e-6 (see the subsample test)
+    for k in range(2):
+        sc = syn.make_scan(N, 80 + k)
+        ref = opipe.process_scan_bin_path(b, sc, Q, cfg, dirs, knn, ms)
+        rec, t, w = device_scan(sc)
+        out = ctx.scan(rec, 16, t, w, N, **scan_kwargs(sc), Q=Q)
+        X, _, z, Lm, h = ctx.get_belief()
+        # scan 0 meets an empty map: the planar WLS is eps-weighted (DESIGN.md section 3): 5e-8 m
+        assert_close(f"C3 scan{k} z_t", np.array(out.z_t[:]), ref["z_t"], rtol=1e-7, atol=5e-8)
+        assert_close(f"C3 scan{k} X_anchor", X, ref["belief"].X_anchor, rtol=1e-7, atol=5e-8)
+        assert_close(f"C3 scan{k} L", Lm, ref["belief"].L, rtol=1e-5, atol=1e-7 * np.abs(ref["belief"].L).max())
+        _check_scan_stats(ctx.get_scan_stats(), ref["scan_bins"], amp=amp)
+        m_dev, _ = ctx.get_map()
+        mref = map_fields(ref["map"].stats)
+        assert_close(f"C3 scan{k} map", m_dev, mref, rtol=1e-7 * amp, atol=1e-9 * max(np.abs(mref).max(), 1.0))
+        b, ms = ref["belief"], ref["map"]
+    ctx.close()
+
+
 def test_scan_lookback_failure_is_reported():
     """k_scan's bounded look-back spin: when it runs out the scan fails loudly (GCS_ERR_HIP ->
     RuntimeError) instead of returning results built on wrong bucket starts; the next scan is

@@ -335,3 +335,95 @@ def test_view_sparse_and_empty_tiles():
         assert np.array_equal(cpu(getattr(g, f)), v[f]), f
     np.testing.assert_allclose(cpu(g.positions), v["positions"], rtol=1e-12, atol=1e-12)
     am.close()
+
+
+def test_reference_size_view_and_map_update():
+    """The reference's map sizes (GC_M_TILE = 50,000 slots, GC_M_TILE_VIEW = 1,024, 7 active tiles,
+    constants.py:392,436-439; N = 512 + 1,024 measurement rows, K = 8, constants.py:350-356): the view's
+    per-tile top-k (k_pm_select over 50,000 keys, ties and an empty tile whose keys are all equal
+    included) and step 12b with novelty insertion into populated tiles (eviction order by the same
+    select) against the oracle."""
+    from types import SimpleNamespace
+    from gcslam import primitive_map as gpm
+    from oracle import se3
+    rng = np.random.default_rng(50)
+    m, N, K, kv = 50_000, 1536, 8, 1024
+    z = np.array([0.9, -0.4, 0.2, 0.01, -0.02, 0.3])
+    R, t = se3.so3_exp(z[3:]), z[:3]
+    p_body = rng.uniform(-5, 5, size=(N, 3))
+    A = rng.normal(size=(N, 3, 3)) * 0.2
+    Lam = np.einsum("nij,nkj->nik", A, A) + np.eye(3)[None] * rng.uniform(1, 5, size=(N, 1, 1))
+    batch = dict(Lambdas=Lam, thetas=np.einsum("nij,nj->ni", Lam, p_body), etas=rng.normal(size=(N, NL, 3)),
+                 weights=rng.random(N), valid_mask=rng.random(N) < 0.9, colors=rng.random((N, 3)),
+                 sources=rng.integers(0, 2, N).astype(np.int32))
+    wtid = opm.tile_ids_from_xyz(p_body @ R.T + t[None], 2.0)
+    uniq, cnts = np.unique(wtid, return_counts=True)
+    active = [int(x) for x in uniq[np.argsort(-cnts, kind="stable")][:7]]
+    assert len(active) == 7
+    tiles = {}
+    for i, tid in enumerate(active[:6]):   # five populated tiles (one full), one empty; the 7th is absent
+        tiles[tid] = _rand_tile(rng, m=m, frac=(0.0 if i == 5 else 0.999 if i == 0 else 0.8), seq_hi=30)
+    am = gpm.AtlasMap(m_tile=m, max_tiles=16, n_lobes=NL, max_merge=0)
+    for tid, tt in tiles.items():
+        am.write_tile(tid, tt)
+    am.next_global_id = 10 * m
+    view = gpm.extract_atlas_map_view(am, active, kv)
+    v = opm.extract_atlas_map_view(tiles, active, kv, m)
+    cpu = lambda x: x.detach().cpu().numpy()  # noqa: E731
+    for f in ("candidate_slots", "candidate_tile_ids", "valid_mask", "primitive_ids", "weights"):
+        assert np.array_equal(cpu(getattr(view, f)), v[f]), f
+    np.testing.assert_allclose(cpu(view.positions), v["positions"], rtol=1e-12, atol=1e-12)
+    ctile = rng.choice(np.array(active + [777], dtype=np.int64), size=(N, K))
+    assoc = dict(responsibilities=rng.random((N, K)) / K, candidate_tile_ids=ctile,
+                 candidate_slots=rng.integers(0, m, size=(N, K)), row_masses=rng.random(N) * 2.0 / N)
+    nxt_ref, st_ref = opm.map_update_step(tiles, 10 * m, batch, assoc, R, t, active, m, 4.0, 31, k_insert_tile=64,
+                                          h_tile=2.0)
+    st = gpm.primitive_map_update(am, SimpleNamespace(**batch), SimpleNamespace(**assoc), z, active, 4.0, 31)
+    assert am.next_global_id == nxt_ref
+    for k in ("fused_count", "insert_count_total", "evicted_count", "merged_count"):
+        assert st[k] == st_ref[k], k
+    for k in ("fused_mass_total", "insert_mass_total", "insert_mass_p95", "evicted_mass_total"):
+        assert st[k] == pytest.approx(st_ref[k], rel=1e-12, abs=1e-300), k
+    for tid in active:
+        _same_tile(am.read_tile(tid), tiles[tid], rtol=1e-11, what=f"tile {tid}")
+        assert am.counts[tid] == int(tiles[tid]["valid_mask"].sum())
+    assert st_ref["insert_count_total"] > 0
+    am.close()
+
+
+def _full_sort_check():
+    """Run in a subprocess with GCSLAM_PM_FULLSORT=1 (the knob is read once per process): the view's
+    and the insert's rocPRIM full-sort path against the oracle."""
+    rng = np.random.default_rng(3)
+    tiles = {5: _rand_tile(rng), 6: _rand_tile(rng, frac=0.1)}
+    am = _map(tiles)
+    from gcslam import primitive_map as gpm
+    v = opm.extract_atlas_map_view(tiles, [5, 6], 1024, M)
+    g = gpm.extract_atlas_map_view(am, [5, 6], 1024)
+    for f in ("candidate_slots", "candidate_tile_ids", "valid_mask", "primitive_ids", "weights"):
+        assert np.array_equal(getattr(g, f).cpu().numpy(), v[f]), f
+    K = 64
+    P = dict(L=rng.normal(size=(1, K, 3, 3)), th=rng.normal(size=(1, K, 3)), e=rng.normal(size=(1, K, NL, 3)),
+             w=rng.random((1, K)), v=rng.random((1, K)) < 0.7)
+    am.next_global_id = 500
+    res = gpm.primitive_map_insert_masked_tiles(am, [5], P["L"], P["th"], P["e"], P["w"], 2.5, P["v"], scan_seq=40)
+    n, ids, _, _ = opm.insert_masked(tiles[5], 500, P["L"][0], P["th"][0], P["e"][0], P["w"][0], 2.5, P["v"][0],
+                                     scan_seq=40)
+    assert res[0][0].n_inserted == n and np.array_equal(res[0][0].new_ids.cpu().numpy(), ids)
+    _same_tile(am.read_tile(5), tiles[5], what="full-sort insert")
+    am.close()
+
+
+def test_full_sort_path_matches_oracle():
+    """The select is the default for k <= 1024; the rocPRIM full sort (GCSLAM_PM_FULLSORT=1, or k above
+    the select's capacity) keeps its own parity check."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_primitive_map as t; t._full_sort_check()"
+            % (here, root, os.path.join(root, "gc-slam_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, GCSLAM_PM_FULLSORT="1"),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]

@@ -12,6 +12,7 @@
 #   pmap         primitive-map timing (tools/pmap_bench.py)    assoc   association timing
 #   ab           same-box A/B of two builds: A = libgcslam_hip.so, B = libgcslam_hip_$B.so
 #   envab        same-box A/B of an environment knob: B runs with $ENVB
+#   sweep        bench C2 + C3 per entry of SWEEP="name:lib_suffix:ENV=V,... ..." (library variants / knobs)
 # Env: O (output dir, default gpurun_out/run), REPS (A/B alternations), PYTEST_K (pytest -k filter).
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
 export TMPDIR=/tmp
@@ -69,6 +70,15 @@ step() {
             > "$O/envab_${v}_c2_$rep.log" 2>&1 || return $?
           env $e timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline \
             > "$O/envab_${v}_c3_$rep.log" 2>&1 || return $?
+        done
+      done ;;
+    sweep)  # SWEEP="name:lib_suffix:ENV=V,ENV2=V2 ..." (lib_suffix '-' = the default library)
+      for spec in $SWEEP; do
+        IFS=: read -r name suf envs <<< "$spec"
+        lib=gc-slam_amd/gcslam/libgcslam_hip.so; [ "$suf" != "-" ] && lib=gc-slam_amd/gcslam/libgcslam_hip_$suf.so
+        e="GCSLAM_LIB=$PWD/$lib ${envs//,/ }"
+        for cfg in ${SWEEP_CONFIGS:-c2 c3}; do
+          env $e timeout -k 10 300 python bench.py --config $cfg --steps ${SWEEP_STEPS:-60} --warmup 5 --no-cpu-baseline             --no-c3 > "$O/sweep_${name}_$cfg.log" 2>&1 || return $?
         done
       done ;;
     *) echo "unknown step $1" >&2; return 2 ;;
