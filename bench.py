@@ -420,7 +420,7 @@ def main():
     torch.cuda.set_device(local_rank)
 
     from gcslam import _lib as L
-    from gcslam.distributed import HypothesisComm, combine_allreduce
+    from gcslam.distributed import HypothesisComm
     from gcslam.synthetic import scan_kwargs
 
     # the per-scan exchange runs in the library over RCCL (torch.distributed only broadcasts the id)
@@ -442,7 +442,15 @@ def main():
     X0 = np.concatenate([rng.normal(0, 0.05, 3) * (rank > 0), rng.normal(0, np.deg2rad(0.5), 3) * (rank > 0)])
     ctx.set_belief(X0, 0.0, np.zeros(22), 1e-6 * np.eye(22), np.zeros(22))
     scans = resident_scans(N, device)
-    scan_kw = [scan_kwargs(sc) for sc, _, _, _ in scans]  # the per-scan host arguments, built once
+    # each resident scan's gcs_scan_inputs (device pointers + its host IMU / odometry arrays) filled
+    # once, as a C caller fills the struct per scan; the step is then one C-ABI call
+    prepared = [ctx.prepare_scan(rec, 16, t, w, N, **scan_kwargs(sc)) for sc, rec, t, w in scans]
+    from gcslam.distributed import hypothesis_weights
+    w_iw, w_bary = (float(x[rank]) for x in hypothesis_weights(world))
+    comm_h = comm.h if comm is not None else None
+
+    def combine(count):  # gcs_combine_allreduce: RCCL sum of the payload (N > 1) + combine + IW updates
+        return ctx.combine_allreduce(comm_h, w_iw, w_bary, count, want_belief=False)
 
     state = dict(count=0, sample=False, sampled=0)
     scan_out = L.GcsScanOutputs()  # one output record for every scan (the caller-owned buffer form)
@@ -457,12 +465,10 @@ def main():
                 ctx.enable_timing(True, stages=["bins"])
             elif phase == 1:
                 ctx.enable_timing(False)
-        i = state["count"] % N_SCANS
-        _, rec, t, w = scans[i]
-        out = ctx.scan(rec, 16, t, w, N, out=scan_out, **scan_kw[i])
+        out = ctx.scan_prepared(prepared[state["count"] % N_SCANS], scan_out)
         if state["count"] % TIMING_STRIDE == TIMING_STRIDE // 2:  # host sub-spans: sampled scans without event stamps
             tc = time.perf_counter()
-            combine_allreduce(ctx, rank, world, state["count"], comm=comm, want_belief=False)
+            combine(state["count"])
             host_ms[4] += (time.perf_counter() - tc) * 1e3
             sm = out.stage_ms
             for k in range(4):
@@ -470,7 +476,7 @@ def main():
                 host_ms[5 + k] += sm[4 + k]
             state["sampled"] += 1
         else:
-            combine_allreduce(ctx, rank, world, state["count"], comm=comm, want_belief=False)
+            combine(state["count"])
         state["count"] += 1
 
     for _ in range(args.warmup):

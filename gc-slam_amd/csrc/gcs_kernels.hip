@@ -290,6 +290,12 @@ __device__ __forceinline__ void ray_dir(double px, double py, double pz, const d
 #ifndef GCS_PROBE_NOPOOL
 #define GCS_PROBE_NOPOOL 0
 #endif
+#ifndef GCS_PROBE_NOFLAGS
+#define GCS_PROBE_NOFLAGS 0  // timing probe (not a parity build): no first-arrival flag stores
+#endif
+#ifndef GCS_TILE_DEDUP
+#define GCS_TILE_DEDUP 1
+#endif
 #ifndef GCS_CAND_GROUP
 #define GCS_CAND_GROUP 16  // candidate direction loads in flight per group (16: all at once)
 #endif
@@ -473,25 +479,36 @@ void k_points(PointKernelArgs a, double* partials) {
         // bucket slot: arrival order only (re-ranked by point index by k_bucket_rank, or by the bin
         // kernel's staging for the direct buckets)
         const uint32_t sl = atomicAdd(a.counts + nearest, 1u);
-        a.slots[i] = sl;
         key = (uint32_t)nearest;
         if (a.members) {
+          // direct buckets: slots / keys only feed the sorted bucketing (an overflowing scan is
+          // redone from k_points with members == nullptr), so they are not written here
           if (sl < (uint32_t)a.capb) a.members[(size_t)nearest * a.capb + sl] = (uint32_t)i;
           else *a.overflow = 1u;  // vector store to host-mapped memory; gcs_scan redoes the scan sorted
-          if (sl == 0u) {  // the bucket's first arrival marks its candidate bins and their tiles
-            const int* kr = a.knn + (size_t)nearest * a.k;
+          if (!GCS_PROBE_NOFLAGS && sl == 0u) {  // first arrival: mark the candidate bins and their tiles
+            const int ts = a.tile_shift;
             uint8_t* tf = a.flags + a.n_bins;
+            // the row's candidates mostly share one or two tiles (Hilbert-ordered bins): a tile flag
+            // is stored only at its first occurrence in the row (each byte store is its own L2
+            // transaction)
+            int row[KC], tl[KC];
 #pragma unroll
-            for (int q = 0; q < KC; q += 4) {
-              const int4 c4 = *(const int4*)(kr + q);
-              a.flags[c4.x] = 1; a.flags[c4.y] = 1; a.flags[c4.z] = 1; a.flags[c4.w] = 1;
-              const int ts = a.tile_shift;
-              tf[c4.x >> ts] = 1; tf[c4.y >> ts] = 1; tf[c4.z >> ts] = 1; tf[c4.w >> ts] = 1;
+            for (int k = 0; k < KC; ++k) row[k] = LP == 1 ? cand[k % KL] : a.knn[(size_t)nearest * KC + k];
+#pragma unroll
+            for (int k = 0; k < KC; ++k) {
+              a.flags[row[k]] = 1;
+              tl[k] = row[k] >> ts;
+              bool seen = false;
+#pragma unroll
+              for (int j = 0; j < k; ++j) seen |= GCS_TILE_DEDUP && tl[j] == tl[k];
+              if (!seen) tf[tl[k]] = 1;
             }
           }
+        } else {
+          a.slots[i] = sl;
         }
       }
-      if (live && sub == 0) a.keys[i] = key;
+      if (live && sub == 0 && !a.members) a.keys[i] = key;
       Z = iz;
     } else {
       for (int b = 0; b < a.n_bins; ++b) {
@@ -2006,9 +2023,11 @@ int bins_tile_for(long cap, int n_bins) {
     const int v = atoi(e);
     if (v == 32 || v == 64 || v == 128 || v == 256) return v;
   }
-  (void)cap;
-  (void)n_bins;
-  return 64;
+  // Sparse maps (under 2.5 points per bin, C3: 262,144 points over 1,048,576 bins) run 128-bin tiles:
+  // half the tiles, each amortising its table phase over twice the bins (C3 bins 88 vs 106 us, sweep
+  // profiles/r03/sweep_tile.txt).  Dense maps (C2: 20,000 bins, 8.5 points each) keep 64-bin tiles, whose
+  // stage fits the heavier per-bin record load (25.5 vs 30.5 us).
+  return (long)cap * 5 < (long)n_bins * 2 ? 128 : 64;
 }
 int bins_scale_blocks(int n_bins, int tile_bins) { return (n_bins + tile_bins - 1) / tile_bins; }
 int bins_partial_nv() { return kBinNV; }

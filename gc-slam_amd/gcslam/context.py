@@ -306,6 +306,20 @@ class HypothesisContext:
         self._chk(self.lib.gcs_scan_finish(self.h, C.byref(ev), C.byref(out)), "gcs_scan_finish")
         return out
 
+    def prepare_scan(self, *args, **kw):
+        """The gcs_scan_inputs of one scan (same arguments as scan()), built once: a caller that holds a
+        scan's host arrays fills the C struct once and hands it to scan_prepared (a C caller fills it in
+        a few hundred nanoseconds; ctypes takes microseconds per field)."""
+        inp, keep = self._scan_inputs(*args, **kw)
+        return (inp, C.byref(inp), keep)
+
+    def scan_prepared(self, prepared, out):
+        """gcs_scan on a prepare_scan() struct into a caller-owned GcsScanOutputs (one ctypes call)."""
+        rc = self.lib.gcs_scan(self.h, prepared[1], C.byref(out))
+        if rc:
+            self._chk(rc, "gcs_scan")
+        return out
+
     def scan(self, xyz_dev, point_step, t_dev, w_dev, n_points, imu_stamps, imu_gyro, imu_accel,
              scan_start_time, scan_end_time, dt_sec, Q=None, L_ext=None, h_ext=None, t_last_scan=None, t_scan=None,
              xyz_f64=False, odom_pose=None, odom_cov_se3=None, odom_twist=None, odom_twist_cov=None, Sigma_g=None,
