@@ -101,6 +101,11 @@ struct gcs_ctx {
   int flags_cur = 0;
   uint8_t* d_touched = nullptr;     // per bin: the map holds mass (k_map_derive / k_pushforward)
   uint8_t* d_tile_dirty = nullptr;  // k_bins_scale: tile output not the zero-bin values (persistent)
+  // multi-round bin grids (C3): block -> tile order built after each pushforward (k_tile_order) from
+  // the scan's active tiles and their staged records (d_tile_work); GCSLAM_TILE_ORDER=0: identity
+  int* d_tile_order = nullptr;
+  uint32_t* d_tile_work = nullptr;
+  bool tile_order_on = false;
   double* d_bins_part = nullptr;    // k_bins_scale partial rows (persistent: clean tiles keep theirs)
   double* d_scan = nullptr;
   double* d_map = nullptr;
@@ -116,6 +121,9 @@ struct gcs_ctx {
   // bucketing kernels; the main stream waits for ev_push before the next bin kernel (join)
   hipStream_t push_stream = nullptr;
   hipEvent_t ev_push = nullptr;
+  // recorded on the main stream behind the scan's device stages; the pushforward's stream waits for
+  // it (wait_mirror returns before the main stream is idle)
+  hipEvent_t ev_stages = nullptr;
   bool push_pending = false;
   bool push_main = false;  // experiment knob (GCSLAM_PUSH_MAIN=1): k_pushforward on the main stream
   // Asynchronous pushforward launch (GCSLAM_PUSH_THREAD=0 turns it off): the launch calls of
@@ -469,6 +477,8 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   b.counts = c->d_counts;
   b.flags = c->d_flags;
   b.tile_dirty = c->d_tile_dirty;
+  b.tile_order = c->d_tile_order;
+  b.tile_work = c->d_tile_work;
   b.rknn_off = c->d_rknn_off;
   b.rknn = c->d_rknn;
   b.rknn_local = c->d_rknn_local;
@@ -539,10 +549,39 @@ int stage_mf(gcs_ctx* c) {
 
 // to_host: the fold also writes the whole scalar block into the mapped host mirror (the scan
 // then only synchronizes; per-operator calls copy with pull_scalars)
+// Wait for the scan's device stages: poll the mapped ready word the PT fold writes after its
+// mirror of the scalars (a stream synchronize returns some microseconds after the kernel ends).
+// Nothing later in the scan reads device memory outside stream order, so the stream is not
+// synchronized once the word is seen; without it after 20 ms (a fault, or a stalled queue) the
+// stream synchronize waits and reports the asynchronous error.  GCSLAM_SYNC_WAIT=stream:
+// synchronize only.
+int wait_mirror(gcs_ctx* c) {
+  static const bool spin = [] {
+    const char* e = getenv("GCSLAM_SYNC_WAIT");
+    return !(e && strcmp(e, "stream") == 0);
+  }();
+  if (spin) {
+    volatile double* ready = c->h_scalars + SC_COUNT;
+    const auto t0 = clk::now();
+    while (*ready == 0.0) {
+      __builtin_ia32_pause();
+      if (clk::now() - t0 > std::chrono::milliseconds(20)) break;
+    }
+    if (*ready != 0.0) {
+      std::atomic_thread_fence(std::memory_order_acquire);
+      return GCS_OK;
+    }
+  }
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
 int stage_pt(gcs_ctx* c, bool to_host = false) {
   StageEv ev = stage_ev(c, ST_PT);
+  if (to_host) c->h_scalars[SC_COUNT] = 0.0;  // re-armed: the fold writes 1 after the mirror
   HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
                       to_host ? c->d_scalars_mirror : nullptr, c->d_flags, c->d_touched, c->stream, ev.e0, ev.e1));
+  if (to_host) HIPCHK(c, hipEventRecord(c->ev_stages, c->stream));
   return GCS_OK;
 }
 
@@ -568,8 +607,12 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, 
     for (int j = 0; j < 3; ++j) pa.G[3 * i + j] = RS[3 * i] * pa.R[3 * j] + RS[3 * i + 1] * pa.R[3 * j + 1] + RS[3 * i + 2] * pa.R[3 * j + 2];
   pa.gamma = gamma;
   StageEv ev = stage_ev(c, ST_PUSH);
+  if (s != c->stream) HIPCHK(ec, hipStreamWaitEvent(s, c->ev_stages, 0));
   HIPCHK(ec, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, partials, c->d_scalars, flags,
                                c->d_touched, s, ev.e0, ev.e1));
+  if (c->tile_order_on)
+    HIPCHK(ec, launch_tile_order(c->d_tile_dirty, c->d_tile_work, bins_scale_blocks(c->B, c->tile_bins),
+                                 c->d_tile_order, s));
   if (s != c->stream) {
     HIPCHK(ec, hipEventRecord(c->ev_push, s));
     c->push_pending = true;
@@ -781,6 +824,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   c->own_stream = true;
   if (bad(hipStreamCreateWithFlags(&c->push_stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
   if (bad(hipEventCreateWithFlags(&c->ev_push, hipEventDisableTiming))) return GCS_ERR_HIP;
+  if (bad(hipEventCreateWithFlags(&c->ev_stages, hipEventDisableTiming))) return GCS_ERR_HIP;
   if (const char* pm = getenv("GCSLAM_PUSH_MAIN")) c->push_main = atoi(pm) != 0;
   if (const char* pt = getenv("GCSLAM_PUSH_THREAD")) c->push_async = atoi(pt) != 0;
   if (const char* sb = getenv("GCSLAM_SORTED_BUCKETS")) c->direct_buckets = atoi(sb) == 0;
@@ -808,7 +852,9 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_tickets, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_parse_flag, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_tickets, 0, sizeof(uint32_t)))) return GCS_ERR_HIP;
-  if (bad(hipHostMalloc(&c->h_scalars, SC_COUNT * sizeof(double), hipHostMallocMapped))) return GCS_ERR_HIP;
+  // SC_COUNT scalars + the ready word k_final<.., mirror> writes last (wait_mirror)
+  if (bad(hipHostMalloc(&c->h_scalars, (SC_COUNT + 8) * sizeof(double), hipHostMallocMapped))) return GCS_ERR_HIP;
+  c->h_scalars[SC_COUNT] = 0.0;
   if (bad(hipHostGetDevicePointer((void**)&c->d_scalars_mirror, c->h_scalars, 0))) return GCS_ERR_HIP;
   if (bad(hipHostMalloc(&c->h_err, 4 * sizeof(uint32_t), hipHostMallocMapped))) return GCS_ERR_HIP;
   c->h_err[0] = c->h_err[1] = c->h_err[2] = c->h_err[3] = 0u;
@@ -839,6 +885,19 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     // every tile starts dirty: the first scan writes all ScanBinStats rows and partial rows
     if (bad(hipMalloc(&c->d_tile_dirty, bins_scale_blocks(c->B, c->tile_bins)))) return GCS_ERR_HIP;
     if (bad(hipMemset(c->d_tile_dirty, 1, bins_scale_blocks(c->B, c->tile_bins)))) return GCS_ERR_HIP;
+    {
+      const int nt = bins_scale_blocks(c->B, c->tile_bins);
+      const char* e = getenv("GCSLAM_TILE_ORDER");
+      c->tile_order_on = nt > 2048 && !(e && atoi(e) == 0);
+      if (c->tile_order_on) {
+        std::vector<int> ident(nt);
+        for (int i = 0; i < nt; ++i) ident[i] = i;
+        if (bad(hipMalloc(&c->d_tile_order, nt * sizeof(int)))) return GCS_ERR_HIP;
+        if (bad(hipMemcpy(c->d_tile_order, ident.data(), nt * sizeof(int), hipMemcpyHostToDevice))) return GCS_ERR_HIP;
+        if (bad(hipMalloc(&c->d_tile_work, nt * sizeof(uint32_t)))) return GCS_ERR_HIP;
+        if (bad(hipMemset(c->d_tile_work, 0, nt * sizeof(uint32_t)))) return GCS_ERR_HIP;
+      }
+    }
     if (bad(hipMalloc(&c->d_bins_part, partials_need(bins_scale_blocks(c->B, c->tile_bins), bins_partial_nv()) * sizeof(double))))
       return GCS_ERR_HIP;
   } else {
@@ -880,7 +939,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
-                  c->d_tile_dirty, c->d_bins_part, c->d_tickets,
+                  c->d_tile_dirty, c->d_tile_order, c->d_tile_work, c->d_bins_part, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
@@ -893,6 +952,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
     for (int k = 0; k < 2; ++k)
       if (c->ev[st][k]) (void)hipEventDestroy(c->ev[st][k]);
   if (c->ev_push) (void)hipEventDestroy(c->ev_push);
+  if (c->ev_stages) (void)hipEventDestroy(c->ev_stages);
   if (c->push_stream) (void)hipStreamDestroy(c->push_stream);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c->scan_st;
@@ -1633,7 +1693,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
   st.Ts = clk::now();
   if ((rc = scan_imu_odom(c, in, st, out))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));  // the PT fold has written the scalars to h_scalars
+  if ((rc = wait_mirror(c))) return rc;  // the PT fold has written the scalars to h_scalars
   if ((rc = check_bucket_err(c))) return rc;
   bool redone = false;
   if (c->use_direct && c->h_err[2]) {

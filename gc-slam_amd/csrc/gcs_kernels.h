@@ -128,6 +128,8 @@ struct BinKernelArgs {
   int pts_blocks;
   uint32_t* zero_after;  // bucketing scratch (mid-list length, look-back words) re-armed for the next scan
   int n_zero_after;
+  const int* tile_order;  // block -> tile (k_tile_order; null: identity)
+  uint32_t* tile_work;    // per tile: records the tile staged (written for active tiles; may be null)
 };
 
 struct PushArgs {
@@ -175,6 +177,8 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
                      double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
                      hipEvent_t e0, hipEvent_t e1);
+// the next scan's bin-tile dispatch order from this scan's active tiles and their staged records
+hipError_t launch_tile_order(const uint8_t* active, const uint32_t* work, int n, int* order, hipStream_t s);
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
                               double* partials, double* scalars, const uint8_t* act, uint8_t* touched, hipStream_t s,
                               hipEvent_t e0, hipEvent_t e1);

@@ -293,9 +293,6 @@ __device__ __forceinline__ void ray_dir(double px, double py, double pz, const d
 #ifndef GCS_PROBE_NOFLAGS
 #define GCS_PROBE_NOFLAGS 0  // timing probe (not a parity build): no first-arrival flag stores
 #endif
-#ifndef GCS_TILE_DEDUP
-#define GCS_TILE_DEDUP 1
-#endif
 #ifndef GCS_CAND_GROUP
 #define GCS_CAND_GROUP 16  // candidate direction loads in flight per group (16: all at once)
 #endif
@@ -486,22 +483,14 @@ void k_points(PointKernelArgs a, double* partials) {
           if (sl < (uint32_t)a.capb) a.members[(size_t)nearest * a.capb + sl] = (uint32_t)i;
           else *a.overflow = 1u;  // vector store to host-mapped memory; gcs_scan redoes the scan sorted
           if (!GCS_PROBE_NOFLAGS && sl == 0u) {  // first arrival: mark the candidate bins and their tiles
+            // (storing each tile flag once per row measured 20 us slower at C3: the compare chain)
             const int ts = a.tile_shift;
             uint8_t* tf = a.flags + a.n_bins;
-            // the row's candidates mostly share one or two tiles (Hilbert-ordered bins): a tile flag
-            // is stored only at its first occurrence in the row (each byte store is its own L2
-            // transaction)
-            int row[KC], tl[KC];
-#pragma unroll
-            for (int k = 0; k < KC; ++k) row[k] = LP == 1 ? cand[k % KL] : a.knn[(size_t)nearest * KC + k];
 #pragma unroll
             for (int k = 0; k < KC; ++k) {
-              a.flags[row[k]] = 1;
-              tl[k] = row[k] >> ts;
-              bool seen = false;
-#pragma unroll
-              for (int j = 0; j < k; ++j) seen |= GCS_TILE_DEDUP && tl[j] == tl[k];
-              if (!seen) tf[tl[k]] = 1;
+              const int c = LP == 1 ? cand[k % KL] : a.knn[(size_t)nearest * KC + k];
+              a.flags[c] = 1;
+              tf[c >> ts] = 1;
             }
           }
         } else {
@@ -856,7 +845,11 @@ __device__ void mf_finish(const double* v, double* scalars) {
   scalars[SC_MF_NEFF] = v[9];
   scalars[SC_MF_SCANN] = v[10];
   double R[9];
+#if GCS_PROBE_NOPOLAR  // timing probe (not a parity build): R = I
+  for (int k = 0; k < 9; ++k) R[k] = k % 4 == 0 ? 1.0 : 0.0;
+#else
   mf_rotation(v, R);
+#endif
   for (int k = 0; k < 9; ++k) scalars[SC_MF_R + k] = R[k];
 }
 
@@ -1034,7 +1027,9 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   __shared__ uint32_t s_wsum[NW];
   __shared__ double lds[NW * 16];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  const int tile = blockIdx.x;
+  // dispatch order: the previous scan's active tiles first, heaviest first (k_tile_order), so the
+  // multi-round C3 grid starts its long tiles early and ends on clean ones; identity if null
+  const int tile = a.tile_order ? a.tile_order[blockIdx.x] : (int)blockIdx.x;
   const int b0 = tile * TB;
   const int nb = min(TB, a.n_bins - b0);
   PROF(0);
@@ -1072,7 +1067,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
         v[3] = (double)nb * c5[3];
         v[4] = c5[4];
-        store_partials<kBinNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_BINS>
+        store_partials<kBinNV>(v, partials, tile);  // folded by k_final<FIN_BINS>
       }
     }
     PROF(6);
@@ -1223,6 +1218,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #pragma unroll
   for (int w = 0; w < NW; ++w) total += s_wsum[w];
   const bool staged = total <= (uint32_t)STAGE;
+  if (t == 0 && a.tile_work) a.tile_work[tile] = total;  // k_tile_order's weight for the next scan
   PROFV(8, total);
 #ifdef GCS_PHASE_PROF
   if (t == 0) {
@@ -1484,7 +1480,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     if (t < kBinNV) {
       double x = lds[t];
       for (int w = 1; w < NW; ++w) x = t == 4 ? fmax(x, lds[w * 16 + t]) : x + lds[w * 16 + t];
-      partials[(size_t)blockIdx.x * pstride<kBinNV>() + t] = x;  // folded by k_final<FIN_BINS>
+      partials[(size_t)tile * pstride<kBinNV>() + t] = x;  // folded by k_final<FIN_BINS>
     }
     PROF(6);
     PROFV(7, 1);
@@ -1516,7 +1512,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   }
   PROF(5);
   wave_reduce_bin_terms(v);
-  store_partials<kBinNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_BINS>
+  store_partials<kBinNV>(v, partials, tile);  // folded by k_final<FIN_BINS>
   PROF(6);
   PROFV(7, 1);
 }
@@ -1898,6 +1894,11 @@ __global__ __launch_bounds__(NT) void k_final(const double* __restrict__ partial
   if (mirror) {
     __syncthreads();
     for (int i = threadIdx.x; i < SC_COUNT; i += NT) mirror[i] = scalars[i];
+    // the block's mirror stores reach host memory before the ready word (the host polls it instead
+    // of a stream synchronize: gcs_capi.cpp wait_mirror)
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) mirror[SC_COUNT] = 1.0;
   }
 }
 
@@ -1948,6 +1949,77 @@ size_t partials_need(long nblocks, int nv) {
   launch_fold<NV, MASK, KIND>((const double*)(partials), (int)(nblk), s, e1, scalars, (double*)(mirror))
 #define GCS_FINAL(NV, MASK, KIND, nblk, s, e1, partials, scalars) \
   GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, nullptr)
+
+// ---------------------------------------------------------------- bin-tile dispatch order
+// One 1024-thread block after the scan's pushforward (off the critical path): the tiles active in this
+// scan (tile_dirty after k_bins_scale) in four classes of staged records against the active mean
+// (>= 1.5x, >= 1x, >= 0.5x, below), then every other tile, tile order inside a class.  The next
+// scan's k_bins_scale dispatches blocks in that order (the sensor's coverage moves little from scan
+// to scan): its long tiles start in the first round and the clean tiles fill the last one.  Only
+// the dispatch order changes -- each tile's rows and partial row are the same whichever block
+// computes them.
+constexpr int kOrderNT = 1024, kOrderClasses = 5;
+__global__ __launch_bounds__(kOrderNT) void k_tile_order(const uint8_t* __restrict__ active,
+                                                         const uint32_t* __restrict__ work, int n, int* order) {
+  __shared__ uint32_t s_sum[2][kOrderNT / 64];
+  __shared__ int s_cnt[kOrderClasses][kOrderNT / 64];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int chunk = (n + kOrderNT - 1) / kOrderNT;
+  const int j0 = min(n, t * chunk), j1 = min(n, j0 + chunk);
+  uint32_t ws = 0, na = 0;
+  for (int j = j0; j < j1; ++j)
+    if (active[j]) { ws += work[j]; ++na; }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    ws += (uint32_t)__shfl_xor((int)ws, off, 64);
+    na += (uint32_t)__shfl_xor((int)na, off, 64);
+  }
+  if (lane == 0) { s_sum[0][wid] = ws; s_sum[1][wid] = na; }
+  __syncthreads();
+  unsigned long long W = 0, A = 0;
+  for (int w = 0; w < kOrderNT / 64; ++w) { W += s_sum[0][w]; A += s_sum[1][w]; }
+  auto cls = [&](int j) -> int {
+    if (!active[j]) return 4;
+    const unsigned long long wa = (unsigned long long)work[j] * A;  // work / mean = wa / W
+    return 2 * wa >= 3 * W ? 0 : (wa >= W ? 1 : (2 * wa >= W ? 2 : 3));
+  };
+  int cnt[kOrderClasses] = {0, 0, 0, 0, 0};
+  for (int j = j0; j < j1; ++j) ++cnt[cls(j)];
+  int pos[kOrderClasses];
+#pragma unroll
+  for (int c = 0; c < kOrderClasses; ++c) {
+    int x = cnt[c];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) s_cnt[c][wid] = x;
+    pos[c] = x - cnt[c];
+  }
+  __syncthreads();
+  int base = 0;
+#pragma unroll
+  for (int c = 0; c < kOrderClasses; ++c) {
+    int pre = 0, tot = 0;
+    for (int w = 0; w < kOrderNT / 64; ++w) {
+      const int v = s_cnt[c][w];
+      pre += w < wid ? v : 0;
+      tot += v;
+    }
+    pos[c] += base + pre;
+    base += tot;
+  }
+  for (int j = j0; j < j1; ++j) {
+    const int c = cls(j);
+    order[pos[c]++] = j;
+  }
+}
+
+hipError_t launch_tile_order(const uint8_t* active, const uint32_t* work, int n, int* order, hipStream_t s) {
+  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(kOrderNT), 0, s, active, work, n, order);
+  return hipGetLastError();
+}
 
 // ---------------------------------------------------------------- launchers
 static int grid_for(long n, int cap_blocks) {
@@ -2023,10 +2095,10 @@ int bins_tile_for(long cap, int n_bins) {
     const int v = atoi(e);
     if (v == 32 || v == 64 || v == 128 || v == 256) return v;
   }
-  // Sparse maps (under 2.5 points per bin, C3: 262,144 points over 1,048,576 bins) run 128-bin tiles:
+  // Sparse maps (under 0.4 points per bin, C3: 262,144 points over 1,048,576 bins) run 128-bin tiles:
   // half the tiles, each amortising its table phase over twice the bins (C3 bins 88 vs 106 us, sweep
-  // profiles/r03/sweep_tile.txt).  Dense maps (C2: 20,000 bins, 8.5 points each) keep 64-bin tiles, whose
-  // stage fits the heavier per-bin record load (25.5 vs 30.5 us).
+  // profiles/r03).  Denser maps (C2: 65,536 points over 100,000 bins) keep 64-bin tiles, whose stage
+  // fits the heavier per-bin record load (25.5 vs 30.5 us).
   return (long)cap * 5 < (long)n_bins * 2 ? 128 : 64;
 }
 int bins_scale_blocks(int n_bins, int tile_bins) { return (n_bins + tile_bins - 1) / tile_bins; }

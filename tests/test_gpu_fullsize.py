@@ -16,7 +16,7 @@ import pytest
 
 torch = pytest.importorskip("torch")
 
-from gpu_util import assert_close, device_scan, map_fields
+from gpu_util import MAP_GROUPS, assert_close, assert_close_groupwise, device_scan, map_fields
 from oracle import ops, pipeline as opipe
 from gcslam.synthetic import scan_kwargs
 from test_gpu_parity import ORIGIN, XI, _check_scan_stats, _ctx, _mm_reference, _synthetic
@@ -124,7 +124,9 @@ def test_c3_full_scans_value_parity():
         _check_scan_stats(ctx.get_scan_stats(), ref["scan_bins"], amp=amp)
         m_dev, _ = ctx.get_map()
         mref = map_fields(ref["map"].stats)
-        assert_close(f"C3 scan{k} map", m_dev, mref, rtol=1e-7 * amp, atol=1e-9 * max(np.abs(mref).max(), 1.0))
+        # norm-wise per bin and field group (the rotated moments' off-diagonals cancel; gpu_util)
+        assert_close_groupwise(f"C3 scan{k} map", m_dev, mref, MAP_GROUPS, rtol=1e-7 * amp,
+                               atol=1e-9 * max(np.abs(mref).max(), 1.0))
         b, ms = ref["belief"], ref["map"]
     ctx.close()
 
