@@ -320,23 +320,28 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select(const uint64_t* __restrict
 // wave-aggregated when every counted lane of the wave has the same digit (an empty or freshly
 // activated tile has one key value everywhere: per-lane atomics on one LDS word serialise the tile),
 // else one LDS atomic per key.
-template <int KPT>
-__global__ __launch_bounds__(kPmRed) void k_pm_select_reg(const uint64_t* __restrict__ keys, int M, int k,
+template <int KPT, int NT>
+__global__ __launch_bounds__(NT) void k_pm_select_reg(const uint64_t* __restrict__ keys, int M, int k,
                                                            uint32_t* __restrict__ sorted) {
   __shared__ uint32_t s_hist[1 << kSelBits];
   __shared__ uint64_t s_key[kSelMax];
   __shared__ uint32_t s_slot[kSelMax];
-  __shared__ uint32_t s_wl[kPmRed / 64], s_we[kPmRed / 64];
+  __shared__ uint32_t s_wl[NT / 64], s_we[NT / 64];
   __shared__ uint64_t s_prefix;
   __shared__ uint32_t s_need;
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint64_t* kt = keys + (size_t)t * M;
-  const uint32_t* kw = reinterpret_cast<const uint32_t*>(kt);  // little endian: [2q] low, [2q + 1] high word
+  // the key words through a buffer descriptor: slot q = tid + j NT is voffset 8 tid (+4: high word) and
+  // the constant soffset 8 j NT, so the unrolled j loops share one address register (flat loads kept a
+  // 64-bit address per j live across the passes and spilled at 49 keys per thread)
+  const __amdgpu_buffer_rsrc_t kr = __builtin_amdgcn_make_buffer_rsrc((void*)kt, 0, M * 8, 0x00020000);
+  auto lo_word = [&](int j) { return __builtin_amdgcn_raw_buffer_load_b32(kr, tid * 8, j * NT * 8, 0); };
+  auto hi_word = [&](int j) { return __builtin_amdgcn_raw_buffer_load_b32(kr, tid * 8 + 4, j * NT * 8, 0); };
   uint32_t xh[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    const int q = tid + j * kPmRed;
-    xh[j] = q < M ? kw[2 * q + 1] : 0u;
+    const int q = tid + j * NT;
+    xh[j] = q < M ? hi_word(j) : 0u;
   }
   uint64_t prefix = 0, pmask = 0;
   uint32_t need = (uint32_t)k;  // rank (1-based) of T among the keys that match the prefix
@@ -346,11 +351,11 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select_reg(const uint64_t* __rest
     const int bits = kBits[pass], shift = kShift[pass];
     const uint32_t dmask = (1u << bits) - 1u;
     const bool hiword = shift >= 32;  // this pass reads only high-word bits (prefix bits are high too)
-    for (int i = tid; i < (1 << kSelBits); i += kPmRed) s_hist[i] = 0u;
+    for (int i = tid; i < (1 << kSelBits); i += NT) s_hist[i] = 0u;
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < KPT; ++j) {
-      const int q = tid + j * kPmRed;
+      const int q = tid + j * NT;
       bool act = q < M;
       uint32_t dg = 0;
       if (hiword) {
@@ -359,7 +364,7 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select_reg(const uint64_t* __rest
       } else {
         act = act && xh[j] == (uint32_t)(prefix >> 32);  // high word fixed by now: its ties only
         if (act) {
-          const uint64_t x = ((uint64_t)xh[j] << 32) | kw[2 * q];
+          const uint64_t x = ((uint64_t)xh[j] << 32) | lo_word(j);
           act = (x & pmask) == prefix;
           dg = (uint32_t)(x >> shift) & dmask;
         }
@@ -408,22 +413,22 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select_reg(const uint64_t* __rest
     __syncthreads();
   }
   // keys < T: exactly k - need of them; keys == T: the first `need` in slot order (slots ascend with j
-  // within a thread and with the thread within a chunk of kPmRed slots)
+  // within a thread and with the thread within a chunk of NT slots)
   const uint32_t nless = (uint32_t)k - need;
   const uint64_t below = (1ull << lane) - 1ull;
   const uint32_t th = (uint32_t)(prefix >> 32);
   uint32_t base_l = 0, base_e = 0;
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    const int q = tid + j * kPmRed;
+    const int q = tid + j * NT;
     bool lt = q < M && xh[j] < th, eq = false;
     uint64_t x = (uint64_t)xh[j] << 32;
     if (q < M && xh[j] == th) {  // high-word tie: the full key decides
-      x |= kw[2 * q];
+      x |= lo_word(j);
       lt = x < prefix;
       eq = x == prefix;
     } else if (lt) {
-      x |= kw[2 * q];
+      x |= lo_word(j);
     }
     const uint64_t bl = __ballot(lt), be = __ballot(eq);
     if (lane == 0) {
@@ -432,7 +437,7 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select_reg(const uint64_t* __rest
     }
     __syncthreads();
     uint32_t ol = 0, oe = 0, tl = 0, te = 0;
-    for (int w = 0; w < kPmRed / 64; ++w) {
+    for (int w = 0; w < NT / 64; ++w) {
       if (w < wid) {
         ol += s_wl[w];
         oe += s_we[w];
@@ -458,28 +463,167 @@ __global__ __launch_bounds__(kPmRed) void k_pm_select_reg(const uint64_t* __rest
   }
   int P = 1;
   while (P < k) P <<= 1;
-  for (int i = k + tid; i < P; i += kPmRed) {
+  for (int i = k + tid; i < P; i += NT) {
     s_key[i] = ~0ull;
     s_slot[i] = ~0u;
   }
   for (int size = 2; size <= P; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       __syncthreads();
-      const int i = tid, j = tid ^ stride;
-      if (i < P && j > i) {
-        const uint64_t ki = s_key[i], kj = s_key[j];
-        const uint32_t si = s_slot[i], sj = s_slot[j];
-        const bool gt = ki > kj || (ki == kj && si > sj);
-        if (gt == ((i & size) == 0)) {
-          s_key[i] = kj;
-          s_key[j] = ki;
-          s_slot[i] = sj;
-          s_slot[j] = si;
+      for (int i = tid; i < P; i += NT) {
+        const int j = i ^ stride;
+        if (j > i) {
+          const uint64_t ki = s_key[i], kj = s_key[j];
+          const uint32_t si = s_slot[i], sj = s_slot[j];
+          const bool gt = ki > kj || (ki == kj && si > sj);
+          if (gt == ((i & size) == 0)) {
+            s_key[i] = kj;
+            s_key[j] = ki;
+            s_slot[i] = sj;
+            s_slot[j] = si;
+          }
         }
       }
     }
   __syncthreads();
-  for (int r = tid; r < k; r += kPmRed) sorted[(size_t)t * M + r] = (uint32_t)((size_t)t * M) + s_slot[r];
+  for (int r = tid; r < k; r += NT) sorted[(size_t)t * M + r] = (uint32_t)((size_t)t * M) + s_slot[r];
+}
+
+// The first k (<= kSelMax) entries of each tile's stable key order by a tree of sorted runs, in one
+// launch and with many CUs of a many-tile call busy (k_pm_select runs one workgroup per tile: 7 on 256
+// CUs at the reference's 7 x 50,000).  Leaf g of tile t (grid.x) sorts the keys of slots
+// [4096 g, 4096 g + 4096) by (key, slot) in LDS -- the stable order: slots are unique, so every pair
+// is distinct -- and keeps the first k as its run.  Two sibling runs are merged by whichever of their
+// two workgroups finishes second (a per-node ticket: the first leaves, so no workgroup waits on
+// another), keeping the first k, and that workgroup climbs; the root writes
+// sorted[t M + r] = t M + slot for r < k.  Merge: an element's rank in the merged run is its own
+// index plus the count of the other run's smaller entries (binary search in LDS).  Runs live in
+// run_key / run_slot at the first leaf of their node (k entries per leaf); the writer's stores are
+// released (agent-scope fence, barrier) before its ticket, the second arrival acquires before reading.
+constexpr int kTopEpt = 4;                  // slots per thread in a leaf
+constexpr int kTopChunk = kTopEpt * kPmRed;  // slots per leaf: 4,096 (13 leaves, 4 merge levels at 50,000)
+constexpr int kTopMaxLevels = 8;             // up to 128 leaves per tile (M <= 524,288)
+constexpr int kTopNodes = 64;                // tickets per level and tile
+__device__ __forceinline__ bool topk_less(uint64_t ka, uint32_t sa, uint64_t kb, uint32_t sb) {
+  return ka < kb || (ka == kb && sa < sb);
+}
+// entries of the node (lv, i)'s run: min(k, the node's slots)
+__device__ __forceinline__ int topk_len(int M, int k, int lv, int i) {
+  const long lo = (long)(i << lv) * kTopChunk, hi = min((long)M, (long)((i + 1) << lv) * kTopChunk);
+  return (int)min((long)k, max(0L, hi - lo));
+}
+__global__ __launch_bounds__(kPmRed) void k_pm_topk(const uint64_t* __restrict__ keys, int M, int k, int G,
+                                                     uint64_t* run_key, uint32_t* run_slot, uint32_t* tickets,
+                                                     uint32_t* __restrict__ sorted) {
+  // leaf: the chunk's keys / slots; merges: own run [0, k), sibling run [kSelMax, 2 kSelMax), merged
+  // run [2 kSelMax, 3 kSelMax) (k <= kSelMax = 1,024)
+  __shared__ uint64_t s_k[kTopChunk];
+  __shared__ uint32_t s_s[kTopChunk];
+  static_assert(3 * kSelMax <= kTopChunk, "merge buffers inside the leaf buffer");
+  uint64_t* const s_ok = s_k + 2 * kSelMax;
+  uint32_t* const s_os = s_s + 2 * kSelMax;
+  __shared__ uint32_t s_go;
+  const int t = blockIdx.y, g = blockIdx.x, tid = threadIdx.x;
+  uint64_t* rk = run_key + (size_t)t * G * k;
+  uint32_t* rs = run_slot + (size_t)t * G * k;
+  uint32_t* tk = tickets + (size_t)t * kTopMaxLevels * kTopNodes;
+  {  // leaf: bitonic sort of the chunk (padding last: key ~0, slot ~0 above every real pair)
+#pragma unroll
+    for (int e = 0; e < kTopEpt; ++e) {
+      const int x = tid + e * kPmRed, q = g * kTopChunk + x;
+      s_k[x] = q < M ? keys[(size_t)t * M + q] : ~0ull;
+      s_s[x] = q < M ? (uint32_t)q : ~0u;
+    }
+    for (int size = 2; size <= kTopChunk; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < kTopEpt / 2; ++e) {  // the chunk's kTopChunk / 2 pairs, two per thread
+          const int pr = tid + e * kPmRed;
+          const int x = ((pr & ~(stride - 1)) << 1) | (pr & (stride - 1)), y = x | stride;
+          const uint64_t kx = s_k[x], ky = s_k[y];
+          const uint32_t sx = s_s[x], sy = s_s[y];
+          if (topk_less(ky, sy, kx, sx) == ((x & size) == 0)) {
+            s_k[x] = ky;
+            s_k[y] = kx;
+            s_s[x] = sy;
+            s_s[y] = sx;
+          }
+        }
+      }
+    __syncthreads();
+  }
+  int lv = 0, i = g;
+  int L = topk_len(M, k, 0, g);
+  for (;;) {
+    if ((1 << lv) >= G) {  // the root: every leaf of the tile is in this run
+      for (int r = tid; r < L; r += kPmRed) sorted[(size_t)t * M + r] = (uint32_t)((size_t)t * M) + s_s[r];
+      return;
+    }
+    const int sib = i ^ 1;
+    if ((sib << lv) >= G) {  // no sibling at this level: the run moves up unchanged
+      i >>= 1;
+      ++lv;
+      continue;
+    }
+    // publish this run, then take the node's ticket
+    const size_t mine = (size_t)(i << lv) * k;
+    for (int r = tid; r < L; r += kPmRed) {
+      rk[mine + r] = s_k[r];
+      rs[mine + r] = s_s[r];
+    }
+    // every wave's stores drained at the barrier, then ONE agent-scope release with the ticket (a
+    // fence per thread wrote the L2 back once per wave: 0.75 ms per call), and the second arrival's
+    // acquire on the same atomic before the workgroup reads the sibling's run
+    __syncthreads();
+    uint32_t* ticket = tk + lv * kTopNodes + (i >> 1);
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (old != 0u) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+      s_go = old;
+    }
+    __syncthreads();
+    if (s_go == 0u) return;  // the sibling merges
+    const int Ls = topk_len(M, k, lv, sib);
+    const size_t other = (size_t)(sib << lv) * k;
+    for (int r = tid; r < Ls; r += kPmRed) {
+      s_k[kSelMax + r] = rk[other + r];
+      s_s[kSelMax + r] = rs[other + r];
+    }
+    __syncthreads();
+    const int Lo = topk_len(M, k, lv + 1, i >> 1);
+    // ranks: own entry r -> r + #{sibling entries below it}; sibling entry r -> r + #{own entries below}
+    for (int side = 0; side < 2; ++side) {
+      const int La = side == 0 ? L : Ls, Lb = side == 0 ? Ls : L;
+      const uint64_t* ak = s_k + (side == 0 ? 0 : kSelMax);
+      const uint32_t* as = s_s + (side == 0 ? 0 : kSelMax);
+      const uint64_t* bk = s_k + (side == 0 ? kSelMax : 0);
+      const uint32_t* bs = s_s + (side == 0 ? kSelMax : 0);
+      if (tid < La) {
+        const uint64_t x = ak[tid];
+        const uint32_t xs = as[tid];
+        int lo = 0, hi = Lb;  // first b not below x
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (topk_less(bk[mid], bs[mid], x, xs)) lo = mid + 1; else hi = mid;
+        }
+        const int rank = tid + lo;
+        if (rank < Lo) {
+          s_ok[rank] = x;
+          s_os[rank] = xs;
+        }
+      }
+    }
+    __syncthreads();
+    for (int r = tid; r < Lo; r += kPmRed) {
+      s_k[r] = s_ok[r];
+      s_s[r] = s_os[r];
+    }
+    __syncthreads();
+    L = Lo;
+    i >>= 1;
+    ++lv;
+  }
 }
 
 // second (stable) pass of the per-tile sort: key = the entry's tile position
@@ -567,11 +711,23 @@ struct PmRows {
 __global__ __launch_bounds__(kPmThreads) void k_pm_insert(PmStore st, const int32_t* tiles, int n, int K,
                                                           const uint32_t* sorted, PmRows r, double ts, long long seq,
                                                           long long next_id, int64_t* ids_out, int32_t* n_ins) {
+  // one workgroup per listed tile (grid n): ids continue tile by tile, so tile t's first id is
+  // next_id + the valid proposals of tiles 0 .. t-1 (counted here; at most n K flags)
   __shared__ int s_w[kPmThreads / 64];
-  long long base = next_id;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   constexpr int ne = 3 * kNL;
-  for (int t = 0; t < n; ++t) {
+  const int t = blockIdx.x;
+  long long base = next_id;
+  {
+    int c = 0;
+    for (int row = threadIdx.x; row < t * K; row += kPmThreads) c += r.valid[row] ? 1 : 0;
+    for (int off = 32; off >= 1; off >>= 1) c += __shfl_xor(c, off, 64);
+    if (lane == 0) s_w[wid] = c;
+    __syncthreads();
+    for (int w = 0; w < kPmThreads / 64; ++w) base += s_w[w];
+    __syncthreads();
+  }
+  {
     const int ti = tiles[t];
     int run = 0;
     for (int q0 = 0; q0 < K; q0 += kPmThreads) {
@@ -626,7 +782,6 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_insert(PmStore st, const int3
       __syncthreads();
     }
     if (threadIdx.x == 0) n_ins[t] = run;
-    base += run;
   }
 }
 
@@ -801,8 +956,10 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st,
 // unique slots per block (grid: blocks of slots x nb): integer atomics into device counters
 __global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(const uint8_t* mark, int M, uint32_t* cnt) {
   __shared__ double lds[kPmThreads / 64];
-  const int q = blockIdx.x * kPmThreads + threadIdx.x, b = blockIdx.y;
-  double c = q < M && mark[(size_t)b * M + q] ? 1.0 : 0.0;
+  const int b = blockIdx.y;
+  double c = 0.0;
+  for (int q = blockIdx.x * kPmThreads + threadIdx.x; q < M; q += gridDim.x * kPmThreads)
+    c += mark[(size_t)b * M + q] ? 1.0 : 0.0;
   c = block_sum_d<kPmThreads>(c, lds);
   if (threadIdx.x == 0 && c > 0.0) atomicAdd(cnt + b, (uint32_t)c);
 }
@@ -1120,7 +1277,45 @@ struct PmRowBuf {
   double *lam, *th, *eta, *w, *resp, *col, *fm;
   uint8_t* valid;
   int32_t *src, *tpos, *slots;
+  double* w_host;  // k_pm_proposals: the proposal weights also into the mapped buffer (may be null)
 };
+
+// step 12b's tile list and active ids as kernel arguments (no host-to-device copy)
+constexpr int kPmArgTiles = 64;
+struct PmTileArgs {
+  int n;
+  int32_t tiles[kPmArgTiles];
+  int64_t ids[kPmArgTiles];
+};
+__global__ void k_pm_stage_tiles(PmTileArgs a, int32_t* tiles, int64_t* ids) {
+  const int i = threadIdx.x;
+  if (i < a.n) {
+    tiles[i] = a.tiles[i];
+    ids[i] = a.ids[i];
+  }
+}
+
+// per association block b and listed tile t: the sum of fm over the block's rows with tpos == t (the
+// fused_mass_total terms, pipeline.py:1306-1308), a fixed-order tree per (b, t), into mapped memory
+__global__ __launch_bounds__(kPmThreads) void k_pm_fm_sums(const double* fm, const int32_t* tpos, int bk, int n,
+                                                           double* out) {
+  __shared__ double lds[kPmThreads / 64];
+  const int b = blockIdx.x;
+  for (int t = 0; t < n; ++t) {
+    double s = 0.0;
+    for (int q = threadIdx.x; q < bk; q += kPmThreads) {
+      const size_t g = (size_t)b * bk + q;
+      s += tpos[g] == t ? fm[g] : 0.0;
+    }
+    s = block_sum_d<kPmThreads>(s, lds);
+    if (threadIdx.x == 0) out[b * n + t] = s;
+  }
+}
+
+// device counters into the mapped buffer (one launch instead of a device-to-host copy)
+__global__ void k_pm_publish_u32(const uint32_t* src, int n, uint32_t* dst) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+}
 
 // block_associations_for_fuse (primitive_association.py:561-588) + the world transform, rows in
 // (block, measurement, candidate) order; fm = w r [valid and tile active] (fused mass terms)
@@ -1263,6 +1458,7 @@ __global__ __launch_bounds__(kPropThreads) void k_pm_proposals(PmMeas m, PmWorld
     const double vf = m.valid[i] ? 1.0 : 0.0;
     const double nov = fmax(vf / asum - m.rmass[i], 0.0);
     o.w[g] = in_tile ? nov * m.w[i] : 0.0;
+    if (o.w_host) o.w_host[g] = o.w[g];
     o.valid[g] = vn ? 1 : 0;
     o.src[g] = m.src ? m.src[i] : 1;
   }
@@ -1304,6 +1500,12 @@ struct gcs_pmap {
   long long* mpp = nullptr;
   uint8_t* mused = nullptr;
   int32_t *msel = nullptr, *mnsel = nullptr;
+  // k_pm_topk: per-tile runs (grown) and the merge tickets (max_tiles x levels x nodes, zeroed once;
+  // each merging workgroup re-arms its ticket)
+  uint64_t* run_key = nullptr;
+  uint32_t* run_slot = nullptr;
+  size_t run_cap = 0;
+  uint32_t* tickets = nullptr;
   // small host-mapped results
   char* h_small = nullptr;
   char* d_small = nullptr;
@@ -1311,7 +1513,9 @@ struct gcs_pmap {
 };
 
 namespace {
-constexpr size_t kSmall = 1 << 20;
+constexpr size_t kSmall = 4 << 20;
+constexpr size_t kWiOff = 1 << 20;  // step 12b: proposal weights (n x k_insert_tile doubles)
+constexpr size_t kFmOff = 2 << 20;  // step 12b: fused mass per (association block, tile)
 constexpr size_t kPartOff = 1 << 16;  // per-(tile, block) reduction partials in the mapped buffer
 constexpr int kMaxBlocksPerTile = 64;
 constexpr int kMaxFuseBlocks = 256;  // association blocks of one map update
@@ -1373,8 +1577,33 @@ int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam, int k) {
       return e && e[0] == '1';
     }();
     const uint64_t* kk = (const uint64_t*)p->keys;
-    if (!glob && p->M <= 8 * kPmRed)
-      hipLaunchKernelGGL(k_pm_select_reg<8>, dim3(n), dim3(kPmRed), 0, p->stream, kk, p->M, k, p->vals);
+    // GCSLAM_PM_SELECT: "radix" (one workgroup, keys read from memory each pass) for A/B; default: the
+    // register select up to 8 keys per thread (M <= 8,192), the tree of sorted runs (k_pm_topk) above.
+    // Measured at 7 x 50,000 (profiles/r03/pmap): tree 61-73 us, radix ~120 us, and the register select
+    // at 98 keys per thread (512 threads, buffer loads, no spill) 186 us -- its LDS histogram atomics
+    // on the keys' low-entropy top bits serialise.
+    static const int mode = [] {
+      const char* e = getenv("GCSLAM_PM_SELECT");
+      return e && strcmp(e, "radix") == 0 ? 2 : 0;
+    }();
+    const int G = (p->M + kTopChunk - 1) / kTopChunk;
+    const bool reg8 = p->M <= 8 * kPmRed;
+    const bool use_tree = !glob && mode == 0 && !reg8 && G > 1 && G <= (1 << (kTopMaxLevels - 1));
+    if (use_tree) {
+      const size_t need = (size_t)n * G * k;
+      if (need > p->run_cap) {
+        if (p->run_key) PMCHK(p, hipFree(p->run_key));
+        if (p->run_slot) PMCHK(p, hipFree(p->run_slot));
+        p->run_key = nullptr;
+        p->run_slot = nullptr;
+        PMCHK(p, hipMalloc(&p->run_key, need * 8));
+        PMCHK(p, hipMalloc(&p->run_slot, need * 4));
+        p->run_cap = need;
+      }
+      hipLaunchKernelGGL(k_pm_topk, dim3(G, n), dim3(kPmRed), 0, p->stream, kk, p->M, k, G, p->run_key, p->run_slot,
+                         p->tickets, p->vals);
+    } else if (!glob && mode != 2 && reg8)
+      hipLaunchKernelGGL((k_pm_select_reg<8, kPmRed>), dim3(n), dim3(kPmRed), 0, p->stream, kk, p->M, k, p->vals);
     else
       hipLaunchKernelGGL(k_pm_select, dim3(n), dim3(kPmRed), 0, p->stream, kk, p->M, k, p->vals);
     PMCHK(p, hipGetLastError());
@@ -1476,6 +1705,8 @@ int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t 
       bad(hipMalloc(&p->d_tiles, max_tiles * 4)) || bad(hipMalloc(&p->d_tids, max_tiles * 8)) ||
       bad(hipMalloc(&p->mark, (size_t)m_tile * 4)) || bad(hipMalloc(&p->dcnt, 4)) ||
       bad(hipMalloc(&p->bcnt, kMaxFuseBlocks * 4)) ||
+      bad(hipMalloc(&p->tickets, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
+      bad(hipMemset(p->tickets, 0, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
       bad(hipHostMalloc((void**)&p->h_small, kSmall, hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&p->d_small, p->h_small, 0)))
     return fail();
@@ -1511,7 +1742,7 @@ int gcs_pmap_destroy(gcs_pmap* p) {
     if (f) (void)hipFree(f);
   void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->seg, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
                   p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->bmark, p->bcnt, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
-                  p->msel, p->mnsel, p->ub};
+                  p->msel, p->mnsel, p->ub, p->run_key, p->run_slot, p->tickets};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (p->h_small) (void)hipHostFree(p->h_small);
@@ -1568,8 +1799,18 @@ int gcs_pmap_extract_view(gcs_pmap* p, const int32_t* tiles, const int64_t* tile
   if (int rc = check_tiles(p, tiles, n, true)) return rc;
   if (n == 0) return GCS_OK;
   PMCHK(p, hipSetDevice(p->device));
-  if (int rc = upload_tiles(p, tiles, n)) return rc;
-  PMCHK(p, hipMemcpyAsync(p->d_tids, tile_ids, n * sizeof(int64_t), hipMemcpyHostToDevice, p->stream));
+  if (n <= kPmArgTiles) {  // the tile list and ids as kernel arguments (no host-to-device copies)
+    PmTileArgs ta{};
+    ta.n = n;
+    for (int t = 0; t < n; ++t) {
+      ta.tiles[t] = tiles[t];
+      ta.ids[t] = tile_ids[t];
+    }
+    hipLaunchKernelGGL(k_pm_stage_tiles, dim3(1), dim3(kPmArgTiles), 0, p->stream, ta, p->d_tiles, p->d_tids);
+  } else {
+    if (int rc = upload_tiles(p, tiles, n)) return rc;
+    PMCHK(p, hipMemcpyAsync(p->d_tids, tile_ids, n * sizeof(int64_t), hipMemcpyHostToDevice, p->stream));
+  }
   if (int rc = sort_tiles(p, n, 0, 0, 0.0, m_view)) return rc;
   PmViewOut v{o->positions, o->covariances, o->directions, o->kappas, o->weights, o->etas, o->colors,
               o->primitive_ids, o->last_supported_scan_seq, o->candidate_tile_ids, o->valid_mask,
@@ -1597,7 +1838,7 @@ int gcs_pmap_insert_masked(gcs_pmap* p, const int32_t* tiles, int32_t n, int32_t
   int32_t* d_ins = (int32_t*)p->d_small;
   if (K > 0) {
     if (int rc = sort_tiles(p, n, 1, scan_seq, lam, K)) return rc;
-    hipLaunchKernelGGL(k_pm_insert, dim3(1), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, K,
+    hipLaunchKernelGGL(k_pm_insert, dim3(n), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, K,
                        (const uint32_t*)p->vals, rows_of(rows), timestamp, (long long)scan_seq,
                        (long long)next_global_id, new_ids, d_ins);
   } else {
@@ -1682,6 +1923,8 @@ int fuse_impl(gcs_pmap* p, const int32_t* tiles, int32_t n, const gcs_pmap_rows*
 // Step 12b's fuse: nb association blocks of rpb rows each (rows block-major), every listed tile
 // (already uploaded to d_tiles), in one sort + one apply (no host syncs between the blocks);
 // nf (host, nb): each block's unique target slots.  One sync at the end.
+// nf == nullptr: no sync -- the counts go to the mapped buffer (h_small + 9216) and the caller
+// checks the slot-range flag (h_small + 8192) after its own sync
 int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int rpb, double timestamp, int64_t scan_seq,
                 double eps_mass, int32_t* nf) {
   const int R = rows->n;
@@ -1732,10 +1975,12 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
   PMCHK(p, hipMemsetAsync(p->mark, 0, (size_t)p->M * 4, p->stream));  // k_pm_fuse_ts marks (unused here)
   hipLaunchKernelGGL(k_pm_fuse_ts, dim3((unsigned)((tr + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
                      p->stream, p->st, (const int32_t*)p->d_tiles, n, r, timestamp, p->mark);
-  hipLaunchKernelGGL(k_pm_count_marks_blocks, dim3((p->M + kPmThreads - 1) / kPmThreads, nb), dim3(kPmThreads), 0,
-                     p->stream, (const uint8_t*)p->bmark, p->M, p->bcnt);
-  PMCHK(p, hipMemcpyAsync(p->h_small + 9216, p->bcnt, nb * 4, hipMemcpyDeviceToHost, p->stream));
+  hipLaunchKernelGGL(k_pm_count_marks_blocks, dim3(std::min(32, (p->M + kPmThreads - 1) / kPmThreads), nb),
+                     dim3(kPmThreads), 0, p->stream, (const uint8_t*)p->bmark, p->M, p->bcnt);
+  hipLaunchKernelGGL(k_pm_publish_u32, dim3(1), dim3(256), 0, p->stream, (const uint32_t*)p->bcnt, nb,
+                     (uint32_t*)(p->d_small + 9216));
   PMCHK(p, hipGetLastError());
+  if (!nf) return GCS_OK;
   PMCHK(p, hipStreamSynchronize(p->stream));
   if (*(uint32_t*)(p->h_small + 8192)) return pm_fail(p, GCS_ERR_ARG, "target slot out of range (rows skipped)");
   for (int b = 0; b < nb; ++b) nf[b] = (int32_t)((const uint32_t*)(p->h_small + 9216))[b];
@@ -1899,16 +2144,29 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   o.tpos = i32; i32 += R;
   o.slots = i32;
   (void)slot_of;
-  PMCHK(p, hipMemcpyAsync(act, tile_ids, n * sizeof(int64_t), hipMemcpyHostToDevice, p->stream));
+  // one device pass, one sync: every count and mass term the stats need goes to the mapped buffer
+  // and is read after the single stream synchronize at the end (the per-operator entry points keep
+  // their own syncs)
+  if (n <= kPmArgTiles) {
+    PmTileArgs ta{};
+    ta.n = n;
+    for (int t = 0; t < n; ++t) {
+      ta.tiles[t] = tiles[t];
+      ta.ids[t] = tile_ids[t];
+    }
+    hipLaunchKernelGGL(k_pm_stage_tiles, dim3(1), dim3(kPmArgTiles), 0, p->stream, ta, p->d_tiles, act);
+  } else {
+    PMCHK(p, hipMemcpyAsync(act, tile_ids, n * sizeof(int64_t), hipMemcpyHostToDevice, p->stream));
+    if (int rc = upload_tiles(p, tiles, n)) return rc;
+  }
   // fuse: per association block, every active tile (pipeline.py:1265-1327)
   hipLaunchKernelGGL(k_pm_fuse_rows, dim3((nrows + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream, m, W,
                      nl, B, nrows, (const int64_t*)act, n, o);
   PMCHK(p, hipGetLastError());
-  std::vector<double> fm(nrows);
-  std::vector<int32_t> tp(nrows);
-  PMCHK(p, hipMemcpyAsync(fm.data(), o.fm, nrows * 8, hipMemcpyDeviceToHost, p->stream));
-  PMCHK(p, hipMemcpyAsync(tp.data(), o.tpos, nrows * 4, hipMemcpyDeviceToHost, p->stream));
-  if (int rc = upload_tiles(p, tiles, n)) return rc;
+  if ((size_t)nb * n * 8 > kSmall - kFmOff || (size_t)nprop * 8 > kFmOff - kWiOff)
+    return pm_fail(p, GCS_ERR_ARG, "map update: stats exceed the mapped buffer");
+  hipLaunchKernelGGL(k_pm_fm_sums, dim3(nb), dim3(kPmThreads), 0, p->stream, (const double*)o.fm,
+                     (const int32_t*)o.tpos, B * K, n, (double*)(p->d_small + kFmOff));
   gcs_pmap_rows ra{};
   ra.Lambdas = o.lam;
   ra.thetas = o.th;
@@ -1921,25 +2179,16 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   ra.tile_pos = o.tpos;
   ra.slots = o.slots;
   ra.n = nrows;
-  std::vector<int32_t> nfb(nb);
-  if (int rc = fuse_blocks(p, n, &ra, nb, B * K, timestamp, scan_seq, cfg->eps_mass, nfb.data())) return rc;
-  for (int b = 0; b < nb; ++b) {
-    const size_t r0 = (size_t)b * B * K;
-    st->fused_count += n * nfb[b];
-    for (int t = 0; t < n; ++t) {  // fused_mass_total: per (block, tile) sums (pipeline.py:1306-1308)
-      double sm = 0.0;
-      for (int q = 0; q < B * K; ++q)
-        if (tp[r0 + q] == t) sm += fm[r0 + q];
-      st->fused_mass_total += sm;
-    }
-  }
-  // novelty insertion per active tile (pipeline.py:1331-1392)
+  if (int rc = fuse_blocks(p, n, &ra, nb, B * K, timestamp, scan_seq, cfg->eps_mass, nullptr)) return rc;
+  // novelty insertion per active tile (pipeline.py:1331-1392): proposals, the eviction order (select of
+  // the lowest retention keys) and the writes; ids continue tile by tile from next_global_id
+  int32_t* d_ins = (int32_t*)p->d_small;
   if (kins > 0) {
+    PmRowBuf ob = o;
+    ob.w_host = (double*)(p->d_small + kWiOff);
     hipLaunchKernelGGL(k_pm_proposals, dim3(n), dim3(kPropThreads), 0, p->stream, m, W, nl, cfg->eps_mass, cfg->h_tile,
-                       (const int64_t*)act, kins, score, mtile, o);
+                       (const int64_t*)act, kins, score, mtile, ob);
     PMCHK(p, hipGetLastError());
-    std::vector<double> wi(nprop);
-    PMCHK(p, hipMemcpyAsync(wi.data(), o.w, nprop * 8, hipMemcpyDeviceToHost, p->stream));
     gcs_pmap_rows rp{};
     rp.Lambdas = o.lam;
     rp.thetas = o.th;
@@ -1949,14 +2198,37 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
     rp.colors = o.col;
     rp.sources = o.src;
     rp.n = nprop;
-    std::vector<int32_t> ni(n);
-    if (int rc = gcs_pmap_insert_masked(p, tiles, n, kins, &rp, timestamp, scan_seq, cfg->recency_decay_lambda,
-                                        *next_global_id, nullptr, ni.data(), counts))
-      return rc;
+    if (int rc = sort_tiles(p, n, 1, scan_seq, cfg->recency_decay_lambda, kins)) return rc;
+    hipLaunchKernelGGL(k_pm_insert, dim3(n), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, kins,
+                       (const uint32_t*)p->vals, rows_of(&rp), timestamp, (long long)scan_seq,
+                       (long long)*next_global_id, (int64_t*)nullptr, d_ins);
+    PMCHK(p, hipGetLastError());
+  }
+  // per tile: cull (its partials carry the valid count after it), forget (pipeline.py:1413-1447)
+  const int nbt = blocks_per_tile(p->M);
+  hipLaunchKernelGGL(k_pm_cull, dim3(n, nbt), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
+                     cfg->cull_threshold, (double*)(p->d_small + kPartOff));
+  const long tm = (long)n * p->M;
+  hipLaunchKernelGGL(k_pm_forget, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
+                     p->stream, p->st, (const int32_t*)p->d_tiles, n, cfg->forgetting_factor);
+  PMCHK(p, hipGetLastError());
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  if (*(uint32_t*)(p->h_small + 8192)) return pm_fail(p, GCS_ERR_ARG, "target slot out of range (rows skipped)");
+  {
+    const uint32_t* nfb = (const uint32_t*)(p->h_small + 9216);
+    const double* fms = (const double*)(p->h_small + kFmOff);
+    for (int b = 0; b < nb; ++b) {
+      st->fused_count += n * (int32_t)nfb[b];
+      for (int t = 0; t < n; ++t) st->fused_mass_total += fms[b * n + t];  // per (block, tile) sums
+    }
+  }
+  if (kins > 0) {
+    const int32_t* ni = (const int32_t*)p->h_small;
+    const double* wi = (const double*)(p->h_small + kWiOff);
     for (int t = 0; t < n; ++t) {
       st->insert_count_total += ni[t];
       *next_global_id += ni[t];
-      std::vector<double> ws(wi.begin() + (size_t)t * kins, wi.begin() + (size_t)(t + 1) * kins);
+      std::vector<double> ws(wi + (size_t)t * kins, wi + (size_t)(t + 1) * kins);
       double sm = 0.0;
       for (double x : ws) sm += x;
       st->insert_mass_total += sm;
@@ -1965,15 +2237,23 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
       st->insert_mass_p95 = std::max(st->insert_mass_p95, ws[i95]);
     }
   }
-  // per tile: cull, forget, merge-reduce (pipeline.py:1413-1447)
   std::vector<int32_t> nc(n);
-  std::vector<double> md(n), wsum(n);
-  if (int rc = gcs_pmap_cull(p, tiles, n, cfg->cull_threshold, nc.data(), md.data(), wsum.data(), counts)) return rc;
+  std::vector<double> md(n);
+  {
+    const double* h = (const double*)(p->h_small + kPartOff);
+    for (int t = 0; t < n; ++t) {  // block partials folded in block order (gcs_pmap_cull)
+      double a[4] = {0.0, 0.0, 0.0, 0.0};
+      for (int b = 0; b < nbt; ++b)
+        for (int k = 0; k < 4; ++k) a[k] += h[4 * (t * nbt + b) + k];
+      nc[t] = (int32_t)a[0];
+      md[t] = a[1];
+      counts[t] = (int32_t)a[3];
+    }
+  }
   for (int t = 0; t < n; ++t) {
     st->evicted_count += nc[t];
     st->evicted_mass_total += nc[t] ? md[t] : 0.0;
   }
-  if (int rc = gcs_pmap_forget(p, tiles, n, cfg->forgetting_factor)) return rc;
   const bool capped = cfg->merge_max_tile_size > 0 && p->M > cfg->merge_max_tile_size;
   if (!capped && cfg->k_merge_pairs > 0 && p->M >= 2) {
     if (p->M > p->max_merge) return pm_fail(p, GCS_ERR_ARG, "map update: merge needs max_merge >= m_tile");

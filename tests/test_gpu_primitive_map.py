@@ -414,6 +414,22 @@ def _full_sort_check():
     am.close()
 
 
+def test_radix_select_path_matches_oracle():
+    """The register select (M <= 8,192) and the tree top-k (k_pm_topk, larger tiles: the 50,000-slot test
+    above) are the defaults; the one-workgroup radix select (GCSLAM_PM_SELECT=radix) keeps its own
+    parity check."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_primitive_map as t; t._full_sort_check()"
+            % (here, root, os.path.join(root, "gc-slam_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, GCSLAM_PM_SELECT="radix"),
+                       capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
 def test_full_sort_path_matches_oracle():
     """The select is the default for k <= 1024; the rocPRIM full sort (GCSLAM_PM_FULLSORT=1, or k above
     the select's capacity) keeps its own parity check."""
