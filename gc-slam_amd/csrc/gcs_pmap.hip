@@ -695,7 +695,7 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_view(PmStore st, const int32_
     for (int c = 0; c < 3; ++c) o.col[3 * g + c] = rgb[c];
   if (o.ids) o.ids[g] = id;
   if (o.lsup) o.lsup[g] = last;
-  if (o.valid) o.valid[g] = v;
+  if (o.valid) o.valid[g] = v ? 1 : 0;  // 0/1 bytes: the caller may view them as bool
   if (o.slots) o.slots[g] = q;
   if (o.tid) o.tid[g] = tile_ids[t];
 }

@@ -261,18 +261,22 @@ def extract_atlas_map_view(atlas_map: AtlasMap, tile_ids: List[int], m_tile_view
     dev = f"cuda:{atlas_map.device}"
     n, k = len(tile_ids), int(m_tile_view)
     R = n * k
-    t = dict(positions=torch.empty((R, 3), dtype=torch.float64, device=dev),
-             covariances=torch.empty((R, 3, 3), dtype=torch.float64, device=dev),
-             directions=torch.empty((R, 3), dtype=torch.float64, device=dev),
-             kappas=torch.empty((R,), dtype=torch.float64, device=dev),
-             weights=torch.empty((R,), dtype=torch.float64, device=dev),
-             primitive_ids=torch.empty((R,), dtype=torch.int64, device=dev),
-             valid_mask=torch.empty((R,), dtype=torch.uint8, device=dev),
-             last_supported_scan_seq=torch.empty((R,), dtype=torch.int64, device=dev),
-             etas=torch.empty((R, atlas_map.n_lobes, 3), dtype=torch.float64, device=dev),
-             colors=torch.empty((R, 3), dtype=torch.float64, device=dev),
-             candidate_slots=torch.empty((R,), dtype=torch.int32, device=dev),
-             candidate_tile_ids=torch.empty((R,), dtype=torch.int64, device=dev))
+    # one device allocation carved into the twelve outputs (8-byte aligned segments); valid_mask is
+    # written as 0/1 bytes straight into a bool view
+    nl = atlas_map.n_lobes
+    spec = (("positions", torch.float64, (R, 3)), ("covariances", torch.float64, (R, 3, 3)),
+            ("directions", torch.float64, (R, 3)), ("kappas", torch.float64, (R,)), ("weights", torch.float64, (R,)),
+            ("primitive_ids", torch.int64, (R,)), ("last_supported_scan_seq", torch.int64, (R,)),
+            ("etas", torch.float64, (R, nl, 3)), ("colors", torch.float64, (R, 3)),
+            ("candidate_tile_ids", torch.int64, (R,)), ("candidate_slots", torch.int32, (R,)),
+            ("valid_mask", torch.bool, (R,)))
+    sizes = [int(np.prod(shape)) * (8 if dt in (torch.float64, torch.int64) else 4 if dt == torch.int32 else 1)
+             for _, dt, shape in spec]
+    buf = torch.empty(sum((z + 7) // 8 * 8 for z in sizes), dtype=torch.uint8, device=dev)
+    t, off = {}, 0
+    for (name, dt, shape), z in zip(spec, sizes):
+        t[name] = buf[off:off + z].view(dt).view(shape)
+        off += (z + 7) // 8 * 8
     v = L.GcsPmapView()
     for name, x in t.items():
         setattr(v, name, x.data_ptr() if R else None)
@@ -282,7 +286,6 @@ def extract_atlas_map_view(atlas_map: AtlasMap, tile_ids: List[int], m_tile_view
     atlas_map._chk(atlas_map.lib.gcs_pmap_extract_view(atlas_map.h, ip, tids.ctypes.data_as(L.c_int64_p), n, k,
                                                        float(eps_lift), float(eps_mass), C.byref(v)),
                    "gcs_pmap_extract_view")
-    t["valid_mask"] = t["valid_mask"].to(torch.bool)
     return AtlasMapView(tile_ids=torch.as_tensor(tids, device=dev), m_tile_view=k, **t)
 
 

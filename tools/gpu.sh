@@ -10,7 +10,7 @@
 #   sq           SQ instruction-mix / wave-state passes of the hot kernels
 #   phase        per-phase clocks of the bin kernel (needs `make -C gc-slam_amd prof`)
 #   pmap         primitive-map timing (tools/pmap_bench.py)    assoc   association timing
-#   pmapprof     rocprofv3 --kernel-trace --stats of tools/pmap_bench.py
+#   pmapprof     rocprofv3 --kernel-trace --stats of tools/pmap_bench.py (assocprof: of tools/assoc_bench.py)
 #   ab           same-box A/B of two builds: A = libgcslam_hip.so, B = libgcslam_hip_$B.so
 #   envab        same-box A/B of an environment knob: B runs with $ENVB
 #   sweep        bench C2 + C3 per entry of SWEEP="name:lib_suffix:ENV=V,... ..." (library variants / knobs)
@@ -55,6 +55,8 @@ step() {
     pmapprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/pmap_prof" -o run --output-format csv -- \
                 python3 tools/pmap_bench.py 10 > "$O/pmap_prof.log" 2>&1 ;;
     assoc) timeout -k 10 300 python tools/assoc_bench.py > "$O/assoc_bench.txt" 2>&1 ;;
+    assocprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/assoc_prof" -o run --output-format csv -- \
+                 python3 tools/assoc_bench.py > "$O/assoc_prof.log" 2>&1 ;;
     ab)
       for rep in $(seq 1 "${REPS:-2}"); do
         for v in A B; do

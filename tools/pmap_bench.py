@@ -85,7 +85,22 @@ def main():
         seq[0] += 1
         gpm.primitive_map_update(am, b, a, z, tids, 1.0, seq[0])
 
+    # the C-ABI call alone (outputs allocated once, tile list prepared once): what a C caller pays
+    import ctypes as C
+    from gcslam import _lib as L
+    out = gpm.extract_atlas_map_view(am, tids, 1024)
+    vs = L.GcsPmapView()
+    for name, _ in vs._fields_:
+        setattr(vs, name, getattr(out, name).data_ptr())
+    idx = np.ascontiguousarray(np.asarray([am.index(t, create=False) for t in tids], np.int32))
+    tid_arr = np.ascontiguousarray(np.asarray(tids, np.int64))
+    ip, tp = L.iptr(idx), tid_arr.ctypes.data_as(L.c_int64_p)
+
+    def view_c():
+        am._chk(am.lib.gcs_pmap_extract_view(am.h, ip, tp, len(tids), 1024, 1e-9, 1e-12, C.byref(vs)), "view")
+
     for name, fn in (("extract_atlas_map_view 7 x 50,000 -> 7 x 1024", lambda: gpm.extract_atlas_map_view(am, tids, 1024)),
+                     ("gcs_pmap_extract_view (C-ABI call alone) 7 x 50,000 -> 7 x 1024", view_c),
                      ("primitive_map_update (step 12b) N=1536 K=8, 7 tiles", upd),
                      ("primitive_map_recency_inflate 7 tiles", lambda: gpm.primitive_map_recency_inflate(am, tids, 70))):
         med, p90 = timed(fn, iters)
