@@ -449,11 +449,12 @@ def main():
     w_iw, w_bary = (float(x[rank]) for x in hypothesis_weights(world))
     comm_h = comm.h if comm is not None else None
 
-    def combine(count):  # gcs_combine_allreduce: RCCL sum of the payload (N > 1) + combine + IW updates
-        return ctx.combine_allreduce(comm_h, w_iw, w_bary, count, want_belief=False)
+    # gcs_combine_allreduce (RCCL sum of the payload at N > 1, combine, IW updates) and gcs_scan bound once
+    combine = ctx.combine_call(comm_h, w_iw, w_bary)
 
     state = dict(count=0, sample=False, sampled=0)
     scan_out = L.GcsScanOutputs()  # one output record for every scan (the caller-owned buffer form)
+    scan_fn = ctx.scan_call(scan_out)
     # pre-device host, device submit+wait, host tail, whole gcs_scan, combine, then the sub-spans
     # (budget launch + predict, device launch calls, tail numerics, pushforward launch calls)
     host_ms = np.zeros(9)
@@ -465,7 +466,8 @@ def main():
                 ctx.enable_timing(True, stages=["bins"])
             elif phase == 1:
                 ctx.enable_timing(False)
-        out = ctx.scan_prepared(prepared[state["count"] % N_SCANS], scan_out)
+        scan_fn(prepared[state["count"] % N_SCANS])
+        out = scan_out
         if state["count"] % TIMING_STRIDE == TIMING_STRIDE // 2:  # host sub-spans: sampled scans without event stamps
             tc = time.perf_counter()
             combine(state["count"])

@@ -124,6 +124,7 @@ struct gcs_ctx {
   // recorded on the main stream behind the scan's device stages; the pushforward's stream waits for
   // it (wait_mirror returns before the main stream is idle)
   hipEvent_t ev_stages = nullptr;
+  bool stages_done = false;  // wait_mirror saw the scan's stages complete (no event wait for the push)
   bool push_pending = false;
   bool push_main = false;  // experiment knob (GCSLAM_PUSH_MAIN=1): k_pushforward on the main stream
   // Asynchronous pushforward launch (GCSLAM_PUSH_THREAD=0 turns it off): the launch calls of
@@ -569,10 +570,12 @@ int wait_mirror(gcs_ctx* c) {
     }
     if (*ready != 0.0) {
       std::atomic_thread_fence(std::memory_order_acquire);
+      c->stages_done = true;
       return GCS_OK;
     }
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->stages_done = true;
   return GCS_OK;
 }
 
@@ -580,8 +583,19 @@ int stage_pt(gcs_ctx* c, bool to_host = false) {
   StageEv ev = stage_ev(c, ST_PT);
   if (to_host) c->h_scalars[SC_COUNT] = 0.0;  // re-armed: the fold writes 1 after the mirror
   HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
-                      to_host ? c->d_scalars_mirror : nullptr, c->d_flags, c->d_touched, c->stream, ev.e0, ev.e1));
+                      to_host ? c->d_scalars_mirror : nullptr, c->d_flags, c->d_touched, c->d_tickets + 1, c->stream,
+                      ev.e0, ev.e1));
   if (to_host) HIPCHK(c, hipEventRecord(c->ev_stages, c->stream));
+  c->stages_done = false;
+  return GCS_OK;
+}
+
+// the next scan's bin-tile dispatch order, queued on the main stream behind the scan's stages (the
+// device is idle while the host runs the tail; the next bin kernel is behind it in stream order)
+int stage_tile_order(gcs_ctx* c) {
+  if (!c->tile_order_on) return GCS_OK;
+  HIPCHK(c, launch_tile_order(c->d_tile_dirty, c->d_tile_work, bins_scale_blocks(c->B, c->tile_bins), c->d_tile_order,
+                              c->stream));
   return GCS_OK;
 }
 
@@ -607,12 +621,11 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, 
     for (int j = 0; j < 3; ++j) pa.G[3 * i + j] = RS[3 * i] * pa.R[3 * j] + RS[3 * i + 1] * pa.R[3 * j + 1] + RS[3 * i + 2] * pa.R[3 * j + 2];
   pa.gamma = gamma;
   StageEv ev = stage_ev(c, ST_PUSH);
-  if (s != c->stream) HIPCHK(ec, hipStreamWaitEvent(s, c->ev_stages, 0));
+  // the main stream's stages are complete once wait_mirror saw the fold's ready word (the fold is
+  // the stream's last kernel before it): only the other paths order the push stream by the event
+  if (s != c->stream && !c->stages_done) HIPCHK(ec, hipStreamWaitEvent(s, c->ev_stages, 0));
   HIPCHK(ec, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, partials, c->d_scalars, flags,
                                c->d_touched, s, ev.e0, ev.e1));
-  if (c->tile_order_on)
-    HIPCHK(ec, launch_tile_order(c->d_tile_dirty, c->d_tile_work, bins_scale_blocks(c->B, c->tile_bins),
-                                 c->d_tile_order, s));
   if (s != c->stream) {
     HIPCHK(ec, hipEventRecord(c->ev_push, s));
     c->push_pending = true;
@@ -849,9 +862,10 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_part_push, partials_need(push_blocks(c->B), 10) * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
-  if (bad(hipMalloc(&c->d_tickets, sizeof(uint32_t)))) return GCS_ERR_HIP;
+  // [0] k_scan's ticket, [1] k_pt's last-block fold ticket (each re-armed by its last block)
+  if (bad(hipMalloc(&c->d_tickets, 4 * sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_parse_flag, sizeof(uint32_t)))) return GCS_ERR_HIP;
-  if (bad(hipMemset(c->d_tickets, 0, sizeof(uint32_t)))) return GCS_ERR_HIP;
+  if (bad(hipMemset(c->d_tickets, 0, 4 * sizeof(uint32_t)))) return GCS_ERR_HIP;
   // SC_COUNT scalars + the ready word k_final<.., mirror> writes last (wait_mirror)
   if (bad(hipHostMalloc(&c->h_scalars, (SC_COUNT + 8) * sizeof(double), hipHostMallocMapped))) return GCS_ERR_HIP;
   c->h_scalars[SC_COUNT] = 0.0;
@@ -1336,8 +1350,10 @@ int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st) {
   cert[38] = st.sigma_warp;
   std::vector<double>& wimu = c->wimu;
   wimu.resize(in->imu_len);
-  for (int i = 0; i < in->imu_len; ++i)
-    wimu[i] = smooth_window(in->imu_stamps[i], in->scan_start_time, in->scan_end_time, st.sigma_warp);
+  for (int i = 0; i < in->imu_len; ++i)  // a repeated stamp (the window's zero padding) reuses its value
+    wimu[i] = i > 0 && in->imu_stamps[i] == in->imu_stamps[i - 1]
+                  ? wimu[i - 1]
+                  : smooth_window(in->imu_stamps[i], in->scan_start_time, in->scan_end_time, st.sigma_warp);
   host::spd_factor_solve(fpred, st.pred.h, st.mu_inc);
   host::world_pose_from_increment(st.prev, st.mu_prev, st.pose0);
   host::preintegrate_imu(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wimu.data(), st.pose0 + 3,
@@ -1358,7 +1374,9 @@ int scan_imu_odom(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st, gcs
   std::vector<double>& wint = c->wint;
   wint.resize(in->imu_len);
   for (int i = 0; i < in->imu_len; ++i)
-    wint[i] = smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, st.sigma_warp);
+    wint[i] = i > 0 && in->imu_stamps[i] == in->imu_stamps[i - 1]
+                  ? wint[i - 1]
+                  : smooth_window(in->imu_stamps[i], in->t_last_scan, in->t_scan, st.sigma_warp);
   host::imu_meas_iw_suffstats(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wint.data(), st.mu_inc + 9,
                               st.mu_inc + 12, st.pose0 + 3, c->grav, out->iw_meas_dPsi, out->iw_meas_dnu);
   host::world_pose_from_increment(st.pred, st.mu_inc, st.pose_pred);
@@ -1691,6 +1709,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
   if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
   if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+  if ((rc = stage_tile_order(c))) return rc;
   st.Ts = clk::now();
   if ((rc = scan_imu_odom(c, in, st, out))) return rc;
   if ((rc = wait_mirror(c))) return rc;  // the PT fold has written the scalars to h_scalars
@@ -1710,7 +1729,9 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
       return rc;
     if ((rc = stage_bins(c))) return rc;
     if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+    if ((rc = stage_tile_order(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->stages_done = true;
     if ((rc = check_bucket_err(c))) return rc;
   }
   st.cert[41] = c->h_err[1] ? 1.0 : 0.0;  // a bucket above the ranking capacity took the compaction path

@@ -1601,11 +1601,40 @@ __global__ __launch_bounds__(kBlock) void k_mf(const double* __restrict__ scan, 
 // Sigma = eps I, gcs_math.h psd_project3): its term is computed from those constants without
 // reading the bin (bitwise the same term).  act == nullptr (dense mode): every bin is read.
 constexpr int kPtNV = 13;
+enum FinalKind : int { FIN_BUDGET, FIN_POINTS, FIN_BINS, FIN_DENSE, FIN_MF, FIN_PT, FIN_TOTALS };
+
+template <int NV, int KIND>
+__device__ __forceinline__ void final_epilogue(const double (&v)[NV], double* scalars) {
+  if (KIND == FIN_BUDGET) {
+    scalars[SC_MASS_IN] = v[0];
+    scalars[SC_MASS_SEL] = v[1];
+    scalars[SC_MASS_SCALE] = v[0] / (v[1] + kEpsMass);  // point_budget.py:80-84
+  } else if (KIND == FIN_POINTS) {
+    for (int k = 0; k < 5; ++k) scalars[SC_DESKEW_WIN + k] = v[k];
+  } else if (KIND == FIN_BINS) {
+    for (int k = 0; k < 5; ++k) scalars[SC_BIN_NSUM + k] = v[k];
+    mf_finish(v + 5, scalars);
+  } else if (KIND == FIN_DENSE) {
+    for (int k = 0; k < 5; ++k) scalars[SC_BIN_NSUM + k] = v[k];
+  } else if (KIND == FIN_MF) {
+    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[11 + k];
+    scalars[SC_MF_MAPND] = v[20];
+    mf_finish(v, scalars);
+  } else if (KIND == FIN_PT) {
+    for (int k = 0; k < 9; ++k) scalars[SC_PT_L + k] = v[k];
+    for (int k = 0; k < 3; ++k) scalars[SC_PT_H + k] = v[9 + k];
+    scalars[SC_PT_NEFF] = v[12];
+  } else if (KIND == FIN_TOTALS) {
+    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[k];
+    scalars[SC_MF_MAPND] = v[9];
+  }
+}
+
 __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, const double* __restrict__ map,
-                                               const double* __restrict__ derived, int B,
-                                               const double* __restrict__ scalars, double* partials,
-                                               const uint8_t* __restrict__ act, const uint8_t* __restrict__ touched) {
-  __shared__ double lds[kWaves * kPtNV];
+                                               const double* __restrict__ derived, int B, double* scalars,
+                                               double* partials, const uint8_t* __restrict__ act,
+                                               const uint8_t* __restrict__ touched) {
+  __shared__ double lds[kWaves * pstride<kPtNV>()];
   double R[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) R[k] = scalars[SC_MF_R + k];
@@ -1853,35 +1882,6 @@ __global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict_
 }
 
 // ---------------------------------------------------------------- one-block folds of block partials
-enum FinalKind : int { FIN_BUDGET, FIN_POINTS, FIN_BINS, FIN_DENSE, FIN_MF, FIN_PT, FIN_TOTALS };
-
-template <int NV, int KIND>
-__device__ __forceinline__ void final_epilogue(const double (&v)[NV], double* scalars) {
-  if (KIND == FIN_BUDGET) {
-    scalars[SC_MASS_IN] = v[0];
-    scalars[SC_MASS_SEL] = v[1];
-    scalars[SC_MASS_SCALE] = v[0] / (v[1] + kEpsMass);  // point_budget.py:80-84
-  } else if (KIND == FIN_POINTS) {
-    for (int k = 0; k < 5; ++k) scalars[SC_DESKEW_WIN + k] = v[k];
-  } else if (KIND == FIN_BINS) {
-    for (int k = 0; k < 5; ++k) scalars[SC_BIN_NSUM + k] = v[k];
-    mf_finish(v + 5, scalars);
-  } else if (KIND == FIN_DENSE) {
-    for (int k = 0; k < 5; ++k) scalars[SC_BIN_NSUM + k] = v[k];
-  } else if (KIND == FIN_MF) {
-    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[11 + k];
-    scalars[SC_MF_MAPND] = v[20];
-    mf_finish(v, scalars);
-  } else if (KIND == FIN_PT) {
-    for (int k = 0; k < 9; ++k) scalars[SC_PT_L + k] = v[k];
-    for (int k = 0; k < 3; ++k) scalars[SC_PT_H + k] = v[9 + k];
-    scalars[SC_PT_NEFF] = v[12];
-  } else if (KIND == FIN_TOTALS) {
-    for (int k = 0; k < 9; ++k) scalars[SC_MF_MAPSCAT + k] = v[k];
-    scalars[SC_MF_MAPND] = v[9];
-  }
-}
-
 // mirror (may be null): after the epilogue the whole scalar block is copied to this mapped host
 // buffer, so the host reads the scan's results without a separate D2H copy.
 template <int NV, unsigned MAXMASK, int KIND, int NT = kBlock>
@@ -1958,11 +1958,25 @@ size_t partials_need(long nblocks, int nv) {
 // to scan): its long tiles start in the first round and the clean tiles fill the last one.  Only
 // the dispatch order changes -- each tile's rows and partial row are the same whichever block
 // computes them.
-constexpr int kOrderNT = 1024, kOrderClasses = 5;
-__global__ __launch_bounds__(kOrderNT) void k_tile_order(const uint8_t* __restrict__ active,
-                                                         const uint32_t* __restrict__ work, int n, int* order) {
+constexpr int kOrderNT = 1024, kOrderClasses = 5, kOrderLds = 8192;
+__global__ __launch_bounds__(kOrderNT) void k_tile_order(const uint8_t* active, const uint32_t* work, int n,
+                                                         int* order) {
   __shared__ uint32_t s_sum[2][kOrderNT / 64];
   __shared__ int s_cnt[kOrderClasses][kOrderNT / 64];
+  // up to kOrderLds tiles: the flags and work staged in LDS by coalesced loads (the per-thread chunks
+  // below then read LDS, not memory: 19 -> a few us at C3's 8,192 tiles)
+  __shared__ uint32_t s_w[kOrderLds];
+  __shared__ uint8_t s_a[kOrderLds];
+  const bool lds = n <= kOrderLds;
+  if (lds) {
+    for (int j = threadIdx.x; j < n; j += kOrderNT) {
+      s_a[j] = active[j];
+      s_w[j] = work[j];
+    }
+    __syncthreads();
+    active = s_a;
+    work = s_w;
+  }
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int chunk = (n + kOrderNT - 1) / kOrderNT;
   const int j0 = min(n, t * chunk), j1 = min(n, j0 + chunk);
@@ -2118,6 +2132,7 @@ hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream
     hipExtLaunchKernelGGL((k_bins_scale<kStage256Big, 256, 1, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else if (a.tile_bins == 256)
     hipExtLaunchKernelGGL((k_bins_scale<kStage256Small, 256, 1, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+  // (eight lanes per bin on the 64-bin tile, 512 threads: 35.2 vs 25.4 us at C2, same box)
   else if (big)
     hipExtLaunchKernelGGL((k_bins_scale<kStageBig, 64, 4, GCS_DALL64>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else
@@ -2145,10 +2160,14 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 }
 
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
-                     hipEvent_t e0, hipEvent_t e1) {
-  hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B,
-                        (const double*)scalars, partials, act, touched);
+                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, uint32_t* ticket,
+                     hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+  // (a last-block fold in k_pt -- ticket with an agent-scope release per block -- measured slower:
+  // 16.4 vs 12.3 us at C2, 46 vs 25 us at C3; each release writes back an L2 full of the bin
+  // kernel's rows)
+  (void)ticket;
+  hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B, scalars, partials,
+                        act, touched);
   GCS_FINAL_M(kPtNV, 0u, FIN_PT, nblk, s, e1, partials, scalars, mirror);
   return hipGetLastError();
 }

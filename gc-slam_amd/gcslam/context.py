@@ -313,6 +313,17 @@ class HypothesisContext:
         inp, keep = self._scan_inputs(*args, **kw)
         return (inp, C.byref(inp), keep)
 
+    def scan_call(self, out):
+        """gcs_scan bound once for prepare_scan() structs into the caller-owned out; returns
+        call(prepared) -> None, raising on failure."""
+        fn, h, po = self.lib.gcs_scan, self.h, C.byref(out)
+
+        def call(prepared):
+            rc = fn(h, prepared[1], po)
+            if rc:
+                self._chk(rc, "gcs_scan")
+        return call
+
     def scan_prepared(self, prepared, out):
         """gcs_scan on a prepare_scan() struct into a caller-owned GcsScanOutputs (one ctypes call)."""
         rc = self.lib.gcs_scan(self.h, prepared[1], C.byref(out))
@@ -378,6 +389,18 @@ class HypothesisContext:
                                                  C.addressof(b) if want_belief else None, cert.ctypes.data),
                   "combine_allreduce")
         return (L.struct_to_arrays(b) if want_belief else None), cert
+
+    def combine_call(self, comm, w_iw, w_bary):
+        """gcs_combine_allreduce bound once (the caller's per-scan loop: arguments converted and the cert
+        buffer allocated here, not per call); returns call(scan_count) -> None, raising on failure."""
+        fn, h, cert = self.lib.gcs_combine_allreduce, self.h, (C.c_double * 4)()
+        comm, w_iw, w_bary = comm, float(w_iw), float(w_bary)
+
+        def call(scan_count):
+            rc = fn(h, comm, w_iw, w_bary, scan_count, None, cert)
+            if rc:
+                self._chk(rc, "combine_allreduce")
+        return call
 
     def hypothesis_combine(self, payload_sum, scan_count, want_belief=True):
         """Barycenter + IW update from the summed payload; returns (belief arrays or None, cert)."""
