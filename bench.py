@@ -82,6 +82,8 @@ def roofline(N, B, kernel_ms, traffic=None, traffic_source=None):
             "read_GBs": rd / s / 1e9, "read_frac": rd / s / 1e9 / HBM_PEAK_GBS,
             "write_GBs": wr / s / 1e9, "write_frac": wr / s / 1e9 / HBM_PEAK_GBS,
             "traffic": traffic, "traffic_source": traffic_source,
+            # the counter-based rate beside the algorithmic one: PMC HBM bytes per launch / the same duration
+            "traffic_frac": (traffic / s / 1e9 / HBM_PEAK_GBS) if traffic else None,
             "kernel": "k_bins_scale (BinSoftAssign+ScanBinMomentMatch+kappa+MF terms)",
             "algorithmic_bytes_per_launch": rd + wr, "algorithmic_read_bytes": rd, "algorithmic_write_bytes": wr,
             "kernel_us": kernel_ms * 1e3}
