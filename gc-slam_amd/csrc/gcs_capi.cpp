@@ -138,7 +138,11 @@ struct gcs_ctx {
   std::mutex push_mu;
   std::condition_variable push_cv;
   struct PushJob {
-    int kind;  // 0: the scan's pushforward, 1: the next scan's k_budget (row 1 mass sums)
+    // 0: the scan's pushforward, 1: the next scan's k_budget (row 1 mass sums), 2: the scan's device
+    // front (k_budget, the gated k_points, the push join, the bin kernel + fold, k_pt + fold, k_tile_order)
+    int kind;
+    const gcs_scan_inputs* in;
+    uint64_t seq;
     double z_t[6], Sig6[36], gamma;
     hipStream_t s;
     double* partials;
@@ -148,6 +152,13 @@ struct gcs_ctx {
   } push_job{};
   int push_rc = 0;
   std::string push_err;
+  // launch gate of the pre-launched point stage (gcs_scan): [0] sequence word, [1..6] the deskew twist;
+  // coherent host memory polled by k_points (GCSLAM_GATE=0: the point stage is launched after the prologue)
+  uint64_t* h_gate = nullptr;
+  uint64_t* d_gate = nullptr;
+  uint64_t gate_seq = 0, gate_next = 0;
+  bool gate_on = true;
+  bool gate_withhold = false;  // fault test (GCS_DEBUG_LAUNCH_GATE = -1): the gate is never opened
   int pts_blocks = 0;
   bool pts_fold_pending = false;
   double* d_scalars = nullptr;
@@ -173,6 +184,12 @@ struct gcs_ctx {
   double* d_payload = nullptr;
   // host state
   Belief belief{};
+  // the lifted Cholesky factor of belief.L and its inverse, left by the last scan's tail (the
+  // recompose factors post.L, and the anchor drift keeps L): the next PredictDiffusion starts from
+  // them instead of factoring and inverting the same matrix again.  Cleared by gcs_ctx_set_belief.
+  bool prev_fac_valid = false;
+  host::SpdFactor prev_fac;
+  double prev_cov[DZ * DZ];
   double iw_nu[7], iw_Psi[7 * 36], Q[DZ * DZ];
   double last_dPsi[7 * 36], last_dnu[7];
   double meas_nu[3], meas_Psi[3 * 9], meas_cert[2] = {0.0, 0.0};  // measurement-noise IW state
@@ -198,16 +215,19 @@ namespace {
 // Without a context (the push worker's calls) the message goes to this thread's slot, so the
 // worker reports the failing call's own error text rather than a later hipGetLastError().
 thread_local std::string t_fail_msg;
+// set on the push worker: its stage calls report into t_fail_msg (the main thread owns c->err), make
+// their launches themselves and do not wait for their own job
+thread_local bool t_on_worker = false;
 
 int fail(gcs_ctx* c, int code, const std::string& m) {
-  if (c) c->err = m;
+  if (c && !t_on_worker) c->err = m;
   else t_fail_msg = m;
   return code;
 }
 
 // wait until the push worker has made the launch calls of the last submitted pushforward
 int push_wait(gcs_ctx* c) {
-  if (!c->push_thread.joinable()) return GCS_OK;
+  if (t_on_worker || !c->push_thread.joinable()) return GCS_OK;
   const uint64_t r = c->push_req.load(std::memory_order_acquire);
   while (c->push_done.load(std::memory_order_acquire) != r) __builtin_ia32_pause();
   if (c->push_rc) {
@@ -388,7 +408,7 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true) {
   c->budget_blocks = red_blocks(std::max(n_raw, 1));
   c->budget_pending = true;
   StageEv ev = stage_ev(c, ST_BUDGET);
-  if (!ev.e0 && c->push_async) return submit_budget(c, ba, c->budget_blocks, s);
+  if (!ev.e0 && c->push_async && !t_on_worker) return submit_budget(c, ba, c->budget_blocks, s);
   if (int rc = push_wait(c)) return rc;  // the worker's queued launches precede this one on the stream
   HIPCHK(c, launch_budget(ba, c->budget_blocks, s, ev.e0, ev.e1));
   return GCS_OK;
@@ -453,6 +473,12 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.nearest_out = c->d_nearest;  // device ids
   a.iz_out = iz_out;
   a.t_out = t_out;
+  if (c->gate_next) {  // pre-launched by the scan front: the twist comes through the gate
+    a.gate = c->d_gate;
+    a.gate_seq = c->gate_next;
+    a.gate_err = c->d_err + 3;
+    c->gate_next = 0;
+  }
   c->iz_valid = false;
   const bool scale = c->cfg.mode == GCS_MODE_SCALE && !deskew_only;
   if (deskew_only) {
@@ -635,8 +661,11 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, 
 
 // The push worker: waits (spin, then sleep) for a submitted job and makes its launch calls with the
 // job's captured arguments (the flags buffer of that scan; the context's device buffers are fixed).
+int scan_front(gcs_ctx* c, const gcs_scan_inputs* in, uint64_t seq);
+
 void push_worker(gcs_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
+  t_on_worker = true;
   uint64_t seen = 0;
   for (;;) {
     // spin for up to 2 ms after the last job (a scan every 0.1-0.3 ms keeps the worker awake: a
@@ -665,6 +694,9 @@ void push_worker(gcs_ctx* c) {
         rc = GCS_ERR_HIP;
         c->push_err = "k_budget launch (worker): " + std::string(hipGetErrorString(e));
       }
+    } else if (j.kind == 2) {
+      rc = scan_front(c, j.in, j.seq);
+      if (rc) c->push_err = "scan front launch (worker): " + t_fail_msg;
     } else {
       rc = stage_push(c, j.z_t, j.Sig6, j.gamma, j.s, j.partials, j.flags, true);
       if (rc) c->push_err = "pushforward launch (worker): " + t_fail_msg;
@@ -718,6 +750,67 @@ int submit_budget(gcs_ctx* c, const BudgetArgs& ba, int nblk, hipStream_t s) {
   }
   return GCS_OK;
 }
+
+// The scan's device front, queued by the worker while the main thread runs the host prologue:
+// k_budget, k_points behind the launch gate (it waits on the device for the twist), the join with
+// the last pushforward, the bin kernel + fold, k_pt + fold (mirror, ready word) and k_tile_order --
+// the launch calls and the dispatch latency of the point stage leave the scan's critical path.
+int scan_front(gcs_ctx* c, const gcs_scan_inputs* in, uint64_t seq) {
+  static const double kNoTwist[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  c->budget_pending = false;
+  c->gate_next = seq;
+  if (int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
+                            in->scan_start_time, in->scan_end_time, kNoTwist, nullptr, nullptr, nullptr,
+                            /*fold_later=*/true, in->xyz_format == 1))
+    return rc;
+  if (int rc = join_push(c)) return rc;
+  if (int rc = stage_bins(c)) return rc;
+  if (int rc = stage_pt(c, /*to_host=*/true)) return rc;
+  return stage_tile_order(c);
+}
+
+int submit_front(gcs_ctx* c, const gcs_scan_inputs* in, uint64_t seq) {
+  if (int rc = push_wait(c)) return rc;  // the previous job (the last scan's pushforward) is launched
+  if (!c->push_thread.joinable()) c->push_thread = std::thread(push_worker, c);
+  gcs_ctx::PushJob& j = c->push_job;
+  j.kind = 2;
+  j.in = in;
+  j.seq = seq;
+  c->push_req.fetch_add(1);
+  if (c->push_sleeping.load()) {
+    std::lock_guard<std::mutex> lk(c->push_mu);
+    c->push_cv.notify_one();
+  }
+  return GCS_OK;
+}
+
+// the twist, then the sequence word (x86 stores are ordered; the fence keeps the compiler's order)
+void open_gate(gcs_ctx* c, const double* xi) {
+  volatile uint64_t* g = c->h_gate;
+  for (int k = 0; k < 6; ++k) {
+    uint64_t u;
+    memcpy(&u, xi + k, sizeof(u));
+    g[1 + k] = u;
+  }
+  std::atomic_thread_fence(std::memory_order_release);
+  __atomic_store_n(c->h_gate, c->gate_seq, __ATOMIC_RELEASE);
+}
+
+// On every early return of a pre-launched scan: opens the gate (zero twist), so no point block waits
+// for its timeout, and waits for the worker's launch calls, which read the context's per-scan state
+struct GateGuard {
+  gcs_ctx* c;
+  bool open = false, joined = false;
+  ~GateGuard() {
+    static const double kNoTwist[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    if (!open && !c->gate_withhold) open_gate(c, kNoTwist);
+    if (!joined) {
+      const std::string keep = c->err;  // the scan's own failure is the message to report
+      (void)push_wait(c);
+      c->err = keep;
+    }
+  }
+};
 
 // after a stream sync: a k_scan whose look-back bound ran out left wrong bucket starts
 int check_bucket_err(gcs_ctx* c) {
@@ -873,6 +966,11 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipHostMalloc(&c->h_err, 4 * sizeof(uint32_t), hipHostMallocMapped))) return GCS_ERR_HIP;
   c->h_err[0] = c->h_err[1] = c->h_err[2] = c->h_err[3] = 0u;
   if (bad(hipHostGetDevicePointer((void**)&c->d_err, c->h_err, 0))) return GCS_ERR_HIP;
+  if (bad(hipHostMalloc(&c->h_gate, 8 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent)))
+    return GCS_ERR_HIP;
+  for (int k = 0; k < 8; ++k) c->h_gate[k] = 0u;
+  if (bad(hipHostGetDevicePointer((void**)&c->d_gate, c->h_gate, 0))) return GCS_ERR_HIP;
+  if (const char* g = getenv("GCSLAM_GATE")) c->gate_on = atoi(g) != 0;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_rknn_off, (B + 1) * sizeof(int)))) return GCS_ERR_HIP;
@@ -960,6 +1058,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
     if (p) (void)hipFree(p);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
   if (c->h_err) (void)hipHostFree(c->h_err);
+  if (c->h_gate) (void)hipHostFree(c->h_gate);
   if (c->h_payload) (void)hipHostFree(c->h_payload);
   if (c->d_payload) (void)hipFree(c->d_payload);
   for (int st = 0; st < kStages; ++st)
@@ -1012,6 +1111,11 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
     case GCS_DEBUG_INJECT_SCAN_FAIL:
       c->inject_scan_fail = value ? 1 : 0;
       return GCS_OK;
+    case GCS_DEBUG_LAUNCH_GATE:
+      if (value < -1 || value > 1) return fail(c, GCS_ERR_ARG, "launch gate: -1, 0 or 1");
+      c->gate_on = value != 0;
+      c->gate_withhold = value < 0;
+      return GCS_OK;
     default:
       return fail(c, GCS_ERR_ARG, "unknown debug key");
   }
@@ -1028,6 +1132,7 @@ int gcs_ctx_enable_timing(gcs_ctx* c, int32_t stage_mask) {
 
 int gcs_ctx_stage_times(gcs_ctx* c, double* ms_sum, int64_t* counts, int32_t reset) {
   if (!c) return GCS_ERR_ARG;
+  if (int rc = push_wait(c)) return rc;  // the worker queues stage events of the scan front
   harvest(c);
   for (int st = 0; st < kStages; ++st) {
     if (ms_sum) ms_sum[st] = c->stage_ms_sum[st];
@@ -1055,6 +1160,7 @@ int gcs_ctx_get_atlas(gcs_ctx* c, double* dirs, int32_t* knn) {
 int gcs_ctx_set_belief(gcs_ctx* c, const gcs_belief* b) {
   if (!c || !b) return GCS_ERR_ARG;
   to_host_belief(*b, c->belief);
+  c->prev_fac_valid = false;
   return GCS_OK;
 }
 
@@ -1323,10 +1429,12 @@ struct LidarTerms {
 
 // 1 (launch), 2 PredictDiffusion, 3 IMU membership window + preintegration -> deskew twist
 // (pipeline.py:399-483)
-int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st) {
+int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st, bool budget = true) {
   st.T0 = clk::now();
-  c->budget_pending = false;
-  if (int rc0 = stage_budget(c, in->weights_dev, in->n_points)) return rc0;  // runs during the prologue
+  if (budget) {  // (the pre-launched front queues k_budget itself)
+    c->budget_pending = false;
+    if (int rc0 = stage_budget(c, in->weights_dev, in->n_points)) return rc0;  // runs during the prologue
+  }
   const double* Q = in->Q ? in->Q : c->Q;
   double* cert = st.cert;
   memset(cert, 0, sizeof(st.cert));
@@ -1336,7 +1444,8 @@ int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st) {
   // 2 PredictDiffusion
   st.prev = c->belief;
   double pinfl[3];
-  host::predict_diffusion(st.prev, Q, in->dt_sec, st.pred, pinfl, st.mu_prev);
+  host::predict_diffusion(st.prev, Q, in->dt_sec, st.pred, pinfl, st.mu_prev,
+                          c->prev_fac_valid ? &c->prev_fac : nullptr, c->prev_cov);
   cert[6] = pinfl[0]; cert[7] = pinfl[1]; cert[8] = pinfl[2];
   st.Tsum += trig(pinfl[0], pinfl[1], 0, 0, 0, pinfl[2], 1, 1, 1);
   st.Tp = clk::now();
@@ -1671,6 +1780,9 @@ int scan_tail(gcs_ctx* c, gcs_scan_state& st, const LidarTerms& lt, gcs_scan_out
   for (int i = 0; i < DZ; ++i)
     if (!std::isfinite(fin.h[i])) return fail(c, GCS_ERR_NONFINITE, "non-finite belief after scan");
   c->belief = fin;
+  c->prev_fac = fpost;  // fin.L == post.L: recompose and the anchor drift change h, not L
+  memcpy(c->prev_cov, covr, sizeof(c->prev_cov));
+  c->prev_fac_valid = true;
   from_host_belief(fin, out->belief);
   c->have_last = true;
   memcpy(out->cert, cert, sizeof(out->cert));
@@ -1699,20 +1811,43 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     ~DirectOff() { c->use_direct = false; }  // per-operator entry points always take the sorted path
   } direct_off{c};
   gcs_scan_state& st = *c->scan_st;
-  if (int rc = scan_prologue(c, in, st)) return rc;
-  // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
-  int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
-                        in->scan_start_time, in->scan_end_time, st.xi, nullptr, nullptr, nullptr, /*fold_later=*/true,
-                        in->xyz_format == 1);
-  if (rc) return rc;
-  if (int rc_ = join_push(c)) return rc_;  // the bin kernel reads the map the previous scan's pushforward wrote
-  if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
-  if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
-  if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
-  if ((rc = stage_tile_order(c))) return rc;
-  st.Ts = clk::now();
-  if ((rc = scan_imu_odom(c, in, st, out))) return rc;
-  if ((rc = wait_mirror(c))) return rc;  // the PT fold has written the scalars to h_scalars
+  int rc = 0;
+  // pre-launched front (direct buckets, worker thread, budget / point stages not event-timed): the
+  // device stages are queued now and the point kernel waits on the device for the prologue's twist
+  const uint32_t front_timed = (1u << ST_BUDGET) | (1u << ST_POINTS);
+  if (c->gate_on && c->push_async && c->use_direct && c->h_gate && !(c->timing_mask & front_timed)) {
+    GateGuard guard{c};
+    ++c->gate_seq;
+    st.T0 = clk::now();
+    if ((rc = submit_front(c, in, c->gate_seq))) return rc;
+    if ((rc = scan_prologue(c, in, st, /*budget=*/false))) return rc;
+    if (!c->gate_withhold) open_gate(c, st.xi);
+    guard.open = true;
+    st.Ts = clk::now();
+    if ((rc = scan_imu_odom(c, in, st, out))) return rc;
+    guard.joined = true;
+    if ((rc = push_wait(c))) return rc;  // the front's launch calls (and their errors)
+    if ((rc = wait_mirror(c))) return rc;
+    if (c->h_err[3]) {
+      c->h_err[3] = 0u;
+      return fail(c, GCS_ERR_HIP, "k_points: launch gate not opened within its timeout");
+    }
+  } else {
+    if ((rc = scan_prologue(c, in, st))) return rc;
+    // 1,3,4-6 device: budget, deskew, soft assign, moment match; 7,8 MF + planar reductions
+    rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
+                      in->scan_start_time, in->scan_end_time, st.xi, nullptr, nullptr, nullptr, /*fold_later=*/true,
+                      in->xyz_format == 1);
+    if (rc) return rc;
+    if (int rc_ = join_push(c)) return rc_;  // the bin kernel reads the map the previous scan's pushforward wrote
+    if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
+    if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
+    if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+    if ((rc = stage_tile_order(c))) return rc;
+    st.Ts = clk::now();
+    if ((rc = scan_imu_odom(c, in, st, out))) return rc;
+    if ((rc = wait_mirror(c))) return rc;  // the PT fold has written the scalars to h_scalars
+  }
   if ((rc = check_bucket_err(c))) return rc;
   bool redone = false;
   if (c->use_direct && c->h_err[2]) {

@@ -50,8 +50,10 @@ void mean_world_pose(const Belief& b, double* pose6);
 void world_pose_from_increment(const Belief& b, const double* dz, double* pose6);
 
 // predict_diffusion (predict.py:43-103); infl = [lift_strength, psd_delta, dt_scale]
+// prev_fac / prev_cov (optional): spd_factor_lifted(prev.L) and its inverse, already computed
 void predict_diffusion(const Belief& prev, const double* Q, double dt, Belief& pred, double* infl3,
-                       double* mean_prev_out = nullptr /*DZ, optional: prev's mean increment*/);
+                       double* mean_prev_out = nullptr /*DZ, optional: prev's mean increment*/,
+                       const SpdFactor* prev_fac = nullptr, const double* prev_cov = nullptr);
 
 struct PreintOut {
   double delta_pose[6];  // [R0^T p, Log(R0^T R_end)]: delta_pose[0:3] is delta_p_body

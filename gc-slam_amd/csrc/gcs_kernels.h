@@ -79,7 +79,15 @@ struct PointKernelArgs {
   int* nearest_out;
   double* iz_out;  // 1 / Z per point (per-operator soft-assign materialisation; the record holds w / Z)
   double* t_out;   // budget-selected timestamps (deskew-only stage: n_bins == 0)
+  // launch gate (gcs_scan's pre-launched point stage; null: xi above is the twist): the kernel is
+  // queued before the host prologue has the deskew twist, and thread 0 of every block polls
+  // gate[0] (host-mapped, coherent) until it holds gate_seq, then reads the twist from gate[1..6].
+  // A gate not opened within kGateTimeoutTicks sets *gate_err and the block runs with a zero twist.
+  const uint64_t* gate;
+  uint64_t gate_seq;
+  uint32_t* gate_err;
 };
+constexpr uint64_t kGateTimeoutTicks = 20000000ull;  // 200 ms of the 100 MHz constant clock
 
 struct BucketArgs {
   int n_bins, k;

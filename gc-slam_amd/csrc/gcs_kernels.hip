@@ -323,6 +323,46 @@ void k_points(PointKernelArgs a, double* partials) {
     brow[k] = r < a.budget_blocks ? *(const double2*)(a.budget_partials + (size_t)r * pstride<2>())
                                   : make_double2(0.0, 0.0);
   }
+  double xi[6];
+  if (a.gate) {
+    // pre-launched (gcs_scan): wait for the host prologue's twist, one poller per block.  Relaxed
+    // system-scope loads (sc0 sc1: they bypass the caches and read the coherent host words); an
+    // acquire load would add a cache invalidate per poll, which with every point block polling
+    // stalled the whole device (C2 device wait 77 -> 395 us).  The host stores the twist before
+    // the sequence word and the twist loads issue after the sequence load has returned, so they
+    // read the twist of this sequence.
+    __shared__ double s_xi[6];
+    __shared__ int s_open;
+    if (threadIdx.x == 0) {
+      const uint64_t t_start = wall_clock64();
+      bool open = false;
+      for (;;) {
+        if (__hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == a.gate_seq) { open = true; break; }
+        if (wall_clock64() - t_start > kGateTimeoutTicks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      s_open = open ? 1 : 0;
+      if (!open) *a.gate_err = 1u;
+    }
+    __syncthreads();
+    // the six twist words in one load instruction (lanes 0-5), issued after the sequence word was seen
+    if (threadIdx.x < 6)
+      s_xi[threadIdx.x] = s_open ? __longlong_as_double((long long)__hip_atomic_load(
+                                       a.gate + 1 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
+                                 : 0.0;
+    __syncthreads();
+    // block-uniform: kept in scalar registers, as the kernel-argument twist is
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const long long u = __double_as_longlong(s_xi[k]);
+      const int lo = __builtin_amdgcn_readfirstlane((int)(u & 0xffffffffll));
+      const int hi = __builtin_amdgcn_readfirstlane((int)(u >> 32));
+      xi[k] = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) xi[k] = a.xi[k];
+  }
   const double denom = a.t1 - a.t0 > 1e-12 ? a.t1 - a.t0 : 1e-12;
   const double inv_tau = 1.0 / a.tau;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sum w_budget, sum wn^2, sum w_out, sum H
@@ -350,7 +390,7 @@ void k_points(PointKernelArgs a, double* partials) {
     }
     double alpha = (t - a.t0) / denom;
     double p0[3];
-    deskew_point(alpha, a.xi, p, p0);
+    deskew_point(alpha, xi, p, p0);
     const double win = smooth_window(t, a.t0, a.t1, kTimeWarpSigmaFrac * denom);
     double d[3];
     ray_dir(p0[0], p0[1], p0[2], a.origin, d);

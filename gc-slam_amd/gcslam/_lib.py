@@ -97,6 +97,7 @@ IMU_ODOM_CERT_LEN = 15
 RCCL_ID_BYTES = 128
 DEBUG_SCAN_SPIN_LIMIT, DEBUG_INJECT_SCAN_FAIL = 1, 2
 DEBUG_SORTED_BUCKETS, DEBUG_BUCKET_CAPACITY = 3, 4
+DEBUG_LAUNCH_GATE = 5
 
 
 # (name, restype, argtypes) for every symbol declared in include/gcslam_hip.h

@@ -391,3 +391,38 @@ def test_full_size_properties(N, B):
     ctx.scan_bin_moment_match()
     assert np.array_equal(ctx.get_scan_stats(), st)
     ctx.close()
+
+
+def test_launch_gate_matches_ungated_bitwise_and_times_out_loudly():
+    """gcs_scan's pre-launched device front (k_points waits on the device for the prologue's deskew
+    twist, GCS_DEBUG_LAUNCH_GATE = 1, the default) against the point stage launched after the prologue
+    (0): the twist reaches the kernel through the gate bit for bit, so three consecutive scans agree
+    exactly.  A gate that is never opened (-1) runs every point block into its timeout and the scan
+    fails with an error instead of hanging; the context then scans normally again."""
+    from gcslam import _lib as L
+    syn = _synthetic()
+    outs = []
+    for gate in (1, 0):
+        ctx = _ctx(n_bins=20000, n_points_cap=8192, mode="scale")
+        ctx.set_debug(L.DEBUG_LAUNCH_GATE, gate)
+        res = []
+        for k in range(3):
+            sc = syn.make_scan(8192, 31 + k)
+            rec, t, w = device_scan(sc)
+            o = ctx.scan(rec, 16, t, w, 8192, **scan_kwargs(sc))
+            res.append((ctx.get_scan_stats(), ctx.get_map()[0], np.array(o.belief.L[:]), np.array(o.z_t[:]),
+                        np.array(o.cert[:])))
+        outs.append(res)
+        if gate == 1:
+            ctx.set_debug(L.DEBUG_LAUNCH_GATE, -1)
+            sc = syn.make_scan(8192, 40)
+            rec, t, w = device_scan(sc)
+            with pytest.raises(RuntimeError, match="gate"):
+                ctx.scan(rec, 16, t, w, 8192, **scan_kwargs(sc))
+            ctx.set_debug(L.DEBUG_LAUNCH_GATE, 1)
+            o = ctx.scan(rec, 16, t, w, 8192, **scan_kwargs(sc))
+            assert np.all(np.isfinite(np.array(o.z_t[:])))
+        ctx.close()
+    for a, b in zip(outs[0], outs[1]):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y)
