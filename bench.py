@@ -396,6 +396,10 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c3", action="store_true")
+    ap.add_argument("--map-mode", default="own", choices=["own", "shared"],
+                    help="own: a map per hypothesis (default); shared: one map, hypothesis 0's (rank 0 leads, "
+                         "the other ranks replay its update: gcslam_hip.h GCS_MAP_FOLLOW); at one GPU the rank "
+                         "follows itself, which times a follower's scan")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="launcher + payload exchange over gloo on CPU (test of the multi-rank path)")
     args = ap.parse_args()
@@ -453,6 +457,13 @@ def main():
 
     # gcs_combine_allreduce (RCCL sum of the payload at N > 1, combine, IW updates) and gcs_scan bound once
     combine = ctx.combine_call(comm_h, w_iw, w_bary)
+    follow = None
+    if args.map_mode == "shared":
+        # one map (backend_node.py:2079-2083): rank 0 leads; a follower skips its own map update and
+        # replays the lead's from the record the all-reduce carried; a single rank follows itself
+        ctx.set_map_mode("lead" if (rank == 0 and world > 1) else "follow")
+        if not (rank == 0 and world > 1):
+            follow = ctx.map_follow_call()
 
     state = dict(count=0, sample=False, sampled=0)
     scan_out = L.GcsScanOutputs()  # one output record for every scan (the caller-owned buffer form)
@@ -481,6 +492,8 @@ def main():
             state["sampled"] += 1
         else:
             combine(state["count"])
+        if follow is not None:
+            follow(prepared[state["count"] % N_SCANS])
         state["count"] += 1
 
     for _ in range(args.warmup):
@@ -538,7 +551,10 @@ def main():
             "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded VLP-16-like scans, box room, IMU 200 Hz, odometry; inputs resident in HBM)",
             "config": {"workload": f"{args.config}: {N}-pt scans vs {B}-bin map, K={K} candidates, "
-                                   f"1 hypothesis per GPU ({world} hypotheses), payload all-reduce per scan",
+                                   f"1 hypothesis per GPU ({world} hypotheses), payload all-reduce per scan"
+                                   + ("; one shared map (hypothesis 0's; followers replay its update)"
+                                      if args.map_mode == "shared" else ""),
+                       "map_mode": args.map_mode,
                        "n_points": N, "n_bins": B, "k_cand": K, "hypotheses": world, "parallelism": f"hyp{world}"},
             "value_definition": "hypothesis-scans/s of the whole job: every GPU runs its own hypothesis of each scan "
                                 "(weak scaling); the node's scans/s is scans_per_s_node = value / n_gpus",

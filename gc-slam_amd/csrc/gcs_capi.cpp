@@ -187,6 +187,12 @@ struct gcs_ctx {
   // the lifted Cholesky factor of belief.L and its inverse, left by the last scan's tail (the
   // recompose factors post.L, and the anchor drift keeps L): the next PredictDiffusion starts from
   // them instead of factoring and inverting the same matrix again.  Cleared by gcs_ctx_set_belief.
+  // one map for all hypotheses (GCS_MAP_*): the last scan's map-update record and the lead's record
+  // carried by the last gcs_combine_allreduce
+  int map_mode = GCS_MAP_OWN;
+  double map_rec[GCS_MAP_REC_LEN] = {};
+  double lead_rec[GCS_MAP_REC_LEN] = {};
+  bool have_lead_rec = false;
   bool prev_fac_valid = false;
   host::SpdFactor prev_fac;
   double prev_cov[DZ * DZ];
@@ -1751,8 +1757,11 @@ int scan_tail(gcs_ctx* c, gcs_scan_state& st, const LidarTerms& lt, gcs_scan_out
   host::world_pose_from_increment(rec, mu_rec, z_t);
   for (int i = 0; i < 6; ++i)
     for (int j = 0; j < 6; ++j) Sig6[6 * i + j] = covr[i * DZ + j];
+  memcpy(c->map_rec, st.xi, 6 * sizeof(double));
+  memcpy(c->map_rec + 6, z_t, 6 * sizeof(double));
+  memcpy(c->map_rec + 12, Sig6, 36 * sizeof(double));
   auto Tq = clk::now();
-  if (push)
+  if (push && c->map_mode != GCS_MAP_FOLLOW)  // a follower's map takes the lead's update (gcs_map_follow)
     if (int rc = submit_push(c, z_t, Sig6, c->cfg.forgetting_factor, c->push_main ? c->stream : c->push_stream,
                              c->d_part_push))
       return rc;
@@ -2096,23 +2105,92 @@ int gcs_rccl_comm_count(void* comm, int32_t* count, int32_t* user_rank) {
 int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, int32_t scan_count,
                           gcs_belief* comb, double* cert) {
   if (!c) return GCS_ERR_ARG;
+  constexpr int kLen = GCS_PAYLOAD_LEN + GCS_MAP_REC_LEN;
   if (!c->h_payload) {
-    HIPCHK(c, hipHostMalloc(&c->h_payload, GCS_PAYLOAD_LEN * sizeof(double), hipHostMallocDefault));
-    HIPCHK(c, hipMalloc(&c->d_payload, GCS_PAYLOAD_LEN * sizeof(double)));
+    HIPCHK(c, hipHostMalloc(&c->h_payload, kLen * sizeof(double), hipHostMallocDefault));
+    HIPCHK(c, hipMalloc(&c->d_payload, kLen * sizeof(double)));
   }
   if (int rc = gcs_hypothesis_payload(c, w_iw, w_bary, c->h_payload)) return rc;
+  // one map (LEAD / FOLLOW): the lead's map-update record rides the same all-reduce (zeros elsewhere)
+  const bool shared_map = c->map_mode != GCS_MAP_OWN;
+  const int len = shared_map ? kLen : GCS_PAYLOAD_LEN;
+  if (shared_map)
+    for (int k = 0; k < GCS_MAP_REC_LEN; ++k)
+      c->h_payload[GCS_PAYLOAD_LEN + k] = c->map_mode == GCS_MAP_LEAD ? c->map_rec[k] : 0.0;
   if (comm) {
     // the reduction rides the context stream; the previous scan's pushforward keeps running on
     // push_stream underneath it
     hipStream_t s = c->stream;
-    HIPCHK(c, hipMemcpyAsync(c->d_payload, c->h_payload, GCS_PAYLOAD_LEN * sizeof(double), hipMemcpyHostToDevice, s));
-    ncclResult_t r = ncclAllReduce(c->d_payload, c->d_payload, GCS_PAYLOAD_LEN, ncclDouble, ncclSum,
-                                   (ncclComm_t)comm, s);
+    HIPCHK(c, hipMemcpyAsync(c->d_payload, c->h_payload, len * sizeof(double), hipMemcpyHostToDevice, s));
+    ncclResult_t r = ncclAllReduce(c->d_payload, c->d_payload, len, ncclDouble, ncclSum, (ncclComm_t)comm, s);
     if (r != ncclSuccess) return fail(c, GCS_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    HIPCHK(c, hipMemcpyAsync(c->h_payload, c->d_payload, GCS_PAYLOAD_LEN * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(c, hipMemcpyAsync(c->h_payload, c->d_payload, len * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(c, hipStreamSynchronize(s));
   }
+  if (shared_map) {  // a single rank carries its own record (a follower then replays its own update)
+    memcpy(c->lead_rec, comm ? c->h_payload + GCS_PAYLOAD_LEN : c->map_rec, sizeof(c->lead_rec));
+    c->have_lead_rec = true;
+  }
   return combine_into_ctx(c, c->h_payload, scan_count, comb, cert);
+}
+
+int gcs_ctx_set_map_mode(gcs_ctx* c, int32_t mode) {
+  if (!c) return GCS_ERR_ARG;
+  if (mode < GCS_MAP_OWN || mode > GCS_MAP_FOLLOW) return fail(c, GCS_ERR_ARG, "map mode: GCS_MAP_OWN, _LEAD or _FOLLOW");
+  c->map_mode = mode;
+  c->have_lead_rec = false;
+  return GCS_OK;
+}
+
+int gcs_ctx_map_record(gcs_ctx* c, double* rec) {
+  if (!c || !rec) return GCS_ERR_ARG;
+  if (!c->have_last) return fail(c, GCS_ERR_STATE, "no scan yet: no map-update record");
+  memcpy(rec, c->map_rec, sizeof(c->map_rec));
+  return GCS_OK;
+}
+
+// The lead's map update replayed on this context: k_budget + k_points at the lead's twist (the raw
+// scan is the same on every hypothesis), the bin kernel (ScanBinStats and active flags: the lead's,
+// bit for bit -- same kernels, same inputs), then k_pushforward at the lead's z_t and covariance.
+// Its certificates and the planar / Matrix-Fisher reductions are not needed and not run.
+int gcs_map_follow(gcs_ctx* c, const gcs_scan_inputs* in, const double* rec) {
+  if (!c || !in) return fail(c, GCS_ERR_ARG, "null argument");
+  if (c->map_mode != GCS_MAP_FOLLOW) return fail(c, GCS_ERR_STATE, "gcs_map_follow needs GCS_MAP_FOLLOW");
+  if (!rec) {
+    if (!c->have_lead_rec) return fail(c, GCS_ERR_STATE, "no lead record: pass rec or combine first");
+    rec = c->lead_rec;
+  }
+  for (int k = 0; k < GCS_MAP_REC_LEN; ++k)
+    if (!std::isfinite(rec[k])) return fail(c, GCS_ERR_NONFINITE, "map-update record not finite");
+  double r[GCS_MAP_REC_LEN];
+  memcpy(r, rec, sizeof(r));  // (rec may be the context's own lead_rec)
+  c->use_direct = c->cfg.mode == GCS_MODE_SCALE && c->direct_buckets && !c->sorted_sticky && c->d_members;
+  struct DirectOff {
+    gcs_ctx* c;
+    ~DirectOff() { c->use_direct = false; }
+  } direct_off{c};
+  for (int pass = 0; pass < 2; ++pass) {
+    if (int rc = push_wait(c)) return rc;
+    c->budget_pending = false;
+    if (int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
+                              in->scan_start_time, in->scan_end_time, r, nullptr, nullptr, nullptr,
+                              /*fold_later=*/true, in->xyz_format == 1))
+      return rc;
+    if (int rc = join_push(c)) return rc;
+    if (int rc = stage_bins(c)) return rc;
+    if (int rc = stage_tile_order(c)) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->stages_done = true;
+    if (int rc = check_bucket_err(c)) return rc;
+    if (!(c->use_direct && c->h_err[2])) break;
+    // a bucket overflowed the direct rows (the lead's scan was redone sorted too): redo sorted
+    c->h_err[2] = 0u;
+    c->sorted_sticky = true;
+    c->use_direct = false;
+  }
+  c->h_err[1] = 0u;
+  return submit_push(c, r + 6, r + 12, c->cfg.forgetting_factor, c->push_main ? c->stream : c->push_stream,
+                     c->d_part_push);
 }
 
 int gcs_hypothesis_barycenter(int32_t n, const double* Ls, const double* hs, const double* zs, const double* w,

@@ -98,6 +98,7 @@ RCCL_ID_BYTES = 128
 DEBUG_SCAN_SPIN_LIMIT, DEBUG_INJECT_SCAN_FAIL = 1, 2
 DEBUG_SORTED_BUCKETS, DEBUG_BUCKET_CAPACITY = 3, 4
 DEBUG_LAUNCH_GATE = 5
+MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 
 # (name, restype, argtypes) for every symbol declared in include/gcslam_hip.h
@@ -205,6 +206,9 @@ _SIGS = [
     ("gcs_ctx_synchronize", C.c_int, [C.c_void_p]),
     ("gcs_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("gcs_ctx_set_debug", C.c_int, [C.c_void_p, C.c_int32, C.c_int64]),
+    ("gcs_ctx_set_map_mode", C.c_int, [C.c_void_p, C.c_int32]),
+    ("gcs_ctx_map_record", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("gcs_map_follow", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("gcs_ctx_stage_times", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int32]),
     ("gcs_ctx_set_atlas", C.c_int, [C.c_void_p, c_double_p]),
     ("gcs_ctx_get_atlas", C.c_int, [C.c_void_p, c_double_p, c_int32_p]),

@@ -373,6 +373,36 @@ class HypothesisContext:
         self._chk(self.lib.gcs_scan(self.h, C.byref(inp), C.byref(out)), "gcs_scan")
         return out
 
+    # ------------------------------------------------------------------ one map for all hypotheses
+    def set_map_mode(self, mode):
+        """"own" (default: this hypothesis' own map), "lead" (hypothesis 0: its map is the node's map)
+        or "follow" (skips its own map update; map_follow replays the lead's), gcslam_hip.h GCS_MAP_*."""
+        m = {"own": L.MAP_OWN, "lead": L.MAP_LEAD, "follow": L.MAP_FOLLOW}[mode]
+        self._chk(self.lib.gcs_ctx_set_map_mode(self.h, m), "set_map_mode")
+
+    def map_record(self):
+        """The last scan's map-update record [deskew twist 6 | z_t 6 | pose covariance 36]."""
+        r = np.empty(L.MAP_REC_LEN)
+        self._chk(self.lib.gcs_ctx_map_record(self.h, r.ctypes.data), "map_record")
+        return r
+
+    def map_follow(self, prepared, rec=None):
+        """Replay the lead's map update of this scan (prepared: prepare_scan() of the same scan; rec: the
+        lead's map_record(), None = the record the last combine_allreduce carried)."""
+        r = None if rec is None else np.ascontiguousarray(rec, np.float64)
+        self._chk(self.lib.gcs_map_follow(self.h, prepared[1], None if r is None else r.ctypes.data), "map_follow")
+
+    def map_follow_call(self):
+        """gcs_map_follow bound once for prepare_scan() structs, with the record the last combine carried;
+        returns call(prepared) -> None, raising on failure."""
+        fn, h = self.lib.gcs_map_follow, self.h
+
+        def call(prepared):
+            rc = fn(h, prepared[1], None)
+            if rc:
+                self._chk(rc, "map_follow")
+        return call
+
     # ------------------------------------------------------------------ hypotheses
     def hypothesis_payload(self, w_iw, w_bary):
         """Packed 840-f64 all-reduce payload of this hypothesis (a fresh array per call)."""

@@ -408,6 +408,35 @@ int gcs_combine_allreduce(gcs_ctx* ctx, void* comm, double w_iw, double w_bary, 
                           gcs_belief* combined_out /*may be NULL*/, double* cert4 /*may be NULL*/);
 
 
+/* ---------------------------------------------------------------- one map for all hypotheses */
+/* The reference node keeps ONE map: every hypothesis of a scan reads self.primitive_map and only
+ * hypothesis 0's update is stored (backend_node.py:2036-2083).  With one hypothesis per GPU each
+ * context holds a copy of that map:
+ *   GCS_MAP_OWN (default)  every context updates its own map from its own scan (per-hypothesis maps,
+ *                          no map traffic; declared);
+ *   GCS_MAP_LEAD           hypothesis 0: updates its map and keeps the scan's map-update record
+ *                          [deskew twist 6 | z_t 6 | pose covariance 6x6] (GCS_MAP_REC_LEN f64);
+ *   GCS_MAP_FOLLOW         hypotheses 1..: gcs_scan skips its own pushforward, and gcs_map_follow
+ *                          replays the lead's update on the same raw scan (point + bin stage at the
+ *                          lead's twist, pushforward at the lead's z_t and covariance), so the map
+ *                          stays bitwise the lead's.  No map rows move between GPUs: the record rides
+ *                          the per-scan payload all-reduce (GCS_PAYLOAD_LEN + GCS_MAP_REC_LEN f64,
+ *                          the lead's record plus zeros) when every rank's context is LEAD or FOLLOW.
+ * A follower's scan s reads the map after the lead's scan s - 1 (declared lag: the reference's
+ * sequential loop lets hypothesis k > 0 read hypothesis 0's update of the same scan). */
+#define GCS_MAP_OWN 0
+#define GCS_MAP_LEAD 1
+#define GCS_MAP_FOLLOW 2
+#define GCS_MAP_REC_LEN 48
+int gcs_ctx_set_map_mode(gcs_ctx* ctx, int32_t mode);
+/* the last gcs_scan's map-update record (any mode) */
+int gcs_ctx_map_record(gcs_ctx* ctx, double* rec /*GCS_MAP_REC_LEN*/);
+/* replay the lead's update of this scan (in: the scan's gcs_scan inputs; only the point stream,
+ * the scan window and n_points are read); rec NULL = the record the last gcs_combine_allreduce
+ * carried from the lead (a single rank, comm NULL: its own record -- bench.py --map-mode follow times
+ * a follower's scan on one GPU that way) */
+int gcs_map_follow(gcs_ctx* ctx, const gcs_scan_inputs* in, const double* rec /*GCS_MAP_REC_LEN or NULL*/);
+
 /* ---------------------------------------------------------------- primitive path: LiDAR surfels */
 /* extract_lidar_surfels (lidar_surfel_extraction.py:339-431) on the GPU: sentinel mask and weighted
  * centre, MA-hex 3D hash-grid cell of every point (ma_hex_web.py:221-303), the first max_occupants

@@ -4,7 +4,8 @@
 # Steps (each under its own time limit, stopping at the first failure; outputs under $O):
 #   tests        pytest -m gpu (the parity suite)          smoke      __graft_entry__.smoke()
 #   bench        bench.py C2 headline line (+ C3 roofline + CPU baseline)
-#   bench3       bench.py --config c3
+#   bench3       bench.py --config c3        benchshared  bench.py --map-mode shared (a follower's scan)
+#   hostbench    host 22-D numerics micro-benchmark (gc-slam_amd/build/host_bench)
 #   prof2/prof3  rocprofv3 --kernel-trace --stats of bench at C2 / C3
 #   pmc          FETCH_SIZE / WRITE_SIZE passes (one counter per run) at C2 and C3 (PMC_CONFIGS)
 #   sq           SQ instruction-mix / wave-state passes of the hot kernels
@@ -29,6 +30,8 @@ step() {
         > "$O/pytest_gpu.log" 2>&1 ;;
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     bench) timeout -k 10 400 python bench.py > "$O/bench_c2.log" 2>&1 ;;
+    benchshared) timeout -k 10 300 python bench.py --map-mode shared --no-cpu-baseline --no-c3 > "$O/bench_shared.log" 2>&1 ;;
+    hostbench) timeout -k 10 120 ./tools/host_bench tools/host_bench_in.bin > "$O/host_bench.txt" 2>&1 ;;
     bench3) timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline \
               > "$O/bench_c3.log" 2>&1 ;;
     prof2) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c2" -o run --output-format csv -- \
