@@ -335,7 +335,7 @@ def cpu_rehearsal(args, rank, world):
     nu, Psi = np.zeros(7), np.zeros(252)
     mnu, mPsi = np.zeros(3), np.zeros(27)
     assert lib.gcs_datasheet_noise_states(nu.ctypes.data, Psi.ctypes.data, mnu.ctypes.data, mPsi.ctypes.data) == 0
-    err, payloads = 0.0, None
+    err, payloads, rec_ok = 0.0, None, True
     t0 = time.perf_counter()
     for step in range(args.warmup + args.steps):
         if step == args.warmup:
@@ -349,12 +349,17 @@ def cpu_rehearsal(args, rank, world):
         dnu = np.ones(7)
         mdPsi = np.ascontiguousarray(np.stack([np.outer(v, v) for v in rng.normal(0, 1e-3, (3, 3))]).reshape(27))
         mdnu = np.array([1.0, 1.0, 0.0])
-        p = np.zeros(840)
+        shared = args.map_mode == "shared"
+        p = np.zeros(840 + (L.MAP_REC_LEN if shared else 0))
         assert lib.gcs_payload_pack(C.byref(bs), dPsi.ctypes.data, dnu.ctypes.data, mdPsi.ctypes.data,
                                     mdnu.ctypes.data, float(w[rank]), float(wn[rank]), p.ctypes.data) == 0
+        if shared:  # the lead's map-update record rides the payload; the followers add zeros
+            lead_rec = np.random.default_rng(7 + step).normal(size=L.MAP_REC_LEN)
+            if rank == 0:
+                p[840:] = lead_rec
         if step == 0:  # every rank's own payload, gathered before the sum (the transport reduces in place)
             if world > 1:
-                got = [torch.zeros(840, dtype=torch.float64) for _ in range(world)]
+                got = [torch.zeros(p.shape[0], dtype=torch.float64) for _ in range(world)]
                 dist.all_gather(got, torch.from_numpy(p.copy()))
                 payloads = np.stack([g.numpy() for g in got])
             else:
@@ -362,6 +367,9 @@ def cpu_rehearsal(args, rank, world):
         tot = np.ascontiguousarray(allreduce_payload(p))
         if step == 0:
             err = float(np.abs(payloads.sum(0) - tot).max())
+        if shared:  # every rank received the lead's record bit for bit
+            rec_ok = rec_ok and bool(np.array_equal(tot[840:], lead_rec))
+            tot = np.ascontiguousarray(tot[:840])
         comb = L.GcsBelief()
         out = [np.zeros(n) for n in (7, 252, 484, 3, 27, 4)]
         assert lib.gcs_payload_apply(tot.ctypes.data, step, np.zeros(6).ctypes.data, 0.0, nu.ctypes.data,
@@ -375,7 +383,7 @@ def cpu_rehearsal(args, rank, world):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
         allr = [None] * world
-        dist.all_gather_object(allr, dict(rank=rank, pid=os.getpid(), Q_sum=float(out[2].sum())))
+        dist.all_gather_object(allr, dict(rank=rank, pid=os.getpid(), Q_sum=float(out[2].sum()), map_record_ok=rec_ok))
         ranks = allr
     if rank == 0:
         print(json.dumps({

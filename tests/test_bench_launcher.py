@@ -57,3 +57,14 @@ def test_launcher_world_mismatch_fails():
                                                                            "LOCAL_RANK": "0"})
     assert r.returncode == 2
     assert "WORLD_SIZE=1" in r.stderr
+
+
+def test_shared_map_record_rides_the_payload_to_every_rank():
+    """--map-mode shared: the lead's (rank 0) map-update record is appended to the payload and the
+    followers add zeros, so after the sum every rank holds the lead's record bit for bit
+    (gcslam_hip.h GCS_MAP_FOLLOW; backend_node.py:2079-2083)."""
+    r = _run(["--cpu-rehearsal", "--gpus", "2", "--map-mode", "shared", "--steps", "4", "--warmup", "1"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _line(r.stdout)
+    assert [x["map_record_ok"] for x in d["ranks"]] == [True, True]
+    assert d["payload_sum_check"]
