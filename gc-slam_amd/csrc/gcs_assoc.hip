@@ -35,7 +35,7 @@ namespace {
 
 constexpr int kAsThreads = 256;
 constexpr int kShThreads = 512;  // 2 waves per SIMD: up to 256 VGPRs for both K_mat copies, no spills
-constexpr int kShCR = 32;        // rows per lane in the Sinkhorn column sums: N <= kShCR * 512 / KM
+constexpr int kShCR = 32;        // Sinkhorn row capacity: N <= kShCR * 512 / KM (= RPT rows per thread)
 constexpr int kMaxStencil = 64;
 constexpr double kLog4Pi = 2.5310242469692907;     // np.log(4.0 * np.pi)
 constexpr double kLog2 = 0.6931471805599453;       // np.log(2.0)
@@ -398,12 +398,41 @@ __device__ __forceinline__ double radix_select(const double (&vals)[CAP], uint32
     __syncthreads();
     if (t < 256) hist[t] = 0u;
     __syncthreads();
+    // Histogram adds aggregated before the LDS atomics: runs of one digit within a thread's values
+    // are counted in a register, and a thread's last run is merged across the wave when every lane's
+    // run has the same digit.  The b-row and a-marginal values repeat (uniform marginals, equal
+    // recency), and one LDS address took every add of a pass (N K serialised atomics x 8 passes).
+    uint32_t run_d = 0u, run_n = 0u;
 #pragma unroll
     for (int j = 0; j < CAP; ++j)
       if ((okmask >> j) & 1u) {
         const unsigned long long kk = order_key(vals[j]);
-        if ((kk & mask) == prefix) atomicAdd(&hist[(kk >> shift) & 255ULL], 1u);
+        if ((kk & mask) == prefix) {
+          const uint32_t d = (uint32_t)((kk >> shift) & 255ULL);
+          if (run_n != 0u && d != run_d) {
+            atomicAdd(&hist[run_d], run_n);
+            run_n = 0u;
+          }
+          run_d = d;
+          ++run_n;
+        }
       }
+    {
+      const bool have = run_n != 0u;
+      const unsigned long long hm = __ballot(have);
+      if (hm != 0ull) {
+        const int first = __ffsll((long long)hm) - 1;
+        const uint32_t d0 = (uint32_t)__shfl((int)run_d, first, 64);
+        if (__ballot(have && run_d != d0) == 0ull) {  // one digit across the wave: one add
+          uint32_t tot = run_n;
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) tot += (uint32_t)__shfl_xor((int)tot, off, 64);
+          if (lane == first) atomicAdd(&hist[d0], tot);
+        } else if (have) {
+          atomicAdd(&hist[run_d], run_n);
+        }
+      }
+    }
     __syncthreads();
     if (t < 64) {
       const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
@@ -449,8 +478,7 @@ template <int KM, int RPT>
 __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p, AsWork w, AsOut o, int n_valid_host) {
 #pragma clang fp contract(off)
   __shared__ double s_red[16 * (KM + 8)];
-  __shared__ double s_u[kShThreads * RPT];
-  __shared__ double s_colp[kShThreads / 32];
+  __shared__ double s_colp[(kShThreads / 64) * KM];
   __shared__ double s_v[KM];
   __shared__ uint32_t s_hist[256], s_sel[4];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
@@ -516,23 +544,20 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const double bk = 1.0 / (double)K;
 #pragma unroll
   for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
-  // column-major copy of K_mat for the column sums: thread t owns column t / TPC and rows
-  // t % TPC + TPC j (the same values: exp of the same cost entries)
-  constexpr int TPC = kShThreads / KM, CR = kShCR;
-  const int kc = t / TPC, cc = t % TPC;
-  __syncthreads();  // the median-scaled costs written back above are visible to every thread
-  double XC[CR];
-#pragma unroll
-  for (int j = 0; j < CR; ++j) {
-    const int r = cc + TPC * j;
-    XC[j] = (r < N && kc < K) ? exp(-o.cost[(size_t)r * K + kc] / eps) : 0.0;
-  }
   double u[RPT], v[KM];
 #pragma unroll
   for (int j = 0; j < RPT; ++j) u[j] = 1.0;
 #pragma unroll
   for (int k = 0; k < KM; ++k) v[k] = 1.0;
-  constexpr int GW = TPC < 64 ? TPC : 64;  // lanes of one column group inside a wave
+  // K^T u from the row-major K_mat rows each thread already holds (no column-major copy: that copy,
+  // 2 x RPT x KM doubles of registers, spilled): per thread its rows' column partials, then a
+  // reduce-scatter across the wave (log2 KM halving exchanges leave lane L the column of its bits
+  // 5..6-log2 KM, then xor adds inside each KM-lane group), then the waves in order.  Fixed order.
+  static_assert(KM == 8 || KM == 16 || KM == 32, "reduce-scatter over 64 lanes");
+  constexpr int LG = KM == 8 ? 3 : (KM == 16 ? 4 : 5);  // halving steps
+  int col = 0;  // the column this lane ends up holding
+#pragma unroll
+  for (int s = 0; s < LG; ++s) col |= ((lane >> (5 - s)) & 1) << (LG - 1 - s);
   for (int it = 0; it < p.iters; ++it) {
     // u = (a / (K v + 1e-12))^ua, one lane per row (K v in column order)
 #pragma unroll
@@ -542,25 +567,38 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
 #pragma unroll
       for (int k = 0; k < KM; ++k) kv += X[j * KM + k] * v[k];
       u[j] = r < N ? pow_sinkhorn(va[j] / (kv + 1e-12), ua) : 0.0;
-      if (r < N) s_u[r] = u[j];
     }
-    __syncthreads();
-    // K^T u: TPC lanes per column, rows in the fixed order cc, cc + TPC, ..., then a fixed xor tree
-    double cs = 0.0;
+    double c[KM];
 #pragma unroll
-    for (int j = 0; j < CR; ++j) {
-      const int r = cc + TPC * j;
-      cs += XC[j] * (r < N ? s_u[r] : 0.0);
+    for (int k = 0; k < KM; ++k) {
+      double sacc = 0.0;
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) sacc += X[j * KM + k] * u[j];
+      c[k] = sacc;
     }
+    // reduce-scatter: step s exchanges half of the live values with the lane 32 >> s apart
 #pragma unroll
-    for (int sh = GW / 2; sh >= 1; sh >>= 1) cs += __shfl_xor(cs, sh, 64);
-    if ((lane & (GW - 1)) == 0) s_colp[t / GW] = cs;
+    for (int s = 0, n = KM; s < LG; ++s, n >>= 1) {
+      const int h = n >> 1;
+      const bool up = (lane >> (5 - s)) & 1;
+#pragma unroll
+      for (int i = 0; i < KM / 2; ++i) {
+        if (i < h) {
+          const double send = up ? c[i] : c[i + h];
+          const double keep = up ? c[i + h] : c[i];
+          c[i] = keep + __shfl_xor(send, 32 >> s, 64);
+        }
+      }
+    }
+    double cs = c[0];
+#pragma unroll
+    for (int sh = (64 >> LG) / 2; sh >= 1; sh >>= 1) cs += __shfl_xor(cs, sh, 64);
+    if ((lane & ((64 >> LG) - 1)) == 0) s_colp[wid * KM + col] = cs;
     __syncthreads();
-    if (t < K) {  // v = (b / (K^T u + 1e-12))^vb: column t's group partials in order
-      constexpr int G = TPC / GW;
-      double sum = s_colp[t * G];
+    if (t < K) {  // v = (b / (K^T u + 1e-12))^vb: column t over the waves in order
+      double sum = s_colp[t];
 #pragma unroll
-      for (int g = 1; g < G; ++g) sum += s_colp[t * G + g];
+      for (int g = 1; g < kShThreads / 64; ++g) sum += s_colp[g * KM + t];
       s_v[t] = pow_sinkhorn(bk / (sum + 1e-12), vb);
     }
     __syncthreads();

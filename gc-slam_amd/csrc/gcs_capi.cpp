@@ -156,6 +156,7 @@ struct gcs_ctx {
   // coherent host memory polled by k_points (GCSLAM_GATE=0: the point stage is launched after the prologue)
   uint64_t* h_gate = nullptr;
   uint64_t* d_gate = nullptr;
+  uint64_t* d_gate_relay = nullptr;  // device memory: k_points block 0 relays the gate to the others
   uint64_t gate_seq = 0, gate_next = 0;
   bool gate_on = true;
   bool gate_withhold = false;  // fault test (GCS_DEBUG_LAUNCH_GATE = -1): the gate is never opened
@@ -483,6 +484,7 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
     a.gate = c->d_gate;
     a.gate_seq = c->gate_next;
     a.gate_err = c->d_err + 3;
+    a.gate_relay = c->d_gate_relay;
     c->gate_next = 0;
   }
   c->iz_valid = false;
@@ -976,6 +978,8 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     return GCS_ERR_HIP;
   for (int k = 0; k < 8; ++k) c->h_gate[k] = 0u;
   if (bad(hipHostGetDevicePointer((void**)&c->d_gate, c->h_gate, 0))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_gate_relay, 8 * sizeof(uint64_t)))) return GCS_ERR_HIP;
+  if (bad(hipMemset(c->d_gate_relay, 0, 8 * sizeof(uint64_t)))) return GCS_ERR_HIP;
   if (const char* g = getenv("GCSLAM_GATE")) c->gate_on = atoi(g) != 0;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
@@ -1055,7 +1059,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   }
   if (c->push_stream) (void)hipStreamSynchronize(c->push_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
+  void* ptrs[] = {c->d_gate_relay, c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_tile_order, c->d_tile_work, c->d_bins_part, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,

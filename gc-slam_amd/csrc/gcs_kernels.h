@@ -86,6 +86,7 @@ struct PointKernelArgs {
   const uint64_t* gate;
   uint64_t gate_seq;
   uint32_t* gate_err;
+  uint64_t* gate_relay;  // device memory, 8 words: block 0's relay of the gate to the other blocks
 };
 constexpr uint64_t kGateTimeoutTicks = 20000000ull;  // 200 ms of the 100 MHz constant clock
 

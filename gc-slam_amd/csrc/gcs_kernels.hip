@@ -325,31 +325,50 @@ void k_points(PointKernelArgs a, double* partials) {
   }
   double xi[6];
   if (a.gate) {
-    // pre-launched (gcs_scan): wait for the host prologue's twist, one poller per block.  Relaxed
-    // system-scope loads (sc0 sc1: they bypass the caches and read the coherent host words); an
-    // acquire load would add a cache invalidate per poll, which with every point block polling
-    // stalled the whole device (C2 device wait 77 -> 395 us).  The host stores the twist before
-    // the sequence word and the twist loads issue after the sequence load has returned, so they
-    // read the twist of this sequence.
+    // pre-launched (gcs_scan): wait for the host prologue's twist.  Only block 0 polls the host word
+    // (relaxed system-scope loads, sc0 sc1: uncached reads of coherent host memory; an acquire load
+    // adds a cache invalidate per poll); it relays [seq, twist 0-2, seq, twist 3-5] to device memory
+    // in one 8-lane store, which every block polls (relaxed agent-scope loads; the sequence word in
+    // both 32-B halves), so a single poller's traffic crosses to the host.
     __shared__ double s_xi[6];
-    __shared__ int s_open;
-    if (threadIdx.x == 0) {
-      const uint64_t t_start = wall_clock64();
+    const uint64_t t_start = wall_clock64();
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
       bool open = false;
+      if (threadIdx.x == 0) {
+        for (;;) {
+          if (__hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == a.gate_seq) { open = true; break; }
+          if (wall_clock64() - t_start > kGateTimeoutTicks) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (!open) *a.gate_err = 1u;
+      }
+      open = __shfl((int)open, 0, 64) != 0;
+      const int l = threadIdx.x;
+      if (l < 8) {
+        uint64_t val = a.gate_seq;  // a timed-out gate relays the sequence with a zero twist
+        if ((l & 3) != 0) {
+          const int k = (l >> 2) * 3 + (l & 3) - 1;
+          val = open ? __hip_atomic_load(a.gate + 1 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
+        }
+        __hip_atomic_store(a.gate_relay + l, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (threadIdx.x < 64) {
+      const int l = threadIdx.x & 7;
+      uint64_t val = 0ull;
       for (;;) {
-        if (__hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == a.gate_seq) { open = true; break; }
-        if (wall_clock64() - t_start > kGateTimeoutTicks) break;
+        val = __hip_atomic_load(a.gate_relay + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t s0 = __shfl((long long)val, 0, 64), s4 = __shfl((long long)val, 4, 64);
+        if (s0 == a.gate_seq && s4 == a.gate_seq) break;
+        if (wall_clock64() - t_start > 2 * kGateTimeoutTicks) {  // block 0 never relayed: zero twist
+          val = 0ull;
+          if (threadIdx.x == 0) *a.gate_err = 1u;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
       }
-      s_open = open ? 1 : 0;
-      if (!open) *a.gate_err = 1u;
+      if (threadIdx.x < 8 && (l & 3) != 0) s_xi[(l >> 2) * 3 + (l & 3) - 1] = __longlong_as_double((long long)val);
     }
-    __syncthreads();
-    // the six twist words in one load instruction (lanes 0-5), issued after the sequence word was seen
-    if (threadIdx.x < 6)
-      s_xi[threadIdx.x] = s_open ? __longlong_as_double((long long)__hip_atomic_load(
-                                       a.gate + 1 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM))
-                                 : 0.0;
     __syncthreads();
     // block-uniform: kept in scalar registers, as the kernel-argument twist is
 #pragma unroll
