@@ -34,8 +34,14 @@ namespace gcs {
 namespace {
 
 constexpr int kAsThreads = 256;
-constexpr int kShThreads = 512;  // 2 waves per SIMD: up to 256 VGPRs for both K_mat copies, no spills
-constexpr int kShCR = 32;        // Sinkhorn row capacity: N <= kShCR * 512 / KM (= RPT rows per thread)
+// the Sinkhorn workgroup: 8 waves, 4 rows per thread at K <= 8 (K_mat rows in registers).  1024
+// threads (4 waves per SIMD, 128 VGPRs: the rows spill) measured slower: 3.2 vs 3.0 us per iteration,
+// 0.480 vs 0.422 ms per call (profiles/r03/assoc/)
+#ifndef GCS_SH_THREADS
+#define GCS_SH_THREADS 512
+#endif
+constexpr int kShThreads = GCS_SH_THREADS;
+constexpr int kShCR = 16 * 1024 / kShThreads;  // Sinkhorn row capacity: N <= kShCR * kShThreads / KM
 constexpr int kMaxStencil = 64;
 constexpr double kLog4Pi = 2.5310242469692907;     // np.log(4.0 * np.pi)
 constexpr double kLog2 = 0.6931471805599453;       // np.log(2.0)
@@ -494,6 +500,8 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     }
     for (int q = t; q < N; q += kShThreads) o.rmass[q] = 0.0;
     if (t < CE_COUNT) o.cert[t] = t == CE_EXACT ? 1.0 : (t == CE_MVALID ? (double)*w.mvalid : 0.0);
+    __syncthreads();
+    if (t == 0) *w.mvalid = 0u;  // re-armed for the next call's k_as_prep count (no per-call memset)
     return;
   }
   // marginal a (:412-424)
@@ -683,6 +691,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     o.cert[CE_SUPPORT] = acc[5] / (double)std::max(N, 1);
     o.cert[CE_EXACT] = 0.0;
     o.cert[CE_MVALID] = (double)*w.mvalid;
+    *w.mvalid = 0u;  // re-armed for the next call (every thread read it before the tail's barriers)
   }
 }
 
@@ -806,7 +815,8 @@ struct gcs_assoc_ctx {
   hipStream_t own = nullptr, stream = nullptr;
   double *d_pos = nullptr, *d_dir = nullptr, *d_kap = nullptr, *d_A1 = nullptr, *d_A2 = nullptr, *d_dt = nullptr;
   int32_t *d_tix = nullptr, *d_cand = nullptr;
-  uint32_t* d_mvalid = nullptr;
+  uint32_t* d_mvalid = nullptr;  // zeroed at creation; re-armed by k_as_sinkhorn after each call
+  int st_ns = -1, st_rxy = -1, st_rz = -1;  // the stencil table in d_st
   int8_t* d_st = nullptr;
   double* h_cert = nullptr;  // pinned, mapped
   double* h_cert_dev = nullptr;
@@ -826,7 +836,7 @@ int as_fail(gcs_assoc_ctx* c, int code, const std::string& m) {
   } while (0)
 
 // rows per Sinkhorn thread for k_assoc <= KM: the K_mat rows stay in registers (both layouts)
-constexpr int rpt_for(int km) { return km <= 8 ? 4 : (km <= 16 ? 2 : 1); }
+constexpr int rpt_for(int km) { return kShCR / km > 1 ? kShCR / km : 1; }  // rows per Sinkhorn thread
 constexpr int max_rows_for(int max_k) { return kShCR * kShThreads / (max_k <= 8 ? 8 : (max_k <= 16 ? 16 : 32)); }
 }  // namespace
 
@@ -903,6 +913,10 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
       bad(hipHostGetDevicePointer((void**)&c->h_cert_dev, c->h_cert, 0)) ||
       bad(hipHostMalloc(&c->h_vpe, 32 * sizeof(double), hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&c->h_vpe_dev, c->h_vpe, 0))) {
+    gcs_assoc_ctx_destroy(c);
+    return GCS_ERR_HIP;
+  }
+  if (bad(hipMemset(c->d_mvalid, 0, 4))) {  // the valid-entry counter starts armed
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
@@ -987,8 +1001,14 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   AsWork w{c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, c->d_mvalid};
   AsOut out{o->responsibilities, o->row_masses, o->cost_matrix, o->candidate_pool_indices, o->candidate_tile_ids,
             o->candidate_slots, c->h_cert_dev};
-  ASCHK(c, hipMemcpyAsync(c->d_st, st, (size_t)ns * 3, hipMemcpyHostToDevice, s));
-  ASCHK(c, hipMemsetAsync(c->d_mvalid, 0, 4, s));
+  if (ns != c->st_ns || rxy != c->st_rxy || rz != c->st_rz) {  // the stencil table changes with the radii only
+    ASCHK(c, hipStreamSynchronize(s));
+    ASCHK(c, hipMemcpy(c->d_st, st, (size_t)ns * 3, hipMemcpyHostToDevice));
+    c->st_ns = ns;
+    c->st_rxy = rxy;
+    c->st_rz = rz;
+  }
+  // (the valid-entry counter k_as_prep adds to is re-armed by the Sinkhorn kernel that reads it)
   const int nprep = (int)((p.n + pool + kAsThreads - 1) / kAsThreads);
   hipLaunchKernelGGL(k_as_prep, dim3(nprep), dim3(kAsThreads), 0, s, in, p, w, (const int8_t*)c->d_st);
   const int km = K <= 8 ? 8 : (K <= 16 ? 16 : 32);
@@ -996,7 +1016,10 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
     uint32_t mv = 0;
     ASCHK(c, hipMemcpyAsync(&mv, c->d_mvalid, 4, hipMemcpyDeviceToHost, s));
     ASCHK(c, hipStreamSynchronize(s));
-    if (m->n_valid != 0 && mv != 0) return as_fail(c, GCS_ERR_ARG, bad_policy);
+    if (m->n_valid != 0 && mv != 0) {
+      ASCHK(c, hipMemset(c->d_mvalid, 0, 4));  // no Sinkhorn kernel re-arms the counter on this path
+      return as_fail(c, GCS_ERR_ARG, bad_policy);
+    }
     // empty: the Sinkhorn kernel's zero path writes the reference's empty result
   }
   if (bad_policy) {

@@ -149,14 +149,17 @@ struct gcs_ctx {
     uint8_t* flags;
     BudgetArgs ba;
     int nblk;
-  } push_job{};
+  };
+  // a ring of two job slots: a submission waits only while both are taken, so the next scan's front
+  // queues behind the last scan's pushforward launches instead of waiting for them
+  PushJob push_jobs[2]{};
   int push_rc = 0;
   std::string push_err;
   // launch gate of the pre-launched point stage (gcs_scan): [0] sequence word, [1..6] the deskew twist;
   // coherent host memory polled by k_points (GCSLAM_GATE=0: the point stage is launched after the prologue)
   uint64_t* h_gate = nullptr;
   uint64_t* d_gate = nullptr;
-  uint64_t* d_gate_relay = nullptr;  // device memory: k_points block 0 relays the gate to the others
+  double* d_gate_xi = nullptr;  // device memory: k_gate's copy of the twist for k_points
   uint64_t gate_seq = 0, gate_next = 0;
   bool gate_on = true;
   bool gate_withhold = false;  // fault test (GCS_DEBUG_LAUNCH_GATE = -1): the gate is never opened
@@ -243,6 +246,13 @@ int push_wait(gcs_ctx* c) {
     return fail(c, rc, c->push_err);
   }
   return GCS_OK;
+}
+
+// a free job slot: waits while both are taken (the worker still launching two jobs)
+gcs_ctx::PushJob& claim_job(gcs_ctx* c) {
+  const uint64_t r = c->push_req.load(std::memory_order_relaxed);
+  while (r - c->push_done.load(std::memory_order_acquire) >= 2) __builtin_ia32_pause();
+  return c->push_jobs[r & 1];
 }
 
 // order the main stream after an in-flight scan pushforward (map, derived, touched, map totals)
@@ -480,11 +490,9 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.nearest_out = c->d_nearest;  // device ids
   a.iz_out = iz_out;
   a.t_out = t_out;
-  if (c->gate_next) {  // pre-launched by the scan front: the twist comes through the gate
-    a.gate = c->d_gate;
-    a.gate_seq = c->gate_next;
-    a.gate_err = c->d_err + 3;
-    a.gate_relay = c->d_gate_relay;
+  if (c->gate_next) {  // pre-launched by the scan front: k_gate waits for the twist, k_points reads it
+    HIPCHK(c, launch_gate(c->d_gate, c->gate_next, c->d_gate_xi, c->d_err + 3, s));
+    a.xi_dev = c->d_gate_xi;
     c->gate_next = 0;
   }
   c->iz_valid = false;
@@ -693,24 +701,29 @@ void push_worker(gcs_ctx* c) {
     }
     const uint64_t r = c->push_req.load(std::memory_order_acquire);
     if (r == seen) return;  // stop requested, nothing pending
-    seen = r;
-    const gcs_ctx::PushJob& j = c->push_job;
-    int rc = GCS_OK;
-    if (j.kind == 1) {
-      const hipError_t e = launch_budget(j.ba, j.nblk, j.s, nullptr, nullptr);
-      if (e != hipSuccess) {
-        rc = GCS_ERR_HIP;
-        c->push_err = "k_budget launch (worker): " + std::string(hipGetErrorString(e));
+    for (; seen < r; ++seen) {  // the queued jobs in submission order
+      const gcs_ctx::PushJob& j = c->push_jobs[seen & 1];
+      int rc = GCS_OK;
+      std::string msg;
+      if (j.kind == 1) {
+        const hipError_t e = launch_budget(j.ba, j.nblk, j.s, nullptr, nullptr);
+        if (e != hipSuccess) {
+          rc = GCS_ERR_HIP;
+          msg = "k_budget launch (worker): " + std::string(hipGetErrorString(e));
+        }
+      } else if (j.kind == 2) {
+        rc = scan_front(c, j.in, j.seq);
+        if (rc) msg = "scan front launch (worker): " + t_fail_msg;
+      } else {
+        rc = stage_push(c, j.z_t, j.Sig6, j.gamma, j.s, j.partials, j.flags, true);
+        if (rc) msg = "pushforward launch (worker): " + t_fail_msg;
       }
-    } else if (j.kind == 2) {
-      rc = scan_front(c, j.in, j.seq);
-      if (rc) c->push_err = "scan front launch (worker): " + t_fail_msg;
-    } else {
-      rc = stage_push(c, j.z_t, j.Sig6, j.gamma, j.s, j.partials, j.flags, true);
-      if (rc) c->push_err = "pushforward launch (worker): " + t_fail_msg;
+      if (rc && !c->push_rc) {  // the first failure is the one push_wait reports
+        c->push_err = msg;
+        c->push_rc = rc;
+      }
+      c->push_done.store(seen + 1, std::memory_order_release);
     }
-    c->push_rc = rc;
-    c->push_done.store(r, std::memory_order_release);
   }
 }
 
@@ -722,9 +735,8 @@ int submit_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma,
     if (int rc = push_wait(c)) return rc;
     return stage_push(c, z_t, Sig6, gamma, s, partials, c->d_flags);
   }
-  if (int rc = push_wait(c)) return rc;  // the previous job is launched: its slot is free
   if (!c->push_thread.joinable()) c->push_thread = std::thread(push_worker, c);
-  gcs_ctx::PushJob& j = c->push_job;
+  gcs_ctx::PushJob& j = claim_job(c);
   j.kind = 0;
   memcpy(j.z_t, z_t, sizeof(j.z_t));
   memcpy(j.Sig6, Sig6, sizeof(j.Sig6));
@@ -744,9 +756,8 @@ int submit_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma,
 // thread goes straight to PredictDiffusion; stage_points waits for the worker (push_wait) before it
 // queues k_points behind it on the same stream, so the device order is the synchronous one.
 int submit_budget(gcs_ctx* c, const BudgetArgs& ba, int nblk, hipStream_t s) {
-  if (int rc = push_wait(c)) return rc;  // the previous job (the last scan's pushforward) is launched
   if (!c->push_thread.joinable()) c->push_thread = std::thread(push_worker, c);
-  gcs_ctx::PushJob& j = c->push_job;
+  gcs_ctx::PushJob& j = claim_job(c);  // (queued behind the last scan's pushforward launches)
   j.kind = 1;
   j.ba = ba;
   j.nblk = nblk;
@@ -778,9 +789,8 @@ int scan_front(gcs_ctx* c, const gcs_scan_inputs* in, uint64_t seq) {
 }
 
 int submit_front(gcs_ctx* c, const gcs_scan_inputs* in, uint64_t seq) {
-  if (int rc = push_wait(c)) return rc;  // the previous job (the last scan's pushforward) is launched
   if (!c->push_thread.joinable()) c->push_thread = std::thread(push_worker, c);
-  gcs_ctx::PushJob& j = c->push_job;
+  gcs_ctx::PushJob& j = claim_job(c);  // (queued behind the last scan's pushforward launches)
   j.kind = 2;
   j.in = in;
   j.seq = seq;
@@ -978,8 +988,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     return GCS_ERR_HIP;
   for (int k = 0; k < 8; ++k) c->h_gate[k] = 0u;
   if (bad(hipHostGetDevicePointer((void**)&c->d_gate, c->h_gate, 0))) return GCS_ERR_HIP;
-  if (bad(hipMalloc(&c->d_gate_relay, 8 * sizeof(uint64_t)))) return GCS_ERR_HIP;
-  if (bad(hipMemset(c->d_gate_relay, 0, 8 * sizeof(uint64_t)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_gate_xi, 8 * sizeof(double)))) return GCS_ERR_HIP;
   if (const char* g = getenv("GCSLAM_GATE")) c->gate_on = atoi(g) != 0;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
@@ -1059,7 +1068,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   }
   if (c->push_stream) (void)hipStreamSynchronize(c->push_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_gate_relay, c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
+  void* ptrs[] = {c->d_gate_xi, c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_tile_order, c->d_tile_work, c->d_bins_part, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,

@@ -79,14 +79,9 @@ struct PointKernelArgs {
   int* nearest_out;
   double* iz_out;  // 1 / Z per point (per-operator soft-assign materialisation; the record holds w / Z)
   double* t_out;   // budget-selected timestamps (deskew-only stage: n_bins == 0)
-  // launch gate (gcs_scan's pre-launched point stage; null: xi above is the twist): the kernel is
-  // queued before the host prologue has the deskew twist, and thread 0 of every block polls
-  // gate[0] (host-mapped, coherent) until it holds gate_seq, then reads the twist from gate[1..6].
-  // A gate not opened within kGateTimeoutTicks sets *gate_err and the block runs with a zero twist.
-  const uint64_t* gate;
-  uint64_t gate_seq;
-  uint32_t* gate_err;
-  uint64_t* gate_relay;  // device memory, 8 words: block 0's relay of the gate to the other blocks
+  // the deskew twist in device memory (gcs_scan's pre-launched front: written by k_gate, which the
+  // stream runs right before this kernel); null: xi above
+  const double* xi_dev;
 };
 constexpr uint64_t kGateTimeoutTicks = 20000000ull;  // 200 ms of the 100 MHz constant clock
 
@@ -157,6 +152,7 @@ hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_
 // fold: run k_points' cert fold now (else k_bins_scale block 0 folds it, BinKernelArgs.pts_partials)
 int points_blocks(long cap, bool scale);  // k_points grid (lanes per point in scale mode)
 int points_max_blocks();
+hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err, hipStream_t s);
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
                          hipEvent_t e0, hipEvent_t e1);
 int scan_tiles(int n_bins);

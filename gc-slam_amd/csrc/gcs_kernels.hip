@@ -323,65 +323,11 @@ void k_points(PointKernelArgs a, double* partials) {
     brow[k] = r < a.budget_blocks ? *(const double2*)(a.budget_partials + (size_t)r * pstride<2>())
                                   : make_double2(0.0, 0.0);
   }
+  // the deskew twist: by value, or (pre-launched scan front) from the device word k_gate wrote
+  // before this kernel started (stream order makes it visible)
   double xi[6];
-  if (a.gate) {
-    // pre-launched (gcs_scan): wait for the host prologue's twist.  Only block 0 polls the host word
-    // (relaxed system-scope loads, sc0 sc1: uncached reads of coherent host memory; an acquire load
-    // adds a cache invalidate per poll); it relays [seq, twist 0-2, seq, twist 3-5] to device memory
-    // in one 8-lane store, which every block polls (relaxed agent-scope loads; the sequence word in
-    // both 32-B halves), so a single poller's traffic crosses to the host.
-    __shared__ double s_xi[6];
-    const uint64_t t_start = wall_clock64();
-    if (blockIdx.x == 0 && threadIdx.x < 64) {
-      bool open = false;
-      if (threadIdx.x == 0) {
-        for (;;) {
-          if (__hip_atomic_load(a.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == a.gate_seq) { open = true; break; }
-          if (wall_clock64() - t_start > kGateTimeoutTicks) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (!open) *a.gate_err = 1u;
-      }
-      open = __shfl((int)open, 0, 64) != 0;
-      const int l = threadIdx.x;
-      if (l < 8) {
-        uint64_t val = a.gate_seq;  // a timed-out gate relays the sequence with a zero twist
-        if ((l & 3) != 0) {
-          const int k = (l >> 2) * 3 + (l & 3) - 1;
-          val = open ? __hip_atomic_load(a.gate + 1 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : 0ull;
-        }
-        __hip_atomic_store(a.gate_relay + l, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    if (threadIdx.x < 64) {
-      const int l = threadIdx.x & 7;
-      uint64_t val = 0ull;
-      for (;;) {
-        val = __hip_atomic_load(a.gate_relay + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t s0 = __shfl((long long)val, 0, 64), s4 = __shfl((long long)val, 4, 64);
-        if (s0 == a.gate_seq && s4 == a.gate_seq) break;
-        if (wall_clock64() - t_start > 2 * kGateTimeoutTicks) {  // block 0 never relayed: zero twist
-          val = 0ull;
-          if (threadIdx.x == 0) *a.gate_err = 1u;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (threadIdx.x < 8 && (l & 3) != 0) s_xi[(l >> 2) * 3 + (l & 3) - 1] = __longlong_as_double((long long)val);
-    }
-    __syncthreads();
-    // block-uniform: kept in scalar registers, as the kernel-argument twist is
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {
-      const long long u = __double_as_longlong(s_xi[k]);
-      const int lo = __builtin_amdgcn_readfirstlane((int)(u & 0xffffffffll));
-      const int hi = __builtin_amdgcn_readfirstlane((int)(u >> 32));
-      xi[k] = __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 6; ++k) xi[k] = a.xi[k];
-  }
+  for (int k = 0; k < 6; ++k) xi[k] = a.xi_dev ? a.xi_dev[k] : a.xi[k];
   const double denom = a.t1 - a.t0 > 1e-12 ? a.t1 - a.t0 : 1e-12;
   const double inv_tau = 1.0 / a.tau;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sum w_budget, sum wn^2, sum w_out, sum H
@@ -2115,6 +2061,37 @@ hipError_t launch_parse(const ParseArgs& a, hipStream_t s) {
 
 hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
   hipExtLaunchKernelGGL(k_budget, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, a);  // folded inside k_points
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- launch gate of the scan front
+// One wave, queued between k_budget and k_points by the pre-launched scan front: lane 0 polls the
+// host gate word (coherent host memory; relaxed system-scope loads are uncached reads, where an
+// acquire would add a cache invalidate per poll) until it holds seq, then copies the deskew twist to
+// device memory for k_points, which the stream starts right behind it.  One poller, one wave: the
+// point kernel itself (~360 registers per lane: one wave per SIMD) is not resident while the host
+// prologue runs, so the previous scan's pushforward keeps the SIMDs (a resident, polling k_points
+// starved it: C2 device wait 77 -> 120 us).  Not opened within kGateTimeoutTicks: zero twist and
+// *err = 1 (gcs_scan fails).
+__global__ __launch_bounds__(64) void k_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  bool open = false;
+  for (;;) {
+    if (__hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == seq) { open = true; break; }
+    if (wall_clock64() - t0 > kGateTimeoutTicks) break;
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __asm__ volatile("" ::: "memory");
+  for (int k = 0; k < 6; ++k)
+    xi_out[k] = open ? __longlong_as_double((long long)__hip_atomic_load(gate + 1 + k, __ATOMIC_RELAXED,
+                                                                        __HIP_MEMORY_SCOPE_SYSTEM))
+                     : 0.0;
+  if (!open) *err = 1u;
+}
+
+hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err, hipStream_t s) {
+  hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, s, gate, seq, xi_out, err);
   return hipGetLastError();
 }
 

@@ -19,17 +19,20 @@ def main():
     from gcslam import association as GA
     batch, view, _ = make_scene(seed=0)
     b, v = _batch(batch), _view(view)
-    cfg = GA.AssociationConfig(scan_seq=10)
-    for _ in range(3):
-        GA.associate_primitives_ot(b, v, cfg)
-    ts = []
-    for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 30):
-        t0 = time.perf_counter()
-        GA.associate_primitives_ot(b, v, cfg)
-        ts.append(time.perf_counter() - t0)
-    ts = np.array(ts) * 1e3
-    print(f"associate_primitives_ot N=1536 K=8 pool=7x1024: median {np.median(ts):.3f} ms, p90 "
-          f"{np.percentile(ts, 90):.3f} ms over {len(ts)} calls")
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
+    # the reference's 50 Sinkhorn iterations, then 0 and 10 (the slope is one iteration's cost)
+    for iters in (50, 0, 10):
+        cfg = GA.AssociationConfig(scan_seq=10, k_sinkhorn=iters)
+        for _ in range(3):
+            GA.associate_primitives_ot(b, v, cfg)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            GA.associate_primitives_ot(b, v, cfg)
+            ts.append(time.perf_counter() - t0)
+        ts = np.array(ts) * 1e3
+        print(f"associate_primitives_ot N=1536 K=8 pool=7x1024 k_sinkhorn={iters}: median {np.median(ts):.3f} ms, "
+              f"p90 {np.percentile(ts, 90):.3f} ms over {len(ts)} calls", flush=True)
     del torch
 
 

@@ -58,6 +58,10 @@ step() {
     pmapprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/pmap_prof" -o run --output-format csv -- \
                 python3 tools/pmap_bench.py 10 > "$O/pmap_prof.log" 2>&1 ;;
     assoc) timeout -k 10 300 python tools/assoc_bench.py > "$O/assoc_bench.txt" 2>&1 ;;
+    assocab) for v in A B; do  # association timing, default library vs libgcslam_hip_$B.so
+               lib=gc-slam_amd/gcslam/libgcslam_hip.so; [ $v = B ] && lib=gc-slam_amd/gcslam/libgcslam_hip_${B:-prev}.so
+               GCSLAM_LIB=$PWD/$lib timeout -k 10 300 python tools/assoc_bench.py > "$O/assocab_$v.txt" 2>&1 || return $?
+             done ;;
     assocprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/assoc_prof" -o run --output-format csv -- \
                  python3 tools/assoc_bench.py > "$O/assoc_prof.log" 2>&1 ;;
     ab)
