@@ -7,17 +7,18 @@
 //                  kappa, the MA-hex stencil tile ids (tiling.py:148-186, :309-336) and their index in
 //                  the view's tile list (first match, -1 none: :338-344); one lane per view entry: A_vmf
 //                  of its kappa and the valid count
-//   k_as_pool      one workgroup per row: the row's pool (n_stencil x m_tile_view entries) costed
+//   k_as_pool      one wave per row: the row's pool (n_stencil x m_tile_view entries) costed
 //                  (:351-365; ||dx||^2 + beta H^2_vMF, 1e12 where invalid or the tile is missing), the
 //                  k_assoc smallest by (cost, pool position) -- lax.sort with num_keys=1 is stable on
-//                  cost alone (:376) -- per-thread sorted lists merged by k rounds of a block argmin;
+//                  cost alone (:376) -- per-lane sorted lists merged by k rounds of a wave argmin;
 //                  then per candidate the unmasked cost + recency, row-min subtraction, addressing
 //                  (:377-403)
-//   k_as_sinkhorn  one 512-thread workgroup: marginals a (policy) and b (uniform), the optional median
+//   k_as_sinkhorn  workgroup 0 (512 threads): marginals a (policy) and b (uniform), the optional median
 //                  scaling, k_sinkhorn fixed unbalanced iterations (:105-138) with the K_mat rows in
 //                  registers and the column sums in a fixed tree, pi, row masses, responsibilities and
-//                  the OTCert / Support / Influence scalars (:465-551) -- the p95 order statistics by an
-//                  8-pass radix select -- into mapped host memory
+//                  the OTCert / Support / Influence scalars (:465-551) into mapped host memory;
+//                  workgroup 1, concurrently: the p95 order statistics of a and of the recency rows
+//                  (8-pass radix selects)
 // No floating-point atomics; every sum has a fixed order: bitwise reproducible.
 #include <hip/hip_runtime.h>
 
@@ -63,7 +64,8 @@ struct AsWork {
   double *pos, *dir, *kap, *A1, *A2, *dt;
   int32_t* tix;
   int32_t* cand;
-  uint32_t* mvalid;
+  uint32_t* mvalid;       // this call's valid-entry count (k_as_prep adds, the Sinkhorn reads)
+  uint32_t* mvalid_next;  // the next call's (zeroed by this call's Sinkhorn workgroup 0)
 };
 
 struct AsIn {
@@ -230,21 +232,29 @@ __device__ __forceinline__ bool kless(unsigned long long ka, int pa, unsigned lo
   return ka < kb || (ka == kb && pa < pb);
 }
 
-// one workgroup per measurement row
+// One wave per measurement row (four rows per 256-thread workgroup): each lane keeps the KM best
+// (cost, pool position) of its strided share of the row's pool, then KM rounds of a wave argmin over
+// the lanes' heads pick the row's candidates -- shuffles only, no workgroup barriers.  (One
+// workgroup per row, 256 lanes of 28 entries each, filled 2,048 per-lane list slots with full vMF
+// costs per row and merged with a barrier per round: 108 us for 1,536 rows.)  The selected set and
+// order are the stable sort's whatever the partition, so the outputs are unchanged bit for bit.
+constexpr int kPoolRows = kAsThreads / 64;
 template <int KM>
 __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsWork w, AsOut o) {
 #pragma clang fp contract(off)
-  __shared__ int s_tix[kMaxStencil];
-  __shared__ unsigned long long s_wk[2][kAsThreads / 64];
-  __shared__ int s_wp[2][kAsThreads / 64];
-  __shared__ int s_sel[32];
-  const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  __shared__ int s_tix[kPoolRows][kMaxStencil];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = blockIdx.x * kPoolRows + wid;
+  if (i >= p.n) return;  // (whole waves: no barrier below)
   const bool row_valid = in.valid[i] != 0;
-  if (t < p.n_stencil) s_tix[t] = w.tix[(size_t)i * p.n_stencil + t];
-  __syncthreads();
+  if (lane < p.n_stencil) s_tix[wid][lane] = w.tix[(size_t)i * p.n_stencil + lane];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const int* tix = s_tix[wid];
   const double mp[3] = {w.pos[3 * i], w.pos[3 * i + 1], w.pos[3 * i + 2]};
   const double md[3] = {w.dir[3 * i], w.dir[3 * i + 1], w.dir[3 * i + 2]};
   const double mk = w.kap[i], A1 = w.A1[i];
+  int sel = 0;  // lane r < k: the pool position of the row's r-th candidate
   if (row_valid) {
     unsigned long long key[KM];
     int idx[KM];
@@ -257,16 +267,16 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
     const bool prune = p.beta >= 0.0;
     // four pool entries per trip, in increasing pool position: their table loads issue together
     constexpr int PB = 4;
-    for (int q0 = t; q0 < P; q0 += PB * kAsThreads) {
+    for (int q0 = lane; q0 < P; q0 += PB * 64) {
       int e[PB];
       bool ok[PB];
 #pragma unroll
       for (int u = 0; u < PB; ++u) {
-        const int q = q0 + u * kAsThreads;
+        const int q = q0 + u * 64;
         // stencil tile and offset of pool position q (shift / mask when m_tile_view is a power of two)
         const int sq = p.m_shift >= 0 ? (q >> p.m_shift) : q / p.m_view;
         const int oq = q - sq * p.m_view;
-        const int ti = q < P ? s_tix[sq] : -1;
+        const int ti = q < P ? tix[sq] : -1;
         e[u] = (ti < 0 ? 0 : ti) * p.m_view + (q < P ? oq : 0);
         ok[u] = ti >= 0;
       }
@@ -282,7 +292,7 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
       }
 #pragma unroll
       for (int u = 0; u < PB; ++u) {
-        const int q = q0 + u * kAsThreads;
+        const int q = q0 + u * 64;
         if (q >= P) break;
         if (ok[u] && vv[u]) {
           // cost = d_pos + beta d_dir >= d_pos (beta >= 0, d_dir >= 0): an entry whose d_pos alone does
@@ -297,7 +307,7 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
         }
       }
     }
-    // k rounds of a block argmin over the lists' heads; the winner's owner pops its head
+    // k rounds of a wave argmin over the lanes' heads; the winner's owner pops its head
     for (int r = 0; r < p.k; ++r) {
       unsigned long long bk = key[0];
       int bp = idx[0];
@@ -310,21 +320,7 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
           bp = op;
         }
       }
-      const int buf = r & 1;
-      if (lane == 0) {
-        s_wk[buf][wid] = bk;
-        s_wp[buf][wid] = bp;
-      }
-      __syncthreads();
-      bk = s_wk[buf][0];
-      bp = s_wp[buf][0];
-#pragma unroll
-      for (int v = 1; v < kAsThreads / 64; ++v)
-        if (kless(s_wk[buf][v], s_wp[buf][v], bk, bp)) {
-          bk = s_wk[buf][v];
-          bp = s_wp[buf][v];
-        }
-      if (t == 0) s_sel[r] = bp;
+      if (lane == r) sel = bp;
       if (idx[0] == bp && key[0] == bk) {  // pool positions are unique: exactly one owner
 #pragma unroll
         for (int j = 0; j < KM - 1; ++j) {
@@ -335,16 +331,13 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
         idx[KM - 1] = 0x7fffffff;
       }
     }
-    __syncthreads();
   }
-  if (wid != 0) return;
   // per candidate (lane k < K): view index, unmasked cost + recency, row min (:377-403)
   const bool act = lane < p.k;
   int e = 0;
   if (act && row_valid) {
-    const int q = s_sel[lane];
-    const int ti = s_tix[q / p.m_view];
-    e = (ti < 0 ? 0 : ti) * p.m_view + q % p.m_view;
+    const int ti = tix[sel / p.m_view];
+    e = (ti < 0 ? 0 : ti) * p.m_view + sel % p.m_view;
   }
   double c = INFINITY, dt = 0.0;
   if (act) {
@@ -474,6 +467,32 @@ __device__ __forceinline__ double radix_select(const double (&vals)[CAP], uint32
   return prefix == ~0ULL ? NAN : __longlong_as_double((long long)b);
 }
 
+// recency-weighted b rows (:441-446): exp(-lambda dt) normalised per row
+template <int KM, int RPT>
+__device__ __forceinline__ void recency_rows(const AsParams& p, const AsWork& w, int N, int K, int t,
+                                             double (&brow)[RPT * KM], uint32_t& okb) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int r = t + j * kShThreads;
+    double dsum = 0.0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      double dd = 0.0;
+      if (r < N && k < K) {
+        dd = exp(-p.lam * w.dt[(size_t)r * K + k]);
+        dd = dd > 0.0 ? dd : 0.0;
+        okb |= 1u << (j * KM + k);
+      }
+      brow[j * KM + k] = dd;
+      dsum += dd;
+    }
+    const double den = fmax(dsum, p.eps_mass);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) brow[j * KM + k] = brow[j * KM + k] / den;
+  }
+}
+
 enum CertSlot : int {
   CE_DEFECT_A, CE_DEFECT_B, CE_MASS_TOTAL, CE_SUM_A, CE_SUM_B, CE_SUM_M, CE_SUM_NOVEL, CE_P95_A, CE_P95_B,
   CE_NONZERO_A, CE_NONZERO_B, CE_B_P95, CE_ESS, CE_MASS_EPS, CE_TOTAL_COST, CE_SUPPORT, CE_EXACT, CE_MVALID,
@@ -490,7 +509,8 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int N = p.n, K = p.k;
   const bool empty = n_valid_host == 0 || *w.mvalid == 0u;
-  if (empty) {  // :272-287 -- zeros, exact cert
+  if (empty) {  // :272-287 -- zeros, exact cert (workgroup 0)
+    if (blockIdx.x != 0) return;
     for (int q = t; q < N * K; q += kShThreads) {
       o.resp[q] = 0.0;
       o.cost[q] = 0.0;
@@ -500,8 +520,41 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     }
     for (int q = t; q < N; q += kShThreads) o.rmass[q] = 0.0;
     if (t < CE_COUNT) o.cert[t] = t == CE_EXACT ? 1.0 : (t == CE_MVALID ? (double)*w.mvalid : 0.0);
-    __syncthreads();
-    if (t == 0) *w.mvalid = 0u;  // re-armed for the next call's k_as_prep count (no per-call memset)
+    if (t == 0) *w.mvalid_next = 0u;  // the next call's counter, armed (no per-call memset)
+    return;
+  }
+  if (blockIdx.x == 1) {
+    // The certificate's p95 order statistics (:445-446, :488-493) depend on the marginal a and the
+    // recency rows only, not on the scalings: a second workgroup computes them on another CU while
+    // workgroup 0 iterates.
+    double va1[RPT];
+    double part1[1] = {0.0};
+    uint32_t oka1 = 0;
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int r = t + j * kShThreads;
+      va1[j] = 0.0;
+      if (r < N) {
+        va1[j] = in.valid[r] ? 1.0 : 0.0;
+        if (p.a_policy == 1) va1[j] = va1[j] * in.weights[r];
+        oka1 |= 1u << j;
+      }
+      part1[0] += va1[j];
+    }
+    bsum<1>(part1, s_red);
+    const double sum_a1 = fmax(part1[0], p.eps_mass);
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) va1[j] = va1[j] / sum_a1;
+    double brow1[RPT * KM];
+    uint32_t okb1 = 0;
+    recency_rows<KM, RPT>(p, w, N, K, t, brow1, okb1);
+    const double p95_a = radix_select<RPT>(va1, oka1, std::min((int)(0.95 * (double)N), N - 1), s_hist, s_sel);
+    const int nbt = N * K;
+    const double p95_b_row = radix_select<RPT * KM>(brow1, okb1, std::min((int)(0.95 * (double)nbt), nbt - 1), s_hist, s_sel);
+    if (t == 0) {
+      o.cert[CE_P95_A] = p95_a;
+      o.cert[CE_B_P95] = p95_b_row;
+    }
     return;
   }
   // marginal a (:412-424)
@@ -642,33 +695,6 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     acc[5] += va[j] > p.eps_mass ? 1.0 : 0.0;
   }
   bsum<7 + KM>(acc, s_red);
-  // recency-weighted b rows (:441-446): exp(-lambda dt) normalised per row
-  double brow[RPT * KM];
-  uint32_t okb = 0, oka = 0;
-#pragma unroll
-  for (int j = 0; j < RPT; ++j) {
-    const int r = t + j * kShThreads;
-    double dsum = 0.0;
-#pragma unroll
-    for (int k = 0; k < KM; ++k) {
-      double dd = 0.0;
-      if (r < N && k < K) {
-        dd = exp(-p.lam * w.dt[(size_t)r * K + k]);
-        dd = dd > 0.0 ? dd : 0.0;
-        okb |= 1u << (j * KM + k);
-      }
-      brow[j * KM + k] = dd;
-      dsum += dd;
-    }
-    const double den = fmax(dsum, p.eps_mass);
-#pragma unroll
-    for (int k = 0; k < KM; ++k) brow[j * KM + k] = brow[j * KM + k] / den;
-    if (r < N) oka |= 1u << j;
-  }
-  // p95 of a (:488-493) and of the b rows (:445-446)
-  const double p95_a = radix_select<RPT>(va, oka, std::min((int)(0.95 * (double)N), N - 1), s_hist, s_sel);
-  const int nbt = N * K;
-  const double p95_b_row = radix_select<RPT * KM>(brow, okb, std::min((int)(0.95 * (double)nbt), nbt - 1), s_hist, s_sel);
   if (t == 0) {
     double db = 0.0;
     for (int k = 0; k < K; ++k) db += (acc[7 + k] - bk) * (acc[7 + k] - bk);
@@ -680,18 +706,16 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     o.cert[CE_SUM_B] = bk * (double)K;
     o.cert[CE_SUM_M] = acc[0];
     o.cert[CE_SUM_NOVEL] = acc[2];
-    o.cert[CE_P95_A] = p95_a;
     o.cert[CE_P95_B] = bk;  // b uniform: every entry is 1 / K
     o.cert[CE_NONZERO_A] = acc[5];
     o.cert[CE_NONZERO_B] = bk > p.eps_mass ? (double)K : 0.0;
-    o.cert[CE_B_P95] = p95_b_row;
     o.cert[CE_ESS] = acc[0] * acc[0] / (acc[1] + p.eps_mass);
     o.cert[CE_MASS_EPS] = p.eps_mass / (tm + p.eps_mass);
     o.cert[CE_TOTAL_COST] = acc[4];
     o.cert[CE_SUPPORT] = acc[5] / (double)std::max(N, 1);
     o.cert[CE_EXACT] = 0.0;
     o.cert[CE_MVALID] = (double)*w.mvalid;
-    *w.mvalid = 0u;  // re-armed for the next call (every thread read it before the tail's barriers)
+    *w.mvalid_next = 0u;  // the next call's counter, armed (no per-call memset)
   }
 }
 
@@ -815,7 +839,8 @@ struct gcs_assoc_ctx {
   hipStream_t own = nullptr, stream = nullptr;
   double *d_pos = nullptr, *d_dir = nullptr, *d_kap = nullptr, *d_A1 = nullptr, *d_A2 = nullptr, *d_dt = nullptr;
   int32_t *d_tix = nullptr, *d_cand = nullptr;
-  uint32_t* d_mvalid = nullptr;  // zeroed at creation; re-armed by k_as_sinkhorn after each call
+  uint32_t* d_mvalid = nullptr;  // two valid-entry counters, by call parity: a call's Sinkhorn zeroes the next's
+  int mv_parity = 0;
   int st_ns = -1, st_rxy = -1, st_rz = -1;  // the stencil table in d_st
   int8_t* d_st = nullptr;
   double* h_cert = nullptr;  // pinned, mapped
@@ -908,7 +933,7 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
       bad(hipMalloc(&c->d_pos, N * 3 * 8)) || bad(hipMalloc(&c->d_dir, N * 3 * 8)) || bad(hipMalloc(&c->d_kap, N * 8)) ||
       bad(hipMalloc(&c->d_A1, N * 8)) || bad(hipMalloc(&c->d_A2, M * 8)) || bad(hipMalloc(&c->d_dt, NK * 8)) ||
       bad(hipMalloc(&c->d_tix, N * kMaxStencil * 4)) || bad(hipMalloc(&c->d_cand, NK * 4)) ||
-      bad(hipMalloc(&c->d_mvalid, 4)) || bad(hipMalloc(&c->d_st, kMaxStencil * 3)) ||
+      bad(hipMalloc(&c->d_mvalid, 8)) || bad(hipMalloc(&c->d_st, kMaxStencil * 3)) ||
       bad(hipHostMalloc(&c->h_cert, GCS_ASSOC_CERT_LEN * sizeof(double), hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&c->h_cert_dev, c->h_cert, 0)) ||
       bad(hipHostMalloc(&c->h_vpe, 32 * sizeof(double), hipHostMallocMapped)) ||
@@ -916,7 +941,7 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
-  if (bad(hipMemset(c->d_mvalid, 0, 4))) {  // the valid-entry counter starts armed
+  if (bad(hipMemset(c->d_mvalid, 0, 8))) {  // both valid-entry counters start armed
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
@@ -998,7 +1023,10 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   AsIn in{m->Lambdas, m->thetas, m->etas, m->weights, m->valid_mask, m->n_lobes, v->tile_ids, v->positions,
           v->directions, v->kappas, v->valid_mask, v->last_supported_scan_seq, v->candidate_tile_ids,
           v->candidate_slots};
-  AsWork w{c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, c->d_mvalid};
+  uint32_t* mv = c->d_mvalid + c->mv_parity;
+  uint32_t* mv_next = c->d_mvalid + (c->mv_parity ^ 1);
+  c->mv_parity ^= 1;
+  AsWork w{c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, mv, mv_next};
   AsOut out{o->responsibilities, o->row_masses, o->cost_matrix, o->candidate_pool_indices, o->candidate_tile_ids,
             o->candidate_slots, c->h_cert_dev};
   if (ns != c->st_ns || rxy != c->st_rxy || rz != c->st_rz) {  // the stencil table changes with the radii only
@@ -1013,26 +1041,26 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   hipLaunchKernelGGL(k_as_prep, dim3(nprep), dim3(kAsThreads), 0, s, in, p, w, (const int8_t*)c->d_st);
   const int km = K <= 8 ? 8 : (K <= 16 ? 16 : 32);
   if (bad_policy) {
-    uint32_t mv = 0;
-    ASCHK(c, hipMemcpyAsync(&mv, c->d_mvalid, 4, hipMemcpyDeviceToHost, s));
+    uint32_t mvh = 0;
+    ASCHK(c, hipMemcpyAsync(&mvh, mv, 4, hipMemcpyDeviceToHost, s));
     ASCHK(c, hipStreamSynchronize(s));
-    if (m->n_valid != 0 && mv != 0) {
-      ASCHK(c, hipMemset(c->d_mvalid, 0, 4));  // no Sinkhorn kernel re-arms the counter on this path
+    if (m->n_valid != 0 && mvh != 0) {
+      ASCHK(c, hipMemset(mv_next, 0, 4));  // no Sinkhorn kernel arms the next call's counter on this path
       return as_fail(c, GCS_ERR_ARG, bad_policy);
     }
     // empty: the Sinkhorn kernel's zero path writes the reference's empty result
   }
   if (bad_policy) {
-    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(1), dim3(kShThreads), 0, s, in, p, w, out, 0);
+    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, 0);
   } else if (km == 8) {
-    hipLaunchKernelGGL(k_as_pool<8>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
-    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(1), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+    hipLaunchKernelGGL(k_as_pool<8>, dim3((p.n + kPoolRows - 1) / kPoolRows), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   } else if (km == 16) {
-    hipLaunchKernelGGL(k_as_pool<16>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
-    hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(1), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+    hipLaunchKernelGGL(k_as_pool<16>, dim3((p.n + kPoolRows - 1) / kPoolRows), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   } else {
-    hipLaunchKernelGGL(k_as_pool<32>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
-    hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(1), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+    hipLaunchKernelGGL(k_as_pool<32>, dim3((p.n + kPoolRows - 1) / kPoolRows), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   }
   ASCHK(c, hipGetLastError());
   ASCHK(c, hipStreamSynchronize(s));
