@@ -161,7 +161,11 @@ struct gcs_ctx {
   uint64_t* d_gate = nullptr;
   double* d_gate_xi = nullptr;  // device memory: k_gate's copy of the twist for k_points
   uint64_t gate_seq = 0, gate_next = 0;
-  bool gate_on = true;
+  // Measured and left off by default (GCSLAM_GATE=1 or GCS_DEBUG_LAUNCH_GATE turns it on): the
+  // worker is still making the last pushforward's launch calls when the front is queued, so k_points
+  // is launched no earlier than from the main thread, and the gate kernel adds a dependency hop:
+  // C2 113.5 vs 106.9 us per step, same box (profiles/r03/gate/)
+  bool gate_on = false;
   bool gate_withhold = false;  // fault test (GCS_DEBUG_LAUNCH_GATE = -1): the gate is never opened
   int pts_blocks = 0;
   bool pts_fold_pending = false;

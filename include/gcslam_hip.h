@@ -210,9 +210,9 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * lowers the direct buckets' row capacity so a test can force the overflow redo (cert[57] = 1). */
 #define GCS_DEBUG_SORTED_BUCKETS 3
 #define GCS_DEBUG_BUCKET_CAPACITY 4
-/* GCS_DEBUG_LAUNCH_GATE: 1 (default) gcs_scan queues its device front before the host prologue and a
- * one-wave gate kernel ahead of k_points waits on the device for the deskew twist; 0 launches the
- * point stage after the prologue;
+/* GCS_DEBUG_LAUNCH_GATE: 1 (off by default; GCSLAM_GATE=1) gcs_scan queues its device front before the host prologue and a
+ * one-wave gate kernel ahead of k_points waits on the device for the deskew twist; 0 (default) launches
+ * the point stage after the prologue;
  * -1 (fault test) never opens the gate, so the gate kernel runs into its timeout and the scan returns
  * GCS_ERR_HIP. */
 #define GCS_DEBUG_LAUNCH_GATE 5
