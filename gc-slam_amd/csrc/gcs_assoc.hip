@@ -7,10 +7,10 @@
 //                  kappa, the MA-hex stencil tile ids (tiling.py:148-186, :309-336) and their index in
 //                  the view's tile list (first match, -1 none: :338-344); one lane per view entry: A_vmf
 //                  of its kappa and the valid count
-//   k_as_pool      one wave per row: the row's pool (n_stencil x m_tile_view entries) costed
+//   k_as_pool      one workgroup per row: the row's pool (n_stencil x m_tile_view entries) costed
 //                  (:351-365; ||dx||^2 + beta H^2_vMF, 1e12 where invalid or the tile is missing), the
 //                  k_assoc smallest by (cost, pool position) -- lax.sort with num_keys=1 is stable on
-//                  cost alone (:376) -- per-lane sorted lists merged by k rounds of a wave argmin;
+//                  cost alone (:376) -- per-thread sorted lists merged by k rounds of a block argmin;
 //                  then per candidate the unmasked cost + recency, row-min subtraction, addressing
 //                  (:377-403)
 //   k_as_sinkhorn  workgroup 0 (512 threads): marginals a (policy) and b (uniform), the optional median
@@ -232,29 +232,22 @@ __device__ __forceinline__ bool kless(unsigned long long ka, int pa, unsigned lo
   return ka < kb || (ka == kb && pa < pb);
 }
 
-// One wave per measurement row (four rows per 256-thread workgroup): each lane keeps the KM best
-// (cost, pool position) of its strided share of the row's pool, then KM rounds of a wave argmin over
-// the lanes' heads pick the row's candidates -- shuffles only, no workgroup barriers.  (One
-// workgroup per row, 256 lanes of 28 entries each, filled 2,048 per-lane list slots with full vMF
-// costs per row and merged with a barrier per round: 108 us for 1,536 rows.)  The selected set and
-// order are the stable sort's whatever the partition, so the outputs are unchanged bit for bit.
-constexpr int kPoolRows = kAsThreads / 64;
+// one workgroup per measurement row
 template <int KM>
 __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsWork w, AsOut o) {
 #pragma clang fp contract(off)
-  __shared__ int s_tix[kPoolRows][kMaxStencil];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int i = blockIdx.x * kPoolRows + wid;
-  if (i >= p.n) return;  // (whole waves: no barrier below)
+  __shared__ int s_tix[kMaxStencil];
+  __shared__ unsigned long long s_wk[2][kAsThreads / 64];
+  __shared__ int s_wp[2][kAsThreads / 64];
+  __shared__ int s_sel[32];
+  __shared__ double s_thr[kAsThreads / 64];
+  const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const bool row_valid = in.valid[i] != 0;
-  if (lane < p.n_stencil) s_tix[wid][lane] = w.tix[(size_t)i * p.n_stencil + lane];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const int* tix = s_tix[wid];
+  if (t < p.n_stencil) s_tix[t] = w.tix[(size_t)i * p.n_stencil + t];
+  __syncthreads();
   const double mp[3] = {w.pos[3 * i], w.pos[3 * i + 1], w.pos[3 * i + 2]};
   const double md[3] = {w.dir[3 * i], w.dir[3 * i + 1], w.dir[3 * i + 2]};
   const double mk = w.kap[i], A1 = w.A1[i];
-  int sel = 0;  // lane r < k: the pool position of the row's r-th candidate
   if (row_valid) {
     unsigned long long key[KM];
     int idx[KM];
@@ -267,16 +260,54 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
     const bool prune = p.beta >= 0.0;
     // four pool entries per trip, in increasing pool position: their table loads issue together
     constexpr int PB = 4;
-    for (int q0 = lane; q0 < P; q0 += PB * 64) {
+    // Block threshold (beta >= 0): cost = d_pos + beta d_dir lies in [d_pos, d_pos + beta] (d_dir in
+    // [0, 1], rounding monotone), so with D an upper bound of the row's K-th smallest valid d_pos at
+    // least K entries cost <= D + beta: an entry with d_pos > D + beta cannot be selected and needs no
+    // vMF term.  D: per thread the smallest d_pos of its share; per wave the K-th smallest of those
+    // (K rounds of a wave min, K distinct entries at or below it); the block's smallest wave value.
+    // Without it every thread's first K entries took full costs (2,048 per row).
+    double thr = INFINITY;
+    if (prune) {
+      double dmin = INFINITY;
+      for (int q0 = t; q0 < P; q0 += PB * kAsThreads) {
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+          const int q = q0 + u * kAsThreads;
+          const int sq = p.m_shift >= 0 ? (q >> p.m_shift) : q / p.m_view;
+          const int ti = q < P ? s_tix[sq] : -1;
+          if (ti < 0) continue;
+          const int e = ti * p.m_view + (q - sq * p.m_view);
+          if (!in.vvalid[e]) continue;
+          const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
+          dmin = fmin(dmin, (dx * dx + dy * dy) + dz * dz);
+        }
+      }
+      double kth = INFINITY, cur = dmin;
+      for (int r = 0; r < p.k; ++r) {  // the r-th smallest lane minimum, lanes popped in turn
+        double m = cur;
+#pragma unroll
+        for (int sh = 32; sh >= 1; sh >>= 1) m = fmin(m, __shfl_xor(m, sh, 64));
+        kth = m;
+        const unsigned long long hit = __ballot(cur == m);
+        if (lane == __ffsll((long long)hit) - 1) cur = INFINITY;  // one lane per round
+      }
+      if (lane == 0) s_thr[wid] = kth;
+      __syncthreads();
+      double d = s_thr[0];
+#pragma unroll
+      for (int v = 1; v < kAsThreads / 64; ++v) d = fmin(d, s_thr[v]);
+      thr = d + p.beta;  // (inf when a wave has fewer than K valid entries: no block pruning)
+    }
+    for (int q0 = t; q0 < P; q0 += PB * kAsThreads) {
       int e[PB];
       bool ok[PB];
 #pragma unroll
       for (int u = 0; u < PB; ++u) {
-        const int q = q0 + u * 64;
+        const int q = q0 + u * kAsThreads;
         // stencil tile and offset of pool position q (shift / mask when m_tile_view is a power of two)
         const int sq = p.m_shift >= 0 ? (q >> p.m_shift) : q / p.m_view;
         const int oq = q - sq * p.m_view;
-        const int ti = q < P ? tix[sq] : -1;
+        const int ti = q < P ? s_tix[sq] : -1;
         e[u] = (ti < 0 ? 0 : ti) * p.m_view + (q < P ? oq : 0);
         ok[u] = ti >= 0;
       }
@@ -292,14 +323,14 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
       }
 #pragma unroll
       for (int u = 0; u < PB; ++u) {
-        const int q = q0 + u * 64;
+        const int q = q0 + u * kAsThreads;
         if (q >= P) break;
         if (ok[u] && vv[u]) {
           // cost = d_pos + beta d_dir >= d_pos (beta >= 0, d_dir >= 0): an entry whose d_pos alone does
           // not beat the list's last (and comes later in the pool) cannot enter; skip its vMF term
           const double dx = mp[0] - px[u], dy = mp[1] - py[u], dz = mp[2] - pz[u];
           const double d_pos = (dx * dx + dy * dy) + dz * dz;
-          if (!(prune && d_pos >= key_value(key[KM - 1])))
+          if (!(prune && (d_pos > thr || d_pos >= key_value(key[KM - 1]))))
             list_insert<KM>(key, idx,
                             order_key(pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e[u], p.beta)), q);
         } else {
@@ -307,7 +338,7 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
         }
       }
     }
-    // k rounds of a wave argmin over the lanes' heads; the winner's owner pops its head
+    // k rounds of a block argmin over the lists' heads; the winner's owner pops its head
     for (int r = 0; r < p.k; ++r) {
       unsigned long long bk = key[0];
       int bp = idx[0];
@@ -320,7 +351,21 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
           bp = op;
         }
       }
-      if (lane == r) sel = bp;
+      const int buf = r & 1;
+      if (lane == 0) {
+        s_wk[buf][wid] = bk;
+        s_wp[buf][wid] = bp;
+      }
+      __syncthreads();
+      bk = s_wk[buf][0];
+      bp = s_wp[buf][0];
+#pragma unroll
+      for (int v = 1; v < kAsThreads / 64; ++v)
+        if (kless(s_wk[buf][v], s_wp[buf][v], bk, bp)) {
+          bk = s_wk[buf][v];
+          bp = s_wp[buf][v];
+        }
+      if (t == 0) s_sel[r] = bp;
       if (idx[0] == bp && key[0] == bk) {  // pool positions are unique: exactly one owner
 #pragma unroll
         for (int j = 0; j < KM - 1; ++j) {
@@ -331,13 +376,16 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
         idx[KM - 1] = 0x7fffffff;
       }
     }
+    __syncthreads();
   }
+  if (wid != 0) return;
   // per candidate (lane k < K): view index, unmasked cost + recency, row min (:377-403)
   const bool act = lane < p.k;
   int e = 0;
   if (act && row_valid) {
-    const int ti = tix[sel / p.m_view];
-    e = (ti < 0 ? 0 : ti) * p.m_view + sel % p.m_view;
+    const int q = s_sel[lane];
+    const int ti = s_tix[q / p.m_view];
+    e = (ti < 0 ? 0 : ti) * p.m_view + q % p.m_view;
   }
   double c = INFINITY, dt = 0.0;
   if (act) {
@@ -1053,13 +1101,13 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   if (bad_policy) {
     hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, 0);
   } else if (km == 8) {
-    hipLaunchKernelGGL(k_as_pool<8>, dim3((p.n + kPoolRows - 1) / kPoolRows), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL(k_as_pool<8>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
     hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   } else if (km == 16) {
-    hipLaunchKernelGGL(k_as_pool<16>, dim3((p.n + kPoolRows - 1) / kPoolRows), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL(k_as_pool<16>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
     hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   } else {
-    hipLaunchKernelGGL(k_as_pool<32>, dim3((p.n + kPoolRows - 1) / kPoolRows), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL(k_as_pool<32>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
     hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   }
   ASCHK(c, hipGetLastError());
