@@ -65,8 +65,6 @@ struct gcs_ctx {
   int* d_rknn = nullptr;
   int* d_pools = nullptr;
   float* d_pool_bound = nullptr;  // per pool entry: dot upper bound of it and every later entry
-  double* d_pool_dirs = nullptr;  // pool entries with their directions inline: (x, y, z, id)
-  double* d_knn_dirs = nullptr;   // per device bin, its K candidates' directions
   std::vector<double> dirs_host;  // reference order
   std::vector<int> knn_host;      // reference rows and ids
   // device bin order (scale mode: Hilbert patches; dense: identity); order[dev] = reference id
@@ -390,20 +388,6 @@ int upload_atlas(gcs_ctx* c) {
     for (int& id : pools)
       if (id >= 0) id = c->inv[id];
     if (int rc = upload(c, c->d_pools, pools)) return rc;
-    {  // the same pool rows and candidate rows with the directions inline (k_points, one round trip each)
-      std::vector<double> pe(pools.size() * 4, 0.0);
-      for (size_t q = 0; q < pools.size(); ++q) {
-        const int id = pools[q];
-        pe[4 * q + 3] = (double)id;
-        if (id >= 0)
-          for (int k = 0; k < 3; ++k) pe[4 * q + k] = d4[(size_t)id * 4 + k];
-      }
-      if (int rc = upload(c, c->d_pool_dirs, pe)) return rc;
-      std::vector<double> kd((size_t)B * K * 3);
-      for (size_t q = 0; q < knn_dev.size(); ++q)
-        for (int k = 0; k < 3; ++k) kd[3 * q + k] = d4[(size_t)knn_dev[q] * 4 + k];
-      if (int rc = upload(c, c->d_knn_dirs, kd)) return rc;
-    }
     HIPCHK(c, hipMemcpy(c->d_knn, knn_dev.data(), knn_dev.size() * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_rknn_off, off.data(), off.size() * sizeof(int), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->d_rknn, idx.data(), idx.size() * sizeof(int), hipMemcpyHostToDevice));
@@ -487,12 +471,6 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   a.k = c->K;
   a.pools = c->d_pools;
   a.pool_bound = c->d_pool_bound;
-  static const bool inline_dirs = [] {  // GCSLAM_INLINE_DIRS=0: the id tables + bin_dirs (A/B knob)
-    const char* e = getenv("GCSLAM_INLINE_DIRS");
-    return !(e && atoi(e) == 0);
-  }();
-  a.pool_dirs = inline_dirs ? c->d_pool_dirs : nullptr;
-  a.knn_dirs = inline_dirs ? c->d_knn_dirs : nullptr;
   a.bin_ref = c->d_bin_ref;
   a.pool_width = c->pool_width;
   a.grid = c->G;
@@ -1094,7 +1072,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   }
   if (c->push_stream) (void)hipStreamSynchronize(c->push_stream);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->d_gate_xi, c->d_pool_dirs, c->d_knn_dirs, c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
+  void* ptrs[] = {c->d_gate_xi, c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_tile_order, c->d_tile_work, c->d_bins_part, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,

@@ -55,11 +55,6 @@ struct PointKernelArgs {
   const int* pools;        // ncell x pool_width, nearest-first (angle from the cell centre), -1 padded
   const float* pool_bound; // per entry: upper bound of the dot with it and every later entry (-2 padded)
   const int* bin_ref;      // device id -> reference id (the nearest-bin tie rule: lower reference id)
-  // the same tables with the directions inline (LP = 1), so each of the two dependent lookups is one
-  // round trip instead of two (ids, then their directions): per pool entry (x, y, z, id), per bin its
-  // K candidates' (x, y, z)
-  const double* pool_dirs;  // ncell x pool_width x 4
-  const double* knn_dirs;   // B x k x 3
   int pool_width, grid;
   // outputs
   PointRec* recs;

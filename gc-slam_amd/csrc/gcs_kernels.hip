@@ -376,35 +376,6 @@ void k_points(PointKernelArgs a, double* partials) {
         const float* pbound = a.pool_bound + prow;
         const int nq = a.pool_width >> 2;
         double best = -INFINITY;
-        if (LP == 1 && a.pool_dirs) {
-          // inline pool rows: 8 entries (x, y, z, id) per batch in one round trip
-          const double4* pe = (const double4*)(a.pool_dirs + prow * 4);
-          for (int q = 0; q < nq; q += 2) {
-            const bool two = q + 1 < nq;
-            const float bnext = q + 2 < nq ? pbound[4 * (q + 2)] : -2.0f;
-            double4 E[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) E[u] = (u < 4 || two) ? pe[4 * q + u] : make_double4(0.0, 0.0, 0.0, -1.0);
-            int ids[8];
-            double sv[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              ids[u] = (int)E[u].w;
-              const double dv = dot3_exact(d[0], d[1], d[2], E[u].x, E[u].y, E[u].z);
-              sv[u] = ids[u] >= 0 ? dv : -INFINITY;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-              if (sv[u] > best) {
-                best = sv[u];
-                nearest = ids[u];
-              } else if (sv[u] == best && ids[u] >= 0 && a.bin_ref[ids[u]] < a.bin_ref[nearest]) {
-                nearest = ids[u];  // an exact tie (measure zero): the lower reference id
-              }
-            }
-            if (ids[7] < 0 || (double)bnext < best) break;
-          }
-        } else {
         // 4 * CH ids per batch and lane: all loads in flight together
         constexpr int CH = LP >= 4 ? 1 : 2;
         // GCS_PROBE_NOPOOL (timing probe, not a parity build): the first pool id only
@@ -435,7 +406,6 @@ void k_points(PointKernelArgs a, double* partials) {
           }
           if ((CH == 2 ? u1.w : u0.w) < 0 || (double)bnext < best) break;
         }
-        }
 #pragma unroll
         for (int off = 1; off < LP; off <<= 1) {  // first maximum in reference-id order
           const double ob = __shfl_xor(best, off, 64);
@@ -456,22 +426,15 @@ void k_points(PointKernelArgs a, double* partials) {
         for (int k = 0; k < KL; ++k) cand[k] = a.knn[(size_t)nearest * KC + sub * KL + k];
       }
       double e[KL];
-      // the candidates' directions in groups of GCS_CAND_GROUP loads in flight (x, y, z only: 24 B);
-      // from the inline table they do not wait for the candidate ids
-      const double* kd = (LP == 1 && a.knn_dirs) ? a.knn_dirs + (size_t)nearest * KC * 3 : nullptr;
+      // the candidates' directions in groups of GCS_CAND_GROUP loads in flight (x, y, z only: 24 B)
 #pragma unroll
       for (int k0 = 0; k0 < KL; k0 += kCandGroup) {
         double3 bd[kCandGroup];
 #pragma unroll
         for (int k = 0; k < kCandGroup; ++k) {
-          if (kd) {
-            const double* p = kd + 3 * (k0 + k);
-            bd[k] = make_double3(p[0], p[1], p[2]);
-          } else {
-            const double* p = a.bin_dirs + 4 * (size_t)cand[k0 + k];
-            const double2 xy = *(const double2*)p;
-            bd[k] = make_double3(xy.x, xy.y, p[2]);
-          }
+          const double* p = a.bin_dirs + 4 * (size_t)cand[k0 + k];
+          const double2 xy = *(const double2*)p;
+          bd[k] = make_double3(xy.x, xy.y, p[2]);
         }
 #pragma unroll
         for (int k = 0; k < kCandGroup; ++k) {
