@@ -551,7 +551,8 @@ template <int KM, int RPT>
 __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p, AsWork w, AsOut o, int n_valid_host) {
 #pragma clang fp contract(off)
   __shared__ double s_red[16 * (KM + 8)];
-  __shared__ double s_colp[2 * (kShThreads / 64) * KM];
+  __shared__ double s_colp[(kShThreads / 64) * KM];
+  __shared__ double s_v[KM];
   __shared__ uint32_t s_hist[256], s_sel[4];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int N = p.n, K = p.k;
@@ -701,22 +702,17 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     double cs = c[0];
 #pragma unroll
     for (int sh = (64 >> LG) / 2; sh >= 1; sh >>= 1) cs += __shfl_xor(cs, sh, 64);
-    // column partials double-buffered by iteration: one barrier per iteration (a wave one iteration
-    // ahead writes the other buffer, and cannot pass the next barrier before every wave has read this one)
-    double* colp = s_colp + (it & 1) * (kShThreads / 64) * KM;
-    if ((lane & ((64 >> LG) - 1)) == 0) colp[wid * KM + col] = cs;
+    if ((lane & ((64 >> LG) - 1)) == 0) s_colp[wid * KM + col] = cs;
     __syncthreads();
-    // v = (b / (K^T u + 1e-12))^vb: every wave, lane k < K, column k over the waves in order (the same
-    // value in every wave), then broadcast in the wave -- no second barrier, no idle waves
-    double vk = 0.0;
-    if (lane < K) {
-      double sum = colp[lane];
+    if (t < K) {  // v = (b / (K^T u + 1e-12))^vb: column t over the waves in order
+      double sum = s_colp[t];
 #pragma unroll
-      for (int g = 1; g < kShThreads / 64; ++g) sum += colp[g * KM + lane];
-      vk = pow_sinkhorn(bk / (sum + 1e-12), vb);
+      for (int g = 1; g < kShThreads / 64; ++g) sum += s_colp[g * KM + t];
+      s_v[t] = pow_sinkhorn(bk / (sum + 1e-12), vb);
     }
+    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < KM; ++k) v[k] = k < K ? __shfl(vk, k, 64) : 0.0;
+    for (int k = 0; k < KM; ++k) v[k] = k < K ? s_v[k] : 0.0;
   }
   // pi, row masses, responsibilities and the cert sums
   // acc: [sum rm, sum rm^2, sum novel, defect_a^2, sum pi C, nonzero_a, sum pi | col masses K]
