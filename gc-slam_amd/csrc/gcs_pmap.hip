@@ -1791,6 +1791,28 @@ int gcs_pmap_write(gcs_pmap* p, int32_t tile, int32_t field, const void* host) {
   return GCS_OK;
 }
 
+// device-to-device copy of whole tiles (every field), on dst's stream: a hypothesis that must not
+// update the node's map works on copies of the tiles its scan touches (same tile size and lobes)
+int gcs_pmap_copy_tiles(gcs_pmap* dst, const int32_t* dst_tiles, const gcs_pmap* src, const int32_t* src_tiles,
+                        int32_t n) {
+  if (!dst || !src || n < 0 || (n > 0 && (!dst_tiles || !src_tiles))) return GCS_ERR_ARG;
+  if (dst->M != src->M || dst->nl != src->nl || dst->device != src->device)
+    return pm_fail(dst, GCS_ERR_ARG, "copy_tiles: maps of different tile size, lobe count or device");
+  for (int i = 0; i < n; ++i)
+    if (dst_tiles[i] < 0 || dst_tiles[i] >= dst->T || src_tiles[i] < 0 || src_tiles[i] >= src->T)
+      return pm_fail(dst, GCS_ERR_ARG, "tile storage index out of range");
+  PMCHK(dst, hipSetDevice(dst->device));
+  if (src->stream != dst->stream) PMCHK(dst, hipStreamSynchronize(src->stream));  // src's pending updates
+  for (int i = 0; i < n; ++i)
+    for (int f = 0; f < GCS_PM_NFIELDS; ++f) {
+      const size_t b = field_elems(dst, f) * kFieldBytes[f];
+      PMCHK(dst, hipMemcpyAsync((char*)dst->fields[f] + b * dst_tiles[i], (const char*)src->fields[f] + b * src_tiles[i],
+                                b, hipMemcpyDeviceToDevice, dst->stream));
+    }
+  PMCHK(dst, hipStreamSynchronize(dst->stream));
+  return GCS_OK;
+}
+
 int gcs_pmap_extract_view(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_ids, int32_t n, int32_t m_view,
                           double eps_lift, double eps_mass, gcs_pmap_view* o) {
   if (!p || !o || !tile_ids) return GCS_ERR_ARG;

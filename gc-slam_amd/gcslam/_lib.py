@@ -298,6 +298,7 @@ _SIGS = [
     ("gcs_pmap_clear_tile", C.c_int, [C.c_void_p, C.c_int32]),
     ("gcs_pmap_read", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
     ("gcs_pmap_write", C.c_int, [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
+    ("gcs_pmap_copy_tiles", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32]),
     ("gcs_pmap_extract_view", C.c_int, [C.c_void_p, c_int32_p, c_int64_p, C.c_int32, C.c_int32, C.c_double,
                                         C.c_double, C.POINTER(GcsPmapView)]),
     ("gcs_pmap_insert_masked", C.c_int, [C.c_void_p, c_int32_p, C.c_int32, C.c_int32, C.POINTER(GcsPmapRows),

@@ -175,6 +175,7 @@ class ScanPipelineResult:
     association: Optional[object] = None
     map_view: Optional[object] = None
     z_lin_pose: Optional[np.ndarray] = None
+    map_record: Optional[dict] = None  # the map update's inputs (primitive_map_follow)
 
 
 IMU_ODOM_CERTS = (("OdomEvidenceGaussian",), ("ImuAccelDirectionTimeResolved", "TransportConsistencyWeighting"),
@@ -312,7 +313,8 @@ def _candidate_stats(batch, view, res, eps_mass):
 
 def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, rec, t, w, imu_stamps, imu_gyro,
                             imu_accel, odom_pose, odom_cov_se3, scan_start_time, scan_end_time, dt_sec, t_last_scan,
-                            t_scan, Q, config: PipelineConfig, odom_twist, odom_twist_cov, scan_seq, L_ext, h_ext):
+                            t_scan, Q, config: PipelineConfig, odom_twist, odom_twist_cov, scan_seq, L_ext, h_ext,
+                            update_map=True):
     """The live pipeline (pipeline.py:316-1591) on the device: gcs_scan_begin (budget, predict, IMU
     preintegration, deskew, IMU/odometry branch, z_lin_pose) -> the map branch (:778-926) -> visual
     pose evidence (:980-1010) -> gcs_scan_finish (tempering, fusion, recompose, anchor drift) ->
@@ -346,6 +348,12 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
     if len(stencil) != int(config.N_STENCIL_TILES):
         raise ValueError(f"stencil tile size mismatch: expected N_STENCIL_TILES={config.N_STENCIL_TILES}, "
                          f"got {len(stencil)}")
+    if not update_map:
+        # a hypothesis k > 0: the node's map is read, never written (the reference stores hypothesis 0's
+        # update only, backend_node.py:2079-2083): this scan's recency, view and step 12b run on device
+        # copies of the tiles it touches
+        primitive_map = ctx._scratch_map = primitive_map.working_copy(list(active) + list(stencil),
+                                                                      into=getattr(ctx, "_scratch_map", None))
     am, c_infl, _, infl = GPM.primitive_map_recency_inflate(primitive_map, active, int(scan_seq),
                                                             config.RECENCY_DECAY_LAMBDA, config.RECENCY_MIN_SCALE)
     view = GPM.extract_atlas_map_view(am, stencil, int(config.M_TILE_VIEW), config.eps_lift, config.eps_mass)
@@ -385,8 +393,27 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
                         **{k: st[k] for k in ("insert_count_total", "insert_mass_total", "insert_mass_p95",
                                               "evicted_count", "evicted_mass_total", "fused_count", "fused_mass_total",
                                               "merged_count")})
+    # the inputs of this scan's map update: replayed on another copy of the node's map, they give this
+    # hypothesis' map bit for bit (primitive_map_follow)
+    record = dict(active=[int(x) for x in active], scan_seq=int(scan_seq), t=float(scan_end_time), z_t=z_t,
+                  batch=batch, association=res)
     return out, dict(map=am, batch=batch, map_update_cert=muc, certs=[c_surf, c_infl, c_assoc, c_vis],
-                     association=res, view=view, z_lin_pose=z_lin_pose)
+                     association=res, view=view, z_lin_pose=z_lin_pose, map_record=record)
+
+
+def primitive_map_follow(primitive_map, record: dict, config: "PipelineConfig"):
+    """Apply a lead hypothesis' map update (its recency inflation and step 12b, pipeline.py:800-809,
+    1232-1492, from `result.map_record`) to another copy of the node's map: every copy stays bitwise the
+    lead's (the node's hypothesis-0 map, backend_node.py:2079-2083) without moving map rows.  Returns the
+    step-12b statistics."""
+    from . import primitive_map as GPM
+    GPM.primitive_map_recency_inflate(primitive_map, record["active"], int(record["scan_seq"]),
+                                      config.RECENCY_DECAY_LAMBDA, config.RECENCY_MIN_SCALE)
+    ucfg = GPM.PrimitiveMapUpdateConfig(k_insert_tile=config.k_insert_tile, H_TILE=config.H_TILE,
+                                        RECENCY_DECAY_LAMBDA=config.RECENCY_DECAY_LAMBDA, eps_lift=config.eps_lift,
+                                        eps_mass=config.eps_mass, eps_psd=config.eps_psd)
+    return GPM.primitive_map_update(primitive_map, record["batch"], record["association"], record["z_t"],
+                                    record["active"], record["t"], int(record["scan_seq"]), config=ucfg)
 
 
 def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, raw_timestamps, raw_weights,
@@ -394,7 +421,7 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
                                    scan_start_time, scan_end_time, dt_sec, t_last_scan, t_scan, Q,
                                    config: PipelineConfig, odom_twist=None, odom_twist_cov=None, camera_batch=None,
                                    scan_seq=0, primitive_map=None, map_bins: Optional[HypothesisContext] = None,
-                                   L_ext=None, h_ext=None) -> ScanPipelineResult:
+                                   L_ext=None, h_ext=None, update_map: bool = True) -> ScanPipelineResult:
     """FS/backend/pipeline.py:316-1591 with the bin path of README.md:105-122.
 
     Every reference input is consumed: the point stream, the IMU window (deskew, scan-to-scan
@@ -408,7 +435,10 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
 
     primitive_map (an AtlasMap): the live primitive path (pipeline.py:778-1011, 1232-1492) replaces the
     bin evidence; map_bins then only carries the hypothesis state (belief, IW), and result.map is the
-    updated AtlasMap (the node keeps hypothesis 0's, backend_node.py:2079-2083)."""
+    updated AtlasMap (the node keeps hypothesis 0's, backend_node.py:2079-2083).  The AtlasMap is updated in
+    place; a hypothesis k > 0 passes update_map=False: its scan reads the node's map and works on device
+    copies of the tiles it touches (result.map is that scratch), as the reference's immutable maps behave.
+    result.map_record holds the update's inputs for primitive_map_follow (one map over several GPUs)."""
     global _camera_warned
     if _camera_batch_has_content(camera_batch):
         if config.camera_batch_policy == "raise":
@@ -424,7 +454,7 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
         out, live = _process_scan_primitive(ctx, primitive_map, belief_prev, rec, t, w, imu_stamps, imu_gyro,
                                             imu_accel, odom_pose, odom_cov_se3, scan_start_time, scan_end_time, dt_sec,
                                             t_last_scan, t_scan, Q, config, odom_twist, odom_twist_cov, scan_seq,
-                                            L_ext, h_ext)
+                                            L_ext, h_ext, update_map=update_map)
     else:
         out = ctx.scan(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
                        dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
@@ -455,6 +485,7 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
         res.association = live["association"]
         res.map_view = live["view"]
         res.z_lin_pose = live["z_lin_pose"]
+        res.map_record = live["map_record"]
         res.map_bins_updated = None
     # the reference's per-scan MinimalScanTape (pipeline.py:1504-1570)
     res.diagnostics_tape = tape_from_result(res, scan_seq, scan_end_time, dt_sec, rec.shape[0], res.L_evidence)

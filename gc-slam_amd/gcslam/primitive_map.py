@@ -69,6 +69,7 @@ class AtlasMap:
             raise (ValueError if rc == -1 else RuntimeError)(f"gcs_pmap_create failed ({rc})")
         self.h = h
         self.m_tile, self.max_tiles, self.n_lobes, self.device = int(m_tile), int(max_tiles), int(n_lobes), int(device)
+        self.max_merge = int(max_merge)
         self.tiles = {}
         self.counts = {}
         self.next_global_id = 0
@@ -149,6 +150,29 @@ class AtlasMap:
             n = int(np.asarray(arrays["valid_mask"]).sum())
             self.total_count += n - self.counts.get(int(tile_id), 0)
             self.counts[int(tile_id)] = n
+
+
+    def working_copy(self, tile_ids, into: "AtlasMap" = None) -> "AtlasMap":
+        """A map holding device copies of the tiles of `tile_ids` this map has, with this map's
+        bookkeeping (ids, counts): what a hypothesis that reads the node's map but must not update it
+        works on -- the reference's maps are immutable and the node stores hypothesis 0's result only
+        (backend_node.py:2062,2079-2083).  `into`: a scratch map to reuse (its tiles are dropped)."""
+        ids = [int(t) for t in dict.fromkeys(int(x) for x in tile_ids)]
+        if into is None or into.m_tile != self.m_tile or into.n_lobes != self.n_lobes or into.max_tiles < len(ids):
+            into = AtlasMap(self.m_tile, max_tiles=max(len(ids), 1), n_lobes=self.n_lobes, max_merge=self.max_merge,
+                            device=self.device)
+        into.tiles, into.counts, into._free = {}, {}, list(range(into.max_tiles))
+        present = [t for t in ids if t in self.tiles]
+        dst = np.array([into._free.pop(0) for _ in present], dtype=np.int32)
+        src = np.array([self.tiles[t] for t in present], dtype=np.int32)
+        for t, d in zip(present, dst):
+            into.tiles[t] = int(d)
+            into.counts[t] = self.counts.get(t, 0)
+        if present:
+            into._chk(self.lib.gcs_pmap_copy_tiles(into.h, dst.ctypes.data, self.h, src.ctypes.data, len(present)),
+                      "gcs_pmap_copy_tiles")
+        into.next_global_id, into.total_count = self.next_global_id, self.total_count
+        return into
 
 
 def create_empty_atlas_map(m_tile: int = GC_PRIMITIVE_MAP_MAX_SIZE, max_tiles: int = 64, device: int = 0) -> AtlasMap:

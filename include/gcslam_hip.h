@@ -678,6 +678,11 @@ int gcs_pmap_clear_tile(gcs_pmap* pm, int32_t tile);
 /* one field of one tile, host buffer of m_tile x width elements */
 int gcs_pmap_read(gcs_pmap* pm, int32_t tile, int32_t field, void* host);
 int gcs_pmap_write(gcs_pmap* pm, int32_t tile, int32_t field, const void* host);
+/* Device-to-device copy of whole tiles (every field) from src storage slots to dst storage slots (maps of
+ * the same m_tile, n_lobes and device; dst == src allowed): the working copy of a hypothesis that reads
+ * the node's map but must not update it (backend_node.py:2062,2079-2083). */
+int gcs_pmap_copy_tiles(gcs_pmap* dst, const int32_t* dst_tiles, const gcs_pmap* src, const int32_t* src_tiles,
+                        int32_t n);
 /* tiles: n host storage indices in view order (-1: a tile missing from the map, viewed as empty);
  * tile_ids: the n MA-hex ids written to candidate_tile_ids */
 int gcs_pmap_extract_view(gcs_pmap* pm, const int32_t* tiles, const int64_t* tile_ids, int32_t n, int32_t m_view,

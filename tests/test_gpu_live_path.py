@@ -109,3 +109,68 @@ def test_live_primitive_path_closed_loop_three_scans(m_tile):
     assert am.total_count == sum(int(t["valid_mask"].sum()) for t in tiles.values())
     am.close()
     ctx.close()
+
+
+def test_live_path_hypotheses_share_hypothesis0_map():
+    """The node's one map over several hypotheses (backend_node.py:2036-2083): hypothesis 0 updates the
+    node map in place; hypothesis 1 (update_map=False) reads it and works on device copies of the tiles
+    it touches -- the node map is bit for bit unchanged by it, and its scan equals the same scan run on
+    an independent copy of the node map; a second copy of the node map (another GPU's) that replays
+    hypothesis 0's map_record with primitive_map_follow stays bitwise the node map."""
+    from gcslam import synthetic
+    from gcslam import primitive_map as gpm
+    from gcslam.pipeline import (BeliefGaussianInfo, PipelineConfig, datasheet_process_noise_state,
+                                 primitive_map_follow, process_noise_state_to_Q, process_scan_single_hypothesis)
+    N, m_tile = 8192, 4096
+    cfg = PipelineConfig(K_HYP=2, N_POINTS_CAP=N, B_BINS=48, soft_assign_mode="dense", lidar_origin_base=ORIGIN,
+                         max_raw_points=N, primitive_map_max_size=m_tile, R_ACTIVE_TILES_Z=1, R_STENCIL_TILES_Z=1,
+                         N_ACTIVE_TILES=21, N_STENCIL_TILES=21)
+    ctx0, ctx1, ctx1r = cfg.make_context(), cfg.make_context(), cfg.make_context()
+    am, am2 = gpm.create_empty_atlas_map(m_tile=m_tile), gpm.create_empty_atlas_map(m_tile=m_tile)
+    scratch_ref = gpm.create_empty_atlas_map(m_tile=m_tile)
+    b0 = BeliefGaussianInfo.create_identity_prior()
+    b1 = BeliefGaussianInfo.create_identity_prior()
+    b1.X_anchor = np.array([0.03, -0.02, 0.0, 0.001, -0.002, 0.004])
+    Q = process_noise_state_to_Q(datasheet_process_noise_state())
+
+    def tiles_of(m):
+        return {t: m.read_tile(t) for t in m.tile_ids}
+
+    def same(a, b):
+        assert set(a) == set(b)
+        for t in a:
+            for f in a[t]:
+                assert np.array_equal(a[t][f], b[t][f]), (t, f)
+
+    for scan_seq in range(3):
+        sc = synthetic.make_scan(N, 90 + scan_seq)
+        kw = dict(raw_points=sc["points"], raw_timestamps=sc["timestamps"], raw_weights=sc["weights"],
+                  raw_ring=np.zeros(N, np.uint8), raw_tag=np.zeros(N, np.uint8), imu_stamps=sc["imu_stamps"],
+                  imu_gyro=sc["imu_gyro"], imu_accel=sc["imu_accel"], odom_pose=sc["odom_pose"],
+                  odom_cov_se3=sc["odom_cov_se3"], scan_start_time=sc["scan_start_time"],
+                  scan_end_time=sc["scan_end_time"], dt_sec=sc["dt_sec"], t_last_scan=sc["t_last_scan"],
+                  t_scan=sc["t_scan"], Q=Q, config=cfg, odom_twist=sc["odom_twist"],
+                  odom_twist_cov=sc["odom_twist_cov"], camera_batch=None, scan_seq=scan_seq)
+        r0 = process_scan_single_hypothesis(belief_prev=b0, primitive_map=am, map_bins=ctx0, **kw)
+        assert r0.map is am
+        node = tiles_of(am)
+        r1 = process_scan_single_hypothesis(belief_prev=b1, primitive_map=am, map_bins=ctx1, update_map=False, **kw)
+        assert r1.map is not am
+        same(tiles_of(am), node)                      # hypothesis 1 left the node map alone
+        full = gpm.create_empty_atlas_map(m_tile=m_tile)
+        am.working_copy(am.tile_ids, into=full)       # 64 slots: room for the tiles step 12b creates
+        r1r = process_scan_single_hypothesis(belief_prev=b1, primitive_map=full, map_bins=ctx1r, **kw)
+        assert np.array_equal(r1.z_t, r1r.z_t) and np.array_equal(r1.belief_updated.L, r1r.belief_updated.L)
+        for t in r1.map.tile_ids:                     # its working tiles = the full copy's after the same scan
+            g, h = r1.map.read_tile(t), full.read_tile(t)
+            for f in g:
+                assert np.array_equal(g[f], h[f]), (scan_seq, t, f)
+        full.close()
+        primitive_map_follow(am2, r0.map_record, cfg)  # another GPU's copy of the node map
+        same(tiles_of(am2), node)
+        assert am2.next_global_id == am.next_global_id and am2.total_count == am.total_count
+        b0, b1 = r0.belief_updated, r1.belief_updated
+    for m in (am, am2, scratch_ref):
+        m.close()
+    for c in (ctx0, ctx1, ctx1r):
+        c.close()
