@@ -1976,8 +1976,9 @@ int gcs_scan_finish(gcs_ctx* c, const gcs_lidar_evidence* ev, gcs_scan_outputs* 
 namespace {
 // Payload layout: [w_iw dPsi 252 | w_iw dnu 7 | w_iw dPsi_meas 27 | w_iw dnu_meas 3 |
 // w L 484 | w h 22 | w z 22 | w mu 22 | w |mu|^2 1]
+// fac (may be null): the lifted factor of b.L, already computed (the context's last tail)
 void pack_payload(const Belief& b, const double* dPsi, const double* dnu, const double* mdPsi, const double* mdnu,
-                  double w_iw, double w_bary, double* p) {
+                  double w_iw, double w_bary, double* p, const host::SpdFactor* fac = nullptr) {
   int k = 0;
   for (int i = 0; i < 252; ++i) p[k++] = w_iw * (dPsi ? dPsi[i] : 0.0);
   for (int i = 0; i < 7; ++i) p[k++] = w_iw * (dnu ? dnu[i] : 0.0);
@@ -1987,7 +1988,8 @@ void pack_payload(const Belief& b, const double* dPsi, const double* dnu, const 
   for (int i = 0; i < DZ; ++i) p[k++] = w_bary * b.h[i];
   for (int i = 0; i < DZ; ++i) p[k++] = w_bary * b.z_lin[i];
   double mu[DZ], n2 = 0.0;
-  host::mean_increment(b, mu);
+  if (fac) host::spd_factor_solve(*fac, b.h, mu);  // mean_increment with the factor already at hand
+  else host::mean_increment(b, mu);
   for (int i = 0; i < DZ; ++i) { p[k++] = w_bary * mu[i]; n2 += mu[i] * mu[i]; }
   p[k++] = w_bary * n2;
 }
@@ -2045,7 +2047,7 @@ int gcs_hypothesis_payload(gcs_ctx* c, double w_iw, double w_bary, double* p) {
   if (!c || !p) return GCS_ERR_ARG;
   const bool h = c->have_last;
   pack_payload(c->belief, h ? c->last_dPsi : nullptr, h ? c->last_dnu : nullptr, h ? c->last_meas_dPsi : nullptr,
-               h ? c->last_meas_dnu : nullptr, w_iw, w_bary, p);
+               h ? c->last_meas_dnu : nullptr, w_iw, w_bary, p, c->prev_fac_valid ? &c->prev_fac : nullptr);
   return GCS_OK;
 }
 
