@@ -2276,10 +2276,11 @@ hipError_t launch_pt(const double* scan, const double* map, const double* derive
   // (a last-block fold in k_pt -- ticket with an agent-scope release per block -- measured slower:
   // 16.4 vs 12.3 us at C2, 46 vs 25 us at C3; each release writes back an L2 full of the bin
   // kernel's rows)
-  // GCSLAM_PT_FOLD=kernel: the separate k_final fold (A/B knob); default: k_pt's last block folds
+  // GCSLAM_PT_FOLD=last: k_pt's last block folds (measured slower: C2 105.4-105.9 vs 103.5-104.1 us per
+  // step, planar stage 14.2 vs 14.0 us, profiles/r03/ptfold/); default: the separate k_final fold
   static const bool last_block = [] {
     const char* e = getenv("GCSLAM_PT_FOLD");
-    return !(e && strcmp(e, "kernel") == 0);
+    return e && strcmp(e, "last") == 0;
   }();
   if (last_block && nblk > 1) {
     hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, scan, map, derived, B, scalars, partials,
