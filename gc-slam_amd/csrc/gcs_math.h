@@ -667,11 +667,14 @@ GCS_HD double exp_short(double x) {  // |x| < 700
 
 // x^y for the Sinkhorn scalings: 0 at x = 0, exp_short(y log_short(x)) for positive finite normal
 // x and |y log x| < 700, the library pow otherwise (a few ulps from pow: |y log x| < ~40 here)
+// The library pow out of line: inlined at each of the Sinkhorn loop's five call sites it made the
+// loop body too large for the instruction cache.
+__host__ __device__ __attribute__((noinline)) inline double pow_lib(double x, double y) { return pow(x, y); }
 GCS_HD double pow_sinkhorn(double x, double y) {
   if (x == 0.0) return 0.0;
-  if (!(x >= 2.2250738585072014e-308) || !(x <= 1.7976931348623157e308)) return pow(x, y);
+  if (!(x >= 2.2250738585072014e-308) || !(x <= 1.7976931348623157e308)) return pow_lib(x, y);
   const double a = y * log_short(x);
-  if (!(fabs(a) < 700.0)) return pow(x, y);
+  if (!(fabs(a) < 700.0)) return pow_lib(x, y);
   return exp_short(a);
 }
 
