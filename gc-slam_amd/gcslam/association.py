@@ -130,6 +130,17 @@ class Associator:
 
     def run(self, batch, view: AtlasMapView, config: AssociationConfig, eps_lift=GC_EPS_LIFT, eps_mass=GC_EPS_MASS):
         """Result tensors (fresh device tensors) + the cert scalars (dict) + exact flag."""
+        call = self.prepare(batch, view, config, eps_lift, eps_mass)
+        o = call()
+        cert = {k: float(o.cert[i]) for i, k in enumerate(L.ASSOC_CERT_FIELDS)}
+        return call.out, cert, bool(o.exact)
+
+    def prepare(self, batch, view: AtlasMapView, config: AssociationConfig, eps_lift=GC_EPS_LIFT,
+                eps_mass=GC_EPS_MASS):
+        """The C-ABI call of `run` with its argument structs and device tensors built: call() runs
+        gcs_associate_primitives_ot again on the same inputs into the same outputs (call.out) and
+        returns the outputs struct -- the boundary call a C caller makes, without the Python argument
+        marshalling (tools/assoc_bench.py times both)."""
         torch = _torch()
         dev = f"cuda:{self.device}"
         f64 = lambda x: torch.as_tensor(x, device=dev).to(torch.float64).contiguous()  # noqa: E731
@@ -174,10 +185,14 @@ class Associator:
         c.scan_seq, c.recency_decay_lambda = int(config.scan_seq), float(config.recency_decay_lambda)
         self._chk(self.lib.gcs_assoc_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
                   "gcs_assoc_ctx_set_stream")
-        self._chk(self.lib.gcs_associate_primitives_ot(self.h, C.byref(c), C.byref(m), C.byref(v), C.byref(o)),
-                  "gcs_associate_primitives_ot")
-        cert = {k: float(o.cert[i]) for i, k in enumerate(L.ASSOC_CERT_FIELDS)}
-        return out, cert, bool(o.exact)
+        lib, h, chk = self.lib, self.h, self._chk
+        args = (h, C.byref(c), C.byref(m), C.byref(v), C.byref(o))
+
+        def call():
+            chk(lib.gcs_associate_primitives_ot(*args), "gcs_associate_primitives_ot")
+            return o
+        call.out, call.keep = out, (keep, c, m, v, o)
+        return call
 
 
     def pose_evidence(self, batch, view: AtlasMapView, result, k_assoc: int, z_lin_pose, eps_lift=GC_EPS_LIFT,

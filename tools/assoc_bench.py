@@ -33,6 +33,18 @@ def main():
         ts = np.array(ts) * 1e3
         print(f"associate_primitives_ot N=1536 K=8 pool=7x1024 k_sinkhorn={iters}: median {np.median(ts):.3f} ms, "
               f"p90 {np.percentile(ts, 90):.3f} ms over {len(ts)} calls", flush=True)
+        # the C-ABI call alone (gcs_associate_primitives_ot on prepared device inputs; it synchronises)
+        call = GA._associator_for(1536, 7 * 1024, 8, 0).prepare(b, v, cfg)
+        for _ in range(3):
+            call()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            call()
+            ts.append(time.perf_counter() - t0)
+        ts = np.array(ts) * 1e3
+        print(f"  C-ABI gcs_associate_primitives_ot k_sinkhorn={iters}: median {np.median(ts):.3f} ms, "
+              f"p90 {np.percentile(ts, 90):.3f} ms over {len(ts)} calls", flush=True)
     del torch
 
 
