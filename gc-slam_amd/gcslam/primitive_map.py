@@ -568,6 +568,15 @@ def primitive_map_update(atlas_map: AtlasMap, measurement_batch, assoc_result, z
     """pipeline.py:1244-1447 (step 12b) on the GPU: the scan's MeasurementBatch (body frame) fused into
     the active tiles at z_t = [t, rotvec] through the association result, novelty insertion, then
     cull / forget / merge-reduce per tile.  Returns the MapUpdateCert counters (:1457-1486)."""
+    return primitive_map_update_call(atlas_map, measurement_batch, assoc_result, z_t, active_tile_ids, timestamp,
+                                     config)(scan_seq)
+
+
+def primitive_map_update_call(atlas_map: AtlasMap, measurement_batch, assoc_result, z_t, active_tile_ids: List[int],
+                              timestamp: float, config: Optional[PrimitiveMapUpdateConfig] = None):
+    """`primitive_map_update` with its C-ABI arguments built once: call(scan_seq) runs
+    gcs_pmap_map_update on them (the boundary call a C caller makes; tools/pmap_bench.py times it
+    beside the Python call) and returns the MapUpdateCert counters."""
     torch = _torch()
     cfg = config or PrimitiveMapUpdateConfig()
     dev = f"cuda:{atlas_map.device}"
@@ -598,16 +607,21 @@ def primitive_map_update(atlas_map: AtlasMap, measurement_batch, assoc_result, z
     cnt = np.zeros(max(len(active_tile_ids), 1), np.int32)
     st = L.GcsPmapUpdateStats()
     atlas_map._stream()
-    atlas_map._chk(atlas_map.lib.gcs_pmap_map_update(
-        atlas_map.h, ip, tids.ctypes.data_as(L.c_int64_p), len(active_tile_ids), L.dptr(z), float(timestamp),
-        int(scan_seq), nxt.ctypes.data_as(L.c_int64_p), C.byref(c), C.byref(inp), C.byref(st), L.iptr(cnt)),
-        "gcs_pmap_map_update")
-    atlas_map.total_count += int(st.insert_count_total) - int(st.evicted_count) - int(st.merged_count)
-    atlas_map.next_global_id = int(nxt[0])
-    for k, t in enumerate(active_tile_ids):
-        atlas_map.counts[int(t)] = int(cnt[k])
-    return dict(n_active_tiles=len(active_tile_ids), tile_ids_active=[int(t) for t in active_tile_ids],
-                insert_count_total=int(st.insert_count_total), insert_mass_total=float(st.insert_mass_total),
-                insert_mass_p95=float(st.insert_mass_p95), evicted_count=int(st.evicted_count),
-                evicted_mass_total=float(st.evicted_mass_total), fused_count=int(st.fused_count),
-                fused_mass_total=float(st.fused_mass_total), merged_count=int(st.merged_count))
+    lib, h = atlas_map.lib, atlas_map.h
+    args = (h, ip, tids.ctypes.data_as(L.c_int64_p), len(active_tile_ids), L.dptr(z), float(timestamp))
+    tail = (nxt.ctypes.data_as(L.c_int64_p), C.byref(c), C.byref(inp), C.byref(st), L.iptr(cnt))
+
+    def call(scan_seq: int) -> dict:
+        nxt[0] = atlas_map.next_global_id
+        atlas_map._chk(lib.gcs_pmap_map_update(*args, int(scan_seq), *tail), "gcs_pmap_map_update")
+        atlas_map.total_count += int(st.insert_count_total) - int(st.evicted_count) - int(st.merged_count)
+        atlas_map.next_global_id = int(nxt[0])
+        for k, t in enumerate(active_tile_ids):
+            atlas_map.counts[int(t)] = int(cnt[k])
+        return dict(n_active_tiles=len(active_tile_ids), tile_ids_active=[int(t) for t in active_tile_ids],
+                    insert_count_total=int(st.insert_count_total), insert_mass_total=float(st.insert_mass_total),
+                    insert_mass_p95=float(st.insert_mass_p95), evicted_count=int(st.evicted_count),
+                    evicted_mass_total=float(st.evicted_mass_total), fused_count=int(st.fused_count),
+                    fused_mass_total=float(st.fused_mass_total), merged_count=int(st.merged_count))
+    call.keep = (keep, inp, c, idx, ip, tids, z, nxt, cnt, st)
+    return call

@@ -99,9 +99,16 @@ def main():
     def view_c():
         am._chk(am.lib.gcs_pmap_extract_view(am.h, ip, tp, len(tids), 1024, 1e-9, 1e-12, C.byref(vs)), "view")
 
+    upd_call = gpm.primitive_map_update_call(am, b, a, z, tids, 1.0)
+
+    def upd_c():
+        seq[0] += 1
+        upd_call(seq[0])
+
     for name, fn in (("extract_atlas_map_view 7 x 50,000 -> 7 x 1024", lambda: gpm.extract_atlas_map_view(am, tids, 1024)),
                      ("gcs_pmap_extract_view (C-ABI call alone) 7 x 50,000 -> 7 x 1024", view_c),
                      ("primitive_map_update (step 12b) N=1536 K=8, 7 tiles", upd),
+                     ("gcs_pmap_map_update (step 12b, C-ABI call alone) N=1536 K=8, 7 tiles", upd_c),
                      ("primitive_map_recency_inflate 7 tiles", lambda: gpm.primitive_map_recency_inflate(am, tids, 70))):
         med, p90 = timed(fn, iters)
         print(f"{name}: median {med:.3f} ms, p90 {p90:.3f} ms over {iters} calls")
