@@ -241,6 +241,10 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
   __shared__ int s_wp[2][kAsThreads / 64];
   __shared__ int s_sel[32];
   __shared__ double s_thr[kAsThreads / 64];
+  // per wave: the ring of entries past the threshold (d_pos, pool position, view index)
+  constexpr unsigned kRing = 512;  // >= 63 pending + PB x 64 appended per trip
+  __shared__ double s_rd[kAsThreads / 64][kRing];
+  __shared__ int s_rq[kAsThreads / 64][kRing], s_re[kAsThreads / 64][kRing];
   const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const bool row_valid = in.valid[i] != 0;
   if (t < p.n_stencil) s_tix[t] = w.tix[(size_t)i * p.n_stencil + t];
@@ -256,7 +260,6 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
       key[j] = ~0ULL;
       idx[j] = 0x7fffffff;
     }
-    const int P = p.n_stencil * p.m_view;
     const bool prune = p.beta >= 0.0;
     // four pool entries per trip, in increasing pool position: their table loads issue together
     constexpr int PB = 4;
@@ -267,19 +270,24 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
     // (K rounds of a wave min, K distinct entries at or below it); the block's smallest wave value.
     // Without it every thread's first K entries took full costs (2,048 per row).
     double thr = INFINITY;
+    const int S = p.n_stencil, MV = p.m_view;
     if (prune) {
+      // tile-major: the stencil tile of a trip is uniform across the workgroup
       double dmin = INFINITY;
-      for (int q0 = t; q0 < P; q0 += PB * kAsThreads) {
+      for (int sq = 0; sq < S; ++sq) {
+        const int ti = s_tix[sq];
+        if (ti < 0) continue;
+        const size_t base = (size_t)ti * MV;
+        for (int o = t; o < MV; o += PB * kAsThreads) {
 #pragma unroll
-        for (int u = 0; u < PB; ++u) {
-          const int q = q0 + u * kAsThreads;
-          const int sq = p.m_shift >= 0 ? (q >> p.m_shift) : q / p.m_view;
-          const int ti = q < P ? s_tix[sq] : -1;
-          if (ti < 0) continue;
-          const int e = ti * p.m_view + (q - sq * p.m_view);
-          if (!in.vvalid[e]) continue;
-          const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
-          dmin = fmin(dmin, (dx * dx + dy * dy) + dz * dz);
+          for (int u = 0; u < PB; ++u) {
+            const int oo = o + u * kAsThreads;
+            if (oo >= MV) break;
+            const size_t e = base + oo;
+            if (!in.vvalid[e]) continue;
+            const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
+            dmin = fmin(dmin, (dx * dx + dy * dy) + dz * dz);
+          }
         }
       }
       double kth = INFINITY, cur = dmin;
@@ -298,46 +306,65 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
       for (int v = 1; v < kAsThreads / 64; ++v) d = fmin(d, s_thr[v]);
       thr = d + p.beta;  // (inf when a wave has fewer than K valid entries: no block pruning)
     }
-    for (int q0 = t; q0 < P; q0 += PB * kAsThreads) {
-      int e[PB];
-      bool ok[PB];
-#pragma unroll
-      for (int u = 0; u < PB; ++u) {
-        const int q = q0 + u * kAsThreads;
-        // stencil tile and offset of pool position q (shift / mask when m_tile_view is a power of two)
-        const int sq = p.m_shift >= 0 ? (q >> p.m_shift) : q / p.m_view;
-        const int oq = q - sq * p.m_view;
-        const int ti = q < P ? s_tix[sq] : -1;
-        e[u] = (ti < 0 ? 0 : ti) * p.m_view + (q < P ? oq : 0);
-        ok[u] = ti >= 0;
+    // Second pass, compacted: the entries that pass the block threshold go into the wave's ring (in
+    // increasing pool position) and are costed 64 at a time, one per lane, so the vMF term and the
+    // list insert run with every lane busy instead of once per trip whenever any lane has one.  Any
+    // partition of the entries over the lanes' lists gives the same K smallest (cost, position)
+    // after the merge below; each lane still takes its entries in increasing position.  Entries
+    // that are invalid or in a missing tile enter the visiting lane's list with the invalid cost.
+    double* rd = s_rd[wid];
+    int* rq = s_rq[wid];
+    int* re = s_re[wid];
+    unsigned head = 0, tail = 0;  // wave-uniform ring counters
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    auto take = [&](int n) {  // lanes < n cost ring entry head + lane
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (lane < n) {
+        const unsigned slot = (head + lane) & (kRing - 1);
+        const double d_pos = rd[slot];
+        const int q = rq[slot], e = re[slot];
+        if (!(prune && d_pos > key_value(key[KM - 1])))
+          list_insert<KM>(key, idx, order_key(pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e, p.beta)),
+                          q);
       }
-      uint8_t vv[PB];
+      head += n;
+    };
+    for (int sq = 0; sq < S; ++sq) {
+      const int ti = s_tix[sq];
+      const size_t base = (size_t)(ti < 0 ? 0 : ti) * MV;
+      for (int ow = t & ~63; ow < MV; ow += PB * kAsThreads) {  // wave-uniform trips (ballots inside)
 #pragma unroll
-      for (int u = 0; u < PB; ++u) vv[u] = ok[u] ? in.vvalid[e[u]] : (uint8_t)0;
-      double px[PB], py[PB], pz[PB];
-#pragma unroll
-      for (int u = 0; u < PB; ++u) {
-        px[u] = in.vpos[3 * e[u]];
-        py[u] = in.vpos[3 * e[u] + 1];
-        pz[u] = in.vpos[3 * e[u] + 2];
-      }
-#pragma unroll
-      for (int u = 0; u < PB; ++u) {
-        const int q = q0 + u * kAsThreads;
-        if (q >= P) break;
-        if (ok[u] && vv[u]) {
-          // cost = d_pos + beta d_dir >= d_pos (beta >= 0, d_dir >= 0): an entry whose d_pos alone does
-          // not beat the list's last (and comes later in the pool) cannot enter; skip its vMF term
-          const double dx = mp[0] - px[u], dy = mp[1] - py[u], dz = mp[2] - pz[u];
-          const double d_pos = (dx * dx + dy * dy) + dz * dz;
-          if (!(prune && (d_pos > thr || d_pos >= key_value(key[KM - 1]))))
-            list_insert<KM>(key, idx,
-                            order_key(pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e[u], p.beta)), q);
-        } else {
-          list_insert<KM>(key, idx, order_key(kCostInvalid), q);
+        for (int u = 0; u < PB; ++u) {
+          const int oo = ow + lane + u * kAsThreads;
+          const bool in_tile = oo < MV;
+          const int q = sq * MV + oo;
+          bool valid = false;
+          double d_pos = 0.0;
+          if (in_tile && ti >= 0 && in.vvalid[base + oo]) {
+            const size_t e = base + oo;
+            const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
+            d_pos = (dx * dx + dy * dy) + dz * dz;
+            valid = true;
+          } else if (in_tile) {
+            list_insert<KM>(key, idx, order_key(kCostInvalid), q);
+          }
+          // cost = d_pos + beta d_dir >= d_pos (beta >= 0, d_dir >= 0): past the threshold no entry
+          // can be selected
+          const bool keep = valid && !(prune && d_pos > thr);
+          const unsigned long long m = __ballot(keep);
+          if (keep) {
+            const unsigned slot = (tail + (unsigned)__popcll(m & lt_mask)) & (kRing - 1);
+            rd[slot] = d_pos;
+            rq[slot] = q;
+            re[slot] = (int)(base + oo);
+          }
+          tail += (unsigned)__popcll(m);
         }
+        while (tail - head >= 64u) take(64);
       }
     }
+    if (tail != head) take((int)(tail - head));
     // k rounds of a block argmin over the lists' heads; the winner's owner pops its head
     for (int r = 0; r < p.k; ++r) {
       unsigned long long bk = key[0];

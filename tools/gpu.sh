@@ -53,6 +53,10 @@ step() {
           --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline --no-c3 \
           > "$O/sq_$cfg.log" 2>&1 || return $?
       done ;;
+    assocsq)  # SQ instruction mix / wave states of the association kernels
+      timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES \
+        SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY --kernel-include-regex "k_as_" -d "$O/assocsq" -o run \
+        --output-format csv -- python3 tools/assoc_bench.py 5 > "$O/assocsq.log" 2>&1 ;;
     phase) for cfg in c2 c3; do timeout -k 10 180 python tools/phase_prof.py $cfg > "$O/phase_$cfg.txt" 2>&1 || return $?; done ;;
     pmap) timeout -k 10 300 python tools/pmap_bench.py 30 > "$O/pmap_bench.txt" 2>&1 ;;
     pmapprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/pmap_prof" -o run --output-format csv -- \
