@@ -170,6 +170,14 @@ __device__ __forceinline__ void solve3_pivot(const double* L, double eps, const 
 __global__ __launch_bounds__(kAsThreads) void k_as_prep(AsIn in, AsParams p, AsWork w, const int8_t* __restrict__ st) {
 #pragma clang fp contract(off)
   const int g = blockIdx.x * kAsThreads + threadIdx.x;
+  // the view's tile ids in LDS (broadcast reads) for the stencil lookups of the row lanes
+  constexpr int kLdsTiles = 256;
+  __shared__ int64_t s_tid[kLdsTiles];
+  const bool lds_tiles = p.n_tiles <= kLdsTiles;
+  if (lds_tiles && blockIdx.x * kAsThreads < p.n) {
+    for (int q = threadIdx.x; q < p.n_tiles; q += kAsThreads) s_tid[q] = in.tile_ids[q];
+    __syncthreads();
+  }
   if (g < p.n) {
     const int i = g;
     double L[9], th[3], x[3];
@@ -191,15 +199,26 @@ __global__ __launch_bounds__(kAsThreads) void k_as_prep(AsIn in, AsParams p, AsW
     const double s1 = x[0];
     const double s2 = x[0] * 0.5 + x[1] * kSqrt3Half;
     const int64_t c1 = (int64_t)floor(s1 / p.h), c2 = (int64_t)floor(s2 / p.h), cz = (int64_t)floor(x[2] / p.h);
-    for (int s = 0; s < p.n_stencil; ++s) {
-      const int64_t id = pack_tile(c1 + st[3 * s], c2 + st[3 * s + 1], cz + st[3 * s + 2]);
-      int hit = -1;
-      for (int q = 0; q < p.n_tiles; ++q)
-        if (in.tile_ids[q] == id) {
-          hit = q;
-          break;
-        }
-      w.tix[(size_t)i * p.n_stencil + s] = hit;
+    // eight stencil tiles per sweep over the view's tile list (the first match of each kept): the
+    // tile loads do not depend on a compare (a search per stencil tile with an early exit was a
+    // chain of dependent loads)
+    for (int s0 = 0; s0 < p.n_stencil; s0 += 8) {
+      int64_t id[8];
+      int hit[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int s = s0 + j < p.n_stencil ? s0 + j : s0;
+        id[j] = pack_tile(c1 + st[3 * s], c2 + st[3 * s + 1], cz + st[3 * s + 2]);
+        hit[j] = -1;
+      }
+      for (int q = p.n_tiles - 1; q >= 0; --q) {  // backwards: the last write is the first match
+        const int64_t v = lds_tiles ? s_tid[q] : in.tile_ids[q];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) hit[j] = v == id[j] ? q : hit[j];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (s0 + j < p.n_stencil) w.tix[(size_t)i * p.n_stencil + s0 + j] = hit[j];
     }
   } else if (g < p.n + p.m_pool) {
     const int e = g - p.n;
@@ -1185,7 +1204,12 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
     hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, 0);
   } else if (km == 8) {
     hipLaunchKernelGGL(k_as_pool<8>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
-    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+    // three rows per thread when they cover the rows (the reference's 1,536 = 3 x 512): no padding
+    // row in the K v / K^T u sums
+    if (3 * kShThreads < rpt_for(8) * kShThreads && p.n <= 3 * kShThreads)
+      hipLaunchKernelGGL((k_as_sinkhorn<8, 3>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+    else
+      hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   } else if (km == 16) {
     hipLaunchKernelGGL(k_as_pool<16>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
     hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
