@@ -55,6 +55,7 @@ constexpr int64_t kMask = (1LL << kBitsPerAxis) - 1;
 
 struct AsParams {
   int n, m_view, m_shift, n_tiles, n_stencil, k, iters, m_pool;
+  int s_center;  // the stencil entry (0, 0, 0): the row's own tile
   int a_policy, row_min, med;
   double beta, eps, tau_a, tau_b, eps_mass, eps_lift, eps_dir, h, lam, eps_lam;
   long long scan_seq;
@@ -291,39 +292,45 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
     double thr = INFINITY;
     const int S = p.n_stencil, MV = p.m_view;
     if (prune) {
-      // tile-major: the stencil tile of a trip is uniform across the workgroup
-      double dmin = INFINITY;
-      for (int sq = 0; sq < S; ++sq) {
-        const int ti = s_tix[sq];
-        if (ti < 0) continue;
-        const size_t base = (size_t)ti * MV;
-        for (int o = t; o < MV; o += PB * kAsThreads) {
+      // The bound from the row's own stencil tile first (its nearest entries are mostly there; a
+      // bound from any subset of the pool is still an upper bound), from every stencil tile only
+      // when that one leaves it infinite.  Tile-major: the stencil tile of a trip is uniform.
+      for (int round = 0; round < 2 && thr == INFINITY; ++round) {
+        double dmin = INFINITY;
+        for (int sq = round == 0 ? p.s_center : 0; sq < (round == 0 ? p.s_center + 1 : S); ++sq) {
+          const int ti = sq >= 0 ? s_tix[sq] : -1;
+          if (ti < 0) continue;
+          const size_t base = (size_t)ti * MV;
+          for (int o = t; o < MV; o += PB * kAsThreads) {
 #pragma unroll
-          for (int u = 0; u < PB; ++u) {
-            const int oo = o + u * kAsThreads;
-            if (oo >= MV) break;
-            const size_t e = base + oo;
-            if (!in.vvalid[e]) continue;
-            const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
-            dmin = fmin(dmin, (dx * dx + dy * dy) + dz * dz);
+            for (int u = 0; u < PB; ++u) {
+              const int oo = o + u * kAsThreads;
+              if (oo >= MV) break;
+              const size_t e = base + oo;
+              if (!in.vvalid[e]) continue;
+              const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1],
+                           dz = mp[2] - in.vpos[3 * e + 2];
+              dmin = fmin(dmin, (dx * dx + dy * dy) + dz * dz);
+            }
           }
         }
-      }
-      double kth = INFINITY, cur = dmin;
-      for (int r = 0; r < p.k; ++r) {  // the r-th smallest lane minimum, lanes popped in turn
-        double m = cur;
+        double kth = INFINITY, cur = dmin;
+        for (int r = 0; r < p.k; ++r) {  // the r-th smallest lane minimum, lanes popped in turn
+          double m = cur;
 #pragma unroll
-        for (int sh = 32; sh >= 1; sh >>= 1) m = fmin(m, __shfl_xor(m, sh, 64));
-        kth = m;
-        const unsigned long long hit = __ballot(cur == m);
-        if (lane == __ffsll((long long)hit) - 1) cur = INFINITY;  // one lane per round
-      }
-      if (lane == 0) s_thr[wid] = kth;
-      __syncthreads();
-      double d = s_thr[0];
+          for (int sh = 32; sh >= 1; sh >>= 1) m = fmin(m, __shfl_xor(m, sh, 64));
+          kth = m;
+          const unsigned long long hit = __ballot(cur == m);
+          if (lane == __ffsll((long long)hit) - 1) cur = INFINITY;  // one lane per round
+        }
+        if (lane == 0) s_thr[wid] = kth;
+        __syncthreads();
+        double d = s_thr[0];
 #pragma unroll
-      for (int v = 1; v < kAsThreads / 64; ++v) d = fmin(d, s_thr[v]);
-      thr = d + p.beta;  // (inf when a wave has fewer than K valid entries: no block pruning)
+        for (int v = 1; v < kAsThreads / 64; ++v) d = fmin(d, s_thr[v]);
+        __syncthreads();  // (s_thr is written again by a second round)
+        thr = d + p.beta;  // (inf when every wave has fewer than K valid entries: the second round)
+      }
     }
     // Second pass, compacted: the entries that pass the block threshold go into the wave's ring (in
     // increasing pool position) and are costed 64 at a time, one per lane, so the vMF term and the
@@ -1143,6 +1150,9 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
         ++ns;
       }
   if ((long)ns * v->m_tile_view < K) return as_fail(c, GCS_ERR_ARG, "pool smaller than k_assoc");
+  int s_center = -1;
+  for (int q = 0; q < ns; ++q)
+    if (st[3 * q] == 0 && st[3 * q + 1] == 0 && st[3 * q + 2] == 0) s_center = q;
   ASCHK(c, hipSetDevice(c->device));
   hipStream_t s = c->stream;
   AsParams p{};
@@ -1156,6 +1166,7 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   p.k = K;
   p.iters = cfg->k_sinkhorn;
   p.m_pool = (int)pool;
+  p.s_center = s_center;
   p.a_policy = cfg->a_policy == GCS_ASSOC_A_WEIGHT ? 1 : 0;
   p.row_min = cfg->cost_subtract_row_min != 0;
   p.med = cfg->cost_scale_by_median != 0;
