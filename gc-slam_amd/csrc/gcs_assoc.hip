@@ -44,6 +44,17 @@ constexpr int kAsThreads = 256;
 constexpr int kShThreads = GCS_SH_THREADS;
 constexpr int kShCR = 16 * 1024 / kShThreads;  // Sinkhorn row capacity: N <= kShCR * kShThreads / KM
 constexpr int kMaxStencil = 64;
+// GCS_SH_PROBE (timing probe builds only): wall-clock stamps of the Sinkhorn's phases, printed by the
+// host call (stderr) -- workgroup 0: start, marginal, K_mat, loop end, end; workgroup 1: end
+#ifndef GCS_SH_PROBE
+#define GCS_SH_PROBE 0
+#endif
+#if GCS_SH_PROBE
+__device__ unsigned long long g_sh_stamp[8];
+#define SH_STAMP(k) do { if (threadIdx.x == 0) g_sh_stamp[k] = wall_clock64(); } while (0)
+#else
+#define SH_STAMP(k) do { } while (0)
+#endif
 constexpr double kLog4Pi = 2.5310242469692907;     // np.log(4.0 * np.pi)
 constexpr double kLog2 = 0.6931471805599453;       // np.log(2.0)
 constexpr double kSqrt3Half = 0.8660254037844386;  // jnp.sqrt(3.0) * 0.5 (:319)
@@ -665,6 +676,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   __shared__ uint32_t s_hist[256], s_sel[4];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int N = p.n, K = p.k;
+  if (blockIdx.x == 0) SH_STAMP(0);
   const bool empty = n_valid_host == 0 || *w.mvalid == 0u;
   if (empty) {  // :272-287 -- zeros, exact cert (workgroup 0)
     if (blockIdx.x != 0) return;
@@ -708,6 +720,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     const double p95_a = radix_select<RPT>(va1, oka1, std::min((int)(0.95 * (double)N), N - 1), s_hist, s_sel);
     const int nbt = N * K;
     const double p95_b_row = radix_select<RPT * KM>(brow1, okb1, std::min((int)(0.95 * (double)nbt), nbt - 1), s_hist, s_sel);
+    SH_STAMP(5);
     if (t == 0) {
       o.cert[CE_P95_A] = p95_a;
       o.cert[CE_B_P95] = p95_b_row;
@@ -729,6 +742,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   }
   bsum<1>(part, s_red);
   const double sum_a = fmax(part[0], p.eps_mass);
+  SH_STAMP(1);
 #pragma unroll
   for (int j = 0; j < RPT; ++j) va[j] = va[j] / sum_a;
   uint32_t okm = 0;
@@ -762,6 +776,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const double bk = 1.0 / (double)K;
 #pragma unroll
   for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
+  SH_STAMP(2);
   double u[RPT], v[KM];
 #pragma unroll
   for (int j = 0; j < RPT; ++j) u[j] = 1.0;
@@ -823,6 +838,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
 #pragma unroll
     for (int k = 0; k < KM; ++k) v[k] = k < K ? s_v[k] : 0.0;
   }
+  SH_STAMP(3);
   // pi, row masses, responsibilities and the cert sums
   // acc: [sum rm, sum rm^2, sum novel, defect_a^2, sum pi C, nonzero_a, sum pi | col masses K]
   double acc[7 + KM];
@@ -851,7 +867,9 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     acc[3] += (rm - va[j]) * (rm - va[j]);
     acc[5] += va[j] > p.eps_mass ? 1.0 : 0.0;
   }
+  SH_STAMP(6);
   bsum<7 + KM>(acc, s_red);
+  SH_STAMP(7);
   if (t == 0) {
     double db = 0.0;
     for (int k = 0; k < K; ++k) db += (acc[7 + k] - bk) * (acc[7 + k] - bk);
@@ -867,6 +885,9 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     o.cert[CE_NONZERO_A] = acc[5];
     o.cert[CE_NONZERO_B] = bk > p.eps_mass ? (double)K : 0.0;
     o.cert[CE_ESS] = acc[0] * acc[0] / (acc[1] + p.eps_mass);
+#if GCS_SH_PROBE
+    g_sh_stamp[4] = wall_clock64();
+#endif
     o.cert[CE_MASS_EPS] = p.eps_mass / (tm + p.eps_mass);
     o.cert[CE_TOTAL_COST] = acc[4];
     o.cert[CE_SUPPORT] = acc[5] / (double)std::max(N, 1);
@@ -1230,6 +1251,15 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   }
   ASCHK(c, hipGetLastError());
   ASCHK(c, hipStreamSynchronize(s));
+#if GCS_SH_PROBE
+  {
+    unsigned long long h[8];
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sh_stamp), sizeof(h));
+    fprintf(stderr, "sh_probe us: marginal %.2f kmat %.2f loop %.2f finish %.2f (pi %.2f bsum %.2f cert %.2f) | wg1 %.2f\n",
+            (h[1] - h[0]) / 100.0, (h[2] - h[1]) / 100.0, (h[3] - h[2]) / 100.0, (h[4] - h[3]) / 100.0,
+            (h[6] - h[3]) / 100.0, (h[7] - h[6]) / 100.0, (h[4] - h[7]) / 100.0, (h[5] - h[0]) / 100.0);
+  }
+#endif
   for (int q = 0; q < GCS_ASSOC_CERT_LEN; ++q) o->cert[q] = c->h_cert[q];
   o->exact = c->h_cert[CE_EXACT] != 0.0;
   o->n_map_valid = (int32_t)c->h_cert[CE_MVALID];
