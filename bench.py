@@ -45,6 +45,7 @@ METRIC = "scans/sec (14-step pipeline) at 64k pts/scan"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 N_SCANS = 8             # distinct synthetic scans resident in HBM, cycled
 TIMING_STRIDE = 8       # roofline kernel stamped on every 8th scan of the timed region
+ROOFLINE_MIN = 16       # stamped launches behind `roofline` (a post-region pass tops short runs up)
 
 
 def bins_kernel_bytes(N, B):
@@ -156,7 +157,7 @@ def cpu_baseline(cfg):
     here) on bounded samples of the same workload, on this host's cores."""
     import multiprocessing as mp
     N, B = cfg["N"], cfg["B"]
-    allowed = sorted(os.sched_getaffinity(0))
+    allowed = process_cpus()  # the job's CPUs, not the rank's NUMA-local share
     prev = set(allowed)
     n1, t1 = _oracle_scans(N, B, "scale", 12, 8.0, core=allowed[0])
     os.sched_setaffinity(0, prev)
@@ -278,13 +279,14 @@ def _free_port():
 
 def launch_ranks(n, cpu):
     """`bench.py --gpus N` with no launcher: start N rank processes of this script (the one-process-per-GPU
-    layout torch.distributed.run gives) and return their exit status.  Nothing here touches a GPU:
-    torch.cuda.device_count() counts devices without initialising one on this image, and each rank
+    layout torch.distributed.run gives) and return their exit status.  Nothing here touches a GPU: the
+    visible GPUs are counted from the KFD topology in sysfs (gcslam.topology, the enumeration the HIP
+    runtime itself does; no torch.cuda call, which can fall back to hipGetDeviceCount), and each rank
     initialises only its own device."""
     import subprocess
     if not cpu:
-        import torch
-        vis = torch.cuda.device_count()
+        from gcslam import topology
+        vis = topology.visible_gpu_count() or 0  # no KFD topology: no AMD GPU driver here
         if n > vis:
             print(f"bench.py: --gpus {n} but only {vis} visible GPU(s)", file=sys.stderr, flush=True)
             return 2
@@ -292,7 +294,7 @@ def launch_ranks(n, cpu):
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), GCS_ALLOWED_CPUS=_allowed_str())
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
     rc = 0
     live = list(procs)
@@ -315,7 +317,17 @@ def launch_ranks(n, cpu):
     return rc
 
 
-def cpu_rehearsal(args, rank, world):
+def _allowed_str():
+    return ",".join(str(c) for c in sorted(os.sched_getaffinity(0)))
+
+
+def process_cpus():
+    """The CPUs this job may use (the launcher's set, passed down before the ranks pin themselves)."""
+    s = os.environ.get("GCS_ALLOWED_CPUS")
+    return sorted(int(c) for c in s.split(",")) if s else sorted(os.sched_getaffinity(0))
+
+
+def cpu_rehearsal(args, rank, world, pin):
     """The multi-rank path without GPUs (gloo): each rank packs its hypothesis' payload with the library
     (gcs_payload_pack: IW statistics with the raw weights, barycenter sums with the floor-renormalised
     ones, backend_node.py:1999-2002,2085-2090, hypothesis.py:83-99), the payloads are summed over
@@ -383,7 +395,8 @@ def cpu_rehearsal(args, rank, world):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
         allr = [None] * world
-        dist.all_gather_object(allr, dict(rank=rank, pid=os.getpid(), Q_sum=float(out[2].sum()), map_record_ok=rec_ok))
+        dist.all_gather_object(allr, dict(rank=rank, pid=os.getpid(), Q_sum=float(out[2].sum()), map_record_ok=rec_ok,
+                                          affinity=pin))
         ranks = allr
     if rank == 0:
         print(json.dumps({
@@ -421,8 +434,12 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
         sys.exit(2)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    # each rank on its GPU's NUMA-local host cores, before any GPU call (threads started later -- the
+    # HIP runtime's, the context's launch worker -- inherit the mask); cpu_baseline restores the job's set
+    from gcslam import topology
+    pin = topology.pin_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
     if args.cpu_rehearsal:
-        return cpu_rehearsal(args, rank, world)
+        return cpu_rehearsal(args, rank, world, pin)
 
     import torch
     import torch.distributed as dist
@@ -480,6 +497,8 @@ def main():
     # (budget launch + predict, device launch calls, tail numerics, pushforward launch calls)
     host_ms = np.zeros(9)
 
+    comb_ms = []  # every timed step's combine (pack, all-reduce, IW / Q apply), for SCALE's attribution
+
     def step():
         if state["sample"]:  # roofline-kernel event stamps on every TIMING_STRIDE-th scan
             phase = state["count"] % TIMING_STRIDE
@@ -499,7 +518,10 @@ def main():
                 host_ms[5 + k] += sm[4 + k]
             state["sampled"] += 1
         else:
+            tc = time.perf_counter()
             combine(state["count"])
+            if state["sample"]:
+                comb_ms.append((time.perf_counter() - tc) * 1e3)
         if follow is not None:
             follow(prepared[state["count"] % N_SCANS])
         state["count"] += 1
@@ -524,6 +546,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    elapsed_rank = elapsed
     per_rank_s = [elapsed]
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
@@ -533,10 +556,29 @@ def main():
         elapsed = max(per_rank_s)  # the slowest rank's clock
     state["sample"] = False
     ms_sum, counts = ctx.stage_times(reset=True)
+    bins_in_region = int(counts[2])
+    # the roofline kernel's duration: the timed region's stamped launches (every TIMING_STRIDE-th scan)
+    # plus, when those are fewer than ROOFLINE_MIN (short runs), a pass stamping it on every scan
+    if bins_in_region < ROOFLINE_MIN:
+        ctx.enable_timing(True, stages=["bins"])
+        for _ in range(ROOFLINE_MIN - bins_in_region):
+            step()
+        ctx.synchronize()
+        ctx.enable_timing(False)
+        ms2, c2 = ctx.stage_times(reset=True)
+        ms_sum, counts = ms_sum + ms2, counts + c2
     bins_ms = float(ms_sum[2] / counts[2]) if counts[2] else None
     bins_samples = int(counts[2])
     host_avg = dict(zip(["pre_device", "device_wait", "tail", "gcs_scan", "combine", "pre_predict", "launch_calls",
                          "tail_numerics", "push_launch"], (host_ms / max(state["sampled"], 1)).tolist()))
+    cm = np.array(comb_ms) if comb_ms else np.zeros(1)
+    me = dict(rank=rank, affinity=pin, host_ms=host_avg, ms_per_step=elapsed_rank / args.steps * 1e3,
+              combine_ms=dict(median=float(np.median(cm)), p90=float(np.percentile(cm, 90)), mean=float(cm.mean()),
+                              max=float(cm.max()), n=int(len(comb_ms))))
+    per_rank = [me]
+    if world > 1:  # every rank's host split and combine latency, so SCALE can attribute a loss
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, me)
     # diagnostic pass after the timed region: every device stage stamped (not part of `value`)
     ctx.enable_timing(True)
     for _ in range(min(args.steps, 20)):
@@ -570,10 +612,13 @@ def main():
             # the per-GPU rate SCALE compares across N (value / n_gpus; at N = 1 it equals value)
             "value_per_gpu": args.steps / elapsed,
             "per_rank_ms_per_step": [t / args.steps * 1e3 for t in per_rank_s],
+            # per rank: host pinning, sampled host split (host_ms keys), every timed step's combine latency
+            "per_rank": per_rank,
             "rccl": rccl,
             "step_ms": {"median": float(np.median(per_step) * 1e3), "p90": float(np.percentile(per_step, 90) * 1e3),
                         "min": float(per_step.min() * 1e3), "max": float(per_step.max() * 1e3)},
-            "roofline": dict(roofline(N, B, bins_ms, *pmc_traffic(args.config)) or {}, timed_launches=bins_samples),
+            "roofline": dict(roofline(N, B, bins_ms, *pmc_traffic(args.config)) or {}, timed_launches=bins_samples,
+                             timed_launches_in_region=bins_in_region),
             "roofline_chain": roofline_chain(N, B, stage_avg, f"{args.config} (diagnostic pass, every stage stamped)"),
             "stage_ms": stage_avg,
             "host_ms": host_avg,

@@ -187,6 +187,11 @@ struct gcs_ctx {
   bool use_direct = false;      // the stages of the current gcs_scan call
   uint32_t spin_limit = 1u << 22;
   int inject_scan_fail = 0;
+  // the round-3 point kernel instead of k_points_lean (GCSLAM_POINTS=legacy / GCS_DEBUG_POINT_KERNEL)
+  bool legacy_points = [] {
+    const char* e = getenv("GCSLAM_POINTS");
+    return e && strcmp(e, "legacy") == 0;
+  }();
   // hypothesis all-reduce payload (gcs_combine_allreduce): pinned host staging + device buffer
   double* h_payload = nullptr;
   double* d_payload = nullptr;
@@ -516,7 +521,8 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   }
   c->pts_blocks = points_blocks(c->cap, scale);
   c->pts_fold_pending = scale && fold_later;
-  HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, ev.e0, ev.e1));
+  HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, ev.e0, ev.e1,
+                          c->legacy_points));
   return GCS_OK;
 }
 
@@ -1141,6 +1147,9 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
       return GCS_OK;
     case GCS_DEBUG_INJECT_SCAN_FAIL:
       c->inject_scan_fail = value ? 1 : 0;
+      return GCS_OK;
+    case GCS_DEBUG_POINT_KERNEL:
+      c->legacy_points = value != 0;
       return GCS_OK;
     case GCS_DEBUG_LAUNCH_GATE:
       if (value < -1 || value > 1) return fail(c, GCS_ERR_ARG, "launch gate: -1, 0 or 1");

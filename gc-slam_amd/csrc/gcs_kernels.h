@@ -153,8 +153,9 @@ hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_
 int points_blocks(long cap, bool scale);  // k_points grid (lanes per point in scale mode)
 int points_max_blocks();
 hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err, hipStream_t s);
+// legacy: the round-3 k_points (scale mode) instead of k_points_lean
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
-                         hipEvent_t e0, hipEvent_t e1);
+                         hipEvent_t e0, hipEvent_t e1, bool legacy = false);
 int scan_tiles(int n_bins);
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 // Bins per k_bins_scale tile: 64 (four lanes per bin); GCSLAM_BIN_TILE=32 selects 32-bin tiles with

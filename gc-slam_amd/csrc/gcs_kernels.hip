@@ -572,6 +572,231 @@ void k_points(PointKernelArgs a, double* partials) {
   store_partials<5>(v, partials, blockIdx.x);
 }
 
+// ---------------------------------------------------------------- row 1+3+5, scale mode: the lean point kernel
+// The same per-point arithmetic as k_points<true, KC, 1> (bitwise the same records, buckets, flags
+// and partial rows), laid out for occupancy and for the XCDs' L2s:
+//  * registers: the budget rows are folded into two doubles as soon as they land, the nearest-bin
+//    batch loads x, y, z only (24 B per id), the candidate directions arrive in groups of CG and the
+//    candidate ids are not kept past their loads (the rare first-arrival flag marking re-reads the
+//    kNN row), so the kernel fits 128 VGPRs: four waves per SIMD, the whole C3 grid (1,024 blocks)
+//    resident in one round instead of four rounds at one wave per SIMD;
+//  * XCD-aware block order: blocks are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md,
+//    "Workgroup dispatch"), so block b computes logical block (b % 8) * (grid / 8) + b / 8: each XCD
+//    takes one contiguous eighth of the scan (an azimuth sector), and the atlas rows that sector
+//    touches (cube-cell pools, bin directions, kNN rows) are fetched into one L2 instead of all
+//    eight.  Partial rows are stored at the logical block index: the fold order is unchanged.
+#ifndef GCS_LEAN_CG
+#define GCS_LEAN_CG 8  // candidate direction loads in flight per group
+#endif
+#ifndef GCS_LEAN_XCD
+#define GCS_LEAN_XCD 1  // XCD-aware block order (0: identity, for A/B)
+#endif
+#ifndef GCS_LEAN_EG
+#define GCS_LEAN_EG 4  // candidate exps interleaved per group (registers)
+#endif
+template <int KC>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+void k_points_lean(PointKernelArgs a, double* partials) {
+  // one point per thread (the grid covers cap: points_blocks); no grid-stride loop, so nothing
+  // loop-invariant is hoisted into registers across the point's chain
+  constexpr int CG = KC < GCS_LEAN_CG ? KC : GCS_LEAN_CG;
+  static_assert(KC % CG == 0, "candidate groups");
+  __shared__ double lds[kWaves * 5];
+  __shared__ double s_mass[2];
+  const int nb = (int)gridDim.x;
+  const int lb = (!GCS_LEAN_XCD || (nb & 7)) ? (int)blockIdx.x
+                                             : (int)(blockIdx.x & 7u) * (nb >> 3) + (int)(blockIdx.x >> 3);
+  static_assert(kBlock * 4 >= 1024, "k_budget launches at most 1024 blocks: four rows per thread");
+  double2 brow[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = threadIdx.x + k * kBlock;
+    brow[k] = r < a.budget_blocks ? *(const double2*)(a.budget_partials + (size_t)r * pstride<2>())
+                                  : make_double2(0.0, 0.0);
+  }
+  const int i = lb * kBlock + (int)threadIdx.x;
+  const bool live = i < a.cap;
+  const bool valid = live && i < a.n_sel;
+  double p[3] = {0.0, 0.0, 0.0}, t = 0.0, w_raw = 0.0;
+  if (valid) {
+    const size_t src = (size_t)i * (size_t)a.stride;
+    if (a.xyz_f64) {
+      const double* rec = (const double*)(a.xyz + src * (size_t)a.point_step);
+      p[0] = rec[0]; p[1] = rec[1]; p[2] = rec[2];
+    } else {
+      const float* rec = (const float*)(a.xyz + src * (size_t)a.point_step);
+      p[0] = (double)rec[0]; p[1] = (double)rec[1]; p[2] = (double)rec[2];
+    }
+    t = a.timestamps[src];
+    w_raw = a.weights[src];
+  }
+  // the budget rows landed before the point's loads: two doubles from here on
+  double bsum[2] = {0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    bsum[0] += brow[k].x;
+    bsum[1] += brow[k].y;
+  }
+  double p0[3], d[3], win;
+  {
+    double xi[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) xi[k] = a.xi_dev ? a.xi_dev[k] : a.xi[k];
+    const double denom = a.t1 - a.t0 > 1e-12 ? a.t1 - a.t0 : 1e-12;
+    const double alpha = (t - a.t0) / denom;
+    deskew_point(alpha, xi, p, p0);
+    win = smooth_window(t, a.t0, a.t1, kTimeWarpSigmaFrac * denom);
+    ray_dir(p0[0], p0[1], p0[2], a.origin, d);
+  }
+  int nearest = 0;
+  // exact nearest atlas bin (k_points: first maximum in reference-id order over the cube cell's
+  // nearest-first pool, stopped once no later entry can reach the best dot)
+  if (!(d[0] == 0.0 && d[1] == 0.0 && d[2] == 0.0)) {
+    const size_t prow = (size_t)cube_cell(d[0], d[1], d[2], a.grid) * a.pool_width;
+    const int4* pool = (const int4*)(a.pools + prow);
+    const float* pbound = a.pool_bound + prow;
+    const int nq = a.pool_width >> 2;
+    double best = -INFINITY;
+    for (int q = 0; q < nq; q += 2) {
+      const int4 u0 = pool[q];
+      const int4 u1 = q + 1 < nq ? pool[q + 1] : make_int4(-1, -1, -1, -1);
+      const float bnext = q + 2 < nq ? pbound[4 * (q + 2)] : -2.0f;
+      const int ids[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+      double s[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double* bp = a.bin_dirs + 4 * (size_t)(ids[u] >= 0 ? ids[u] : 0);
+        const double2 xy = *(const double2*)bp;
+        const double sv = dot3_exact(d[0], d[1], d[2], xy.x, xy.y, bp[2]);
+        s[u] = ids[u] >= 0 ? sv : -INFINITY;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (s[u] > best) {
+          best = s[u];
+          nearest = ids[u];
+        } else if (s[u] == best && ids[u] >= 0 && a.bin_ref[ids[u]] < a.bin_ref[nearest]) {
+          nearest = ids[u];
+        }
+      }
+      if (u1.w < 0 || (double)bnext < best) break;
+    }
+  }
+  double e[KC];
+  double m = -INFINITY;
+  {
+    const int* krow = a.knn + (size_t)nearest * KC;
+#pragma unroll
+    for (int k0 = 0; k0 < KC; k0 += CG) {
+      int cid[CG];
+#pragma unroll
+      for (int k = 0; k < CG; k += 4) {
+        const int4 c4 = *(const int4*)(krow + k0 + k);
+        cid[k] = c4.x; cid[k + 1] = c4.y; cid[k + 2] = c4.z; cid[k + 3] = c4.w;
+      }
+      // a later group's direction loads wait for the previous group's dots (the compiler would
+      // otherwise issue all KC loads at once: 6 KC registers in flight)
+      if (k0 > 0)
+#pragma unroll
+        for (int k = 0; k < CG; ++k) __asm__ volatile("" : "+v"(cid[k]) : "v"(m));
+      double3 bd[CG];
+#pragma unroll
+      for (int k = 0; k < CG; ++k) {
+        const double* bp = a.bin_dirs + 4 * (size_t)cid[k];
+        const double2 xy = *(const double2*)bp;
+        bd[k] = make_double3(xy.x, xy.y, bp[2]);
+      }
+#pragma unroll
+      for (int k = 0; k < CG; ++k) {
+        e[k0 + k] = dot3_exact(d[0], d[1], d[2], bd[k].x, bd[k].y, bd[k].z);
+        m = fmax(m, e[k0 + k]);
+      }
+      if (CG < KC) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  const double inv_tau = 1.0 / a.tau;
+  double Z = 0.0, sxe = 0.0;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const double x = (e[k] - m) * inv_tau;
+    e[k] = exp(x);
+    Z += e[k];
+    sxe += x * e[k];
+    if ((k & (GCS_LEAN_EG - 1)) == GCS_LEAN_EG - 1) __builtin_amdgcn_sched_barrier(0);  // bound the exps in flight
+  }
+  const double iz = 1.0 / Z;
+  double corr = 0.0, rm = 0.0;
+#pragma unroll
+  for (int k = 0; k < KC; ++k) {
+    const double r = e[k] * iz;
+    corr += r * __builtin_amdgcn_rcp(r + kEpsMass);
+    rm = fmax(rm, r);
+  }
+  const double H = log(Z) - sxe * iz - kEpsMass * corr;
+  if (valid) {
+    const uint32_t sl = atomicAdd(a.counts + nearest, 1u);
+    if (a.members) {
+      if (sl < (uint32_t)a.capb) a.members[(size_t)nearest * a.capb + sl] = (uint32_t)i;
+      else *a.overflow = 1u;
+      if (sl == 0u) {  // first arrival: mark the candidate bins and their tiles active
+        const int ts = a.tile_shift;
+        uint8_t* tf = a.flags + a.n_bins;
+        const int* krow = a.knn + (size_t)nearest * KC;
+        for (int k = 0; k < KC; k += 4) {
+          const int4 c4 = *(const int4*)(krow + k);
+          a.flags[c4.x] = 1; tf[c4.x >> ts] = 1;
+          a.flags[c4.y] = 1; tf[c4.y >> ts] = 1;
+          a.flags[c4.z] = 1; tf[c4.z >> ts] = 1;
+          a.flags[c4.w] = 1; tf[c4.w >> ts] = 1;
+        }
+      }
+    } else {
+      a.slots[i] = sl;
+    }
+  }
+  if (live && !a.members) a.keys[i] = valid ? (uint32_t)nearest : (uint32_t)a.n_bins;
+  // the budget fold (block-uniform)
+  block_sum<2>(bsum, lds);
+  if (threadIdx.x == 0) {
+    s_mass[0] = bsum[0];
+    s_mass[1] = bsum[0] / (bsum[1] + kEpsMass);  // mass_scale, point_budget.py:80-84
+    if (lb == 0) {
+      a.scalars[SC_MASS_IN] = bsum[0];
+      a.scalars[SC_MASS_SEL] = bsum[1];
+      a.scalars[SC_MASS_SCALE] = s_mass[1];
+    }
+  }
+  __syncthreads();
+  const double mass_scale = s_mass[1], mass_in = s_mass[0];
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sum w_budget, sum wn^2, sum w_out, sum H
+  double rmax = -INFINITY;
+  if (live) {
+    const double wb = w_raw * mass_scale;
+    const double wout = wb * win;
+    PointRec pr;
+    pr.x = p0[0]; pr.y = p0[1]; pr.z = p0[2];
+    pr.dx = d[0]; pr.dy = d[1]; pr.dz = d[2];
+    pr.m = m; pr.wz = wout * iz;
+    a.recs[i] = pr;
+    if (a.t_out) a.t_out[i] = t;
+    if (a.iz_out) a.iz_out[i] = iz;
+    if (a.p0_out) { a.p0_out[3 * (size_t)i] = p0[0]; a.p0_out[3 * (size_t)i + 1] = p0[1]; a.p0_out[3 * (size_t)i + 2] = p0[2]; }
+    if (a.w_out) a.w_out[i] = wout;
+    if (a.w_budget_out) a.w_budget_out[i] = wb;
+    if (a.nearest_out) a.nearest_out[i] = nearest;
+    const double wn = wb / (mass_in + kEpsMass);
+    acc[0] = 0.0 + wb;
+    acc[1] = 0.0 + wn * wn;
+    acc[2] = 0.0 + wout;
+    acc[3] = 0.0 + H;
+    rmax = fmax(rmax, rm);
+  }
+  block_sum<4>(acc, lds);
+  rmax = block_max(rmax, lds);
+  double v[5] = {acc[0], acc[1], acc[2], acc[3], rmax};
+  store_partials<5>(v, partials, lb);
+}
+
 // ---------------------------------------------------------------- deterministic bucketing by nearest bin
 // k_points took an arrival slot per point (atomic per-bucket counts).  k_scan: start[] =
 // exclusive scan of the counts in one pass (decoupled look-back over 4096-bucket tiles, one
@@ -2183,10 +2408,18 @@ int points_blocks(long cap, bool scale) {
 }
 
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
-                         hipEvent_t e0, hipEvent_t e1) {
+                         hipEvent_t e0, hipEvent_t e1, bool legacy) {
   // without the fold (it rides in k_bins_scale's block 0) the stage ends with k_points itself
   hipEvent_t ek = fold ? nullptr : e1;
-  if (scale) {
+  // legacy: the round-3 point kernel (one wave per SIMD; GCSLAM_POINTS=legacy / GCS_DEBUG_POINT_KERNEL), for A/B
+  if (scale && !legacy && kPointLanes == 1 && (long)nblk * kBlock >= (long)a.cap) {  // one point per thread
+    switch (a.k) {
+      case 8: hipExtLaunchKernelGGL((k_points_lean<8>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
+      case 16: hipExtLaunchKernelGGL((k_points_lean<16>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
+      case 32: hipExtLaunchKernelGGL((k_points_lean<32>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (scale) {
     switch (a.k) {
       case 8: hipExtLaunchKernelGGL((k_points<true, 8, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
       case 16: hipExtLaunchKernelGGL((k_points<true, 16, kPointLanes>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;

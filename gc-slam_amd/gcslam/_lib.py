@@ -98,6 +98,7 @@ RCCL_ID_BYTES = 128
 DEBUG_SCAN_SPIN_LIMIT, DEBUG_INJECT_SCAN_FAIL = 1, 2
 DEBUG_SORTED_BUCKETS, DEBUG_BUCKET_CAPACITY = 3, 4
 DEBUG_LAUNCH_GATE = 5
+DEBUG_POINT_KERNEL = 6
 MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 

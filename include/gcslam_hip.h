@@ -216,6 +216,9 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * -1 (fault test) never opens the gate, so the gate kernel runs into its timeout and the scan returns
  * GCS_ERR_HIP. */
 #define GCS_DEBUG_LAUNCH_GATE 5
+/* GCS_DEBUG_POINT_KERNEL != 0: scale-mode scans run the round-3 point kernel (one wave per SIMD)
+ * instead of k_points_lean (same arithmetic, bitwise the same outputs; A/B and its parity test). */
+#define GCS_DEBUG_POINT_KERNEL 6
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*GCS_N_STAGES*/, int64_t* counts /*GCS_N_STAGES*/,
                         int32_t reset);

@@ -10,6 +10,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BENCH = os.path.join(ROOT, "bench.py")
 
@@ -37,6 +39,38 @@ def test_launcher_spawns_two_gloo_ranks_and_payload_sums_match():
     assert ranks[0]["pid"] != ranks[1]["pid"]  # two processes, not one
     assert d["payload_sum_check"] and d["payload_sum_max_abs_err"] == 0.0
     assert ranks[0]["Q_sum"] == ranks[1]["Q_sum"]  # the applied sum gives every rank the same Q
+
+
+@pytest.mark.parametrize("map_mode", ["own", "shared"])
+def test_launcher_eight_gloo_ranks(map_mode):
+    """The C4 layout (8 hypotheses, one rank each) rehearsed on CPU: eight processes, each pinned
+    to its share of the job's CPUs, the summed payload equal to the sum of the eight payloads, every
+    rank applying the same Q, and (shared map) the lead's record reaching every rank bit for bit."""
+    r = _run(["--cpu-rehearsal", "--gpus", "8", "--map-mode", map_mode, "--steps", "4", "--warmup", "1"], timeout=420)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _line(r.stdout)
+    assert d["n_gpus"] == 8 and d["transport"] == "gloo"
+    ranks = d["ranks"]
+    assert [x["rank"] for x in ranks] == list(range(8))
+    assert len({x["pid"] for x in ranks}) == 8
+    assert d["payload_sum_check"]
+    assert len({x["Q_sum"] for x in ranks}) == 1
+    if map_mode == "shared":
+        assert all(x["map_record_ok"] for x in ranks)
+    # each rank pinned itself (or says why not); with >= 16 CPUs the shares are disjoint
+    aff = [x["affinity"] for x in ranks]
+    assert all("how" in a for a in aff)
+    if len(os.sched_getaffinity(0)) >= 16:
+        sets = [set(_cpus(a["cpus"])) for a in aff]
+        assert sum(len(s) for s in sets) == len(set().union(*sets))
+
+
+def _cpus(s):
+    out = []
+    for part in s.split(","):
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
 
 
 def test_single_rank_rehearsal_is_unchanged():

@@ -330,6 +330,34 @@ def test_direct_buckets_match_sorted_bitwise(capacity):
         assert np.array_equal(ca, cb)
 
 
+@pytest.mark.parametrize("B,cap,n_raw,k", [(20000, 8192, 8192, 16), (20000, 8192, 12345, 8), (60000, 65536, 65536, 16),
+                                            (2000, 4096, 4096, 16), (20000, 3000, 9000, 32)])
+def test_lean_point_kernel_matches_legacy_bitwise(B, cap, n_raw, k):
+    """k_points_lean (one point per thread, 128 registers, XCD-ordered blocks, partial rows at the
+    logical block) against the round-3 k_points (GCS_DEBUG_POINT_KERNEL): the same per-point
+    arithmetic, so over three consecutive scans the ScanBinStats, the map, the posterior and the
+    certificate vector agree bit for bit -- grids that are and are not multiples of 8 blocks, strided
+    budgets, overflowing buckets (B = 2000) and K = 8 / 32."""
+    from gcslam import _lib as L
+    syn = _synthetic()
+    outs = []
+    for legacy in (False, True):
+        ctx = _ctx(n_bins=B, n_points_cap=cap, mode="scale", k_cand=k)
+        ctx.set_debug(L.DEBUG_POINT_KERNEL, int(legacy))
+        res = []
+        for s in range(3):
+            sc = syn.make_scan(16 * ((n_raw + 15) // 16), 31 + s)
+            rec, t, w = device_scan(sc)
+            o = ctx.scan(rec, 16, t, w, n_raw, **scan_kwargs(sc))
+            res.append((ctx.get_scan_stats(), ctx.get_map()[0], np.array(o.belief.L[:]), np.array(o.z_t[:]),
+                        np.array(o.cert[:])))
+        outs.append(res)
+        ctx.close()
+    for s in range(3):
+        for a, b in zip(outs[0][s], outs[1][s]):
+            assert np.array_equal(a, b, equal_nan=True)
+
+
 @pytest.mark.parametrize("n", [4096, 12288])
 def test_degenerate_same_direction_points(n):
     """All points on one ray (one giant bucket: ranked in-wave at 4096, compacted at 12288)
