@@ -1221,15 +1221,22 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   // (the valid-entry counter k_as_prep adds to is re-armed by the Sinkhorn kernel that reads it)
   const int nprep = (int)((p.n + pool + kAsThreads - 1) / kAsThreads);
   hipLaunchKernelGGL(k_as_prep, dim3(nprep), dim3(kAsThreads), 0, s, in, p, w, (const int8_t*)c->d_st);
+  // every return between here and the Sinkhorn's launch skips the kernel that zeroes the next
+  // call's counter: this guard zeroes it instead (the next call would otherwise start from the
+  // count of the call before this one)
+  struct RearmNext {
+    uint32_t* next;
+    bool armed = true;
+    ~RearmNext() {
+      if (armed) (void)hipMemset(next, 0, 4);
+    }
+  } rearm{mv_next};
   const int km = K <= 8 ? 8 : (K <= 16 ? 16 : 32);
   if (bad_policy) {
     uint32_t mvh = 0;
     ASCHK(c, hipMemcpyAsync(&mvh, mv, 4, hipMemcpyDeviceToHost, s));
     ASCHK(c, hipStreamSynchronize(s));
-    if (m->n_valid != 0 && mvh != 0) {
-      ASCHK(c, hipMemset(mv_next, 0, 4));  // no Sinkhorn kernel arms the next call's counter on this path
-      return as_fail(c, GCS_ERR_ARG, bad_policy);
-    }
+    if (m->n_valid != 0 && mvh != 0) return as_fail(c, GCS_ERR_ARG, bad_policy);  // rearm zeroes the next counter
     // empty: the Sinkhorn kernel's zero path writes the reference's empty result
   }
   if (bad_policy) {
@@ -1250,6 +1257,7 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
     hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   }
   ASCHK(c, hipGetLastError());
+  rearm.armed = false;  // the Sinkhorn is queued: it zeroes mv_next
   ASCHK(c, hipStreamSynchronize(s));
 #if GCS_SH_PROBE
   {

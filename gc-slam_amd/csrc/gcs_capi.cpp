@@ -643,7 +643,7 @@ int stage_pt(gcs_ctx* c, bool to_host = false) {
   StageEv ev = stage_ev(c, ST_PT);
   if (to_host) c->h_scalars[SC_COUNT] = 0.0;  // re-armed: the fold writes 1 after the mirror
   HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
-                      to_host ? c->d_scalars_mirror : nullptr, c->d_flags, c->d_touched, c->d_tickets + 1, c->stream,
+                      to_host ? c->d_scalars_mirror : nullptr, c->d_flags, c->d_touched, c->stream,
                       ev.e0, ev.e1));
   if (to_host) HIPCHK(c, hipEventRecord(c->ev_stages, c->stream));
   c->stages_done = false;
@@ -682,7 +682,12 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, 
   pa.gamma = gamma;
   StageEv ev = stage_ev(c, ST_PUSH);
   // the main stream's stages are complete once wait_mirror saw the fold's ready word (the fold is
-  // the stream's last kernel before it): only the other paths order the push stream by the event
+  // the stream's last kernel before it): only the other paths order the push stream by the event.
+  // k_tile_order (stage_tile_order) is queued on the main stream after that fold and may still run
+  // beside this pushforward: it reads d_tile_dirty / d_tile_work and writes d_tile_order, and the
+  // pushforward reads d_scan / d_flags and writes d_map / d_derived / d_touched / its partials and
+  // map-total scalars -- disjoint buffers, which the two must keep.  A fault in k_tile_order is
+  // reported by the next call that synchronises the main stream.
   if (s != c->stream && !c->stages_done) HIPCHK(ec, hipStreamWaitEvent(s, c->ev_stages, 0));
   HIPCHK(ec, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, partials, c->d_scalars, flags,
                                c->d_touched, s, ev.e0, ev.e1));

@@ -180,10 +180,9 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 // mirror (may be null): mapped host buffer that receives the whole scalar block after the fold
 // act (scan-active bin flags, null = all) and touched (bin has map mass) let k_pt and
 // k_pushforward skip bins that are zero in both the scan and the map
-// ticket: a zeroed device word; the last k_pt block folds the partial rows (and re-arms it)
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, uint32_t* ticket,
-                     hipStream_t s, hipEvent_t e0, hipEvent_t e1);
+                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
+                     hipEvent_t e0, hipEvent_t e1);
 // the next scan's bin-tile dispatch order from this scan's active tiles and their staged records
 hipError_t launch_tile_order(const uint8_t* active, const uint32_t* work, int n, int* order, hipStream_t s);
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,

@@ -405,7 +405,9 @@ void k_points(PointKernelArgs a, double* partials) {
               nearest = ids[u];  // an exact tie (measure zero): the lower reference id
             }
           }
-          if ((CH == 2 ? u1.w : u0.w) < 0 || (double)bnext < best) break;
+          // the bound is for unit directions and |d| < 1 (ray_dir divides by nrm + eps): it bounds the
+          // scaled dot of a later entry only while best > 0 (always, for any atlas of >= 48 bins)
+          if ((CH == 2 ? u1.w : u0.w) < 0 || (best > 0.0 && (double)bnext < best)) break;
         }
 #pragma unroll
         for (int off = 1; off < LP; off <<= 1) {  // first maximum in reference-id order
@@ -679,7 +681,7 @@ void k_points_lean(PointKernelArgs a, double* partials) {
           nearest = ids[u];
         }
       }
-      if (u1.w < 0 || (double)bnext < best) break;
+      if (u1.w < 0 || (best > 0.0 && (double)bnext < best)) break;  // (k_points: the bound needs best > 0)
     }
   }
   double e[KC];
@@ -1861,55 +1863,10 @@ __device__ __forceinline__ void final_epilogue(const double (&v)[NV], double* sc
   }
 }
 
-// Last-block fold (ticket != null): each block stores its partial row with sc1 stores (they leave
-// the XCD's L2), waits for them, and adds to one agent-scope ticket; the block whose add returns
-// nblocks - 1 folds every row with sc1 loads in the fixed order of k_final and runs its epilogue and
-// the host mirror, then re-arms the ticket -- no release fence (a per-block buffer_wbl2 of an L2 full
-// of the bin kernel's rows made the fenced form slower than the separate fold launch) and no second
-// kernel: the hand-off of MI355X_MICROARCH.md's sc1 table (one adder lane per workgroup after its
-// wave's vmcnt wait; every load of the rows sc1).
-template <int NV, unsigned MAXMASK>
-__device__ __forceinline__ void reduce_partials_sc1(const double* partials, int nblocks, double (&v)[NV], double* lds) {
-  constexpr int S = pstride<NV>();
-  constexpr int G = S / 4;
-  constexpr int R = kBlock / G;
-  const int c0 = 4 * (threadIdx.x % G), r0 = threadIdx.x / G;
-  double a[4] = {0.0, 0.0, 0.0, 0.0};
-  static_assert(MAXMASK == 0u, "sum-only fold");
-#pragma unroll 8
-  for (int b = r0; b < nblocks; b += R) {
-    const double* row = partials + (size_t)b * S + c0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      a[k] += __longlong_as_double((long long)__hip_atomic_load((const unsigned long long*)(row + k), __ATOMIC_RELAXED,
-                                                                __HIP_MEMORY_SCOPE_AGENT));
-  }
-#pragma unroll
-  for (int off = G; off < 64; off <<= 1)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) a[k] += __shfl_xor(a[k], off, 64);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane < G)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) lds[wid * S + c0 + k] = a[k];
-  __syncthreads();
-  double sres = 0.0;
-  if (threadIdx.x < NV) {
-    sres = lds[threadIdx.x];
-    for (int w = 1; w < kBlock / 64; ++w) sres += lds[w * S + threadIdx.x];
-  }
-  if (threadIdx.x < 64) {
-#pragma unroll
-    for (int k = 0; k < NV; ++k) v[k] = __shfl(sres, k, 64);
-  }
-  __syncthreads();
-}
-
 __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, const double* __restrict__ map,
                                                const double* __restrict__ derived, int B, double* scalars,
                                                double* partials, const uint8_t* __restrict__ act,
-                                               const uint8_t* __restrict__ touched, uint32_t* ticket,
-                                               double* mirror) {
+                                               const uint8_t* __restrict__ touched) {
   __shared__ double lds[kWaves * pstride<kPtNV>()];
   double R[9];
 #pragma unroll
@@ -1963,36 +1920,7 @@ __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, 
     v[12] += wb;
   }
   block_sum<kPtNV>(v, lds);
-  if (!ticket) {
-    store_partials<kPtNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_PT>
-    return;
-  }
-  __shared__ int s_last;
-  if (threadIdx.x == 0) {
-    double* row = partials + (size_t)blockIdx.x * pstride<kPtNV>();
-#pragma unroll
-    for (int k = 0; k < kPtNV; ++k)
-      __hip_atomic_store((unsigned long long*)(row + k), (unsigned long long)__double_as_longlong(v[k]),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = t == gridDim.x - 1 ? 1 : 0;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  double f[kPtNV];
-  reduce_partials_sc1<kPtNV, 0u>(partials, gridDim.x, f, lds);
-  if (threadIdx.x == 0) {
-    final_epilogue<kPtNV, FIN_PT>(f, scalars);
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed for the next launch
-  }
-  if (mirror) {  // as k_final: the scalar block, then the ready word behind a system fence
-    __syncthreads();
-    for (int i = threadIdx.x; i < SC_COUNT; i += kBlock) mirror[i] = scalars[i];
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) mirror[SC_COUNT] = 1.0;
-  }
+  store_partials<kPtNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_PT>
 }
 
 // ---------------------------------------------------------------- row 11: pushforward (declared)
@@ -2504,25 +2432,14 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 }
 
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, uint32_t* ticket,
-                     hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
-  // (a last-block fold in k_pt -- ticket with an agent-scope release per block -- measured slower:
-  // 16.4 vs 12.3 us at C2, 46 vs 25 us at C3; each release writes back an L2 full of the bin
-  // kernel's rows)
-  // GCSLAM_PT_FOLD=last: k_pt's last block folds (measured slower: C2 105.4-105.9 vs 103.5-104.1 us per
-  // step, planar stage 14.2 vs 14.0 us, profiles/r03/ptfold/); default: the separate k_final fold
-  static const bool last_block = [] {
-    const char* e = getenv("GCSLAM_PT_FOLD");
-    return e && strcmp(e, "last") == 0;
-  }();
-  if (last_block && nblk > 1) {
-    hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, e1, 0, scan, map, derived, B, scalars, partials,
-                          act, touched, ticket, mirror);
-  } else {
-    hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B, scalars,
-                          partials, act, touched, (uint32_t*)nullptr, (double*)nullptr);
-    GCS_FINAL_M(kPtNV, 0u, FIN_PT, nblk, s, e1, partials, scalars, mirror);
-  }
+                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
+                     hipEvent_t e0, hipEvent_t e1) {
+  // (measured slower and removed: a last-block fold in k_pt, ticket + agent-scope release per block:
+  // 16.4 vs 12.3 us at C2, 46 vs 25 us at C3; the same with sc1 stores / loads and no fence: C2
+  // 105.4-105.9 vs 103.5-104.1 us per step, profiles/r03/ptfold/)
+  hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B, scalars, partials,
+                        act, touched);
+  GCS_FINAL_M(kPtNV, 0u, FIN_PT, nblk, s, e1, partials, scalars, mirror);
   return hipGetLastError();
 }
 

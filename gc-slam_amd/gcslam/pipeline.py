@@ -438,6 +438,8 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
     updated AtlasMap (the node keeps hypothesis 0's, backend_node.py:2079-2083).  The AtlasMap is updated in
     place; a hypothesis k > 0 passes update_map=False: its scan reads the node's map and works on device
     copies of the tiles it touches (result.map is that scratch), as the reference's immutable maps behave.
+    The scratch is cached on the map_bins context and rewritten by its next update_map=False scan: such
+    a result.map is valid until then (copy it -- AtlasMap.working_copy -- to keep it longer).
     result.map_record holds the update's inputs for primitive_map_follow (one map over several GPUs)."""
     global _camera_warned
     if _camera_batch_has_content(camera_batch):
