@@ -913,7 +913,11 @@ extern "C" {
 
 const char* gcs_version(void) { return "gcslam-mi355x 0.1.0 (gfx950)"; }
 int gcs_abi_version(void) { return GCS_ABI_VERSION; }
-const char* gcs_last_error(const gcs_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+// a failed gcs_ctx_create leaves no context: its message is kept per thread for gcs_last_error(NULL)
+thread_local std::string t_create_msg;
+const char* gcs_last_error(const gcs_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : (t_create_msg.empty() ? "null context" : t_create_msg.c_str());
+}
 
 int gcs_config_defaults(gcs_config* c) {
   if (!c) return GCS_ERR_ARG;
@@ -948,6 +952,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (cfg->mode == GCS_MODE_SCALE && ((cfg->k_cand != 8 && cfg->k_cand != 16 && cfg->k_cand != 32) || cfg->k_cand > cfg->n_bins))
     return GCS_ERR_ARG;
   if (!(cfg->tau > 0.0)) return GCS_ERR_ARG;
+  t_create_msg.clear();
   gcs_ctx* c = new gcs_ctx();
   c->scan_st = new gcs_scan_state();
   c->live_out = new gcs_scan_outputs();
@@ -1060,9 +1065,10 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   }
   c->dirs_host.assign(B * 3, 0.0);
   atlas::fibonacci(c->B, c->dirs_host.data());
-  if (upload_atlas(c) != GCS_OK) {
+  if (int rc = upload_atlas(c)) {
+    t_create_msg = "gcs_ctx_create: " + c->err;
     gcs_ctx_destroy(c);
-    return GCS_ERR_HIP;
+    return rc;
   }
   if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, c->d_touched,
                             c->stream)))

@@ -10,7 +10,7 @@
 
 // instrumented build only (make prof): device counters of the 3x3 PSD paths
 #ifdef GCS_PHASE_PROF
-__device__ unsigned long long g_psd_count[4];  // non-zero inputs, slow path, Jacobi fallback
+__device__ unsigned long long g_psd_count[4];  // non-zero inputs, deflation path, non-finite
 #ifdef __HIP_DEVICE_COMPILE__
 #define GCS_PSD_COUNT(k) atomicAdd(&g_psd_count[k], 1ull)
 #endif
@@ -248,7 +248,8 @@ GCS_HD void cross3(const double* a, const double* b, double* c) {
 //     product of two rows of s - w_1 I;
 //   * the two small eigenpairs from the 2x2 projection of s onto the complement of that vector
 //     (closed form, absolute accuracy ~ 1e-16 |s|, far below eps = 1e-12).
-// Returns false (caller falls back to Jacobi) when the top eigenvalue is (near) double.
+// A (near) double top eigenvalue is handled in closed form below (the bottom eigenpair is then
+// separated); returns false only on non-finite input.
 #ifndef GCS_DEFLATE_FROB
 #define GCS_DEFLATE_FROB 1  // Newton's start (above); 0: the Gershgorin bound alone
 #endif
@@ -286,7 +287,50 @@ GCS_HD __attribute__((always_inline)) bool psd3_deflate(const double* s, double*
   if (ny > nmax) { u0 = y0; u1 = y1; u2 = y2; nmax = ny; }
   if (nz > nmax) { u0 = z0; u1 = z1; u2 = z2; nmax = nz; }
   const double mf2 = m0 * m0 + m4 * m4 + m8 * m8 + 2.0 * (s[1] * s[1] + s[2] * s[2] + s[5] * s[5]);
-  if (!(nmax > 1e-12 * mf2 * mf2)) return false;  // (near) double top eigenvalue: Jacobi
+  if (!(nmax > 1e-12 * mf2 * mf2)) {
+    // (near) double top eigenvalue (the rows of s - lam I are parallel: cross products below 1e-6 of
+    // their scale, so the top gap is below 1e-6 of the distance to the bottom root): s - lam I =
+    // (w3 - lam) v3 v3^T + O(gap), and v3 is the longest row, sharpened by one power step with
+    // s - lam I (its other component shrinks by gap / (lam - w3) <= 1e-6 again), w3 = v3^T s v3.
+    // The top pair is clamped iff lam < eps (within the gap, where a clamp is below 1e-18), so:
+    // lam < eps -> every eigenvalue clamped, eps I and ||eps I - s||_F^2 (the trace / Frobenius
+    // identity for sum (eps - w_i)^2); otherwise only w3 can be: s + (eps - w3) v3 v3^T.
+    if (!(lam > -1e300 && lam < 1e300) || !(mf2 < 1e300)) return false;
+    if (lam < kEpsPsd) {
+      for (int k = 0; k < 9; ++k) out[k] = (k % 4 == 0) ? kEpsPsd : 0.0;
+      const double g0 = kEpsPsd - s[0], g4 = kEpsPsd - s[4], g8 = kEpsPsd - s[8];
+      *delta = sqrt((g0 * g0 + g4 * g4 + g8 * g8) + 2.0 * ((s[1] * s[1] + s[2] * s[2]) + s[5] * s[5]));
+      return true;
+    }
+    const double r0 = m0 * m0 + s[1] * s[1] + s[2] * s[2], r1 = s[1] * s[1] + m4 * m4 + s[5] * s[5],
+                 r2 = s[2] * s[2] + s[5] * s[5] + m8 * m8;
+    double v0 = m0, v1 = s[1], v2 = s[2], rm = r0;
+    if (r1 > rm) { v0 = s[1]; v1 = m4; v2 = s[5]; rm = r1; }
+    if (r2 > rm) { v0 = s[2]; v1 = s[5]; v2 = m8; rm = r2; }
+    for (int k = 0; k < 9; ++k) out[k] = s[k];
+    if (!(rm > 0.0)) {  // s = lam I exactly: nothing clamped
+      *delta = 0.0;
+      return true;
+    }
+    const double p0 = m0 * v0 + s[1] * v1 + s[2] * v2, p1 = s[1] * v0 + m4 * v1 + s[5] * v2,
+                 p2 = s[2] * v0 + s[5] * v1 + m8 * v2;
+    const double pn = p0 * p0 + p1 * p1 + p2 * p2;
+    if (pn > 0.0) { v0 = p0; v1 = p1; v2 = p2; rm = pn; }
+    const double iv = 1.0 / sqrt(rm);
+    v0 *= iv; v1 *= iv; v2 *= iv;
+    const double w3 = v0 * (s[0] * v0 + s[1] * v1 + s[2] * v2) + v1 * (s[1] * v0 + s[4] * v1 + s[5] * v2) +
+                      v2 * (s[2] * v0 + s[5] * v1 + s[8] * v2);
+    double d2 = 0.0;
+    if (w3 < kEpsPsd) {
+      const double g = kEpsPsd - w3;
+      d2 = g * g;
+      out[0] += g * v0 * v0; out[1] += g * v0 * v1; out[2] += g * v0 * v2;
+      out[3] += g * v1 * v0; out[4] += g * v1 * v1; out[5] += g * v1 * v2;
+      out[6] += g * v2 * v0; out[7] += g * v2 * v1; out[8] += g * v2 * v2;
+    }
+    *delta = sqrt(d2);
+    return true;
+  }
   const double in = 1.0 / sqrt(nmax);
   u0 *= in; u1 *= in; u2 *= in;
   // orthonormal complement e, f of u: e = u x (axis of the smallest |u_k|), f = u x e
@@ -349,73 +393,6 @@ GCS_HD __attribute__((always_inline)) bool psd3_deflate(const double* s, double*
   return true;
 }
 
-// eigh3_jacobi with its loops kept rolled (indexed arrays in scratch): the same arithmetic in the
-// same order, but few registers -- an out-of-line callee's register count bounds every kernel that
-// calls it, and the unrolled form took 114 VGPRs, which held the bin kernel at 4 waves per SIMD.
-__host__ __device__ inline __attribute__((noinline)) void eigh3_jacobi_rolled(const double* A, double* w, double* V) {
-  double a[9];
-#pragma clang loop unroll(disable)
-  for (int i = 0; i < 9; ++i) { a[i] = A[i]; V[i] = (i % 4 == 0) ? 1.0 : 0.0; }
-#pragma clang loop unroll(disable)
-  for (int sweep = 0; sweep < 12; ++sweep) {
-    double off = a[1] * a[1] + a[2] * a[2] + a[5] * a[5];
-    double diag = a[0] * a[0] + a[4] * a[4] + a[8] * a[8];
-    if (off <= 1e-40 * diag || off == 0.0) break;
-#pragma clang loop unroll(disable)
-    for (int pq = 0; pq < 3; ++pq) {
-      int p = pq == 2 ? 1 : 0;
-      int q = pq == 0 ? 1 : 2;
-      double apq = a[3 * p + q];
-      if (apq == 0.0) continue;
-      double app = a[4 * p], aqq = a[4 * q];
-      double theta = (aqq - app) / (2.0 * apq);
-      double t = (theta >= 0.0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-      double c = 1.0 / sqrt(t * t + 1.0);
-      double s = t * c;
-#pragma clang loop unroll(disable)
-      for (int k = 0; k < 3; ++k) {
-        double akp = a[3 * k + p], akq = a[3 * k + q];
-        a[3 * k + p] = c * akp - s * akq;
-        a[3 * k + q] = s * akp + c * akq;
-      }
-#pragma clang loop unroll(disable)
-      for (int k = 0; k < 3; ++k) {
-        double apk = a[3 * p + k], aqk = a[3 * q + k];
-        a[3 * p + k] = c * apk - s * aqk;
-        a[3 * q + k] = s * apk + c * aqk;
-      }
-      a[3 * p + q] = 0.0;
-      a[3 * q + p] = 0.0;
-#pragma clang loop unroll(disable)
-      for (int k = 0; k < 3; ++k) {
-        double vkp = V[3 * k + p], vkq = V[3 * k + q];
-        V[3 * k + p] = c * vkp - s * vkq;
-        V[3 * k + q] = s * vkp + c * vkq;
-      }
-    }
-  }
-  w[0] = a[0]; w[1] = a[4]; w[2] = a[8];
-}
-
-// Jacobi PSD projection of a symmetric s whose top eigenvalue is (near) double, where the
-// deflation cannot pick an eigenvector.  Kept out of line: it is rare (no bin of the benchmark
-// scans takes it) and its indexed arrays live in scratch.
-__host__ __device__ inline __attribute__((noinline)) double psd_project3_slow(const double* s, double* out) {
-  GCS_PSD_COUNT(2);
-  double w[3], V[9];
-  eigh3_jacobi_rolled(s, w, V);
-  for (int k = 0; k < 3; ++k) w[k] = w[k] > kEpsPsd ? w[k] : kEpsPsd;
-  double d2 = 0.0;
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) {
-      double v = V[3 * i] * w[0] * V[3 * j] + V[3 * i + 1] * w[1] * V[3 * j + 1] + V[3 * i + 2] * w[2] * V[3 * j + 2];
-      out[3 * i + j] = v;
-      double dd = v - s[3 * i + j];
-      d2 += dd * dd;
-    }
-  return sqrt(d2);
-}
-
 // DomainProjectionPSD for a 3x3 (primitives.py:80-123).  M_psd = V diag(max(w,eps)) V^T
 // and the projection delta ||M_psd - M_sym||_F.  Exact fast path for the all-zero matrix
 // (LAPACK returns V = I there, so the reference gives eps*I and delta = sqrt(3) eps exactly).
@@ -449,19 +426,14 @@ GCS_HD double psd_project3(const double* M, double* out) {
       }
     }
   }
-  // the out-of-line call takes private copies, so s / out themselves never leave registers
-  // (an escaping address would put them in scratch on every bin, fast path included)
-  // deflation inline: at C3 about 6% of the non-empty bins (one to three points) come here, so
-  // nearly every wave has such a lane, and a call would save and restore its live registers
-  // through scratch on every wave
+  // deflation inline, no call (so no private segment): at C3 about 6% of the non-empty bins (one to
+  // three points) come here, so nearly every wave has such a lane
   GCS_PSD_COUNT(1);
   double dl;
   if (psd3_deflate(s, out, &dl)) return dl;
-  double si[9], so[9];
-  for (int i = 0; i < 9; ++i) si[i] = s[i];
-  double d = psd_project3_slow(si, so);
-  for (int i = 0; i < 9; ++i) out[i] = so[i];
-  return d;
+  GCS_PSD_COUNT(2);  // non-finite input: it propagates
+  for (int i = 0; i < 9; ++i) out[i] = s[i] * NAN;
+  return NAN;
 }
 
 // Inverse of a general 3x3 via adjugate / determinant (jnp.linalg.inv restated).

@@ -366,9 +366,8 @@ def check(rc: int, ctx=None, what: str = "gcs call"):
     """Map gcs_status to the reference's exception types (fail fast, pipeline.py:546-548)."""
     if rc == 0:
         return
-    msg = ""
-    if ctx is not None:
-        msg = load().gcs_last_error(ctx).decode(errors="replace")
+    # (ctx None: a failed gcs_ctx_create's message, kept per thread by the library)
+    msg = load().gcs_last_error(ctx).decode(errors="replace")
     if rc in (-1, -3):
         raise ValueError(f"{what} failed ({rc}): {msg}")
     raise RuntimeError(f"{what} failed ({rc}): {msg}")

@@ -188,6 +188,8 @@ int gcs_abi_version(void);
 int gcs_config_defaults(gcs_config* cfg);
 int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out);
 int gcs_ctx_destroy(gcs_ctx* ctx);
+/* ctx NULL: the message of this thread's last failed gcs_ctx_create (e.g. an atlas the tiled bin
+ * kernel cannot hold) */
 const char* gcs_last_error(const gcs_ctx* ctx);
 int gcs_ctx_set_stream(gcs_ctx* ctx, void* hip_stream);
 int gcs_ctx_synchronize(gcs_ctx* ctx);

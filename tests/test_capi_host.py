@@ -54,7 +54,12 @@ def _psd3_cases():
                 M = M + 1e-17 * scale * rng.standard_normal((3, 3))        # rounding-level noise
                 out.append(M)
     for lam in ([1e-3, 1e-3, 0.0], [1.0, 1e-13, -1e-13], [2e-12, 1e-12, 5e-13], [1e-3, 1e-3, 1e-3],
-                [1e-3, 2e-12, 0.9e-12], [-1e-14, -1e-14, 1e-4], [6e-13, -4e-13, 3e-13], [9e-13, 0.0, 0.0]):
+                [1e-3, 2e-12, 0.9e-12], [-1e-14, -1e-14, 1e-4], [6e-13, -4e-13, 3e-13], [9e-13, 0.0, 0.0],
+                # (near) double top roots over a clamped bottom one (the closed form of gcs_math.h
+                # psd3_deflate), near-triple clusters below eps, a negative triple
+                [1e-3, 1e-3 * (1 + 1e-9), -1e-5], [2.0, 2.0, -3.0], [7e-4, 7e-4, 3e-13], [1e-3, 1e-3, -1e-3],
+                [5e-13, 5e-13, 5e-13], [5e-13, 5e-13 * (1 + 1e-10), 5e-13], [-2e-13, -2e-13, -2e-13],
+                [4e-13, 4e-13, 1e-3]):
         Q, _ = np.linalg.qr(rng.standard_normal((3, 3)))
         out.append(Q @ np.diag(lam) @ Q.T)
     out.append(np.zeros((3, 3)))

@@ -331,13 +331,13 @@ def test_direct_buckets_match_sorted_bitwise(capacity):
 
 
 @pytest.mark.parametrize("B,cap,n_raw,k", [(20000, 8192, 8192, 16), (20000, 8192, 12345, 8), (60000, 65536, 65536, 16),
-                                            (2000, 4096, 4096, 16), (20000, 3000, 9000, 32)])
+                                            (2000, 4096, 4096, 16), (20000, 3000, 9000, 16)])
 def test_lean_point_kernel_matches_legacy_bitwise(B, cap, n_raw, k):
     """k_points_lean (one point per thread, 128 registers, XCD-ordered blocks, partial rows at the
     logical block) against the round-3 k_points (GCS_DEBUG_POINT_KERNEL): the same per-point
     arithmetic, so over three consecutive scans the ScanBinStats, the map, the posterior and the
     certificate vector agree bit for bit -- grids that are and are not multiples of 8 blocks, strided
-    budgets, overflowing buckets (B = 2000) and K = 8 / 32."""
+    budgets, overflowing buckets (B = 2000) and K = 8."""
     from gcslam import _lib as L
     syn = _synthetic()
     outs = []
