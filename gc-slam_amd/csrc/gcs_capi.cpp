@@ -2398,6 +2398,28 @@ int gcs_meas_iw_apply(const double* nu, const double* Psi, const double* dPsi, c
   if (cert2) { cert2[0] = c2[0]; cert2[1] = c2[1]; }
   return GCS_OK;
 }
+int gcs_debug_tile_order(int32_t device, const uint8_t* active, const uint32_t* work, int32_t n, int32_t xcd,
+                         int32_t* order) {
+  if (!active || !work || !order || n < 1) return GCS_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return GCS_ERR_HIP;
+  uint8_t* da = nullptr;
+  uint32_t* dw = nullptr;
+  int* dord = nullptr;
+  int rc = GCS_OK;
+  if (hipMalloc(&da, n) != hipSuccess || hipMalloc(&dw, n * sizeof(uint32_t)) != hipSuccess ||
+      hipMalloc(&dord, n * sizeof(int)) != hipSuccess ||
+      hipMemcpy(da, active, n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(dw, work, n * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(dord, 0xff, n * sizeof(int)) != hipSuccess ||
+      launch_tile_order_variant(da, dw, n, dord, xcd != 0, nullptr) != hipSuccess ||
+      hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(order, dord, n * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    rc = GCS_ERR_HIP;
+  if (da) (void)hipFree(da);
+  if (dw) (void)hipFree(dw);
+  if (dord) (void)hipFree(dord);
+  return rc;
+}
 int gcs_psd_project3(const double* M, double* out, double* delta) {
   if (!M || !out) return GCS_ERR_ARG;
   const double d = psd_project3(M, out);

@@ -185,6 +185,9 @@ hipError_t launch_pt(const double* scan, const double* map, const double* derive
                      hipEvent_t e0, hipEvent_t e1);
 // the next scan's bin-tile dispatch order from this scan's active tiles and their staged records
 hipError_t launch_tile_order(const uint8_t* active, const uint32_t* work, int n, int* order, hipStream_t s);
+// xcd: the XCD-grouped order (k_tile_order_xcd, n % 8 == 0), else the class order alone
+hipError_t launch_tile_order_variant(const uint8_t* active, const uint32_t* work, int n, int* order, bool xcd,
+                                     hipStream_t s);
 hipError_t launch_pushforward(const double* scan, double* map, double* derived, int B, const PushArgs& pa,
                               double* partials, double* scalars, const uint8_t* act, uint8_t* touched, hipStream_t s,
                               hipEvent_t e0, hipEvent_t e1);

@@ -2263,9 +2263,138 @@ __global__ __launch_bounds__(kOrderNT) void k_tile_order(const uint8_t* active, 
   }
 }
 
-hipError_t launch_tile_order(const uint8_t* active, const uint32_t* work, int n, int* order, hipStream_t s) {
-  hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(kOrderNT), 0, s, active, work, n, order);
+// The same classes, dealt to the 8 XCDs (blocks are dealt round-robin over them: block b runs on the
+// XCD of b % 8; MI355X_MICROARCH.md "Workgroup dispatch", for speed only).  The active tiles, in tile
+// (Hilbert) order, are cut into 8 contiguous groups of equal count, the inactive tiles likewise so
+// that every group holds n / 8 tiles; group g's tiles go to blocks g, g + 8, g + 16, ... in the class
+// order above (heaviest first, then tile order; its inactive tiles last).  Each XCD then stages the
+// records of one compact patch of the scan's coverage -- a bucket feeds ~2.3 neighbouring tiles,
+// which now share that XCD's L2 -- instead of every XCD touching the whole band.  n % 8 == 0.
+__global__ __launch_bounds__(kOrderNT) void k_tile_order_xcd(const uint8_t* active, const uint32_t* work, int n,
+                                                             int* order) {
+  constexpr int NC = kOrderClasses - 1;  // active classes
+  __shared__ uint32_t s_sum[2][kOrderNT / 64];
+  __shared__ int s_cnt[kOrderClasses][kOrderNT / 64];
+  __shared__ int s_gstart[8][NC];  // per-class prefix at each group's first active tile
+  __shared__ int s_gcnt[8][NC];    // per-group class counts
+  __shared__ uint32_t s_w[kOrderLds];
+  __shared__ uint8_t s_a[kOrderLds];
+  const bool lds = n <= kOrderLds;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  if (t < 8 * NC) {
+    (&s_gcnt[0][0])[t] = 0;
+    (&s_gstart[0][0])[t] = 0;
+  }
+  if (lds) {
+    for (int j = t; j < n; j += kOrderNT) {
+      s_a[j] = active[j];
+      s_w[j] = work[j];
+    }
+    active = s_a;
+    work = s_w;
+  }
+  __syncthreads();
+  const int chunk = (n + kOrderNT - 1) / kOrderNT;
+  const int j0 = min(n, t * chunk), j1 = min(n, j0 + chunk);
+  uint32_t ws = 0, na = 0;
+  for (int j = j0; j < j1; ++j)
+    if (active[j]) { ws += work[j]; ++na; }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    ws += (uint32_t)__shfl_xor((int)ws, off, 64);
+    na += (uint32_t)__shfl_xor((int)na, off, 64);
+  }
+  if (lane == 0) { s_sum[0][wid] = ws; s_sum[1][wid] = na; }
+  __syncthreads();
+  unsigned long long W = 0, A = 0;
+  for (int w = 0; w < kOrderNT / 64; ++w) { W += s_sum[0][w]; A += s_sum[1][w]; }
+  auto cls = [&](int j) -> int {
+    if (!active[j]) return NC;
+    const unsigned long long wa = (unsigned long long)work[j] * A;  // work / mean = wa / W
+    return 2 * wa >= 3 * W ? 0 : (wa >= W ? 1 : (2 * wa >= W ? 2 : 3));
+  };
+  // per-class exclusive prefixes at the chunk start (class NC: the inactive tiles' rank)
+  int cnt[kOrderClasses] = {0, 0, 0, 0, 0};
+  for (int j = j0; j < j1; ++j) ++cnt[cls(j)];
+  int pre[kOrderClasses];
+#pragma unroll
+  for (int c = 0; c < kOrderClasses; ++c) {
+    int x = cnt[c];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) s_cnt[c][wid] = x;
+    pre[c] = x - cnt[c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < kOrderClasses; ++c)
+    for (int w = 0; w < wid; ++w) pre[c] += s_cnt[c][w];
+  const int nq = n >> 3;                     // tiles per group
+  const int Ai = (int)A;
+  auto gbound = [&](int g) { return (int)(((long long)g * Ai + 7) / 8); };  // first active rank of group g
+  // pass 2: each group's class counts, and the class prefixes at its first active tile
+  {
+    int P[kOrderClasses];
+#pragma unroll
+    for (int c = 0; c < kOrderClasses; ++c) P[c] = pre[c];
+    for (int j = j0; j < j1; ++j) {
+      const int c = cls(j);
+      if (c < NC) {
+        const int r = P[0] + P[1] + P[2] + P[3];  // active rank
+        const int g = (int)((8LL * r) / Ai);
+        if (r == gbound(g))
+#pragma unroll
+          for (int cc = 0; cc < NC; ++cc) s_gstart[g][cc] = P[cc];
+        atomicAdd(&s_gcnt[g][c], 1);
+      }
+      ++P[c];
+    }
+  }
+  __syncthreads();
+  // pass 3: positions
+  {
+    int P[kOrderClasses];
+#pragma unroll
+    for (int c = 0; c < kOrderClasses; ++c) P[c] = pre[c];
+    for (int j = j0; j < j1; ++j) {
+      const int c = cls(j);
+      int g, pos;
+      if (c < NC) {
+        const int r = P[0] + P[1] + P[2] + P[3];
+        g = (int)((8LL * r) / Ai);
+        pos = P[c] - s_gstart[g][c];
+        for (int cc = 0; cc < c; ++cc) pos += s_gcnt[g][cc];
+      } else {
+        // inactive rank q: group g holds ranks [g nq - gbound(g), (g + 1) nq - gbound(g + 1))
+        const int q = P[NC];
+        g = 0;
+        while (g < 7 && q >= (g + 1) * nq - gbound(g + 1)) ++g;
+        pos = (gbound(g + 1) - gbound(g)) + (q - (g * nq - gbound(g)));
+      }
+      order[8 * pos + g] = j;
+      ++P[c];
+    }
+  }
+}
+
+hipError_t launch_tile_order_variant(const uint8_t* active, const uint32_t* work, int n, int* order, bool xcd,
+                                     hipStream_t s) {
+  if (xcd && (n & 7) == 0)
+    hipLaunchKernelGGL(k_tile_order_xcd, dim3(1), dim3(kOrderNT), 0, s, active, work, n, order);
+  else
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(kOrderNT), 0, s, active, work, n, order);
   return hipGetLastError();
+}
+hipError_t launch_tile_order(const uint8_t* active, const uint32_t* work, int n, int* order, hipStream_t s) {
+  // GCSLAM_TILE_XCD=0: the round-3 order (classes only), for A/B
+  static const bool xcd = [] {
+    const char* e = getenv("GCSLAM_TILE_XCD");
+    return !(e && atoi(e) == 0);
+  }();
+  return launch_tile_order_variant(active, work, n, order, xcd, s);
 }
 
 // ---------------------------------------------------------------- launchers

@@ -242,6 +242,7 @@ _SIGS = [
     ("gcs_spd_inverse_lifted", C.c_int, [C.c_int32, c_double_p, C.c_double, c_double_p]),
     ("gcs_svd3", C.c_int, [c_double_p, c_double_p, c_double_p, c_double_p]),
     ("gcs_psd_project3", C.c_int, [c_double_p, c_double_p, c_double_p]),
+    ("gcs_debug_tile_order", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
     ("gcs_mf_rotation", C.c_int, [c_double_p, c_double_p]),
     ("gcs_predict_diffusion", C.c_int, [C.POINTER(GcsBelief), c_double_p, C.c_double, C.POINTER(GcsBelief),
                                         c_double_p]),

@@ -328,6 +328,10 @@ int gcs_svd3(const double* H, double* U, double* s, double* V);
  * and Cholesky fast paths, clamped-eigenpair deflation, Jacobi fallback), host build of the same
  * code; delta = ||M_psd - M_sym||_F. */
 int gcs_psd_project3(const double* M /*3x3*/, double* M_psd /*3x3*/, double* delta);
+/* Test entry: the bin kernel's tile dispatch order for per-tile active flags and staged-record counts
+ * (n tiles; xcd != 0: grouped per XCD, n % 8 == 0), computed on `device` into order[n]. */
+int gcs_debug_tile_order(int32_t device, const uint8_t* active, const uint32_t* work, int32_t n, int32_t xcd,
+                         int32_t* order);
 /* det-fixed Matrix-Fisher rotation R = U diag(1,1,det(UV^T)) V^T of H (matrix_fisher_evidence.py:215-222):
  * the same routine the device fold runs (polar Newton, SVD for reflections / rank deficiency) */
 int gcs_mf_rotation(const double* H /*3x3*/, double* R /*3x3*/);
