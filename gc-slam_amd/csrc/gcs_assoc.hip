@@ -608,8 +608,72 @@ __device__ __forceinline__ void recency_rows(const AsParams& p, const AsWork& w,
 enum CertSlot : int {
   CE_DEFECT_A, CE_DEFECT_B, CE_MASS_TOTAL, CE_SUM_A, CE_SUM_B, CE_SUM_M, CE_SUM_NOVEL, CE_P95_A, CE_P95_B,
   CE_NONZERO_A, CE_NONZERO_B, CE_B_P95, CE_ESS, CE_MASS_EPS, CE_TOTAL_COST, CE_SUPPORT, CE_EXACT, CE_MVALID,
+  CE_CAND_TILES, CE_CAND_PRIMS, CE_CAND_PRIMS_P95,
   CE_COUNT
 };
+static_assert(CE_COUNT == GCS_ASSOC_CERT_LEN, "certificate slots");
+
+// The map branch's candidate statistics of the MapUpdateCert (pipeline.py:879-905) from the selected
+// candidates: per valid measurement row, the candidates whose view entry is valid (count) and their
+// distinct tile ids other than -1; the means of both over the valid rows (denominator max(rows,
+// eps_mass)) and the p95 order statistic of the counts with invalid rows at -1 (jnp.sort, index
+// min(int(0.95 n), n - 1)).  Every sum is of small integers, so the values are exact in any order; one
+// workgroup, LDS integer counters.  e_of(q): the view entry of candidate q.
+template <int NT, class EOF_>
+__device__ __forceinline__ void cand_stats(const AsIn& in, const AsParams& p, double eps_mass, EOF_ e_of, double* cert) {
+  __shared__ unsigned long long s_cs[3];  // valid rows, sum counts, sum distinct tiles
+  __shared__ uint32_t s_ch[33];            // histogram of the valid rows' counts (K <= 32)
+  const int t = threadIdx.x, K = p.k, N = p.n;
+  if (t < 3) s_cs[t] = 0ull;
+  if (t < 33) s_ch[t] = 0u;
+  __syncthreads();
+  uint32_t nv = 0, sc = 0, sd = 0;
+  const bool no_view = (long long)p.n_tiles * p.m_view <= 0;  // no entry to index: nothing valid
+  for (int r = t; r < N; r += NT) {
+    if (!in.valid[r]) continue;
+    int cnt = 0, dist = 0;
+    for (int k = 0; k < K && !no_view; ++k) {
+      const int e = e_of((size_t)r * K + k);
+      if (!in.vvalid[e]) continue;
+      ++cnt;
+      const long long tile = (long long)in.vtile[e];
+      if (tile == -1) continue;
+      bool seen = false;
+      for (int k2 = 0; k2 < k; ++k2) {
+        const int e2 = e_of((size_t)r * K + k2);
+        seen = seen || (in.vvalid[e2] && (long long)in.vtile[e2] == tile);
+      }
+      dist += seen ? 0 : 1;
+    }
+    ++nv;
+    sc += (uint32_t)cnt;
+    sd += (uint32_t)dist;
+    atomicAdd(&s_ch[cnt], 1u);
+  }
+  atomicAdd(&s_cs[0], (unsigned long long)nv);
+  atomicAdd(&s_cs[1], (unsigned long long)sc);
+  atomicAdd(&s_cs[2], (unsigned long long)sd);
+  __syncthreads();
+  if (t == 0) {
+    double tiles = 0.0, prims = 0.0, p95 = 0.0;
+    const unsigned long long nvalid = s_cs[0];
+    if (nvalid > 0 && N > 0) {
+      const double den = fmax((double)nvalid, eps_mass);
+      tiles = (double)s_cs[2] / den;
+      prims = (double)s_cs[1] / den;
+      const long long i95 = std::min((long long)(0.95 * (double)N), (long long)N - 1);
+      long long at = (long long)N - (long long)nvalid;  // the -1 entries sort first
+      p95 = -1.0;
+      for (int c = 0; c <= K && at <= i95; ++c) {
+        at += s_ch[c];
+        if (at > i95) p95 = (double)c;
+      }
+    }
+    cert[CE_CAND_TILES] = tiles;
+    cert[CE_CAND_PRIMS] = prims;
+    cert[CE_CAND_PRIMS_P95] = p95;
+  }
+}
 
 // The scaling updates' arithmetic (the Sinkhorn loop is VALU-bound on one CU: ~600 f64 operations
 // per thread and iteration at two waves per SIMD).  gcs_math.h's log_short / exp_short with the
@@ -688,8 +752,10 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
       if (o.slot) o.slot[q] = 0;
     }
     for (int q = t; q < N; q += kShThreads) o.rmass[q] = 0.0;
-    if (t < CE_COUNT) o.cert[t] = t == CE_EXACT ? 1.0 : (t == CE_MVALID ? (double)*w.mvalid : 0.0);
+    if (t < CE_CAND_TILES) o.cert[t] = t == CE_EXACT ? 1.0 : (t == CE_MVALID ? (double)*w.mvalid : 0.0);
     if (t == 0) *w.mvalid_next = 0u;  // the next call's counter, armed (no per-call memset)
+    // the empty result selects view entry 0 for every candidate (the outputs above)
+    cand_stats<kShThreads>(in, p, p.eps_mass, [](size_t) { return 0; }, o.cert);
     return;
   }
   if (blockIdx.x == 1) {
@@ -725,6 +791,10 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
       o.cert[CE_P95_A] = p95_a;
       o.cert[CE_B_P95] = p95_b_row;
     }
+    // this workgroup ends well inside workgroup 0's iterations: the MapUpdateCert's candidate
+    // statistics ride here, with no host sync of their own
+    const int32_t* cand = w.cand;
+    cand_stats<kShThreads>(in, p, p.eps_mass, [cand](size_t q) { return (int)cand[q]; }, o.cert);
     return;
   }
   // marginal a (:412-424)

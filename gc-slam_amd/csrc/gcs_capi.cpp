@@ -972,9 +972,21 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     return false;
   };
   if (bad(hipSetDevice(cfg->device))) return GCS_ERR_HIP;
-  if (bad(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
-  c->own_stream = true;
-  if (bad(hipStreamCreateWithFlags(&c->push_stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
+  // GCSLAM_STREAM_PRIO=1: the scan stages' stream at the device's highest priority and the pushforward's
+  // at its lowest, so the next scan's front takes the CUs the previous pushforward frees (A/B knob)
+  {
+    const char* e = getenv("GCSLAM_STREAM_PRIO");
+    int lo = 0, hi = 0;
+    if (e && atoi(e) != 0 && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess) {
+      if (bad(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi))) return GCS_ERR_HIP;
+      c->own_stream = true;
+      if (bad(hipStreamCreateWithPriority(&c->push_stream, hipStreamNonBlocking, lo))) return GCS_ERR_HIP;
+    } else {
+      if (bad(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
+      c->own_stream = true;
+      if (bad(hipStreamCreateWithFlags(&c->push_stream, hipStreamNonBlocking))) return GCS_ERR_HIP;
+    }
+  }
   if (bad(hipEventCreateWithFlags(&c->ev_push, hipEventDisableTiming))) return GCS_ERR_HIP;
   if (bad(hipEventCreateWithFlags(&c->ev_stages, hipEventDisableTiming))) return GCS_ERR_HIP;
   if (const char* pm = getenv("GCSLAM_PUSH_MAIN")) c->push_main = atoi(pm) != 0;

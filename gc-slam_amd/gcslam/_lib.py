@@ -120,10 +120,11 @@ class GcsSurfelOutputs(C.Structure):
                [("center", C.c_double * 3), ("n_valid", C.c_int32), ("cert", C.c_double * 2)]
 
 
-GCS_ASSOC_CERT_LEN = 18
+GCS_ASSOC_CERT_LEN = 21
 ASSOC_CERT_FIELDS = ("marginal_defect_a", "marginal_defect_b", "transport_mass_total", "sum_a", "sum_b", "sum_m",
                      "sum_novel", "p95_a", "p95_b", "nonzero_a", "nonzero_b", "b_recency_p95", "ess_total",
-                     "mass_epsilon_ratio", "total_cost", "support_frac", "exact", "map_valid")
+                     "mass_epsilon_ratio", "total_cost", "support_frac", "exact", "map_valid",
+                     "cand_tiles_mean", "cand_prims_mean", "cand_prims_p95")
 
 
 class GcsAssocConfig(C.Structure):

@@ -93,6 +93,10 @@ class PrimitiveAssociationResult:
     candidate_slots: object        # (N, K) int64
     row_masses: object             # (N,)
     cost_matrix: object            # (N, K)
+    # this build's addition: the MapUpdateCert's candidate statistics (pipeline.py:879-905: distinct
+    # candidate tiles and valid candidates per valid measurement, their means and the counts' p95),
+    # computed by the library beside the Sinkhorn, so the pipeline needs no device round trip for them
+    candidate_stats: tuple = (0.0, 0.0, 0.0)
 
 
 def _torch():
@@ -253,7 +257,8 @@ def associate_primitives_ot(measurement_batch, map_view: AtlasMapView, config: O
     pool = int(np.asarray(map_view.tile_ids.shape)[0]) * int(map_view.m_tile_view)
     a = associator or _associator_for(N, pool, K, device)
     out, cv, exact = a.run(measurement_batch, map_view, config, eps_lift=eps_lift, eps_mass=eps_mass)
-    result = PrimitiveAssociationResult(**out)
+    result = PrimitiveAssociationResult(**out, candidate_stats=(cv["cand_tiles_mean"], cv["cand_prims_mean"],
+                                                                cv["cand_prims_p95"]))
     if exact:
         cert = CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id)
         return result, cert, ExpectedEffect(objective_name="primitive_association_ot", predicted=0.0, realized=0.0)

@@ -288,29 +288,6 @@ def _camera_batch_has_content(camera_batch):
     return True
 
 
-def _candidate_stats(batch, view, res, eps_mass):
-    """The map branch's candidate statistics for the MapUpdateCert (pipeline.py:879-905), on the device."""
-    import torch
-    valid = batch.valid_mask.to(torch.bool)
-    nv = int(valid.sum().item())
-    if nv == 0:
-        return 0.0, 0.0, 0.0
-    cp = res.candidate_pool_indices.to(torch.int64)
-    cand_valid = view.valid_mask.to(torch.bool)[cp]
-    cand_tiles = torch.where(cand_valid, res.candidate_tile_ids.to(torch.int64), torch.full_like(cp, -1))
-    cand_counts = cand_valid.to(torch.float64).sum(1)
-    ts = torch.sort(cand_tiles, dim=1).values
-    is_new = torch.cat([torch.ones_like(ts[:, :1], dtype=torch.bool), ts[:, 1:] != ts[:, :-1]], dim=1)
-    distinct = ((is_new & (ts != -1)).to(torch.float64)).sum(1)
-    vr = valid.to(torch.float64)
-    denom = max(float(vr.sum().item()), eps_mass)
-    tiles_mean = float((distinct * vr).sum().item()) / denom
-    prims_mean = float((cand_counts * vr).sum().item()) / denom
-    cs = torch.sort(torch.where(valid, cand_counts, torch.full_like(cand_counts, -1.0))).values
-    i95 = min(int(0.95 * float(cs.shape[0])), int(cs.shape[0]) - 1)
-    return tiles_mean, prims_mean, float(cs[i95].item())
-
-
 def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, rec, t, w, imu_stamps, imu_gyro,
                             imu_accel, odom_pose, odom_cov_se3, scan_start_time, scan_end_time, dt_sec, t_last_scan,
                             t_scan, Q, config: PipelineConfig, odom_twist, odom_twist_cov, scan_seq, L_ext, h_ext,
@@ -363,7 +340,9 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
                                 r_stencil_tiles_z=config.R_STENCIL_TILES_Z, scan_seq=int(scan_seq),
                                 recency_decay_lambda=config.RECENCY_DECAY_LAMBDA)
     res, c_assoc, _ = GA.associate_primitives_ot(batch, view, acfg, chart_id=CHART_ID, device=config.device)
-    cand = _candidate_stats(batch, view, res, config.eps_mass)
+    # the MapUpdateCert's candidate statistics (pipeline.py:879-905) come with the association
+    # (computed in the library beside the Sinkhorn: no device round trip here)
+    cand = res.candidate_stats
     z_lin_pose = np.array(b.z_lin_pose[:])
     vis, c_vis, _ = GA.visual_pose_evidence(res, batch, view, eps_lift=config.eps_lift, eps_mass=config.eps_mass,
                                             chart_id=CHART_ID, z_lin_pose=z_lin_pose, device=config.device)

@@ -517,13 +517,17 @@ int gcs_extract_lidar_surfels(gcs_surfel_ctx* ctx, const double* points_dev, con
  * SupportCert / InfluenceCert scalars land in cert[] (GCS_ASSOC_CERT_* slots).  An association
  * context owns the workspace for up to max_meas rows, max_pool view entries and k_assoc <= max_k
  * (<= 32; max_meas <= 2048 / 1024 / 512 for max_k <= 8 / 16 / 32). */
-#define GCS_ASSOC_CERT_LEN 18
+/* slots CAND_*: the MapUpdateCert's candidate statistics (pipeline.py:879-905: distinct candidate tiles
+ * and valid candidates per valid measurement, means over the valid rows and the counts' p95), computed
+ * beside the Sinkhorn iterations */
+#define GCS_ASSOC_CERT_LEN 21
 enum {
   GCS_ASSOC_CERT_DEFECT_A = 0, GCS_ASSOC_CERT_DEFECT_B, GCS_ASSOC_CERT_MASS_TOTAL, GCS_ASSOC_CERT_SUM_A,
   GCS_ASSOC_CERT_SUM_B, GCS_ASSOC_CERT_SUM_M, GCS_ASSOC_CERT_SUM_NOVEL, GCS_ASSOC_CERT_P95_A, GCS_ASSOC_CERT_P95_B,
   GCS_ASSOC_CERT_NONZERO_A, GCS_ASSOC_CERT_NONZERO_B, GCS_ASSOC_CERT_B_RECENCY_P95, GCS_ASSOC_CERT_ESS,
   GCS_ASSOC_CERT_MASS_EPS_RATIO, GCS_ASSOC_CERT_TOTAL_COST, GCS_ASSOC_CERT_SUPPORT_FRAC, GCS_ASSOC_CERT_EXACT,
-  GCS_ASSOC_CERT_MAP_VALID
+  GCS_ASSOC_CERT_MAP_VALID, GCS_ASSOC_CERT_CAND_TILES_MEAN, GCS_ASSOC_CERT_CAND_PRIMS_MEAN,
+  GCS_ASSOC_CERT_CAND_PRIMS_P95
 };
 enum { GCS_ASSOC_A_UNIFORM = 0, GCS_ASSOC_A_WEIGHT = 1 };  /* MeasurementMassPolicy (:40-48) */
 enum { GCS_ASSOC_B_UNIFORM = 0 };                          /* MapMassPolicy (:51-59): only UNIFORM runs */

@@ -263,3 +263,26 @@ def associate_primitives_ot(batch, view, cfg=None, eps_lift=GC_EPS_LIFT, eps_mas
                 segment_sum_k=K)
     cert["support_frac"] = float(cert["nonzero_a"]) / float(max(N, 1))
     return res, cert
+
+
+def candidate_stats(meas_valid, view_valid, candidate_pool_indices, candidate_tile_ids, eps_mass=GC_EPS_MASS):
+    """The MapUpdateCert's candidate statistics of the map branch (FS/backend/pipeline.py:879-905):
+    per measurement row the candidates whose view entry is valid, their distinct tile ids (-1
+    excluded), the means of both over the valid rows (denominator max(valid rows, eps_mass)) and the
+    p95 of the valid rows' counts with the invalid rows at -1 (sorted, index min(int(0.95 n), n - 1)).
+    Returns (tiles_mean, prims_mean, prims_p95); zeros without a valid row."""
+    valid = np.asarray(meas_valid).astype(bool)
+    if int(valid.sum()) == 0:
+        return 0.0, 0.0, 0.0
+    cp = np.asarray(candidate_pool_indices)
+    cand_valid = np.asarray(view_valid).astype(bool)[cp]
+    cand_tiles = np.where(cand_valid, np.asarray(candidate_tile_ids), -1)
+    cand_counts = cand_valid.astype(np.float64).sum(1)
+    ts = np.sort(cand_tiles, axis=1)
+    is_new = np.concatenate([np.ones((ts.shape[0], 1), bool), ts[:, 1:] != ts[:, :-1]], axis=1)
+    distinct = (is_new & (ts != -1)).astype(np.float64).sum(1)
+    vr = valid.astype(np.float64)
+    denom = max(float(vr.sum()), eps_mass)
+    cs = np.sort(np.where(valid, cand_counts, -1.0))
+    i95 = min(int(0.95 * float(cs.shape[0])), int(cs.shape[0]) - 1)
+    return float((distinct * vr).sum() / denom), float((cand_counts * vr).sum() / denom), float(cs[i95])

@@ -53,7 +53,11 @@ def _gcfg(c: OA.AssociationConfig) -> GA.AssociationConfig:
     return GA.AssociationConfig(**d)
 
 
+_VIEW_VALID = [None]
+
+
 def _run_both(batch, view, cfg):
+    _VIEW_VALID[0] = np.asarray(view["valid_mask"]).astype(bool)
     ref, rc = OA.associate_primitives_ot(batch, view, cfg)
     res, cert, eff = GA.associate_primitives_ot(_batch(batch), _view(view), _gcfg(cfg))
     torch.cuda.synchronize()
@@ -71,6 +75,10 @@ def _check(ref, rc, res, cert, eff, valid):
     np.testing.assert_allclose(g(res.row_masses), ref["row_masses"], rtol=1e-9,
                                atol=1e-12 * max(np.abs(ref["row_masses"]).max(), 1e-300))
     assert np.all(R[~valid] == 0.0)
+    # the MapUpdateCert's candidate statistics (pipeline.py:879-905), computed by the library beside the
+    # Sinkhorn, against the restatement on the device's own candidate outputs: exact (integer sums)
+    cs = OA.candidate_stats(valid, _VIEW_VALID[0], g(res.candidate_pool_indices), g(res.candidate_tile_ids))
+    assert tuple(res.candidate_stats) == cs, (res.candidate_stats, cs)
     if rc["exact"]:
         assert cert.exact and eff.predicted == 0.0
         return

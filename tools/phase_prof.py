@@ -36,7 +36,7 @@ def main():
     pc = (C.c_ulonglong * 4)()
     ctx.lib.gcs_debug_psd_count.argtypes = [C.c_void_p, C.c_int]
     assert ctx.lib.gcs_debug_psd_count(pc, 1) == 0
-    print(f"3x3 PSD over 3 scans: non-zero inputs {pc[0]}, slow path {pc[1]}, Jacobi fallback {pc[2]}")
+    print(f"3x3 PSD over 3 scans: non-zero inputs {pc[0]}, deflation path {pc[1]}, non-finite {pc[2]}")
     import re
     tb = int(re.search(r"(\d+)-bin tiles", ctx.describe()["backends"]["moment_match"]).group(1))
     nblk = (B + tb - 1) // tb
