@@ -270,6 +270,202 @@ def c3_roofline(device, steps=16, warmup=3):
     return r, roofline_chain(cfg["N"], cfg["B"], avg, label)
 
 
+def live_path_bench(device, steps=30, warmup=10):
+    """The live primitive path -- the LiDAR evidence the reference runs today (surfels, recency + atlas
+    view, OT association, visual pose evidence, fusion, step 12b; pipeline.py:778-926, 980-1011,
+    1232-1492) -- through the drop-in process_scan_single_hypothesis(..., primitive_map=) at the
+    reference's sizes (PipelineConfig defaults = constants.py: N_POINTS_CAP 8,192, m_tile 50,000, 7
+    active / stencil tiles, M_TILE_VIEW 1,024, n_surfel 1,024 + n_feat 512, k_assoc 8, 50 Sinkhorn
+    iterations), one hypothesis over consecutive synthetic scans along the trajectory (the map fills as
+    it would).  The call takes the reference's numpy inputs (its H2D included).  ms per call over the
+    timed scans, then a diagnostic pass with config.enable_timing for the stage split."""
+    import torch
+    from gcslam import synthetic, primitive_map as gpm
+    from gcslam.pipeline import (BeliefGaussianInfo, PipelineConfig, datasheet_process_noise_state,
+                                 process_noise_state_to_Q, process_scan_single_hypothesis)
+    N = 8192
+    cfg = PipelineConfig(K_HYP=1, N_POINTS_CAP=N, B_BINS=48, soft_assign_mode="dense",
+                         lidar_origin_base=tuple(synthetic.LIDAR_ORIGIN), max_raw_points=N, device=device)
+    ctx = cfg.make_context()
+    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, device=device)
+    Q = process_noise_state_to_Q(datasheet_process_noise_state())
+    n_total = warmup + steps + 10
+    scans = [synthetic.make_scan(N, k) for k in range(n_total)]
+    state = dict(belief=BeliefGaussianInfo.create_identity_prior(), seq=0)
+
+    def one(sc):
+        r = process_scan_single_hypothesis(
+            belief_prev=state["belief"], raw_points=sc["points"], raw_timestamps=sc["timestamps"],
+            raw_weights=sc["weights"], raw_ring=np.zeros(N, np.uint8), raw_tag=np.zeros(N, np.uint8),
+            imu_stamps=sc["imu_stamps"], imu_gyro=sc["imu_gyro"], imu_accel=sc["imu_accel"], odom_pose=sc["odom_pose"],
+            odom_cov_se3=sc["odom_cov_se3"], scan_start_time=sc["scan_start_time"], scan_end_time=sc["scan_end_time"],
+            dt_sec=sc["dt_sec"], t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"], Q=Q, config=cfg,
+            odom_twist=sc["odom_twist"], odom_twist_cov=sc["odom_twist_cov"], camera_batch=None,
+            scan_seq=state["seq"], primitive_map=am, map_bins=ctx)
+        state["belief"] = r.belief_updated
+        state["seq"] += 1
+        return r
+
+    for k in range(warmup):
+        one(scans[k])
+    torch.cuda.synchronize()
+    per = np.zeros(steps)
+    for i in range(steps):
+        t0 = time.perf_counter()
+        r = one(scans[warmup + i])
+        per[i] = time.perf_counter() - t0
+    # diagnostic pass: every stage synced and timed (config.enable_timing, the reference's _record_timing)
+    cfg.enable_timing = True
+    split = []
+    for k in range(warmup + steps, n_total):
+        split.append(one(scans[k]).stage_ms)
+    cfg.enable_timing = False
+    mu = r.map_update_cert
+    out = dict(ms_per_call=float(per.mean() * 1e3), ms_median=float(np.median(per) * 1e3),
+               ms_p90=float(np.percentile(per, 90) * 1e3), calls=int(steps),
+               stage_ms={k: float(np.mean([s[k] for s in split])) for k in split[0]},
+               stage_note="diagnostic pass: a device sync before each stage clock (the reference's enable_timing)",
+               sizes=dict(n_points_cap=N, m_tile=cfg.primitive_map_max_size, n_active_tiles=cfg.N_ACTIVE_TILES,
+                          n_stencil_tiles=cfg.N_STENCIL_TILES, m_tile_view=cfg.M_TILE_VIEW, n_surfel=cfg.n_surfel,
+                          n_feat=cfg.n_feat, k_assoc=cfg.k_assoc, k_sinkhorn=cfg.k_sinkhorn),
+               map_primitives=int(am.total_count), last_scan_inserted=int(mu.insert_count_total),
+               last_scan_fused=int(mu.fused_count), n_valid_measurements=int(r.measurement_batch.n_valid))
+    am.close()
+    ctx.close()
+    return out
+
+
+def primitive_path_main(args, rank, world, local_rank, pin):
+    """`--path primitive`: the live primitive path (live_path_bench's sizes) as the multi-hypothesis node
+    runs it, one hypothesis per rank: each step every rank runs process_scan_single_hypothesis on the same
+    synthetic scan and the ranks exchange the combine payload.  --map-mode shared keeps the reference's
+    one map, hypothesis 0's (backend_node.py:2036-2083): rank 0 updates the node map and broadcasts the
+    update record (gcslam.distributed.MapRecordChannel: RCCL, or gloo with --share-device); the other
+    ranks scan with update_map=False and replay the lead's record on their copy of the node map
+    (primitive_map_follow) -- with the bin path's declared one-scan lag (a follower's scan s reads the
+    map after the lead's scan s - 1, so the ranks run concurrently).  At the end every follower replays
+    the last record and the ranks compare map hashes: `map_bitwise_equal`.  --share-device puts every
+    rank on device 0 with a gloo transport (a rehearsal on one GPU; RCCL needs one GPU per rank)."""
+    import hashlib
+    import torch
+    import torch.distributed as dist
+    from gcslam import synthetic, primitive_map as gpm
+    from gcslam.distributed import HypothesisComm, MapRecordChannel, hypothesis_weights
+    from gcslam.pipeline import (BeliefGaussianInfo, PipelineConfig, datasheet_process_noise_state,
+                                 primitive_map_follow, process_noise_state_to_Q, process_scan_single_hypothesis)
+    dev = 0 if args.share_device else local_rank
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if args.share_device:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+    comm = HypothesisComm(rank, world, dev) if (world > 1 and not args.share_device) else None
+    N = 8192
+    cfg = PipelineConfig(K_HYP=world, N_POINTS_CAP=N, B_BINS=48, soft_assign_mode="dense",
+                         lidar_origin_base=tuple(synthetic.LIDAR_ORIGIN), max_raw_points=N, device=dev)
+    ctx = cfg.make_context()
+    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, device=dev)
+    shared = args.map_mode == "shared"
+    lead = rank == 0
+    chan = MapRecordChannel(cfg.n_feat + cfg.n_surfel, 1, cfg.k_assoc, dev, comm) if (shared and world > 1) else None
+    Q = process_noise_state_to_Q(datasheet_process_noise_state())
+    rng = np.random.default_rng(1000 + rank)
+    belief = BeliefGaussianInfo.create_identity_prior()
+    if rank > 0:  # SURVEY 8d: hypothesis priors perturbed by N(0, (0.05 m, 0.5 deg))
+        belief.X_anchor = np.concatenate([rng.normal(0, 0.05, 3), rng.normal(0, np.deg2rad(0.5), 3)])
+    w_iw, w_bary = (float(x[rank]) for x in hypothesis_weights(world))
+    combine = ctx.combine_call(comm.h if comm is not None else None, w_iw, w_bary)
+    n_total = args.warmup + args.steps
+    scans = [synthetic.make_scan(N, k) for k in range(n_total)]
+    st = dict(belief=belief, pending=None)
+    comb_ms, follow_ms, bcast_ms = [], [], []
+
+    def step(s):
+        if shared and not lead and st["pending"] is not None:  # the lead's update of scan s - 1
+            t0 = time.perf_counter()
+            primitive_map_follow(am, st["pending"], cfg)
+            follow_ms.append((time.perf_counter() - t0) * 1e3)
+        sc = scans[s]
+        r = process_scan_single_hypothesis(
+            belief_prev=st["belief"], raw_points=sc["points"], raw_timestamps=sc["timestamps"],
+            raw_weights=sc["weights"], raw_ring=np.zeros(N, np.uint8), raw_tag=np.zeros(N, np.uint8),
+            imu_stamps=sc["imu_stamps"], imu_gyro=sc["imu_gyro"], imu_accel=sc["imu_accel"], odom_pose=sc["odom_pose"],
+            odom_cov_se3=sc["odom_cov_se3"], scan_start_time=sc["scan_start_time"], scan_end_time=sc["scan_end_time"],
+            dt_sec=sc["dt_sec"], t_last_scan=sc["t_last_scan"], t_scan=sc["t_scan"], Q=Q, config=cfg,
+            odom_twist=sc["odom_twist"], odom_twist_cov=sc["odom_twist_cov"], camera_batch=None, scan_seq=s,
+            primitive_map=am, map_bins=ctx, update_map=(lead or not shared))
+        st["belief"] = r.belief_updated
+        if chan is not None:
+            t0 = time.perf_counter()
+            if lead:
+                chan.pack(r.map_record)
+            chan.broadcast(root=0)
+            if not lead:
+                st["pending"] = chan.unpack()
+            bcast_ms.append((time.perf_counter() - t0) * 1e3)
+        t0 = time.perf_counter()
+        if comm is not None or world == 1:
+            combine(s)
+        else:  # gloo transport of the library-packed payload (ranks sharing one device)
+            from gcslam.distributed import combine_allreduce
+            combine_allreduce(ctx, rank, world, s, want_belief=False)
+        comb_ms.append((time.perf_counter() - t0) * 1e3)
+
+    for s in range(args.warmup):
+        step(s)
+    comb_ms.clear(); follow_ms.clear(); bcast_ms.clear()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for s in range(args.warmup, n_total):
+        step(s)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el_rank = time.perf_counter() - t0
+    el = el_rank
+    if world > 1:  # the slowest rank's clock
+        tt = torch.tensor([el], dtype=torch.float64, device="cpu" if args.share_device else f"cuda:{dev}")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    if shared and not lead and st["pending"] is not None:  # catch up with the lead's last update
+        primitive_map_follow(am, st["pending"], cfg)
+    torch.cuda.synchronize()
+    h = hashlib.sha256()
+    for t in sorted(am.tile_ids):
+        for k, v in sorted(am.read_tile(int(t)).items()):
+            h.update(k.encode())
+            h.update(np.ascontiguousarray(v).tobytes())
+    med = lambda x: float(np.median(x)) if x else None  # noqa: E731
+    me = dict(rank=rank, affinity=pin, ms_per_step=el_rank / args.steps * 1e3, map_sha=h.hexdigest()[:16],
+              map_primitives=int(am.total_count), combine_ms=med(comb_ms), follow_ms=med(follow_ms),
+              record_bcast_ms=med(bcast_ms))
+    per_rank = [me]
+    if world > 1:
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, me)
+    if rank == 0:
+        line = {"metric": "live primitive path: hypothesis-scans/s (process_scan_single_hypothesis, primitive_map=)",
+                "value": world * args.steps / el, "unit": "scans/s", "n_gpus": 1 if args.share_device else world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3,
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+                "data": "synthetic (seeded VLP-16-like scans along the trajectory; numpy inputs per call)",
+                "config": {"workload": f"live path at the reference sizes, {world} hypotheses, map {args.map_mode}",
+                           "path": "primitive", "map_mode": args.map_mode, "hypotheses": world,
+                           "transport": ("gloo (shared device)" if args.share_device else "rccl") if world > 1 else None},
+                "map_bitwise_equal": len({p["map_sha"] for p in per_rank}) == 1 if shared else None,
+                "record_bytes": chan.nbytes if chan is not None else None, "per_rank": per_rank}
+        print(json.dumps(line), flush=True)
+    am.close()
+    ctx.close()
+    if comm is not None:
+        comm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def _free_port():
     import socket
     with socket.socket() as so:
@@ -417,16 +613,23 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c3", action="store_true")
+    ap.add_argument("--no-live", action="store_true", help="skip the live primitive path's timing (live_path)")
     ap.add_argument("--map-mode", default="own", choices=["own", "shared"],
                     help="own: a map per hypothesis (default); shared: one map, hypothesis 0's (rank 0 leads, "
                          "the other ranks replay its update: gcslam_hip.h GCS_MAP_FOLLOW); at one GPU the rank "
                          "follows itself, which times a follower's scan")
+    ap.add_argument("--path", default="bins", choices=["bins", "primitive"],
+                    help="bins: the 14-step bin path (the headline metric); primitive: the live primitive path "
+                         "through the drop-in, one hypothesis per rank (primitive_path_main)")
+    ap.add_argument("--share-device", action="store_true",
+                    help="--path primitive: every rank on device 0, gloo transport (a rehearsal on one GPU)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="launcher + payload exchange over gloo on CPU (test of the multi-rank path)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
-        sys.exit(launch_ranks(args.gpus, args.cpu_rehearsal))  # before any GPU call in this process
+        # before any GPU call in this process
+        sys.exit(launch_ranks(args.gpus, args.cpu_rehearsal or args.share_device))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -440,6 +643,8 @@ def main():
     pin = topology.pin_rank(local_rank, int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
     if args.cpu_rehearsal:
         return cpu_rehearsal(args, rank, world, pin)
+    if args.path == "primitive":
+        return primitive_path_main(args, rank, world, local_rank, pin)
 
     import torch
     import torch.distributed as dist
@@ -628,6 +833,8 @@ def main():
         }
         if world == 1 and args.config == "c2" and not args.no_c3:
             line["roofline_c3"], line["roofline_chain_c3"] = c3_roofline(local_rank)
+        if world == 1 and not args.no_live:
+            line["live_path"] = live_path_bench(local_rank)
         line["cpu_baseline"] = cpu_baseline(cfg) if (world == 1 and not args.no_cpu_baseline) else None
         print(json.dumps(line), flush=True)
     if comm is not None:

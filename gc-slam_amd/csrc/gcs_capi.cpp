@@ -2151,6 +2151,14 @@ int gcs_rccl_comm_destroy(void* comm) {
   return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? GCS_OK : GCS_ERR_HIP;
 }
 
+int gcs_rccl_broadcast(void* comm, void* buf, int64_t bytes, int32_t root, void* stream) {
+  if (!comm || (!buf && bytes > 0) || bytes < 0 || root < 0) return GCS_ERR_ARG;
+  if (bytes == 0) return GCS_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (ncclBroadcast(buf, buf, (size_t)bytes, ncclUint8, root, (ncclComm_t)comm, s) != ncclSuccess) return GCS_ERR_HIP;
+  return hipStreamSynchronize(s) == hipSuccess ? GCS_OK : GCS_ERR_HIP;
+}
+
 int gcs_rccl_comm_count(void* comm, int32_t* count, int32_t* user_rank) {
   if (!comm || !count || !user_rank) return GCS_ERR_ARG;
   int n = 0, r = 0;

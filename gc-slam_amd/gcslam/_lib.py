@@ -270,6 +270,7 @@ _SIGS = [
     ("gcs_rccl_comm_destroy", C.c_int, [C.c_void_p]),
     ("gcs_datasheet_noise_states", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("gcs_rccl_comm_count", C.c_int, [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    ("gcs_rccl_broadcast", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]),
     ("gcs_combine_allreduce", C.c_int, [C.c_void_p, C.c_void_p, C.c_double, C.c_double, C.c_int32, C.c_void_p,
                                         C.c_void_p]),
     ("gcs_process_iw_apply", C.c_int, [c_double_p] * 7),

@@ -16,6 +16,7 @@ Two LiDAR evidence paths behind the one signature:
 from __future__ import annotations
 
 import json
+import time
 import warnings
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
@@ -85,6 +86,10 @@ class PipelineConfig:
     camera_batch_policy: str = "warn"  # camera evidence is out of scope here: "warn" once | "raise" | "ignore"
     max_raw_points: int = 1 << 20
     device: int = 0
+    # PipelineConfig.enable_timing (pipeline.py:380-394; default off, backend_node.py:152): the live
+    # path's stages are timed with a device sync + perf_counter each, into result.stage_ms and the
+    # tape's t_*_ms fields (a diagnostic: the syncs serialise host and device)
+    enable_timing: bool = False
     # live primitive path (pipeline.py:179-211; constants.py:350-477)
     n_feat: int = 512
     n_surfel: int = 1024
@@ -176,6 +181,7 @@ class ScanPipelineResult:
     map_view: Optional[object] = None
     z_lin_pose: Optional[np.ndarray] = None
     map_record: Optional[dict] = None  # the map update's inputs (primitive_map_follow)
+    stage_ms: Optional[dict] = None    # live path, config.enable_timing: wall ms per stage (synced)
 
 
 IMU_ODOM_CERTS = (("OdomEvidenceGaussian",), ("ImuAccelDirectionTimeResolved", "TransportConsistencyWeighting"),
@@ -306,16 +312,28 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
         bufs = ctx._live_bufs = (torch.empty((cap, 3), dtype=torch.float64, device=dev),
                                  torch.empty(cap, dtype=torch.float64, device=dev),
                                  torch.empty(cap, dtype=torch.float64, device=dev))
+    stage_ms = {}
+    clock = [time.perf_counter()]
+
+    def tick(name):  # the reference's _record_timing: block until ready, then the wall clock
+        if config.enable_timing:
+            torch.cuda.synchronize(dev)
+            now = time.perf_counter()
+            stage_ms[name] = (now - clock[0]) * 1e3
+            clock[0] = now
+
     b = ctx.scan_begin(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
                        dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
                        odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
                        odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a, buffers=bufs)
+    tick("scan_begin_ms")  # budget, predict, IMU preintegration, deskew, IMU / odometry branch
     # the map branch (pipeline.py:778-926)
     scfg = SurfelExtractionConfig(n_surfel=config.n_surfel, n_feat=config.n_feat,
                                   voxel_size_m=config.surfel_voxel_size_m,
                                   min_points_per_voxel=config.surfel_min_points_per_voxel, eps_lift=config.eps_lift)
     batch, c_surf, _ = extract_lidar_surfels(bufs[0], bufs[1], bufs[2], config=scfg, chart_id=CHART_ID,
                                              device=config.device)
+    tick("surfel_extraction_ms")
     centre = np.array(b.pose_pred[:3])
     active = GPM.ma_hex_stencil_tile_ids(centre, config.H_TILE, config.R_ACTIVE_TILES_XY, config.R_ACTIVE_TILES_Z)
     stencil = GPM.ma_hex_stencil_tile_ids(centre, config.H_TILE, config.R_STENCIL_TILES_XY, config.R_STENCIL_TILES_Z)
@@ -334,12 +352,14 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
     am, c_infl, _, infl = GPM.primitive_map_recency_inflate(primitive_map, active, int(scan_seq),
                                                             config.RECENCY_DECAY_LAMBDA, config.RECENCY_MIN_SCALE)
     view = GPM.extract_atlas_map_view(am, stencil, int(config.M_TILE_VIEW), config.eps_lift, config.eps_mass)
+    tick("map_view_ms")  # recency inflation + the atlas view over the stencil
     acfg = GA.AssociationConfig(k_assoc=config.k_assoc, k_sinkhorn=config.k_sinkhorn, epsilon=config.ot_epsilon,
                                 tau_a=config.ot_tau_a, tau_b=config.ot_tau_b, eps_mass=config.eps_mass,
                                 h_tile=config.H_TILE, r_stencil_tiles_xy=config.R_STENCIL_TILES_XY,
                                 r_stencil_tiles_z=config.R_STENCIL_TILES_Z, scan_seq=int(scan_seq),
                                 recency_decay_lambda=config.RECENCY_DECAY_LAMBDA)
     res, c_assoc, _ = GA.associate_primitives_ot(batch, view, acfg, chart_id=CHART_ID, device=config.device)
+    tick("association_ms")
     # the MapUpdateCert's candidate statistics (pipeline.py:879-905) come with the association
     # (computed in the library beside the Sinkhorn: no device round trip here)
     cand = res.candidate_stats
@@ -347,6 +367,7 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
     vis, c_vis, _ = GA.visual_pose_evidence(res, batch, view, eps_lift=config.eps_lift, eps_mass=config.eps_mass,
                                             chart_id=CHART_ID, z_lin_pose=z_lin_pose, device=config.device)
     L_lidar, h_lidar = GA.build_visual_pose_evidence_22d(vis)
+    tick("visual_pose_ms")
     # the map branch's + visual certs enter all_certs (T, pipeline.py:1211); the LiDAR evidence aggregate
     # is [deskew, surfel, association, visual] (:1049-1056)
     trig = sum(c.total_trigger_magnitude() for c in (c_surf, c_infl, c_assoc, c_vis))
@@ -354,11 +375,13 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
     out = ctx.scan_finish(L_lidar, h_lidar, trig, sum(c.support.ess_total for c in lid), len(lid),
                           sum(c.mismatch.nll_per_ess for c in lid))
     z_t = np.array(out.z_t[:])
+    tick("scan_finish_ms")  # evidence sum, tempering, fusion, recompose, anchor drift
     # step 12b: the primitive map update at z_t (pipeline.py:1232-1492)
     ucfg = GPM.PrimitiveMapUpdateConfig(k_insert_tile=config.k_insert_tile, H_TILE=config.H_TILE,
                                         RECENCY_DECAY_LAMBDA=config.RECENCY_DECAY_LAMBDA, eps_lift=config.eps_lift,
                                         eps_mass=config.eps_mass, eps_psd=config.eps_psd)
     st = GPM.primitive_map_update(am, batch, res, z_t, active, float(scan_end_time), int(scan_seq), config=ucfg)
+    tick("map_update_ms")
     act = set(active)
     inactive = [int(x) for x in am.tile_ids if int(x) not in act]
     hits = len([x for x in active if int(x) in set(am.tile_ids)])
@@ -377,7 +400,7 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
     record = dict(active=[int(x) for x in active], scan_seq=int(scan_seq), t=float(scan_end_time), z_t=z_t,
                   batch=batch, association=res)
     return out, dict(map=am, batch=batch, map_update_cert=muc, certs=[c_surf, c_infl, c_assoc, c_vis],
-                     association=res, view=view, z_lin_pose=z_lin_pose, map_record=record)
+                     association=res, view=view, z_lin_pose=z_lin_pose, map_record=record, stage_ms=stage_ms)
 
 
 def primitive_map_follow(primitive_map, record: dict, config: "PipelineConfig"):
@@ -467,9 +490,19 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
         res.map_view = live["view"]
         res.z_lin_pose = live["z_lin_pose"]
         res.map_record = live["map_record"]
+        res.stage_ms = live["stage_ms"]
         res.map_bins_updated = None
     # the reference's per-scan MinimalScanTape (pipeline.py:1504-1570)
     res.diagnostics_tape = tape_from_result(res, scan_seq, scan_end_time, dt_sec, rec.shape[0], res.L_evidence)
+    sm = getattr(res, "stage_ms", None) or {}
+    if sm:  # the reference's live-path timing fields (diagnostics.py:58-67)
+        t = res.diagnostics_tape
+        t.t_surfel_extraction_ms = sm.get("surfel_extraction_ms", 0.0)
+        t.t_association_ms = sm.get("association_ms", 0.0)
+        t.t_visual_pose_ms = sm.get("visual_pose_ms", 0.0)
+        t.t_map_branch_ms = sum(sm.get(k, 0.0) for k in ("surfel_extraction_ms", "map_view_ms", "association_ms"))
+        t.t_map_update_ms = sm.get("map_update_ms", 0.0)
+        t.t_total_ms = sum(sm.values())
     if map_bins is None:
         ctx.close()
         res.map_bins_updated = None

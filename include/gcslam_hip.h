@@ -414,6 +414,11 @@ int gcs_rccl_comm_destroy(void* comm);
 /* Ranks the communicator holds (ncclCommCount) and this rank's index in it (ncclCommUserRank):
  * bench.py reports them so a multi-GPU line shows RCCL saw every rank. */
 int gcs_rccl_comm_count(void* comm, int32_t* count, int32_t* user_rank);
+/* In-place ncclBroadcast of `bytes` bytes of device memory from rank `root` on `stream` (NULL: the
+ * device's null stream), then a stream synchronize: the live primitive map's per-scan update record
+ * (gcslam.distributed.MapRecordChannel, ~0.5 MB at the reference sizes) from the lead to the ranks
+ * that replay it (backend_node.py:2079-2083). */
+int gcs_rccl_broadcast(void* comm, void* buf, int64_t bytes, int32_t root, void* stream);
 int gcs_combine_allreduce(gcs_ctx* ctx, void* comm, double w_iw, double w_bary, int32_t scan_count,
                           gcs_belief* combined_out /*may be NULL*/, double* cert4 /*may be NULL*/);
 

@@ -206,3 +206,67 @@ def test_hypothesis_weights_floor():
     from gcslam.distributed import hypothesis_weights
     w, wn = hypothesis_weights(8)
     assert np.allclose(w, 1 / 8) and np.isclose(wn.sum(), 1.0)
+
+
+def _record(rng, N, lobes, K):
+    from types import SimpleNamespace
+    import torch
+    b = SimpleNamespace(Lambdas=torch.from_numpy(rng.normal(size=(N, 3, 3))), thetas=torch.from_numpy(rng.normal(size=(N, 3))),
+                        etas=torch.from_numpy(rng.normal(size=(N, lobes, 3))), weights=torch.from_numpy(rng.random(N)),
+                        valid_mask=torch.from_numpy(rng.random(N) < 0.7), colors=torch.from_numpy(rng.random((N, 3))),
+                        sources=torch.from_numpy(rng.integers(0, 2, N).astype(np.int32)))
+    a = SimpleNamespace(responsibilities=torch.from_numpy(rng.random((N, K))),
+                        candidate_tile_ids=torch.from_numpy(rng.integers(-5, 10**12, (N, K))),
+                        candidate_slots=torch.from_numpy(rng.integers(0, 50000, (N, K))),
+                        row_masses=torch.from_numpy(rng.random(N)))
+    return dict(active=[int(x) for x in rng.integers(-10**9, 10**9, 7)], scan_seq=int(rng.integers(0, 10**6)),
+                t=float(rng.random() * 1e9), z_t=rng.normal(size=6), batch=b, association=a)
+
+
+def _rec_worker(rank, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "gc-slam_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from gcslam.distributed import MapRecordChannel
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    N, lobes, K = 1536, 1, 8
+    ch = MapRecordChannel(N, lobes, K, device=-1)
+    out = []
+    for s in range(3):  # three scans: rank 0 (the lead) packs, everyone receives the same bytes
+        rec = _record(np.random.default_rng(50 + s), N, lobes, K)
+        if rank == 0:
+            ch.pack(rec)
+        ch.broadcast(root=0)
+        got = ch.unpack()
+        ok = (got["active"] == rec["active"] and got["scan_seq"] == rec["scan_seq"] and got["t"] == rec["t"]
+              and np.array_equal(got["z_t"], rec["z_t"]))
+        for grp in ("batch", "association"):
+            for name, v in vars(rec[grp]).items():
+                g = getattr(got[grp], name).numpy()
+                ok = ok and np.array_equal(g.reshape(-1), v.numpy().reshape(-1)) and g.dtype == v.numpy().dtype
+        out.append(bool(ok))
+    q.put((rank, out, ch.nbytes))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_map_record_channel_bitwise():
+    """gcslam.distributed.MapRecordChannel over gloo (the transport of ranks without an RCCL
+    communicator of their own): the lead's live-map update record -- active tiles, scan seq / time,
+    z_t, the MeasurementBatch and association fields step 12b reads -- reaches the other rank bit for
+    bit, three scans in a row (backend_node.py:2079-2083); ~0.5 MB at the reference sizes."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rec_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    got = dict((r, (o, n)) for r, o, n in (q.get(timeout=120) for _ in range(WORLD)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got[0][0] == [True] * 3 and got[1][0] == [True] * 3
+    assert 0.4e6 < got[0][1] < 0.7e6

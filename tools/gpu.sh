@@ -3,7 +3,8 @@
 #   bash tools/gpu.sh STEP [STEP ...]
 # Steps (each under its own time limit, stopping at the first failure; outputs under $O):
 #   tests        pytest -m gpu (the parity suite)          smoke      __graft_entry__.smoke()
-#   bench        bench.py C2 headline line (+ C3 roofline + CPU baseline)
+#   bench        bench.py C2 headline line (+ C3 roofline + live path + CPU baseline)
+#   live         bench.py C2, short, with the live primitive path's timing (live_path)
 #   bench3       bench.py --config c3        benchshared  bench.py --map-mode shared (a follower's scan)
 #   hostbench    host 22-D numerics micro-benchmark (gc-slam_amd/build/host_bench)
 #   prof2/prof3  rocprofv3 --kernel-trace --stats of bench at C2 / C3
@@ -30,19 +31,20 @@ step() {
         > "$O/pytest_gpu.log" 2>&1 ;;
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
     bench) timeout -k 10 400 python bench.py > "$O/bench_c2.log" 2>&1 ;;
-    benchshared) timeout -k 10 300 python bench.py --map-mode shared --no-cpu-baseline --no-c3 > "$O/bench_shared.log" 2>&1 ;;
+    live) timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-c3 > "$O/bench_live.log" 2>&1 ;;
+    benchshared) timeout -k 10 300 python bench.py --map-mode shared --no-cpu-baseline --no-c3 --no-live > "$O/bench_shared.log" 2>&1 ;;
     hostbench) timeout -k 10 120 ./tools/host_bench tools/host_bench_in.bin > "$O/host_bench.txt" 2>&1 ;;
-    bench3) timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline \
+    bench3) timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline --no-live \
               > "$O/bench_c3.log" 2>&1 ;;
     prof2) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c2" -o run --output-format csv -- \
-             python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-c3 > "$O/prof_c2.log" 2>&1 ;;
+             python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-c3 --no-live > "$O/prof_c2.log" 2>&1 ;;
     prof3) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c3" -o run --output-format csv -- \
-             python3 bench.py --config c3 --steps 30 --warmup 5 --no-cpu-baseline > "$O/prof_c3.log" 2>&1 ;;
+             python3 bench.py --config c3 --steps 30 --warmup 5 --no-cpu-baseline --no-live > "$O/prof_c3.log" 2>&1 ;;
     pmc)
       for cfg in ${PMC_CONFIGS:-c2 c3}; do
         for ctr in FETCH_SIZE WRITE_SIZE; do
           timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "$RE" -d "$O/pmc/${cfg}_$ctr" -o run \
-            --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline --no-c3 \
+            --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline --no-c3 --no-live \
             > "$O/pmc_${cfg}_$ctr.log" 2>&1 || return $?
         done
       done ;;
@@ -50,7 +52,7 @@ step() {
       for cfg in c2 c3; do
         timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES \
           SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY --kernel-include-regex "$RE" -d "$O/sq/${cfg}" -o run \
-          --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline --no-c3 \
+          --output-format csv -- python3 bench.py --config "$cfg" --steps 10 --warmup 2 --no-cpu-baseline --no-c3 --no-live \
           > "$O/sq_$cfg.log" 2>&1 || return $?
       done ;;
     assocsq)  # SQ instruction mix / wave states of the association kernels
@@ -72,9 +74,9 @@ step() {
       for rep in $(seq 1 "${REPS:-2}"); do
         for v in A B; do
           lib=gc-slam_amd/gcslam/libgcslam_hip.so; [ $v = B ] && lib=gc-slam_amd/gcslam/libgcslam_hip_${B:-prev}.so
-          GCSLAM_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-c3 \
+          GCSLAM_LIB=$PWD/$lib timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-c3 --no-live \
             > "$O/ab_${v}_c2_$rep.log" 2>&1 || return $?
-          GCSLAM_LIB=$PWD/$lib timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline \
+          GCSLAM_LIB=$PWD/$lib timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline --no-live \
             > "$O/ab_${v}_c3_$rep.log" 2>&1 || return $?
         done
       done ;;
@@ -82,9 +84,9 @@ step() {
       for rep in $(seq 1 "${REPS:-2}"); do
         for v in A B; do
           e=""; [ $v = B ] && e="$ENVB"
-          env $e timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-c3 \
+          env $e timeout -k 10 300 python bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-c3 --no-live \
             > "$O/envab_${v}_c2_$rep.log" 2>&1 || return $?
-          env $e timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline \
+          env $e timeout -k 10 300 python bench.py --config c3 --steps 40 --warmup 5 --no-cpu-baseline --no-live \
             > "$O/envab_${v}_c3_$rep.log" 2>&1 || return $?
         done
       done ;;
@@ -94,7 +96,7 @@ step() {
         lib=gc-slam_amd/gcslam/libgcslam_hip.so; [ "$suf" != "-" ] && lib=gc-slam_amd/gcslam/libgcslam_hip_$suf.so
         e="GCSLAM_LIB=$PWD/$lib ${envs//,/ }"
         for cfg in ${SWEEP_CONFIGS:-c2 c3}; do
-          env $e timeout -k 10 300 python bench.py --config $cfg --steps ${SWEEP_STEPS:-60} --warmup 5 --no-cpu-baseline             --no-c3 > "$O/sweep_${name}_$cfg.log" 2>&1 || return $?
+          env $e timeout -k 10 300 python bench.py --config $cfg --steps ${SWEEP_STEPS:-60} --warmup 5 --no-cpu-baseline --no-c3 --no-live > "$O/sweep_${name}_$cfg.log" 2>&1 || return $?
         done
       done ;;
     *) echo "unknown step $1" >&2; return 2 ;;
