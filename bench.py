@@ -287,7 +287,10 @@ def live_path_bench(device, steps=30, warmup=10):
     cfg = PipelineConfig(K_HYP=1, N_POINTS_CAP=N, B_BINS=48, soft_assign_mode="dense",
                          lidar_origin_base=tuple(synthetic.LIDAR_ORIGIN), max_raw_points=N, device=device)
     ctx = cfg.make_context()
-    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, device=device)
+    # the reference's AtlasMap is a dict of tiles; this one preallocates: 256 tiles x 50,000 slots hold
+    # the synthetic trajectory's coverage over the run (its z hovers at a tile boundary, so the one-slab
+    # stencil alternates between two layers of tiles)
+    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, max_tiles=256, device=device)
     Q = process_noise_state_to_Q(datasheet_process_noise_state())
     n_total = warmup + steps + 10
     scans = [synthetic.make_scan(N, k) for k in range(n_total)]
@@ -365,10 +368,12 @@ def primitive_path_main(args, rank, world, local_rank, pin):
     cfg = PipelineConfig(K_HYP=world, N_POINTS_CAP=N, B_BINS=48, soft_assign_mode="dense",
                          lidar_origin_base=tuple(synthetic.LIDAR_ORIGIN), max_raw_points=N, device=dev)
     ctx = cfg.make_context()
-    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, device=dev)
+    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, max_tiles=256, device=dev)
     shared = args.map_mode == "shared"
     lead = rank == 0
-    chan = MapRecordChannel(cfg.n_feat + cfg.n_surfel, 1, cfg.k_assoc, dev, comm) if (shared and world > 1) else None
+    from gcslam.surfels import GC_VMF_N_LOBES
+    chan = (MapRecordChannel(cfg.n_feat + cfg.n_surfel, GC_VMF_N_LOBES, cfg.k_assoc, dev, comm)
+            if (shared and world > 1) else None)
     Q = process_noise_state_to_Q(datasheet_process_noise_state())
     rng = np.random.default_rng(1000 + rank)
     belief = BeliefGaussianInfo.create_identity_prior()

@@ -232,7 +232,7 @@ def _rec_worker(rank, port, q):
     import torch.distributed as dist
     from gcslam.distributed import MapRecordChannel
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
-    N, lobes, K = 1536, 1, 8
+    N, lobes, K = 1536, 3, 8  # GC_VMF_N_LOBES = 3 (constants.py:463)
     ch = MapRecordChannel(N, lobes, K, device=-1)
     out = []
     for s in range(3):  # three scans: rank 0 (the lead) packs, everyone receives the same bytes
