@@ -1143,6 +1143,9 @@ constexpr int kStageBig = GCS_STAGE_BIG, kStageSmall = 256;
 #ifndef GCS_DALL64
 #define GCS_DALL64 false  // 64-bin tiles: phase D on wave 0 (every wave measured slower in round 1)
 #endif
+#ifndef GCS_DALL128
+#define GCS_DALL128 false  // 128-bin tiles: phase D on waves 0-1, one lane per bin (true: on every wave)
+#endif
 constexpr int kStage128Big = GCS_STAGE_128_BIG, kStage128Small = GCS_STAGE_128_SMALL;
 constexpr int kStage256Big = GCS_STAGE_256_BIG, kStage256Small = GCS_STAGE_256_SMALL;
 // staged record: x y z dx dy dz m w/Z as four double2 chunks (+ GCS_REC_PAD doubles of stride
@@ -1237,7 +1240,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   constexpr int NT = TB * LANES, NW = NT / 64;
   constexpr int kMaxSrc = max_src(TB), kMaxRl = max_rl(TB);
   static_assert(LANES == 1 || LANES == 2 || LANES == 4 || LANES == 8, "phase C splits each bin over 1-8 lanes");
-  static_assert(DALL || TB <= 64, "phase D on wave 0: one lane per bin");
+  static_assert(DALL || TB <= 64 || (TB % 64 == 0 && TB <= NT), "phase D on the first TB / 64 waves: one lane per bin");
   static_assert(DALL || STAGE * kRecD >= 19 * TB, "phase D reuses the record stage for the bin sums");
   __shared__ uint32_t s_cnt[kMaxSrc], s_off[kMaxSrc], s_st[kMaxSrc];
   __shared__ double s_rec[STAGE * kRecD];
@@ -1289,7 +1292,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   if (!tile_active) {
     // every bin of the tile has exact-zero sums: the zero-bin finalize writes its rows (N = 0,
     // Sigma = eps I, ...); partial row = nb x the zero bin's terms, no MF term
-    if (DALL || wid == 0) {
+    if (DALL || t < TB) {
       double z[19], c5[5] = {0.0, 0.0, 0.0, 0.0, -INFINITY};
 #pragma unroll
       for (int f = 0; f < 19; ++f) z[f] = 0.0;
@@ -1727,7 +1730,13 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #pragma unroll
     for (int f = 0; f < 19; ++f) s_rec[f * TB + lb] = acc[f];
   __syncthreads();
-  if (wid != 0) return;
+  // Phase D on the first TB / 64 waves, one lane per bin (full waves: a 128-bin tile's finalize is
+  // issued by 2 waves of 64 bins, not by 4 waves with one lane in LANES owning a bin)
+  if (TB <= 64 && wid != 0) return;
+  if (TB > 64 && t >= TB) {  // the other waves take the partial-row barrier only
+    __syncthreads();
+    return;
+  }
   PROF(14);
   // phase D: finalize + this bin's Matrix-Fisher term (row 7, matrix_fisher_evidence.py:181-211).
   // A bin with no scan mass contributes exact zeros to H, so only active bins read the map.
@@ -1745,7 +1754,19 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   }
   PROF(5);
   wave_reduce_bin_terms(v);
-  store_partials<kBinNV>(v, partials, tile);  // folded by k_final<FIN_BINS>
+  if constexpr (TB <= 64) {
+    store_partials<kBinNV>(v, partials, tile);  // folded by k_final<FIN_BINS>
+  } else {  // the finalizing waves in order
+    if (lane == 0)
+#pragma unroll
+      for (int f = 0; f < kBinNV; ++f) lds[wid * 16 + f] = v[f];
+    __syncthreads();
+    if (t < kBinNV) {
+      double x = lds[t];
+      for (int w = 1; w < TB / 64; ++w) x = t == 4 ? fmax(x, lds[w * 16 + t]) : x + lds[w * 16 + t];
+      partials[(size_t)tile * pstride<kBinNV>() + t] = x;  // folded by k_final<FIN_BINS>
+    }
+  }
   PROF(6);
   PROFV(7, 1);
 }
@@ -2526,9 +2547,9 @@ hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream
   if (a.tile_bins == 32)  // half the records of a 64-bin tile: the small stage holds them
     hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 32, 8, false>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else if (a.tile_bins == 128 && big)
-    hipExtLaunchKernelGGL((k_bins_scale<kStage128Big, 128, 2, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL((k_bins_scale<kStage128Big, 128, 2, GCS_DALL128>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else if (a.tile_bins == 128)
-    hipExtLaunchKernelGGL((k_bins_scale<kStage128Small, 128, 2, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
+    hipExtLaunchKernelGGL((k_bins_scale<kStage128Small, 128, 2, GCS_DALL128>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else if (a.tile_bins == 256 && big)
     hipExtLaunchKernelGGL((k_bins_scale<kStage256Big, 256, 1, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else if (a.tile_bins == 256)
