@@ -587,6 +587,12 @@ void k_points(PointKernelArgs a, double* partials) {
 //    takes one contiguous eighth of the scan (an azimuth sector), and the atlas rows that sector
 //    touches (cube-cell pools, bin directions, kNN rows) are fetched into one L2 instead of all
 //    eight.  Partial rows are stored at the logical block index: the fold order is unchanged.
+#ifndef GCS_PROBE_NOEXP
+#define GCS_PROBE_NOEXP 0
+#endif
+#ifndef GCS_PROBE_NOFIN
+#define GCS_PROBE_NOFIN 0  // timing probe (not a parity build): phase D skips finalize_bin / the MF term
+#endif
 #ifndef GCS_LEAN_CG
 #define GCS_LEAN_CG 8  // candidate direction loads in flight per group
 #endif
@@ -596,12 +602,15 @@ void k_points(PointKernelArgs a, double* partials) {
 #ifndef GCS_LEAN_EG
 #define GCS_LEAN_EG 4  // candidate exps interleaved per group (registers)
 #endif
-template <int KC>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
+// WIDE: grids of at most one wave per SIMD (cap <= 256 CUs x 4 SIMDs x 64 lanes, C2): occupancy is
+// one wave per SIMD whatever the registers, so the 128-register target is dropped and the candidate
+// directions go out in one group (one dependent memory round trip fewer on the point's chain).
+template <int KC, bool WIDE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(WIDE ? 1 : 4)))
 void k_points_lean(PointKernelArgs a, double* partials) {
   // one point per thread (the grid covers cap: points_blocks); no grid-stride loop, so nothing
   // loop-invariant is hoisted into registers across the point's chain
-  constexpr int CG = KC < GCS_LEAN_CG ? KC : GCS_LEAN_CG;
+  constexpr int CG = (WIDE || KC < GCS_LEAN_CG) ? KC : GCS_LEAN_CG;
   static_assert(KC % CG == 0, "candidate groups");
   __shared__ double lds[kWaves * 5];
   __shared__ double s_mass[2];
@@ -984,8 +993,8 @@ __device__ __forceinline__ void finalize_bin(const double* r, double* __restrict
                                              double* cert /*5*/) {
   double N = r[0];
   double den = N + kEpsMass + kF64Eps;          // inv_mass_core, primitives.py:195-212
-  double invN = 1.0 / den;
-  double epsr = kEpsMass / den;
+  double invN = rcp_fast(den);
+  double epsr = kEpsMass * invN;
   double pb[3] = {r[10] * invN, r[11] * invN, r[12] * invN};
   const double* q = r + 13;
   double sc[9];
@@ -999,10 +1008,21 @@ __device__ __forceinline__ void finalize_bin(const double* r, double* __restrict
   sc[7] = q[4] * invN - pb[2] * pb[1];
   sc[8] = q[5] * invN - pb[2] * pb[2];
   double sig[9];
+#if GCS_PROBE_NOFIN == 3  // timing probe: no PSD / kappa (the stores stay)
+  double delta = 0.0;
+  for (int k = 0; k < 9; ++k) sig[k] = sc[k];
+  double kap = r[1];
+#else
   double delta = psd_project3(sc, sig);
   double sn = sqrt(dot3_exact(r[1], r[2], r[3], r[1], r[2], r[3]));
   double kap = kappa_from_rbar(sn * invN);
+#endif
   size_t Bs = (size_t)B;
+#if GCS_PROBE_NOFIN == 2  // timing probe: the arithmetic without the 26 row stores
+  if (delta == 12345.0) scan[b] = kap + sig[4];
+  if (r[0] == 12345.0)
+#endif
+  {
   scan[SF_N * Bs + b] = N;
   scan[(SF_SD + 0) * Bs + b] = r[1];
   scan[(SF_SD + 1) * Bs + b] = r[2];
@@ -1016,9 +1036,10 @@ __device__ __forceinline__ void finalize_bin(const double* r, double* __restrict
 #pragma unroll
   for (int k = 0; k < 9; ++k) scan[(SF_SIG + k) * Bs + b] = sig[k];
   scan[SF_KAPPA * Bs + b] = kap;
+  }
   cert[0] += N;
   cert[1] += N * N;
-  cert[2] += N / (N + kEpsMass);
+  cert[2] += N * rcp_fast(N + kEpsMass);
   cert[3] += delta;
   cert[4] = fmax(cert[4], epsr);
 }
@@ -1058,9 +1079,11 @@ __device__ __forceinline__ void mf_bin_term(double Ns, double sx, double sy, dou
   double wb = sqrt(Ns * Nm + kEpsMass);
   double sn = sqrt(dot3_exact(sx, sy, sz, sx, sy, sz));
   double mn = sqrt(dot3_exact(mx, my, mz, mx, my, mz));
-  double us[3] = {sx / (sn + kEpsMass), sy / (sn + kEpsMass), sz / (sn + kEpsMass)};
-  double um[3] = {mx / (mn + kEpsMass), my / (mn + kEpsMass), mz / (mn + kEpsMass)};
-  double conf = (sn * (1.0 / (Ns + kEpsMass))) * (mn * (1.0 / (Nm + kEpsMass)));
+  // four reciprocals for the eight divisions of the restatement (matrix_fisher_evidence.py:181-211)
+  const double isn = rcp_fast(sn + kEpsMass), imn = rcp_fast(mn + kEpsMass);
+  double us[3] = {sx * isn, sy * isn, sz * isn};
+  double um[3] = {mx * imn, my * imn, mz * imn};
+  double conf = (sn * rcp_fast(Ns + kEpsMass)) * (mn * rcp_fast(Nm + kEpsMass));
   double wf = wb * conf;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
@@ -1167,7 +1190,11 @@ __device__ __forceinline__ void bin_contrib(double* acc, const double4& bd, doub
   double p[3] = {px, py, pz};
   double sim = dot3_exact(dx, dy, dz, bd.x, bd.y, bd.z);
   // w r = w exp((s - m)/tau) / Z   (binning.py:69 softmax, :159-160 weighting)
+#if GCS_PROBE_NOEXP  // timing probe (not a parity build): the exp's share of the gather
+  add_contrib(acc, wz * fmax(1.0 + (sim - m) * inv_tau, 1e-3), d, p);
+#else
   add_contrib(acc, wz * exp((sim - m) * inv_tau), d, p);
+#endif
 }
 
 #ifdef GCS_PHASE_PROF
@@ -1744,7 +1771,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #pragma unroll
   for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
   v[4] = -INFINITY;
-  if (own) {
+  if (own && GCS_PROBE_NOFIN != 1) {
 #pragma unroll
     for (int f = 0; f < 19; ++f) acc[f] = s_rec[f * TB + t];
     finalize_bin(acc, a.scan, a.n_bins, b0 + t, v);
@@ -2491,10 +2518,25 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
   hipEvent_t ek = fold ? nullptr : e1;
   // legacy: the round-3 point kernel (one wave per SIMD; GCSLAM_POINTS=legacy / GCS_DEBUG_POINT_KERNEL), for A/B
   if (scale && !legacy && kPointLanes == 1 && (long)nblk * kBlock >= (long)a.cap) {  // one point per thread
+    // at most one wave per SIMD (GCSLAM_POINTS_WIDE=0 turns the wide form off, for A/B)
+    static const bool wide_ok = [] {
+      const char* e = getenv("GCSLAM_POINTS_WIDE");
+      return !(e && atoi(e) == 0);
+    }();
+    const bool wide = wide_ok && (long)nblk * kBlock <= 1024L * 64;
     switch (a.k) {
-      case 8: hipExtLaunchKernelGGL((k_points_lean<8>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
-      case 16: hipExtLaunchKernelGGL((k_points_lean<16>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
-      case 32: hipExtLaunchKernelGGL((k_points_lean<32>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials); break;
+      case 8:
+        if (wide) hipExtLaunchKernelGGL((k_points_lean<8, true>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
+        else hipExtLaunchKernelGGL((k_points_lean<8, false>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
+        break;
+      case 16:
+        if (wide) hipExtLaunchKernelGGL((k_points_lean<16, true>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
+        else hipExtLaunchKernelGGL((k_points_lean<16, false>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
+        break;
+      case 32:
+        if (wide) hipExtLaunchKernelGGL((k_points_lean<32, true>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
+        else hipExtLaunchKernelGGL((k_points_lean<32, false>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
+        break;
       default: return hipErrorInvalidValue;
     }
   } else if (scale) {

@@ -45,6 +45,20 @@ GCS_HD double dot3_exact(double ax, double ay, double az, double bx, double by, 
   return s + zz;
 }
 
+// 1 / d for a positive normal d.  Device: v_rcp_f64 and two Newton steps (within an ulp of the IEEE
+// quotient, 5 instructions against the ~10 of the division's scale / fmas / fixup sequence); host: the
+// division.  The bin kernels' per-bin finalize takes its reciprocals here (the tolerances of the
+// quantities involved are >= 1e-12 relative).
+GCS_HD double rcp_fast(double d) {
+#ifdef __HIP_DEVICE_COMPILE__
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(fma(-d, r, 1.0), r, r);
+  return fma(fma(-d, r, 1.0), r, r);
+#else
+  return 1.0 / d;
+#endif
+}
+
 GCS_HD double sigmoid(double x) {
   // numerically symmetric logistic; above 40, exp(-x) < 2^-57 and 1 / (1 + exp(-x)) rounds to
   // exactly 1.0, which is returned without the exp (bitwise the same value)
@@ -73,7 +87,7 @@ GCS_HD double kappa_from_rbar(double rbar) {
   double R = rbar < 0.0 ? 0.0 : rbar;
   R = R > 1.0 - kEpsR ? 1.0 - kEpsR : R;
   double R2 = R * R;
-  double k_low = (R * (3.0 - R2)) / (1.0 - R2 + kEpsR);
+  double k_low = (R * (3.0 - R2)) * rcp_fast(1.0 - R2 + kEpsR);
   double om = 1.0 - R2;
   double k_high = -log(om > kEpsR ? om : kEpsR);
   double s = sigmoid((R - kKappaR0) / kKappaTau);
@@ -414,10 +428,12 @@ GCS_HD double psd_project3(const double* M, double* out) {
   {
     double a00 = s[0] - kEpsPsd;
     if (a00 > 0.0) {
-      double l00 = sqrt(a00), l10 = s[3] / l00, l20 = s[6] / l00;
+      // (a positivity test: the reciprocals' last-ulp rounding only moves matrices within rounding of
+      // a clamp between this exact path and the deflation, which agree there)
+      double l00 = sqrt(a00), i00 = rcp_fast(l00), l10 = s[3] * i00, l20 = s[6] * i00;
       double a11 = s[4] - kEpsPsd - l10 * l10;
       if (a11 > 0.0) {
-        double l11 = sqrt(a11), l21 = (s[7] - l20 * l10) / l11;
+        double l11 = sqrt(a11), l21 = (s[7] - l20 * l10) * rcp_fast(l11);
         double a22 = s[8] - kEpsPsd - l20 * l20 - l21 * l21;
         if (a22 > 0.0) {
           for (int i = 0; i < 9; ++i) out[i] = s[i];
