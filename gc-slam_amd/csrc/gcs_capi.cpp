@@ -167,6 +167,15 @@ struct gcs_ctx {
   // C2 113.5 vs 106.9 us per step, same box (profiles/r03/gate/)
   bool gate_on = false;
   bool gate_withhold = false;  // fault test (GCS_DEBUG_LAUNCH_GATE = -1): the gate is never opened
+  // IMU weights + preintegration on the device (k_preint, GCSLAM_DEVICE_PREINT=1 or
+  // GCS_DEBUG_DEVICE_PREINT; not with the launch gate): the prologue stages the IMU window in pinned
+  // memory and queues k_preint, k_points reads its twist, the tail reads its record after the sync
+  bool device_preint = false;
+  bool preint_pending = false;       // the next point stage reads the device twist (d_gate_xi)
+  bool preint_host_pending = false;  // st.xi / st.pre / cert[10] still to be read from h_preint_out
+  double* h_preint_in = nullptr;     // pinned: the staged window (7 doubles per sample)
+  int64_t preint_in_cap = 0;
+  double* h_preint_out = nullptr;    // pinned: xi[6], ess, delta_pose[6], delta_v[3]
   int pts_blocks = 0;
   bool pts_fold_pending = false;
   double* d_scalars = nullptr;
@@ -511,6 +520,9 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
     HIPCHK(c, launch_gate(c->d_gate, c->gate_next, c->d_gate_xi, c->d_err + 3, s));
     a.xi_dev = c->d_gate_xi;
     c->gate_next = 0;
+  } else if (c->preint_pending) {  // k_preint, queued by the prologue on this stream, wrote the twist
+    a.xi_dev = c->d_gate_xi;
+    c->preint_pending = false;
   }
   c->iz_valid = false;
   const bool scale = c->cfg.mode == GCS_MODE_SCALE && !deskew_only;
@@ -1030,6 +1042,9 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipHostGetDevicePointer((void**)&c->d_gate, c->h_gate, 0))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_gate_xi, 8 * sizeof(double)))) return GCS_ERR_HIP;
   if (const char* g = getenv("GCSLAM_GATE")) c->gate_on = atoi(g) != 0;
+  if (const char* g = getenv("GCSLAM_DEVICE_PREINT")) c->device_preint = atoi(g) != 0;
+  if (bad(hipHostMalloc(&c->h_preint_out, 16 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent)))
+    return GCS_ERR_HIP;
   if (cfg->mode == GCS_MODE_SCALE) {
     if (bad(hipMalloc(&c->d_knn, B * c->K * sizeof(int)))) return GCS_ERR_HIP;
     if (bad(hipMalloc(&c->d_rknn_off, (B + 1) * sizeof(int)))) return GCS_ERR_HIP;
@@ -1119,6 +1134,8 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
   if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_gate) (void)hipHostFree(c->h_gate);
+  if (c->h_preint_in) (void)hipHostFree(c->h_preint_in);
+  if (c->h_preint_out) (void)hipHostFree(c->h_preint_out);
   if (c->h_payload) (void)hipHostFree(c->h_payload);
   if (c->d_payload) (void)hipFree(c->d_payload);
   for (int st = 0; st < kStages; ++st)
@@ -1173,6 +1190,9 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
       return GCS_OK;
     case GCS_DEBUG_POINT_KERNEL:
       c->legacy_points = value != 0;
+      return GCS_OK;
+    case GCS_DEBUG_DEVICE_PREINT:
+      c->device_preint = value != 0;
       return GCS_OK;
     case GCS_DEBUG_LAUNCH_GATE:
       if (value < -1 || value > 1) return fail(c, GCS_ERR_ARG, "launch gate: -1, 0 or 1");
@@ -1492,8 +1512,65 @@ struct LidarTerms {
 
 // 1 (launch), 2 PredictDiffusion, 3 IMU membership window + preintegration -> deskew twist
 // (pipeline.py:399-483)
+// Device preintegration (k_preint): the window is staged in pinned memory (the trailing run of
+// repeated stamps -- the zero padding -- trimmed to its first sample: its steps are exact identities
+// and only their weights enter ess), the kernel is queued on the scan stream, and the point stage
+// reads the twist from the device word.  st.xi / st.pre arrive after the scan's sync (finish_preint).
+int launch_device_preint(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st) {
+  const int m = in->imu_len;
+  int r = m - 1;
+  while (r > 0 && in->imu_stamps[r - 1] == in->imu_stamps[r]) --r;
+  const int me = r + 1;
+  if (c->preint_in_cap < 7 * (int64_t)me) {
+    if (c->h_preint_in) (void)hipHostFree(c->h_preint_in);  // (the last scan's k_preint has completed)
+    c->h_preint_in = nullptr;
+    c->preint_in_cap = 0;
+    const int64_t cap = 7 * (int64_t)std::max(me, 512);
+    HIPCHK(c, hipHostMalloc(&c->h_preint_in, cap * sizeof(double), hipHostMallocMapped));
+    c->preint_in_cap = cap;
+  }
+  double* hin = c->h_preint_in;
+  memcpy(hin, in->imu_stamps, me * sizeof(double));
+  memcpy(hin + me, in->imu_gyro, 3 * me * sizeof(double));
+  memcpy(hin + 4 * me, in->imu_accel, 3 * me * sizeof(double));
+  PreintArgs a{};
+  a.imu = hin;
+  a.m = me;
+  a.n_tail = m - me;
+  a.tail_stamp = in->imu_stamps[r];
+  a.t0 = in->scan_start_time;
+  a.t1 = in->scan_end_time;
+  a.sigma = st.sigma_warp;
+  for (int k = 0; k < 3; ++k) {
+    a.rotvec[k] = st.pose0[3 + k];
+    a.gb[k] = st.mu_inc[9 + k];
+    a.ab[k] = st.mu_inc[12 + k];
+    a.g[k] = c->grav[k];
+  }
+  a.rotation_only = c->cfg.deskew_rotation_only ? 1 : 0;
+  a.xi_dev = c->d_gate_xi;
+  a.host_out = c->h_preint_out;
+  HIPCHK(c, launch_preint(a, c->stream));
+  c->preint_pending = true;
+  c->preint_host_pending = true;
+  return GCS_OK;
+}
+
+// after the scan's sync: the device preintegration's record into the scan state
+void finish_preint(gcs_ctx* c, gcs_scan_state& st) {
+  if (!c->preint_host_pending) return;
+  c->preint_host_pending = false;
+  const volatile double* o = c->h_preint_out;
+  for (int k = 0; k < 6; ++k) st.xi[k] = o[k];
+  st.pre.ess = o[6];
+  for (int k = 0; k < 6; ++k) st.pre.delta_pose[k] = o[7 + k];
+  for (int k = 0; k < 3; ++k) st.pre.delta_v[k] = o[13 + k];
+  st.cert[10] = st.pre.ess;
+}
+
 int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st, bool budget = true) {
   st.T0 = clk::now();
+  c->preint_pending = c->preint_host_pending = false;  // (a failed scan may have left them set)
   if (budget) {  // (the pre-launched front queues k_budget itself)
     c->budget_pending = false;
     if (int rc0 = stage_budget(c, in->weights_dev, in->n_points)) return rc0;  // runs during the prologue
@@ -1520,14 +1597,19 @@ int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st, boo
   host::spd_factor_solve(fpred, e15, col15);  // column 15 of the predicted covariance
   st.sigma_warp = std::max(sqrt(col15[15]), 0.01);
   cert[38] = st.sigma_warp;
+  host::spd_factor_solve(fpred, st.pred.h, st.mu_inc);
+  host::world_pose_from_increment(st.prev, st.mu_prev, st.pose0);
+  if (budget && c->device_preint) {  // k_preint on the stream ahead of the point stage
+    if (int rc = launch_device_preint(c, in, st)) return rc;
+    st.T1 = clk::now();
+    return GCS_OK;
+  }
   std::vector<double>& wimu = c->wimu;
   wimu.resize(in->imu_len);
   for (int i = 0; i < in->imu_len; ++i)  // a repeated stamp (the window's zero padding) reuses its value
     wimu[i] = i > 0 && in->imu_stamps[i] == in->imu_stamps[i - 1]
                   ? wimu[i - 1]
                   : smooth_window(in->imu_stamps[i], in->scan_start_time, in->scan_end_time, st.sigma_warp);
-  host::spd_factor_solve(fpred, st.pred.h, st.mu_inc);
-  host::world_pose_from_increment(st.prev, st.mu_prev, st.pose0);
   host::preintegrate_imu(in->imu_len, in->imu_stamps, in->imu_gyro, in->imu_accel, wimu.data(), st.pose0 + 3,
                          st.mu_inc + 9, st.mu_inc + 12, c->grav, st.pre);
   host::se3_log(st.pre.delta_pose, st.xi);
@@ -1913,6 +1995,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     st.Ts = clk::now();
     if ((rc = scan_imu_odom(c, in, st, out))) return rc;
     if ((rc = wait_mirror(c))) return rc;  // the PT fold has written the scalars to h_scalars
+    finish_preint(c, st);
   }
   if ((rc = check_bucket_err(c))) return rc;
   bool redone = false;
@@ -1964,6 +2047,7 @@ int gcs_scan_begin(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs
   st.Ts = clk::now();
   if ((rc = scan_imu_odom(c, in, st, c->live_out))) return rc;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  finish_preint(c, st);
   if ((rc = pull_scalars(c))) return rc;
   st.T2 = clk::now();
   if ((rc = scan_point_certs(c, in, st))) return rc;
@@ -2438,6 +2522,57 @@ int gcs_debug_tile_order(int32_t device, const uint8_t* active, const uint32_t* 
   if (da) (void)hipFree(da);
   if (dw) (void)hipFree(dw);
   if (dord) (void)hipFree(dord);
+  return rc;
+}
+int gcs_debug_preintegrate(int32_t device, int32_t m, const double* stamps, const double* gyro, const double* accel,
+                           double t0, double t1, double sigma, const double* rotvec, const double* gyro_bias,
+                           const double* accel_bias, const double* gravity, int32_t rotation_only, double* out) {
+  if (m < 1 || !stamps || !gyro || !accel || !rotvec || !gyro_bias || !accel_bias || !gravity || !out)
+    return GCS_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return GCS_ERR_HIP;
+  double *hin = nullptr, *hout = nullptr, *dxi = nullptr;
+  int rc = GCS_OK;
+  if (hipHostMalloc(&hin, 7 * (size_t)m * sizeof(double), hipHostMallocMapped) != hipSuccess ||
+      hipHostMalloc(&hout, 16 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipMalloc(&dxi, 8 * sizeof(double)) != hipSuccess) {
+    rc = GCS_ERR_HIP;
+  } else {
+    int r = m - 1;  // the same trailing-run trim as the scan prologue
+    while (r > 0 && stamps[r - 1] == stamps[r]) --r;
+    const int me = r + 1;
+    memcpy(hin, stamps, me * sizeof(double));
+    memcpy(hin + me, gyro, 3 * me * sizeof(double));
+    memcpy(hin + 4 * me, accel, 3 * me * sizeof(double));
+    PreintArgs a{};
+    a.imu = hin;
+    a.m = me;
+    a.n_tail = m - me;
+    a.tail_stamp = stamps[r];
+    a.t0 = t0;
+    a.t1 = t1;
+    a.sigma = sigma;
+    for (int k = 0; k < 3; ++k) {
+      a.rotvec[k] = rotvec[k];
+      a.gb[k] = gyro_bias[k];
+      a.ab[k] = accel_bias[k];
+      a.g[k] = gravity[k];
+    }
+    a.rotation_only = rotation_only;
+    a.xi_dev = dxi;
+    a.host_out = hout;
+    double xi_dev[8];
+    if (launch_preint(a, nullptr) != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpy(xi_dev, dxi, 6 * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+      rc = GCS_ERR_HIP;
+    } else {
+      memcpy(out, hout, 16 * sizeof(double));
+      for (int k = 0; k < 6; ++k)  // the device word k_points reads must equal the host record
+        if (memcmp(&xi_dev[k], &hout[k], sizeof(double)) != 0) rc = GCS_ERR_HIP;
+    }
+  }
+  if (hin) (void)hipHostFree(hin);
+  if (hout) (void)hipHostFree(hout);
+  if (dxi) (void)hipFree(dxi);
   return rc;
 }
 int gcs_psd_project3(const double* M, double* out, double* delta) {

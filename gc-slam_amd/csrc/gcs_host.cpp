@@ -379,28 +379,8 @@ void se3_inverse(const double* a, double* out) {
   so3_log(Rt, out + 3);
 }
 
-// se3_log, se3_jax.py:210-245 (with _se3_V_inv, :169-207)
-void se3_log(const double* T, double* out) {
-  double R[9], phi[3];
-  so3_exp(T + 3, R);
-  so3_log(R, phi);
-  double theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
-  double theta = sqrt(theta_sq);
-  bool small = theta < kSmallAngle;
-  double st = small ? 1.0 : theta;
-  double st2 = theta_sq < kSmallAngle * kSmallAngle ? 1.0 : theta_sq;
-  double denom = 2.0 * st * sin(st) + 1e-12;
-  double D = small ? 1.0 / 12.0 + theta_sq / 720.0 : (1.0 / st2) - (1.0 + cos(st)) / denom;
-  double K[9], K2[9];
-  skew3(phi, K);
-  mat3_mul(K, K, K2);
-  for (int i = 0; i < 3; ++i) {
-    double acc = T[i];
-    for (int j = 0; j < 3; ++j) acc += (-0.5 * K[3 * i + j] + D * K2[3 * i + j]) * T[j];
-    out[i] = acc;
-  }
-  out[3] = phi[0]; out[4] = phi[1]; out[5] = phi[2];
-}
+// se3_log, se3_jax.py:210-245: the shared host/device routine (gcs_math.h se3_log_hd)
+void se3_log(const double* T, double* out) { se3_log_hd(T, out); }
 
 // BeliefGaussianInfo.mean_increment / mean_world_pose, belief.py:373-434
 void mean_increment(const Belief& b, double* dz) { spd_solve_lifted(DZ, b.L, b.h, kEpsLift, dz); }

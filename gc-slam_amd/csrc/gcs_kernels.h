@@ -152,6 +152,19 @@ hipError_t launch_budget(const BudgetArgs& a, int nblk, hipStream_t s, hipEvent_
 // fold: run k_points' cert fold now (else k_bins_scale block 0 folds it, BinKernelArgs.pts_partials)
 int points_blocks(long cap, bool scale);  // k_points grid (lanes per point in scale mode)
 int points_max_blocks();
+// IMU window weights + preintegration on the device (gcs_preint.hip; imu_preintegration.py:20-147)
+struct PreintArgs {
+  const double* imu;  // pinned host: stamps[m], gyro[m*3], accel[m*3]
+  int m;              // samples kept (the trailing run of repeated stamps trimmed to its first)
+  int n_tail;         // trimmed samples: zero steps carrying weight w(tail_stamp) each
+  double tail_stamp;
+  double t0, t1, sigma;  // smooth_window(t, t0, t1, sigma)
+  double rotvec[3], gb[3], ab[3], g[3];
+  int rotation_only;
+  double* xi_dev;     // device: the deskew twist (PointKernelArgs.xi_dev)
+  double* host_out;   // pinned host or null: xi[6], ess, delta_pose[6], delta_v[3]
+};
+hipError_t launch_preint(const PreintArgs& a, hipStream_t s);
 hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err, hipStream_t s);
 // legacy: the round-3 k_points (scale mode) instead of k_points_lean
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,

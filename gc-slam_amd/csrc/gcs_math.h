@@ -181,6 +181,29 @@ GCS_HD void se3_exp(const double* xi, double* out) {
   out[3] = phi[0]; out[4] = phi[1]; out[5] = phi[2];
 }
 
+// se3_log, se3_jax.py:210-245 (with _se3_V_inv, :169-207)
+GCS_HD void se3_log_hd(const double* T, double* out) {
+  double R[9], phi[3];
+  so3_exp(T + 3, R);
+  so3_log(R, phi);
+  double theta_sq = phi[0] * phi[0] + phi[1] * phi[1] + phi[2] * phi[2];
+  double theta = sqrt(theta_sq);
+  bool small = theta < kSmallAngle;
+  double st = small ? 1.0 : theta;
+  double st2 = theta_sq < kSmallAngle * kSmallAngle ? 1.0 : theta_sq;
+  double denom = 2.0 * st * sin(st) + 1e-12;
+  double D = small ? 1.0 / 12.0 + theta_sq / 720.0 : (1.0 / st2) - (1.0 + cos(st)) / denom;
+  double K[9], K2[9];
+  skew3(phi, K);
+  mat3_mul(K, K, K2);
+  for (int i = 0; i < 3; ++i) {
+    double acc = T[i];
+    for (int j = 0; j < 3; ++j) acc += (-0.5 * K[3 * i + j] + D * K2[3 * i + j]) * T[j];
+    out[i] = acc;
+  }
+  out[3] = phi[0]; out[4] = phi[1]; out[5] = phi[2];
+}
+
 // Per-point deskew: T = se3_exp(alpha xi); p0 = R^T (p - t)  (deskew_constant_twist.py:51-58)
 GCS_HD void deskew_point(double alpha, const double* xi, const double* p, double* p0) {
   double rho[3] = {alpha * xi[0], alpha * xi[1], alpha * xi[2]};

@@ -880,7 +880,10 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_ts(PmStore st, const int
 
 // Step 12b's per-block fuse calls in one pass: key = ((tile position x M + slot) x nb + block) for
 // the contributing rows, so a (tile, slot) group's rows sort by block and, within a block, by row.
-__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmRows r, int n_tiles, int M, int nb, int rpb,
+// Also timestamps.at[unique(target_slots)].set(ts) in every listed tile (:1112; k_pm_fuse_ts's
+// writes: no kernel of the fuse reads ts, so they move here).
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmStore st, const int32_t* tiles, double ts,
+                                                                    PmRows r, int n_tiles, int M, int nb, int rpb,
                                                                     uint32_t* keys, uint32_t* vals, uint8_t* mark,
                                                                     uint32_t* err) {
   const int g = blockIdx.x * kPmThreads + threadIdx.x;
@@ -889,6 +892,8 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmRows r, in
   const bool ok = q >= 0 && q < M;
   if (!ok) err[0] = 1u;
   else mark[(size_t)b * M + q] = 1;  // every row's slot counts for n_fused (np.unique(target_slots))
+  if (ok)
+    for (int t = 0; t < n_tiles; ++t) st.ts[sidx(st, tiles[t], q)] = ts;
   const bool v = (r.valid ? r.valid[g] != 0 : true) && tp >= 0 && tp < n_tiles && ok;
   keys[g] = v ? ((uint32_t)tp * (uint32_t)M + (uint32_t)q) * (uint32_t)nb + (uint32_t)b : kNoKey;
   vals[g] = (uint32_t)g;
@@ -954,12 +959,17 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st,
 }
 
 // unique slots per block (grid: blocks of slots x nb): integer atomics into device counters
-__global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(const uint8_t* mark, int M, uint32_t* cnt) {
+// Each mark is read by one lane, which clears it: the marks are all zero again for the next call
+// (zeroed once at allocation; no per-call fill).
+__global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(uint8_t* mark, int M, uint32_t* cnt) {
   __shared__ double lds[kPmThreads / 64];
   const int b = blockIdx.y;
   double c = 0.0;
-  for (int q = blockIdx.x * kPmThreads + threadIdx.x; q < M; q += gridDim.x * kPmThreads)
-    c += mark[(size_t)b * M + q] ? 1.0 : 0.0;
+  for (int q = blockIdx.x * kPmThreads + threadIdx.x; q < M; q += gridDim.x * kPmThreads) {
+    uint8_t& mk = mark[(size_t)b * M + q];
+    c += mk ? 1.0 : 0.0;
+    if (mk) mk = 0;
+  }
   c = block_sum_d<kPmThreads>(c, lds);
   if (threadIdx.x == 0 && c > 0.0) atomicAdd(cnt + b, (uint32_t)c);
 }
@@ -989,7 +999,10 @@ __global__ __launch_bounds__(kPmRed) void k_pm_count(PmStore st, const int32_t* 
 
 // cull (:1217-1250): below = valid & w < thr -> invalid; culled count, mass dropped, sum of all weights,
 // valid count after (one workgroup per tile, fixed-order sums)
-__global__ __launch_bounds__(kPmRed) void k_pm_cull(PmStore st, const int32_t* tiles, double thr, double* part) {
+// forget != 0: the forgetting pass of step 12b rides along (w := gamma w after the cull read it,
+// :1443-1447 -- the same product k_pm_forget writes, one pass over the tile instead of two)
+__global__ __launch_bounds__(kPmRed) void k_pm_cull(PmStore st, const int32_t* tiles, double thr, double* part,
+                                                    int forget, double gamma) {
   __shared__ double lds[kPmRed / 64];
   const int ti = tiles[blockIdx.x];
   double nb = 0.0, md = 0.0, ws = 0.0, nv = 0.0;
@@ -1003,6 +1016,7 @@ __global__ __launch_bounds__(kPmRed) void k_pm_cull(PmStore st, const int32_t* t
     ws += w;
     nv += (v && !b) ? 1.0 : 0.0;
     if (b) st.valid[i] = 0;
+    if (forget) st.w[i] = gamma * w;
   }
   nb = block_sum_d<kPmRed>(nb, lds);
   md = block_sum_d<kPmRed>(md, lds);
@@ -1313,8 +1327,12 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fm_sums(const double* fm, con
 }
 
 // device counters into the mapped buffer (one launch instead of a device-to-host copy)
-__global__ void k_pm_publish_u32(const uint32_t* src, int n, uint32_t* dst) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) dst[i] = src[i];
+// copies the counters out and re-zeroes them for the next call (no per-call fill)
+__global__ void k_pm_publish_u32(uint32_t* src, int n, uint32_t* dst) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    dst[i] = src[i];
+    src[i] = 0u;
+  }
 }
 
 // block_associations_for_fuse (primitive_association.py:561-588) + the world transform, rows in
@@ -1705,6 +1723,7 @@ int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t 
       bad(hipMalloc(&p->d_tiles, max_tiles * 4)) || bad(hipMalloc(&p->d_tids, max_tiles * 8)) ||
       bad(hipMalloc(&p->mark, (size_t)m_tile * 4)) || bad(hipMalloc(&p->dcnt, 4)) ||
       bad(hipMalloc(&p->bcnt, kMaxFuseBlocks * 4)) ||
+      bad(hipMemset(p->bcnt, 0, kMaxFuseBlocks * 4)) ||  // once: k_pm_publish_u32 re-zeroes
       bad(hipMalloc(&p->tickets, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
       bad(hipMemset(p->tickets, 0, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
       bad(hipHostMalloc((void**)&p->h_small, kSmall, hipHostMallocMapped)) ||
@@ -1973,16 +1992,15 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
     if (p->bmark) PMCHK(p, hipFree(p->bmark));
     p->bmark = nullptr;
     PMCHK(p, hipMalloc(&p->bmark, mb));
+    PMCHK(p, hipMemsetAsync(p->bmark, 0, mb, p->stream));  // once: k_pm_count_marks_blocks re-zeroes
     p->bmark_bytes = mb;
   }
   uint32_t* d_err = (uint32_t*)(p->d_small + 8192);
   *(uint32_t*)(p->h_small + 8192) = 0u;
-  PMCHK(p, hipMemsetAsync(p->bmark, 0, mb, p->stream));
-  PMCHK(p, hipMemsetAsync(p->bcnt, 0, nb * 4, p->stream));
   const PmRows r = rows_of(rows);
   const int rb = (R + kPmThreads - 1) / kPmThreads;
-  hipLaunchKernelGGL(k_pm_fuse_keys_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, r, n, p->M, nb, rpb, p->fk, p->fv,
-                     p->bmark, d_err);
+  hipLaunchKernelGGL(k_pm_fuse_keys_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st,
+                     (const int32_t*)p->d_tiles, timestamp, r, n, p->M, nb, rpb, p->fk, p->fv, p->bmark, d_err);
   unsigned bits = 1;
   while (bits < 32 && ((double)(1ull << bits)) < (double)n * p->M * nb + 1.0) ++bits;
   size_t tb = p->ftemp_bytes;
@@ -1993,13 +2011,9 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
   const long tm = (long)n * p->M;
   hipLaunchKernelGGL(k_pm_fuse_rgb, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
                      p->stream, p->st, (const int32_t*)p->d_tiles, n, eps_mass);
-  const long tr = (long)n * R;
-  PMCHK(p, hipMemsetAsync(p->mark, 0, (size_t)p->M * 4, p->stream));  // k_pm_fuse_ts marks (unused here)
-  hipLaunchKernelGGL(k_pm_fuse_ts, dim3((unsigned)((tr + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
-                     p->stream, p->st, (const int32_t*)p->d_tiles, n, r, timestamp, p->mark);
   hipLaunchKernelGGL(k_pm_count_marks_blocks, dim3(std::min(32, (p->M + kPmThreads - 1) / kPmThreads), nb),
-                     dim3(kPmThreads), 0, p->stream, (const uint8_t*)p->bmark, p->M, p->bcnt);
-  hipLaunchKernelGGL(k_pm_publish_u32, dim3(1), dim3(256), 0, p->stream, (const uint32_t*)p->bcnt, nb,
+                     dim3(kPmThreads), 0, p->stream, p->bmark, p->M, p->bcnt);
+  hipLaunchKernelGGL(k_pm_publish_u32, dim3(1), dim3(256), 0, p->stream, p->bcnt, nb,
                      (uint32_t*)(p->d_small + 9216));
   PMCHK(p, hipGetLastError());
   if (!nf) return GCS_OK;
@@ -2021,7 +2035,7 @@ int gcs_pmap_cull(gcs_pmap* p, const int32_t* tiles, int32_t n, double thr, int3
   if (int rc = upload_tiles(p, tiles, n)) return rc;
   const int nbt = blocks_per_tile(p->M);
   hipLaunchKernelGGL(k_pm_cull, dim3(n, nbt), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles, thr,
-                     (double*)(p->d_small + kPartOff));
+                     (double*)(p->d_small + kPartOff), 0, 1.0);
   PMCHK(p, hipGetLastError());
   PMCHK(p, hipStreamSynchronize(p->stream));
   const double* h = (const double*)(p->h_small + kPartOff);
@@ -2226,13 +2240,11 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
                        (long long)*next_global_id, (int64_t*)nullptr, d_ins);
     PMCHK(p, hipGetLastError());
   }
-  // per tile: cull (its partials carry the valid count after it), forget (pipeline.py:1413-1447)
+  // per tile: cull (its partials carry the valid count after it) and forget in one pass
+  // (pipeline.py:1413-1447)
   const int nbt = blocks_per_tile(p->M);
   hipLaunchKernelGGL(k_pm_cull, dim3(n, nbt), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
-                     cfg->cull_threshold, (double*)(p->d_small + kPartOff));
-  const long tm = (long)n * p->M;
-  hipLaunchKernelGGL(k_pm_forget, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
-                     p->stream, p->st, (const int32_t*)p->d_tiles, n, cfg->forgetting_factor);
+                     cfg->cull_threshold, (double*)(p->d_small + kPartOff), 1, cfg->forgetting_factor);
   PMCHK(p, hipGetLastError());
   PMCHK(p, hipStreamSynchronize(p->stream));
   if (*(uint32_t*)(p->h_small + 8192)) return pm_fail(p, GCS_ERR_ARG, "target slot out of range (rows skipped)");

@@ -99,6 +99,7 @@ DEBUG_SCAN_SPIN_LIMIT, DEBUG_INJECT_SCAN_FAIL = 1, 2
 DEBUG_SORTED_BUCKETS, DEBUG_BUCKET_CAPACITY = 3, 4
 DEBUG_LAUNCH_GATE = 5
 DEBUG_POINT_KERNEL = 6
+DEBUG_DEVICE_PREINT = 7
 MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 
@@ -244,6 +245,9 @@ _SIGS = [
     ("gcs_svd3", C.c_int, [c_double_p, c_double_p, c_double_p, c_double_p]),
     ("gcs_psd_project3", C.c_int, [c_double_p, c_double_p, c_double_p]),
     ("gcs_debug_tile_order", C.c_int, [C.c_int32, C.c_void_p, C.c_void_p, C.c_int32, C.c_int32, C.c_void_p]),
+    ("gcs_debug_preintegrate", C.c_int, [C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_double,
+                                         C.c_double, C.c_double, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                         C.c_int32, C.c_void_p]),
     ("gcs_mf_rotation", C.c_int, [c_double_p, c_double_p]),
     ("gcs_predict_diffusion", C.c_int, [C.POINTER(GcsBelief), c_double_p, C.c_double, C.POINTER(GcsBelief),
                                         c_double_p]),
@@ -348,6 +352,10 @@ def load():
         pass
     lib = C.CDLL(path)
     for name, res, args in _SIGS:
+        # test-only entries (gcs_debug_*) may be absent from an older build loaded through GCSLAM_LIB
+        # for a same-box A/B; every other entry point is required
+        if name.startswith("gcs_debug_") and path != LIB_PATH and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

@@ -221,6 +221,10 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
 /* GCS_DEBUG_POINT_KERNEL != 0: scale-mode scans run the round-3 point kernel (one wave per SIMD)
  * instead of k_points_lean (same arithmetic, bitwise the same outputs; A/B and its parity test). */
 #define GCS_DEBUG_POINT_KERNEL 6
+/* GCS_DEBUG_DEVICE_PREINT != 0 (or GCSLAM_DEVICE_PREINT=1): gcs_scan / gcs_scan_begin compute the
+ * IMU window weights and the preintegration (deskew twist) on the device (k_preint) instead of the
+ * host prologue; ignored with the launch gate.  A/B knob and its parity test. */
+#define GCS_DEBUG_DEVICE_PREINT 7
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*GCS_N_STAGES*/, int64_t* counts /*GCS_N_STAGES*/,
                         int32_t reset);
@@ -332,6 +336,14 @@ int gcs_psd_project3(const double* M /*3x3*/, double* M_psd /*3x3*/, double* del
  * (n tiles; xcd != 0: grouped per XCD, n % 8 == 0), computed on `device` into order[n]. */
 int gcs_debug_tile_order(int32_t device, const uint8_t* active, const uint32_t* work, int32_t n, int32_t xcd,
                          int32_t* order);
+/* Test entry: k_preint on `device` over one IMU window (m samples; stamps[m], gyro/accel[m*3]):
+ * smooth_window_weights(stamps, t0, t1, sigma) then preintegrate_imu_relative_pose_jax
+ * (imu_preintegration.py:20-147) and the deskew twist se3_log(delta_pose) (pipeline.py:466-483;
+ * rotation_only zeroes its translation).  out[16] = xi[6], ess, delta_pose[6], delta_v[3]. */
+int gcs_debug_preintegrate(int32_t device, int32_t m, const double* stamps, const double* gyro, const double* accel,
+                           double t0, double t1, double sigma, const double* rotvec /*3*/, const double* gyro_bias /*3*/,
+                           const double* accel_bias /*3*/, const double* gravity /*3*/, int32_t rotation_only,
+                           double* out /*16*/);
 /* det-fixed Matrix-Fisher rotation R = U diag(1,1,det(UV^T)) V^T of H (matrix_fisher_evidence.py:215-222):
  * the same routine the device fold runs (polar Newton, SVD for reflections / rank deficiency) */
 int gcs_mf_rotation(const double* H /*3x3*/, double* R /*3x3*/);

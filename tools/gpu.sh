@@ -15,6 +15,8 @@
 #   pmapprof     rocprofv3 --kernel-trace --stats of tools/pmap_bench.py (assocprof: of tools/assoc_bench.py)
 #   ab           same-box A/B of two builds: A = libgcslam_hip.so, B = libgcslam_hip_$B.so
 #   envab        same-box A/B of an environment knob: B runs with $ENVB
+#   graphab      hipGraph vs stream launches of a six-kernel chain (tools/graph_ab, built in-tree)
+#   gaps         device idle gaps per kernel from prof2's trace (tools/trace_gaps.py)
 #   sweep        bench C2 + C3 per entry of SWEEP="name:lib_suffix:ENV=V,... ..." (library variants / knobs)
 # Env: O (output dir, default gpurun_out/run), REPS (A/B alternations), PYTEST_K (pytest -k filter).
 cd "${GRAFT_REPO_ROOT:-/root/repo}" || exit 1
@@ -99,6 +101,10 @@ step() {
           env $e timeout -k 10 300 python bench.py --config $cfg --steps ${SWEEP_STEPS:-60} --warmup 5 --no-cpu-baseline --no-c3 --no-live > "$O/sweep_${name}_$cfg.log" 2>&1 || return $?
         done
       done ;;
+    graphab) timeout -k 10 120 ./tools/graph_ab 2000 > "$O/graph_ab.json" 2>&1 ;;
+    gaps)  # device idle gaps of the C2 step, from prof2's kernel trace
+      local tr; tr=$(find "$O/prof_c2" -name '*kernel_trace.csv' | head -1)
+      [ -n "$tr" ] && python3 tools/trace_gaps.py "$tr" --json "$O/gaps_c2.json" > "$O/gaps_c2.txt" 2>&1 ;;
     *) echo "unknown step $1" >&2; return 2 ;;
   esac
 }
