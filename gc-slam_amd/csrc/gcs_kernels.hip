@@ -2518,10 +2518,12 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
   hipEvent_t ek = fold ? nullptr : e1;
   // legacy: the round-3 point kernel (one wave per SIMD; GCSLAM_POINTS=legacy / GCS_DEBUG_POINT_KERNEL), for A/B
   if (scale && !legacy && kPointLanes == 1 && (long)nblk * kBlock >= (long)a.cap) {  // one point per thread
-    // at most one wave per SIMD (GCSLAM_POINTS_WIDE=0 turns the wide form off, for A/B)
+    // at most one wave per SIMD: the wide form (all 16 candidate directions in one load group, one
+    // wave per SIMD) measured slower than the 4-wave form on the same grid -- C2 points 19.8-19.9 vs
+    // 18.9 us (profiles/r04/rcp/) -- so it is opt-in (GCSLAM_POINTS_WIDE=1), kept for A/B
     static const bool wide_ok = [] {
       const char* e = getenv("GCSLAM_POINTS_WIDE");
-      return !(e && atoi(e) == 0);
+      return e && atoi(e) != 0;
     }();
     const bool wide = wide_ok && (long)nblk * kBlock <= 1024L * 64;
     switch (a.k) {

@@ -527,30 +527,94 @@ __global__ __launch_bounds__(kPmRed) void k_pm_topk(const uint64_t* __restrict__
   uint64_t* rk = run_key + (size_t)t * G * k;
   uint32_t* rs = run_slot + (size_t)t * G * k;
   uint32_t* tk = tickets + (size_t)t * kTopMaxLevels * kTopNodes;
-  {  // leaf: bitonic sort of the chunk (padding last: key ~0, slot ~0 above every real pair)
+  {  // leaf: bitonic sort of the chunk (padding last: key ~0, slot ~0 above every real pair).  Each
+     // thread holds 4 consecutive entries in registers: strides 1-2 are exchanges inside the thread,
+     // strides 4-128 between lanes of one wave (shuffles, no barrier), and only strides 256-2048 go
+     // through LDS (10 of the 78 stages; the all-LDS network took a barrier per stage).  (key, slot)
+     // pairs are distinct, so any sorting network gives the same order.
+    uint64_t rk4[kTopEpt];
+    uint32_t rs4[kTopEpt];
 #pragma unroll
     for (int e = 0; e < kTopEpt; ++e) {
-      const int x = tid + e * kPmRed, q = g * kTopChunk + x;
-      s_k[x] = q < M ? keys[(size_t)t * M + q] : ~0ull;
-      s_s[x] = q < M ? (uint32_t)q : ~0u;
+      const int x = kTopEpt * tid + e, q = g * kTopChunk + x;
+      rk4[e] = q < M ? keys[(size_t)t * M + q] : ~0ull;
+      rs4[e] = q < M ? (uint32_t)q : ~0u;
     }
-    for (int size = 2; size <= kTopChunk; size <<= 1)
-      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+    const int lane = tid & 63;
+    for (int size = 2; size <= kTopChunk; size <<= 1) {
+      int stride = size >> 1;
+      if (stride >= 4 * 64) {  // the LDS stages of this size, then back to registers
         __syncthreads();
 #pragma unroll
-        for (int e = 0; e < kTopEpt / 2; ++e) {  // the chunk's kTopChunk / 2 pairs, two per thread
-          const int pr = tid + e * kPmRed;
-          const int x = ((pr & ~(stride - 1)) << 1) | (pr & (stride - 1)), y = x | stride;
-          const uint64_t kx = s_k[x], ky = s_k[y];
-          const uint32_t sx = s_s[x], sy = s_s[y];
-          if (topk_less(ky, sy, kx, sx) == ((x & size) == 0)) {
-            s_k[x] = ky;
-            s_k[y] = kx;
-            s_s[x] = sy;
-            s_s[y] = sx;
+        for (int e = 0; e < kTopEpt; ++e) {
+          s_k[kTopEpt * tid + e] = rk4[e];
+          s_s[kTopEpt * tid + e] = rs4[e];
+        }
+        for (; stride >= 4 * 64; stride >>= 1) {
+          __syncthreads();
+#pragma unroll
+          for (int e = 0; e < kTopEpt / 2; ++e) {  // the chunk's kTopChunk / 2 pairs, two per thread
+            const int pr = tid + e * kPmRed;
+            const int x = ((pr & ~(stride - 1)) << 1) | (pr & (stride - 1)), y = x | stride;
+            const uint64_t kx = s_k[x], ky = s_k[y];
+            const uint32_t sx = s_s[x], sy = s_s[y];
+            if (topk_less(ky, sy, kx, sx) == ((x & size) == 0)) {
+              s_k[x] = ky;
+              s_k[y] = kx;
+              s_s[x] = sy;
+              s_s[y] = sx;
+            }
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < kTopEpt; ++e) {
+          rk4[e] = s_k[kTopEpt * tid + e];
+          rs4[e] = s_s[kTopEpt * tid + e];
+        }
+      }
+      for (; stride >= kTopEpt; stride >>= 1) {  // partner lane = lane ^ (stride / 4), same e
+        const int lx = stride / kTopEpt;
+        const bool lower = (lane & lx) == 0;
+#pragma unroll
+        for (int e = 0; e < kTopEpt; ++e) {
+          const int x = kTopEpt * tid + e;
+          const uint64_t ok = (uint64_t)__shfl_xor((unsigned long long)rk4[e], lx, 64);
+          const uint32_t os = (uint32_t)__shfl_xor((int)rs4[e], lx, 64);
+          const bool asc = (x & size) == 0;
+          const bool other_less = topk_less(ok, os, rk4[e], rs4[e]);
+          // the lower index keeps the smaller entry when ascending, the larger otherwise
+          if (other_less == (lower == asc)) {
+            rk4[e] = ok;
+            rs4[e] = os;
           }
         }
       }
+      for (; stride > 0; stride >>= 1) {  // inside the thread: entries e and e ^ stride
+#pragma unroll
+        for (int e = 0; e < kTopEpt; ++e) {
+          const int f = e ^ stride;
+          if (f > e) {
+            const int x = kTopEpt * tid + e;
+            const bool asc = (x & size) == 0;
+            if (topk_less(rk4[f], rs4[f], rk4[e], rs4[e]) == asc) {
+              const uint64_t tk = rk4[e];
+              const uint32_t ts = rs4[e];
+              rk4[e] = rk4[f];
+              rs4[e] = rs4[f];
+              rk4[f] = tk;
+              rs4[f] = ts;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < kTopEpt; ++e) {
+      s_k[kTopEpt * tid + e] = rk4[e];
+      s_s[kTopEpt * tid + e] = rs4[e];
+    }
     __syncthreads();
   }
   int lv = 0, i = g;
@@ -1311,19 +1375,19 @@ __global__ void k_pm_stage_tiles(PmTileArgs a, int32_t* tiles, int64_t* ids) {
 
 // per association block b and listed tile t: the sum of fm over the block's rows with tpos == t (the
 // fused_mass_total terms, pipeline.py:1306-1308), a fixed-order tree per (b, t), into mapped memory
+// grid (blocks, tiles): one workgroup per (association block, tile) -- the tiles' sums used to run
+// one after another in the block's workgroup (n passes and n reductions in sequence)
 __global__ __launch_bounds__(kPmThreads) void k_pm_fm_sums(const double* fm, const int32_t* tpos, int bk, int n,
                                                            double* out) {
   __shared__ double lds[kPmThreads / 64];
-  const int b = blockIdx.x;
-  for (int t = 0; t < n; ++t) {
-    double s = 0.0;
-    for (int q = threadIdx.x; q < bk; q += kPmThreads) {
-      const size_t g = (size_t)b * bk + q;
-      s += tpos[g] == t ? fm[g] : 0.0;
-    }
-    s = block_sum_d<kPmThreads>(s, lds);
-    if (threadIdx.x == 0) out[b * n + t] = s;
+  const int b = blockIdx.x, t = blockIdx.y;
+  double s = 0.0;
+  for (int q = threadIdx.x; q < bk; q += kPmThreads) {
+    const size_t g = (size_t)b * bk + q;
+    s += tpos[g] == t ? fm[g] : 0.0;
   }
+  s = block_sum_d<kPmThreads>(s, lds);
+  if (threadIdx.x == 0) out[b * n + t] = s;
 }
 
 // device counters into the mapped buffer (one launch instead of a device-to-host copy)
@@ -2201,8 +2265,9 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   PMCHK(p, hipGetLastError());
   if ((size_t)nb * n * 8 > kSmall - kFmOff || (size_t)nprop * 8 > kFmOff - kWiOff)
     return pm_fail(p, GCS_ERR_ARG, "map update: stats exceed the mapped buffer");
-  hipLaunchKernelGGL(k_pm_fm_sums, dim3(nb), dim3(kPmThreads), 0, p->stream, (const double*)o.fm,
-                     (const int32_t*)o.tpos, B * K, n, (double*)(p->d_small + kFmOff));
+  if (n > 0)
+    hipLaunchKernelGGL(k_pm_fm_sums, dim3(nb, n), dim3(kPmThreads), 0, p->stream, (const double*)o.fm,
+                       (const int32_t*)o.tpos, B * K, n, (double*)(p->d_small + kFmOff));
   gcs_pmap_rows ra{};
   ra.Lambdas = o.lam;
   ra.thetas = o.th;
