@@ -35,6 +35,10 @@ namespace gcs {
 namespace {
 
 constexpr int kAsThreads = 256;
+#ifndef GCS_POOL_THREADS
+#define GCS_POOL_THREADS 128
+#endif
+constexpr int kPoolThreads = GCS_POOL_THREADS;
 // the Sinkhorn workgroup: 8 waves, 4 rows per thread at K <= 8 (K_mat rows in registers).  1024
 // threads (4 waves per SIMD, 128 VGPRs: the rows spill) measured slower: 3.2 vs 3.0 us per iteration,
 // 0.480 vs 0.422 ms per call (profiles/r03/assoc/)
@@ -263,19 +267,22 @@ __device__ __forceinline__ bool kless(unsigned long long ka, int pa, unsigned lo
   return ka < kb || (ka == kb && pa < pb);
 }
 
-// one workgroup per measurement row
+// one workgroup per measurement row: kPoolThreads = 128 (two waves) puts all 1,536 rows of the reference
+// sizes in flight at once (eight workgroups per CU by registers and LDS); 256 threads took two rounds
+// of workgroups (GCS_POOL_THREADS=256 for A/B; any split of the pool over the lanes gives the same
+// candidates, see the merge below)
 template <int KM>
-__global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsWork w, AsOut o) {
+__global__ __launch_bounds__(kPoolThreads) void k_as_pool(AsIn in, AsParams p, AsWork w, AsOut o) {
 #pragma clang fp contract(off)
   __shared__ int s_tix[kMaxStencil];
-  __shared__ unsigned long long s_wk[2][kAsThreads / 64];
-  __shared__ int s_wp[2][kAsThreads / 64];
+  __shared__ unsigned long long s_wk[2][kPoolThreads / 64];
+  __shared__ int s_wp[2][kPoolThreads / 64];
   __shared__ int s_sel[32];
-  __shared__ double s_thr[kAsThreads / 64];
+  __shared__ double s_thr[kPoolThreads / 64];
   // per wave: the ring of entries past the threshold (d_pos, pool position, view index)
   constexpr unsigned kRing = 512;  // >= 63 pending + PB x 64 appended per trip
-  __shared__ double s_rd[kAsThreads / 64][kRing];
-  __shared__ int s_rq[kAsThreads / 64][kRing], s_re[kAsThreads / 64][kRing];
+  __shared__ double s_rd[kPoolThreads / 64][kRing];
+  __shared__ int s_rq[kPoolThreads / 64][kRing], s_re[kPoolThreads / 64][kRing];
   const int i = blockIdx.x, t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const bool row_valid = in.valid[i] != 0;
   if (t < p.n_stencil) s_tix[t] = w.tix[(size_t)i * p.n_stencil + t];
@@ -312,10 +319,10 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
           const int ti = sq >= 0 ? s_tix[sq] : -1;
           if (ti < 0) continue;
           const size_t base = (size_t)ti * MV;
-          for (int o = t; o < MV; o += PB * kAsThreads) {
+          for (int o = t; o < MV; o += PB * kPoolThreads) {
 #pragma unroll
             for (int u = 0; u < PB; ++u) {
-              const int oo = o + u * kAsThreads;
+              const int oo = o + u * kPoolThreads;
               if (oo >= MV) break;
               const size_t e = base + oo;
               if (!in.vvalid[e]) continue;
@@ -338,7 +345,7 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
         __syncthreads();
         double d = s_thr[0];
 #pragma unroll
-        for (int v = 1; v < kAsThreads / 64; ++v) d = fmin(d, s_thr[v]);
+        for (int v = 1; v < kPoolThreads / 64; ++v) d = fmin(d, s_thr[v]);
         __syncthreads();  // (s_thr is written again by a second round)
         thr = d + p.beta;  // (inf when every wave has fewer than K valid entries: the second round)
       }
@@ -370,10 +377,10 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
     for (int sq = 0; sq < S; ++sq) {
       const int ti = s_tix[sq];
       const size_t base = (size_t)(ti < 0 ? 0 : ti) * MV;
-      for (int ow = t & ~63; ow < MV; ow += PB * kAsThreads) {  // wave-uniform trips (ballots inside)
+      for (int ow = t & ~63; ow < MV; ow += PB * kPoolThreads) {  // wave-uniform trips (ballots inside)
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
-          const int oo = ow + lane + u * kAsThreads;
+          const int oo = ow + lane + u * kPoolThreads;
           const bool in_tile = oo < MV;
           const int q = sq * MV + oo;
           bool valid = false;
@@ -424,7 +431,7 @@ __global__ __launch_bounds__(kAsThreads) void k_as_pool(AsIn in, AsParams p, AsW
       bk = s_wk[buf][0];
       bp = s_wp[buf][0];
 #pragma unroll
-      for (int v = 1; v < kAsThreads / 64; ++v)
+      for (int v = 1; v < kPoolThreads / 64; ++v)
         if (kless(s_wk[buf][v], s_wp[buf][v], bk, bp)) {
           bk = s_wk[buf][v];
           bp = s_wp[buf][v];
@@ -1312,7 +1319,7 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   if (bad_policy) {
     hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, 0);
   } else if (km == 8) {
-    hipLaunchKernelGGL(k_as_pool<8>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL(k_as_pool<8>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
     // three rows per thread when they cover the rows (the reference's 1,536 = 3 x 512): no padding
     // row in the K v / K^T u sums
     if (3 * kShThreads < rpt_for(8) * kShThreads && p.n <= 3 * kShThreads)
@@ -1320,10 +1327,10 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
     else
       hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   } else if (km == 16) {
-    hipLaunchKernelGGL(k_as_pool<16>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL(k_as_pool<16>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
     hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   } else {
-    hipLaunchKernelGGL(k_as_pool<32>, dim3(p.n), dim3(kAsThreads), 0, s, in, p, w, out);
+    hipLaunchKernelGGL(k_as_pool<32>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
     hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
   }
   ASCHK(c, hipGetLastError());

@@ -98,6 +98,10 @@ struct gcs_ctx {
   // previous scan's k_pushforward (on push_stream) still reads the other
   uint8_t* d_flags = nullptr;
   uint8_t* d_flags_buf[2] = {nullptr, nullptr};
+  // zeroed for the next scan by gcs_scan's k_pt (PtClear): that scan's k_budget skips the clears
+  bool counts_clean = false;
+  bool flags_clean[2] = {false, false};
+  bool pt_clear = true;  // GCSLAM_PT_CLEAR=0 / GCS_DEBUG_PT_CLEAR 0: k_budget clears as before (A/B)
   int flags_cur = 0;
   uint8_t* d_touched = nullptr;     // per bin: the map holds mass (k_map_derive / k_pushforward)
   uint8_t* d_tile_dirty = nullptr;  // k_bins_scale: tile output not the zero-bin values (persistent)
@@ -448,6 +452,12 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true) {
   ba.n_zero32 = c->d_counts ? c->B : 0;
   ba.zero8 = c->d_flags;
   ba.n_zero8 = c->d_flags ? c->B + bins_scale_blocks(c->B, c->tile_bins) : 0;
+  if (c->counts_clean) ba.n_zero32 = 0;  // the last scan's k_pt zeroed them
+  c->counts_clean = false;
+  if (c->d_flags_buf[0]) {
+    if (c->flags_clean[c->flags_cur]) ba.n_zero8 = 0;
+    c->flags_clean[c->flags_cur] = false;
+  }
   c->budget_blocks = red_blocks(std::max(n_raw, 1));
   c->budget_pending = true;
   StageEv ev = stage_ev(c, ST_BUDGET);
@@ -651,12 +661,27 @@ int wait_mirror(gcs_ctx* c) {
   return GCS_OK;
 }
 
-int stage_pt(gcs_ctx* c, bool to_host = false) {
+// clear_next (gcs_scan): k_pt also zeroes the bucket counts (the bin kernel, their last reader, is
+// behind it on this stream) and the other flag buffer -- the next scan's -- whose last reader, the
+// previous scan's pushforward, completed before this scan's bin kernel (join_push); the next
+// k_budget then only sums the weights.  Measured: DESIGN.md section 5 (round 4).
+int stage_pt(gcs_ctx* c, bool to_host = false, bool clear_next = false) {
   StageEv ev = stage_ev(c, ST_PT);
   if (to_host) c->h_scalars[SC_COUNT] = 0.0;  // re-armed: the fold writes 1 after the mirror
+  PtClear clr{};
+  if (clear_next && c->pt_clear && c->d_counts && c->d_flags_buf[0]) {
+    clr.c32 = c->d_counts;
+    clr.n32 = c->B;
+    clr.c8 = c->d_flags_buf[c->flags_cur ^ 1];
+    clr.n8 = c->B + bins_scale_blocks(c->B, c->tile_bins);
+  }
   HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
                       to_host ? c->d_scalars_mirror : nullptr, c->d_flags, c->d_touched, c->stream,
-                      ev.e0, ev.e1));
+                      ev.e0, ev.e1, clr));
+  if (clr.c32) {
+    c->counts_clean = true;
+    c->flags_clean[c->flags_cur ^ 1] = true;
+  }
   if (to_host) HIPCHK(c, hipEventRecord(c->ev_stages, c->stream));
   c->stages_done = false;
   return GCS_OK;
@@ -819,7 +844,7 @@ int scan_front(gcs_ctx* c, const gcs_scan_inputs* in, uint64_t seq) {
     return rc;
   if (int rc = join_push(c)) return rc;
   if (int rc = stage_bins(c)) return rc;
-  if (int rc = stage_pt(c, /*to_host=*/true)) return rc;
+  if (int rc = stage_pt(c, /*to_host=*/true, /*clear_next=*/true)) return rc;
   return stage_tile_order(c);
 }
 
@@ -1043,6 +1068,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_gate_xi, 8 * sizeof(double)))) return GCS_ERR_HIP;
   if (const char* g = getenv("GCSLAM_GATE")) c->gate_on = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_DEVICE_PREINT")) c->device_preint = atoi(g) != 0;
+  if (const char* g = getenv("GCSLAM_PT_CLEAR")) c->pt_clear = atoi(g) != 0;
   if (bad(hipHostMalloc(&c->h_preint_out, 16 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent)))
     return GCS_ERR_HIP;
   if (cfg->mode == GCS_MODE_SCALE) {
@@ -1193,6 +1219,9 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
       return GCS_OK;
     case GCS_DEBUG_DEVICE_PREINT:
       c->device_preint = value != 0;
+      return GCS_OK;
+    case GCS_DEBUG_PT_CLEAR:
+      c->pt_clear = value != 0;
       return GCS_OK;
     case GCS_DEBUG_LAUNCH_GATE:
       if (value < -1 || value > 1) return fail(c, GCS_ERR_ARG, "launch gate: -1, 0 or 1");
@@ -1990,7 +2019,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     if (int rc_ = join_push(c)) return rc_;  // the bin kernel reads the map the previous scan's pushforward wrote
     if ((rc = stage_bins(c))) return rc;  // scale mode: Matrix-Fisher reduction + R_mf fused in
     if (c->cfg.mode != GCS_MODE_SCALE && (rc = stage_mf(c))) return rc;
-    if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+    if ((rc = stage_pt(c, /*to_host=*/true, /*clear_next=*/true))) return rc;
     if ((rc = stage_tile_order(c))) return rc;
     st.Ts = clk::now();
     if ((rc = scan_imu_odom(c, in, st, out))) return rc;
@@ -2012,7 +2041,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
                            in->xyz_format == 1)))
       return rc;
     if ((rc = stage_bins(c))) return rc;
-    if ((rc = stage_pt(c, /*to_host=*/true))) return rc;
+    if ((rc = stage_pt(c, /*to_host=*/true, /*clear_next=*/true))) return rc;
     if ((rc = stage_tile_order(c))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->stages_done = true;

@@ -34,6 +34,15 @@ struct BudgetArgs {
   int n_zero8;
 };
 
+// Clears k_pt does for the next scan (gcs_scan only): its bucket counts (n32 words) and its
+// active-flag buffer (n8 bytes)
+struct PtClear {
+  uint32_t* c32 = nullptr;
+  long n32 = 0;
+  uint8_t* c8 = nullptr;
+  long n8 = 0;
+};
+
 struct PointKernelArgs {
   // raw PointCloud2-like input (device)
   const uint8_t* xyz;  // float x,y,z at byte offsets 0,4,8 of each record (double when xyz_f64)
@@ -195,7 +204,7 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 // k_pushforward skip bins that are zero in both the scan and the map
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
                      double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
-                     hipEvent_t e0, hipEvent_t e1);
+                     hipEvent_t e0, hipEvent_t e1, PtClear clr = PtClear{});
 // the next scan's bin-tile dispatch order from this scan's active tiles and their staged records
 hipError_t launch_tile_order(const uint8_t* active, const uint32_t* work, int n, int* order, hipStream_t s);
 // xcd: the XCD-grouped order (k_tile_order_xcd, n % 8 == 0), else the class order alone

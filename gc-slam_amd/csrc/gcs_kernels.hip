@@ -213,33 +213,26 @@ __global__ __launch_bounds__(kBlock) void k_parse_time_scale(double* t, int n, c
 // Also clears the scale-mode bucketing state of this scan (counts, flags, look-back status),
 // replacing three memsets.  mass_scale = total_mass_in / (total_mass_selected + eps_mass)
 // (point_budget.py:80-84) is produced by k_final<FIN_BUDGET>.
+// zero nb bytes at p with the grid's threads: 16-B stores for the aligned body, byte stores for the
+// head and tail (nb and p need no alignment; nb <= 0 or p null: nothing)
+__device__ __forceinline__ void clear_bytes16(uint8_t* p, long nb, long gid, long gsz) {
+  if (!p || nb <= 0) return;
+  long head = (long)((16 - ((uintptr_t)p & 15)) & 15);
+  head = head > nb ? nb : head;
+  for (long j = gid; j < head; j += gsz) p[j] = 0u;
+  const long nq = (nb - head) / 16;
+  uint4* q = reinterpret_cast<uint4*>(p + head);
+  for (long j = gid; j < nq; j += gsz) q[j] = make_uint4(0u, 0u, 0u, 0u);
+  for (long j = head + 16 * nq + gid; j < nb; j += gsz) p[j] = 0u;
+}
+
 __global__ __launch_bounds__(kBlock) void k_budget(BudgetArgs a) {
   __shared__ double lds[kWaves * 2];
   const int gid = blockIdx.x * kBlock + threadIdx.x, gsz = gridDim.x * kBlock;
   // 16-B stores for the aligned body, element stores for the head and tail (1-B stores ran the C3
   // clear at ~0.4 TB/s)
-  {
-    uint8_t* p = reinterpret_cast<uint8_t*>(a.zero32);
-    const long nb = 4L * a.n_zero32;
-    long head = (long)((16 - ((uintptr_t)p & 15)) & 15);
-    head = head > nb ? nb : head;
-    for (long j = gid; j < head / 4; j += gsz) a.zero32[j] = 0u;
-    const long nq = (nb - head) / 16;
-    uint4* q = reinterpret_cast<uint4*>(p + head);
-    for (long j = gid; j < nq; j += gsz) q[j] = make_uint4(0u, 0u, 0u, 0u);
-    for (long j = (head + 16 * nq) / 4 + gid; j < a.n_zero32; j += gsz) a.zero32[j] = 0u;
-  }
-  {
-    uint8_t* p = a.zero8;
-    const long nb = a.n_zero8;
-    long head = (long)((16 - ((uintptr_t)p & 15)) & 15);
-    head = head > nb ? nb : head;
-    for (long j = gid; j < head; j += gsz) p[j] = 0u;
-    const long nq = (nb - head) / 16;
-    uint4* q = reinterpret_cast<uint4*>(p + head);
-    for (long j = gid; j < nq; j += gsz) q[j] = make_uint4(0u, 0u, 0u, 0u);
-    for (long j = head + 16 * nq + gid; j < nb; j += gsz) p[j] = 0u;
-  }
+  clear_bytes16(reinterpret_cast<uint8_t*>(a.zero32), 4L * a.n_zero32, gid, gsz);
+  clear_bytes16(a.zero8, a.n_zero8, gid, gsz);
   double v[2] = {0.0, 0.0};
   for (int j = gid; j < a.n_raw; j += gsz) {
     double x = a.w[j];
@@ -1911,11 +1904,19 @@ __device__ __forceinline__ void final_epilogue(const double (&v)[NV], double* sc
   }
 }
 
+// clr32 / clr8 (may be null): the next scan's bucket counts and active-flag buffer, zeroed here (their
+// last readers -- the bin kernel, the previous scan's pushforward -- are behind on the device), so
+// the next k_budget skips the clears (PtClear in gcs_kernels.h)
 __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, const double* __restrict__ map,
                                                const double* __restrict__ derived, int B, double* scalars,
                                                double* partials, const uint8_t* __restrict__ act,
-                                               const uint8_t* __restrict__ touched) {
+                                               const uint8_t* __restrict__ touched, PtClear clr) {
   __shared__ double lds[kWaves * pstride<kPtNV>()];
+  {
+    const long gid = (long)blockIdx.x * kBlock + threadIdx.x, gsz = (long)gridDim.x * kBlock;
+    clear_bytes16(reinterpret_cast<uint8_t*>(clr.c32), 4L * clr.n32, gid, gsz);
+    clear_bytes16(clr.c8, clr.n8, gid, gsz);
+  }
   double R[9];
 #pragma unroll
   for (int k = 0; k < 9; ++k) R[k] = scalars[SC_MF_R + k];
@@ -2627,12 +2628,12 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
                      double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
-                     hipEvent_t e0, hipEvent_t e1) {
+                     hipEvent_t e0, hipEvent_t e1, PtClear clr) {
   // (measured slower and removed: a last-block fold in k_pt, ticket + agent-scope release per block:
   // 16.4 vs 12.3 us at C2, 46 vs 25 us at C3; the same with sc1 stores / loads and no fence: C2
   // 105.4-105.9 vs 103.5-104.1 us per step, profiles/r03/ptfold/)
   hipExtLaunchKernelGGL(k_pt, dim3(nblk), dim3(kBlock), 0, s, e0, nullptr, 0, scan, map, derived, B, scalars, partials,
-                        act, touched);
+                        act, touched, clr);
   GCS_FINAL_M(kPtNV, 0u, FIN_PT, nblk, s, e1, partials, scalars, mirror);
   return hipGetLastError();
 }

@@ -500,6 +500,9 @@ __global__ __launch_bounds__(NT) void k_pm_select_reg(const uint64_t* __restrict
 // index plus the count of the other run's smaller entries (binary search in LDS).  Runs live in
 // run_key / run_slot at the first leaf of their node (k entries per leaf); the writer's stores are
 // released (agent-scope fence, barrier) before its ticket, the second arrival acquires before reading.
+#ifndef GCS_TOPK_SC1
+#define GCS_TOPK_SC1 1  // write-through run hand-off (0: the acq_rel ticket, for A/B)
+#endif
 constexpr int kTopEpt = 4;                  // slots per thread in a leaf
 constexpr int kTopChunk = kTopEpt * kPmRed;  // slots per leaf: 4,096 (13 leaves, 4 merge levels at 50,000)
 constexpr int kTopMaxLevels = 8;             // up to 128 leaves per tile (M <= 524,288)
@@ -632,6 +635,30 @@ __global__ __launch_bounds__(kPmRed) void k_pm_topk(const uint64_t* __restrict__
     }
     // publish this run, then take the node's ticket
     const size_t mine = (size_t)(i << lv) * k;
+    uint32_t* ticket = tk + lv * kTopNodes + (i >> 1);
+#if GCS_TOPK_SC1
+    // The hand-off of cdna_hip_programming.md Guideline 16 (counter form): the run is stored
+    // write-through (agent-scope relaxed atomic stores: sc1), every wave drains its stores before the
+    // barrier, ONE lane adds to the ticket relaxed -- no release fence, whose L2 write-back the
+    // acq_rel ticket paid once per workgroup and level -- and the second arrival's lane takes ONE
+    // agent-scope acquire (the CU's stale lines dropped) before the workgroup's plain loads.
+    for (int r = tid; r < L; r += kPmRed) {
+      __hip_atomic_store(rk + mine + r, s_k[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(rs + mine + r, s_s[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old != 0u) {
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      s_go = old;
+    }
+    __syncthreads();
+#else
     for (int r = tid; r < L; r += kPmRed) {
       rk[mine + r] = s_k[r];
       rs[mine + r] = s_s[r];
@@ -640,13 +667,13 @@ __global__ __launch_bounds__(kPmRed) void k_pm_topk(const uint64_t* __restrict__
     // fence per thread wrote the L2 back once per wave: 0.75 ms per call), and the second arrival's
     // acquire on the same atomic before the workgroup reads the sibling's run
     __syncthreads();
-    uint32_t* ticket = tk + lv * kTopNodes + (i >> 1);
     if (tid == 0) {
       const uint32_t old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       if (old != 0u) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
       s_go = old;
     }
     __syncthreads();
+#endif
     if (s_go == 0u) return;  // the sibling merges
     const int Ls = topk_len(M, k, lv, sib);
     const size_t other = (size_t)(sib << lv) * k;

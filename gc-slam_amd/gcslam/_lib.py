@@ -100,6 +100,7 @@ DEBUG_SORTED_BUCKETS, DEBUG_BUCKET_CAPACITY = 3, 4
 DEBUG_LAUNCH_GATE = 5
 DEBUG_POINT_KERNEL = 6
 DEBUG_DEVICE_PREINT = 7
+DEBUG_PT_CLEAR = 8
 MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 

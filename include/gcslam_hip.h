@@ -225,6 +225,10 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * IMU window weights and the preintegration (deskew twist) on the device (k_preint) instead of the
  * host prologue; ignored with the launch gate.  A/B knob and its parity test. */
 #define GCS_DEBUG_DEVICE_PREINT 7
+/* GCS_DEBUG_PT_CLEAR (default 1; GCSLAM_PT_CLEAR=0 turns it off): gcs_scan's k_pt zeroes the next
+ * scan's bucket counts and active-flag buffer, so that scan's k_budget only sums the weights; 0 keeps
+ * the clears in k_budget (A/B knob and its bitwise test). */
+#define GCS_DEBUG_PT_CLEAR 8
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*GCS_N_STAGES*/, int64_t* counts /*GCS_N_STAGES*/,
                         int32_t reset);

@@ -454,3 +454,32 @@ def test_launch_gate_matches_ungated_bitwise_and_times_out_loudly():
     for a, b in zip(outs[0], outs[1]):
         for x, y in zip(a, b):
             assert np.array_equal(x, y)
+
+
+@pytest.mark.parametrize("capacity", [32, 4])
+def test_pt_clear_handoff_matches_budget_clears_bitwise(capacity):
+    """gcs_scan's k_pt zeroing the next scan's bucket counts and flag buffer (GCS_DEBUG_PT_CLEAR = 1,
+    the default; k_budget then only sums the weights) against k_budget doing the clears (0): four
+    consecutive scans agree bit for bit -- the flag buffers alternate, so every buffer is reused
+    after a k_pt clear.  capacity 4: the first scan overflows the direct rows and is redone sorted
+    (a second k_budget on the same buffers, after the first attempt's k_pt cleared the counts)."""
+    from gcslam import _lib as L
+    syn = _synthetic()
+    outs = []
+    for clear in (1, 0):
+        ctx = _ctx(n_bins=20000 if capacity == 32 else 2000, n_points_cap=8192, mode="scale")
+        ctx.set_debug(L.DEBUG_PT_CLEAR, clear)
+        if capacity != 32:
+            ctx.set_debug(L.DEBUG_BUCKET_CAPACITY, capacity)
+        res = []
+        for k in range(4):
+            sc = syn.make_scan(8192, 61 + k)
+            rec, t, w = device_scan(sc)
+            o = ctx.scan(rec, 16, t, w, 8192, **scan_kwargs(sc))
+            res.append((ctx.get_scan_stats(), ctx.get_map()[0], np.array(o.belief.L[:]), np.array(o.z_t[:]),
+                        np.array(o.cert[:])))
+        outs.append(res)
+        ctx.close()
+    for a, b in zip(outs[0], outs[1]):
+        for x, y in zip(a, b):
+            assert np.array_equal(x, y, equal_nan=True)
