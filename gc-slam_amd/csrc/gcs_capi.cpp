@@ -102,6 +102,7 @@ struct gcs_ctx {
   bool counts_clean = false;
   bool flags_clean[2] = {false, false};
   bool pt_clear = true;  // GCSLAM_PT_CLEAR=0 / GCS_DEBUG_PT_CLEAR 0: k_budget clears as before (A/B)
+  int budget_max = 128;  // k_budget's block cap (GCSLAM_BUDGET_BLOCKS, 1..1024)
   int flags_cur = 0;
   uint8_t* d_touched = nullptr;     // per bin: the map holds mass (k_map_derive / k_pushforward)
   uint8_t* d_tile_dirty = nullptr;  // k_bins_scale: tile output not the zero-bin values (persistent)
@@ -458,7 +459,9 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true) {
     if (c->flags_clean[c->flags_cur]) ba.n_zero8 = 0;
     c->flags_clean[c->flags_cur] = false;
   }
-  c->budget_blocks = red_blocks(std::max(n_raw, 1));
+  // k_budget's grid: at most budget_max blocks (every k_points block folds all of its partial rows,
+  // and on a busy GPU -- the previous scan's pushforward -- each block waits for a CU slot)
+  c->budget_blocks = std::min(red_blocks(std::max(n_raw, 1)), c->budget_max);
   c->budget_pending = true;
   StageEv ev = stage_ev(c, ST_BUDGET);
   if (!ev.e0 && c->push_async && !t_on_worker) return submit_budget(c, ba, c->budget_blocks, s);
@@ -1069,6 +1072,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (const char* g = getenv("GCSLAM_GATE")) c->gate_on = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_DEVICE_PREINT")) c->device_preint = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_PT_CLEAR")) c->pt_clear = atoi(g) != 0;
+  if (const char* g = getenv("GCSLAM_BUDGET_BLOCKS")) c->budget_max = std::max(1, std::min(1024, atoi(g)));
   if (bad(hipHostMalloc(&c->h_preint_out, 16 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent)))
     return GCS_ERR_HIP;
   if (cfg->mode == GCS_MODE_SCALE) {
