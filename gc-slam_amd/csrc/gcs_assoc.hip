@@ -852,7 +852,10 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const double ua = 1.0 / (1.0 + p.tau_a / eps), vb = 1.0 / (1.0 + p.tau_b / eps);
   const double bk = 1.0 / (double)K;
 #pragma unroll
-  for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
+  for (int q = 0; q < RPT * KM; ++q) {  // K_mat: the short exp in its range (as the iterations), the library beyond
+    const double a = -X[q] / eps;
+    X[q] = ((okm >> q) & 1u) ? (fabs(a) < 700.0 ? exp_fast(a) : exp(a)) : 0.0;
+  }
   SH_STAMP(2);
   double u[RPT], v[KM];
 #pragma unroll
@@ -921,18 +924,35 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   double acc[7 + KM];
 #pragma unroll
   for (int q = 0; q < 7 + KM; ++q) acc[q] = 0.0;
+  // the cost rows and the row flags first, all loads in flight together: in the loop below every
+  // load would wait behind the preceding resp store it may alias (8.6 us of serial round trips)
+  // (the reference shape, 3 rows x 8 candidates; the wider instantiations keep the direct loads:
+  // their registers are already at the limit)
+  constexpr bool kPre = RPT * KM <= 24;
+  double Cr[kPre ? RPT * KM : 1];
+  bool rvj[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int r = t + j * kShThreads;
+    rvj[j] = r < N && in.valid[r] != 0;
+    if constexpr (kPre) {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) Cr[j * KM + k] = r < N && k < K ? o.cost[(size_t)r * K + k] : 0.0;
+    }
+  }
 #pragma unroll
   for (int j = 0; j < RPT; ++j) {
     const int r = t + j * kShThreads;
     if (r >= N) continue;
-    const bool rv = in.valid[r] != 0;
+    const bool rv = rvj[j];
     double rm = 0.0;
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
       if (k >= K) continue;
       const double pik = (u[j] * X[j * KM + k]) * v[k];
       rm += pik;
-      acc[4] += pik * o.cost[(size_t)r * K + k];
+      if constexpr (kPre) acc[4] += pik * Cr[j * KM + k];
+      else acc[4] += pik * o.cost[(size_t)r * K + k];
       acc[6] += pik;
       acc[7 + k] += pik;
       o.resp[(size_t)r * K + k] = rv ? pik : 0.0;
