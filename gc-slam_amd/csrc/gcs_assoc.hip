@@ -852,10 +852,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const double ua = 1.0 / (1.0 + p.tau_a / eps), vb = 1.0 / (1.0 + p.tau_b / eps);
   const double bk = 1.0 / (double)K;
 #pragma unroll
-  for (int q = 0; q < RPT * KM; ++q) {  // K_mat: the short exp in its range (as the iterations), the library beyond
-    const double a = -X[q] / eps;
-    X[q] = ((okm >> q) & 1u) ? (fabs(a) < 700.0 ? exp_fast(a) : exp(a)) : 0.0;
-  }
+  for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
   SH_STAMP(2);
   double u[RPT], v[KM];
 #pragma unroll
