@@ -46,6 +46,9 @@ constexpr int kPoolThreads = GCS_POOL_THREADS;
 #define GCS_SH_THREADS 512
 #endif
 constexpr int kShThreads = GCS_SH_THREADS;
+#ifndef GCS_SH_LOGA
+#define GCS_SH_LOGA 1  // 0: u = pow(a / Kv, ua) with the quotient in every iteration (A/B)
+#endif
 constexpr int kShCR = 16 * 1024 / kShThreads;  // Sinkhorn row capacity: N <= kShCR * kShThreads / KM
 constexpr int kMaxStencil = 64;
 // GCS_SH_PROBE (timing probe builds only): wall-clock stamps of the Sinkhorn's phases, printed by the
@@ -822,6 +825,14 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   SH_STAMP(1);
 #pragma unroll
   for (int j = 0; j < RPT; ++j) va[j] = va[j] / sum_a;
+#if GCS_SH_LOGA
+  // log a once: each iteration's u = (a / Kv)^ua is exp(ua (log a - log Kv)) -- the quotient (and its
+  // rcp / Newton / residual steps) leaves the loop (rounding-level change; the tests' 1e-9 bars)
+  double lva[RPT];
+#pragma unroll
+  for (int j = 0; j < RPT; ++j)
+    lva[j] = va[j] >= 2.2250738585072014e-308 && va[j] <= 1.7976931348623157e308 ? log_fast(va[j]) : NAN;
+#endif
   uint32_t okm = 0;
 #pragma unroll
   for (int j = 0; j < RPT; ++j)
@@ -876,7 +887,20 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
       double kv = 0.0;
 #pragma unroll
       for (int k = 0; k < KM; ++k) kv = fma(X[j * KM + k], v[k], kv);
+#if GCS_SH_LOGA
+      const double kvv = kv + 1e-12;
+      double uj = 0.0;
+      if (r < N) {
+        const double a_ = ua * (lva[j] - log_fast(kvv));
+        // (NaN lva: a zero or denormal marginal; a Kv outside the short log's range; |a_| >= 700)
+        uj = kvv >= 2.2250738585072014e-308 && kvv <= 1.7976931348623157e308 && fabs(a_) < 700.0
+                 ? exp_fast(a_)
+                 : pow_fast(div_fast(va[j], kvv), ua);
+      }
+      u[j] = uj;
+#else
       u[j] = r < N ? pow_fast(div_fast(va[j], kv + 1e-12), ua) : 0.0;
+#endif
     }
     double c[KM];
 #pragma unroll
