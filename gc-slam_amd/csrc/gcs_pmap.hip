@@ -990,11 +990,71 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmStore st, 
   vals[g] = (uint32_t)g;
 }
 
-// one lane per (tile, slot) group: for each block in order, d = the block's rows summed in row order,
-// then slot += d -- the reference's block-by-block fuse calls (pipeline.py:1272-1327)
+// Long runs of one (tile, slot, block) key -- many measurements associated to the same primitive, as
+// in a sparse map -- were one lane's serial walk (the live path's map update spent 0.5 ms in it).  A run
+// longer than kFuseChunk rows is cut into chunks: the run's first chunk ends at the first position
+// b with b % kFuseChunk == 0 and b - kFuseChunk at or after the run start, later chunks at every such
+// b; one lane per chunk sums its rows in row order into P (field-major, kFT fields) and its length
+// into Lc, and the group's lane adds the chunk sums in order.  Runs of at most kFuseChunk rows are
+// never cut: their sums are bitwise the per-row walk's.  (Deterministic either way.)
+constexpr int kFuseChunk = 64;
+constexpr int kFT = 28;  // L 9 | theta 3 | eta 9 | r w | r | camera w | lidar w | rgb accumulation 3
+__device__ __forceinline__ bool fuse_long_start(const uint32_t* keys, int n, int pos, uint32_t key) {
+  if (pos == 0 || keys[pos - 1] != key) return pos + kFuseChunk < n && keys[pos + kFuseChunk] == key;
+  return pos % kFuseChunk == 0 && pos >= kFuseChunk && keys[pos - kFuseChunk] == key;
+}
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_chunks(PmRows r, const uint32_t* keys, const uint32_t* vals,
+                                                               double* P, int* Lc) {
+#pragma clang fp contract(off)
+  const int pos = blockIdx.x * kPmThreads + threadIdx.x;
+  if (pos >= r.n) return;
+  const uint32_t key = keys[pos];
+  if (key == kNoKey || !fuse_long_start(keys, r.n, pos, key)) return;
+  constexpr int ne = 3 * kNL;
+  static_assert(9 + 3 + ne + 4 + 3 == kFT, "fuse chunk layout");
+  double dL[9], dth[3], de[ne], dw = 0.0, drs = 0.0, dcam = 0.0, dlid = 0.0, dacc[3] = {0.0, 0.0, 0.0};
+  for (int c = 0; c < 9; ++c) dL[c] = 0.0;
+  for (int c = 0; c < 3; ++c) dth[c] = 0.0;
+  for (int c = 0; c < ne; ++c) de[c] = 0.0;
+  int q = pos;
+  for (; q < r.n && keys[q] == key; ++q) {
+    if (q > pos && q % kFuseChunk == 0 && keys[q - kFuseChunk] == key) break;  // the next chunk's start
+    const size_t row = vals[q];
+    const double rr = r.resp[row] * 1.0;
+    for (int c = 0; c < 9; ++c) dL[c] = dL[c] + rr * r.lam[9 * row + c];
+    for (int c = 0; c < 3; ++c) dth[c] = dth[c] + rr * r.th[3 * row + c];
+    for (int c = 0; c < ne; ++c) de[c] = de[c] + rr * r.eta[(size_t)ne * row + c];
+    const double rw = rr * r.w[row];
+    dw = dw + rw;
+    drs = drs + rr;
+    if (r.src) {
+      const int sv = r.src[row];
+      const double wc = rw * (sv == 0 ? 1.0 : 0.0);
+      dcam = dcam + wc;
+      dlid = dlid + rw * (sv == 1 ? 1.0 : 0.0);
+      if (r.col)
+        for (int c = 0; c < 3; ++c) dacc[c] = dacc[c] + clip01(r.col[3 * row + c]) * wc;
+    }
+  }
+  const size_t n = (size_t)r.n;
+  for (int c = 0; c < 9; ++c) P[c * n + pos] = dL[c];
+  for (int c = 0; c < 3; ++c) P[(9 + c) * n + pos] = dth[c];
+  for (int c = 0; c < ne; ++c) P[(12 + c) * n + pos] = de[c];
+  P[21 * n + pos] = dw;
+  P[22 * n + pos] = drs;
+  P[23 * n + pos] = dcam;
+  P[24 * n + pos] = dlid;
+  for (int c = 0; c < 3; ++c) P[(25 + c) * n + pos] = dacc[c];
+  Lc[pos] = q - pos;
+}
+
+// one lane per (tile, slot) group: for each block in order, d = the block's rows summed in row order
+// (a long run: its chunk sums in order, k_pm_fuse_chunks), then slot += d -- the reference's
+// block-by-block fuse calls (pipeline.py:1272-1327)
 __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st, const int32_t* tiles, PmRows r,
                                                                      const uint32_t* keys, const uint32_t* vals,
-                                                                     int nb, long long seq) {
+                                                                     int nb, long long seq, const double* P,
+                                                                     const int* Lc) {
 #pragma clang fp contract(off)
   const int g = blockIdx.x * kPmThreads + threadIdx.x;
   if (g >= r.n) return;
@@ -1012,6 +1072,45 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st,
     for (int c = 0; c < 9; ++c) dL[c] = 0.0;
     for (int c = 0; c < 3; ++c) dth[c] = 0.0;
     for (int c = 0; c < ne; ++c) de[c] = 0.0;
+    if (P && fuse_long_start(keys, r.n, pos, kb)) {  // a long run: its chunk sums, in order
+      const size_t n = (size_t)r.n;
+      bool first = true;
+      while (pos < r.n && keys[pos] == kb) {
+        const int len = Lc[pos];
+        if (first) {
+          for (int c = 0; c < 9; ++c) dL[c] = P[c * n + pos];
+          for (int c = 0; c < 3; ++c) dth[c] = P[(9 + c) * n + pos];
+          for (int c = 0; c < ne; ++c) de[c] = P[(12 + c) * n + pos];
+          dw = P[21 * n + pos];
+          drs = P[22 * n + pos];
+          if (r.src) {
+            dcam = P[23 * n + pos];
+            dlid = P[24 * n + pos];
+            if (r.col) {
+              for (int c = 0; c < 3; ++c) dacc[c] = P[(25 + c) * n + pos];
+              dden = dcam;
+            }
+          }
+          first = false;
+        } else {
+          for (int c = 0; c < 9; ++c) dL[c] = dL[c] + P[c * n + pos];
+          for (int c = 0; c < 3; ++c) dth[c] = dth[c] + P[(9 + c) * n + pos];
+          for (int c = 0; c < ne; ++c) de[c] = de[c] + P[(12 + c) * n + pos];
+          dw = dw + P[21 * n + pos];
+          drs = drs + P[22 * n + pos];
+          if (r.src) {
+            const double wc = P[23 * n + pos];
+            dcam = dcam + wc;
+            dlid = dlid + P[24 * n + pos];
+            if (r.col) {
+              for (int c = 0; c < 3; ++c) dacc[c] = dacc[c] + P[(25 + c) * n + pos];
+              dden = dden + wc;
+            }
+          }
+        }
+        pos += len;
+      }
+    }
     for (; pos < r.n && keys[pos] == kb; ++pos) {
       const size_t row = vals[pos];
       const double rr = r.resp[row] * 1.0;
@@ -1596,6 +1695,9 @@ struct gcs_pmap {
   void* ftemp = nullptr;
   size_t ftemp_bytes = 0;
   int frows = 0;
+  double* fterm = nullptr;  // step 12b: chunk sums of long fuse runs (k_pm_fuse_chunks), grown
+  int* flen = nullptr;
+  size_t fterm_n = 0;
   uint32_t* mark = nullptr;  // fuse: slots seen (n_fused)
   uint32_t* dcnt = nullptr;  // fuse: unique-slot counter (device memory: atomics stay off the mapped buffer)
   uint8_t* bmark = nullptr;   // step 12b: slots seen per association block (grown)
@@ -1852,7 +1954,7 @@ int gcs_pmap_destroy(gcs_pmap* p) {
     if (f) (void)hipFree(f);
   void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->seg, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
                   p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->bmark, p->bcnt, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
-                  p->msel, p->mnsel, p->ub, p->run_key, p->run_slot, p->tickets};
+                  p->msel, p->mnsel, p->ub, p->run_key, p->run_slot, p->tickets, p->fterm, p->flen};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (p->h_small) (void)hipHostFree(p->h_small);
@@ -2097,8 +2199,20 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
   size_t tb = p->ftemp_bytes;
   PMCHK(p, rocprim::radix_sort_pairs(p->ftemp, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)R, 0u, 32u, p->stream));
   (void)bits;
+  if ((size_t)R * kFT > p->fterm_n) {
+    if (p->fterm) PMCHK(p, hipFree(p->fterm));
+    if (p->flen) PMCHK(p, hipFree(p->flen));
+    p->fterm = nullptr;
+    p->flen = nullptr;
+    p->fterm_n = (size_t)std::max(R, 16384) * kFT;
+    PMCHK(p, hipMalloc(&p->fterm, p->fterm_n * sizeof(double)));
+    PMCHK(p, hipMalloc(&p->flen, (p->fterm_n / kFT) * sizeof(int)));
+  }
+  hipLaunchKernelGGL(k_pm_fuse_chunks, dim3(rb), dim3(kPmThreads), 0, p->stream, r, (const uint32_t*)p->fk_s,
+                     (const uint32_t*)p->fv_s, p->fterm, p->flen);
   hipLaunchKernelGGL(k_pm_fuse_apply_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
-                     r, (const uint32_t*)p->fk_s, (const uint32_t*)p->fv_s, nb, (long long)scan_seq);
+                     r, (const uint32_t*)p->fk_s, (const uint32_t*)p->fv_s, nb, (long long)scan_seq,
+                     (const double*)p->fterm, (const int*)p->flen);
   const long tm = (long)n * p->M;
   hipLaunchKernelGGL(k_pm_fuse_rgb, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
                      p->stream, p->st, (const int32_t*)p->d_tiles, n, eps_mass);

@@ -255,16 +255,20 @@ def test_map_update_step_matches_oracle():
     am.close()
 
 
-@pytest.mark.parametrize("case", ["all_invalid", "ragged_blocks", "no_insert", "populated", "empty_active"])
+CASES = ["all_invalid", "ragged_blocks", "no_insert", "populated", "empty_active", "hot_slots"]
+
+
+@pytest.mark.parametrize("case", CASES)
 def test_map_update_edge_cases(case):
     """Step 12b edge cases against the oracle: an all-invalid MeasurementBatch (zero fused and
     inserted mass, cull / forget still run), a ragged last association block (N = 301, block 128), a zero
-    insert budget, tiles already holding primitives (retention evictions on insert, merges), and an
-    empty active-tile list (exact no-op)."""
+    insert budget, tiles already holding primitives (retention evictions on insert, merges), an
+    empty active-tile list (exact no-op), and every candidate on three slots per tile (runs of ~100 rows
+    per (tile, slot, block): k_pm_fuse_chunks cuts them into chunk sums, at the step-12b bar)."""
     from types import SimpleNamespace
     from gcslam import primitive_map as gpm
     from oracle import se3
-    rng = np.random.default_rng(20 + ["all_invalid", "ragged_blocks", "no_insert", "populated", "empty_active"].index(case))
+    rng = np.random.default_rng(20 + CASES.index(case))
     m, N, K = 1024, (301 if case == "ragged_blocks" else 400), 8
     block = 128 if case == "ragged_blocks" else 256
     kins = 0 if case == "no_insert" else 64
@@ -294,7 +298,8 @@ def test_map_update_edge_cases(case):
     before = {tid: {k: v.copy() for k, v in tt.items()} for tid, tt in tiles.items()}
     ctile = rng.choice(np.array(active + [777], dtype=np.int64), size=(N, K))
     assoc = dict(responsibilities=rng.random((N, K)) / K, candidate_tile_ids=ctile,
-                 candidate_slots=rng.integers(0, m, size=(N, K)), row_masses=rng.random(N) * 2.0 / N)
+                 candidate_slots=rng.integers(0, 3 if case == "hot_slots" else m, size=(N, K)),
+                 row_masses=rng.random(N) * 2.0 / N)
     nxt_ref, st_ref = opm.map_update_step(tiles, 50_000, batch, assoc, R, t, active, m, 7.0, 33,
                                           k_insert_tile=kins, h_tile=2.0, block_size=block)
     st = gpm.primitive_map_update(am, SimpleNamespace(**batch), SimpleNamespace(**assoc), z, active, 7.0, 33, cfg)
