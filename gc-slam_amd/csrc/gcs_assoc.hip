@@ -1023,7 +1023,10 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
 //   L_t += (sum_j r) Lambda_reg; h_t += Lambda_reg sum_j r (m - R p); cost_t += r q^T Lambda_reg q,
 //   q = m - R p - t (:121-148);  w = r sqrt(k kv + 1e-12), S += w v u^T, cost_r += w (1 - (R u).v)
 //   (:209-222).  out: L_t 9, h_t 3, cost_t, S 9, cost_r, sum row masses, rows used, map valid count.
-constexpr int kVpeThreads = 1024;
+#ifndef GCS_VPE_THREADS
+#define GCS_VPE_THREADS 512  // 1024 capped the kernel at 128 VGPRs (73 spilled); at 512 it takes 193, no spills
+#endif
+constexpr int kVpeThreads = GCS_VPE_THREADS;
 constexpr int kVpeVals = 27;
 struct VpeIn {
   const double *Lambdas, *thetas, *etas;
@@ -1041,7 +1044,7 @@ struct VpeIn {
 __global__ __launch_bounds__(kVpeThreads) void k_as_vpe(VpeIn in, double* out) {
 #pragma clang fp contract(off)
   __shared__ int s_w[kVpeThreads / 64];
-  __shared__ double lds[kVpeThreads / 64];
+  __shared__ double lds_all[(kVpeThreads / 64) * kVpeVals];
   double acc[kVpeVals];
   for (int q = 0; q < kVpeVals; ++q) acc[q] = 0.0;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -1109,17 +1112,20 @@ __global__ __launch_bounds__(kVpeThreads) void k_as_vpe(VpeIn in, double* out) {
     acc[24] += 1.0;
   }
   for (int e = threadIdx.x; e < in.m_view; e += kVpeThreads) acc[25] += in.vvalid[e] ? 1.0 : 0.0;
-  for (int q = 0; q < kVpeVals; ++q) {
-    double v = acc[q];
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    __syncthreads();
-    if (lane == 0) lds[wid] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      double sum = lds[0];
-      for (int w = 1; w < kVpeThreads / 64; ++w) sum += lds[w];
-      out[q] = sum;
-    }
+  // all 27 sums at once: the same xor tree per value in every wave, then thread q adds value q's wave
+  // rows in wave order (the per-value form paid two barriers per value)
+#pragma unroll
+  for (int q = 0; q < kVpeVals; ++q)
+    for (int off = 32; off >= 1; off >>= 1) acc[q] += __shfl_xor(acc[q], off, 64);
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < kVpeVals; ++q) lds_all[wid * kVpeVals + q] = acc[q];
+  __syncthreads();
+  if (threadIdx.x < kVpeVals) {
+    const int q = threadIdx.x;
+    double sum = lds_all[q];
+    for (int w = 1; w < kVpeThreads / 64; ++w) sum += lds_all[w * kVpeVals + q];
+    out[q] = sum;
   }
 }
 

@@ -992,12 +992,12 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmStore st, 
 
 // Long runs of one (tile, slot, block) key -- many measurements associated to the same primitive, as
 // in a sparse map -- were one lane's serial walk (the live path's map update spent 0.5 ms in it).  A run
-// longer than kFuseChunk rows is cut into chunks: the run's first chunk ends at the first position
+// longer than kFuseChunk (32) rows is cut into chunks: the run's first chunk ends at the first position
 // b with b % kFuseChunk == 0 and b - kFuseChunk at or after the run start, later chunks at every such
 // b; one lane per chunk sums its rows in row order into P (field-major, kFT fields) and its length
 // into Lc, and the group's lane adds the chunk sums in order.  Runs of at most kFuseChunk rows are
 // never cut: their sums are bitwise the per-row walk's.  (Deterministic either way.)
-constexpr int kFuseChunk = 64;
+constexpr int kFuseChunk = 32;
 constexpr int kFT = 28;  // L 9 | theta 3 | eta 9 | r w | r | camera w | lidar w | rgb accumulation 3
 __device__ __forceinline__ bool fuse_long_start(const uint32_t* keys, int n, int pos, uint32_t key) {
   if (pos == 0 || keys[pos - 1] != key) return pos + kFuseChunk < n && keys[pos + kFuseChunk] == key;
@@ -1016,9 +1016,12 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_chunks(PmRows r, const u
   for (int c = 0; c < 9; ++c) dL[c] = 0.0;
   for (int c = 0; c < 3; ++c) dth[c] = 0.0;
   for (int c = 0; c < ne; ++c) de[c] = 0.0;
-  int q = pos;
-  for (; q < r.n && keys[q] == key; ++q) {
-    if (q > pos && q % kFuseChunk == 0 && keys[q - kFuseChunk] == key) break;  // the next chunk's start
+  // the chunk's end first (contiguous key reads), then the rows with a known trip count, so that
+  // several rows' loads are in flight at once (the sum itself stays in row order)
+  int end = pos + 1;
+  while (end < r.n && keys[end] == key && !(end % kFuseChunk == 0 && keys[end - kFuseChunk] == key)) ++end;
+#pragma unroll 2
+  for (int q = pos; q < end; ++q) {
     const size_t row = vals[q];
     const double rr = r.resp[row] * 1.0;
     for (int c = 0; c < 9; ++c) dL[c] = dL[c] + rr * r.lam[9 * row + c];
@@ -1045,7 +1048,7 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_chunks(PmRows r, const u
   P[23 * n + pos] = dcam;
   P[24 * n + pos] = dlid;
   for (int c = 0; c < 3; ++c) P[(25 + c) * n + pos] = dacc[c];
-  Lc[pos] = q - pos;
+  Lc[pos] = end - pos;
 }
 
 // one lane per (tile, slot) group: for each block in order, d = the block's rows summed in row order
@@ -1573,6 +1576,7 @@ __global__ __launch_bounds__(kPropThreads) void k_pm_proposals(PmMeas m, PmWorld
   __shared__ double lds[kPropThreads / 64];
   __shared__ double s_sc[kPropLds];
   __shared__ int s_in[kPropLds], s_pre[kPropLds], s_slot[kPropMaxIns];
+  __shared__ double s_key[kPropLds];  // the compacted rows' keys -score, in index order
   __shared__ int s_wsum[kPropThreads / 64];
   __shared__ int s_any;
   const int t = blockIdx.x;
@@ -1627,16 +1631,22 @@ __global__ __launch_bounds__(kPropThreads) void k_pm_proposals(PmMeas m, PmWorld
   }
   __syncthreads();
   const int c = run;
-  for (int a = threadIdx.x; a < c; a += kPropThreads) {
-    const int i = s_in[a];
-    const double ki = -scr[i];
-    int rank = 0;
-    for (int b = 0; b < c && rank < kins; ++b) {
-      const int j = s_in[b];
-      const double kj = -scr[j];
-      rank += (kj < ki || (kj == ki && j < i)) ? 1 : 0;
+  // the compacted keys in their own array (s_in is in index order, so the index tie-break is the
+  // position's)
+  for (int a = threadIdx.x; a < c; a += kPropThreads) s_key[a] = -scr[s_in[a]];
+  __syncthreads();
+  // one wave per row: its lanes count the smaller keys over strided slices of the list and add the
+  // counts (integers: exact in any order), so every row costs c / 64 steps -- a lane per row with an
+  // early exit left the top-ranked rows scanning the whole list while the rest of the block waited
+  for (int a = wid; a < c; a += kPropThreads / 64) {
+    const double ka = s_key[a];
+    int cnt = 0;
+    for (int b = lane; b < c; b += 64) {
+      const double kb = s_key[b];
+      cnt += (kb < ka || (kb == ka && b < a)) ? 1 : 0;
     }
-    if (rank < kins) slot_of[rank] = i;
+    for (int off = 32; off >= 1; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+    if (lane == 0 && cnt < kins) slot_of[cnt] = s_in[a];
   }
   for (int i = threadIdx.x; i < m.n; i += kPropThreads) {
     if (scr[i] > -1e29) continue;

@@ -75,6 +75,9 @@ class AtlasMap:
         self.next_global_id = 0
         self.total_count = 0
         self._free = list(range(self.max_tiles))
+        # storage slots that may hold data; every other slot is as gcs_pmap_create cleared it, so a tile
+        # created there needs no clear (a kernel and a stream sync per new tile on the live path)
+        self._written = set()
 
     # ------------------------------------------------------------------ plumbing
     def close(self):
@@ -117,7 +120,9 @@ class AtlasMap:
         if not self._free:
             raise RuntimeError(f"primitive map holds max_tiles={self.max_tiles} tiles")
         idx = self._free.pop(0)
-        self._chk(self.lib.gcs_pmap_clear_tile(self.h, idx), "gcs_pmap_clear_tile")
+        if idx in self._written:
+            self._chk(self.lib.gcs_pmap_clear_tile(self.h, idx), "gcs_pmap_clear_tile")
+        self._written.add(idx)
         self.tiles[tid] = idx
         self.counts[tid] = 0
         return idx
@@ -171,6 +176,7 @@ class AtlasMap:
         if present:
             into._chk(self.lib.gcs_pmap_copy_tiles(into.h, dst.ctypes.data, self.h, src.ctypes.data, len(present)),
                       "gcs_pmap_copy_tiles")
+            into._written.update(int(d) for d in dst)
         into.next_global_id, into.total_count = self.next_global_id, self.total_count
         return into
 
