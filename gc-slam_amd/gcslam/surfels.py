@@ -87,14 +87,22 @@ def _torch():
 
 
 def create_empty_measurement_batch(n_feat=GC_N_FEAT, n_surfel=GC_N_SURFEL, device="cuda:0"):
-    """measurement_batch.py:137-157 (device arrays)."""
+    """measurement_batch.py:137-157 (device arrays): one zeroed allocation carved into the nine arrays
+    (one fill kernel, not nine)."""
     torch = _torch()
     nt = n_feat + n_surfel
-    z = lambda *sh, dt=torch.float64: torch.zeros(sh, dtype=dt, device=device)  # noqa: E731
-    return MeasurementBatch(Lambdas=z(nt, 3, 3), thetas=z(nt, 3), etas=z(nt, GC_VMF_N_LOBES, 3), weights=z(nt),
-                            sources=z(nt, dt=torch.int32), source_indices=z(nt, dt=torch.int32),
-                            valid_mask=z(nt, dt=torch.bool), timestamps=z(nt), colors=z(nt, 3), n_feat=n_feat,
-                            n_surfel=n_surfel, n_camera_valid=0, n_lidar_valid=0)
+    spec = (("Lambdas", torch.float64, (nt, 3, 3)), ("thetas", torch.float64, (nt, 3)),
+            ("etas", torch.float64, (nt, GC_VMF_N_LOBES, 3)), ("weights", torch.float64, (nt,)),
+            ("timestamps", torch.float64, (nt,)), ("colors", torch.float64, (nt, 3)),
+            ("sources", torch.int32, (nt,)), ("source_indices", torch.int32, (nt,)), ("valid_mask", torch.bool, (nt,)))
+    size = {torch.float64: 8, torch.int32: 4, torch.bool: 1}
+    nbytes = [int(np.prod(sh)) * size[dt] for _, dt, sh in spec]
+    buf = torch.zeros(sum((z + 7) // 8 * 8 for z in nbytes), dtype=torch.uint8, device=device)
+    t, off = {}, 0
+    for (name, dt, sh), z in zip(spec, nbytes):
+        t[name] = buf[off:off + z].view(dt).view(sh)
+        off += (z + 7) // 8 * 8
+    return MeasurementBatch(**t, n_feat=n_feat, n_surfel=n_surfel, n_camera_valid=0, n_lidar_valid=0)
 
 
 class SurfelExtractor:
@@ -138,9 +146,11 @@ class SurfelExtractor:
             msg = self.lib.gcs_surfel_last_error(self.h).decode(errors="replace")
             raise (ValueError if rc in (-1, -3) else RuntimeError)(f"{what} failed ({rc}): {msg}")
 
-    def extract(self, points, timestamps, weights, want_intermediates=False):
+    def extract(self, points, timestamps, weights, want_intermediates=False, into=None):
         """Surfel arrays (device tensors) + n_valid + centre; points (N,3) / timestamps / weights f64.
-        The output tensors belong to the extractor and are overwritten by its next call."""
+        The output tensors belong to the extractor and are overwritten by its next call.  into: a dict of
+        the batch-slice tensors (Lambdas, thetas, etas, weights, timestamps, colors, valid_mask as uint8,
+        source_indices; n_surfel rows each) the kernel writes instead of the extractor's own arrays."""
         torch = _torch()
         dev = f"cuda:{self.device}"
         cf = self.config
@@ -167,6 +177,14 @@ class SurfelExtractor:
             self._bufs[key] = (out, o)
         out, o = self._bufs[key]
         out = dict(out)
+        if into is not None:  # write the MeasurementBatch's LiDAR slice in place (padding rows: zeros)
+            o2 = L.GcsSurfelOutputs()
+            for k in ("positions", "covariances", "normals", "kappas", "cell_ids", "bucket", "count"):
+                setattr(o2, k, getattr(o, k))
+            for k, v in into.items():
+                setattr(o2, k, v.data_ptr())
+                out[k] = v
+            o = o2
         self._chk(self.lib.gcs_surfel_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
                   "gcs_surfel_ctx_set_stream")
         self._chk(self.lib.gcs_extract_lidar_surfels(self.h, C.c_void_p(p.data_ptr()), C.c_void_p(t.data_ptr()),
@@ -202,27 +220,36 @@ def extract_lidar_surfels(points, timestamps, weights, config: Optional[SurfelEx
     config = config or SurfelExtractionConfig()
     n = int(np.asarray(points.shape)[0]) if hasattr(points, "shape") else len(points)
     ex = extractor or _extractor_for(config, n, device)
-    r = ex.extract(points, timestamps, weights)
-    nv = r["n_valid"]
     dev = f"cuda:{ex.device}"
     if base_batch is None:
+        # the kernel writes the LiDAR slice of a fresh zeroed batch directly: its padding rows are the
+        # empty batch's zeros, so only the sources of the valid rows remain to set
         batch = create_empty_measurement_batch(config.n_feat, config.n_surfel, dev)
+        s = batch.n_feat
+        sl = slice(s, s + config.n_surfel)
+        into = dict(Lambdas=batch.Lambdas[sl], thetas=batch.thetas[sl], etas=batch.etas[sl], weights=batch.weights[sl],
+                    timestamps=batch.timestamps[sl], colors=batch.colors[sl],
+                    valid_mask=batch.valid_mask[sl].view(torch.uint8), source_indices=batch.source_indices[sl])
+        nv = ex.extract(points, timestamps, weights, into=into)["n_valid"]
+        batch.sources[s:s + nv] = 1
     else:
         if base_batch.n_surfel != config.n_surfel:
             raise ValueError("base_batch.n_surfel differs from config.n_surfel")
+        r = ex.extract(points, timestamps, weights)
+        nv = r["n_valid"]
         batch = replace(base_batch, **{k: getattr(base_batch, k).clone() for k in
                                        ("Lambdas", "thetas", "etas", "weights", "sources", "source_indices",
                                         "valid_mask", "timestamps", "colors")})
-    s, e = batch.n_feat, batch.n_feat + nv
-    batch.Lambdas[s:e] = r["Lambdas"][:nv]
-    batch.thetas[s:e] = r["thetas"][:nv]
-    batch.etas[s:e] = r["etas"][:nv]
-    batch.weights[s:e] = r["weights"][:nv]
-    batch.sources[s:e] = 1
-    batch.source_indices[s:e] = r["source_indices"][:nv]
-    batch.valid_mask[s:e] = True
-    batch.timestamps[s:e] = r["timestamps"][:nv]
-    batch.colors[s:e] = r["colors"][:nv]
+        s, e = batch.n_feat, batch.n_feat + nv
+        batch.Lambdas[s:e] = r["Lambdas"][:nv]
+        batch.thetas[s:e] = r["thetas"][:nv]
+        batch.etas[s:e] = r["etas"][:nv]
+        batch.weights[s:e] = r["weights"][:nv]
+        batch.sources[s:e] = 1
+        batch.source_indices[s:e] = r["source_indices"][:nv]
+        batch.valid_mask[s:e] = True
+        batch.timestamps[s:e] = r["timestamps"][:nv]
+        batch.colors[s:e] = r["colors"][:nv]
     batch.n_lidar_valid = nv
     support = float(nv) / float(max(config.n_surfel, 1))
     cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id,
