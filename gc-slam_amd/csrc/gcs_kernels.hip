@@ -2452,7 +2452,18 @@ static int grid_for(long n, int cap_blocks) {
   if (g < 1) g = 1;
   return (int)(g > cap_blocks ? cap_blocks : g);
 }
-int push_blocks(int n_bins) { return grid_for(n_bins, 4096); }
+// The pushforward's grid is capped at 1,024 blocks (a grid-stride loop of four bins per thread at C3):
+// the 4,096-block grid took every CU's registers (256 VGPRs, two waves per SIMD) for its whole
+// length, so the next scan's budget and point kernels, which overlap it, waited for its blocks to
+// drain.  Same box, alternated (profiles/r04/pushb/): C3 0.2201 vs 0.2392-0.2396 ms per step, the
+// pushforward itself 56.8 vs 65.5-66.1 us; 256 / 512 blocks 0.2249-0.2275 ms.  GCSLAM_PUSH_BLOCKS for A/B.
+int push_blocks(int n_bins) {
+  static const int cap = [] {
+    const char* e = getenv("GCSLAM_PUSH_BLOCKS");
+    return e ? std::max(1, std::min(4096, atoi(e))) : 1024;
+  }();
+  return grid_for(n_bins, cap);
+}
 
 hipError_t launch_parse(const ParseArgs& a, hipStream_t s) {
   if (a.n <= 0) return hipSuccess;
