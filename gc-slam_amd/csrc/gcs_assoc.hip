@@ -39,6 +39,12 @@ constexpr int kAsThreads = 256;
 #define GCS_POOL_THREADS 128
 #endif
 constexpr int kPoolThreads = GCS_POOL_THREADS;
+#ifndef GCS_POOL_FLAT
+#define GCS_POOL_FLAT 1  // 0: each trip's position loads wait on its flag loads (A/B)
+#endif
+#ifndef GCS_POOL_PB
+#define GCS_POOL_PB 8  // pool entries per thread and trip
+#endif
 // the Sinkhorn workgroup: 8 waves, 4 rows per thread at K <= 8 (K_mat rows in registers).  1024
 // threads (4 waves per SIMD, 128 VGPRs: the rows spill) measured slower: 3.2 vs 3.0 us per iteration,
 // 0.480 vs 0.422 ms per call (profiles/r03/assoc/)
@@ -46,6 +52,12 @@ constexpr int kPoolThreads = GCS_POOL_THREADS;
 #define GCS_SH_THREADS 512
 #endif
 constexpr int kShThreads = GCS_SH_THREADS;
+#ifndef GCS_SH_ONEBAR
+#define GCS_SH_ONEBAR 0  // 1: v in every wave, one barrier per iteration (A/B: no faster, profiles/r04/sh1/)
+#endif
+#ifndef GCS_SH_LOGB
+#define GCS_SH_LOGB 1  // 0: v = pow(b / K^T u, vb) with the quotient in every iteration (A/B)
+#endif
 #ifndef GCS_SH_LOGA
 #define GCS_SH_LOGA 1  // 0: u = pow(a / Kv, ua) with the quotient in every iteration (A/B)
 #endif
@@ -302,8 +314,9 @@ __global__ __launch_bounds__(kPoolThreads) void k_as_pool(AsIn in, AsParams p, A
       idx[j] = 0x7fffffff;
     }
     const bool prune = p.beta >= 0.0;
-    // four pool entries per trip, in increasing pool position: their table loads issue together
-    constexpr int PB = 4;
+    // PB pool entries per trip, in increasing pool position: their flag and position loads issue
+    // together, none behind another's result (the pass is bound by L2 round trips, not VALU)
+    constexpr int PB = GCS_POOL_PB;
     // Block threshold (beta >= 0): cost = d_pos + beta d_dir lies in [d_pos, d_pos + beta] (d_dir in
     // [0, 1], rounding monotone), so with D an upper bound of the row's K-th smallest valid d_pos at
     // least K entries cost <= D + beta: an entry with d_pos > D + beta cannot be selected and needs no
@@ -323,6 +336,25 @@ __global__ __launch_bounds__(kPoolThreads) void k_as_pool(AsIn in, AsParams p, A
           if (ti < 0) continue;
           const size_t base = (size_t)ti * MV;
           for (int o = t; o < MV; o += PB * kPoolThreads) {
+#if GCS_POOL_FLAT
+            uint8_t vv[PB];
+            double px[PB], py[PB], pz[PB];
+#pragma unroll
+            for (int u = 0; u < PB; ++u) {  // every load of the trip first (in-range entries only)
+              const int oo = o + u * kPoolThreads;
+              const size_t e = base + (oo < MV ? oo : 0);
+              vv[u] = oo < MV ? in.vvalid[e] : 0;
+              px[u] = in.vpos[3 * e];
+              py[u] = in.vpos[3 * e + 1];
+              pz[u] = in.vpos[3 * e + 2];
+            }
+#pragma unroll
+            for (int u = 0; u < PB; ++u) {
+              if (!vv[u]) continue;
+              const double dx = mp[0] - px[u], dy = mp[1] - py[u], dz = mp[2] - pz[u];
+              dmin = fmin(dmin, (dx * dx + dy * dy) + dz * dz);
+            }
+#else
 #pragma unroll
             for (int u = 0; u < PB; ++u) {
               const int oo = o + u * kPoolThreads;
@@ -333,6 +365,7 @@ __global__ __launch_bounds__(kPoolThreads) void k_as_pool(AsIn in, AsParams p, A
                            dz = mp[2] - in.vpos[3 * e + 2];
               dmin = fmin(dmin, (dx * dx + dy * dy) + dz * dz);
             }
+#endif
           }
         }
         double kth = INFINITY, cur = dmin;
@@ -381,6 +414,19 @@ __global__ __launch_bounds__(kPoolThreads) void k_as_pool(AsIn in, AsParams p, A
       const int ti = s_tix[sq];
       const size_t base = (size_t)(ti < 0 ? 0 : ti) * MV;
       for (int ow = t & ~63; ow < MV; ow += PB * kPoolThreads) {  // wave-uniform trips (ballots inside)
+#if GCS_POOL_FLAT
+        uint8_t vv[PB];
+        double px[PB], py[PB], pz[PB];
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {  // every load of the trip first (a missing tile reads tile 0)
+          const int oo = ow + lane + u * kPoolThreads;
+          const size_t e = base + (oo < MV ? oo : 0);
+          vv[u] = oo < MV && ti >= 0 ? in.vvalid[e] : 0;
+          px[u] = in.vpos[3 * e];
+          py[u] = in.vpos[3 * e + 1];
+          pz[u] = in.vpos[3 * e + 2];
+        }
+#endif
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
           const int oo = ow + lane + u * kPoolThreads;
@@ -388,9 +434,14 @@ __global__ __launch_bounds__(kPoolThreads) void k_as_pool(AsIn in, AsParams p, A
           const int q = sq * MV + oo;
           bool valid = false;
           double d_pos = 0.0;
+#if GCS_POOL_FLAT
+          if (in_tile && vv[u]) {
+            const double dx = mp[0] - px[u], dy = mp[1] - py[u], dz = mp[2] - pz[u];
+#else
           if (in_tile && ti >= 0 && in.vvalid[base + oo]) {
             const size_t e = base + oo;
             const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
+#endif
             d_pos = (dx * dx + dy * dy) + dz * dz;
             valid = true;
           } else if (in_tile) {
@@ -745,8 +796,12 @@ template <int KM, int RPT>
 __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p, AsWork w, AsOut o, int n_valid_host) {
 #pragma clang fp contract(off)
   __shared__ double s_red[16 * (KM + 8)];
+#if GCS_SH_ONEBAR
+  __shared__ double s_colp2[2][(kShThreads / 64) * KM];  // alternate iterations (one barrier each)
+#else
   __shared__ double s_colp[(kShThreads / 64) * KM];
   __shared__ double s_v[KM];
+#endif
   __shared__ uint32_t s_hist[256], s_sel[4];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int N = p.n, K = p.k;
@@ -862,6 +917,20 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const double eps = fmax(p.eps, 1e-12);
   const double ua = 1.0 / (1.0 + p.tau_a / eps), vb = 1.0 / (1.0 + p.tau_b / eps);
   const double bk = 1.0 / (double)K;
+#if GCS_SH_LOGB
+  // v = (b / (K^T u + 1e-12))^vb as exp(vb (log b - log K^T u)): log b once per call, no quotient in
+  // the loop (as u; the short log / exp outside their ranges fall back to the quotient form)
+  const double lbk = log(bk);
+  auto v_scale = [&](double sum) {
+    const double ss = sum + 1e-12;
+    const double b_ = vb * (lbk - log_fast(ss));
+    return ss >= 2.2250738585072014e-308 && ss <= 1.7976931348623157e308 && fabs(b_) < 700.0
+               ? exp_fast(b_)
+               : pow_fast(div_fast(bk, ss), vb);
+  };
+#else
+  auto v_scale = [&](double sum) { return pow_fast(div_fast(bk, sum + 1e-12), vb); };
+#endif
 #pragma unroll
   for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
   SH_STAMP(2);
@@ -927,17 +996,43 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     double cs = c[0];
 #pragma unroll
     for (int sh = (64 >> LG) / 2; sh >= 1; sh >>= 1) cs += __shfl_xor(cs, sh, 64);
+#if GCS_SH_ONEBAR
+    // every wave finishes v itself: lane k (< KM) sums column k over the waves in order and takes its
+    // power, then v[k] comes from lane k.  The partials alternate between two buffers, so one barrier
+    // per iteration separates a buffer's writes from its reads and from its next writes (a wave
+    // rewriting it two iterations on has passed the barrier every reader reached after reading)
+    double* cp = s_colp2[it & 1];
+    if ((lane & ((64 >> LG) - 1)) == 0) cp[wid * KM + col] = cs;
+    __syncthreads();
+    double vk = 0.0;
+    {
+      const int kk = lane & (KM - 1);
+      double sum = cp[kk];
+#pragma unroll
+      for (int g = 1; g < kShThreads / 64; ++g) sum += cp[g * KM + kk];
+      if (kk < K) vk = v_scale(sum);
+    }
+    // v is wave-uniform: lane k's value read into scalar registers (no cross-lane permute)
+    const unsigned long long vbits = (unsigned long long)__double_as_longlong(vk);
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      const unsigned lo = __builtin_amdgcn_readlane((unsigned)vbits, k);
+      const unsigned hi = __builtin_amdgcn_readlane((unsigned)(vbits >> 32), k);
+      v[k] = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+    }
+#else
     if ((lane & ((64 >> LG) - 1)) == 0) s_colp[wid * KM + col] = cs;
     __syncthreads();
     if (t < K) {  // v = (b / (K^T u + 1e-12))^vb: column t over the waves in order
       double sum = s_colp[t];
 #pragma unroll
       for (int g = 1; g < kShThreads / 64; ++g) sum += s_colp[g * KM + t];
-      s_v[t] = pow_fast(div_fast(bk, sum + 1e-12), vb);
+      s_v[t] = v_scale(sum);
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < KM; ++k) v[k] = k < K ? s_v[k] : 0.0;
+#endif
   }
   SH_STAMP(3);
   // pi, row masses, responsibilities and the cert sums

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Timing of gcs_associate_primitives_ot at the reference sizes (N_total = 512 + 1024 rows, k_assoc 8,
 7 stencil tiles x m_tile_view 1024, 50 Sinkhorn iterations) on a seeded scene (tests/assoc_util.py):
-wall time per call (the call synchronises).  Run under rocprofv3 --kernel-trace --stats for the
+wall time per call (the call synchronises).  python tools/assoc_bench.py [reps=30] [iters=50,0,10].
+Run under rocprofv3 --kernel-trace --stats for the
 per-kernel split."""
 import os
 import sys
@@ -21,7 +22,8 @@ def main():
     b, v = _batch(batch), _view(view)
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 30
     # the reference's 50 Sinkhorn iterations, then 0 and 10 (the slope is one iteration's cost)
-    for iters in (50, 0, 10):
+    its = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else (50, 0, 10)
+    for iters in its:
         cfg = GA.AssociationConfig(scan_seq=10, k_sinkhorn=iters)
         for _ in range(3):
             GA.associate_primitives_ot(b, v, cfg)

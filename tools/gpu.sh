@@ -13,6 +13,7 @@
 #   phase        per-phase clocks of the bin kernel (needs `make -C gc-slam_amd prof`)
 #   pmap         primitive-map timing (tools/pmap_bench.py)    assoc   association timing
 #   pmapprof     rocprofv3 --kernel-trace --stats of tools/pmap_bench.py (assocprof: of tools/assoc_bench.py)
+#   assocsq / assocpmc   SQ passes / FETCH, WRITE, L2 hit and TCP passes of the association kernels
 #   ab           same-box A/B of two builds: A = libgcslam_hip.so, B = libgcslam_hip_$B.so
 #   envab        same-box A/B of an environment knob: B runs with $ENVB
 #   graphab      hipGraph vs stream launches of a six-kernel chain (tools/graph_ab, built in-tree)
@@ -61,6 +62,12 @@ step() {
       timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES \
         SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY --kernel-include-regex "k_as_" -d "$O/assocsq" -o run \
         --output-format csv -- python3 tools/assoc_bench.py 5 > "$O/assocsq.log" 2>&1 ;;
+    assocpmc)  # HBM fetch / write and L2 hit counts of the association kernels, one pass each
+      for ctr in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"; do
+        local nm=${ctr// /_}
+        timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "k_as_" -d "$O/assocpmc/$nm" -o run \
+          --output-format csv -- python3 tools/assoc_bench.py 5 50 > "$O/assocpmc_$nm.log" 2>&1 || return $?
+      done ;;
     phase) for cfg in c2 c3; do timeout -k 10 180 python tools/phase_prof.py $cfg > "$O/phase_$cfg.txt" 2>&1 || return $?; done ;;
     pmap) timeout -k 10 300 python tools/pmap_bench.py 30 > "$O/pmap_bench.txt" 2>&1 ;;
     pmapprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/pmap_prof" -o run --output-format csv -- \
@@ -71,7 +78,7 @@ step() {
                GCSLAM_LIB=$PWD/$lib timeout -k 10 300 python tools/assoc_bench.py > "$O/assocab_$v.txt" 2>&1 || return $?
              done ;;
     assocprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/assoc_prof" -o run --output-format csv -- \
-                 python3 tools/assoc_bench.py > "$O/assoc_prof.log" 2>&1 ;;
+                 python3 tools/assoc_bench.py 30 ${ASSOC_ITERS:-50,0,10} > "$O/assoc_prof.log" 2>&1 ;;
     ab)
       for rep in $(seq 1 "${REPS:-2}"); do
         for v in A B; do
