@@ -58,6 +58,18 @@ constexpr int kShThreads = GCS_SH_THREADS;
 #ifndef GCS_SH_LOGB
 #define GCS_SH_LOGB 1  // 0: v = pow(b / K^T u, vb) with the quotient in every iteration (A/B)
 #endif
+#ifndef GCS_SH_TAB
+#define GCS_SH_TAB 1  // 0: the loop's log / exp are log_fast / exp_fast (fdlibm forms with a divide; A/B)
+#endif
+#ifndef GCS_SH_ILV
+#define GCS_SH_ILV 1  // 0: each row's u under its own branches (the chains one after another; A/B)
+#endif
+#ifndef GCS_SH_SPLIT
+#define GCS_SH_SPLIT 1  // 0: log_tab / exp_tab called whole per row (their table reads not hoisted; A/B)
+#endif
+#ifndef GCS_SH_ZSKIP
+#define GCS_SH_ZSKIP 1  // 0: zero-marginal rows take the fallback branch (A/B)
+#endif
 #ifndef GCS_SH_LOGA
 #define GCS_SH_LOGA 1  // 0: u = pow(a / Kv, ua) with the quotient in every iteration (A/B)
 #endif
@@ -69,10 +81,14 @@ constexpr int kMaxStencil = 64;
 #define GCS_SH_PROBE 0
 #endif
 #if GCS_SH_PROBE
-__device__ unsigned long long g_sh_stamp[8];
+__device__ unsigned long long g_sh_stamp[16];
 #define SH_STAMP(k) do { if (threadIdx.x == 0) g_sh_stamp[k] = wall_clock64(); } while (0)
+// the iteration's parts, summed over the iterations by thread 0 (u, K^T u + reduce-scatter, first
+// barrier, v, second barrier + v read)
+#define SH_ACC(k) do { const unsigned long long tn_ = wall_clock64(); sh_pa[k] += tn_ - sh_tp; sh_tp = tn_; } while (0)
 #else
 #define SH_STAMP(k) do { } while (0)
+#define SH_ACC(k) do { } while (0)
 #endif
 constexpr double kLog4Pi = 2.5310242469692907;     // np.log(4.0 * np.pi)
 constexpr double kLog2 = 0.6931471805599453;       // np.log(2.0)
@@ -862,6 +878,17 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     cand_stats<kShThreads>(in, p, p.eps_mass, [cand](size_t q) { return (int)cand[q]; }, o.cert);
     return;
   }
+#if GCS_SH_TAB
+  // the loop's log / exp tables (gcs_sh_tables.h) in LDS: per-lane indexed reads at LDS latency
+  __shared__ double s_lt[kShLogTabLen], s_et[kShExpTabLen];
+  for (int q = t; q < kShLogTabLen; q += kShThreads) s_lt[q] = kShLogTab[q];
+  for (int q = t; q < kShExpTabLen; q += kShThreads) s_et[q] = kShExpTab[q];  // (bsum's barriers publish them)
+#define SH_LOG(x) log_tab((x), s_lt)
+#define SH_EXP(x) exp_tab((x), s_et)
+#else
+#define SH_LOG(x) log_fast(x)
+#define SH_EXP(x) exp_fast(x)
+#endif
   // marginal a (:412-424)
   double va[RPT], X[RPT * KM];  // X: the cost rows, then K_mat = exp(-C / eps) in place
   double part[1] = {0.0};
@@ -923,9 +950,9 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const double lbk = log(bk);
   auto v_scale = [&](double sum) {
     const double ss = sum + 1e-12;
-    const double b_ = vb * (lbk - log_fast(ss));
+    const double b_ = vb * (lbk - SH_LOG(ss));
     return ss >= 2.2250738585072014e-308 && ss <= 1.7976931348623157e308 && fabs(b_) < 700.0
-               ? exp_fast(b_)
+               ? SH_EXP(b_)
                : pow_fast(div_fast(bk, ss), vb);
   };
 #else
@@ -948,8 +975,79 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   int col = 0;  // the column this lane ends up holding
 #pragma unroll
   for (int s = 0; s < LG; ++s) col |= ((lane >> (5 - s)) & 1) << (LG - 1 - s);
+#if GCS_SH_PROBE
+  unsigned long long sh_pa[5] = {0, 0, 0, 0, 0}, sh_tp = wall_clock64();
+#endif
   for (int it = 0; it < p.iters; ++it) {
     // u = (a / (K v + 1e-12))^ua, one lane per row (K v in column order)
+#if GCS_SH_LOGA && GCS_SH_ILV
+    // the rows' chains side by side, branch-free (log and exp of an in-range stand-in where the row's
+    // arguments are out of range), the rare fallback rows after them: the per-row branches serialised
+    // the RPT chains (K v -> log -> exp), which is the loop's critical path
+    {
+      double kvv[RPT], a_[RPT], ue[RPT];
+      bool ok[RPT];
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        double kv = 0.0;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) kv = fma(X[j * KM + k], v[k], kv);
+        kvv[j] = kv + 1e-12;
+        ok[j] = kvv[j] >= 2.2250738585072014e-308 && kvv[j] <= 1.7976931348623157e308;
+      }
+#if GCS_SH_TAB && GCS_SH_SPLIT
+      // every row's table reads first, then the polynomials
+      double lm[RPT], li[RPT], lh[RPT], ll[RPT];
+      int le[RPT], lj[RPT];
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        log_tab_reduce(ok[j] ? kvv[j] : 1.0, lm[j], le[j], lj[j]);
+        li[j] = s_lt[3 * lj[j]];
+        lh[j] = s_lt[3 * lj[j] + 1];
+        ll[j] = s_lt[3 * lj[j] + 2];
+      }
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        a_[j] = ua * (lva[j] - log_tab_poly(lm[j], le[j], li[j], lh[j], ll[j]));
+        ok[j] = ok[j] && fabs(a_[j]) < 700.0;
+      }
+      double er[RPT], eh[RPT], el[RPT];
+      int em[RPT];
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        int ej;
+        exp_tab_reduce(ok[j] ? a_[j] : 0.0, er[j], ej, em[j]);
+        eh[j] = s_et[2 * ej];
+        el[j] = s_et[2 * ej + 1];
+      }
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) ue[j] = exp_tab_poly(er[j], em[j], eh[j], el[j]);
+#else
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        a_[j] = ua * (lva[j] - SH_LOG(ok[j] ? kvv[j] : 1.0));
+        // (NaN lva: a zero or denormal marginal; |a_| >= 700; NaN a_ fails the compare)
+        ok[j] = ok[j] && fabs(a_[j]) < 700.0;
+      }
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) ue[j] = SH_EXP(ok[j] ? a_[j] : 0.0);
+#endif
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int r = t + j * kShThreads;
+        double uj = ue[j];
+        // a zero marginal (an invalid row) gives u = 0 exactly (pow_sinkhorn(0, ua)) without the
+        // fallback branch, so waves holding invalid rows do not diverge into it every iteration
+#if GCS_SH_ZSKIP
+        if (!ok[j] && va[j] != 0.0) uj = pow_fast(div_fast(va[j], kvv[j]), ua);
+        u[j] = r < N && va[j] != 0.0 ? uj : 0.0;
+#else
+        if (!ok[j]) uj = pow_fast(div_fast(va[j], kvv[j]), ua);
+        u[j] = r < N ? uj : 0.0;
+#endif
+      }
+    }
+#else
 #pragma unroll
     for (int j = 0; j < RPT; ++j) {
       const int r = t + j * kShThreads;
@@ -960,10 +1058,10 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
       const double kvv = kv + 1e-12;
       double uj = 0.0;
       if (r < N) {
-        const double a_ = ua * (lva[j] - log_fast(kvv));
+        const double a_ = ua * (lva[j] - SH_LOG(kvv));
         // (NaN lva: a zero or denormal marginal; a Kv outside the short log's range; |a_| >= 700)
         uj = kvv >= 2.2250738585072014e-308 && kvv <= 1.7976931348623157e308 && fabs(a_) < 700.0
-                 ? exp_fast(a_)
+                 ? SH_EXP(a_)
                  : pow_fast(div_fast(va[j], kvv), ua);
       }
       u[j] = uj;
@@ -971,6 +1069,8 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
       u[j] = r < N ? pow_fast(div_fast(va[j], kv + 1e-12), ua) : 0.0;
 #endif
     }
+#endif
+    SH_ACC(0);
     double c[KM];
 #pragma unroll
     for (int k = 0; k < KM; ++k) {
@@ -1022,19 +1122,29 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     }
 #else
     if ((lane & ((64 >> LG) - 1)) == 0) s_colp[wid * KM + col] = cs;
+    SH_ACC(1);
     __syncthreads();
+    SH_ACC(2);
     if (t < K) {  // v = (b / (K^T u + 1e-12))^vb: column t over the waves in order
       double sum = s_colp[t];
 #pragma unroll
       for (int g = 1; g < kShThreads / 64; ++g) sum += s_colp[g * KM + t];
       s_v[t] = v_scale(sum);
     }
+    SH_ACC(3);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < KM; ++k) v[k] = k < K ? s_v[k] : 0.0;
+    SH_ACC(4);
 #endif
   }
   SH_STAMP(3);
+#if GCS_SH_PROBE
+  if (t == 0)
+    for (int k = 0; k < 5; ++k) g_sh_stamp[8 + k] = sh_pa[k];
+#endif
+#undef SH_LOG
+#undef SH_EXP
   // pi, row masses, responsibilities and the cert sums
   // acc: [sum rm, sum rm^2, sum novel, defect_a^2, sum pi C, nonzero_a, sum pi | col masses K]
   double acc[7 + KM];
@@ -1274,6 +1384,16 @@ int gcs_debug_short_log_exp(const double* x, int32_t n, double y, double* log_ou
   return GCS_OK;
 }
 
+int gcs_debug_tab_log_exp(const double* x, int32_t n, double* log_out, double* exp_out) {
+  if (n < 0 || (n > 0 && (!x || !log_out || !exp_out))) return GCS_ERR_ARG;
+  for (int i = 0; i < n; ++i) {
+    log_out[i] = x[i] >= 2.2250738585072014e-308 && x[i] <= 1.7976931348623157e308 ? gcs::log_tab(x[i], gcs::kShLogTab)
+                                                                                  : NAN;
+    exp_out[i] = fabs(x[i]) < 700.0 ? gcs::exp_tab(x[i], gcs::kShExpTab) : NAN;
+  }
+  return GCS_OK;
+}
+
 int gcs_assoc_config_defaults(gcs_assoc_config* c) {
   if (!c) return GCS_ERR_ARG;
   memset(c, 0, sizeof(*c));
@@ -1480,11 +1600,14 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   ASCHK(c, hipStreamSynchronize(s));
 #if GCS_SH_PROBE
   {
-    unsigned long long h[8];
+    unsigned long long h[16];
     (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_sh_stamp), sizeof(h));
     fprintf(stderr, "sh_probe us: marginal %.2f kmat %.2f loop %.2f finish %.2f (pi %.2f bsum %.2f cert %.2f) | wg1 %.2f\n",
             (h[1] - h[0]) / 100.0, (h[2] - h[1]) / 100.0, (h[3] - h[2]) / 100.0, (h[4] - h[3]) / 100.0,
             (h[6] - h[3]) / 100.0, (h[7] - h[6]) / 100.0, (h[4] - h[7]) / 100.0, (h[5] - h[0]) / 100.0);
+    const double it = p.iters > 0 ? 100.0 * p.iters : 1.0;  // per iteration, us
+    fprintf(stderr, "sh_probe per iteration us: u %.3f KTu+scatter %.3f barrier1 %.3f v %.3f barrier2+read %.3f\n",
+            h[8] / it, h[9] / it, h[10] / it, h[11] / it, h[12] / it);
   }
 #endif
   for (int q = 0; q < GCS_ASSOC_CERT_LEN; ++q) o->cert[q] = c->h_cert[q];

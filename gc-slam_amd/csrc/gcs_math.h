@@ -7,6 +7,9 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <string.h>
+
+#include "gcs_sh_tables.h"
 
 // instrumented build only (make prof): device counters of the 3x3 PSD paths
 #ifdef GCS_PHASE_PROF
@@ -674,6 +677,57 @@ GCS_HD double exp_short(double x) {  // |x| < 700
   const double c = r - rr * (P1 + rr * (P2 + rr * (P3 + rr * (P4 + rr * P5))));
   const double y = 1.0 - ((lo - (r * c) / (2.0 - c)) - hi);
   return ldexp(y, k);
+}
+
+// Table-driven f64 log / exp for the Sinkhorn loop (about half of log_short / exp_short's operations,
+// no divide): the argument reduced by a 129- / 64-entry table (gcs_sh_tables.h, passed in -- the
+// kernel reads its LDS copy) to |f| < 2^-8 / |r| < ln2 / 128, where a degree-7 log1p / degree-5 expm1
+// Taylor polynomial is below an ulp (truncation ~2e-18 / 4e-17 relative).  Within ~1 ulp of the
+// library; host and device round alike (explicit fma, no contraction).
+// (each split in two: the reduction with its table index, then the polynomial on the table values --
+// a caller with several arguments issues every table read before the first polynomial)
+GCS_HD void log_tab_reduce(double x, double& m, int& e, int& j) {  // x > 0, finite, normal
+  uint64_t b;
+  memcpy(&b, &x, 8);
+  e = (int)(b >> 52) - 1023;
+  const uint64_t mb = b & 0x000fffffffffffffull;
+  j = (int)((mb + (1ull << 44)) >> 45);  // nearest 1/128 of the mantissa: 0..128
+  const uint64_t mbits = mb | 0x3ff0000000000000ull;
+  memcpy(&m, &mbits, 8);  // [1, 2)
+}
+GCS_HD double log_tab_poly(double m, int e, double inv_c, double l_hi, double l_lo) {
+#pragma clang fp contract(off)
+  const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+  const double f = fma(m, inv_c, -1.0);  // m inv_c_j - 1 (exact product, one rounding)
+  const double p = f * f *
+                   fma(f, fma(f, fma(f, fma(f, fma(f, 1.0 / 7.0, -1.0 / 6.0), 0.2), -0.25), 1.0 / 3.0), -0.5);
+  const double dk = (double)e;
+  return fma(dk, ln2_hi, l_hi) + (f + (p + fma(dk, ln2_lo, l_lo)));
+}
+GCS_HD double log_tab(double x, const double* lt) {  // x > 0, finite, normal
+  double m;
+  int e, j;
+  log_tab_reduce(x, m, e, j);
+  return log_tab_poly(m, e, lt[3 * j], lt[3 * j + 1], lt[3 * j + 2]);
+}
+GCS_HD void exp_tab_reduce(double x, double& r, int& j, int& m) {  // |x| < 700
+#pragma clang fp contract(off)
+  const double kd = rint(x * kSh64ByLn2);
+  const int k = (int)kd;
+  r = fma(-kd, kShLn2By64Lo, fma(-kd, kShLn2By64Hi, x));
+  j = k & 63;
+  m = k >> 6;  // k = 64 m + j (arithmetic shift: floor)
+}
+GCS_HD double exp_tab_poly(double r, int m, double t_hi, double t_lo) {
+#pragma clang fp contract(off)
+  const double p = fma(r * r, fma(r, fma(r, fma(r, 1.0 / 120.0, 1.0 / 24.0), 1.0 / 6.0), 0.5), r);  // expm1(r)
+  return ldexp(t_hi + fma(t_hi, p, t_lo), m);
+}
+GCS_HD double exp_tab(double x, const double* et) {  // |x| < 700
+  double r;
+  int j, m;
+  exp_tab_reduce(x, r, j, m);
+  return exp_tab_poly(r, m, et[2 * j], et[2 * j + 1]);
 }
 
 // x^y for the Sinkhorn scalings: 0 at x = 0, exp_short(y log_short(x)) for positive finite normal

@@ -291,6 +291,7 @@ _SIGS = [
                                             C.POINTER(GcsSurfelOutputs)]),
     ("gcs_assoc_config_defaults", C.c_int, [C.POINTER(GcsAssocConfig)]),
     ("gcs_debug_short_log_exp", C.c_int, [c_double_p, C.c_int32, C.c_double, c_double_p, c_double_p, c_double_p]),
+    ("gcs_debug_tab_log_exp", C.c_int, [c_double_p, C.c_int32, c_double_p, c_double_p]),
     ("gcs_assoc_ctx_create", C.c_int, [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]),
     ("gcs_assoc_ctx_destroy", C.c_int, [C.c_void_p]),
     ("gcs_assoc_last_error", C.c_char_p, [C.c_void_p]),

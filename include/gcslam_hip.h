@@ -607,6 +607,9 @@ int gcs_assoc_config_defaults(gcs_assoc_config* cfg);
 /* Host evaluation of the Sinkhorn's short log / exp / x^y (gcs_math.h log_short, exp_short,
  * pow_sinkhorn; the device runs the same code) for the accuracy test against numpy. */
 int gcs_debug_short_log_exp(const double* x, int32_t n, double y, double* log_out, double* exp_out, double* pow_out);
+/* Host evaluation of the table-driven log / exp of the Sinkhorn loop (gcs_math.h log_tab, exp_tab;
+ * NaN outside their domains: positive normal x / |x| < 700), for the same accuracy test. */
+int gcs_debug_tab_log_exp(const double* x, int32_t n, double* log_out, double* exp_out);
 int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int32_t device, gcs_assoc_ctx** out);
 int gcs_assoc_ctx_destroy(gcs_assoc_ctx* ctx);
 const char* gcs_assoc_last_error(const gcs_assoc_ctx* ctx);

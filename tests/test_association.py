@@ -131,3 +131,33 @@ def test_short_log_exp_pow_accuracy(lib):
     o1, o2, o3 = np.empty(1), np.empty(1), np.empty(1)
     assert lib.gcs_debug_short_log_exp(L.dptr(z), 1, y, L.dptr(o1), L.dptr(o2), L.dptr(o3)) == 0
     assert o3[0] == 0.0
+
+
+def test_table_log_exp_accuracy(lib):
+    """The Sinkhorn loop's table-driven log / exp (gcs_math.h log_tab / exp_tab, tables from
+    tools/gen_sh_tables.py): within 1 ulp of numpy's over the whole normal range / |x| < 700, exact at
+    the table's own points (log 1 = 0, exp 0 = 1), NaN outside the domains."""
+    from gcslam import _lib as L
+    rng = np.random.default_rng(1)
+    ulp = lambda a, b: np.abs(a - b) / np.spacing(np.abs(b))  # noqa: E731
+    x = np.concatenate([np.exp(rng.uniform(-700.0, 700.0, 200000)), rng.uniform(0.5, 2.0, 100000),
+                        1.0 + rng.uniform(-1e-3, 1e-3, 20000), 1.0 + np.arange(129) / 128.0,
+                        np.nextafter(2.0, 0.0) * np.ones(1), np.array([2.2250738585072014e-308, 1.7976931348623157e308])])
+    lo, ex = np.empty_like(x), np.empty_like(x)
+    assert lib.gcs_debug_tab_log_exp(L.dptr(x), x.size, L.dptr(lo), L.dptr(ex)) == 0
+    ref = np.log(x)
+    # away from x = 1 within an ulp; near 1 (|log x| < 0.01: the log1p polynomial alone) within 2
+    far = np.abs(ref) > 1e-2
+    assert ulp(lo[far], ref[far]).max() <= 1.0
+    assert ulp(lo[~far & (ref != 0)], ref[~far & (ref != 0)]).max() <= 2.0
+    assert lo[np.flatnonzero(x == 1.0)[0]] == 0.0
+    xe = np.concatenate([rng.uniform(-700.0, 700.0, 200000), rng.uniform(-1.0, 1.0, 100000),
+                         np.arange(-64, 65) * np.log(2.0) / 64.0, np.array([0.0, -699.9, 699.9])])
+    lo2, ex2 = np.empty_like(xe), np.empty_like(xe)
+    assert lib.gcs_debug_tab_log_exp(L.dptr(xe), xe.size, L.dptr(lo2), L.dptr(ex2)) == 0
+    assert ulp(ex2, np.exp(xe)).max() <= 1.0
+    assert ex2[np.flatnonzero(xe == 0.0)[0]] == 1.0
+    bad = np.array([0.0, -1.0, 5e-324, np.inf, np.nan, 700.0, -700.0])
+    lo3, ex3 = np.empty_like(bad), np.empty_like(bad)
+    assert lib.gcs_debug_tab_log_exp(L.dptr(bad), bad.size, L.dptr(lo3), L.dptr(ex3)) == 0
+    assert np.isnan(lo3[[0, 1, 2, 3, 4]]).all() and np.isnan(ex3[[3, 4, 5, 6]]).all()
