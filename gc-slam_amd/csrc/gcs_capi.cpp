@@ -111,6 +111,14 @@ struct gcs_ctx {
   int* d_tile_order = nullptr;
   uint32_t* d_tile_work = nullptr;
   bool tile_order_on = false;
+  // GCSLAM_TILE_ORDER_PUSH=1: k_tile_order deferred to the push stream behind the scan's
+  // pushforward (or onto the main stream ahead of the next bin kernel when no pushforward went out on
+  // its own stream).  Off: measured slower at C3 (0.2245 -> 0.2355 ms per step, profiles/r04/tod1/):
+  // on the main stream behind the PT fold it fills the device while the host runs the tail, the
+  // combine and the next prologue; behind the pushforward and its fold it ends after k_points and
+  // the next bin kernel waits for it.
+  bool tile_order_defer = false;
+  bool tile_order_pending = false;
   double* d_bins_part = nullptr;    // k_bins_scale partial rows (persistent: clean tiles keep theirs)
   double* d_scan = nullptr;
   double* d_map = nullptr;
@@ -590,8 +598,10 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   return b;
 }
 
+int flush_tile_order(gcs_ctx* c, hipStream_t s, gcs_ctx* ec);
 int stage_bins(gcs_ctx* c) {
   hipStream_t s = c->stream;
+  if (int rc = flush_tile_order(c, s, c)) return rc;  // (a tile order no pushforward took)
   BinKernelArgs b = bin_args(c);
   if (c->cfg.mode == GCS_MODE_SCALE) {
     if (!c->use_direct) {  // sorted bucketing (direct buckets: k_points placed and flagged them)
@@ -690,13 +700,25 @@ int stage_pt(gcs_ctx* c, bool to_host = false, bool clear_next = false) {
   return GCS_OK;
 }
 
-// the next scan's bin-tile dispatch order, queued on the main stream behind the scan's stages (the
-// device is idle while the host runs the tail; the next bin kernel is behind it in stream order)
+// the next scan's bin-tile dispatch order from this scan's bin kernel (d_tile_dirty / d_tile_work ->
+// d_tile_order; read only by the next bin kernel, written by nothing else), queued on the main stream
+// behind the scan's stages: the device runs it while the host runs the tail (the next bin kernel is
+// behind it in stream order).  Deferred (GCSLAM_TILE_ORDER_PUSH=1, measured slower): the scan's
+// pushforward takes it onto the push stream behind itself (stage_push, after the stages) and the next
+// bin kernel is ordered after it by join_push; a scan whose pushforward does not go out on its own
+// stream leaves it pending, and the next stage_bins queues it on the main stream.
+int flush_tile_order(gcs_ctx* c, hipStream_t s, gcs_ctx* ec) {
+  if (!c->tile_order_pending) return GCS_OK;
+  c->tile_order_pending = false;
+  HIPCHK(ec, launch_tile_order(c->d_tile_dirty, c->d_tile_work, bins_scale_blocks(c->B, c->tile_bins), c->d_tile_order,
+                               s));
+  return GCS_OK;
+}
 int stage_tile_order(gcs_ctx* c) {
   if (!c->tile_order_on) return GCS_OK;
-  HIPCHK(c, launch_tile_order(c->d_tile_dirty, c->d_tile_work, bins_scale_blocks(c->B, c->tile_bins), c->d_tile_order,
-                              c->stream));
-  return GCS_OK;
+  c->tile_order_pending = true;
+  if (c->tile_order_defer && !c->push_main && c->push_stream) return GCS_OK;
+  return flush_tile_order(c, c->stream, c);
 }
 
 // on_worker: called by the push worker; errors are returned, not written to the context's message
@@ -723,14 +745,16 @@ int stage_push(gcs_ctx* c, const double* z_t, const double* Sig6, double gamma, 
   StageEv ev = stage_ev(c, ST_PUSH);
   // the main stream's stages are complete once wait_mirror saw the fold's ready word (the fold is
   // the stream's last kernel before it): only the other paths order the push stream by the event.
-  // k_tile_order (stage_tile_order) is queued on the main stream after that fold and may still run
-  // beside this pushforward: it reads d_tile_dirty / d_tile_work and writes d_tile_order, and the
-  // pushforward reads d_scan / d_flags and writes d_map / d_derived / d_touched / its partials and
-  // map-total scalars -- disjoint buffers, which the two must keep.  A fault in k_tile_order is
-  // reported by the next call that synchronises the main stream.
+  // k_tile_order runs on the main stream after that fold, where it may run beside this pushforward
+  // (or behind it on the same stream, GCSLAM_TILE_ORDER_PUSH=1): it reads d_tile_dirty / d_tile_work
+  // and writes d_tile_order, and the pushforward reads d_scan / d_flags and writes d_map / d_derived /
+  // d_touched / its partials and map-total scalars -- disjoint buffers, which the two must keep.  A fault in k_tile_order is reported by the
+  // next call that synchronises its stream.
   if (s != c->stream && !c->stages_done) HIPCHK(ec, hipStreamWaitEvent(s, c->ev_stages, 0));
   HIPCHK(ec, launch_pushforward(c->d_scan, c->d_map, c->d_derived, c->B, pa, partials, c->d_scalars, flags,
                                c->d_touched, s, ev.e0, ev.e1));
+  // the deferred tile order behind it (the stages it reads are complete, as for the pushforward)
+  if (int rc = flush_tile_order(c, s, ec)) return rc;
   if (s != c->stream) {
     HIPCHK(ec, hipEventRecord(c->ev_push, s));
     c->push_pending = true;
@@ -1105,6 +1129,8 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
       const int nt = bins_scale_blocks(c->B, c->tile_bins);
       const char* e = getenv("GCSLAM_TILE_ORDER");
       c->tile_order_on = nt > 2048 && !(e && atoi(e) == 0);
+      const char* ep = getenv("GCSLAM_TILE_ORDER_PUSH");
+      c->tile_order_defer = ep && atoi(ep) == 1;
       if (c->tile_order_on) {
         std::vector<int> ident(nt);
         for (int i = 0; i < nt; ++i) ident[i] = i;
