@@ -147,8 +147,11 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_clear(PmStore st, int t) {
 }
 
 // mode 0: -score (score = w, -1e30 where invalid), mode 1: retention w exp(-lam dt) (-inf where invalid)
+// other_bm (may be null): bit g set where the key is not the mode's empty-slot key (k_pm_topk_sparse),
+// one 32-bit word per half wave (g is wave-aligned: 64 consecutive g per wave)
 __global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_t* tiles, int n, int mode,
-                                                        long long seq, double lam, uint64_t* keys, uint32_t* vals) {
+                                                        long long seq, double lam, uint64_t* keys, uint32_t* vals,
+                                                        uint32_t* other_bm) {
   const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
   if (g >= (long)n * st.M) return;
   const int t = (int)(g / st.M), q = (int)(g % st.M);
@@ -170,8 +173,13 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_
     const double decay = exp(-lam * (double)dt);
     key = v ? w * decay : -INFINITY;
   }
-  keys[g] = ord_key(key);
+  const uint64_t kb = ord_key(key);
+  keys[g] = kb;
   vals[g] = (uint32_t)g;  // tile position x M + slot
+  if (other_bm) {
+    const uint64_t b = __ballot(kb != ord_key(mode == 0 ? 1e30 : -INFINITY));
+    if ((threadIdx.x & 31) == 0) other_bm[g >> 5] = (uint32_t)(b >> (threadIdx.x & 32));
+  }
 }
 
 // the first k (<= kSelMax) entries of each tile's stable key order without sorting the tile: one
@@ -517,7 +525,8 @@ __device__ __forceinline__ int topk_len(int M, int k, int lv, int i) {
 }
 __global__ __launch_bounds__(kPmRed) void k_pm_topk(const uint64_t* __restrict__ keys, int M, int k, int G,
                                                      uint64_t* run_key, uint32_t* run_slot, uint32_t* tickets,
-                                                     uint32_t* __restrict__ sorted) {
+                                                     uint32_t* __restrict__ sorted, const uint32_t* __restrict__ skip) {
+  if (skip && skip[blockIdx.y]) return;  // k_pm_topk_sparse wrote this tile's result
   // leaf: the chunk's keys / slots; merges: own run [0, k), sibling run [kSelMax, 2 kSelMax), merged
   // run [2 kSelMax, 3 kSelMax) (k <= kSelMax = 1,024)
   __shared__ uint64_t s_k[kTopChunk];
@@ -714,6 +723,152 @@ __global__ __launch_bounds__(kPmRed) void k_pm_topk(const uint64_t* __restrict__
     L = Lo;
     i >>= 1;
     ++lv;
+  }
+}
+
+// Sparse tiles first (GCSLAM_PM_TOPK_SPARSE=0: the tree for every tile).  A tile's slots split into
+// the empty-slot group -- every slot whose key is the mode's empty-slot key E (mode 0: the key of
+// score -1e30, mode 1: of retention -inf), whose stable order is slot order -- and the rest.  With at
+// most kSpMax of the rest (a map tile of 50,000 slots holds a few hundred primitives), the stable
+// order is [rest below E by (key, slot)] ++ [the E slots ascending] ++ [rest above E by (key, slot)]:
+// its first k come from one LDS sort of the rest and the first clear bits of the tile's bitmap of
+// non-E slots, which k_pm_keys writes (one ballot per half wave): the kernel reads 6 KB of bitmap
+// and gathers the few keys it marks, never the 50,000.  One workgroup per tile; a tile with more
+// than kSpMax writes skip[t] = 0 and the tree takes it (the tree's other tiles' workgroups return at
+// once).  Same result as the tree: (key, slot) pairs are distinct.
+constexpr int kSpMax = 2048;    // entries besides the empty slots
+constexpr int kSpWords = 2048;  // slot bitmap words per tile: M <= 65,536
+__global__ __launch_bounds__(kPmRed) void k_pm_topk_sparse(const uint64_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ other_bm, int M, int k,
+                                                          int mode, uint32_t* __restrict__ skip,
+                                                          uint32_t* __restrict__ sorted) {
+  __shared__ uint64_t s_k[kSpMax];
+  __shared__ uint32_t s_s[kSpMax];
+  __shared__ uint32_t s_wo[kPmRed / 64], s_wz[kPmRed / 64];
+  __shared__ uint32_t s_clo;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) s_clo = 0u;
+  // the tile's words of k_pm_keys' bitmap (bit q of the tile = global bit t M + q, not word-aligned):
+  // WPT consecutive tile words per thread, their set (other) and clear (empty) bits counted
+  constexpr int WPT = kSpWords / kPmRed;
+  const int nw = (M + 31) >> 5;
+  const long b0 = (long)t * M;
+  uint32_t ow[WPT];
+  uint32_t no = 0u, nz = 0u;
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int w = WPT * tid + u;
+    uint32_t x = 0u, valid = 0u;
+    if (w < nw) {
+      const long gb = b0 + 32L * w;
+      const int sh = (int)(gb & 31);
+      const uint32_t lo = other_bm[gb >> 5], hi = sh ? other_bm[(gb >> 5) + 1] : 0u;
+      x = sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+      const int nb = min(32, M - 32 * w);
+      valid = nb == 32 ? ~0u : ((1u << nb) - 1u);
+      x &= valid;
+    }
+    ow[u] = x;
+    no += (uint32_t)__popc(x);
+    nz += (uint32_t)__popc(~x & valid);
+  }
+  // exclusive block scans of both counts (slot order: the other entries land in slot order)
+  uint32_t xo = no, xz = nz;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t yo = (uint32_t)__shfl_up((int)xo, off, 64), yz = (uint32_t)__shfl_up((int)xz, off, 64);
+    if (lane >= off) {
+      xo += yo;
+      xz += yz;
+    }
+  }
+  if (lane == 63) {
+    s_wo[wid] = xo;
+    s_wz[wid] = xz;
+  }
+  __syncthreads();
+  uint32_t ro = xo - no, rz = xz - nz, n = 0u;
+  for (int w = 0; w < kPmRed / 64; ++w) {
+    if (w < wid) {
+      ro += s_wo[w];
+      rz += s_wz[w];
+    }
+    n += s_wo[w];
+  }
+  if (n > (uint32_t)kSpMax) {  // the tree's
+    if (tid == 0) skip[t] = 0u;
+    return;
+  }
+  if (tid == 0) skip[t] = 1u;
+  // gather the other entries' keys into LDS in slot order
+  const uint64_t* kt = keys + (size_t)t * M;
+  {
+    uint32_t r = ro;
+#pragma unroll
+    for (int u = 0; u < WPT; ++u) {
+      uint32_t x = ow[u];
+      while (x) {
+        const int bit = __ffs((int)x) - 1;
+        x &= x - 1u;
+        const int q = 32 * (WPT * tid + u) + bit;
+        s_k[r] = kt[q];
+        s_s[r] = (uint32_t)q;
+        ++r;
+      }
+    }
+  }
+  // bitonic sort of the n entries by (key, slot) in LDS (padding above every real pair)
+  int P = 1;
+  while (P < (int)n) P <<= 1;
+  for (int i = (int)n + tid; i < P; i += kPmRed) {
+    s_k[i] = ~0ull;
+    s_s[i] = ~0u;
+  }
+  for (int size = 2; size <= P; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int pr = tid; pr < P / 2; pr += kPmRed) {
+        const int x = ((pr & ~(stride - 1)) << 1) | (pr & (stride - 1)), y = x | stride;
+        const uint64_t kx = s_k[x], ky = s_k[y];
+        const uint32_t sx = s_s[x], sy = s_s[y];
+        if (topk_less(ky, sy, kx, sx) == ((x & size) == 0)) {
+          s_k[x] = ky;
+          s_k[y] = kx;
+          s_s[x] = sy;
+          s_s[y] = sx;
+        }
+      }
+    }
+  __syncthreads();
+  // c_lo = the entries below the empty-slot key E (a prefix of the sorted run: one boundary writer)
+  const uint64_t E = ord_key(mode == 0 ? 1e30 : -INFINITY);  // k_pm_keys' empty-slot keys
+  for (int i = tid; i < (int)n; i += kPmRed)
+    if (s_k[i] < E && (i + 1 == (int)n || s_k[i + 1] >= E)) s_clo = (uint32_t)(i + 1);
+  __syncthreads();
+  const int clo = (int)s_clo, ne = M - (int)n, kk = min(k, M);
+  uint32_t* out = sorted + (size_t)t * M;
+  const uint32_t tb = (uint32_t)((size_t)t * M);
+  for (int r = tid; r < (int)n; r += kPmRed) {
+    const int pos = r < clo ? r : r + ne;
+    if (pos < kk) out[pos] = tb + s_s[r];
+  }
+  // the empty slots at positions clo.. : the first `need` clear bits, in slot order
+  const int need = kk > clo ? min(kk - clo, ne) : 0;
+  uint32_t rank = rz;
+#pragma unroll
+  for (int u = 0; u < WPT; ++u) {
+    const int w = WPT * tid + u;
+    uint32_t zb = 0u;
+    if (w < nw) {
+      const int nb = min(32, M - 32 * w);
+      zb = ~ow[u] & (nb == 32 ? ~0u : ((1u << nb) - 1u));
+    }
+    while (zb != 0u && rank < (uint32_t)need) {
+      const int bit = __ffs((int)zb) - 1;
+      zb &= zb - 1u;
+      out[clo + (int)rank] = tb + (uint32_t)(32 * w + bit);
+      ++rank;
+    }
+    rank += (uint32_t)__popc(zb);
   }
 }
 
@@ -1727,6 +1882,8 @@ struct gcs_pmap {
   uint32_t* run_slot = nullptr;
   size_t run_cap = 0;
   uint32_t* tickets = nullptr;
+  uint32_t* topk_skip = nullptr;  // k_pm_topk_sparse -> k_pm_topk: the tiles it finished (max_tiles)
+  uint32_t* other_bm = nullptr;   // k_pm_keys -> k_pm_topk_sparse: non-empty-key bitmap (max_tiles x M bits)
   // small host-mapped results
   char* h_small = nullptr;
   char* d_small = nullptr;
@@ -1783,8 +1940,13 @@ int upload_tiles(gcs_pmap* p, const int32_t* tiles, int n) {
 int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam, int k) {
   const long total = (long)n * p->M;
   const unsigned gb = (unsigned)((total + kPmThreads - 1) / kPmThreads);
+  static const bool sparse = [] {
+    const char* e = getenv("GCSLAM_PM_TOPK_SPARSE");
+    return !(e && e[0] == '0');
+  }();
+  const bool sp = sparse && k >= 1 && k <= kSelMax && p->M > 8 * kPmRed && p->M <= 32 * kSpWords;
   hipLaunchKernelGGL(k_pm_keys, dim3(gb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, mode,
-                     seq, lam, p->keys, p->vals);
+                     seq, lam, p->keys, p->vals, sp ? p->other_bm : nullptr);
   // only the first k of each tile are read: a per-tile select + LDS sort replaces the full radix sort
   // (GCSLAM_PM_FULLSORT=1 keeps the full sort, for A/B)
   static const bool full = [] {
@@ -1803,13 +1965,13 @@ int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam, int k) {
     // Measured at 7 x 50,000 (profiles/r03/pmap): tree 61-73 us, radix ~120 us, and the register select
     // at 98 keys per thread (512 threads, buffer loads, no spill) 186 us -- its LDS histogram atomics
     // on the keys' low-entropy top bits serialise.
-    static const int mode = [] {
+    static const int sel = [] {
       const char* e = getenv("GCSLAM_PM_SELECT");
       return e && strcmp(e, "radix") == 0 ? 2 : 0;
     }();
     const int G = (p->M + kTopChunk - 1) / kTopChunk;
     const bool reg8 = p->M <= 8 * kPmRed;
-    const bool use_tree = !glob && mode == 0 && !reg8 && G > 1 && G <= (1 << (kTopMaxLevels - 1));
+    const bool use_tree = !glob && sel == 0 && !reg8 && G > 1 && G <= (1 << (kTopMaxLevels - 1));
     if (use_tree) {
       const size_t need = (size_t)n * G * k;
       if (need > p->run_cap) {
@@ -1821,9 +1983,12 @@ int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam, int k) {
         PMCHK(p, hipMalloc(&p->run_slot, need * 4));
         p->run_cap = need;
       }
+      if (sp)  // sparse tiles (most map tiles): their result directly; the tree takes the others
+        hipLaunchKernelGGL(k_pm_topk_sparse, dim3(n), dim3(kPmRed), 0, p->stream, kk, (const uint32_t*)p->other_bm,
+                           p->M, k, mode, p->topk_skip, p->vals);
       hipLaunchKernelGGL(k_pm_topk, dim3(G, n), dim3(kPmRed), 0, p->stream, kk, p->M, k, G, p->run_key, p->run_slot,
-                         p->tickets, p->vals);
-    } else if (!glob && mode != 2 && reg8)
+                         p->tickets, p->vals, sp ? (const uint32_t*)p->topk_skip : nullptr);
+    } else if (!glob && sel != 2 && reg8)
       hipLaunchKernelGGL((k_pm_select_reg<8, kPmRed>), dim3(n), dim3(kPmRed), 0, p->stream, kk, p->M, k, p->vals);
     else
       hipLaunchKernelGGL(k_pm_select, dim3(n), dim3(kPmRed), 0, p->stream, kk, p->M, k, p->vals);
@@ -1929,6 +2094,9 @@ int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t 
       bad(hipMemset(p->bcnt, 0, kMaxFuseBlocks * 4)) ||  // once: k_pm_publish_u32 re-zeroes
       bad(hipMalloc(&p->tickets, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
       bad(hipMemset(p->tickets, 0, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
+      bad(hipMalloc(&p->topk_skip, (size_t)max_tiles * 4)) ||
+      bad(hipMalloc(&p->other_bm, ((size_t)max_tiles * m_tile / 32 + 4) * 4)) ||
+      bad(hipMemset(p->other_bm, 0, ((size_t)max_tiles * m_tile / 32 + 4) * 4)) ||
       bad(hipHostMalloc((void**)&p->h_small, kSmall, hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&p->d_small, p->h_small, 0)))
     return fail();
@@ -1964,7 +2132,7 @@ int gcs_pmap_destroy(gcs_pmap* p) {
     if (f) (void)hipFree(f);
   void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->seg, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
                   p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->bmark, p->bcnt, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
-                  p->msel, p->mnsel, p->ub, p->run_key, p->run_slot, p->tickets, p->fterm, p->flen};
+                  p->msel, p->mnsel, p->ub, p->run_key, p->run_slot, p->tickets, p->fterm, p->flen, p->topk_skip, p->other_bm};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (p->h_small) (void)hipHostFree(p->h_small);

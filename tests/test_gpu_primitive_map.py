@@ -342,12 +342,16 @@ def test_view_sparse_and_empty_tiles():
     am.close()
 
 
-def test_reference_size_view_and_map_update():
+@pytest.mark.parametrize("fracs", [(0.999, 0.8, 0.8, 0.8, 0.8, 0.0), (0.01, 0.02, 0.04, 0.05, 0.001, 0.0)],
+                         ids=["dense", "sparse"])
+def test_reference_size_view_and_map_update(fracs):
     """The reference's map sizes (GC_M_TILE = 50,000 slots, GC_M_TILE_VIEW = 1,024, 7 active tiles,
     constants.py:392,436-439; N = 512 + 1,024 measurement rows, K = 8, constants.py:350-356): the view's
-    per-tile top-k (k_pm_select over 50,000 keys, ties and an empty tile whose keys are all equal
-    included) and step 12b with novelty insertion into populated tiles (eviction order by the same
-    select) against the oracle."""
+    per-tile top-k over 50,000 keys (ties and an empty tile whose keys are all equal included) and
+    step 12b with novelty insertion into populated tiles (eviction order by the same top-k) against
+    the oracle.  dense: full and 80 % tiles (the tree of sorted runs, k_pm_topk); sparse: tiles of
+    50-2,500 primitives (k_pm_topk_sparse -- a few hundred to ~2,000 besides the empty slots, the
+    5 % tile past its 2,048 capacity back on the tree)."""
     from types import SimpleNamespace
     from gcslam import primitive_map as gpm
     from oracle import se3
@@ -367,7 +371,7 @@ def test_reference_size_view_and_map_update():
     assert len(active) == 7
     tiles = {}
     for i, tid in enumerate(active[:6]):   # five populated tiles (one full), one empty; the 7th is absent
-        tiles[tid] = _rand_tile(rng, m=m, frac=(0.0 if i == 5 else 0.999 if i == 0 else 0.8), seq_hi=30)
+        tiles[tid] = _rand_tile(rng, m=m, frac=fracs[i], seq_hi=30)
     am = gpm.AtlasMap(m_tile=m, max_tiles=16, n_lobes=NL, max_merge=0)
     for tid, tt in tiles.items():
         am.write_tile(tid, tt)
