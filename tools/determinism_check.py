@@ -4,7 +4,8 @@ N = 4,096, the hypothesis combine after each): REPS fresh contexts in one proces
 per-scan z_t compared bitwise with the first's.  Prints the number of distinct sequences and the
 largest z_t difference.
 
-  python tools/determinism_check.py [reps=20]
+  python tools/determinism_check.py [reps=20]      (DET_STAGES=1: also the first differing scan of
+                                                   ScanBinStats and of the map, per differing run)
 """
 import os
 import sys
@@ -12,6 +13,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STAGES = os.environ.get("DET_STAGES", "0") == "1"  # also compare ScanBinStats / map per scan (syncs)
 sys.path[:0] = [os.path.join(ROOT, "gc-slam_amd"), os.path.join(ROOT, "tests"), ROOT]
 
 
@@ -24,8 +26,9 @@ def main():
     from gcslam.distributed import combine_allreduce
     from gcslam.synthetic import scan_kwargs
     scans = [synthetic.make_scan(4096, s) for s in range(12)]
-    runs = []
+    runs, st_runs, map_runs = [], [], []
     for r in range(reps):
+        stats, maps = [], []
         ctx = HypothesisContext(n_bins=5000, n_points_cap=4096, max_raw_points=4096, mode="scale",
                                 lidar_origin=tuple(ORIGIN))
         zs = []
@@ -36,10 +39,17 @@ def main():
                 w = torch.from_numpy(sc["weights"]).cuda()
                 out = ctx.scan(rec, 16, t, w, 4096, **scan_kwargs(sc))
                 zs.append(np.array(out.z_t[:], np.float64))
+                if STAGES:  # the scan's ScanBinStats and the map after its pushforward, as checksums
+                    stats.append(ctx.get_scan_stats().tobytes())
                 combine_allreduce(ctx, 0, 1, s, want_belief=False)
+                if STAGES:
+                    torch.cuda.synchronize()
+                    maps.append(np.asarray(ctx.get_map()[0]).tobytes())
         finally:
             ctx.close()
         runs.append(np.stack(zs))
+        st_runs.append(stats)
+        map_runs.append(maps)
         # other GPU work between the sequences (fresh allocations land on reused memory)
         junk = torch.randn(1 << 22, device="cuda") * (r + 1)
         del junk
@@ -48,6 +58,13 @@ def main():
     distinct = len({z.tobytes() for z in runs})
     print(f"{reps} sequences: {distinct} distinct; max |z - z_first| per run: "
           + " ".join(f"{d:.1e}" for d in diffs), flush=True)
+    if STAGES:  # per differing run: the first scan whose z_t, ScanBinStats or map differs
+        for r in range(1, reps):
+            fz = next((i for i in range(len(scans)) if not np.array_equal(runs[r][i], base[i])), None)
+            fs = next((i for i in range(len(scans)) if st_runs[r][i] != st_runs[0][i]), None)
+            fm = next((i for i in range(len(scans)) if map_runs[r][i] != map_runs[0][i]), None)
+            if fz is not None or fs is not None or fm is not None:
+                print(f"run {r}: first differing scan -- z_t {fz}, ScanBinStats {fs}, map {fm}", flush=True)
 
 
 if __name__ == "__main__":
