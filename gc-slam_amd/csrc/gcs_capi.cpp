@@ -192,11 +192,17 @@ struct gcs_ctx {
   int pts_blocks = 0;
   bool pts_fold_pending = false;
   double* d_scalars = nullptr;
-  double* h_scalars = nullptr;  // pinned, mapped
+  // the scan's host mirror (gcs_layout.h Mirror): pinned, coherent, mapped; written by the PT fold
+  double* h_scalars = nullptr;
   double* d_scalars_mirror = nullptr;  // device view of h_scalars
-  // bucketing error words (pinned, mapped; BucketArgs.err): [0] look-back bound exhausted, [1]
-  // degenerate-bucket compaction taken.  Debug knobs (gcs_ctx_set_debug).
-  uint32_t* h_err = nullptr;
+  uint64_t mirror_seq = 0;             // sequence number of the last mirror-writing PT fold
+  int64_t mirror_scans = 0, mirror_rereads = 0, mirror_syncs = 0;  // accepted / re-read / via stream sync
+  int mirror_torn = 0;                 // test knob (GCS_DEBUG_MIRROR_TORN): data stores delayed, in us
+  // device error words (BucketArgs.err, k_points' overflow, k_gate): [0] look-back bound exhausted,
+  // [1] degenerate-bucket compaction taken, [2] a direct bucket overflowed, [3] launch gate timeout.
+  // Device memory, carried to the host by the mirror (zeroed there) or by pull_err; h_err holds them
+  // until the host check that reads a word clears it.
+  uint32_t h_err[4] = {0u, 0u, 0u, 0u};
   uint32_t* d_err = nullptr;
   // direct buckets (gcs_scan, scale mode): k_points writes each bucket's members into a fixed row of
   // capb slots and marks the active bins itself; the bin kernel ranks them while staging, so the
@@ -643,33 +649,64 @@ int stage_mf(gcs_ctx* c) {
   return GCS_OK;
 }
 
-// to_host: the fold also writes the whole scalar block into the mapped host mirror (the scan
-// then only synchronizes; per-operator calls copy with pull_scalars)
-// Wait for the scan's device stages: poll the mapped ready word the PT fold writes after its
-// mirror of the scalars (a stream synchronize returns some microseconds after the kernel ends).
-// Nothing later in the scan reads device memory outside stream order, so the stream is not
-// synchronized once the word is seen; without it after 20 ms (a fault, or a stalled queue) the
-// stream synchronize waits and reports the asynchronous error.  GCSLAM_SYNC_WAIT=stream:
-// synchronize only.
+// checksum of the mirror as read from host memory (k_final's, gcs_layout.h Mirror)
+uint64_t mirror_sum(const volatile uint64_t* m) {
+  uint64_t s = 0;
+  for (int i = 0; i < MIR_SEQ; ++i) s += mirror_word_hash(m[i], (uint32_t)i);
+  return s + mirror_word_hash(m[MIR_SEQ], MIR_SEQ);
+}
+
+// a validated mirror's error words into h_err (a word stays set until the check that reads it clears it)
+void take_mirror_err(gcs_ctx* c) {
+  const uint64_t* m = reinterpret_cast<const uint64_t*>(c->h_scalars);
+  for (int k = 0; k < 2; ++k) {
+    c->h_err[2 * k] |= (uint32_t)(m[MIR_ERR + k] & 0xffffffffu);
+    c->h_err[2 * k + 1] |= (uint32_t)(m[MIR_ERR + k] >> 32);
+  }
+}
+
+// Wait for the scan's device stages: the PT fold writes the scalar block and the error words to the
+// host mirror, then the checksum and the scan's sequence number (k_final).  The host polls the
+// sequence word (a stream synchronize returns some microseconds after the kernel ends) and accepts the
+// mirror only when the checksum of what it reads matches: a mirror whose data words have not all
+// reached host memory when the sequence word has is re-read (mirror_rereads), never consumed.  Without
+// a valid mirror after 20 ms (a fault, or a stalled queue) the stream synchronize waits and reports
+// the asynchronous error, and the mirror must then be complete.  Nothing later in the scan reads
+// device memory outside stream order.  GCSLAM_SYNC_WAIT=stream: synchronize only.
 int wait_mirror(gcs_ctx* c) {
   static const bool spin = [] {
     const char* e = getenv("GCSLAM_SYNC_WAIT");
     return !(e && strcmp(e, "stream") == 0);
   }();
+  const volatile uint64_t* m = reinterpret_cast<const volatile uint64_t*>(c->h_scalars);
+  const uint64_t seq = c->mirror_seq;
   if (spin) {
-    volatile double* ready = c->h_scalars + SC_COUNT;
     const auto t0 = clk::now();
-    while (*ready == 0.0) {
+    bool reread = false;
+    for (;;) {
+      if (m[MIR_SEQ] == seq) {
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (mirror_sum(m) == m[MIR_SUM]) {
+          std::atomic_thread_fence(std::memory_order_acquire);
+          take_mirror_err(c);
+          ++c->mirror_scans;
+          if (reread) ++c->mirror_rereads;
+          c->stages_done = true;
+          return GCS_OK;
+        }
+        reread = true;  // the sequence word is here, some data word is not yet: read again
+      }
       __builtin_ia32_pause();
       if (clk::now() - t0 > std::chrono::milliseconds(20)) break;
     }
-    if (*ready != 0.0) {
-      std::atomic_thread_fence(std::memory_order_acquire);
-      c->stages_done = true;
-      return GCS_OK;
-    }
+    ++c->mirror_syncs;
   }
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (m[MIR_SEQ] != seq || mirror_sum(m) != m[MIR_SUM])
+    return fail(c, GCS_ERR_HIP, "scan mirror: sequence " + std::to_string((unsigned long long)m[MIR_SEQ]) + " / checksum do not match scan " +
+                                    std::to_string((unsigned long long)seq) + " after the stream synchronized");
+  take_mirror_err(c);
+  ++c->mirror_scans;
   c->stages_done = true;
   return GCS_OK;
 }
@@ -680,7 +717,13 @@ int wait_mirror(gcs_ctx* c) {
 // k_budget then only sums the weights.  Measured: DESIGN.md section 5 (round 4).
 int stage_pt(gcs_ctx* c, bool to_host = false, bool clear_next = false) {
   StageEv ev = stage_ev(c, ST_PT);
-  if (to_host) c->h_scalars[SC_COUNT] = 0.0;  // re-armed: the fold writes 1 after the mirror
+  MirrorArgs mir{};
+  if (to_host) {
+    mir.mirror = c->d_scalars_mirror;
+    mir.err = c->d_err;
+    mir.seq = ++c->mirror_seq;
+    mir.torn = c->mirror_torn;
+  }
   PtClear clr{};
   if (clear_next && c->pt_clear && c->d_counts && c->d_flags_buf[0]) {
     clr.c32 = c->d_counts;
@@ -689,8 +732,7 @@ int stage_pt(gcs_ctx* c, bool to_host = false, bool clear_next = false) {
     clr.n8 = c->B + bins_scale_blocks(c->B, c->tile_bins);
   }
   HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
-                      to_host ? c->d_scalars_mirror : nullptr, c->d_flags, c->d_touched, c->stream,
-                      ev.e0, ev.e1, clr));
+                      mir, c->d_flags, c->d_touched, c->stream, ev.e0, ev.e1, clr));
   if (clr.c32) {
     c->counts_clean = true;
     c->flags_clean[c->flags_cur ^ 1] = true;
@@ -919,17 +961,26 @@ struct GateGuard {
 
 // after a stream sync: a k_scan whose look-back bound ran out left wrong bucket starts
 int check_bucket_err(gcs_ctx* c) {
-  if (c->h_err && c->h_err[0]) {
+  if (c->h_err[0]) {
     c->h_err[0] = 0u;
     return fail(c, GCS_ERR_HIP, "k_scan: decoupled look-back exceeded its spin bound; bucket starts invalid, scan failed");
   }
   return GCS_OK;
 }
 
+// the device error words into h_err after the stream's work (paths without the scan mirror), re-armed
+int pull_err(gcs_ctx* c) {
+  uint32_t e[4];
+  HIPCHK(c, hipMemcpyAsync(e, c->d_err, sizeof(e), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->d_err, 0, sizeof(e), c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  for (int k = 0; k < 4; ++k) c->h_err[k] |= e[k];
+  return GCS_OK;
+}
+
 int pull_scalars(gcs_ctx* c) {
   HIPCHK(c, hipMemcpyAsync(c->h_scalars, c->d_scalars, SC_COUNT * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  return GCS_OK;
+  return pull_err(c);
 }
 
 // The IMU/odometry branch from the quantities the reference reads (pipeline.py:442-566,595-776):
@@ -1081,13 +1132,14 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_tickets, 4 * sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_parse_flag, sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_tickets, 0, 4 * sizeof(uint32_t)))) return GCS_ERR_HIP;
-  // SC_COUNT scalars + the ready word k_final<.., mirror> writes last (wait_mirror)
-  if (bad(hipHostMalloc(&c->h_scalars, (SC_COUNT + 8) * sizeof(double), hipHostMallocMapped))) return GCS_ERR_HIP;
-  c->h_scalars[SC_COUNT] = 0.0;
+  // the scan mirror (gcs_layout.h Mirror; k_final writes it, wait_mirror validates it): coherent, so
+  // the device's stores go to host memory uncached instead of waiting in an XCD's L2
+  if (bad(hipHostMalloc(&c->h_scalars, (MIR_WORDS + 4) * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent)))
+    return GCS_ERR_HIP;
+  memset(c->h_scalars, 0, (MIR_WORDS + 4) * sizeof(double));  // sequence 0: no scan's
   if (bad(hipHostGetDevicePointer((void**)&c->d_scalars_mirror, c->h_scalars, 0))) return GCS_ERR_HIP;
-  if (bad(hipHostMalloc(&c->h_err, 4 * sizeof(uint32_t), hipHostMallocMapped))) return GCS_ERR_HIP;
-  c->h_err[0] = c->h_err[1] = c->h_err[2] = c->h_err[3] = 0u;
-  if (bad(hipHostGetDevicePointer((void**)&c->d_err, c->h_err, 0))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_err, 4 * sizeof(uint32_t)))) return GCS_ERR_HIP;
+  if (bad(hipMemset(c->d_err, 0, 4 * sizeof(uint32_t)))) return GCS_ERR_HIP;
   if (bad(hipHostMalloc(&c->h_gate, 8 * sizeof(uint64_t), hipHostMallocMapped | hipHostMallocCoherent)))
     return GCS_ERR_HIP;
   for (int k = 0; k < 8; ++k) c->h_gate[k] = 0u;
@@ -1188,7 +1240,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_scalars) (void)hipHostFree(c->h_scalars);
-  if (c->h_err) (void)hipHostFree(c->h_err);
+  if (c->d_err) (void)hipFree(c->d_err);
   if (c->h_gate) (void)hipHostFree(c->h_gate);
   if (c->h_preint_in) (void)hipHostFree(c->h_preint_in);
   if (c->h_preint_out) (void)hipHostFree(c->h_preint_out);
@@ -1258,9 +1310,58 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
       c->gate_on = value != 0;
       c->gate_withhold = value < 0;
       return GCS_OK;
+    case GCS_DEBUG_MIRROR_TORN:
+      if (value < 0 || value > 10000) return fail(c, GCS_ERR_ARG, "mirror torn delay: 0..10000 us");
+      c->mirror_torn = (int)value;
+      return GCS_OK;
     default:
       return fail(c, GCS_ERR_ARG, "unknown debug key");
   }
+}
+
+int gcs_ctx_mirror_stats(gcs_ctx* c, int64_t* out) {
+  if (!c || !out) return GCS_ERR_ARG;
+  out[0] = c->mirror_scans;
+  out[1] = c->mirror_rereads;
+  out[2] = c->mirror_syncs;
+  return GCS_OK;
+}
+
+namespace {
+uint64_t fnv1a(const void* p, size_t n, uint64_t h = 1469598103934665603ULL) {
+  const uint8_t* b = (const uint8_t*)p;
+  for (size_t i = 0; i < n; ++i) h = (h ^ b[i]) * 1099511628211ULL;
+  return h;
+}
+// checksum of n bytes of device memory (synchronous copy)
+int dev_fnv(gcs_ctx* c, const void* d, size_t n, uint64_t* out) {
+  *out = 0;
+  if (!d || !n) return GCS_OK;
+  std::vector<uint8_t> h(n);
+  HIPCHK(c, hipMemcpy(h.data(), d, n, hipMemcpyDeviceToHost));
+  *out = fnv1a(h.data(), n);
+  return GCS_OK;
+}
+}  // namespace
+
+int gcs_debug_state_checksums(gcs_ctx* c, uint64_t* out) {
+  if (!c || !out) return GCS_ERR_ARG;
+  if (int rc = push_wait(c)) return rc;
+  if (c->push_stream) HIPCHK(c, hipStreamSynchronize(c->push_stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const size_t B = c->B;
+  int rc = 0;
+  if ((rc = dev_fnv(c, c->d_scan, B * SF_COUNT * sizeof(double), &out[0]))) return rc;
+  if ((rc = dev_fnv(c, c->d_map, B * MF_COUNT * sizeof(double), &out[1]))) return rc;
+  if ((rc = dev_fnv(c, c->d_derived, B * MD_COUNT * sizeof(double), &out[2]))) return rc;
+  if ((rc = dev_fnv(c, c->d_touched, B, &out[3]))) return rc;
+  const size_t nflags = c->d_flags_buf[0] ? 2 * ((B + bins_scale_blocks(c->B, c->tile_bins) + 15) & ~(size_t)15) : 0;
+  if ((rc = dev_fnv(c, c->d_flags_buf[0], nflags, &out[4]))) return rc;
+  const size_t npart = c->d_bins_part ? (size_t)bins_scale_blocks(c->B, c->tile_bins) * partial_stride(bins_partial_nv()) : 0;
+  if ((rc = dev_fnv(c, c->d_bins_part, npart * sizeof(double), &out[5]))) return rc;
+  if ((rc = dev_fnv(c, c->d_scalars, SC_COUNT * sizeof(double), &out[6]))) return rc;
+  out[7] = fnv1a(c->h_scalars, SC_COUNT * sizeof(double));
+  return GCS_OK;
 }
 
 int gcs_ctx_enable_timing(gcs_ctx* c, int32_t stage_mask) {
@@ -2073,8 +2174,7 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     if ((rc = stage_bins(c))) return rc;
     if ((rc = stage_pt(c, /*to_host=*/true, /*clear_next=*/true))) return rc;
     if ((rc = stage_tile_order(c))) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
-    c->stages_done = true;
+    if ((rc = wait_mirror(c))) return rc;
     if ((rc = check_bucket_err(c))) return rc;
   }
   st.cert[41] = c->h_err[1] ? 1.0 : 0.0;  // a bucket above the ranking capacity took the compaction path
@@ -2391,6 +2491,7 @@ int gcs_map_follow(gcs_ctx* c, const gcs_scan_inputs* in, const double* rec) {
     if (int rc = stage_tile_order(c)) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->stages_done = true;
+    if (int rc = pull_err(c)) return rc;
     if (int rc = check_bucket_err(c)) return rc;
     if (!(c->use_direct && c->h_err[2])) break;
     // a bucket overflowed the direct rows (the lead's scan was redone sorted too): redo sorted

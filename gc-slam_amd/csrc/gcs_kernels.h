@@ -43,6 +43,17 @@ struct PtClear {
   long n8 = 0;
 };
 
+// The PT fold's copy of the scan's results to the pinned host mirror (gcs_layout.h Mirror): the
+// scalar block, the device error words (read, then zeroed for the next scan), the sequence number and
+// the checksum.  torn != 0 (test knob): the sequence word and checksum are stored first and the data
+// ~torn microseconds later, so the host meets a mirror whose words have not all arrived.
+struct MirrorArgs {
+  double* mirror = nullptr;  // device view of the host mirror (null: no copy)
+  uint32_t* err = nullptr;   // 4 device error words
+  uint64_t seq = 0;
+  int torn = 0;
+};
+
 struct PointKernelArgs {
   // raw PointCloud2-like input (device)
   const uint8_t* xyz;  // float x,y,z at byte offsets 0,4,8 of each record (double when xyz_f64)
@@ -199,12 +210,12 @@ hipError_t launch_dense(const BinKernelArgs& a, double* bin_partials, double* pa
                         hipEvent_t e1);
 hipError_t launch_mf(const double* scan, const double* map, int B, double* partials, int nblk, double* scalars,
                      hipStream_t s, hipEvent_t e0, hipEvent_t e1);
-// mirror (may be null): mapped host buffer that receives the whole scalar block after the fold
+// mir.mirror (may be null): host mirror that receives the scalar block after the fold (MirrorArgs)
 // act (scan-active bin flags, null = all) and touched (bin has map mass) let k_pt and
 // k_pushforward skip bins that are zero in both the scan and the map
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
-                     hipEvent_t e0, hipEvent_t e1, PtClear clr = PtClear{});
+                     double* scalars, const MirrorArgs& mir, const uint8_t* act, const uint8_t* touched,
+                     hipStream_t s, hipEvent_t e0, hipEvent_t e1, PtClear clr = PtClear{});
 // the next scan's bin-tile dispatch order from this scan's active tiles and their staged records
 hipError_t launch_tile_order(const uint8_t* active, const uint32_t* work, int n, int* order, hipStream_t s);
 // xcd: the XCD-grouped order (k_tile_order_xcd, n % 8 == 0), else the class order alone

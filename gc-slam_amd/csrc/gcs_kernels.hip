@@ -2164,23 +2164,63 @@ __global__ __launch_bounds__(kBlock) void k_map_derive(const double* __restrict_
 }
 
 // ---------------------------------------------------------------- one-block folds of block partials
-// mirror (may be null): after the epilogue the whole scalar block is copied to this mapped host
-// buffer, so the host reads the scan's results without a separate D2H copy.
+// mir.mirror (may be null): after the epilogue the whole scalar block, the device error words, the
+// scan's sequence number and a checksum go to the pinned host mirror (gcs_layout.h Mirror), so the
+// host reads the scan's results without a separate D2H copy and never consumes a torn mirror.
 template <int NV, unsigned MAXMASK, int KIND, int NT = kBlock>
 __global__ __launch_bounds__(NT) void k_final(const double* __restrict__ partials, int nblocks, double* scalars,
-                                              double* mirror) {
+                                              MirrorArgs mir) {
+  static_assert(NT >= MIR_SEQ, "one mirror word per thread");
   __shared__ double lds[(NT / 64) * pstride<NV>()];
   double v[NV];
   reduce_partials<NV, MAXMASK, NT>(partials, nblocks, v, lds);
   if (threadIdx.x == 0) final_epilogue<NV, KIND>(v, scalars);
-  if (mirror) {
+  if (mir.mirror) {
+    __syncthreads();  // thread 0's epilogue stores before every thread's loads (one workgroup)
+    const int i = threadIdx.x, lane = i & 63, wid = i >> 6;
+    uint64_t* mw = reinterpret_cast<uint64_t*>(mir.mirror);
+    uint64_t w = 0;
+    if (i < SC_COUNT) {
+      w = (uint64_t)__double_as_longlong(scalars[i]);
+    } else if (i < MIR_SEQ) {  // the error words, read and re-armed for the next scan
+      const int e = 2 * (i - MIR_ERR);
+      w = (uint64_t)mir.err[e] | ((uint64_t)mir.err[e + 1] << 32);
+      mir.err[e] = 0u;
+      mir.err[e + 1] = 0u;
+    }
+    // the checksum: an integer sum, so any reduction order gives the same value
+    unsigned long long h = i < MIR_SEQ ? mirror_word_hash(w, (uint32_t)i) : 0ull;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) h += __shfl_xor(h, off, 64);
+    unsigned long long* lh = reinterpret_cast<unsigned long long*>(lds);
+    if (lane == 0) lh[wid] = h;
     __syncthreads();
-    for (int i = threadIdx.x; i < SC_COUNT; i += NT) mirror[i] = scalars[i];
-    // the block's mirror stores reach host memory before the ready word (the host polls it instead
-    // of a stream synchronize: gcs_capi.cpp wait_mirror)
+    uint64_t sum = 0;
+    if (i == 0) {
+      for (int k = 0; k < NT / 64; ++k) sum += lh[k];
+      sum += mirror_word_hash(mir.seq, MIR_SEQ);
+    }
+    if (mir.torn) {  // test knob: the sequence word and checksum first, the data torn microseconds later
+      if (i == 0) {
+        mw[MIR_SUM] = sum;
+        mw[MIR_SEQ] = mir.seq;
+      }
+      __threadfence_system();
+      __syncthreads();
+      const uint64_t t0 = wall_clock64();
+      while (wall_clock64() - t0 < 100ull * (uint64_t)mir.torn) __builtin_amdgcn_s_sleep(8);
+      if (i < MIR_SEQ) mw[i] = w;
+      return;
+    }
+    if (i < MIR_SEQ) mw[i] = w;
+    // the block's data stores complete before the checksum and the sequence word are stored (the
+    // host still checks the sum, so a transport that reorders them costs a re-read, not a torn result)
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0) mirror[SC_COUNT] = 1.0;
+    if (i == 0) {
+      mw[MIR_SUM] = sum;
+      mw[MIR_SEQ] = mir.seq;
+    }
   }
 }
 
@@ -2208,7 +2248,7 @@ __global__ __launch_bounds__(kBlock) void k_fold(const double* __restrict__ part
 // behind the nblk rows of `partials` (partials_need() reserves them).
 // e0 / e1 (may be null): the first kernel's start / the last kernel's end.
 template <int NV, unsigned MAXMASK, int KIND>
-void launch_fold(const double* partials, int nblk, hipStream_t s, hipEvent_t e1, double* scalars, double* mirror,
+void launch_fold(const double* partials, int nblk, hipStream_t s, hipEvent_t e1, double* scalars, const MirrorArgs& mirror,
                  hipEvent_t e0 = nullptr) {
   if (nblk > kFoldDirect) {
     double* lvl = (double*)partials + (size_t)nblk * pstride<NV>();
@@ -2228,9 +2268,9 @@ size_t partials_need(long nblocks, int nv) {
   return (size_t)(nblocks + (nblocks + kFoldRows - 1) / kFoldRows + 1) * partial_stride(nv);
 }
 #define GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, mirror) \
-  launch_fold<NV, MASK, KIND>((const double*)(partials), (int)(nblk), s, e1, scalars, (double*)(mirror))
+  launch_fold<NV, MASK, KIND>((const double*)(partials), (int)(nblk), s, e1, scalars, mirror)
 #define GCS_FINAL(NV, MASK, KIND, nblk, s, e1, partials, scalars) \
-  GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, nullptr)
+  GCS_FINAL_M(NV, MASK, KIND, nblk, s, e1, partials, scalars, MirrorArgs{})
 
 // ---------------------------------------------------------------- bin-tile dispatch order
 // One 1024-thread block after the scan's pushforward (off the critical path): the tiles active in this
@@ -2615,7 +2655,7 @@ hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream
     hipExtLaunchKernelGGL((k_bins_scale<kStageBig, 64, 4, GCS_DALL64>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else
     hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 64, 4, GCS_DALL64>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
-  launch_fold<kBinNV, 16u, FIN_BINS>(partials, nblk, s, f1, a.scalars, nullptr, f0);
+  launch_fold<kBinNV, 16u, FIN_BINS>(partials, nblk, s, f1, a.scalars, MirrorArgs{}, f0);
   return hipGetLastError();
 }
 
@@ -2638,8 +2678,8 @@ hipError_t launch_mf(const double* scan, const double* map, int B, double* parti
 }
 
 hipError_t launch_pt(const double* scan, const double* map, const double* derived, int B, double* partials, int nblk,
-                     double* scalars, double* mirror, const uint8_t* act, const uint8_t* touched, hipStream_t s,
-                     hipEvent_t e0, hipEvent_t e1, PtClear clr) {
+                     double* scalars, const MirrorArgs& mirror, const uint8_t* act, const uint8_t* touched,
+                     hipStream_t s, hipEvent_t e0, hipEvent_t e1, PtClear clr) {
   // (measured slower and removed: a last-block fold in k_pt, ticket + agent-scope release per block:
   // 16.4 vs 12.3 us at C2, 46 vs 25 us at C3; the same with sc1 stores / loads and no fence: C2
   // 105.4-105.9 vs 103.5-104.1 us per step, profiles/r03/ptfold/)

@@ -1,5 +1,6 @@
 // Device data layout shared by kernels and host code (DESIGN.md "Data layout in HBM").
 #pragma once
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace gcs {
@@ -76,5 +77,25 @@ enum Scalar : int {
   SC_PT_NEFF = 76,
   SC_COUNT = 96
 };
+
+// The scan's host mirror (pinned, coherent, mapped): the PT fold copies the scalar block and the
+// four device error words into it, then the scan's sequence number and a checksum of all of it.
+// The host accepts the mirror only when the sequence word is the scan's and the checksum of what it
+// reads matches (gcs_capi.cpp wait_mirror), so a read that overtakes any of the device's stores is
+// re-read, never consumed -- whatever order the stores reach host memory in.
+enum Mirror : int {
+  MIR_ERR = SC_COUNT,      // 2 words: error words [0..1] | [2..3] (uint32 pairs)
+  MIR_SEQ = SC_COUNT + 2,  // uint64 sequence number of the scan that wrote the mirror
+  MIR_SUM = SC_COUNT + 3,  // uint64 checksum of words [0, MIR_SEQ] (mirror_word_hash summed) + seq
+  MIR_WORDS = SC_COUNT + 4
+};
+// splitmix64's finalizer over (word + position x golden ratio): a torn mirror (any subset of stale
+// words) sums to the fresh checksum with probability ~2^-64
+__host__ __device__ inline uint64_t mirror_word_hash(uint64_t w, uint32_t i) {
+  uint64_t z = w + 0x9e3779b97f4a7c15ULL * (uint64_t)(i + 1);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
 
 }  // namespace gcs

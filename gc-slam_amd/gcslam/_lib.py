@@ -15,6 +15,7 @@ import numpy as np
 LIB_NAME = "libgcslam_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
+ABI_VERSION = 3  # include/gcslam_hip.h GCS_ABI_VERSION
 D_Z = 22
 CERT_LEN = 64
 PAYLOAD_LEN = 840
@@ -101,6 +102,7 @@ DEBUG_LAUNCH_GATE = 5
 DEBUG_POINT_KERNEL = 6
 DEBUG_DEVICE_PREINT = 7
 DEBUG_PT_CLEAR = 8
+DEBUG_MIRROR_TORN = 9
 MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 
@@ -210,6 +212,8 @@ _SIGS = [
     ("gcs_ctx_synchronize", C.c_int, [C.c_void_p]),
     ("gcs_ctx_enable_timing", C.c_int, [C.c_void_p, C.c_int32]),
     ("gcs_ctx_set_debug", C.c_int, [C.c_void_p, C.c_int32, C.c_int64]),
+    ("gcs_ctx_mirror_stats", C.c_int, [C.c_void_p, c_int64_p]),
+    ("gcs_debug_state_checksums", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     ("gcs_ctx_set_map_mode", C.c_int, [C.c_void_p, C.c_int32]),
     ("gcs_ctx_map_record", C.c_int, [C.c_void_p, C.c_void_p]),
     ("gcs_map_follow", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -353,6 +357,13 @@ def load():
     except ImportError:
         pass
     lib = C.CDLL(path)
+    # the structs above mirror include/gcslam_hip.h of this ABI: a library of another ABI would read
+    # or write past them (ABI 3: gcs_assoc_outputs.cert grew to GCS_ASSOC_CERT_LEN 21)
+    lib.gcs_abi_version.restype = C.c_int
+    abi = lib.gcs_abi_version()
+    if abi != ABI_VERSION:
+        raise RuntimeError(f"{path}: ABI {abi}, this binding is ABI {ABI_VERSION}; rebuild the library "
+                           "(make -C gc-slam_amd)")
     for name, res, args in _SIGS:
         # test-only entries (gcs_debug_*) may be absent from an older build loaded through GCSLAM_LIB
         # for a same-box A/B; every other entry point is required

@@ -182,6 +182,20 @@ class HypothesisContext:
         """gcs_ctx_set_debug (test knobs: L.DEBUG_SCAN_SPIN_LIMIT, L.DEBUG_INJECT_SCAN_FAIL)."""
         self._chk(self.lib.gcs_ctx_set_debug(self.h, int(key), int(value)), "set_debug")
 
+    def mirror_stats(self):
+        """gcs_ctx_mirror_stats: (mirrors accepted, of them re-read at least once, via stream sync)."""
+        out = np.zeros(3, np.int64)
+        self._chk(self.lib.gcs_ctx_mirror_stats(self.h, out.ctypes.data_as(L.c_int64_p)), "mirror_stats")
+        return tuple(int(x) for x in out)
+
+    def state_checksums(self):
+        """gcs_debug_state_checksums: FNV-1a of [ScanBinStats, map, derived, touched, flags, bin-kernel
+        partial rows, device scalars, host mirror scalars] after the context's streams drain."""
+        out = np.zeros(8, np.uint64)
+        self._chk(self.lib.gcs_debug_state_checksums(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64))),
+                  "state_checksums")
+        return tuple(int(x) for x in out)
+
     def synchronize(self):
         self._chk(self.lib.gcs_ctx_synchronize(self.h), "synchronize")
 

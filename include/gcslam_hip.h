@@ -47,7 +47,9 @@
 extern "C" {
 #endif
 
-#define GCS_ABI_VERSION 2
+/* 3: GCS_ASSOC_CERT_LEN 18 -> 21 (gcs_assoc_outputs grew), the scan mirror's sequence / checksum
+ * (gcs_ctx_mirror_stats) and the state checksums (gcs_debug_state_checksums) */
+#define GCS_ABI_VERSION 3
 #define GCS_D_Z 22
 #define GCS_SCAN_FIELDS 26   /* ScanBinStats, field-major: N, s_dir[3], S_dir_scatter[9], p_bar[3], Sigma_p[9], kappa */
 #define GCS_MAP_FIELDS 26    /* MapBinStats: S_dir[3], S_dir_scatter[9], N_dir, N_pos, sum_p[3], sum_ppT[9] */
@@ -229,7 +231,22 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * scan's bucket counts and active-flag buffer, so that scan's k_budget only sums the weights; 0 keeps
  * the clears in k_budget (A/B knob and its bitwise test). */
 #define GCS_DEBUG_PT_CLEAR 8
+/* GCS_DEBUG_MIRROR_TORN (microseconds, 0 = off): the PT fold stores the scan mirror's sequence word
+ * and checksum first and its data that long after, so the host meets a mirror whose data words have
+ * not arrived; gcs_scan must re-read until the checksum matches (gcs_ctx_mirror_stats counts it) and
+ * return the same results.  Test knob of the mirror guard. */
+#define GCS_DEBUG_MIRROR_TORN 9
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
+/* The scan mirror (the PT fold's copy of the scan's scalars and device error words to pinned host
+ * memory, with the scan's sequence number and a checksum; the host accepts it only when both match):
+ * out[0] mirrors accepted, out[1] of them after at least one re-read (a data word arrived after the
+ * sequence word), out[2] accepted only after the 20 ms poll gave up and the stream synchronized. */
+int gcs_ctx_mirror_stats(gcs_ctx* ctx, int64_t* out /*3*/);
+/* Determinism diagnostics (tools/determinism_check.py, tests): 64-bit FNV-1a checksums of the
+ * context's device state after its streams drain: [0] ScanBinStats, [1] MapBinStats, [2] derived map
+ * stats, [3] touched bytes, [4] both active-flag buffers, [5] the bin kernel's partial rows, [6] the
+ * device scalar block, [7] the host mirror's scalar block (device order; byte images). */
+int gcs_debug_state_checksums(gcs_ctx* ctx, uint64_t* out /*8*/);
 int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*GCS_N_STAGES*/, int64_t* counts /*GCS_N_STAGES*/,
                         int32_t reset);
 int gcs_ctx_set_atlas(gcs_ctx* ctx, const double* dirs_host /*B*3*/);

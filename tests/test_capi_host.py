@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol(lib):
     assert declared == set(L.SYMBOLS), declared ^ set(L.SYMBOLS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.gcs_abi_version() == 2
+    assert lib.gcs_abi_version() == 3
 
 
 @pytest.mark.parametrize("n", [3, 6, 22])

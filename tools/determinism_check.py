@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Run-to-run determinism of the scale-mode scan sequence (the trajectory test's: 12 scans, B = 5,000,
 N = 4,096, the hypothesis combine after each): REPS fresh contexts in one process, each sequence's
-per-scan z_t compared bitwise with the first's.  Prints the number of distinct sequences and the
-largest z_t difference.
+per-scan z_t compared bitwise with the first's.  Prints the number of distinct sequences, the
+largest z_t difference and any scan mirror that was re-read or taken after a stream synchronize.
 
-  python tools/determinism_check.py [reps=20]      (DET_STAGES=1: also the first differing scan of
-                                                   ScanBinStats and of the map, per differing run)
+  python tools/determinism_check.py [reps=20]      (DET_STAGES=1: also the first differing scan of each
+                                                   device state checksum, gcs_debug_state_checksums)
 """
 import os
 import sys
@@ -13,7 +13,8 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-STAGES = os.environ.get("DET_STAGES", "0") == "1"  # also compare ScanBinStats / map per scan (syncs)
+STAGES = os.environ.get("DET_STAGES", "0") == "1"  # also compare the device state checksums per scan (syncs)
+PARTS = ["ScanBinStats", "map", "derived", "touched", "flags", "bin partial rows", "device scalars", "host mirror"]
 sys.path[:0] = [os.path.join(ROOT, "gc-slam_amd"), os.path.join(ROOT, "tests"), ROOT]
 
 
@@ -26,9 +27,9 @@ def main():
     from gcslam.distributed import combine_allreduce
     from gcslam.synthetic import scan_kwargs
     scans = [synthetic.make_scan(4096, s) for s in range(12)]
-    runs, st_runs, map_runs = [], [], []
+    runs, st_runs = [], []
     for r in range(reps):
-        stats, maps = [], []
+        stats = []
         ctx = HypothesisContext(n_bins=5000, n_points_cap=4096, max_raw_points=4096, mode="scale",
                                 lidar_origin=tuple(ORIGIN))
         zs = []
@@ -39,17 +40,16 @@ def main():
                 w = torch.from_numpy(sc["weights"]).cuda()
                 out = ctx.scan(rec, 16, t, w, 4096, **scan_kwargs(sc))
                 zs.append(np.array(out.z_t[:], np.float64))
-                if STAGES:  # the scan's ScanBinStats and the map after its pushforward, as checksums
-                    stats.append(ctx.get_scan_stats().tobytes())
                 combine_allreduce(ctx, 0, 1, s, want_belief=False)
-                if STAGES:
-                    torch.cuda.synchronize()
-                    maps.append(np.asarray(ctx.get_map()[0]).tobytes())
+                if STAGES:  # the device state the next scan reads, after this scan's pushforward
+                    stats.append(ctx.state_checksums())
+            mstats = ctx.mirror_stats()
         finally:
             ctx.close()
+        if mstats[1] or mstats[2]:
+            print(f"run {r}: mirror accepted {mstats[0]}, re-read {mstats[1]}, via stream sync {mstats[2]}", flush=True)
         runs.append(np.stack(zs))
         st_runs.append(stats)
-        map_runs.append(maps)
         # other GPU work between the sequences (fresh allocations land on reused memory)
         junk = torch.randn(1 << 22, device="cuda") * (r + 1)
         del junk
@@ -58,13 +58,16 @@ def main():
     distinct = len({z.tobytes() for z in runs})
     print(f"{reps} sequences: {distinct} distinct; max |z - z_first| per run: "
           + " ".join(f"{d:.1e}" for d in diffs), flush=True)
-    if STAGES:  # per differing run: the first scan whose z_t, ScanBinStats or map differs
+    if STAGES:  # per differing run: the first scan whose z_t or any state checksum differs
         for r in range(1, reps):
             fz = next((i for i in range(len(scans)) if not np.array_equal(runs[r][i], base[i])), None)
-            fs = next((i for i in range(len(scans)) if st_runs[r][i] != st_runs[0][i]), None)
-            fm = next((i for i in range(len(scans)) if map_runs[r][i] != map_runs[0][i]), None)
-            if fz is not None or fs is not None or fm is not None:
-                print(f"run {r}: first differing scan -- z_t {fz}, ScanBinStats {fs}, map {fm}", flush=True)
+            first = {}
+            for k, name in enumerate(PARTS):
+                i = next((i for i in range(len(scans)) if st_runs[r][i][k] != st_runs[0][i][k]), None)
+                if i is not None:
+                    first[name] = i
+            if fz is not None or first:
+                print(f"run {r}: first differing scan -- z_t {fz}, state {first}", flush=True)
 
 
 if __name__ == "__main__":
