@@ -44,8 +44,17 @@ CONFIGS = {
 METRIC = "scans/sec (14-step pipeline) at 64k pts/scan"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 N_SCANS = 8             # distinct synthetic scans resident in HBM, cycled
-TIMING_STRIDE = 8       # roofline kernel stamped on every 8th scan of the timed region
-ROOFLINE_MIN = 16       # stamped launches behind `roofline` (a post-region pass tops short runs up)
+ROOFLINE_MIN = 16       # stamped launches of the roofline kernel inside the timed region (at least)
+
+
+def timing_stride(steps):
+    """Every TIMING_STRIDE-th scan of the timed region stamps the roofline kernel with HIP events on its
+    stream: the largest stride (at most 8) that still stamps ROOFLINE_MIN launches inside the region
+    (the driver's 20-step run: every scan).  GCSLAM_BENCH_STRIDE overrides (A/B of the stamping cost)."""
+    e = os.environ.get("GCSLAM_BENCH_STRIDE")
+    if e:
+        return max(1, int(e))
+    return max(1, min(8, steps // ROOFLINE_MIN))
 
 
 def bins_kernel_bytes(N, B):
@@ -628,6 +637,8 @@ def main():
                          "through the drop-in, one hypothesis per rank (primitive_path_main)")
     ap.add_argument("--share-device", action="store_true",
                     help="--path primitive: every rank on device 0, gloo transport (a rehearsal on one GPU)")
+    ap.add_argument("--no-rccl", action="store_true",
+                    help="N = 1 only: combine on the host without a world-1 RCCL communicator (A/B of the collective)")
     ap.add_argument("--cpu-rehearsal", action="store_true",
                     help="launcher + payload exchange over gloo on CPU (test of the multi-rank path)")
     args = ap.parse_args()
@@ -664,16 +675,22 @@ def main():
     from gcslam.distributed import HypothesisComm
     from gcslam.synthetic import scan_kwargs
 
-    # the per-scan exchange runs in the library over RCCL (torch.distributed only broadcasts the id)
-    comm = HypothesisComm(rank, world, local_rank) if world > 1 else None
+    # the per-scan exchange runs in the library over RCCL (torch.distributed only broadcasts the id); at
+    # N = 1 too (a world-1 communicator), so the timed step runs the ncclAllReduce path of the N-GPU run
+    comm = HypothesisComm(rank, world, local_rank) if (world > 1 or not args.no_rccl) else None
     rccl = None
     if comm is not None:
         n_comm, r_comm = comm.count()
-        cnt = torch.tensor([n_comm, r_comm], dtype=torch.int64, device=device)
-        allc = [torch.zeros_like(cnt) for _ in range(world)]
-        dist.all_gather(allc, cnt)
-        rccl = dict(comm_count=n_comm, user_ranks=[int(c[1]) for c in allc], counts=[int(c[0]) for c in allc])
-        if any(int(c[0]) != world for c in allc):
+        allc = [(n_comm, r_comm)]
+        if world > 1:
+            cnt = torch.tensor([n_comm, r_comm], dtype=torch.int64, device=device)
+            allc = [torch.zeros_like(cnt) for _ in range(world)]
+            dist.all_gather(allc, cnt)
+            allc = [(int(c[0]), int(c[1])) for c in allc]
+        rccl = dict(comm_count=n_comm, user_ranks=[c[1] for c in allc], counts=[c[0] for c in allc],
+                    collective="ncclAllReduce(sum, f64) of the 840-word payload per scan on the context's combine "
+                               "stream, inside the timed step")
+        if any(c[0] != world for c in allc):
             raise RuntimeError(f"RCCL communicator holds {rccl['counts']} ranks, expected {world}")
     cfg = CONFIGS[args.config]
     N, B, K = cfg["N"], cfg["B"], cfg["K"]
@@ -709,6 +726,8 @@ def main():
 
     comb_ms = []  # every timed step's combine (pack, all-reduce, IW / Q apply), for SCALE's attribution
 
+    TIMING_STRIDE = timing_stride(args.steps)
+
     def step():
         if state["sample"]:  # roofline-kernel event stamps on every TIMING_STRIDE-th scan
             phase = state["count"] % TIMING_STRIDE
@@ -718,20 +737,18 @@ def main():
                 ctx.enable_timing(False)
         scan_fn(prepared[state["count"] % N_SCANS])
         out = scan_out
-        if state["count"] % TIMING_STRIDE == TIMING_STRIDE // 2:  # host sub-spans: sampled scans without event stamps
-            tc = time.perf_counter()
-            combine(state["count"])
-            host_ms[4] += (time.perf_counter() - tc) * 1e3
+        tc = time.perf_counter()
+        combine(state["count"])
+        dc = (time.perf_counter() - tc) * 1e3
+        if state["sample"]:
+            comb_ms.append(dc)
+        if state["count"] % TIMING_STRIDE == TIMING_STRIDE // 2:  # host sub-spans (stride 1: every scan)
+            host_ms[4] += dc
             sm = out.stage_ms
             for k in range(4):
                 host_ms[k] += sm[k]
                 host_ms[5 + k] += sm[4 + k]
             state["sampled"] += 1
-        else:
-            tc = time.perf_counter()
-            combine(state["count"])
-            if state["sample"]:
-                comb_ms.append((time.perf_counter() - tc) * 1e3)
         if follow is not None:
             follow(prepared[state["count"] % N_SCANS])
         state["count"] += 1
@@ -798,6 +815,11 @@ def main():
     stage_avg = {name: (float(ms_sum[i] / counts[i]) if counts[i] else None) for i, name in enumerate(ctx.STAGES)}
     ctx.enable_timing(False)
     manifest = ctx.describe()
+    ms_ = ctx.mirror_stats()
+    mirror = dict(scan_mirrors=ms_[0], scan_rereads=ms_[1], scan_sync_fallbacks=ms_[2], allreduces=ms_[3],
+                  allreduce_rereads=ms_[4], allreduce_sync_fallbacks=ms_[5],
+                  note="host hand-offs accepted by sequence word + checksum (gcs_layout.h Mirror); a re-read is a "
+                       "buffer whose data reached host memory after its sequence word")
     ctx.close()
 
     if rank == 0:
@@ -825,10 +847,11 @@ def main():
             # per rank: host pinning, sampled host split (host_ms keys), every timed step's combine latency
             "per_rank": per_rank,
             "rccl": rccl,
+            "mirror": mirror,
             "step_ms": {"median": float(np.median(per_step) * 1e3), "p90": float(np.percentile(per_step, 90) * 1e3),
                         "min": float(per_step.min() * 1e3), "max": float(per_step.max() * 1e3)},
             "roofline": dict(roofline(N, B, bins_ms, *pmc_traffic(args.config)) or {}, timed_launches=bins_samples,
-                             timed_launches_in_region=bins_in_region),
+                             timed_launches_in_region=bins_in_region, stamp_stride=TIMING_STRIDE),
             "roofline_chain": roofline_chain(N, B, stage_avg, f"{args.config} (diagnostic pass, every stage stamped)"),
             "stage_ms": stage_avg,
             "host_ms": host_avg,

@@ -221,8 +221,21 @@ struct gcs_ctx {
     return e && strcmp(e, "legacy") == 0;
   }();
   // hypothesis all-reduce payload (gcs_combine_allreduce): pinned host staging + device buffer
-  double* h_payload = nullptr;
-  double* d_payload = nullptr;
+  double* h_payload = nullptr;   // pinned, coherent, mapped: the packed payload (dh_payload: device view)
+  double* dh_payload = nullptr;
+  double* d_payload = nullptr;   // device: RCCL's in-place buffer
+  double* h_psum = nullptr;      // pinned, coherent, mapped: the sum + sequence + checksum (k_payload_out)
+  double* dh_psum = nullptr;
+  hipStream_t comm_stream = nullptr;  // the all-reduce's own stream (never queued behind the scan's kernels)
+  uint64_t pay_seq = 0;          // host copy of d_pay_seq (k_payload_out increments it once per launch)
+  uint64_t* d_pay_seq = nullptr;
+  // the all-reduce as one captured graph [stage in, ncclAllReduce, stage out] per (communicator,
+  // length): one launch call instead of RCCL's per-call enqueue (GCSLAM_COMBINE_GRAPH=0: direct calls)
+  hipGraph_t comb_graph = nullptr;
+  hipGraphExec_t comb_exec = nullptr;
+  void* comb_comm = nullptr;
+  int comb_len = 0;
+  int64_t pay_rereads = 0, pay_syncs = 0;
   // host state
   Belief belief{};
   // the lifted Cholesky factor of belief.L and its inverse, left by the last scan's tail (the
@@ -250,9 +263,11 @@ struct gcs_ctx {
   double grav[3] = {0.0, 0.0, 0.0};  // gravity_W * imu_gravity_scale
   // device stage timing (hipEvents on the context stream; harvested lazily)
   uint32_t timing_mask = 0;
-  bool pending = false;
-  hipEvent_t ev[kStages][2] = {};
-  bool ev_rec[kStages] = {};
+  // a ring of event pairs per stage: each stamped launch takes the next pair, and the pairs are read
+  // back (harvest) only by gcs_ctx_stage_times or when a ring is full -- never on the scan's path
+  static constexpr int kEvRing = 256;
+  std::vector<hipEvent_t> ev[kStages];  // 2 * kEvRing events per stage once timing is enabled
+  int ev_n[kStages] = {};               // pairs recorded since the last harvest
   double stage_ms_sum[kStages] = {};
   long stage_count[kStages] = {};
 };
@@ -318,19 +333,20 @@ int join_push(gcs_ctx* c) {
 constexpr int kRedBlocks = 1024;
 int red_blocks(long n) { return (int)std::max(1L, std::min((long)kRedBlocks, (n + 255) / 256)); }
 
-void harvest(gcs_ctx* c) {
-  if (!c->pending) return;
-  for (int st = 0; st < kStages; ++st) {
-    if (!c->ev_rec[st]) continue;
-    (void)hipEventSynchronize(c->ev[st][1]);
+// read back a stage's recorded event pairs (oldest first; each waits for its end event)
+void harvest_stage(gcs_ctx* c, int st) {
+  for (int i = 0; i < c->ev_n[st]; ++i) {
+    (void)hipEventSynchronize(c->ev[st][2 * i + 1]);
     float ms = 0.0f;
-    if (hipEventElapsedTime(&ms, c->ev[st][0], c->ev[st][1]) == hipSuccess) {
+    if (hipEventElapsedTime(&ms, c->ev[st][2 * i], c->ev[st][2 * i + 1]) == hipSuccess) {
       c->stage_ms_sum[st] += ms;
       c->stage_count[st] += 1;
     }
-    c->ev_rec[st] = false;
   }
-  c->pending = false;
+  c->ev_n[st] = 0;
+}
+void harvest(gcs_ctx* c) {
+  for (int st = 0; st < kStages; ++st) harvest_stage(c, st);
 }
 
 // Stage events are stamped by the stage's own kernel dispatches (hipExtLaunchKernel), so timing
@@ -340,11 +356,11 @@ struct StageEv {
 };
 StageEv stage_ev(gcs_ctx* c, int st) {
   StageEv e;
-  if ((c->timing_mask >> st) & 1u) {
-    e.e0 = c->ev[st][0];
-    e.e1 = c->ev[st][1];
-    c->ev_rec[st] = true;
-    c->pending = true;
+  if (((c->timing_mask >> st) & 1u) && !c->ev[st].empty()) {
+    if (c->ev_n[st] == gcs_ctx::kEvRing) harvest_stage(c, st);  // a full ring (long timed runs)
+    const int i = c->ev_n[st]++;
+    e.e0 = c->ev[st][2 * i];
+    e.e1 = c->ev[st][2 * i + 1];
   }
   return e;
 }
@@ -491,7 +507,6 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
                  bool xyz_f64 = false, double* iz_out = nullptr, bool deskew_only = false, double* t_out = nullptr) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
   if (point_step < (xyz_f64 ? 24 : 12)) return fail(c, GCS_ERR_ARG, "point_step too small for x, y, z");
-  harvest(c);
   StageEv ev = stage_ev(c, ST_POINTS);
   if (!c->budget_pending)  // k_budget not queued earlier by gcs_scan
     if (int rc = stage_budget(c, w, n_raw)) return rc;
@@ -649,13 +664,6 @@ int stage_mf(gcs_ctx* c) {
   return GCS_OK;
 }
 
-// checksum of the mirror as read from host memory (k_final's, gcs_layout.h Mirror)
-uint64_t mirror_sum(const volatile uint64_t* m) {
-  uint64_t s = 0;
-  for (int i = 0; i < MIR_SEQ; ++i) s += mirror_word_hash(m[i], (uint32_t)i);
-  return s + mirror_word_hash(m[MIR_SEQ], MIR_SEQ);
-}
-
 // a validated mirror's error words into h_err (a word stays set until the check that reads it clears it)
 void take_mirror_err(gcs_ctx* c) {
   const uint64_t* m = reinterpret_cast<const uint64_t*>(c->h_scalars);
@@ -665,33 +673,36 @@ void take_mirror_err(gcs_ctx* c) {
   }
 }
 
-// Wait for the scan's device stages: the PT fold writes the scalar block and the error words to the
-// host mirror, then the checksum and the scan's sequence number (k_final).  The host polls the
-// sequence word (a stream synchronize returns some microseconds after the kernel ends) and accepts the
-// mirror only when the checksum of what it reads matches: a mirror whose data words have not all
-// reached host memory when the sequence word has is re-read (mirror_rereads), never consumed.  Without
-// a valid mirror after 20 ms (a fault, or a stalled queue) the stream synchronize waits and reports
-// the asynchronous error, and the mirror must then be complete.  Nothing later in the scan reads
-// device memory outside stream order.  GCSLAM_SYNC_WAIT=stream: synchronize only.
-int wait_mirror(gcs_ctx* c) {
+// Wait for a stamped host buffer: words [0, n) of data, [n] the sequence number of the launch that
+// writes it, [n + 1] the checksum sum_i mirror_word_hash(w_i, i) + mirror_word_hash(seq, n) (k_final's
+// scan mirror, k_payload_out's all-reduce sum).  The host polls the sequence word (a stream
+// synchronize returns some microseconds after the kernel ends) and accepts the buffer only when the
+// checksum of what it reads matches: a buffer whose data words have not all reached host memory when
+// the sequence word has is re-read (*rereads), never consumed.  Without a valid buffer after 20 ms (a
+// fault, or a stalled queue) the stream synchronize waits and reports the asynchronous error (*syncs),
+// and the buffer must then be complete.  GCSLAM_SYNC_WAIT=stream: synchronize only.
+uint64_t stamped_sum(const volatile uint64_t* m, int n) {
+  uint64_t s = 0;
+  for (int i = 0; i < n; ++i) s += mirror_word_hash(m[i], (uint32_t)i);
+  return s + mirror_word_hash(m[n], (uint32_t)n);
+}
+
+int wait_stamped(gcs_ctx* c, const double* buf, int n, uint64_t seq, hipStream_t stream, int64_t* rereads,
+                 int64_t* syncs, const char* what) {
   static const bool spin = [] {
     const char* e = getenv("GCSLAM_SYNC_WAIT");
     return !(e && strcmp(e, "stream") == 0);
   }();
-  const volatile uint64_t* m = reinterpret_cast<const volatile uint64_t*>(c->h_scalars);
-  const uint64_t seq = c->mirror_seq;
+  const volatile uint64_t* m = reinterpret_cast<const volatile uint64_t*>(buf);
   if (spin) {
     const auto t0 = clk::now();
     bool reread = false;
     for (;;) {
-      if (m[MIR_SEQ] == seq) {
+      if (m[n] == seq) {
         std::atomic_thread_fence(std::memory_order_acquire);
-        if (mirror_sum(m) == m[MIR_SUM]) {
+        if (stamped_sum(m, n) == m[n + 1]) {
           std::atomic_thread_fence(std::memory_order_acquire);
-          take_mirror_err(c);
-          ++c->mirror_scans;
-          if (reread) ++c->mirror_rereads;
-          c->stages_done = true;
+          if (reread) ++*rereads;
           return GCS_OK;
         }
         reread = true;  // the sequence word is here, some data word is not yet: read again
@@ -699,12 +710,22 @@ int wait_mirror(gcs_ctx* c) {
       __builtin_ia32_pause();
       if (clk::now() - t0 > std::chrono::milliseconds(20)) break;
     }
-    ++c->mirror_syncs;
+    ++*syncs;
   }
-  HIPCHK(c, hipStreamSynchronize(c->stream));
-  if (m[MIR_SEQ] != seq || mirror_sum(m) != m[MIR_SUM])
-    return fail(c, GCS_ERR_HIP, "scan mirror: sequence " + std::to_string((unsigned long long)m[MIR_SEQ]) + " / checksum do not match scan " +
-                                    std::to_string((unsigned long long)seq) + " after the stream synchronized");
+  HIPCHK(c, hipStreamSynchronize(stream));
+  if (m[n] != seq || stamped_sum(m, n) != m[n + 1])
+    return fail(c, GCS_ERR_HIP, std::string(what) + ": sequence " + std::to_string((unsigned long long)m[n]) +
+                                    " / checksum do not match launch " + std::to_string((unsigned long long)seq) +
+                                    " after the stream synchronized");
+  return GCS_OK;
+}
+
+// Wait for the scan's device stages: the PT fold's scan mirror (k_final; gcs_layout.h Mirror) through
+// wait_stamped.  Nothing later in the scan reads device memory outside stream order.
+int wait_mirror(gcs_ctx* c) {
+  if (int rc = wait_stamped(c, c->h_scalars, MIR_SEQ, c->mirror_seq, c->stream, &c->mirror_rereads, &c->mirror_syncs,
+                            "scan mirror"))
+    return rc;
   take_mirror_err(c);
   ++c->mirror_scans;
   c->stages_done = true;
@@ -1244,11 +1265,18 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (c->h_gate) (void)hipHostFree(c->h_gate);
   if (c->h_preint_in) (void)hipHostFree(c->h_preint_in);
   if (c->h_preint_out) (void)hipHostFree(c->h_preint_out);
+  if (c->comm_stream) {
+    (void)hipStreamSynchronize(c->comm_stream);
+    if (c->comb_exec) (void)hipGraphExecDestroy(c->comb_exec);
+    if (c->comb_graph) (void)hipGraphDestroy(c->comb_graph);
+    (void)hipStreamDestroy(c->comm_stream);
+  }
+  if (c->d_pay_seq) (void)hipFree(c->d_pay_seq);
   if (c->h_payload) (void)hipHostFree(c->h_payload);
+  if (c->h_psum) (void)hipHostFree(c->h_psum);
   if (c->d_payload) (void)hipFree(c->d_payload);
   for (int st = 0; st < kStages; ++st)
-    for (int k = 0; k < 2; ++k)
-      if (c->ev[st][k]) (void)hipEventDestroy(c->ev[st][k]);
+    for (hipEvent_t e : c->ev[st]) (void)hipEventDestroy(e);
   if (c->ev_push) (void)hipEventDestroy(c->ev_push);
   if (c->ev_stages) (void)hipEventDestroy(c->ev_stages);
   if (c->push_stream) (void)hipStreamDestroy(c->push_stream);
@@ -1324,6 +1352,9 @@ int gcs_ctx_mirror_stats(gcs_ctx* c, int64_t* out) {
   out[0] = c->mirror_scans;
   out[1] = c->mirror_rereads;
   out[2] = c->mirror_syncs;
+  out[3] = (int64_t)c->pay_seq;
+  out[4] = c->pay_rereads;
+  out[5] = c->pay_syncs;
   return GCS_OK;
 }
 
@@ -1366,9 +1397,11 @@ int gcs_debug_state_checksums(gcs_ctx* c, uint64_t* out) {
 
 int gcs_ctx_enable_timing(gcs_ctx* c, int32_t stage_mask) {
   if (!c) return GCS_ERR_ARG;
-  if (stage_mask && !c->ev[0][0])
-    for (int st = 0; st < kStages; ++st)
-      for (int k = 0; k < 2; ++k) HIPCHK(c, hipEventCreate(&c->ev[st][k]));
+  if (stage_mask && c->ev[0].empty())
+    for (int st = 0; st < kStages; ++st) {
+      c->ev[st].resize(2 * gcs_ctx::kEvRing, nullptr);
+      for (hipEvent_t& e : c->ev[st]) HIPCHK(c, hipEventCreate(&e));
+    }
   c->timing_mask = (uint32_t)stage_mask;
   return GCS_OK;
 }
@@ -2417,8 +2450,16 @@ int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, in
   if (!c) return GCS_ERR_ARG;
   constexpr int kLen = GCS_PAYLOAD_LEN + GCS_MAP_REC_LEN;
   if (!c->h_payload) {
-    HIPCHK(c, hipHostMalloc(&c->h_payload, kLen * sizeof(double), hipHostMallocDefault));
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    HIPCHK(c, hipHostMalloc(&c->h_payload, kLen * sizeof(double), fl));
+    HIPCHK(c, hipHostGetDevicePointer((void**)&c->dh_payload, c->h_payload, 0));
+    HIPCHK(c, hipHostMalloc(&c->h_psum, (kLen + 2) * sizeof(double), fl));
+    memset(c->h_psum, 0, (kLen + 2) * sizeof(double));
+    HIPCHK(c, hipHostGetDevicePointer((void**)&c->dh_psum, c->h_psum, 0));
     HIPCHK(c, hipMalloc(&c->d_payload, kLen * sizeof(double)));
+    HIPCHK(c, hipMalloc(&c->d_pay_seq, sizeof(uint64_t)));
+    HIPCHK(c, hipMemset(c->d_pay_seq, 0, sizeof(uint64_t)));
+    c->pay_seq = 0;
   }
   if (int rc = gcs_hypothesis_payload(c, w_iw, w_bary, c->h_payload)) return rc;
   // one map (LEAD / FOLLOW): the lead's map-update record rides the same all-reduce (zeros elsewhere)
@@ -2427,21 +2468,65 @@ int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, in
   if (shared_map)
     for (int k = 0; k < GCS_MAP_REC_LEN; ++k)
       c->h_payload[GCS_PAYLOAD_LEN + k] = c->map_mode == GCS_MAP_LEAD ? c->map_rec[k] : 0.0;
+  const double* sum = c->h_payload;
   if (comm) {
-    // the reduction rides the context stream; the previous scan's pushforward keeps running on
-    // push_stream underneath it
-    hipStream_t s = c->stream;
-    HIPCHK(c, hipMemcpyAsync(c->d_payload, c->h_payload, len * sizeof(double), hipMemcpyHostToDevice, s));
-    ncclResult_t r = ncclAllReduce(c->d_payload, c->d_payload, len, ncclDouble, ncclSum, (ncclComm_t)comm, s);
-    if (r != ncclSuccess) return fail(c, GCS_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-    HIPCHK(c, hipMemcpyAsync(c->h_payload, c->d_payload, len * sizeof(double), hipMemcpyDeviceToHost, s));
-    HIPCHK(c, hipStreamSynchronize(s));
+    // The reduction rides its own stream: nothing the scan queued on the context stream (k_tile_order
+    // behind the PT fold) or the push stream (the pushforward) is ahead of it.  The payload needs no
+    // device ordering: it is host data of the finished scan.  Stage in (mapped read), ncclAllReduce in
+    // place, stage out with sequence + checksum, host poll: no copy call and no stream synchronize.
+    if (!c->comm_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    hipStream_t s = c->comm_stream;
+    static const bool use_graph = [] {
+      const char* e = getenv("GCSLAM_COMBINE_GRAPH");
+      return !(e && atoi(e) == 0);
+    }();
+    static const bool probe_noccl = [] {  // timing probe (world 1 only): the staging without the collective
+      const char* e = getenv("GCSLAM_COMBINE_PROBE");
+      return e && strcmp(e, "noccl") == 0;
+    }();
+    auto enqueue = [&]() -> int {
+      HIPCHK(c, launch_payload_in(c->dh_payload, c->d_payload, len, s));
+      if (!probe_noccl) {
+        ncclResult_t r = ncclAllReduce(c->d_payload, c->d_payload, len, ncclDouble, ncclSum, (ncclComm_t)comm, s);
+        if (r != ncclSuccess) return fail(c, GCS_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+      }
+      HIPCHK(c, launch_payload_out(c->d_payload, c->dh_psum, len, c->d_pay_seq, s));
+      return GCS_OK;
+    };
+    if (use_graph && (c->comb_exec == nullptr || c->comb_comm != comm || c->comb_len != len)) {
+      if (c->comb_exec) HIPCHK(c, hipGraphExecDestroy(c->comb_exec));
+      if (c->comb_graph) HIPCHK(c, hipGraphDestroy(c->comb_graph));
+      c->comb_exec = nullptr;
+      c->comb_graph = nullptr;
+      HIPCHK(c, hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      const int rc = enqueue();
+      hipGraph_t g = nullptr;
+      const hipError_t ce = hipStreamEndCapture(s, &g);
+      if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+      }
+      HIPCHK(c, ce);
+      c->comb_graph = g;
+      HIPCHK(c, hipGraphInstantiate(&c->comb_exec, g, nullptr, nullptr, 0));
+      c->comb_comm = comm;
+      c->comb_len = len;
+    }
+    if (use_graph) {
+      HIPCHK(c, hipGraphLaunch(c->comb_exec, s));
+    } else if (int rc = enqueue()) {
+      return rc;
+    }
+    const uint64_t seq = ++c->pay_seq;
+    if (int rc = wait_stamped(c, c->h_psum, len, seq, s, &c->pay_rereads, &c->pay_syncs, "hypothesis all-reduce"))
+      return rc;
+    sum = c->h_psum;
   }
   if (shared_map) {  // a single rank carries its own record (a follower then replays its own update)
-    memcpy(c->lead_rec, comm ? c->h_payload + GCS_PAYLOAD_LEN : c->map_rec, sizeof(c->lead_rec));
+    memcpy(c->lead_rec, comm ? sum + GCS_PAYLOAD_LEN : c->map_rec, sizeof(c->lead_rec));
     c->have_lead_rec = true;
   }
-  return combine_into_ctx(c, c->h_payload, scan_count, comb, cert);
+  return combine_into_ctx(c, sum, scan_count, comb, cert);
 }
 
 int gcs_ctx_set_map_mode(gcs_ctx* c, int32_t mode) {

@@ -1246,6 +1246,78 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
 // 5 waves per SIMD needs <= 96 VGPRs (the register allocator spills ~28 dwords to reach it)
 #define GCS_BINS_WAVES_SMALL 0
 #endif
+#ifndef GCS_GATHER_BAL
+// phase C's lanes (tiles finalized by the first waves, !DALL): 1 gives each bin of a wave a lane group
+// sized by its records (balanced), 0 the fixed LANES lanes per bin of rounds 1-4
+#define GCS_GATHER_BAL 1
+#endif
+// Balanced phase-C lanes.  Wave wid gathers the bins [wid BW, wid BW + BW) (BW = 64 / LANES, the fixed
+// partition of rounds 1-4), but the 64 lanes are dealt by work: with W records and nz non-empty bins
+// in the wave and c = ceil(W / (64 - nz)), bin b gets cnt_b = ceil(w_b / c) contiguous lanes (sum <= 64:
+// ceil(w_b / c) < w_b / c + 1), so no lane visits more than c records (the fixed split let the
+// heaviest bin's lanes visit w_max / LANES: C2 55 / 4 against a balanced 10, C3 50 / 2 against 12).
+// Lane j of a group takes records [w_b j / cnt_b, w_b (j + 1) / cnt_b) of the bin's list; the group's
+// sums meet in a fixed segmented tree (seg_reduce), so the result is deterministic.  All integer,
+// wave-uniform control; lanes past the last group idle (lb valid, empty range).
+template <int LANES>
+__device__ __forceinline__ void balanced_lanes(const uint32_t* s_work, int wid, int lane, int& lb, uint32_t& i0,
+                                               uint32_t& i1, int& j, int& cnt_b, int& maxl) {
+  constexpr int BW = 64 / LANES;
+  const uint32_t wk = lane < BW ? s_work[wid * BW + lane] : 0u;
+  uint32_t W = wk, nz = wk ? 1u : 0u;
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    W += (uint32_t)__shfl_xor((int)W, off, 64);
+    nz += (uint32_t)__shfl_xor((int)nz, off, 64);
+  }
+  const uint32_t avail = 64u - nz;
+  const uint32_t c = avail ? (W + avail - 1u) / avail : 0u;
+  const uint32_t cnt = wk ? (avail ? (wk + c - 1u) / c : 1u) : 0u;
+  uint32_t incl = cnt, mx = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)incl, off, 64);
+    if (lane >= off) incl += y;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+  maxl = (int)mx;
+  const uint32_t used = (uint32_t)__shfl((int)incl, BW - 1, 64);
+  // the lane's bin: the smallest b with incl_b > lane (incl is non-decreasing over b)
+  int b = 0;
+#pragma unroll
+  for (int bit = BW >> 1; bit >= 1; bit >>= 1) {
+    const uint32_t v = (uint32_t)__shfl((int)incl, b + bit - 1, 64);
+    if (v <= (uint32_t)lane) b += bit;
+  }
+  const uint32_t inc_b = (uint32_t)__shfl((int)incl, b, 64);
+  const uint32_t cn_b = (uint32_t)__shfl((int)cnt, b, 64);
+  const uint32_t wk_b = (uint32_t)__shfl((int)wk, b, 64);
+  lb = wid * BW + b;
+  if ((uint32_t)lane >= used) {  // idle lane
+    j = 0;
+    cnt_b = 0;
+    i0 = i1 = 0u;
+    return;
+  }
+  j = lane - (int)(inc_b - cn_b);
+  cnt_b = (int)cn_b;
+  i0 = wk_b * (uint32_t)j / cn_b;
+  i1 = wk_b * (uint32_t)(j + 1) / cn_b;
+}
+// the lane groups' sums in a fixed tree: ((s0 + s1) + (s2 + s3)) + ..., the result in the group's lane 0
+template <int NF>
+__device__ __forceinline__ void seg_reduce(double (&acc)[NF], int j, int cnt_b, int maxl) {
+  for (int off = 1; off < maxl; off <<= 1) {
+    const bool take = (j & (2 * off - 1)) == 0 && j + off < cnt_b;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const double y = __shfl_down(acc[f], off, 64);
+      if (take) acc[f] += y;
+    }
+  }
+}
+
 // DALL: phase D on every wave -- the first lane of each bin's lane group finalizes the bin from its
 // registers right after the lanes' xor tree (no LDS hand-off, no idle waves); required for tiles
 // wider than one wave (TB > 64).  !DALL: wave 0 alone, one lane per bin (the 64-bin tile's form).
@@ -1571,12 +1643,22 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   // phase C: four lanes per bin; the bin's records (sources in order, points in order) are one
   // flattened list and lane l takes the l-th quarter, so every lane's trip count is its own share
   // (no per-source max over the wave's lanes).
-  const int lb = t / LANES, l = t % LANES;
+  constexpr bool BAL = GCS_GATHER_BAL && !DALL;
+  int lb, l, seg_j = 0, seg_n = 0, seg_max = 1;
+  uint32_t i0, i1;
+  if constexpr (BAL) {
+    l = 0;
+    balanced_lanes<LANES>(s_work, wid, lane, lb, i0, i1, seg_j, seg_n, seg_max);
+  } else {
+    lb = t / LANES;
+    l = t % LANES;
+    const uint32_t work = s_work[lb];
+    i0 = work * (uint32_t)l / (uint32_t)LANES;
+    i1 = work * (uint32_t)(l + 1) / (uint32_t)LANES;
+  }
   double acc[19];
 #pragma unroll
   for (int f = 0; f < 19; ++f) acc[f] = 0.0;
-  const uint32_t work = s_work[lb];
-  const uint32_t i0 = work * (uint32_t)l / (uint32_t)LANES, i1 = work * (uint32_t)(l + 1) / (uint32_t)LANES;
   if (i1 > i0) {
     const double4 bd = s_bd[lb];
     const double inv_tau = 1.0 / a.tau;
@@ -1710,10 +1792,14 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       }
     }
   }
+  if constexpr (BAL) {
+    seg_reduce<19>(acc, seg_j, seg_n, seg_max);
+  } else {
 #pragma unroll
-  for (int f = 0; f < 19; ++f)  // the lanes' shares in a fixed xor tree: ((s0 + s1) + (s2 + s3)) + ...
+    for (int f = 0; f < 19; ++f)  // the lanes' shares in a fixed xor tree: ((s0 + s1) + (s2 + s3)) + ...
 #pragma unroll
-    for (int off = 1; off < LANES; off <<= 1) acc[f] += __shfl_xor(acc[f], off, 64);
+      for (int off = 1; off < LANES; off <<= 1) acc[f] += __shfl_xor(acc[f], off, 64);
+  }
   PROF(4);
   if constexpr (DALL) {
     // phase D on every wave: the group's first lane finalizes its bin from the summed registers
@@ -1746,7 +1832,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   if (lane == 0 && wid > 0 && wid < 4) g_prof[blockIdx.x * 16 + 10 + wid] = wall_clock64();  // waves 1-3 gather end
 #endif
   __syncthreads();  // the record stage is free: it now carries the bin sums [19][TB]
-  if (l == 0)
+  if (BAL ? (seg_n > 0 && seg_j == 0) : l == 0)  // (balanced: a bin without records has no lane group)
 #pragma unroll
     for (int f = 0; f < 19; ++f) s_rec[f * TB + lb] = acc[f];
   __syncthreads();
@@ -1765,8 +1851,9 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
   v[4] = -INFINITY;
   if (own && GCS_PROBE_NOFIN != 1) {
+    const bool has = !BAL || s_work[t] != 0u;  // a bin without records: exact-zero sums
 #pragma unroll
-    for (int f = 0; f < 19; ++f) acc[f] = s_rec[f * TB + t];
+    for (int f = 0; f < 19; ++f) acc[f] = has ? s_rec[f * TB + t] : 0.0;
     finalize_bin(acc, a.scan, a.n_bins, b0 + t, v);
     PROF(15);
     if (!GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + t);
@@ -2545,6 +2632,48 @@ __global__ __launch_bounds__(64) void k_gate(const uint64_t* gate, uint64_t seq,
                                                                         __HIP_MEMORY_SCOPE_SYSTEM))
                      : 0.0;
   if (!open) *err = 1u;
+}
+
+// ---------------------------------------------------------------- hypothesis payload staging
+// The per-scan all-reduce (gcs_combine_allreduce) on the context's combine stream without copy calls
+// or a stream synchronize: k_payload_in copies the host-packed payload (pinned, coherent, mapped) to
+// the device buffer RCCL reduces in place, k_payload_out copies the sum back to a second host buffer
+// followed by the call's sequence number and a checksum (the scan mirror's protocol, gcs_layout.h),
+// and the host polls that.  One 256-thread block each (<= 888 words: a few per thread).
+__global__ __launch_bounds__(kBlock) void k_payload_in(const double* __restrict__ src, double* dst, int n) {
+  for (int i = threadIdx.x; i < n; i += kBlock) dst[i] = src[i];
+}
+__global__ __launch_bounds__(kBlock) void k_payload_out(const double* __restrict__ src, double* host, int n,
+                                                        uint64_t* dseq) {
+  __shared__ unsigned long long lh[kWaves];
+  unsigned long long h = 0;
+  uint64_t* hw = reinterpret_cast<uint64_t*>(host);
+  for (int i = threadIdx.x; i < n; i += kBlock) {
+    const uint64_t w = (uint64_t)__double_as_longlong(src[i]);
+    hw[i] = w;
+    h += mirror_word_hash(w, (uint32_t)i);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) h += __shfl_xor(h, off, 64);
+  if ((threadIdx.x & 63) == 0) lh[threadIdx.x >> 6] = h;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {  // the launch's sequence number: a device counter (graph launches take no arguments)
+    const uint64_t seq = *dseq + 1u;
+    *dseq = seq;
+    uint64_t sum = mirror_word_hash(seq, (uint32_t)n);
+    for (int k = 0; k < kWaves; ++k) sum += lh[k];
+    hw[n + 1] = sum;
+    hw[n] = seq;
+  }
+}
+hipError_t launch_payload_in(const double* src, double* dst, int n, hipStream_t s) {
+  hipLaunchKernelGGL(k_payload_in, dim3(1), dim3(kBlock), 0, s, src, dst, n);
+  return hipGetLastError();
+}
+hipError_t launch_payload_out(const double* src, double* host, int n, uint64_t* dseq, hipStream_t s) {
+  hipLaunchKernelGGL(k_payload_out, dim3(1), dim3(kBlock), 0, s, src, host, n, dseq);
+  return hipGetLastError();
 }
 
 hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err, hipStream_t s) {

@@ -183,8 +183,9 @@ class HypothesisContext:
         self._chk(self.lib.gcs_ctx_set_debug(self.h, int(key), int(value)), "set_debug")
 
     def mirror_stats(self):
-        """gcs_ctx_mirror_stats: (mirrors accepted, of them re-read at least once, via stream sync)."""
-        out = np.zeros(3, np.int64)
+        """gcs_ctx_mirror_stats: (scan mirrors accepted, of them re-read at least once, via stream sync,
+        all-reduce sums accepted, re-read, via stream sync)."""
+        out = np.zeros(6, np.int64)
         self._chk(self.lib.gcs_ctx_mirror_stats(self.h, out.ctypes.data_as(L.c_int64_p)), "mirror_stats")
         return tuple(int(x) for x in out)
 

@@ -240,8 +240,10 @@ int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 /* The scan mirror (the PT fold's copy of the scan's scalars and device error words to pinned host
  * memory, with the scan's sequence number and a checksum; the host accepts it only when both match):
  * out[0] mirrors accepted, out[1] of them after at least one re-read (a data word arrived after the
- * sequence word), out[2] accepted only after the 20 ms poll gave up and the stream synchronized. */
-int gcs_ctx_mirror_stats(gcs_ctx* ctx, int64_t* out /*3*/);
+ * sequence word), out[2] accepted only after the 20 ms poll gave up and the stream synchronized;
+ * out[3..5] the same for the hypothesis all-reduce's stamped sum (gcs_combine_allreduce with a
+ * communicator): all-reduces run, re-read, via stream sync. */
+int gcs_ctx_mirror_stats(gcs_ctx* ctx, int64_t* out /*6*/);
 /* Determinism diagnostics (tools/determinism_check.py, tests): 64-bit FNV-1a checksums of the
  * context's device state after its streams drain: [0] ScanBinStats, [1] MapBinStats, [2] derived map
  * stats, [3] touched bytes, [4] both active-flag buffers, [5] the bin kernel's partial rows, [6] the
