@@ -817,7 +817,7 @@ def main():
     manifest = ctx.describe()
     ms_ = ctx.mirror_stats()
     mirror = dict(scan_mirrors=ms_[0], scan_rereads=ms_[1], scan_sync_fallbacks=ms_[2], allreduces=ms_[3],
-                  allreduce_rereads=ms_[4], allreduce_sync_fallbacks=ms_[5],
+                  allreduce_rereads=ms_[4], allreduce_sync_fallbacks=ms_[5], allreduce_discarded=ms_[6],
                   note="host hand-offs accepted by sequence word + checksum (gcs_layout.h Mirror); a re-read is a "
                        "buffer whose data reached host memory after its sequence word")
     ctx.close()

@@ -1247,9 +1247,11 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
 #define GCS_BINS_WAVES_SMALL 0
 #endif
 #ifndef GCS_GATHER_BAL
-// phase C's lanes (tiles finalized by the first waves, !DALL): 1 gives each bin of a wave a lane group
-// sized by its records (balanced), 0 the fixed LANES lanes per bin of rounds 1-4
-#define GCS_GATHER_BAL 1
+// phase C's lanes (tiles finalized by the first waves, !DALL): bin tiles of at least GCS_GATHER_BAL bins
+// give each bin of a wave a lane group sized by its records (balanced), smaller ones the fixed LANES
+// lanes per bin of rounds 1-4.  Same box, alternated (profiles/r05/bal/): C3 (128-bin tiles) bins
+// 84.6-85.3 -> 82.3-82.7 us; C2 (64-bin tiles) 26.9 -> 28.5-28.9 us, so 128 (0: never).
+#define GCS_GATHER_BAL 128
 #endif
 // Balanced phase-C lanes.  Wave wid gathers the bins [wid BW, wid BW + BW) (BW = 64 / LANES, the fixed
 // partition of rounds 1-4), but the 64 lanes are dealt by work: with W records and nz non-empty bins
@@ -1643,7 +1645,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   // phase C: four lanes per bin; the bin's records (sources in order, points in order) are one
   // flattened list and lane l takes the l-th quarter, so every lane's trip count is its own share
   // (no per-source max over the wave's lanes).
-  constexpr bool BAL = GCS_GATHER_BAL && !DALL;
+  constexpr bool BAL = GCS_GATHER_BAL && TB >= GCS_GATHER_BAL && !DALL;
   int lb, l, seg_j = 0, seg_n = 0, seg_max = 1;
   uint32_t i0, i1;
   if constexpr (BAL) {
@@ -2635,13 +2637,35 @@ __global__ __launch_bounds__(64) void k_gate(const uint64_t* gate, uint64_t seq,
 }
 
 // ---------------------------------------------------------------- hypothesis payload staging
-// The per-scan all-reduce (gcs_combine_allreduce) on the context's combine stream without copy calls
-// or a stream synchronize: k_payload_in copies the host-packed payload (pinned, coherent, mapped) to
-// the device buffer RCCL reduces in place, k_payload_out copies the sum back to a second host buffer
-// followed by the call's sequence number and a checksum (the scan mirror's protocol, gcs_layout.h),
-// and the host polls that.  One 256-thread block each (<= 888 words: a few per thread).
-__global__ __launch_bounds__(kBlock) void k_payload_in(const double* __restrict__ src, double* dst, int n) {
-  for (int i = threadIdx.x; i < n; i += kBlock) dst[i] = src[i];
+// The per-scan all-reduce (gcs_combine_allreduce) as an armed chain on the context's combine stream,
+// queued before the host has the payload: k_pay_gate waits on the device for the host's go (so the
+// chain's launch and dispatch latency -- ~13 us for a kernel round trip from an idle stream,
+// profiles/r05/combine/ -- leave the step), ncclAllReduce reads the payload from the pinned host buffer,
+// k_payload_out copies the sum back to a second host buffer followed by the chain's sequence number
+// and a checksum (the scan mirror's protocol, gcs_layout.h), and the host polls that.
+//
+// k_pay_gate: one lane polls the host gate word (coherent host memory, relaxed system-scope loads with
+// a short sleep) for the chain's sequence number (the device counter + 1: what k_payload_out will
+// stamp), then writes the validity word payload[n]: 1 when the host opened the gate, 0 when it
+// cancelled (the sequence number with bit 63) or the gate stayed shut for timeout ticks.  The
+// all-reduce sums that word, so every rank sees the same count: a chain that some rank did not open is
+// discarded by all of them alike (gcs_capi.cpp combine_fire).
+__global__ __launch_bounds__(64) void k_pay_gate(const uint64_t* gate, const uint64_t* dseq, double* payload, int n,
+                                                 uint64_t timeout) {
+  if (threadIdx.x != 0) return;
+  const uint64_t want = *dseq + 1u;
+  const uint64_t t0 = wall_clock64();
+  double ok = 0.0;
+  for (;;) {
+    const uint64_t g = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (g == want) {
+      ok = 1.0;
+      break;
+    }
+    if (g == (want | (1ull << 63)) || wall_clock64() - t0 > timeout) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  payload[n] = ok;
 }
 __global__ __launch_bounds__(kBlock) void k_payload_out(const double* __restrict__ src, double* host, int n,
                                                         uint64_t* dseq) {
@@ -2658,7 +2682,7 @@ __global__ __launch_bounds__(kBlock) void k_payload_out(const double* __restrict
   if ((threadIdx.x & 63) == 0) lh[threadIdx.x >> 6] = h;
   __threadfence_system();
   __syncthreads();
-  if (threadIdx.x == 0) {  // the launch's sequence number: a device counter (graph launches take no arguments)
+  if (threadIdx.x == 0) {  // the launch's sequence number: a device counter (the chain is queued ahead)
     const uint64_t seq = *dseq + 1u;
     *dseq = seq;
     uint64_t sum = mirror_word_hash(seq, (uint32_t)n);
@@ -2667,8 +2691,9 @@ __global__ __launch_bounds__(kBlock) void k_payload_out(const double* __restrict
     hw[n] = seq;
   }
 }
-hipError_t launch_payload_in(const double* src, double* dst, int n, hipStream_t s) {
-  hipLaunchKernelGGL(k_payload_in, dim3(1), dim3(kBlock), 0, s, src, dst, n);
+hipError_t launch_pay_gate(const uint64_t* gate, const uint64_t* dseq, double* payload, int n, uint64_t timeout,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_pay_gate, dim3(1), dim3(64), 0, s, gate, dseq, payload, n, timeout);
   return hipGetLastError();
 }
 hipError_t launch_payload_out(const double* src, double* host, int n, uint64_t* dseq, hipStream_t s) {
