@@ -717,7 +717,7 @@ def main():
         if not (rank == 0 and world > 1):
             follow = ctx.map_follow_call()
 
-    state = dict(count=0, sample=False, sampled=0)
+    state = dict(count=0, sample=False, sampled=0, stamp=True, combine=combine)
     scan_out = L.GcsScanOutputs()  # one output record for every scan (the caller-owned buffer form)
     scan_fn = ctx.scan_call(scan_out)
     # pre-device host, device submit+wait, host tail, whole gcs_scan, combine, then the sub-spans
@@ -729,7 +729,8 @@ def main():
     TIMING_STRIDE = timing_stride(args.steps)
 
     def step():
-        if state["sample"]:  # roofline-kernel event stamps on every TIMING_STRIDE-th scan
+        combine = state["combine"]
+        if state["sample"] and state["stamp"]:  # roofline-kernel event stamps on every TIMING_STRIDE-th scan
             phase = state["count"] % TIMING_STRIDE
             if phase == 0:
                 ctx.enable_timing(True, stages=["bins"])
@@ -784,6 +785,29 @@ def main():
     state["sample"] = False
     ms_sum, counts = ctx.stage_times(reset=True)
     bins_in_region = int(counts[2])
+    ctx.enable_timing(False)
+
+    def side_loop():  # the same steps again, a variant of the step (not `value`): its ms per step
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ta = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        ctx.synchronize()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        return (time.perf_counter() - ta) / args.steps * 1e3
+    # the decomposition of ms_per_step: without the roofline stamps, and (N = 1) with the host-only
+    # combine instead of the world-1 RCCL all-reduce -- what round 4's line measured
+    state["stamp"] = False
+    variants = {"unstamped_ms_per_step": side_loop()}
+    if world == 1 and comm is not None:
+        state["combine"] = ctx.combine_call(None, w_iw, w_bary)
+        variants["host_combine_unstamped_ms_per_step"] = side_loop()
+        state["combine"] = combine
+    state["stamp"] = True
     # the roofline kernel's duration: the timed region's stamped launches (every TIMING_STRIDE-th scan)
     # plus, when those are fewer than ROOFLINE_MIN (short runs), a pass stamping it on every scan
     if bins_in_region < ROOFLINE_MIN:
@@ -817,7 +841,7 @@ def main():
     manifest = ctx.describe()
     ms_ = ctx.mirror_stats()
     mirror = dict(scan_mirrors=ms_[0], scan_rereads=ms_[1], scan_sync_fallbacks=ms_[2], allreduces=ms_[3],
-                  allreduce_rereads=ms_[4], allreduce_sync_fallbacks=ms_[5], allreduce_discarded=ms_[6],
+                  allreduce_rereads=ms_[4], allreduce_sync_fallbacks=ms_[5],
                   note="host hand-offs accepted by sequence word + checksum (gcs_layout.h Mirror); a re-read is a "
                        "buffer whose data reached host memory after its sequence word")
     ctx.close()
@@ -848,6 +872,9 @@ def main():
             "per_rank": per_rank,
             "rccl": rccl,
             "mirror": mirror,
+            "step_variants": dict(variants, note="the same step count again after the timed region, not `value`: "
+                                  "without the roofline kernel's event stamps, and (N = 1) with the host-only "
+                                  "combine in place of the world-1 ncclAllReduce"),
             "step_ms": {"median": float(np.median(per_step) * 1e3), "p90": float(np.percentile(per_step, 90) * 1e3),
                         "min": float(per_step.min() * 1e3), "max": float(per_step.max() * 1e3)},
             "roofline": dict(roofline(N, B, bins_ms, *pmc_traffic(args.config)) or {}, timed_launches=bins_samples,

@@ -227,18 +227,8 @@ struct gcs_ctx {
   double* h_psum = nullptr;      // pinned, coherent, mapped: the sum + sequence + checksum (k_payload_out)
   double* dh_psum = nullptr;
   hipStream_t comm_stream = nullptr;  // the all-reduce's own stream (never queued behind the scan's kernels)
-  uint64_t pay_seq = 0;          // host copy of d_pay_seq (k_payload_out increments it once per chain)
+  uint64_t pay_seq = 0;          // host copy of d_pay_seq (k_payload_out increments it once per call)
   uint64_t* d_pay_seq = nullptr;
-  // the armed all-reduce chain [k_pay_gate, ncclAllReduce, k_payload_out] queued on comm_stream ahead of
-  // the next combine (GCSLAM_COMBINE_ARMED=0: queued and opened inside each call)
-  uint64_t* h_cgate = nullptr;   // pinned, coherent, mapped: the gate word the chain's k_pay_gate polls
-  uint64_t* d_cgate = nullptr;
-  bool armed = false;
-  void* armed_comm = nullptr;
-  int armed_len = 0;
-  bool comm_leaked = false;      // a cancelled chain did not drain at destroy: its buffers are kept
-  int64_t pay_invalid = 0;       // chains discarded on every rank (a gate some rank did not open)
-  uint64_t gate_ticks = 200000000ull;  // k_pay_gate's timeout: 2 s of the 100 MHz clock (GCS_DEBUG_COMBINE_GATE_US)
   int64_t pay_rereads = 0, pay_syncs = 0;
   // host state
   Belief belief{};
@@ -1244,18 +1234,6 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   return GCS_OK;
 }
 
-void combine_disarm(gcs_ctx* c);
-// contexts whose armed all-reduce chain is queued (gcs_rccl_comm_destroy cancels those on its
-// communicator before destroying it)
-static std::mutex g_armed_mu;
-static std::vector<gcs_ctx*> g_armed;
-static void armed_set(gcs_ctx* c, bool on) {
-  std::lock_guard<std::mutex> lk(g_armed_mu);
-  auto it = std::find(g_armed.begin(), g_armed.end(), c);
-  if (on && it == g_armed.end()) g_armed.push_back(c);
-  if (!on && it != g_armed.end()) g_armed.erase(it);
-}
-
 int gcs_ctx_destroy(gcs_ctx* c) {
   if (!c) return GCS_OK;
   if (c->push_thread.joinable()) {
@@ -1281,18 +1259,14 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (c->h_gate) (void)hipHostFree(c->h_gate);
   if (c->h_preint_in) (void)hipHostFree(c->h_preint_in);
   if (c->h_preint_out) (void)hipHostFree(c->h_preint_out);
-  combine_disarm(c);
-  if (c->comm_stream && !c->comm_leaked) {
+  if (c->comm_stream) {
     (void)hipStreamSynchronize(c->comm_stream);
     (void)hipStreamDestroy(c->comm_stream);
   }
-  if (!c->comm_leaked) {  // (a chain that never drained may still read or write these)
-    if (c->d_pay_seq) (void)hipFree(c->d_pay_seq);
-    if (c->h_payload) (void)hipHostFree(c->h_payload);
-    if (c->h_psum) (void)hipHostFree(c->h_psum);
-    if (c->h_cgate) (void)hipHostFree(c->h_cgate);
-    if (c->d_payload) (void)hipFree(c->d_payload);
-  }
+  if (c->d_pay_seq) (void)hipFree(c->d_pay_seq);
+  if (c->h_payload) (void)hipHostFree(c->h_payload);
+  if (c->h_psum) (void)hipHostFree(c->h_psum);
+  if (c->d_payload) (void)hipFree(c->d_payload);
   for (int st = 0; st < kStages; ++st)
     for (hipEvent_t e : c->ev[st]) (void)hipEventDestroy(e);
   if (c->ev_push) (void)hipEventDestroy(c->ev_push);
@@ -1356,10 +1330,6 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
       c->gate_on = value != 0;
       c->gate_withhold = value < 0;
       return GCS_OK;
-    case GCS_DEBUG_COMBINE_GATE_US:
-      if (value < 1 || value > 60000000) return fail(c, GCS_ERR_ARG, "combine gate timeout: 1 us .. 60 s");
-      c->gate_ticks = (uint64_t)value * 100u;
-      return GCS_OK;
     case GCS_DEBUG_MIRROR_TORN:
       if (value < 0 || value > 10000) return fail(c, GCS_ERR_ARG, "mirror torn delay: 0..10000 us");
       c->mirror_torn = (int)value;
@@ -1377,7 +1347,6 @@ int gcs_ctx_mirror_stats(gcs_ctx* c, int64_t* out) {
   out[3] = (int64_t)c->pay_seq;
   out[4] = c->pay_rereads;
   out[5] = c->pay_syncs;
-  out[6] = c->pay_invalid;
   return GCS_OK;
 }
 
@@ -2449,15 +2418,7 @@ int gcs_rccl_comm_init(int32_t device, int32_t n_ranks, int32_t rank, const uint
 
 int gcs_rccl_comm_destroy(void* comm) {
   if (!comm) return GCS_OK;
-  {
-    std::vector<gcs_ctx*> on;
-    {
-      std::lock_guard<std::mutex> lk(g_armed_mu);
-      for (gcs_ctx* c : g_armed)
-        if (c->armed_comm == comm) on.push_back(c);
-    }
-    for (gcs_ctx* c : on) combine_disarm(c);  // (their chains use this communicator)
-  }
+
   return ncclCommDestroy((ncclComm_t)comm) == ncclSuccess ? GCS_OK : GCS_ERR_HIP;
 }
 
@@ -2479,66 +2440,16 @@ int gcs_rccl_comm_count(void* comm, int32_t* count, int32_t* user_rank) {
   return GCS_OK;
 }
 
-// The armed all-reduce chain (k_pay_gate, ncclAllReduce of payload + validity word from the pinned host
-// buffer, k_payload_out) queued on the combine stream; its gate opens at the next combine_fire.
-int combine_arm(gcs_ctx* c, void* comm, int len) {
-  hipStream_t s = c->comm_stream;
-  HIPCHK(c, launch_pay_gate(c->d_cgate, c->d_pay_seq, c->dh_payload, len, c->gate_ticks, s));
-  ncclResult_t r = ncclAllReduce(c->dh_payload, c->d_payload, len + 1, ncclDouble, ncclSum, (ncclComm_t)comm, s);
-  if (r != ncclSuccess) return fail(c, GCS_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
-  HIPCHK(c, launch_payload_out(c->d_payload, c->dh_psum, len + 1, c->d_pay_seq, s));
-  c->armed = true;
-  c->armed_comm = comm;
-  c->armed_len = len;
-  armed_set(c, true);
-  return GCS_OK;
-}
-// open the armed chain's gate (after the payload is in h_payload; cancel: the chain runs and marks its
-// sum invalid) and wait for its stamped sum (wait_stamped: sequence + checksum)
-int combine_fire(gcs_ctx* c, bool cancel) {
-  const uint64_t want = c->pay_seq + 1u;
-  c->armed = false;
-  armed_set(c, false);
-  std::atomic_thread_fence(std::memory_order_release);
-  __atomic_store_n(c->h_cgate, cancel ? (want | (1ull << 63)) : want, __ATOMIC_RELEASE);
-  if (int rc = wait_stamped(c, c->h_psum, c->armed_len + 1, want, c->comm_stream, &c->pay_rereads, &c->pay_syncs,
-                            "hypothesis all-reduce"))
-    return rc;
-  c->pay_seq = want;
-  return GCS_OK;
-}
-// at destroy: cancel an armed chain and give it up to 2 s to drain (its collective needs the other
-// ranks' matching chains); one that does not drain keeps its buffers and stream (never freed under it)
-void combine_disarm(gcs_ctx* c) {
-  if (!c->armed) return;
-  c->armed = false;
-  armed_set(c, false);
-  const uint64_t want = c->pay_seq + 1u;
-  __atomic_store_n(c->h_cgate, want | (1ull << 63), __ATOMIC_RELEASE);
-  const auto t0 = clk::now();
-  while (hipStreamQuery(c->comm_stream) == hipErrorNotReady) {
-    if (clk::now() - t0 > std::chrono::seconds(2)) {
-      c->comm_leaked = true;
-      return;
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
-  }
-  c->pay_seq = want;
-}
-
 int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, int32_t scan_count,
                           gcs_belief* comb, double* cert) {
   if (!c) return GCS_ERR_ARG;
   constexpr int kLen = GCS_PAYLOAD_LEN + GCS_MAP_REC_LEN;
   if (!c->h_payload) {
     const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-    HIPCHK(c, hipHostMalloc(&c->h_payload, (kLen + 1) * sizeof(double), fl));  // + the chain's validity word
+    HIPCHK(c, hipHostMalloc(&c->h_payload, kLen * sizeof(double), fl));
     HIPCHK(c, hipHostGetDevicePointer((void**)&c->dh_payload, c->h_payload, 0));
-    HIPCHK(c, hipHostMalloc(&c->h_psum, (kLen + 3) * sizeof(double), fl));
-    memset(c->h_psum, 0, (kLen + 3) * sizeof(double));
-    HIPCHK(c, hipHostMalloc(&c->h_cgate, 8 * sizeof(uint64_t), fl));
-    memset(c->h_cgate, 0, 8 * sizeof(uint64_t));
-    HIPCHK(c, hipHostGetDevicePointer((void**)&c->d_cgate, c->h_cgate, 0));
+    HIPCHK(c, hipHostMalloc(&c->h_psum, (kLen + 2) * sizeof(double), fl));
+    memset(c->h_psum, 0, (kLen + 2) * sizeof(double));
     HIPCHK(c, hipHostGetDevicePointer((void**)&c->dh_psum, c->h_psum, 0));
     HIPCHK(c, hipMalloc(&c->d_payload, kLen * sizeof(double)));
     HIPCHK(c, hipMalloc(&c->d_pay_seq, sizeof(uint64_t)));
@@ -2554,33 +2465,39 @@ int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, in
       c->h_payload[GCS_PAYLOAD_LEN + k] = c->map_mode == GCS_MAP_LEAD ? c->map_rec[k] : 0.0;
   const double* sum = c->h_payload;
   if (comm) {
-    // The reduction rides its own stream (nothing the scan queued on the context stream -- k_tile_order
-    // behind the PT fold -- or the push stream is ahead of it) as the armed chain: queued at the end of
-    // the previous call, it waits on the device for this call's go, so only its execution is left on
-    // the step (combine_arm / combine_fire).  The payload needs no device ordering: it is host data of
-    // the finished scan.
-    if (!c->comm_stream) HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-    static const bool pre_arm = [] {
-      const char* e = getenv("GCSLAM_COMBINE_ARMED");
-      return !(e && atoi(e) == 0);
-    }();
-    int world = 1;
-    if (ncclCommCount((ncclComm_t)comm, &world) != ncclSuccess) return fail(c, GCS_ERR_HIP, "ncclCommCount failed");
-    if (c->armed && (c->armed_comm != comm || c->armed_len != len))
-      if (int rc = combine_fire(c, /*cancel=*/true)) return rc;  // armed for another communicator / length
-    for (int attempt = 0;; ++attempt) {
-      if (!c->armed)
-        if (int rc = combine_arm(c, comm, len)) return rc;
-      if (int rc = combine_fire(c, false)) return rc;
-      if (c->h_psum[len] == (double)world) break;  // every rank opened its gate: the sum is this call's
-      // a chain some rank did not open (its gate timed out or was cancelled): every rank saw the same
-      // count and discards it alike, then all of them reduce once more with their gates opened at once
-      ++c->pay_invalid;
-      if (attempt) return fail(c, GCS_ERR_HIP, "hypothesis all-reduce: a rank's gate did not open twice in a row");
+    // The reduction rides its own stream: nothing the scan queued on the context stream (k_tile_order
+    // behind the PT fold) or the push stream (the pushforward) is ahead of it.  The payload needs no
+    // device ordering: it is host data of the finished scan.  ncclAllReduce reads it from the pinned
+    // host buffer, k_payload_out copies the sum back with the call's sequence number and a checksum,
+    // and the host polls that (wait_stamped): no copy call and no stream synchronize.  Measured at world
+    // size 1 (profiles/r05/combine/, rccl/): 16.5 us per call alone and 19 us inside the C2 pipeline,
+    // against 3.3 us for the host-only combine; the stage-out kernel alone takes 16.7 alone (a kernel
+    // round trip from an idle stream).  A separate stage-in kernel, a captured graph, the context
+    // stream, the sum written straight to pinned memory with hipStreamQuery polled, and a device-side
+    // gate queued ahead of the call (which also held every device-wide synchronize until its timeout)
+    // gave nothing.
+    if (!c->comm_stream) {
+      // the device's highest priority: the combine's kernels are dispatched ahead of the pushforward
+      // that was just queued on the push stream (same box, alternated, profiles/r05/rccl/: combine 32 ->
+      // 19 us in the C2 pipeline, 0.1275-0.1295 -> 0.1154-0.1161 ms per step; GCSLAM_COMBINE_PRIO=0)
+      static const bool prio = [] {
+        const char* e = getenv("GCSLAM_COMBINE_PRIO");
+        return !(e && atoi(e) == 0);
+      }();
+      int lo = 0, hi = 0;
+      if (prio && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess)
+        HIPCHK(c, hipStreamCreateWithPriority(&c->comm_stream, hipStreamNonBlocking, hi));
+      else
+        HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     }
+    hipStream_t s = c->comm_stream;
+    ncclResult_t r = ncclAllReduce(c->dh_payload, c->d_payload, len, ncclDouble, ncclSum, (ncclComm_t)comm, s);
+    if (r != ncclSuccess) return fail(c, GCS_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+    HIPCHK(c, launch_payload_out(c->d_payload, c->dh_psum, len, c->d_pay_seq, s));
+    const uint64_t seq = ++c->pay_seq;
+    if (int rc = wait_stamped(c, c->h_psum, len, seq, s, &c->pay_rereads, &c->pay_syncs, "hypothesis all-reduce"))
+      return rc;
     sum = c->h_psum;
-    if (pre_arm)
-      if (int rc = combine_arm(c, comm, len)) return rc;  // the next call's chain, waiting at its gate
   }
   if (shared_map) {  // a single rank carries its own record (a follower then replays its own update)
     memcpy(c->lead_rec, comm ? sum + GCS_PAYLOAD_LEN : c->map_rec, sizeof(c->lead_rec));

@@ -186,11 +186,8 @@ struct PreintArgs {
 };
 hipError_t launch_preint(const PreintArgs& a, hipStream_t s);
 hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err, hipStream_t s);
-// the hypothesis all-reduce's armed chain (gcs_combine_allreduce): the device-side gate (validity word
-// payload[n]), and the stamp-out of the device sum to a host buffer of n words + [n] sequence number
-// (*dseq + 1, stored back to *dseq) + [n + 1] checksum (mirror_word_hash, gcs_layout.h)
-hipError_t launch_pay_gate(const uint64_t* gate, const uint64_t* dseq, double* payload, int n, uint64_t timeout,
-                           hipStream_t s);
+// the hypothesis all-reduce's stage-out (gcs_combine_allreduce): the device sum to a host buffer of n
+// words + [n] sequence number (*dseq + 1, stored back to *dseq) + [n + 1] checksum (mirror_word_hash)
 hipError_t launch_payload_out(const double* src, double* host, int n, uint64_t* dseq, hipStream_t s);
 // legacy: the round-3 k_points (scale mode) instead of k_points_lean
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,

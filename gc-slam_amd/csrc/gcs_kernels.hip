@@ -2637,36 +2637,10 @@ __global__ __launch_bounds__(64) void k_gate(const uint64_t* gate, uint64_t seq,
 }
 
 // ---------------------------------------------------------------- hypothesis payload staging
-// The per-scan all-reduce (gcs_combine_allreduce) as an armed chain on the context's combine stream,
-// queued before the host has the payload: k_pay_gate waits on the device for the host's go (so the
-// chain's launch and dispatch latency -- ~13 us for a kernel round trip from an idle stream,
-// profiles/r05/combine/ -- leave the step), ncclAllReduce reads the payload from the pinned host buffer,
-// k_payload_out copies the sum back to a second host buffer followed by the chain's sequence number
-// and a checksum (the scan mirror's protocol, gcs_layout.h), and the host polls that.
-//
-// k_pay_gate: one lane polls the host gate word (coherent host memory, relaxed system-scope loads with
-// a short sleep) for the chain's sequence number (the device counter + 1: what k_payload_out will
-// stamp), then writes the validity word payload[n]: 1 when the host opened the gate, 0 when it
-// cancelled (the sequence number with bit 63) or the gate stayed shut for timeout ticks.  The
-// all-reduce sums that word, so every rank sees the same count: a chain that some rank did not open is
-// discarded by all of them alike (gcs_capi.cpp combine_fire).
-__global__ __launch_bounds__(64) void k_pay_gate(const uint64_t* gate, const uint64_t* dseq, double* payload, int n,
-                                                 uint64_t timeout) {
-  if (threadIdx.x != 0) return;
-  const uint64_t want = *dseq + 1u;
-  const uint64_t t0 = wall_clock64();
-  double ok = 0.0;
-  for (;;) {
-    const uint64_t g = __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    if (g == want) {
-      ok = 1.0;
-      break;
-    }
-    if (g == (want | (1ull << 63)) || wall_clock64() - t0 > timeout) break;
-    __builtin_amdgcn_s_sleep(2);
-  }
-  payload[n] = ok;
-}
+// The per-scan all-reduce (gcs_combine_allreduce) on the context's combine stream: ncclAllReduce reads
+// the host-packed payload from pinned memory, k_payload_out copies the sum back to a second pinned host
+// buffer followed by the call's sequence number and a checksum (the scan mirror's protocol,
+// gcs_layout.h), and the host polls that instead of a copy call and a stream synchronize.
 __global__ __launch_bounds__(kBlock) void k_payload_out(const double* __restrict__ src, double* host, int n,
                                                         uint64_t* dseq) {
   __shared__ unsigned long long lh[kWaves];
@@ -2690,11 +2664,6 @@ __global__ __launch_bounds__(kBlock) void k_payload_out(const double* __restrict
     hw[n + 1] = sum;
     hw[n] = seq;
   }
-}
-hipError_t launch_pay_gate(const uint64_t* gate, const uint64_t* dseq, double* payload, int n, uint64_t timeout,
-                           hipStream_t s) {
-  hipLaunchKernelGGL(k_pay_gate, dim3(1), dim3(64), 0, s, gate, dseq, payload, n, timeout);
-  return hipGetLastError();
 }
 hipError_t launch_payload_out(const double* src, double* host, int n, uint64_t* dseq, hipStream_t s) {
   hipLaunchKernelGGL(k_payload_out, dim3(1), dim3(kBlock), 0, s, src, host, n, dseq);

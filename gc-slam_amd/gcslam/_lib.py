@@ -103,7 +103,6 @@ DEBUG_POINT_KERNEL = 6
 DEBUG_DEVICE_PREINT = 7
 DEBUG_PT_CLEAR = 8
 DEBUG_MIRROR_TORN = 9
-DEBUG_COMBINE_GATE_US = 10
 MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 

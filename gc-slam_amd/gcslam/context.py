@@ -184,8 +184,8 @@ class HypothesisContext:
 
     def mirror_stats(self):
         """gcs_ctx_mirror_stats: (scan mirrors accepted, of them re-read at least once, via stream sync,
-        all-reduce chains run, re-read, via stream sync, chains discarded for an unopened gate)."""
-        out = np.zeros(7, np.int64)
+        all-reduces run, re-read, via stream sync)."""
+        out = np.zeros(6, np.int64)
         self._chk(self.lib.gcs_ctx_mirror_stats(self.h, out.ctypes.data_as(L.c_int64_p)), "mirror_stats")
         return tuple(int(x) for x in out)
 

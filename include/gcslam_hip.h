@@ -236,19 +236,14 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * not arrived; gcs_scan must re-read until the checksum matches (gcs_ctx_mirror_stats counts it) and
  * return the same results.  Test knob of the mirror guard. */
 #define GCS_DEBUG_MIRROR_TORN 9
-/* GCS_DEBUG_COMBINE_GATE_US (default 2,000,000): how long the armed all-reduce chain's device gate
- * waits for the next gcs_combine_allreduce before it runs on its own and marks its sum invalid (the
- * call then reduces once more); a test shortens it to exercise that path. */
-#define GCS_DEBUG_COMBINE_GATE_US 10
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 /* The scan mirror (the PT fold's copy of the scan's scalars and device error words to pinned host
  * memory, with the scan's sequence number and a checksum; the host accepts it only when both match):
  * out[0] mirrors accepted, out[1] of them after at least one re-read (a data word arrived after the
  * sequence word), out[2] accepted only after the 20 ms poll gave up and the stream synchronized;
  * out[3..5] the same for the hypothesis all-reduce's stamped sum (gcs_combine_allreduce with a
- * communicator): all-reduce chains run, re-read, via stream sync; out[6] chains discarded because a
- * rank's device gate had timed out or been cancelled (the call then reduced once more). */
-int gcs_ctx_mirror_stats(gcs_ctx* ctx, int64_t* out /*7*/);
+ * communicator): all-reduces run, re-read, via stream sync. */
+int gcs_ctx_mirror_stats(gcs_ctx* ctx, int64_t* out /*6*/);
 /* Determinism diagnostics (tools/determinism_check.py, tests): 64-bit FNV-1a checksums of the
  * context's device state after its streams drain: [0] ScanBinStats, [1] MapBinStats, [2] derived map
  * stats, [3] touched bytes, [4] both active-flag buffers, [5] the bin kernel's partial rows, [6] the
