@@ -1394,7 +1394,13 @@ int gcs_ctx_enable_timing(gcs_ctx* c, int32_t stage_mask) {
       c->ev[st].resize(2 * gcs_ctx::kEvRing, nullptr);
       // timing only: no system-scope fence when a stamp completes (the fence's cache write-back and
       // invalidate measured ~8 us per stamped scan at C2, profiles/r05/stamp/)
-      for (hipEvent_t& e : c->ev[st]) HIPCHK(c, hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+      static const unsigned fl = [] {  // A/B knob GCSLAM_STAMP_EVENT=default|device (fence-free by default)
+        const char* e = getenv("GCSLAM_STAMP_EVENT");
+        if (e && strcmp(e, "default") == 0) return (unsigned)hipEventDefault;
+        if (e && strcmp(e, "device") == 0) return (unsigned)hipEventReleaseToDevice;
+        return (unsigned)hipEventDisableSystemFence;
+      }();
+      for (hipEvent_t& e : c->ev[st]) HIPCHK(c, hipEventCreateWithFlags(&e, fl));
     }
   c->timing_mask = (uint32_t)stage_mask;
   return GCS_OK;
