@@ -64,7 +64,25 @@ def bins_kernel_bytes(N, B):
     return N * (3 * 4 + 8 + 8) + B * 3 * 8, B * 26 * 8
 
 
-def roofline_chain(N, B, stage_avg, label):
+def pmc_chain_traffic(config):
+    """HBM bytes per scan of the chain's kernels (k_budget, k_points*, k_bins_scale*, the bins fold's
+    k_fold<16>/k_final<16>) from the committed PMC passes (profiles/pmc_bins_<cfg>.json)."""
+    path = os.path.join(ROOT, "profiles", f"pmc_bins_{config}.json")
+    if not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    per = {}
+    for k, v in d.get("kernels", {}).items():
+        for tag, pat in (("budget", "k_budget"), ("points", "k_points"), ("bins", "k_bins_scale"),
+                         ("bins_fold", "k_fold<16"), ("bins_fold", "k_final<16")):
+            if pat in k:
+                per[tag] = per.get(tag, 0.0) + v["hbm_bytes"]
+    if set(per) != {"budget", "points", "bins", "bins_fold"}:
+        return None, None
+    return per, f"profiles/pmc_bins_{config}.json ({d.get('round', '?')})"
+
+
+def roofline_chain(N, B, stage_avg, label, config=None):
     """The north star's "BinSoftAssign + ScanBinMomentMatch" as the kernel chain that implements it:
     k_budget (row 1) + k_points (rows 1, 3, 5: gather, deskew, direction, nearest bin, K-candidate
     softmax normaliser) + k_bins_scale (rows 4-6 + MF terms) + the bin kernel's partial-row fold,
@@ -76,10 +94,15 @@ def roofline_chain(N, B, stage_avg, label):
     rd, wr = bins_kernel_bytes(N, B)
     s = ms * 1e-3
     ach = (rd + wr) / s / 1e9
-    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "read_frac": rd / s / 1e9 / HBM_PEAK_GBS, "write_frac": wr / s / 1e9 / HBM_PEAK_GBS,
-            "chain_us": ms * 1e3, "kernels_us": {k: stage_avg[k] * 1e3 for k in names},
-            "algorithmic_bytes": rd + wr, "config": label}
+    out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+           "read_frac": rd / s / 1e9 / HBM_PEAK_GBS, "write_frac": wr / s / 1e9 / HBM_PEAK_GBS,
+           "chain_us": ms * 1e3, "kernels_us": {k: stage_avg[k] * 1e3 for k in names},
+           "algorithmic_bytes": rd + wr, "config": label}
+    per, src = pmc_chain_traffic(config) if config else (None, None)
+    if per:  # the counter-based traffic of the same kernels beside the algorithmic bytes
+        t = sum(per.values())
+        out.update(traffic=t, traffic_per_kernel=per, traffic_source=src, traffic_frac=t / s / 1e9 / HBM_PEAK_GBS)
+    return out
 
 
 def roofline(N, B, kernel_ms, traffic=None, traffic_source=None):
@@ -276,7 +299,7 @@ def c3_roofline(device, steps=16, warmup=3):
     label = "c3: 262144-pt scans vs 1048576-bin map, K=16"
     if r:
         r.update(config=label, timed_launches=int(cnt[2]), scans_per_s_with_chain_stamps=steps / el)
-    return r, roofline_chain(cfg["N"], cfg["B"], avg, label)
+    return r, roofline_chain(cfg["N"], cfg["B"], avg, label, config="c3")
 
 
 def live_path_bench(device, steps=30, warmup=10):
@@ -879,7 +902,8 @@ def main():
                         "min": float(per_step.min() * 1e3), "max": float(per_step.max() * 1e3)},
             "roofline": dict(roofline(N, B, bins_ms, *pmc_traffic(args.config)) or {}, timed_launches=bins_samples,
                              timed_launches_in_region=bins_in_region, stamp_stride=TIMING_STRIDE),
-            "roofline_chain": roofline_chain(N, B, stage_avg, f"{args.config} (diagnostic pass, every stage stamped)"),
+            "roofline_chain": roofline_chain(N, B, stage_avg, f"{args.config} (diagnostic pass, every stage stamped)",
+                                             config=args.config),
             "stage_ms": stage_avg,
             "host_ms": host_avg,
             "pcie_inclusive": {"h2d_bytes_per_scan": h2d_bytes, "scans_per_s": 1e3 / (ms_step / world + h2d) * world,

@@ -326,6 +326,15 @@ int join_push(gcs_ctx* c) {
 
 constexpr int kRedBlocks = 1024;
 int red_blocks(long n) { return (int)std::max(1L, std::min((long)kRedBlocks, (n + 255) / 256)); }
+// k_pt's grid: GCSLAM_PT_BLOCKS caps it (default kRedBlocks: four bins per thread at C3)
+constexpr int kPtBlocksMax = 8192;
+int pt_blocks(long n) {
+  static const int cap = [] {
+    const char* e = getenv("GCSLAM_PT_BLOCKS");
+    return e ? std::max(1, std::min(kPtBlocksMax, atoi(e))) : kRedBlocks;
+  }();
+  return (int)std::max(1L, std::min((long)cap, (n + 255) / 256));
+}
 
 // read back a stage's recorded event pairs (oldest first; each waits for its end event)
 void harvest_stage(gcs_ctx* c, int st) {
@@ -746,7 +755,7 @@ int stage_pt(gcs_ctx* c, bool to_host = false, bool clear_next = false) {
     clr.c8 = c->d_flags_buf[c->flags_cur ^ 1];
     clr.n8 = c->B + bins_scale_blocks(c->B, c->tile_bins);
   }
-  HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, red_blocks(c->B), c->d_scalars,
+  HIPCHK(c, launch_pt(c->d_scan, c->d_map, c->d_derived, c->B, c->d_partials, pt_blocks(c->B), c->d_scalars,
                       mir, c->d_flags, c->d_touched, c->stream, ev.e0, ev.e1, clr));
   if (clr.c32) {
     c->counts_clean = true;
@@ -1136,7 +1145,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMemset(c->d_map, 0, B * MF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scan, 0, B * SF_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_touched, B))) return GCS_ERR_HIP;
-  c->partials_len = std::max<size_t>({partials_need(kRedBlocks, 24), partials_need(bins_scale_blocks(c->B, c->tile_bins), bins_partial_nv()),
+  c->partials_len = std::max<size_t>({partials_need(kRedBlocks, 24), partials_need(pt_blocks(c->B), 13), partials_need(bins_scale_blocks(c->B, c->tile_bins), bins_partial_nv()),
                                       partials_need(push_blocks(c->B), 10)});
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_part_pts, partials_need(std::max(kRedBlocks, points_max_blocks()), 5) * sizeof(double)))) return GCS_ERR_HIP;
