@@ -2013,14 +2013,30 @@ __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, 
 #pragma unroll
   for (int k = 0; k < kPtNV; ++k) v[k] = 0.0;
   size_t Bs = (size_t)B;
-  for (int b = blockIdx.x * kBlock + threadIdx.x; b < B; b += gridDim.x * kBlock) {
+  // the grid-stride bins of this thread in chunks of kPtU: every flag byte of a chunk is loaded before
+  // the first bin's rows (one dependent round trip per chunk, not one per bin; C3: four bins per
+  // thread).  The bins and their sums keep the one-bin loop's order.
+  constexpr int kPtU = 4;
+  const int gstride = gridDim.x * kBlock;
+  for (int b0 = blockIdx.x * kBlock + threadIdx.x; b0 < B; b0 += kPtU * gstride) {
+    bool scu[kPtU], tcu[kPtU];
+#pragma unroll
+    for (int u = 0; u < kPtU; ++u) {
+      const int bu = b0 + u * gstride;
+      scu[u] = bu < B && (!act || act[bu]);
+      tcu[u] = bu < B && act && touched[bu];  // (dense mode: act null, every bin read)
+    }
+#pragma unroll
+    for (int u = 0; u < kPtU; ++u) {
+    const int b = b0 + u * gstride;
+    if (b >= B) break;
     double Ns = 0.0, Nm = 0.0;
     double pb[3] = {0.0, 0.0, 0.0}, c[3] = {0.0, 0.0, 0.0};
     double Sp[9] = {kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd};
     double Sc[9] = {kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd, 0.0, 0.0, 0.0, kEpsPsd};
     // scan rows of a bin without scan mass hold the zero-bin values the defaults above restate,
     // map / derived rows of a bin the map never reached hold them too: only the rest is read
-    const bool sc = !act || act[b];
+    const bool sc = scu[u];
     if (sc) {
       Ns = scan[SF_N * Bs + b];
 #pragma unroll
@@ -2028,7 +2044,7 @@ __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, 
 #pragma unroll
       for (int k = 0; k < 9; ++k) Sp[k] = scan[(SF_SIG + k) * Bs + b];
     }
-    if (sc || touched[b]) {
+    if (sc || tcu[u]) {
       Nm = map[MF_NP * Bs + b];
 #pragma unroll
       for (int k = 0; k < 3; ++k) c[k] = derived[(MD_C + k) * Bs + b];
@@ -2056,6 +2072,7 @@ __global__ __launch_bounds__(kBlock) void k_pt(const double* __restrict__ scan, 
 #pragma unroll
     for (int i = 0; i < 3; ++i) v[9 + i] += Si[3 * i] * tb[0] + Si[3 * i + 1] * tb[1] + Si[3 * i + 2] * tb[2];
     v[12] += wb;
+    }
   }
   block_sum<kPtNV>(v, lds);
   store_partials<kPtNV>(v, partials, blockIdx.x);  // folded by k_final<FIN_PT>
