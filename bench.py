@@ -310,7 +310,9 @@ def live_path_bench(device, steps=30, warmup=10):
     active / stencil tiles, M_TILE_VIEW 1,024, n_surfel 1,024 + n_feat 512, k_assoc 8, 50 Sinkhorn
     iterations), one hypothesis over consecutive synthetic scans along the trajectory (the map fills as
     it would).  The call takes the reference's numpy inputs (its H2D included).  ms per call over the
-    timed scans, then a diagnostic pass with config.enable_timing for the stage split."""
+    timed scans (the one-call path, gcs_live_scan), the same count of following scans through the
+    per-operator path (GCSLAM_LIVE_CHAIN=0) beside it, then a diagnostic pass with config.enable_timing
+    for the stage split."""
     import torch
     from gcslam import synthetic, primitive_map as gpm
     from gcslam.pipeline import (BeliefGaussianInfo, PipelineConfig, datasheet_process_noise_state,
@@ -319,12 +321,12 @@ def live_path_bench(device, steps=30, warmup=10):
     cfg = PipelineConfig(K_HYP=1, N_POINTS_CAP=N, B_BINS=48, soft_assign_mode="dense",
                          lidar_origin_base=tuple(synthetic.LIDAR_ORIGIN), max_raw_points=N, device=device)
     ctx = cfg.make_context()
-    # the reference's AtlasMap is a dict of tiles; this one preallocates: 256 tiles x 50,000 slots hold
+    # the reference's AtlasMap is a dict of tiles; this one preallocates: 512 tiles x 50,000 slots hold
     # the synthetic trajectory's coverage over the run (its z hovers at a tile boundary, so the one-slab
     # stencil alternates between two layers of tiles)
-    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, max_tiles=256, device=device)
+    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, max_tiles=512, device=device)
     Q = process_noise_state_to_Q(datasheet_process_noise_state())
-    n_total = warmup + steps + 10
+    n_total = warmup + 2 * steps + 10
     scans = [synthetic.make_scan(N, k) for k in range(n_total)]
     state = dict(belief=BeliefGaussianInfo.create_identity_prior(), seq=0)
 
@@ -349,15 +351,32 @@ def live_path_bench(device, steps=30, warmup=10):
         t0 = time.perf_counter()
         r = one(scans[warmup + i])
         per[i] = time.perf_counter() - t0
+    chain_on = r.stage_ms == {} and os.environ.get("GCSLAM_LIVE_CHAIN", "1") != "0"
+    prev = os.environ.get("GCSLAM_LIVE_CHAIN")
+    os.environ["GCSLAM_LIVE_CHAIN"] = "0"
+    per_op = np.zeros(steps)
+    try:
+        for i in range(steps):
+            t0 = time.perf_counter()
+            one(scans[warmup + steps + i])
+            per_op[i] = time.perf_counter() - t0
+    finally:
+        if prev is None:
+            os.environ.pop("GCSLAM_LIVE_CHAIN")
+        else:
+            os.environ["GCSLAM_LIVE_CHAIN"] = prev
     # diagnostic pass: every stage synced and timed (config.enable_timing, the reference's _record_timing)
     cfg.enable_timing = True
     split = []
-    for k in range(warmup + steps, n_total):
+    for k in range(warmup + 2 * steps, n_total):
         split.append(one(scans[k]).stage_ms)
     cfg.enable_timing = False
     mu = r.map_update_cert
     out = dict(ms_per_call=float(per.mean() * 1e3), ms_median=float(np.median(per) * 1e3),
                ms_p90=float(np.percentile(per, 90) * 1e3), calls=int(steps),
+               path="gcs_live_scan (one C call per scan)" if chain_on else "per-operator C calls",
+               per_operator_ms_per_call=float(per_op.mean() * 1e3),
+               per_operator_ms_median=float(np.median(per_op) * 1e3),
                stage_ms={k: float(np.mean([s[k] for s in split])) for k in split[0]},
                stage_note="diagnostic pass: a device sync before each stage clock (the reference's enable_timing)",
                sizes=dict(n_points_cap=N, m_tile=cfg.primitive_map_max_size, n_active_tiles=cfg.N_ACTIVE_TILES,

@@ -30,6 +30,7 @@
 
 #include "gcs_math.h"
 #include "gcslam_hip.h"
+#include "gcs_live.h"
 
 namespace gcs {
 namespace {
@@ -1354,6 +1355,7 @@ struct gcs_assoc_ctx {
   double* h_cert_dev = nullptr;
   double* h_vpe = nullptr;   // pinned, mapped: k_as_vpe's sums
   double* h_vpe_dev = nullptr;
+  int probe_iters = 0;       // GCS_SH_PROBE builds: the last launch's Sinkhorn iterations
 };
 
 namespace {
@@ -1469,14 +1471,20 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
 
 int gcs_assoc_ctx_set_stream(gcs_assoc_ctx* c, void* stream) {
   if (!c) return GCS_ERR_ARG;
+  hipStream_t ns = stream ? (hipStream_t)stream : c->own;
+  if (ns == c->stream) return GCS_OK;
   ASCHK(c, hipSetDevice(c->device));
   ASCHK(c, hipStreamSynchronize(c->stream));  // work queued on the old stream completes first
-  c->stream = stream ? (hipStream_t)stream : c->own;
+  c->stream = ns;
   return GCS_OK;
 }
 
-int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_meas* m,
-                                const gcs_assoc_view* v, gcs_assoc_outputs* o) {
+}  // extern "C"
+
+namespace gcs {
+namespace live {
+int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_meas* m, const gcs_assoc_view* v,
+                 gcs_assoc_outputs* o) {
   if (!c || !cfg || !m || !v || !o) return GCS_ERR_ARG;
   if (!o->responsibilities || !o->row_masses || !o->cost_matrix)
     return as_fail(c, GCS_ERR_ARG, "responsibilities, row_masses and cost_matrix are required outputs");
@@ -1597,7 +1605,19 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   }
   ASCHK(c, hipGetLastError());
   rearm.armed = false;  // the Sinkhorn is queued: it zeroes mv_next
-  ASCHK(c, hipStreamSynchronize(s));
+  c->probe_iters = p.iters;
+  return GCS_OK;
+}
+
+int assoc_bind_stream(gcs_assoc_ctx* c, void* s) {
+  if ((hipStream_t)s == c->stream) return GCS_OK;
+  ASCHK(c, hipSetDevice(c->device));
+  ASCHK(c, hipStreamSynchronize(c->stream));
+  c->stream = (hipStream_t)s;
+  return GCS_OK;
+}
+
+void assoc_collect(gcs_assoc_ctx* c, gcs_assoc_outputs* o) {
 #if GCS_SH_PROBE
   {
     unsigned long long h[16];
@@ -1605,7 +1625,7 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
     fprintf(stderr, "sh_probe us: marginal %.2f kmat %.2f loop %.2f finish %.2f (pi %.2f bsum %.2f cert %.2f) | wg1 %.2f\n",
             (h[1] - h[0]) / 100.0, (h[2] - h[1]) / 100.0, (h[3] - h[2]) / 100.0, (h[4] - h[3]) / 100.0,
             (h[6] - h[3]) / 100.0, (h[7] - h[6]) / 100.0, (h[4] - h[7]) / 100.0, (h[5] - h[0]) / 100.0);
-    const double it = p.iters > 0 ? 100.0 * p.iters : 1.0;  // per iteration, us
+    const double it = c->probe_iters > 0 ? 100.0 * c->probe_iters : 1.0;  // per iteration, us
     fprintf(stderr, "sh_probe per iteration us: u %.3f KTu+scatter %.3f barrier1 %.3f v %.3f barrier2+read %.3f\n",
             h[8] / it, h[9] / it, h[10] / it, h[11] / it, h[12] / it);
   }
@@ -1613,6 +1633,16 @@ int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, c
   for (int q = 0; q < GCS_ASSOC_CERT_LEN; ++q) o->cert[q] = c->h_cert[q];
   o->exact = c->h_cert[CE_EXACT] != 0.0;
   o->n_map_valid = (int32_t)c->h_cert[CE_MVALID];
+}
+}  // namespace live
+}  // namespace gcs
+
+extern "C" {
+int gcs_associate_primitives_ot(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_meas* m,
+                                const gcs_assoc_view* v, gcs_assoc_outputs* o) {
+  if (int rc = gcs::live::assoc_launch(c, cfg, m, v, o)) return rc;
+  ASCHK(c, hipStreamSynchronize(c->stream));
+  gcs::live::assoc_collect(c, o);
   return GCS_OK;
 }
 

@@ -21,6 +21,7 @@
 #include "gcs_host.h"
 #include "gcs_kernels.h"
 #include "gcs_layout.h"
+#include "gcs_live.h"
 #include "gcs_math.h"
 
 using namespace gcs;
@@ -86,6 +87,7 @@ struct gcs_ctx {
   gcs_scan_state* scan_st = nullptr;
   gcs_scan_outputs* live_out = nullptr;
   bool live_pending = false;
+  gcs_pmap* live_map = nullptr;  // gcs_live_scan: the map whose step 12b gcs_live_collect has to read
   uint32_t *d_keys = nullptr, *d_slots = nullptr, *d_sorted = nullptr;
   int* d_nearest = nullptr;
   // per-bin bucketing
@@ -2295,6 +2297,211 @@ int gcs_scan_finish(gcs_ctx* c, const gcs_lidar_evidence* ev, gcs_scan_outputs* 
   st.Tsum += ev->trigger_sum;  // the map branch's and the visual certs in all_certs (pipeline.py:964-1002)
   st.cert[58] = ev->trigger_sum;
   return scan_tail(c, st, lt, out, /*push=*/false);
+}
+
+// ---------------------------------------------------------------- live primitive path: one call
+namespace {
+// tiling.py:167-209 (ma_hex_stencil_tile_ids): the packed ids of the hex disk (radius_xy, axial order
+// sorted by (q, r)) x the z slab (radius_z, outer loop) around the cell of center; -1 past cap
+int ma_hex_stencil(const double* ctr, double h_tile, int rxy, int rz, int64_t* out, int cap) {
+#pragma clang fp contract(off)
+  const double x = ctr[0], y = ctr[1], z = ctr[2];
+  const double h = std::max(h_tile, 1e-12);
+  const int64_t c1 = (int64_t)std::floor(x / h);
+  const int64_t c2 = (int64_t)std::floor((x * 0.5 + y * (std::sqrt(3.0) * 0.5)) / h);
+  const int64_t cz = (int64_t)std::floor(z / h);
+  constexpr int64_t bias = int64_t(1) << 20, mask = (int64_t(1) << 21) - 1;
+  auto pack = [&](int64_t a, int64_t b, int64_t c) {
+    return (((a + bias) & mask) << 42) | (((b + bias) & mask) << 21) | ((c + bias) & mask);
+  };
+  if (rxy < 0 || rz < 0) return -1;
+  int n = 0;
+  for (int dz = -rz; dz <= rz; ++dz)
+    for (int q = -rxy; q <= rxy; ++q)
+      for (int r = std::max(-rxy, -q - rxy); r <= std::min(rxy, -q + rxy); ++r) {
+        if (n >= cap) return -1;
+        out[n++] = pack(c1 + q, c2 + r, cz + dz);
+      }
+  return n;
+}
+
+int sub_fail(gcs_ctx* c, int rc, const char* what, const char* msg) {
+  return fail(c, rc, std::string(what) + ": " + (msg ? msg : ""));
+}
+}  // namespace
+
+int gcs_ma_hex_stencil(const double* center3, double h_tile, int32_t radius_xy, int32_t radius_z, int64_t* out,
+                       int32_t cap) {
+  if (!center3 || !out || cap < 0) return GCS_ERR_ARG;
+  const int n = ma_hex_stencil(center3, h_tile, radius_xy, radius_z, out, cap);
+  return n < 0 ? GCS_ERR_ARG : n;
+}
+
+int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs* bo, const gcs_live_args* a,
+                  gcs_live_outputs* lo, gcs_scan_outputs* out) {
+  if (!c || !bo || !a || !lo || !out) return fail(c, GCS_ERR_ARG, "null argument");
+  if (!a->surfels || !a->assoc || !a->map || !a->assoc_cfg || !a->update_cfg || !a->surfel_out || !a->view ||
+      !a->view_tile_ids_dev || !a->assoc_out || !a->vpe_out || !a->lidar_sources_dev ||
+      !a->assoc_out->candidate_pool_indices || !a->assoc_out->candidate_tile_ids || !a->assoc_out->candidate_slots)
+    return fail(c, GCS_ERR_ARG, "gcs_live_scan: missing context, output or association array");
+  if (a->n_tiles < 0 || a->n_free < 0 || (a->n_tiles > 0 && (!a->tile_ids || !a->tile_slots)) ||
+      (a->n_free > 0 && !a->free_slots))
+    return fail(c, GCS_ERR_ARG, "gcs_live_scan: bad tile directory");
+  if (c->live_map) return fail(c, GCS_ERR_STATE, "gcs_live_scan: the previous scan's step 12b was not collected");
+  memset(lo, 0, sizeof(*lo));
+  int rc;
+  if (in) {
+    if ((rc = gcs_scan_begin(c, in, bo))) return rc;
+  } else if (!c->live_pending) {
+    return fail(c, GCS_ERR_STATE, "gcs_live_scan without gcs_scan_begin");
+  }
+  // the scan's tiles around the predicted position (pipeline.py:783-797)
+  const int na = ma_hex_stencil(bo->pose_pred, a->h_tile, a->r_active_xy, a->r_active_z, lo->active_ids,
+                                GCS_LIVE_MAX_TILES);
+  const int ns = ma_hex_stencil(bo->pose_pred, a->h_tile, a->r_stencil_xy, a->r_stencil_z, lo->stencil_ids,
+                                GCS_LIVE_MAX_TILES);
+  if (na < 0 || ns < 0) return fail(c, GCS_ERR_ARG, "gcs_live_scan: a stencil exceeds GCS_LIVE_MAX_TILES tiles");
+  if (na != a->n_active_expected)
+    return fail(c, GCS_ERR_ARG, "active tile stencil size mismatch: expected N_ACTIVE_TILES=" +
+                                    std::to_string(a->n_active_expected) + ", got " + std::to_string(na));
+  if (ns != a->n_stencil_expected)
+    return fail(c, GCS_ERR_ARG, "stencil tile size mismatch: expected N_STENCIL_TILES=" +
+                                    std::to_string(a->n_stencil_expected) + ", got " + std::to_string(ns));
+  lo->n_active = na;
+  lo->n_stencil = ns;
+  // the AtlasMap directory: present tiles for the recency inflation and the view, new tiles for step 12b
+  std::vector<std::pair<int64_t, int32_t>> dir((size_t)a->n_tiles);
+  for (int i = 0; i < a->n_tiles; ++i) dir[i] = {a->tile_ids[i], a->tile_slots[i]};
+  std::sort(dir.begin(), dir.end());
+  auto find = [&](int64_t id) -> int32_t {
+    auto it = std::lower_bound(dir.begin(), dir.end(), std::make_pair(id, (int32_t)INT32_MIN));
+    return (it != dir.end() && it->first == id) ? it->second : -1;
+  };
+  int32_t rec[GCS_LIVE_MAX_TILES], vs[GCS_LIVE_MAX_TILES];
+  int nrec = 0;
+  for (int i = 0; i < na; ++i) {
+    const int32_t s = find(lo->active_ids[i]);
+    if (s >= 0) rec[nrec++] = s;
+  }
+  lo->n_present_active = nrec;
+  for (int i = 0; i < ns; ++i) vs[i] = find(lo->stencil_ids[i]);  // -1: viewed as empty
+  int32_t clear[GCS_LIVE_MAX_TILES];
+  int ncl = 0, nfree = 0;
+  for (int i = 0; i < na; ++i) {
+    int32_t s = find(lo->active_ids[i]);
+    if (s < 0) {  // AtlasMap.index(create=True): the first free slot (stencil ids are distinct)
+      if (nfree >= a->n_free) return fail(c, GCS_ERR_STATE, "primitive map holds max_tiles tiles");
+      s = a->free_slots[nfree++];
+      if (a->slot_written && a->slot_written[s]) clear[ncl++] = s;
+      lo->created_ids[lo->n_created] = lo->active_ids[i];
+      lo->created_slots[lo->n_created++] = s;
+    }
+    lo->active_slots[i] = s;
+  }
+  gcs_surfel_ctx* sf = a->surfels;
+  gcs_assoc_ctx* as = a->assoc;
+  gcs_pmap* pm = a->map;
+  hipStream_t s = c->stream;
+  if (live::surfel_bind_stream(sf, s)) return sub_fail(c, GCS_ERR_HIP, "surfels", gcs_surfel_last_error(sf));
+  if (live::assoc_bind_stream(as, s)) return sub_fail(c, GCS_ERR_HIP, "association", gcs_assoc_last_error(as));
+  if (live::pmap_bind_stream(pm, s)) return sub_fail(c, GCS_ERR_HIP, "map", gcs_pmap_last_error(pm));
+  // surfels of the deskewed points (pipeline.py:778-782); the batch's LiDAR count feeds the launches
+  gcs_surfel_outputs* so = a->surfel_out;
+  if ((rc = live::surfel_launch(sf, a->points_dev, a->timestamps_dev, a->weights_dev, a->n_points, so)))
+    return sub_fail(c, rc, "gcs_extract_lidar_surfels", gcs_surfel_last_error(sf));
+  HIPCHK(c, hipStreamSynchronize(s));
+  live::surfel_collect(sf, so);
+  const int nv = so->n_valid;
+  if (nv > 0) HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)a->lidar_sources_dev, 1, (size_t)nv, s));
+  // recency inflation of the active tiles the map holds, then the view over the stencil (:800-815)
+  if ((rc = live::pmap_recency_launch(pm, rec, nrec, a->scan_seq, a->recency_lambda, a->recency_min_scale)))
+    return sub_fail(c, rc, "gcs_pmap_recency_inflate", gcs_pmap_last_error(pm));
+  if ((rc = live::pmap_view_launch(pm, vs, lo->stencil_ids, ns, a->m_tile_view, a->eps_lift, a->eps_mass, a->view)))
+    return sub_fail(c, rc, "gcs_pmap_extract_view", gcs_pmap_last_error(pm));
+  if ((rc = live::pmap_copy_staged_ids(pm, a->view_tile_ids_dev, ns)))
+    return sub_fail(c, rc, "gcs_pmap_extract_view", gcs_pmap_last_error(pm));
+  // OT association (:816-878)
+  gcs_assoc_meas m = a->meas;
+  m.n_valid = nv;  // n_camera_valid (0: a LiDAR-only batch) + n_lidar_valid
+  gcs_assoc_view v{};
+  v.tile_ids = a->view_tile_ids_dev;
+  v.n_tiles = ns;
+  v.m_tile_view = a->m_tile_view;
+  v.positions = a->view->positions;
+  v.directions = a->view->directions;
+  v.kappas = a->view->kappas;
+  v.valid_mask = a->view->valid_mask;
+  v.last_supported_scan_seq = a->view->last_supported_scan_seq;
+  v.candidate_tile_ids = a->view->candidate_tile_ids;
+  v.candidate_slots = a->view->candidate_slots;
+  gcs_assoc_outputs* ao = a->assoc_out;
+  if ((rc = live::assoc_launch(as, a->assoc_cfg, &m, &v, ao)))
+    return sub_fail(c, rc, "gcs_associate_primitives_ot", gcs_assoc_last_error(as));
+  // visual pose evidence at z_lin_pose (:980-1010); its wait covers the association and the recency
+  gcs_assoc_view vv{};
+  vv.positions = v.positions;
+  vv.directions = v.directions;
+  vv.kappas = v.kappas;
+  vv.valid_mask = v.valid_mask;
+  vv.n_tiles = 1;
+  vv.m_tile_view = ns * a->m_tile_view;
+  gcs_vpe_outputs* vo = a->vpe_out;
+  if ((rc = gcs_visual_pose_evidence(as, &m, &vv, ao->responsibilities, ao->candidate_pool_indices, ao->row_masses,
+                                     a->assoc_cfg->k_assoc, bo->z_lin_pose, a->eps_lift, a->eps_mass, vo)))
+    return sub_fail(c, rc, "gcs_visual_pose_evidence", gcs_assoc_last_error(as));
+  live::assoc_collect(as, ao);
+  live::pmap_recency_collect(pm, nrec, lo->recency_stats);
+  // the finish: trigger magnitudes of the surfel (identity influence), recency (exact), association
+  // (mass_epsilon_ratio unless exact) and visual (lift_strength = eps_lift unless exact) certs; ESS of
+  // the surfel (n_valid), association and visual certs; no mismatch terms (pipeline.py:1049-1056,1211)
+  const double t_assoc = ao->exact ? 0.0 : ao->cert[GCS_ASSOC_CERT_MASS_EPS_RATIO];
+  const double t_vis = vo->exact ? 0.0 : a->eps_lift;
+  const double e_assoc = ao->exact ? 0.0 : ao->cert[GCS_ASSOC_CERT_ESS];
+  const double e_vis = vo->exact ? 0.0 : vo->ess_total;
+  gcs_lidar_evidence ev{};
+  ev.L_lidar = vo->L_pose;
+  ev.h_lidar = vo->h_pose;
+  ev.trigger_sum = ((0.0 + 0.0) + t_assoc) + t_vis;  // the per-cert sums in the pipeline's order
+  ev.ess_sum = ((0.0 + (double)nv) + e_assoc) + e_vis;
+  ev.n_certs = 3;
+  ev.nll_sum = 0.0;
+  lo->trigger_sum = ev.trigger_sum;
+  lo->ess_sum = ev.ess_sum;
+  if ((rc = gcs_scan_finish(c, &ev, out))) return rc;
+  // step 12b at z_t over the active tiles (:1232-1492); new tiles on written slots start cleared
+  for (int k = 0; k < ncl; ++k)
+    if ((rc = live::pmap_clear_tile_launch(pm, clear[k]))) return sub_fail(c, rc, "gcs_pmap_clear_tile", gcs_pmap_last_error(pm));
+  gcs_pmap_update_inputs ui{};
+  ui.Lambdas = m.Lambdas;
+  ui.thetas = m.thetas;
+  ui.etas = m.etas;
+  ui.weights = m.weights;
+  ui.valid = m.valid_mask;
+  ui.colors = a->batch_colors;
+  ui.sources = a->batch_sources;
+  ui.n_total = m.n_total;
+  ui.n_lobes = m.n_lobes;
+  ui.responsibilities = ao->responsibilities;
+  ui.candidate_tile_ids = ao->candidate_tile_ids;
+  ui.candidate_slots = ao->candidate_slots;
+  ui.row_masses = ao->row_masses;
+  ui.k_assoc = a->assoc_cfg->k_assoc;
+  if ((rc = live::pmap_update_launch(pm, lo->active_slots, lo->active_ids, na, out->z_t, a->timestamp, a->scan_seq,
+                                     a->next_global_id, a->update_cfg, &ui)))
+    return sub_fail(c, rc, "gcs_pmap_map_update", gcs_pmap_last_error(pm));
+  lo->next_global_id = a->next_global_id;
+  c->live_map = pm;
+  return GCS_OK;
+}
+
+int gcs_live_collect(gcs_ctx* c, gcs_live_outputs* lo) {
+  if (!c || !lo) return fail(c, GCS_ERR_ARG, "null argument");
+  if (!c->live_map) return fail(c, GCS_ERR_STATE, "gcs_live_collect without gcs_live_scan");
+  gcs_pmap* pm = c->live_map;
+  c->live_map = nullptr;
+  if (int rc = live::pmap_update_collect(pm, &lo->next_global_id, &lo->update, lo->counts))
+    return sub_fail(c, rc, "gcs_pmap_map_update", gcs_pmap_last_error(pm));
+  return GCS_OK;
 }
 
 // ---------------------------------------------------------------- hypothesis payload / combine

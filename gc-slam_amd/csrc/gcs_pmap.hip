@@ -34,6 +34,7 @@
 
 #include "gcs_math.h"
 #include "gcslam_hip.h"
+#include "gcs_live.h"
 
 namespace gcs {
 namespace {
@@ -1888,12 +1889,21 @@ struct gcs_pmap {
   char* h_small = nullptr;
   char* d_small = nullptr;
   std::string err;
+  // step 12b queued by gcs::live::pmap_update_launch, read by pmap_update_collect
+  struct {
+    bool on = false;
+    int n = 0, nb = 0, kins = 0, nbt = 0;
+    int64_t next_id = 0;
+    std::vector<int32_t> tiles;
+    gcs_pmap_update_config cfg{};
+  } pend;
 };
 
 namespace {
 constexpr size_t kSmall = 4 << 20;
 constexpr size_t kWiOff = 1 << 20;  // step 12b: proposal weights (n x k_insert_tile doubles)
 constexpr size_t kFmOff = 2 << 20;  // step 12b: fused mass per (association block, tile)
+constexpr size_t kRecOff = 3 << 20; // recency inflation partials (kept apart from step 12b's cull partials)
 constexpr size_t kPartOff = 1 << 16;  // per-(tile, block) reduction partials in the mapped buffer
 constexpr int kMaxBlocksPerTile = 64;
 constexpr int kMaxFuseBlocks = 256;  // association blocks of one map update
@@ -2145,18 +2155,16 @@ const char* gcs_pmap_last_error(const gcs_pmap* p) { return p ? p->err.c_str() :
 
 int gcs_pmap_set_stream(gcs_pmap* p, void* stream) {
   if (!p) return GCS_ERR_ARG;
+  hipStream_t ns = stream ? (hipStream_t)stream : p->own;
+  if (ns == p->stream) return GCS_OK;
   PMCHK(p, hipSetDevice(p->device));
   PMCHK(p, hipStreamSynchronize(p->stream));
-  p->stream = stream ? (hipStream_t)stream : p->own;
+  p->stream = ns;
   return GCS_OK;
 }
 
 int gcs_pmap_clear_tile(gcs_pmap* p, int32_t tile) {
-  if (!p) return GCS_ERR_ARG;
-  if (tile < 0 || tile >= p->T) return pm_fail(p, GCS_ERR_ARG, "tile storage index out of range");
-  PMCHK(p, hipSetDevice(p->device));
-  hipLaunchKernelGGL(k_pm_clear, dim3((p->M + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream, p->st,
-                     tile);
+  if (int rc = gcs::live::pmap_clear_tile_launch(p, tile)) return rc;
   PMCHK(p, hipStreamSynchronize(p->stream));
   return GCS_OK;
 }
@@ -2205,6 +2213,39 @@ int gcs_pmap_copy_tiles(gcs_pmap* dst, const int32_t* dst_tiles, const gcs_pmap*
 
 int gcs_pmap_extract_view(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_ids, int32_t n, int32_t m_view,
                           double eps_lift, double eps_mass, gcs_pmap_view* o) {
+  if (int rc = gcs::live::pmap_view_launch(p, tiles, tile_ids, n, m_view, eps_lift, eps_mass, o)) return rc;
+  if (n > 0) PMCHK(p, hipStreamSynchronize(p->stream));
+  return GCS_OK;
+}
+}  // extern "C"
+
+namespace gcs {
+namespace live {
+int pmap_bind_stream(gcs_pmap* p, void* s) {
+  if ((hipStream_t)s == p->stream) return GCS_OK;
+  PMCHK(p, hipSetDevice(p->device));
+  PMCHK(p, hipStreamSynchronize(p->stream));
+  p->stream = (hipStream_t)s;
+  return GCS_OK;
+}
+
+int pmap_clear_tile_launch(gcs_pmap* p, int32_t tile) {
+  if (!p) return GCS_ERR_ARG;
+  if (tile < 0 || tile >= p->T) return pm_fail(p, GCS_ERR_ARG, "tile storage index out of range");
+  PMCHK(p, hipSetDevice(p->device));
+  hipLaunchKernelGGL(k_pm_clear, dim3((p->M + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream, p->st,
+                     tile);
+  PMCHK(p, hipGetLastError());
+  return GCS_OK;
+}
+
+int pmap_copy_staged_ids(gcs_pmap* p, int64_t* dst, int32_t n) {
+  if (n > 0) PMCHK(p, hipMemcpyAsync(dst, p->d_tids, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToDevice, p->stream));
+  return GCS_OK;
+}
+
+int pmap_view_launch(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_ids, int32_t n, int32_t m_view,
+                     double eps_lift, double eps_mass, gcs_pmap_view* o) {
   if (!p || !o || !tile_ids) return GCS_ERR_ARG;
   if (m_view <= 0) return pm_fail(p, GCS_ERR_ARG, "extract_atlas_map_view: m_tile_view must be > 0");
   if (m_view > p->M) return pm_fail(p, GCS_ERR_ARG, "m_tile_view exceeds the tile size");
@@ -2231,9 +2272,12 @@ int gcs_pmap_extract_view(gcs_pmap* p, const int32_t* tiles, const int64_t* tile
                      p->st, (const int32_t*)p->d_tiles, (const int64_t*)p->d_tids, n, m_view,
                      (const uint32_t*)p->vals, eps_lift, eps_mass, v);
   PMCHK(p, hipGetLastError());
-  PMCHK(p, hipStreamSynchronize(p->stream));
   return GCS_OK;
 }
+}  // namespace live
+}  // namespace gcs
+
+extern "C" {
 
 int gcs_pmap_insert_masked(gcs_pmap* p, const int32_t* tiles, int32_t n, int32_t K, const gcs_pmap_rows* rows,
                            double timestamp, int64_t scan_seq, double lam, int64_t next_global_id, int64_t* new_ids,
@@ -2451,25 +2495,46 @@ int gcs_pmap_forget(gcs_pmap* p, const int32_t* tiles, int32_t n, double gamma) 
 int gcs_pmap_recency_inflate(gcs_pmap* p, const int32_t* tiles, int32_t n, int64_t scan_seq, double lam,
                              double min_scale, double* stats) {
   if (!p || !stats) return GCS_ERR_ARG;
+  if (int rc = gcs::live::pmap_recency_launch(p, tiles, n, scan_seq, lam, min_scale)) return rc;
+  if (n > 0) PMCHK(p, hipStreamSynchronize(p->stream));
+  gcs::live::pmap_recency_collect(p, n, stats);
+  return GCS_OK;
+}
+}  // extern "C"
+
+namespace gcs {
+namespace live {
+int pmap_recency_launch(gcs_pmap* p, const int32_t* tiles, int32_t n, int64_t scan_seq, double lam,
+                        double min_scale) {
+  if (!p) return GCS_ERR_ARG;
   if (int rc = check_tiles(p, tiles, n, false)) return rc;
-  stats[0] = stats[1] = stats[2] = 0.0;
   if (n == 0) return GCS_OK;
+  const int nbt = blocks_per_tile(p->M);
+  if ((size_t)n * nbt * 3 * sizeof(double) > kSmall - kRecOff)
+    return pm_fail(p, GCS_ERR_ARG, "recency inflation: partials exceed the mapped buffer");
   PMCHK(p, hipSetDevice(p->device));
   if (int rc = upload_tiles(p, tiles, n)) return rc;
-  const int nbt = blocks_per_tile(p->M);
   hipLaunchKernelGGL(k_pm_recency, dim3(n, nbt), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
-                     (long long)scan_seq, lam, min_scale, (double*)(p->d_small + kPartOff));
+                     (long long)scan_seq, lam, min_scale, (double*)(p->d_small + kRecOff));
   PMCHK(p, hipGetLastError());
-  PMCHK(p, hipStreamSynchronize(p->stream));
-  const double* h = (const double*)(p->h_small + kPartOff);
+  return GCS_OK;
+}
+
+void pmap_recency_collect(gcs_pmap* p, int32_t n, double* stats) {
+  stats[0] = stats[1] = stats[2] = 0.0;
+  const int nbt = blocks_per_tile(p->M);
+  const double* h = (const double*)(p->h_small + kRecOff);
   for (int t = 0; t < n; ++t) {  // per tile (block partials in order), then the reference's sums over tiles
     double a[3] = {0.0, 0.0, 0.0};
     for (int b = 0; b < nbt; ++b)
       for (int k = 0; k < 3; ++k) a[k] += h[3 * (t * nbt + b) + k];
     for (int k = 0; k < 3; ++k) stats[k] += a[k];
   }
-  return GCS_OK;
 }
+}  // namespace live
+}  // namespace gcs
+
+extern "C" {
 
 int gcs_pmap_merge_reduce(gcs_pmap* p, int32_t tile, double thr, int32_t max_pairs, double eps_psd, double eps_lift,
                           int32_t* n_merged, int32_t* pairs, int32_t* count) {
@@ -2510,7 +2575,22 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
                         double timestamp, int64_t scan_seq, int64_t* next_global_id,
                         const gcs_pmap_update_config* cfg, const gcs_pmap_update_inputs* in,
                         gcs_pmap_update_stats* st, int32_t* counts) {
-  if (!p || !z_t6 || !next_global_id || !cfg || !in || !st || !counts || !tile_ids) return GCS_ERR_ARG;
+  if (!p || !next_global_id || !st || !counts) return GCS_ERR_ARG;
+  memset(st, 0, sizeof(*st));
+  if (int rc = gcs::live::pmap_update_launch(p, tiles, tile_ids, n, z_t6, timestamp, scan_seq, *next_global_id, cfg,
+                                             in))
+    return rc;
+  return gcs::live::pmap_update_collect(p, next_global_id, st, counts);
+}
+}  // extern "C"
+
+namespace gcs {
+namespace live {
+int pmap_update_launch(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_ids, int32_t n, const double* z_t6,
+                       double timestamp, int64_t scan_seq, int64_t next_global_id, const gcs_pmap_update_config* cfg,
+                       const gcs_pmap_update_inputs* in) {
+  if (!p || !z_t6 || !cfg || !in || !tile_ids) return GCS_ERR_ARG;
+  p->pend.on = false;
   if (int rc = check_tiles(p, tiles, n, false)) return rc;
   if (in->n_total < 1 || in->k_assoc < 1 || !in->Lambdas || !in->thetas || !in->etas || !in->weights || !in->valid ||
       !in->responsibilities || !in->candidate_tile_ids || !in->candidate_slots || !in->row_masses)
@@ -2518,8 +2598,14 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   if (cfg->block_size < 1 || cfg->k_insert_tile < 0 || cfg->k_insert_tile > kPropMaxIns || in->n_lobes != p->nl)
     return pm_fail(p, GCS_ERR_ARG, "map update: bad block size, insert budget (<= 1024) or lobe count");
   if (in->n_total > kPropLds) return pm_fail(p, GCS_ERR_ARG, "map update: more than 2048 measurement rows");
-  memset(st, 0, sizeof(*st));
-  if (n == 0) return GCS_OK;
+  p->pend.n = n;
+  p->pend.next_id = next_global_id;
+  p->pend.cfg = *cfg;
+  p->pend.tiles.assign(tiles, tiles + n);
+  if (n == 0) {
+    p->pend.on = true;
+    return GCS_OK;
+  }
   PMCHK(p, hipSetDevice(p->device));
   PmWorld W{};
   so3_exp(z_t6 + 3, W.R);
@@ -2582,7 +2668,7 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   hipLaunchKernelGGL(k_pm_fuse_rows, dim3((nrows + kPmThreads - 1) / kPmThreads), dim3(kPmThreads), 0, p->stream, m, W,
                      nl, B, nrows, (const int64_t*)act, n, o);
   PMCHK(p, hipGetLastError());
-  if ((size_t)nb * n * 8 > kSmall - kFmOff || (size_t)nprop * 8 > kFmOff - kWiOff)
+  if ((size_t)nb * n * 8 > kRecOff - kFmOff || (size_t)nprop * 8 > kFmOff - kWiOff)
     return pm_fail(p, GCS_ERR_ARG, "map update: stats exceed the mapped buffer");
   if (n > 0)
     hipLaunchKernelGGL(k_pm_fm_sums, dim3(nb, n), dim3(kPmThreads), 0, p->stream, (const double*)o.fm,
@@ -2621,7 +2707,7 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
     if (int rc = sort_tiles(p, n, 1, scan_seq, cfg->recency_decay_lambda, kins)) return rc;
     hipLaunchKernelGGL(k_pm_insert, dim3(n), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, kins,
                        (const uint32_t*)p->vals, rows_of(&rp), timestamp, (long long)scan_seq,
-                       (long long)*next_global_id, (int64_t*)nullptr, d_ins);
+                       (long long)next_global_id, (int64_t*)nullptr, d_ins);
     PMCHK(p, hipGetLastError());
   }
   // per tile: cull (its partials carry the valid count after it) and forget in one pass
@@ -2630,6 +2716,24 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   hipLaunchKernelGGL(k_pm_cull, dim3(n, nbt), dim3(kPmRed), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
                      cfg->cull_threshold, (double*)(p->d_small + kPartOff), 1, cfg->forgetting_factor);
   PMCHK(p, hipGetLastError());
+  p->pend.nb = nb;
+  p->pend.kins = kins;
+  p->pend.nbt = nbt;
+  p->pend.on = true;
+  return GCS_OK;
+}
+
+int pmap_update_collect(gcs_pmap* p, int64_t* next_global_id, gcs_pmap_update_stats* st, int32_t* counts) {
+  if (!p || !next_global_id || !st || !counts) return GCS_ERR_ARG;
+  memset(st, 0, sizeof(*st));
+  if (!p->pend.on) return pm_fail(p, GCS_ERR_STATE, "map update: nothing queued");
+  p->pend.on = false;
+  const int n = p->pend.n, nb = p->pend.nb, kins = p->pend.kins, nbt = p->pend.nbt;
+  const gcs_pmap_update_config* cfg = &p->pend.cfg;
+  const int32_t* tiles = p->pend.tiles.data();
+  *next_global_id = p->pend.next_id;
+  if (n == 0) return GCS_OK;
+  PMCHK(p, hipSetDevice(p->device));
   PMCHK(p, hipStreamSynchronize(p->stream));
   if (*(uint32_t*)(p->h_small + 8192)) return pm_fail(p, GCS_ERR_ARG, "target slot out of range (rows skipped)");
   {
@@ -2687,5 +2791,5 @@ int gcs_pmap_map_update(gcs_pmap* p, const int32_t* tiles, const int64_t* tile_i
   }
   return GCS_OK;
 }
-
-}  // extern "C"
+}  // namespace live
+}  // namespace gcs

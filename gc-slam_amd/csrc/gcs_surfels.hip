@@ -31,6 +31,7 @@
 
 #include "gcs_math.h"
 #include "gcslam_hip.h"
+#include "gcs_live.h"
 
 namespace gcs {
 namespace {
@@ -559,14 +560,28 @@ int gcs_surfel_ctx_create(const gcs_surfel_config* cfg, gcs_surfel_ctx** out) {
 
 int gcs_surfel_ctx_set_stream(gcs_surfel_ctx* c, void* stream) {
   if (!c) return GCS_ERR_ARG;
+  hipStream_t ns = stream ? (hipStream_t)stream : c->own;
+  if (ns == c->stream) return GCS_OK;
   SFCHK(c, hipSetDevice(c->device));
   SFCHK(c, hipStreamSynchronize(c->stream));  // work queued on the old stream completes first
-  c->stream = stream ? (hipStream_t)stream : c->own;
+  c->stream = ns;
   return GCS_OK;
 }
 
-int gcs_extract_lidar_surfels(gcs_surfel_ctx* c, const double* points, const double* timestamps,
-                              const double* weights, int32_t n, gcs_surfel_outputs* o) {
+}  // extern "C"
+
+namespace gcs {
+namespace live {
+int surfel_bind_stream(gcs_surfel_ctx* c, void* s) {
+  if ((hipStream_t)s == c->stream) return GCS_OK;
+  SFCHK(c, hipSetDevice(c->device));
+  SFCHK(c, hipStreamSynchronize(c->stream));
+  c->stream = (hipStream_t)s;
+  return GCS_OK;
+}
+
+int surfel_launch(gcs_surfel_ctx* c, const double* points, const double* timestamps, const double* weights,
+                  int32_t n, gcs_surfel_outputs* o) {
   if (!c || !o) return GCS_ERR_ARG;
   if (n < 0 || n > c->cfg.max_points) return sf_fail(c, GCS_ERR_ARG, "n exceeds max_points");
   if (n > 0 && (!points || !timestamps || !weights)) return sf_fail(c, GCS_ERR_ARG, "null input");
@@ -603,14 +618,26 @@ int gcs_extract_lidar_surfels(gcs_surfel_ctx* c, const double* points, const dou
   if (o->bucket)
     SFCHK(c, hipMemcpyAsync(o->bucket, c->d_bucket, (size_t)a.n_cells * a.max_occ * 4, hipMemcpyDeviceToDevice, s));
   if (o->count) SFCHK(c, hipMemcpyAsync(o->count, c->d_count, (size_t)a.n_cells * 4, hipMemcpyDeviceToDevice, s));
-  SFCHK(c, hipStreamSynchronize(s));
+  return GCS_OK;
+}
+
+void surfel_collect(gcs_surfel_ctx* c, gcs_surfel_outputs* o) {
   for (int k = 0; k < 3; ++k) o->center[k] = c->h_scal[k];
   int32_t nv;
   memcpy(&nv, c->h_scal + 3, sizeof(nv));
   o->n_valid = nv;
   o->cert[0] = (double)nv;
   o->cert[1] = (double)nv / (double)std::max(c->cfg.n_surfel, 1);
+}
+}  // namespace live
+}  // namespace gcs
+
+extern "C" {
+int gcs_extract_lidar_surfels(gcs_surfel_ctx* c, const double* points, const double* timestamps,
+                              const double* weights, int32_t n, gcs_surfel_outputs* o) {
+  if (int rc = gcs::live::surfel_launch(c, points, timestamps, weights, n, o)) return rc;
+  SFCHK(c, hipStreamSynchronize(c->stream));
+  gcs::live::surfel_collect(c, o);
   return GCS_OK;
 }
-
 }  // extern "C"

@@ -15,7 +15,7 @@ import numpy as np
 LIB_NAME = "libgcslam_hip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 
-ABI_VERSION = 3  # include/gcslam_hip.h GCS_ABI_VERSION
+ABI_VERSION = 4  # include/gcslam_hip.h GCS_ABI_VERSION
 D_Z = 22
 CERT_LEN = 64
 PAYLOAD_LEN = 840
@@ -201,6 +201,34 @@ class GcsAssocOutputs(C.Structure):
                [("cert", C.c_double * GCS_ASSOC_CERT_LEN), ("exact", C.c_int32), ("n_map_valid", C.c_int32)]
 
 
+LIVE_MAX_TILES = 64
+
+
+class GcsLiveArgs(C.Structure):
+    _fields_ = [("surfels", C.c_void_p), ("assoc", C.c_void_p), ("map", C.c_void_p),
+                ("n_tiles", C.c_int32), ("tile_ids", C.c_void_p), ("tile_slots", C.c_void_p), ("n_free", C.c_int32),
+                ("free_slots", C.c_void_p), ("slot_written", C.c_void_p), ("next_global_id", C.c_int64),
+                ("h_tile", C.c_double), ("r_active_xy", C.c_int32), ("r_active_z", C.c_int32),
+                ("r_stencil_xy", C.c_int32), ("r_stencil_z", C.c_int32), ("n_active_expected", C.c_int32),
+                ("n_stencil_expected", C.c_int32), ("scan_seq", C.c_int64), ("recency_lambda", C.c_double),
+                ("recency_min_scale", C.c_double), ("m_tile_view", C.c_int32), ("eps_lift", C.c_double),
+                ("eps_mass", C.c_double), ("assoc_cfg", C.c_void_p), ("update_cfg", C.c_void_p),
+                ("timestamp", C.c_double), ("points_dev", C.c_void_p), ("timestamps_dev", C.c_void_p),
+                ("weights_dev", C.c_void_p), ("n_points", C.c_int32), ("surfel_out", C.c_void_p),
+                ("lidar_sources_dev", C.c_void_p), ("meas", GcsAssocMeas), ("batch_colors", C.c_void_p),
+                ("batch_sources", C.c_void_p), ("view", C.c_void_p), ("view_tile_ids_dev", C.c_void_p),
+                ("assoc_out", C.c_void_p), ("vpe_out", C.c_void_p)]
+
+
+class GcsLiveOutputs(C.Structure):
+    _fields_ = [("n_active", C.c_int32), ("n_stencil", C.c_int32), ("active_ids", C.c_int64 * LIVE_MAX_TILES),
+                ("stencil_ids", C.c_int64 * LIVE_MAX_TILES), ("active_slots", C.c_int32 * LIVE_MAX_TILES),
+                ("n_present_active", C.c_int32), ("n_created", C.c_int32),
+                ("created_ids", C.c_int64 * LIVE_MAX_TILES), ("created_slots", C.c_int32 * LIVE_MAX_TILES),
+                ("recency_stats", C.c_double * 3), ("trigger_sum", C.c_double), ("ess_sum", C.c_double),
+                ("update", GcsPmapUpdateStats), ("counts", C.c_int32 * LIVE_MAX_TILES), ("next_global_id", C.c_int64)]
+
+
 _SIGS = [
     ("gcs_version", C.c_char_p, []),
     ("gcs_abi_version", C.c_int, []),
@@ -330,6 +358,10 @@ _SIGS = [
     ("gcs_pmap_map_update", C.c_int, [C.c_void_p, c_int32_p, c_int64_p, C.c_int32, c_double_p, C.c_double, C.c_int64,
                                       c_int64_p, C.POINTER(GcsPmapUpdateConfig), C.POINTER(GcsPmapUpdateInputs),
                                       C.POINTER(GcsPmapUpdateStats), c_int32_p]),
+    ("gcs_live_scan", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(GcsScanBeginOutputs), C.POINTER(GcsLiveArgs),
+                                C.POINTER(GcsLiveOutputs), C.POINTER(GcsScanOutputs)]),
+    ("gcs_live_collect", C.c_int, [C.c_void_p, C.POINTER(GcsLiveOutputs)]),
+    ("gcs_ma_hex_stencil", C.c_int, [c_double_p, C.c_double, C.c_int32, C.c_int32, c_int64_p, C.c_int32]),
 ]
 
 SYMBOLS = [s[0] for s in _SIGS]
@@ -358,7 +390,8 @@ def load():
         pass
     lib = C.CDLL(path)
     # the structs above mirror include/gcslam_hip.h of this ABI: a library of another ABI would read
-    # or write past them (ABI 3: gcs_assoc_outputs.cert grew to GCS_ASSOC_CERT_LEN 21)
+    # or write past them (ABI 3: gcs_assoc_outputs.cert grew to GCS_ASSOC_CERT_LEN 21; ABI 4: the one-call
+    # live path's structs)
     lib.gcs_abi_version.restype = C.c_int
     abi = lib.gcs_abi_version()
     if abi != ABI_VERSION:

@@ -165,28 +165,8 @@ class Associator:
         v.n_tiles, v.m_tile_view = int(keep[5].shape[0]), int(view.m_tile_view)
         (v.positions, v.directions, v.kappas, v.valid_mask, v.last_supported_scan_seq, v.candidate_tile_ids,
          v.candidate_slots) = (t.data_ptr() for t in keep[6:])
-        K = int(config.k_assoc)
-        out = dict(responsibilities=torch.empty((N, K), dtype=torch.float64, device=dev),
-                   candidate_pool_indices=torch.empty((N, K), dtype=torch.int32, device=dev),
-                   candidate_tile_ids=torch.empty((N, K), dtype=torch.int64, device=dev),
-                   candidate_slots=torch.empty((N, K), dtype=torch.int64, device=dev),
-                   row_masses=torch.empty((N,), dtype=torch.float64, device=dev),
-                   cost_matrix=torch.empty((N, K), dtype=torch.float64, device=dev))
-        o = L.GcsAssocOutputs()
-        for k, t in out.items():
-            setattr(o, k, t.data_ptr())
-        c = L.GcsAssocConfig()
-        self._chk(self.lib.gcs_assoc_config_defaults(C.byref(c)), "gcs_assoc_config_defaults")
-        c.k_assoc, c.k_sinkhorn = K, int(config.k_sinkhorn)
-        c.beta, c.epsilon, c.tau_a, c.tau_b = float(config.beta), float(config.epsilon), float(config.tau_a), \
-            float(config.tau_b)
-        c.cost_subtract_row_min, c.cost_scale_by_median = int(bool(config.cost_subtract_row_min)), \
-            int(bool(config.cost_scale_by_median))
-        c.a_policy, c.b_policy = _A_CODE[config.a_policy], _B_CODE[config.b_policy]
-        c.eps_mass, c.eps_lift, c.eps_mass_dir = float(config.eps_mass), float(eps_lift), float(eps_mass)
-        c.h_tile = float(config.h_tile)
-        c.r_stencil_tiles_xy, c.r_stencil_tiles_z = int(config.r_stencil_tiles_xy), int(config.r_stencil_tiles_z)
-        c.scan_seq, c.recency_decay_lambda = int(config.scan_seq), float(config.recency_decay_lambda)
+        out, o = assoc_outputs(N, int(config.k_assoc), dev)
+        c = assoc_config_struct(config, eps_lift, eps_mass)
         self._chk(self.lib.gcs_assoc_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
                   "gcs_assoc_ctx_set_stream")
         lib, h, chk = self.lib, self.h, self._chk
@@ -230,6 +210,70 @@ class Associator:
         return o
 
 
+def assoc_outputs(N: int, K: int, dev: str):
+    """Fresh PrimitiveAssociationResult tensors (N x K) and the gcs_assoc_outputs struct naming them."""
+    torch = _torch()
+    out = dict(responsibilities=torch.empty((N, K), dtype=torch.float64, device=dev),
+               candidate_pool_indices=torch.empty((N, K), dtype=torch.int32, device=dev),
+               candidate_tile_ids=torch.empty((N, K), dtype=torch.int64, device=dev),
+               candidate_slots=torch.empty((N, K), dtype=torch.int64, device=dev),
+               row_masses=torch.empty((N,), dtype=torch.float64, device=dev),
+               cost_matrix=torch.empty((N, K), dtype=torch.float64, device=dev))
+    o = L.GcsAssocOutputs()
+    for k, t in out.items():
+        setattr(o, k, t.data_ptr())
+    return out, o
+
+
+def assoc_config_struct(config: AssociationConfig, eps_lift=GC_EPS_LIFT, eps_mass=GC_EPS_MASS):
+    """gcs_assoc_config of an AssociationConfig and the operator's eps_lift / eps_mass arguments."""
+    c = L.GcsAssocConfig()
+    L.check(L.load().gcs_assoc_config_defaults(C.byref(c)), None, "gcs_assoc_config_defaults")
+    c.k_assoc, c.k_sinkhorn = int(config.k_assoc), int(config.k_sinkhorn)
+    c.beta, c.epsilon, c.tau_a, c.tau_b = float(config.beta), float(config.epsilon), float(config.tau_a), \
+        float(config.tau_b)
+    c.cost_subtract_row_min, c.cost_scale_by_median = int(bool(config.cost_subtract_row_min)), \
+        int(bool(config.cost_scale_by_median))
+    c.a_policy, c.b_policy = _A_CODE[config.a_policy], _B_CODE[config.b_policy]
+    c.eps_mass, c.eps_lift, c.eps_mass_dir = float(config.eps_mass), float(eps_lift), float(eps_mass)
+    c.h_tile = float(config.h_tile)
+    c.r_stencil_tiles_xy, c.r_stencil_tiles_z = int(config.r_stencil_tiles_xy), int(config.r_stencil_tiles_z)
+    c.scan_seq, c.recency_decay_lambda = int(config.scan_seq), float(config.recency_decay_lambda)
+    return c
+
+
+def association_result(out: dict, o) -> "PrimitiveAssociationResult":
+    """The PrimitiveAssociationResult of filled outputs (candidate statistics from the cert slots)."""
+    cs = (float(o.cert[18]), float(o.cert[19]), float(o.cert[20]))
+    return PrimitiveAssociationResult(**out, candidate_stats=cs)
+
+
+def association_cert(o, config: AssociationConfig, N: int, chart_id: str = CHART_ID, anchor_id: str = "primitive_ot"):
+    """(CertBundle, ExpectedEffect) of an association call's host results (o: gcs_assoc_outputs)."""
+    if o.exact:
+        cert = CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id)
+        return cert, ExpectedEffect(objective_name="primitive_association_ot", predicted=0.0, realized=0.0)
+    cv = {k: float(o.cert[i]) for i, k in enumerate(L.ASSOC_CERT_FIELDS)}
+    K = int(config.k_assoc)
+    compute = ComputeCert(alloc_bytes_est=int(N * K * 8 * 4), largest_tensor_shape=(N, K), segment_sum_k=K,
+                          psd_projection_count=0, chol_solve_count=0)
+    cert = CertBundle.create_approx(
+        chart_id=chart_id, anchor_id=anchor_id, triggers=["sinkhorn_fixed_iter", "sinkhorn_unbalanced_kl_relax"],
+        frobenius_applied=False, support=SupportCert(ess_total=cv["ess_total"], support_frac=cv["support_frac"]),
+        influence=InfluenceCert.identity().with_overrides(mass_epsilon_ratio=cv["mass_epsilon_ratio"]),
+        compute=compute)
+    cert.ot = OTCert(marginal_defect_a=cv["marginal_defect_a"], marginal_defect_b=cv["marginal_defect_b"],
+                     transport_mass_total=cv["transport_mass_total"], dual_gap_proxy=0.0, sum_a=cv["sum_a"],
+                     sum_b=cv["sum_b"], sum_m=cv["sum_m"], sum_novel=cv["sum_novel"], p95_a=cv["p95_a"],
+                     p95_b=cv["p95_b"], nonzero_a=int(cv["nonzero_a"]), nonzero_b=int(cv["nonzero_b"]),
+                     epsilon=float(config.epsilon), tau_a=float(config.tau_a), tau_b=float(config.tau_b),
+                     n_iters=int(config.k_sinkhorn), b_policy=str(config.b_policy.value),
+                     b_recency_decay_lambda=float(config.recency_decay_lambda), b_recency_p95=cv["b_recency_p95"])
+    effect = ExpectedEffect(objective_name="primitive_association_ot", predicted=cv["total_cost"],
+                            realized=cv["total_cost"])
+    return cert, effect
+
+
 _associators = {}
 
 
@@ -256,29 +300,10 @@ def associate_primitives_ot(measurement_batch, map_view: AtlasMapView, config: O
     K = int(config.k_assoc)
     pool = int(np.asarray(map_view.tile_ids.shape)[0]) * int(map_view.m_tile_view)
     a = associator or _associator_for(N, pool, K, device)
-    out, cv, exact = a.run(measurement_batch, map_view, config, eps_lift=eps_lift, eps_mass=eps_mass)
-    result = PrimitiveAssociationResult(**out, candidate_stats=(cv["cand_tiles_mean"], cv["cand_prims_mean"],
-                                                                cv["cand_prims_p95"]))
-    if exact:
-        cert = CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id)
-        return result, cert, ExpectedEffect(objective_name="primitive_association_ot", predicted=0.0, realized=0.0)
-    compute = ComputeCert(alloc_bytes_est=int(N * K * 8 * 4), largest_tensor_shape=(N, K), segment_sum_k=K,
-                          psd_projection_count=0, chol_solve_count=0)
-    cert = CertBundle.create_approx(
-        chart_id=chart_id, anchor_id=anchor_id, triggers=["sinkhorn_fixed_iter", "sinkhorn_unbalanced_kl_relax"],
-        frobenius_applied=False, support=SupportCert(ess_total=cv["ess_total"], support_frac=cv["support_frac"]),
-        influence=InfluenceCert.identity().with_overrides(mass_epsilon_ratio=cv["mass_epsilon_ratio"]),
-        compute=compute)
-    cert.ot = OTCert(marginal_defect_a=cv["marginal_defect_a"], marginal_defect_b=cv["marginal_defect_b"],
-                     transport_mass_total=cv["transport_mass_total"], dual_gap_proxy=0.0, sum_a=cv["sum_a"],
-                     sum_b=cv["sum_b"], sum_m=cv["sum_m"], sum_novel=cv["sum_novel"], p95_a=cv["p95_a"],
-                     p95_b=cv["p95_b"], nonzero_a=int(cv["nonzero_a"]), nonzero_b=int(cv["nonzero_b"]),
-                     epsilon=float(config.epsilon), tau_a=float(config.tau_a), tau_b=float(config.tau_b),
-                     n_iters=int(config.k_sinkhorn), b_policy=str(config.b_policy.value),
-                     b_recency_decay_lambda=float(config.recency_decay_lambda), b_recency_p95=cv["b_recency_p95"])
-    effect = ExpectedEffect(objective_name="primitive_association_ot", predicted=cv["total_cost"],
-                            realized=cv["total_cost"])
-    return result, cert, effect
+    call = a.prepare(measurement_batch, map_view, config, eps_lift, eps_mass)
+    o = call()
+    cert, effect = association_cert(o, config, N, chart_id, anchor_id)
+    return association_result(call.out, o), cert, effect
 
 
 @dataclass
@@ -311,6 +336,11 @@ def visual_pose_evidence(association_result: PrimitiveAssociationResult, measure
     pool = int(np.asarray(map_view.valid_mask.shape)[0])
     a = associator or _associator_for(max(N, 1), pool, max(K, 1), device)
     o = a.pose_evidence(measurement_batch, map_view, association_result, K, z_lin_pose, eps_lift, eps_mass)
+    return visual_pose_result(o, eps_lift, chart_id, anchor_id)
+
+
+def visual_pose_result(o, eps_lift=GC_EPS_LIFT, chart_id: str = CHART_ID, anchor_id: str = "visual_pose_evidence"):
+    """(VisualPoseEvidenceResult, CertBundle, ExpectedEffect) of gcs_visual_pose_evidence's outputs."""
     view = np.ctypeslib.as_array
     res = VisualPoseEvidenceResult(L_pose=view(o.L_pose).reshape(22, 22).copy(), h_pose=view(o.h_pose).copy(),
                                    L_trans=view(o.L_trans).reshape(3, 3).copy(), h_trans=view(o.h_trans).copy(),

@@ -68,11 +68,13 @@ class HypothesisContext:
         rc = self.lib.gcs_ctx_create(C.byref(cfg), C.byref(h))
         L.check(rc, None, "gcs_ctx_create")
         self.h = h
+        self.stream_ptr = None  # the torch stream the context runs on (None: its own)
         if use_torch_stream:
             torch = _torch()
             with torch.cuda.device(self.device):
                 s = torch.cuda.current_stream().cuda_stream
             L.check(self.lib.gcs_ctx_set_stream(self.h, C.c_void_p(s)), self.h, "set_stream")
+            self.stream_ptr = int(s)
 
     # ------------------------------------------------------------------ lifetime
     def close(self):

@@ -23,6 +23,8 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
+import ctypes as C
+
 from . import _lib as L
 from .certificates import (CertBundle, ConditioningCert, ExpectedEffect, InfluenceCert, MismatchCert, SupportCert,
                            aggregate_certificates)
@@ -305,6 +307,10 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
     import torch
     from . import association as GA, primitive_map as GPM
     from .surfels import SurfelExtractionConfig, extract_lidar_surfels
+    if _live_chain_enabled(ctx, config):
+        return _process_scan_live_chain(ctx, primitive_map, rec, t, w, imu_stamps, imu_gyro, imu_accel, odom_pose,
+                                        odom_cov_se3, scan_start_time, scan_end_time, dt_sec, t_last_scan, t_scan, Q,
+                                        config, odom_twist, odom_twist_cov, scan_seq, L_ext, h_ext, update_map)
     cap = ctx.cfg.n_points_cap
     dev = f"cuda:{config.device}"
     bufs = getattr(ctx, "_live_bufs", None)
@@ -403,6 +409,210 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
                      association=res, view=view, z_lin_pose=z_lin_pose, map_record=record, stage_ms=stage_ms)
 
 
+def _live_chain_enabled(ctx: HypothesisContext, config: "PipelineConfig") -> bool:
+    """The one-call live path (gcs_live_scan) unless per-stage wall times are asked for
+    (config.enable_timing: the per-operator path syncs between stages), GCSLAM_LIVE_CHAIN=0, or the context
+    runs on a stream other than torch's current one (the batch / view / association tensors are
+    allocated on torch's stream; the chain queues on the context's)."""
+    import os
+    import torch
+    if config.enable_timing or os.environ.get("GCSLAM_LIVE_CHAIN", "1") == "0":
+        return False
+    return ctx.stream_ptr is not None and ctx.stream_ptr == torch.cuda.current_stream(config.device).cuda_stream
+
+
+def _live_chain_state(ctx: HypothesisContext, config: "PipelineConfig"):
+    """gcs_live_scan's per-(context, config) arguments: the surfel / association contexts, the config
+    structs and the fields of gcs_live_args that do not change between scans (cached on the context)."""
+    from . import association as GA, primitive_map as GPM
+    from .surfels import SurfelExtractionConfig, _extractor_for
+    key = (config.n_surfel, config.n_feat, config.surfel_voxel_size_m, config.surfel_min_points_per_voxel,
+           config.eps_lift, config.eps_mass, config.eps_psd, config.k_assoc, config.k_sinkhorn, config.ot_epsilon,
+           config.ot_tau_a, config.ot_tau_b, config.H_TILE, config.R_ACTIVE_TILES_XY, config.R_ACTIVE_TILES_Z,
+           config.R_STENCIL_TILES_XY, config.R_STENCIL_TILES_Z, config.N_ACTIVE_TILES, config.N_STENCIL_TILES,
+           config.RECENCY_DECAY_LAMBDA, config.RECENCY_MIN_SCALE, config.M_TILE_VIEW, config.k_insert_tile,
+           config.device, ctx.cfg.n_points_cap)
+    st = getattr(ctx, "_live_chain", None)
+    if st is not None and st["key"] == key:
+        return st
+    cap = ctx.cfg.n_points_cap
+    scfg = SurfelExtractionConfig(n_surfel=config.n_surfel, n_feat=config.n_feat,
+                                  voxel_size_m=config.surfel_voxel_size_m,
+                                  min_points_per_voxel=config.surfel_min_points_per_voxel, eps_lift=config.eps_lift)
+    # the association runs with its operator defaults for eps_lift / eps_mass, as the per-operator path
+    # calls it (associate_primitives_ot(batch, view, acfg)); the view and the pose evidence take the config's
+    acfg = GA.AssociationConfig(k_assoc=config.k_assoc, k_sinkhorn=config.k_sinkhorn, epsilon=config.ot_epsilon,
+                                tau_a=config.ot_tau_a, tau_b=config.ot_tau_b, eps_mass=config.eps_mass,
+                                h_tile=config.H_TILE, r_stencil_tiles_xy=config.R_STENCIL_TILES_XY,
+                                r_stencil_tiles_z=config.R_STENCIL_TILES_Z, scan_seq=0,
+                                recency_decay_lambda=config.RECENCY_DECAY_LAMBDA)
+    c_as = GA.assoc_config_struct(acfg)
+    N, K = config.n_feat + config.n_surfel, int(config.k_assoc)
+    ucfg = GPM.PrimitiveMapUpdateConfig(k_insert_tile=config.k_insert_tile, H_TILE=config.H_TILE,
+                                        RECENCY_DECAY_LAMBDA=config.RECENCY_DECAY_LAMBDA, eps_lift=config.eps_lift,
+                                        eps_mass=config.eps_mass, eps_psd=config.eps_psd)
+    c_up = GPM.update_config_struct(ucfg)
+    dev = f"cuda:{config.device}"
+    import torch
+    bufs = getattr(ctx, "_live_bufs", None)
+    if bufs is None:
+        bufs = ctx._live_bufs = (torch.empty((cap, 3), dtype=torch.float64, device=dev),
+                                 torch.empty(cap, dtype=torch.float64, device=dev),
+                                 torch.empty(cap, dtype=torch.float64, device=dev))
+    a = L.GcsLiveArgs()
+    a.h_tile = float(config.H_TILE)
+    a.r_active_xy, a.r_active_z = int(config.R_ACTIVE_TILES_XY), int(config.R_ACTIVE_TILES_Z)
+    a.r_stencil_xy, a.r_stencil_z = int(config.R_STENCIL_TILES_XY), int(config.R_STENCIL_TILES_Z)
+    a.n_active_expected, a.n_stencil_expected = int(config.N_ACTIVE_TILES), int(config.N_STENCIL_TILES)
+    a.recency_lambda, a.recency_min_scale = float(config.RECENCY_DECAY_LAMBDA), float(config.RECENCY_MIN_SCALE)
+    a.m_tile_view = int(config.M_TILE_VIEW)
+    a.eps_lift, a.eps_mass = float(config.eps_lift), float(config.eps_mass)
+    a.assoc_cfg, a.update_cfg = C.addressof(c_as), C.addressof(c_up)
+    a.points_dev, a.timestamps_dev, a.weights_dev = (x.data_ptr() for x in bufs)
+    a.n_points = cap
+    vpe = L.GcsVpeOutputs()
+    a.vpe_out = C.addressof(vpe)
+    st = dict(key=key, scfg=scfg, pool=int(config.N_STENCIL_TILES) * int(config.M_TILE_VIEW), acfg=acfg, c_as=c_as, c_up=c_up, args=a, vpe=vpe, bufs=bufs, N=N, K=K,
+              lo=L.GcsLiveOutputs())
+    ctx._live_chain = st
+    return st
+
+
+def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, imu_stamps, imu_gyro, imu_accel,
+                             odom_pose, odom_cov_se3, scan_start_time, scan_end_time, dt_sec, t_last_scan, t_scan, Q,
+                             config: "PipelineConfig", odom_twist, odom_twist_cov, scan_seq, L_ext, h_ext, update_map):
+    """_process_scan_primitive through gcs_live_scan: begin -> surfels -> recency -> view -> association ->
+    visual pose evidence -> finish -> step 12b in one C call on the context's stream (pipeline.py:316-1591;
+    :778-1011, 1232-1492), with this scan's fresh result tensors handed in.  Step 12b is left running:
+    live["finish"]() waits for it and fills the MapUpdateCert and the map's bookkeeping."""
+    import torch
+    from . import association as GA, primitive_map as GPM
+    from .association import AtlasMapView
+    from .surfels import _extractor_for, create_empty_measurement_batch, surfel_cert
+    st = _live_chain_state(ctx, config)
+    lib, a, lo = ctx.lib, st["args"], st["lo"]
+    # the operator contexts (looked up per scan: another caller may have replaced a cached one)
+    ex = _extractor_for(st["scfg"], ctx.cfg.n_points_cap, config.device)
+    asc = GA._associator_for(st["N"], st["pool"], st["K"], config.device)
+    a.surfels, a.assoc = ex.h.value, asc.h.value
+    dev = f"cuda:{config.device}"
+    inp, keep = ctx._scan_inputs(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time,
+                                 scan_end_time, dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan,
+                                 t_scan=t_scan, odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
+                                 odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a)
+    bo = L.GcsScanBeginOutputs()
+    bo.points_dev, bo.timestamps_dev, bo.weights_dev = a.points_dev, a.timestamps_dev, a.weights_dev
+    in_ref = C.byref(inp)
+    if not update_map:
+        # a hypothesis k > 0 works on device copies of the tiles it touches (see _process_scan_primitive):
+        # the copy needs the tiles around the predicted pose, so the begin runs first here
+        ctx._chk(lib.gcs_scan_begin(ctx.h, in_ref, C.byref(bo)), "gcs_scan_begin")
+        in_ref = None
+        centre = np.array(bo.pose_pred[:3])
+        ids = GPM.ma_hex_stencil_tile_ids(centre, config.H_TILE, config.R_ACTIVE_TILES_XY, config.R_ACTIVE_TILES_Z) + \
+            GPM.ma_hex_stencil_tile_ids(centre, config.H_TILE, config.R_STENCIL_TILES_XY, config.R_STENCIL_TILES_Z)
+        primitive_map = ctx._scratch_map = primitive_map.working_copy(ids, into=getattr(ctx, "_scratch_map", None))
+    am = primitive_map
+    # this scan's result tensors (the results keep them): the batch, the view, the association
+    batch = create_empty_measurement_batch(config.n_feat, config.n_surfel, dev)
+    s0, ns_ = batch.n_feat, config.n_surfel
+    sl = slice(s0, s0 + ns_)
+    into = dict(Lambdas=batch.Lambdas[sl], thetas=batch.thetas[sl], etas=batch.etas[sl], weights=batch.weights[sl],
+                timestamps=batch.timestamps[sl], colors=batch.colors[sl],
+                valid_mask=batch.valid_mask[sl].view(torch.uint8), source_indices=batch.source_indices[sl])
+    o_sf, _ = ex.outputs(False, into)
+    n_st, k_v = int(config.N_STENCIL_TILES), int(config.M_TILE_VIEW)
+    vt, v = GPM.view_buffers(am.n_lobes, n_st, k_v, dev)
+    view_tids = torch.empty(n_st, dtype=torch.int64, device=dev)
+    N, K = st["N"], st["K"]
+    a_out, ao = GA.assoc_outputs(N, K, dev)
+    m = a.meas
+    m.Lambdas, m.thetas, m.etas, m.weights = (batch.Lambdas.data_ptr(), batch.thetas.data_ptr(),
+                                              batch.etas.data_ptr(), batch.weights.data_ptr())
+    m.valid_mask, m.n_total, m.n_lobes, m.n_valid = batch.valid_mask.data_ptr(), N, int(batch.etas.shape[1]), 0
+    ids, slots, free, written = am.directory()
+    a.map = am.h.value
+    a.n_tiles, a.tile_ids, a.tile_slots = len(ids), ids.ctypes.data, slots.ctypes.data
+    a.n_free, a.free_slots, a.slot_written = len(free), free.ctypes.data, written.ctypes.data
+    a.next_global_id = int(am.next_global_id)
+    a.scan_seq = st["c_as"].scan_seq = int(scan_seq)
+    a.timestamp = float(scan_end_time)
+    a.surfel_out = C.addressof(o_sf)
+    a.lidar_sources_dev = batch.sources[sl].data_ptr()
+    a.batch_colors, a.batch_sources = batch.colors.data_ptr(), batch.sources.data_ptr()
+    a.view, a.view_tile_ids_dev, a.assoc_out = C.addressof(v), view_tids.data_ptr(), C.addressof(ao)
+    out = L.GcsScanOutputs()
+    rc = lib.gcs_live_scan(ctx.h, in_ref, C.byref(bo), C.byref(a), C.byref(lo), C.byref(out))
+    del keep
+    if lo.n_created:  # tiles created (and cleared where written) before the device failed or ran
+        am.adopt_created(lo.created_ids[:lo.n_created], lo.created_slots[:lo.n_created])
+    ctx._chk(rc, "gcs_live_scan")
+    try:
+        return out, _live_chain_results(ctx, am, st, lo, o_sf, bo, out, batch, vt, view_tids, a_out, ao, scan_seq,
+                                        scan_end_time, config)
+    except BaseException:
+        lib.gcs_live_collect(ctx.h, C.byref(lo))  # step 12b is queued: drain it before the error propagates
+        raise
+
+
+def _live_chain_results(ctx, am, st, lo, o_sf, bo, out, batch, vt, view_tids, a_out, ao, scan_seq, scan_end_time,
+                        config):
+    """The live dict of _process_scan_primitive from gcs_live_scan's outputs (host work that overlaps
+    the queued step 12b); live["finish"]() collects step 12b."""
+    from . import association as GA, primitive_map as GPM
+    from .association import AtlasMapView
+    from .surfels import surfel_cert
+    lib = ctx.lib
+    N, k_v = st["N"], int(config.M_TILE_VIEW)
+    nv = int(o_sf.n_valid)
+    batch.n_lidar_valid = nv
+    c_surf, _ = surfel_cert(nv, config.n_surfel, CHART_ID)
+    down, infl_tr, nrec = (float(x) for x in lo.recency_stats)
+    infl = GPM.PrimitiveMapRecencyInflateStats(down / max(nrec, 1.0), infl_tr, down)
+    c_infl = CertBundle.create_exact(chart_id=CHART_ID, anchor_id="primitive_map_recency_inflate")
+    view = AtlasMapView(tile_ids=view_tids, m_tile_view=k_v, **vt)
+    res = GA.association_result(a_out, ao)
+    c_assoc, _ = GA.association_cert(ao, st["acfg"], N, CHART_ID)
+    vis, c_vis, _ = GA.visual_pose_result(st["vpe"], config.eps_lift, CHART_ID)
+    z_t = np.array(out.z_t[:])
+    z_lin_pose = np.array(bo.z_lin_pose[:])
+    active = [int(x) for x in lo.active_ids[:lo.n_active]]
+    cand = res.candidate_stats
+    record = dict(active=active, scan_seq=int(scan_seq), t=float(scan_end_time), z_t=z_t, batch=batch,
+                  association=res)
+    live = dict(map=am, batch=batch, map_update_cert=None, certs=[c_surf, c_infl, c_assoc, c_vis], association=res,
+                view=view, z_lin_pose=z_lin_pose, map_record=record, stage_ms={})
+
+    def finish():
+        if live["map_update_cert"] is not None:
+            return live["map_update_cert"]
+        ctx._chk(lib.gcs_live_collect(ctx.h, C.byref(lo)), "gcs_live_collect")
+        u = lo.update
+        am.total_count += int(u.insert_count_total) - int(u.evicted_count) - int(u.merged_count)
+        am.next_global_id = int(lo.next_global_id)
+        for k, tid in enumerate(active):
+            am.counts[tid] = int(lo.counts[k])
+        act = set(active)
+        held = am.tiles
+        inactive = [int(x) for x in held if int(x) not in act]
+        hits = len([x for x in active if x in held])
+        live["map_update_cert"] = MapUpdateCert(
+            n_active_tiles=len(active), tile_ids_active=list(active), n_inactive_tiles=len(inactive),
+            staleness_inflation_strength=infl.staleness_inflation_strength,
+            staleness_cov_inflation_trace=infl.staleness_cov_inflation_trace,
+            stale_precision_downscale_total=infl.stale_precision_downscale_total, tile_ids_inactive=inactive,
+            tile_cache_hits=hits, tile_cache_misses=len(act) - hits, candidate_tiles_per_meas_mean=cand[0],
+            candidate_primitives_per_meas_mean=cand[1], candidate_primitives_per_meas_p95=cand[2],
+            insert_count_total=int(u.insert_count_total), insert_mass_total=float(u.insert_mass_total),
+            insert_mass_p95=float(u.insert_mass_p95), evicted_count=int(u.evicted_count),
+            evicted_mass_total=float(u.evicted_mass_total), fused_count=int(u.fused_count),
+            fused_mass_total=float(u.fused_mass_total), merged_count=int(u.merged_count))
+        return live["map_update_cert"]
+
+    live["finish"] = finish
+    return live
+
+
 def primitive_map_follow(primitive_map, record: dict, config: "PipelineConfig"):
     """Apply a lead hypothesis' map update (its recency inflation and step 12b, pipeline.py:800-809,
     1232-1492, from `result.map_record`) to another copy of the node's map: every copy stays bitwise the
@@ -464,6 +674,21 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
                        dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
                        odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
                        odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a)
+    try:
+        res = _scan_result(ctx, out, live, belief_prev, scan_seq, scan_end_time, dt_sec, rec.shape[0])
+    finally:
+        if live is not None and "finish" in live:  # the one-call path's step 12b (queued): its cert
+            live["map_update_cert"] = live["finish"]()
+    if live is not None:
+        res.map_update_cert = live["map_update_cert"]
+    if map_bins is None:
+        ctx.close()
+        res.map_bins_updated = None
+    return res
+
+
+def _scan_result(ctx, out, live, belief_prev, scan_seq, scan_end_time, dt_sec, n_raw):
+    """ScanPipelineResult of a scan's outputs (and the live path's dict)."""
     X, stamp, z, Lm, h = ctx.get_belief()
     cert = np.array(out.cert[:])
     certs = _certs_from_vector(cert, np.array(out.imu_odom_certs[:]), CHART_ID, belief_prev.anchor_id,
@@ -493,7 +718,7 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
         res.stage_ms = live["stage_ms"]
         res.map_bins_updated = None
     # the reference's per-scan MinimalScanTape (pipeline.py:1504-1570)
-    res.diagnostics_tape = tape_from_result(res, scan_seq, scan_end_time, dt_sec, rec.shape[0], res.L_evidence)
+    res.diagnostics_tape = tape_from_result(res, scan_seq, scan_end_time, dt_sec, n_raw, res.L_evidence)
     sm = getattr(res, "stage_ms", None) or {}
     if sm:  # the reference's live-path timing fields (diagnostics.py:58-67)
         t = res.diagnostics_tape
@@ -503,9 +728,6 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
         t.t_map_branch_ms = sum(sm.get(k, 0.0) for k in ("surfel_extraction_ms", "map_view_ms", "association_ms"))
         t.t_map_update_ms = sm.get("map_update_ms", 0.0)
         t.t_total_ms = sum(sm.values())
-    if map_bins is None:
-        ctx.close()
-        res.map_bins_updated = None
     return res
 
 

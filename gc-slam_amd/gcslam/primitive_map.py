@@ -78,6 +78,7 @@ class AtlasMap:
         # storage slots that may hold data; every other slot is as gcs_pmap_create cleared it, so a tile
         # created there needs no clear (a kernel and a stream sync per new tile on the live path)
         self._written = set()
+        self._dir_ver, self._dir = 0, None  # directory arrays for gcs_live_scan, rebuilt on change
 
     # ------------------------------------------------------------------ plumbing
     def close(self):
@@ -125,7 +126,36 @@ class AtlasMap:
         self._written.add(idx)
         self.tiles[tid] = idx
         self.counts[tid] = 0
+        self._dir_ver += 1
         return idx
+
+    def directory(self):
+        """The tile directory as gcs_live_args takes it: (ids int64, slots int32, free slots int32 in the
+        order index() takes them, written uint8 per slot); cached until the directory changes."""
+        if self._dir is None or self._dir[0] != self._dir_ver:
+            n = len(self.tiles)
+            ids = np.fromiter(self.tiles.keys(), np.int64, n)
+            slots = np.fromiter(self.tiles.values(), np.int32, n)
+            free = np.array(self._free, np.int32)
+            written = np.zeros(max(self.max_tiles, 1), np.uint8)
+            if self._written:
+                written[np.fromiter(self._written, np.int64, len(self._written))] = 1
+            self._dir = (self._dir_ver, ids, slots, free, written)
+        return self._dir[1:]
+
+    def adopt_created(self, ids, slots):
+        """Record tiles gcs_live_scan created (index(create=True) of each, in order: the slots are the
+        first free ones, cleared on the device where written)."""
+        for tid, idx in zip(ids, slots):
+            tid, idx = int(tid), int(idx)
+            if self._free[0] != idx:
+                raise RuntimeError(f"live scan created tile {tid} in slot {idx}, expected {self._free[0]}")
+            self._free.pop(0)
+            self._written.add(idx)
+            self.tiles[tid] = idx
+            self.counts[tid] = 0
+        if len(ids):
+            self._dir_ver += 1
 
     def _width(self, f):
         return {"Lambdas": (3, 3), "thetas": (3,), "etas": (self.n_lobes, 3), "colors": (3,), "rgb_cam_accum": (3,),
@@ -167,6 +197,7 @@ class AtlasMap:
             into = AtlasMap(self.m_tile, max_tiles=max(len(ids), 1), n_lobes=self.n_lobes, max_merge=self.max_merge,
                             device=self.device)
         into.tiles, into.counts, into._free = {}, {}, list(range(into.max_tiles))
+        into._dir_ver += 1
         present = [t for t in ids if t in self.tiles]
         dst = np.array([into._free.pop(0) for _ in present], dtype=np.int32)
         src = np.array([self.tiles[t] for t in present], dtype=np.int32)
@@ -280,24 +311,16 @@ def _tiles_arg(idx):
 
 
 # ---------------------------------------------------------------------- operators
-def extract_atlas_map_view(atlas_map: AtlasMap, tile_ids: List[int], m_tile_view: int,
-                           eps_lift: float = GC_EPS_LIFT, eps_mass: float = GC_EPS_MASS) -> AtlasMapView:
-    """:356-450: per listed tile the top m_tile_view slots by weight (stable on -score; a missing tile
-    is viewed as empty), stitched in tile order, with means, covariances, resultant directions and
-    kappas (:474-498)."""
-    if int(m_tile_view) <= 0:
-        raise ValueError(f"extract_atlas_map_view: m_tile_view must be > 0, got {m_tile_view}")
+def view_buffers(n_lobes: int, n: int, k: int, dev: str):
+    """Fresh AtlasMapView arrays of n tiles x k entries (one device allocation carved into the twelve
+    outputs, 8-byte aligned segments; valid_mask written as 0/1 bytes straight into a bool view) and
+    the gcs_pmap_view struct naming them."""
     torch = _torch()
-    dev = f"cuda:{atlas_map.device}"
-    n, k = len(tile_ids), int(m_tile_view)
     R = n * k
-    # one device allocation carved into the twelve outputs (8-byte aligned segments); valid_mask is
-    # written as 0/1 bytes straight into a bool view
-    nl = atlas_map.n_lobes
     spec = (("positions", torch.float64, (R, 3)), ("covariances", torch.float64, (R, 3, 3)),
             ("directions", torch.float64, (R, 3)), ("kappas", torch.float64, (R,)), ("weights", torch.float64, (R,)),
             ("primitive_ids", torch.int64, (R,)), ("last_supported_scan_seq", torch.int64, (R,)),
-            ("etas", torch.float64, (R, nl, 3)), ("colors", torch.float64, (R, 3)),
+            ("etas", torch.float64, (R, n_lobes, 3)), ("colors", torch.float64, (R, 3)),
             ("candidate_tile_ids", torch.int64, (R,)), ("candidate_slots", torch.int32, (R,)),
             ("valid_mask", torch.bool, (R,)))
     sizes = [int(np.prod(shape)) * (8 if dt in (torch.float64, torch.int64) else 4 if dt == torch.int32 else 1)
@@ -310,6 +333,20 @@ def extract_atlas_map_view(atlas_map: AtlasMap, tile_ids: List[int], m_tile_view
     v = L.GcsPmapView()
     for name, x in t.items():
         setattr(v, name, x.data_ptr() if R else None)
+    return t, v
+
+
+def extract_atlas_map_view(atlas_map: AtlasMap, tile_ids: List[int], m_tile_view: int,
+                           eps_lift: float = GC_EPS_LIFT, eps_mass: float = GC_EPS_MASS) -> AtlasMapView:
+    """:356-450: per listed tile the top m_tile_view slots by weight (stable on -score; a missing tile
+    is viewed as empty), stitched in tile order, with means, covariances, resultant directions and
+    kappas (:474-498)."""
+    if int(m_tile_view) <= 0:
+        raise ValueError(f"extract_atlas_map_view: m_tile_view must be > 0, got {m_tile_view}")
+    torch = _torch()
+    dev = f"cuda:{atlas_map.device}"
+    n, k = len(tile_ids), int(m_tile_view)
+    t, v = view_buffers(atlas_map.n_lobes, n, k, dev)
     idx, ip = _tiles_arg([atlas_map.index(tid, create=False) for tid in tile_ids])
     tids = np.ascontiguousarray(np.asarray(tile_ids, dtype=np.int64))
     atlas_map._stream()
@@ -569,6 +606,15 @@ class PrimitiveMapUpdateConfig:
     eps_psd: float = GC_EPS_PSD
 
 
+def update_config_struct(cfg: PrimitiveMapUpdateConfig):
+    """gcs_pmap_update_config of a PrimitiveMapUpdateConfig."""
+    return L.GcsPmapUpdateConfig(int(cfg.k_insert_tile), int(cfg.block_size), int(cfg.k_merge_pairs_tile),
+                                 int(cfg.primitive_merge_max_tile_size), float(cfg.H_TILE),
+                                 float(cfg.RECENCY_DECAY_LAMBDA), float(cfg.primitive_cull_weight_threshold),
+                                 float(cfg.primitive_forgetting_factor), float(cfg.primitive_merge_threshold),
+                                 float(cfg.eps_lift), float(cfg.eps_mass), float(cfg.eps_psd))
+
+
 def primitive_map_update(atlas_map: AtlasMap, measurement_batch, assoc_result, z_t, active_tile_ids: List[int],
                          timestamp: float, scan_seq: int, config: Optional[PrimitiveMapUpdateConfig] = None) -> dict:
     """pipeline.py:1244-1447 (step 12b) on the GPU: the scan's MeasurementBatch (body frame) fused into
@@ -601,11 +647,7 @@ def primitive_map_update_call(atlas_map: AtlasMap, measurement_batch, assoc_resu
                         "candidate_tile_ids", "candidate_slots", "row_masses"), keep):
         setattr(inp, name, t.data_ptr() if t is not None else None)
     inp.n_total, inp.n_lobes, inp.k_assoc = N, int(keep[2].reshape(N, -1, 3).shape[1]), K
-    c = L.GcsPmapUpdateConfig(int(cfg.k_insert_tile), int(cfg.block_size), int(cfg.k_merge_pairs_tile),
-                              int(cfg.primitive_merge_max_tile_size), float(cfg.H_TILE), float(cfg.RECENCY_DECAY_LAMBDA),
-                              float(cfg.primitive_cull_weight_threshold), float(cfg.primitive_forgetting_factor),
-                              float(cfg.primitive_merge_threshold), float(cfg.eps_lift), float(cfg.eps_mass),
-                              float(cfg.eps_psd))
+    c = update_config_struct(cfg)
     idx, ip = _tiles_arg([atlas_map.index(t, create=True) for t in active_tile_ids])
     tids = np.ascontiguousarray(np.asarray(active_tile_ids, dtype=np.int64))
     z = np.ascontiguousarray(np.asarray(z_t, dtype=np.float64).reshape(6))

@@ -160,6 +160,23 @@ class SurfelExtractor:
         n = int(p.shape[0])
         if t.shape[0] != n or w.shape[0] != n:
             raise ValueError("points, timestamps and weights must have the same length")
+        o, out = self.outputs(want_intermediates, into)
+        self._chk(self.lib.gcs_surfel_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
+                  "gcs_surfel_ctx_set_stream")
+        self._chk(self.lib.gcs_extract_lidar_surfels(self.h, C.c_void_p(p.data_ptr()), C.c_void_p(t.data_ptr()),
+                                                     C.c_void_p(w.data_ptr()), n, C.byref(o)),
+                  "gcs_extract_lidar_surfels")
+        out["n_valid"] = int(o.n_valid)
+        out["center"] = np.array(o.center[:])
+        out["cert"] = np.array(o.cert[:])
+        return out
+
+    def outputs(self, want_intermediates=False, into=None):
+        """(gcs_surfel_outputs, tensors) of one call: the extractor's arrays, with the batch-slice
+        tensors of `into` (extract's argument) in place of its own."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        cf = self.config
         key = bool(want_intermediates)
         if key not in self._bufs:  # allocated once per extractor (and per intermediates flag)
             ns = cf.n_surfel
@@ -185,15 +202,7 @@ class SurfelExtractor:
                 setattr(o2, k, v.data_ptr())
                 out[k] = v
             o = o2
-        self._chk(self.lib.gcs_surfel_ctx_set_stream(self.h, C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)),
-                  "gcs_surfel_ctx_set_stream")
-        self._chk(self.lib.gcs_extract_lidar_surfels(self.h, C.c_void_p(p.data_ptr()), C.c_void_p(t.data_ptr()),
-                                                     C.c_void_p(w.data_ptr()), n, C.byref(o)),
-                  "gcs_extract_lidar_surfels")
-        out["n_valid"] = int(o.n_valid)
-        out["center"] = np.array(o.center[:])
-        out["cert"] = np.array(o.cert[:])
-        return out
+        return o, out
 
 
 _extractors = {}
@@ -251,11 +260,16 @@ def extract_lidar_surfels(points, timestamps, weights, config: Optional[SurfelEx
         batch.timestamps[s:e] = r["timestamps"][:nv]
         batch.colors[s:e] = r["colors"][:nv]
     batch.n_lidar_valid = nv
-    support = float(nv) / float(max(config.n_surfel, 1))
+    cert, effect = surfel_cert(nv, config.n_surfel, chart_id, anchor_id)
+    del torch
+    return batch, cert, effect
+
+
+def surfel_cert(nv: int, n_surfel: int, chart_id: str = CHART_ID, anchor_id: str = "surfel_extraction"):
+    """(CertBundle, ExpectedEffect) of a surfel extraction with nv valid surfels (:420-431)."""
+    support = float(nv) / float(max(n_surfel, 1))
     cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id,
                                     triggers=["ma_hex3d_binning", "plane_fit_batched", "wishart_regularization"],
                                     support=SupportCert(ess_total=float(nv), support_frac=support),
                                     influence=InfluenceCert.identity())
-    effect = ExpectedEffect(objective_name="surfel_extraction", predicted=float(nv), realized=float(nv))
-    del torch
-    return batch, cert, effect
+    return cert, ExpectedEffect(objective_name="surfel_extraction", predicted=float(nv), realized=float(nv))

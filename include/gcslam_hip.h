@@ -47,9 +47,11 @@
 extern "C" {
 #endif
 
-/* 3: GCS_ASSOC_CERT_LEN 18 -> 21 (gcs_assoc_outputs grew), the scan mirror's sequence / checksum
+/* 4: the one-call live path (gcs_live_scan / gcs_live_collect, gcs_live_args / gcs_live_outputs) and
+ * gcs_ma_hex_stencil.
+ * 3: GCS_ASSOC_CERT_LEN 18 -> 21 (gcs_assoc_outputs grew), the scan mirror's sequence / checksum
  * (gcs_ctx_mirror_stats) and the state checksums (gcs_debug_state_checksums) */
-#define GCS_ABI_VERSION 3
+#define GCS_ABI_VERSION 4
 #define GCS_D_Z 22
 #define GCS_SCAN_FIELDS 26   /* ScanBinStats, field-major: N, s_dir[3], S_dir_scatter[9], p_bar[3], Sigma_p[9], kappa */
 #define GCS_MAP_FIELDS 26    /* MapBinStats: S_dir[3], S_dir_scatter[9], N_dir, N_pos, sum_p[3], sum_ppT[9] */
@@ -812,6 +814,87 @@ int gcs_pmap_map_update(gcs_pmap* pm, const int32_t* tiles, const int64_t* tile_
                         double timestamp, int64_t scan_seq, int64_t* next_global_id,
                         const gcs_pmap_update_config* cfg, const gcs_pmap_update_inputs* in,
                         gcs_pmap_update_stats* stats, int32_t* counts);
+
+/* ---------------------------------------------------------------- the live primitive path in one call */
+/* process_scan_single_hypothesis's live primitive path (pipeline.py:316-1591: the map branch :778-926,
+ * visual pose evidence :980-1010, step 12b :1232-1492) as one stream-ordered chain on the context's
+ * stream:
+ *   gcs_scan_begin -> the active and stencil MA-hex tiles around the predicted position
+ *   (tiling.py:167-209) -> surfels of the deskewed points -> recency inflation of the active tiles the
+ *   map holds -> the atlas view over the stencil (a tile the map lacks is viewed as empty) -> OT
+ *   association -> visual pose evidence at z_lin_pose -> gcs_scan_finish (trigger / ESS sums of the
+ *   surfel, recency, association and visual certificates, pipeline.py:1049-1056,1211) -> step 12b at
+ *   z_t over the active tiles (new tiles take free storage slots in order, AtlasMap.index).
+ * The same kernels on the same arguments as the per-operator entry points, bit for bit, with host
+ * waits only where a host value feeds the next launch (begin, the surfel count, the pose evidence).
+ * Step 12b is left queued: gcs_live_collect waits for it and returns its statistics; no other call
+ * on the context or the map may come between the two.  Contexts: the surfel / association / map
+ * contexts are switched to the gcs_ctx's stream.  Stencils of at most 64 tiles. */
+#define GCS_LIVE_MAX_TILES 64
+typedef struct {
+  gcs_surfel_ctx* surfels;
+  gcs_assoc_ctx* assoc;
+  gcs_pmap* map;
+  /* the AtlasMap's tile directory (primitive_map.py:182-227; AtlasMap.tiles / _free / _written) */
+  int32_t n_tiles;
+  const int64_t* tile_ids;       /* [n_tiles] MA-hex ids held */
+  const int32_t* tile_slots;     /* [n_tiles] their storage indices */
+  int32_t n_free;
+  const int32_t* free_slots;     /* [n_free] free storage indices, in the order new tiles take them */
+  const uint8_t* slot_written;   /* [max_tiles] 1: the slot may hold data (a new tile there is cleared) */
+  int64_t next_global_id;
+  /* tiling and operator parameters (PipelineConfig) */
+  double h_tile;
+  int32_t r_active_xy, r_active_z, r_stencil_xy, r_stencil_z;
+  int32_t n_active_expected, n_stencil_expected;  /* N_ACTIVE_TILES / N_STENCIL_TILES (checked) */
+  int64_t scan_seq;
+  double recency_lambda, recency_min_scale;
+  int32_t m_tile_view;
+  double eps_lift, eps_mass;
+  const gcs_assoc_config* assoc_cfg;          /* scan_seq / recency_decay_lambda as above */
+  const gcs_pmap_update_config* update_cfg;
+  double timestamp;                            /* scan_end_time: step 12b's timestamp */
+  /* the scan's device buffers (caller-allocated; the surfels read points / timestamps / weights) */
+  const double* points_dev;
+  const double* timestamps_dev;
+  const double* weights_dev;
+  int32_t n_points;
+  gcs_surfel_outputs* surfel_out;  /* device pointers: the batch's LiDAR slice + the extractor arrays */
+  int32_t* lidar_sources_dev;      /* the batch's sources from the LiDAR slice start: 1 on valid rows */
+  gcs_assoc_meas meas;             /* the whole MeasurementBatch; n_valid is set from the surfel count */
+  const double* batch_colors;      /* n_total x 3 (step 12b) */
+  const int32_t* batch_sources;    /* n_total (step 12b) */
+  gcs_pmap_view* view;             /* n_stencil x m_tile_view rows */
+  int64_t* view_tile_ids_dev;      /* n_stencil: AtlasMapView.tile_ids */
+  gcs_assoc_outputs* assoc_out;
+  gcs_vpe_outputs* vpe_out;
+} gcs_live_args;
+
+typedef struct {
+  int32_t n_active, n_stencil;
+  int64_t active_ids[GCS_LIVE_MAX_TILES], stencil_ids[GCS_LIVE_MAX_TILES];
+  int32_t active_slots[GCS_LIVE_MAX_TILES];        /* storage index of each active tile (step 12b) */
+  int32_t n_present_active;                        /* active tiles the map held before the scan */
+  int32_t n_created;                               /* new tiles, in creation order */
+  int64_t created_ids[GCS_LIVE_MAX_TILES];
+  int32_t created_slots[GCS_LIVE_MAX_TILES];
+  double recency_stats[3];                         /* gcs_pmap_recency_inflate's stats */
+  double trigger_sum, ess_sum;                     /* the gcs_lidar_evidence handed to the finish */
+  /* after gcs_live_collect */
+  gcs_pmap_update_stats update;
+  int32_t counts[GCS_LIVE_MAX_TILES];              /* valid counts of the active tiles */
+  int64_t next_global_id;
+} gcs_live_outputs;
+
+/* in: the scan (NULL: gcs_scan_begin already ran on ctx and begin holds its outputs).  begin, out:
+ * as gcs_scan_begin / gcs_scan_finish. */
+int gcs_live_scan(gcs_ctx* ctx, const gcs_scan_inputs* in, gcs_scan_begin_outputs* begin, const gcs_live_args* a,
+                  gcs_live_outputs* lo, gcs_scan_outputs* out);
+int gcs_live_collect(gcs_ctx* ctx, gcs_live_outputs* lo);
+/* the MA-hex tile ids of tiling.py:167-209 (ma_hex_stencil_tile_ids) around center; returns the count
+ * (or GCS_ERR_ARG when it exceeds cap) */
+int gcs_ma_hex_stencil(const double* center3, double h_tile, int32_t radius_xy, int32_t radius_z, int64_t* out,
+                       int32_t cap);
 
 #ifdef __cplusplus
 }

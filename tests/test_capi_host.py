@@ -22,7 +22,7 @@ def test_library_exports_every_header_symbol(lib):
     assert declared == set(L.SYMBOLS), declared ^ set(L.SYMBOLS)
     for name in declared:
         assert hasattr(lib, name), name
-    assert lib.gcs_abi_version() == 3
+    assert lib.gcs_abi_version() == 4
 
 
 @pytest.mark.parametrize("n", [3, 6, 22])
@@ -257,3 +257,19 @@ def test_missing_library_fails_loudly(monkeypatch, tmp_path):
     monkeypatch.setattr(L, "_lib", None)
     with pytest.raises(RuntimeError):
         L.load()
+
+
+def test_ma_hex_stencil_matches_tiling():
+    """gcs_ma_hex_stencil (gcs_live_scan's tiles, host code) against ma_hex_stencil_tile_ids (tiling.py:167-209)."""
+    from gcslam import _lib as L
+    from gcslam.primitive_map import ma_hex_stencil_tile_ids
+    lib = L.load()
+    rng = np.random.default_rng(3)
+    out = np.zeros(L.LIVE_MAX_TILES, np.int64)
+    for _ in range(200):
+        c = np.ascontiguousarray(rng.normal(0, 50, 3))
+        h = float(rng.choice([0.5, 1.0, 2.0, 3.7]))
+        rxy, rz = int(rng.integers(0, 3)), int(rng.integers(0, 2))
+        n = lib.gcs_ma_hex_stencil(L.dptr(c), h, rxy, rz, out.ctypes.data_as(L.c_int64_p), len(out))
+        assert n >= 0
+        assert out[:n].tolist() == ma_hex_stencil_tile_ids(c, h, rxy, rz)
