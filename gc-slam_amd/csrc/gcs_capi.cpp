@@ -88,6 +88,7 @@ struct gcs_ctx {
   gcs_scan_outputs* live_out = nullptr;
   bool live_pending = false;
   gcs_pmap* live_map = nullptr;  // gcs_live_scan: the map whose step 12b gcs_live_collect has to read
+  bool begin_mirror = true;      // gcs_scan_begin reads the point fold's mirror (GCSLAM_BEGIN_MIRROR=0: copies)
   uint32_t *d_keys = nullptr, *d_slots = nullptr, *d_sorted = nullptr;
   int* d_nearest = nullptr;
   // per-bin bucketing
@@ -509,7 +510,8 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true) {
 // p0_out / w_out / t_out, no soft assign
 int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, const double* w, int n_raw, double t0,
                  double t1, const double* xi, double* p0_out, double* w_out, double* wb_out, bool fold_later = false,
-                 bool xyz_f64 = false, double* iz_out = nullptr, bool deskew_only = false, double* t_out = nullptr) {
+                 bool xyz_f64 = false, double* iz_out = nullptr, bool deskew_only = false, double* t_out = nullptr,
+                 bool to_host = false) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
   if (point_step < (xyz_f64 ? 24 : 12)) return fail(c, GCS_ERR_ARG, "point_step too small for x, y, z");
   StageEv ev = stage_ev(c, ST_POINTS);
@@ -580,8 +582,15 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   }
   c->pts_blocks = points_blocks(c->cap, scale);
   c->pts_fold_pending = scale && fold_later;
+  MirrorArgs mir{};
+  if (to_host && !c->pts_fold_pending) {  // the fold hands the scalars and error words to the host mirror
+    mir.mirror = c->d_scalars_mirror;
+    mir.err = c->d_err;
+    mir.seq = ++c->mirror_seq;
+    mir.torn = c->mirror_torn;
+  }
   HIPCHK(c, launch_points(a, scale, c->d_part_pts, c->pts_blocks, !c->pts_fold_pending, s, ev.e0, ev.e1,
-                          c->legacy_points));
+                          c->legacy_points, mir));
   return GCS_OK;
 }
 
@@ -1174,6 +1183,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (const char* g = getenv("GCSLAM_GATE")) c->gate_on = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_DEVICE_PREINT")) c->device_preint = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_PT_CLEAR")) c->pt_clear = atoi(g) != 0;
+  if (const char* g = getenv("GCSLAM_BEGIN_MIRROR")) c->begin_mirror = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_BUDGET_BLOCKS")) c->budget_max = std::max(1, std::min(1024, atoi(g)));
   if (bad(hipHostMalloc(&c->h_preint_out, 16 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent)))
     return GCS_ERR_HIP;
@@ -2245,13 +2255,18 @@ int gcs_scan_begin(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs
   double* ww = out->weights_dev ? out->weights_dev : c->d_live_w;
   int rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
                         in->scan_start_time, in->scan_end_time, st.xi, p0, ww, nullptr,
-                        /*fold_later=*/false, in->xyz_format == 1, nullptr, /*deskew_only=*/true, tt);
+                        /*fold_later=*/false, in->xyz_format == 1, nullptr, /*deskew_only=*/true, tt,
+                        /*to_host=*/c->begin_mirror);
   if (rc) return rc;
   st.Ts = clk::now();
   if ((rc = scan_imu_odom(c, in, st, c->live_out))) return rc;
-  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->begin_mirror) {  // the point fold's stamped mirror: its scalars and error words, no D2H copies
+    if ((rc = wait_mirror(c))) return rc;
+  } else {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if ((rc = pull_scalars(c))) return rc;
+  }
   finish_preint(c, st);
-  if ((rc = pull_scalars(c))) return rc;
   st.T2 = clk::now();
   if ((rc = scan_point_certs(c, in, st))) return rc;
   // the map branch's linearisation point: z_lin = solve(PSD(L_pred + L_imu_odom), h_pred + h_imu_odom),
@@ -2349,12 +2364,15 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
     return fail(c, GCS_ERR_ARG, "gcs_live_scan: bad tile directory");
   if (c->live_map) return fail(c, GCS_ERR_STATE, "gcs_live_scan: the previous scan's step 12b was not collected");
   memset(lo, 0, sizeof(*lo));
+  const clk::time_point t_in = clk::now();
+  auto mark = [&](int k) { lo->phase_us[k] = 1e3 * ms_between(t_in, clk::now()); };
   int rc;
   if (in) {
     if ((rc = gcs_scan_begin(c, in, bo))) return rc;
   } else if (!c->live_pending) {
     return fail(c, GCS_ERR_STATE, "gcs_live_scan without gcs_scan_begin");
   }
+  mark(0);
   // the scan's tiles around the predicted position (pipeline.py:783-797)
   const int na = ma_hex_stencil(bo->pose_pred, a->h_tile, a->r_active_xy, a->r_active_z, lo->active_ids,
                                 GCS_LIVE_MAX_TILES);
@@ -2405,12 +2423,14 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   if (live::surfel_bind_stream(sf, s)) return sub_fail(c, GCS_ERR_HIP, "surfels", gcs_surfel_last_error(sf));
   if (live::assoc_bind_stream(as, s)) return sub_fail(c, GCS_ERR_HIP, "association", gcs_assoc_last_error(as));
   if (live::pmap_bind_stream(pm, s)) return sub_fail(c, GCS_ERR_HIP, "map", gcs_pmap_last_error(pm));
+  if (a->zero_dev && a->zero_bytes > 0) HIPCHK(c, hipMemsetAsync(a->zero_dev, 0, (size_t)a->zero_bytes, s));
   // surfels of the deskewed points (pipeline.py:778-782); the batch's LiDAR count feeds the launches
   gcs_surfel_outputs* so = a->surfel_out;
   if ((rc = live::surfel_launch(sf, a->points_dev, a->timestamps_dev, a->weights_dev, a->n_points, so)))
     return sub_fail(c, rc, "gcs_extract_lidar_surfels", gcs_surfel_last_error(sf));
   HIPCHK(c, hipStreamSynchronize(s));
   live::surfel_collect(sf, so);
+  mark(1);
   const int nv = so->n_valid;
   if (nv > 0) HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)a->lidar_sources_dev, 1, (size_t)nv, s));
   // recency inflation of the active tiles the map holds, then the view over the stencil (:800-815)
@@ -2451,6 +2471,7 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
     return sub_fail(c, rc, "gcs_visual_pose_evidence", gcs_assoc_last_error(as));
   live::assoc_collect(as, ao);
   live::pmap_recency_collect(pm, nrec, lo->recency_stats);
+  mark(2);
   // the finish: trigger magnitudes of the surfel (identity influence), recency (exact), association
   // (mass_epsilon_ratio unless exact) and visual (lift_strength = eps_lift unless exact) certs; ESS of
   // the surfel (n_valid), association and visual certs; no mismatch terms (pipeline.py:1049-1056,1211)
@@ -2468,6 +2489,7 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   lo->trigger_sum = ev.trigger_sum;
   lo->ess_sum = ev.ess_sum;
   if ((rc = gcs_scan_finish(c, &ev, out))) return rc;
+  mark(3);
   // step 12b at z_t over the active tiles (:1232-1492); new tiles on written slots start cleared
   for (int k = 0; k < ncl; ++k)
     if ((rc = live::pmap_clear_tile_launch(pm, clear[k]))) return sub_fail(c, rc, "gcs_pmap_clear_tile", gcs_pmap_last_error(pm));
@@ -2491,6 +2513,7 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
     return sub_fail(c, rc, "gcs_pmap_map_update", gcs_pmap_last_error(pm));
   lo->next_global_id = a->next_global_id;
   c->live_map = pm;
+  mark(4);
   return GCS_OK;
 }
 
@@ -2499,8 +2522,10 @@ int gcs_live_collect(gcs_ctx* c, gcs_live_outputs* lo) {
   if (!c->live_map) return fail(c, GCS_ERR_STATE, "gcs_live_collect without gcs_live_scan");
   gcs_pmap* pm = c->live_map;
   c->live_map = nullptr;
+  const clk::time_point t_in = clk::now();
   if (int rc = live::pmap_update_collect(pm, &lo->next_global_id, &lo->update, lo->counts))
     return sub_fail(c, rc, "gcs_pmap_map_update", gcs_pmap_last_error(pm));
+  lo->phase_us[5] = 1e3 * ms_between(t_in, clk::now());
   return GCS_OK;
 }
 

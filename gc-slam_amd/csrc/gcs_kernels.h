@@ -189,9 +189,10 @@ hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint3
 // the hypothesis all-reduce's stage-out (gcs_combine_allreduce): the device sum to a host buffer of n
 // words + [n] sequence number (*dseq + 1, stored back to *dseq) + [n + 1] checksum (mirror_word_hash)
 hipError_t launch_payload_out(const double* src, double* host, int n, uint64_t* dseq, hipStream_t s);
-// legacy: the round-3 k_points (scale mode) instead of k_points_lean
+// legacy: the round-3 k_points (scale mode) instead of k_points_lean; mir: the fold's host mirror
+// (gcs_scan_begin: the scalars and error words without a D2H copy)
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
-                         hipEvent_t e0, hipEvent_t e1, bool legacy = false);
+                         hipEvent_t e0, hipEvent_t e1, bool legacy = false, const MirrorArgs& mir = MirrorArgs{});
 int scan_tiles(int n_bins);
 hipError_t launch_bucketing(const BucketArgs& b, int n, hipStream_t s, hipEvent_t e0, hipEvent_t e1);
 // Bins per k_bins_scale tile: 64 (four lanes per bin); GCSLAM_BIN_TILE=32 selects 32-bin tiles with

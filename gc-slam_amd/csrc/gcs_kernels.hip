@@ -2705,7 +2705,7 @@ int points_blocks(long cap, bool scale) {
 }
 
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,
-                         hipEvent_t e0, hipEvent_t e1, bool legacy) {
+                         hipEvent_t e0, hipEvent_t e1, bool legacy, const MirrorArgs& mir) {
   // without the fold (it rides in k_bins_scale's block 0) the stage ends with k_points itself
   hipEvent_t ek = fold ? nullptr : e1;
   // legacy: the round-3 point kernel (one wave per SIMD; GCSLAM_POINTS=legacy / GCS_DEBUG_POINT_KERNEL), for A/B
@@ -2745,7 +2745,7 @@ hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials,
   } else {
     hipExtLaunchKernelGGL((k_points<false, 1, 1>), dim3(nblk), dim3(kBlock), 0, s, e0, ek, 0, a, partials);
   }
-  if (fold) GCS_FINAL(5, 16u, FIN_POINTS, nblk, s, e1, partials, a.scalars);
+  if (fold) GCS_FINAL_M(5, 16u, FIN_POINTS, nblk, s, e1, partials, a.scalars, mir);
   return hipGetLastError();
 }
 

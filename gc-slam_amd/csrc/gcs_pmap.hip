@@ -1397,16 +1397,16 @@ __global__ __launch_bounds__(kPmRed) void k_pm_recency(PmStore st, const int32_t
   double dn = 0.0, inf = 0.0, nv = 0.0;
   for (int q = blockIdx.y * kPmRed + threadIdx.x; q < st.M; q += gridDim.y * kPmRed) {
     const size_t i = sidx(st, ti, q);
-    const bool v = st.valid[i] != 0;
+    // an empty slot's factor is 1 and its terms are zero (x * 1.0 == x): only valid slots are read
+    // and written (the map is sparse: the reference sizes' 50,000-slot tiles hold a few thousand)
+    if (st.valid[i] == 0) continue;
     const long long dt = max(0ll, seq - st.lsup[i]);
-    double d = fmin(fmax(exp(-lam * (double)dt), min_scale), 1.0);
-    d = v ? d : 1.0;
+    const double d = fmin(fmax(exp(-lam * (double)dt), min_scale), 1.0);
     for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = st.lam[9 * i + c] * d;
     for (int c = 0; c < 3; ++c) st.th[3 * i + c] = st.th[3 * i + c] * d;
-    const double vf = v ? 1.0 : 0.0;
-    nv += vf;
-    dn += (1.0 - d) * vf;
-    inf += ((1.0 / d) - 1.0) * vf;
+    nv += 1.0;
+    dn += (1.0 - d) * 1.0;
+    inf += ((1.0 / d) - 1.0) * 1.0;
   }
   dn = block_sum_d<kPmRed>(dn, lds);
   inf = block_sum_d<kPmRed>(inf, lds);

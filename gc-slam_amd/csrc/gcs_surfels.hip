@@ -24,6 +24,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -424,6 +425,107 @@ __global__ __launch_bounds__(kSfThreads) void k_sf_write(const double* __restric
   if (o.source_indices) o.source_indices[s] = s;
 }
 
+// One workgroup for clouds of up to kSortMax points: the stable sort of k_sf_keys' (key, point index)
+// pairs by key and k_sf_bounds' run bounds, in LDS (replaces the rocPRIM radix sort's kernels and
+// k_sf_bounds: the same permutation, as both sorts are stable on the key with the points in index
+// order).  Each key is packed above its 13-bit index and sorted by LSD passes of 7-bit digits: per
+// wave a contiguous 512-entry segment in 64-lane steps, equal digits found by ballots, ranks from
+// per-(wave, digit) offsets (digit-major, then wave order).
+constexpr int kSortThreads = 1024;
+constexpr int kSortMax = 8192;
+constexpr int kSortIdxBits = 13;
+constexpr int kSortDigitBits = 7;
+constexpr int kSortDigits = 1 << kSortDigitBits;
+constexpr int kSortWaves = kSortThreads / 64;
+constexpr int kSortSeg = kSortMax / kSortWaves;  // entries per wave
+static_assert(kSortMax == 1 << kSortIdxBits, "index field");
+static_assert(kSortThreads <= 1024 && kSortSeg % 64 == 0, "sort shape");
+
+__global__ __launch_bounds__(kSortThreads) void k_sf_sort_lds(const uint32_t* __restrict__ keys, int n, SfParams a,
+                                                               int end_bit, uint32_t* __restrict__ vals_s,
+                                                               int32_t* __restrict__ run) {
+  __shared__ uint32_t s_buf[2][kSortMax];
+  __shared__ uint32_t s_off[kSortWaves][kSortDigits];
+  __shared__ uint32_t s_tot[kSortDigits], s_dsum[kSortDigits / 64];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  for (int i = t; i < n; i += kSortThreads) s_buf[0][i] = (keys[i] << kSortIdxBits) | (uint32_t)i;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  const int npass = (end_bit + kSortDigitBits - 1) / kSortDigitBits;
+  for (int pass = 0; pass < npass; ++pass) {
+    const uint32_t* src = s_buf[pass & 1];
+    uint32_t* dst = s_buf[(pass + 1) & 1];
+    const int shift = kSortIdxBits + pass * kSortDigitBits;
+    for (int q = t; q < kSortWaves * kSortDigits; q += kSortThreads) (&s_off[0][0])[q] = 0u;
+    __syncthreads();
+    // per (wave, digit) counts
+    for (int j = 0; j < kSortSeg; j += 64) {
+      const int e = wid * kSortSeg + j + lane;
+      const bool ok = e < n;
+      const uint32_t d = ok ? (src[e] >> shift) & (kSortDigits - 1) : 0u;
+      unsigned long long peers = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < kSortDigitBits; ++b) {
+        const unsigned long long m = __ballot(ok && ((d >> b) & 1u));
+        peers &= ((d >> b) & 1u) ? m : ~m;
+      }
+      if (ok && (peers & lt) == 0ull) s_off[wid][d] += (uint32_t)__popcll(peers);  // the group's first lane
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    // offsets: digit-major, then wave order (thread d owns digit d)
+    if (t < kSortDigits) {
+      uint32_t tot = 0;
+      for (int w = 0; w < kSortWaves; ++w) tot += s_off[w][t];
+      uint32_t x = tot;  // inclusive scan over the digits: per wave, then the waves in order
+      for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off, 64);
+        if (lane >= off) x += y;
+      }
+      if (lane == 63) s_dsum[wid] = x;
+      s_tot[t] = x - tot;  // exclusive within the wave
+    }
+    __syncthreads();
+    if (t < kSortDigits) {
+      uint32_t r = s_tot[t];
+      for (int w = 0; w < wid; ++w) r += s_dsum[w];
+      for (int w = 0; w < kSortWaves; ++w) {
+        const uint32_t c = s_off[w][t];
+        s_off[w][t] = r;
+        r += c;
+      }
+    }
+    __syncthreads();
+    // scatter: each wave's entries in order, equal digits by lane order
+    for (int j = 0; j < kSortSeg; j += 64) {
+      const int e = wid * kSortSeg + j + lane;
+      const bool ok = e < n;
+      const uint32_t x = ok ? src[e] : 0u;
+      const uint32_t d = (x >> shift) & (kSortDigits - 1);
+      unsigned long long peers = __ballot(ok);
+#pragma unroll
+      for (int b = 0; b < kSortDigitBits; ++b) {
+        const unsigned long long m = __ballot(ok && ((d >> b) & 1u));
+        peers &= ((d >> b) & 1u) ? m : ~m;
+      }
+      if (ok) dst[s_off[wid][d] + (uint32_t)__popcll(peers & lt)] = x;
+      __builtin_amdgcn_wave_barrier();
+      if (ok && (peers & lt) == 0ull) s_off[wid][d] += (uint32_t)__popcll(peers);
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+  }
+  // sorted point indices and k_sf_bounds' runs (run[] zeroed by k_sf_partials)
+  const uint32_t* srt = s_buf[npass & 1];
+  for (int q = t; q < n; q += kSortThreads) {
+    const uint32_t x = srt[q];
+    vals_s[q] = x & (kSortMax - 1);
+    const uint32_t k = x >> kSortIdxBits;
+    if (k >= (uint32_t)a.n_cells) continue;  // masked points sort last
+    if (q == 0 || (srt[q - 1] >> kSortIdxBits) != k) run[2 * k] = q;
+    if (q == n - 1 || (srt[q + 1] >> kSortIdxBits) != k) run[2 * k + 1] = q + 1;
+  }
+}
+
 }  // namespace
 }  // namespace gcs
 
@@ -440,6 +542,7 @@ struct gcs_surfel_ctx {
   void* d_temp = nullptr;
   size_t temp_bytes = 0;
   unsigned end_bit = 1;
+  bool lds_sort = true;  // k_sf_keys_sort for clouds of <= kSortMax points (GCSLAM_SF_LDS_SORT=0: rocPRIM)
   int32_t *d_bucket = nullptr, *d_count = nullptr, *d_run = nullptr, *d_slot_cell = nullptr;
   double *d_mom = nullptr, *d_fit = nullptr;
   uint8_t* d_valid = nullptr;
@@ -529,6 +632,7 @@ int gcs_surfel_ctx_create(const gcs_surfel_config* cfg, gcs_surfel_ctx** out) {
   a.eig_min = cfg->eig_min;
   a.eps_lift = cfg->eps_lift;
   while ((1UL << c->end_bit) <= (unsigned long)n_cells) ++c->end_bit;  // keys 0..n_cells
+  if (const char* e = getenv("GCSLAM_SF_LDS_SORT")) c->lds_sort = atoi(e) != 0;
   auto bad = [&](hipError_t e) { return e != hipSuccess; };
   const size_t N = (size_t)cfg->max_points;
   if (bad(hipSetDevice(cfg->device)) || bad(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) ||
@@ -593,7 +697,10 @@ int surfel_launch(gcs_surfel_ctx* c, const double* points, const double* timesta
                      2 * a.n_cells);
   hipLaunchKernelGGL(k_sf_keys, dim3(nblk), dim3(kSfThreads), 0, s, points, n, (const double*)c->d_partials, nblk, a,
                      c->d_keys, c->d_vals, c->d_scal, c->h_scal_dev);
-  if (n > 0) {
+  if (n > 0 && c->lds_sort && n <= kSortMax && c->end_bit + kSortIdxBits <= 32) {
+    hipLaunchKernelGGL(k_sf_sort_lds, dim3(1), dim3(kSortThreads), 0, s, (const uint32_t*)c->d_keys, n, a,
+                       (int)c->end_bit, c->d_vals_s, c->d_run);
+  } else if (n > 0) {
     size_t tb = c->temp_bytes;
     SFCHK(c, rocprim::radix_sort_pairs(c->d_temp, tb, c->d_keys, c->d_keys_s, c->d_vals, c->d_vals_s, (unsigned)n, 0u,
                                        c->end_bit, s));

@@ -217,7 +217,8 @@ class GcsLiveArgs(C.Structure):
                 ("weights_dev", C.c_void_p), ("n_points", C.c_int32), ("surfel_out", C.c_void_p),
                 ("lidar_sources_dev", C.c_void_p), ("meas", GcsAssocMeas), ("batch_colors", C.c_void_p),
                 ("batch_sources", C.c_void_p), ("view", C.c_void_p), ("view_tile_ids_dev", C.c_void_p),
-                ("assoc_out", C.c_void_p), ("vpe_out", C.c_void_p)]
+                ("assoc_out", C.c_void_p), ("vpe_out", C.c_void_p), ("zero_dev", C.c_void_p),
+                ("zero_bytes", C.c_int64)]
 
 
 class GcsLiveOutputs(C.Structure):
@@ -226,6 +227,7 @@ class GcsLiveOutputs(C.Structure):
                 ("n_present_active", C.c_int32), ("n_created", C.c_int32),
                 ("created_ids", C.c_int64 * LIVE_MAX_TILES), ("created_slots", C.c_int32 * LIVE_MAX_TILES),
                 ("recency_stats", C.c_double * 3), ("trigger_sum", C.c_double), ("ess_sum", C.c_double),
+                ("phase_us", C.c_double * 6),
                 ("update", GcsPmapUpdateStats), ("counts", C.c_int32 * LIVE_MAX_TILES), ("next_global_id", C.c_int64)]
 
 

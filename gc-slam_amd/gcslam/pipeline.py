@@ -16,6 +16,7 @@ Two LiDAR evidence paths behind the one signature:
 from __future__ import annotations
 
 import json
+import os
 import time
 import warnings
 from dataclasses import dataclass, field
@@ -265,6 +266,17 @@ def _to_device(a, dtype, device, role):
     return out
 
 
+# GCSLAM_LIVE_STAMPS=1: host wall-clock stamps of each call's phases (tools/live_bench.py prints their
+# mean differences); off, _stamp is a no-op
+LIVE_STAMPS, LIVE_PHASES = [], []
+_STAMPS_ON = os.environ.get("GCSLAM_LIVE_STAMPS", "0") == "1"
+
+
+def _stamp(name):
+    if _STAMPS_ON:
+        LIVE_STAMPS.append((name, time.perf_counter()))
+
+
 def _as_device_scan(raw_points, raw_timestamps, raw_weights, device):
     """The node's parsed cloud (backend_node.py:1675-1690) as device inputs: xyz as the float32
     PointCloud2 record the point kernel reads (x, y, z, pad), t and w f64."""
@@ -272,6 +284,33 @@ def _as_device_scan(raw_points, raw_timestamps, raw_weights, device):
     if isinstance(raw_points, torch.Tensor) and raw_points.dim() == 2 and raw_points.shape[1] == 4 \
             and raw_points.dtype == torch.float32:
         rec = raw_points.to(f"cuda:{device}").contiguous()
+    elif not any(isinstance(x, torch.Tensor) for x in (raw_points, raw_timestamps, raw_weights)):
+        # host arrays: the three through one pinned staging buffer and one H2D copy
+        p = np.asarray(raw_points, np.float64).reshape(-1, 3)
+        n = p.shape[0]
+        ts, ws = np.asarray(raw_timestamps).reshape(-1), np.asarray(raw_weights).reshape(-1)
+        if ts.shape[0] != n or ws.shape[0] != n:
+            raise ValueError("points, timestamps and weights must have the same length")
+        key = ("scan", device, n)
+        ent = _pinned.get(key)
+        if ent is None:
+            hb = torch.empty(32 * n, dtype=torch.uint8).pin_memory()
+            hn = hb.numpy()
+            ent = _pinned[key] = [hb, None, (hn[:16 * n].view(np.float32).reshape(n, 4),
+                                             hn[16 * n:24 * n].view(np.float64), hn[24 * n:].view(np.float64))]
+        hb, ev, (hr, ht, hw) = ent
+        if ev is not None:
+            ev.synchronize()  # the previous copy out of the staging buffer
+        hr[:, :3] = p  # PointCloud2 x,y,z are float32 (backend_node.py:377-468)
+        hr[:, 3] = 0.0
+        ht[...] = ts
+        hw[...] = ws
+        d = hb.to(f"cuda:{device}", non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(device))
+        ent[1] = ev
+        return d[:16 * n].view(torch.float32).view(n, 4), d[16 * n:24 * n].view(torch.float64), \
+            d[24 * n:].view(torch.float64)
     else:
         p = np.asarray(raw_points.cpu() if isinstance(raw_points, torch.Tensor) else raw_points,
                        np.float64).reshape(-1, 3)
@@ -472,10 +511,53 @@ def _live_chain_state(ctx: HypothesisContext, config: "PipelineConfig"):
     a.n_points = cap
     vpe = L.GcsVpeOutputs()
     a.vpe_out = C.addressof(vpe)
-    st = dict(key=key, scfg=scfg, pool=int(config.N_STENCIL_TILES) * int(config.M_TILE_VIEW), acfg=acfg, c_as=c_as, c_up=c_up, args=a, vpe=vpe, bufs=bufs, N=N, K=K,
+    st = dict(key=key, scfg=scfg, pool=int(config.N_STENCIL_TILES) * int(config.M_TILE_VIEW), acfg=acfg,
+              arena=_live_arena(config, N, K), c_as=c_as, c_up=c_up, args=a, vpe=vpe, bufs=bufs, N=N, K=K,
               lo=L.GcsLiveOutputs())
     ctx._live_chain = st
     return st
+
+
+def _live_arena(config: "PipelineConfig", N: int, K: int) -> dict:
+    """Layout of one scan's result arrays in one device allocation (8-byte aligned segments): the
+    MeasurementBatch (create_empty_measurement_batch's arrays; zeroed by gcs_live_scan on its stream),
+    the AtlasMapView (view_buffers' arrays), the view's tile ids and the PrimitiveAssociationResult.
+    Pointers go to the C call before it; the tensors are views made after it, beside step 12b."""
+    import torch
+    from .surfels import GC_VMF_N_LOBES
+    nt, R = config.n_feat + config.n_surfel, int(config.N_STENCIL_TILES) * int(config.M_TILE_VIEW)
+    f64, i64, i32, b8 = torch.float64, torch.int64, torch.int32, torch.bool
+    size = {f64: 8, i64: 8, i32: 4, b8: 1}
+    parts = {
+        "batch": (("Lambdas", f64, (nt, 3, 3)), ("thetas", f64, (nt, 3)), ("etas", f64, (nt, GC_VMF_N_LOBES, 3)),
+                  ("weights", f64, (nt,)), ("timestamps", f64, (nt,)), ("colors", f64, (nt, 3)),
+                  ("sources", i32, (nt,)), ("source_indices", i32, (nt,)), ("valid_mask", b8, (nt,))),
+        "view": (("positions", f64, (R, 3)), ("covariances", f64, (R, 3, 3)), ("directions", f64, (R, 3)),
+                 ("kappas", f64, (R,)), ("weights", f64, (R,)), ("primitive_ids", i64, (R,)),
+                 ("last_supported_scan_seq", i64, (R,)), ("etas", f64, (R, GC_VMF_N_LOBES, 3)),
+                 ("colors", f64, (R, 3)), ("candidate_tile_ids", i64, (R,)), ("candidate_slots", i32, (R,)),
+                 ("valid_mask", b8, (R,)), ("tile_ids", i64, (int(config.N_STENCIL_TILES),))),
+        "assoc": (("responsibilities", f64, (N, K)), ("candidate_pool_indices", i32, (N, K)),
+                  ("candidate_tile_ids", i64, (N, K)), ("candidate_slots", i64, (N, K)), ("row_masses", f64, (N,)),
+                  ("cost_matrix", f64, (N, K))),
+    }
+    lay, off = {}, 0
+    for part, spec in parts.items():
+        rows = []
+        for name, dt, shape in spec:
+            z = int(np.prod(shape)) * size[dt]
+            rows.append((name, dt, shape, off, z))
+            off += (z + 7) // 8 * 8
+        lay[part] = rows
+        if part == "batch":
+            lay["zero_bytes"] = off
+    lay["total"] = off
+    lay["off"] = {(p, r[0]): r[3] for p in parts for r in lay[p]}
+    return lay
+
+
+def _arena_tensors(buf, rows) -> dict:
+    return {name: buf[off:off + z].view(dt).view(shape) for name, dt, shape, off, z in rows}
 
 
 def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, imu_stamps, imu_gyro, imu_accel,
@@ -488,7 +570,7 @@ def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, i
     import torch
     from . import association as GA, primitive_map as GPM
     from .association import AtlasMapView
-    from .surfels import _extractor_for, create_empty_measurement_batch, surfel_cert
+    from .surfels import GC_VMF_N_LOBES, MeasurementBatch, _extractor_for
     st = _live_chain_state(ctx, config)
     lib, a, lo = ctx.lib, st["args"], st["lo"]
     # the operator contexts (looked up per scan: another caller may have replaced a cached one)
@@ -513,23 +595,32 @@ def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, i
             GPM.ma_hex_stencil_tile_ids(centre, config.H_TILE, config.R_STENCIL_TILES_XY, config.R_STENCIL_TILES_Z)
         primitive_map = ctx._scratch_map = primitive_map.working_copy(ids, into=getattr(ctx, "_scratch_map", None))
     am = primitive_map
-    # this scan's result tensors (the results keep them): the batch, the view, the association
-    batch = create_empty_measurement_batch(config.n_feat, config.n_surfel, dev)
-    s0, ns_ = batch.n_feat, config.n_surfel
-    sl = slice(s0, s0 + ns_)
-    into = dict(Lambdas=batch.Lambdas[sl], thetas=batch.thetas[sl], etas=batch.etas[sl], weights=batch.weights[sl],
-                timestamps=batch.timestamps[sl], colors=batch.colors[sl],
-                valid_mask=batch.valid_mask[sl].view(torch.uint8), source_indices=batch.source_indices[sl])
-    o_sf, _ = ex.outputs(False, into)
-    n_st, k_v = int(config.N_STENCIL_TILES), int(config.M_TILE_VIEW)
-    vt, v = GPM.view_buffers(am.n_lobes, n_st, k_v, dev)
-    view_tids = torch.empty(n_st, dtype=torch.int64, device=dev)
-    N, K = st["N"], st["K"]
-    a_out, ao = GA.assoc_outputs(N, K, dev)
+    if am.n_lobes != GC_VMF_N_LOBES:
+        raise ValueError(f"live path: the map's n_lobes {am.n_lobes} differs from the batch's {GC_VMF_N_LOBES}")
+    # this scan's result arrays (the results keep them) in one allocation: pointers now, tensors after
+    lay = st["arena"]
+    buf = torch.empty(lay["total"], dtype=torch.uint8, device=dev)
+    base, off = buf.data_ptr(), lay["off"]
+    nt, s0 = st["N"], config.n_feat
+    row = {"Lambdas": 72, "thetas": 24, "etas": 24 * GC_VMF_N_LOBES, "weights": 8, "timestamps": 8,
+           "colors": 24, "valid_mask": 1, "source_indices": 4}
+    o_sf = L.GcsSurfelOutputs()
+    o_ex, _ = ex.outputs(False)
+    for k in ("positions", "covariances", "normals", "kappas", "cell_ids"):
+        setattr(o_sf, k, getattr(o_ex, k))
+    for k, rb in row.items():  # the batch's LiDAR slice
+        setattr(o_sf, k, base + off[("batch", k)] + s0 * rb)
+    o_v = L.GcsPmapView()
+    for name, *_ in lay["view"][:-1]:
+        setattr(o_v, name, base + off[("view", name)])
+    ao = L.GcsAssocOutputs()
+    for name, *_ in lay["assoc"]:
+        setattr(ao, name, base + off[("assoc", name)])
     m = a.meas
-    m.Lambdas, m.thetas, m.etas, m.weights = (batch.Lambdas.data_ptr(), batch.thetas.data_ptr(),
-                                              batch.etas.data_ptr(), batch.weights.data_ptr())
-    m.valid_mask, m.n_total, m.n_lobes, m.n_valid = batch.valid_mask.data_ptr(), N, int(batch.etas.shape[1]), 0
+    m.Lambdas, m.thetas, m.etas, m.weights, m.valid_mask = (base + off[("batch", k)] for k in (
+        "Lambdas", "thetas", "etas", "weights", "valid_mask"))
+    m.n_total, m.n_lobes, m.n_valid = nt, GC_VMF_N_LOBES, 0
+    a.zero_dev, a.zero_bytes = base, lay["zero_bytes"]
     ids, slots, free, written = am.directory()
     a.map = am.h.value
     a.n_tiles, a.tile_ids, a.tile_slots = len(ids), ids.ctypes.data, slots.ctypes.data
@@ -538,18 +629,28 @@ def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, i
     a.scan_seq = st["c_as"].scan_seq = int(scan_seq)
     a.timestamp = float(scan_end_time)
     a.surfel_out = C.addressof(o_sf)
-    a.lidar_sources_dev = batch.sources[sl].data_ptr()
-    a.batch_colors, a.batch_sources = batch.colors.data_ptr(), batch.sources.data_ptr()
-    a.view, a.view_tile_ids_dev, a.assoc_out = C.addressof(v), view_tids.data_ptr(), C.addressof(ao)
+    a.lidar_sources_dev = base + off[("batch", "sources")] + 4 * s0
+    a.batch_colors, a.batch_sources = base + off[("batch", "colors")], base + off[("batch", "sources")]
+    a.view, a.view_tile_ids_dev, a.assoc_out = C.addressof(o_v), base + off[("view", "tile_ids")], C.addressof(ao)
     out = L.GcsScanOutputs()
+    _stamp("args")
     rc = lib.gcs_live_scan(ctx.h, in_ref, C.byref(bo), C.byref(a), C.byref(lo), C.byref(out))
+    _stamp("live_scan")
     del keep
     if lo.n_created:  # tiles created (and cleared where written) before the device failed or ran
         am.adopt_created(lo.created_ids[:lo.n_created], lo.created_slots[:lo.n_created])
     ctx._chk(rc, "gcs_live_scan")
     try:
-        return out, _live_chain_results(ctx, am, st, lo, o_sf, bo, out, batch, vt, view_tids, a_out, ao, scan_seq,
-                                        scan_end_time, config)
+        bt = _arena_tensors(buf, lay["batch"])
+        batch = MeasurementBatch(**bt, n_feat=config.n_feat, n_surfel=config.n_surfel, n_camera_valid=0,
+                                 n_lidar_valid=0)
+        vt = _arena_tensors(buf, lay["view"])
+        view_tids = vt.pop("tile_ids")
+        a_out = _arena_tensors(buf, lay["assoc"])
+        r = _live_chain_results(ctx, am, st, lo, o_sf, bo, out, batch, vt, view_tids, a_out, ao, scan_seq,
+                                scan_end_time, config)
+        _stamp("live_results")
+        return out, r
     except BaseException:
         lib.gcs_live_collect(ctx.h, C.byref(lo))  # step 12b is queued: drain it before the error propagates
         raise
@@ -587,6 +688,8 @@ def _live_chain_results(ctx, am, st, lo, o_sf, bo, out, batch, vt, view_tids, a_
         if live["map_update_cert"] is not None:
             return live["map_update_cert"]
         ctx._chk(lib.gcs_live_collect(ctx.h, C.byref(lo)), "gcs_live_collect")
+        if _STAMPS_ON:
+            LIVE_PHASES.append(list(lo.phase_us))
         u = lo.update
         am.total_count += int(u.insert_count_total) - int(u.evicted_count) - int(u.merged_count)
         am.next_global_id = int(lo.next_global_id)
@@ -660,9 +763,11 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
         if config.camera_batch_policy == "warn" and not _camera_warned:
             warnings.warn("camera_batch ignored: the bin-path backend has no visual evidence (DESIGN.md section 9)")
             _camera_warned = True
+    _stamp("enter")
     ctx = map_bins if map_bins is not None else config.make_context()
     ctx.set_belief(belief_prev.X_anchor, belief_prev.stamp_sec, belief_prev.z_lin, belief_prev.L, belief_prev.h)
     rec, t, w = _as_device_scan(raw_points, raw_timestamps, raw_weights, config.device)
+    _stamp("h2d")
     live = None
     if primitive_map is not None:
         out, live = _process_scan_primitive(ctx, primitive_map, belief_prev, rec, t, w, imu_stamps, imu_gyro,
@@ -676,11 +781,13 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
                        odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a)
     try:
         res = _scan_result(ctx, out, live, belief_prev, scan_seq, scan_end_time, dt_sec, rec.shape[0])
+        _stamp("result")
     finally:
         if live is not None and "finish" in live:  # the one-call path's step 12b (queued): its cert
             live["map_update_cert"] = live["finish"]()
     if live is not None:
         res.map_update_cert = live["map_update_cert"]
+    _stamp("collect")
     if map_bins is None:
         ctx.close()
         res.map_bins_updated = None

@@ -868,6 +868,8 @@ typedef struct {
   int64_t* view_tile_ids_dev;      /* n_stencil: AtlasMapView.tile_ids */
   gcs_assoc_outputs* assoc_out;
   gcs_vpe_outputs* vpe_out;
+  void* zero_dev;                  /* zeroed on the stream before the surfels (the batch's arrays), may be NULL */
+  int64_t zero_bytes;
 } gcs_live_args;
 
 typedef struct {
@@ -880,6 +882,8 @@ typedef struct {
   int32_t created_slots[GCS_LIVE_MAX_TILES];
   double recency_stats[3];                         /* gcs_pmap_recency_inflate's stats */
   double trigger_sum, ess_sum;                     /* the gcs_lidar_evidence handed to the finish */
+  double phase_us[6];   /* host clock since the call's entry: begin returned, surfel count read, pose evidence
+                           read, finish returned, step 12b queued; gcs_live_collect: [5] its wait */
   /* after gcs_live_collect */
   gcs_pmap_update_stats update;
   int32_t counts[GCS_LIVE_MAX_TILES];              /* valid counts of the active tiles */

@@ -139,3 +139,29 @@ def test_sentinels_empty_input_and_capacity():
             assert torch.equal(a[k], b[k])      # bitwise reproducible
     finally:
         ex.close()
+
+
+@pytest.mark.parametrize("n_points,scan,cells", [(8192, 0, (32, 32, 8)), (8192, 5, (32, 32, 8)), (5000, 2, (16, 16, 8)),
+                                                 (300, 1, (64, 64, 16))])
+def test_lds_key_sort_equals_radix_sort(monkeypatch, n_points, scan, cells):
+    """k_sf_keys_sort (one workgroup: the centre fold, the cell keys, the stable (key, index) sort in LDS and
+    the run bounds; clouds <= 8,192 points) against the rocPRIM radix-sort path (GCSLAM_SF_LDS_SORT=0): every
+    output and intermediate bitwise equal, parse sentinels included."""
+    sc = synthetic.make_scan(8192, scan)
+    pts = np.ascontiguousarray(sc["points"][:n_points], np.float64).copy()
+    pts[::97] = 1e6                      # masked points: the key past the last cell, sorted last
+    t, w = sc["timestamps"][:n_points], sc["weights"][:n_points]
+    cfg = SurfelExtractionConfig(hex3d_num_cells_1=cells[0], hex3d_num_cells_2=cells[1], hex3d_num_cells_z=cells[2])
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GCSLAM_SF_LDS_SORT", flag)
+        ex = SurfelExtractor(cfg, max_points=8192)
+        try:
+            r = ex.extract(pts, t, w, want_intermediates=True)
+            outs.append({k: (v.cpu().numpy().copy() if torch.is_tensor(v) else np.asarray(v)) for k, v in r.items()})
+        finally:
+            ex.close()
+    a, b = outs
+    assert a["n_valid"] == b["n_valid"] and a["n_valid"] > 0
+    for k in a:
+        assert a[k].tobytes() == b[k].tobytes(), k

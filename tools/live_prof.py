@@ -29,7 +29,7 @@ def main():
     cfg = PipelineConfig(K_HYP=1, N_POINTS_CAP=N, B_BINS=48, soft_assign_mode="dense",
                          lidar_origin_base=tuple(synthetic.LIDAR_ORIGIN), max_raw_points=N, device=0)
     ctx = cfg.make_context()
-    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, max_tiles=256, device=0)
+    am = gpm.create_empty_atlas_map(m_tile=cfg.primitive_map_max_size, max_tiles=512, device=0)
     Q = process_noise_state_to_Q(datasheet_process_noise_state())
     warm = 10
     scans = [synthetic.make_scan(N, k) for k in range(warm + calls)]
