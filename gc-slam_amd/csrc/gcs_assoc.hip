@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -810,7 +811,8 @@ __device__ __forceinline__ double pow_fast(double x, double y) {
 }
 
 template <int KM, int RPT>
-__global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p, AsWork w, AsOut o, int n_valid_host) {
+__global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p, AsWork w, AsOut o, int n_valid_host,
+                                                            const int32_t* n_valid_dev) {
 #pragma clang fp contract(off)
   __shared__ double s_red[16 * (KM + 8)];
 #if GCS_SH_ONEBAR
@@ -823,7 +825,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int N = p.n, K = p.k;
   if (blockIdx.x == 0) SH_STAMP(0);
-  const bool empty = n_valid_host == 0 || *w.mvalid == 0u;
+  const bool empty = (n_valid_dev ? *n_valid_dev : n_valid_host) == 0 || *w.mvalid == 0u;
   if (empty) {  // :272-287 -- zeros, exact cert (workgroup 0)
     if (blockIdx.x != 0) return;
     for (int q = t; q < N * K; q += kShThreads) {
@@ -1238,6 +1240,7 @@ struct VpeIn {
   const double *Lambdas, *thetas, *etas;
   const uint8_t* valid;
   int n, n_lobes, n_meas;
+  const int32_t* n_meas_dev;  // (may be null) the count on the device, read instead of n_meas
   const double *vpos, *vdir, *vkap;
   const uint8_t* vvalid;
   int m_view;
@@ -1247,13 +1250,80 @@ struct VpeIn {
   double R[9], t[3], eps_lift, eps_mass;
 };
 
-__global__ __launch_bounds__(kVpeThreads) void k_as_vpe(VpeIn in, double* out) {
+// the 25 sums of row i (L_t 9, h_t 3, cost_t, S 9, cost_r, row mass, 1), in the kernel's operation order
+constexpr int kVpeRowVals = 25;
+__device__ __forceinline__ void vpe_row(const VpeIn& in, int i, double* o) {
+#pragma clang fp contract(off)
+  double p[3];
+  solve3_pivot(in.Lambdas + 9 * (size_t)i, in.eps_lift, in.thetas + 3 * (size_t)i, p);
+  double es[3] = {0.0, 0.0, 0.0};
+  for (int b = 0; b < in.n_lobes; ++b)
+    for (int c = 0; c < 3; ++c) {
+      const double e = in.etas[(size_t)3 * in.n_lobes * i + 3 * b + c];
+      es[c] = b == 0 ? e : es[c] + e;
+    }
+  const double kap = sqrt((es[0] * es[0] + es[1] * es[1]) + es[2] * es[2]);
+  const double u[3] = {es[0] / (kap + in.eps_mass), es[1] / (kap + in.eps_mass), es[2] / (kap + in.eps_mass)};
+  double Lr[9];
+  for (int c = 0; c < 9; ++c) Lr[c] = in.Lambdas[9 * (size_t)i + c] + ((c % 4) == 0 ? in.eps_lift : 0.0);
+  double Rp[3], Ru[3];
+  for (int r = 0; r < 3; ++r) {
+    Rp[r] = (in.R[3 * r] * p[0] + in.R[3 * r + 1] * p[1]) + in.R[3 * r + 2] * p[2];
+    Ru[r] = (in.R[3 * r] * u[0] + in.R[3 * r + 1] * u[1]) + in.R[3 * r + 2] * u[2];
+  }
+  double rs = 0.0, wt[3] = {0.0, 0.0, 0.0}, ct = 0.0, cr = 0.0, S[9];
+  for (int c = 0; c < 9; ++c) S[c] = 0.0;
+  for (int j = 0; j < in.k; ++j) {
+    const double r = in.resp[(size_t)i * in.k + j];
+    const int e = in.cand[(size_t)i * in.k + j];
+    const double m[3] = {in.vpos[3 * (size_t)e], in.vpos[3 * (size_t)e + 1], in.vpos[3 * (size_t)e + 2]};
+    const double vd[3] = {in.vdir[3 * (size_t)e], in.vdir[3 * (size_t)e + 1], in.vdir[3 * (size_t)e + 2]};
+    rs = rs + r;
+    double q[3], Lq[3];
+    for (int c = 0; c < 3; ++c) {
+      wt[c] = wt[c] + r * (m[c] - Rp[c]);
+      q[c] = (m[c] - Rp[c]) - in.t[c];
+    }
+    for (int a = 0; a < 3; ++a) Lq[a] = (Lr[3 * a] * q[0] + Lr[3 * a + 1] * q[1]) + Lr[3 * a + 2] * q[2];
+    ct = ct + r * ((q[0] * Lq[0] + q[1] * Lq[1]) + q[2] * Lq[2]);
+    const double w = r * sqrt(kap * in.vkap[e] + 1e-12);
+    for (int a = 0; a < 3; ++a)
+      for (int b = 0; b < 3; ++b) S[3 * a + b] = S[3 * a + b] + (w * vd[a]) * u[b];
+    cr = cr + w * (1.0 - ((Ru[0] * vd[0] + Ru[1] * vd[1]) + Ru[2] * vd[2]));
+  }
+  for (int c = 0; c < 9; ++c) o[c] = rs * Lr[c];
+  for (int a = 0; a < 3; ++a) o[9 + a] = (Lr[3 * a] * wt[0] + Lr[3 * a + 1] * wt[1]) + Lr[3 * a + 2] * wt[2];
+  o[12] = ct;
+  for (int c = 0; c < 9; ++c) o[13 + c] = S[c];
+  o[22] = cr;
+  o[23] = in.rmass[i];
+  o[24] = 1.0;
+}
+
+// GCS_VPE_SPLIT (default): every valid row's sums computed by its own lane over the grid (k_as_vpe_rows,
+// rows x 25 in rowv), then k_as_vpe adds them in its per-thread row order -- the same additions on the
+// same values as the one-workgroup form (whose threads each walked three rows' candidate loads in
+// series: 29 us at the reference sizes).
+#ifndef GCS_VPE_SPLIT
+#define GCS_VPE_SPLIT 1
+#endif
+__global__ __launch_bounds__(256) void k_as_vpe_rows(VpeIn in, double* __restrict__ rowv) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= in.n || !in.valid[i]) return;
+  double o[kVpeRowVals];
+  vpe_row(in, i, o);
+#pragma unroll
+  for (int q = 0; q < kVpeRowVals; ++q) rowv[(size_t)q * in.n + i] = o[q];
+}
+
+__global__ __launch_bounds__(kVpeThreads) void k_as_vpe(VpeIn in, const double* __restrict__ rowv, double* out) {
 #pragma clang fp contract(off)
   __shared__ int s_w[kVpeThreads / 64];
   __shared__ double lds_all[(kVpeThreads / 64) * kVpeVals];
   double acc[kVpeVals];
   for (int q = 0; q < kVpeVals; ++q) acc[q] = 0.0;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int n_meas = in.n_meas_dev ? max(0, *in.n_meas_dev) : in.n_meas;
   int base = 0;  // valid rows before this chunk
   for (int c0 = 0; c0 < in.n; c0 += kVpeThreads) {
     const int i = c0 + threadIdx.x;
@@ -1271,51 +1341,16 @@ __global__ __launch_bounds__(kVpeThreads) void k_as_vpe(VpeIn in, double* out) {
     int tot = 0;
     for (int w = 0; w < kVpeThreads / 64; ++w) tot += s_w[w];
     base += tot;
-    if (!v || rank >= in.n_meas) continue;
-    double p[3];
-    solve3_pivot(in.Lambdas + 9 * (size_t)i, in.eps_lift, in.thetas + 3 * (size_t)i, p);
-    double es[3] = {0.0, 0.0, 0.0};
-    for (int b = 0; b < in.n_lobes; ++b)
-      for (int c = 0; c < 3; ++c) {
-        const double e = in.etas[(size_t)3 * in.n_lobes * i + 3 * b + c];
-        es[c] = b == 0 ? e : es[c] + e;
-      }
-    const double kap = sqrt((es[0] * es[0] + es[1] * es[1]) + es[2] * es[2]);
-    const double u[3] = {es[0] / (kap + in.eps_mass), es[1] / (kap + in.eps_mass), es[2] / (kap + in.eps_mass)};
-    double Lr[9];
-    for (int c = 0; c < 9; ++c) Lr[c] = in.Lambdas[9 * (size_t)i + c] + ((c % 4) == 0 ? in.eps_lift : 0.0);
-    double Rp[3], Ru[3];
-    for (int r = 0; r < 3; ++r) {
-      Rp[r] = (in.R[3 * r] * p[0] + in.R[3 * r + 1] * p[1]) + in.R[3 * r + 2] * p[2];
-      Ru[r] = (in.R[3 * r] * u[0] + in.R[3 * r + 1] * u[1]) + in.R[3 * r + 2] * u[2];
+    if (!v || rank >= n_meas) continue;
+    double o[kVpeRowVals];
+    if (rowv) {
+#pragma unroll
+      for (int q = 0; q < kVpeRowVals; ++q) o[q] = rowv[(size_t)q * in.n + i];
+    } else {
+      vpe_row(in, i, o);
     }
-    double rs = 0.0, wt[3] = {0.0, 0.0, 0.0}, ct = 0.0, cr = 0.0, S[9];
-    for (int c = 0; c < 9; ++c) S[c] = 0.0;
-    for (int j = 0; j < in.k; ++j) {
-      const double r = in.resp[(size_t)i * in.k + j];
-      const int e = in.cand[(size_t)i * in.k + j];
-      const double m[3] = {in.vpos[3 * (size_t)e], in.vpos[3 * (size_t)e + 1], in.vpos[3 * (size_t)e + 2]};
-      const double vd[3] = {in.vdir[3 * (size_t)e], in.vdir[3 * (size_t)e + 1], in.vdir[3 * (size_t)e + 2]};
-      rs = rs + r;
-      double q[3], Lq[3];
-      for (int c = 0; c < 3; ++c) {
-        wt[c] = wt[c] + r * (m[c] - Rp[c]);
-        q[c] = (m[c] - Rp[c]) - in.t[c];
-      }
-      for (int a = 0; a < 3; ++a) Lq[a] = (Lr[3 * a] * q[0] + Lr[3 * a + 1] * q[1]) + Lr[3 * a + 2] * q[2];
-      ct = ct + r * ((q[0] * Lq[0] + q[1] * Lq[1]) + q[2] * Lq[2]);
-      const double w = r * sqrt(kap * in.vkap[e] + 1e-12);
-      for (int a = 0; a < 3; ++a)
-        for (int b = 0; b < 3; ++b) S[3 * a + b] = S[3 * a + b] + (w * vd[a]) * u[b];
-      cr = cr + w * (1.0 - ((Ru[0] * vd[0] + Ru[1] * vd[1]) + Ru[2] * vd[2]));
-    }
-    for (int c = 0; c < 9; ++c) acc[c] += rs * Lr[c];
-    for (int a = 0; a < 3; ++a) acc[9 + a] += (Lr[3 * a] * wt[0] + Lr[3 * a + 1] * wt[1]) + Lr[3 * a + 2] * wt[2];
-    acc[12] += ct;
-    for (int c = 0; c < 9; ++c) acc[13 + c] += S[c];
-    acc[22] += cr;
-    acc[23] += in.rmass[i];
-    acc[24] += 1.0;
+#pragma unroll
+    for (int q = 0; q < kVpeRowVals; ++q) acc[q] += o[q];
   }
   for (int e = threadIdx.x; e < in.m_view; e += kVpeThreads) acc[25] += in.vvalid[e] ? 1.0 : 0.0;
   // all 27 sums at once: the same xor tree per value in every wave, then thread q adds value q's wave
@@ -1355,6 +1390,8 @@ struct gcs_assoc_ctx {
   double* h_cert_dev = nullptr;
   double* h_vpe = nullptr;   // pinned, mapped: k_as_vpe's sums
   double* h_vpe_dev = nullptr;
+  double* d_vpe_rows = nullptr;  // k_as_vpe_rows: 25 sums per row (field-major, max_meas rows)
+  bool vpe_split = GCS_VPE_SPLIT != 0;  // GCSLAM_VPE_SPLIT=0: the one-workgroup form (A/B, bitwise test)
   int probe_iters = 0;       // GCS_SH_PROBE builds: the last launch's Sinkhorn iterations
 };
 
@@ -1426,7 +1463,8 @@ int gcs_assoc_ctx_destroy(gcs_assoc_ctx* c) {
   if (!c) return GCS_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* bufs[] = {c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, c->d_mvalid, c->d_st};
+  void* bufs[] = {c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, c->d_mvalid, c->d_st,
+                  c->d_vpe_rows};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_cert) (void)hipHostFree(c->h_cert);
@@ -1453,6 +1491,7 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
       bad(hipMalloc(&c->d_A1, N * 8)) || bad(hipMalloc(&c->d_A2, M * 8)) || bad(hipMalloc(&c->d_dt, NK * 8)) ||
       bad(hipMalloc(&c->d_tix, N * kMaxStencil * 4)) || bad(hipMalloc(&c->d_cand, NK * 4)) ||
       bad(hipMalloc(&c->d_mvalid, 8)) || bad(hipMalloc(&c->d_st, kMaxStencil * 3)) ||
+      bad(hipMalloc(&c->d_vpe_rows, N * kVpeRowVals * 8)) ||
       bad(hipHostMalloc(&c->h_cert, GCS_ASSOC_CERT_LEN * sizeof(double), hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&c->h_cert_dev, c->h_cert, 0)) ||
       bad(hipHostMalloc(&c->h_vpe, 32 * sizeof(double), hipHostMallocMapped)) ||
@@ -1464,6 +1503,7 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
+  if (const char* e = getenv("GCSLAM_VPE_SPLIT")) c->vpe_split = atoi(e) != 0;
   c->stream = c->own;
   *out = c;
   return GCS_OK;
@@ -1484,7 +1524,7 @@ int gcs_assoc_ctx_set_stream(gcs_assoc_ctx* c, void* stream) {
 namespace gcs {
 namespace live {
 int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_meas* m, const gcs_assoc_view* v,
-                 gcs_assoc_outputs* o) {
+                 gcs_assoc_outputs* o, const int32_t* n_valid_dev) {
   if (!c || !cfg || !m || !v || !o) return GCS_ERR_ARG;
   if (!o->responsibilities || !o->row_masses || !o->cost_matrix)
     return as_fail(c, GCS_ERR_ARG, "responsibilities, row_masses and cost_matrix are required outputs");
@@ -1581,27 +1621,29 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
   const int km = K <= 8 ? 8 : (K <= 16 ? 16 : 32);
   if (bad_policy) {
     uint32_t mvh = 0;
+    int32_t nvh = m->n_valid;
     ASCHK(c, hipMemcpyAsync(&mvh, mv, 4, hipMemcpyDeviceToHost, s));
+    if (n_valid_dev) ASCHK(c, hipMemcpyAsync(&nvh, n_valid_dev, 4, hipMemcpyDeviceToHost, s));
     ASCHK(c, hipStreamSynchronize(s));
-    if (m->n_valid != 0 && mvh != 0) return as_fail(c, GCS_ERR_ARG, bad_policy);  // rearm zeroes the next counter
+    if (nvh != 0 && mvh != 0) return as_fail(c, GCS_ERR_ARG, bad_policy);  // rearm zeroes the next counter
     // empty: the Sinkhorn kernel's zero path writes the reference's empty result
   }
   if (bad_policy) {
-    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, 0);
+    hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, 0, (const int32_t*)nullptr);
   } else if (km == 8) {
     hipLaunchKernelGGL(k_as_pool<8>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
     // three rows per thread when they cover the rows (the reference's 1,536 = 3 x 512): no padding
     // row in the K v / K^T u sums
     if (3 * kShThreads < rpt_for(8) * kShThreads && p.n <= 3 * kShThreads)
-      hipLaunchKernelGGL((k_as_sinkhorn<8, 3>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+      hipLaunchKernelGGL((k_as_sinkhorn<8, 3>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
     else
-      hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+      hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
   } else if (km == 16) {
     hipLaunchKernelGGL(k_as_pool<16>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
-    hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+    hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
   } else {
     hipLaunchKernelGGL(k_as_pool<32>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
-    hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid);
+    hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
   }
   ASCHK(c, hipGetLastError());
   rearm.armed = false;  // the Sinkhorn is queued: it zeroes mv_next
@@ -1650,7 +1692,22 @@ int gcs_visual_pose_evidence(gcs_assoc_ctx* c, const gcs_assoc_meas* m, const gc
                              const double* responsibilities, const int32_t* candidate_pool_indices,
                              const double* row_masses, int32_t k_assoc, const double* z_lin_pose, double eps_lift,
                              double eps_mass, gcs_vpe_outputs* o) {
-  if (!c || !m || !v || !o || !z_lin_pose) return GCS_ERR_ARG;
+  if (!o) return GCS_ERR_ARG;
+  if (int rc = gcs::live::vpe_launch(c, m, v, responsibilities, candidate_pool_indices, row_masses, k_assoc,
+                                     z_lin_pose, eps_lift, eps_mass))
+    return rc;
+  ASCHK(c, hipStreamSynchronize(c->stream));
+  gcs::live::vpe_collect(c, m->n_valid, k_assoc, z_lin_pose, eps_lift, o);
+  return GCS_OK;
+}
+}  // extern "C"
+
+namespace gcs {
+namespace live {
+int vpe_launch(gcs_assoc_ctx* c, const gcs_assoc_meas* m, const gcs_assoc_view* v, const double* responsibilities,
+               const int32_t* candidate_pool_indices, const double* row_masses, int32_t k_assoc,
+               const double* z_lin_pose, double eps_lift, double eps_mass, const int32_t* n_valid_dev) {
+  if (!c || !m || !v || !z_lin_pose) return GCS_ERR_ARG;
   if (m->n_total < 1 || k_assoc < 1 || !responsibilities || !candidate_pool_indices || !row_masses || !m->Lambdas ||
       !m->thetas || !m->etas || !m->valid_mask || !v->positions || !v->directions || !v->kappas || !v->valid_mask)
     return as_fail(c, GCS_ERR_ARG, "visual_pose_evidence: missing measurement, view or association array");
@@ -1663,6 +1720,7 @@ int gcs_visual_pose_evidence(gcs_assoc_ctx* c, const gcs_assoc_meas* m, const gc
   in.n = m->n_total;
   in.n_lobes = m->n_lobes;
   in.n_meas = std::max(0, m->n_valid);
+  in.n_meas_dev = n_valid_dev;
   in.vpos = v->positions;
   in.vdir = v->directions;
   in.vkap = v->kappas;
@@ -1676,16 +1734,28 @@ int gcs_visual_pose_evidence(gcs_assoc_ctx* c, const gcs_assoc_meas* m, const gc
   for (int q = 0; q < 3; ++q) in.t[q] = z_lin_pose[q];
   in.eps_lift = eps_lift;
   in.eps_mass = eps_mass;
-  hipLaunchKernelGGL(k_as_vpe, dim3(1), dim3(kVpeThreads), 0, c->stream, in, c->h_vpe_dev);
+  if (c->vpe_split && in.n <= c->max_meas) {
+    hipLaunchKernelGGL(k_as_vpe_rows, dim3((in.n + 255) / 256), dim3(256), 0, c->stream, in, c->d_vpe_rows);
+    hipLaunchKernelGGL(k_as_vpe, dim3(1), dim3(kVpeThreads), 0, c->stream, in, (const double*)c->d_vpe_rows,
+                       c->h_vpe_dev);
+  } else {
+    hipLaunchKernelGGL(k_as_vpe, dim3(1), dim3(kVpeThreads), 0, c->stream, in, (const double*)nullptr, c->h_vpe_dev);
+  }
   ASCHK(c, hipGetLastError());
-  ASCHK(c, hipStreamSynchronize(c->stream));
+  return GCS_OK;
+}
+
+void vpe_collect(gcs_assoc_ctx* c, int32_t n_valid, int32_t k_assoc, const double* z_lin_pose, double eps_lift,
+                 gcs_vpe_outputs* o) {
+  double Rz[9];
+  so3_exp(z_lin_pose + 3, Rz);
   const double* a = c->h_vpe;
   memset(o, 0, sizeof(*o));
   for (int q = 0; q < 22; ++q) o->L_pose[23 * q] = eps_lift;
   const int rows = (int)a[24];
-  if (m->n_valid == 0 || rows == 0 || a[25] == 0.0) {  // the empty case (:293-318)
+  if (n_valid == 0 || rows == 0 || a[25] == 0.0) {  // the empty case (:293-318)
     o->exact = 1;
-    return GCS_OK;
+    return;
   }
   for (int q = 0; q < 9; ++q) o->L_trans[q] = a[q] + ((q % 4) == 0 ? eps_lift : 0.0);
   for (int q = 0; q < 3; ++q) o->h_trans[q] = a[9 + q];
@@ -1702,7 +1772,7 @@ int gcs_visual_pose_evidence(gcs_assoc_ctx* c, const gcs_assoc_meas* m, const gc
   double Rd[9];
   for (int r = 0; r < 3; ++r)
     for (int q = 0; q < 3; ++q)
-      Rd[3 * r + q] = (Rs[3 * r] * in.R[3 * q] + Rs[3 * r + 1] * in.R[3 * q + 1]) + Rs[3 * r + 2] * in.R[3 * q + 2];
+      Rd[3 * r + q] = (Rs[3 * r] * Rz[3 * q] + Rs[3 * r + 1] * Rz[3 * q + 1]) + Rs[3 * r + 2] * Rz[3 * q + 2];
   double w[3];
   so3_log(Rd, w);
   for (int q = 0; q < 3; ++q) {
@@ -1722,9 +1792,12 @@ int gcs_visual_pose_evidence(gcs_assoc_ctx* c, const gcs_assoc_meas* m, const gc
   o->n_associations = rows * k_assoc;
   o->mean_transported_mass = a[23] / (double)rows;
   o->ess_total = a[23];
-  o->support_frac = (double)rows / (double)std::max(m->n_valid, 1);
+  o->support_frac = (double)rows / (double)std::max(n_valid, 1);
   o->exact = 0;
-  return GCS_OK;
 }
+}  // namespace live
+}  // namespace gcs
+
+extern "C" {
 
 }  // extern "C"

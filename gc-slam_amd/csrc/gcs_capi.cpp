@@ -2424,15 +2424,14 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   if (live::assoc_bind_stream(as, s)) return sub_fail(c, GCS_ERR_HIP, "association", gcs_assoc_last_error(as));
   if (live::pmap_bind_stream(pm, s)) return sub_fail(c, GCS_ERR_HIP, "map", gcs_pmap_last_error(pm));
   if (a->zero_dev && a->zero_bytes > 0) HIPCHK(c, hipMemsetAsync(a->zero_dev, 0, (size_t)a->zero_bytes, s));
-  // surfels of the deskewed points (pipeline.py:778-782); the batch's LiDAR count feeds the launches
-  gcs_surfel_outputs* so = a->surfel_out;
-  if ((rc = live::surfel_launch(sf, a->points_dev, a->timestamps_dev, a->weights_dev, a->n_points, so)))
+  // surfels of the deskewed points (pipeline.py:778-782), the batch's LiDAR sources set on its valid
+  // rows; the launches behind them read the surfel count on the device (no host wait here)
+  gcs_surfel_outputs sfo = *a->surfel_out;
+  sfo.sources = a->lidar_sources_dev;
+  if ((rc = live::surfel_launch(sf, a->points_dev, a->timestamps_dev, a->weights_dev, a->n_points, &sfo)))
     return sub_fail(c, rc, "gcs_extract_lidar_surfels", gcs_surfel_last_error(sf));
-  HIPCHK(c, hipStreamSynchronize(s));
-  live::surfel_collect(sf, so);
+  const int32_t* nv_dev = live::surfel_nvalid_dev(sf);
   mark(1);
-  const int nv = so->n_valid;
-  if (nv > 0) HIPCHK(c, hipMemsetD32Async((hipDeviceptr_t)a->lidar_sources_dev, 1, (size_t)nv, s));
   // recency inflation of the active tiles the map holds, then the view over the stencil (:800-815)
   if ((rc = live::pmap_recency_launch(pm, rec, nrec, a->scan_seq, a->recency_lambda, a->recency_min_scale)))
     return sub_fail(c, rc, "gcs_pmap_recency_inflate", gcs_pmap_last_error(pm));
@@ -2442,7 +2441,7 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
     return sub_fail(c, rc, "gcs_pmap_extract_view", gcs_pmap_last_error(pm));
   // OT association (:816-878)
   gcs_assoc_meas m = a->meas;
-  m.n_valid = nv;  // n_camera_valid (0: a LiDAR-only batch) + n_lidar_valid
+  m.n_valid = 0;  // n_camera_valid (0: a LiDAR-only batch) + n_lidar_valid: read on the device (nv_dev)
   gcs_assoc_view v{};
   v.tile_ids = a->view_tile_ids_dev;
   v.n_tiles = ns;
@@ -2455,9 +2454,10 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   v.candidate_tile_ids = a->view->candidate_tile_ids;
   v.candidate_slots = a->view->candidate_slots;
   gcs_assoc_outputs* ao = a->assoc_out;
-  if ((rc = live::assoc_launch(as, a->assoc_cfg, &m, &v, ao)))
+  if ((rc = live::assoc_launch(as, a->assoc_cfg, &m, &v, ao, nv_dev)))
     return sub_fail(c, rc, "gcs_associate_primitives_ot", gcs_assoc_last_error(as));
-  // visual pose evidence at z_lin_pose (:980-1010); its wait covers the association and the recency
+  // visual pose evidence at z_lin_pose (:980-1010); one wait for the surfels, the recency, the view, the
+  // association and the pose evidence
   gcs_assoc_view vv{};
   vv.positions = v.positions;
   vv.directions = v.directions;
@@ -2466,12 +2466,21 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   vv.n_tiles = 1;
   vv.m_tile_view = ns * a->m_tile_view;
   gcs_vpe_outputs* vo = a->vpe_out;
-  if ((rc = gcs_visual_pose_evidence(as, &m, &vv, ao->responsibilities, ao->candidate_pool_indices, ao->row_masses,
-                                     a->assoc_cfg->k_assoc, bo->z_lin_pose, a->eps_lift, a->eps_mass, vo)))
+  if ((rc = live::vpe_launch(as, &m, &vv, ao->responsibilities, ao->candidate_pool_indices, ao->row_masses,
+                             a->assoc_cfg->k_assoc, bo->z_lin_pose, a->eps_lift, a->eps_mass, nv_dev)))
     return sub_fail(c, rc, "gcs_visual_pose_evidence", gcs_assoc_last_error(as));
+  mark(3);
+  HIPCHK(c, hipStreamSynchronize(s));
+  live::surfel_collect(sf, &sfo);
+  gcs_surfel_outputs* so = a->surfel_out;
+  memcpy(so->center, sfo.center, sizeof(so->center));
+  so->n_valid = sfo.n_valid;
+  memcpy(so->cert, sfo.cert, sizeof(so->cert));
+  const int nv = so->n_valid;
   live::assoc_collect(as, ao);
   live::pmap_recency_collect(pm, nrec, lo->recency_stats);
-  mark(2);
+  live::vpe_collect(as, nv, a->assoc_cfg->k_assoc, bo->z_lin_pose, a->eps_lift, vo);
+  mark(4);
   // the finish: trigger magnitudes of the surfel (identity influence), recency (exact), association
   // (mass_epsilon_ratio unless exact) and visual (lift_strength = eps_lift unless exact) certs; ESS of
   // the surfel (n_valid), association and visual certs; no mismatch terms (pipeline.py:1049-1056,1211)
@@ -2489,7 +2498,7 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   lo->trigger_sum = ev.trigger_sum;
   lo->ess_sum = ev.ess_sum;
   if ((rc = gcs_scan_finish(c, &ev, out))) return rc;
-  mark(3);
+  mark(5);
   // step 12b at z_t over the active tiles (:1232-1492); new tiles on written slots start cleared
   for (int k = 0; k < ncl; ++k)
     if ((rc = live::pmap_clear_tile_launch(pm, clear[k]))) return sub_fail(c, rc, "gcs_pmap_clear_tile", gcs_pmap_last_error(pm));
@@ -2513,7 +2522,7 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
     return sub_fail(c, rc, "gcs_pmap_map_update", gcs_pmap_last_error(pm));
   lo->next_global_id = a->next_global_id;
   c->live_map = pm;
-  mark(4);
+  mark(6);
   return GCS_OK;
 }
 
@@ -2525,7 +2534,7 @@ int gcs_live_collect(gcs_ctx* c, gcs_live_outputs* lo) {
   const clk::time_point t_in = clk::now();
   if (int rc = live::pmap_update_collect(pm, &lo->next_global_id, &lo->update, lo->counts))
     return sub_fail(c, rc, "gcs_pmap_map_update", gcs_pmap_last_error(pm));
-  lo->phase_us[5] = 1e3 * ms_between(t_in, clk::now());
+  lo->phase_us[7] = 1e3 * ms_between(t_in, clk::now());
   return GCS_OK;
 }
 

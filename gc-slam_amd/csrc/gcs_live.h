@@ -15,14 +15,23 @@ namespace live {
 int surfel_launch(gcs_surfel_ctx* c, const double* points, const double* timestamps, const double* weights,
                   int32_t n, gcs_surfel_outputs* o);
 void surfel_collect(gcs_surfel_ctx* c, gcs_surfel_outputs* o);
+// the surfel count on the device (written by the extraction's slot kernel), for launches queued behind it
+const int32_t* surfel_nvalid_dev(gcs_surfel_ctx* c);
 // queue the context's work on stream s (the null stream allowed), after what it queued before
 int surfel_bind_stream(gcs_surfel_ctx* c, void* s);
 
 // gcs_associate_primitives_ot (primitive_association.py:239-553)
+// n_valid_dev (may be null): the measurement count on the device, read by the kernels instead of m->n_valid
 int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_meas* m, const gcs_assoc_view* v,
-                 gcs_assoc_outputs* o);
+                 gcs_assoc_outputs* o, const int32_t* n_valid_dev = nullptr);
 void assoc_collect(gcs_assoc_ctx* c, gcs_assoc_outputs* o);
 int assoc_bind_stream(gcs_assoc_ctx* c, void* s);
+// gcs_visual_pose_evidence (visual_pose_evidence.py:260-412) split at its wait; collect takes the count
+int vpe_launch(gcs_assoc_ctx* c, const gcs_assoc_meas* m, const gcs_assoc_view* v, const double* responsibilities,
+               const int32_t* candidate_pool_indices, const double* row_masses, int32_t k_assoc,
+               const double* z_lin_pose, double eps_lift, double eps_mass, const int32_t* n_valid_dev = nullptr);
+void vpe_collect(gcs_assoc_ctx* c, int32_t n_valid, int32_t k_assoc, const double* z_lin_pose, double eps_lift,
+                 gcs_vpe_outputs* o);
 
 int pmap_bind_stream(gcs_pmap* p, void* s);
 // create_empty_tile (primitive_map.py:148-174) without the wait

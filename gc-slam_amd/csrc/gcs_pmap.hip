@@ -1132,7 +1132,7 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_ts(PmStore st, const int
 __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmStore st, const int32_t* tiles, double ts,
                                                                     PmRows r, int n_tiles, int M, int nb, int rpb,
                                                                     uint32_t* keys, uint32_t* vals, uint8_t* mark,
-                                                                    uint32_t* err) {
+                                                                    uint32_t* err, uint32_t nokey) {
   const int g = blockIdx.x * kPmThreads + threadIdx.x;
   if (g >= r.n) return;
   const int tp = r.tpos[g], q = r.slots[g], b = g / rpb;
@@ -1142,7 +1142,7 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmStore st, 
   if (ok)
     for (int t = 0; t < n_tiles; ++t) st.ts[sidx(st, tiles[t], q)] = ts;
   const bool v = (r.valid ? r.valid[g] != 0 : true) && tp >= 0 && tp < n_tiles && ok;
-  keys[g] = v ? ((uint32_t)tp * (uint32_t)M + (uint32_t)q) * (uint32_t)nb + (uint32_t)b : kNoKey;
+  keys[g] = v ? ((uint32_t)tp * (uint32_t)M + (uint32_t)q) * (uint32_t)nb + (uint32_t)b : nokey;
   vals[g] = (uint32_t)g;
 }
 
@@ -1160,12 +1160,12 @@ __device__ __forceinline__ bool fuse_long_start(const uint32_t* keys, int n, int
   return pos % kFuseChunk == 0 && pos >= kFuseChunk && keys[pos - kFuseChunk] == key;
 }
 __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_chunks(PmRows r, const uint32_t* keys, const uint32_t* vals,
-                                                               double* P, int* Lc) {
+                                                               double* P, int* Lc, uint32_t nokey) {
 #pragma clang fp contract(off)
   const int pos = blockIdx.x * kPmThreads + threadIdx.x;
   if (pos >= r.n) return;
   const uint32_t key = keys[pos];
-  if (key == kNoKey || !fuse_long_start(keys, r.n, pos, key)) return;
+  if (key == nokey || !fuse_long_start(keys, r.n, pos, key)) return;
   constexpr int ne = 3 * kNL;
   static_assert(9 + 3 + ne + 4 + 3 == kFT, "fuse chunk layout");
   double dL[9], dth[3], de[ne], dw = 0.0, drs = 0.0, dcam = 0.0, dlid = 0.0, dacc[3] = {0.0, 0.0, 0.0};
@@ -1207,25 +1207,112 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_chunks(PmRows r, const u
   Lc[pos] = end - pos;
 }
 
+// GCS_FUSE_RUNS (default): a long run is summed by one wave instead of chunk by chunk -- lane l takes
+// rows start + l, + 64, ... in order, the lanes meet in a fixed xor tree -- and stored as one chunk of
+// the run's length (k_pm_fuse_apply_blocks then adds one sum per long run).  The chunk walk was a
+// serial chain of dependent row loads per lane (up to 63 rows): 40-50 us per map update on scans
+// whose sparse map draws hundreds of associations to one primitive.  Deterministic either way; runs of
+// at most kFuseChunk rows are untouched (the per-row walk's sums).
+#ifndef GCS_FUSE_RUNS
+#define GCS_FUSE_RUNS 1
+#endif
+__global__ __launch_bounds__(kPmThreads) void k_pm_fuse_runs(PmRows r, const uint32_t* keys, const uint32_t* vals,
+                                                             double* P, int* Lc, uint32_t nokey) {
+#pragma clang fp contract(off)
+  __shared__ int s_start[kPmThreads];
+  __shared__ int s_wn[kPmThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int pos = blockIdx.x * kPmThreads + t;
+  bool st = false;
+  if (pos < r.n) {
+    const uint32_t key = keys[pos];
+    st = key != nokey && (pos == 0 || keys[pos - 1] != key) && pos + kFuseChunk < r.n && keys[pos + kFuseChunk] == key;
+  }
+  // the block's long-run starts in position order
+  const unsigned long long m = __ballot(st);
+  if (lane == 0) s_wn[wid] = __popcll(m);
+  __syncthreads();
+  int base = 0, total = 0;
+  for (int w = 0; w < kPmThreads / 64; ++w) {
+    if (w < wid) base += s_wn[w];
+    total += s_wn[w];
+  }
+  if (st) s_start[base + __popcll(m & ((1ull << lane) - 1ull))] = pos;
+  __syncthreads();
+  constexpr int ne = 3 * kNL;
+  static_assert(9 + 3 + ne + 4 + 3 == kFT, "fuse chunk layout");
+  const size_t n = (size_t)r.n;
+  for (int k = wid; k < total; k += kPmThreads / 64) {  // one wave per long run
+    const int s = s_start[k];
+    const uint32_t key = keys[s];
+    int e = s + kFuseChunk;  // the run's end: the first position past it (64 probes per step)
+    for (;;) {
+      const int p = e + lane;
+      const unsigned long long out = __ballot(!(p < r.n && keys[p] == key));
+      if (out) {
+        e += __ffsll((long long)out) - 1;
+        break;
+      }
+      e += 64;
+    }
+    double f[kFT];
+#pragma unroll
+    for (int c = 0; c < kFT; ++c) f[c] = 0.0;
+    for (int q = s + lane; q < e; q += 64) {
+      const size_t row = vals[q];
+      const double rr = r.resp[row] * 1.0;
+#pragma unroll
+      for (int c = 0; c < 9; ++c) f[c] = f[c] + rr * r.lam[9 * row + c];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) f[9 + c] = f[9 + c] + rr * r.th[3 * row + c];
+#pragma unroll
+      for (int c = 0; c < ne; ++c) f[12 + c] = f[12 + c] + rr * r.eta[(size_t)ne * row + c];
+      const double rw = rr * r.w[row];
+      f[21] = f[21] + rw;
+      f[22] = f[22] + rr;
+      if (r.src) {
+        const int sv = r.src[row];
+        const double wc = rw * (sv == 0 ? 1.0 : 0.0);
+        f[23] = f[23] + wc;
+        f[24] = f[24] + rw * (sv == 1 ? 1.0 : 0.0);
+        if (r.col)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) f[25 + c] = f[25 + c] + clip01(r.col[3 * row + c]) * wc;
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1)
+#pragma unroll
+      for (int c = 0; c < kFT; ++c) f[c] = f[c] + __shfl_xor(f[c], off, 64);
+    if (lane < kFT) {  // lane c stores field c (every lane holds the whole sum)
+      double v = f[0];
+#pragma unroll
+      for (int c = 1; c < kFT; ++c) v = lane == c ? f[c] : v;
+      P[(size_t)lane * n + s] = v;
+    }
+    if (lane == 0) Lc[s] = e - s;
+  }
+}
+
 // one lane per (tile, slot) group: for each block in order, d = the block's rows summed in row order
 // (a long run: its chunk sums in order, k_pm_fuse_chunks), then slot += d -- the reference's
 // block-by-block fuse calls (pipeline.py:1272-1327)
 __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st, const int32_t* tiles, PmRows r,
                                                                      const uint32_t* keys, const uint32_t* vals,
                                                                      int nb, long long seq, const double* P,
-                                                                     const int* Lc) {
+                                                                     const int* Lc, uint32_t nokey) {
 #pragma clang fp contract(off)
   const int g = blockIdx.x * kPmThreads + threadIdx.x;
   if (g >= r.n) return;
   const uint32_t key = keys[g];
-  if (key == kNoKey) return;
+  if (key == nokey) return;
   const uint32_t grp = key / (uint32_t)nb;
-  if (g > 0 && keys[g - 1] != kNoKey && keys[g - 1] / (uint32_t)nb == grp) return;
+  if (g > 0 && keys[g - 1] != nokey && keys[g - 1] / (uint32_t)nb == grp) return;
   constexpr int ne = 3 * kNL;
   const int t = (int)(grp / (uint32_t)st.M), q = (int)(grp % (uint32_t)st.M);
   const size_t i = sidx(st, tiles[t], q);
   int pos = g;
-  while (pos < r.n && keys[pos] != kNoKey && keys[pos] / (uint32_t)nb == grp) {
+  while (pos < r.n && keys[pos] != nokey && keys[pos] / (uint32_t)nb == grp) {
     const uint32_t kb = keys[pos];
     double dL[9], dth[3], de[ne], dw = 0.0, drs = 0.0, dcam = 0.0, dlid = 0.0, dacc[3] = {0.0, 0.0, 0.0}, dden = 0.0;
     for (int c = 0; c < 9; ++c) dL[c] = 0.0;
@@ -2414,13 +2501,14 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
   *(uint32_t*)(p->h_small + 8192) = 0u;
   const PmRows r = rows_of(rows);
   const int rb = (R + kPmThreads - 1) / kPmThreads;
-  hipLaunchKernelGGL(k_pm_fuse_keys_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st,
-                     (const int32_t*)p->d_tiles, timestamp, r, n, p->M, nb, rpb, p->fk, p->fv, p->bmark, d_err);
+  // keys below n M nb, the skipped rows' key 2^bits - 1 above them: the sort needs only the low bits
   unsigned bits = 1;
   while (bits < 32 && ((double)(1ull << bits)) < (double)n * p->M * nb + 1.0) ++bits;
+  const uint32_t nokey = bits >= 32 ? kNoKey : (uint32_t)((1ull << bits) - 1ull);
+  hipLaunchKernelGGL(k_pm_fuse_keys_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st,
+                     (const int32_t*)p->d_tiles, timestamp, r, n, p->M, nb, rpb, p->fk, p->fv, p->bmark, d_err, nokey);
   size_t tb = p->ftemp_bytes;
-  PMCHK(p, rocprim::radix_sort_pairs(p->ftemp, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)R, 0u, 32u, p->stream));
-  (void)bits;
+  PMCHK(p, rocprim::radix_sort_pairs(p->ftemp, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)R, 0u, bits, p->stream));
   if ((size_t)R * kFT > p->fterm_n) {
     if (p->fterm) PMCHK(p, hipFree(p->fterm));
     if (p->flen) PMCHK(p, hipFree(p->flen));
@@ -2430,11 +2518,15 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
     PMCHK(p, hipMalloc(&p->fterm, p->fterm_n * sizeof(double)));
     PMCHK(p, hipMalloc(&p->flen, (p->fterm_n / kFT) * sizeof(int)));
   }
-  hipLaunchKernelGGL(k_pm_fuse_chunks, dim3(rb), dim3(kPmThreads), 0, p->stream, r, (const uint32_t*)p->fk_s,
-                     (const uint32_t*)p->fv_s, p->fterm, p->flen);
+  if (GCS_FUSE_RUNS)
+    hipLaunchKernelGGL(k_pm_fuse_runs, dim3(rb), dim3(kPmThreads), 0, p->stream, r, (const uint32_t*)p->fk_s,
+                       (const uint32_t*)p->fv_s, p->fterm, p->flen, nokey);
+  else
+    hipLaunchKernelGGL(k_pm_fuse_chunks, dim3(rb), dim3(kPmThreads), 0, p->stream, r, (const uint32_t*)p->fk_s,
+                       (const uint32_t*)p->fv_s, p->fterm, p->flen, nokey);
   hipLaunchKernelGGL(k_pm_fuse_apply_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles,
                      r, (const uint32_t*)p->fk_s, (const uint32_t*)p->fv_s, nb, (long long)scan_seq,
-                     (const double*)p->fterm, (const int*)p->flen);
+                     (const double*)p->fterm, (const int*)p->flen, nokey);
   const long tm = (long)n * p->M;
   hipLaunchKernelGGL(k_pm_fuse_rgb, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
                      p->stream, p->st, (const int32_t*)p->d_tiles, n, eps_mass);

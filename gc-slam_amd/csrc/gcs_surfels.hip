@@ -334,7 +334,7 @@ struct SelOut {
   double *positions, *covariances, *normals, *kappas, *weights, *timestamps;
   double *Lambdas, *thetas, *etas, *colors;
   uint8_t* valid_mask;
-  int32_t *source_indices, *cell_ids;
+  int32_t *source_indices, *cell_ids, *sources;
 };
 
 // one workgroup: valid cells in cell-id order -> slot_cell[slot], n_valid (device + mapped host)
@@ -423,6 +423,7 @@ __global__ __launch_bounds__(kSfThreads) void k_sf_write(const double* __restric
   }
   if (o.valid_mask) o.valid_mask[s] = 1;
   if (o.source_indices) o.source_indices[s] = s;
+  if (o.sources) o.sources[s] = 1;  // measurement_batch_add_lidar_surfels: LiDAR rows
 }
 
 // One workgroup for clouds of up to kSortMax points: the stable sort of k_sf_keys' (key, point index)
@@ -718,7 +719,7 @@ int surfel_launch(gcs_surfel_ctx* c, const double* points, const double* timesta
   hipLaunchKernelGGL(k_sf_slots, dim3(1), dim3(kSelThreads), 0, s, (const uint8_t*)c->d_valid, a, c->d_slot_cell,
                      (int32_t*)(c->d_scal + 3), (int32_t*)(c->h_scal_dev + 3));
   SelOut so{o->positions, o->covariances, o->normals, o->kappas, o->weights, o->timestamps, o->Lambdas, o->thetas,
-            o->etas, o->colors, o->valid_mask, o->source_indices, o->cell_ids};
+            o->etas, o->colors, o->valid_mask, o->source_indices, o->cell_ids, o->sources};
   hipLaunchKernelGGL(k_sf_write, dim3((a.n_surfel + kSfThreads - 1) / kSfThreads), dim3(kSfThreads), 0, s,
                      (const double*)c->d_fit, (const int32_t*)c->d_slot_cell, (const int32_t*)(c->d_scal + 3), a, so);
   SFCHK(c, hipGetLastError());
@@ -727,6 +728,8 @@ int surfel_launch(gcs_surfel_ctx* c, const double* points, const double* timesta
   if (o->count) SFCHK(c, hipMemcpyAsync(o->count, c->d_count, (size_t)a.n_cells * 4, hipMemcpyDeviceToDevice, s));
   return GCS_OK;
 }
+
+const int32_t* surfel_nvalid_dev(gcs_surfel_ctx* c) { return (const int32_t*)(c->d_scal + 3); }
 
 void surfel_collect(gcs_surfel_ctx* c, gcs_surfel_outputs* o) {
   for (int k = 0; k < 3; ++k) o->center[k] = c->h_scal[k];

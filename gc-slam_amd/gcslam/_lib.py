@@ -120,7 +120,7 @@ class GcsSurfelConfig(C.Structure):
 class GcsSurfelOutputs(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in ("positions", "covariances", "normals", "kappas", "weights", "timestamps",
                                           "Lambdas", "thetas", "etas", "colors", "valid_mask", "source_indices",
-                                          "cell_ids", "bucket", "count")] + \
+                                          "cell_ids", "bucket", "count", "sources")] + \
                [("center", C.c_double * 3), ("n_valid", C.c_int32), ("cert", C.c_double * 2)]
 
 
@@ -227,7 +227,7 @@ class GcsLiveOutputs(C.Structure):
                 ("n_present_active", C.c_int32), ("n_created", C.c_int32),
                 ("created_ids", C.c_int64 * LIVE_MAX_TILES), ("created_slots", C.c_int32 * LIVE_MAX_TILES),
                 ("recency_stats", C.c_double * 3), ("trigger_sum", C.c_double), ("ess_sum", C.c_double),
-                ("phase_us", C.c_double * 6),
+                ("phase_us", C.c_double * 12),
                 ("update", GcsPmapUpdateStats), ("counts", C.c_int32 * LIVE_MAX_TILES), ("next_global_id", C.c_int64)]
 
 
@@ -432,13 +432,18 @@ def check(rc: int, ctx=None, what: str = "gcs call"):
     raise RuntimeError(f"{what} failed ({rc}): {msg}")
 
 
+_BELIEF_FIELDS = (("X_anchor", 6), ("z_lin", D_Z), ("L", D_Z * D_Z), ("h", D_Z))
+
+
 def belief_to_struct(X_anchor, stamp, z_lin, L, h) -> GcsBelief:
     b = GcsBelief()
-    b.X_anchor[:] = np.asarray(X_anchor, np.float64).ravel().tolist()
+    base = C.addressof(b)
+    for (name, n), v in zip(_BELIEF_FIELDS, (X_anchor, z_lin, L, h)):
+        a = np.ascontiguousarray(v, np.float64).reshape(-1)
+        if a.shape[0] != n:
+            raise ValueError(f"belief {name}: {a.shape[0]} values, expected {n}")
+        C.memmove(base + getattr(GcsBelief, name).offset, a.ctypes.data, 8 * n)
     b.stamp_sec = float(stamp)
-    b.z_lin[:] = np.asarray(z_lin, np.float64).ravel().tolist()
-    b.L[:] = np.asarray(L, np.float64).ravel().tolist()
-    b.h[:] = np.asarray(h, np.float64).ravel().tolist()
     return b
 
 

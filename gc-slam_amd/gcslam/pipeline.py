@@ -291,26 +291,31 @@ def _as_device_scan(raw_points, raw_timestamps, raw_weights, device):
         ts, ws = np.asarray(raw_timestamps).reshape(-1), np.asarray(raw_weights).reshape(-1)
         if ts.shape[0] != n or ws.shape[0] != n:
             raise ValueError("points, timestamps and weights must have the same length")
-        key = ("scan", device, n)
+        # the device copy is reused by the next scan on the same stream (stream order keeps the begin's
+        # reads of it ahead of the next copy); the staging buffer waits for its previous copy's event
+        stream = torch.cuda.current_stream(device)
+        key = ("scan", device, n, stream.cuda_stream)
         ent = _pinned.get(key)
         if ent is None:
             hb = torch.empty(32 * n, dtype=torch.uint8).pin_memory()
             hn = hb.numpy()
-            ent = _pinned[key] = [hb, None, (hn[:16 * n].view(np.float32).reshape(n, 4),
-                                             hn[16 * n:24 * n].view(np.float64), hn[24 * n:].view(np.float64))]
-        hb, ev, (hr, ht, hw) = ent
-        if ev is not None:
+            d = torch.empty(32 * n, dtype=torch.uint8, device=f"cuda:{device}")
+            ent = _pinned[key] = [hb, torch.cuda.Event(), (hn[:16 * n].view(np.float32).reshape(n, 4),
+                                                           hn[16 * n:24 * n].view(np.float64),
+                                                           hn[24 * n:].view(np.float64)), d,
+                                  (d[:16 * n].view(torch.float32).view(n, 4), d[16 * n:24 * n].view(torch.float64),
+                                   d[24 * n:].view(torch.float64)), False]
+        hb, ev, (hr, ht, hw), d, views, used = ent
+        if used:
             ev.synchronize()  # the previous copy out of the staging buffer
         hr[:, :3] = p  # PointCloud2 x,y,z are float32 (backend_node.py:377-468)
         hr[:, 3] = 0.0
         ht[...] = ts
         hw[...] = ws
-        d = hb.to(f"cuda:{device}", non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(device))
-        ent[1] = ev
-        return d[:16 * n].view(torch.float32).view(n, 4), d[16 * n:24 * n].view(torch.float64), \
-            d[24 * n:].view(torch.float64)
+        d.copy_(hb, non_blocking=True)
+        ev.record(stream)
+        ent[5] = True
+        return views
     else:
         p = np.asarray(raw_points.cpu() if isinstance(raw_points, torch.Tensor) else raw_points,
                        np.float64).reshape(-1, 3)
@@ -511,7 +516,7 @@ def _live_chain_state(ctx: HypothesisContext, config: "PipelineConfig"):
     a.n_points = cap
     vpe = L.GcsVpeOutputs()
     a.vpe_out = C.addressof(vpe)
-    st = dict(key=key, scfg=scfg, pool=int(config.N_STENCIL_TILES) * int(config.M_TILE_VIEW), acfg=acfg,
+    st = dict(key=key, scfg=scfg, ex=None, ex_key=None, pool=int(config.N_STENCIL_TILES) * int(config.M_TILE_VIEW), acfg=acfg,
               arena=_live_arena(config, N, K), c_as=c_as, c_up=c_up, args=a, vpe=vpe, bufs=bufs, N=N, K=K,
               lo=L.GcsLiveOutputs())
     ctx._live_chain = st
@@ -545,19 +550,29 @@ def _live_arena(config: "PipelineConfig", N: int, K: int) -> dict:
     for part, spec in parts.items():
         rows = []
         for name, dt, shape in spec:
+            shape = tuple(int(x) for x in shape)
             z = int(np.prod(shape)) * size[dt]
-            rows.append((name, dt, shape, off, z))
+            stride = tuple(int(np.prod(shape[k + 1:])) for k in range(len(shape)))
+            rows.append((name, dt, shape, stride, off // size[dt], off))
             off += (z + 7) // 8 * 8
-        lay[part] = rows
+        lay[part] = [r[:5] for r in rows]
+        lay.setdefault("off", {}).update({(part, r[0]): r[5] for r in rows})
         if part == "batch":
             lay["zero_bytes"] = off
     lay["total"] = off
-    lay["off"] = {(p, r[0]): r[3] for p in parts for r in lay[p]}
     return lay
 
 
-def _arena_tensors(buf, rows) -> dict:
-    return {name: buf[off:off + z].view(dt).view(shape) for name, dt, shape, off, z in rows}
+def _arena_tensors(typed, rows) -> dict:
+    """The arena's tensors: one as_strided view per array over the arena's typed views."""
+    import torch
+    st = torch.as_strided
+    return {name: st(typed[dt], shape, stride, item_off) for name, dt, shape, stride, item_off in rows}
+
+
+def _arena_typed(buf) -> dict:
+    import torch
+    return {dt: buf.view(dt) for dt in (torch.float64, torch.int64, torch.int32, torch.bool)}
 
 
 def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, imu_stamps, imu_gyro, imu_accel,
@@ -570,11 +585,14 @@ def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, i
     import torch
     from . import association as GA, primitive_map as GPM
     from .association import AtlasMapView
-    from .surfels import GC_VMF_N_LOBES, MeasurementBatch, _extractor_for
+    from .surfels import GC_VMF_N_LOBES, MeasurementBatch, _extractor_for, _extractors
     st = _live_chain_state(ctx, config)
     lib, a, lo = ctx.lib, st["args"], st["lo"]
     # the operator contexts (looked up per scan: another caller may have replaced a cached one)
-    ex = _extractor_for(st["scfg"], ctx.cfg.n_points_cap, config.device)
+    ex = st.get("ex")
+    if ex is None or ex.h is None or _extractors.get(st["ex_key"]) is not ex:
+        ex = st["ex"] = _extractor_for(st["scfg"], ctx.cfg.n_points_cap, config.device)
+        st["ex_key"] = next(k for k, v in _extractors.items() if v is ex)
     asc = GA._associator_for(st["N"], st["pool"], st["K"], config.device)
     a.surfels, a.assoc = ex.h.value, asc.h.value
     dev = f"cuda:{config.device}"
@@ -641,12 +659,13 @@ def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, i
         am.adopt_created(lo.created_ids[:lo.n_created], lo.created_slots[:lo.n_created])
     ctx._chk(rc, "gcs_live_scan")
     try:
-        bt = _arena_tensors(buf, lay["batch"])
+        typed = _arena_typed(buf)
+        bt = _arena_tensors(typed, lay["batch"])
         batch = MeasurementBatch(**bt, n_feat=config.n_feat, n_surfel=config.n_surfel, n_camera_valid=0,
                                  n_lidar_valid=0)
-        vt = _arena_tensors(buf, lay["view"])
+        vt = _arena_tensors(typed, lay["view"])
         view_tids = vt.pop("tile_ids")
-        a_out = _arena_tensors(buf, lay["assoc"])
+        a_out = _arena_tensors(typed, lay["assoc"])
         r = _live_chain_results(ctx, am, st, lo, o_sf, bo, out, batch, vt, view_tids, a_out, ao, scan_seq,
                                 scan_end_time, config)
         _stamp("live_results")

@@ -533,6 +533,8 @@ typedef struct {
   int32_t* cell_ids;     /* n_surfel       MA-hex cell of each slot (-1 past n_valid) */
   int32_t* bucket;       /* n_cells x max_occupants point indices (-1 padding) */
   int32_t* count;        /* n_cells        occupancy clipped to max_occupants */
+  int32_t* sources;      /* n_surfel       MeasurementBatch sources of the LiDAR slice: 1 on valid rows (the
+                            rows past n_valid are not written) */
   /* host results */
   double center[3];      /* the weighted centre the cells are hashed around (:264-267) */
   int32_t n_valid;       /* surfels in the LiDAR slice */
@@ -882,8 +884,10 @@ typedef struct {
   int32_t created_slots[GCS_LIVE_MAX_TILES];
   double recency_stats[3];                         /* gcs_pmap_recency_inflate's stats */
   double trigger_sum, ess_sum;                     /* the gcs_lidar_evidence handed to the finish */
-  double phase_us[6];   /* host clock since the call's entry: begin returned, surfel count read, pose evidence
-                           read, finish returned, step 12b queued; gcs_live_collect: [5] its wait */
+  double phase_us[12];  /* host clock since the call's entry: [0] begin returned, [1] surfels queued, [2] surfel
+                           count read, [3] recency / view / association queued, [4] pose evidence read, [5]
+                           finish returned, [6] step 12b queued; [7] gcs_live_collect's wait; [8] begin's
+                           mirror wait started (in begin) */
   /* after gcs_live_collect */
   gcs_pmap_update_stats update;
   int32_t counts[GCS_LIVE_MAX_TILES];              /* valid counts of the active tiles */

@@ -50,3 +50,22 @@ def test_visual_pose_evidence_empty_case():
     out, cert, eff = GA.visual_pose_evidence(res, gb, gv, z_lin_pose=np.zeros(6))
     assert cert.exact and eff.predicted == 0.0 and out.n_associations == 0
     assert np.array_equal(out.L_pose, 1e-9 * np.eye(22)) and not out.h_pose.any()
+
+
+@pytest.mark.parametrize("seed", [0, 5])
+def test_split_pose_evidence_bitwise(monkeypatch, seed):
+    """k_as_vpe_rows + the ordered fold (default) against the one-workgroup kernel (GCSLAM_VPE_SPLIT=0):
+    the same additions on the same values, so every output bit for bit."""
+    batch, view, _ = make_scene(seed=seed)
+    gb, gv = _batch(batch), _view(view)
+    res, _, _ = GA.associate_primitives_ot(gb, gv, GA.AssociationConfig(scan_seq=10))
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GCSLAM_VPE_SPLIT", flag)
+        a = GA.Associator(max_meas=1536, max_pool=7 * 1024, max_k=8)
+        try:
+            o = a.pose_evidence(gb, gv, res, 8, np.array([0.3, -0.1, 0.2, 0.05, -0.1, 0.4]))
+            outs.append(bytes(o))
+        finally:
+            a.close()
+    assert outs[0] == outs[1]

@@ -17,17 +17,24 @@ def main():
     import bench
     r = bench.live_path_bench(0, steps=steps)
     from gcslam import pipeline as P
-    if P.LIVE_STAMPS:  # GCSLAM_LIVE_STAMPS=1: mean us between consecutive phase stamps (calls of the chain path)
-        seq, acc, cnt = P.LIVE_STAMPS, {}, {}
-        for (a, ta), (b, tb) in zip(seq, seq[1:]):
-            k = f"{a}->{b}"
-            acc[k] = acc.get(k, 0.0) + (tb - ta) * 1e6
-            cnt[k] = cnt.get(k, 0) + 1
-        r["host_phases_us"] = {k: round(acc[k] / cnt[k], 1) for k in acc if cnt[k] >= 5}
+    if P.LIVE_STAMPS:  # GCSLAM_LIVE_STAMPS=1: mean us between the phase stamps of the timed chain calls
         import numpy as np
-        ph = np.array(P.LIVE_PHASES)
-        r["live_scan_phases_us"] = dict(zip(("begin", "surfels_read", "pose_evidence_read", "finish", "12b_queued",
-                                             "collect_wait"), np.round(ph.mean(0), 1).tolist()))
+        calls, cur = [], None
+        for name, t in P.LIVE_STAMPS:
+            if name == "enter":
+                cur = []
+                calls.append(cur)
+            cur.append((name, t))
+        timed = calls[10:10 + steps]  # live_path_bench: 10 warm-up calls, then `steps` timed chain calls
+        acc = {}
+        for c in timed:
+            for (a, ta), (b, tb) in zip(c, c[1:]):
+                acc.setdefault(f"{a}->{b}", []).append((tb - ta) * 1e6)
+        r["host_phases_us"] = {k: round(float(np.mean(v)), 1) for k, v in acc.items()}
+        ph = np.array(P.LIVE_PHASES[10:10 + steps])
+        names = ("begin", "surfels_queued", "surfels_read", "assoc_queued", "pose_evidence_read", "finish",
+                 "12b_queued", "collect_wait")
+        r["live_scan_phases_us"] = dict(zip(names, np.round(ph.mean(0)[:8], 1).tolist()))
     print(json.dumps(r), flush=True)
 
 
