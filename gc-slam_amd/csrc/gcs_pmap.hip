@@ -26,6 +26,7 @@
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -2501,9 +2502,18 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
   *(uint32_t*)(p->h_small + 8192) = 0u;
   const PmRows r = rows_of(rows);
   const int rb = (R + kPmThreads - 1) / kPmThreads;
-  // keys below n M nb, the skipped rows' key 2^bits - 1 above them: the sort needs only the low bits
-  unsigned bits = 1;
-  while (bits < 32 && ((double)(1ull << bits)) < (double)n * p->M * nb + 1.0) ++bits;
+  // GCSLAM_FUSE_SORT_BITS=1: keys below n M nb, the skipped rows' key 2^bits - 1 above them, sorted on
+  // the low bits only -- one onesweep pass fewer on the device, but measured ~35 us more host time per
+  // map update in the radix sort's dispatch (live path, profiles/r05/live): off by default
+  static const bool sig_bits = [] {
+    const char* e = getenv("GCSLAM_FUSE_SORT_BITS");
+    return e && atoi(e) != 0;
+  }();
+  unsigned bits = 32;
+  if (sig_bits) {
+    bits = 1;
+    while (bits < 32 && ((double)(1ull << bits)) < (double)n * p->M * nb + 1.0) ++bits;
+  }
   const uint32_t nokey = bits >= 32 ? kNoKey : (uint32_t)((1ull << bits) - 1ull);
   hipLaunchKernelGGL(k_pm_fuse_keys_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st,
                      (const int32_t*)p->d_tiles, timestamp, r, n, p->M, nb, rpb, p->fk, p->fv, p->bmark, d_err, nokey);

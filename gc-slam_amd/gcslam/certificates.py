@@ -121,26 +121,37 @@ def aggregate_certificates(certs: List[CertBundle]) -> CertBundle:
         return CertBundle.create_exact("GC-RIGHT-01", "unknown")
     t = certs[0]
     n = len(certs)
+    # one pass over the certs; every sum in list order from 0 and every min / max from the first cert,
+    # as the per-field generator expressions (sum(), min(), max()) take them
+    c0 = certs[0]
+    cd, sp, mm, inf = c0.conditioning, c0.support, c0.mismatch, c0.influence
+    exact, frob, trig = c0.exact, c0.frobenius_applied, list(c0.approximation_triggers)
+    e_min, e_max, cond, nn = cd.eig_min, cd.eig_max, cd.cond, 0 + cd.near_null_count
+    ess, sfr, nll, dsc = 0 + sp.ess_total, 0 + sp.support_frac, 0 + mm.nll_per_ess, 0 + mm.directional_score
+    ls, pd, nd = 0 + inf.lift_strength, 0 + inf.psd_projection_delta, 0 + inf.nu_projection_delta
+    me, ad, dts, ext, ta, pb = (inf.mass_epsilon_ratio, inf.anchor_drift_rho, inf.dt_scale, inf.extrinsic_scale,
+                                inf.trust_alpha, inf.power_beta)
+    for c in certs[1:]:
+        cd, sp, mm, inf = c.conditioning, c.support, c.mismatch, c.influence
+        exact = exact and c.exact
+        frob = frob or c.frobenius_applied
+        trig.extend(c.approximation_triggers)
+        e_min, e_max, cond = min(e_min, cd.eig_min), max(e_max, cd.eig_max), max(cond, cd.cond)
+        nn += cd.near_null_count
+        ess += sp.ess_total
+        sfr += sp.support_frac
+        nll += mm.nll_per_ess
+        dsc += mm.directional_score
+        ls += inf.lift_strength
+        pd += inf.psd_projection_delta
+        nd += inf.nu_projection_delta
+        me, ad = max(me, inf.mass_epsilon_ratio), max(ad, inf.anchor_drift_rho)
+        dts, ext = min(dts, inf.dt_scale), min(ext, inf.extrinsic_scale)
+        ta, pb = min(ta, inf.trust_alpha), min(pb, inf.power_beta)
     return CertBundle(
-        chart_id=t.chart_id, anchor_id=t.anchor_id, exact=all(c.exact for c in certs),
-        approximation_triggers=[x for c in certs for x in c.approximation_triggers],
-        frobenius_applied=any(c.frobenius_applied for c in certs),
-        conditioning=ConditioningCert(min(c.conditioning.eig_min for c in certs),
-                                      max(c.conditioning.eig_max for c in certs),
-                                      max(c.conditioning.cond for c in certs),
-                                      sum(c.conditioning.near_null_count for c in certs)),
-        support=SupportCert(sum(c.support.ess_total for c in certs) / n,
-                            sum(c.support.support_frac for c in certs) / n),
-        mismatch=MismatchCert(sum(c.mismatch.nll_per_ess for c in certs),
-                              sum(c.mismatch.directional_score for c in certs) / n),
-        influence=InfluenceCert(
-            lift_strength=sum(c.influence.lift_strength for c in certs),
-            psd_projection_delta=sum(c.influence.psd_projection_delta for c in certs),
-            nu_projection_delta=sum(c.influence.nu_projection_delta for c in certs),
-            mass_epsilon_ratio=max(c.influence.mass_epsilon_ratio for c in certs),
-            anchor_drift_rho=max(c.influence.anchor_drift_rho for c in certs),
-            dt_scale=min(c.influence.dt_scale for c in certs),
-            extrinsic_scale=min(c.influence.extrinsic_scale for c in certs),
-            trust_alpha=min(c.influence.trust_alpha for c in certs),
-            power_beta=min(c.influence.power_beta for c in certs)),
-    )
+        chart_id=t.chart_id, anchor_id=t.anchor_id, exact=bool(exact), approximation_triggers=trig,
+        frobenius_applied=bool(frob), conditioning=ConditioningCert(e_min, e_max, cond, nn),
+        support=SupportCert(ess / n, sfr / n), mismatch=MismatchCert(nll, dsc / n),
+        influence=InfluenceCert(lift_strength=ls, psd_projection_delta=pd, nu_projection_delta=nd,
+                                mass_epsilon_ratio=me, anchor_drift_rho=ad, dt_scale=dts, extrinsic_scale=ext,
+                                trust_alpha=ta, power_beta=pb))

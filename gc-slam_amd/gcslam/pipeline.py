@@ -198,6 +198,8 @@ def _certs_from_vector(c, io, chart, anchor, live_certs=None):
     cert vector and the eleven IMU/odometry certificate rows (DESIGN.md cert slots).  live_certs: the
     live path's map-branch + visual certs, which take the place of the bin path's LiDAR certs."""
     I = InfluenceCert
+    c = c.tolist() if hasattr(c, "tolist") else list(c)      # Python floats: no numpy scalar per field
+    io = io.tolist() if hasattr(io, "tolist") else list(io)
     certs = [
         CertBundle.create_approx(chart, anchor, ["PointBudgetResample"], support=SupportCert(c[0], c[1]),
                                  influence=I(mass_epsilon_ratio=c[2])),
@@ -207,7 +209,7 @@ def _certs_from_vector(c, io, chart, anchor, live_certs=None):
     ]
     for k, trig in enumerate(IMU_ODOM_CERTS):
         r = io[7 * k:7 * k + 7]
-        if not np.any(r):
+        if not any(r):
             continue   # branch disabled
         certs.append(CertBundle.create_approx(chart, anchor, list(trig), support=SupportCert(r[0], r[1]),
                                               mismatch=MismatchCert(nll_per_ess=r[2]),
@@ -279,7 +281,8 @@ def _stamp(name):
 
 def _as_device_scan(raw_points, raw_timestamps, raw_weights, device):
     """The node's parsed cloud (backend_node.py:1675-1690) as device inputs: xyz as the float32
-    PointCloud2 record the point kernel reads (x, y, z, pad), t and w f64."""
+    PointCloud2 records the point kernel reads ((x, y, z) from host arrays, (x, y, z, pad) from a
+    float32 (N, 4) tensor; point_step 4 x columns), t and w f64."""
     import torch
     if isinstance(raw_points, torch.Tensor) and raw_points.dim() == 2 and raw_points.shape[1] == 4 \
             and raw_points.dtype == torch.float32:
@@ -297,19 +300,20 @@ def _as_device_scan(raw_points, raw_timestamps, raw_weights, device):
         key = ("scan", device, n, stream.cuda_stream)
         ent = _pinned.get(key)
         if ent is None:
+            # xyz as compact float32 triples (point_step 12: one contiguous cast, not a strided one), then
+            # t and w (8-byte aligned at 16 n)
             hb = torch.empty(32 * n, dtype=torch.uint8).pin_memory()
             hn = hb.numpy()
             d = torch.empty(32 * n, dtype=torch.uint8, device=f"cuda:{device}")
-            ent = _pinned[key] = [hb, torch.cuda.Event(), (hn[:16 * n].view(np.float32).reshape(n, 4),
+            ent = _pinned[key] = [hb, torch.cuda.Event(), (hn[:12 * n].view(np.float32).reshape(n, 3),
                                                            hn[16 * n:24 * n].view(np.float64),
                                                            hn[24 * n:].view(np.float64)), d,
-                                  (d[:16 * n].view(torch.float32).view(n, 4), d[16 * n:24 * n].view(torch.float64),
+                                  (d[:12 * n].view(torch.float32).view(n, 3), d[16 * n:24 * n].view(torch.float64),
                                    d[24 * n:].view(torch.float64)), False]
         hb, ev, (hr, ht, hw), d, views, used = ent
         if used:
             ev.synchronize()  # the previous copy out of the staging buffer
-        hr[:, :3] = p  # PointCloud2 x,y,z are float32 (backend_node.py:377-468)
-        hr[:, 3] = 0.0
+        np.copyto(hr, p, casting="unsafe")  # PointCloud2 x,y,z are float32 (backend_node.py:377-468)
         ht[...] = ts
         hw[...] = ws
         d.copy_(hb, non_blocking=True)
@@ -372,7 +376,7 @@ def _process_scan_primitive(ctx: HypothesisContext, primitive_map, belief_prev, 
             stage_ms[name] = (now - clock[0]) * 1e3
             clock[0] = now
 
-    b = ctx.scan_begin(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
+    b = ctx.scan_begin(rec, 4 * rec.shape[1], t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
                        dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
                        odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
                        odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a, buffers=bufs)
@@ -469,7 +473,7 @@ def _live_chain_state(ctx: HypothesisContext, config: "PipelineConfig"):
     """gcs_live_scan's per-(context, config) arguments: the surfel / association contexts, the config
     structs and the fields of gcs_live_args that do not change between scans (cached on the context)."""
     from . import association as GA, primitive_map as GPM
-    from .surfels import SurfelExtractionConfig, _extractor_for
+    from .surfels import GC_VMF_N_LOBES, SurfelExtractionConfig
     key = (config.n_surfel, config.n_feat, config.surfel_voxel_size_m, config.surfel_min_points_per_voxel,
            config.eps_lift, config.eps_mass, config.eps_psd, config.k_assoc, config.k_sinkhorn, config.ot_epsilon,
            config.ot_tau_a, config.ot_tau_b, config.H_TILE, config.R_ACTIVE_TILES_XY, config.R_ACTIVE_TILES_Z,
@@ -516,8 +520,23 @@ def _live_chain_state(ctx: HypothesisContext, config: "PipelineConfig"):
     a.n_points = cap
     vpe = L.GcsVpeOutputs()
     a.vpe_out = C.addressof(vpe)
-    st = dict(key=key, scfg=scfg, ex=None, ex_key=None, pool=int(config.N_STENCIL_TILES) * int(config.M_TILE_VIEW), acfg=acfg,
-              arena=_live_arena(config, N, K), c_as=c_as, c_up=c_up, args=a, vpe=vpe, bufs=bufs, N=N, K=K,
+    lay = _live_arena(config, N, K)
+    off, s0 = lay["off"], config.n_feat
+    o_sf, o_v, ao = L.GcsSurfelOutputs(), L.GcsPmapView(), L.GcsAssocOutputs()
+    row = {"Lambdas": 72, "thetas": 24, "etas": 24 * GC_VMF_N_LOBES, "weights": 8, "timestamps": 8,
+           "colors": 24, "valid_mask": 1, "source_indices": 4}
+    ptr = [(o_sf, k, off[("batch", k)] + s0 * rb) for k, rb in row.items()]  # the batch's LiDAR slice
+    ptr += [(o_v, r[0], off[("view", r[0])]) for r in lay["view"][:-1]]
+    ptr += [(ao, r[0], off[("assoc", r[0])]) for r in lay["assoc"]]
+    ptr += [(a.meas, k, off[("batch", k)]) for k in ("Lambdas", "thetas", "etas", "weights", "valid_mask")]
+    ptr += [(a, "zero_dev", 0), (a, "lidar_sources_dev", off[("batch", "sources")] + 4 * s0),
+            (a, "batch_colors", off[("batch", "colors")]), (a, "batch_sources", off[("batch", "sources")]),
+            (a, "view_tile_ids_dev", off[("view", "tile_ids")])]
+    a.meas.n_total, a.meas.n_lobes, a.meas.n_valid = N, GC_VMF_N_LOBES, 0
+    a.zero_bytes = lay["zero_bytes"]
+    a.surfel_out, a.view, a.assoc_out = C.addressof(o_sf), C.addressof(o_v), C.addressof(ao)
+    st = dict(key=key, scfg=scfg, ex=None, ex_key=None, o_sf=o_sf, o_v=o_v, ao=ao, o_sf_ex=None, ptr_fields=ptr, pool=int(config.N_STENCIL_TILES) * int(config.M_TILE_VIEW), acfg=acfg,
+              arena=lay, c_as=c_as, c_up=c_up, args=a, vpe=vpe, bufs=bufs, N=N, K=K,
               lo=L.GcsLiveOutputs())
     ctx._live_chain = st
     return st
@@ -596,7 +615,7 @@ def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, i
     asc = GA._associator_for(st["N"], st["pool"], st["K"], config.device)
     a.surfels, a.assoc = ex.h.value, asc.h.value
     dev = f"cuda:{config.device}"
-    inp, keep = ctx._scan_inputs(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time,
+    inp, keep = ctx._scan_inputs(rec, 4 * rec.shape[1], t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time,
                                  scan_end_time, dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan,
                                  t_scan=t_scan, odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
                                  odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a)
@@ -618,27 +637,15 @@ def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, i
     # this scan's result arrays (the results keep them) in one allocation: pointers now, tensors after
     lay = st["arena"]
     buf = torch.empty(lay["total"], dtype=torch.uint8, device=dev)
-    base, off = buf.data_ptr(), lay["off"]
-    nt, s0 = st["N"], config.n_feat
-    row = {"Lambdas": 72, "thetas": 24, "etas": 24 * GC_VMF_N_LOBES, "weights": 8, "timestamps": 8,
-           "colors": 24, "valid_mask": 1, "source_indices": 4}
-    o_sf = L.GcsSurfelOutputs()
-    o_ex, _ = ex.outputs(False)
-    for k in ("positions", "covariances", "normals", "kappas", "cell_ids"):
-        setattr(o_sf, k, getattr(o_ex, k))
-    for k, rb in row.items():  # the batch's LiDAR slice
-        setattr(o_sf, k, base + off[("batch", k)] + s0 * rb)
-    o_v = L.GcsPmapView()
-    for name, *_ in lay["view"][:-1]:
-        setattr(o_v, name, base + off[("view", name)])
-    ao = L.GcsAssocOutputs()
-    for name, *_ in lay["assoc"]:
-        setattr(ao, name, base + off[("assoc", name)])
-    m = a.meas
-    m.Lambdas, m.thetas, m.etas, m.weights, m.valid_mask = (base + off[("batch", k)] for k in (
-        "Lambdas", "thetas", "etas", "weights", "valid_mask"))
-    m.n_total, m.n_lobes, m.n_valid = nt, GC_VMF_N_LOBES, 0
-    a.zero_dev, a.zero_bytes = base, lay["zero_bytes"]
+    base = buf.data_ptr()
+    o_sf, o_v, ao = st["o_sf"], st["o_v"], st["ao"]
+    if st["o_sf_ex"] is not ex:  # the extractor's own arrays (positions, covariances, normals, kappas, cell ids)
+        o_ex, _ = ex.outputs(False)
+        for k in ("positions", "covariances", "normals", "kappas", "cell_ids"):
+            setattr(o_sf, k, getattr(o_ex, k))
+        st["o_sf_ex"] = ex
+    for obj, name, o in st["ptr_fields"]:  # the arena's arrays in the argument structs
+        setattr(obj, name, base + o)
     ids, slots, free, written = am.directory()
     a.map = am.h.value
     a.n_tiles, a.tile_ids, a.tile_slots = len(ids), ids.ctypes.data, slots.ctypes.data
@@ -646,10 +653,6 @@ def _process_scan_live_chain(ctx: HypothesisContext, primitive_map, rec, t, w, i
     a.next_global_id = int(am.next_global_id)
     a.scan_seq = st["c_as"].scan_seq = int(scan_seq)
     a.timestamp = float(scan_end_time)
-    a.surfel_out = C.addressof(o_sf)
-    a.lidar_sources_dev = base + off[("batch", "sources")] + 4 * s0
-    a.batch_colors, a.batch_sources = base + off[("batch", "colors")], base + off[("batch", "sources")]
-    a.view, a.view_tile_ids_dev, a.assoc_out = C.addressof(o_v), base + off[("view", "tile_ids")], C.addressof(ao)
     out = L.GcsScanOutputs()
     _stamp("args")
     rc = lib.gcs_live_scan(ctx.h, in_ref, C.byref(bo), C.byref(a), C.byref(lo), C.byref(out))
@@ -794,7 +797,7 @@ def process_scan_single_hypothesis(belief_prev: BeliefGaussianInfo, raw_points, 
                                             t_last_scan, t_scan, Q, config, odom_twist, odom_twist_cov, scan_seq,
                                             L_ext, h_ext, update_map=update_map)
     else:
-        out = ctx.scan(rec, 16, t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
+        out = ctx.scan(rec, 4 * rec.shape[1], t, w, rec.shape[0], imu_stamps, imu_gyro, imu_accel, scan_start_time, scan_end_time,
                        dt_sec, Q=Q, L_ext=L_ext, h_ext=h_ext, t_last_scan=t_last_scan, t_scan=t_scan,
                        odom_pose=odom_pose, odom_cov_se3=odom_cov_se3, odom_twist=odom_twist,
                        odom_twist_cov=odom_twist_cov, Sigma_g=config.Sigma_g, Sigma_a=config.Sigma_a)
