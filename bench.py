@@ -759,9 +759,13 @@ def main():
         if not (rank == 0 and world > 1):
             follow = ctx.map_follow_call()
 
-    state = dict(count=0, sample=False, sampled=0, stamp=True, combine=combine)
     scan_out = L.GcsScanOutputs()  # one output record for every scan (the caller-owned buffer form)
     scan_fn = ctx.scan_call(scan_out)
+    # the step as one C call (gcs_scan_combine: scan + all-reduce combine, no Python between them);
+    # GCSLAM_BENCH_FUSED=0 times the two calls instead (also reported as a variant)
+    fused_on = os.environ.get("GCSLAM_BENCH_FUSED", "1") != "0" and follow is None
+    fused = ctx.scan_combine_call(scan_out, comm_h, w_iw, w_bary) if fused_on else None
+    state = dict(count=0, sample=False, sampled=0, stamp=True, combine=combine, fused=fused)
     # pre-device host, device submit+wait, host tail, whole gcs_scan, combine, then the sub-spans
     # (budget launch + predict, device launch calls, tail numerics, pushforward launch calls)
     host_ms = np.zeros(9)
@@ -778,11 +782,14 @@ def main():
                 ctx.enable_timing(True, stages=["bins"])
             elif phase == 1:
                 ctx.enable_timing(False)
-        scan_fn(prepared[state["count"] % N_SCANS])
+        if state["fused"] is not None:
+            dc = state["fused"](prepared[state["count"] % N_SCANS], state["count"])
+        else:
+            scan_fn(prepared[state["count"] % N_SCANS])
+            tc = time.perf_counter()
+            combine(state["count"])
+            dc = (time.perf_counter() - tc) * 1e3
         out = scan_out
-        tc = time.perf_counter()
-        combine(state["count"])
-        dc = (time.perf_counter() - tc) * 1e3
         if state["sample"]:
             comb_ms.append(dc)
         if state["count"] % TIMING_STRIDE == TIMING_STRIDE // 2:  # host sub-spans (stride 1: every scan)
@@ -845,10 +852,16 @@ def main():
     # combine instead of the world-1 RCCL all-reduce -- what round 4's line measured
     state["stamp"] = False
     variants = {"unstamped_ms_per_step": side_loop()}
+    if fused is not None:  # the same step as two C calls (gcs_scan, then gcs_combine_allreduce)
+        state["fused"] = None
+        variants["two_call_unstamped_ms_per_step"] = side_loop()
     if world == 1 and comm is not None:
         state["combine"] = ctx.combine_call(None, w_iw, w_bary)
+        if fused is not None:
+            state["fused"] = ctx.scan_combine_call(scan_out, None, w_iw, w_bary)
         variants["host_combine_unstamped_ms_per_step"] = side_loop()
         state["combine"] = combine
+    state["fused"] = fused
     state["stamp"] = True
     # the roofline kernel's duration: the timed region's stamped launches (every TIMING_STRIDE-th scan)
     # plus, when those are fewer than ROOFLINE_MIN (short runs), a pass stamping it on every scan
@@ -914,9 +927,12 @@ def main():
             "per_rank": per_rank,
             "rccl": rccl,
             "mirror": mirror,
-            "step_variants": dict(variants, note="the same step count again after the timed region, not `value`: "
-                                  "without the roofline kernel's event stamps, and (N = 1) with the host-only "
-                                  "combine in place of the world-1 ncclAllReduce"),
+            "step_variants": dict(variants, step_call="gcs_scan_combine (one C call)" if fused is not None
+                                  else "gcs_scan + gcs_combine_allreduce",
+                                  note="the same step count again after the timed region, not `value`: "
+                                  "without the roofline kernel's event stamps, as two C calls (scan, then "
+                                  "combine), and (N = 1) with the host-only combine in place of the world-1 "
+                                  "ncclAllReduce"),
             "step_ms": {"median": float(np.median(per_step) * 1e3), "p90": float(np.percentile(per_step, 90) * 1e3),
                         "min": float(per_step.min() * 1e3), "max": float(per_step.max() * 1e3)},
             "roofline": dict(roofline(N, B, bins_ms, *pmc_traffic(args.config)) or {}, timed_launches=bins_samples,

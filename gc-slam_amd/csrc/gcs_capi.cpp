@@ -2697,6 +2697,18 @@ int gcs_rccl_comm_count(void* comm, int32_t* count, int32_t* user_rank) {
 }
 
 int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, int32_t scan_count,
+                          gcs_belief* comb, double* cert);
+
+int gcs_scan_combine(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out, void* comm, double w_iw,
+                     double w_bary, int32_t scan_count, gcs_belief* comb, double* cert, double* combine_ms) {
+  if (int rc = gcs_scan(c, in, out)) return rc;
+  const clk::time_point t0 = clk::now();
+  const int rc = gcs_combine_allreduce(c, comm, w_iw, w_bary, scan_count, comb, cert);
+  if (combine_ms) *combine_ms = ms_between(t0, clk::now());
+  return rc;
+}
+
+int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, int32_t scan_count,
                           gcs_belief* comb, double* cert) {
   if (!c) return GCS_ERR_ARG;
   constexpr int kLen = GCS_PAYLOAD_LEN + GCS_MAP_REC_LEN;

@@ -312,6 +312,8 @@ _SIGS = [
     ("gcs_rccl_broadcast", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.c_int32, C.c_void_p]),
     ("gcs_combine_allreduce", C.c_int, [C.c_void_p, C.c_void_p, C.c_double, C.c_double, C.c_int32, C.c_void_p,
                                         C.c_void_p]),
+    ("gcs_scan_combine", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(GcsScanOutputs), C.c_void_p, C.c_double,
+                                   C.c_double, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("gcs_process_iw_apply", C.c_int, [c_double_p] * 7),
     ("gcs_process_noise_Q", C.c_int, [c_double_p] * 3),
     ("gcs_meas_iw_mode", C.c_int, [c_double_p, c_double_p, C.c_int32, c_double_p]),

@@ -449,6 +449,20 @@ class HypothesisContext:
                 self._chk(rc, "combine_allreduce")
         return call
 
+    def scan_combine_call(self, out, comm, w_iw, w_bary):
+        """gcs_scan_combine (gcs_scan + gcs_combine_allreduce in one C call) bound once: returns
+        call(prepared, scan_count) -> the combine's host ms, raising on failure."""
+        fn, h, po = self.lib.gcs_scan_combine, self.h, C.byref(out)
+        cert, cms = (C.c_double * 4)(), C.c_double()
+        comm, w_iw, w_bary, pc = comm, float(w_iw), float(w_bary), C.byref(cms)
+
+        def call(prepared, scan_count):
+            rc = fn(h, prepared[1], po, comm, w_iw, w_bary, scan_count, None, cert, pc)
+            if rc:
+                self._chk(rc, "gcs_scan_combine")
+            return cms.value
+        return call
+
     def hypothesis_combine(self, payload_sum, scan_count, want_belief=True):
         """Barycenter + IW update from the summed payload; returns (belief arrays or None, cert)."""
         p = np.ascontiguousarray(payload_sum, np.float64)

@@ -456,6 +456,11 @@ int gcs_rccl_comm_count(void* comm, int32_t* count, int32_t* user_rank);
  * (gcslam.distributed.MapRecordChannel, ~0.5 MB at the reference sizes) from the lead to the ranks
  * that replay it (backend_node.py:2079-2083). */
 int gcs_rccl_broadcast(void* comm, void* buf, int64_t bytes, int32_t root, void* stream);
+/* gcs_scan then gcs_combine_allreduce in one call (the node's per-scan step, backend_node.py:2036-2119,
+ * without a caller round trip between them); combine_ms (may be NULL): the combine's host wall time. */
+int gcs_scan_combine(gcs_ctx* ctx, const gcs_scan_inputs* in, gcs_scan_outputs* out, void* comm, double w_iw,
+                     double w_bary, int32_t scan_count, gcs_belief* combined_out, double* cert /*4*/,
+                     double* combine_ms);
 int gcs_combine_allreduce(gcs_ctx* ctx, void* comm, double w_iw, double w_bary, int32_t scan_count,
                           gcs_belief* combined_out /*may be NULL*/, double* cert4 /*may be NULL*/);
 
