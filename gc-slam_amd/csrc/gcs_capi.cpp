@@ -88,6 +88,9 @@ struct gcs_ctx {
   gcs_scan_outputs* live_out = nullptr;
   bool live_pending = false;
   gcs_pmap* live_map = nullptr;  // gcs_live_scan: the map whose step 12b gcs_live_collect has to read
+  // gcs_live_scan hands step 12b's launch calls (~20 kernels) to the worker thread and returns while it
+  // makes them (GCSLAM_LIVE_ASYNC=0: inline); gcs_live_collect waits for the worker first
+  bool live_async = true;
   bool begin_mirror = true;      // gcs_scan_begin reads the point fold's mirror (GCSLAM_BEGIN_MIRROR=0: copies)
   uint32_t *d_keys = nullptr, *d_slots = nullptr, *d_sorted = nullptr;
   int* d_nearest = nullptr;
@@ -165,6 +168,15 @@ struct gcs_ctx {
     uint8_t* flags;
     BudgetArgs ba;
     int nblk;
+    // 3: the live path's step 12b (gcs_live_scan): the new tiles' clears and the map update's launches
+    gcs_pmap* pm;
+    int32_t n12, ncl;
+    int32_t tiles12[GCS_LIVE_MAX_TILES], clear12[GCS_LIVE_MAX_TILES];
+    int64_t tids12[GCS_LIVE_MAX_TILES];
+    double ts12;
+    int64_t seq12, next12;
+    gcs_pmap_update_config ucfg;
+    gcs_pmap_update_inputs uin;
   };
   // a ring of two job slots: a submission waits only while both are taken, so the next scan's front
   // queues behind the last scan's pushforward launches instead of waiting for them
@@ -878,6 +890,12 @@ void push_worker(gcs_ctx* c) {
       } else if (j.kind == 2) {
         rc = scan_front(c, j.in, j.seq);
         if (rc) msg = "scan front launch (worker): " + t_fail_msg;
+      } else if (j.kind == 3) {
+        for (int k = 0; k < j.ncl && !rc; ++k) rc = live::pmap_clear_tile_launch(j.pm, j.clear12[k]);
+        if (!rc)
+          rc = live::pmap_update_launch(j.pm, j.tiles12, j.tids12, j.n12, j.z_t, j.ts12, j.seq12, j.next12, &j.ucfg,
+                                        &j.uin);
+        if (rc) msg = "gcs_pmap_map_update (live path, worker): " + std::string(gcs_pmap_last_error(j.pm));
       } else {
         rc = stage_push(c, j.z_t, j.Sig6, j.gamma, j.s, j.partials, j.flags, true);
         if (rc) msg = "pushforward launch (worker): " + t_fail_msg;
@@ -1184,6 +1202,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (const char* g = getenv("GCSLAM_DEVICE_PREINT")) c->device_preint = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_PT_CLEAR")) c->pt_clear = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_BEGIN_MIRROR")) c->begin_mirror = atoi(g) != 0;
+  if (const char* g = getenv("GCSLAM_LIVE_ASYNC")) c->live_async = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_BUDGET_BLOCKS")) c->budget_max = std::max(1, std::min(1024, atoi(g)));
   if (bad(hipHostMalloc(&c->h_preint_out, 16 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent)))
     return GCS_ERR_HIP;
@@ -2500,6 +2519,47 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   if ((rc = gcs_scan_finish(c, &ev, out))) return rc;
   mark(5);
   // step 12b at z_t over the active tiles (:1232-1492); new tiles on written slots start cleared
+  if (c->live_async && c->push_async) {  // the launch calls on the worker: the caller builds its results meanwhile
+    if (!c->push_thread.joinable()) c->push_thread = std::thread(push_worker, c);
+    gcs_ctx::PushJob& j = claim_job(c);
+    j.kind = 3;
+    j.pm = pm;
+    j.n12 = na;
+    j.ncl = ncl;
+    memcpy(j.tiles12, lo->active_slots, sizeof(int32_t) * na);
+    memcpy(j.tids12, lo->active_ids, sizeof(int64_t) * na);
+    memcpy(j.clear12, clear, sizeof(int32_t) * ncl);
+    memcpy(j.z_t, out->z_t, sizeof(j.z_t));
+    j.ts12 = a->timestamp;
+    j.seq12 = a->scan_seq;
+    j.next12 = a->next_global_id;
+    j.ucfg = *a->update_cfg;
+    gcs_pmap_update_inputs& ui = j.uin;
+    ui = gcs_pmap_update_inputs{};
+    ui.Lambdas = m.Lambdas;
+    ui.thetas = m.thetas;
+    ui.etas = m.etas;
+    ui.weights = m.weights;
+    ui.valid = m.valid_mask;
+    ui.colors = a->batch_colors;
+    ui.sources = a->batch_sources;
+    ui.n_total = m.n_total;
+    ui.n_lobes = m.n_lobes;
+    ui.responsibilities = ao->responsibilities;
+    ui.candidate_tile_ids = ao->candidate_tile_ids;
+    ui.candidate_slots = ao->candidate_slots;
+    ui.row_masses = ao->row_masses;
+    ui.k_assoc = a->assoc_cfg->k_assoc;
+    c->push_req.fetch_add(1);
+    if (c->push_sleeping.load()) {
+      std::lock_guard<std::mutex> lk(c->push_mu);
+      c->push_cv.notify_one();
+    }
+    lo->next_global_id = a->next_global_id;
+    c->live_map = pm;
+    mark(6);
+    return GCS_OK;
+  }
   for (int k = 0; k < ncl; ++k)
     if ((rc = live::pmap_clear_tile_launch(pm, clear[k]))) return sub_fail(c, rc, "gcs_pmap_clear_tile", gcs_pmap_last_error(pm));
   gcs_pmap_update_inputs ui{};
@@ -2532,6 +2592,7 @@ int gcs_live_collect(gcs_ctx* c, gcs_live_outputs* lo) {
   gcs_pmap* pm = c->live_map;
   c->live_map = nullptr;
   const clk::time_point t_in = clk::now();
+  if (int rc = push_wait(c)) return rc;  // step 12b's launch calls (worker)
   if (int rc = live::pmap_update_collect(pm, &lo->next_global_id, &lo->update, lo->counts))
     return sub_fail(c, rc, "gcs_pmap_map_update", gcs_pmap_last_error(pm));
   lo->phase_us[7] = 1e3 * ms_between(t_in, clk::now());
