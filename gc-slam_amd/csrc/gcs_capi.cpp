@@ -199,6 +199,8 @@ struct gcs_ctx {
   // GCS_DEBUG_DEVICE_PREINT; not with the launch gate): the prologue stages the IMU window in pinned
   // memory and queues k_preint, k_points reads its twist, the tail reads its record after the sync
   bool device_preint = false;
+  hipEvent_t ev_preint = nullptr;  // recorded after each k_preint: its window and record are not touched before it
+  bool ev_preint_pending = false;
   bool preint_pending = false;       // the next point stage reads the device twist (d_gate_xi)
   bool preint_host_pending = false;  // st.xi / st.pre / cert[10] still to be read from h_preint_out
   double* h_preint_in = nullptr;     // pinned: the staged window (7 doubles per sample)
@@ -1311,6 +1313,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
     for (hipEvent_t e : c->ev[st]) (void)hipEventDestroy(e);
   if (c->ev_push) (void)hipEventDestroy(c->ev_push);
   if (c->ev_stages) (void)hipEventDestroy(c->ev_stages);
+  if (c->ev_preint) (void)hipEventDestroy(c->ev_preint);
   if (c->push_stream) (void)hipStreamDestroy(c->push_stream);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c->scan_st;
@@ -1754,8 +1757,14 @@ int launch_device_preint(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& 
   int r = m - 1;
   while (r > 0 && in->imu_stamps[r - 1] == in->imu_stamps[r]) --r;
   const int me = r + 1;
+  // the previous k_preint may still read the window (a scan that failed after queuing it): wait for it
+  // before the window is rewritten or freed
+  if (c->ev_preint_pending) {
+    HIPCHK(c, hipEventSynchronize(c->ev_preint));
+    c->ev_preint_pending = false;
+  }
   if (c->preint_in_cap < 7 * (int64_t)me) {
-    if (c->h_preint_in) (void)hipHostFree(c->h_preint_in);  // (the last scan's k_preint has completed)
+    if (c->h_preint_in) (void)hipHostFree(c->h_preint_in);
     c->h_preint_in = nullptr;
     c->preint_in_cap = 0;
     const int64_t cap = 7 * (int64_t)std::max(me, 512);
@@ -1784,6 +1793,9 @@ int launch_device_preint(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& 
   a.xi_dev = c->d_gate_xi;
   a.host_out = c->h_preint_out;
   HIPCHK(c, launch_preint(a, c->stream));
+  if (!c->ev_preint) HIPCHK(c, hipEventCreateWithFlags(&c->ev_preint, hipEventDisableTiming));
+  HIPCHK(c, hipEventRecord(c->ev_preint, c->stream));
+  c->ev_preint_pending = true;
   c->preint_pending = true;
   c->preint_host_pending = true;
   return GCS_OK;
@@ -1793,6 +1805,12 @@ int launch_device_preint(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& 
 void finish_preint(gcs_ctx* c, gcs_scan_state& st) {
   if (!c->preint_host_pending) return;
   c->preint_host_pending = false;
+  // k_preint's record is read after its own completion event (the mirror that precedes this call is
+  // a later kernel's; the event makes the order explicit and costs a query once it has fired)
+  if (c->ev_preint_pending) {
+    if (hipEventQuery(c->ev_preint) != hipSuccess) (void)hipEventSynchronize(c->ev_preint);
+    c->ev_preint_pending = false;
+  }
   const volatile double* o = c->h_preint_out;
   for (int k = 0; k < 6; ++k) st.xi[k] = o[k];
   st.pre.ess = o[6];

@@ -510,8 +510,15 @@ __global__ __launch_bounds__(NT) void k_pm_select_reg(const uint64_t* __restrict
 // index plus the count of the other run's smaller entries (binary search in LDS).  Runs live in
 // run_key / run_slot at the first leaf of their node (k entries per leaf); the writer's stores are
 // released (agent-scope fence, barrier) before its ticket, the second arrival acquires before reading.
+// GCS_TOPK_SC1 (default): the write-through run hand-off of cdna_hip_programming.md Guideline 16.
+// Hardware assumption (gfx950, not promised by the HIP / HSA memory model): agent-scope relaxed atomic
+// stores of the run go to the shared L2 (sc1) and complete before the storing wave passes
+// s_waitcnt vmcnt(0), so a relaxed ticket add after the workgroup barrier orders them for the second
+// arrival, whose one agent-scope acquire drops its CU's stale lines before it reads the run.  Checked
+// under repetition by tests/test_gpu_primitive_map.py::test_topk_tree_handoff_stress (24 views of seven
+// dense 50,000-slot tiles against the oracle's stable top-k); GCS_TOPK_SC1=0 builds the acq_rel ticket.
 #ifndef GCS_TOPK_SC1
-#define GCS_TOPK_SC1 1  // write-through run hand-off (0: the acq_rel ticket, for A/B)
+#define GCS_TOPK_SC1 1
 #endif
 constexpr int kTopEpt = 4;                  // slots per thread in a leaf
 constexpr int kTopChunk = kTopEpt * kPmRed;  // slots per leaf: 4,096 (13 leaves, 4 merge levels at 50,000)

@@ -452,3 +452,35 @@ def test_full_sort_path_matches_oracle():
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, GCSLAM_PM_FULLSORT="1"),
                        capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_topk_tree_handoff_stress():
+    """The tree top-k's run hand-off between workgroups (k_pm_topk, GCS_TOPK_SC1: write-through stores,
+    a relaxed ticket and one acquire by the second arrival; cdna_hip_programming.md Guideline 16) under
+    repetition: 24 views of seven dense 50,000-slot tiles with fresh weights each time (ties included),
+    every candidate slot against the oracle's stable top-k (primitive_map.py:303-322).  A stale run
+    handed to the next merge level would show as a wrong or duplicated slot."""
+    from gcslam import primitive_map as gpm
+    rng = np.random.default_rng(77)
+    m, kv, n_t = 50_000, 1024, 7
+    am = gpm.AtlasMap(m_tile=m, max_tiles=8, n_lobes=NL, max_merge=0)
+    tids = [1000 + 3 * k for k in range(n_t)]
+    base = {t: _rand_tile(rng, m=m, frac=0.8, seq_hi=30) for t in tids}
+    for t in tids:
+        am.write_tile(t, base[t])
+    try:
+        for rep in range(24):
+            w = {}
+            for t in tids:
+                ww = rng.random(m)
+                if rep % 3 == 0:
+                    ww = np.round(ww * 64) / 64.0  # many exact ties: the slot order decides
+                w[t] = ww
+                am.write_tile(t, {"weights": ww})
+            view = gpm.extract_atlas_map_view(am, tids, kv)
+            got = view.candidate_slots.detach().cpu().numpy().reshape(n_t, kv)
+            for i, t in enumerate(tids):
+                ref = opm.select_topk_slots(w[t], base[t]["valid_mask"], kv)
+                assert np.array_equal(got[i], ref), (rep, t, np.flatnonzero(got[i] != ref)[:8])
+    finally:
+        am.close()
