@@ -27,6 +27,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <string>
 
 #include "gcs_math.h"
@@ -75,6 +76,12 @@ constexpr int kShThreads = GCS_SH_THREADS;
 #ifndef GCS_SH_LOGA
 #define GCS_SH_LOGA 1  // 0: u = pow(a / Kv, ua) with the quotient in every iteration (A/B)
 #endif
+#ifndef GCS_SH_DPP
+#define GCS_SH_DPP 1  // 0: the Sinkhorn's reduce-scatter through ds_bpermute xor shuffles (A/B)
+#endif
+#ifndef GCS_SH_ROOT
+#define GCS_SH_ROOT 1  // 0: no Newton root for exponents 1 / n (the log / exp tables every iteration; A/B)
+#endif
 constexpr int kShCR = 16 * 1024 / kShThreads;  // Sinkhorn row capacity: N <= kShCR * kShThreads / KM
 constexpr int kMaxStencil = 64;
 // GCS_SH_PROBE (timing probe builds only): wall-clock stamps of the Sinkhorn's phases, printed by the
@@ -105,6 +112,8 @@ struct AsParams {
   int n, m_view, m_shift, n_tiles, n_stencil, k, iters, m_pool;
   int s_center;  // the stencil entry (0, 0, 0): the row's own tile
   int a_policy, row_min, med;
+  int fin_split;  // the finish (pi, responsibilities, certificate sums): GCS_SH_FINSPLIT's modes
+  unsigned epoch; // this launch's hand-off value of the Sinkhorn's flag (never 0)
   double beta, eps, tau_a, tau_b, eps_mass, eps_lift, eps_dir, h, lam, eps_lam;
   long long scan_seq;
 };
@@ -115,6 +124,18 @@ struct AsWork {
   int32_t* cand;
   uint32_t* mvalid;       // this call's valid-entry count (k_as_prep adds, the Sinkhorn reads)
   uint32_t* mvalid_next;  // the next call's (zeroed by this call's Sinkhorn workgroup 0)
+  float4* vc;             // k_as_stage: each view tile's valid entries, (x, y, z, slot) in f32 (k_as_pool_lds)
+  int32_t* vcnt;          // k_as_stage: valid entries per view tile
+  int32_t* order;         // k_as_stage: rows grouped by bucket, each bucket padded to a chunk (-1)
+  int32_t *ctile, *cpre;  // k_as_stage: per chunk, its stencil tiles and the prefix of their valid counts (64 each)
+  uint32_t* tcnt;         // k_as_prep: valid entries per view tile (read and re-armed by k_as_stage)
+  double* kmat;           // the pools: K_mat = exp(-C / eps) beside the cost (read by the Sinkhorn when the
+                          // median scaling is off: the exps run on the whole grid, not one workgroup)
+  int chunk;              // rows per k_as_pool_lds workgroup (0: the buckets are not used)
+  double* su;             // the Sinkhorn's scalings for k_as_finish: u (N), v (KM), sum a
+  double* fpart;          // k_as_finish: per workgroup, its rows' certificate sums (7 + KM)
+  uint32_t* ticket;       // k_as_finish: workgroups done (the last folds; re-armed by it)
+  uint32_t* flag;         // the Sinkhorn workgroup's u / v hand-off to the finish workgroups (= epoch)
 };
 
 struct AsIn {
@@ -266,13 +287,31 @@ __global__ __launch_bounds__(kAsThreads) void k_as_prep(AsIn in, AsParams p, AsW
         for (int j = 0; j < 8; ++j) hit[j] = v == id[j] ? q : hit[j];
       }
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < 8; ++j) {
         if (s0 + j < p.n_stencil) w.tix[(size_t)i * p.n_stencil + s0 + j] = hit[j];
+      }
     }
-  } else if (g < p.n + p.m_pool) {
-    const int e = g - p.n;
-    w.A2[e] = a_vmf(fmax(in.vkap[e], kEigMin));
-    if (in.vvalid[e]) atomicAdd(w.mvalid, 1u);  // integer count (order-free)
+  }
+  // the view lanes: A_vmf of the entry's kappa; the valid count (and per view tile, for k_as_stage's
+  // chunk records), one integer add per wave and tile (order-free)
+  const int e = g - p.n;
+  const bool vl = g >= p.n && g < p.n + p.m_pool;
+  const bool vv = vl && in.vvalid[e] != 0;
+  if (vl) w.A2[e] = a_vmf(fmax(in.vkap[e], kEigMin));
+  const unsigned long long vm = __ballot(vv);
+  const int lane = threadIdx.x & 63;
+  if (vm != 0ull) {
+    const int first = __ffsll((long long)vm) - 1;
+    if (lane == first) atomicAdd(w.mvalid, (unsigned)__popcll(vm));
+    if (w.chunk) {
+      const int te = vv ? e / p.m_view : -1;
+      const int t0 = __shfl(te, first, 64);
+      if (__ballot(vv && te != t0) == 0ull) {
+        if (lane == first) atomicAdd(&w.tcnt[t0], (unsigned)__popcll(vm));
+      } else if (vv) {
+        atomicAdd(&w.tcnt[te], 1u);
+      }
+    }
   }
 }
 
@@ -544,11 +583,534 @@ __global__ __launch_bounds__(kPoolThreads) void k_as_pool(AsIn in, AsParams p, A
     if (p.row_min) c = c - mn;
     const size_t o_ = (size_t)i * p.k + lane;
     o.cost[o_] = c;
+    if (!p.med) w.kmat[o_] = exp(-c / fmax(p.eps, 1e-12));  // (the Sinkhorn's own expression)
     w.cand[o_] = e;
     w.dt[o_] = dt;
     if (o.cand) o.cand[o_] = e;
     if (o.tile) o.tile[o_] = in.vtile[e];
     if (o.slot) o.slot[o_] = (int64_t)in.vslot[e];
+  }
+}
+
+// The pool by center-tile bucket (GCS_POOL_LDS).  Rows whose own tile is view tile c share their
+// stencil's view tiles (the stencil is a fixed offset set around the row's cell), so the rows are
+// grouped by c (k_as_stage lays them out, each bucket padded to a chunk of kPoolLdsWaves rows) and a
+// workgroup of kPoolLdsWaves waves stages its chunk's stencil tiles in LDS once and each wave selects
+// one row's K candidates from them (k_as_pool, one workgroup per row, re-read 25 B per entry from L2
+// for every row).  The staged tiles hold only their VALID entries (k_as_stage compacts each view tile:
+// f32 position + the entry's slot in the tile, 16 B), so a row's pass visits the ~30 % of the pool
+// that can be selected.  Invalid entries and missing tiles carry the invalid cost (1e12) and enter
+// the selection only when fewer than K valid entries cost less than that: the row's K-th selected key
+// then reaches order_key(1e12) and the row is selected again over every pool position, exactly as
+// k_as_pool does (a rare slow path).  Rows whose own tile is not in the view (bucket -1) or stencils
+// too large for LDS read the compacted table from L2.
+//
+// The f32 distances only prune; what is selected is decided on the exact f64 costs, so the
+// candidates are k_as_pool's (bit-exact indices).  With m32, v32 the f32 roundings (2^-24 relative
+// per axis), |v| <= |m| + |m - v|, the f32 difference and sum of squares (a few 2^-24 relative), the
+// exact distance de and the table distance da = sqrt(d32) satisfy, with E = 2^-20 |m|_1 + 1e-30:
+//   de <= (da + E)(1 + 2^-19),  de >= (da - E)(1 - 2^-19)   (margins ~4x the rounding terms).
+// The bound D (an upper bound of the row's K-th smallest valid d_pos) comes from upper bounds of the
+// table distances (an order statistic of entrywise upper bounds bounds the exact one); an entry is
+// pruned only when its lower bound exceeds D + beta (threshold rounded up into f32); the list-max skip
+// uses the exact d_pos.  One wave per row: the lists' merge needs no block barrier.
+#ifndef GCS_POOL_LDS
+#define GCS_POOL_LDS 1
+#endif
+constexpr int kPoolLdsWaves = 8;
+constexpr int kLRing = 256;  // per wave: >= 63 pending + kLdsPB x 64 appended per trip
+constexpr int kLdsPB = 2;
+constexpr int kPoolLdsMaxView = (160 * 1024 - kPoolLdsWaves * kLRing * 8) / 16;  // 9,216 stencil slots
+constexpr int kMaxBuckets = 4096;
+constexpr int kBucketRows = 4;
+// GCS_POOL_PROBE (timing probe builds only): per row, wall-clock stamps of k_as_pool_lds's phases
+// (block start, staged, pass 1, ring + costing, merge, slow path, end) and the ring count, printed by
+// the host collect (stderr)
+#ifndef GCS_POOL_PROBE
+#define GCS_POOL_PROBE 0
+#endif
+#if GCS_POOL_PROBE
+__device__ unsigned long long g_pool_probe[4096 * 10];
+#define PP_STAMP(k) do { if (lane == 0) g_pool_probe[(size_t)i * 10 + (k)] = wall_clock64(); } while (0)
+#else
+#define PP_STAMP(k) do { } while (0)
+#endif  // rows per k_as_stage thread: <= 4,096 rows (the Sinkhorn caps them at 2,048)
+
+// workgroups 0..n_tiles-1: view tile b's valid entries in slot order (a block scan of wave ballots)
+// into vc[b MV ..] as (x, y, z, slot) in f32, their count in vcnt[b].  Workgroup n_tiles: each row's
+// slot in its bucket (LDS counters), bucket b's padded start (exclusive scan of ceil(count / chunk) x
+// chunk), the order list (-1 everywhere first), every row at its bucket's start + its slot.
+__global__ __launch_bounds__(1024) void k_as_stage(AsIn in, AsParams p, AsWork w, int nb, int cap) {
+  __shared__ uint32_t s_wsum[16];
+  __shared__ uint32_t s_cnt[kMaxBuckets];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int MV = p.m_view;
+  if ((int)blockIdx.x < p.n_tiles) {
+    const int tb = blockIdx.x;
+    uint32_t base = 0;
+    for (int c0 = 0; c0 < MV; c0 += 1024) {
+      const int oo = c0 + t;
+      const size_t e = (size_t)tb * MV + oo;
+      const bool v = oo < MV && in.vvalid[e] != 0;
+      const unsigned long long bm = __ballot(v);
+      if (lane == 0) s_wsum[wid] = (uint32_t)__popcll(bm);
+      __syncthreads();
+      uint32_t off = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull)), tot = 0;
+      for (int q = 0; q < 16; ++q) {
+        const uint32_t c = s_wsum[q];
+        if (q < wid) off += c;
+        tot += c;
+      }
+      if (v)
+        w.vc[(size_t)tb * MV + off] = make_float4((float)in.vpos[3 * e], (float)in.vpos[3 * e + 1],
+                                                  (float)in.vpos[3 * e + 2], (float)oo);
+      base += tot;
+      __syncthreads();  // (s_wsum is rewritten by the next chunk)
+    }
+    if (t == 0) w.vcnt[tb] = (int32_t)base;
+    return;
+  }
+  const int C = w.chunk, S = p.n_stencil;
+  constexpr int kPer = kMaxBuckets / 1024;
+  __shared__ uint32_t s_tc[kMaxBuckets];  // valid entries per view tile
+  for (int b = t; b < nb; b += 1024) s_cnt[b] = 0u;
+  for (int q = t; q < cap; q += 1024) w.order[q] = -1;
+  __syncthreads();
+  for (int b = t; b < p.n_tiles; b += 1024) {  // k_as_prep's per-tile valid counts, re-armed for the next call
+    s_tc[b] = w.tcnt[b];
+    w.tcnt[b] = 0u;
+  }
+  int rb[kBucketRows];
+  uint32_t rs[kBucketRows];
+#pragma unroll
+  for (int j = 0; j < kBucketRows; ++j) {
+    const int i = t + j * 1024;
+    rb[j] = 0;
+    rs[j] = 0u;
+    if (i < p.n) {
+      rb[j] = (p.s_center >= 0 ? w.tix[(size_t)i * S + p.s_center] : -1) + 1;
+      rs[j] = atomicAdd(&s_cnt[rb[j]], 1u);  // (arrival order: any -- each row's result is its own)
+    }
+  }
+  __syncthreads();
+  uint32_t pc[kPer], mine = 0;
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int b = t * kPer + q;
+    pc[q] = b < nb ? (s_cnt[b] + (uint32_t)C - 1u) / (uint32_t)C * (uint32_t)C : 0u;
+    mine += pc[q];
+  }
+  uint32_t inc = mine;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)inc, off, 64);
+    if (lane >= off) inc += y;
+  }
+  if (lane == 63) s_wsum[wid] = inc;
+  __syncthreads();
+  uint32_t run = inc - mine;
+  for (int v = 0; v < wid; ++v) run += s_wsum[v];
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int b = t * kPer + q;
+    if (b < nb) s_cnt[b] = run << 12;  // (the bucket's first slot in the order list)
+    run += pc[q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kBucketRows; ++j) {
+    const int i = t + j * 1024;
+    if (i < p.n) w.order[(s_cnt[rb[j]] >> 12) + rs[j]] = i;
+  }
+  __syncthreads();
+  // every chunk's record -- its stencil tiles (its first row's tix: rows of a bucket share them) and
+  // the inclusive prefix of their valid counts -- so k_as_pool_lds reads one record and the compacted
+  // entries (two round trips).  One (chunk, slot) per thread and pass: the loads of a pass are
+  // independent (no store between them)
+  const int nch = cap / C, np = nch * S;
+  for (int q = t; q < np; q += 1024) {
+    const int c = q / S, sq = q - c * S;
+    const int row = w.order[c * C];
+    w.ctile[(size_t)c * 64 + sq] = row >= 0 ? w.tix[(size_t)row * S + sq] : -1;
+  }
+  __syncthreads();
+  for (int q = t; q < np; q += 1024) {
+    const int c = q / S, sq = q - c * S;
+    int pre = 0;
+    for (int s2 = 0; s2 <= sq; ++s2) {
+      const int tj = w.ctile[(size_t)c * 64 + s2];
+      pre += tj >= 0 ? (int)s_tc[tj] : 0;
+    }
+    w.cpre[(size_t)c * 64 + sq] = pre;
+  }
+}
+
+// Cross-lane exchange for wave reductions without the LDS crossbar (ds_bpermute: ~100+ cycles per
+// step on a row's latency chain): step 0, 1 quad_perm [1,0,3,2] / [2,3,0,1] (xor 1, 2), step 2, 3
+// row_half_mirror / row_mirror (DPP), step 4, 5 v_permlane16_swap / v_permlane32_swap (the other row /
+// half).  Not an xor for steps 2 and 3, but each step pairs every lane of one aligned group of
+// 2^step lanes with a lane of the neighbouring group, so after a reduction's step s every aligned
+// group of 2^(s+1) lanes holds its reduction (min / argmin: commutative, associative, idempotent).
+template <int STEP>
+__device__ __forceinline__ unsigned xlane(unsigned x, int lane) {
+  if constexpr (STEP == 0) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);
+  else if constexpr (STEP == 1) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);
+  else if constexpr (STEP == 2) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);
+  else if constexpr (STEP == 3) return (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);
+  else if constexpr (STEP == 4) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (lane & 16) ? r[0] : r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (lane & 32) ? r[0] : r[1];
+  }
+}
+template <int STEP>
+__device__ __forceinline__ void argmin_step(unsigned long long& k, int& p, int lane) {
+  const unsigned lo = xlane<STEP>((unsigned)k, lane), hi = xlane<STEP>((unsigned)(k >> 32), lane);
+  const int op = (int)xlane<STEP>((unsigned)p, lane);
+  const unsigned long long ok = ((unsigned long long)hi << 32) | lo;
+  if (kless(ok, op, k, p)) {
+    k = ok;
+    p = op;
+  }
+}
+// the wave's smallest (key, position): in every lane
+__device__ __forceinline__ void wave_argmin(unsigned long long& k, int& p, int lane) {
+  argmin_step<0>(k, p, lane);
+  argmin_step<1>(k, p, lane);
+  argmin_step<2>(k, p, lane);
+  argmin_step<3>(k, p, lane);
+  argmin_step<4>(k, p, lane);
+  argmin_step<5>(k, p, lane);
+}
+template <int STEP>
+__device__ __forceinline__ float fmin_step(float x, int lane) {
+  return fminf(x, __uint_as_float(xlane<STEP>(__float_as_uint(x), lane)));
+}
+template <int STEP>
+__device__ __forceinline__ double dmin_step(double x, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = xlane<STEP>((unsigned)b, lane), hi = xlane<STEP>((unsigned)(b >> 32), lane);
+  return fmin(x, __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo)));
+}
+__device__ __forceinline__ double wave_min_f64(double x, int lane) {
+  x = dmin_step<0>(x, lane);
+  x = dmin_step<1>(x, lane);
+  x = dmin_step<2>(x, lane);
+  x = dmin_step<3>(x, lane);
+  x = dmin_step<4>(x, lane);
+  return dmin_step<5>(x, lane);
+}
+// a double through xlane<st> (st folds to a constant in unrolled loops)
+__device__ __forceinline__ double xlane_d(double x, int st, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  unsigned lo, hi;
+  switch (st) {
+    case 0: lo = xlane<0>((unsigned)b, lane); hi = xlane<0>((unsigned)(b >> 32), lane); break;
+    case 1: lo = xlane<1>((unsigned)b, lane); hi = xlane<1>((unsigned)(b >> 32), lane); break;
+    case 2: lo = xlane<2>((unsigned)b, lane); hi = xlane<2>((unsigned)(b >> 32), lane); break;
+    case 3: lo = xlane<3>((unsigned)b, lane); hi = xlane<3>((unsigned)(b >> 32), lane); break;
+    case 4: lo = xlane<4>((unsigned)b, lane); hi = xlane<4>((unsigned)(b >> 32), lane); break;
+    default: lo = xlane<5>((unsigned)b, lane); hi = xlane<5>((unsigned)(b >> 32), lane); break;
+  }
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ float wave_min_f32(float x, int lane) {
+  x = fmin_step<0>(x, lane);
+  x = fmin_step<1>(x, lane);
+  x = fmin_step<2>(x, lane);
+  x = fmin_step<3>(x, lane);
+  x = fmin_step<4>(x, lane);
+  return fmin_step<5>(x, lane);
+}
+
+// the wave's K rounds of argmin over the lanes' sorted lists (the winner's lane pops its head): lane r
+// receives the r-th selected position; returns the K-th selected key (wave-uniform)
+template <int KM>
+__device__ __forceinline__ unsigned long long wave_merge(unsigned long long (&key)[KM], int (&idx)[KM], int K, int lane,
+                                                         int& my_sel) {
+  unsigned long long last = ~0ULL;
+  for (int r = 0; r < K; ++r) {
+    unsigned long long bk = key[0];
+    int bp = idx[0];
+    wave_argmin(bk, bp, lane);
+    if (lane == r) my_sel = bp;
+    last = bk;
+    if (idx[0] == bp && key[0] == bk) {  // pool positions are unique: exactly one owner
+#pragma unroll
+      for (int j = 0; j < KM - 1; ++j) {
+        key[j] = key[j + 1];
+        idx[j] = idx[j + 1];
+      }
+      key[KM - 1] = ~0ULL;
+      idx[KM - 1] = 0x7fffffff;
+    }
+  }
+  return last;
+}
+
+// one row's selection (one wave); LDS: the chunk's compacted stencil tiles are staged in s_vp (else
+// read from L2) -- two instantiations, so neither path's loads go through generic pointers
+template <int KM, bool LDS>
+__device__ __forceinline__ void pool_row(const AsIn& in, const AsParams& p, const AsWork& w, const AsOut& o,
+                                         const float4* s_vp, int* rq, int* re, int i, int lane, int my_tix,
+                                         int my_cnt) {
+#pragma clang fp contract(off)
+  const int MV = p.m_view, S = p.n_stencil;
+  const bool row_valid = in.valid[i] != 0;
+  auto ld = [&](int sq, int ti, int j) -> float4 {
+    if constexpr (LDS) return s_vp[sq * MV + j];
+    else return w.vc[(size_t)ti * MV + j];
+  };
+  const double mp[3] = {w.pos[3 * i], w.pos[3 * i + 1], w.pos[3 * i + 2]};
+  const double md[3] = {w.dir[3 * i], w.dir[3 * i + 1], w.dir[3 * i + 2]};
+  const double mk = w.kap[i], A1 = w.A1[i];
+  int my_sel = 0;
+  if (row_valid) {
+    unsigned long long key[KM];
+    int idx[KM];
+#pragma unroll
+    for (int j = 0; j < KM; ++j) {
+      key[j] = ~0ULL;
+      idx[j] = 0x7fffffff;
+    }
+    const bool prune = p.beta >= 0.0;
+    const double E = 0x1p-20 * ((fabs(mp[0]) + fabs(mp[1])) + fabs(mp[2])) + 1e-30;
+    const double rup = 1.0 + 0x1p-19, rdn = 1.0 - 0x1p-19;
+    const float m0 = (float)mp[0], m1 = (float)mp[1], m2 = (float)mp[2];
+    auto d32 = [&](const float4& v) {
+      const float dx = m0 - v.x, dy = m1 - v.y, dz = m2 - v.z;
+      return (dx * dx + dy * dy) + dz * dz;
+    };
+    float thrA = INFINITY;  // prune an entry whose table distance^2 exceeds this
+    PP_STAMP(2);
+    if (prune) {
+      double thr = INFINITY;
+      for (int round = 0; round < 2 && thr == INFINITY; ++round) {
+        float dmin = INFINITY;
+        for (int sq = round == 0 ? p.s_center : 0; sq < (round == 0 ? p.s_center + 1 : S); ++sq) {
+          const int ti = sq >= 0 ? __shfl(my_tix, sq, 64) : -1;
+          const int n = sq >= 0 ? __shfl(my_cnt, sq, 64) : 0;
+          if (ti < 0) continue;
+          for (int j = lane; j < n; j += 64) dmin = fminf(dmin, d32(ld(sq, ti, j)));
+        }
+        float kth = INFINITY, cur = dmin;
+        for (int r = 0; r < p.k; ++r) {  // the r-th smallest lane minimum, lanes popped in turn
+          const float m = wave_min_f32(cur, lane);
+          kth = m;
+          const unsigned long long hit = __ballot(cur == m);
+          if (lane == __ffsll((long long)hit) - 1) cur = INFINITY;
+        }
+        if (kth < INFINITY) {
+          const double du = (sqrt((double)kth) + E) * rup;
+          thr = du * du * (1.0 + 0x1p-40) + p.beta;
+        }
+      }
+      if (thr < INFINITY) {
+        const double dl = sqrt(thr) / rdn + E;
+        thrA = (float)(dl * dl * (1.0 + 0x1p-20));  // (rounded to f32: still above the f64 value)
+      }
+    }
+    PP_STAMP(3);
+    unsigned head = 0, tail = 0;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    auto take = [&](int n) {  // lanes < n cost ring entry head + lane (exact f64)
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (lane < n) {
+        const unsigned slot = (head + lane) & (kLRing - 1);
+        const int q = rq[slot], e = re[slot];
+        const double dx = mp[0] - in.vpos[3 * e], dy = mp[1] - in.vpos[3 * e + 1], dz = mp[2] - in.vpos[3 * e + 2];
+        const double d_pos = (dx * dx + dy * dy) + dz * dz;
+        if (!(prune && d_pos > key_value(key[KM - 1])))
+          list_insert<KM>(key, idx, order_key(pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e, p.beta)),
+                          q);
+      }
+      head += n;
+    };
+    for (int sq = 0; sq < S; ++sq) {
+      const int ti = __shfl(my_tix, sq, 64);
+      const int n = __shfl(my_cnt, sq, 64);  // (0 for a missing tile)
+      for (int j0 = 0; j0 < n; j0 += kLdsPB * 64) {
+        float4 vv[kLdsPB];
+#pragma unroll
+        for (int u = 0; u < kLdsPB; ++u) {
+          const int j = j0 + lane + u * 64;
+          vv[u] = j < n ? ld(sq, ti, j) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < kLdsPB; ++u) {
+          const int j = j0 + lane + u * 64;
+          const bool keep = j < n && !(prune && d32(vv[u]) > thrA);
+          const unsigned long long m = __ballot(keep);
+          if (keep) {
+            const int oo = (int)vv[u].w;
+            const unsigned slot = (tail + (unsigned)__popcll(m & lt_mask)) & (kLRing - 1);
+            rq[slot] = sq * MV + oo;
+            re[slot] = ti * MV + oo;
+          }
+          tail += (unsigned)__popcll(m);
+        }
+        while (tail - head >= 64u) take(64);
+      }
+    }
+    if (tail != head) take((int)(tail - head));
+    PP_STAMP(4);
+#if GCS_POOL_PROBE
+    if (lane == 0) g_pool_probe[(size_t)i * 10 + 8] = tail;
+#endif
+    const unsigned long long kth_key = wave_merge<KM>(key, idx, p.k, lane, my_sel);
+    PP_STAMP(5);
+    if (kth_key >= order_key(kCostInvalid)) {
+      // Fewer than K valid entries cost less than the invalid cost.  No valid entry was pruned here
+      // (a finite threshold has K valid entries at or below it, and a pruned one is above them all),
+      // so the K selected are the K smallest valid (cost, position); the invalid entries and missing
+      // tiles all cost 1e12, ordered by position: the K smallest of both sets are the K first invalid
+      // positions (wave-ordered ballots over the pool) merged with the selected ones.
+      // lane r < K: the r-th selected key again (the merge popped it; empty: ~0, position 0x7fffffff)
+      const bool has = lane < p.k && my_sel != 0x7fffffff;
+      const int sel_t = __shfl(my_tix, has ? my_sel / MV : 0, 64);
+      unsigned long long my_key = ~0ULL;
+      if (has)
+        my_key = order_key(pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, sel_t * MV + my_sel % MV, p.beta));
+      int inv_pos = 0x7fffffff;  // lane r < K: the r-th invalid position
+      int found = 0;
+      for (int sq = 0; sq < S && found < p.k; ++sq) {
+        const int ti = __shfl(my_tix, sq, 64);
+        for (int o0 = 0; o0 < MV && found < p.k; o0 += 64) {
+          const int oo = o0 + lane;
+          const bool inv = oo < MV && (ti < 0 || !in.vvalid[(size_t)ti * MV + oo]);
+          const unsigned long long bm = __ballot(inv);
+          const int rank = found + (int)__popcll(bm & ((1ull << lane) - 1ull));
+          if (inv && rank < p.k) rq[rank] = sq * MV + oo;  // (the wave's ring as scratch: no take pending)
+          found += (int)__popcll(bm);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      if (lane < std::min(found, p.k)) inv_pos = rq[lane];
+      // lanes 0..K-1: the selected (key, position); lanes K..2K-1: the invalid positions at 1e12
+      unsigned long long ck = my_key;
+      int cp = lane < p.k ? my_sel : 0x7fffffff;
+      if (lane >= p.k) ck = ~0ULL;
+      const int il = lane - p.k;
+      const int ipos = __shfl(inv_pos, il >= 0 && il < 64 ? il : 0, 64);
+      if (il >= 0 && il < p.k && il < found) {
+        ck = order_key(kCostInvalid);
+        cp = ipos;
+      }
+      for (int r = 0; r < p.k; ++r) {
+        unsigned long long bk = ck;
+        int bp = cp;
+        wave_argmin(bk, bp, lane);
+        if (lane == r) my_sel = bp;
+        if (ck == bk && cp == bp) {  // (positions are unique: one owner)
+          ck = ~0ULL;
+          cp = 0x7fffffff;
+        }
+      }
+#if GCS_POOL_PROBE
+      if (lane == 0) g_pool_probe[(size_t)i * 10 + 9] = 1;
+#endif
+    }
+  }
+  PP_STAMP(6);
+  // per candidate (lane k < K): view index, unmasked cost + recency, row min (:377-403)
+  const bool act = lane < p.k;
+  const int sel_ti = __shfl(my_tix, row_valid && act ? my_sel / MV : 0, 64);
+  int e = 0;
+  if (act && row_valid) e = (sel_ti < 0 ? 0 : sel_ti) * MV + my_sel % MV;
+  double c = INFINITY, dt = 0.0;
+  if (act) {
+    c = pair_cost(mp, md, mk, A1, in.vpos, in.vdir, in.vkap, w.A2, e, p.beta);
+    const long long last = (long long)in.vlast[e];
+    dt = (double)(p.scan_seq - last > 0 ? p.scan_seq - last : 0);
+    c = c + p.eps_lam * dt;
+  }
+  const double mn = wave_min_f64(c, lane);
+  if (act) {
+    if (p.row_min) c = c - mn;
+    const size_t o_ = (size_t)i * p.k + lane;
+    o.cost[o_] = c;
+    if (!p.med) w.kmat[o_] = exp(-c / fmax(p.eps, 1e-12));  // (the Sinkhorn's own expression)
+    w.cand[o_] = e;
+    w.dt[o_] = dt;
+    if (o.cand) o.cand[o_] = e;
+    if (o.tile) o.tile[o_] = in.vtile[e];
+    if (o.slot) o.slot[o_] = (int64_t)in.vslot[e];
+  }
+  PP_STAMP(7);
+}
+
+template <int KM>
+__global__ __launch_bounds__(kPoolLdsWaves * 64) void k_as_pool_lds(AsIn in, AsParams p, AsWork w, AsOut o,
+                                                                    int lds_slots) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float4* s_vp = (float4*)smem;
+  const int MV = p.m_view, S = p.n_stencil;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+#if GCS_POOL_PROBE
+  const unsigned long long t_start = wall_clock64();
+#endif
+  const int r0 = w.order[blockIdx.x * kPoolLdsWaves];
+  const int i = w.order[blockIdx.x * kPoolLdsWaves + wid];
+  const int my_st = lane < S ? w.ctile[(size_t)blockIdx.x * 64 + lane] : -1;  // (S <= 64: in every wave)
+  const int my_pre = lane < S ? w.cpre[(size_t)blockIdx.x * 64 + lane] : 0;
+  if (r0 < 0) return;  // a chunk past the last bucket (every thread: before the block barrier)
+  const int cb = p.s_center >= 0 ? __shfl(my_st, p.s_center, 64) : -1;
+  const bool lds = cb >= 0 && lds_slots > 0;  // (uniform)
+  if (lds) {
+    // each stencil tile's valid entries at sq MV, the tiles' entries concatenated over the threads:
+    // eight 16-B loads in flight per thread, then their LDS stores (one round trip, not one per tile)
+    const int tot = __shfl(my_pre, S - 1, 64);
+    for (int g0 = 0; g0 < tot; g0 += 8 * kPoolLdsWaves * 64) {
+      float4 v[8];
+      int dst[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int g = g0 + u * kPoolLdsWaves * 64 + t;
+        // the stencil slot holding concatenated entry g: the first whose inclusive prefix exceeds g
+        int sq = -1, base = 0, ti = 0, prev = 0;
+        for (int q = 0; q < S; ++q) {
+          const int pre = __builtin_amdgcn_readlane(my_pre, q), tq = __builtin_amdgcn_readlane(my_st, q);
+          if (sq < 0 && g < pre) {
+            sq = q;
+            base = prev;
+            ti = tq;
+          }
+          prev = pre;
+        }
+        dst[u] = -1;
+        v[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (g < tot && sq >= 0) {
+          dst[u] = sq * MV + (g - base);
+          v[u] = w.vc[(size_t)ti * MV + (g - base)];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (dst[u] >= 0) s_vp[dst[u]] = v[u];
+    }
+  }
+  __syncthreads();
+  if (i < 0) return;  // a bucket's padding (after the only block barrier)
+#if GCS_POOL_PROBE
+  if (lane == 0) {
+    g_pool_probe[(size_t)i * 10 + 0] = t_start;
+    g_pool_probe[(size_t)i * 10 + 1] = wall_clock64();
+    for (int q = 2; q < 10; ++q) g_pool_probe[(size_t)i * 10 + q] = 0;
+  }
+#endif
+  int* rq = (int*)(smem + (size_t)lds_slots * 16) + wid * 2 * kLRing;
+  int* re = rq + kLRing;
+  if (lds) {  // the row's stencil tiles are the chunk's (lane s: tile, valid count)
+    const int prv = __shfl_up(my_pre, 1, 64);
+    pool_row<KM, true>(in, p, w, o, s_vp, rq, re, i, lane, my_st, lane == 0 ? my_pre : my_pre - prv);
+  } else {
+    const int my_tix = lane < S ? w.tix[(size_t)i * S + lane] : -1;
+    const int my_cnt = lane < S && my_tix >= 0 ? w.vcnt[my_tix] : 0;
+    pool_row<KM, false>(in, p, w, o, s_vp, rq, re, i, lane, my_tix, my_cnt);
   }
 }
 
@@ -801,6 +1363,39 @@ __device__ __forceinline__ double exp_fast(double x) {  // |x| < 700
   const double y = 1.0 - ((lo - div_fast(r * c, 2.0 - c)) - hi);
   return ldexp(y, k);
 }
+// x^(-1/n) for a uniform integer n >= 1 and x in [2^-100, 2^100]: an f32 seed (v_log_f32 / v_exp_f32,
+// a few e-7 relative) and two Newton steps y <- y ((n + 1) - x y^n) / n in f64 (the error squares per
+// step: ~3e-11, then below the f64 rounding), y^n by squaring.  The Sinkhorn's scaling exponents
+// ua = 1 / (1 + tau_a / eps), vb = 1 / (1 + tau_b / eps) are fl(1 / n) for the reference defaults
+// (tau 0.5, eps 0.1: n = 6), so (a / x)^ua = a^ua x^(-1/n) -- a^ua once per call -- replaces a log
+// and an exp per row and iteration (a few ulps apart from the pow: the tests' 1e-9 bars)
+constexpr double kRootLo = 7.888609052210118e-31;  // 2^-100
+constexpr double kRootHi = 1.2676506002282294e30;  // 2^100
+__device__ __forceinline__ double ipow_u(double y, int n) {  // y^n, n >= 1 (uniform)
+  double r = 1.0;
+  for (;;) {
+    if (n & 1) r *= y;
+    n >>= 1;
+    if (!n) return r;
+    y *= y;
+  }
+}
+__device__ __forceinline__ double root_seed(double x, float inv_n) {
+  return (double)__builtin_amdgcn_exp2f(-inv_n * __builtin_amdgcn_logf((float)x));
+}
+__device__ __forceinline__ double root_step(double y, double x, int n, double inv_n) {
+  return (y * fma(-x, ipow_u(y, n), (double)(n + 1))) * inv_n;
+}
+template <int N>
+__device__ __forceinline__ double ipow_c(double y) {
+  if constexpr (N == 1) return y;
+  else if constexpr (N % 2 == 0) { const double h = ipow_c<N / 2>(y); return h * h; }
+  else return ipow_c<N - 1>(y) * y;
+}
+template <int N>
+__device__ __forceinline__ double root_step_c(double y, double x, double inv_n) {
+  return (y * fma(-x, ipow_c<N>(y), (double)(N + 1))) * inv_n;
+}
 // x^y as pow_sinkhorn (0 at x = 0; the library pow outside the short path's range)
 __device__ __forceinline__ double pow_fast(double x, double y) {
   if (x == 0.0) return 0.0;
@@ -808,6 +1403,159 @@ __device__ __forceinline__ double pow_fast(double x, double y) {
   const double a = y * log_fast(x);
   if (!(fabs(a) < 700.0)) return pow_lib(x, y);
   return exp_fast(a);
+}
+
+// GCS_SH_FINSPLIT: the Sinkhorn's finish over several workgroups, one row per thread -- pi = u K v, the
+// responsibilities and row masses, and the certificate sums (per workgroup in a fixed tree, then the
+// workgroups in index order by the last one to finish).  1 (default): extra workgroups of the Sinkhorn
+// launch, which load their rows' costs while workgroup 0 iterates and wait for its u / v hand-off
+// (sc1 stores + a flag); 2: a launch of its own after the Sinkhorn (k_as_finish); 0: workgroup 0
+// finishes alone (~13 us: three rows per thread, their loads and stores on one CU).
+#ifndef GCS_SH_FINSPLIT
+#define GCS_SH_FINSPLIT 1
+#endif
+template <int STEP>
+__device__ __forceinline__ double dsum_step(double x, int lane) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  const unsigned lo = xlane<STEP>((unsigned)b, lane), hi = xlane<STEP>((unsigned)(b >> 32), lane);
+  return x + __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+constexpr int kFinThreads = 256;
+// one block of the finish: rows blk NT + t.  The rows' cost / K_mat loads issue first, then wait()
+// (the in-kernel form polls the Sinkhorn workgroup's flag there), then u, v and sum a -- sc1 loads
+// (the in-kernel form's hand-off; harmless across a launch boundary).  The block's sums (a fixed
+// tree) are written sc1 and drained before the ticket; the last block folds them in block order with
+// sc1 loads and writes the certificate.
+template <int KM, int NT, class Wait>
+__device__ __forceinline__ void finish_block(const AsIn& in, const AsParams& p, const AsWork& w, const AsOut& o, int blk,
+                                             int nblk, double* s_red /*(NT / 64) x (7 + KM)*/, Wait wait) {
+#pragma clang fp contract(off)
+  constexpr int NV = 7 + KM;
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6, N = p.n, K = p.k;
+  const double eps = fmax(p.eps, 1e-12);
+  const double bk = 1.0 / (double)K;
+  const int r = blk * NT + t;
+  bool rv = false;
+  double va = 0.0, Cr[KM], Xr[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) Cr[k] = Xr[k] = 0.0;
+  if (r < N) {
+    rv = in.valid[r] != 0;
+    va = rv ? 1.0 : 0.0;
+    if (p.a_policy == 1) va = va * in.weights[r];
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      Cr[k] = k < K && !p.med ? o.cost[(size_t)r * K + k] : 0.0;
+      Xr[k] = k < K && !p.med ? w.kmat[(size_t)r * K + k] : 0.0;
+    }
+  }
+  if (!wait()) return;
+  if (p.med && r < N)  // the median-scaled costs: written by the Sinkhorn workgroup (sc1) before its hand-off
+#pragma unroll
+    for (int k = 0; k < KM; ++k)
+      Cr[k] = k < K ? __hip_atomic_load(&o.cost[(size_t)r * K + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+  const double sum_a = __hip_atomic_load(&w.su[N + KM], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double v[KM];
+#pragma unroll
+  for (int k = 0; k < KM; ++k) v[k] = k < K ? __hip_atomic_load(&w.su[N + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+  // acc: [sum rm, sum rm^2, sum novel, defect_a^2, sum pi C, nonzero_a, sum pi | col masses K]
+  double acc[NV];
+#pragma unroll
+  for (int q = 0; q < NV; ++q) acc[q] = 0.0;
+  if (r < N) {
+    va = va / sum_a;
+    const double u = __hip_atomic_load(&w.su[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    double rm = 0.0;
+#pragma unroll
+    for (int k = 0; k < KM; ++k) {
+      if (k >= K) continue;
+      const double X = p.med ? exp(-Cr[k] / eps) : Xr[k];
+      const double pik = (u * X) * v[k];
+      rm += pik;
+      acc[4] += pik * Cr[k];
+      acc[6] += pik;
+      acc[7 + k] += pik;
+      o.resp[(size_t)r * K + k] = rv ? pik : 0.0;
+    }
+    o.rmass[r] = rm;
+    acc[0] += rm;
+    acc[1] += rm * rm;
+    acc[2] += fmax(va - rm, 0.0);
+    acc[3] += (rm - va) * (rm - va);
+    acc[5] += va > p.eps_mass ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int q = 0; q < NV; ++q) {
+    double x = acc[q];
+    x = dsum_step<0>(x, lane);
+    x = dsum_step<1>(x, lane);
+    x = dsum_step<2>(x, lane);
+    x = dsum_step<3>(x, lane);
+    x = dsum_step<4>(x, lane);
+    x = dsum_step<5>(x, lane);
+    acc[q] = x;
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < NV; ++q) s_red[wid * NV + q] = acc[q];
+  __syncthreads();
+  if (wid != 0) return;
+  // wave 0: this block's sums (lane q), the ticket, and -- in the last block -- the fold.  The sums are
+  // write-through (sc1) stores drained before the ticket (the guide's R1 publish: no release fence,
+  // whose L2 write-back costs more than the finish); the last block reads them with sc1 loads
+  if (lane < NV) {
+    double sum = s_red[lane];
+    for (int g = 1; g < NT / 64; ++g) sum += s_red[g * NV + lane];
+    __hip_atomic_store(&w.fpart[(size_t)blk * NV + lane], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned tk = 0;
+  if (lane == 0) tk = __hip_atomic_fetch_add(w.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tk = (unsigned)__shfl((int)tk, 0, 64);
+  if (tk != (unsigned)nblk - 1u) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (keeps the loads below the ticket)
+  double f = 0.0;
+  if (lane < NV)
+    for (int g = 0; g < nblk; ++g)
+      f += __hip_atomic_load(&w.fpart[(size_t)g * NV + lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double tot[7];
+#pragma unroll
+  for (int q = 0; q < 7; ++q) tot[q] = __shfl(f, q, 64);
+  double db = 0.0;  // (every lane: the shuffles read lanes 7 ..)
+  for (int k = 0; k < K; ++k) {
+    const double ck = __shfl(f, 7 + k, 64);
+    db += (ck - bk) * (ck - bk);
+  }
+  if (lane == 0) {
+    const double tm = tot[6];
+    o.cert[CE_DEFECT_A] = sqrt(tot[3]);
+    o.cert[CE_DEFECT_B] = sqrt(db);
+    o.cert[CE_MASS_TOTAL] = tm;
+    o.cert[CE_SUM_A] = sum_a;
+    o.cert[CE_SUM_B] = bk * (double)K;
+    o.cert[CE_SUM_M] = tot[0];
+    o.cert[CE_SUM_NOVEL] = tot[2];
+    o.cert[CE_P95_B] = bk;  // b uniform: every entry is 1 / K
+    o.cert[CE_NONZERO_A] = tot[5];
+    o.cert[CE_NONZERO_B] = bk > p.eps_mass ? (double)K : 0.0;
+    o.cert[CE_ESS] = tot[0] * tot[0] / (tot[1] + p.eps_mass);
+    o.cert[CE_MASS_EPS] = p.eps_mass / (tm + p.eps_mass);
+    o.cert[CE_TOTAL_COST] = tot[4];
+    o.cert[CE_SUPPORT] = tot[5] / (double)std::max(N, 1);
+    o.cert[CE_EXACT] = 0.0;
+    o.cert[CE_MVALID] = (double)*w.mvalid;
+    *w.mvalid_next = 0u;  // the next call's counter, armed
+    __hip_atomic_store(w.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-armed
+  }
+}
+
+// GCSLAM_SH_FINSPLIT=2: the finish as its own launch after the Sinkhorn (A/B of the in-kernel form)
+template <int KM>
+__global__ __launch_bounds__(kFinThreads) void k_as_finish(AsIn in, AsParams p, AsWork w, AsOut o, int n_valid_host,
+                                                           const int32_t* n_valid_dev) {
+  __shared__ double s_red[(kFinThreads / 64) * (7 + KM)];
+  if ((n_valid_dev ? *n_valid_dev : n_valid_host) == 0 || *w.mvalid == 0u) return;  // the Sinkhorn's empty result
+  finish_block<KM, kFinThreads>(in, p, w, o, blockIdx.x, gridDim.x, s_red, [] { return true; });
 }
 
 template <int KM, int RPT>
@@ -840,6 +1588,26 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     if (t == 0) *w.mvalid_next = 0u;  // the next call's counter, armed (no per-call memset)
     // the empty result selects view entry 0 for every candidate (the outputs above)
     cand_stats<kShThreads>(in, p, p.eps_mass, [](size_t) { return 0; }, o.cert);
+    return;
+  }
+  if (blockIdx.x >= 2) {  // a finish workgroup (GCS_SH_FINSPLIT 1): its rows' costs, then workgroup 0's u, v
+    __shared__ double s_fin[(kShThreads / 64) * (7 + KM)];
+    __shared__ int s_ok;
+    auto wait = [&]() -> bool {
+      if (t == 0) {
+        bool ok = false;
+        for (unsigned it = 0; it < (1u << 22) && !ok; ++it) {  // bounded: a lost hand-off fails loudly
+          ok = __hip_atomic_load(w.flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == p.epoch;
+          if (!ok) __builtin_amdgcn_s_sleep(2);
+        }
+        if (!ok) o.cert[CE_MASS_TOTAL] = NAN;
+        s_ok = ok ? 1 : 0;
+      }
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (keeps the hand-off's sc1 loads below)
+      return s_ok != 0;
+    };
+    finish_block<KM, kShThreads>(in, p, w, o, blockIdx.x - 2, gridDim.x - 2, s_fin, wait);
     return;
   }
   if (blockIdx.x == 1) {
@@ -925,7 +1693,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     for (int k = 0; k < KM; ++k) {
       const int r = t + j * kShThreads;
       const bool ok = r < N && k < K;
-      X[j * KM + k] = ok ? o.cost[(size_t)r * K + k] : 0.0;
+      X[j * KM + k] = ok ? (p.med ? o.cost[(size_t)r * K + k] : w.kmat[(size_t)r * K + k]) : 0.0;
       if (ok) okm |= 1u << (j * KM + k);
     }
   if (p.med) {  // cost_scale_by_median (:405-407)
@@ -941,18 +1709,39 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
 #pragma unroll
     for (int q = 0; q < RPT * KM; ++q) {
       X[q] = X[q] / (med + 1e-12);
-      if ((okm >> q) & 1u) o.cost[(size_t)(t + (q / KM) * kShThreads) * K + q % KM] = X[q];  // result.cost_matrix
+      if ((okm >> q) & 1u)  // result.cost_matrix (sc1: the finish workgroups read it after the hand-off)
+        __hip_atomic_store(&o.cost[(size_t)(t + (q / KM) * kShThreads) * K + q % KM], X[q], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   const double eps = fmax(p.eps, 1e-12);
   const double ua = 1.0 / (1.0 + p.tau_a / eps), vb = 1.0 / (1.0 + p.tau_b / eps);
   const double bk = 1.0 / (double)K;
+  // exponents of the form fl(1 / n): the Newton root (uniform)
+  auto root_n = [](double e) {
+    const double r = 1.0 / e;
+    const int n = r >= 1.0 && r <= 64.0 ? (int)rint(r) : 0;
+    return n >= 1 && 1.0 / (double)n == e ? n : 0;
+  };
+  const int na = GCS_SH_ROOT ? root_n(ua) : 0, nb = GCS_SH_ROOT ? root_n(vb) : 0;
+  const double ina = na ? 1.0 / (double)na : 0.0, inb = nb ? 1.0 / (double)nb : 0.0;
+  const float ina_f = (float)ina, inb_f = (float)inb;
+  double apow[RPT];  // a^ua (the row's factor of u on the root path)
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) apow[j] = na ? pow_fast(va[j], ua) : 0.0;
+  const double bpow = nb ? pow_fast(bk, vb) : 0.0;
 #if GCS_SH_LOGB
   // v = (b / (K^T u + 1e-12))^vb as exp(vb (log b - log K^T u)): log b once per call, no quotient in
   // the loop (as u; the short log / exp outside their ranges fall back to the quotient form)
   const double lbk = log(bk);
   auto v_scale = [&](double sum) {
     const double ss = sum + 1e-12;
+    if (nb && ss >= kRootLo && ss <= kRootHi) {
+      double y = root_seed(ss, inb_f);
+      y = nb == 6 ? root_step_c<6>(y, ss, inb) : root_step(y, ss, nb, inb);
+      y = nb == 6 ? root_step_c<6>(y, ss, inb) : root_step(y, ss, nb, inb);
+      return bpow * y;
+    }
     const double b_ = vb * (lbk - SH_LOG(ss));
     return ss >= 2.2250738585072014e-308 && ss <= 1.7976931348623157e308 && fabs(b_) < 700.0
                ? SH_EXP(b_)
@@ -961,8 +1750,9 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
 #else
   auto v_scale = [&](double sum) { return pow_fast(div_fast(bk, sum + 1e-12), vb); };
 #endif
+  if (p.med)  // (else the pool kernel wrote K_mat)
 #pragma unroll
-  for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
+    for (int q = 0; q < RPT * KM; ++q) X[q] = ((okm >> q) & 1u) ? exp(-X[q] / eps) : 0.0;
   SH_STAMP(2);
   double u[RPT], v[KM];
 #pragma unroll
@@ -983,6 +1773,41 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
 #endif
   for (int it = 0; it < p.iters; ++it) {
     // u = (a / (K v + 1e-12))^ua, one lane per row (K v in column order)
+    // ua = fl(1 / na): u = a^ua (K v + 1e-12)^(-1/na), the rows side by side (na = 6, the reference
+    // defaults, with y^6 unrolled: the runtime-n squaring loop kept the rows' chains apart)
+    auto root_rows = [&](auto nc) {
+      constexpr int NC = decltype(nc)::value;
+      double kvv[RPT], y[RPT];
+      bool ok[RPT];
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        double kv = 0.0;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) kv = fma(X[j * KM + k], v[k], kv);
+        kvv[j] = kv + 1e-12;
+        ok[j] = kvv[j] >= kRootLo && kvv[j] <= kRootHi;
+        y[j] = root_seed(ok[j] ? kvv[j] : 1.0, ina_f);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int j = 0; j < RPT; ++j) {
+          const double x = ok[j] ? kvv[j] : 1.0;
+          y[j] = NC ? root_step_c<NC>(y[j], x, ina) : root_step(y[j], x, na, ina);
+        }
+#pragma unroll
+      for (int j = 0; j < RPT; ++j) {
+        const int r = t + j * kShThreads;
+        double uj = apow[j] * y[j];
+        if (!ok[j] && va[j] != 0.0) uj = pow_fast(div_fast(va[j], kvv[j]), ua);  // (rare: K v out of range)
+        u[j] = r < N && va[j] != 0.0 ? uj : 0.0;
+      }
+    };
+    if (na == 6) {
+      root_rows(std::integral_constant<int, 6>{});
+    } else if (na) {
+      root_rows(std::integral_constant<int, 0>{});
+    } else {
 #if GCS_SH_LOGA && GCS_SH_ILV
     // the rows' chains side by side, branch-free (log and exp of an in-range stand-in where the row's
     // arguments are out of range), the rare fallback rows after them: the per-row branches serialised
@@ -1073,6 +1898,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
 #endif
     }
 #endif
+    }
     SH_ACC(0);
     double c[KM];
 #pragma unroll
@@ -1082,7 +1908,9 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
       for (int j = 0; j < RPT; ++j) sacc = fma(X[j * KM + k], u[j], sacc);
       c[k] = sacc;
     }
-    // reduce-scatter: step s exchanges half of the live values with the lane 32 >> s apart
+    // reduce-scatter: step s exchanges half of the live values with a lane of the other half of its
+    // 64 >> s group (GCS_SH_DPP: xlane's DPP / permlane pairings -- xor 32, 16, then the mirrors -- in
+    // place of the ds_bpermute xor shuffles: each lane still ends with its column summed over all 64)
 #pragma unroll
     for (int s = 0, n = KM; s < LG; ++s, n >>= 1) {
       const int h = n >> 1;
@@ -1092,13 +1920,22 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
         if (i < h) {
           const double send = up ? c[i] : c[i + h];
           const double keep = up ? c[i + h] : c[i];
+#if GCS_SH_DPP
+          c[i] = keep + xlane_d(send, 5 - s, lane);
+#else
           c[i] = keep + __shfl_xor(send, 32 >> s, 64);
+#endif
         }
       }
     }
     double cs = c[0];
+#if GCS_SH_DPP
+#pragma unroll
+    for (int st = 5 - LG; st >= 0; --st) cs += xlane_d(cs, st, lane);
+#else
 #pragma unroll
     for (int sh = (64 >> LG) / 2; sh >= 1; sh >>= 1) cs += __shfl_xor(cs, sh, 64);
+#endif
 #if GCS_SH_ONEBAR
     // every wave finishes v itself: lane k (< KM) sums column k over the waves in order and takes its
     // power, then v[k] comes from lane k.  The partials alternate between two buffers, so one barrier
@@ -1148,6 +1985,25 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
 #endif
 #undef SH_LOG
 #undef SH_EXP
+  if (p.fin_split) {  // the finish runs in other workgroups: hand them u, v and sum a
+    // (sc1 stores drained by every storing wave, then one flag store: the guide's R1 publish)
+#pragma unroll
+    for (int j = 0; j < RPT; ++j) {
+      const int r = t + j * kShThreads;
+      if (r < N) __hip_atomic_store(&w.su[r], u[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t == 0) {
+#pragma unroll
+      for (int k = 0; k < KM; ++k) __hip_atomic_store(&w.su[N + k], v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&w.su[N + KM], sum_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (p.fin_split == 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (t == 0) __hip_atomic_store(w.flag, p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   // pi, row masses, responsibilities and the cert sums
   // acc: [sum rm, sum rm^2, sum novel, defect_a^2, sum pi C, nonzero_a, sum pi | col masses K]
   double acc[7 + KM];
@@ -1391,8 +2247,21 @@ struct gcs_assoc_ctx {
   double* h_vpe = nullptr;   // pinned, mapped: k_as_vpe's sums
   double* h_vpe_dev = nullptr;
   double* d_vpe_rows = nullptr;  // k_as_vpe_rows: 25 sums per row (field-major, max_meas rows)
+  float4* d_vc = nullptr;        // k_as_stage: the view tiles' valid entries in f32 (max_pool entries)
+  int32_t* d_vcnt = nullptr;     // k_as_stage: valid entries per view tile (kMaxBuckets)
+  int32_t* d_order = nullptr;    // k_as_stage's row order: max_meas + kMaxBuckets x chunk
+  double* d_kmat = nullptr;      // the pools' K_mat (max_meas x max_k)
+  int32_t *d_ctile = nullptr, *d_cpre = nullptr;  // k_as_stage's chunk records (64 each per chunk)
+  uint32_t* d_tcnt = nullptr;    // k_as_prep's per-view-tile valid counts (kMaxBuckets; zero between calls)
+  double *d_su = nullptr, *d_fpart = nullptr;  // k_as_finish: u, v, sum a; per-workgroup sums
+  uint32_t* d_ticket = nullptr;
+  int fin_split = GCS_SH_FINSPLIT;  // GCSLAM_SH_FINSPLIT: 0 the Sinkhorn workgroup, 2 a launch of its own (A/B)
+  uint32_t* d_flag = nullptr;        // the Sinkhorn's hand-off flag
+  unsigned epoch = 0;
+  bool pool_lds = GCS_POOL_LDS != 0;  // GCSLAM_POOL_LDS=0: k_as_pool from L2 for every view (A/B)
   bool vpe_split = GCS_VPE_SPLIT != 0;  // GCSLAM_VPE_SPLIT=0: the one-workgroup form (A/B, bitwise test)
   int probe_iters = 0;       // GCS_SH_PROBE builds: the last launch's Sinkhorn iterations
+  int probe_rows = 0;        // GCS_POOL_PROBE builds: the last launch's rows
 };
 
 namespace {
@@ -1464,7 +2333,7 @@ int gcs_assoc_ctx_destroy(gcs_assoc_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, c->d_mvalid, c->d_st,
-                  c->d_vpe_rows};
+                  c->d_vpe_rows, c->d_vc, c->d_vcnt, c->d_order, c->d_kmat, c->d_su, c->d_fpart, c->d_ticket, c->d_ctile, c->d_cpre, c->d_tcnt, c->d_flag};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_cert) (void)hipHostFree(c->h_cert);
@@ -1491,7 +2360,12 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
       bad(hipMalloc(&c->d_A1, N * 8)) || bad(hipMalloc(&c->d_A2, M * 8)) || bad(hipMalloc(&c->d_dt, NK * 8)) ||
       bad(hipMalloc(&c->d_tix, N * kMaxStencil * 4)) || bad(hipMalloc(&c->d_cand, NK * 4)) ||
       bad(hipMalloc(&c->d_mvalid, 8)) || bad(hipMalloc(&c->d_st, kMaxStencil * 3)) ||
-      bad(hipMalloc(&c->d_vpe_rows, N * kVpeRowVals * 8)) ||
+      bad(hipMalloc(&c->d_vpe_rows, N * kVpeRowVals * 8)) || bad(hipMalloc(&c->d_vc, M * sizeof(float4))) || bad(hipMalloc(&c->d_kmat, NK * 8)) ||
+      bad(hipMalloc(&c->d_su, (N + 40) * 8)) || bad(hipMalloc(&c->d_fpart, ((N + kFinThreads - 1) / kFinThreads) * 40 * 8)) ||
+      bad(hipMalloc(&c->d_ticket, 4)) ||
+      bad(hipMalloc(&c->d_ctile, (N / kPoolLdsWaves + kMaxBuckets + 1) * 64 * 4)) ||
+      bad(hipMalloc(&c->d_cpre, (N / kPoolLdsWaves + kMaxBuckets + 1) * 64 * 4)) || bad(hipMalloc(&c->d_tcnt, kMaxBuckets * 4)) || bad(hipMalloc(&c->d_flag, 4)) || bad(hipMalloc(&c->d_vcnt, kMaxBuckets * 4)) ||
+      bad(hipMalloc(&c->d_order, (N + (size_t)kMaxBuckets * kPoolLdsWaves) * 4)) ||
       bad(hipHostMalloc(&c->h_cert, GCS_ASSOC_CERT_LEN * sizeof(double), hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&c->h_cert_dev, c->h_cert, 0)) ||
       bad(hipHostMalloc(&c->h_vpe, 32 * sizeof(double), hipHostMallocMapped)) ||
@@ -1499,11 +2373,18 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
-  if (bad(hipMemset(c->d_mvalid, 0, 8))) {  // both valid-entry counters start armed
+  if (bad(hipMemset(c->d_mvalid, 0, 8)) || bad(hipMemset(c->d_ticket, 0, 4)) || bad(hipMemset(c->d_tcnt, 0, kMaxBuckets * 4)) || bad(hipMemset(c->d_flag, 0, 4))) {
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
   if (const char* e = getenv("GCSLAM_VPE_SPLIT")) c->vpe_split = atoi(e) != 0;
+  if (const char* e = getenv("GCSLAM_POOL_LDS")) c->pool_lds = atoi(e) != 0;
+  if (const char* e = getenv("GCSLAM_SH_FINSPLIT")) c->fin_split = atoi(e);
+  // the LDS pool's dynamic LDS reaches 160 KB (the view table + the waves' rings)
+  (void)hipFuncSetAttribute((const void*)k_as_pool_lds<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipGetLastError();
+  (void)hipFuncSetAttribute((const void*)k_as_pool_lds<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  (void)hipFuncSetAttribute((const void*)k_as_pool_lds<32>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   c->stream = c->own;
   *out = c;
   return GCS_OK;
@@ -1578,6 +2459,9 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
   p.a_policy = cfg->a_policy == GCS_ASSOC_A_WEIGHT ? 1 : 0;
   p.row_min = cfg->cost_subtract_row_min != 0;
   p.med = cfg->cost_scale_by_median != 0;
+  p.fin_split = !bad_policy && c->fin_split >= 1 && c->fin_split <= 2 ? c->fin_split : 0;
+  if (++c->epoch == 0u) c->epoch = 1u;
+  p.epoch = c->epoch;
   p.beta = cfg->beta;
   p.eps = cfg->epsilon;
   p.tau_a = cfg->tau_a;
@@ -1595,7 +2479,10 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
   uint32_t* mv = c->d_mvalid + c->mv_parity;
   uint32_t* mv_next = c->d_mvalid + (c->mv_parity ^ 1);
   c->mv_parity ^= 1;
-  AsWork w{c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, mv, mv_next};
+  // the bucketed pool (k_as_pool_lds) for views of at most kMaxBuckets - 1 tiles
+  const bool bucketed = c->pool_lds && !bad_policy && v->n_tiles + 1 <= kMaxBuckets && m->n_total <= kBucketRows * 1024;
+  AsWork w{c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, mv, mv_next, c->d_vc, c->d_vcnt,
+           c->d_order, c->d_ctile, c->d_cpre, c->d_tcnt, c->d_kmat, bucketed ? kPoolLdsWaves : 0, c->d_su, c->d_fpart, c->d_ticket, c->d_flag};
   AsOut out{o->responsibilities, o->row_masses, o->cost_matrix, o->candidate_pool_indices, o->candidate_tile_ids,
             o->candidate_slots, c->h_cert_dev};
   if (ns != c->st_ns || rxy != c->st_rxy || rz != c->st_rz) {  // the stencil table changes with the radii only
@@ -1619,6 +2506,21 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
     }
   } rearm{mv_next};
   const int km = K <= 8 ? 8 : (K <= 16 ? 16 : 32);
+  // the pool: the whole view staged in LDS when it fits (one wave per row, as many waves per
+  // workgroup as spread the rows over 256 workgroups), else one 128-thread workgroup per row from L2
+  auto launch_pool = [&](auto k_l2, auto k_lds) {
+    if (bucketed) {
+      const int nb = v->n_tiles + 1;
+      const int cap = p.n + nb * kPoolLdsWaves;  // rows + every bucket's padding, at most
+      hipLaunchKernelGGL(k_as_stage, dim3(v->n_tiles + 1), dim3(1024), 0, s, in, p, w, nb, cap);
+      const int lds_slots = (long)ns * p.m_view <= kPoolLdsMaxView ? ns * p.m_view : 0;
+      const size_t lds = (size_t)lds_slots * 16 + (size_t)kPoolLdsWaves * kLRing * 8;
+      hipLaunchKernelGGL(k_lds, dim3((cap + kPoolLdsWaves - 1) / kPoolLdsWaves), dim3(kPoolLdsWaves * 64), lds, s, in, p,
+                         w, out, lds_slots);
+    } else {
+      hipLaunchKernelGGL(k_l2, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
+    }
+  };
   if (bad_policy) {
     uint32_t mvh = 0;
     int32_t nvh = m->n_valid;
@@ -1628,26 +2530,35 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
     if (nvh != 0 && mvh != 0) return as_fail(c, GCS_ERR_ARG, bad_policy);  // rearm zeroes the next counter
     // empty: the Sinkhorn kernel's zero path writes the reference's empty result
   }
+  const int nfin = (p.n + kFinThreads - 1) / kFinThreads;  // (GCS_SH_FINSPLIT 2)
+  const int gsh = 2 + (p.fin_split == 1 ? (p.n + kShThreads - 1) / kShThreads : 0);  // the Sinkhorn's grid
   if (bad_policy) {
     hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, 0, (const int32_t*)nullptr);
   } else if (km == 8) {
-    hipLaunchKernelGGL(k_as_pool<8>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
+    launch_pool(k_as_pool<8>, k_as_pool_lds<8>);
     // three rows per thread when they cover the rows (the reference's 1,536 = 3 x 512): no padding
     // row in the K v / K^T u sums
     if (3 * kShThreads < rpt_for(8) * kShThreads && p.n <= 3 * kShThreads)
-      hipLaunchKernelGGL((k_as_sinkhorn<8, 3>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
+      hipLaunchKernelGGL((k_as_sinkhorn<8, 3>), dim3(gsh), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
     else
-      hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
+      hipLaunchKernelGGL((k_as_sinkhorn<8, rpt_for(8)>), dim3(gsh), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
+    if (p.fin_split == 2)
+      hipLaunchKernelGGL(k_as_finish<8>, dim3(nfin), dim3(kFinThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
   } else if (km == 16) {
-    hipLaunchKernelGGL(k_as_pool<16>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
-    hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
+    launch_pool(k_as_pool<16>, k_as_pool_lds<16>);
+    hipLaunchKernelGGL((k_as_sinkhorn<16, rpt_for(16)>), dim3(gsh), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
+    if (p.fin_split == 2)
+      hipLaunchKernelGGL(k_as_finish<16>, dim3(nfin), dim3(kFinThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
   } else {
-    hipLaunchKernelGGL(k_as_pool<32>, dim3(p.n), dim3(kPoolThreads), 0, s, in, p, w, out);
-    hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(2), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
+    launch_pool(k_as_pool<32>, k_as_pool_lds<32>);
+    hipLaunchKernelGGL((k_as_sinkhorn<32, rpt_for(32)>), dim3(gsh), dim3(kShThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
+    if (p.fin_split == 2)
+      hipLaunchKernelGGL(k_as_finish<32>, dim3(nfin), dim3(kFinThreads), 0, s, in, p, w, out, m->n_valid, n_valid_dev);
   }
   ASCHK(c, hipGetLastError());
   rearm.armed = false;  // the Sinkhorn is queued: it zeroes mv_next
   c->probe_iters = p.iters;
+  c->probe_rows = p.n;
   return GCS_OK;
 }
 
@@ -1670,6 +2581,38 @@ void assoc_collect(gcs_assoc_ctx* c, gcs_assoc_outputs* o) {
     const double it = c->probe_iters > 0 ? 100.0 * c->probe_iters : 1.0;  // per iteration, us
     fprintf(stderr, "sh_probe per iteration us: u %.3f KTu+scatter %.3f barrier1 %.3f v %.3f barrier2+read %.3f\n",
             h[8] / it, h[9] / it, h[10] / it, h[11] / it, h[12] / it);
+  }
+#endif
+#if GCS_POOL_PROBE
+  {
+    static unsigned long long h[4096 * 10];
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pool_probe), sizeof(h));
+    const int n = std::min(c->probe_rows, 4096);
+    double sum[8] = {0}, mx[8] = {0}, ring = 0, rmax = 0;
+    int slow = 0, cnt = 0;
+    unsigned long long t0 = ~0ull, t1 = 0;
+    for (int i = 0; i < n; ++i) {
+      const unsigned long long* r = h + (size_t)i * 10;
+      if (!r[0] || !r[7]) continue;  // invalid rows skip stamps 2..6
+      ++cnt;
+      t0 = std::min(t0, r[0]);
+      t1 = std::max(t1, r[7]);
+      for (int k = 1; k < 8; ++k) {
+        unsigned long long prev = r[k - 1];
+        for (int j = k - 1; j >= 0 && !prev; --j) prev = r[j];
+        const double d = r[k] ? (double)(r[k] - prev) / 100.0 : 0.0;
+        sum[k] += d;
+        mx[k] = std::max(mx[k], d);
+      }
+      ring += (double)r[8];
+      rmax = std::max(rmax, (double)r[8]);
+      slow += (int)r[9];
+    }
+    if (cnt)
+      fprintf(stderr, "pool_probe rows %d span %.2f us | mean/max us: stage %.2f/%.2f pro %.2f/%.2f pass1 %.2f/%.2f "
+              "ring %.2f/%.2f merge %.2f/%.2f slow %.2f/%.2f final %.2f/%.2f | ring %.1f/%.0f slow rows %d\n",
+              cnt, (t1 - t0) / 100.0, sum[1] / cnt, mx[1], sum[2] / cnt, mx[2], sum[3] / cnt, mx[3], sum[4] / cnt, mx[4],
+              sum[5] / cnt, mx[5], sum[6] / cnt, mx[6], sum[7] / cnt, mx[7], ring / cnt, rmax, slow);
   }
 #endif
   for (int q = 0; q < GCS_ASSOC_CERT_LEN; ++q) o->cert[q] = c->h_cert[q];
