@@ -136,6 +136,7 @@ struct AsWork {
   double* fpart;          // k_as_finish: per workgroup, its rows' certificate sums (7 + KM)
   uint32_t* ticket;       // k_as_finish: workgroups done (the last folds; re-armed by it)
   uint32_t* flag;         // the Sinkhorn workgroup's u / v hand-off to the finish workgroups (= epoch)
+  uint32_t* cstat;        // the pools: per row, valid candidates | distinct tiles << 16 (cand_stats)
 };
 
 struct AsIn {
@@ -590,6 +591,18 @@ __global__ __launch_bounds__(kPoolThreads) void k_as_pool(AsIn in, AsParams p, A
     if (o.tile) o.tile[o_] = in.vtile[e];
     if (o.slot) o.slot[o_] = (int64_t)in.vslot[e];
   }
+  {  // the MapUpdateCert's per-row candidate statistics (cand_stats): valid candidates, distinct tiles
+    const bool cv = act && row_valid && in.vvalid[e] != 0;
+    const long long tile = cv ? (long long)in.vtile[e] : -1;
+    bool seen = false;
+    for (int k2 = 0; k2 < p.k; ++k2) {  // (every lane: the shuffles read lanes < K)
+      const long long t2 = __shfl(tile, k2, 64);
+      seen = seen || (k2 < lane && t2 != -1 && t2 == tile);
+    }
+    const unsigned cnt = (unsigned)__popcll(__ballot(cv));
+    const unsigned dist = (unsigned)__popcll(__ballot(cv && tile != -1 && !seen));
+    if (lane == 0) w.cstat[i] = cnt | (dist << 16);
+  }
 }
 
 // The pool by center-tile bucket (GCS_POOL_LDS).  Rows whose own tile is view tile c share their
@@ -1040,6 +1053,18 @@ __device__ __forceinline__ void pool_row(const AsIn& in, const AsParams& p, cons
     if (o.tile) o.tile[o_] = in.vtile[e];
     if (o.slot) o.slot[o_] = (int64_t)in.vslot[e];
   }
+  {  // the MapUpdateCert's per-row candidate statistics (cand_stats): valid candidates, distinct tiles
+    const bool cv = act && row_valid && in.vvalid[e] != 0;
+    const long long tile = cv ? (long long)in.vtile[e] : -1;
+    bool seen = false;
+    for (int k2 = 0; k2 < p.k; ++k2) {  // (every lane: the shuffles read lanes < K)
+      const long long t2 = __shfl(tile, k2, 64);
+      seen = seen || (k2 < lane && t2 != -1 && t2 == tile);
+    }
+    const unsigned cnt = (unsigned)__popcll(__ballot(cv));
+    const unsigned dist = (unsigned)__popcll(__ballot(cv && tile != -1 && !seen));
+    if (lane == 0) w.cstat[i] = cnt | (dist << 16);
+  }
   PP_STAMP(7);
 }
 
@@ -1260,8 +1285,12 @@ static_assert(CE_COUNT == GCS_ASSOC_CERT_LEN, "certificate slots");
 // eps_mass)) and the p95 order statistic of the counts with invalid rows at -1 (jnp.sort, index
 // min(int(0.95 n), n - 1)).  Every sum is of small integers, so the values are exact in any order; one
 // workgroup, LDS integer counters.  e_of(q): the view entry of candidate q.
+// (cstat: per row, cnt | dist << 16 from the pool kernel -- each row's candidates sit in its wave's
+// lanes there, so the count and the distinct tiles take a few shuffles; the per-row loop below
+// walked K^2 dependent loads per row, ~50 us of this workgroup; null: computed here)
 template <int NT, class EOF_>
-__device__ __forceinline__ void cand_stats(const AsIn& in, const AsParams& p, double eps_mass, EOF_ e_of, double* cert) {
+__device__ __forceinline__ void cand_stats(const AsIn& in, const AsParams& p, double eps_mass, EOF_ e_of, double* cert,
+                                           const uint32_t* cstat = nullptr) {
   __shared__ unsigned long long s_cs[3];  // valid rows, sum counts, sum distinct tiles
   __shared__ uint32_t s_ch[33];            // histogram of the valid rows' counts (K <= 32)
   const int t = threadIdx.x, K = p.k, N = p.n;
@@ -1273,7 +1302,12 @@ __device__ __forceinline__ void cand_stats(const AsIn& in, const AsParams& p, do
   for (int r = t; r < N; r += NT) {
     if (!in.valid[r]) continue;
     int cnt = 0, dist = 0;
-    for (int k = 0; k < K && !no_view; ++k) {
+    if (cstat) {
+      const uint32_t cs = cstat[r];
+      cnt = (int)(cs & 0xffffu);
+      dist = (int)(cs >> 16);
+    }
+    for (int k = 0; k < K && !no_view && !cstat; ++k) {
       const int e = e_of((size_t)r * K + k);
       if (!in.vvalid[e]) continue;
       ++cnt;
@@ -1646,7 +1680,7 @@ __global__ __launch_bounds__(kShThreads) void k_as_sinkhorn(AsIn in, AsParams p,
     // this workgroup ends well inside workgroup 0's iterations: the MapUpdateCert's candidate
     // statistics ride here, with no host sync of their own
     const int32_t* cand = w.cand;
-    cand_stats<kShThreads>(in, p, p.eps_mass, [cand](size_t q) { return (int)cand[q]; }, o.cert);
+    cand_stats<kShThreads>(in, p, p.eps_mass, [cand](size_t q) { return (int)cand[q]; }, o.cert, w.cstat);
     return;
   }
 #if GCS_SH_TAB
@@ -2257,6 +2291,7 @@ struct gcs_assoc_ctx {
   uint32_t* d_ticket = nullptr;
   int fin_split = GCS_SH_FINSPLIT;  // GCSLAM_SH_FINSPLIT: 0 the Sinkhorn workgroup, 2 a launch of its own (A/B)
   uint32_t* d_flag = nullptr;        // the Sinkhorn's hand-off flag
+  uint32_t* d_cstat = nullptr;       // the pools' per-row candidate statistics
   unsigned epoch = 0;
   bool pool_lds = GCS_POOL_LDS != 0;  // GCSLAM_POOL_LDS=0: k_as_pool from L2 for every view (A/B)
   bool vpe_split = GCS_VPE_SPLIT != 0;  // GCSLAM_VPE_SPLIT=0: the one-workgroup form (A/B, bitwise test)
@@ -2333,7 +2368,7 @@ int gcs_assoc_ctx_destroy(gcs_assoc_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* bufs[] = {c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, c->d_mvalid, c->d_st,
-                  c->d_vpe_rows, c->d_vc, c->d_vcnt, c->d_order, c->d_kmat, c->d_su, c->d_fpart, c->d_ticket, c->d_ctile, c->d_cpre, c->d_tcnt, c->d_flag};
+                  c->d_vpe_rows, c->d_vc, c->d_vcnt, c->d_order, c->d_kmat, c->d_su, c->d_fpart, c->d_ticket, c->d_ctile, c->d_cpre, c->d_tcnt, c->d_flag, c->d_cstat};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_cert) (void)hipHostFree(c->h_cert);
@@ -2364,7 +2399,7 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
       bad(hipMalloc(&c->d_su, (N + 40) * 8)) || bad(hipMalloc(&c->d_fpart, ((N + kFinThreads - 1) / kFinThreads) * 40 * 8)) ||
       bad(hipMalloc(&c->d_ticket, 4)) ||
       bad(hipMalloc(&c->d_ctile, (N / kPoolLdsWaves + kMaxBuckets + 1) * 64 * 4)) ||
-      bad(hipMalloc(&c->d_cpre, (N / kPoolLdsWaves + kMaxBuckets + 1) * 64 * 4)) || bad(hipMalloc(&c->d_tcnt, kMaxBuckets * 4)) || bad(hipMalloc(&c->d_flag, 4)) || bad(hipMalloc(&c->d_vcnt, kMaxBuckets * 4)) ||
+      bad(hipMalloc(&c->d_cpre, (N / kPoolLdsWaves + kMaxBuckets + 1) * 64 * 4)) || bad(hipMalloc(&c->d_tcnt, kMaxBuckets * 4)) || bad(hipMalloc(&c->d_flag, 4)) || bad(hipMalloc(&c->d_cstat, N * 4)) || bad(hipMalloc(&c->d_vcnt, kMaxBuckets * 4)) ||
       bad(hipMalloc(&c->d_order, (N + (size_t)kMaxBuckets * kPoolLdsWaves) * 4)) ||
       bad(hipHostMalloc(&c->h_cert, GCS_ASSOC_CERT_LEN * sizeof(double), hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&c->h_cert_dev, c->h_cert, 0)) ||
@@ -2482,7 +2517,7 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
   // the bucketed pool (k_as_pool_lds) for views of at most kMaxBuckets - 1 tiles
   const bool bucketed = c->pool_lds && !bad_policy && v->n_tiles + 1 <= kMaxBuckets && m->n_total <= kBucketRows * 1024;
   AsWork w{c->d_pos, c->d_dir, c->d_kap, c->d_A1, c->d_A2, c->d_dt, c->d_tix, c->d_cand, mv, mv_next, c->d_vc, c->d_vcnt,
-           c->d_order, c->d_ctile, c->d_cpre, c->d_tcnt, c->d_kmat, bucketed ? kPoolLdsWaves : 0, c->d_su, c->d_fpart, c->d_ticket, c->d_flag};
+           c->d_order, c->d_ctile, c->d_cpre, c->d_tcnt, c->d_kmat, bucketed ? kPoolLdsWaves : 0, c->d_su, c->d_fpart, c->d_ticket, c->d_flag, c->d_cstat};
   AsOut out{o->responsibilities, o->row_masses, o->cost_matrix, o->candidate_pool_indices, o->candidate_tile_ids,
             o->candidate_slots, c->h_cert_dev};
   if (ns != c->st_ns || rxy != c->st_rxy || rz != c->st_rz) {  // the stencil table changes with the radii only
