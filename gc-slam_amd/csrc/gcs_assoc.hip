@@ -56,7 +56,9 @@ constexpr int kPoolThreads = GCS_POOL_THREADS;
 #endif
 constexpr int kShThreads = GCS_SH_THREADS;
 #ifndef GCS_SH_ONEBAR
-#define GCS_SH_ONEBAR 0  // 1: v in every wave, one barrier per iteration (A/B: no faster, profiles/r04/sh1/)
+// 1: v in every wave, one barrier per iteration -- no faster while v took a pow (profiles/r04/sh1/),
+// 0.150 -> 0.144 ms per call with the Newton root (profiles/r05/assoc/); 0: v by wave 0 + a second barrier
+#define GCS_SH_ONEBAR 1
 #endif
 #ifndef GCS_SH_LOGB
 #define GCS_SH_LOGB 1  // 0: v = pow(b / K^T u, vb) with the quotient in every iteration (A/B)
