@@ -151,9 +151,11 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_clear(PmStore st, int t) {
 // mode 0: -score (score = w, -1e30 where invalid), mode 1: retention w exp(-lam dt) (-inf where invalid)
 // other_bm (may be null): bit g set where the key is not the mode's empty-slot key (k_pm_topk_sparse),
 // one 32-bit word per half wave (g is wave-aligned: 64 consecutive g per wave)
+// below (with other_bm, mode 1): per tile, the keys under the empty-slot key (a NaN retention with the
+// sign bit: none in practice) -- k_pm_topk_sparse's dense-tile shortcut needs there to be none
 __global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_t* tiles, int n, int mode,
                                                         long long seq, double lam, uint64_t* keys, uint32_t* vals,
-                                                        uint32_t* other_bm) {
+                                                        uint32_t* other_bm, uint32_t* below) {
   const long g = (long)blockIdx.x * kPmThreads + threadIdx.x;
   if (g >= (long)n * st.M) return;
   const int t = (int)(g / st.M), q = (int)(g % st.M);
@@ -179,8 +181,10 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_keys(PmStore st, const int32_
   keys[g] = kb;
   vals[g] = (uint32_t)g;  // tile position x M + slot
   if (other_bm) {
-    const uint64_t b = __ballot(kb != ord_key(mode == 0 ? 1e30 : -INFINITY));
+    const uint64_t E = ord_key(mode == 0 ? 1e30 : -INFINITY);
+    const uint64_t b = __ballot(kb != E);
     if ((threadIdx.x & 31) == 0) other_bm[g >> 5] = (uint32_t)(b >> (threadIdx.x & 32));
+    if (mode == 1 && kb < E) atomicAdd(&below[t], 1u);
   }
 }
 
@@ -747,16 +751,24 @@ __global__ __launch_bounds__(kPmRed) void k_pm_topk(const uint64_t* __restrict__
 // once).  Same result as the tree: (key, slot) pairs are distinct.
 constexpr int kSpMax = 2048;    // entries besides the empty slots
 constexpr int kSpWords = 2048;  // slot bitmap words per tile: M <= 65,536
+// Dense tiles (more than kSpMax others) in mode 1 (the eviction order) with at least k empty slots and
+// no key below the empty-slot key E: the first k of the stable order are the first k empty slots in slot
+// order (every other key is above E) -- read from the bitmap alone.  The tree took these tiles
+// (50,000 keys each, ~54 us at 7 tiles of the reference size) for an answer the bitmap holds.
 __global__ __launch_bounds__(kPmRed) void k_pm_topk_sparse(const uint64_t* __restrict__ keys,
                                                           const uint32_t* __restrict__ other_bm, int M, int k,
                                                           int mode, uint32_t* __restrict__ skip,
-                                                          uint32_t* __restrict__ sorted) {
+                                                          uint32_t* __restrict__ sorted, uint32_t* __restrict__ below) {
   __shared__ uint64_t s_k[kSpMax];
   __shared__ uint32_t s_s[kSpMax];
   __shared__ uint32_t s_wo[kPmRed / 64], s_wz[kPmRed / 64];
-  __shared__ uint32_t s_clo;
+  __shared__ uint32_t s_clo, s_below;
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid == 0) s_clo = 0u;
+  if (tid == 0) {
+    s_clo = 0u;
+    s_below = below[t];
+    below[t] = 0u;  // re-armed for the next k_pm_keys
+  }
   // the tile's words of k_pm_keys' bitmap (bit q of the tile = global bit t M + q, not word-aligned):
   // WPT consecutive tile words per thread, their set (other) and clear (empty) bits counted
   constexpr int WPT = kSpWords / kPmRed;
@@ -795,16 +807,41 @@ __global__ __launch_bounds__(kPmRed) void k_pm_topk_sparse(const uint64_t* __res
     s_wz[wid] = xz;
   }
   __syncthreads();
-  uint32_t ro = xo - no, rz = xz - nz, n = 0u;
+  uint32_t ro = xo - no, rz = xz - nz, n = 0u, nzt = 0u;
   for (int w = 0; w < kPmRed / 64; ++w) {
     if (w < wid) {
       ro += s_wo[w];
       rz += s_wz[w];
     }
     n += s_wo[w];
+    nzt += s_wz[w];
   }
-  if (n > (uint32_t)kSpMax) {  // the tree's
-    if (tid == 0) skip[t] = 0u;
+  const int kk0 = min(k, M);
+  if (n > (uint32_t)kSpMax) {
+    if (!(mode == 1 && s_below == 0u && nzt >= (uint32_t)kk0)) {  // the tree's
+      if (tid == 0) skip[t] = 0u;
+      return;
+    }
+    if (tid == 0) skip[t] = 1u;
+    uint32_t* out = sorted + (size_t)t * M;
+    const uint32_t tb = (uint32_t)((size_t)t * M);
+    uint32_t rank = rz;
+#pragma unroll
+    for (int u = 0; u < WPT; ++u) {
+      const int w = WPT * tid + u;
+      uint32_t zb = 0u;
+      if (w < nw) {
+        const int nb = min(32, M - 32 * w);
+        zb = ~ow[u] & (nb == 32 ? ~0u : ((1u << nb) - 1u));
+      }
+      while (zb != 0u && rank < (uint32_t)kk0) {
+        const int bit = __ffs((int)zb) - 1;
+        zb &= zb - 1u;
+        out[rank] = tb + (uint32_t)(32 * w + bit);
+        ++rank;
+      }
+      rank += (uint32_t)__popc(zb);
+    }
     return;
   }
   if (tid == 0) skip[t] = 1u;
@@ -1152,6 +1189,69 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmStore st, 
   const bool v = (r.valid ? r.valid[g] != 0 : true) && tp >= 0 && tp < n_tiles && ok;
   keys[g] = v ? ((uint32_t)tp * (uint32_t)M + (uint32_t)q) * (uint32_t)nb + (uint32_t)b : nokey;
   vals[g] = (uint32_t)g;
+}
+
+// The fuse's (key, row) sort for up to kSsMax rows in two launches (GCS_FUSE_SMALLSORT; rocPRIM's radix
+// sort took five launches at these sizes -- a block sort and four merge passes, ~33 us plus their host
+// dispatch).  Each pair is one u64 (key << 32 | row), so the pairs are distinct and their order is the
+// stable key order.  k_ss_block: 1,024-pair runs sorted in LDS (bitonic); k_ss_merge: every pair's
+// final position = its rank in its run + the pairs below it in every other run (a binary search of each
+// run, all runs staged in LDS), then the scatter.
+#ifndef GCS_FUSE_SMALLSORT
+#define GCS_FUSE_SMALLSORT 1
+#endif
+constexpr int kSsRun = 1024;
+constexpr int kSsMax = 16 * kSsRun;  // 128 KB of runs in k_ss_merge's LDS
+__global__ __launch_bounds__(512) void k_ss_block(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
+                                                 int n, uint64_t* __restrict__ runs) {
+  __shared__ uint64_t s[kSsRun];
+  const int t = threadIdx.x, base = blockIdx.x * kSsRun;
+  for (int i = t; i < kSsRun; i += 512) {
+    const int g = base + i;
+    s[i] = g < n ? ((uint64_t)keys[g] << 32) | (uint64_t)vals[g] : ~0ull;
+  }
+  for (int size = 2; size <= kSsRun; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      const int x = ((t & ~(stride - 1)) << 1) | (t & (stride - 1)), y = x | stride;
+      const uint64_t a = s[x], b = s[y];
+      if ((b < a) == ((x & size) == 0)) {
+        s[x] = b;
+        s[y] = a;
+      }
+    }
+  __syncthreads();
+  for (int i = t; i < kSsRun; i += 512) runs[base + i] = s[i];
+}
+__global__ __launch_bounds__(kSsRun) void k_ss_merge(const uint64_t* __restrict__ runs, int n, int nrun,
+                                                     uint32_t* __restrict__ keys_s, uint32_t* __restrict__ vals_s) {
+  __shared__ uint64_t s[kSsMax];
+  const int t = threadIdx.x;
+  for (int i = t; i < nrun * kSsRun; i += kSsRun) s[i] = runs[i];
+  __syncthreads();
+  const int g = blockIdx.x * kSsRun + t;
+  if (g >= nrun * kSsRun) return;
+  const uint64_t x = s[g];
+  if (x == ~0ull) return;  // padding (after every real pair of the last run)
+  const int j = g / kSsRun;
+  int pos = g - j * kSsRun;
+  for (int i = 0; i < nrun; ++i) {
+    if (i == j) continue;
+    const uint64_t* r = s + i * kSsRun;
+    int lo = 0, len = kSsRun;  // lower bound: the pairs of run i below x
+    while (len > 0) {
+      const int h = len >> 1;
+      if (r[lo + h] < x) {
+        lo += h + 1;
+        len -= h + 1;
+      } else {
+        len = h;
+      }
+    }
+    pos += lo;
+  }
+  keys_s[pos] = (uint32_t)(x >> 32);
+  vals_s[pos] = (uint32_t)x;
 }
 
 // Long runs of one (tile, slot, block) key -- many measurements associated to the same primitive, as
@@ -1980,6 +2080,7 @@ struct gcs_pmap {
   uint32_t* tickets = nullptr;
   uint32_t* topk_skip = nullptr;  // k_pm_topk_sparse -> k_pm_topk: the tiles it finished (max_tiles)
   uint32_t* other_bm = nullptr;   // k_pm_keys -> k_pm_topk_sparse: non-empty-key bitmap (max_tiles x M bits)
+  uint32_t* below = nullptr;      // k_pm_keys -> k_pm_topk_sparse: per tile, keys under the empty-slot key
   // small host-mapped results
   char* h_small = nullptr;
   char* d_small = nullptr;
@@ -2049,34 +2150,36 @@ int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam, int k) {
     const char* e = getenv("GCSLAM_PM_TOPK_SPARSE");
     return !(e && e[0] == '0');
   }();
-  const bool sp = sparse && k >= 1 && k <= kSelMax && p->M > 8 * kPmRed && p->M <= 32 * kSpWords;
-  hipLaunchKernelGGL(k_pm_keys, dim3(gb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, mode,
-                     seq, lam, p->keys, p->vals, sp ? p->other_bm : nullptr);
   // only the first k of each tile are read: a per-tile select + LDS sort replaces the full radix sort
   // (GCSLAM_PM_FULLSORT=1 keeps the full sort, for A/B)
   static const bool full = [] {
     const char* e = getenv("GCSLAM_PM_FULLSORT");
     return e && e[0] == '1';
   }();
-  if (k >= 1 && k <= kSelMax && !full) {
-    // high key words in registers up to 8 per thread (M <= 8,192; 52 per thread spills at 1024 threads)
-    static const bool glob = [] {
-      const char* e = getenv("GCSLAM_PM_SELECT_GLOBAL");  // A/B: the global-memory passes
-      return e && e[0] == '1';
-    }();
+  // high key words in registers up to 8 per thread (M <= 8,192; 52 per thread spills at 1024 threads)
+  static const bool glob = [] {
+    const char* e = getenv("GCSLAM_PM_SELECT_GLOBAL");  // A/B: the global-memory passes
+    return e && e[0] == '1';
+  }();
+  // GCSLAM_PM_SELECT: "radix" (one workgroup, keys read from memory each pass) for A/B; default: the
+  // register select up to 8 keys per thread (M <= 8,192), the tree of sorted runs (k_pm_topk) above.
+  // Measured at 7 x 50,000 (profiles/r03/pmap): tree 61-73 us, radix ~120 us, and the register select
+  // at 98 keys per thread (512 threads, buffer loads, no spill) 186 us -- its LDS histogram atomics
+  // on the keys' low-entropy top bits serialise.
+  static const int sel = [] {
+    const char* e = getenv("GCSLAM_PM_SELECT");
+    return e && strcmp(e, "radix") == 0 ? 2 : 0;
+  }();
+  const bool part = k >= 1 && k <= kSelMax && !full;
+  const int G = (p->M + kTopChunk - 1) / kTopChunk;
+  const bool reg8 = p->M <= 8 * kPmRed;
+  const bool use_tree = part && !glob && sel == 0 && !reg8 && G > 1 && G <= (1 << (kTopMaxLevels - 1));
+  // the sparse / dense-shortcut pass runs exactly when k_pm_keys writes its bitmap and counts
+  const bool sp = use_tree && sparse && p->M > 8 * kPmRed && p->M <= 32 * kSpWords;
+  hipLaunchKernelGGL(k_pm_keys, dim3(gb), dim3(kPmThreads), 0, p->stream, p->st, (const int32_t*)p->d_tiles, n, mode,
+                     seq, lam, p->keys, p->vals, sp ? p->other_bm : nullptr, p->below);
+  if (part) {
     const uint64_t* kk = (const uint64_t*)p->keys;
-    // GCSLAM_PM_SELECT: "radix" (one workgroup, keys read from memory each pass) for A/B; default: the
-    // register select up to 8 keys per thread (M <= 8,192), the tree of sorted runs (k_pm_topk) above.
-    // Measured at 7 x 50,000 (profiles/r03/pmap): tree 61-73 us, radix ~120 us, and the register select
-    // at 98 keys per thread (512 threads, buffer loads, no spill) 186 us -- its LDS histogram atomics
-    // on the keys' low-entropy top bits serialise.
-    static const int sel = [] {
-      const char* e = getenv("GCSLAM_PM_SELECT");
-      return e && strcmp(e, "radix") == 0 ? 2 : 0;
-    }();
-    const int G = (p->M + kTopChunk - 1) / kTopChunk;
-    const bool reg8 = p->M <= 8 * kPmRed;
-    const bool use_tree = !glob && sel == 0 && !reg8 && G > 1 && G <= (1 << (kTopMaxLevels - 1));
     if (use_tree) {
       const size_t need = (size_t)n * G * k;
       if (need > p->run_cap) {
@@ -2088,9 +2191,9 @@ int sort_tiles(gcs_pmap* p, int n, int mode, long long seq, double lam, int k) {
         PMCHK(p, hipMalloc(&p->run_slot, need * 4));
         p->run_cap = need;
       }
-      if (sp)  // sparse tiles (most map tiles): their result directly; the tree takes the others
+      if (sp)  // sparse tiles (most map tiles) and empty-rich dense ones: their result directly; the tree the others
         hipLaunchKernelGGL(k_pm_topk_sparse, dim3(n), dim3(kPmRed), 0, p->stream, kk, (const uint32_t*)p->other_bm,
-                           p->M, k, mode, p->topk_skip, p->vals);
+                           p->M, k, mode, p->topk_skip, p->vals, p->below);
       hipLaunchKernelGGL(k_pm_topk, dim3(G, n), dim3(kPmRed), 0, p->stream, kk, p->M, k, G, p->run_key, p->run_slot,
                          p->tickets, p->vals, sp ? (const uint32_t*)p->topk_skip : nullptr);
     } else if (!glob && sel != 2 && reg8)
@@ -2199,7 +2302,8 @@ int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t 
       bad(hipMemset(p->bcnt, 0, kMaxFuseBlocks * 4)) ||  // once: k_pm_publish_u32 re-zeroes
       bad(hipMalloc(&p->tickets, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
       bad(hipMemset(p->tickets, 0, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
-      bad(hipMalloc(&p->topk_skip, (size_t)max_tiles * 4)) ||
+      bad(hipMalloc(&p->topk_skip, (size_t)max_tiles * 4)) || bad(hipMalloc(&p->below, (size_t)max_tiles * 4)) ||
+      bad(hipMemset(p->below, 0, (size_t)max_tiles * 4)) ||
       bad(hipMalloc(&p->other_bm, ((size_t)max_tiles * m_tile / 32 + 4) * 4)) ||
       bad(hipMemset(p->other_bm, 0, ((size_t)max_tiles * m_tile / 32 + 4) * 4)) ||
       bad(hipHostMalloc((void**)&p->h_small, kSmall, hipHostMallocMapped)) ||
@@ -2237,7 +2341,7 @@ int gcs_pmap_destroy(gcs_pmap* p) {
     if (f) (void)hipFree(f);
   void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->seg, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
                   p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->bmark, p->bcnt, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
-                  p->msel, p->mnsel, p->ub, p->run_key, p->run_slot, p->tickets, p->fterm, p->flen, p->topk_skip, p->other_bm};
+                  p->msel, p->mnsel, p->ub, p->run_key, p->run_slot, p->tickets, p->fterm, p->flen, p->topk_skip, p->other_bm, p->below};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (p->h_small) (void)hipHostFree(p->h_small);
@@ -2493,7 +2597,7 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
     PMCHK(p, hipMalloc(&p->fv_s, cap * 4));
     size_t tb = 0;
     PMCHK(p, rocprim::radix_sort_pairs(nullptr, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)cap, 0u, 32u, p->stream));
-    p->ftemp_bytes = std::max<size_t>(tb, 16);
+    p->ftemp_bytes = std::max<size_t>(tb, (size_t)kSsMax * 8);  // (also k_ss_block's runs)
     PMCHK(p, hipMalloc(&p->ftemp, p->ftemp_bytes));
     p->frows = cap;
   }
@@ -2524,8 +2628,20 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
   const uint32_t nokey = bits >= 32 ? kNoKey : (uint32_t)((1ull << bits) - 1ull);
   hipLaunchKernelGGL(k_pm_fuse_keys_blocks, dim3(rb), dim3(kPmThreads), 0, p->stream, p->st,
                      (const int32_t*)p->d_tiles, timestamp, r, n, p->M, nb, rpb, p->fk, p->fv, p->bmark, d_err, nokey);
-  size_t tb = p->ftemp_bytes;
-  PMCHK(p, rocprim::radix_sort_pairs(p->ftemp, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)R, 0u, bits, p->stream));
+  static const bool small_sort = [] {
+    const char* e = getenv("GCSLAM_FUSE_SMALLSORT");
+    return GCS_FUSE_SMALLSORT && !(e && e[0] == '0');
+  }();
+  if (small_sort && R <= kSsMax && p->ftemp_bytes >= (size_t)kSsMax * 8) {
+    const int nrun = (R + kSsRun - 1) / kSsRun;
+    hipLaunchKernelGGL(k_ss_block, dim3(nrun), dim3(512), 0, p->stream, (const uint32_t*)p->fk, (const uint32_t*)p->fv, R,
+                       (uint64_t*)p->ftemp);
+    hipLaunchKernelGGL(k_ss_merge, dim3(nrun), dim3(kSsRun), 0, p->stream, (const uint64_t*)p->ftemp, R, nrun, p->fk_s,
+                       p->fv_s);
+  } else {
+    size_t tb = p->ftemp_bytes;
+    PMCHK(p, rocprim::radix_sort_pairs(p->ftemp, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)R, 0u, bits, p->stream));
+  }
   if ((size_t)R * kFT > p->fterm_n) {
     if (p->fterm) PMCHK(p, hipFree(p->fterm));
     if (p->flen) PMCHK(p, hipFree(p->flen));
