@@ -1212,7 +1212,13 @@ __global__ __launch_bounds__(512) void k_ss_block(const uint32_t* __restrict__ k
   }
   for (int size = 2; size <= kSsRun; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      __syncthreads();
+      // strides below 64: a wave's pairs lie in its own 128 entries (wave-ordered LDS, no block barrier)
+      if (stride >= 64 || size == 2) {
+        __syncthreads();
+      } else {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      }
       const int x = ((t & ~(stride - 1)) << 1) | (t & (stride - 1)), y = x | stride;
       const uint64_t a = s[x], b = s[y];
       if ((b < a) == ((x & size) == 0)) {
@@ -1235,21 +1241,18 @@ __global__ __launch_bounds__(kSsRun) void k_ss_merge(const uint64_t* __restrict_
   if (x == ~0ull) return;  // padding (after every real pair of the last run)
   const int j = g / kSsRun;
   int pos = g - j * kSsRun;
-  for (int i = 0; i < nrun; ++i) {
-    if (i == j) continue;
-    const uint64_t* r = s + i * kSsRun;
-    int lo = 0, len = kSsRun;  // lower bound: the pairs of run i below x
-    while (len > 0) {
-      const int h = len >> 1;
-      if (r[lo + h] < x) {
-        lo += h + 1;
-        len -= h + 1;
-      } else {
-        len = h;
-      }
-    }
-    pos += lo;
-  }
+  // the pairs of every other run below x: fixed-step lower bounds, the runs' searches side by side
+  int lo[kSsMax / kSsRun];
+#pragma unroll
+  for (int i = 0; i < kSsMax / kSsRun; ++i) lo[i] = 0;
+#pragma unroll
+  for (int step = kSsRun / 2; step >= 1; step >>= 1)
+#pragma unroll
+    for (int i = 0; i < kSsMax / kSsRun; ++i)
+      if (i < nrun && s[i * kSsRun + lo[i] + step - 1] < x) lo[i] += step;
+#pragma unroll
+  for (int i = 0; i < kSsMax / kSsRun; ++i)
+    if (i < nrun && i != j) pos += lo[i] + (lo[i] == kSsRun - 1 && s[i * kSsRun + kSsRun - 1] < x ? 1 : 0);
   keys_s[pos] = (uint32_t)(x >> 32);
   vals_s[pos] = (uint32_t)x;
 }
@@ -1419,6 +1422,15 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st,
   constexpr int ne = 3 * kNL;
   const int t = (int)(grp / (uint32_t)st.M), q = (int)(grp % (uint32_t)st.M);
   const size_t i = sidx(st, tiles[t], q);
+  // the slot's accumulators first: their loads overlap the rows' (the adds below keep their order)
+  double sL[9], sth[3], sacc[3], se[ne], sw = st.w[i], scam = st.cam[i], slid = st.lid[i], sden = st.den[i];
+  for (int c = 0; c < 9; ++c) sL[c] = st.lam[9 * i + c];
+  for (int c = 0; c < 3; ++c) {
+    sth[c] = st.th[3 * i + c];
+    sacc[c] = st.acc[3 * i + c];
+  }
+  for (int c = 0; c < ne; ++c) se[c] = st.eta[(size_t)ne * i + c];
+  bool sup = false;
   int pos = g;
   while (pos < r.n && keys[pos] != nokey && keys[pos] / (uint32_t)nb == grp) {
     const uint32_t kb = keys[pos];
@@ -1485,20 +1497,32 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st,
         }
       }
     }
-    for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = st.lam[9 * i + c] + dL[c];
+    // (one block's run: added to the slot in block order, as the per-block fuse steps do)
+    for (int c = 0; c < 9; ++c) sL[c] = sL[c] + dL[c];
     for (int c = 0; c < 3; ++c) {
-      st.th[3 * i + c] = st.th[3 * i + c] + dth[c];
-      st.acc[3 * i + c] = st.acc[3 * i + c] + dacc[c];
+      sth[c] = sth[c] + dth[c];
+      sacc[c] = sacc[c] + dacc[c];
     }
-    for (int c = 0; c < ne; ++c) st.eta[(size_t)ne * i + c] = st.eta[(size_t)ne * i + c] + de[c];
-    st.w[i] = st.w[i] + dw;
-    st.cam[i] = st.cam[i] + dcam;
-    st.lid[i] = st.lid[i] + dlid;
-    st.den[i] = st.den[i] + dden;
-    if (drs > 0.0) {
-      st.lsup[i] = seq;
-      st.lupd[i] = seq;
-    }
+    for (int c = 0; c < ne; ++c) se[c] = se[c] + de[c];
+    sw = sw + dw;
+    scam = scam + dcam;
+    slid = slid + dlid;
+    sden = sden + dden;
+    sup = sup || drs > 0.0;
+  }
+  for (int c = 0; c < 9; ++c) st.lam[9 * i + c] = sL[c];
+  for (int c = 0; c < 3; ++c) {
+    st.th[3 * i + c] = sth[c];
+    st.acc[3 * i + c] = sacc[c];
+  }
+  for (int c = 0; c < ne; ++c) st.eta[(size_t)ne * i + c] = se[c];
+  st.w[i] = sw;
+  st.cam[i] = scam;
+  st.lid[i] = slid;
+  st.den[i] = sden;
+  if (sup) {
+    st.lsup[i] = seq;
+    st.lupd[i] = seq;
   }
 }
 
