@@ -163,3 +163,33 @@ def test_association_deterministic():
     r2, _, _ = GA.associate_primitives_ot(b, v)
     for k in ("responsibilities", "cost_matrix", "row_masses", "candidate_pool_indices"):
         assert torch.equal(getattr(r1, k), getattr(r2, k)), k
+
+
+def _knob_paths_check():
+    """Run in a subprocess with one of the association's A/B knobs set (they are read once per context
+    creation / process): the reference-size scene and two config variants against the oracle."""
+    for seed in (0, 1):
+        batch, view, _ = make_scene(seed=seed)
+        _check(*_run_both(batch, view, OA.AssociationConfig(scan_seq=10)), batch["valid_mask"])
+    kw = dict(seed=7, n_feat=128, n_surfel=256, n_valid_cam=60, n_valid_lidar=200, m_tile=256, m_tile_view=256)
+    batch, view, _ = make_scene(**kw)
+    for extra in (dict(cost_scale_by_median=True, cost_subtract_row_min=False), dict(k_sinkhorn=0)):
+        _check(*_run_both(batch, view, OA.AssociationConfig(scan_seq=10, **extra)), batch["valid_mask"])
+
+
+@pytest.mark.parametrize("env", [{"GCSLAM_POOL_LDS": "0"}, {"GCSLAM_SH_FINSPLIT": "0"}, {"GCSLAM_SH_FINSPLIT": "2"}],
+                         ids=["pool_l2", "finish_in_wg0", "finish_own_launch"])
+def test_association_knob_paths_match_oracle(env):
+    """The defaults are the bucketed LDS pool (k_as_stage + k_as_pool_lds) and the finish in extra
+    workgroups of the Sinkhorn launch; the one-workgroup-per-row pool from L2 and the two other finish
+    forms stay selectable (A/B) and keep their own parity check."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_association as t; t._knob_paths_check()"
+            % (here, root, os.path.join(root, "gc-slam_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]

@@ -484,3 +484,23 @@ def test_topk_tree_handoff_stress():
                 assert np.array_equal(got[i], ref), (rep, t, np.flatnonzero(got[i] != ref)[:8])
     finally:
         am.close()
+
+
+@pytest.mark.parametrize("env", [{"GCSLAM_FUSE_SMALLSORT": "0"}, {"GCSLAM_PM_TOPK_SPARSE": "0"}],
+                         ids=["fuse_rocprim_sort", "topk_tree_only"])
+def test_reference_size_map_update_knob_paths(env):
+    """Step 12b's defaults are the two-launch LDS sort of the fuse keys (k_ss_block + k_ss_merge) and the
+    empty-slot shortcut of the eviction order on dense tiles (k_pm_topk_sparse); rocPRIM's radix sort
+    and the tree of sorted runs for every tile stay selectable (A/B) and keep their own parity check on
+    the reference-size dense scene."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_primitive_map as t; "
+            "t.test_reference_size_view_and_map_update((0.999, 0.8, 0.8, 0.8, 0.8, 0.0))"
+            % (here, root, os.path.join(root, "gc-slam_amd")))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
