@@ -28,6 +28,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -811,8 +812,19 @@ def main():
             follow(prepared[state["count"] % N_SCANS])
         state["count"] += 1
 
-    for _ in range(args.warmup):
+    share = sorted(os.sched_getaffinity(0))
+    for wi in range(args.warmup):
         step()
+        # after the warm-up's first scan (which starts the launch worker; it keeps the whole share) the
+        # main thread runs on one core of the rank's share -- the last one, away from the low CPUs that
+        # take interrupts: the scan's serial host numerics stop migrating between cores, and the rest of
+        # the warm-up warms that core (GCSLAM_BENCH_PIN_MAIN=0: the share for every thread, for A/B)
+        if wi == 0 and os.environ.get("GCSLAM_BENCH_PIN_MAIN", "1") != "0" and len(share) >= 4:
+            try:
+                os.sched_setaffinity(threading.get_native_id(), {share[-1]})
+                pin = dict(pin, main_thread_cpu=share[-1])
+            except OSError:
+                pass
     state["warm_stamp"] = False
     state["sample"] = True
     ctx.synchronize()
@@ -875,6 +887,8 @@ def main():
         state["combine"] = combine
     state["fused"] = fused
     state["stamp"] = True
+    if "main_thread_cpu" in pin:  # the share again (the C3 pass, the live path, the CPU baseline's processes)
+        os.sched_setaffinity(threading.get_native_id(), set(share))
     # the roofline kernel's duration: the timed region's stamped launches (every TIMING_STRIDE-th scan)
     # plus, when those are fewer than ROOFLINE_MIN (short runs), a pass stamping it on every scan
     if bins_in_region < ROOFLINE_MIN:
