@@ -240,17 +240,12 @@ __device__ __forceinline__ void solve3_pivot(const double* L, double eps, const 
   x[0] = ((A[0][3] - A[0][1] * x[1]) - A[0][2] * x[2]) / A[0][0];
 }
 
-__global__ __launch_bounds__(kAsThreads) void k_as_prep(AsIn in, AsParams p, AsWork w, const int8_t* __restrict__ st) {
+// one lane of the prep: row lanes g < n (mean position, direction, kappa, A_vmf, the stencil tiles'
+// view indices), view lanes n <= g < n + m_pool (A_vmf of the entry's kappa, the valid counts)
+__device__ __forceinline__ void prep_lane(const AsIn& in, const AsParams& p, const AsWork& w,
+                                          const int8_t* __restrict__ st, int g, const int64_t* s_tid, bool lds_tiles,
+                                          bool count_tiles) {
 #pragma clang fp contract(off)
-  const int g = blockIdx.x * kAsThreads + threadIdx.x;
-  // the view's tile ids in LDS (broadcast reads) for the stencil lookups of the row lanes
-  constexpr int kLdsTiles = 256;
-  __shared__ int64_t s_tid[kLdsTiles];
-  const bool lds_tiles = p.n_tiles <= kLdsTiles;
-  if (lds_tiles && blockIdx.x * kAsThreads < p.n) {
-    for (int q = threadIdx.x; q < p.n_tiles; q += kAsThreads) s_tid[q] = in.tile_ids[q];
-    __syncthreads();
-  }
   if (g < p.n) {
     const int i = g;
     double L[9], th[3], x[3];
@@ -306,7 +301,7 @@ __global__ __launch_bounds__(kAsThreads) void k_as_prep(AsIn in, AsParams p, AsW
   if (vm != 0ull) {
     const int first = __ffsll((long long)vm) - 1;
     if (lane == first) atomicAdd(w.mvalid, (unsigned)__popcll(vm));
-    if (w.chunk) {
+    if (w.chunk && count_tiles) {
       const int te = vv ? e / p.m_view : -1;
       const int t0 = __shfl(te, first, 64);
       if (__ballot(vv && te != t0) == 0ull) {
@@ -316,6 +311,19 @@ __global__ __launch_bounds__(kAsThreads) void k_as_prep(AsIn in, AsParams p, AsW
       }
     }
   }
+}
+
+__global__ __launch_bounds__(kAsThreads) void k_as_prep(AsIn in, AsParams p, AsWork w, const int8_t* __restrict__ st) {
+  const int g = blockIdx.x * kAsThreads + threadIdx.x;
+  // the view's tile ids in LDS (broadcast reads) for the stencil lookups of the row lanes
+  constexpr int kLdsTiles = 256;
+  __shared__ int64_t s_tid[kLdsTiles];
+  const bool lds_tiles = p.n_tiles <= kLdsTiles;
+  if (lds_tiles && blockIdx.x * kAsThreads < p.n) {
+    for (int q = threadIdx.x; q < p.n_tiles; q += kAsThreads) s_tid[q] = in.tile_ids[q];
+    __syncthreads();
+  }
+  prep_lane(in, p, w, st, g, s_tid, lds_tiles, true);
 }
 
 template <int KM>
@@ -655,34 +663,42 @@ __device__ unsigned long long g_pool_probe[4096 * 10];
 // into vc[b MV ..] as (x, y, z, slot) in f32, their count in vcnt[b].  Workgroup n_tiles: each row's
 // slot in its bucket (LDS counters), bucket b's padded start (exclusive scan of ceil(count / chunk) x
 // chunk), the order list (-1 everywhere first), every row at its bucket's start + its slot.
+// view tile tb's valid entries in slot order (a block scan of wave ballots, 1,024 threads) into
+// vc[tb MV ..] as (x, y, z, slot) in f32, their count in vcnt[tb]
+__device__ __forceinline__ void compact_tile(const AsIn& in, const AsParams& p, const AsWork& w, int tb,
+                                             uint32_t* s_wsum /*16*/) {
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int MV = p.m_view;
+  uint32_t base = 0;
+  for (int c0 = 0; c0 < MV; c0 += 1024) {
+    const int oo = c0 + t;
+    const size_t e = (size_t)tb * MV + oo;
+    const bool v = oo < MV && in.vvalid[e] != 0;
+    const unsigned long long bm = __ballot(v);
+    if (lane == 0) s_wsum[wid] = (uint32_t)__popcll(bm);
+    __syncthreads();
+    uint32_t off = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull)), tot = 0;
+    for (int q = 0; q < 16; ++q) {
+      const uint32_t c = s_wsum[q];
+      if (q < wid) off += c;
+      tot += c;
+    }
+    if (v)
+      w.vc[(size_t)tb * MV + off] = make_float4((float)in.vpos[3 * e], (float)in.vpos[3 * e + 1],
+                                                (float)in.vpos[3 * e + 2], (float)oo);
+    base += tot;
+    __syncthreads();  // (s_wsum is rewritten by the next chunk)
+  }
+  if (t == 0) w.vcnt[tb] = (int32_t)base;
+}
+
 __global__ __launch_bounds__(1024) void k_as_stage(AsIn in, AsParams p, AsWork w, int nb, int cap) {
   __shared__ uint32_t s_wsum[16];
   __shared__ uint32_t s_cnt[kMaxBuckets];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int MV = p.m_view;
   if ((int)blockIdx.x < p.n_tiles) {
-    const int tb = blockIdx.x;
-    uint32_t base = 0;
-    for (int c0 = 0; c0 < MV; c0 += 1024) {
-      const int oo = c0 + t;
-      const size_t e = (size_t)tb * MV + oo;
-      const bool v = oo < MV && in.vvalid[e] != 0;
-      const unsigned long long bm = __ballot(v);
-      if (lane == 0) s_wsum[wid] = (uint32_t)__popcll(bm);
-      __syncthreads();
-      uint32_t off = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull)), tot = 0;
-      for (int q = 0; q < 16; ++q) {
-        const uint32_t c = s_wsum[q];
-        if (q < wid) off += c;
-        tot += c;
-      }
-      if (v)
-        w.vc[(size_t)tb * MV + off] = make_float4((float)in.vpos[3 * e], (float)in.vpos[3 * e + 1],
-                                                  (float)in.vpos[3 * e + 2], (float)oo);
-      base += tot;
-      __syncthreads();  // (s_wsum is rewritten by the next chunk)
-    }
-    if (t == 0) w.vcnt[tb] = (int32_t)base;
+    compact_tile(in, p, w, blockIdx.x, s_wsum);
     return;
   }
   const int C = w.chunk, S = p.n_stencil;
@@ -756,6 +772,163 @@ __global__ __launch_bounds__(1024) void k_as_stage(AsIn in, AsParams p, AsWork w
       const int tj = w.ctile[(size_t)c * 64 + s2];
       pre += tj >= 0 ? (int)s_tc[tj] : 0;
     }
+    w.cpre[(size_t)c * 64 + sq] = pre;
+  }
+}
+
+// GCS_PREP_FUSED: k_as_prep and k_as_stage as one launch for views of at most kFusedTiles tiles
+// (1,024-thread blocks): the prep's row and view lanes, one block per view tile compacting it, and one
+// block that buckets the rows.  That block cannot read the row lanes' results (same launch), so it
+// recomputes what it needs from the inputs with the same device code: each row's mean position and
+// own tile (bitwise the row lanes' values), the view tiles' valid counts, and per bucket the stencil
+// tiles of its cell (rows of a bucket share the cell modulo the 21-bit tile id fields).  Measured
+// slower (profiles/r05/assoc/prepfused_*: the launch 29 us against 8.6 + 7.7 us for the two, the bucket
+// block's serial recomputation being the longest lane of it; C-ABI 0.156 vs 0.145 ms): off by default,
+// GCSLAM_PREP_FUSED=1 for A/B.
+#ifndef GCS_PREP_FUSED
+#define GCS_PREP_FUSED 0
+#endif
+constexpr int kFusedTiles = 256;
+constexpr int kFusedBuckets = kFusedTiles + 1;
+__global__ __launch_bounds__(1024) void k_as_prep_fused(AsIn in, AsParams p, AsWork w, const int8_t* __restrict__ st,
+                                                        int lane_blocks, int cap) {
+#pragma clang fp contract(off)
+  __shared__ int64_t s_tid[kFusedTiles];
+  __shared__ uint32_t s_wsum[16];
+  __shared__ uint32_t s_cnt[kFusedBuckets], s_off[kFusedBuckets], s_tc[kFusedTiles];
+  __shared__ int32_t s_bcell[kFusedBuckets * 3];
+  __shared__ int32_t s_btix[kFusedBuckets * kMaxStencil];
+  __shared__ int16_t s_cbk[kMaxBuckets];  // chunk -> bucket (chunks <= rows / 8 + buckets)
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int b = blockIdx.x;
+  const int NT = p.n_tiles, S = p.n_stencil, MV = p.m_view, C = w.chunk;
+  if (b < lane_blocks) {
+    if (b * 1024 < p.n) {
+      for (int q = t; q < NT; q += 1024) s_tid[q] = in.tile_ids[q];
+      __syncthreads();
+    }
+    prep_lane(in, p, w, st, b * 1024 + t, s_tid, true, false);
+    return;
+  }
+  if (b < lane_blocks + NT) {
+    compact_tile(in, p, w, b - lane_blocks, s_wsum);
+    return;
+  }
+  // ---- the bucket block
+  const int nb = NT + 1;
+  for (int q = t; q < NT; q += 1024) {
+    s_tid[q] = in.tile_ids[q];
+    s_tc[q] = 0u;
+  }
+  for (int q = t; q < nb; q += 1024) s_cnt[q] = 0u;
+  for (int q = t; q < cap; q += 1024) w.order[q] = -1;
+  __syncthreads();
+  {  // the view tiles' valid counts (loads first, then one LDS add per tile run of the thread's bytes)
+    const int tot = NT * MV;
+    constexpr int kB = 32;  // bytes per thread and pass
+    for (int e0 = t * kB; e0 < tot; e0 += 1024 * kB) {
+      uint8_t v[kB];
+#pragma unroll
+      for (int u = 0; u < kB; ++u) v[u] = e0 + u < tot ? in.vvalid[e0 + u] : 0;
+      int run_t = e0 / MV;
+      uint32_t run_n = 0u;
+#pragma unroll
+      for (int u = 0; u < kB; ++u) {
+        if (e0 + u >= tot) break;
+        const int tb = (e0 + u) / MV;
+        if (tb != run_t) {
+          if (run_n) atomicAdd(&s_tc[run_t], run_n);
+          run_t = tb;
+          run_n = 0u;
+        }
+        run_n += v[u] != 0 ? 1u : 0u;
+      }
+      if (run_n) atomicAdd(&s_tc[run_t], run_n);
+    }
+  }
+  // each row's own tile: the row lanes' solve and cell (the same code), its first match in the view
+  int rb[kBucketRows];
+  uint32_t rs[kBucketRows];
+#pragma unroll
+  for (int j = 0; j < kBucketRows; ++j) {
+    const int i = t + j * 1024;
+    rb[j] = 0;
+    rs[j] = 0u;
+    if (i < p.n) {
+      double L[9], th[3], x[3];
+      for (int k = 0; k < 9; ++k) L[k] = in.Lambdas[9 * i + k];
+      for (int k = 0; k < 3; ++k) th[k] = in.thetas[3 * i + k];
+      solve3_pivot(L, p.eps_lift, th, x);
+      const double s1 = x[0];
+      const double s2 = x[0] * 0.5 + x[1] * kSqrt3Half;
+      const int64_t c1 = (int64_t)floor(s1 / p.h), c2 = (int64_t)floor(s2 / p.h), cz = (int64_t)floor(x[2] / p.h);
+      int cb = -1;
+      if (p.s_center >= 0) {
+        const int sc = p.s_center;
+        const int64_t id = pack_tile(c1 + st[3 * sc], c2 + st[3 * sc + 1], cz + st[3 * sc + 2]);
+        for (int q = NT - 1; q >= 0; --q) cb = s_tid[q] == id ? q : cb;
+      }
+      rb[j] = cb + 1;
+      rs[j] = atomicAdd(&s_cnt[rb[j]], 1u);  // (arrival order: any -- each row's result is its own)
+      if (rs[j] == 0u) {  // the bucket's cell (any row's: they agree in the tile id's 21-bit fields)
+        s_bcell[3 * rb[j]] = (int32_t)(c1 & kMask);
+        s_bcell[3 * rb[j] + 1] = (int32_t)(c2 & kMask);
+        s_bcell[3 * rb[j] + 2] = (int32_t)(cz & kMask);
+      }
+    }
+  }
+  __syncthreads();
+  // buckets' padded starts (exclusive scan of ceil(count / C) x C over the <= 257 buckets)
+  {
+    const uint32_t pc = t < nb ? (s_cnt[t] + (uint32_t)C - 1u) / (uint32_t)C * (uint32_t)C : 0u;
+    uint32_t inc = pc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)inc, off, 64);
+      if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_wsum[wid] = inc;
+    __syncthreads();
+    uint32_t run = inc - pc;
+    for (int v2 = 0; v2 < wid; ++v2) run += s_wsum[v2];
+    if (t < nb) s_off[t] = run;
+  }
+  __syncthreads();
+  // the order list, the chunk -> bucket map, per bucket its stencil tiles' view indices
+#pragma unroll
+  for (int j = 0; j < kBucketRows; ++j) {
+    const int i = t + j * 1024;
+    if (i < p.n) w.order[s_off[rb[j]] + rs[j]] = i;
+  }
+  const int nch = cap / C;
+  for (int q = t; q < nch; q += 1024) s_cbk[q] = -1;
+  __syncthreads();
+  for (int bk = t; bk < nb; bk += 1024) {
+    const int c0 = (int)(s_off[bk] / (uint32_t)C), nc = (int)((s_cnt[bk] + (uint32_t)C - 1u) / (uint32_t)C);
+    for (int c = 0; c < nc; ++c) s_cbk[c0 + c] = (int16_t)bk;
+  }
+  for (int q = t; q < nb * S; q += 1024) {
+    const int bk = q / S, sq = q - bk * S;
+    int hit = -1;
+    if (s_cnt[bk] > 0u) {
+      const int64_t id = pack_tile((int64_t)s_bcell[3 * bk] + st[3 * sq], (int64_t)s_bcell[3 * bk + 1] + st[3 * sq + 1],
+                                   (int64_t)s_bcell[3 * bk + 2] + st[3 * sq + 2]);
+      for (int qq = NT - 1; qq >= 0; --qq) hit = s_tid[qq] == id ? qq : hit;
+    }
+    s_btix[bk * S + sq] = hit;
+  }
+  __syncthreads();
+  // every chunk's record: its bucket's stencil tiles and the inclusive prefix of their valid counts
+  for (int q = t; q < nch * S; q += 1024) {
+    const int c = q / S, sq = q - c * S;
+    const int bk = s_cbk[c];
+    if (bk < 0) continue;
+    int pre = 0;
+    for (int s2 = 0; s2 <= sq; ++s2) {
+      const int tj = s_btix[bk * S + s2];
+      pre += tj >= 0 ? (int)s_tc[tj] : 0;
+    }
+    w.ctile[(size_t)c * 64 + sq] = s_btix[bk * S + sq];
     w.cpre[(size_t)c * 64 + sq] = pre;
   }
 }
@@ -2296,6 +2469,7 @@ struct gcs_assoc_ctx {
   uint32_t* d_cstat = nullptr;       // the pools' per-row candidate statistics
   unsigned epoch = 0;
   bool pool_lds = GCS_POOL_LDS != 0;  // GCSLAM_POOL_LDS=0: k_as_pool from L2 for every view (A/B)
+  bool prep_fused = GCS_PREP_FUSED != 0;  // GCSLAM_PREP_FUSED=1: k_as_prep and k_as_stage as one launch (A/B)
   bool vpe_split = GCS_VPE_SPLIT != 0;  // GCSLAM_VPE_SPLIT=0: the one-workgroup form (A/B, bitwise test)
   int probe_iters = 0;       // GCS_SH_PROBE builds: the last launch's Sinkhorn iterations
   int probe_rows = 0;        // GCS_POOL_PROBE builds: the last launch's rows
@@ -2416,6 +2590,7 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
   }
   if (const char* e = getenv("GCSLAM_VPE_SPLIT")) c->vpe_split = atoi(e) != 0;
   if (const char* e = getenv("GCSLAM_POOL_LDS")) c->pool_lds = atoi(e) != 0;
+  if (const char* e = getenv("GCSLAM_PREP_FUSED")) c->prep_fused = atoi(e) != 0;
   if (const char* e = getenv("GCSLAM_SH_FINSPLIT")) c->fin_split = atoi(e);
   // the LDS pool's dynamic LDS reaches 160 KB (the view table + the waves' rings)
   (void)hipFuncSetAttribute((const void*)k_as_pool_lds<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -2531,7 +2706,17 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
   }
   // (the valid-entry counter k_as_prep adds to is re-armed by the Sinkhorn kernel that reads it)
   const int nprep = (int)((p.n + pool + kAsThreads - 1) / kAsThreads);
-  hipLaunchKernelGGL(k_as_prep, dim3(nprep), dim3(kAsThreads), 0, s, in, p, w, (const int8_t*)c->d_st);
+  // (the fused prep: prep + stage in one launch -- bucketed pools on views of <= kFusedTiles tiles)
+  const bool fused_prep = bucketed && c->prep_fused && v->n_tiles <= kFusedTiles &&
+                          (long)p.n + (long)(v->n_tiles + 1) * kPoolLdsWaves <= (long)kMaxBuckets * 8;
+  if (fused_prep) {
+    const int lane_blocks = (int)((p.n + pool + 1023) / 1024);
+    const int cap = p.n + (v->n_tiles + 1) * kPoolLdsWaves;
+    hipLaunchKernelGGL(k_as_prep_fused, dim3(lane_blocks + v->n_tiles + 1), dim3(1024), 0, s, in, p, w,
+                       (const int8_t*)c->d_st, lane_blocks, cap);
+  } else {
+    hipLaunchKernelGGL(k_as_prep, dim3(nprep), dim3(kAsThreads), 0, s, in, p, w, (const int8_t*)c->d_st);
+  }
   // every return between here and the Sinkhorn's launch skips the kernel that zeroes the next
   // call's counter: this guard zeroes it instead (the next call would otherwise start from the
   // count of the call before this one)
@@ -2549,7 +2734,7 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
     if (bucketed) {
       const int nb = v->n_tiles + 1;
       const int cap = p.n + nb * kPoolLdsWaves;  // rows + every bucket's padding, at most
-      hipLaunchKernelGGL(k_as_stage, dim3(v->n_tiles + 1), dim3(1024), 0, s, in, p, w, nb, cap);
+      if (!fused_prep) hipLaunchKernelGGL(k_as_stage, dim3(v->n_tiles + 1), dim3(1024), 0, s, in, p, w, nb, cap);
       const int lds_slots = (long)ns * p.m_view <= kPoolLdsMaxView ? ns * p.m_view : 0;
       const size_t lds = (size_t)lds_slots * 16 + (size_t)kPoolLdsWaves * kLRing * 8;
       hipLaunchKernelGGL(k_lds, dim3((cap + kPoolLdsWaves - 1) / kPoolLdsWaves), dim3(kPoolLdsWaves * 64), lds, s, in, p,

@@ -177,12 +177,14 @@ def _knob_paths_check():
         _check(*_run_both(batch, view, OA.AssociationConfig(scan_seq=10, **extra)), batch["valid_mask"])
 
 
-@pytest.mark.parametrize("env", [{"GCSLAM_POOL_LDS": "0"}, {"GCSLAM_SH_FINSPLIT": "0"}, {"GCSLAM_SH_FINSPLIT": "2"}],
-                         ids=["pool_l2", "finish_in_wg0", "finish_own_launch"])
+@pytest.mark.parametrize("env", [{"GCSLAM_POOL_LDS": "0"}, {"GCSLAM_SH_FINSPLIT": "0"}, {"GCSLAM_SH_FINSPLIT": "2"},
+                                 {"GCSLAM_PREP_FUSED": "1"}],
+                         ids=["pool_l2", "finish_in_wg0", "finish_own_launch", "prep_stage_one_launch"])
 def test_association_knob_paths_match_oracle(env):
-    """The defaults are the bucketed LDS pool (k_as_stage + k_as_pool_lds) and the finish in extra
-    workgroups of the Sinkhorn launch; the one-workgroup-per-row pool from L2 and the two other finish
-    forms stay selectable (A/B) and keep their own parity check."""
+    """The defaults are the bucketed LDS pool (k_as_prep, k_as_stage, k_as_pool_lds) and the finish in
+    extra workgroups of the Sinkhorn launch; the one-workgroup-per-row pool from L2, the prep and staging
+    as one launch (k_as_prep_fused) and the two other finish forms stay selectable (A/B) and keep their
+    own parity check."""
     import os
     import subprocess
     import sys
