@@ -1233,7 +1233,14 @@ __global__ __launch_bounds__(kSsRun) void k_ss_merge(const uint64_t* __restrict_
                                                      uint32_t* __restrict__ keys_s, uint32_t* __restrict__ vals_s) {
   __shared__ uint64_t s[kSsMax];
   const int t = threadIdx.x;
-  for (int i = t; i < nrun * kSsRun; i += kSsRun) s[i] = runs[i];
+  {  // every run's loads in flight before the LDS stores (one round trip, not one per run)
+    uint64_t v[kSsMax / kSsRun];
+#pragma unroll
+    for (int i = 0; i < kSsMax / kSsRun; ++i) v[i] = i < nrun ? runs[i * kSsRun + t] : 0ull;
+#pragma unroll
+    for (int i = 0; i < kSsMax / kSsRun; ++i)
+      if (i < nrun) s[i * kSsRun + t] = v[i];
+  }
   __syncthreads();
   const int g = blockIdx.x * kSsRun + t;
   if (g >= nrun * kSsRun) return;
