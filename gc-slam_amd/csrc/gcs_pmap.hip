@@ -1536,8 +1536,14 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st,
 // unique slots per block (grid: blocks of slots x nb): integer atomics into device counters
 // Each mark is read by one lane, which clears it: the marks are all zero again for the next call
 // (zeroed once at allocation; no per-call fill).
-__global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(uint8_t* mark, int M, uint32_t* cnt) {
+// ticket (may be null): the last block to finish publishes the nb counters to dst (the mapped buffer)
+// and re-arms them and the ticket -- the counts are device-scope atomics drained (vmcnt) before each
+// block's relaxed ticket add and read back as agent-scope atomic loads (no release fence, no L2
+// write-back); this was a launch of its own (k_pm_publish_u32, ~5 us of step 12b)
+__global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(uint8_t* mark, int M, uint32_t* cnt,
+                                                                      uint32_t* ticket, int nb, uint32_t* dst) {
   __shared__ double lds[kPmThreads / 64];
+  __shared__ int s_last;
   const int b = blockIdx.y;
   double c = 0.0;
   for (int q = blockIdx.x * kPmThreads + threadIdx.x; q < M; q += gridDim.x * kPmThreads) {
@@ -1547,6 +1553,20 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(uint8_t* m
   }
   c = block_sum_d<kPmThreads>(c, lds);
   if (threadIdx.x == 0 && c > 0.0) atomicAdd(cnt + b, (uint32_t)c);
+  if (!ticket) return;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = tk == gridDim.x * gridDim.y - 1u ? 1 : 0;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  for (int i = threadIdx.x; i < nb; i += kPmThreads) {
+    dst[i] = __hip_atomic_load(cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(cnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // unique target slots: per-block counts of the marks, added with an integer atomic (exact in any order)
@@ -1901,15 +1921,6 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fm_sums(const double* fm, con
   if (threadIdx.x == 0) out[b * n + t] = s;
 }
 
-// device counters into the mapped buffer (one launch instead of a device-to-host copy)
-// copies the counters out and re-zeroes them for the next call (no per-call fill)
-__global__ void k_pm_publish_u32(uint32_t* src, int n, uint32_t* dst) {
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    dst[i] = src[i];
-    src[i] = 0u;
-  }
-}
-
 // block_associations_for_fuse (primitive_association.py:561-588) + the world transform, rows in
 // (block, measurement, candidate) order; fm = w r [valid and tile active] (fused mass terms)
 __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_rows(PmMeas m, PmWorld W, int nl, int block, int nrows,
@@ -2095,6 +2106,7 @@ struct gcs_pmap {
   uint8_t* bmark = nullptr;   // step 12b: slots seen per association block (grown)
   size_t bmark_bytes = 0;
   uint32_t* bcnt = nullptr;   // step 12b: unique slots per block (kMaxFuseBlocks)
+  uint32_t* bticket = nullptr;  // step 12b: k_pm_count_marks_blocks' arrival ticket
   // step-12b scratch (grown on demand)
   void* ub = nullptr;
   size_t ub_bytes = 0;
@@ -2330,7 +2342,8 @@ int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t 
       bad(hipMalloc(&p->d_tiles, max_tiles * 4)) || bad(hipMalloc(&p->d_tids, max_tiles * 8)) ||
       bad(hipMalloc(&p->mark, (size_t)m_tile * 4)) || bad(hipMalloc(&p->dcnt, 4)) ||
       bad(hipMalloc(&p->bcnt, kMaxFuseBlocks * 4)) ||
-      bad(hipMemset(p->bcnt, 0, kMaxFuseBlocks * 4)) ||  // once: k_pm_publish_u32 re-zeroes
+      bad(hipMemset(p->bcnt, 0, kMaxFuseBlocks * 4)) ||  // once: the last counting block re-zeroes
+      bad(hipMalloc(&p->bticket, 4)) || bad(hipMemset(p->bticket, 0, 4)) ||
       bad(hipMalloc(&p->tickets, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
       bad(hipMemset(p->tickets, 0, (size_t)max_tiles * kTopMaxLevels * kTopNodes * 4)) ||
       bad(hipMalloc(&p->topk_skip, (size_t)max_tiles * 4)) || bad(hipMalloc(&p->below, (size_t)max_tiles * 4)) ||
@@ -2371,7 +2384,7 @@ int gcs_pmap_destroy(gcs_pmap* p) {
   for (void* f : p->fields)
     if (f) (void)hipFree(f);
   void* bufs[] = {p->keys, p->keys_s, p->vals, p->vals_s, p->seg, p->d_tiles, p->d_tids, p->temp, p->fk, p->fk_s,
-                  p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->bmark, p->bcnt, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
+                  p->fv, p->fv_s, p->ftemp, p->mark, p->dcnt, p->bmark, p->bcnt, p->bticket, p->mmu, p->msig, p->mdet, p->mdist, p->mpd, p->mpp, p->mused,
                   p->msel, p->mnsel, p->ub, p->run_key, p->run_slot, p->tickets, p->fterm, p->flen, p->topk_skip, p->other_bm, p->below};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
@@ -2695,8 +2708,7 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
   hipLaunchKernelGGL(k_pm_fuse_rgb, dim3((unsigned)((tm + kPmThreads - 1) / kPmThreads)), dim3(kPmThreads), 0,
                      p->stream, p->st, (const int32_t*)p->d_tiles, n, eps_mass);
   hipLaunchKernelGGL(k_pm_count_marks_blocks, dim3(std::min(32, (p->M + kPmThreads - 1) / kPmThreads), nb),
-                     dim3(kPmThreads), 0, p->stream, p->bmark, p->M, p->bcnt);
-  hipLaunchKernelGGL(k_pm_publish_u32, dim3(1), dim3(256), 0, p->stream, p->bcnt, nb,
+                     dim3(kPmThreads), 0, p->stream, p->bmark, p->M, p->bcnt, p->bticket, nb,
                      (uint32_t*)(p->d_small + 9216));
   PMCHK(p, hipGetLastError());
   if (!nf) return GCS_OK;
