@@ -156,17 +156,19 @@ __global__ __launch_bounds__(kSfThreads) void k_sf_bounds(const uint32_t* __rest
   if (q == n - 1 || keys_s[q + 1] != k) run[2 * k + 1] = q + 1;
 }
 
-// per cell: the first max_occ point indices of its run (stable: index order), the clipped count
+// per (cell, occupant slot): the first max_occ point indices of the cell's run (stable: index
+// order) and the clipped count -- one thread per bucket entry, so an occupied cell's entries cost one
+// dependent round trip (run bounds, then the index), not one per occupant
 __global__ __launch_bounds__(kSfThreads) void k_sf_cells(const int32_t* __restrict__ run,
                                                           const uint32_t* __restrict__ vals_s, SfParams a,
                                                           int32_t* __restrict__ bucket, int32_t* __restrict__ count) {
-  const int k = blockIdx.x * kSfThreads + threadIdx.x;
-  if (k >= a.n_cells) return;
+  const long j = (long)blockIdx.x * kSfThreads + threadIdx.x;
+  if (j >= (long)a.n_cells * a.max_occ) return;
+  const int k = (int)(j / a.max_occ), r = (int)(j - (long)k * a.max_occ);
   const int s = run[2 * k], e = run[2 * k + 1];
   const int c = min(e - s, a.max_occ);
-  count[k] = c;
-  int32_t* row = bucket + (size_t)k * a.max_occ;
-  for (int r = 0; r < a.max_occ; ++r) row[r] = r < c ? (int32_t)vals_s[s + r] : -1;
+  if (r == 0) count[k] = c;
+  bucket[j] = r < c ? (int32_t)vals_s[s + r] : -1;
 }
 
 __device__ __forceinline__ void normalize3(double* v) {
@@ -345,8 +347,16 @@ __global__ __launch_bounds__(kSelThreads) void k_sf_slots(const uint8_t* __restr
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const int per = (a.n_cells + kSelThreads - 1) / kSelThreads;
   const int k0 = min(a.n_cells, t * per), k1 = min(a.n_cells, k0 + per);
+  // the thread's first kSelBatch flags loaded together (one round trip for grids up to
+  // kSelBatch x kSelThreads cells), the rest one by one
+  constexpr int kSelBatch = 16;
+  uint8_t vb[kSelBatch];
+#pragma unroll
+  for (int u = 0; u < kSelBatch; ++u) vb[u] = k0 + u < k1 ? valid[k0 + u] : (uint8_t)0;
   int mine = 0;
-  for (int k = k0; k < k1; ++k) mine += valid[k];
+#pragma unroll
+  for (int u = 0; u < kSelBatch; ++u) mine += vb[u];
+  for (int k = k0 + kSelBatch; k < k1; ++k) mine += valid[k];
   int x = mine;
   for (int off = 1; off < 64; off <<= 1) {
     const int y = __shfl_up(x, off, 64);
@@ -356,7 +366,10 @@ __global__ __launch_bounds__(kSelThreads) void k_sf_slots(const uint8_t* __restr
   __syncthreads();
   int run = x - mine;
   for (int q = 0; q < wid; ++q) run += s_wsum[q];
-  for (int k = k0; k < k1 && run < a.n_surfel; ++k)
+#pragma unroll
+  for (int u = 0; u < kSelBatch; ++u)
+    if (vb[u] && run < a.n_surfel) slot_cell[run++] = k0 + u;
+  for (int k = k0 + kSelBatch; k < k1 && run < a.n_surfel; ++k)
     if (valid[k]) slot_cell[run++] = k;
   if (t == kSelThreads - 1) {
     int tot = 0;
@@ -449,7 +462,15 @@ __global__ __launch_bounds__(kSortThreads) void k_sf_sort_lds(const uint32_t* __
   __shared__ uint32_t s_off[kSortWaves][kSortDigits];
   __shared__ uint32_t s_tot[kSortDigits], s_dsum[kSortDigits / 64];
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
-  for (int i = t; i < n; i += kSortThreads) s_buf[0][i] = (keys[i] << kSortIdxBits) | (uint32_t)i;
+  {  // every key load issued before the first LDS store (one round trip, not one per key)
+    constexpr int KPT = kSortMax / kSortThreads;
+    uint32_t kv[KPT];
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) kv[u] = t + u * kSortThreads < n ? keys[t + u * kSortThreads] : 0u;
+#pragma unroll
+    for (int u = 0; u < KPT; ++u)
+      if (t + u * kSortThreads < n) s_buf[0][t + u * kSortThreads] = (kv[u] << kSortIdxBits) | (uint32_t)(t + u * kSortThreads);
+  }
   const unsigned long long lt = (1ull << lane) - 1ull;
   const int npass = (end_bit + kSortDigitBits - 1) / kSortDigitBits;
   for (int pass = 0; pass < npass; ++pass) {
@@ -709,7 +730,9 @@ int surfel_launch(gcs_surfel_ctx* c, const double* points, const double* timesta
                        (const uint32_t*)c->d_keys_s, n, a.n_cells, c->d_run);
   }
   const int cblk = (a.n_cells + kSfThreads - 1) / kSfThreads;
-  hipLaunchKernelGGL(k_sf_cells, dim3(cblk), dim3(kSfThreads), 0, s, (const int32_t*)c->d_run,
+  const long n_entries = (long)a.n_cells * a.max_occ;
+  hipLaunchKernelGGL(k_sf_cells, dim3((unsigned)((n_entries + kSfThreads - 1) / kSfThreads)), dim3(kSfThreads), 0, s,
+                     (const int32_t*)c->d_run,
                      (const uint32_t*)c->d_vals_s, a, c->d_bucket, c->d_count);
   hipLaunchKernelGGL(k_sf_moments, dim3((a.n_cells + kCellsPerBlock - 1) / kCellsPerBlock), dim3(kSfThreads), 0, s,
                      points, timestamps, weights, (const double*)c->d_scal, (const int32_t*)c->d_bucket,
