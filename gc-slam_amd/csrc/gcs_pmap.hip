@@ -845,21 +845,27 @@ __global__ __launch_bounds__(kPmRed) void k_pm_topk_sparse(const uint64_t* __res
     return;
   }
   if (tid == 0) skip[t] = 1u;
-  // gather the other entries' keys into LDS in slot order
+  // gather the other entries' keys into LDS in slot order: a word's marked keys are loaded together
+  // (predicated), then stored (one round trip per word; the map's primitives fill the first slots of
+  // a tile, so a few threads hold full words, and a load-store chain per bit cost them 32 each)
   const uint64_t* kt = keys + (size_t)t * M;
   {
     uint32_t r = ro;
 #pragma unroll
     for (int u = 0; u < WPT; ++u) {
-      uint32_t x = ow[u];
-      while (x) {
-        const int bit = __ffs((int)x) - 1;
-        x &= x - 1u;
-        const int q = 32 * (WPT * tid + u) + bit;
-        s_k[r] = kt[q];
-        s_s[r] = (uint32_t)q;
-        ++r;
-      }
+      const uint32_t x = ow[u];
+      if (x == 0u) continue;
+      const int qb = 32 * (WPT * tid + u);
+      uint64_t kv[32];
+#pragma unroll
+      for (int b = 0; b < 32; ++b) kv[b] = (x >> b) & 1u ? kt[qb + b] : 0ull;
+#pragma unroll
+      for (int b = 0; b < 32; ++b)
+        if ((x >> b) & 1u) {
+          s_k[r] = kv[b];
+          s_s[r] = (uint32_t)(qb + b);
+          ++r;
+        }
     }
   }
   // bitonic sort of the n entries by (key, slot) in LDS (padding above every real pair)
