@@ -479,17 +479,33 @@ __global__ __launch_bounds__(kSortThreads) void k_sf_sort_lds(const uint32_t* __
     const int shift = kSortIdxBits + pass * kSortDigitBits;
     for (int q = t; q < kSortWaves * kSortDigits; q += kSortThreads) (&s_off[0][0])[q] = 0u;
     __syncthreads();
-    // per (wave, digit) counts
-    for (int j = 0; j < kSortSeg; j += 64) {
-      const int e = wid * kSortSeg + j + lane;
+    // per (wave, digit) counts.  Each entry's word, digit and peer mask (the wave's lanes with the same
+    // digit) are kept in registers for the scatter.  The peer mask is the AND over the digit's bits of
+    // the bit's ballot or its complement, as ~(ballot ^ -bit): a few VALU ops per bit (the pass is
+    // VALU-bound: 16 waves on one CU).
+    constexpr int kIt = kSortSeg / 64;
+    uint32_t xv[kIt], dv[kIt];
+    uint64_t pv[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      const int e = wid * kSortSeg + it * 64 + lane;
+      xv[it] = dv[it] = 0u;
+      pv[it] = 0ull;
+      if (wid * kSortSeg + it * 64 >= n) continue;  // wave-uniform: no entry in this step
       const bool ok = e < n;
-      const uint32_t d = ok ? (src[e] >> shift) & (kSortDigits - 1) : 0u;
-      unsigned long long peers = __ballot(ok);
+      const uint32_t x = ok ? src[e] : 0u;
+      const uint32_t d = (x >> shift) & (kSortDigits - 1);
+      uint64_t peers = __builtin_amdgcn_ballot_w64(ok);
 #pragma unroll
       for (int b = 0; b < kSortDigitBits; ++b) {
-        const unsigned long long m = __ballot(ok && ((d >> b) & 1u));
-        peers &= ((d >> b) & 1u) ? m : ~m;
+        const uint32_t bit = (d >> b) & 1u;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(bit != 0u);
+        peers &= ~(m ^ (0ull - (uint64_t)bit));
       }
+      if (!ok) peers = 0ull;
+      xv[it] = x;
+      dv[it] = d;
+      pv[it] = peers;
       if (ok && (peers & lt) == 0ull) s_off[wid][d] += (uint32_t)__popcll(peers);  // the group's first lane
       __builtin_amdgcn_wave_barrier();
     }
@@ -518,20 +534,13 @@ __global__ __launch_bounds__(kSortThreads) void k_sf_sort_lds(const uint32_t* __
     }
     __syncthreads();
     // scatter: each wave's entries in order, equal digits by lane order
-    for (int j = 0; j < kSortSeg; j += 64) {
-      const int e = wid * kSortSeg + j + lane;
-      const bool ok = e < n;
-      const uint32_t x = ok ? src[e] : 0u;
-      const uint32_t d = (x >> shift) & (kSortDigits - 1);
-      unsigned long long peers = __ballot(ok);
 #pragma unroll
-      for (int b = 0; b < kSortDigitBits; ++b) {
-        const unsigned long long m = __ballot(ok && ((d >> b) & 1u));
-        peers &= ((d >> b) & 1u) ? m : ~m;
-      }
-      if (ok) dst[s_off[wid][d] + (uint32_t)__popcll(peers & lt)] = x;
+    for (int it = 0; it < kIt; ++it) {
+      const uint64_t peers = pv[it];
+      const uint32_t d = dv[it];
+      if (peers) dst[s_off[wid][d] + (uint32_t)__popcll(peers & lt)] = xv[it];
       __builtin_amdgcn_wave_barrier();
-      if (ok && (peers & lt) == 0ull) s_off[wid][d] += (uint32_t)__popcll(peers);
+      if (peers && (peers & lt) == 0ull) s_off[wid][d] += (uint32_t)__popcll(peers);
       __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
