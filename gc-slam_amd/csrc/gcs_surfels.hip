@@ -195,18 +195,33 @@ __device__ __forceinline__ void sf_wave_sum(double (&v)[NV]) {
 // xor trees.  Moment row = sum w, centroid (3), sum t, sum w d d^T (xx xy xz yy yz zz).
 constexpr int kMomFields = 11;
 constexpr int kCellsPerBlock = kSfThreads / 64;
+// run / vals_s (may be null: the bucket rows of k_sf_cells are read instead): the wave also writes its
+// cell's bucket row and clipped count from the sorted run (k_sf_cells folded in: one launch fewer,
+// the same rows) and reads the occupants from the run
 __global__ __launch_bounds__(kSfThreads) void k_sf_moments(const double* __restrict__ p, const double* __restrict__ t,
                                                             const double* __restrict__ w,
                                                             const double* __restrict__ center,
-                                                            const int32_t* __restrict__ bucket,
-                                                            const int32_t* __restrict__ count, SfParams a,
-                                                            double* __restrict__ mom) {
+                                                            int32_t* __restrict__ bucket,
+                                                            int32_t* __restrict__ count, SfParams a,
+                                                            double* __restrict__ mom, const int32_t* __restrict__ run,
+                                                            const uint32_t* __restrict__ vals_s) {
   const int lane = threadIdx.x & 63;
   const int k = blockIdx.x * kCellsPerBlock + (threadIdx.x >> 6);
   if (k >= a.n_cells) return;  // wave-uniform
-  const int c = count[k];
+  int c;
+  const int32_t* row;
+  if (run) {
+    const int s0 = run[2 * k], e0 = run[2 * k + 1];
+    c = min(e0 - s0, a.max_occ);
+    int32_t* brow = bucket + (size_t)k * a.max_occ;
+    for (int r = lane; r < a.max_occ; r += 64) brow[r] = r < c ? (int32_t)vals_s[s0 + r] : -1;
+    if (lane == 0) count[k] = c;
+    row = reinterpret_cast<const int32_t*>(vals_s + s0);
+  } else {
+    c = count[k];
+    row = bucket + (size_t)k * a.max_occ;
+  }
   if (c == 0) return;          // k_sf_fit does not read the row of an empty cell
-  const int32_t* row = bucket + (size_t)k * a.max_occ;
   const double cx = center[0], cy = center[1], cz = center[2];
   double s5[5] = {0.0, 0.0, 0.0, 0.0, 0.0};  // w, w x, w y, w z, t
   double px[2] = {0.0, 0.0}, py[2] = {0.0, 0.0}, pz[2] = {0.0, 0.0}, pw[2] = {0.0, 0.0};
@@ -574,6 +589,7 @@ struct gcs_surfel_ctx {
   size_t temp_bytes = 0;
   unsigned end_bit = 1;
   bool lds_sort = true;  // k_sf_keys_sort for clouds of <= kSortMax points (GCSLAM_SF_LDS_SORT=0: rocPRIM)
+  bool fold_cells = true;  // k_sf_moments writes the bucket rows (GCSLAM_SF_FOLD_CELLS=0: k_sf_cells)
   int32_t *d_bucket = nullptr, *d_count = nullptr, *d_run = nullptr, *d_slot_cell = nullptr;
   double *d_mom = nullptr, *d_fit = nullptr;
   uint8_t* d_valid = nullptr;
@@ -664,6 +680,7 @@ int gcs_surfel_ctx_create(const gcs_surfel_config* cfg, gcs_surfel_ctx** out) {
   a.eps_lift = cfg->eps_lift;
   while ((1UL << c->end_bit) <= (unsigned long)n_cells) ++c->end_bit;  // keys 0..n_cells
   if (const char* e = getenv("GCSLAM_SF_LDS_SORT")) c->lds_sort = atoi(e) != 0;
+  if (const char* e = getenv("GCSLAM_SF_FOLD_CELLS")) c->fold_cells = atoi(e) != 0;
   auto bad = [&](hipError_t e) { return e != hipSuccess; };
   const size_t N = (size_t)cfg->max_points;
   if (bad(hipSetDevice(cfg->device)) || bad(hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking)) ||
@@ -739,13 +756,18 @@ int surfel_launch(gcs_surfel_ctx* c, const double* points, const double* timesta
                        (const uint32_t*)c->d_keys_s, n, a.n_cells, c->d_run);
   }
   const int cblk = (a.n_cells + kSfThreads - 1) / kSfThreads;
-  const long n_entries = (long)a.n_cells * a.max_occ;
-  hipLaunchKernelGGL(k_sf_cells, dim3((unsigned)((n_entries + kSfThreads - 1) / kSfThreads)), dim3(kSfThreads), 0, s,
-                     (const int32_t*)c->d_run,
-                     (const uint32_t*)c->d_vals_s, a, c->d_bucket, c->d_count);
-  hipLaunchKernelGGL(k_sf_moments, dim3((a.n_cells + kCellsPerBlock - 1) / kCellsPerBlock), dim3(kSfThreads), 0, s,
-                     points, timestamps, weights, (const double*)c->d_scal, (const int32_t*)c->d_bucket,
-                     (const int32_t*)c->d_count, a, c->d_mom);
+  if (c->fold_cells) {  // the bucket rows and counts written by k_sf_moments' waves
+    hipLaunchKernelGGL(k_sf_moments, dim3((a.n_cells + kCellsPerBlock - 1) / kCellsPerBlock), dim3(kSfThreads), 0, s,
+                       points, timestamps, weights, (const double*)c->d_scal, c->d_bucket, c->d_count, a, c->d_mom,
+                       (const int32_t*)c->d_run, (const uint32_t*)c->d_vals_s);
+  } else {
+    const long n_entries = (long)a.n_cells * a.max_occ;
+    hipLaunchKernelGGL(k_sf_cells, dim3((unsigned)((n_entries + kSfThreads - 1) / kSfThreads)), dim3(kSfThreads), 0, s,
+                       (const int32_t*)c->d_run, (const uint32_t*)c->d_vals_s, a, c->d_bucket, c->d_count);
+    hipLaunchKernelGGL(k_sf_moments, dim3((a.n_cells + kCellsPerBlock - 1) / kCellsPerBlock), dim3(kSfThreads), 0, s,
+                       points, timestamps, weights, (const double*)c->d_scal, c->d_bucket, c->d_count, a, c->d_mom,
+                       (const int32_t*)nullptr, (const uint32_t*)nullptr);
+  }
   hipLaunchKernelGGL(k_sf_fit, dim3(cblk), dim3(kSfThreads), 0, s, (const double*)c->d_mom, (const double*)c->d_scal,
                      (const int32_t*)c->d_count, a, c->d_fit, c->d_valid);
   hipLaunchKernelGGL(k_sf_slots, dim3(1), dim3(kSelThreads), 0, s, (const uint8_t*)c->d_valid, a, c->d_slot_cell,

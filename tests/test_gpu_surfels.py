@@ -165,3 +165,27 @@ def test_lds_key_sort_equals_radix_sort(monkeypatch, n_points, scan, cells):
     assert a["n_valid"] == b["n_valid"] and a["n_valid"] > 0
     for k in a:
         assert a[k].tobytes() == b[k].tobytes(), k
+
+
+@pytest.mark.parametrize("n_points,scan,cells", [(8192, 3, (32, 32, 8)), (300, 1, (64, 64, 16))])
+def test_folded_bucket_fill_equals_cells_kernel(monkeypatch, n_points, scan, cells):
+    """The bucket rows and counts written by k_sf_moments' waves (default) against the separate k_sf_cells
+    launch (GCSLAM_SF_FOLD_CELLS=0): every output and intermediate bitwise equal."""
+    sc = synthetic.make_scan(8192, scan)
+    pts = np.ascontiguousarray(sc["points"][:n_points], np.float64).copy()
+    pts[::89] = 1e6
+    t, w = sc["timestamps"][:n_points], sc["weights"][:n_points]
+    cfg = SurfelExtractionConfig(hex3d_num_cells_1=cells[0], hex3d_num_cells_2=cells[1], hex3d_num_cells_z=cells[2])
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("GCSLAM_SF_FOLD_CELLS", flag)
+        ex = SurfelExtractor(cfg, max_points=8192)
+        try:
+            r = ex.extract(pts, t, w, want_intermediates=True)
+            outs.append({k: (v.cpu().numpy().copy() if torch.is_tensor(v) else np.asarray(v)) for k, v in r.items()})
+        finally:
+            ex.close()
+    a, b = outs
+    assert a["n_valid"] == b["n_valid"] and a["n_valid"] > 0
+    for k in a:
+        assert a[k].tobytes() == b[k].tobytes(), k
