@@ -347,11 +347,71 @@ def live_path_bench(device, steps=30, warmup=10):
     for k in range(warmup):
         one(scans[k])
     torch.cuda.synchronize()
+    # The start-up heap (torch, numpy, the earlier passes) into the collector's permanent generation: a
+    # full collection in the timed calls then scans only this loop's objects.  The serving loop of the
+    # drop-in does the same after start-up.  Every collection that still runs during a
+    # timed call is clocked (gc.callbacks) and charged to that call.
+    import gc
+    import resource
+    from gcslam import pipeline as GP
+    gc.collect()
+    gc.freeze()
+    gc_ev = []
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_ev.append([time.perf_counter(), None, info.get("generation", -1)])
+        elif gc_ev and gc_ev[-1][1] is None:
+            gc_ev[-1][1] = time.perf_counter()
+    gc.callbacks.append(_gc_cb)
+    stamps_prev = GP._STAMPS_ON
+    GP._STAMPS_ON = True  # the drop-in's phase stamps (GCSLAM_LIVE_STAMPS): a list append per phase
+    ru0 = resource.getrusage(resource.RUSAGE_THREAD)
     per = np.zeros(steps)
+    cpu = np.zeros(steps)
+    bounds = []
+    phases = []
     for i in range(steps):
+        GP.LIVE_STAMPS.clear()
+        c0 = time.thread_time()
         t0 = time.perf_counter()
         r = one(scans[warmup + i])
-        per[i] = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        per[i] = t1 - t0
+        cpu[i] = time.thread_time() - c0
+        bounds.append((t0, t1))
+        st = [(n, t) for n, t in GP.LIVE_STAMPS]
+        phases.append({st[k][0]: (st[k][1] - (st[k - 1][1] if k else t0)) * 1e3 for k in range(len(st))})
+    ru1 = resource.getrusage(resource.RUSAGE_THREAD)
+    GP._STAMPS_ON = stamps_prev
+    gc.callbacks.remove(_gc_cb)
+    gc_ms = np.zeros(steps)
+    for ta, tb, _ in gc_ev:
+        if tb is None:
+            continue
+        for i, (t0, t1) in enumerate(bounds):
+            if t0 <= ta < t1:
+                gc_ms[i] += (tb - ta) * 1e3
+    med = float(np.median(per))
+    slow = np.nonzero(per > 2.0 * med)[0]
+    names = list(phases[0].keys()) if phases else []
+    pct = lambda a, q: float(np.percentile(a, q))  # noqa: E731
+    attribution = dict(
+        phase_ms={n: dict(p50=pct([p.get(n, 0.0) for p in phases], 50), p90=pct([p.get(n, 0.0) for p in phases], 90),
+                          max=float(max(p.get(n, 0.0) for p in phases))) for n in names},
+        phase_note="drop-in phase clocks per call: h2d (host arrays staged), args (the C call's arguments), "
+                   "live_scan (the one C call: begin, surfels .. pose evidence, finish, step 12b queued), "
+                   "live_results (result objects, step 12b running), result, collect (step 12b's wait)",
+        calls_over_2x_median=int(len(slow)), slow_calls=[dict(call=int(i), ms=float(per[i] * 1e3),
+                                                            gc_ms=float(gc_ms[i]),
+                                                            offcpu_ms=float((per[i] - cpu[i]) * 1e3),
+                                                            phases=phases[i]) for i in slow[:5]],
+        gc=dict(collections=len(gc_ev), ms_total=float(gc_ms.sum()), ms_max=float(gc_ms.max()) if steps else 0.0,
+                frozen_objects=gc.get_freeze_count()),
+        offcpu_ms=dict(p50=pct((per - cpu) * 1e3, 50), p90=pct((per - cpu) * 1e3, 90),
+                       max=float(((per - cpu) * 1e3).max())),
+        offcpu_note="wall - this thread's CPU time per call: waiting that is not a spin (sleeps, descheduling)",
+        ctx_switches=dict(voluntary=int(ru1.ru_nvcsw - ru0.ru_nvcsw), involuntary=int(ru1.ru_nivcsw - ru0.ru_nivcsw)))
     chain_on = r.stage_ms == {} and os.environ.get("GCSLAM_LIVE_CHAIN", "1") != "0"
     prev = os.environ.get("GCSLAM_LIVE_CHAIN")
     os.environ["GCSLAM_LIVE_CHAIN"] = "0"
@@ -374,10 +434,12 @@ def live_path_bench(device, steps=30, warmup=10):
     cfg.enable_timing = False
     mu = r.map_update_cert
     out = dict(ms_per_call=float(per.mean() * 1e3), ms_median=float(np.median(per) * 1e3),
-               ms_p90=float(np.percentile(per, 90) * 1e3), calls=int(steps),
+               ms_p90=float(np.percentile(per, 90) * 1e3), ms_max=float(per.max() * 1e3), calls=int(steps),
+               attribution=attribution,
                path="gcs_live_scan (one C call per scan)" if chain_on else "per-operator C calls",
                per_operator_ms_per_call=float(per_op.mean() * 1e3),
                per_operator_ms_median=float(np.median(per_op) * 1e3),
+               per_operator_ms_max=float(per_op.max() * 1e3),
                stage_ms={k: float(np.mean([s[k] for s in split])) for k in split[0]},
                stage_note="diagnostic pass: a device sync before each stage clock (the reference's enable_timing)",
                sizes=dict(n_points_cap=N, m_tile=cfg.primitive_map_max_size, n_active_tiles=cfg.N_ACTIVE_TILES,
@@ -385,6 +447,7 @@ def live_path_bench(device, steps=30, warmup=10):
                           n_feat=cfg.n_feat, k_assoc=cfg.k_assoc, k_sinkhorn=cfg.k_sinkhorn),
                map_primitives=int(am.total_count), last_scan_inserted=int(mu.insert_count_total),
                last_scan_fused=int(mu.fused_count), n_valid_measurements=int(r.measurement_batch.n_valid))
+    gc.unfreeze()  # (frozen for the per-operator pass too)
     am.close()
     ctx.close()
     return out
@@ -411,10 +474,8 @@ def primitive_path_main(args, rank, world, local_rank, pin):
     dev = 0 if args.share_device else local_rank
     torch.cuda.set_device(dev)
     if world > 1:
-        if args.share_device:
-            dist.init_process_group("gloo", rank=rank, world_size=world)
-        else:
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+        # gloo in both cases: the RCCL communicator is the library's (HypothesisComm), not torch's
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = HypothesisComm(rank, world, dev) if (world > 1 and not args.share_device) else None
     N = 8192
     cfg = PipelineConfig(K_HYP=world, N_POINTS_CAP=N, B_BINS=48, soft_assign_mode="dense",
@@ -484,7 +545,7 @@ def primitive_path_main(args, rank, world, local_rank, pin):
     el_rank = time.perf_counter() - t0
     el = el_rank
     if world > 1:  # the slowest rank's clock
-        tt = torch.tensor([el], dtype=torch.float64, device="cpu" if args.share_device else f"cuda:{dev}")
+        tt = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
     if shared and not lead and st["pending"] is not None:  # catch up with the lead's last update
@@ -709,8 +770,11 @@ def main():
     import torch.distributed as dist
 
     if world > 1:
+        # torch.distributed over gloo (host): it broadcasts the RCCL id and carries the bench's barriers and
+        # per-rank clocks; the one RCCL communicator is the library's (HypothesisComm), which runs the
+        # per-scan all-reduce -- no second (torch NCCL) communicator on the GPUs
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     device = f"cuda:{local_rank}"
     torch.cuda.set_device(local_rank)
 
@@ -726,7 +790,7 @@ def main():
         n_comm, r_comm = comm.count()
         allc = [(n_comm, r_comm)]
         if world > 1:
-            cnt = torch.tensor([n_comm, r_comm], dtype=torch.int64, device=device)
+            cnt = torch.tensor([n_comm, r_comm], dtype=torch.int64)
             allc = [torch.zeros_like(cnt) for _ in range(world)]
             dist.all_gather(allc, cnt)
             allc = [(int(c[0]), int(c[1])) for c in allc]
@@ -768,16 +832,9 @@ def main():
     fused = ctx.scan_combine_call(scan_out, comm_h, w_iw, w_bary) if fused_on else None
     state = dict(count=0, sample=False, sampled=0, stamp=True, combine=combine, fused=fused, warm_stamp=True,
                  timing_on=False)
-    # pre-device host, device submit+wait, host tail, whole gcs_scan, combine, then the sub-spans
-    # (budget launch + predict, device launch calls, tail numerics, pushforward launch calls)
-    host_ms = np.zeros(9)
-
     comb_ms = []  # every timed step's combine (pack, all-reduce, IW / Q apply), for SCALE's attribution
 
     TIMING_STRIDE = timing_stride(args.steps)
-    # the host sub-spans are read (eight ctypes reads) on every fourth scan at most: at stride 1 they
-    # were read on every scan of the driver's 20-step region
-    HOST_STRIDE = max(TIMING_STRIDE, 4)
 
     def step():
         combine = state["combine"]
@@ -801,13 +858,6 @@ def main():
         out = scan_out
         if state["sample"]:
             comb_ms.append(dc)
-        if state["count"] % HOST_STRIDE == HOST_STRIDE // 2:  # host sub-spans (every HOST_STRIDE-th scan)
-            host_ms[4] += dc
-            sm = out.stage_ms
-            for k in range(4):
-                host_ms[k] += sm[k]
-                host_ms[5 + k] += sm[4 + k]
-            state["sampled"] += 1
         if follow is not None:
             follow(prepared[state["count"] % N_SCANS])
         state["count"] += 1
@@ -823,6 +873,12 @@ def main():
             try:
                 os.sched_setaffinity(threading.get_native_id(), {share[-1]})
                 pin = dict(pin, main_thread_cpu=share[-1])
+                # the launch worker (it spins 2 ms after each job, so at a scan per 0.1 ms it never sleeps)
+                # keeps the rest of the share, never the main thread's core
+                wt = ctx.worker_tid()
+                if wt:
+                    os.sched_setaffinity(wt, set(share[:-1]))
+                    pin = dict(pin, worker_cpus=f"{share[0]}-{share[-2]} ({len(share) - 1})")
             except OSError:
                 pass
     state["warm_stamp"] = False
@@ -831,8 +887,7 @@ def main():
     ctx.enable_timing(False)
     state["timing_on"] = False
     ctx.stage_times(reset=True)
-    host_ms[:] = 0.0
-    state["sampled"] = 0
+    ctx.host_split(reset=True)  # the library sums every timed scan's host split (gcs_ctx_host_split)
     per_step = np.zeros(args.steps)
     if world > 1:
         dist.barrier()
@@ -850,40 +905,51 @@ def main():
     elapsed_rank = elapsed
     per_rank_s = [elapsed]
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        tt = torch.tensor([elapsed], dtype=torch.float64)
         allt = [torch.zeros_like(tt) for _ in range(world)]
         dist.all_gather(allt, tt)
         per_rank_s = [float(x.item()) for x in allt]
         elapsed = max(per_rank_s)  # the slowest rank's clock
     state["sample"] = False
+    hsum, (n_scans_h, n_calls_h) = ctx.host_split(reset=True)
     ms_sum, counts = ctx.stage_times(reset=True)
     bins_in_region = int(counts[2])
     ctx.enable_timing(False)
 
-    def side_loop():  # the same steps again, a variant of the step (not `value`): its ms per step
+    def side_loop(name):  # the same steps again, a variant of the step (not `value`)
+        # its own warm-up after the switch (round 5's single 20-step mean met one stall: 0.241 vs 0.10 ms),
+        # then the mean and the median of the per-step times
+        for _ in range(max(5, args.warmup)):
+            step()
+        ctx.synchronize()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        per = np.zeros(args.steps)
         ta = time.perf_counter()
-        for _ in range(args.steps):
+        for i in range(args.steps):
+            ts = time.perf_counter()
             step()
+            per[i] = time.perf_counter() - ts
         ctx.synchronize()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        return (time.perf_counter() - ta) / args.steps * 1e3
+        variants[name + "_ms_per_step"] = (time.perf_counter() - ta) / args.steps * 1e3
+        variants[name + "_median_ms"] = float(np.median(per) * 1e3)
     # the decomposition of ms_per_step: without the roofline stamps, and (N = 1) with the host-only
     # combine instead of the world-1 RCCL all-reduce -- what round 4's line measured
     state["stamp"] = False
-    variants = {"unstamped_ms_per_step": side_loop()}
+    variants = {}
+    side_loop("unstamped")
     if fused is not None:  # the same step as two C calls (gcs_scan, then gcs_combine_allreduce)
         state["fused"] = None
-        variants["two_call_unstamped_ms_per_step"] = side_loop()
+        side_loop("two_call_unstamped")
     if world == 1 and comm is not None:
         state["combine"] = ctx.combine_call(None, w_iw, w_bary)
         if fused is not None:
             state["fused"] = ctx.scan_combine_call(scan_out, None, w_iw, w_bary)
-        variants["host_combine_unstamped_ms_per_step"] = side_loop()
+        side_loop("host_combine_unstamped")
         state["combine"] = combine
     state["fused"] = fused
     state["stamp"] = True
@@ -901,8 +967,17 @@ def main():
         ms_sum, counts = ms_sum + ms2, counts + c2
     bins_ms = float(ms_sum[2] / counts[2]) if counts[2] else None
     bins_samples = int(counts[2])
-    host_avg = dict(zip(["pre_device", "device_wait", "tail", "gcs_scan", "combine", "pre_predict", "launch_calls",
-                         "tail_numerics", "push_launch"], (host_ms / max(state["sampled"], 1)).tolist()))
+    # every timed step's host split, summed by the library (not a sample): its parts add up to the
+    # C call, and python_other is the rest of ms_per_step (the Python loop around the call)
+    host_avg = {k: v / max(n_scans_h, 1) for k, v in hsum.items() if k not in ("combine", "scan_combine_call")}
+    host_avg["combine"] = (hsum["combine"] / n_calls_h) if n_calls_h else float(np.mean(comb_ms)) if comb_ms else 0.0
+    if n_calls_h:
+        host_avg["scan_combine_call"] = hsum["scan_combine_call"] / n_calls_h
+    call_ms = host_avg.get("scan_combine_call", host_avg["gcs_scan"] + host_avg["combine"])
+    host_avg["python_other"] = elapsed_rank / args.steps * 1e3 - call_ms
+    host_avg["scans_counted"] = n_scans_h
+    host_avg["note"] = ("every timed step (gcs_ctx_host_split sums in the library): pre_device + device_wait + tail "
+                        "= gcs_scan; gcs_scan + combine = the C call; + python_other = ms_per_step of this rank")
     cm = np.array(comb_ms) if comb_ms else np.zeros(1)
     me = dict(rank=rank, affinity=pin, host_ms=host_avg, ms_per_step=elapsed_rank / args.steps * 1e3,
               combine_ms=dict(median=float(np.median(cm)), p90=float(np.percentile(cm, 90)), mean=float(cm.mean()),

@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <chrono>
 #include <condition_variable>
 #include <mutex>
@@ -240,7 +242,11 @@ struct gcs_ctx {
   // hypothesis all-reduce payload (gcs_combine_allreduce): pinned host staging + device buffer
   double* h_payload = nullptr;   // pinned, coherent, mapped: the packed payload (dh_payload: device view)
   double* dh_payload = nullptr;
-  double* d_payload = nullptr;   // device: RCCL's in-place buffer
+  double* d_payload = nullptr;   // device: RCCL's receive buffer
+  double* d_payload_in = nullptr;  // device: the send buffer when the communicator spans > 1 rank
+  int sendbuf_mode = -1;         // GCS_DEBUG_SENDBUF: -1 by world size, 0 host, 1 device
+  void* comm_seen = nullptr;     // the communicator whose rank count comm_world holds
+  int comm_world = 1;
   double* h_psum = nullptr;      // pinned, coherent, mapped: the sum + sequence + checksum (k_payload_out)
   double* dh_psum = nullptr;
   hipStream_t comm_stream = nullptr;  // the all-reduce's own stream (never queued behind the scan's kernels)
@@ -268,7 +274,21 @@ struct gcs_ctx {
   bool have_last = false;
   int last_n_sel = 0, last_stride = 1;
   int budget_blocks = 0;
+  // gcs_ctx_host_split: every scan's stage_ms and combine, summed
+  double host_sums[10] = {};
+  int64_t host_n[2] = {0, 0};
+  std::atomic<int64_t> worker_tid{0};
   bool budget_pending = false;  // k_budget already queued for the coming point stage (gcs_scan)
+  // self-budget scans (round 6; GCSLAM_SELF_BUDGET=0 for A/B): no k_budget -- k_points writes per-block
+  // mass rows (d_mass_rows) and unscaled records, the bin kernel folds the rows and applies mass_scale
+  // (PointKernelArgs.mass_rows).  budget_self: the pending point stage runs so; recs_deferred: the
+  // records the next bin kernel stages carry no mass_scale yet.
+  bool self_budget = [] {
+    const char* e = getenv("GCSLAM_SELF_BUDGET");
+    return !(e && atoi(e) == 0);
+  }();
+  bool budget_self = false, recs_deferred = false;
+  double2* d_mass_rows = nullptr;
   std::vector<double> wimu, wint;  // IMU window weights: within-scan, scan-to-scan (scratch)
   host::ImuOdomOut io;             // step 9 IMU/odometry evidence of the current scan (scratch)
   double grav[3] = {0.0, 0.0, 0.0};  // gravity_W * imu_gravity_scale
@@ -482,7 +502,9 @@ int submit_budget(gcs_ctx* c, const BudgetArgs& ba, int nblk, hipStream_t s);
 // Row 1's mass sums (k_budget) need only the weights: gcs_scan queues them before its host
 // prologue so they run while the host predicts and preintegrates.  Timed (stage ST_BUDGET), the launch
 // is made here with the kernel's own start / end events; otherwise by the worker thread.
-int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true) {
+// self: a self-budget scan (gcs_ctx::self_budget): only the per-scan clears are launched, when the last
+// scan's k_pt did not do them (k_budget with no weights to sum); usually nothing is.
+int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true, bool self = false) {
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
   int stride = std::max(1, (int)((n_raw + (long)c->cap - 1) / c->cap));  // ceil(N/cap), point_budget.py:160
   int n_sel = (n_raw + stride - 1) / stride;
@@ -513,6 +535,11 @@ int stage_budget(gcs_ctx* c, const double* w, int n_raw, bool toggle = true) {
   // and on a busy GPU -- the previous scan's pushforward -- each block waits for a CU slot)
   c->budget_blocks = std::min(red_blocks(std::max(n_raw, 1)), c->budget_max);
   c->budget_pending = true;
+  c->budget_self = self;
+  if (self) {
+    if (ba.n_zero32 == 0 && ba.n_zero8 == 0) return GCS_OK;  // nothing to clear: no launch
+    ba.n_raw = 0;  // the clears only (its zero partial rows are read by nobody)
+  }
   StageEv ev = stage_ev(c, ST_BUDGET);
   if (!ev.e0 && c->push_async && !t_on_worker) return submit_budget(c, ba, c->budget_blocks, s);
   if (int rc = push_wait(c)) return rc;  // the worker's queued launches precede this one on the stream
@@ -529,8 +556,13 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
   if (n_raw < 0 || n_raw > c->max_raw) return fail(c, GCS_ERR_ARG, "n_points exceeds max_raw_points");
   if (point_step < (xyz_f64 ? 24 : 12)) return fail(c, GCS_ERR_ARG, "point_step too small for x, y, z");
   StageEv ev = stage_ev(c, ST_POINTS);
+  // a self-budget scan: scale mode, the cert fold left to the bin kernel, no per-point outputs (they
+  // carry the budget weights) -- gcs_scan, its pre-launched front and gcs_map_follow
+  const bool self_ok = c->self_budget && c->cfg.mode == GCS_MODE_SCALE && !deskew_only && fold_later && !p0_out &&
+                       !w_out && !wb_out && !iz_out && !t_out;
   if (!c->budget_pending)  // k_budget not queued earlier by gcs_scan
-    if (int rc = stage_budget(c, w, n_raw)) return rc;
+    if (int rc = stage_budget(c, w, n_raw, true, self_ok)) return rc;
+  if (c->budget_self && !self_ok) return fail(c, GCS_ERR_STATE, "self-budget point stage with per-point outputs");
   if (int rc = push_wait(c)) return rc;  // k_budget's launch call (worker) precedes k_points on the stream
   c->budget_pending = false;
   const int n_sel = c->last_n_sel, stride = c->last_stride;
@@ -570,8 +602,10 @@ int stage_points(gcs_ctx* c, const void* xyz, int point_step, const double* t, c
     a.tile_shift = c->tile_shift;
     a.overflow = c->d_err + 2;
   }
-  a.budget_partials = c->d_partials;
-  a.budget_blocks = c->budget_blocks;
+  a.budget_partials = c->budget_self ? nullptr : c->d_partials;
+  a.budget_blocks = c->budget_self ? 0 : c->budget_blocks;
+  a.mass_rows = c->budget_self ? c->d_mass_rows : nullptr;
+  c->recs_deferred = c->budget_self && c->cfg.mode == GCS_MODE_SCALE && !deskew_only;
   a.scalars = c->d_scalars;
   a.p0_out = p0_out;
   a.w_out = w_out;
@@ -639,6 +673,10 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   if (c->pts_fold_pending) {
     b.pts_partials = c->d_part_pts;
     b.pts_blocks = c->pts_blocks;
+  }
+  if (c->recs_deferred) {  // the self-budget point stage's mass rows (one per k_points block)
+    b.mass_rows = c->d_mass_rows;
+    b.mass_nrows = c->pts_blocks;
   }
   if (c->d_counts) {
     b.zero_after = c->d_counts + c->B;
@@ -859,6 +897,7 @@ int scan_front(gcs_ctx* c, const gcs_scan_inputs* in, uint64_t seq);
 
 void push_worker(gcs_ctx* c) {
   (void)hipSetDevice(c->cfg.device);
+  c->worker_tid.store((int64_t)syscall(SYS_gettid));
   t_on_worker = true;
   uint64_t seen = 0;
   for (;;) {
@@ -1180,6 +1219,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
                                       partials_need(push_blocks(c->B), 10)});
   if (bad(hipMalloc(&c->d_partials, c->partials_len * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_part_pts, partials_need(std::max(kRedBlocks, points_max_blocks()), 5) * sizeof(double)))) return GCS_ERR_HIP;
+  if (bad(hipMalloc(&c->d_mass_rows, (size_t)points_max_blocks() * sizeof(double2)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_part_push, partials_need(push_blocks(c->B), 10) * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMalloc(&c->d_scalars, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
   if (bad(hipMemset(c->d_scalars, 0, SC_COUNT * sizeof(double)))) return GCS_ERR_HIP;
@@ -1292,7 +1332,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   void* ptrs[] = {c->d_gate_xi, c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
                   c->d_tile_dirty, c->d_tile_order, c->d_tile_work, c->d_bins_part, c->d_tickets,
-                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_part_push, c->d_parse_flag,
+                  c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_mass_rows, c->d_part_push, c->d_parse_flag,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -1309,6 +1349,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (c->h_payload) (void)hipHostFree(c->h_payload);
   if (c->h_psum) (void)hipHostFree(c->h_psum);
   if (c->d_payload) (void)hipFree(c->d_payload);
+  if (c->d_payload_in) (void)hipFree(c->d_payload_in);
   for (int st = 0; st < kStages; ++st)
     for (hipEvent_t e : c->ev[st]) (void)hipEventDestroy(e);
   if (c->ev_push) (void)hipEventDestroy(c->ev_push);
@@ -1377,10 +1418,28 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
       if (value < 0 || value > 10000) return fail(c, GCS_ERR_ARG, "mirror torn delay: 0..10000 us");
       c->mirror_torn = (int)value;
       return GCS_OK;
+    case GCS_DEBUG_SENDBUF:
+      if (value < -1 || value > 1) return fail(c, GCS_ERR_ARG, "send buffer: -1 (by world size), 0 host, 1 device");
+      c->sendbuf_mode = (int)value;
+      return GCS_OK;
     default:
       return fail(c, GCS_ERR_ARG, "unknown debug key");
   }
 }
+
+int gcs_ctx_host_split(gcs_ctx* c, double* ms_sum, int64_t* n, int32_t reset) {
+  if (!c || !ms_sum || !n) return GCS_ERR_ARG;
+  memcpy(ms_sum, c->host_sums, sizeof(c->host_sums));
+  n[0] = c->host_n[0];
+  n[1] = c->host_n[1];
+  if (reset) {
+    memset(c->host_sums, 0, sizeof(c->host_sums));
+    c->host_n[0] = c->host_n[1] = 0;
+  }
+  return GCS_OK;
+}
+
+int64_t gcs_ctx_worker_tid(gcs_ctx* c) { return c ? c->worker_tid.load() : 0; }
 
 int gcs_ctx_mirror_stats(gcs_ctx* c, int64_t* out) {
   if (!c || !out) return GCS_ERR_ARG;
@@ -1636,19 +1695,26 @@ __global__ void k_materialize(const PointRec* recs, const double* iz, const int*
                               double oy, double oz, double tau, int* ids, double* r) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= cap) return;
-  PointRec pr = recs[i];
   const double izi = iz[i];
-  double d0 = pr.dx, d1 = pr.dy, d2 = pr.dz;
   double it = 1.0 / tau;
   if (scale) {
-    const int* row = knn + (size_t)nearest[i] * K;  // d_nearest holds device ids
+    // the 32-B record: d and m re-derived as the bin kernel's staging does (gcs_layout.h PointRec32)
+    const double4 p = reinterpret_cast<const double4*>(recs)[i];
+    const double o[3] = {ox, oy, oz};
+    double d[3];
+    ray_dir(p.x, p.y, p.z, o, d);
+    const double* nb = bin_dirs + 4 * (size_t)nearest[i];  // d_nearest holds device ids
+    const double m = dot3_exact(d[0], d[1], d[2], nb[0], nb[1], nb[2]);
+    const int* row = knn + (size_t)nearest[i] * K;
     for (int k = 0; k < K; ++k) {
       const double* bd = bin_dirs + 4 * (size_t)row[k];
-      double s = dot3_exact(d0, d1, d2, bd[0], bd[1], bd[2]);
+      double s = dot3_exact(d[0], d[1], d[2], bd[0], bd[1], bd[2]);
       if (ids) ids[(size_t)i * K + k] = bin_ref[row[k]];
-      if (r) r[(size_t)i * K + k] = exp((s - pr.m) * it) * izi;
+      if (r) r[(size_t)i * K + k] = exp((s - m) * it) * izi;
     }
   } else {
+    PointRec pr = recs[i];
+    double d0 = pr.dx, d1 = pr.dy, d2 = pr.dz;
     for (int b = 0; b < B; ++b) {
       const double* bd = bin_dirs + 4 * (size_t)b;
       double s = dot3_exact(d0, d1, d2, bd[0], bd[1], bd[2]);
@@ -1824,7 +1890,9 @@ int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st, boo
   c->preint_pending = c->preint_host_pending = false;  // (a failed scan may have left them set)
   if (budget) {  // (the pre-launched front queues k_budget itself)
     c->budget_pending = false;
-    if (int rc0 = stage_budget(c, in->weights_dev, in->n_points)) return rc0;  // runs during the prologue
+    if (int rc0 = stage_budget(c, in->weights_dev, in->n_points, true,
+                               c->self_budget && c->cfg.mode == GCS_MODE_SCALE))  // runs during the prologue
+      return rc0;
   }
   const double* Q = in->Q ? in->Q : c->Q;
   double* cert = st.cert;
@@ -2194,6 +2262,8 @@ int scan_tail(gcs_ctx* c, gcs_scan_state& st, const LidarTerms& lt, gcs_scan_out
   out->stage_ms[5] = ms_between(st.T1, st.Ts);  // of [1]: the device stages' launch calls
   out->stage_ms[6] = ms_between(st.T2, Tq);     // of [2]: tail numerics up to the pushforward launch
   out->stage_ms[7] = ms_between(Tq, Tr);        // of [2]: pushforward launch calls
+  for (int k = 0; k < 8; ++k) c->host_sums[k] += out->stage_ms[k];
+  ++c->host_n[0];
   return GCS_OK;
 }
 
@@ -2203,6 +2273,8 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
   if (!c || !in || !out) return fail(c, GCS_ERR_ARG, "null argument");
   if (in->imu_len < 1 || !in->imu_stamps || !in->imu_gyro || !in->imu_accel) return fail(c, GCS_ERR_ARG, "IMU window required");
   c->live_pending = false;
+  // this scan's device error words arrive with its own mirror: none of an earlier, failed call's stays
+  memset(c->h_err, 0, sizeof(c->h_err));
   // direct buckets for this call's stages (scale mode, unless a bucket overflowed before)
   c->use_direct = c->cfg.mode == GCS_MODE_SCALE && c->direct_buckets && !c->sorted_sticky && c->d_members;
   struct DirectOff {
@@ -2257,7 +2329,9 @@ int gcs_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out) {
     c->sorted_sticky = true;
     c->use_direct = false;
     redone = true;
-    if ((rc = stage_budget(c, in->weights_dev, in->n_points, /*toggle=*/false))) return rc;
+    if ((rc = stage_budget(c, in->weights_dev, in->n_points, /*toggle=*/false,
+                           c->self_budget && c->cfg.mode == GCS_MODE_SCALE)))
+      return rc;
     if ((rc = stage_points(c, in->xyz_dev, in->point_step, in->timestamps_dev, in->weights_dev, in->n_points,
                            in->scan_start_time, in->scan_end_time, st.xi, nullptr, nullptr, nullptr, true,
                            in->xyz_format == 1)))
@@ -2283,6 +2357,8 @@ int gcs_scan_begin(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs
   if (!c || !in || !out) return fail(c, GCS_ERR_ARG, "null argument");
   if (in->imu_len < 1 || !in->imu_stamps || !in->imu_gyro || !in->imu_accel) return fail(c, GCS_ERR_ARG, "IMU window required");
   c->live_pending = false;
+  // this scan's device error words arrive with its own mirror: none of an earlier, failed call's stays
+  memset(c->h_err, 0, sizeof(c->h_err));
   c->use_direct = false;
   gcs_scan_state& st = *c->scan_st;
   if (int rc = scan_prologue(c, in, st)) return rc;
@@ -2440,19 +2516,6 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   }
   lo->n_present_active = nrec;
   for (int i = 0; i < ns; ++i) vs[i] = find(lo->stencil_ids[i]);  // -1: viewed as empty
-  int32_t clear[GCS_LIVE_MAX_TILES];
-  int ncl = 0, nfree = 0;
-  for (int i = 0; i < na; ++i) {
-    int32_t s = find(lo->active_ids[i]);
-    if (s < 0) {  // AtlasMap.index(create=True): the first free slot (stencil ids are distinct)
-      if (nfree >= a->n_free) return fail(c, GCS_ERR_STATE, "primitive map holds max_tiles tiles");
-      s = a->free_slots[nfree++];
-      if (a->slot_written && a->slot_written[s]) clear[ncl++] = s;
-      lo->created_ids[lo->n_created] = lo->active_ids[i];
-      lo->created_slots[lo->n_created++] = s;
-    }
-    lo->active_slots[i] = s;
-  }
   gcs_surfel_ctx* sf = a->surfels;
   gcs_assoc_ctx* as = a->assoc;
   gcs_pmap* pm = a->map;
@@ -2460,6 +2523,31 @@ int gcs_live_scan(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs*
   if (live::surfel_bind_stream(sf, s)) return sub_fail(c, GCS_ERR_HIP, "surfels", gcs_surfel_last_error(sf));
   if (live::assoc_bind_stream(as, s)) return sub_fail(c, GCS_ERR_HIP, "association", gcs_assoc_last_error(as));
   if (live::pmap_bind_stream(pm, s)) return sub_fail(c, GCS_ERR_HIP, "map", gcs_pmap_last_error(pm));
+  int32_t clear[GCS_LIVE_MAX_TILES];
+  int ncl = 0, nfree = 0;
+  for (int i = 0; i < na; ++i) {
+    int32_t s = find(lo->active_ids[i]);
+    if (s < 0) {  // AtlasMap.index(create=True): the first free slot (stencil ids are distinct)
+      if (nfree >= a->n_free) {
+        lo->n_created = 0;  // nothing was created: the caller adopts no tile
+        return fail(c, GCS_ERR_STATE, "primitive map holds max_tiles tiles");
+      }
+      s = a->free_slots[nfree++];
+      if (a->slot_written && a->slot_written[s]) clear[ncl++] = s;
+      lo->created_ids[lo->n_created] = lo->active_ids[i];
+      lo->created_slots[lo->n_created++] = s;
+    }
+    lo->active_slots[i] = s;
+  }
+  // a created tile on a written slot is cleared now, ahead of every launch that can fail: the caller
+  // adopts the created tiles (slot written, count 0) whatever the call returns, so their device
+  // storage must be empty from here on (index(create=True) of the per-operator path clears at once too)
+  for (int k = 0; k < ncl; ++k)
+    if ((rc = live::pmap_clear_tile_launch(pm, clear[k]))) {
+      lo->n_created = 0;
+      return sub_fail(c, rc, "gcs_pmap_clear_tile", gcs_pmap_last_error(pm));
+    }
+  ncl = 0;
   if (a->zero_dev && a->zero_bytes > 0) HIPCHK(c, hipMemsetAsync(a->zero_dev, 0, (size_t)a->zero_bytes, s));
   // surfels of the deskewed points (pipeline.py:778-782), the batch's LiDAR sources set on its valid
   // rows; the launches behind them read the surfel count on the device (no host wait here)
@@ -2780,10 +2868,16 @@ int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, in
 
 int gcs_scan_combine(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* out, void* comm, double w_iw,
                      double w_bary, int32_t scan_count, gcs_belief* comb, double* cert, double* combine_ms) {
+  const clk::time_point tc = clk::now();
   if (int rc = gcs_scan(c, in, out)) return rc;
   const clk::time_point t0 = clk::now();
   const int rc = gcs_combine_allreduce(c, comm, w_iw, w_bary, scan_count, comb, cert);
-  if (combine_ms) *combine_ms = ms_between(t0, clk::now());
+  const clk::time_point t1 = clk::now();
+  const double cm = ms_between(t0, t1);
+  if (combine_ms) *combine_ms = cm;
+  c->host_sums[8] += cm;
+  c->host_sums[9] += ms_between(tc, t1);
+  ++c->host_n[1];
   return rc;
 }
 
@@ -2799,6 +2893,7 @@ int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, in
     memset(c->h_psum, 0, (kLen + 2) * sizeof(double));
     HIPCHK(c, hipHostGetDevicePointer((void**)&c->dh_psum, c->h_psum, 0));
     HIPCHK(c, hipMalloc(&c->d_payload, kLen * sizeof(double)));
+    HIPCHK(c, hipMalloc(&c->d_payload_in, kLen * sizeof(double)));
     HIPCHK(c, hipMalloc(&c->d_pay_seq, sizeof(uint64_t)));
     HIPCHK(c, hipMemset(c->d_pay_seq, 0, sizeof(uint64_t)));
     c->pay_seq = 0;
@@ -2838,7 +2933,23 @@ int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, in
         HIPCHK(c, hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     }
     hipStream_t s = c->comm_stream;
-    ncclResult_t r = ncclAllReduce(c->dh_payload, c->d_payload, len, ncclDouble, ncclSum, (ncclComm_t)comm, s);
+    if (comm != c->comm_seen) {
+      int n = 1;
+      if (ncclCommCount((ncclComm_t)comm, &n) != ncclSuccess) return fail(c, GCS_ERR_HIP, "ncclCommCount");
+      c->comm_seen = comm;
+      c->comm_world = n;
+    }
+    // The send buffer: at world size 1 the collective is a local copy and reads the pinned host buffer
+    // directly (measured above).  With more ranks RCCL's ring kernels would read it across PCIe inside
+    // the collective (and a transport that registers user buffers expects device memory), so the
+    // payload is first copied to device memory by the copy engine on the same stream.
+    const bool dev_send = c->sendbuf_mode == 1 || (c->sendbuf_mode < 0 && c->comm_world > 1);
+    const double* send = c->dh_payload;
+    if (dev_send) {
+      HIPCHK(c, hipMemcpyAsync(c->d_payload_in, c->h_payload, len * sizeof(double), hipMemcpyHostToDevice, s));
+      send = c->d_payload_in;
+    }
+    ncclResult_t r = ncclAllReduce(send, c->d_payload, len, ncclDouble, ncclSum, (ncclComm_t)comm, s);
     if (r != ncclSuccess) return fail(c, GCS_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     HIPCHK(c, launch_payload_out(c->d_payload, c->dh_psum, len, c->d_pay_seq, s));
     const uint64_t seq = ++c->pay_seq;
@@ -2883,6 +2994,7 @@ int gcs_map_follow(gcs_ctx* c, const gcs_scan_inputs* in, const double* rec) {
     if (!std::isfinite(rec[k])) return fail(c, GCS_ERR_NONFINITE, "map-update record not finite");
   double r[GCS_MAP_REC_LEN];
   memcpy(r, rec, sizeof(r));  // (rec may be the context's own lead_rec)
+  memset(c->h_err, 0, sizeof(c->h_err));  // (as gcs_scan: this call's error words only)
   c->use_direct = c->cfg.mode == GCS_MODE_SCALE && c->direct_buckets && !c->sorted_sticky && c->d_members;
   struct DirectOff {
     gcs_ctx* c;

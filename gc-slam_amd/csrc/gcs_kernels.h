@@ -91,6 +91,12 @@ struct PointKernelArgs {
   uint32_t* overflow;
   const double* budget_partials;  // k_budget block partials (folded by every k_points block)
   int budget_blocks;
+  // self-budget mode (gcs_scan / gcs_map_follow, scale mode; round 6): no k_budget -- each block writes
+  // its points' raw mass sums (sum of every raw weight it covers, sum of the selected ones) to
+  // mass_rows[block], the records carry w / Z without the budget's mass_scale (the bin kernel folds the
+  // rows and applies it as it stages them), and the cert partial row holds raw sums
+  // [sum w, sum w^2, sum w win, sum H, max r] that the bin kernel's block 0 scales.  Null: k_budget ran.
+  double2* mass_rows;
   double* scalars;
   // optional debug/parity outputs (may be null)
   double* p0_out;
@@ -150,6 +156,10 @@ struct BinKernelArgs {
   double* scalars;
   const double* pts_partials;  // if set: k_points' partial rows, folded by block 0
   int pts_blocks;
+  // k_points' self-budget mass rows (PointKernelArgs.mass_rows; null: the records carry mass_scale):
+  // every staging block folds them (fixed order) into mass_scale; block 0 publishes the budget scalars
+  const double2* mass_rows;
+  int mass_nrows;
   uint32_t* zero_after;  // bucketing scratch (mid-list length, look-back words) re-armed for the next scan
   int n_zero_after;
   const int* tile_order;  // block -> tile (k_tile_order; null: identity)

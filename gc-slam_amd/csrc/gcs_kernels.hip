@@ -260,12 +260,7 @@ __device__ __forceinline__ int cube_cell(double dx, double dy, double dz, int G)
   return (face * G + iu) * G + iv;
 }
 
-__device__ __forceinline__ void ray_dir(double px, double py, double pz, const double* o, double* d) {
-  double rx = px - o[0], ry = py - o[1], rz = pz - o[2];
-  double nrm = sqrt(dot3_exact(rx, ry, rz, rx, ry, rz));
-  double den = nrm + kEpsMass;
-  d[0] = rx / den; d[1] = ry / den; d[2] = rz / den;
-}
+// ray_dir (the point direction from the LiDAR origin): gcs_math.h
 
 // ---------------------------------------------------------------- row 1+3+5: the point kernel
 // One thread per budget output slot i in [0, cap).  SCALE = candidate-restricted softmax.
@@ -327,6 +322,10 @@ void k_points(PointKernelArgs a, double* partials) {
   double acc[4] = {0.0, 0.0, 0.0, 0.0};  // sum w_budget, sum wn^2, sum w_out, sum H
   double rmax = -INFINITY;
   double mass_scale = 0.0, mass_in = 0.0;
+  // self-budget (PointKernelArgs.mass_rows, scale mode): no fold; the block's raw mass sums go to its row
+  const bool self = SCALE && a.mass_rows != nullptr;
+  double msum[2] = {0.0, 0.0};
+  if (self) mass_scale = 1.0;
   // uniform trip count (the budget fold inside the first iteration has barriers)
   const int gstride = gridDim.x * kPB;
   const int niter = (a.cap + gstride - 1) / gstride;
@@ -346,6 +345,12 @@ void k_points(PointKernelArgs a, double* partials) {
       }
       t = a.timestamps[src];
       w_raw = a.weights[src];
+      if (self && sub == 0) {
+        double wall = w_raw;
+        for (int q = 1; q < a.stride && src + q < (size_t)a.n_raw; ++q) wall += a.weights[src + q];
+        msum[0] += wall;
+        msum[1] += w_raw;
+      }
     }
     double alpha = (t - a.t0) / denom;
     double p0[3];
@@ -518,7 +523,7 @@ void k_points(PointKernelArgs a, double* partials) {
       }
       Z = iz;
     }
-    if (it == 0) {  // block-uniform: the budget fold
+    if (it == 0 && !self) {  // block-uniform: the budget fold
       double v[2] = {0.0, 0.0};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -543,22 +548,30 @@ void k_points(PointKernelArgs a, double* partials) {
     const double wb = w_raw * mass_scale;
     const double wout = wb * win;
     if (a.t_out) a.t_out[i] = t;
-    PointRec pr;
-    pr.x = p0[0]; pr.y = p0[1]; pr.z = p0[2];
-    pr.dx = d[0]; pr.dy = d[1]; pr.dz = d[2];
-    pr.m = m; pr.wz = wout * Z;
-    if (KC != 0) a.recs[i] = pr;
+    if constexpr (SCALE) {  // the 32-B record (gcs_layout.h PointRec32)
+      reinterpret_cast<double4*>(a.recs)[i] = make_double4(p0[0], p0[1], p0[2], wout * Z);
+    } else if constexpr (KC != 0) {
+      PointRec pr;
+      pr.x = p0[0]; pr.y = p0[1]; pr.z = p0[2];
+      pr.dx = d[0]; pr.dy = d[1]; pr.dz = d[2];
+      pr.m = m; pr.wz = wout * Z;
+      a.recs[i] = pr;
+    }
     if (a.iz_out) a.iz_out[i] = Z;
     if (a.p0_out) { a.p0_out[3 * (size_t)i] = p0[0]; a.p0_out[3 * (size_t)i + 1] = p0[1]; a.p0_out[3 * (size_t)i + 2] = p0[2]; }
     if (a.w_out) a.w_out[i] = wout;
     if (a.w_budget_out) a.w_budget_out[i] = wb;
     if (a.nearest_out) a.nearest_out[i] = nearest;
-    double wn = wb / (mass_in + kEpsMass);
+    double wn = self ? wb : wb / (mass_in + kEpsMass);  // (self-budget: raw sums, k_lean's convention)
     acc[0] += wb;
     acc[1] += wn * wn;
     acc[2] += wout;
     acc[3] += H;
     rmax = fmax(rmax, rm);
+  }
+  if (self) {
+    block_sum<2>(msum, lds);
+    if (threadIdx.x == 0) a.mass_rows[blockIdx.x] = make_double2(msum[0], msum[1]);
   }
   block_sum<4>(acc, lds);
   rmax = block_max(rmax, lds);
@@ -634,12 +647,23 @@ void k_points_lean(PointKernelArgs a, double* partials) {
     t = a.timestamps[src];
     w_raw = a.weights[src];
   }
-  // the budget rows landed before the point's loads: two doubles from here on
+  // the budget rows landed before the point's loads: two doubles from here on.  Self-budget (no
+  // k_budget, PointKernelArgs.mass_rows): this point's own raw mass instead -- every raw weight of its
+  // stride window (point_budget.py:80-84's mass_in) and its selected one (mass_sel)
   double bsum[2] = {0.0, 0.0};
+  if (a.mass_rows) {
+    if (valid) {
+      const size_t src = (size_t)i * (size_t)a.stride;
+      bsum[0] = w_raw;
+      for (int q = 1; q < a.stride && src + q < (size_t)a.n_raw; ++q) bsum[0] += a.weights[src + q];
+      bsum[1] = w_raw;
+    }
+  } else {
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    bsum[0] += brow[k].x;
-    bsum[1] += brow[k].y;
+    for (int k = 0; k < 4; ++k) {
+      bsum[0] += brow[k].x;
+      bsum[1] += brow[k].y;
+    }
   }
   double p0[3], d[3], win;
   {
@@ -759,15 +783,21 @@ void k_points_lean(PointKernelArgs a, double* partials) {
     }
   }
   if (live && !a.members) a.keys[i] = valid ? (uint32_t)nearest : (uint32_t)a.n_bins;
-  // the budget fold (block-uniform)
+  // the budget fold (block-uniform); self-budget: the block's mass row (the bin kernel folds the rows)
   block_sum<2>(bsum, lds);
   if (threadIdx.x == 0) {
-    s_mass[0] = bsum[0];
-    s_mass[1] = bsum[0] / (bsum[1] + kEpsMass);  // mass_scale, point_budget.py:80-84
-    if (lb == 0) {
-      a.scalars[SC_MASS_IN] = bsum[0];
-      a.scalars[SC_MASS_SEL] = bsum[1];
-      a.scalars[SC_MASS_SCALE] = s_mass[1];
+    if (a.mass_rows) {
+      a.mass_rows[lb] = make_double2(bsum[0], bsum[1]);
+      s_mass[0] = 0.0;
+      s_mass[1] = 1.0;
+    } else {
+      s_mass[0] = bsum[0];
+      s_mass[1] = bsum[0] / (bsum[1] + kEpsMass);  // mass_scale, point_budget.py:80-84
+      if (lb == 0) {
+        a.scalars[SC_MASS_IN] = bsum[0];
+        a.scalars[SC_MASS_SEL] = bsum[1];
+        a.scalars[SC_MASS_SCALE] = s_mass[1];
+      }
     }
   }
   __syncthreads();
@@ -777,18 +807,16 @@ void k_points_lean(PointKernelArgs a, double* partials) {
   if (live) {
     const double wb = w_raw * mass_scale;
     const double wout = wb * win;
-    PointRec pr;
-    pr.x = p0[0]; pr.y = p0[1]; pr.z = p0[2];
-    pr.dx = d[0]; pr.dy = d[1]; pr.dz = d[2];
-    pr.m = m; pr.wz = wout * iz;
-    a.recs[i] = pr;
+    // the 32-B record: d and m are recomputed by the bin kernel's staging (gcs_layout.h PointRec32)
+    reinterpret_cast<double4*>(a.recs)[i] = make_double4(p0[0], p0[1], p0[2], wout * iz);
     if (a.t_out) a.t_out[i] = t;
     if (a.iz_out) a.iz_out[i] = iz;
     if (a.p0_out) { a.p0_out[3 * (size_t)i] = p0[0]; a.p0_out[3 * (size_t)i + 1] = p0[1]; a.p0_out[3 * (size_t)i + 2] = p0[2]; }
     if (a.w_out) a.w_out[i] = wout;
     if (a.w_budget_out) a.w_budget_out[i] = wb;
     if (a.nearest_out) a.nearest_out[i] = nearest;
-    const double wn = wb / (mass_in + kEpsMass);
+    // (self-budget: raw sums -- wb is w and the second column sum w^2; k_bins_scale's block 0 scales them)
+    const double wn = a.mass_rows ? wb : wb / (mass_in + kEpsMass);
     acc[0] = 0.0 + wb;
     acc[1] = 0.0 + wn * wn;
     acc[2] = 0.0 + wout;
@@ -1177,7 +1205,20 @@ __device__ __forceinline__ uint32_t rec_swz(uint32_t r) { return GCS_REC_SWZ ? (
 int bins_max_tile_sources(int tile_bins) { return max_src(tile_bins); }
 int bins_max_tile_entries(int tile_bins) { return max_rl(tile_bins); }
 
-__device__ __forceinline__ void bin_contrib(double* acc, const double4& bd, double inv_tau, double px, double py,
+// ray_dir (gcs_math.h) with its three divisions issued one after another: the same operations, so the
+// same bits, for the rare unstaged gather, whose loop otherwise set the kernel's register peak
+__device__ __forceinline__ void ray_dir_serial(double px, double py, double pz, const double* o, double* d) {
+#pragma clang fp contract(off)
+  const double rx = px - o[0], ry = py - o[1], rz = pz - o[2];
+  const double den = sqrt(dot3_exact(rx, ry, rz, rx, ry, rz)) + kEpsMass;
+  d[0] = rx / den;
+  __builtin_amdgcn_sched_barrier(0);
+  d[1] = ry / den;
+  __builtin_amdgcn_sched_barrier(0);
+  d[2] = rz / den;
+}
+
+__device__ __forceinline__ void bin_contrib(double* acc, const double3& bd, double inv_tau, double px, double py,
                                             double pz, double dx, double dy, double dz, double m, double wz) {
   double d[3] = {dx, dy, dz};
   double p[3] = {px, py, pz};
@@ -1234,6 +1275,9 @@ __device__ __forceinline__ void wave_reduce_bin_terms(double (&v)[kBinNV]) {
 // phase C: 1 loads the next staged record while accumulating the current one; 2 takes two
 // records per trip (two independent exp chains in flight)
 #define GCS_GATHER_PIPE 2
+#endif
+#ifndef GCS_STAGE_SERIAL
+#define GCS_STAGE_SERIAL 1  // phase B expands its staged 32-B records one after another (register peak)
 #endif
 #ifndef GCS_MAPV_EARLY
 #define GCS_MAPV_EARLY 1  // phase D's map direction stats are loaded before phase A
@@ -1320,6 +1364,45 @@ __device__ __forceinline__ void seg_reduce(double (&acc)[NF], int j, int cnt_b, 
   }
 }
 
+// Self-budget scans (BinKernelArgs.mass_rows): the budget's mass sums from k_points' per-block rows.
+// Thread t sums rows t, t + NT, ... in order, a fixed xor tree sums the wave, and mass_totals adds the
+// waves in order -- every block of the launch gets the same bits (point_budget.py:80-84).
+template <int NT>
+__device__ __forceinline__ double2 mass_rows_wave(const double2* __restrict__ rows, int n) {
+  double sx = 0.0, sy = 0.0;
+  for (int r0 = 0; r0 < n; r0 += 4 * NT) {
+    double2 x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = r0 + (int)threadIdx.x + k * NT;
+      x[k] = r < n ? rows[r] : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sx += x[k].x;
+      sy += x[k].y;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    sx += __shfl_xor(sx, off, 64);
+    sy += __shfl_xor(sy, off, 64);
+  }
+  return make_double2(sx, sy);
+}
+template <int NW>
+__device__ __forceinline__ double mass_scale_of(const double2* s_mw, double* m_in = nullptr, double* m_sel = nullptr) {
+  double mi = s_mw[0].x, ms = s_mw[0].y;
+#pragma unroll
+  for (int w = 1; w < NW; ++w) {
+    mi += s_mw[w].x;
+    ms += s_mw[w].y;
+  }
+  if (m_in) *m_in = mi;
+  if (m_sel) *m_sel = ms;
+  return mi / (ms + kEpsMass);  // mass_scale (point_budget.py:80-84)
+}
+
 // DALL: phase D on every wave -- the first lane of each bin's lane group finalizes the bin from its
 // registers right after the lanes' xor tree (no LDS hand-off, no idle waves); required for tiles
 // wider than one wave (TB > 64).  !DALL: wave 0 alone, one lane per bin (the 64-bin tile's form).
@@ -1356,6 +1439,11 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   __shared__ uint32_t s_work[TB];
   __shared__ uint32_t s_wsum[NW];
   __shared__ double lds[NW * 16];
+  // the LiDAR origin for the staging's ray directions, from LDS: as kernel-argument SGPRs live through
+  // the phases it pushed the kernel past its scalar registers (spilled to a VGPR lane: 3 waves / SIMD)
+  __shared__ double s_org[3];
+  __shared__ double2 s_mw[NW];  // self-budget: the waves' mass-row sums
+  __shared__ double s_msc;      // self-budget: mass_scale (thread 0, after phase A's first barrier)
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   // dispatch order: the previous scan's active tiles first, heaviest first (k_tile_order), so the
   // multi-round C3 grid starts its long tiles early and ends on clean ones; identity if null
@@ -1364,10 +1452,27 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   const int nb = min(TB, a.n_bins - b0);
   PROF(0);
   for (int j = blockIdx.x * NT + t; j < a.n_zero_after; j += gridDim.x * NT) a.zero_after[j] = 0u;
-  if (blockIdx.x == 0 && a.pts_partials) {  // k_points' cert partials (off the critical path here)
-    double pv[5];
-    reduce_partials<5, 16u, NT>(a.pts_partials, a.pts_blocks, pv, lds);
-    if (t == 0)
+  if (blockIdx.x == 0 && (a.pts_partials || a.mass_rows)) {  // k_points' cert partials (off the critical path here)
+    double pv[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    if (a.pts_partials) reduce_partials<5, 16u, NT>(a.pts_partials, a.pts_blocks, pv, lds);
+    if (a.mass_rows) {  // self-budget: the budget scalars, and the raw cert sums scaled by mass_scale
+      const double2 ws = mass_rows_wave<NT>(a.mass_rows, a.mass_nrows);
+      if (lane == 0) s_mw[wid] = ws;
+      __syncthreads();
+      if (t == 0) {
+        double m_in, m_sel;
+        const double msc = mass_scale_of<NW>(s_mw, &m_in, &m_sel);
+        a.scalars[SC_MASS_IN] = m_in;
+        a.scalars[SC_MASS_SEL] = m_sel;
+        a.scalars[SC_MASS_SCALE] = msc;
+        const double q = msc / (m_in + kEpsMass);  // w_budget / (mass_in + eps) = q w
+        pv[0] *= msc;      // sum w_budget
+        pv[1] = pv[1] * q * q;  // sum (w_budget / (mass_in + eps))^2
+        pv[2] *= msc;      // sum w_out
+      }
+      __syncthreads();  // (phase A rewrites s_mw with the same values)
+    }
+    if (t == 0 && a.pts_partials)
       for (int f = 0; f < 5; ++f) a.scalars[SC_DESKEW_WIN + f] = pv[f];
   }
   // the tile flags and phase A's first-level table loads are issued together
@@ -1414,6 +1519,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   if (GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + own_b);
   // phase A
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
+  if (t < 3) s_org[t] = a.origin[t];
   if (t < nb) s_q[t] = q_t;
   if (t == 0) s_q[nb] = q1t;
 #if GCS_RANK_LANES == 4
@@ -1441,6 +1547,10 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       // sorted bucketing: the bucket's start in perm; direct buckets: its member row
       st[k] = t + k * NT < ns ? (a.members ? (uint32_t)src[k] * (uint32_t)a.capb : a.starts[src[k]]) : 0u;
     }
+    if (a.mass_rows) {  // self-budget: the mass rows, loaded behind the tables (one round trip for all)
+      const double2 ws = mass_rows_wave<NT>(a.mass_rows, a.mass_nrows);
+      if (lane == 0) s_mw[wid] = ws;
+    }
 #pragma unroll
     for (int k = 0; k < RL; ++k)
       if (q0 + t + k * NT < q1t) s_rl[t + k * NT] = rl[k];
@@ -1453,6 +1563,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   }
   __syncthreads();
   PROF(1);
+  if (a.mass_rows && t == 0) s_msc = mass_scale_of<NW>(s_mw);  // (read after the next barrier)
 #if GCS_RANK_LANES == 4
   {
     // Records each bin visits (0: inactive / out of range), on the bin's four phase-C lanes: lane l
@@ -1565,18 +1676,20 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     // at most RPT records per thread: every perm load is issued before any record load, so a
     // tile with more records than threads still pays two dependent round trips, not 2 x RPT
     constexpr int RPT = (STAGE + NT - 1) / NT;
-    uint32_t pi[RPT], dst[RPT];
+    uint32_t pi[RPT], dst[RPT], sid[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint32_t r = t + k * NT;
       pi[k] = 0u;
       dst[k] = r;
+      sid[k] = 0u;
       if (r < total) {
         int lo = 0, hi = ns - 1;
         while (lo < hi) {
           int mid = (lo + hi + 1) >> 1;
           if (s_off[mid] <= r) lo = mid; else hi = mid - 1;
         }
+        sid[k] = (uint32_t)a.tile_src[s0 + lo];  // (L2: phase A read the list; no LDS for it)
         const uint32_t pos = s_st[lo] + (r - s_off[lo]);
         if (a.members) {
           // direct buckets hold arrival order: the record's slot is its source's offset + the rank
@@ -1596,21 +1709,34 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         }
       }
     }
-    PointRec pr[RPT];
+    // the 32-B records and their sources' directions in one round trip; each staged record is then
+    // expanded to the 64-B LDS form: d = ray_dir(p), m = d . dir(source) (gcs_layout.h PointRec32)
+    const double4* recs4 = reinterpret_cast<const double4*>(a.recs);
+    double4 pr[RPT];
+    double3 sd[RPT];
 #pragma unroll
     for (int k = 0; k < RPT; ++k)
-      if (t + k * NT < total) pr[k] = a.recs[pi[k]];
+      if (t + k * NT < total) {
+        pr[k] = recs4[pi[k]];
+        const double* sp = a.bin_dirs + 4 * (size_t)sid[k];
+        const double2 xy = *(const double2*)sp;
+        sd[k] = make_double3(xy.x, xy.y, sp[2]);
+      }
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const uint32_t r = dst[k];
       if (t + k * NT < total) {
+        double dd[3];
+        ray_dir(pr[k].x, pr[k].y, pr[k].z, s_org, dd);
+        const double m = dot3_exact(dd[0], dd[1], dd[2], sd[k].x, sd[k].y, sd[k].z);
         double2* d = (double2*)(s_rec + (size_t)r * kRecD);
         const uint32_t sw = rec_swz(r);
         d[0 ^ sw] = make_double2(pr[k].x, pr[k].y);
-        d[1 ^ sw] = make_double2(pr[k].z, pr[k].dx);
-        d[2 ^ sw] = make_double2(pr[k].dy, pr[k].dz);
-        d[3 ^ sw] = make_double2(pr[k].m, pr[k].wz);
+        d[1 ^ sw] = make_double2(pr[k].z, dd[0]);
+        d[2 ^ sw] = make_double2(dd[1], dd[2]);
+        d[3 ^ sw] = make_double2(m, pr[k].w);
       }
+      if (GCS_STAGE_SERIAL) __builtin_amdgcn_sched_barrier(0);  // one record's expansion at a time (registers)
     }
   }
 #if GCS_UNSTAGED_IDX
@@ -1662,7 +1788,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #pragma unroll
   for (int f = 0; f < 19; ++f) acc[f] = 0.0;
   if (i1 > i0) {
-    const double4 bd = s_bd[lb];
+    const double3 bd = make_double3(s_bd[lb].x, s_bd[lb].y, s_bd[lb].z);  // (not the pad: registers)
     const double inv_tau = 1.0 / a.tau;
     // cursor: source q (local j), record k within it
     int q = s_q[lb];
@@ -1783,8 +1909,12 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         } else {
           pidx = a.perm[s_st[j] + kk];
         }
-        const PointRec pr = a.recs[pidx];
-        bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, pr.dx, pr.dy, pr.dz, pr.m, pr.wz);
+        const double4 pr = reinterpret_cast<const double4*>(a.recs)[pidx];
+        const double* sp = a.bin_dirs + 4 * (size_t)a.tile_src[s0 + j];
+        double dd[3];
+        ray_dir_serial(pr.x, pr.y, pr.z, s_org, dd);
+        const double m = dot3_exact(dd[0], dd[1], dd[2], sp[0], sp[1], sp[2]);
+        bin_contrib(acc, bd, inv_tau, pr.x, pr.y, pr.z, dd[0], dd[1], dd[2], m, pr.w);
         if (++kk == c && i + 1 < i1) {  // next source (compacted: non-empty)
           kk = 0;
           ++q;
@@ -1793,6 +1923,11 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         }
       }
     }
+  }
+  if (a.mass_rows) {  // self-budget: the lane's sums times mass_scale (the records carry w / Z without it)
+    const double msc = s_msc;
+#pragma unroll
+    for (int f = 0; f < 19; ++f) acc[f] *= msc;
   }
   if constexpr (BAL) {
     seg_reduce<19>(acc, seg_j, seg_n, seg_max);

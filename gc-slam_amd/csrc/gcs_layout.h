@@ -48,6 +48,17 @@ struct PointRec {
 };
 static_assert(sizeof(PointRec) == 64, "point record");
 
+// Scale mode's point record (round 6): the deskewed point and w / Z only.  The bin kernel's staging
+// recomputes the other two fields bit for bit: d = ray_dir(p) (the point kernel's own expression), and
+// the softmax shift m, which is the dot of d with the point's nearest bin -- the record's source bucket
+// -- because that bin maximises the exact dot over the whole atlas and is one of its own K candidates.
+// Half the bytes the point kernel writes and every bin tile fed by the bucket re-reads.
+struct PointRec32 {
+  double x, y, z;  // deskewed point (scan-start base frame)
+  double wz;       // w / Z as in PointRec
+};
+static_assert(sizeof(PointRec32) == 32, "scale-mode point record");
+
 // Scalar results slots (device buffer of doubles, copied to host once per scan).
 enum Scalar : int {
   SC_MASS_IN = 0,       // sum w (raw)

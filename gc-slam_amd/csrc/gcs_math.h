@@ -48,6 +48,17 @@ GCS_HD double dot3_exact(double ax, double ay, double az, double bx, double by, 
   return s + zz;
 }
 
+// Ray direction of a deskewed point from the LiDAR origin (pipeline.py:589-593): (p - o) / (|p - o| +
+// eps).  One expression for every kernel that forms it -- the point kernel, and the bin kernel's staging
+// that re-derives it from the 32-B record (gcs_layout.h PointRec32) -- so they agree bit for bit.
+GCS_HD void ray_dir(double px, double py, double pz, const double* o, double* d) {
+#pragma clang fp contract(off)
+  double rx = px - o[0], ry = py - o[1], rz = pz - o[2];
+  double nrm = sqrt(dot3_exact(rx, ry, rz, rx, ry, rz));
+  double den = nrm + kEpsMass;
+  d[0] = rx / den; d[1] = ry / den; d[2] = rz / den;
+}
+
 // 1 / d for a positive normal d.  Device: v_rcp_f64 and two Newton steps (within an ulp of the IEEE
 // quotient, 5 instructions against the ~10 of the division's scale / fmas / fixup sequence); host: the
 // division.  The bin kernels' per-bin finalize takes its reciprocals here (the tolerances of the

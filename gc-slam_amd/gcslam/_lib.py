@@ -103,6 +103,7 @@ DEBUG_POINT_KERNEL = 6
 DEBUG_DEVICE_PREINT = 7
 DEBUG_PT_CLEAR = 8
 DEBUG_MIRROR_TORN = 9
+DEBUG_SENDBUF = 10
 MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 
@@ -248,6 +249,8 @@ _SIGS = [
     ("gcs_ctx_map_record", C.c_int, [C.c_void_p, C.c_void_p]),
     ("gcs_map_follow", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("gcs_ctx_stage_times", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int32]),
+    ("gcs_ctx_host_split", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int32]),
+    ("gcs_ctx_worker_tid", C.c_int64, [C.c_void_p]),
     ("gcs_ctx_set_atlas", C.c_int, [C.c_void_p, c_double_p]),
     ("gcs_ctx_get_atlas", C.c_int, [C.c_void_p, c_double_p, c_int32_p]),
     ("gcs_ctx_set_belief", C.c_int, [C.c_void_p, C.POINTER(GcsBelief)]),
@@ -373,6 +376,9 @@ SYMBOLS = [s[0] for s in _SIGS]
 _lib = None
 
 
+_AB_OPTIONAL = ("gcs_ctx_host_split", "gcs_ctx_worker_tid")  # (round 6 diagnostics)
+
+
 def load():
     """Load the HIP library (raises RuntimeError if it was not built: no CPU fallback)."""
     global _lib
@@ -402,9 +408,9 @@ def load():
         raise RuntimeError(f"{path}: ABI {abi}, this binding is ABI {ABI_VERSION}; rebuild the library "
                            "(make -C gc-slam_amd)")
     for name, res, args in _SIGS:
-        # test-only entries (gcs_debug_*) may be absent from an older build loaded through GCSLAM_LIB
+        # test-only and diagnostic entries may be absent from an older build loaded through GCSLAM_LIB
         # for a same-box A/B; every other entry point is required
-        if name.startswith("gcs_debug_") and path != LIB_PATH and not hasattr(lib, name):
+        if (name.startswith("gcs_debug_") or name in _AB_OPTIONAL) and path != LIB_PATH and not hasattr(lib, name):
             continue
         fn = getattr(lib, name)
         fn.restype = res

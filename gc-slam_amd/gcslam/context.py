@@ -184,6 +184,24 @@ class HypothesisContext:
         """gcs_ctx_set_debug (test knobs: L.DEBUG_SCAN_SPIN_LIMIT, L.DEBUG_INJECT_SCAN_FAIL)."""
         self._chk(self.lib.gcs_ctx_set_debug(self.h, int(key), int(value)), "set_debug")
 
+    HOST_SPLIT = ("pre_device", "device_wait", "tail", "gcs_scan", "pre_predict", "launch_calls", "tail_numerics",
+                  "push_launch", "combine", "scan_combine_call")
+
+    def host_split(self, reset=False):
+        """gcs_ctx_host_split: the host split of every scan since the last reset, summed in the library
+        (ms; HOST_SPLIT names), and (scans, gcs_scan_combine calls) counted."""
+        ms = np.zeros(10)
+        n = np.zeros(2, np.int64)
+        if not hasattr(self.lib, "gcs_ctx_host_split"):  # an older build in a same-box A/B
+            return dict(zip(self.HOST_SPLIT, ms.tolist())), (0, 0)
+        self._chk(self.lib.gcs_ctx_host_split(self.h, L.dptr(ms), n.ctypes.data_as(L.c_int64_p), int(reset)),
+                  "host_split")
+        return dict(zip(self.HOST_SPLIT, ms.tolist())), (int(n[0]), int(n[1]))
+
+    def worker_tid(self):
+        """gcs_ctx_worker_tid: the OS thread id of the context's launch worker (0: not started)."""
+        return int(self.lib.gcs_ctx_worker_tid(self.h)) if hasattr(self.lib, "gcs_ctx_worker_tid") else 0
+
     def mirror_stats(self):
         """gcs_ctx_mirror_stats: (scan mirrors accepted, of them re-read at least once, via stream sync,
         all-reduces run, re-read, via stream sync)."""

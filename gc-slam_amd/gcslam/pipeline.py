@@ -246,20 +246,25 @@ _pinned = {}
 
 
 def _to_device(a, dtype, device, role):
-    """Host array -> device tensor through a pinned staging buffer per (role, shape), reused across
-    scans: one async H2D, and before a buffer is refilled the event of its previous copy is waited
-    on (the copy may still be reading it)."""
+    """Host array -> device tensor through one pinned staging buffer per role, grown to the largest
+    array seen (not one per shape: scan sizes vary) and reused across scans: one async H2D, and before
+    the buffer is refilled the event of its previous copy is waited on (the copy may still read it)."""
     import torch
     if isinstance(a, torch.Tensor):
         return a.to(f"cuda:{device}", dtype=dtype).contiguous()
     a = np.ascontiguousarray(a)
-    key = (role, device, dtype, a.shape)
+    key = (role, device, dtype)
     ent = _pinned.get(key)
+    if ent is not None and ent[0].numel() < a.size:
+        if ent[1] is not None:
+            ent[1].synchronize()
+        ent = None
     if ent is None:
-        ent = _pinned[key] = [torch.empty(a.shape, dtype=dtype).pin_memory(), None]
-    buf, ev = ent
+        ent = _pinned[key] = [torch.empty(max(a.size, 4096), dtype=dtype).pin_memory(), None]
+    flat, ev = ent
     if ev is not None:
         ev.synchronize()
+    buf = flat[:a.size].view(a.shape)
     buf.numpy()[...] = a
     out = buf.to(f"cuda:{device}", non_blocking=True)
     ev = torch.cuda.Event()
@@ -297,29 +302,33 @@ def _as_device_scan(raw_points, raw_timestamps, raw_weights, device):
         # the device copy is reused by the next scan on the same stream (stream order keeps the begin's
         # reads of it ahead of the next copy); the staging buffer waits for its previous copy's event
         stream = torch.cuda.current_stream(device)
-        key = ("scan", device, n, stream.cuda_stream)
+        # one staging pair per (device, stream), sized to the largest scan seen: a LiDAR scan's point count
+        # changes from scan to scan, so a buffer per count would grow without bound over a long run
+        key = ("scan", device, stream.cuda_stream)
         ent = _pinned.get(key)
+        if ent is not None and ent[0] < n:
+            if ent[5]:
+                ent[2].synchronize()  # the last copy out of the old buffer before it is dropped
+            ent = None
         if ent is None:
-            # xyz as compact float32 triples (point_step 12: one contiguous cast, not a strided one), then
-            # t and w (8-byte aligned at 16 n)
-            hb = torch.empty(32 * n, dtype=torch.uint8).pin_memory()
-            hn = hb.numpy()
-            d = torch.empty(32 * n, dtype=torch.uint8, device=f"cuda:{device}")
-            ent = _pinned[key] = [hb, torch.cuda.Event(), (hn[:12 * n].view(np.float32).reshape(n, 3),
-                                                           hn[16 * n:24 * n].view(np.float64),
-                                                           hn[24 * n:].view(np.float64)), d,
-                                  (d[:12 * n].view(torch.float32).view(n, 3), d[16 * n:24 * n].view(torch.float64),
-                                   d[24 * n:].view(torch.float64)), False]
-        hb, ev, (hr, ht, hw), d, views, used = ent
+            cap = max(n, 4096)
+            cap = -(-max(cap, (_pinned[key][0] * 3) // 2 if key in _pinned else cap) // 4096) * 4096
+            hb = torch.empty(32 * cap, dtype=torch.uint8).pin_memory()
+            d = torch.empty(32 * cap, dtype=torch.uint8, device=f"cuda:{device}")
+            ent = _pinned[key] = [cap, hb, torch.cuda.Event(), hb.numpy(), d, False]
+        cap, hb, ev, hn, d, used = ent
         if used:
             ev.synchronize()  # the previous copy out of the staging buffer
-        np.copyto(hr, p, casting="unsafe")  # PointCloud2 x,y,z are float32 (backend_node.py:377-468)
-        ht[...] = ts
-        hw[...] = ws
-        d.copy_(hb, non_blocking=True)
+        # this scan's first 32 n bytes: xyz as compact float32 triples at [0, 12 n) (point_step 12: one
+        # contiguous cast, not a strided one), t at [16 n, 24 n), w at [24 n, 32 n); one H2D copy
+        np.copyto(hn[:12 * n].view(np.float32).reshape(n, 3), p, casting="unsafe")  # PointCloud2 x,y,z: float32
+        hn[16 * n:24 * n].view(np.float64)[...] = ts
+        hn[24 * n:32 * n].view(np.float64)[...] = ws
+        d[:32 * n].copy_(hb[:32 * n], non_blocking=True)
         ev.record(stream)
         ent[5] = True
-        return views
+        return (d[:12 * n].view(torch.float32).view(n, 3), d[16 * n:24 * n].view(torch.float64),
+                d[24 * n:32 * n].view(torch.float64))
     else:
         p = np.asarray(raw_points.cpu() if isinstance(raw_points, torch.Tensor) else raw_points,
                        np.float64).reshape(-1, 3)

@@ -238,6 +238,12 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * not arrived; gcs_scan must re-read until the checksum matches (gcs_ctx_mirror_stats counts it) and
  * return the same results.  Test knob of the mirror guard. */
 #define GCS_DEBUG_MIRROR_TORN 9
+/* GCS_DEBUG_SENDBUF: where gcs_combine_allreduce's ncclAllReduce reads its send buffer.  -1 (default):
+ * device memory when the communicator spans more than one rank (the packed payload is copied from the
+ * pinned host buffer by the copy engine on the combine stream, so RCCL's ring kernels never read host
+ * memory across PCIe inside the collective), the pinned host buffer itself at world size 1; 0: always
+ * the host buffer; 1: always device memory (the world-1 test of the world > 1 path). */
+#define GCS_DEBUG_SENDBUF 10
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 /* The scan mirror (the PT fold's copy of the scan's scalars and device error words to pinned host
  * memory, with the scan's sequence number and a checksum; the host accepts it only when both match):
@@ -253,6 +259,15 @@ int gcs_ctx_mirror_stats(gcs_ctx* ctx, int64_t* out /*6*/);
 int gcs_debug_state_checksums(gcs_ctx* ctx, uint64_t* out /*8*/);
 int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*GCS_N_STAGES*/, int64_t* counts /*GCS_N_STAGES*/,
                         int32_t reset);
+/* The host split of every gcs_scan since the last reset, summed (ms): [0..7] the scan's stage_ms
+ * (gcs_scan_outputs: pre-device, device submit + wait, tail, whole scan, budget launch + predict,
+ * device launch calls, tail numerics, pushforward launch calls), [8] gcs_scan_combine's combine, [9]
+ * gcs_scan_combine's whole call; *n the scans counted (n_combine[0]: the combines).  Accumulated in the
+ * library on every scan, so a caller's timed region decomposes exactly, with no per-scan reads. */
+int gcs_ctx_host_split(gcs_ctx* ctx, double* ms_sum /*10*/, int64_t* n /*2*/, int32_t reset);
+/* The OS thread id of the context's launch worker (0 before its first job): a caller that pins its
+ * own thread can keep the worker off that core (bench.py). */
+int64_t gcs_ctx_worker_tid(gcs_ctx* ctx);
 int gcs_ctx_set_atlas(gcs_ctx* ctx, const double* dirs_host /*B*3*/);
 int gcs_ctx_get_atlas(gcs_ctx* ctx, double* dirs_host /*B*3*/, int32_t* knn_host /*B*K*/);
 int gcs_ctx_set_belief(gcs_ctx* ctx, const gcs_belief* b);
@@ -889,10 +904,11 @@ typedef struct {
   int32_t created_slots[GCS_LIVE_MAX_TILES];
   double recency_stats[3];                         /* gcs_pmap_recency_inflate's stats */
   double trigger_sum, ess_sum;                     /* the gcs_lidar_evidence handed to the finish */
-  double phase_us[12];  /* host clock since the call's entry: [0] begin returned, [1] surfels queued, [2] surfel
-                           count read, [3] recency / view / association queued, [4] pose evidence read, [5]
-                           finish returned, [6] step 12b queued; [7] gcs_live_collect's wait; [8] begin's
-                           mirror wait started (in begin) */
+  double phase_us[12];  /* host clock since the call's entry: [0] begin returned, [1] surfels queued,
+                           [3] recency / view / association / pose evidence queued, [4] the one wait for them
+                           returned and their results collected, [5] finish returned, [6] step 12b queued;
+                           [7] gcs_live_collect's wait (set by gcs_live_collect); [2], [8]-[11] unused (the
+                           surfel count is read on the device) */
   /* after gcs_live_collect */
   gcs_pmap_update_stats update;
   int32_t counts[GCS_LIVE_MAX_TILES];              /* valid counts of the active tiles */

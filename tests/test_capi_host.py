@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def test_library_exports_every_header_symbol(lib):
     hdr = open(os.path.join(ROOT, "include", "gcslam_hip.h")).read()
-    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(gcs_\w+)\s*\(", hdr, re.M))
+    declared = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(gcs_\w+)\s*\(", hdr, re.M))
     assert declared, "no declarations parsed"
     assert declared == set(L.SYMBOLS), declared ^ set(L.SYMBOLS)
     for name in declared:

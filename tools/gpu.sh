@@ -33,6 +33,10 @@ step() {
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 120 --timeout-method thread "${k[@]}" \
         > "$O/pytest_gpu.log" 2>&1 ;;
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    snap)  # bitwise snapshot of the bin path (tools/bitwise_snapshot.py), compared with $SNAP_BASE if set
+      timeout -k 10 300 python -u tools/bitwise_snapshot.py save "$O/snap.npz" > "$O/snap.log" 2>&1 || return $?
+      [ -n "$SNAP_BASE" ] && python tools/bitwise_snapshot.py compare "$SNAP_BASE" "$O/snap.npz" > "$O/snap_cmp.txt" 2>&1
+      return 0 ;;
     bench) timeout -k 10 400 python bench.py > "$O/bench_c2.log" 2>&1 ;;
     live) timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-c3 > "$O/bench_live.log" 2>&1 ;;
     benchshared) timeout -k 10 300 python bench.py --map-mode shared --no-cpu-baseline --no-c3 --no-live > "$O/bench_shared.log" 2>&1 ;;
