@@ -128,6 +128,7 @@ struct gcs_ctx {
   bool tile_order_defer = false;
   bool tile_order_pending = false;
   double* d_bins_part = nullptr;    // k_bins_scale partial rows (persistent: clean tiles keep theirs)
+  double* d_bins_raw = nullptr;     // split bin path: active bins' 19 raw sums (field-major; 128-bin tiles)
   double* d_scan = nullptr;
   double* d_map = nullptr;
   double* d_derived = nullptr;
@@ -666,6 +667,7 @@ BinKernelArgs bin_args(gcs_ctx* c) {
   b.n_bins = c->B;
   b.cap = c->cap;
   b.tile_bins = c->tile_bins;
+  b.raw = c->d_bins_raw;
   memcpy(b.origin, c->cfg.lidar_origin, 3 * sizeof(double));
   b.tau = c->cfg.tau;
   b.scan = c->d_scan;
@@ -1291,6 +1293,13 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     }
     if (bad(hipMalloc(&c->d_bins_part, partials_need(bins_scale_blocks(c->B, c->tile_bins), bins_partial_nv()) * sizeof(double))))
       return GCS_ERR_HIP;
+    // the split bin path's raw sums (128-bin tiles; GCSLAM_BINS_SPLIT=0: the fused phase D)
+    static const bool split = [] {
+      const char* e = getenv("GCSLAM_BINS_SPLIT");
+      return !(e && atoi(e) == 0);
+    }();
+    if (split && c->tile_bins == 128 && bad(hipMalloc(&c->d_bins_raw, (size_t)19 * B * sizeof(double))))
+      return GCS_ERR_HIP;
   } else {
     size_t nchunks = (cap + 255) / 256;
     if (bad(hipMalloc(&c->d_bin_partials, nchunks * 19 * B * sizeof(double)))) return GCS_ERR_HIP;
@@ -1331,7 +1340,7 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->d_gate_xi, c->d_members, c->d_bin_dirs, c->d_knn, c->d_rknn_off, c->d_rknn, c->d_pools, c->d_pool_bound, c->d_recs, c->d_iz, c->d_live_p0, c->d_live_w, c->d_live_t, c->d_keys, c->d_slots,
                   c->d_sorted, c->d_nearest, c->d_counts, c->d_starts, c->d_perm, c->d_flags_buf[0], c->d_touched,
-                  c->d_tile_dirty, c->d_tile_order, c->d_tile_work, c->d_bins_part, c->d_tickets,
+                  c->d_tile_dirty, c->d_tile_order, c->d_tile_work, c->d_bins_part, c->d_bins_raw, c->d_tickets,
                   c->d_bin_ref, c->d_tile_src_off, c->d_tile_src, c->d_rknn_local, c->d_part_pts, c->d_mass_rows, c->d_part_push, c->d_parse_flag,
                   c->d_scan, c->d_map, c->d_derived, c->d_bin_partials, c->d_partials, c->d_scalars};
   for (void* p : ptrs)

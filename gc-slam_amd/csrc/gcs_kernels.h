@@ -162,6 +162,10 @@ struct BinKernelArgs {
   int mass_nrows;
   uint32_t* zero_after;  // bucketing scratch (mid-list length, look-back words) re-armed for the next scan
   int n_zero_after;
+  // split finalize (sparse maps, 128-bin tiles; round 6): the gather kernel leaves each active bin's 19
+  // raw sums here (field-major, 19 x B) and k_bins_finalize, one thread per bin at full occupancy, writes
+  // ScanBinStats, the Matrix-Fisher terms and the active tiles' partial rows.  Null: fused phase D.
+  double* raw;
   const int* tile_order;  // block -> tile (k_tile_order; null: identity)
   uint32_t* tile_work;    // per tile: records the tile staged (written for active tiles; may be null)
 };

@@ -1406,7 +1406,10 @@ __device__ __forceinline__ double mass_scale_of(const double2* s_mw, double* m_i
 // DALL: phase D on every wave -- the first lane of each bin's lane group finalizes the bin from its
 // registers right after the lanes' xor tree (no LDS hand-off, no idle waves); required for tiles
 // wider than one wave (TB > 64).  !DALL: wave 0 alone, one lane per bin (the 64-bin tile's form).
-template <int STAGE, int TB, int LANES, bool DALL>
+// SPLIT (sparse maps, 128-bin tiles): phases 0 and A-C only -- each active bin's 19 raw sums go to a.raw
+// and k_bins_finalize runs phase D one thread per bin at full occupancy (the two-wave serial phase D held
+// the tile's workgroup, its LDS and its registers; the gather's register peak is lower without it).
+template <int STAGE, int TB, int LANES, bool DALL, bool SPLIT = false>
 __global__ __launch_bounds__(TB * LANES)
 #if GCS_BINS_WAVES
 __attribute__((amdgpu_waves_per_eu(GCS_BINS_WAVES)))
@@ -1516,7 +1519,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   const bool act_t = t < nb && a.flags[b0 + t];  // bin b0 + t (the phase-A rank's table)
   const bool own_act = DALL ? own && a.flags[b0 + own_b] : act_t;
   MapDir mapv{0.0, 0.0, 0.0, 0.0};
-  if (GCS_MAPV_EARLY && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + own_b);
+  if (GCS_MAPV_EARLY && !SPLIT && own_act) mapv = load_map_dir(a.map, a.n_bins, b0 + own_b);
   // phase A
   if (t < nb) s_bd[t] = *(const double4*)(a.bin_dirs + 4 * (size_t)(b0 + t));
   if (t < 3) s_org[t] = a.origin[t];
@@ -1938,6 +1941,19 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       for (int off = 1; off < LANES; off <<= 1) acc[f] += __shfl_xor(acc[f], off, 64);
   }
   PROF(4);
+  if constexpr (SPLIT) {
+    // the bin's raw sums for k_bins_finalize: the lane group's first lane (a bin without records has no
+    // group and is not active: the finalize takes exact zeros for it, as phase D does)
+    static_assert(BAL && !DALL, "the split gather is the balanced 128-bin form");
+    if (seg_n > 0 && seg_j == 0) {
+      const size_t Bs = (size_t)a.n_bins, b = (size_t)(b0 + lb);
+#pragma unroll
+      for (int f = 0; f < 19; ++f) a.raw[f * Bs + b] = acc[f];
+    }
+    PROF(6);
+    PROFV(7, 1);
+    return;
+  }
   if constexpr (DALL) {
     // phase D on every wave: the group's first lane finalizes its bin from the summed registers
     double v[kBinNV];
@@ -2013,6 +2029,52 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   }
   PROF(6);
   PROFV(7, 1);
+}
+
+// Phase D of the split bin path, one thread per bin of a tile (TB threads, one tile per workgroup): the
+// active tiles' bins (tile flag) from k_bins_scale<..., SPLIT>'s raw sums -- finalize (PSD, kappa, the 26
+// ScanBinStats rows), the Matrix-Fisher term of active bins, and the tile's partial row in the order of
+// the fused kernel's phase D (a fixed xor tree per 64-bin wave, the waves in order): the same bits.
+// Inactive tiles were finished by the gather kernel (zero-bin rows, closed-form partial row).
+template <int TB>
+__global__ __launch_bounds__(TB) void k_bins_finalize(BinKernelArgs a, double* partials) {
+  static_assert(TB % 64 == 0, "whole waves");
+  __shared__ double lds[(TB / 64) * 16];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  const int tile = (int)blockIdx.x;
+  if (!a.flags[a.n_bins + tile]) return;  // block-uniform
+  const int b0 = tile * TB, nb = min(TB, a.n_bins - b0);
+  const bool own = t < nb;
+  const bool act = own && a.flags[b0 + t];
+  const size_t Bs = (size_t)a.n_bins;
+  double acc[19];
+  MapDir mapv{0.0, 0.0, 0.0, 0.0};
+  if (act) {
+    mapv = load_map_dir(a.map, a.n_bins, b0 + t);
+#pragma unroll
+    for (int f = 0; f < 19; ++f) acc[f] = a.raw[f * Bs + b0 + t];
+  } else {
+#pragma unroll
+    for (int f = 0; f < 19; ++f) acc[f] = 0.0;
+  }
+  double v[kBinNV];
+#pragma unroll
+  for (int f = 0; f < kBinNV; ++f) v[f] = 0.0;
+  v[4] = -INFINITY;
+  if (own) {
+    finalize_bin(acc, a.scan, a.n_bins, b0 + t, v);
+    if (act) mf_bin_term(acc[0], acc[1], acc[2], acc[3], mapv, v + 5);
+  }
+  wave_reduce_bin_terms(v);
+  if (lane == 0)
+#pragma unroll
+    for (int f = 0; f < kBinNV; ++f) lds[wid * 16 + f] = v[f];
+  __syncthreads();
+  if (t < kBinNV) {
+    double x = lds[t];
+    for (int w = 1; w < TB / 64; ++w) x = t == 4 ? fmax(x, lds[w * 16 + t]) : x + lds[w * 16 + t];
+    partials[(size_t)tile * pstride<kBinNV>() + t] = x;  // folded by k_final<FIN_BINS>
+  }
 }
 
 // ---------------------------------------------------------------- row 5+6 dense mode (B small)
@@ -2919,7 +2981,11 @@ hipError_t launch_bins_scale(const BinKernelArgs& a, double* partials, hipStream
     hipExtLaunchKernelGGL((k_bins_scale<kStageSmall, 32, 8, false>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else if (a.tile_bins == 128 && big)
     hipExtLaunchKernelGGL((k_bins_scale<kStage128Big, 128, 2, GCS_DALL128>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
-  else if (a.tile_bins == 128)
+  else if (a.tile_bins == 128 && a.raw) {  // split: the gather, then phase D one thread per bin (e0 .. e1: both)
+    hipExtLaunchKernelGGL((k_bins_scale<kStage128Small, 128, 2, false, true>), dim3(nblk), dim3(256), 0, s, e0, nullptr, 0, a,
+                          partials);
+    hipExtLaunchKernelGGL(k_bins_finalize<128>, dim3(nblk), dim3(128), 0, s, nullptr, e1, 0, a, partials);
+  } else if (a.tile_bins == 128)
     hipExtLaunchKernelGGL((k_bins_scale<kStage128Small, 128, 2, GCS_DALL128>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
   else if (a.tile_bins == 256 && big)
     hipExtLaunchKernelGGL((k_bins_scale<kStage256Big, 256, 1, true>), dim3(nblk), dim3(256), 0, s, e0, e1, 0, a, partials);
