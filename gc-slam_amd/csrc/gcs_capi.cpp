@@ -21,6 +21,7 @@
 
 #include "gcs_atlas.h"
 #include "gcs_host.h"
+#include "gcs_imu_odom_core.h"
 #include "gcs_kernels.h"
 #include "gcs_layout.h"
 #include "gcs_live.h"
@@ -202,6 +203,20 @@ struct gcs_ctx {
   // GCS_DEBUG_DEVICE_PREINT; not with the launch gate): the prologue stages the IMU window in pinned
   // memory and queues k_preint, k_points reads its twist, the tail reads its record after the sync
   bool device_preint = false;
+  // the IMU / odometry evidence family on the device (k_imu_odom, gcs_imu_odom.hip; GCSLAM_DEVICE_IMU_ODOM=1
+  // or GCS_DEBUG_DEVICE_IMU_ODOM): launched on io_stream by scan_imu_odom, its stamped record read by
+  // finish_imu_odom before the tail needs the evidence
+  bool device_imu_odom = false;
+  bool io_dev_pending = false;
+  hipStream_t io_stream = nullptr;
+  double* h_io_stage = nullptr;   // pinned: the window + small inputs (the H2D copy's source)
+  double* d_io_win = nullptr;     // device: the same
+  double* d_io_out = nullptr;     // device: the kernel's record (kIoOutWords)
+  double* h_io_out = nullptr;     // pinned, coherent, mapped: the stamped copy (kIoOutWords + 2)
+  double* dh_io_out = nullptr;
+  uint64_t* d_io_seq = nullptr;
+  uint64_t io_seq = 0;
+  int64_t io_rereads = 0, io_syncs = 0;
   hipEvent_t ev_preint = nullptr;  // recorded after each k_preint: its window and record are not touched before it
   bool ev_preint_pending = false;
   bool preint_pending = false;       // the next point stage reads the device twist (d_gate_xi)
@@ -1244,6 +1259,7 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
   if (bad(hipMalloc(&c->d_gate_xi, 8 * sizeof(double)))) return GCS_ERR_HIP;
   if (const char* g = getenv("GCSLAM_GATE")) c->gate_on = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_DEVICE_PREINT")) c->device_preint = atoi(g) != 0;
+  if (const char* g = getenv("GCSLAM_DEVICE_IMU_ODOM")) c->device_imu_odom = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_PT_CLEAR")) c->pt_clear = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_BEGIN_MIRROR")) c->begin_mirror = atoi(g) != 0;
   if (const char* g = getenv("GCSLAM_LIVE_ASYNC")) c->live_async = atoi(g) != 0;
@@ -1364,6 +1380,15 @@ int gcs_ctx_destroy(gcs_ctx* c) {
   if (c->ev_push) (void)hipEventDestroy(c->ev_push);
   if (c->ev_stages) (void)hipEventDestroy(c->ev_stages);
   if (c->ev_preint) (void)hipEventDestroy(c->ev_preint);
+  if (c->io_stream) {
+    (void)hipStreamSynchronize(c->io_stream);
+    (void)hipStreamDestroy(c->io_stream);
+  }
+  if (c->h_io_stage) (void)hipHostFree(c->h_io_stage);
+  if (c->h_io_out) (void)hipHostFree(c->h_io_out);
+  if (c->d_io_win) (void)hipFree(c->d_io_win);
+  if (c->d_io_out) (void)hipFree(c->d_io_out);
+  if (c->d_io_seq) (void)hipFree(c->d_io_seq);
   if (c->push_stream) (void)hipStreamDestroy(c->push_stream);
   if (c->own_stream && c->stream) (void)hipStreamDestroy(c->stream);
   delete c->scan_st;
@@ -1414,6 +1439,9 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
       return GCS_OK;
     case GCS_DEBUG_DEVICE_PREINT:
       c->device_preint = value != 0;
+      return GCS_OK;
+    case GCS_DEBUG_DEVICE_IMU_ODOM:
+      c->device_imu_odom = value != 0;
       return GCS_OK;
     case GCS_DEBUG_PT_CLEAR:
       c->pt_clear = value != 0;
@@ -1947,6 +1975,84 @@ int scan_prologue(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st, boo
   return GCS_OK;
 }
 
+// The IMU / odometry branch on the device (k_imu_odom): the window and the small inputs packed into pinned
+// memory, one H2D copy and the one-workgroup kernel on the context's io_stream (beside the bin path's
+// kernels); finish_imu_odom_dev reads the stamped record (wait_stamped: sequence + checksum).
+int launch_imu_odom_dev(gcs_ctx* c, const gcs_imu_odom_inputs& in) {
+  const int m = in.m;
+  if (m < 2 || m > kImuOdomMaxM)
+    return fail(c, GCS_ERR_ARG, "device IMU/odometry branch: the window holds 2 .. " + std::to_string(kImuOdomMaxM) +
+                                    " samples");
+  const size_t words = (size_t)8 * kImuOdomMaxM + kIoSmallLen;
+  if (!c->d_io_win) {
+    HIPCHK(c, hipHostMalloc(&c->h_io_stage, words * sizeof(double), hipHostMallocDefault));
+    HIPCHK(c, hipMalloc(&c->d_io_win, words * sizeof(double)));
+    HIPCHK(c, hipMalloc(&c->d_io_out, kIoOutWords * sizeof(double)));
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    HIPCHK(c, hipHostMalloc(&c->h_io_out, (kIoOutWords + 2) * sizeof(double), fl));
+    memset(c->h_io_out, 0, (kIoOutWords + 2) * sizeof(double));
+    HIPCHK(c, hipHostGetDevicePointer((void**)&c->dh_io_out, c->h_io_out, 0));
+    HIPCHK(c, hipMalloc(&c->d_io_seq, sizeof(uint64_t)));
+    HIPCHK(c, hipMemset(c->d_io_seq, 0, sizeof(uint64_t)));
+    HIPCHK(c, hipStreamCreateWithFlags(&c->io_stream, hipStreamNonBlocking));
+    c->io_seq = 0;
+  }
+  // the previous call's copy out of the staging buffer has completed (its record was read after it; a
+  // scan that failed before reading it leaves it pending: drain the stream first)
+  if (c->io_dev_pending) {
+    HIPCHK(c, hipStreamSynchronize(c->io_stream));
+    c->io_dev_pending = false;
+  }
+  double* w = c->h_io_stage;
+  memcpy(w, in.stamps, m * sizeof(double));
+  memcpy(w + m, in.gyro, 3 * m * sizeof(double));
+  memcpy(w + 4 * m, in.accel, 3 * m * sizeof(double));
+  memcpy(w + 7 * m, in.w_int, m * sizeof(double));
+  double* sm = w + 8 * m;
+  memcpy(sm + kIoPose0, in.pose0, 6 * sizeof(double));
+  memcpy(sm + kIoPosePred, in.pose_pred, 6 * sizeof(double));
+  memcpy(sm + kIoMuPrev, in.mu_prev, DZ * sizeof(double));
+  memcpy(sm + kIoMuInc, in.mu_inc, DZ * sizeof(double));
+  memcpy(sm + kIoGravity, in.gravity_W, 3 * sizeof(double));
+  memcpy(sm + kIoSigmaG, in.Sigma_g, 9 * sizeof(double));
+  memcpy(sm + kIoSigmaA, in.Sigma_a, 9 * sizeof(double));
+  memcpy(sm + kIoOdomPose, in.odom_pose, 6 * sizeof(double));
+  memcpy(sm + kIoOdomCov, in.odom_cov_se3, 36 * sizeof(double));
+  memcpy(sm + kIoOdomTwist, in.odom_twist, 6 * sizeof(double));
+  memcpy(sm + kIoOdomTwistCov, in.odom_twist_cov, 36 * sizeof(double));
+  HIPCHK(c, hipMemcpyAsync(c->d_io_win, w, ((size_t)8 * m + kIoSmallLen) * sizeof(double), hipMemcpyHostToDevice,
+                           c->io_stream));
+  ImuOdomDevArgs a{};
+  a.win = c->d_io_win;
+  a.m = m;
+  a.t_last_scan = in.t_last_scan;
+  a.t_scan = in.t_scan;
+  a.dt_sec = in.dt_sec;
+  a.planar_z_ref = in.planar_z_ref;
+  a.planar_z_sigma = in.planar_z_sigma;
+  a.planar_vz_sigma = in.planar_vz_sigma;
+  a.out = c->d_io_out;
+  a.host = c->dh_io_out;
+  a.dseq = c->d_io_seq;
+  HIPCHK(c, launch_imu_odom(a, c->io_stream));
+  ++c->io_seq;
+  c->io_dev_pending = true;
+  return GCS_OK;
+}
+
+int finish_imu_odom_dev(gcs_ctx* c, host::ImuOdomOut& io, double* extra) {
+  if (!c->io_dev_pending) return GCS_OK;
+  c->io_dev_pending = false;
+  if (int rc = wait_stamped(c, c->h_io_out, kIoOutWords, c->io_seq, c->io_stream, &c->io_rereads, &c->io_syncs,
+                            "device IMU/odometry evidence"))
+    return rc;
+  memcpy(&io, c->h_io_out, sizeof(host::ImuOdomOut));
+  if (extra) memcpy(extra, c->h_io_out + kIoOutWords - 5, 5 * sizeof(double));
+  for (int k = 0; k < DZ * DZ; ++k)
+    if (!std::isfinite(io.L[k])) return fail(c, GCS_ERR_NONFINITE, "IMU/odometry evidence contains NaN");
+  return GCS_OK;
+}
+
 // 13 measurement-noise IW statistics over the scan-to-scan IMU window (pipeline.py:448-453, 522-566)
 // and 9 the IMU/odometry evidence branch (pipeline.py:595-776), computed while the device stages
 // run (they need no device result); padded samples (stamp <= 0) carry weight 0 (the reference's
@@ -1982,9 +2088,13 @@ int scan_imu_odom(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_state& st, gcs
     ii.odom_twist_cov = in->odom_twist_cov ? in->odom_twist_cov : kBigCov6.v;
     ii.planar_z_ref = c->cfg.planar_z_ref; ii.planar_z_sigma = c->cfg.planar_z_sigma;
     ii.planar_vz_sigma = c->cfg.planar_vz_sigma;
-    run_imu_odom(ii, c->io, st.io_extra);
-    for (int k = 0; k < DZ * DZ; ++k)
-      if (!std::isfinite(c->io.L[k])) return fail(c, GCS_ERR_NONFINITE, "IMU/odometry evidence contains NaN");
+    if (c->device_imu_odom) {  // k_imu_odom beside the device stages; finish_imu_odom_dev reads it
+      if (int rc = launch_imu_odom_dev(c, ii)) return rc;
+    } else {
+      run_imu_odom(ii, c->io, st.io_extra);
+      for (int k = 0; k < DZ * DZ; ++k)
+        if (!std::isfinite(c->io.L[k])) return fail(c, GCS_ERR_NONFINITE, "IMU/odometry evidence contains NaN");
+    }
   } else {
     memset(c->io.L, 0, sizeof(c->io.L));
     memset(c->io.h, 0, sizeof(c->io.h));
@@ -2104,6 +2214,7 @@ void scan_bin_lidar(gcs_ctx* c, gcs_scan_state& st, LidarTerms& lt, gcs_scan_out
 // PoseCovInflationPushforward (push: the bin path; the live path's map update is the caller's step
 // 12b), 14 AnchorDriftUpdate (pipeline.py:1038-1230, 1494-1502)
 int scan_tail(gcs_ctx* c, gcs_scan_state& st, const LidarTerms& lt, gcs_scan_outputs* out, bool push) {
+  if (int rc = finish_imu_odom_dev(c, c->io, st.io_extra)) return rc;  // (the device branch, when it ran)
   double* cert = st.cert;
   Belief& pred = st.pred;
   double Lraw[DZ * DZ], hraw[DZ];
@@ -2391,6 +2502,7 @@ int gcs_scan_begin(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_begin_outputs
   finish_preint(c, st);
   st.T2 = clk::now();
   if ((rc = scan_point_certs(c, in, st))) return rc;
+  if ((rc = finish_imu_odom_dev(c, c->io, st.io_extra))) return rc;  // (the device branch, when it ran)
   // the map branch's linearisation point: z_lin = solve(PSD(L_pred + L_imu_odom), h_pred + h_imu_odom),
   // its pose block (pipeline.py:751-755); read by visual_pose_evidence as [t, rotvec] (:318-322)
   double Lf[DZ * DZ], Lp[DZ * DZ], hf[DZ], zl[DZ];
@@ -3175,6 +3287,31 @@ int gcs_imu_odom_evidence(const gcs_imu_odom_inputs* in, double* L, double* h, d
   }
   delete io;
   return GCS_OK;
+}
+
+int gcs_imu_odom_evidence_device(gcs_ctx* c, const gcs_imu_odom_inputs* in, double* L, double* h, double* cert) {
+  if (!c) return GCS_ERR_ARG;
+  if (!in || !L || !h || in->m < 2 || !in->stamps || !in->gyro || !in->accel || !in->w_int || !in->pose0 ||
+      !in->pose_pred || !in->mu_prev || !in->mu_inc || !in->gravity_W || !in->Sigma_g || !in->Sigma_a ||
+      !in->odom_pose || !in->odom_cov_se3 || !in->odom_twist || !in->odom_twist_cov || !(in->planar_z_sigma > 0.0) ||
+      !(in->planar_vz_sigma > 0.0))
+    return fail(c, GCS_ERR_ARG, "gcs_imu_odom_evidence_device: missing input");
+  if (int rc = launch_imu_odom_dev(c, *in)) return rc;
+  host::ImuOdomOut* io = new host::ImuOdomOut();
+  double ex[5];
+  const int rc = finish_imu_odom_dev(c, *io, ex);
+  if (rc == GCS_OK) {
+    memcpy(L, io->L, sizeof(io->L));
+    memcpy(h, io->h, sizeof(io->h));
+    if (cert) {
+      const double v[GCS_IMU_ODOM_CERT_LEN] = {io->trigger, io->ess_weighted, io->kappa, io->transport_sigma,
+                                               io->imu_scale, io->odom_scale, io->mean_reliability, io->odom.nll,
+                                               io->imu.nll, io->gyro.nll, ex[0], ex[1], ex[2], ex[3], ex[4]};
+      memcpy(cert, v, sizeof(v));
+    }
+  }
+  delete io;
+  return rc;
 }
 
 int gcs_imu_meas_iw_suffstats(int32_t m, const double* stamps, const double* gyro, const double* accel,

@@ -1,0 +1,271 @@
+// Step 9's IMU / odometry evidence family on the device: the reference's
+// _compute_imu_odom_branch (FS/backend/pipeline.py:442-566, 595-776) with its eleven factors
+// (imu_evidence.py:276-589, imu_gyro_evidence.py:38-163, imu_preintegration_factor.py:46-180,
+// odom_evidence.py:39-154, odom_twist_evidence.py:58-430, planar_prior.py:55-195) as one workgroup:
+//   * the window statistics -- dt_int (the sorted in-window stamps' positive gaps), dt_imu, omega_avg
+//     (pipeline.py:262-313, 522-548) -- as block reductions and a bitonic sort in LDS;
+//   * the scan-to-scan preintegration as gcs_preint_scan.h's parallel scans (k_preint's form);
+//   * the IMU vMF factor's per-sample transport consistency, its two medians (bitonic sorts) and the
+//     reliability-weighted sums (fixed-order block sums);
+//   * lane 0 then runs the shared assembly (gcs_imu_odom_core.h imu_odom_assemble) -- the very code
+//     the host branch runs -- into device memory, and every lane copies the result to a pinned host
+//     record stamped with a sequence number and a checksum (the scan mirror's protocol, gcs_layout.h).
+// The host form (gcs_evidence.cpp) stays the default; GCSLAM_DEVICE_IMU_ODOM=1 / GCS_DEBUG_DEVICE_IMU_ODOM
+// selects this one, on its own stream beside the bin path's kernels.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include "gcs_imu_odom_core.h"
+#include "gcs_kernels.h"
+#include "gcs_layout.h"
+#include "gcs_preint_scan.h"
+
+namespace gcs {
+namespace {
+
+constexpr int kIoThreads = preint::kPreintThreads;  // 512
+constexpr int kIoWaves = kIoThreads / 64;
+static_assert(kImuOdomMaxM <= 2 * kIoThreads, "the sorts hold two keys per lane");
+
+// block reductions in a fixed order: a xor tree per wave, then the waves in order (every lane gets it)
+__device__ __forceinline__ double io_block_sum(double v, double* s) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if (lane == 0) s[wid] = v;
+  __syncthreads();
+  double r = s[0];
+  for (int w = 1; w < kIoWaves; ++w) r += s[w];
+  return r;
+}
+__device__ __forceinline__ double io_block_min(double v, double* s) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  __syncthreads();
+  if (lane == 0) s[wid] = v;
+  __syncthreads();
+  double r = s[0];
+  for (int w = 1; w < kIoWaves; ++w) r = fmin(r, s[w]);
+  return r;
+}
+__device__ __forceinline__ double io_block_max(double v, double* s) { return -io_block_min(-v, s); }
+
+// ascending bitonic sort of n (a power of two, <= 2 kIoThreads) keys in LDS
+__device__ void io_sort(double* k, int n) {
+  for (int size = 2; size <= n; size <<= 1)
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      __syncthreads();
+      for (int i = threadIdx.x; i < n / 2; i += kIoThreads) {
+        const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+        const bool up = (lo & size) == 0;
+        const double a = k[lo], b = k[hi];
+        if ((a > b) == up) {
+          k[lo] = b;
+          k[hi] = a;
+        }
+      }
+    }
+  __syncthreads();
+}
+
+// numpy median of the first n sorted keys: the middle one, or the mean of the two middle ones
+__device__ __forceinline__ double io_median(const double* k, int n) {
+  const int h = n / 2;
+  return (n % 2) ? k[h] : 0.5 * (k[h - 1] + k[h]);
+}
+
+__global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
+  __shared__ double s_key[2 * kIoThreads];
+  __shared__ double s_e[2 * kIoThreads];
+  __shared__ double s_red[kIoWaves];
+  __shared__ int s_cnt[kIoWaves + 1];
+  __shared__ double s_pre[9];
+  const int tid = (int)threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int m = a.m;
+  const double* stamps = a.win;
+  const double* gyro = a.win + m;
+  const double* accel = a.win + 4 * m;
+  const double* w_int = a.win + 7 * m;
+  const double* sm = a.win + 8 * m;  // the small inputs (ImuOdomDevArgs layout)
+  const double* pose0 = sm + kIoPose0;
+  const double* mu_inc = sm + kIoMuInc;
+  const double* gb = mu_inc + 9;
+  const double* ab = mu_inc + 12;
+  const double* grav = sm + kIoGravity;
+  const double t0 = a.t_last_scan, t1 = a.t_scan;
+  // ---- dt_imu and omega_avg (pipeline.py:522-548): the valid stamps (> 0)
+  double tmin = INFINITY, tmax = -INFINITY, ws = 0.0;
+  int nv = 0;
+  for (int i = tid; i < m; i += kIoThreads)
+    if (stamps[i] > 0.0) {
+      ++nv;
+      tmin = fmin(tmin, stamps[i]);
+      tmax = fmax(tmax, stamps[i]);
+      ws += w_int[i];
+    }
+  tmin = io_block_min(tmin, s_red);
+  tmax = io_block_max(tmax, s_red);
+  const double wsum = io_block_sum(ws, s_red);
+  const int n_valid = (int)io_block_sum((double)nv, s_red);
+  double dt_imu = n_valid >= 2 ? (tmax - tmin) / (double)(n_valid - 1 > 1 ? n_valid - 1 : 1) : 0.0;
+  dt_imu = dt_imu > 1e-12 ? dt_imu : 1e-12;
+  const double inv = 1.0 / (wsum + kEpsMass);
+  double om[3] = {0.0, 0.0, 0.0};
+  for (int i = tid; i < m; i += kIoThreads)
+    if (stamps[i] > 0.0) {
+      const double wn = w_int[i] * inv;
+      for (int k = 0; k < 3; ++k) om[k] += wn * (gyro[3 * i + k] - gb[k]);
+    }
+  for (int k = 0; k < 3; ++k) om[k] = io_block_sum(om[k], s_red);
+  // ---- dt_int (pipeline.py:262-313): the in-window stamps in order, sorted, their positive gaps summed
+  const double eps = 1e-9;
+  int n_in = 0;
+  {
+    int base = 0;
+    for (int c0 = 0; c0 < m; c0 += kIoThreads) {  // order-preserving compaction into s_key
+      const int i = c0 + tid;
+      const bool in = i < m && stamps[i] > t0 - eps && stamps[i] <= t1 + eps && stamps[i] > 0.0;
+      const unsigned long long bal = __ballot(in);
+      const int before = __popcll(bal & ((1ull << lane) - 1ull));
+      __syncthreads();
+      if (lane == 0) s_cnt[wid] = __popcll(bal);
+      __syncthreads();
+      int off = base;
+      for (int w = 0; w < wid; ++w) off += s_cnt[w];
+      if (in) s_key[off + before] = stamps[i];
+      int tot = 0;
+      for (int w = 0; w < kIoWaves; ++w) tot += s_cnt[w];
+      base += tot;
+    }
+    n_in = base;
+  }
+  int np = 2;
+  while (np < n_in) np <<= 1;
+  for (int i = n_in + tid; i < np; i += kIoThreads) s_key[i] = INFINITY;
+  io_sort(s_key, np);
+  double gaps = 0.0;
+  for (int i = 1 + tid; i < n_in; i += kIoThreads) {
+    const double g = s_key[i] - s_key[i - 1];
+    gaps += g > 0.0 ? g : 0.0;
+  }
+  gaps = io_block_sum(gaps, s_red);
+  double dt_int = 0.0;
+  if (n_in >= 2) {
+    const double span = t1 - t0;
+    dt_int = gaps < span ? gaps : span;
+    dt_int = dt_int > 0.0 ? dt_int : 0.0;
+  }
+  // ---- the scan-to-scan preintegration (pipeline.py:442-453; imu_preintegration.py:47-147)
+  double Pc[9], vc[3], pc[3], ess;
+  preint::window_carry(stamps, gyro, accel, m, [=](int i, double) { return w_int[i]; }, pose0 + 3, gb, ab, grav, Pc,
+                       vc, pc, ess);
+  if (tid == 0) {
+    double R0[9], Re[9], dR[9];
+    so3_exp(pose0 + 3, R0);
+    preint::mat3_mul_inplace(R0, Pc, Re);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) dR[3 * i + j] = R0[i] * Re[j] + R0[3 + i] * Re[3 + j] + R0[6 + i] * Re[6 + j];
+    for (int i = 0; i < 3; ++i) s_pre[i] = R0[i] * pc[0] + R0[3 + i] * pc[1] + R0[6 + i] * pc[2];  // dp (body)
+    for (int i = 0; i < 3; ++i) s_pre[6 + i] = R0[i] * vc[0] + R0[3 + i] * vc[1] + R0[6 + i] * vc[2];  // dv
+    so3_log(dR, s_pre + 3);  // drot
+  }
+  // ---- the IMU vMF factor's per-sample statistics (imu_evidence.py:276-399)
+  for (int i = tid; i < m; i += kIoThreads) {  // transport consistency e_i (central differences)
+    double df[3], ai[3], c[3];
+    for (int k = 0; k < 3; ++k) {
+      ai[k] = accel[3 * i + k] - ab[k];
+      if (i == 0) df[k] = ((accel[3 + k] - ab[k]) - ai[k]) / (dt_imu + kEpsMass);
+      else if (i == m - 1) df[k] = (ai[k] - (accel[3 * (i - 1) + k] - ab[k])) / (dt_imu + kEpsMass);
+      else df[k] = ((accel[3 * (i + 1) + k] - ab[k]) - (accel[3 * (i - 1) + k] - ab[k])) / (2 * dt_imu + kEpsMass);
+    }
+    cross3(gyro + 3 * i, ai, c);
+    const double ex = df[0] + c[0], ey = df[1] + c[1], ez = df[2] + c[2];
+    s_e[i] = sqrt(ex * ex + ey * ey + ez * ez);
+  }
+  int mp = 2;
+  while (mp < m) mp <<= 1;
+  __syncthreads();
+  for (int i = tid; i < mp; i += kIoThreads) s_key[i] = i < m ? s_e[i] : INFINITY;
+  io_sort(s_key, mp);
+  const double med = io_median(s_key, m);
+  __syncthreads();
+  for (int i = tid; i < mp; i += kIoThreads) s_key[i] = i < m ? fabs(s_e[i] - med) : INFINITY;
+  io_sort(s_key, mp);
+  host::ImuVmfStats v{};
+  v.sigma = io_median(s_key, m) / 0.6745 + kEpsMass;
+  double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // rel, w, w_int, S[3]
+  for (int i = tid; i < m; i += kIoThreads) {
+    const double q = s_e[i] / v.sigma;
+    const double rel = exp(-0.5 * (q * q));
+    const double w = w_int[i] * rel;
+    acc[0] += rel;
+    acc[1] += w;
+    acc[2] += w_int[i];
+    double ai[3];
+    for (int k = 0; k < 3; ++k) ai[k] = accel[3 * i + k] - ab[k];
+    const double n = sqrt(ai[0] * ai[0] + ai[1] * ai[1] + ai[2] * ai[2]);
+    for (int k = 0; k < 3; ++k) acc[3 + k] += w * (ai[k] / (n + kEpsMass));
+  }
+  v.rel_sum = io_block_sum(acc[0], s_red);
+  v.ess_w = io_block_sum(acc[1], s_red);
+  v.ess_raw = io_block_sum(acc[2], s_red);
+  for (int k = 0; k < 3; ++k) v.S[k] = io_block_sum(acc[3 + k], s_red);
+  // ---- lane 0: the eleven factors and their sum (the host branch's code), into device memory
+  host::ImuOdomOut* out = reinterpret_cast<host::ImuOdomOut*>(a.out);
+  double* extra = a.out + kIoOutWords - 5;
+  if (tid == 0) {
+    host::ImuOdomInputs in{};
+    in.m = m;
+    in.stamps = stamps; in.gyro = gyro; in.accel = accel; in.w_int = w_int;
+    in.dt_imu = dt_imu; in.dt_int = dt_int; in.dt_sec = a.dt_sec;
+    in.omega_avg = om;
+    in.dp_int = s_pre; in.drot_int = s_pre + 3; in.dv_int = s_pre + 6;
+    in.pose0 = pose0; in.pose_pred = sm + kIoPosePred; in.mu_prev = sm + kIoMuPrev; in.mu_inc = mu_inc;
+    in.accel_bias = ab;
+    in.gravity = grav;
+    in.Sigma_g = sm + kIoSigmaG; in.Sigma_a = sm + kIoSigmaA;
+    in.odom_pose = sm + kIoOdomPose; in.odom_cov = sm + kIoOdomCov; in.odom_twist = sm + kIoOdomTwist;
+    in.odom_twist_cov = sm + kIoOdomTwistCov;
+    in.planar_z_ref = a.planar_z_ref; in.planar_z_sigma = a.planar_z_sigma; in.planar_vz_sigma = a.planar_vz_sigma;
+    host::imu_odom_assemble(in, v, *out);
+    extra[0] = dt_int; extra[1] = dt_imu; extra[2] = om[0]; extra[3] = om[1]; extra[4] = om[2];
+  }
+  __syncthreads();
+  // ---- the stamped copy to the pinned host record: kIoOutWords words, sequence, checksum
+  if (!a.host) return;
+  uint64_t* hw = reinterpret_cast<uint64_t*>(a.host);
+  const uint64_t* dw = reinterpret_cast<const uint64_t*>(a.out);
+  unsigned long long h = 0;
+  for (int i = tid; i < kIoOutWords; i += kIoThreads) {
+    const uint64_t w = dw[i];
+    hw[i] = w;
+    h += mirror_word_hash(w, (uint32_t)i);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) h += __shfl_xor(h, o, 64);
+  __shared__ unsigned long long s_h[kIoWaves];
+  if (lane == 0) s_h[wid] = h;
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) {
+    const uint64_t seq = *a.dseq + 1u;
+    *a.dseq = seq;
+    uint64_t sum = mirror_word_hash(seq, (uint32_t)kIoOutWords);
+    for (int w = 0; w < kIoWaves; ++w) sum += s_h[w];
+    hw[kIoOutWords + 1] = sum;
+    hw[kIoOutWords] = seq;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_imu_odom(const ImuOdomDevArgs& a, hipStream_t s) {
+  if (a.m < 2 || a.m > kImuOdomMaxM) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_imu_odom, dim3(1), dim3(kIoThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace gcs

@@ -199,6 +199,25 @@ struct PreintArgs {
   double* host_out;   // pinned host or null: xi[6], ess, delta_pose[6], delta_v[3]
 };
 hipError_t launch_preint(const PreintArgs& a, hipStream_t s);
+// the IMU / odometry evidence family on the device (gcs_imu_odom.hip): one workgroup, windows of at most
+// kImuOdomMaxM samples.  win (device): stamps[m], gyro[3m], accel[3m], w_int[m], then the small inputs at
+// the ImuOdomSmall offsets; out (device): host::ImuOdomOut + [dt_int, dt_imu, omega_avg 3] (kIoOutWords
+// words); host (pinned, mapped; may be null): out's words, the call's sequence number, a checksum
+constexpr int kImuOdomMaxM = 1024;
+enum ImuOdomSmall : int {
+  kIoPose0 = 0, kIoPosePred = 6, kIoMuPrev = 12, kIoMuInc = 34, kIoGravity = 56, kIoSigmaG = 59, kIoSigmaA = 68,
+  kIoOdomPose = 77, kIoOdomCov = 83, kIoOdomTwist = 119, kIoOdomTwistCov = 125, kIoSmallLen = 161
+};
+struct ImuOdomDevArgs {
+  const double* win;
+  int m;
+  double t_last_scan, t_scan, dt_sec;
+  double planar_z_ref, planar_z_sigma, planar_vz_sigma;
+  double* out;
+  double* host;
+  uint64_t* dseq;  // device: the calls' sequence counter
+};
+hipError_t launch_imu_odom(const ImuOdomDevArgs& a, hipStream_t s);
 hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err, hipStream_t s);
 // the hypothesis all-reduce's stage-out (gcs_combine_allreduce): the device sum to a host buffer of n
 // words + [n] sequence number (*dseq + 1, stored back to *dseq) + [n + 1] checksum (mirror_word_hash)

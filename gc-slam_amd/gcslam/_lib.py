@@ -104,6 +104,7 @@ DEBUG_DEVICE_PREINT = 7
 DEBUG_PT_CLEAR = 8
 DEBUG_MIRROR_TORN = 9
 DEBUG_SENDBUF = 10
+DEBUG_DEVICE_IMU_ODOM = 11
 MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 
@@ -295,6 +296,8 @@ _SIGS = [
                                        c_double_p, c_double_p, c_double_p, c_double_p, c_double_p]),
     ("gcs_belief_world_pose", C.c_int, [C.POINTER(GcsBelief), c_double_p]),
     ("gcs_imu_odom_evidence", C.c_int, [C.POINTER(GcsImuOdomInputs), c_double_p, c_double_p, c_double_p]),
+    ("gcs_imu_odom_evidence_device", C.c_int, [C.c_void_p, C.POINTER(GcsImuOdomInputs), c_double_p, c_double_p,
+                                               c_double_p]),
     ("gcs_imu_meas_iw_suffstats", C.c_int, [C.c_int32] + [c_double_p] * 10),
     ("gcs_meas_iw_apply", C.c_int, [c_double_p] * 7),
     ("gcs_fibonacci_atlas", C.c_int, [C.c_int32, c_double_p]),

@@ -244,6 +244,10 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * memory across PCIe inside the collective), the pinned host buffer itself at world size 1; 0: always
  * the host buffer; 1: always device memory (the world-1 test of the world > 1 path). */
 #define GCS_DEBUG_SENDBUF 10
+/* GCS_DEBUG_DEVICE_IMU_ODOM != 0 (or GCSLAM_DEVICE_IMU_ODOM=1): the step-9 IMU / odometry branch of gcs_scan /
+ * gcs_scan_begin runs on the device (gcs_imu_odom_evidence_device's kernel) beside the bin path's kernels,
+ * instead of the host C++ branch (the default). */
+#define GCS_DEBUG_DEVICE_IMU_ODOM 11
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 /* The scan mirror (the PT fold's copy of the scan's scalars and device error words to pinned host
  * memory, with the scan's sequence number and a checksum; the host accepts it only when both match):
@@ -401,6 +405,11 @@ int gcs_belief_world_pose(const gcs_belief* b, double* pose6); /* belief.py:410-
  *         odom scale, mean reliability, odom nll, imu nll/ess, gyro nll, dt_int, dt_imu, omega_avg(3)] */
 #define GCS_IMU_ODOM_CERT_LEN 15
 int gcs_imu_odom_evidence(const gcs_imu_odom_inputs* in, double* L, double* h, double* cert);
+/* The same branch on the device (gcs_imu_odom.hip k_imu_odom: one workgroup; window statistics, the
+ * scan-to-scan preintegration and the IMU factor's medians and weighted sums in parallel, the eleven
+ * factors' assembly -- the host branch's own code -- on lane 0) on ctx's stream for it, same outputs.
+ * m <= 1024.  gcs_scan / gcs_scan_begin take it under GCS_DEBUG_DEVICE_IMU_ODOM / GCSLAM_DEVICE_IMU_ODOM=1. */
+int gcs_imu_odom_evidence_device(gcs_ctx* ctx, const gcs_imu_odom_inputs* in, double* L, double* h, double* cert);
 int gcs_imu_meas_iw_suffstats(int32_t m, const double* stamps, const double* gyro, const double* accel,
                               const double* w_int, const double* gyro_bias, const double* accel_bias,
                               const double* rotvec0, const double* gravity_W, double* dPsi3x9, double* dnu3);
