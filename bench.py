@@ -303,6 +303,26 @@ def c3_roofline(device, steps=16, warmup=3):
     return r, roofline_chain(cfg["N"], cfg["B"], avg, label, config="c3")
 
 
+def pin_main_and_worker(ctx, share):
+    """The main thread on the share's last core, the context's launch worker on the rest of it (disjoint):
+    the worker spins 2 ms after each job, and a worker woken onto the main thread's core (wake-affine
+    placement) time-slices with it for up to a scheduler slice -- the multi-millisecond calls of the
+    round-5 driver line.  Returns the placement for the line, or {} when the share
+    is too small (fewer than 4 CPUs) or the kernel refuses."""
+    if os.environ.get("GCSLAM_BENCH_PIN_MAIN", "1") == "0" or len(share) < 4:
+        return {}
+    try:
+        os.sched_setaffinity(threading.get_native_id(), {share[-1]})
+        out = dict(main_thread_cpu=share[-1])
+        wt = ctx.worker_tid()
+        if wt:
+            os.sched_setaffinity(wt, set(share[:-1]))
+            out["worker_cpus"] = f"{share[0]}-{share[-2]} ({len(share) - 1})"
+        return out
+    except OSError:
+        return {}
+
+
 def live_path_bench(device, steps=30, warmup=10):
     """The live primitive path -- the LiDAR evidence the reference runs today (surfels, recency + atlas
     view, OT association, visual pose evidence, fusion, step 12b; pipeline.py:778-926, 980-1011,
@@ -344,8 +364,12 @@ def live_path_bench(device, steps=30, warmup=10):
         state["seq"] += 1
         return r
 
+    share = sorted(os.sched_getaffinity(0))
+    placement = {}
     for k in range(warmup):
         one(scans[k])
+        if k == 0:  # the first call started the context's worker (step 12b's launches)
+            placement = pin_main_and_worker(ctx, share)
     torch.cuda.synchronize()
     # The start-up heap (torch, numpy, the earlier passes) into the collector's permanent generation: a
     # full collection in the timed calls then scans only this loop's objects.  The serving loop of the
@@ -435,7 +459,7 @@ def live_path_bench(device, steps=30, warmup=10):
     mu = r.map_update_cert
     out = dict(ms_per_call=float(per.mean() * 1e3), ms_median=float(np.median(per) * 1e3),
                ms_p90=float(np.percentile(per, 90) * 1e3), ms_max=float(per.max() * 1e3), calls=int(steps),
-               attribution=attribution,
+               attribution=attribution, placement=placement or "share (not pinned)",
                path="gcs_live_scan (one C call per scan)" if chain_on else "per-operator C calls",
                per_operator_ms_per_call=float(per_op.mean() * 1e3),
                per_operator_ms_median=float(np.median(per_op) * 1e3),
@@ -450,6 +474,7 @@ def live_path_bench(device, steps=30, warmup=10):
     gc.unfreeze()  # (frozen for the per-operator pass too)
     am.close()
     ctx.close()
+    os.sched_setaffinity(threading.get_native_id(), set(share))
     return out
 
 
@@ -869,18 +894,9 @@ def main():
         # main thread runs on one core of the rank's share -- the last one, away from the low CPUs that
         # take interrupts: the scan's serial host numerics stop migrating between cores, and the rest of
         # the warm-up warms that core (GCSLAM_BENCH_PIN_MAIN=0: the share for every thread, for A/B)
-        if wi == 0 and os.environ.get("GCSLAM_BENCH_PIN_MAIN", "1") != "0" and len(share) >= 4:
-            try:
-                os.sched_setaffinity(threading.get_native_id(), {share[-1]})
-                pin = dict(pin, main_thread_cpu=share[-1])
-                # the launch worker (it spins 2 ms after each job, so at a scan per 0.1 ms it never sleeps)
-                # keeps the rest of the share, never the main thread's core
-                wt = ctx.worker_tid()
-                if wt:
-                    os.sched_setaffinity(wt, set(share[:-1]))
-                    pin = dict(pin, worker_cpus=f"{share[0]}-{share[-2]} ({len(share) - 1})")
-            except OSError:
-                pass
+        # (pin_main_and_worker: the launch worker keeps the rest of the share, never the main thread's core)
+        if wi == 0:
+            pin = dict(pin, **pin_main_and_worker(ctx, share))
     state["warm_stamp"] = False
     state["sample"] = True
     ctx.synchronize()
@@ -911,6 +927,7 @@ def main():
         per_rank_s = [float(x.item()) for x in allt]
         elapsed = max(per_rank_s)  # the slowest rank's clock
     state["sample"] = False
+    hist = ctx.host_split_history(args.steps)  # (before the reset) every timed scan's own split
     hsum, (n_scans_h, n_calls_h) = ctx.host_split(reset=True)
     ms_sum, counts = ctx.stage_times(reset=True)
     bins_in_region = int(counts[2])
@@ -952,6 +969,17 @@ def main():
         side_loop("host_combine_unstamped")
         state["combine"] = combine
     state["fused"] = fused
+    # the step with the IMU / odometry branch on the device (k_imu_odom on its own stream
+    # beside the bin path's kernels) instead of the host C++ branch, same box, its own warm-up
+    try:
+        ctx.set_debug(L.DEBUG_DEVICE_IMU_ODOM, 1)
+    except (RuntimeError, ValueError) as e:  # an older library in a same-box A/B
+        variants["device_imu_odom_unstamped_error"] = str(e)[:200]
+    else:
+        try:
+            side_loop("device_imu_odom_unstamped")
+        finally:
+            ctx.set_debug(L.DEBUG_DEVICE_IMU_ODOM, 0)
     state["stamp"] = True
     if "main_thread_cpu" in pin:  # the share again (the C3 pass, the live path, the CPU baseline's processes)
         os.sched_setaffinity(threading.get_native_id(), set(share))
@@ -978,6 +1006,19 @@ def main():
     host_avg["scans_counted"] = n_scans_h
     host_avg["note"] = ("every timed step (gcs_ctx_host_split sums in the library): pre_device + device_wait + tail "
                         "= gcs_scan; gcs_scan + combine = the C call; + python_other = ms_per_step of this rank")
+    if hist is not None and len(hist):
+        # the per-step distribution of the same split (the library's per-scan record), and the steps
+        # over twice the median step with their own split: a host stall names its phase
+        q = lambda a, p: float(np.percentile(a, p))  # noqa: E731
+        host_avg["per_step"] = {n: dict(p50=q(hist[:, k], 50), p90=q(hist[:, k], 90), max=float(hist[:, k].max()))
+                                for k, n in enumerate(ctx.HOST_HIST) if hist[:, k].any()}
+        med_step = float(np.median(per_step))
+        slow = np.nonzero(per_step > 2.0 * med_step)[0]
+        host_avg["steps_over_2x_median"] = int(len(slow))
+        if len(hist) == len(per_step):
+            host_avg["slow_steps"] = [dict(step=int(i), ms=float(per_step[i] * 1e3),
+                                           split={n: float(hist[i, k]) for k, n in enumerate(ctx.HOST_HIST)})
+                                      for i in slow[:5]]
     cm = np.array(comb_ms) if comb_ms else np.zeros(1)
     me = dict(rank=rank, affinity=pin, host_ms=host_avg, ms_per_step=elapsed_rank / args.steps * 1e3,
               combine_ms=dict(median=float(np.median(cm)), p90=float(np.percentile(cm, 90)), mean=float(cm.mean()),
@@ -1030,10 +1071,11 @@ def main():
             "mirror": mirror,
             "step_variants": dict(variants, step_call="gcs_scan_combine (one C call)" if fused is not None
                                   else "gcs_scan + gcs_combine_allreduce",
-                                  note="the same step count again after the timed region, not `value`: "
-                                  "without the roofline kernel's event stamps, as two C calls (scan, then "
-                                  "combine), and (N = 1) with the host-only combine in place of the world-1 "
-                                  "ncclAllReduce"),
+                                  note="the same step count again after the timed region, not `value`, each "
+                                  "after its own warm-up (mean and median): without the roofline kernel's event "
+                                  "stamps, as two C calls (scan, then combine), (N = 1) with the host-only combine "
+                                  "in place of the world-1 ncclAllReduce, and with the IMU / odometry branch on the "
+                                  "device (k_imu_odom) instead of the host"),
             "step_ms": {"median": float(np.median(per_step) * 1e3), "p90": float(np.percentile(per_step, 90) * 1e3),
                         "min": float(per_step.min() * 1e3), "max": float(per_step.max() * 1e3)},
             "roofline": dict(roofline(N, B, bins_ms, *pmc_traffic(args.config)) or {}, timed_launches=bins_samples,

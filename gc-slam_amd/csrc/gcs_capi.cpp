@@ -293,6 +293,10 @@ struct gcs_ctx {
   // gcs_ctx_host_split: every scan's stage_ms and combine, summed
   double host_sums[10] = {};
   int64_t host_n[2] = {0, 0};
+  // the same split per scan since the last reset, the latest kHostHist scans: [pre-device, device
+  // submit + wait, tail, whole scan, combine, whole gcs_scan_combine call] (ms; gcs_ctx_host_split_history)
+  static constexpr int kHostHist = 4096;
+  std::vector<float> host_hist = std::vector<float>((size_t)kHostHist * 6, 0.0f);
   std::atomic<int64_t> worker_tid{0};
   bool budget_pending = false;  // k_budget already queued for the coming point stage (gcs_scan)
   // self-budget scans (round 6; GCSLAM_SELF_BUDGET=0 for A/B): no k_budget -- k_points writes per-block
@@ -1476,6 +1480,18 @@ int gcs_ctx_host_split(gcs_ctx* c, double* ms_sum, int64_t* n, int32_t reset) {
   return GCS_OK;
 }
 
+int gcs_ctx_host_split_history(gcs_ctx* c, float* out, int32_t n_max, int32_t* n_out) {
+  if (!c || !out || !n_out || n_max < 0) return GCS_ERR_ARG;
+  const int64_t have = std::min<int64_t>(c->host_n[0], gcs_ctx::kHostHist);
+  const int64_t n = std::min<int64_t>(have, n_max);
+  for (int64_t i = 0; i < n; ++i) {  // the latest n scans, oldest first
+    const int64_t k = c->host_n[0] - n + i;
+    memcpy(out + 6 * i, c->host_hist.data() + (size_t)(k % gcs_ctx::kHostHist) * 6, 6 * sizeof(float));
+  }
+  *n_out = (int32_t)n;
+  return GCS_OK;
+}
+
 int64_t gcs_ctx_worker_tid(gcs_ctx* c) { return c ? c->worker_tid.load() : 0; }
 
 int gcs_ctx_mirror_stats(gcs_ctx* c, int64_t* out) {
@@ -1987,7 +2003,7 @@ int launch_imu_odom_dev(gcs_ctx* c, const gcs_imu_odom_inputs& in) {
   if (!c->d_io_win) {
     HIPCHK(c, hipHostMalloc(&c->h_io_stage, words * sizeof(double), hipHostMallocDefault));
     HIPCHK(c, hipMalloc(&c->d_io_win, words * sizeof(double)));
-    HIPCHK(c, hipMalloc(&c->d_io_out, kIoOutWords * sizeof(double)));
+    HIPCHK(c, hipMalloc(&c->d_io_out, (kIoOutWords + kImuOdomStatWords) * sizeof(double)));
     const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
     HIPCHK(c, hipHostMalloc(&c->h_io_out, (kIoOutWords + 2) * sizeof(double), fl));
     memset(c->h_io_out, 0, (kIoOutWords + 2) * sizeof(double));
@@ -2383,6 +2399,9 @@ int scan_tail(gcs_ctx* c, gcs_scan_state& st, const LidarTerms& lt, gcs_scan_out
   out->stage_ms[6] = ms_between(st.T2, Tq);     // of [2]: tail numerics up to the pushforward launch
   out->stage_ms[7] = ms_between(Tq, Tr);        // of [2]: pushforward launch calls
   for (int k = 0; k < 8; ++k) c->host_sums[k] += out->stage_ms[k];
+  float* hh = c->host_hist.data() + (size_t)(c->host_n[0] % gcs_ctx::kHostHist) * 6;
+  for (int k = 0; k < 4; ++k) hh[k] = (float)out->stage_ms[k];
+  hh[4] = hh[5] = 0.0f;
   ++c->host_n[0];
   return GCS_OK;
 }
@@ -2999,6 +3018,11 @@ int gcs_scan_combine(gcs_ctx* c, const gcs_scan_inputs* in, gcs_scan_outputs* ou
   c->host_sums[8] += cm;
   c->host_sums[9] += ms_between(tc, t1);
   ++c->host_n[1];
+  if (c->host_n[0] > 0) {
+    float* hh = c->host_hist.data() + (size_t)((c->host_n[0] - 1) % gcs_ctx::kHostHist) * 6;
+    hh[4] = (float)cm;
+    hh[5] = (float)ms_between(tc, t1);
+  }
   return rc;
 }
 

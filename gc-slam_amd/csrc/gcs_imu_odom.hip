@@ -27,6 +27,7 @@ namespace {
 constexpr int kIoThreads = preint::kPreintThreads;  // 512
 constexpr int kIoWaves = kIoThreads / 64;
 static_assert(kImuOdomMaxM <= 2 * kIoThreads, "the sorts hold two keys per lane");
+static_assert(kIoThreads == 512, "io_sort's network: 1,024 positions");
 
 // block reductions in a fixed order: a xor tree per wave, then the waves in order (every lane gets it)
 __device__ __forceinline__ double io_block_sum(double v, double* s) {
@@ -53,21 +54,43 @@ __device__ __forceinline__ double io_block_min(double v, double* s) {
 }
 __device__ __forceinline__ double io_block_max(double v, double* s) { return -io_block_min(-v, s); }
 
-// ascending bitonic sort of n (a power of two, <= 2 kIoThreads) keys in LDS
-__device__ void io_sort(double* k, int n) {
-  for (int size = 2; size <= n; size <<= 1)
+// ascending bitonic sort of the 2 kIoThreads keys in k (LDS; pad with +inf): lane t holds positions 2t and
+// 2t + 1, so a stride-1 exchange stays in the lane, strides 2-64 are shuffles inside the wave (a wave holds
+// 128 consecutive positions) and only the six stages with strides of 128-512 go through LDS
+constexpr int kIoKeys = 2 * kIoThreads;
+__device__ void io_sort(double* k) {
+  const int t = (int)threadIdx.x;
+  __syncthreads();
+  double v[2] = {k[2 * t], k[2 * t + 1]};
+  for (int size = 2; size <= kIoKeys; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      __syncthreads();
-      for (int i = threadIdx.x; i < n / 2; i += kIoThreads) {
-        const int lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-        const bool up = (lo & size) == 0;
-        const double a = k[lo], b = k[hi];
-        if ((a > b) == up) {
-          k[lo] = b;
-          k[hi] = a;
-        }
+      double o[2];
+      if (stride >= 128) {  // across waves
+        __syncthreads();
+        k[2 * t] = v[0];
+        k[2 * t + 1] = v[1];
+        __syncthreads();
+        o[0] = k[(2 * t) ^ stride];
+        o[1] = k[(2 * t + 1) ^ stride];
+      } else if (stride == 1) {
+        o[0] = v[1];
+        o[1] = v[0];
+      } else {
+        o[0] = __shfl_xor(v[0], stride >> 1, 64);
+        o[1] = __shfl_xor(v[1], stride >> 1, 64);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int p = 2 * t + j;
+        const bool up = (p & size) == 0, low = (p & stride) == 0;
+        // the lower position of an ascending pair keeps the smaller key, and so on
+        const bool keep_small = low == up;
+        v[j] = keep_small ? (o[j] < v[j] ? o[j] : v[j]) : (o[j] > v[j] ? o[j] : v[j]);
       }
     }
+  __syncthreads();
+  k[2 * t] = v[0];
+  k[2 * t + 1] = v[1];
   __syncthreads();
 }
 
@@ -142,10 +165,15 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
     }
     n_in = base;
   }
-  int np = 2;
-  while (np < n_in) np <<= 1;
-  for (int i = n_in + tid; i < np; i += kIoThreads) s_key[i] = INFINITY;
-  io_sort(s_key, np);
+  // IMU stamps arrive in order: the sort runs only when a pair of the in-window stamps is not (the
+  // reference sorts unconditionally; the sorted keys are the same)
+  bool unsorted = false;
+  __syncthreads();
+  for (int i = 1 + tid; i < n_in; i += kIoThreads) unsorted = unsorted || s_key[i] < s_key[i - 1];
+  if (__syncthreads_or(unsorted)) {
+    for (int i = n_in + tid; i < kIoKeys; i += kIoThreads) s_key[i] = INFINITY;
+    io_sort(s_key);
+  }
   double gaps = 0.0;
   for (int i = 1 + tid; i < n_in; i += kIoThreads) {
     const double g = s_key[i] - s_key[i - 1];
@@ -185,15 +213,13 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
     const double ex = df[0] + c[0], ey = df[1] + c[1], ez = df[2] + c[2];
     s_e[i] = sqrt(ex * ex + ey * ey + ez * ez);
   }
-  int mp = 2;
-  while (mp < m) mp <<= 1;
   __syncthreads();
-  for (int i = tid; i < mp; i += kIoThreads) s_key[i] = i < m ? s_e[i] : INFINITY;
-  io_sort(s_key, mp);
+  for (int i = tid; i < kIoKeys; i += kIoThreads) s_key[i] = i < m ? s_e[i] : INFINITY;
+  io_sort(s_key);
   const double med = io_median(s_key, m);
   __syncthreads();
-  for (int i = tid; i < mp; i += kIoThreads) s_key[i] = i < m ? fabs(s_e[i] - med) : INFINITY;
-  io_sort(s_key, mp);
+  for (int i = tid; i < kIoKeys; i += kIoThreads) s_key[i] = i < m ? fabs(s_e[i] - med) : INFINITY;
+  io_sort(s_key);
   host::ImuVmfStats v{};
   v.sigma = io_median(s_key, m) / 0.6745 + kEpsMass;
   double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // rel, w, w_int, S[3]
@@ -213,19 +239,46 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
   v.ess_w = io_block_sum(acc[1], s_red);
   v.ess_raw = io_block_sum(acc[2], s_red);
   for (int k = 0; k < 3; ++k) v.S[k] = io_block_sum(acc[3 + k], s_red);
-  // ---- lane 0: the eleven factors and their sum (the host branch's code), into device memory
+  // ---- the statistics for the assembly kernel (one wave, its registers free of this kernel's sorts)
+  if (tid == 0) {
+    double* st = a.out + kIoOutWords;
+    st[0] = v.S[0]; st[1] = v.S[1]; st[2] = v.S[2];
+    st[3] = v.ess_w; st[4] = v.ess_raw; st[5] = v.rel_sum; st[6] = v.sigma;
+    st[7] = dt_imu; st[8] = dt_int; st[9] = om[0]; st[10] = om[1]; st[11] = om[2];
+    for (int k = 0; k < 9; ++k) st[12 + k] = s_pre[k];
+  }
+}
+
+// lane 0: the eleven factors and their sum (the host branch's code) into device memory; then the wave
+// copies the record to the pinned host record, stamped
+__global__ __launch_bounds__(64) void k_imu_odom_assemble(ImuOdomDevArgs a) {
+  const int tid = (int)threadIdx.x;
+  const int m = a.m;
+  const double* stamps = a.win;
+  const double* gyro = a.win + m;
+  const double* accel = a.win + 4 * m;
+  const double* w_int = a.win + 7 * m;
+  const double* sm = a.win + 8 * m;
+  const double* mu_inc = sm + kIoMuInc;
   host::ImuOdomOut* out = reinterpret_cast<host::ImuOdomOut*>(a.out);
   double* extra = a.out + kIoOutWords - 5;
+  const double* st = a.out + kIoOutWords;
   if (tid == 0) {
+    host::ImuVmfStats v{};
+    v.S[0] = st[0]; v.S[1] = st[1]; v.S[2] = st[2];
+    v.ess_w = st[3]; v.ess_raw = st[4]; v.rel_sum = st[5]; v.sigma = st[6];
+    const double dt_imu = st[7], dt_int = st[8];
+    double om[3] = {st[9], st[10], st[11]}, pre[9];
+    for (int k = 0; k < 9; ++k) pre[k] = st[12 + k];
     host::ImuOdomInputs in{};
     in.m = m;
     in.stamps = stamps; in.gyro = gyro; in.accel = accel; in.w_int = w_int;
     in.dt_imu = dt_imu; in.dt_int = dt_int; in.dt_sec = a.dt_sec;
     in.omega_avg = om;
-    in.dp_int = s_pre; in.drot_int = s_pre + 3; in.dv_int = s_pre + 6;
-    in.pose0 = pose0; in.pose_pred = sm + kIoPosePred; in.mu_prev = sm + kIoMuPrev; in.mu_inc = mu_inc;
-    in.accel_bias = ab;
-    in.gravity = grav;
+    in.dp_int = pre; in.drot_int = pre + 3; in.dv_int = pre + 6;
+    in.pose0 = sm + kIoPose0; in.pose_pred = sm + kIoPosePred; in.mu_prev = sm + kIoMuPrev; in.mu_inc = mu_inc;
+    in.accel_bias = mu_inc + 12;
+    in.gravity = sm + kIoGravity;
     in.Sigma_g = sm + kIoSigmaG; in.Sigma_a = sm + kIoSigmaA;
     in.odom_pose = sm + kIoOdomPose; in.odom_cov = sm + kIoOdomCov; in.odom_twist = sm + kIoOdomTwist;
     in.odom_twist_cov = sm + kIoOdomTwistCov;
@@ -239,22 +292,18 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
   uint64_t* hw = reinterpret_cast<uint64_t*>(a.host);
   const uint64_t* dw = reinterpret_cast<const uint64_t*>(a.out);
   unsigned long long h = 0;
-  for (int i = tid; i < kIoOutWords; i += kIoThreads) {
+  for (int i = tid; i < kIoOutWords; i += 64) {
     const uint64_t w = dw[i];
     hw[i] = w;
     h += mirror_word_hash(w, (uint32_t)i);
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) h += __shfl_xor(h, o, 64);
-  __shared__ unsigned long long s_h[kIoWaves];
-  if (lane == 0) s_h[wid] = h;
   __threadfence_system();
-  __syncthreads();
   if (tid == 0) {
     const uint64_t seq = *a.dseq + 1u;
     *a.dseq = seq;
-    uint64_t sum = mirror_word_hash(seq, (uint32_t)kIoOutWords);
-    for (int w = 0; w < kIoWaves; ++w) sum += s_h[w];
+    const uint64_t sum = mirror_word_hash(seq, (uint32_t)kIoOutWords) + h;
     hw[kIoOutWords + 1] = sum;
     hw[kIoOutWords] = seq;
   }
@@ -265,6 +314,7 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
 hipError_t launch_imu_odom(const ImuOdomDevArgs& a, hipStream_t s) {
   if (a.m < 2 || a.m > kImuOdomMaxM) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_imu_odom, dim3(1), dim3(kIoThreads), 0, s, a);
+  hipLaunchKernelGGL(k_imu_odom_assemble, dim3(1), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -48,8 +48,8 @@ GCS_HD double ev_quad3(const double* A, const double* x) {
 // PSD-project a 3x3 covariance, then its lifted Cholesky inverse (lift_strength = eps_lift * 3)
 GCS_HD void ev_info_from_cov3(const double* S, double* L3) {
   double Sp[9];
-  small::psd_project(3, S, kEpsPsd, Sp);
-  small::spd_inverse_lifted(3, Sp, kEpsLift, L3);
+  small::psd_project<3>(S, kEpsPsd, Sp);
+  small::spd_inverse_lifted<3>(Sp, kEpsLift, L3);
 }
 
 // kappa_from_resultant_v2 / _kappa_continuous_formula, FS/backend/operators/kappa.py:84-127,172-234
@@ -86,8 +86,8 @@ GCS_HD void imu_odom_assemble(const ImuOdomInputs& in, const ImuVmfStats& v, Imu
     small::se3_compose(inv_pred, in.odom_pose, Terr);  // se3_relative(odom, pred) = pred^-1 o odom
     se3_log_hd(Terr, xi_od);
     double cp[36];
-    small::psd_project(6, in.odom_cov, kEpsPsd, cp);
-    small::spd_inverse_lifted(6, cp, kEpsLift, Lod);
+    small::psd_project<6>(in.odom_cov, kEpsPsd, cp);
+    small::spd_inverse_lifted<6>(cp, kEpsLift, Lod);
     for (int i = 0; i < 6; ++i) {
       double s = 0.0;
       for (int j = 0; j < 6; ++j) s += Lod[6 * i + j] * xi_od[j];
@@ -126,7 +126,7 @@ GCS_HD void imu_odom_assemble(const ImuOdomInputs& in, const ImuVmfStats& v, Imu
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) Hs[3 * i + j] = 0.5 * (H[3 * i + j] + H[3 * j + i]);
     double c6[6];
-    small::psd_project(3, Hs, kEpsPsd, Himu, c6);
+    small::psd_project<3>(Hs, kEpsPsd, Himu, c6);
     const double mean_rel = rel_sum / m;
     out.imu.ess = ess_w;
     out.imu.support = mean_rel;

@@ -203,7 +203,9 @@ hipError_t launch_preint(const PreintArgs& a, hipStream_t s);
 // kImuOdomMaxM samples.  win (device): stamps[m], gyro[3m], accel[3m], w_int[m], then the small inputs at
 // the ImuOdomSmall offsets; out (device): host::ImuOdomOut + [dt_int, dt_imu, omega_avg 3] (kIoOutWords
 // words); host (pinned, mapped; may be null): out's words, the call's sequence number, a checksum
+// ... and past those words, kImuOdomStatWords of the window statistics the assembly kernel reads
 constexpr int kImuOdomMaxM = 1024;
+constexpr int kImuOdomStatWords = 24;
 enum ImuOdomSmall : int {
   kIoPose0 = 0, kIoPosePred = 6, kIoMuPrev = 12, kIoMuInc = 34, kIoGravity = 56, kIoSigmaG = 59, kIoSigmaA = 68,
   kIoOdomPose = 77, kIoOdomCov = 83, kIoOdomTwist = 119, kIoOdomTwistCov = 125, kIoSmallLen = 161

@@ -1543,9 +1543,10 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_apply_blocks(PmStore st,
 // Each mark is read by one lane, which clears it: the marks are all zero again for the next call
 // (zeroed once at allocation; no per-call fill).
 // ticket (may be null): the last block to finish publishes the nb counters to dst (the mapped buffer)
-// and re-arms them and the ticket -- the counts are device-scope atomics drained (vmcnt) before each
-// block's relaxed ticket add and read back as agent-scope atomic loads (no release fence, no L2
-// write-back); this was a launch of its own (k_pm_publish_u32, ~5 us of step 12b)
+// and re-arms them and the ticket -- each block's count add happens before its ticket add, which is a
+// release at agent scope (one lane per block), and the last block acquires at agent scope before it
+// reads the counts back as agent-scope atomic loads; this was a launch of its own (k_pm_publish_u32,
+// ~5 us of step 12b)
 __global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(uint8_t* mark, int M, uint32_t* cnt,
                                                                       uint32_t* ticket, int nb, uint32_t* dst) {
   __shared__ double lds[kPmThreads / 64];
@@ -1561,13 +1562,12 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_count_marks_blocks(uint8_t* m
   if (threadIdx.x == 0 && c > 0.0) atomicAdd(cnt + b, (uint32_t)c);
   if (!ticket) return;
   if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned tk = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     s_last = tk == gridDim.x * gridDim.y - 1u ? 1 : 0;
   }
   __syncthreads();
   if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   for (int i = threadIdx.x; i < nb; i += kPmThreads) {
     dst[i] = __hip_atomic_load(cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(cnt + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -12,8 +12,13 @@ namespace small {
 
 constexpr int kN = 6;
 
+// Each routine takes its size as a template argument NC when it is known at the call (the loops then unroll
+// and the device keeps the arrays in registers), or NC = 0 and the run-time n (the zero-row split below).
+
 // cyclic Jacobi, row-major n x n; w unsorted, V columns (gcs_host.cpp jacobi_eigh)
-GCS_HD void jacobi_eigh(int n, const double* A, double* w, double* V) {
+template <int NC>
+GCS_HD void jacobi_eigh(int n_rt, const double* A, double* w, double* V) {
+  const int n = NC ? NC : n_rt;
   double a[kN * kN];
   for (int i = 0; i < n * n; ++i) a[i] = A[i];
   for (int i = 0; i < n * n; ++i) V[i] = 0.0;
@@ -61,7 +66,9 @@ GCS_HD void jacobi_eigh(int n, const double* A, double* w, double* V) {
 
 // right-looking Cholesky of A (row-major lower factor Lc, reciprocal diagonals rd): the operation order
 // of gcs_host.cpp cholesky_n<N>; false when a pivot is not positive
-GCS_HD bool cholesky(int n, const double* A, double* Lc, double* rd) {
+template <int NC>
+GCS_HD bool cholesky(int n_rt, const double* A, double* Lc, double* rd) {
+  const int n = NC ? NC : n_rt;
   double W[kN * kN], col[kN];
   for (int i = 0; i < n * n; ++i) W[i] = A[i];
   for (int j = 0; j < n; ++j) {
@@ -83,11 +90,13 @@ GCS_HD bool cholesky(int n, const double* A, double* Lc, double* rd) {
 
 // (L + eps_lift I)^{-1} through its Cholesky factor (gcs_host.cpp spd_factor_lifted + factor_inverse_n);
 // a matrix not positive definite even lifted gives NaN, which the callers' finiteness checks report
-GCS_HD void spd_inverse_lifted(int n, const double* L, double eps_lift, double* Linv) {
+template <int NC>
+GCS_HD void spd_inverse_lifted(const double* L, double eps_lift, double* Linv) {
+  constexpr int n = NC;
   double A[kN * kN], Lc[kN * kN], rd[kN];
   for (int i = 0; i < n * n; ++i) A[i] = L[i];
   for (int i = 0; i < n; ++i) A[i * n + i] += eps_lift;
-  if (!cholesky(n, A, Lc, rd))
+  if (!cholesky<NC>(n, A, Lc, rd))
     for (int i = 0; i < n; ++i) rd[i] = NAN;
   double X[kN * kN], R[kN * kN];
   for (int i = 0; i < n; ++i) {
@@ -115,7 +124,9 @@ GCS_HD void spd_inverse_lifted(int n, const double* L, double eps_lift, double* 
 // domain_projection_psd_core (primitives.py:80-123) with the host's declared fast paths (DESIGN.md
 // section 3 item 5): exactly-zero rows split off, and sym(M) returned when sym(M) - eps I has a
 // Cholesky factor; cert6 (the certificate form) always takes the eigen-decomposition.
-GCS_HD double psd_project(int n, const double* M, double eps_psd, double* out, double* cert6 = nullptr) {
+template <int NC>
+GCS_HD double psd_project(const double* M, double eps_psd, double* out, double* cert6 = nullptr) {
+  constexpr int n = NC;
   double s[kN * kN];
   double sym2 = 0.0;
   for (int i = 0; i < n; ++i)
@@ -145,10 +156,10 @@ GCS_HD double psd_project(int n, const double* M, double eps_psd, double* out, d
         double da = 0.0;
         for (int i = 0; i < na * na; ++i) A[i] = sub[i];
         for (int i = 0; i < na; ++i) A[i * na + i] -= eps_psd;
-        if (cholesky(na, A, Lc, rd)) {
+        if (cholesky<0>(na, A, Lc, rd)) {
           for (int i = 0; i < na * na; ++i) so[i] = sub[i];
         } else {
-          jacobi_eigh(na, sub, w, V);
+          jacobi_eigh<0>(na, sub, w, V);
           for (int k = 0; k < na; ++k) w[k] = w[k] > eps_psd ? w[k] : eps_psd;
           double dd2 = 0.0;
           for (int i = 0; i < na; ++i)
@@ -170,7 +181,7 @@ GCS_HD double psd_project(int n, const double* M, double eps_psd, double* out, d
     double A[kN * kN], Lc[kN * kN], rd[kN];
     for (int i = 0; i < n * n; ++i) A[i] = s[i];
     for (int i = 0; i < n; ++i) A[i * n + i] -= eps_psd;
-    if (cholesky(n, A, Lc, rd)) {
+    if (cholesky<NC>(n, A, Lc, rd)) {
       for (int i = 0; i < n * n; ++i) out[i] = s[i];
       return 0.0;
     }
@@ -181,7 +192,7 @@ GCS_HD double psd_project(int n, const double* M, double eps_psd, double* out, d
     for (int i = 0; i < n * n; ++i) V[i] = (i % (n + 1) == 0) ? 1.0 : 0.0;
     for (int i = 0; i < n; ++i) w[i] = 0.0;
   } else {
-    jacobi_eigh(n, s, w, V);
+    jacobi_eigh<NC>(n, s, w, V);
   }
   double emin = INFINITY, emax = -INFINITY, nn = 0.0;
   for (int k = 0; k < n; ++k) {

@@ -252,6 +252,7 @@ _SIGS = [
     ("gcs_ctx_stage_times", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int32]),
     ("gcs_ctx_host_split", C.c_int, [C.c_void_p, c_double_p, c_int64_p, C.c_int32]),
     ("gcs_ctx_worker_tid", C.c_int64, [C.c_void_p]),
+    ("gcs_ctx_host_split_history", C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.c_int32, C.POINTER(C.c_int32)]),
     ("gcs_ctx_set_atlas", C.c_int, [C.c_void_p, c_double_p]),
     ("gcs_ctx_get_atlas", C.c_int, [C.c_void_p, c_double_p, c_int32_p]),
     ("gcs_ctx_set_belief", C.c_int, [C.c_void_p, C.POINTER(GcsBelief)]),
@@ -379,7 +380,8 @@ SYMBOLS = [s[0] for s in _SIGS]
 _lib = None
 
 
-_AB_OPTIONAL = ("gcs_ctx_host_split", "gcs_ctx_worker_tid")  # (round 6 diagnostics)
+_AB_OPTIONAL = ("gcs_ctx_host_split", "gcs_ctx_worker_tid", "gcs_imu_odom_evidence_device",
+                "gcs_ctx_host_split_history")  # (round 6 entries)
 
 
 def load():

@@ -198,6 +198,19 @@ class HypothesisContext:
                   "host_split")
         return dict(zip(self.HOST_SPLIT, ms.tolist())), (int(n[0]), int(n[1]))
 
+    HOST_HIST = ("pre_device", "device_wait", "tail", "gcs_scan", "combine", "scan_combine_call")
+
+    def host_split_history(self, n_max=4096):
+        """gcs_ctx_host_split_history: the per-scan host split of the latest scans since the last reset
+        (oldest first), an (n, 6) float32 array with columns HOST_HIST (ms); None from an older build."""
+        if not hasattr(self.lib, "gcs_ctx_host_split_history"):
+            return None
+        out = np.zeros((int(n_max), 6), np.float32)
+        n = C.c_int32(0)
+        self._chk(self.lib.gcs_ctx_host_split_history(self.h, out.ctypes.data_as(C.POINTER(C.c_float)), int(n_max),
+                                                      C.byref(n)), "host_split_history")
+        return out[:n.value]
+
     def worker_tid(self):
         """gcs_ctx_worker_tid: the OS thread id of the context's launch worker (0: not started)."""
         return int(self.lib.gcs_ctx_worker_tid(self.h)) if hasattr(self.lib, "gcs_ctx_worker_tid") else 0

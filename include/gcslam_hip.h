@@ -269,6 +269,11 @@ int gcs_ctx_stage_times(gcs_ctx* ctx, double* ms_sum /*GCS_N_STAGES*/, int64_t* 
  * gcs_scan_combine's whole call; *n the scans counted (n_combine[0]: the combines).  Accumulated in the
  * library on every scan, so a caller's timed region decomposes exactly, with no per-scan reads. */
 int gcs_ctx_host_split(gcs_ctx* ctx, double* ms_sum /*10*/, int64_t* n /*2*/, int32_t reset);
+/* The same split per scan, for its distribution (p50 / p90 / max, slow scans): the latest
+ * min(n_max, scans since the reset, 4096) scans, oldest first, 6 floats each -- [pre-device, device
+ * submit + wait, tail, whole gcs_scan, combine, whole gcs_scan_combine call] in ms (the last two 0 for
+ * a scan not run by gcs_scan_combine); *n_out the scans written. */
+int gcs_ctx_host_split_history(gcs_ctx* ctx, float* out /*n_max*6*/, int32_t n_max, int32_t* n_out);
 /* The OS thread id of the context's launch worker (0 before its first job): a caller that pins its
  * own thread can keep the worker off that core (bench.py). */
 int64_t gcs_ctx_worker_tid(gcs_ctx* ctx);

@@ -77,6 +77,9 @@ def _shrink(out):
         if v.size > (1 << 16):
             res[k + "#sha1"] = np.array(hashlib.sha1(v.view(np.uint8)).hexdigest())
             res[k + "#sample"] = v.reshape(-1)[::61].copy()
+            if v.ndim == 2 and v.shape[0] <= 32:  # field-major (F, B): a hash per field row
+                for f in range(v.shape[0]):
+                    res[f"{k}#f{f:02d}"] = np.array(hashlib.sha1(np.ascontiguousarray(v[f]).view(np.uint8)).hexdigest())
         else:
             res[k] = v
     return res

@@ -16,6 +16,7 @@
 #   assocsq / assocpmc   SQ passes / FETCH, WRITE, L2 hit and TCP passes of the association kernels
 #   ab           same-box A/B of two builds: A = libgcslam_hip.so, B = libgcslam_hip_$B.so
 #   envab        same-box A/B of an environment knob: B runs with $ENVB
+#   io / ioprof  IMU / odometry branch timing, host vs device (tools/io_bench.py) / its rocprofv3 kernel stats
 #   graphab      hipGraph vs stream launches of a six-kernel chain (tools/graph_ab, built in-tree)
 #   gaps         device idle gaps per kernel from prof2's trace (tools/trace_gaps.py)
 #   sweep        bench C2 + C3 per entry of SWEEP="name:lib_suffix:ENV=V,... ..." (library variants / knobs)
@@ -30,9 +31,12 @@ step() {
   case "$1" in
     tests)
       local k=(); [ -n "$PYTEST_K" ] && k=(-k "$PYTEST_K")
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rA --timeout 120 --timeout-method thread "${k[@]}" \
+      timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail="${MAXFAIL:-8}" -v -rA --timeout 120 --timeout-method thread "${k[@]}" \
         > "$O/pytest_gpu.log" 2>&1 ;;
     smoke) timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    snapprev)  # the same snapshot with the A/B library (libgcslam_hip_$B.so)
+      GCSLAM_LIB=$PWD/gc-slam_amd/gcslam/libgcslam_hip_${B:-prev}.so timeout -k 10 300 python -u tools/bitwise_snapshot.py \
+        save "$O/snap_prev.npz" > "$O/snap_prev.log" 2>&1 ;;
     snap)  # bitwise snapshot of the bin path (tools/bitwise_snapshot.py), compared with $SNAP_BASE if set
       timeout -k 10 300 python -u tools/bitwise_snapshot.py save "$O/snap.npz" > "$O/snap.log" 2>&1 || return $?
       [ -n "$SNAP_BASE" ] && python tools/bitwise_snapshot.py compare "$SNAP_BASE" "$O/snap.npz" > "$O/snap_cmp.txt" 2>&1
@@ -112,6 +116,9 @@ step() {
           env $e timeout -k 10 300 python bench.py --config $cfg --steps ${SWEEP_STEPS:-60} --warmup 5 --no-cpu-baseline --no-c3 --no-live > "$O/sweep_${name}_$cfg.log" 2>&1 || return $?
         done
       done ;;
+    io) timeout -k 10 120 python tools/io_bench.py > "$O/io_bench.txt" 2>&1 ;;
+    ioprof) timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$O/io_prof" -o run --output-format csv -- \
+              python3 tools/io_bench.py 100 > "$O/io_prof.log" 2>&1 ;;
     graphab) timeout -k 10 120 ./tools/graph_ab 2000 > "$O/graph_ab.json" 2>&1 ;;
     gaps)  # device idle gaps of the C2 step, from prof2's kernel trace
       local tr; tr=$(find "$O/prof_c2" -name '*kernel_trace.csv' | head -1)
