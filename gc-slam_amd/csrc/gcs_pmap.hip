@@ -1197,17 +1197,19 @@ __global__ __launch_bounds__(kPmThreads) void k_pm_fuse_keys_blocks(PmStore st, 
   vals[g] = (uint32_t)g;
 }
 
-// The fuse's (key, row) sort for up to kSsMax rows in two launches (GCS_FUSE_SMALLSORT; rocPRIM's radix
-// sort took five launches at these sizes -- a block sort and four merge passes, ~33 us plus their host
-// dispatch).  Each pair is one u64 (key << 32 | row), so the pairs are distinct and their order is the
-// stable key order.  k_ss_block: 1,024-pair runs sorted in LDS (bitonic); k_ss_merge: every pair's
+// The fuse's (key, row) sort for up to kSsWideMax rows in two launches (GCS_FUSE_SMALLSORT; rocPRIM's
+// radix sort took five launches at these sizes -- a block sort and four merge passes, ~33 us plus their
+// host dispatch).  Each pair is one u64 (key << 32 | row), so the pairs are distinct and their order is
+// the stable key order.  k_ss_block: 1,024-pair runs sorted in LDS (bitonic); k_ss_merge: every pair's
 // final position = its rank in its run + the pairs below it in every other run (a binary search of each
-// run, all runs staged in LDS), then the scatter.
+// run, the runs staged in LDS sixteen at a time: one group up to kSsMax rows -- the reference's 1,536 x 8
+// fuse rows --, four groups up to kSsWideMax), then the scatter.
 #ifndef GCS_FUSE_SMALLSORT
 #define GCS_FUSE_SMALLSORT 1
 #endif
 constexpr int kSsRun = 1024;
-constexpr int kSsMax = 16 * kSsRun;  // 128 KB of runs in k_ss_merge's LDS
+constexpr int kSsMax = 16 * kSsRun;  // 128 KB of runs in k_ss_merge's LDS: one group
+constexpr int kSsWideMax = 4 * kSsMax;  // 65,536 rows: four groups
 __global__ __launch_bounds__(512) void k_ss_block(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                  int n, uint64_t* __restrict__ runs) {
   __shared__ uint64_t s[kSsRun];
@@ -1237,35 +1239,38 @@ __global__ __launch_bounds__(512) void k_ss_block(const uint32_t* __restrict__ k
 }
 __global__ __launch_bounds__(kSsRun) void k_ss_merge(const uint64_t* __restrict__ runs, int n, int nrun,
                                                      uint32_t* __restrict__ keys_s, uint32_t* __restrict__ vals_s) {
+  constexpr int kG = kSsMax / kSsRun;  // runs per LDS group
   __shared__ uint64_t s[kSsMax];
   const int t = threadIdx.x;
-  {  // every run's loads in flight before the LDS stores (one round trip, not one per run)
-    uint64_t v[kSsMax / kSsRun];
-#pragma unroll
-    for (int i = 0; i < kSsMax / kSsRun; ++i) v[i] = i < nrun ? runs[i * kSsRun + t] : 0ull;
-#pragma unroll
-    for (int i = 0; i < kSsMax / kSsRun; ++i)
-      if (i < nrun) s[i * kSsRun + t] = v[i];
-  }
-  __syncthreads();
   const int g = blockIdx.x * kSsRun + t;
-  if (g >= nrun * kSsRun) return;
-  const uint64_t x = s[g];
+  const int j = blockIdx.x;  // this block's run
+  const uint64_t x = runs[g];  // (the grid is nrun blocks: g < nrun kSsRun)
+  int pos = t;
+  for (int r0 = 0; r0 < nrun; r0 += kG) {
+    if (r0 > 0) __syncthreads();  // the previous group's searches are done with s
+    {  // every run's loads in flight before the LDS stores (one round trip, not one per run)
+      uint64_t v[kG];
+#pragma unroll
+      for (int i = 0; i < kG; ++i) v[i] = r0 + i < nrun ? runs[(r0 + i) * kSsRun + t] : 0ull;
+#pragma unroll
+      for (int i = 0; i < kG; ++i)
+        if (r0 + i < nrun) s[i * kSsRun + t] = v[i];
+    }
+    __syncthreads();
+    // the pairs of every other run below x: fixed-step lower bounds, the runs' searches side by side
+    int lo[kG];
+#pragma unroll
+    for (int i = 0; i < kG; ++i) lo[i] = 0;
+#pragma unroll
+    for (int step = kSsRun / 2; step >= 1; step >>= 1)
+#pragma unroll
+      for (int i = 0; i < kG; ++i)
+        if (r0 + i < nrun && s[i * kSsRun + lo[i] + step - 1] < x) lo[i] += step;
+#pragma unroll
+    for (int i = 0; i < kG; ++i)
+      if (r0 + i < nrun && r0 + i != j) pos += lo[i] + (lo[i] == kSsRun - 1 && s[i * kSsRun + kSsRun - 1] < x ? 1 : 0);
+  }
   if (x == ~0ull) return;  // padding (after every real pair of the last run)
-  const int j = g / kSsRun;
-  int pos = g - j * kSsRun;
-  // the pairs of every other run below x: fixed-step lower bounds, the runs' searches side by side
-  int lo[kSsMax / kSsRun];
-#pragma unroll
-  for (int i = 0; i < kSsMax / kSsRun; ++i) lo[i] = 0;
-#pragma unroll
-  for (int step = kSsRun / 2; step >= 1; step >>= 1)
-#pragma unroll
-    for (int i = 0; i < kSsMax / kSsRun; ++i)
-      if (i < nrun && s[i * kSsRun + lo[i] + step - 1] < x) lo[i] += step;
-#pragma unroll
-  for (int i = 0; i < kSsMax / kSsRun; ++i)
-    if (i < nrun && i != j) pos += lo[i] + (lo[i] == kSsRun - 1 && s[i * kSsRun + kSsRun - 1] < x ? 1 : 0);
   keys_s[pos] = (uint32_t)(x >> 32);
   vals_s[pos] = (uint32_t)x;
 }
@@ -2647,7 +2652,8 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
     PMCHK(p, hipMalloc(&p->fv_s, cap * 4));
     size_t tb = 0;
     PMCHK(p, rocprim::radix_sort_pairs(nullptr, tb, p->fk, p->fk_s, p->fv, p->fv_s, (unsigned)cap, 0u, 32u, p->stream));
-    p->ftemp_bytes = std::max<size_t>(tb, (size_t)kSsMax * 8);  // (also k_ss_block's runs)
+    // (also k_ss_block's runs: up to kSsWideMax rows)
+    p->ftemp_bytes = std::max<size_t>(tb, (size_t)std::min(((cap + kSsRun - 1) / kSsRun) * kSsRun, kSsWideMax) * 8);
     PMCHK(p, hipMalloc(&p->ftemp, p->ftemp_bytes));
     p->frows = cap;
   }
@@ -2682,7 +2688,7 @@ int fuse_blocks(gcs_pmap* p, int32_t n, const gcs_pmap_rows* rows, int nb, int r
     const char* e = getenv("GCSLAM_FUSE_SMALLSORT");
     return GCS_FUSE_SMALLSORT && !(e && e[0] == '0');
   }();
-  if (small_sort && R <= kSsMax && p->ftemp_bytes >= (size_t)kSsMax * 8) {
+  if (small_sort && R <= kSsWideMax && p->ftemp_bytes >= (size_t)((R + kSsRun - 1) / kSsRun) * kSsRun * 8) {
     const int nrun = (R + kSsRun - 1) / kSsRun;
     hipLaunchKernelGGL(k_ss_block, dim3(nrun), dim3(512), 0, p->stream, (const uint32_t*)p->fk, (const uint32_t*)p->fv, R,
                        (uint64_t*)p->ftemp);

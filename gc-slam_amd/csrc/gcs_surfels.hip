@@ -457,22 +457,25 @@ __global__ __launch_bounds__(kSfThreads) void k_sf_write(const double* __restric
 // One workgroup for clouds of up to kSortMax points: the stable sort of k_sf_keys' (key, point index)
 // pairs by key and k_sf_bounds' run bounds, in LDS (replaces the rocPRIM radix sort's kernels and
 // k_sf_bounds: the same permutation, as both sorts are stable on the key with the points in index
-// order).  Each key is packed above its 13-bit index and sorted by LSD passes of 7-bit digits: per
-// wave a contiguous 512-entry segment in 64-lane steps, equal digits found by ballots, ranks from
-// per-(wave, digit) offsets (digit-major, then wave order).
+// order).  Each key is packed above its IDXB-bit index and sorted by LSD passes of 7-bit digits: per
+// wave a contiguous segment in 64-lane steps, equal digits found by ballots, ranks from per-(wave,
+// digit) offsets (digit-major, then wave order).  IDXB 13: up to 8,192 points (the reference's
+// N_POINTS_CAP; 64 KB of LDS); IDXB 14: up to 16,384 (twice it; 128 KB of the CU's 160 KB).
 constexpr int kSortThreads = 1024;
-constexpr int kSortMax = 8192;
 constexpr int kSortIdxBits = 13;
+constexpr int kSortMax = 1 << kSortIdxBits;
+constexpr int kSortMaxWide = 2 * kSortMax;
 constexpr int kSortDigitBits = 7;
 constexpr int kSortDigits = 1 << kSortDigitBits;
 constexpr int kSortWaves = kSortThreads / 64;
-constexpr int kSortSeg = kSortMax / kSortWaves;  // entries per wave
-static_assert(kSortMax == 1 << kSortIdxBits, "index field");
-static_assert(kSortThreads <= 1024 && kSortSeg % 64 == 0, "sort shape");
 
+template <int IDXB>
 __global__ __launch_bounds__(kSortThreads) void k_sf_sort_lds(const uint32_t* __restrict__ keys, int n, SfParams a,
                                                                int end_bit, uint32_t* __restrict__ vals_s,
                                                                int32_t* __restrict__ run) {
+  constexpr int kSortMax = 1 << IDXB, kSortIdxBits = IDXB;
+  constexpr int kSortSeg = kSortMax / kSortWaves;  // entries per wave
+  static_assert(kSortThreads <= 1024 && kSortSeg % 64 == 0, "sort shape");
   __shared__ uint32_t s_buf[2][kSortMax];
   __shared__ uint32_t s_off[kSortWaves][kSortDigits];
   __shared__ uint32_t s_tot[kSortDigits], s_dsum[kSortDigits / 64];
@@ -588,7 +591,7 @@ struct gcs_surfel_ctx {
   void* d_temp = nullptr;
   size_t temp_bytes = 0;
   unsigned end_bit = 1;
-  bool lds_sort = true;  // k_sf_keys_sort for clouds of <= kSortMax points (GCSLAM_SF_LDS_SORT=0: rocPRIM)
+  bool lds_sort = true;  // k_sf_sort_lds for clouds of <= kSortMaxWide points (GCSLAM_SF_LDS_SORT=0: rocPRIM)
   bool fold_cells = true;  // k_sf_moments writes the bucket rows (GCSLAM_SF_FOLD_CELLS=0: k_sf_cells)
   int32_t *d_bucket = nullptr, *d_count = nullptr, *d_run = nullptr, *d_slot_cell = nullptr;
   double *d_mom = nullptr, *d_fit = nullptr;
@@ -746,8 +749,11 @@ int surfel_launch(gcs_surfel_ctx* c, const double* points, const double* timesta
   hipLaunchKernelGGL(k_sf_keys, dim3(nblk), dim3(kSfThreads), 0, s, points, n, (const double*)c->d_partials, nblk, a,
                      c->d_keys, c->d_vals, c->d_scal, c->h_scal_dev);
   if (n > 0 && c->lds_sort && n <= kSortMax && c->end_bit + kSortIdxBits <= 32) {
-    hipLaunchKernelGGL(k_sf_sort_lds, dim3(1), dim3(kSortThreads), 0, s, (const uint32_t*)c->d_keys, n, a,
-                       (int)c->end_bit, c->d_vals_s, c->d_run);
+    hipLaunchKernelGGL(k_sf_sort_lds<kSortIdxBits>, dim3(1), dim3(kSortThreads), 0, s, (const uint32_t*)c->d_keys, n,
+                       a, (int)c->end_bit, c->d_vals_s, c->d_run);
+  } else if (n > 0 && c->lds_sort && n <= kSortMaxWide && c->end_bit + kSortIdxBits + 1 <= 32) {
+    hipLaunchKernelGGL(k_sf_sort_lds<kSortIdxBits + 1>, dim3(1), dim3(kSortThreads), 0, s, (const uint32_t*)c->d_keys,
+                       n, a, (int)c->end_bit, c->d_vals_s, c->d_run);
   } else if (n > 0) {
     size_t tb = c->temp_bytes;
     SFCHK(c, rocprim::radix_sort_pairs(c->d_temp, tb, c->d_keys, c->d_keys_s, c->d_vals, c->d_vals_s, (unsigned)n, 0u,

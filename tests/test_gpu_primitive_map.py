@@ -345,6 +345,16 @@ def test_view_sparse_and_empty_tiles():
 @pytest.mark.parametrize("fracs", [(0.999, 0.8, 0.8, 0.8, 0.8, 0.0), (0.01, 0.02, 0.04, 0.05, 0.001, 0.0)],
                          ids=["dense", "sparse"])
 def test_reference_size_view_and_map_update(fracs):
+    _reference_size_update(fracs)
+
+
+def test_twice_reference_rows_map_update():
+    """Step 12b with twice the reference's measurement rows (3,072 x K = 8: 24,576 fuse rows, past the
+    one-group LDS merge's 16,384): the fuse sort's four-group k_ss_merge (no rocPRIM), against the oracle."""
+    _reference_size_update((0.999, 0.8, 0.8, 0.8, 0.8, 0.0), N=3072, seed=51)
+
+
+def _reference_size_update(fracs, N=1536, seed=50):
     """The reference's map sizes (GC_M_TILE = 50,000 slots, GC_M_TILE_VIEW = 1,024, 7 active tiles,
     constants.py:392,436-439; N = 512 + 1,024 measurement rows, K = 8, constants.py:350-356): the view's
     per-tile top-k over 50,000 keys (ties and an empty tile whose keys are all equal included) and
@@ -355,8 +365,8 @@ def test_reference_size_view_and_map_update(fracs):
     from types import SimpleNamespace
     from gcslam import primitive_map as gpm
     from oracle import se3
-    rng = np.random.default_rng(50)
-    m, N, K, kv = 50_000, 1536, 8, 1024
+    rng = np.random.default_rng(seed)
+    m, K, kv = 50_000, 8, 1024
     z = np.array([0.9, -0.4, 0.2, 0.01, -0.02, 0.3])
     R, t = se3.so3_exp(z[3:]), z[:3]
     p_body = rng.uniform(-5, 5, size=(N, 3))
@@ -499,7 +509,8 @@ def test_reference_size_map_update_knob_paths(env):
     here = os.path.dirname(os.path.abspath(__file__))
     root = os.path.dirname(here)
     code = ("import sys; sys.path[:0] = [%r, %r, %r]; import test_gpu_primitive_map as t; "
-            "t.test_reference_size_view_and_map_update((0.999, 0.8, 0.8, 0.8, 0.8, 0.0))"
+            "t.test_reference_size_view_and_map_update((0.999, 0.8, 0.8, 0.8, 0.8, 0.0)); "
+            "t.test_twice_reference_rows_map_update()"
             % (here, root, os.path.join(root, "gc-slam_amd")))
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
                        timeout=110)

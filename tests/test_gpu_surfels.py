@@ -142,12 +142,15 @@ def test_sentinels_empty_input_and_capacity():
 
 
 @pytest.mark.parametrize("n_points,scan,cells", [(8192, 0, (32, 32, 8)), (8192, 5, (32, 32, 8)), (5000, 2, (16, 16, 8)),
-                                                 (300, 1, (64, 64, 16))])
+                                                 (300, 1, (64, 64, 16)), (16384, 0, (32, 32, 8)),
+                                                 (12000, 4, (64, 64, 16))])
 def test_lds_key_sort_equals_radix_sort(monkeypatch, n_points, scan, cells):
-    """k_sf_keys_sort (one workgroup: the centre fold, the cell keys, the stable (key, index) sort in LDS and
-    the run bounds; clouds <= 8,192 points) against the rocPRIM radix-sort path (GCSLAM_SF_LDS_SORT=0): every
-    output and intermediate bitwise equal, parse sentinels included."""
-    sc = synthetic.make_scan(8192, scan)
+    """k_sf_sort_lds (one workgroup: the stable (key, index) sort in LDS and the run bounds; clouds of up to
+    8,192 points with 13-bit indices, up to 16,384 -- twice the reference's N_POINTS_CAP -- with 14-bit
+    indices in 128 KB of LDS) against the rocPRIM radix-sort path (GCSLAM_SF_LDS_SORT=0): every output and
+    intermediate bitwise equal, parse sentinels included."""
+    cap = max(8192, n_points)
+    sc = synthetic.make_scan(cap, scan)
     pts = np.ascontiguousarray(sc["points"][:n_points], np.float64).copy()
     pts[::97] = 1e6                      # masked points: the key past the last cell, sorted last
     t, w = sc["timestamps"][:n_points], sc["weights"][:n_points]
@@ -155,7 +158,7 @@ def test_lds_key_sort_equals_radix_sort(monkeypatch, n_points, scan, cells):
     outs = []
     for flag in ("1", "0"):
         monkeypatch.setenv("GCSLAM_SF_LDS_SORT", flag)
-        ex = SurfelExtractor(cfg, max_points=8192)
+        ex = SurfelExtractor(cfg, max_points=cap)
         try:
             r = ex.extract(pts, t, w, want_intermediates=True)
             outs.append({k: (v.cpu().numpy().copy() if torch.is_tensor(v) else np.asarray(v)) for k, v in r.items()})
