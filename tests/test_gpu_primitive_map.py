@@ -349,12 +349,13 @@ def test_reference_size_view_and_map_update(fracs):
 
 
 def test_twice_reference_rows_map_update():
-    """Step 12b with twice the reference's measurement rows (3,072 x K = 8: 24,576 fuse rows, past the
-    one-group LDS merge's 16,384): the fuse sort's four-group k_ss_merge (no rocPRIM), against the oracle."""
-    _reference_size_update((0.999, 0.8, 0.8, 0.8, 0.8, 0.0), N=3072, seed=51)
+    """Step 12b past the one-group LDS merge's 16,384 fuse rows: 2,048 measurement rows (the map update's
+    limit, kPropLds) x K = 12 candidates = 24,576 rows, twice the reference's 1,536 x 8 -- the fuse sort's
+    multi-group k_ss_merge (no rocPRIM), against the oracle."""
+    _reference_size_update((0.999, 0.8, 0.8, 0.8, 0.8, 0.0), N=2048, K=12, seed=51)
 
 
-def _reference_size_update(fracs, N=1536, seed=50):
+def _reference_size_update(fracs, N=1536, K=8, seed=50):
     """The reference's map sizes (GC_M_TILE = 50,000 slots, GC_M_TILE_VIEW = 1,024, 7 active tiles,
     constants.py:392,436-439; N = 512 + 1,024 measurement rows, K = 8, constants.py:350-356): the view's
     per-tile top-k over 50,000 keys (ties and an empty tile whose keys are all equal included) and
@@ -366,7 +367,7 @@ def _reference_size_update(fracs, N=1536, seed=50):
     from gcslam import primitive_map as gpm
     from oracle import se3
     rng = np.random.default_rng(seed)
-    m, K, kv = 50_000, 8, 1024
+    m, kv = 50_000, 1024
     z = np.array([0.9, -0.4, 0.2, 0.01, -0.02, 0.3])
     R, t = se3.so3_exp(z[3:]), z[:3]
     p_body = rng.uniform(-5, 5, size=(N, 3))
