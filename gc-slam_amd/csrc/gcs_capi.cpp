@@ -1313,10 +1313,13 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     }
     if (bad(hipMalloc(&c->d_bins_part, partials_need(bins_scale_blocks(c->B, c->tile_bins), bins_partial_nv()) * sizeof(double))))
       return GCS_ERR_HIP;
-    // the split bin path's raw sums (128-bin tiles; GCSLAM_BINS_SPLIT=0: the fused phase D)
+    // the split bin path's raw sums (128-bin tiles, GCSLAM_BINS_SPLIT=1; default: the fused phase D).
+    // Same-box A/B at C3 (profiles/r06/split/): split 94 us (gather + finalize) against 84 us fused --
+    // the 19 raw sums of every active bin written and read back (~2 x 90 MB) cost more than the
+    // two-wave finalize they free
     static const bool split = [] {
       const char* e = getenv("GCSLAM_BINS_SPLIT");
-      return !(e && atoi(e) == 0);
+      return e && atoi(e) == 1;
     }();
     if (split && c->tile_bins == 128 && bad(hipMalloc(&c->d_bins_raw, (size_t)19 * B * sizeof(double))))
       return GCS_ERR_HIP;
