@@ -137,43 +137,52 @@ GCS_HD double psd_project(const double* M, double eps_psd, double* out, double* 
     }
   double w[kN], V[kN * kN];
   if (!cert6) {
-    int act[kN], na = 0;
+    // the exactly-zero rows split off (the host's compacted active block), here in place: the active
+    // block keeps its indices, an inactive row / column is the identity in the Cholesky test (its pivot
+    // 1, its column 0: the active entries take the compact factorisation's operations) and zero in the
+    // Jacobi (its pairs are skipped, so the active pairs rotate in the compact order).  Every index is
+    // static, so the device keeps the arrays in registers.
+    bool act[kN];
+    int na = 0;
     for (int i = 0; i < n; ++i) {
       bool z = true;
-      for (int j = 0; j < n && z; ++j) z = s[i * n + j] == 0.0;
-      if (!z) act[na++] = i;
+      for (int j = 0; j < n; ++j) z = z && s[i * n + j] == 0.0;
+      act[i] = !z;
+      na += z ? 0 : 1;
     }
     if (na < n) {
       for (int i = 0; i < n * n; ++i) out[i] = 0.0;
       for (int i = 0; i < n; ++i) out[i * n + i] = eps_psd;
       double d2 = (double)(n - na) * eps_psd * eps_psd;
       if (na > 0) {
-        // the active block has no zero row (a row's non-zeros lie in active columns, by symmetry): the
-        // host's recursive call takes the paths below, inlined here
-        double sub[kN * kN], so[kN * kN], A[kN * kN], Lc[kN * kN], rd[kN];
-        for (int i = 0; i < na; ++i)
-          for (int j = 0; j < na; ++j) sub[i * na + j] = 0.5 * (s[act[i] * n + act[j]] + s[act[j] * n + act[i]]);
+        double sub[kN * kN], A[kN * kN], Lc[kN * kN], rd[kN];
+        for (int i = 0; i < n; ++i)
+          for (int j = 0; j < n; ++j) {
+            const bool aa = act[i] && act[j];
+            sub[i * n + j] = aa ? 0.5 * (s[i * n + j] + s[j * n + i]) : 0.0;
+            A[i * n + j] = aa ? sub[i * n + j] - (i == j ? eps_psd : 0.0) : (i == j ? 1.0 : 0.0);
+          }
         double da = 0.0;
-        for (int i = 0; i < na * na; ++i) A[i] = sub[i];
-        for (int i = 0; i < na; ++i) A[i * na + i] -= eps_psd;
-        if (cholesky<0>(na, A, Lc, rd)) {
-          for (int i = 0; i < na * na; ++i) so[i] = sub[i];
+        if (cholesky<NC>(n, A, Lc, rd)) {
+          for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j)
+              if (act[i] && act[j]) out[i * n + j] = sub[i * n + j];
         } else {
-          jacobi_eigh<0>(na, sub, w, V);
-          for (int k = 0; k < na; ++k) w[k] = w[k] > eps_psd ? w[k] : eps_psd;
+          jacobi_eigh<NC>(n, sub, w, V);
+          for (int k = 0; k < n; ++k) w[k] = w[k] > eps_psd ? w[k] : eps_psd;
           double dd2 = 0.0;
-          for (int i = 0; i < na; ++i)
-            for (int j = 0; j < na; ++j) {
+          for (int i = 0; i < n; ++i)
+            for (int j = 0; j < n; ++j) {
+              if (!(act[i] && act[j])) continue;
               double v = 0.0;
-              for (int k = 0; k < na; ++k) v += V[i * na + k] * w[k] * V[j * na + k];
-              so[i * na + j] = v;
-              const double dd = v - sub[i * na + j];
+              for (int k = 0; k < n; ++k)
+                if (act[k]) v += V[i * n + k] * w[k] * V[j * n + k];
+              out[i * n + j] = v;
+              const double dd = v - sub[i * n + j];
               dd2 += dd * dd;
             }
           da = sqrt(dd2);
         }
-        for (int i = 0; i < na; ++i)
-          for (int j = 0; j < na; ++j) out[act[i] * n + act[j]] = so[i * na + j];
         d2 += da * da;
       }
       return sqrt(d2);
