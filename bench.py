@@ -311,13 +311,23 @@ def pin_main_and_worker(ctx, share):
     is too small (fewer than 4 CPUs) or the kernel refuses."""
     if os.environ.get("GCSLAM_BENCH_PIN_MAIN", "1") == "0" or len(share) < 4:
         return {}
+    main = share[-1]
+    # the worker stays off the main thread's physical core too (its SMT siblings share the core's pipes)
+    sib = {main}
     try:
-        os.sched_setaffinity(threading.get_native_id(), {share[-1]})
-        out = dict(main_thread_cpu=share[-1])
+        from gcslam.topology import parse_cpulist
+        with open(f"/sys/devices/system/cpu/cpu{main}/topology/thread_siblings_list") as f:
+            sib |= set(parse_cpulist(f.read()))
+    except (OSError, ValueError, ImportError):
+        pass
+    rest = [c for c in share if c not in sib] or share[:-1]
+    try:
+        os.sched_setaffinity(threading.get_native_id(), {main})
+        out = dict(main_thread_cpu=main, main_core_siblings=sorted(sib - {main}))
         wt = ctx.worker_tid()
         if wt:
-            os.sched_setaffinity(wt, set(share[:-1]))
-            out["worker_cpus"] = f"{share[0]}-{share[-2]} ({len(share) - 1})"
+            os.sched_setaffinity(wt, set(rest))
+            out["worker_cpus"] = f"{len(rest)} of the share, not the main thread's core"
         return out
     except OSError:
         return {}
@@ -441,6 +451,8 @@ def live_path_bench(device, steps=30, warmup=10):
     os.environ["GCSLAM_LIVE_CHAIN"] = "0"
     per_op = np.zeros(steps)
     try:
+        for i in range(3):  # its own warm-up: the per-operator calls' first-use allocations
+            one(scans[warmup + steps + i])
         for i in range(steps):
             t0 = time.perf_counter()
             one(scans[warmup + steps + i])

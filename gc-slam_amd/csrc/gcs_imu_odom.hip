@@ -21,6 +21,12 @@
 #include "gcs_layout.h"
 #include "gcs_preint_scan.h"
 
+// timing probes (not parity builds; `make variant VSRC=gcs_imu_odom.hip VDEF=-DGCS_IO_PROBE=n`): 1 skips
+// the three sorts, 2 the preintegration scan, 4 the vMF per-sample terms (bit mask)
+#ifndef GCS_IO_PROBE
+#define GCS_IO_PROBE 0
+#endif
+
 namespace gcs {
 namespace {
 
@@ -170,7 +176,7 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
   bool unsorted = false;
   __syncthreads();
   for (int i = 1 + tid; i < n_in; i += kIoThreads) unsorted = unsorted || s_key[i] < s_key[i - 1];
-  if (__syncthreads_or(unsorted)) {
+  if (__syncthreads_or(unsorted) && !(GCS_IO_PROBE & 1)) {
     for (int i = n_in + tid; i < kIoKeys; i += kIoThreads) s_key[i] = INFINITY;
     io_sort(s_key);
   }
@@ -187,9 +193,10 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
     dt_int = dt_int > 0.0 ? dt_int : 0.0;
   }
   // ---- the scan-to-scan preintegration (pipeline.py:442-453; imu_preintegration.py:47-147)
-  double Pc[9], vc[3], pc[3], ess;
-  preint::window_carry(stamps, gyro, accel, m, [=](int i, double) { return w_int[i]; }, pose0 + 3, gb, ab, grav, Pc,
-                       vc, pc, ess);
+  double Pc[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, vc[3] = {0, 0, 0}, pc[3] = {0, 0, 0}, ess = 0.0;
+  if (!(GCS_IO_PROBE & 2))
+    preint::window_carry(stamps, gyro, accel, m, [=](int i, double) { return w_int[i]; }, pose0 + 3, gb, ab, grav,
+                         Pc, vc, pc, ess);
   if (tid == 0) {
     double R0[9], Re[9], dR[9];
     so3_exp(pose0 + 3, R0);
@@ -201,7 +208,7 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
     so3_log(dR, s_pre + 3);  // drot
   }
   // ---- the IMU vMF factor's per-sample statistics (imu_evidence.py:276-399)
-  for (int i = tid; i < m; i += kIoThreads) {  // transport consistency e_i (central differences)
+  for (int i = tid; i < m && !(GCS_IO_PROBE & 4); i += kIoThreads) {  // transport consistency e_i (central differences)
     double df[3], ai[3], c[3];
     for (int k = 0; k < 3; ++k) {
       ai[k] = accel[3 * i + k] - ab[k];
@@ -215,11 +222,11 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
   }
   __syncthreads();
   for (int i = tid; i < kIoKeys; i += kIoThreads) s_key[i] = i < m ? s_e[i] : INFINITY;
-  io_sort(s_key);
+  if (!(GCS_IO_PROBE & 1)) io_sort(s_key);
   const double med = io_median(s_key, m);
   __syncthreads();
   for (int i = tid; i < kIoKeys; i += kIoThreads) s_key[i] = i < m ? fabs(s_e[i] - med) : INFINITY;
-  io_sort(s_key);
+  if (!(GCS_IO_PROBE & 1)) io_sort(s_key);
   host::ImuVmfStats v{};
   v.sigma = io_median(s_key, m) / 0.6745 + kEpsMass;
   double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // rel, w, w_int, S[3]

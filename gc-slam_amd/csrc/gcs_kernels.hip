@@ -1390,6 +1390,37 @@ __device__ __forceinline__ double2 mass_rows_wave(const double2* __restrict__ ro
   }
   return make_double2(sx, sy);
 }
+// mass_rows_wave with its first chunk (rows t + k NT, k < 4) already loaded into x0: the same sums in the
+// same order, so every block's mass_scale is bit for bit block 0's
+template <int NT>
+__device__ __forceinline__ double2 mass_rows_wave_pre(const double2* __restrict__ rows, int n, const double2 (&x0)[4]) {
+  double sx = 0.0, sy = 0.0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    sx += x0[k].x;
+    sy += x0[k].y;
+  }
+  for (int r0 = 4 * NT; r0 < n; r0 += 4 * NT) {
+    double2 x[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = r0 + (int)threadIdx.x + k * NT;
+      x[k] = r < n ? rows[r] : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      sx += x[k].x;
+      sy += x[k].y;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    sx += __shfl_xor(sx, off, 64);
+    sy += __shfl_xor(sy, off, 64);
+  }
+  return make_double2(sx, sy);
+}
+
 template <int NW>
 __device__ __forceinline__ double mass_scale_of(const double2* s_mw, double* m_in = nullptr, double* m_sel = nullptr) {
   double mi = s_mw[0].x, ms = s_mw[0].y;
@@ -1531,8 +1562,15 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
   {
     // fixed trip counts: every thread issues all of its table loads before the first LDS write,
     // so the reverse-kNN entries (up to kMaxRl / NT per thread) cost one round trip, not one each,
-    // and the sources two (tile_src, then their counts / starts)
+    // and the sources two (tile_src, then their counts / starts).  Self-budget: the mass rows' first
+    // chunk is loaded first and summed after the LDS writes (its round trip hidden behind the tables')
     constexpr int RL = (kMaxRl + NT - 1) / NT, SR = (kMaxSrc + NT - 1) / NT;
+    double2 mw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int r = t + k * NT;
+      mw[k] = a.mass_rows && r < a.mass_nrows ? a.mass_rows[r] : make_double2(0.0, 0.0);
+    }
     uint16_t rl[RL];
 #pragma unroll
     for (int k = 0; k < RL; ++k) {
@@ -1550,10 +1588,6 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
       // sorted bucketing: the bucket's start in perm; direct buckets: its member row
       st[k] = t + k * NT < ns ? (a.members ? (uint32_t)src[k] * (uint32_t)a.capb : a.starts[src[k]]) : 0u;
     }
-    if (a.mass_rows) {  // self-budget: the mass rows, loaded behind the tables (one round trip for all)
-      const double2 ws = mass_rows_wave<NT>(a.mass_rows, a.mass_nrows);
-      if (lane == 0) s_mw[wid] = ws;
-    }
 #pragma unroll
     for (int k = 0; k < RL; ++k)
       if (q0 + t + k * NT < q1t) s_rl[t + k * NT] = rl[k];
@@ -1563,6 +1597,10 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
         s_cnt[t + k * NT] = cn[k];
         s_st[t + k * NT] = st[k];
       }
+    if (a.mass_rows) {
+      const double2 ws = mass_rows_wave_pre<NT>(a.mass_rows, a.mass_nrows, mw);
+      if (lane == 0) s_mw[wid] = ws;
+    }
   }
   __syncthreads();
   PROF(1);

@@ -38,6 +38,8 @@ step() {
     snapprev)  # the same snapshot with the A/B library (libgcslam_hip_$B.so)
       GCSLAM_LIB=$PWD/gc-slam_amd/gcslam/libgcslam_hip_${B:-prev}.so timeout -k 10 300 python -u tools/bitwise_snapshot.py \
         save "$O/snap_prev.npz" > "$O/snap_prev.log" 2>&1 ;;
+    snapenv)  # the same snapshot with $ENVB set (an environment knob)
+      env $ENVB timeout -k 10 300 python -u tools/bitwise_snapshot.py save "$O/snap_env.npz" > "$O/snap_env.log" 2>&1 ;;
     snap)  # bitwise snapshot of the bin path (tools/bitwise_snapshot.py), compared with $SNAP_BASE if set
       timeout -k 10 300 python -u tools/bitwise_snapshot.py save "$O/snap.npz" > "$O/snap.log" 2>&1 || return $?
       [ -n "$SNAP_BASE" ] && python tools/bitwise_snapshot.py compare "$SNAP_BASE" "$O/snap.npz" > "$O/snap_cmp.txt" 2>&1
@@ -120,6 +122,12 @@ step() {
     io) timeout -k 10 120 python tools/io_bench.py > "$O/io_bench.txt" 2>&1 ;;
     ioprof) timeout -k 10 180 rocprofv3 --kernel-trace --stats -d "$O/io_prof" -o run --output-format csv -- \
               python3 tools/io_bench.py 100 > "$O/io_prof.log" 2>&1 ;;
+    ioprobe)  # the IMU kernels' time per probe variant (IOPROBE="- io1 io2 ...": libgcslam_hip_<v>.so; - = default)
+      for v in ${IOPROBE:-- io1 io2 io4 io7}; do
+        lib=gc-slam_amd/gcslam/libgcslam_hip.so; [ "$v" != "-" ] && lib=gc-slam_amd/gcslam/libgcslam_hip_$v.so
+        GCSLAM_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$O/ioprobe_${v/-/base}" -o run \
+          --output-format csv -- python3 tools/io_bench.py 50 > "$O/ioprobe_${v/-/base}.log" 2>&1 || return $?
+      done ;;
     graphab) timeout -k 10 120 ./tools/graph_ab 2000 > "$O/graph_ab.json" 2>&1 ;;
     gaps)  # device idle gaps of the C2 step, from prof2's kernel trace
       local tr; tr=$(find "$O/prof_c2" -name '*kernel_trace.csv' | head -1)
