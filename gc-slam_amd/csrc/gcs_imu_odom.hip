@@ -60,15 +60,18 @@ __device__ __forceinline__ double io_block_min(double v, double* s) {
 }
 __device__ __forceinline__ double io_block_max(double v, double* s) { return -io_block_min(-v, s); }
 
-// ascending bitonic sort of the 2 kIoThreads keys in k (LDS; pad with +inf): lane t holds positions 2t and
-// 2t + 1, so a stride-1 exchange stays in the lane, strides 2-64 are shuffles inside the wave (a wave holds
-// 128 consecutive positions) and only the six stages with strides of 128-512 go through LDS
+// ascending bitonic sort of the first np2 (a power of two, block-uniform) of the 2 kIoThreads keys in k
+// (LDS; pad with +inf): lane t holds positions 2t and 2t + 1, so a stride-1 exchange stays in the lane,
+// strides 2-64 are shuffles inside the wave (a wave holds 128 consecutive positions) and only strides of
+// 128-512 go through LDS.  A network over np2 positions leaves the positions past np2 in place (a
+// partner of such a position lies past np2 too), so a window of m samples costs log2(np2) (log2(np2) +
+// 1) / 2 stages: 15 at the reference's ~20-sample windows instead of 55.
 constexpr int kIoKeys = 2 * kIoThreads;
-__device__ void io_sort(double* k) {
+__device__ void io_sort(double* k, int np2) {
   const int t = (int)threadIdx.x;
   __syncthreads();
   double v[2] = {k[2 * t], k[2 * t + 1]};
-  for (int size = 2; size <= kIoKeys; size <<= 1)
+  for (int size = 2; size <= np2; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
       double o[2];
       if (stride >= 128) {  // across waves
@@ -98,6 +101,12 @@ __device__ void io_sort(double* k) {
   k[2 * t] = v[0];
   k[2 * t + 1] = v[1];
   __syncthreads();
+}
+
+__device__ __forceinline__ int io_pow2(int n) {
+  int p = 2;
+  while (p < n) p <<= 1;
+  return p;
 }
 
 // numpy median of the first n sorted keys: the middle one, or the mean of the two middle ones
@@ -178,7 +187,7 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
   for (int i = 1 + tid; i < n_in; i += kIoThreads) unsorted = unsorted || s_key[i] < s_key[i - 1];
   if (__syncthreads_or(unsorted) && !(GCS_IO_PROBE & 1)) {
     for (int i = n_in + tid; i < kIoKeys; i += kIoThreads) s_key[i] = INFINITY;
-    io_sort(s_key);
+    io_sort(s_key, io_pow2(n_in));
   }
   double gaps = 0.0;
   for (int i = 1 + tid; i < n_in; i += kIoThreads) {
@@ -222,11 +231,11 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
   }
   __syncthreads();
   for (int i = tid; i < kIoKeys; i += kIoThreads) s_key[i] = i < m ? s_e[i] : INFINITY;
-  if (!(GCS_IO_PROBE & 1)) io_sort(s_key);
+  if (!(GCS_IO_PROBE & 1)) io_sort(s_key, io_pow2(m));
   const double med = io_median(s_key, m);
   __syncthreads();
   for (int i = tid; i < kIoKeys; i += kIoThreads) s_key[i] = i < m ? fabs(s_e[i] - med) : INFINITY;
-  if (!(GCS_IO_PROBE & 1)) io_sort(s_key);
+  if (!(GCS_IO_PROBE & 1)) io_sort(s_key, io_pow2(m));
   host::ImuVmfStats v{};
   v.sigma = io_median(s_key, m) / 0.6745 + kEpsMass;
   double acc[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // rel, w, w_int, S[3]
@@ -256,31 +265,32 @@ __global__ __launch_bounds__(kIoThreads) void k_imu_odom(ImuOdomDevArgs a) {
   }
 }
 
-// lane 0: the eleven factors and their sum (the host branch's code) into device memory; then the wave
-// copies the record to the pinned host record, stamped
-__global__ __launch_bounds__(64) void k_imu_odom_assemble(ImuOdomDevArgs a) {
-  const int tid = (int)threadIdx.x;
+// The eleven factors and their sum (the host branch's code, gcs_imu_odom_core.h) into device memory:
+// the four waves' lane 0 run the six factor parts -- the 6x6 odometry factor alone, the others in pairs
+// (the parts read only the inputs; their results meet in LDS) --, then lane 0 adds them in the
+// pipeline's order; the first wave then copies the record to the pinned host record, stamped.  One wave
+// per SIMD: a part's fixed-size algebra (the 6x6 Jacobi) keeps its arrays in up to 512 registers.
+constexpr int kIoAsmWaves = 4;
+__global__ __launch_bounds__(64 * kIoAsmWaves) void k_imu_odom_assemble(ImuOdomDevArgs a) {
+  __shared__ host::ImuOdomParts s_p;
+  const int tid = (int)threadIdx.x, wid = tid >> 6, lane = tid & 63;
   const int m = a.m;
-  const double* stamps = a.win;
-  const double* gyro = a.win + m;
-  const double* accel = a.win + 4 * m;
-  const double* w_int = a.win + 7 * m;
   const double* sm = a.win + 8 * m;
   const double* mu_inc = sm + kIoMuInc;
   host::ImuOdomOut* out = reinterpret_cast<host::ImuOdomOut*>(a.out);
   double* extra = a.out + kIoOutWords - 5;
   const double* st = a.out + kIoOutWords;
-  if (tid == 0) {
-    host::ImuVmfStats v{};
+  host::ImuVmfStats v{};
+  double om[3], pre[9];
+  host::ImuOdomInputs in{};
+  if (lane == 0) {
     v.S[0] = st[0]; v.S[1] = st[1]; v.S[2] = st[2];
     v.ess_w = st[3]; v.ess_raw = st[4]; v.rel_sum = st[5]; v.sigma = st[6];
-    const double dt_imu = st[7], dt_int = st[8];
-    double om[3] = {st[9], st[10], st[11]}, pre[9];
+    om[0] = st[9]; om[1] = st[10]; om[2] = st[11];
     for (int k = 0; k < 9; ++k) pre[k] = st[12 + k];
-    host::ImuOdomInputs in{};
     in.m = m;
-    in.stamps = stamps; in.gyro = gyro; in.accel = accel; in.w_int = w_int;
-    in.dt_imu = dt_imu; in.dt_int = dt_int; in.dt_sec = a.dt_sec;
+    in.stamps = a.win; in.gyro = a.win + m; in.accel = a.win + 4 * m; in.w_int = a.win + 7 * m;
+    in.dt_imu = st[7]; in.dt_int = st[8]; in.dt_sec = a.dt_sec;
     in.omega_avg = om;
     in.dp_int = pre; in.drot_int = pre + 3; in.dv_int = pre + 6;
     in.pose0 = sm + kIoPose0; in.pose_pred = sm + kIoPosePred; in.mu_prev = sm + kIoMuPrev; in.mu_inc = mu_inc;
@@ -290,12 +300,22 @@ __global__ __launch_bounds__(64) void k_imu_odom_assemble(ImuOdomDevArgs a) {
     in.odom_pose = sm + kIoOdomPose; in.odom_cov = sm + kIoOdomCov; in.odom_twist = sm + kIoOdomTwist;
     in.odom_twist_cov = sm + kIoOdomTwistCov;
     in.planar_z_ref = a.planar_z_ref; in.planar_z_sigma = a.planar_z_sigma; in.planar_vz_sigma = a.planar_vz_sigma;
-    host::imu_odom_assemble(in, v, *out);
-    extra[0] = dt_int; extra[1] = dt_imu; extra[2] = om[0]; extra[3] = om[1]; extra[4] = om[2];
+  }
+  if (tid == 0) host::io_init(*out);
+  __syncthreads();
+  if (lane == 0) {  // parts {0}, {1, 4}, {2, 3}, {5}
+    constexpr int kFirst[kIoAsmWaves] = {0, 1, 2, 5}, kSecond[kIoAsmWaves] = {-1, 4, 3, -1};
+    host::io_part(kFirst[wid], in, v, s_p, *out);
+    if (kSecond[wid] >= 0) host::io_part(kSecond[wid], in, v, s_p, *out);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    host::io_sum(in, s_p, *out);
+    extra[0] = in.dt_int; extra[1] = in.dt_imu; extra[2] = om[0]; extra[3] = om[1]; extra[4] = om[2];
   }
   __syncthreads();
   // ---- the stamped copy to the pinned host record: kIoOutWords words, sequence, checksum
-  if (!a.host) return;
+  if (!a.host || wid != 0) return;
   uint64_t* hw = reinterpret_cast<uint64_t*>(a.host);
   const uint64_t* dw = reinterpret_cast<const uint64_t*>(a.out);
   unsigned long long h = 0;
@@ -321,7 +341,7 @@ __global__ __launch_bounds__(64) void k_imu_odom_assemble(ImuOdomDevArgs a) {
 hipError_t launch_imu_odom(const ImuOdomDevArgs& a, hipStream_t s) {
   if (a.m < 2 || a.m > kImuOdomMaxM) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_imu_odom, dim3(1), dim3(kIoThreads), 0, s, a);
-  hipLaunchKernelGGL(k_imu_odom_assemble, dim3(1), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_imu_odom_assemble, dim3(1), dim3(64 * kIoAsmWaves), 0, s, a);
   return hipGetLastError();
 }
 

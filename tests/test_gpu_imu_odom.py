@@ -127,16 +127,18 @@ def test_scans_with_device_branch_match_host_branch(mode, B, cap, n):
     # downstream outputs at the pipeline's multi-scan bar (tests/test_gpu_fullsize.py: rtol 1e-7) on the
     # first two scans, and the pose-6 conditioning (cert[49], an eigenvalue ratio of the summed evidence:
     # a scale-mode scan measured 1.1e-5 relative between the two branches' sum orders) at 1e-4.  The loop
-    # feeds each branch's z_t back into its own map: by the third scale-mode scan (20,000 bins, 8,192
-    # points) the sum-order differences had grown to 1.8e-7 m in an 8e-5 m z translation and 1.2e-5
-    # relative in L (profiles/r06/imu_odom/), so that scan's z_t / L take atol 1e-6 m / rtol 1e-4.
+    # feeds each branch's z_t back into its own deskew and map, and the reference's nearest-bin step is
+    # discontinuous: a point within ~1e-9 of a Voronoi boundary between two bins changes its candidate
+    # set under a 1e-9 m pose change.  By the third scale-mode scan (20,000 bins, 8,192 points) that had
+    # moved z_t by 1.8e-7 m and single L entries by up to 1.2e-5 of max|L| (profiles/r06/imu_odom/), so
+    # that scan's z_t / L take atol 1e-6 m / 1e-4 max|L|.
     bad = []
     for s in range(3):
         a, b = runs[0][s], runs[1][s]
         late = s >= 2
         checks = [("Lio", 1e-9, 1e-12 * np.abs(a["Lio"]).max()), ("hio", 1e-9, 1e-12 * max(np.abs(a["hio"]).max(), 1.0)),
                   ("certs", 1e-8, 1e-12), ("z_t", 1e-7, 1e-6 if late else 1e-9),
-                  ("L", 1e-4 if late else 1e-7, 1e-7 * np.abs(a["L"]).max())]
+                  ("L", 1e-7, (1e-4 if late else 1e-7) * np.abs(a["L"]).max())]
         for k, rt, at in checks:
             if not np.allclose(b[k], a[k], rtol=rt, atol=at):
                 i = int(np.argmax(np.abs(b[k] - a[k]) - rt * np.abs(a[k])))
