@@ -78,7 +78,7 @@ def pmc_chain_traffic(config):
                          ("bins_fold", "k_fold<16"), ("bins_fold", "k_final<16")):
             if pat in k:
                 per[tag] = per.get(tag, 0.0) + v["hbm_bytes"]
-    if set(per) != {"budget", "points", "bins", "bins_fold"}:
+    if not {"points", "bins", "bins_fold"} <= set(per):
         return None, None
     return per, f"profiles/pmc_bins_{config}.json ({d.get('round', '?')})"
 
@@ -89,8 +89,11 @@ def roofline_chain(N, B, stage_avg, label, config=None):
     softmax normaliser) + k_bins_scale (rows 4-6 + MF terms) + the bin kernel's partial-row fold,
     each timed by its own dispatch events, against the same SURVEY 8(d) bytes as `roofline`."""
     names = ("budget", "points", "bins", "bins_fold")
-    if any(stage_avg.get(k) is None for k in names):
+    if any(stage_avg.get(k) is None for k in names[1:]):
         return None
+    # self-budget scans launch no k_budget (k_points sums the stride windows, the bin kernel folds the
+    # rows): the chain is the three kernels that run
+    names = names if stage_avg.get("budget") is not None else names[1:]
     ms = sum(stage_avg[k] for k in names)
     rd, wr = bins_kernel_bytes(N, B)
     s = ms * 1e-3
@@ -98,9 +101,11 @@ def roofline_chain(N, B, stage_avg, label, config=None):
     out = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
            "read_frac": rd / s / 1e9 / HBM_PEAK_GBS, "write_frac": wr / s / 1e9 / HBM_PEAK_GBS,
            "chain_us": ms * 1e3, "kernels_us": {k: stage_avg[k] * 1e3 for k in names},
+           "budget": "k_budget" if "budget" in names else "in k_points (self-budget: no k_budget launch)",
            "algorithmic_bytes": rd + wr, "config": label}
     per, src = pmc_chain_traffic(config) if config else (None, None)
     if per:  # the counter-based traffic of the same kernels beside the algorithmic bytes
+        per = {k: v for k, v in per.items() if k in names}
         t = sum(per.values())
         out.update(traffic=t, traffic_per_kernel=per, traffic_source=src, traffic_frac=t / s / 1e9 / HBM_PEAK_GBS)
     return out
@@ -920,11 +925,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    import resource
+    ru0 = resource.getrusage(resource.RUSAGE_THREAD)  # the main thread's context switches over the region
     t0 = time.perf_counter()
     for i in range(args.steps):
         ts = time.perf_counter()
         step()
         per_step[i] = time.perf_counter() - ts
+    ru1 = resource.getrusage(resource.RUSAGE_THREAD)
     ctx.synchronize()
     torch.cuda.synchronize()
     if world > 1:
@@ -1027,6 +1035,10 @@ def main():
         med_step = float(np.median(per_step))
         slow = np.nonzero(per_step > 2.0 * med_step)[0]
         host_avg["steps_over_2x_median"] = int(len(slow))
+        host_avg["ctx_switches"] = dict(voluntary=int(ru1.ru_nvcsw - ru0.ru_nvcsw),
+                                        involuntary=int(ru1.ru_nivcsw - ru0.ru_nivcsw),
+                                        note="main thread, over the timed region: a preempted step shows as "
+                                             "an involuntary switch, a device-side delay as device_wait alone")
         if len(hist) == len(per_step):
             host_avg["slow_steps"] = [dict(step=int(i), ms=float(per_step[i] * 1e3),
                                            split={n: float(hist[i, k]) for k, n in enumerate(ctx.HOST_HIST)})
