@@ -596,6 +596,9 @@ void k_points(PointKernelArgs a, double* partials) {
 #ifndef GCS_PROBE_NOEXP
 #define GCS_PROBE_NOEXP 0
 #endif
+#ifndef GCS_PROBE_NOMASS
+#define GCS_PROBE_NOMASS 0  // timing probe (not a parity build): the bin kernel's blocks skip the mass-row loads
+#endif
 #ifndef GCS_PROBE_NOFIN
 #define GCS_PROBE_NOFIN 0  // timing probe (not a parity build): phase D skips finalize_bin / the MF term
 #endif
@@ -1569,7 +1572,7 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int r = t + k * NT;
-      mw[k] = a.mass_rows && r < a.mass_nrows ? a.mass_rows[r] : make_double2(0.0, 0.0);
+      mw[k] = a.mass_rows && r < a.mass_nrows && !GCS_PROBE_NOMASS ? a.mass_rows[r] : make_double2(1.0, 1.0);
     }
     uint16_t rl[RL];
 #pragma unroll

@@ -79,6 +79,9 @@ step() {
         timeout -s KILL 120 rocprofv3 --pmc $ctr --kernel-include-regex "k_as_" -d "$O/assocpmc/$nm" -o run \
           --output-format csv -- python3 tools/assoc_bench.py 5 50 > "$O/assocpmc_$nm.log" 2>&1 || return $?
       done ;;
+    phasev)  # the phase clocks with PHASE_LIB (a GCS_PHASE_PROF variant: libgcslam_hip_<PHASE_LIB>.so), C3
+      GCSLAM_LIB=$PWD/gc-slam_amd/gcslam/libgcslam_hip_${PHASE_LIB}.so timeout -k 10 180 python tools/phase_prof.py c3 \
+        > "$O/phase_${PHASE_LIB}_c3.txt" 2>&1 ;;
     phase) for cfg in c2 c3; do timeout -k 10 180 python tools/phase_prof.py $cfg > "$O/phase_$cfg.txt" 2>&1 || return $?; done ;;
     pmap) timeout -k 10 300 python tools/pmap_bench.py 30 > "$O/pmap_bench.txt" 2>&1 ;;
     pmapprof) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/pmap_prof" -o run --output-format csv -- \
