@@ -1572,7 +1572,8 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int r = t + k * NT;
-      mw[k] = a.mass_rows && r < a.mass_nrows && !GCS_PROBE_NOMASS ? a.mass_rows[r] : make_double2(1.0, 1.0);
+      const bool ok = a.mass_rows && r < a.mass_nrows;
+      mw[k] = ok ? (GCS_PROBE_NOMASS ? make_double2(1.0, 1.0) : a.mass_rows[r]) : make_double2(0.0, 0.0);
     }
     uint16_t rl[RL];
 #pragma unroll
