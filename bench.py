@@ -879,6 +879,12 @@ def main():
     TIMING_STRIDE = timing_stride(args.steps)
 
     def step():
+        try:
+            _step()
+        except (RuntimeError, ValueError) as e:  # name the failing scan (its index in the bench's sequence)
+            raise type(e)(f"{e} [bench scan {state['count']}, scan {state['count'] % N_SCANS} of the cycle]") from e
+
+    def _step():
         combine = state["combine"]
         # roofline-kernel event stamps on every TIMING_STRIDE-th scan (also in the warm-up, so the timed
         # region's first stamped scan does not pay the events' first use)
