@@ -998,6 +998,8 @@ def main():
     # the step with the IMU / odometry branch on the device (k_imu_odom on its own stream
     # beside the bin path's kernels) instead of the host C++ branch, same box, its own warm-up
     try:
+        if os.environ.get("GCSLAM_BENCH_NO_DEVIO") == "1":
+            raise RuntimeError("skipped (GCSLAM_BENCH_NO_DEVIO=1)")
         ctx.set_debug(L.DEBUG_DEVICE_IMU_ODOM, 1)
     except (RuntimeError, ValueError) as e:  # an older library in a same-box A/B
         variants["device_imu_odom_unstamped_error"] = str(e)[:200]
