@@ -131,6 +131,9 @@ step() {
         GCSLAM_LIB=$PWD/$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$O/ioprobe_${v/-/base}" -o run \
           --output-format csv -- python3 tools/io_bench.py 50 > "$O/ioprobe_${v/-/base}.log" 2>&1 || return $?
       done ;;
+    longrun) for cfg in ${LONG_CONFIGS:-c3}; do  # tools/long_run.py: a long cycled sequence's per-scan diagnostics
+        timeout -k 10 240 python tools/long_run.py $cfg ${LONG_SCANS:-400} > "$O/long_run_$cfg.txt" 2>&1 || return $?
+      done ;;
     graphab) timeout -k 10 120 ./tools/graph_ab 2000 > "$O/graph_ab.json" 2>&1 ;;
     gaps)  # device idle gaps of the C2 step, from prof2's kernel trace
       local tr; tr=$(find "$O/prof_c2" -name '*kernel_trace.csv' | head -1)
