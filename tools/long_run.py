@@ -35,10 +35,13 @@ def main():
     out = L.GcsScanOutputs()
     scan_fn = ctx.scan_call(out)
     combine = ctx.combine_call(None, 1.0, 1.0)
+    restart = os.environ.get("LONG_RESTART", "1") == "1"  # bench.py's per-pass restart of the belief
     hist = []
     err = None
     for s in range(total):
         try:
+            if restart and s and s % bench.N_SCANS == 0:
+                ctx.set_belief(np.zeros(6), 0.0, np.zeros(22), 1e-6 * np.eye(22), np.zeros(22))
             scan_fn(prepared[s % bench.N_SCANS])
             combine(s)
         except (RuntimeError, ValueError) as e:
@@ -59,7 +62,7 @@ def main():
     show = hist[-12:] if err else hist[::50] + hist[-2:]
     for r in show:
         print(json.dumps(r), flush=True)
-    print(json.dumps(dict(config=cfg_name, scans_run=len(hist), error=err)), flush=True)
+    print(json.dumps(dict(config=cfg_name, scans_run=len(hist), error=err, restart=restart)), flush=True)
     ctx.close()
 
 
