@@ -292,10 +292,14 @@ def c3_roofline(device, steps=16, warmup=3):
     ctx.synchronize()
     ctx.enable_timing(True, stages=["budget", "points", "bins", "bins_fold"])
     ctx.stage_times(reset=True)
+    # the step's shape: each scan followed by the hypothesis combine (host form: one rank here), so a
+    # scan's point kernel does not start under the previous scan's pushforward, as it would back to back
+    combine = ctx.combine_call(None, 1.0, 1.0)
     t0 = time.perf_counter()
     for k in range(steps):
         sc, rec, t, w = scans[k % 2]
         ctx.scan(rec, 16, t, w, cfg["N"], **scan_kwargs(sc))
+        combine(k)
     ctx.synchronize()
     el = time.perf_counter() - t0
     ms_sum, cnt = ctx.stage_times(reset=True)
