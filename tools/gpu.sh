@@ -45,6 +45,7 @@ step() {
       [ -n "$SNAP_BASE" ] && python tools/bitwise_snapshot.py compare "$SNAP_BASE" "$O/snap.npz" > "$O/snap_cmp.txt" 2>&1
       return 0 ;;
     bench) timeout -k 10 400 python bench.py > "$O/bench_c2.log" 2>&1 ;;
+    driver) timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_driver.log" 2>&1 ;;
     live) timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-c3 > "$O/bench_live.log" 2>&1 ;;
     benchshared) timeout -k 10 300 python bench.py --map-mode shared --no-cpu-baseline --no-c3 --no-live > "$O/bench_shared.log" 2>&1 ;;
     hostbench) timeout -k 10 120 ./tools/host_bench tools/host_bench_in.bin > "$O/host_bench.txt" 2>&1 ;;
