@@ -135,6 +135,8 @@ step() {
     longrun) for cfg in ${LONG_CONFIGS:-c3}; do  # tools/long_run.py: a long cycled sequence's per-scan diagnostics
         timeout -k 10 240 python tools/long_run.py $cfg ${LONG_SCANS:-400} > "$O/long_run_$cfg.txt" 2>&1 || return $?
       done ;;
+    repeat)  # REPEAT="tests/file.py test_name N": one test function N times in one process
+      timeout -k 10 600 python -u tools/repeat_test.py $REPEAT > "$O/repeat.log" 2>&1 ;;
     graphab) timeout -k 10 120 ./tools/graph_ab 2000 > "$O/graph_ab.json" 2>&1 ;;
     gaps)  # device idle gaps of the C2 step, from prof2's kernel trace
       local tr; tr=$(find "$O/prof_c2" -name '*kernel_trace.csv' | head -1)
