@@ -292,15 +292,17 @@ def c3_roofline(device, steps=16, warmup=3):
     ctx.synchronize()
     ctx.enable_timing(True, stages=["budget", "points", "bins", "bins_fold"])
     ctx.stage_times(reset=True)
-    # the step's shape: each scan followed by the hypothesis combine (host form: one rank here), so a
-    # scan's point kernel does not start under the previous scan's pushforward, as it would back to back
+    # each scan followed by the hypothesis combine (host form: one rank here) and a device sync: the
+    # chain's kernels are timed alone, not under the previous scan's pushforward (at C3 a 55 us kernel on
+    # the push stream that the step's 20 us of host work does not cover: k_points 41 us alone, ~52 us
+    # under it -- a pipelining cost of the step, which ms_per_step at --config c3 carries)
     combine = ctx.combine_call(None, 1.0, 1.0)
     t0 = time.perf_counter()
     for k in range(steps):
         sc, rec, t, w = scans[k % 2]
         ctx.scan(rec, 16, t, w, cfg["N"], **scan_kwargs(sc))
         combine(k)
-    ctx.synchronize()
+        ctx.synchronize()
     el = time.perf_counter() - t0
     ms_sum, cnt = ctx.stage_times(reset=True)
     ctx.close()
