@@ -135,6 +135,10 @@ step() {
     longrun) for cfg in ${LONG_CONFIGS:-c3}; do  # tools/long_run.py: a long cycled sequence's per-scan diagnostics
         timeout -k 10 240 python tools/long_run.py $cfg ${LONG_SCANS:-400} > "$O/long_run_$cfg.txt" 2>&1 || return $?
       done ;;
+    tests2)  # the same pytest selection a second time into pytest_gpu_2.log (a flakiness check; failures do not stop)
+      local k2=(); [ -n "$PYTEST_K" ] && k2=(-k "$PYTEST_K")
+      timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail="${MAXFAIL:-8}" -v -rA --timeout 120 --timeout-method thread "${k2[@]}" \
+        > "$O/pytest_gpu_2.log" 2>&1; local rc=$?; [ $rc -le 1 ] && return 0; return $rc ;;
     repeat)  # REPEAT="tests/file.py test_name N": one test function N times in one process
       timeout -k 10 600 python -u tools/repeat_test.py $REPEAT > "$O/repeat.log" 2>&1 ;;
     graphab) timeout -k 10 120 ./tools/graph_ab 2000 > "$O/graph_ab.json" 2>&1 ;;
