@@ -5,7 +5,8 @@ per-scan z_t compared bitwise with the first's.  Prints the number of distinct s
 largest z_t difference and any scan mirror that was re-read or taken after a stream synchronize.
 
   python tools/determinism_check.py [reps=20]      (DET_STAGES=1: also the first differing scan of each
-                                                   device state checksum, gcs_debug_state_checksums)
+                                                   device state checksum, gcs_debug_state_checksums;
+                                                   DET_N / DET_B / DET_SCANS: the size, e.g. C3)
 """
 import os
 import sys
@@ -26,11 +27,14 @@ def main():
     from gcslam.context import HypothesisContext
     from gcslam.distributed import combine_allreduce
     from gcslam.synthetic import scan_kwargs
-    scans = [synthetic.make_scan(4096, s) for s in range(12)]
+    N = int(os.environ.get("DET_N", "4096"))
+    B = int(os.environ.get("DET_B", "5000"))
+    n_scans = int(os.environ.get("DET_SCANS", "12"))
+    scans = [synthetic.make_scan(N, s) for s in range(n_scans)]
     runs, st_runs = [], []
     for r in range(reps):
         stats = []
-        ctx = HypothesisContext(n_bins=5000, n_points_cap=4096, max_raw_points=4096, mode="scale",
+        ctx = HypothesisContext(n_bins=B, n_points_cap=N, max_raw_points=N, mode="scale",
                                 lidar_origin=tuple(ORIGIN))
         zs = []
         try:
@@ -38,7 +42,7 @@ def main():
                 rec = torch.from_numpy(sc["xyz_record"]).cuda()
                 t = torch.from_numpy(sc["timestamps"]).cuda()
                 w = torch.from_numpy(sc["weights"]).cuda()
-                out = ctx.scan(rec, 16, t, w, 4096, **scan_kwargs(sc))
+                out = ctx.scan(rec, 16, t, w, N, **scan_kwargs(sc))
                 zs.append(np.array(out.z_t[:], np.float64))
                 combine_allreduce(ctx, 0, 1, s, want_belief=False)
                 if STAGES:  # the device state the next scan reads, after this scan's pushforward

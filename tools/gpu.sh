@@ -139,6 +139,7 @@ step() {
       local k2=(); [ -n "$PYTEST_K" ] && k2=(-k "$PYTEST_K")
       timeout -k 10 900 python -u -m pytest tests -m gpu --maxfail="${MAXFAIL:-8}" -v -rA --timeout 120 --timeout-method thread "${k2[@]}" \
         > "$O/pytest_gpu_2.log" 2>&1; local rc=$?; [ $rc -le 1 ] && return 0; return $rc ;;
+    det) timeout -k 10 600 python -u tools/determinism_check.py ${DET_REPS:-12} > "$O/det.txt" 2>&1 ;;
     repeat)  # REPEAT="tests/file.py test_name N": one test function N times in one process
       timeout -k 10 600 python -u tools/repeat_test.py $REPEAT > "$O/repeat.log" 2>&1 ;;
     graphab) timeout -k 10 120 ./tools/graph_ab 2000 > "$O/graph_ab.json" 2>&1 ;;
