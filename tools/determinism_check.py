@@ -32,6 +32,8 @@ def main():
     n_scans = int(os.environ.get("DET_SCANS", "12"))
     scans = [synthetic.make_scan(N, s) for s in range(n_scans)]
     runs, st_runs = [], []
+    DUMP = os.environ.get("DET_DUMP", "0") == "1"
+    ref_ss = [None]
     for r in range(reps):
         stats = []
         ctx = HypothesisContext(n_bins=B, n_points_cap=N, max_raw_points=N, mode="scale",
@@ -47,6 +49,20 @@ def main():
                 combine_allreduce(ctx, 0, 1, s, want_belief=False)
                 if STAGES:  # the device state the next scan reads, after this scan's pushforward
                     stats.append(ctx.state_checksums())
+                if DUMP and s == 0:  # scan 0's ScanBinStats against the first run's: which fields / bins differ
+                    ss = ctx.get_scan_stats()
+                    if r == 0:
+                        ref_ss[0] = ss
+                    else:
+                        d = np.nonzero(ss != ref_ss[0])
+                        if len(d[0]):
+                            fields = sorted(set(d[0].tolist()))
+                            bins = sorted(set(d[1].tolist()))
+                            ex = [(int(f), int(b), float(ref_ss[0][f, b]), float(ss[f, b]), float(ref_ss[0][0, b]),
+                                   float(ss[0, b])) for f, b in list(zip(d[0], d[1]))[:8]]
+                            print(f"run {r} scan 0: {len(d[0])} values differ; fields {fields}; {len(bins)} bins "
+                                  f"(first {bins[:6]}); (field, bin, first run, this run, N first, N this) {ex}",
+                                  flush=True)
             mstats = ctx.mirror_stats()
         finally:
             ctx.close()
