@@ -2584,7 +2584,8 @@ int gcs_assoc_ctx_create(int32_t max_meas, int32_t max_pool, int32_t max_k, int3
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
-  if (bad(hipMemset(c->d_mvalid, 0, 8)) || bad(hipMemset(c->d_ticket, 0, 4)) || bad(hipMemset(c->d_tcnt, 0, kMaxBuckets * 4)) || bad(hipMemset(c->d_flag, 0, 4))) {
+  if (bad(hipMemset(c->d_mvalid, 0, 8)) || bad(hipMemset(c->d_ticket, 0, 4)) || bad(hipMemset(c->d_tcnt, 0, kMaxBuckets * 4)) || bad(hipMemset(c->d_flag, 0, 4)) ||
+      bad(hipStreamSynchronize(nullptr))) {  // (null-stream clears: done before the context's stream runs)
     gcs_assoc_ctx_destroy(c);
     return GCS_ERR_HIP;
   }
@@ -2700,6 +2701,7 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
   if (ns != c->st_ns || rxy != c->st_rxy || rz != c->st_rz) {  // the stencil table changes with the radii only
     ASCHK(c, hipStreamSynchronize(s));
     ASCHK(c, hipMemcpy(c->d_st, st, (size_t)ns * 3, hipMemcpyHostToDevice));
+    ASCHK(c, hipStreamSynchronize(nullptr));  // (a pageable copy may return before its DMA lands)
     c->st_ns = ns;
     c->st_rxy = rxy;
     c->st_rz = rz;
@@ -2724,7 +2726,10 @@ int assoc_launch(gcs_assoc_ctx* c, const gcs_assoc_config* cfg, const gcs_assoc_
     uint32_t* next;
     bool armed = true;
     ~RearmNext() {
-      if (armed) (void)hipMemset(next, 0, 4);
+      if (armed) {
+        (void)hipMemset(next, 0, 4);
+        (void)hipStreamSynchronize(nullptr);  // (the null stream does not order the context's stream)
+      }
     }
   } rearm{mv_next};
   const int km = K <= 8 ? 8 : (K <= 16 ? 16 : 32);

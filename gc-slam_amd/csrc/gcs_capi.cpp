@@ -512,6 +512,7 @@ int upload_atlas(gcs_ctx* c) {
     if (int rc = upload(c, c->d_tile_src, src)) return rc;
     if (int rc = upload(c, c->d_rknn_local, local)) return rc;
   }
+  HIPCHK(c, hipStreamSynchronize(nullptr));  // pageable copies may return before their DMA lands
   return GCS_OK;
 }
 
@@ -1334,6 +1335,12 @@ int gcs_ctx_create(const gcs_config* cfg, gcs_ctx** out) {
     gcs_ctx_destroy(c);
     return rc;
   }
+  // the hipMemset / hipMemcpy calls above ran on the null stream, which does not order the context's
+  // non-blocking streams: they may still be in flight when hipMemset or a pageable hipMemcpy returns,
+  // so the first kernels would race them (a 218 MB ScanBinStats clear overwrote rows the first C3
+  // scan's bin kernel had written -- run-to-run differences of the zero bins' Sigma, tools/
+  // determinism_check.py at C3).  Drain the null stream first.
+  if (bad(hipStreamSynchronize(nullptr))) return GCS_ERR_HIP;
   if (bad(launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, c->d_touched,
                             c->stream)))
     return GCS_ERR_HIP;
@@ -1611,6 +1618,7 @@ int gcs_ctx_set_map(gcs_ctx* c, const double* map) {
   std::vector<double> dev((size_t)c->B * MF_COUNT);
   to_device_order(c, MF_COUNT, map, dev.data());
   HIPCHK(c, hipMemcpy(c->d_map, dev.data(), dev.size() * sizeof(double), hipMemcpyHostToDevice));
+  HIPCHK(c, hipStreamSynchronize(nullptr));  // a pageable copy may return before its DMA lands
   HIPCHK(c, launch_map_derive(c->d_map, c->d_derived, c->B, c->d_partials, c->d_scalars, c->d_touched,
                               c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -2013,6 +2021,7 @@ int launch_imu_odom_dev(gcs_ctx* c, const gcs_imu_odom_inputs& in) {
     HIPCHK(c, hipHostGetDevicePointer((void**)&c->dh_io_out, c->h_io_out, 0));
     HIPCHK(c, hipMalloc(&c->d_io_seq, sizeof(uint64_t)));
     HIPCHK(c, hipMemset(c->d_io_seq, 0, sizeof(uint64_t)));
+    HIPCHK(c, hipStreamSynchronize(nullptr));  // (the null stream does not order io_stream)
     HIPCHK(c, hipStreamCreateWithFlags(&c->io_stream, hipStreamNonBlocking));
     c->io_seq = 0;
   }
@@ -3044,6 +3053,7 @@ int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, in
     HIPCHK(c, hipMalloc(&c->d_payload_in, kLen * sizeof(double)));
     HIPCHK(c, hipMalloc(&c->d_pay_seq, sizeof(uint64_t)));
     HIPCHK(c, hipMemset(c->d_pay_seq, 0, sizeof(uint64_t)));
+    HIPCHK(c, hipStreamSynchronize(nullptr));  // (the null stream does not order the combine stream)
     c->pay_seq = 0;
   }
   if (int rc = gcs_hypothesis_payload(c, w_iw, w_bary, c->h_payload)) return rc;

@@ -2361,6 +2361,7 @@ int gcs_pmap_create(int32_t m_tile, int32_t max_tiles, int32_t n_lobes, int32_t 
       bad(hipMemset(p->below, 0, (size_t)max_tiles * 4)) ||
       bad(hipMalloc(&p->other_bm, ((size_t)max_tiles * m_tile / 32 + 4) * 4)) ||
       bad(hipMemset(p->other_bm, 0, ((size_t)max_tiles * m_tile / 32 + 4) * 4)) ||
+      bad(hipStreamSynchronize(nullptr)) ||  // (null-stream clears: done before p->stream's kernels)
       bad(hipHostMalloc((void**)&p->h_small, kSmall, hipHostMallocMapped)) ||
       bad(hipHostGetDevicePointer((void**)&p->d_small, p->h_small, 0)))
     return fail();
