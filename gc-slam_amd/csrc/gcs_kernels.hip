@@ -1524,8 +1524,15 @@ void k_bins_scale(BinKernelArgs a, double* partials) {
     PROFV(7, 2);
     return;
   }
-  if (t == 0 && tile_active != tile_dirty) a.tile_dirty[tile] = tile_active ? 1 : 0;
+  // every wave reads the tile's dirty word itself (with phase A's loads): an inactive tile's is cleared
+  // only after the barrier below, which every wave of such a tile reaches -- a clear before another
+  // wave's read sent that wave out through the clean-tile return above, leaving its 64 bins' rows
+  // unwritten (stale rows of the previous scan, or the allocation's zeros: the run-to-run differences
+  // of tools/determinism_check.py at C3, and the one C3 parity failure of round 6)
+  if (t == 0 && tile_active && !tile_dirty) a.tile_dirty[tile] = 1;
   if (!tile_active) {
+    __syncthreads();
+    if (t == 0) a.tile_dirty[tile] = 0;
     // every bin of the tile has exact-zero sums: the zero-bin finalize writes its rows (N = 0,
     // Sigma = eps I, ...); partial row = nb x the zero bin's terms, no MF term
     if (DALL || t < TB) {
