@@ -85,6 +85,17 @@ def test_scan_sequence_bitwise_c2_shape():
     assert _first_difference(a, b) is None, _first_difference(a, b)
 
 
+def test_scan_sequence_bitwise_c3_shape():
+    """The north-star shape (262,144 points, 1,048,576 bins: 128-bin tiles, two finalizing waves): four
+    fresh contexts, three scans each, bitwise equal including the ScanBinStats checksum -- the round-6
+    race (a tile's dirty word cleared by wave 0 before wave 1 read it: wave 1 took the clean-tile exit and
+    left its 64 bins' rows unwritten) showed here in 6 of 9 runs."""
+    runs = [_run(1_048_576, 262_144, 262_144, 3)[0] for _ in range(4)]
+    for r in range(1, 4):
+        diff = _first_difference(runs[0], runs[r])
+        assert diff is None, f"run {r} differs from run 0 first at {diff}"
+
+
 def test_torn_mirror_is_reread_not_consumed():
     """The PT fold stores the mirror's sequence word and checksum 300 us before its data: the host sees
     a mirror of the right scan whose data have not arrived, must re-read it until the checksum
