@@ -260,6 +260,7 @@ struct gcs_ctx {
   double* dh_payload = nullptr;
   double* d_payload = nullptr;   // device: RCCL's receive buffer
   double* d_payload_in = nullptr;  // device: the send buffer when the communicator spans > 1 rank
+  int combine_delay_us = 0;      // GCS_DEBUG_COMBINE_DELAY: a straggling peer, simulated on the combine stream
   int sendbuf_mode = -1;         // GCS_DEBUG_SENDBUF: -1 by world size, 0 host, 1 device
   void* comm_seen = nullptr;     // the communicator whose rank count comm_world holds
   int comm_world = 1;
@@ -1468,6 +1469,10 @@ int gcs_ctx_set_debug(gcs_ctx* c, int32_t key, int64_t value) {
     case GCS_DEBUG_MIRROR_TORN:
       if (value < 0 || value > 10000) return fail(c, GCS_ERR_ARG, "mirror torn delay: 0..10000 us");
       c->mirror_torn = (int)value;
+      return GCS_OK;
+    case GCS_DEBUG_COMBINE_DELAY:
+      if (value < 0 || value > 1000000) return fail(c, GCS_ERR_ARG, "combine delay: 0..1000000 us");
+      c->combine_delay_us = (int)value;
       return GCS_OK;
     case GCS_DEBUG_SENDBUF:
       if (value < -1 || value > 1) return fail(c, GCS_ERR_ARG, "send buffer: -1 (by world size), 0 host, 1 device");
@@ -3107,6 +3112,7 @@ int gcs_combine_allreduce(gcs_ctx* c, void* comm, double w_iw, double w_bary, in
       HIPCHK(c, hipMemcpyAsync(c->d_payload_in, c->h_payload, len * sizeof(double), hipMemcpyHostToDevice, s));
       send = c->d_payload_in;
     }
+    if (c->combine_delay_us) HIPCHK(c, launch_delay(c->combine_delay_us, s));
     ncclResult_t r = ncclAllReduce(send, c->d_payload, len, ncclDouble, ncclSum, (ncclComm_t)comm, s);
     if (r != ncclSuccess) return fail(c, GCS_ERR_HIP, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
     HIPCHK(c, launch_payload_out(c->d_payload, c->dh_psum, len, c->d_pay_seq, s));

@@ -224,6 +224,7 @@ hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint3
 // the hypothesis all-reduce's stage-out (gcs_combine_allreduce): the device sum to a host buffer of n
 // words + [n] sequence number (*dseq + 1, stored back to *dseq) + [n + 1] checksum (mirror_word_hash)
 hipError_t launch_payload_out(const double* src, double* host, int n, uint64_t* dseq, hipStream_t s);
+hipError_t launch_delay(int us, hipStream_t s);  // GCS_DEBUG_COMBINE_DELAY
 // legacy: the round-3 k_points (scale mode) instead of k_points_lean; mir: the fold's host mirror
 // (gcs_scan_begin: the scalars and error words without a D2H copy)
 hipError_t launch_points(const PointKernelArgs& a, bool scale, double* partials, int nblk, bool fold, hipStream_t s,

@@ -2933,6 +2933,17 @@ hipError_t launch_payload_out(const double* src, double* host, int n, uint64_t* 
   return hipGetLastError();
 }
 
+// GCS_DEBUG_COMBINE_DELAY's stand-in for a late peer: one wave sleeps on the 100 MHz wall clock
+__global__ __launch_bounds__(64) void k_delay(uint32_t us) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < 100ull * (uint64_t)us) __builtin_amdgcn_s_sleep(64);
+}
+
+hipError_t launch_delay(int us, hipStream_t s) {
+  hipLaunchKernelGGL(k_delay, dim3(1), dim3(64), 0, s, (uint32_t)us);
+  return hipGetLastError();
+}
+
 hipError_t launch_gate(const uint64_t* gate, uint64_t seq, double* xi_out, uint32_t* err, hipStream_t s) {
   hipLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, s, gate, seq, xi_out, err);
   return hipGetLastError();

@@ -105,6 +105,7 @@ DEBUG_PT_CLEAR = 8
 DEBUG_MIRROR_TORN = 9
 DEBUG_SENDBUF = 10
 DEBUG_DEVICE_IMU_ODOM = 11
+DEBUG_COMBINE_DELAY = 12
 MAP_OWN, MAP_LEAD, MAP_FOLLOW, MAP_REC_LEN = 0, 1, 2, 48
 
 

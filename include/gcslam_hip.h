@@ -248,6 +248,11 @@ int gcs_ctx_enable_timing(gcs_ctx* ctx, int32_t stage_mask);
  * gcs_scan_begin runs on the device (gcs_imu_odom_evidence_device's kernel) beside the bin path's kernels,
  * instead of the host C++ branch (the default). */
 #define GCS_DEBUG_DEVICE_IMU_ODOM 11
+/* GCS_DEBUG_COMBINE_DELAY (microseconds, 0 = off, at most 1,000,000): gcs_combine_allreduce queues a
+ * kernel that waits this long on the combine stream ahead of ncclAllReduce -- the world-1 form of a
+ * straggling peer rank.  A delay past the host poll's 20 ms sends the wait to its stream-synchronize
+ * path (gcs_ctx_mirror_stats' payload syncs count it); the combined state must not change.  Test knob. */
+#define GCS_DEBUG_COMBINE_DELAY 12
 int gcs_ctx_set_debug(gcs_ctx* ctx, int32_t key, int64_t value);
 /* The scan mirror (the PT fold's copy of the scan's scalars and device error words to pinned host
  * memory, with the scan's sequence number and a checksum; the host accepts it only when both match):

@@ -129,3 +129,43 @@ def test_device_sendbuf_allreduce_matches_host_buffer():
             ctx2.set_debug(L.DEBUG_SENDBUF, 2)
         finally:
             ctx2.close()
+
+
+def test_straggling_peer_takes_the_synchronize_path_same_state():
+    """A peer that reaches the all-reduce late (GCS_DEBUG_COMBINE_DELAY: a 30 ms wait queued on the combine
+    stream ahead of ncclAllReduce, the world-1 stand-in for a straggling rank) outlasts the host poll's
+    20 ms: the wait falls to its stream synchronize, which returns once the collective is done, and the
+    sum is checked as on the poll path.  Over four scans with the delay on scans 1 and 3: bitwise the
+    undelayed state, exactly two payload syncs, and each delayed combine takes at least the delay."""
+    import time
+    from gcslam import _lib as L, synthetic
+    from gcslam.context import HypothesisContext
+    from gcslam.distributed import HypothesisComm, combine_allreduce
+    comm = HypothesisComm(0, 1, 0)
+    outs, waits = [], []
+    try:
+        for delayed in (False, True):
+            ctx = HypothesisContext(n_bins=48, n_points_cap=2048, max_raw_points=4096, mode="dense",
+                                    lidar_origin=ORIGIN)
+            ctx.set_debug(L.DEBUG_SENDBUF, 1)  # the world > 1 form of the exchange
+            for s in range(4):
+                sc = synthetic.make_scan(4096, 90 + s)
+                rec = torch.from_numpy(sc["xyz_record"]).cuda()
+                t = torch.from_numpy(sc["timestamps"]).cuda()
+                w = torch.from_numpy(sc["weights"]).cuda()
+                ctx.scan(rec, 16, t, w, 4096, **synthetic.scan_kwargs(sc))
+                ctx.set_debug(L.DEBUG_COMBINE_DELAY, 30000 if delayed and s % 2 else 0)
+                t0 = time.perf_counter()
+                (X, _, z, Lm, h), cert = combine_allreduce(ctx, 0, 1, s, comm=comm)
+                if delayed and s % 2:
+                    waits.append(time.perf_counter() - t0)
+            st = ctx.mirror_stats()
+            assert st[3] == 4 and st[5] == (2 if delayed else 0), st
+            outs.append((Lm, h, z, *ctx.iw_state(), *ctx.meas_iw_state()[:2]))
+            ctx.close()
+    finally:
+        comm.close()
+    for x, y in zip(*outs):
+        assert np.array_equal(x, y)
+    assert min(waits) >= 0.030, waits
+    print("straggler combine s:", [round(x, 4) for x in waits])
