@@ -10,7 +10,7 @@ empty map, and the absolute trajectory error between their per-scan poses z_t mu
 fixtures show (1e-6 m) and reports the error against the synthetic ground truth for information
 (both paths drift from it alike: the scan carries the LiDAR bin evidence and the eleven IMU /
 odometry factors of pipeline.py:595-776, and the drift is the reference's own dynamics -- DESIGN.md
-section 3, declared item 12).  Measured on MI355X: 3.3e-17 m (dense, B=48) and 5.9e-11 m (scale,
+section 3, declared item 12; its mechanism is pinned on the CPU by tests/test_oracle_trajectory_drift.py).  Measured on MI355X: 3.3e-17 m (dense, B=48) and 5.9e-11 m (scale,
 B=5000) over the 12 scans.  Run-to-run bitwise agreement of the same sequence, with the device state
 checksums and the scan mirror's guard, is tests/test_gpu_determinism.py.
 """
