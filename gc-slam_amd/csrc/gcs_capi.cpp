@@ -2991,7 +2991,12 @@ int gcs_rccl_comm_init(int32_t device, int32_t n_ranks, int32_t rank, const uint
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
   ncclComm_t cm = nullptr;
-  if (ncclCommInitRank(&cm, n_ranks, u, rank) != ncclSuccess) return GCS_ERR_HIP;
+  const ncclResult_t r = ncclCommInitRank(&cm, n_ranks, u, rank);
+  if (r != ncclSuccess) {  // the reason, for gcs_last_error(NULL) (e.g. two ranks on one device)
+    const char* last = ncclGetLastError(nullptr);
+    t_create_msg = std::string("ncclCommInitRank: ") + ncclGetErrorString(r) + (last && *last ? std::string(": ") + last : "");
+    return GCS_ERR_HIP;
+  }
   *comm = (void*)cm;
   return GCS_OK;
 }
